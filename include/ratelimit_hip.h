@@ -1,0 +1,191 @@
+/*
+ * ratelimit_hip.h — C ABI of libratelimit_hip.so, the MI355X fixed-window
+ * rate-limit backend.
+ *
+ * Drop-in boundary: this library replaces the box below
+ *   limiter.RateLimitCache.DoLimit           (reference src/limiter/cache.go:11-29)
+ * as implemented by
+ *   redis.fixedRateLimitCacheImpl.DoLimit    (src/redis/fixed_cache_impl.go:33-113)
+ *   + limiter.BaseRateLimiter                (src/limiter/base_limiter.go:45-197)
+ *   + limiter.CacheKeyGenerator              (src/limiter/cache_key.go:48-80)
+ *   + redis-server INCRBY/EXPIRE and the freecache local over-limit cache.
+ * A Go cgo adapter packs many in-flight DoLimit calls into
+ * one rl_batch and calls rl_do_limit from a single batcher goroutine.
+ *
+ * Plain C types only: no torch, no HIP types in any signature.
+ * Threading: one rl_ctx is driven by one host thread at a time.
+ * Errors: every int-returning call returns RL_OK (0) or an rl_status code and
+ * records a message readable with rl_last_error(); the Go adapter turns a
+ * non-zero status into panic(redis.RedisError("gpu: "+msg)), exactly the
+ * reference's backend-failure convention (src/redis/driver_impl.go:60-64).
+ */
+#ifndef RATELIMIT_HIP_H
+#define RATELIMIT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RL_ABI_VERSION 1u
+
+/* Status codes. */
+enum rl_status {
+  RL_OK = 0,
+  RL_E_INVALID = 1,    /* malformed batch: unit out of 1..4, offsets, sizes */
+  RL_E_TABLE_FULL = 2, /* open-addressing table has no free slot on the probe path */
+  RL_E_ARENA_FULL = 3, /* long-stem overflow arena exhausted */
+  RL_E_HIP = 4,        /* HIP runtime error */
+  RL_E_CAPACITY = 5,   /* batch larger than rl_config.max_* */
+  RL_E_TIME = 6,       /* now outside [0, 2^32 - 2*86400) or decreasing */
+  RL_E_COMM = 7,       /* multi-GPU routing (RCCL) error */
+  RL_E_INTERNAL = 8
+};
+
+/* pb.RateLimitResponse_RateLimit_Unit (go-control-plane v0.9.7 rls.proto). */
+enum rl_unit { RL_UNIT_SECOND = 1, RL_UNIT_MINUTE = 2, RL_UNIT_HOUR = 3, RL_UNIT_DAY = 4 };
+/* pb.RateLimitResponse_Code. */
+enum rl_code { RL_CODE_OK = 1, RL_CODE_OVER_LIMIT = 2 };
+/* rl_batch.flags bits. */
+#define RL_FLAG_SHADOW 0x1u /* config.RateLimit.ShadowMode (src/config/config.go:24) */
+
+/* Per-rule stats counters, in stats.RateLimitStats order (src/stats/manager.go:47-55). */
+enum rl_stat {
+  RL_STAT_TOTAL_HITS = 0,
+  RL_STAT_OVER_LIMIT = 1,
+  RL_STAT_NEAR_LIMIT = 2,
+  RL_STAT_OVER_LIMIT_WITH_LOCAL_CACHE = 3,
+  RL_STAT_WITHIN_LIMIT = 4,
+  RL_STAT_SHADOW_MODE = 5,
+  RL_NUM_STATS = 6
+};
+
+/* Backend configuration: the knobs NewFixedRateLimitCacheImpl receives
+ * (src/redis/fixed_cache_impl.go:118-125, src/settings/settings.go:45-50)
+ * plus capacity sizing for HBM. */
+typedef struct rl_config {
+  uint64_t table_slots;      /* 128-B slots in the HBM table (power of 2; 0 = default 2^24) */
+  uint64_t arena_bytes;      /* overflow arena for stems longer than 80 B (0 = default 64 MiB) */
+  uint32_t max_batch;        /* max descriptors per rl_do_limit call (0 = default 1<<20) */
+  uint32_t max_requests;     /* max requests per call (0 = max_batch) */
+  uint32_t max_rules;        /* max distinct rule ids per call (0 = default 65536) */
+  uint32_t max_stem_bytes;   /* max total stem bytes per call (0 = 128 * max_batch) */
+  float near_limit_ratio;    /* NEAR_LIMIT_RATIO (float32, settings.go:48) */
+  int32_t local_cache_enabled;  /* LOCAL_CACHE_SIZE_IN_BYTES != 0 (runner.go:95-98) */
+  int32_t per_second_split;     /* REDIS_PERSECOND: SECOND-unit keys in a separate store */
+  int32_t device;               /* HIP device ordinal */
+  int64_t expiration_jitter_max_seconds; /* EXPIRATION_JITTER_MAX_SECONDS: accepted; the
+                                            backend fixes the draw at 0 */
+  int32_t reserved[8];
+} rl_config;
+
+/* One packed batch (struct of arrays). Only descriptors whose limit is
+ * non-nil are packed (nil limits -> {OK, nil, 0} host-side,
+ * base_limiter.go:78-81); unlimited rules are nil by then (ratelimit.go:140-143).
+ * Descriptors appear in arrival order: request-major, descriptor order inside
+ * the request; req_idx is non-decreasing and now[] is non-decreasing.
+ * The stem is the cache key without its window suffix:
+ *   prefix ‖ domain ‖ '_' ‖ Σ(key ‖ '_' ‖ value ‖ '_')   (cache_key.go:62-71)
+ * The full key is stem ‖ decimal((now/div)*div) (cache_key.go:73-74). */
+typedef struct rl_batch {
+  uint32_t n;            /* descriptors */
+  uint32_t n_requests;   /* requests (length of now[]) */
+  uint32_t n_rules;      /* rule ids are < n_rules (length of stats / RL_NUM_STATS) */
+  uint32_t reserved;
+  const uint8_t* stem_bytes;  /* concatenated stems */
+  const uint32_t* stem_off;   /* n+1 offsets into stem_bytes, stem_off[0] == 0 */
+  const int64_t* now;         /* [n_requests] UnixNow() of each request (seconds) */
+  const uint32_t* req_idx;    /* [n] request of each descriptor */
+  const uint8_t* unit;        /* [n] rl_unit of the descriptor's limit */
+  const uint8_t* flags;       /* [n] RL_FLAG_* */
+  const uint32_t* limit;      /* [n] RequestsPerUnit */
+  const uint32_t* hits;       /* [n] request.HitsAddend (max(1, h) applied by the backend) */
+  const uint32_t* rule_id;    /* [n] dense id of limit.Stats.Key */
+} rl_batch;
+
+/* Results, same order as the batch. stats holds THIS call's deltas
+ * (n_rules x RL_NUM_STATS, row-major, overwritten); the adapter adds them to the
+ * gostats counters. CurrentLimit is re-attached host-side (= limits[i].Limit). */
+typedef struct rl_result {
+  uint8_t* code;              /* [n] rl_code */
+  uint32_t* limit_remaining;  /* [n] LimitRemaining */
+  uint32_t* reset_s;          /* [n] DurationUntilReset.Seconds (1..86400) */
+  uint64_t* stats;            /* [n_rules * RL_NUM_STATS] */
+} rl_result;
+
+/* Table restore / seed records: set the fixed-window counter of key
+ * stem ‖ decimal(ws(now[i], unit[i])) to count[i] with EXPIRE div (as if the last
+ * INCRBY happened at now[i]); lc[i] != 0 also inserts the key into the local
+ * over-limit cache with TTL div. Host memory. */
+typedef struct rl_restore_batch {
+  uint32_t n;
+  uint32_t reserved;
+  const uint8_t* stem_bytes;
+  const uint32_t* stem_off;   /* n+1 */
+  const uint8_t* unit;        /* [n] */
+  const int64_t* now;         /* [n] */
+  const uint32_t* count;      /* [n] */
+  const uint8_t* lc;          /* [n] */
+} rl_restore_batch;
+
+typedef struct rl_table_info {
+  uint64_t table_slots;
+  uint64_t live_slots;        /* occupied (non-empty, non-tombstone) slots */
+  uint64_t tombstones;
+  uint64_t arena_bytes_used;
+  uint64_t exact_stems;       /* slots flagged multi-unit (exact slow path) */
+  uint64_t batches;
+  uint64_t decisions;
+} rl_table_info;
+
+typedef struct rl_ctx rl_ctx;
+
+uint32_t rl_abi_version(void);
+
+/* Create / destroy a backend on cfg->device. NULL on failure (message in err). */
+rl_ctx* rl_create(const rl_config* cfg, char* err, size_t errlen);
+void rl_destroy(rl_ctx* ctx);
+const char* rl_last_error(const rl_ctx* ctx);
+
+/* DoLimit for a whole batch. Host buffers (pinned via rl_alloc_host is fastest).
+ * Synchronous: returns after results are in *out. */
+int rl_do_limit(rl_ctx* ctx, const rl_batch* in, rl_result* out);
+
+/* Same, with every pointer in *in / *out in device memory of ctx's GPU,
+ * enqueued on `stream` (a hipStream_t, NULL = ctx's own stream). Returns once
+ * the work is enqueued; errors detected on the GPU surface at rl_synchronize. */
+int rl_do_limit_async(rl_ctx* ctx, const rl_batch* in, rl_result* out, void* stream);
+int rl_synchronize(rl_ctx* ctx);
+
+/* Epoch sweep (replaces Redis EXPIRE): tombstones every slot whose counter
+ * and local-cache entries have all expired at `now`. */
+int rl_sweep(rl_ctx* ctx, int64_t now, uint64_t* n_evicted);
+
+/* Seed / restore counters (host buffers). */
+int rl_restore(rl_ctx* ctx, const rl_restore_batch* in);
+
+int rl_table_info_get(rl_ctx* ctx, rl_table_info* info);
+
+/* Pinned host memory for the packed buffers (hipHostMalloc). */
+void* rl_alloc_host(size_t bytes);
+void rl_free_host(void* p);
+
+/* Diagnostics used by the parity tests (host buffers):
+ * rl_debug_keys materialises each descriptor's full Redis key
+ * (stem ‖ decimal window start) on the GPU into out_bytes/out_off (n+1). */
+int rl_debug_keys(rl_ctx* ctx, const rl_batch* in, uint8_t* out_bytes, uint32_t* out_off,
+                  uint32_t out_cap);
+/* rl_debug_decide runs the device GetResponseDescriptorStatus on explicit
+ * (before, after, local-cache flag) tuples: base_limiter.go:76-135. */
+int rl_debug_decide(rl_ctx* ctx, uint32_t n, const uint32_t* before, const uint32_t* after,
+                    const uint8_t* lc_hit, const uint32_t* hits, const uint32_t* limit,
+                    const uint8_t* unit, const uint8_t* flags, const int64_t* now,
+                    uint8_t* code, uint32_t* remaining, uint32_t* reset_s,
+                    uint64_t* stat_deltas /* n * RL_NUM_STATS */, uint8_t* lc_set);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RATELIMIT_HIP_H */

@@ -1,0 +1,108 @@
+"""Host packer: DoLimit calls -> one struct-of-arrays rl_batch (numpy, host memory).
+
+This is the Python twin of the Go adapter's packer: for every
+in-flight ``DoLimit(request, limits)`` call it
+  * drops nil-limit descriptors (they answer {OK, nil, 0} host-side,
+    base_limiter.go:78-81 / cache_key.go:51-56),
+  * rejects UNKNOWN units up front (utils.UnitToDivider panics, utilities.go:29),
+  * builds the key stem prefix ‖ domain ‖ '_' ‖ Σ(key ‖ '_' ‖ value ‖ '_')
+    (cache_key.go:62-71) — the window suffix is added on the GPU,
+  * interns limit.Stats.Key into a dense rule id (stats.RateLimitStats identity).
+"""
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+
+
+class RuleInterner:
+    """limit.Stats.Key -> dense rule id (stable across batches)."""
+
+    def __init__(self):
+        self.ids: Dict[str, int] = {}
+        self.keys: List[str] = []
+
+    def intern(self, key: str) -> int:
+        i = self.ids.get(key)
+        if i is None:
+            i = len(self.keys)
+            self.ids[key] = i
+            self.keys.append(key)
+        return i
+
+
+def stem_of(prefix: str, domain: str, entries: Sequence[Tuple[str, str]]) -> bytes:
+    parts = [prefix, domain, "_"]
+    for k, v in entries:
+        parts += [k, "_", v, "_"]
+    return "".join(parts).encode("utf-8")
+
+
+@dataclass
+class PackedBatch:
+    arrays: Dict[str, np.ndarray]
+    n: int
+    n_requests: int
+    n_rules: int
+    # (call index, descriptor index) for each packed descriptor
+    origin: List[Tuple[int, int]] = field(default_factory=list)
+
+    def batch_struct(self):
+        return abi.make_batch_struct(self.arrays, self.n, self.n_requests, self.n_rules)
+
+    def alloc_result(self):
+        return {"code": np.zeros(max(self.n, 1), np.uint8),
+                "limit_remaining": np.zeros(max(self.n, 1), np.uint32),
+                "reset_s": np.zeros(max(self.n, 1), np.uint32),
+                "stats": np.zeros(max(self.n_rules, 1) * abi.RL_NUM_STATS, np.uint64)}
+
+
+def arrays_from_lists(stems: List[bytes], now: Sequence[int], req_idx, unit, flags, limit, hits,
+                      rule_id) -> Dict[str, np.ndarray]:
+    n = len(stems)
+    off = np.zeros(n + 1, np.uint32)
+    if n:
+        off[1:] = np.cumsum([len(s) for s in stems], dtype=np.uint64).astype(np.uint32)
+    blob = np.frombuffer(b"".join(stems), np.uint8).copy() if n else np.zeros(1, np.uint8)
+    if blob.size == 0:
+        blob = np.zeros(1, np.uint8)
+    return {"stem_bytes": blob, "stem_off": off,
+            "now": np.asarray(now, np.int64).reshape(-1) if len(now) else np.zeros(1, np.int64),
+            "req_idx": np.asarray(req_idx, np.uint32), "unit": np.asarray(unit, np.uint8),
+            "flags": np.asarray(flags, np.uint8), "limit": np.asarray(limit, np.uint32),
+            "hits": np.asarray(hits, np.uint32), "rule_id": np.asarray(rule_id, np.uint32)}
+
+
+def pack_calls(calls, prefix: str, interner: RuleInterner, n_rules: Optional[int] = None) -> PackedBatch:
+    """calls: sequence of (request, limits, now) in arrival order.
+
+    ``request`` / ``limits`` follow the reference's data model (RateLimitRequest with
+    .domain/.descriptors[.entries]/.hits_addend, RateLimit with .limit/.stats/.shadow_mode).
+    """
+    stems, req_idx, unit, flags, limit, hits, rule_id, origin = [], [], [], [], [], [], [], []
+    now_list = []
+    for c, (request, limits, now) in enumerate(calls):
+        if len(request.descriptors) != len(limits):
+            raise AssertionError("len(descriptors) != len(limits)")  # base_limiter.go:47
+        q = len(now_list)
+        now_list.append(int(now))
+        h = int(request.hits_addend)
+        for i, (d, lim) in enumerate(zip(request.descriptors, limits)):
+            if lim is None:
+                continue
+            u = int(lim.limit.unit)
+            if u not in (1, 2, 3, 4):
+                raise RuntimeError("should not get here")  # utils.UnitToDivider panic
+            stems.append(stem_of(prefix, request.domain, d.entries))
+            req_idx.append(q)
+            unit.append(u)
+            flags.append(abi.RL_FLAG_SHADOW if lim.shadow_mode else 0)
+            limit.append(int(lim.limit.requests_per_unit))
+            hits.append(h)
+            rule_id.append(interner.intern(lim.stats.key))
+            origin.append((c, i))
+    arrays = arrays_from_lists(stems, now_list, req_idx, unit, flags, limit, hits, rule_id)
+    nr = len(interner.keys) if n_rules is None else n_rules
+    return PackedBatch(arrays, len(stems), len(now_list), nr, origin)

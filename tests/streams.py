@@ -1,0 +1,92 @@
+"""Seeded random DoLimit call streams (structured), for parity tests.
+
+Each stream is a list of (request, limits, now) in arrival order, built from the
+oracle's data model. Streams stress every row of SURVEY.md §8a: nil limits,
+duplicate descriptors inside one request, hits_addend > 1, shadow rules,
+per-request overrides with a different unit than the rule (so SECOND/MINUTE/
+HOUR keys of one stem can share a Redis key at aligned window starts), window
+rollover across second/minute/hour boundaries, and hot keys.
+"""
+import random
+
+from oracle import oracle as O
+
+UNITS = [O.SECOND, O.MINUTE, O.HOUR, O.DAY]
+
+
+def random_stream(seed, n_calls=300, n_stems=12, start_now=1_700_000_035, max_step=3,
+                  p_override=0.1, p_nil=0.1, p_shadow=0.2, max_hits=8, max_desc=4, limit_range=(0, 40),
+                  domains=("dom", "other"), zipf=False):
+    rng = random.Random(seed)
+    reg = {}
+
+    def stats(key):
+        if key not in reg:
+            reg[key] = O.RateLimitStats(key)
+        return reg[key]
+
+    # rules: one per (domain, entries) — like a loaded config; unit fixed per rule
+    rules = []
+    for s in range(n_stems):
+        dom = rng.choice(domains)
+        depth = rng.randint(1, 4)
+        entries = [("k%d" % j, "v%d_%d" % (s % 5, j)) if rng.random() < 0.8 else ("k%d" % j, "")
+                   for j in range(depth)]
+        unit = rng.choice(UNITS)
+        shadow = rng.random() < p_shadow
+        limit = rng.randint(*limit_range)
+        fk = dom + "." + ".".join(k + ("_" + v if v else "") for k, v in entries)
+        rules.append((dom, entries, unit, limit, shadow, fk))
+    now = start_now
+    calls = []
+    weights = [1.0 / (i + 1) ** 1.1 for i in range(n_stems)] if zipf else None
+    for _ in range(n_calls):
+        now += rng.choice([0] * 6 + list(range(1, max_step + 1)))
+        dom = rng.choice(domains)
+        descs, limits = [], []
+        for _d in range(rng.randint(1, max_desc)):
+            if weights:
+                r = rng.choices(rules, weights)[0]
+            else:
+                r = rng.choice(rules)
+            rdom, entries, unit, limit, shadow, fk = r
+            if rdom != dom or rng.random() < p_nil:
+                descs.append(O.Descriptor(list(entries)))
+                limits.append(None)
+                continue
+            if rng.random() < p_override:
+                # config_impl.go:254-265: override -> fresh RateLimit, stats key from descriptorKey
+                ou = rng.choice(UNITS)
+                ol = rng.randint(*limit_range)
+                key = dom + "." + ".".join(k + ("_" + v if v else "") for k, v in entries)
+                descs.append(O.Descriptor(list(entries), O.Limit(ol, ou)))
+                limits.append(O.RateLimit(key, stats(key), O.Limit(ol, ou), False, False))
+            else:
+                descs.append(O.Descriptor(list(entries)))
+                limits.append(O.RateLimit(fk, stats(fk), O.Limit(limit, unit), False, shadow))
+        hits = rng.choice([0, 1, 1, 1, 2, 3, rng.randint(1, max_hits)])
+        calls.append((O.RateLimitRequest(dom, descs, hits), limits, now))
+    return calls
+
+
+def reset_stats(calls):
+    seen = set()
+    for _, limits, _ in calls:
+        for l in limits:
+            if l is not None and id(l.stats) not in seen:
+                seen.add(id(l.stats))
+                for f in O.STAT_FIELDS:
+                    setattr(l.stats, f, 0)
+
+
+def python_oracle_run(calls, ratio=0.8, local_cache=False, prefix="", per_second=False):
+    """Sequential replay through the pure-Python oracle; returns (statuses per call, stats dict)."""
+    reset_stats(calls)
+    cache = O.OracleFixedRateLimitCache(ratio, local_cache, prefix, per_second)
+    outs = [cache.do_limit(req, limits, now) for req, limits, now in calls]
+    stats = {}
+    for _, limits, _ in calls:
+        for l in limits:
+            if l is not None:
+                stats[l.stats.key] = l.stats.as_tuple()
+    return outs, stats
