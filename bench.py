@@ -1,0 +1,234 @@
+"""Benchmark: rate-limit decisions/sec of the MI355X fixed-window backend.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2]
+
+A step is one DoLimit batch over device-resident packed input (BASELINE.json
+configs[1] = C1 by default: 10M tenant stems x {sec, min} per GPU, 500k
+requests = 1M descriptors per batch, uniform tenants, `now` +1 s per step).
+Before timing, every key is inserted ("warm-up inserts all 20M keys").
+N>1 (torch.distributed.run, one process per GPU): each rank owns a disjoint
+10M-tenant key range (hash-sharded by construction, weak scaling, no
+data-path collective); value = all ranks' decisions / max-over-ranks time.
+
+Besides the contract line, rank 0 reports:
+  roofline      dominant kernel (k_runs) achieved GB/s on the canonical
+                B_alg = key_len + 16 + 12 + 64 B per decision,
+                from HIP events on the library's stream;
+  cpu_baseline  the C restatement oracle (sequential, 1 core) on a bounded
+                sample of the same C1 stream.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "rate-limit decisions/sec (whole node) at 10M/1B keys; p99 batch latency"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c1", choices=["c1", "c2"])
+    ap.add_argument("--requests", type=int, default=500_000, help="requests per batch per GPU (2 descriptors each)")
+    ap.add_argument("--tenants", type=int, default=10_000_000, help="tenants per GPU")
+    ap.add_argument("--distinct-batches", type=int, default=4)
+    ap.add_argument("--latency-steps", type=int, default=50)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fill", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from ratelimit_amd import workloads as W
+    from ratelimit_amd.limiter import Backend
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    nq = args.requests
+    n = 2 * nq
+    T = args.tenants
+    keys_per_gpu = 2 * T
+    slots = 1 << max(16, int(np.ceil(np.log2(2 * keys_per_gpu))))
+    be = Backend(0.8, False, table_slots=slots, max_batch=n, max_rules=8, device=local)
+    base_t = rank * T  # this rank's tenant range (disjoint across ranks)
+    now0 = W.NOW0
+
+    # ---- fill: insert every key of this rank's range (not timed)
+    t_fill = time.perf_counter()
+    if not args.no_fill:
+        for s0 in range(0, T, nq):
+            ids = np.arange(s0, min(s0 + nq, T), dtype=np.int64) + base_t
+            a, bn, bq, br = W.c1_batch(ids, now0 - 1)
+            be.do_limit_arrays(a, bn, bq, br)
+    t_fill = time.perf_counter() - t_fill
+
+    # ---- device-resident input batches + per-step clocks
+    rng = np.random.default_rng((0xC1 if args.config == "c1" else 0xC2) + 7919 * rank)
+    sampler = W.ZipfSampler(T, 1.1) if args.config == "c2" else None
+    dev_batches = []
+    for _ in range(args.distinct_batches):
+        if sampler is None:
+            a, bn, bq, br = W.c1_batch(rng.integers(0, T, nq) + base_t, now0)
+        else:
+            a, bn, bq, br = W.c1_batch(sampler.sample(rng, nq) + base_t, now0,
+                                       rng.integers(1, 9, nq).astype(np.uint32))
+        dev_batches.append({k: torch.from_numpy(np.ascontiguousarray(v).view(np.int32) if v.dtype == np.uint32
+                                                else np.ascontiguousarray(v)).cuda()
+                            for k, v in a.items() if k != "now"})
+    stem_len = 34
+    total_steps = args.warmup + args.steps + args.steps + args.latency_steps
+    nows = [torch.full((nq,), now0 + s, dtype=torch.int64, device="cuda") for s in range(total_steps)]
+    out = {"code": torch.empty(n, dtype=torch.uint8, device="cuda"),
+           "limit_remaining": torch.empty(n, dtype=torch.int32, device="cuda"),
+           "reset_s": torch.empty(n, dtype=torch.int32, device="cuda"),
+           "stats": torch.zeros(2 * 6, dtype=torch.int64, device="cuda")}
+    torch.cuda.synchronize()
+
+    step = [0]
+
+    def run_step():
+        s = step[0]
+        inp = dict(dev_batches[s % len(dev_batches)])
+        inp["now"] = nows[s]
+        be.do_limit_device(inp, out, n, nq, 2)
+        step[0] += 1
+
+    # ---- warmup
+    for _ in range(args.warmup):
+        run_step()
+    be.synchronize()
+    torch.cuda.synchronize()
+
+    # ---- timed region: exactly K steps
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run_step()
+    be.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = world * n * args.steps / elapsed
+
+    # ---- per-stage device times (HIP events on the library stream)
+    be.profile(True)
+    for _ in range(args.steps):
+        run_step()
+    be.synchronize()
+    stage_ms, nb = be.profile_read()
+    be.profile(False)
+    stage_avg = {k: v / max(nb, 1) for k, v in stage_ms.items()}
+
+    # ---- batch latency: submit -> outputs ready, one batch at a time
+    lat = []
+    for _ in range(args.latency_steps):
+        t1 = time.perf_counter()
+        run_step()
+        be.synchronize()
+        lat.append((time.perf_counter() - t1) * 1e3)
+    lat = np.array(lat) if lat else np.array([float("nan")])
+    info = be.table_info()
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    b_alg = stem_len + 10 + 16 + 12 + 64  # key = stem + 10-digit window
+    runs_ms = stage_avg["runs"]
+    achieved = b_alg * n / (runs_ms * 1e-3) / 1e9 if runs_ms > 0 else None
+    pipe_ms = sum(stage_avg.values())
+    traffic = None
+    tp = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
+    if os.path.exists(tp):
+        try:
+            traffic = json.load(open(tp)).get("k_runs_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "kernel": "k_runs", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                "bytes_alg_per_decision": b_alg, "decisions_per_launch": n,
+                "stage_ms": {k: round(v, 4) for k, v in stage_avg.items()},
+                "pipeline_achieved": b_alg * n / (pipe_ms * 1e-3) / 1e9 if pipe_ms > 0 else None}
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, W)
+
+    line = {
+        "metric": METRIC, "value": value, "unit": "decisions/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "%s: %dM tenant stems x {sec,min} per GPU, %d-descriptor batches, %s tenants%s, "
+                               "now +1 s per batch, all keys pre-inserted" %
+                               (args.config.upper(), T // 1_000_000, n,
+                                "uniform" if args.config == "c1" else "Zipf(1.1)",
+                                "" if args.config == "c1" else ", hits 1..8"),
+                   "global_batch": world * n, "batch_per_gpu": n, "live_stem_slots_per_gpu": info["live_slots"],
+                   "table_slots": slots, "parallelism": "hash-sharded key ranges x%d (no data-path collective)" % world},
+        "p50_batch_ms": float(np.percentile(lat, 50)), "p99_batch_ms": float(np.percentile(lat, 99)),
+        "roofline": roofline, "cpu_baseline": cpu, "fill_s": round(t_fill, 2),
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, W):
+    """The C restatement oracle (sequential, 1 thread) on a bounded sample of the same stream."""
+    from oracle.c_oracle import COracle
+    co = COracle(0.8, False, False)
+    rng = np.random.default_rng(0xC1 + 1)
+    sampler = W.ZipfSampler(args.tenants, 1.1) if args.config == "c2" else None
+    done = 0
+    spent = 0.0
+    k = 0
+    while spent < args.cpu_seconds and k < 40:
+        if sampler is None:
+            a, n, nq, nr = W.c1_batch(rng.integers(0, args.tenants, args.requests), W.NOW0 + k)
+        else:
+            a, n, nq, nr = W.c1_batch(sampler.sample(rng, args.requests), W.NOW0 + k,
+                                      rng.integers(1, 9, args.requests).astype(np.uint32))
+        t = time.perf_counter()
+        co.do_limit(a, n, nq, nr)
+        spent += time.perf_counter() - t
+        done += n
+        k += 1
+    co.close()
+    return {"value": done / spent, "unit": "decisions/s", "cores": 1, "kind": "port",
+            "sample": "%d consecutive %s batches x %d descriptors (%.1f s of CPU work), C restatement oracle, "
+                      "sequential" % (k, args.config.upper(), 2 * args.requests, spent)}
+
+
+if __name__ == "__main__":
+    main()

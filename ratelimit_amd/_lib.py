@@ -1,0 +1,60 @@
+"""Loads the in-tree libratelimit_hip.so (the HIP product library) via ctypes.
+
+There is deliberately no fallback: if the library is missing or cannot be
+loaded, every entry point raises. Build it with ``python -m ratelimit_amd.build``.
+"""
+import ctypes as C
+import os
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libratelimit_hip.so")
+
+EXPORTS = ["rl_abi_version", "rl_create", "rl_destroy", "rl_last_error", "rl_do_limit", "rl_do_limit_async",
+           "rl_synchronize", "rl_sweep", "rl_restore", "rl_table_info_get", "rl_alloc_host", "rl_free_host",
+           "rl_debug_keys", "rl_debug_decide", "rl_profile", "rl_profile_read"]
+
+_lib = None
+
+
+class RedisError(RuntimeError):
+    """Mirror of redis.RedisError (src/redis/driver.go:6-10): backend failure."""
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libratelimit_hip.so not built (%s): run `python -m ratelimit_amd.build`" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    L.rl_abi_version.restype = C.c_uint32
+    L.rl_create.restype = C.c_void_p
+    L.rl_create.argtypes = [C.POINTER(abi.RlConfig), C.c_char_p, C.c_size_t]
+    L.rl_destroy.argtypes = [C.c_void_p]
+    L.rl_last_error.restype = C.c_char_p
+    L.rl_last_error.argtypes = [C.c_void_p]
+    L.rl_do_limit.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.POINTER(abi.RlResult)]
+    L.rl_do_limit_async.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.POINTER(abi.RlResult), C.c_void_p]
+    L.rl_synchronize.argtypes = [C.c_void_p]
+    L.rl_sweep.argtypes = [C.c_void_p, C.c_int64, C.POINTER(C.c_uint64)]
+    L.rl_restore.argtypes = [C.c_void_p, C.POINTER(abi.RlRestoreBatch)]
+    L.rl_table_info_get.argtypes = [C.c_void_p, C.POINTER(abi.RlTableInfo)]
+    L.rl_alloc_host.restype = C.c_void_p
+    L.rl_alloc_host.argtypes = [C.c_size_t]
+    L.rl_free_host.argtypes = [C.c_void_p]
+    L.rl_debug_keys.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.c_void_p, C.c_void_p, C.c_uint32]
+    L.rl_debug_decide.argtypes = [C.c_void_p, C.c_uint32] + [C.c_void_p] * 14
+    L.rl_profile.argtypes = [C.c_void_p, C.c_int]
+    L.rl_profile_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_uint32, C.POINTER(C.c_uint64)]
+    if L.rl_abi_version() != 1:
+        raise RuntimeError("libratelimit_hip.so ABI mismatch")
+    _lib = L
+    return L
+
+
+def check(ctx, rc):
+    if rc != 0:
+        msg = lib().rl_last_error(ctx).decode(errors="replace")
+        raise RedisError("%s [%s]" % (msg, abi.STATUS_NAMES.get(rc, rc)))

@@ -1,0 +1,517 @@
+// rl_api.hip — the extern "C" boundary of libratelimit_hip.so
+// (include/ratelimit_hip.h). Owns the HBM table, per-batch scratch and the
+// HIP stream; every entry point maps a device error word to an rl_status.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/ratelimit_hip.h"
+#include "rl_device.h"
+#include "rl_kernels.h"
+
+using namespace rl;
+
+struct rl_ctx {
+  rl_config cfg;
+  hipStream_t stream = nullptr;
+  // table
+  Slot* slots = nullptr;
+  uint64_t nslots = 0;
+  uint8_t* arena = nullptr;
+  uint64_t arena_cap16 = 0;
+  // scratch
+  Scratch s{};
+  // device staging for the host-buffer entry points
+  uint8_t* d_stem = nullptr;
+  uint32_t *d_off = nullptr, *d_req = nullptr, *d_limit = nullptr, *d_hits = nullptr, *d_rule = nullptr;
+  int64_t* d_now = nullptr;
+  uint8_t *d_unit = nullptr, *d_flags = nullptr, *d_code = nullptr;
+  uint32_t *d_rem = nullptr, *d_reset = nullptr;
+  unsigned long long* d_stats = nullptr;
+  uint32_t* h_err = nullptr;  // pinned
+  unsigned long long* h_counters = nullptr;
+  std::string last_error;
+  uint64_t batches = 0, decisions = 0;
+  // rl_profile: events of the in-flight timed batch, accumulated stage sums
+  bool prof = false;
+  bool prof_pending = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  double stage_ms[RL_NUM_STAGES] = {0, 0, 0};
+  uint64_t prof_batches = 0;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(rl_ctx* c, int code, const std::string& msg);
+
+// Fold the previous timed batch's events into the stage sums (waits for it).
+void prof_fold(rl_ctx* c) {
+  if (!c->prof_pending) return;
+  c->prof_pending = false;
+  if (hipEventSynchronize(c->ev[3]) != hipSuccess) return;
+  for (int i = 0; i < RL_NUM_STAGES; i++) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]) == hipSuccess) c->stage_ms[i] += ms;
+  }
+  c->prof_batches++;
+}
+
+hipEvent_t* prof_events(rl_ctx* c) {
+  if (!c->prof) return nullptr;
+  prof_fold(c);  // one batch in flight at a time per event set
+  c->prof_pending = true;
+  return c->ev;
+}
+
+int set_err(rl_ctx* c, int code, const std::string& msg) {
+  if (c) c->last_error = msg;
+  else g_err = msg;
+  return code;
+}
+
+#define HIPCHK(c, expr)                                                                        \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess)                                                                      \
+      return set_err((c), RL_E_HIP, std::string("gpu: ") + #expr + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+template <typename T>
+hipError_t dalloc(T** p, size_t count) {
+  return hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T));
+}
+
+int map_err(rl_ctx* c, uint32_t e) {
+  if (!e) return RL_OK;
+  if (e & ERR_TIME)
+    return set_err(c, RL_E_TIME, "gpu: now outside [0, 2^32-172800] or earlier than a previous request");
+  if (e & ERR_INVALID) return set_err(c, RL_E_INVALID, "gpu: malformed batch (unit, rule id, request index or stem offsets)");
+  if (e & ERR_TABLE_FULL) return set_err(c, RL_E_TABLE_FULL, "gpu: counter table full (raise table_slots or sweep)");
+  if (e & ERR_ARENA_FULL) return set_err(c, RL_E_ARENA_FULL, "gpu: long-stem arena full (raise arena_bytes)");
+  if (e & ERR_COLLISIONS) return set_err(c, RL_E_INTERNAL, "gpu: too many stems share one 32-bit hash prefix");
+  return set_err(c, RL_E_INTERNAL, "gpu: unknown device error");
+}
+
+// Read (and clear) the sticky device error word; synchronises the stream.
+int collect(rl_ctx* c) {
+  HIPCHK(c, hipMemcpyAsync(c->h_err, c->s.err, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint32_t e = *c->h_err;
+  if (e) HIPCHK(c, hipMemsetAsync(c->s.err, 0, sizeof(uint32_t), c->stream));
+  return map_err(c, e);
+}
+
+int check_sizes(rl_ctx* c, const rl_batch* in, uint64_t stem_bytes) {
+  if (!in) return set_err(c, RL_E_INVALID, "gpu: null batch");
+  if (in->n > c->cfg.max_batch || in->n_requests > c->cfg.max_requests || in->n_rules > c->cfg.max_rules ||
+      stem_bytes > c->cfg.max_stem_bytes)
+    return set_err(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_rules/max_stem_bytes");
+  if (in->n && in->n_requests == 0) return set_err(c, RL_E_INVALID, "gpu: descriptors without requests");
+  return RL_OK;
+}
+
+BatchDev dev_view(const rl_batch* in, uint32_t stem_cap) {
+  BatchDev b;
+  b.n = in->n;
+  b.n_req = in->n_requests;
+  b.n_rules = in->n_rules;
+  b.stem_cap = stem_cap;
+  b.stem = in->stem_bytes;
+  b.off = in->stem_off;
+  b.now = in->now;
+  b.req = in->req_idx;
+  b.unit = in->unit;
+  b.flags = in->flags;
+  b.limit = in->limit;
+  b.hits = in->hits;
+  b.rule = in->rule_id;
+  return b;
+}
+
+TableDev table_view(rl_ctx* c) {
+  TableDev t;
+  t.slots = c->slots;
+  t.mask = c->nslots - 1;
+  t.arena = c->arena;
+  t.arena_used16 = c->s.counters + 4;
+  t.arena_cap16 = c->arena_cap16;
+  t.max_probe = (uint32_t)std::min<uint64_t>(c->nslots, 1u << 16);
+  return t;
+}
+
+Params params(rl_ctx* c) {
+  Params P;
+  P.ratio = c->cfg.near_limit_ratio;
+  P.lc_en = c->cfg.local_cache_enabled != 0;
+  P.per_second = c->cfg.per_second_split != 0;
+  return P;
+}
+
+// Copy a host batch into the staging buffers; returns the device view.
+int stage(rl_ctx* c, const rl_batch* in, BatchDev* out) {
+  const uint32_t n = in->n, nq = in->n_requests;
+  const uint64_t nb = n ? in->stem_off[n] : 0;
+  int rc = check_sizes(c, in, nb);
+  if (rc) return rc;
+  hipStream_t st = c->stream;
+  if (nb) HIPCHK(c, hipMemcpyAsync(c->d_stem, in->stem_bytes, nb, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->d_off, in->stem_off, (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  if (nq) HIPCHK(c, hipMemcpyAsync(c->d_now, in->now, nq * sizeof(int64_t), hipMemcpyHostToDevice, st));
+  if (n) {
+    HIPCHK(c, hipMemcpyAsync(c->d_req, in->req_idx, n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->d_unit, in->unit, n, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->d_flags, in->flags, n, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->d_limit, in->limit, n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->d_hits, in->hits, n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->d_rule, in->rule_id, n * 4, hipMemcpyHostToDevice, st));
+  }
+  rl_batch d = *in;
+  d.stem_bytes = c->d_stem;
+  d.stem_off = c->d_off;
+  d.now = c->d_now;
+  d.req_idx = c->d_req;
+  d.unit = c->d_unit;
+  d.flags = c->d_flags;
+  d.limit = c->d_limit;
+  d.hits = c->d_hits;
+  d.rule_id = c->d_rule;
+  *out = dev_view(&d, c->cfg.max_stem_bytes);
+  return RL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t rl_abi_version(void) { return RL_ABI_VERSION; }
+
+const char* rl_last_error(const rl_ctx* c) { return c ? c->last_error.c_str() : g_err.c_str(); }
+
+rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
+  auto fail = [&](const std::string& m, rl_ctx* c) -> rl_ctx* {
+    if (err && errlen) snprintf(err, errlen, "%s", m.c_str());
+    g_err = m;
+    if (c) rl_destroy(c);
+    return nullptr;
+  };
+  if (!cfg_in) return fail("gpu: null config", nullptr);
+  rl_config cfg = *cfg_in;
+  if (!cfg.table_slots) cfg.table_slots = 1ull << 24;
+  if (cfg.table_slots & (cfg.table_slots - 1)) return fail("gpu: table_slots must be a power of two", nullptr);
+  if (!cfg.arena_bytes) cfg.arena_bytes = 64ull << 20;
+  if (!cfg.max_batch) cfg.max_batch = 1u << 20;
+  if (!cfg.max_requests) cfg.max_requests = cfg.max_batch;
+  if (!cfg.max_rules) cfg.max_rules = 65536;
+  if (!cfg.max_stem_bytes) cfg.max_stem_bytes = 128u * cfg.max_batch;
+  if (hipSetDevice(cfg.device) != hipSuccess) return fail("gpu: hipSetDevice failed", nullptr);
+
+  rl_ctx* c = new rl_ctx();
+  c->cfg = cfg;
+  c->nslots = cfg.table_slots;
+  c->arena_cap16 = cfg.arena_bytes / 16;
+  const uint32_t n = cfg.max_batch;
+  const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
+  bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
+  ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess;
+  ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess;
+  ok = ok && dalloc(&c->s.hstem, n) == hipSuccess;
+  for (int i = 0; i < 2; i++) {
+    ok = ok && dalloc(&c->s.keys[i], n) == hipSuccess;
+    ok = ok && dalloc(&c->s.vals[i], n) == hipSuccess;
+  }
+  ok = ok && dalloc(&c->s.hist, 256ull * std::max(ntiles, 1u)) == hipSuccess;
+  ok = ok && dalloc(&c->s.repid, n) == hipSuccess;
+  ok = ok && dalloc(&c->s.err, 1) == hipSuccess;
+  ok = ok && dalloc(&c->s.last_now, 1) == hipSuccess;
+  ok = ok && dalloc(&c->s.counters, 8) == hipSuccess;
+  ok = ok && dalloc(&c->d_stem, (size_t)cfg.max_stem_bytes + 64) == hipSuccess;
+  ok = ok && dalloc(&c->d_off, (size_t)n + 1) == hipSuccess;
+  ok = ok && dalloc(&c->d_now, cfg.max_requests) == hipSuccess;
+  ok = ok && dalloc(&c->d_req, n) == hipSuccess && dalloc(&c->d_unit, n) == hipSuccess &&
+       dalloc(&c->d_flags, n) == hipSuccess && dalloc(&c->d_limit, n) == hipSuccess &&
+       dalloc(&c->d_hits, n) == hipSuccess && dalloc(&c->d_rule, n) == hipSuccess;
+  ok = ok && dalloc(&c->d_code, n) == hipSuccess && dalloc(&c->d_rem, n) == hipSuccess &&
+       dalloc(&c->d_reset, n) == hipSuccess;
+  ok = ok && dalloc(&c->d_stats, (size_t)cfg.max_rules * RL_NUM_STATS) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_err, sizeof(uint32_t)) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_counters, 8 * sizeof(unsigned long long)) == hipSuccess;
+  if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
+  ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
+       hipMemsetAsync(c->s.err, 0, 4, c->stream) == hipSuccess &&
+       hipMemsetAsync(c->s.last_now, 0, 8, c->stream) == hipSuccess &&
+       hipMemsetAsync(c->s.counters, 0, 64, c->stream) == hipSuccess &&
+       hipMemsetAsync(c->d_stem, 0, (size_t)cfg.max_stem_bytes + 64, c->stream) == hipSuccess &&
+       hipStreamSynchronize(c->stream) == hipSuccess;
+  if (!ok) return fail("gpu: device initialisation failed", c);
+  return c;
+}
+
+void rl_destroy(rl_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->cfg.device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (int i = 0; i < 4; i++)
+    if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+  void* bufs[] = {c->slots, c->arena, c->s.hstem, c->s.keys[0], c->s.keys[1], c->s.vals[0], c->s.vals[1],
+                  c->s.hist, c->s.repid, c->s.err, c->s.last_now, c->s.counters, c->d_stem, c->d_off, c->d_now,
+                  c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_rem,
+                  c->d_reset, c->d_stats};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+  if (c->h_err) (void)hipHostFree(c->h_err);
+  if (c->h_counters) (void)hipHostFree(c->h_counters);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int rl_do_limit_async(rl_ctx* c, const rl_batch* in, rl_result* out, void* stream) {
+  if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  // device pointers: the total stem size is only known on the device; the
+  // kernels bound-check offsets against max_stem_bytes (stem_cap)
+  int rc = check_sizes(c, in, 0);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  if (in->n_rules) HIPCHK(c, hipMemsetAsync(out->stats, 0, (size_t)in->n_rules * RL_NUM_STATS * 8, st));
+  BatchDev b = dev_view(in, c->cfg.max_stem_bytes);
+  OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats};
+  launch_do_limit(b, o, table_view(c), params(c), c->s, 0, st, prof_events(c));
+  HIPCHK(c, hipGetLastError());
+  c->batches++;
+  c->decisions += in->n;
+  return RL_OK;
+}
+
+int rl_profile(rl_ctx* c, int enable) {
+  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (enable && !c->ev[0])
+    for (int i = 0; i < 4; i++) HIPCHK(c, hipEventCreate(&c->ev[i]));
+  prof_fold(c);
+  c->prof = enable != 0;
+  return RL_OK;
+}
+
+int rl_profile_read(rl_ctx* c, double* ms, uint32_t n, uint64_t* batches) {
+  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  prof_fold(c);
+  for (uint32_t i = 0; i < n && i < RL_NUM_STAGES; i++) ms[i] = c->stage_ms[i];
+  if (batches) *batches = c->prof_batches;
+  for (int i = 0; i < RL_NUM_STAGES; i++) c->stage_ms[i] = 0;
+  c->prof_batches = 0;
+  return RL_OK;
+}
+
+int rl_synchronize(rl_ctx* c) {
+  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, hipDeviceSynchronize());
+  return collect(c);
+}
+
+int rl_do_limit(rl_ctx* c, const rl_batch* in, rl_result* out) {
+  if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  BatchDev b;
+  int rc = stage(c, in, &b);
+  if (rc) return rc;
+  hipStream_t st = c->stream;
+  if (in->n_rules) HIPCHK(c, hipMemsetAsync(c->d_stats, 0, (size_t)in->n_rules * RL_NUM_STATS * 8, st));
+  OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats};
+  launch_do_limit(b, o, table_view(c), params(c), c->s, 0, st, prof_events(c));
+  HIPCHK(c, hipGetLastError());
+  const uint32_t n = in->n;
+  if (n) {
+    HIPCHK(c, hipMemcpyAsync(out->code, c->d_code, n, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(out->limit_remaining, c->d_rem, n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(out->reset_s, c->d_reset, n * 4, hipMemcpyDeviceToHost, st));
+  }
+  if (in->n_rules)
+    HIPCHK(c, hipMemcpyAsync(out->stats, c->d_stats, (size_t)in->n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost, st));
+  c->batches++;
+  c->decisions += n;
+  return collect(c);
+}
+
+int rl_restore(rl_ctx* c, const rl_restore_batch* r) {
+  if (!c || !r) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (!r->n) return RL_OK;
+  // A restore batch is a batch of SET records: req = record index, hits = count,
+  // flags = local-cache bit. It runs through the same grouping pipeline.
+  std::string* e = &c->last_error;
+  (void)e;
+  const uint32_t n = r->n;
+  uint32_t* req = new uint32_t[n];
+  uint32_t* zero = new uint32_t[n]();
+  uint8_t* lcf = new uint8_t[n]();
+  for (uint32_t i = 0; i < n; i++) {
+    req[i] = i;
+    if (r->lc) lcf[i] = r->lc[i] ? 1 : 0;
+  }
+  rl_batch in{};
+  in.n = n;
+  in.n_requests = n;
+  in.n_rules = 1;
+  in.stem_bytes = r->stem_bytes;
+  in.stem_off = r->stem_off;
+  in.now = r->now;
+  in.req_idx = req;
+  in.unit = r->unit;
+  in.flags = lcf;
+  in.limit = zero;
+  in.hits = r->count;
+  in.rule_id = zero;
+  BatchDev b;
+  int rc = stage(c, &in, &b);
+  if (!rc) {
+    OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats};
+    launch_do_limit(b, o, table_view(c), params(c), c->s, 1, c->stream);
+    hipError_t he = hipGetLastError();
+    rc = he != hipSuccess ? set_err(c, RL_E_HIP, std::string("gpu: ") + hipGetErrorString(he)) : collect(c);
+  }
+  delete[] req;
+  delete[] zero;
+  delete[] lcf;
+  return rc;
+}
+
+int rl_sweep(rl_ctx* c, int64_t now, uint64_t* n_evicted) {
+  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
+  if (now < 0 || now > (int64_t)NOW_MAX) return set_err(c, RL_E_TIME, "gpu: sweep time out of range");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  // later batches must not run at an earlier time than the sweep
+  int64_t last = 0;
+  HIPCHK(c, hipMemcpyAsync(&last, c->s.last_now, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (now > last) HIPCHK(c, hipMemcpyAsync(c->s.last_now, &now, 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->s.counters, 0, 8, c->stream));
+  launch_sweep(c->slots, c->nslots, (uint32_t)now, c->s.counters, c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s.counters, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (n_evicted) *n_evicted = c->h_counters[0];
+  return RL_OK;
+}
+
+int rl_table_info_get(rl_ctx* c, rl_table_info* info) {
+  if (!c || !info) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, hipMemsetAsync(c->s.counters, 0, 24, c->stream));
+  launch_table_info(c->slots, c->nslots, c->s.counters, c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s.counters, 40, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  info->table_slots = c->nslots;
+  info->live_slots = c->h_counters[0];
+  info->tombstones = c->h_counters[1];
+  info->exact_stems = c->h_counters[2];
+  info->arena_bytes_used = c->h_counters[4] * 16;
+  info->batches = c->batches;
+  info->decisions = c->decisions;
+  return RL_OK;
+}
+
+void* rl_alloc_host(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1) != hipSuccess) return nullptr;
+  return p;
+}
+
+void rl_free_host(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
+int rl_debug_keys(rl_ctx* c, const rl_batch* in, uint8_t* out_bytes, uint32_t* out_off, uint32_t out_cap) {
+  if (!c || !in || !out_off) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  BatchDev b;
+  int rc = stage(c, in, &b);
+  if (rc) return rc;
+  const uint32_t n = in->n;
+  const size_t cap = (size_t)(n ? in->stem_off[n] : 0) + 24ull * n + 1;
+  uint8_t* d_out = nullptr;
+  uint32_t* d_len = nullptr;
+  HIPCHK(c, dalloc(&d_out, cap));
+  HIPCHK(c, dalloc(&d_len, (size_t)n + 1));
+  launch_debug_keys(b, d_out, d_len, c->stream);
+  uint8_t* h_out = new uint8_t[cap];
+  uint32_t* h_len = new uint32_t[n + 1];
+  hipError_t e1 = hipMemcpyAsync(h_out, d_out, cap, hipMemcpyDeviceToHost, c->stream);
+  hipError_t e2 = hipMemcpyAsync(h_len, d_len, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream);
+  hipError_t e3 = hipStreamSynchronize(c->stream);
+  (void)hipFree(d_out);
+  (void)hipFree(d_len);
+  rc = (e1 || e2 || e3) ? set_err(c, RL_E_HIP, "gpu: debug_keys copy failed") : RL_OK;
+  uint32_t pos = 0;
+  out_off[0] = 0;
+  for (uint32_t i = 0; i < n && rc == RL_OK; i++) {
+    if (pos + h_len[i] > out_cap) {
+      rc = set_err(c, RL_E_CAPACITY, "gpu: debug_keys output buffer too small");
+      break;
+    }
+    memcpy(out_bytes + pos, h_out + in->stem_off[i] + 24ull * i, h_len[i]);
+    pos += h_len[i];
+    out_off[i + 1] = pos;
+  }
+  delete[] h_out;
+  delete[] h_len;
+  return rc;
+}
+
+int rl_debug_decide(rl_ctx* c, uint32_t n, const uint32_t* before, const uint32_t* after, const uint8_t* lc_hit,
+                    const uint32_t* hits, const uint32_t* limit, const uint8_t* unit, const uint8_t* flags,
+                    const int64_t* now, uint8_t* code, uint32_t* remaining, uint32_t* reset_s,
+                    uint64_t* stat_deltas, uint8_t* lc_set) {
+  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
+  if (!n) return RL_OK;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  for (uint32_t i = 0; i < n; i++)
+    if (unit[i] < 1 || unit[i] > 4) return set_err(c, RL_E_INVALID, "gpu: unit out of range");
+  uint32_t *d_b, *d_a, *d_h, *d_l, *d_rem, *d_rs;
+  uint8_t *d_lc, *d_u, *d_f, *d_code, *d_set;
+  int64_t* d_now;
+  unsigned long long* d_del;
+  HIPCHK(c, dalloc(&d_b, n));
+  HIPCHK(c, dalloc(&d_a, n));
+  HIPCHK(c, dalloc(&d_h, n));
+  HIPCHK(c, dalloc(&d_l, n));
+  HIPCHK(c, dalloc(&d_rem, n));
+  HIPCHK(c, dalloc(&d_rs, n));
+  HIPCHK(c, dalloc(&d_lc, n));
+  HIPCHK(c, dalloc(&d_u, n));
+  HIPCHK(c, dalloc(&d_f, n));
+  HIPCHK(c, dalloc(&d_code, n));
+  HIPCHK(c, dalloc(&d_set, n));
+  HIPCHK(c, dalloc(&d_now, n));
+  HIPCHK(c, dalloc(&d_del, (size_t)n * RL_NUM_STATS));
+  hipStream_t st = c->stream;
+  HIPCHK(c, hipMemcpyAsync(d_b, before, n * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(d_a, after, n * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(d_h, hits, n * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(d_l, limit, n * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(d_lc, lc_hit, n, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(d_u, unit, n, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(d_f, flags, n, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(d_now, now, n * 8, hipMemcpyHostToDevice, st));
+  launch_debug_decide(n, d_b, d_a, d_lc, d_h, d_l, d_u, d_f, d_now, c->cfg.near_limit_ratio,
+                      c->cfg.local_cache_enabled, d_code, d_rem, d_rs, d_del, d_set, st);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(code, d_code, n, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(remaining, d_rem, n * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(reset_s, d_rs, n * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(stat_deltas, d_del, (size_t)n * RL_NUM_STATS * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(lc_set, d_set, n, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  void* bufs[] = {d_b, d_a, d_h, d_l, d_rem, d_rs, d_lc, d_u, d_f, d_code, d_set, d_now, d_del};
+  for (void* p : bufs) (void)hipFree(p);
+  return RL_OK;
+}
+
+}  // extern "C"

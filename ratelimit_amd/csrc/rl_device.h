@@ -1,0 +1,152 @@
+// rl_device.h — HBM table layout, hashing and the per-descriptor decision
+// function shared by every kernel of libratelimit_hip.so (gfx950).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ratelimit_hip.h"
+
+namespace rl {
+
+// ---------------------------------------------------------------------------
+// HBM counter table.
+//
+// One slot per (stem, unit). The Redis key of the reference is
+// stem ‖ decimal(windowStart) (cache_key.go:62-74); a slot holds the state of
+// the last two window keys of its (stem, unit): `cur` and `prev`.  For a stem
+// used with a single unit the current window is the only live key, so the slot
+// is recycled in place when the window advances (no insert per window, no
+// EXPIRE traffic).  `prev` exists so that a stem later seen with a second unit
+// (only possible through per-request overrides, config_impl.go:254-265) can
+// reproduce Redis key sharing exactly (DESIGN.md §"Exact key identity").
+// ---------------------------------------------------------------------------
+constexpr uint32_t WS_INVALID = 0xFFFFFFFFu;  // record never written
+constexpr uint64_t TAG_EMPTY = 0;
+constexpr uint64_t TAG_TOMB = 1;
+constexpr uint32_t INLINE_KEY = 80;           // stem bytes stored in the slot
+constexpr uint8_t SLOT_EXACT = 0x1;           // stem has >1 unit slot: exact (serial) path
+
+struct __attribute__((aligned(16))) Win {
+  uint32_t ws;      // window start (Redis key suffix); WS_INVALID = no record
+  uint32_t count;   // INCRBY value (u32, radix decodes into *uint32)
+  uint32_t expire;  // Redis key live while now <= expire (EXPIRE = now + div)
+  uint32_t lc;      // freecache entry live while now < lc (Set ttl = div)
+};
+
+struct __attribute__((aligned(128))) Slot {
+  uint64_t tag;       // TAG_EMPTY / TAG_TOMB / mix(hash(stem), unit) >= 2
+  uint16_t key_len;   // stem length
+  uint8_t unit;       // rl_unit
+  uint8_t flags;      // SLOT_EXACT
+  uint32_t ext_off;   // arena offset in 16-B units for bytes >= INLINE_KEY
+  Win cur;
+  Win prev;
+  uint8_t key[INLINE_KEY];
+};
+static_assert(sizeof(Slot) == 128, "slot must be one 128-B line");
+
+__host__ __device__ inline uint32_t div_of(uint32_t unit) {  // utils.UnitToDivider
+  return unit == RL_UNIT_SECOND ? 1u : unit == RL_UNIT_MINUTE ? 60u : unit == RL_UNIT_HOUR ? 3600u : 86400u;
+}
+
+__host__ __device__ inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+
+__host__ __device__ inline uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33; k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+// 64-bit stem hash: one 8-byte little-endian word per round (bytes past the end = 0).
+struct StemHasher {
+  uint64_t h;
+  __host__ __device__ explicit StemHasher(uint32_t len) : h(0x9E3779B97F4A7C15ull ^ (uint64_t(len) * 0xC2B2AE3D27D4EB4Full)) {}
+  __host__ __device__ inline void word(uint64_t w) {
+    uint64_t k = w * 0x87c37b91114253d5ull;
+    k = rotl64(k, 31) * 0x4cf5ad432745937full;
+    h ^= k;
+    h = rotl64(h, 27) * 5 + 0x52dce729ull;
+  }
+  __host__ __device__ inline uint64_t finish() const {
+    uint64_t x = fmix64(h);
+    return x ? x : 1;
+  }
+};
+
+__host__ __device__ inline uint64_t slot_tag(uint64_t hstem, uint32_t unit) {
+  uint64_t t = fmix64(hstem + uint64_t(unit) * 0x9E3779B97F4A7C15ull);
+  return t < 2 ? t + 2 : t;
+}
+
+// ---------------------------------------------------------------------------
+// GetResponseDescriptorStatus (base_limiter.go:76-135) for a non-empty key,
+// including checkOverLimitThreshold / checkNearLimitThreshold (:150-179).
+// All arithmetic in uint32 like the Go code, widened to u64 for the counters.
+// ---------------------------------------------------------------------------
+struct Decision {
+  uint8_t code;
+  uint8_t set_lc;
+  uint32_t remaining;
+  uint32_t d_over, d_near, d_lc, d_within, d_shadow;
+};
+
+// uint32(math.Floor(float64(float32(limit) * ratio))): a single IEEE fp32
+// multiply (no FMA contraction), then Go's uint32(float64) = low 32 bits of a
+// truncating int64 conversion (0x8000000000000000 when out of range).
+__host__ __device__ inline uint32_t near_threshold(uint32_t limit, float ratio) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  float prod = __fmul_rn((float)limit, ratio);
+#else
+  volatile float prod = (float)limit * ratio;
+#endif
+  double f = floor((double)prod);
+  int64_t v = (f >= -9223372036854775808.0 && f < 9223372036854775808.0) ? (int64_t)f : INT64_MIN;
+  return (uint32_t)v;
+}
+
+__host__ __device__ inline Decision decide(uint32_t before, uint32_t after, bool lc_hit, uint32_t h,
+                                           uint32_t thr, float ratio, bool shadow, bool lc_enabled) {
+  Decision r = {RL_CODE_OK, 0, 0, 0, 0, 0, 0, 0};
+  bool over = false;
+  if (lc_hit) {
+    over = true;
+    r.d_over = h; r.d_lc = h; r.code = RL_CODE_OVER_LIMIT;
+  } else {
+    uint32_t near = near_threshold(thr, ratio);
+    if (after > thr) {
+      over = true;
+      r.code = RL_CODE_OVER_LIMIT;
+      if (before >= thr) {
+        r.d_over = h;
+      } else {
+        r.d_over = after - thr;
+        r.d_near = thr - (near > before ? near : before);
+      }
+      r.set_lc = lc_enabled ? 1 : 0;
+    } else {
+      r.remaining = thr - after;
+      if (after > near) r.d_near = (before >= near) ? h : after - near;
+      r.d_within = h;
+    }
+  }
+  if (over && shadow) {
+    r.code = RL_CODE_OK;
+    r.d_shadow = h;
+  }
+  return r;
+}
+
+// Device error word bits (mapped to rl_status by the host).
+enum : uint32_t {
+  ERR_INVALID = 1u << 0,
+  ERR_TABLE_FULL = 1u << 1,
+  ERR_ARENA_FULL = 1u << 2,
+  ERR_TIME = 1u << 3,
+  ERR_COLLISIONS = 1u << 4,  // more than MAX_REPS distinct stems in one hash run
+};
+
+constexpr uint32_t NOW_MAX = 0xFFFFFFFFu - 2u * 86400u;  // now + 2*div must fit u32
+
+}  // namespace rl

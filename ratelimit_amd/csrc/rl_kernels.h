@@ -1,0 +1,75 @@
+// rl_kernels.h — device-side views of a batch / the table and the kernel entry
+// points of rl_kernels.hip (launched from rl_api.hip through the wrappers).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rl_device.h"
+
+namespace rl {
+
+constexpr uint32_t RS_ITEMS = 16;
+constexpr uint32_t RS_TILE = 256 * RS_ITEMS;
+
+struct BatchDev {
+  uint32_t n, n_req, n_rules, stem_cap;
+  const uint8_t* stem;
+  const uint32_t* off;
+  const int64_t* now;
+  const uint32_t* req;
+  const uint8_t* unit;
+  const uint8_t* flags;
+  const uint32_t* limit;
+  const uint32_t* hits;
+  const uint32_t* rule;
+};
+
+struct OutDev {
+  uint8_t* code;
+  uint32_t* rem;
+  uint32_t* reset;
+  unsigned long long* stats;
+};
+
+struct TableDev {
+  Slot* slots;
+  uint64_t mask;
+  uint8_t* arena;
+  unsigned long long* arena_used16;
+  uint64_t arena_cap16;
+  uint32_t max_probe;
+};
+
+struct Params {
+  float ratio;
+  int lc_en;
+  int per_second;
+};
+
+// Per-batch scratch (device), sized for max_batch.
+struct Scratch {
+  uint64_t* hstem;
+  uint32_t* keys[2];
+  uint32_t* vals[2];
+  uint32_t* hist;
+  uint8_t* repid;
+  uint32_t* err;
+  int64_t* last_now;
+  unsigned long long* counters;  // [0..3] sweep / info outputs
+};
+
+// Launch the whole DoLimit pipeline (restore = 1: table seeding records).
+// ev (optional, 4 events): recorded before k_prepare, after it, after the
+// sort and after k_runs on stream st (per-stage timing, rl_profile).
+void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
+                     int restore, hipStream_t st, hipEvent_t* ev = nullptr);
+void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st);
+void launch_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out, hipStream_t st);
+void launch_debug_keys(const BatchDev& b, uint8_t* out, uint32_t* klen, hipStream_t st);
+void launch_debug_decide(uint32_t n, const uint32_t* before, const uint32_t* after, const uint8_t* lc_hit,
+                         const uint32_t* hits, const uint32_t* limit, const uint8_t* unit, const uint8_t* flags,
+                         const int64_t* now, float ratio, int lc_en, uint8_t* code, uint32_t* rem, uint32_t* reset,
+                         unsigned long long* deltas, uint8_t* lc_set, hipStream_t st);
+
+}  // namespace rl

@@ -1,0 +1,754 @@
+// rl_kernels.hip — gfx950 kernels of the fixed-window rate-limit backend.
+//
+// Pipeline for one batch (all on one HIP stream, inputs already in HBM):
+//   k_prepare     validate the packed batch; hash every stem (LDS-staged bytes)
+//   radix sort    stable LSD sort of (hash[63:32], index): groups each stem's
+//                 descriptors together, in arrival (sequence) order
+//   k_runs        one lane per same-hash run = one stem (hash ties split
+//                 exactly by byte compare): find-or-insert the (stem, unit)
+//                 slot in the HBM table and replay the run in order — the
+//                 reference's sequential INCRBY/EXPIRE/local-cache semantics
+//   k_finish      record the batch's last `now` (time must not go backwards)
+// plus k_sweep (epoch sweep = Redis EXPIRE), k_table_info, debug kernels.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rl_device.h"
+#include "rl_kernels.h"
+
+namespace rl {
+
+// ===========================================================================
+// k_prepare: validation + stem hashing.
+// Each 256-thread block stages the contiguous byte range of its 256 stems in
+// LDS with coalesced dword loads, then every lane hashes its own stem from LDS.
+// ===========================================================================
+constexpr uint32_t HASH_LDS_BYTES = 16384;
+
+template <typename Rd>
+__device__ inline uint64_t hash_stem(Rd rd, uint32_t a, uint32_t len) {
+  StemHasher hs(len);
+  uint32_t i = 0;
+  for (; i + 8 <= len; i += 8) hs.word(rd(a + i));
+  if (i < len) {
+    uint32_t rem = len - i;
+    uint64_t w = rd(a + i) & ((rem == 8) ? ~0ull : ((1ull << (rem * 8)) - 1));
+    hs.word(w);
+  }
+  return hs.finish();
+}
+
+// 8 bytes starting at byte address a of a dword array (little-endian); dwords
+// at index >= nw read as 0 (no access past the stem buffer).
+struct DwordReader {
+  const uint32_t* p;
+  uint32_t nw;
+  __device__ inline uint32_t at(uint32_t i) const { return i < nw ? p[i] : 0u; }
+  __device__ inline uint64_t operator()(uint32_t a) const {
+    uint32_t idx = a >> 2, sh = (a & 3) * 8;
+    uint64_t lo = at(idx), mid = at(idx + 1);
+    uint64_t x = lo | (mid << 32);
+    if (sh) x = (x >> sh) | (uint64_t(at(idx + 2)) << (64 - sh));
+    return x;
+  }
+};
+
+__global__ __launch_bounds__(256) void k_prepare(BatchDev b, uint64_t* __restrict__ hstem,
+                                                 uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                 uint32_t* err, const int64_t* last_now, int check_order) {
+  __shared__ uint32_t lds[HASH_LDS_BYTES / 4 + 4];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t i = blockIdx.x * 256 + tid;
+  uint32_t bad = 0;
+
+  // ---- per-request clock checks: now in [0, NOW_MAX], non-decreasing (also across batches)
+  if (i < b.n_req) {
+    int64_t t = b.now[i];
+    int64_t prev = i ? b.now[i - 1] : *last_now;
+    if (t < 0 || t > (int64_t)NOW_MAX || (check_order && t < prev)) bad |= ERR_TIME;
+  }
+
+  // ---- per-descriptor checks
+  uint32_t s0 = 0, len = 0;
+  if (i < b.n) {
+    s0 = b.off[i];
+    uint32_t s1 = b.off[i + 1];
+    uint32_t u = b.unit[i];
+    if (u < 1 || u > 4 || b.rule[i] >= b.n_rules || b.req[i] >= b.n_req || (i && b.req[i - 1] > b.req[i]) ||
+        s1 < s0 || s1 > b.stem_cap || s1 - s0 == 0 || s1 - s0 > 65535)
+      bad |= ERR_INVALID;
+    else
+      len = s1 - s0;
+  }
+  if (bad) atomicOr(err, bad);
+
+  // ---- stage this block's stem bytes in LDS (uniform decision per block)
+  const uint32_t b0 = blockIdx.x * 256;
+  if (b0 >= b.n) return;  // whole block past the descriptors (request checks done)
+  const uint32_t b1 = min(b0 + 256u, b.n);
+  uint32_t lo = b.off[b0], hi = b.off[b1];
+  bool range_ok = hi >= lo && hi <= b.stem_cap;
+  const uintptr_t base_addr = (uintptr_t)(b.stem + lo) & ~uintptr_t(3);
+  const uint32_t lead = (uint32_t)((uintptr_t)(b.stem + lo) - base_addr);
+  const uint32_t nbytes = range_ok ? hi - lo + lead : 0;
+  const bool use_lds = range_ok && nbytes + 8 <= HASH_LDS_BYTES;
+  if (use_lds) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(base_addr);
+    const uint32_t nw = (nbytes + 3) / 4;
+    for (uint32_t w = tid; w < nw; w += 256) lds[w] = src[w];
+    if (tid < 4) lds[nw + tid] = 0;
+  }
+  __syncthreads();
+  if (i >= b.n) return;
+  uint64_t h = 0;
+  if (len) {
+    if (use_lds) {
+      h = hash_stem(DwordReader{lds, HASH_LDS_BYTES / 4 + 4}, s0 - lo + lead, len);
+    } else {
+      const uintptr_t a = (uintptr_t)(b.stem + s0);
+      const uintptr_t ab = a & ~uintptr_t(3);
+      const uint32_t nw = (uint32_t)(((uintptr_t)(b.stem + s0 + len) - ab + 3) / 4);
+      h = hash_stem(DwordReader{reinterpret_cast<const uint32_t*>(ab), nw}, (uint32_t)(a - ab), len);
+    }
+  }
+  hstem[i] = h;
+  keys[i] = (uint32_t)(h >> 32);
+  vals[i] = i;
+}
+
+// ===========================================================================
+// Stable LSD radix sort of (u32 key, u32 value), 8-bit digits, 256-thread
+// tiles of RS_ITEMS x 256 elements. Per pass: tile histograms -> one exclusive
+// scan (digit-major) -> stable scatter. Ranks inside a wave come from 8
+// ballots (peer mask per digit); across the 4 waves of a tile from LDS counts.
+// ===========================================================================
+__global__ __launch_bounds__(256) void k_rs_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t shift,
+                                                 uint32_t ntiles, uint32_t* __restrict__ hist, const uint32_t* err) {
+  __shared__ uint32_t h[256];
+  if (*err) return;
+  const uint32_t tid = threadIdx.x;
+  h[tid] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * RS_TILE;
+#pragma unroll 4
+  for (uint32_t c = 0; c < RS_ITEMS; c++) {
+    uint32_t j = base + c * 256 + tid;
+    if (j < n) atomicAdd(&h[(keys[j] >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  hist[tid * ntiles + blockIdx.x] = h[tid];
+}
+
+// Exclusive scan of len u32 in place, one 1024-thread block.
+__global__ __launch_bounds__(1024) void k_scan_u32(uint32_t* __restrict__ a, uint32_t len, const uint32_t* err) {
+  __shared__ uint32_t part[1024];
+  if (*err) return;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t chunk = (len + 1023) / 1024;
+  const uint32_t s = tid * chunk, e = min(s + chunk, len);
+  uint32_t sum = 0;
+  for (uint32_t j = s; j < e; j++) sum += a[j];
+  part[tid] = sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    uint32_t v = tid >= off ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[tid] - sum;
+  for (uint32_t j = s; j < e; j++) {
+    uint32_t v = a[j];
+    a[j] = run;
+    run += v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                    uint32_t n, uint32_t shift, uint32_t ntiles,
+                                                    const uint32_t* __restrict__ hist, const uint32_t* err) {
+  __shared__ uint32_t gbase[256], lbase[256], wcnt[4][256];
+  if (*err) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  gbase[tid] = hist[tid * ntiles + blockIdx.x];
+  lbase[tid] = 0;
+  const uint64_t lt_mask = (1ull << lane) - 1;
+  const uint32_t base = blockIdx.x * RS_TILE;
+  for (uint32_t c = 0; c < RS_ITEMS; c++) {
+    const uint32_t j = base + c * 256 + tid;
+    const bool valid = j < n;
+    const uint32_t k = valid ? kin[j] : 0u;
+    const uint32_t v = valid ? vin[j] : 0u;
+    const uint32_t d = (k >> shift) & 255u;
+    wcnt[0][tid] = 0; wcnt[1][tid] = 0; wcnt[2][tid] = 0; wcnt[3][tid] = 0;
+    __syncthreads();
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (uint32_t bit = 0; bit < 8; bit++) {
+      const bool s = (d >> bit) & 1u;
+      const uint64_t bal = __ballot(s);
+      peers &= s ? bal : ~bal;
+    }
+    const uint32_t rank = __popcll(peers & lt_mask);
+    if (valid && rank == 0) wcnt[wave][d] = __popcll(peers);
+    __syncthreads();
+    uint32_t tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 4; w++) {
+      uint32_t t = wcnt[w][tid];
+      wcnt[w][tid] = tot;
+      tot += t;
+    }
+    __syncthreads();
+    if (valid) {
+      const uint32_t pos = gbase[d] + lbase[d] + wcnt[wave][d] + rank;
+      kout[pos] = k;
+      vout[pos] = v;
+    }
+    __syncthreads();
+    lbase[tid] += tot;
+  }
+}
+
+// ===========================================================================
+// HBM table probing.
+// ===========================================================================
+__device__ inline bool stems_equal(const uint8_t* a, const uint8_t* b, uint32_t len) {
+  for (uint32_t i = 0; i < len; i++)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+__device__ inline bool slot_key_equal(const Slot* s, const uint8_t* stem, uint32_t len, const uint8_t* arena) {
+  if (s->key_len != len) return false;
+  const uint32_t il = len < INLINE_KEY ? len : INLINE_KEY;
+  if (!stems_equal(s->key, stem, il)) return false;
+  if (len > INLINE_KEY) return stems_equal(arena + (size_t)s->ext_off * 16, stem + INLINE_KEY, len - INLINE_KEY);
+  return true;
+}
+
+__device__ inline void slot_init(const TableDev& t, Slot* s, const uint8_t* stem, uint32_t len, uint32_t unit,
+                                 uint32_t* err) {
+  s->key_len = (uint16_t)len;
+  s->unit = (uint8_t)unit;
+  s->flags = 0;
+  s->ext_off = 0;
+  const uint32_t il = len < INLINE_KEY ? len : INLINE_KEY;
+  for (uint32_t i = 0; i < il; i++) s->key[i] = stem[i];
+  if (len > INLINE_KEY) {
+    const uint32_t n16 = (len - INLINE_KEY + 15) / 16;
+    unsigned long long off = atomicAdd(t.arena_used16, (unsigned long long)n16);
+    if (off + n16 > t.arena_cap16) {
+      atomicOr(err, ERR_ARENA_FULL);
+    } else {
+      s->ext_off = (uint32_t)off;
+      uint8_t* dst = t.arena + off * 16;
+      for (uint32_t i = INLINE_KEY; i < len; i++) dst[i - INLINE_KEY] = stem[i];
+    }
+  }
+  s->cur = Win{WS_INVALID, 0, 0, 0};
+  s->prev = Win{WS_INVALID, 0, 0, 0};
+}
+
+// Find (and optionally insert) the slot of (stem, unit). Returns -1 when absent
+// and insert == false, or on a full table (error bit set).
+__device__ int64_t find_slot(const TableDev& t, uint64_t tag, const uint8_t* stem, uint32_t len, uint32_t unit,
+                             bool insert, bool* inserted, uint32_t* err) {
+  uint64_t i = tag & t.mask;
+  int64_t tomb = -1;
+  *inserted = false;
+  for (uint32_t p = 0; p < t.max_probe; p++, i = (i + 1) & t.mask) {
+    Slot* s = &t.slots[i];
+    const uint64_t st = __hip_atomic_load(&s->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (st == tag) {
+      if (slot_key_equal(s, stem, len, t.arena)) return (int64_t)i;
+      continue;
+    }
+    if (st == TAG_TOMB) {
+      if (tomb < 0) tomb = (int64_t)i;
+      continue;
+    }
+    if (st != TAG_EMPTY) continue;
+    // (stem, unit) is absent: claim the first tombstone on the path, else this slot.
+    if (!insert) return -1;
+    if (tomb >= 0) {
+      Slot* ts = &t.slots[tomb];
+      if (atomicCAS((unsigned long long*)&ts->tag, (unsigned long long)TAG_TOMB, (unsigned long long)tag) ==
+          TAG_TOMB) {
+        slot_init(t, ts, stem, len, unit, err);
+        *inserted = true;
+        return tomb;
+      }
+    }
+    const unsigned long long prev =
+        atomicCAS((unsigned long long*)&s->tag, (unsigned long long)TAG_EMPTY, (unsigned long long)tag);
+    if (prev == TAG_EMPTY) {
+      slot_init(t, s, stem, len, unit, err);
+      *inserted = true;
+      return (int64_t)i;
+    }
+    // another stem claimed this slot concurrently: keep probing
+  }
+  atomicOr(err, ERR_TABLE_FULL);
+  return -1;
+}
+
+// ===========================================================================
+// k_runs: replay each stem's descriptors in arrival order.
+//
+// Per descriptor (fixed_cache_impl.go:33-113, base_limiter.go:45-197):
+//   h = max(1, HitsAddend); TotalHits += h
+//   local-cache check against the state BEFORE this request's statuses
+//   (all of a request's checks precede its INCRBYs; its Sets follow them)
+//   hit & !shadow -> OVER via local cache, no INCRBY
+//   hit &  shadow -> no INCRBY, after = 0 (quirk: OK with the full limit)
+//   else          -> INCRBY (a key past its EXPIRE reads 0), EXPIRE = now+div
+//   status + stats (decide), localCache.Set(key, div) when over.
+// ===========================================================================
+constexpr uint32_t LDS_RULES = 512;
+constexpr uint32_t MAX_REPS = 8;
+
+struct StatAcc {
+  unsigned long long* lds;  // LDS_RULES * RL_NUM_STATS, or null
+  unsigned long long* glob;
+  __device__ inline void add(uint32_t rule, uint32_t which, uint32_t v) {
+    if (!v) return;
+    if (lds) atomicAdd(&lds[rule * RL_NUM_STATS + which], (unsigned long long)v);
+    else atomicAdd(&glob[(size_t)rule * RL_NUM_STATS + which], (unsigned long long)v);
+  }
+};
+
+struct Elem {
+  uint32_t e, req, now, unit, d, w, h, thr, rule;
+  bool shadow;
+};
+
+__device__ inline Elem load_elem(const BatchDev& b, uint32_t e, bool restore) {
+  Elem x;
+  x.e = e;
+  x.req = b.req[e];
+  x.now = (uint32_t)b.now[x.req];
+  x.unit = b.unit[e];
+  x.d = div_of(x.unit);
+  x.w = x.now - x.now % x.d;
+  const uint32_t hv = b.hits[e];
+  x.h = restore ? hv : (hv > 1 ? hv : 1u);  // utils.Max(1, HitsAddend)
+  x.thr = b.limit[e];
+  x.rule = b.rule[e];
+  x.shadow = (b.flags[e] & RL_FLAG_SHADOW) != 0;
+  return x;
+}
+
+__device__ inline void emit(const OutDev& o, StatAcc& acc, const Elem& x, const Decision& r) {
+  o.code[x.e] = r.code;
+  o.rem[x.e] = r.remaining;
+  o.reset[x.e] = x.d - x.now % x.d;  // utils.CalculateReset
+  acc.add(x.rule, RL_STAT_TOTAL_HITS, x.h);
+  acc.add(x.rule, RL_STAT_OVER_LIMIT, r.d_over);
+  acc.add(x.rule, RL_STAT_NEAR_LIMIT, r.d_near);
+  acc.add(x.rule, RL_STAT_OVER_LIMIT_WITH_LOCAL_CACHE, r.d_lc);
+  acc.add(x.rule, RL_STAT_WITHIN_LIMIT, r.d_within);
+  acc.add(x.rule, RL_STAT_SHADOW_MODE, r.d_shadow);
+}
+
+// ---- single (stem, unit) slot, stem never seen with another unit: registers only
+struct SimpleState {
+  Win cur, prev;
+  uint32_t cur_req;
+  bool pend;
+  uint32_t pend_w, pend_e;
+  __device__ inline void apply_pending() {
+    if (pend) {
+      if (cur.ws == pend_w) cur.lc = pend_e;
+      else if (prev.ws == pend_w) prev.lc = pend_e;
+      pend = false;
+    }
+  }
+};
+
+__device__ inline void simple_step(const Params& P, const OutDev& o, StatAcc& acc, SimpleState& S, const Elem& x,
+                                   bool restore, uint8_t restore_lc) {
+  if (x.req != S.cur_req) {
+    S.apply_pending();
+    S.cur_req = x.req;
+  }
+  if (restore) {
+    if (S.cur.ws != x.w) {
+      S.prev = S.cur;
+      S.cur = Win{x.w, 0, 0, 0};
+    }
+    S.cur.count = x.h;
+    S.cur.expire = x.now + x.d;
+    if (restore_lc) S.cur.lc = x.now + x.d;
+    return;
+  }
+  const bool lc_hit = P.lc_en && ((S.cur.ws == x.w && x.now < S.cur.lc) || (S.prev.ws == x.w && x.now < S.prev.lc));
+  uint32_t after = 0;
+  if (!lc_hit) {
+    uint32_t v = 0;
+    if (S.cur.ws == x.w) {
+      if (x.now <= S.cur.expire) v = S.cur.count;
+    } else {
+      S.prev = S.cur;
+      S.cur = Win{x.w, 0, 0, 0};
+    }
+    S.cur.count = v + x.h;
+    S.cur.expire = x.now + x.d;
+    after = S.cur.count;
+  }
+  const Decision r = decide(after - x.h, after, lc_hit && !x.shadow, x.h, x.thr, P.ratio, x.shadow, P.lc_en);
+  if (r.set_lc) {
+    S.pend = true;
+    S.pend_w = x.w;
+    S.pend_e = x.now + x.d;
+  }
+  emit(o, acc, x, r);
+}
+
+// ---- general: every unit slot of the stem, Redis keys shared across units
+struct GeneralState {
+  int64_t sidx[4];
+  Win cur[4], prev[4];
+  uint32_t present;  // bit u-1
+  uint32_t cur_req;
+  uint32_t npend;
+  uint32_t pend_w[4], pend_e[4];
+};
+
+__device__ inline bool ps_class(const Params& P, uint32_t k) { return P.per_second && k == 0; }
+
+__device__ inline void general_apply_pending(GeneralState& G) {
+  for (uint32_t j = 0; j < G.npend; j++) {
+    for (uint32_t k = 0; k < 4; k++) {
+      if (!(G.present >> k & 1)) continue;
+      if (G.cur[k].ws == G.pend_w[j]) G.cur[k].lc = G.pend_e[j];
+      if (G.prev[k].ws == G.pend_w[j]) G.prev[k].lc = G.pend_e[j];
+    }
+  }
+  G.npend = 0;
+}
+
+__device__ inline void general_step(const Params& P, const OutDev& o, StatAcc& acc, GeneralState& G, const Elem& x,
+                                    bool restore, uint8_t restore_lc) {
+  if (x.req != G.cur_req) {
+    general_apply_pending(G);
+    G.cur_req = x.req;
+  }
+  const uint32_t ui = x.unit - 1;
+  const bool ps_e = ps_class(P, ui);
+  bool lc_hit = false;
+  uint32_t v = 0, lcw = 0;
+  bool vfound = false;
+  for (uint32_t k = 0; k < 4; k++) {
+    if (!(G.present >> k & 1)) continue;
+    const Win* recs[2] = {&G.cur[k], &G.prev[k]};
+    for (uint32_t r = 0; r < 2; r++) {
+      const Win& R = *recs[r];
+      if (R.ws != x.w) continue;
+      if (x.now < R.lc) lc_hit = true;
+      lcw = R.lc > lcw ? R.lc : lcw;
+      if (ps_class(P, k) == ps_e && !vfound && x.now <= R.expire) {
+        v = R.count;
+        vfound = true;
+      }
+    }
+  }
+  lc_hit = lc_hit && P.lc_en && !restore;
+  uint32_t after = 0;
+  if (!lc_hit) {
+    const uint32_t nv = restore ? x.h : v + x.h;
+    const uint32_t ex = x.now + x.d;
+    if (G.cur[ui].ws != x.w) {
+      G.prev[ui] = G.cur[ui];
+      G.cur[ui] = Win{x.w, 0, 0, lcw};
+    }
+    for (uint32_t k = 0; k < 4; k++) {  // Redis key stem‖w in this store: every alias record
+      if (!(G.present >> k & 1) || ps_class(P, k) != ps_e) continue;
+      if (G.cur[k].ws == x.w) { G.cur[k].count = nv; G.cur[k].expire = ex; }
+      if (G.prev[k].ws == x.w) { G.prev[k].count = nv; G.prev[k].expire = ex; }
+    }
+    after = nv;
+  }
+  if (restore) {
+    if (restore_lc) {
+      for (uint32_t k = 0; k < 4; k++) {
+        if (!(G.present >> k & 1)) continue;
+        if (G.cur[k].ws == x.w) G.cur[k].lc = x.now + x.d;
+        if (G.prev[k].ws == x.w) G.prev[k].lc = x.now + x.d;
+      }
+    }
+    return;
+  }
+  const Decision r = decide(after - x.h, after, lc_hit && !x.shadow, x.h, x.thr, P.ratio, x.shadow, P.lc_en);
+  if (r.set_lc) {  // freecache Set: last write wins, applied after this request
+    uint32_t j = 0;
+    while (j < G.npend && G.pend_w[j] != x.w) j++;
+    if (j == G.npend) G.npend++;
+    G.pend_w[j] = x.w;
+    G.pend_e[j] = x.now + x.d;
+  }
+  emit(o, acc, x, r);
+}
+
+__global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, Params P,
+                                              const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ svals,
+                                              const uint64_t* __restrict__ hstem, uint8_t* __restrict__ repid,
+                                              uint32_t* err, int restore) {
+  __shared__ unsigned long long sacc[LDS_RULES * RL_NUM_STATS];
+  __shared__ uint32_t s_err;
+  // err may change while this kernel runs (other blocks): read it once per block
+  if (threadIdx.x == 0) s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_err) return;
+  const bool use_lds = !restore && b.n_rules <= LDS_RULES;
+  if (use_lds) {
+    for (uint32_t j = threadIdx.x; j < b.n_rules * RL_NUM_STATS; j += 256) sacc[j] = 0;
+    __syncthreads();
+  }
+  StatAcc acc{use_lds ? sacc : nullptr, o.stats};
+  const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+  const bool head = p < b.n && (p == 0 || skeys[p - 1] != skeys[p]);
+  if (head) {
+    const uint32_t key = skeys[p];
+    uint32_t end = p + 1;
+    while (end < b.n && skeys[end] == key) end++;
+    // ---- split the run into distinct stems (hash, then bytes)
+    uint32_t rep[MAX_REPS];
+    uint32_t umask[MAX_REPS];
+    uint32_t nrep = 1;
+    rep[0] = svals[p];
+    umask[0] = 1u << (b.unit[rep[0]] - 1);
+    for (uint32_t q = p + 1; q < end; q++) {
+      const uint32_t e = svals[q];
+      const uint64_t he = hstem[e];
+      const uint32_t le = b.off[e + 1] - b.off[e];
+      uint32_t k = 0;
+      for (; k < nrep; k++) {
+        const uint32_t r = rep[k];
+        if (hstem[r] == he && b.off[r + 1] - b.off[r] == le && stems_equal(b.stem + b.off[r], b.stem + b.off[e], le))
+          break;
+      }
+      if (k == nrep) {
+        if (nrep == MAX_REPS) { atomicOr(err, ERR_COLLISIONS); k = 0; }
+        else { rep[nrep] = e; umask[nrep] = 0; nrep++; }
+      }
+      repid[q] = (uint8_t)k;
+      umask[k] |= 1u << (b.unit[e] - 1);
+    }
+    for (uint32_t k = 0; k < nrep; k++) {
+      const uint32_t r0 = rep[k];
+      const uint8_t* stem = b.stem + b.off[r0];
+      const uint32_t len = b.off[r0 + 1] - b.off[r0];
+      const uint64_t hs = hstem[r0];
+      // ---- resolve the slot(s)
+      bool simple = false;
+      int64_t s0 = -1;
+      if (__popc(umask[k]) == 1) {
+        const uint32_t u0 = __ffs(umask[k]);
+        bool ins;
+        s0 = find_slot(t, slot_tag(hs, u0), stem, len, u0, true, &ins, err);
+        if (s0 < 0) break;
+        if (!(t.slots[s0].flags & SLOT_EXACT)) {
+          simple = true;
+          if (ins) {  // new (stem, unit): the stem must not exist under another unit
+            for (uint32_t u = 1; u <= 4 && simple; u++) {
+              bool dummy;
+              if (u != u0 && find_slot(t, slot_tag(hs, u), stem, len, u, false, &dummy, err) >= 0) simple = false;
+            }
+          }
+        }
+      }
+      if (simple) {
+        Slot* s = &t.slots[s0];
+        SimpleState S;
+        S.cur = s->cur;
+        S.prev = s->prev;
+        S.cur_req = 0xFFFFFFFFu;
+        S.pend = false;
+        for (uint32_t q = p; q < end; q++) {
+          if (q != p && repid[q] != k) continue;
+          if (q == p && k != 0) continue;
+          const uint32_t e = svals[q];
+          simple_step(P, o, acc, S, load_elem(b, e, restore), restore, b.flags[e]);
+        }
+        S.apply_pending();
+        s->cur = S.cur;
+        s->prev = S.prev;
+      } else {
+        GeneralState G;
+        G.present = 0;
+        G.cur_req = 0xFFFFFFFFu;
+        G.npend = 0;
+        bool fail = false;
+        for (uint32_t u = 1; u <= 4; u++) {
+          bool ins;
+          G.sidx[u - 1] = find_slot(t, slot_tag(hs, u), stem, len, u, (umask[k] >> (u - 1)) & 1, &ins, err);
+          if (G.sidx[u - 1] >= 0) {
+            G.present |= 1u << (u - 1);
+            G.cur[u - 1] = t.slots[G.sidx[u - 1]].cur;
+            G.prev[u - 1] = t.slots[G.sidx[u - 1]].prev;
+          } else if ((umask[k] >> (u - 1)) & 1) {
+            fail = true;
+          }
+        }
+        if (fail) break;
+        for (uint32_t q = p; q < end; q++) {
+          if (q != p && repid[q] != k) continue;
+          if (q == p && k != 0) continue;
+          const uint32_t e = svals[q];
+          general_step(P, o, acc, G, load_elem(b, e, restore), restore, b.flags[e]);
+        }
+        general_apply_pending(G);
+        const uint8_t fl = __popc(G.present) >= 2 ? SLOT_EXACT : 0;
+        for (uint32_t u = 0; u < 4; u++) {
+          if (!(G.present >> u & 1)) continue;
+          Slot* s = &t.slots[G.sidx[u]];
+          s->cur = G.cur[u];
+          s->prev = G.prev[u];
+          s->flags |= fl;
+        }
+      }
+    }
+  }
+  if (use_lds) {
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < b.n_rules * RL_NUM_STATS; j += 256) {
+      const unsigned long long v = sacc[j];
+      if (v) atomicAdd(&o.stats[j], v);
+    }
+  }
+}
+
+__global__ void k_finish(const int64_t* now, uint32_t n_req, int64_t* last_now, const uint32_t* err) {
+  if (*err == 0 && n_req) *last_now = now[n_req - 1];
+}
+
+// ===========================================================================
+// Epoch sweep: a slot whose window records are all dead (Redis key past its
+// EXPIRE and local-cache entry past its TTL) becomes a tombstone.
+// ===========================================================================
+__device__ inline bool win_alive(const Win& w, uint32_t now) {
+  return w.ws != WS_INVALID && (now <= w.expire || now < w.lc);
+}
+
+__global__ __launch_bounds__(256) void k_sweep(Slot* slots, uint64_t nslots, uint32_t now,
+                                               unsigned long long* evicted) {
+  uint32_t local = 0;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * 256) {
+    Slot* s = &slots[i];
+    if (s->tag < 2) continue;
+    if (!win_alive(s->cur, now) && !win_alive(s->prev, now)) {
+      s->tag = TAG_TOMB;
+      local++;
+    }
+  }
+  if (local) atomicAdd(evicted, (unsigned long long)local);
+}
+
+__global__ __launch_bounds__(256) void k_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out) {
+  uint32_t live = 0, tomb = 0, exact = 0;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t tg = slots[i].tag;
+    if (tg == TAG_TOMB) tomb++;
+    else if (tg >= 2) { live++; if (slots[i].flags & SLOT_EXACT) exact++; }
+  }
+  if (live) atomicAdd(&out[0], (unsigned long long)live);
+  if (tomb) atomicAdd(&out[1], (unsigned long long)tomb);
+  if (exact) atomicAdd(&out[2], (unsigned long long)exact);
+}
+
+// ===========================================================================
+// Diagnostics
+// ===========================================================================
+// Full Redis key stem ‖ strconv.FormatInt((now/div)*div, 10) into a padded
+// buffer: descriptor i writes at off[i] + 24*i, its length in klen[i].
+__global__ __launch_bounds__(256) void k_debug_keys(BatchDev b, uint8_t* out, uint32_t* klen) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= b.n) return;
+  const uint32_t s0 = b.off[i], len = b.off[i + 1] - s0;
+  uint8_t* dst = out + s0 + 24ull * i;
+  for (uint32_t j = 0; j < len; j++) dst[j] = b.stem[s0 + j];
+  const uint32_t now = (uint32_t)b.now[b.req[i]];
+  const uint32_t d = div_of(b.unit[i]);
+  uint32_t ws = now / d * d;
+  uint8_t tmp[12];
+  uint32_t nd = 0;
+  do { tmp[nd++] = (uint8_t)('0' + ws % 10); ws /= 10; } while (ws);
+  for (uint32_t j = 0; j < nd; j++) dst[len + j] = tmp[nd - 1 - j];
+  klen[i] = len + nd;
+}
+
+__global__ __launch_bounds__(256) void k_debug_decide(uint32_t n, const uint32_t* before, const uint32_t* after,
+                                                      const uint8_t* lc_hit, const uint32_t* hits,
+                                                      const uint32_t* limit, const uint8_t* unit,
+                                                      const uint8_t* flags, const int64_t* now, float ratio,
+                                                      int lc_en, uint8_t* code, uint32_t* rem, uint32_t* reset,
+                                                      unsigned long long* deltas, uint8_t* lc_set) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const bool shadow = flags[i] & RL_FLAG_SHADOW;
+  const Decision r = decide(before[i], after[i], lc_hit[i] != 0, hits[i], limit[i], ratio, shadow, lc_en != 0);
+  code[i] = r.code;
+  rem[i] = r.remaining;
+  const uint32_t d = div_of(unit[i]);
+  reset[i] = d - (uint32_t)(now[i] % d);
+  unsigned long long* s = deltas + (size_t)i * RL_NUM_STATS;
+  s[RL_STAT_TOTAL_HITS] = 0;  // TotalHits is counted in GenerateCacheKeys, not here
+  s[RL_STAT_OVER_LIMIT] = r.d_over;
+  s[RL_STAT_NEAR_LIMIT] = r.d_near;
+  s[RL_STAT_OVER_LIMIT_WITH_LOCAL_CACHE] = r.d_lc;
+  s[RL_STAT_WITHIN_LIMIT] = r.d_within;
+  s[RL_STAT_SHADOW_MODE] = r.d_shadow;
+  lc_set[i] = r.set_lc;
+}
+
+// ===========================================================================
+// Launch wrappers
+// ===========================================================================
+static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
+                     int restore, hipStream_t st, hipEvent_t* ev) {
+  const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
+  if (ev) (void)hipEventRecord(ev[0], st);
+  if (g0) k_prepare<<<g0, 256, 0, st>>>(b, s.hstem, s.keys[0], s.vals[0], s.err, s.last_now, !restore);
+  if (ev) (void)hipEventRecord(ev[1], st);
+  if (b.n) {
+    const uint32_t ntiles = cdiv(b.n, RS_TILE);
+    for (uint32_t pass = 0; pass < 4; pass++) {
+      const uint32_t src = pass & 1, dst = src ^ 1, shift = 8 * pass;
+      k_rs_hist<<<ntiles, 256, 0, st>>>(s.keys[src], b.n, shift, ntiles, s.hist, s.err);
+      k_scan_u32<<<1, 1024, 0, st>>>(s.hist, 256 * ntiles, s.err);
+      k_rs_scatter<<<ntiles, 256, 0, st>>>(s.keys[src], s.vals[src], s.keys[dst], s.vals[dst], b.n, shift, ntiles,
+                                           s.hist, s.err);
+    }
+  }
+  if (ev) (void)hipEventRecord(ev[2], st);
+  if (b.n) k_runs<<<cdiv(b.n, 256), 256, 0, st>>>(b, o, t, P, s.keys[0], s.vals[0], s.hstem, s.repid, s.err, restore);
+  if (ev) (void)hipEventRecord(ev[3], st);
+  if (!restore) k_finish<<<1, 1, 0, st>>>(b.now, b.n_req, s.last_now, s.err);
+}
+
+void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st) {
+  k_sweep<<<2048, 256, 0, st>>>(slots, nslots, now, evicted);
+}
+
+void launch_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out, hipStream_t st) {
+  k_table_info<<<2048, 256, 0, st>>>(slots, nslots, out);
+}
+
+void launch_debug_keys(const BatchDev& b, uint8_t* out, uint32_t* klen, hipStream_t st) {
+  if (b.n) k_debug_keys<<<cdiv(b.n, 256), 256, 0, st>>>(b, out, klen);
+}
+
+void launch_debug_decide(uint32_t n, const uint32_t* before, const uint32_t* after, const uint8_t* lc_hit,
+                         const uint32_t* hits, const uint32_t* limit, const uint8_t* unit, const uint8_t* flags,
+                         const int64_t* now, float ratio, int lc_en, uint8_t* code, uint32_t* rem, uint32_t* reset,
+                         unsigned long long* deltas, uint8_t* lc_set, hipStream_t st) {
+  if (n)
+    k_debug_decide<<<cdiv(n, 256), 256, 0, st>>>(n, before, after, lc_hit, hits, limit, unit, flags, now, ratio,
+                                                 lc_en, code, rem, reset, deltas, lc_set);
+}
+
+}  // namespace rl

@@ -1,0 +1,212 @@
+"""Host-side mirror of the reference's RateLimitCache interface over the C ABI.
+
+``GpuRateLimitCache`` is what a user of the reference's
+``limiter.RateLimitCache`` (src/limiter/cache.go:11-29) switches to:
+
+    cache = GpuRateLimitCache(time_source, near_limit_ratio=0.8, local_cache=True,
+                              cache_key_prefix="", per_second=False)
+    statuses = cache.do_limit(ctx, request, limits)   # DoLimit
+    cache.flush()                                     # Flush
+
+Same argument meaning and error behaviour as
+``redis.NewFixedRateLimitCacheImpl`` / ``fixedRateLimitCacheImpl.DoLimit``
+(src/redis/fixed_cache_impl.go:33-125): nil limits answer {OK, nil, 0}; the
+per-rule stats counters (limit.stats) are incremented; backend failures raise
+``RedisError`` (the reference panics with redis.RedisError).  ``do_limit_batch``
+is the batcher's entry point: many in-flight calls, one GPU launch sequence.
+"""
+import ctypes as C
+import time
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import abi
+from ._lib import RedisError, check, lib
+from .packing import PackedBatch, RuleInterner, pack_calls
+from .types import OK, DescriptorStatus, Limit  # noqa: F401  (re-exported data model)
+
+__all__ = ["GpuRateLimitCache", "RedisError", "TimeSource"]
+
+
+class TimeSource:
+    """utils.TimeSource (src/utils/utilities.go:9-12)."""
+
+    def unix_now(self) -> int:
+        return int(time.time())
+
+
+class FixedTimeSource(TimeSource):
+    def __init__(self, now: int):
+        self.now = now
+
+    def unix_now(self) -> int:
+        return self.now
+
+
+def _config(near_limit_ratio, local_cache, per_second, jitter, table_slots, max_batch, max_rules, device,
+            arena_bytes, max_stem_bytes):
+    cfg = abi.RlConfig()
+    cfg.table_slots = table_slots
+    cfg.arena_bytes = arena_bytes
+    cfg.max_batch = max_batch
+    cfg.max_requests = max_batch
+    cfg.max_rules = max_rules
+    cfg.max_stem_bytes = max_stem_bytes
+    cfg.near_limit_ratio = near_limit_ratio
+    cfg.local_cache_enabled = 1 if local_cache else 0
+    cfg.per_second_split = 1 if per_second else 0
+    cfg.device = device
+    cfg.expiration_jitter_max_seconds = jitter
+    return cfg
+
+
+class Backend:
+    """Owns one rl_ctx (one GPU's table)."""
+
+    def __init__(self, near_limit_ratio=0.8, local_cache=False, per_second=False, jitter=0,
+                 table_slots=1 << 20, max_batch=1 << 16, max_rules=1 << 12, device=0, arena_bytes=0,
+                 max_stem_bytes=0):
+        L = lib()
+        err = C.create_string_buffer(512)
+        self.cfg = _config(near_limit_ratio, local_cache, per_second, jitter, table_slots, max_batch, max_rules,
+                           device, arena_bytes, max_stem_bytes)
+        self.ctx = L.rl_create(C.byref(self.cfg), err, 512)
+        if not self.ctx:
+            raise RedisError(err.value.decode())
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            lib().rl_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- raw packed-batch entry points
+    def do_limit_packed(self, pb: PackedBatch):
+        out = pb.alloc_result()
+        b = pb.batch_struct()
+        r = abi.make_result_struct(out)
+        check(self.ctx, lib().rl_do_limit(self.ctx, C.byref(b), C.byref(r)))
+        n, nr = pb.n, pb.n_rules
+        return {"code": out["code"][:n], "limit_remaining": out["limit_remaining"][:n],
+                "reset_s": out["reset_s"][:n], "stats": out["stats"][:nr * abi.RL_NUM_STATS]}
+
+    def do_limit_arrays(self, arrays, n, n_requests, n_rules):
+        return self.do_limit_packed(PackedBatch(arrays, n, n_requests, n_rules))
+
+    def do_limit_device(self, dev_in: dict, dev_out: dict, n, n_requests, n_rules, stream=None):
+        """All arrays are torch CUDA tensors (device memory); asynchronous."""
+        b = abi.make_batch_struct(dev_in, n, n_requests, n_rules)
+        r = abi.make_result_struct(dev_out)
+        check(self.ctx, lib().rl_do_limit_async(self.ctx, C.byref(b), C.byref(r),
+                                                C.c_void_p(stream) if stream else None))
+
+    def profile(self, enable: bool):
+        check(self.ctx, lib().rl_profile(self.ctx, 1 if enable else 0))
+
+    def profile_read(self):
+        """-> ({prepare, sort, runs} summed ms, batches timed); resets the sums."""
+        ms = (C.c_double * 3)()
+        nb = C.c_uint64(0)
+        check(self.ctx, lib().rl_profile_read(self.ctx, ms, 3, C.byref(nb)))
+        return dict(zip(("prepare", "sort", "runs"), list(ms))), nb.value
+
+    def synchronize(self):
+        check(self.ctx, lib().rl_synchronize(self.ctx))
+
+    def restore(self, stems: Sequence[bytes], units, nows, counts, lc=None):
+        from .packing import arrays_from_lists
+        n = len(stems)
+        a = arrays_from_lists(list(stems), [], [0] * n, units, [0] * n, [0] * n, [0] * n, [0] * n)
+        nowa = np.asarray(nows, np.int64)
+        cnt = np.asarray(counts, np.uint32)
+        lca = np.asarray(lc if lc is not None else [0] * n, np.uint8)
+        rb = abi.RlRestoreBatch()
+        rb.n = n
+        rb.stem_bytes, rb.stem_off, rb.unit = abi.ptr(a["stem_bytes"]), abi.ptr(a["stem_off"]), abi.ptr(a["unit"])
+        rb.now, rb.count, rb.lc = abi.ptr(nowa), abi.ptr(cnt), abi.ptr(lca)
+        check(self.ctx, lib().rl_restore(self.ctx, C.byref(rb)))
+
+    def sweep(self, now: int) -> int:
+        ev = C.c_uint64(0)
+        check(self.ctx, lib().rl_sweep(self.ctx, now, C.byref(ev)))
+        return ev.value
+
+    def table_info(self) -> dict:
+        info = abi.RlTableInfo()
+        check(self.ctx, lib().rl_table_info_get(self.ctx, C.byref(info)))
+        return {f: getattr(info, f) for f, _ in abi.RlTableInfo._fields_}
+
+    def debug_keys(self, pb: PackedBatch) -> List[str]:
+        cap = int(pb.arrays["stem_off"][-1]) + 24 * pb.n + 1
+        buf = np.zeros(cap, np.uint8)
+        off = np.zeros(pb.n + 1, np.uint32)
+        b = pb.batch_struct()
+        check(self.ctx, lib().rl_debug_keys(self.ctx, C.byref(b), abi.ptr(buf), abi.ptr(off), cap))
+        return [bytes(buf[off[i]:off[i + 1]]).decode() for i in range(pb.n)]
+
+    def debug_decide(self, before, after, lc_hit, hits, limit, unit, flags, now):
+        n = len(before)
+        a = [np.ascontiguousarray(x, dt) for x, dt in
+             ((before, np.uint32), (after, np.uint32), (lc_hit, np.uint8), (hits, np.uint32), (limit, np.uint32),
+              (unit, np.uint8), (flags, np.uint8), (now, np.int64))]
+        code = np.zeros(n, np.uint8)
+        rem = np.zeros(n, np.uint32)
+        reset = np.zeros(n, np.uint32)
+        deltas = np.zeros(n * abi.RL_NUM_STATS, np.uint64)
+        lc_set = np.zeros(n, np.uint8)
+        check(self.ctx, lib().rl_debug_decide(self.ctx, n, *[abi.ptr(x) for x in a], abi.ptr(code), abi.ptr(rem),
+                                              abi.ptr(reset), abi.ptr(deltas), abi.ptr(lc_set)))
+        return code, rem, reset, deltas.reshape(n, abi.RL_NUM_STATS), lc_set
+
+
+class GpuRateLimitCache:
+    """limiter.RateLimitCache backed by libratelimit_hip.so (BACKEND_TYPE=gpu)."""
+
+    def __init__(self, time_source: Optional[TimeSource] = None, near_limit_ratio: float = 0.8,
+                 local_cache: bool = False, cache_key_prefix: str = "", per_second: bool = False,
+                 expiration_jitter_max_seconds: int = 0, **backend_kw):
+        self.time_source = time_source or TimeSource()
+        self.prefix = cache_key_prefix
+        self.interner = RuleInterner()
+        self.backend = Backend(near_limit_ratio, local_cache, per_second, expiration_jitter_max_seconds,
+                               **backend_kw)
+
+    def close(self):
+        self.backend.close()
+
+    def do_limit(self, ctx, request, limits) -> List[DescriptorStatus]:
+        """fixedRateLimitCacheImpl.DoLimit semantics for one request."""
+        return self.do_limit_batch([(request, limits, self.time_source.unix_now())])[0]
+
+    def do_limit_batch(self, calls) -> List[List[DescriptorStatus]]:
+        """Many in-flight DoLimit calls (request, limits, now) as one GPU batch, in arrival order."""
+        pb = pack_calls(calls, self.prefix, self.interner)
+        res = self.backend.do_limit_packed(pb)
+        outs = [[DescriptorStatus(OK, None, 0, None) for _ in req.descriptors] for req, _, _ in calls]
+        code, rem, rst = res["code"], res["limit_remaining"], res["reset_s"]
+        for j, (c, i) in enumerate(pb.origin):
+            lim = calls[c][1][i]
+            outs[c][i] = DescriptorStatus(int(code[j]), lim.limit, int(rem[j]), int(rst[j]))
+        st = res["stats"].reshape(-1, abi.RL_NUM_STATS)
+        # apply the per-rule deltas to the gostats counters (limit.Stats)
+        seen = {}
+        for request, limits, _ in calls:
+            for lim in limits:
+                if lim is not None:
+                    seen[lim.stats.key] = lim.stats
+        for key, stats in seen.items():
+            row = st[self.interner.ids[key]]
+            for f, v in zip(abi.STAT_FIELDS, row):
+                if v:
+                    setattr(stats, f, getattr(stats, f) + int(v))
+        return outs
+
+    def flush(self):
+        """Flush(): nothing is asynchronous on the host path."""
+        return None

@@ -1,0 +1,313 @@
+"""GPU parity: libratelimit_hip.so (through the C ABI) vs the oracle.
+
+* golden vectors transcribed from the reference's own tests (tests/golden);
+* randomized structured streams vs the pure-Python oracle (overrides, shared
+  keys across units, shadow, local cache, per-second split, window rollover);
+* large packed streams (C0/C1/C2 shapes) vs the C oracle, bit-exact;
+* size-independent properties at BASELINE sizes (determinism, conservation).
+"""
+import numpy as np
+import pytest
+
+from oracle import c_oracle
+from oracle import oracle as O
+from ratelimit_amd import abi, workloads
+from ratelimit_amd.limiter import Backend, FixedTimeSource, GpuRateLimitCache, RedisError
+from ratelimit_amd.packing import RuleInterner, pack_calls, stem_of
+import golden_util as G
+import streams
+
+pytestmark = pytest.mark.gpu
+
+SMALL = dict(table_slots=1 << 16, max_batch=1 << 14, max_rules=1 << 10)
+
+
+def full_key(stem: bytes, unit: int, now: int) -> str:
+    d = O.unit_to_divider(unit)
+    return stem.decode() + str(now // d * d)
+
+
+# --------------------------------------------------------------------------- golden
+@pytest.mark.parametrize("name", G.names("do_limit"))
+def test_gpu_golden_do_limit(name):
+    fx = G.load(name)
+    c = fx["config"]
+    ts = FixedTimeSource(0)
+    cache = GpuRateLimitCache(ts, c["near_limit_ratio"], c["local_cache"], c["prefix"], c["per_second"],
+                              c["jitter_max"], **SMALL)
+    reg = G.StatsRegistry(O)
+    try:
+        for step in fx["steps"]:
+            ts.now = step["now"]
+            req = G.make_request(O, step["request"])
+            limits = [G.make_limit(O, reg, l) for l in step["limits"]]
+            if step["seed"]:  # the mocked INCRBY reply N, restated as a stored count N - hits
+                by_key = {}
+                for d, lim in zip(req.descriptors, limits):
+                    if lim is not None:
+                        st = stem_of(c["prefix"], req.domain, d.entries)
+                        by_key[full_key(st, lim.limit.unit, step["now"])] = (st, lim.limit.unit)
+                for sd in step["seed"]:
+                    st, u = by_key[sd["key"]]
+                    cache.backend.restore([st], [u], [step["now"]], [sd["count"]])
+            out = cache.do_limit(None, req, limits)
+            assert [G.status_tuple(s) for s in out] == [G.expect_tuple(e) for e in step["expect_statuses"]]
+            G.check_stats(reg, step["expect_stats"])
+    finally:
+        cache.close()
+
+
+def test_gpu_golden_cache_keys():
+    fx = G.load("ref_generate_cache_keys")
+    for case in fx["cases"]:
+        be = Backend(**SMALL)
+        reg = G.StatsRegistry(O)
+        req = G.make_request(O, case["request"])
+        limits = [G.make_limit(O, reg, l) for l in case["limits"]]
+        pb = pack_calls([(req, limits, case["now"])], case["prefix"], RuleInterner())
+        assert be.debug_keys(pb) == [k for k in case["expect_keys"] if k]
+        be.close()
+
+
+def test_gpu_golden_decide():
+    for case in G.load("ref_base_limiter_decide")["cases"]:
+        if case["limit"] is None:
+            continue  # empty key: answered host-side without the GPU (base_limiter.go:78-81)
+        be = Backend(near_limit_ratio=case["ratio"], local_cache=case["local_cache"], **SMALL)
+        lim = case["limit"]
+        code, rem, reset, deltas, lc_set = be.debug_decide(
+            [case["before"]], [case["after"]], [case["lc"]], [case["hits"]], [lim["rpu"]], [lim["unit"]],
+            [abi.RL_FLAG_SHADOW if lim["shadow"] else 0], [case["now"]])
+        e = case["expect"]
+        assert code[0] == e["code"] and rem[0] == e["remaining"]
+        if e.get("local_cache_set"):
+            assert lc_set[0] == 1
+        got = dict(zip(abi.STAT_FIELDS, deltas[0].tolist()))
+        for f, v in case["expect_stats"].get(lim["stats_key"], {}).items():
+            assert got[f] == v, (f, got)
+        be.close()
+
+
+def test_gpu_near_threshold_known_answers():
+    cases = G.load("own_near_threshold")["cases"]
+    for ratio in sorted({c[1] for c in cases}):
+        cs = [c for c in cases if c[1] == ratio]
+        be = Backend(near_limit_ratio=ratio, **SMALL)
+        L = [c[0] for c in cs]
+        # OK branch with before=0, after=L, hits=L: near_limit delta = L - near
+        code, rem, reset, deltas, _ = be.debug_decide([0] * len(L), L, [0] * len(L), L, L, [1] * len(L),
+                                                      [0] * len(L), [0] * len(L))
+        near = [l - int(d) for l, d in zip(L, deltas[:, abi.STAT_FIELDS.index("near_limit")])]
+        assert near == [c[2] for c in cs]
+        be.close()
+
+
+# --------------------------------------------------------------------------- random structured streams
+def _gpu_stream_run(calls, ratio, lc, prefix, ps, chunks):
+    streams.reset_stats(calls)
+    cache = GpuRateLimitCache(None, ratio, lc, prefix, ps, **SMALL)
+    outs = []
+    try:
+        i = 0
+        for k in chunks:
+            outs += cache.do_limit_batch(calls[i:i + k])
+            i += k
+    finally:
+        cache.close()
+    stats = {}
+    for _, limits, _ in calls:
+        for l in limits:
+            if l is not None:
+                stats[l.stats.key] = tuple(getattr(l.stats, f) for f in O.STAT_FIELDS)
+    return outs, stats
+
+
+@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("lc,ps,prefix,ratio", [(False, False, "", 0.8), (True, False, "p:", 0.8),
+                                                (False, True, "", 0.9), (True, True, "", 0.75)])
+def test_gpu_random_streams_vs_python_oracle(seed, lc, ps, prefix, ratio):
+    calls = streams.random_stream(seed, n_calls=400, zipf=seed % 2 == 0)
+    py_out, py_stats = streams.python_oracle_run(calls, ratio, lc, prefix, ps)
+    exp = [[s.as_tuple() for s in o] for o in py_out]
+    rng = np.random.default_rng(seed)
+    chunks = []
+    left = len(calls)
+    while left:
+        k = int(min(left, rng.integers(1, 120)))
+        chunks.append(k)
+        left -= k
+    outs, stats = _gpu_stream_run(calls, ratio, lc, prefix, ps, chunks)
+    got = [[G.status_tuple(s) for s in o] for o in outs]
+    for i, (g, e) in enumerate(zip(got, exp)):
+        assert g == e, "call %d: gpu %s oracle %s" % (i, g, e)
+    assert stats == py_stats
+
+
+def test_gpu_aligned_window_key_sharing():
+    """SECOND and MINUTE limits on one stem share a Redis key at t % 60 == 0
+    (cache_key.go:73-74: identical key strings) — only reachable via overrides."""
+    dom = "d"
+    ent = [("k", "v")]
+    reg = {}
+
+    def L(rpu, unit, key, shadow=False):
+        if key not in reg:
+            reg[key] = O.RateLimitStats(key)
+        return O.RateLimit(key, reg[key], O.Limit(rpu, unit), False, shadow)
+
+    calls = []
+    t0 = 1_700_000_040  # multiple of 60
+    for t in [t0, t0, t0 + 1, t0 + 1, t0 + 59, t0 + 60, t0 + 60, t0 + 61]:
+        for unit, rpu in [(O.SECOND, 3), (O.MINUTE, 5), (O.HOUR, 7)]:
+            calls.append((O.RateLimitRequest(dom, [O.Descriptor(list(ent)), O.Descriptor(list(ent))], 2),
+                          [L(rpu, unit, "r%d" % unit), L(rpu + 1, unit, "s%d" % unit, True)], t))
+    for lc in (False, True):
+        for ps in (False, True):
+            py_out, py_stats = streams.python_oracle_run(calls, 0.8, lc, "", ps)
+            outs, stats = _gpu_stream_run(calls, 0.8, lc, "", ps, [1] * 5 + [7, 12])
+            assert [[G.status_tuple(s) for s in o] for o in outs] == [[s.as_tuple() for s in o] for o in py_out]
+            assert stats == py_stats
+
+
+# --------------------------------------------------------------------------- packed streams vs C oracle
+def _compare_packed(batches, ratio=0.8, lc=False, ps=False, table_slots=1 << 22, max_batch=1 << 20):
+    be = Backend(ratio, lc, ps, table_slots=table_slots, max_batch=max_batch, max_rules=64)
+    co = c_oracle.COracle(ratio, lc, ps)
+    try:
+        for a, n, nq, nr in batches:
+            g = be.do_limit_arrays(a, n, nq, nr)
+            o = co.do_limit(a, n, nq, nr)
+            for k in ("code", "limit_remaining", "reset_s", "stats"):
+                if not np.array_equal(g[k], o[k]):
+                    bad = np.nonzero(g[k] != o[k])[0][:5]
+                    raise AssertionError("%s differs at %s: gpu %s oracle %s" % (k, bad, g[k][bad], o[k][bad]))
+    finally:
+        be.close()
+        co.close()
+
+
+def test_gpu_c1_uniform_vs_c_oracle():
+    _compare_packed(list(workloads.c1_stream(n_tenants=1_000_000, requests_per_batch=200_000, batches=3)))
+
+
+@pytest.mark.parametrize("lc", [False, True])
+def test_gpu_c2_zipf_hits_vs_c_oracle(lc):
+    z = workloads.ZipfSampler(200_000, 1.1)
+    _compare_packed(list(workloads.c2_stream(n_tenants=200_000, requests_per_batch=100_000, batches=3,
+                                             sampler=z)), lc=lc)
+
+
+def test_gpu_c0_vs_c_oracle():
+    _compare_packed(list(workloads.c0_stream(n_requests=300_000, per_batch=100_000)), lc=True)
+
+
+def test_gpu_batch_boundaries_do_not_matter():
+    """One big batch == the same stream split into many small batches."""
+    bs = list(workloads.c2_stream(n_tenants=5_000, requests_per_batch=20_000, batches=1,
+                                  sampler=workloads.ZipfSampler(5_000)))
+    a, n, nq, nr = bs[0]
+    one = Backend(0.8, True, table_slots=1 << 16, max_batch=1 << 16, max_rules=8)
+    many = Backend(0.8, True, table_slots=1 << 16, max_batch=1 << 16, max_rules=8)
+    r1 = one.do_limit_arrays(a, n, nq, nr)
+    codes, rems = [], []
+    stats = np.zeros_like(r1["stats"])
+    step = 777  # requests per small batch
+    for q0 in range(0, nq, step):
+        q1 = min(q0 + step, nq)
+        d0, d1 = 2 * q0, 2 * q1
+        sub = {k: a[k][d0:d1] for k in ("req_idx", "unit", "flags", "limit", "hits", "rule_id")}
+        sub["req_idx"] = (sub["req_idx"] - q0).astype(np.uint32)
+        sub["now"] = a["now"][q0:q1]
+        off = a["stem_off"][d0:d1 + 1]
+        sub["stem_bytes"] = a["stem_bytes"][off[0]:off[-1]].copy()
+        sub["stem_off"] = (off - off[0]).astype(np.uint32)
+        r = many.do_limit_arrays(sub, d1 - d0, q1 - q0, nr)
+        codes.append(r["code"])
+        rems.append(r["limit_remaining"])
+        stats += r["stats"]
+    assert np.array_equal(np.concatenate(codes), r1["code"])
+    assert np.array_equal(np.concatenate(rems), r1["limit_remaining"])
+    assert np.array_equal(stats, r1["stats"])
+    one.close()
+    many.close()
+
+
+# --------------------------------------------------------------------------- full-size properties
+def test_gpu_c1_full_batch_properties():
+    """At the BASELINE batch size (1M descriptors over 10M tenants): deterministic
+    across fresh tables, hits conserved in the stats, and — with limits far above
+    the per-window count — every counter equals the number of hits seen."""
+    a, n, nq, nr = next(workloads.c1_stream(batches=1))
+    r = []
+    for _ in range(2):
+        be = Backend(0.8, False, table_slots=1 << 22, max_batch=1 << 20, max_rules=8)
+        r.append(be.do_limit_arrays(a, n, nq, nr))
+        info = be.table_info()
+        be.close()
+    for k in r[0]:
+        assert np.array_equal(r[0][k], r[1][k])
+    st = r[0]["stats"].reshape(-1, 6)
+    assert st[:, 0].sum() == n  # total_hits
+    assert (st[:, 4] + st[:, 1] - st[:, 3] >= 0).all()
+    # distinct stems == live slots (each (stem, unit) exactly once)
+    stems = a["stem_bytes"].reshape(n, 34)
+    assert info["live_slots"] == len(np.unique(stems.view("S34")))
+    # remaining = limit - count: count of a key = its arrival rank among equal keys
+    _, inv, cnt = np.unique(stems.view("S34").ravel(), return_inverse=True, return_counts=True)
+    assert (r[0]["code"] == 1).all()
+    order = np.argsort(inv, kind="stable")
+    rank = np.empty(n, np.int64)
+    starts = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+    rank[order] = np.arange(n) - np.repeat(starts, cnt) + 1
+    assert np.array_equal(r[0]["limit_remaining"], a["limit"] - rank)
+
+
+def test_gpu_sweep_evicts_dead_windows():
+    be = Backend(0.8, True, **SMALL)
+    a, n, nq, nr = workloads.c1_batch(np.arange(1000), workloads.NOW0)
+    be.do_limit_arrays(a, n, nq, nr)
+    assert be.table_info()["live_slots"] == 2000
+    assert be.sweep(workloads.NOW0 + 1) == 0          # sec keys live while now <= t+1
+    assert be.sweep(workloads.NOW0 + 2) == 1000       # sec windows dead, minute windows live
+    assert be.sweep(workloads.NOW0 + 61) == 1000
+    info = be.table_info()
+    assert info["live_slots"] == 0 and info["tombstones"] == 2000
+    # tombstones are reused and state restarts from zero
+    a2, *_ = workloads.c1_batch(np.arange(1000), workloads.NOW0 + 61)
+    g = be.do_limit_arrays(a2, n, nq, nr)
+    assert (g["limit_remaining"] == a2["limit"] - 1).all()
+    with pytest.raises(RedisError):  # time cannot go back behind the sweep
+        be.do_limit_arrays(*workloads.c1_batch(np.arange(3), workloads.NOW0 + 30))
+    be.close()
+
+
+def test_gpu_errors_are_redis_errors():
+    be = Backend(**SMALL)
+    a, n, nq, nr = workloads.c1_batch(np.arange(4), workloads.NOW0)
+    bad = dict(a)
+    bad["unit"] = a["unit"].copy()
+    bad["unit"][1] = 0
+    with pytest.raises(RedisError, match="RL_E_INVALID"):
+        be.do_limit_arrays(bad, n, nq, nr)
+    be.do_limit_arrays(a, n, nq, nr)  # the context is still usable
+    with pytest.raises(RedisError, match="RL_E_TIME"):
+        be.do_limit_arrays(*workloads.c1_batch(np.arange(4), workloads.NOW0 - 5))
+    be.close()
+    tiny = Backend(table_slots=64, max_batch=1 << 10, max_rules=4)
+    with pytest.raises(RedisError, match="RL_E_TABLE_FULL"):
+        tiny.do_limit_arrays(*workloads.c1_batch(np.arange(100), workloads.NOW0))
+    tiny.close()
+
+
+def test_gpu_long_stems_use_arena():
+    dom = "x" * 200
+    reg = {}
+    calls = []
+    for i in range(50):
+        key = "r"
+        reg.setdefault(key, O.RateLimitStats(key))
+        calls.append((O.RateLimitRequest(dom, [O.Descriptor([("k" * 50, "v%d" % (i % 7))])], 1),
+                      [O.RateLimit(key, reg[key], O.Limit(5, O.MINUTE))], 1_700_000_000 + i))
+    py_out, _ = streams.python_oracle_run(calls, 0.8, True, "", False)
+    outs, _ = _gpu_stream_run(calls, 0.8, True, "", False, [10] * 5)
+    assert [[G.status_tuple(s) for s in o] for o in outs] == [[s.as_tuple() for s in o] for o in py_out]
