@@ -39,7 +39,8 @@ enum rl_status {
   RL_E_ARENA_FULL = 3, /* long-stem overflow arena exhausted */
   RL_E_HIP = 4,        /* HIP runtime error */
   RL_E_CAPACITY = 5,   /* batch larger than rl_config.max_* */
-  RL_E_TIME = 6,       /* now outside [0, 2^32 - 2*86400) or decreasing */
+  RL_E_TIME = 6,       /* now outside [0, 2^32 - 2*86400], before the last sweep, or
+                          moved back more than one window on one key */
   RL_E_COMM = 7,       /* multi-GPU routing (RCCL) error */
   RL_E_INTERNAL = 8
 };
@@ -85,7 +86,9 @@ typedef struct rl_config {
  * non-nil are packed (nil limits -> {OK, nil, 0} host-side,
  * base_limiter.go:78-81); unlimited rules are nil by then (ratelimit.go:140-143).
  * Descriptors appear in arrival order: request-major, descriptor order inside
- * the request; req_idx is non-decreasing and now[] is non-decreasing.
+ * the request; req_idx is non-decreasing. now[] may move backwards (the
+ * reference's tests do, on different keys); per (stem, unit) it may return to
+ * the previous window but not older (RL_E_TIME).
  * The stem is the cache key without its window suffix:
  *   prefix ‖ domain ‖ '_' ‖ Σ(key ‖ '_' ‖ value ‖ '_')   (cache_key.go:62-71)
  * The full key is stem ‖ decimal((now/div)*div) (cache_key.go:73-74). */
@@ -160,7 +163,8 @@ int rl_do_limit_async(rl_ctx* ctx, const rl_batch* in, rl_result* out, void* str
 int rl_synchronize(rl_ctx* ctx);
 
 /* Epoch sweep (replaces Redis EXPIRE): tombstones every slot whose counter
- * and local-cache entries have all expired at `now`. */
+ * and local-cache entries have all expired at `now`; `now` becomes a floor
+ * (later requests with an earlier time fail with RL_E_TIME). */
 int rl_sweep(rl_ctx* ctx, int64_t now, uint64_t* n_evicted);
 
 /* Seed / restore counters (host buffers). */

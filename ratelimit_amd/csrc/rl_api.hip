@@ -88,8 +88,9 @@ hipError_t dalloc(T** p, size_t count) {
 
 int map_err(rl_ctx* c, uint32_t e) {
   if (!e) return RL_OK;
-  if (e & ERR_TIME)
-    return set_err(c, RL_E_TIME, "gpu: now outside [0, 2^32-172800] or earlier than a previous request");
+  if (e & ERR_TIME) return set_err(c, RL_E_TIME, "gpu: now outside [0, 2^32-172800] or before the last sweep");
+  if (e & ERR_HISTORY)
+    return set_err(c, RL_E_TIME, "gpu: time moved back beyond the previous window of a key (table keeps 2 windows)");
   if (e & ERR_INVALID) return set_err(c, RL_E_INVALID, "gpu: malformed batch (unit, rule id, request index or stem offsets)");
   if (e & ERR_TABLE_FULL) return set_err(c, RL_E_TABLE_FULL, "gpu: counter table full (raise table_slots or sweep)");
   if (e & ERR_ARENA_FULL) return set_err(c, RL_E_ARENA_FULL, "gpu: long-stem arena full (raise arena_bytes)");
@@ -227,7 +228,7 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && dalloc(&c->s.hist, 256ull * std::max(ntiles, 1u)) == hipSuccess;
   ok = ok && dalloc(&c->s.repid, n) == hipSuccess;
   ok = ok && dalloc(&c->s.err, 1) == hipSuccess;
-  ok = ok && dalloc(&c->s.last_now, 1) == hipSuccess;
+  ok = ok && dalloc(&c->s.time_floor, 1) == hipSuccess;
   ok = ok && dalloc(&c->s.counters, 8) == hipSuccess;
   ok = ok && dalloc(&c->d_stem, (size_t)cfg.max_stem_bytes + 64) == hipSuccess;
   ok = ok && dalloc(&c->d_off, (size_t)n + 1) == hipSuccess;
@@ -243,7 +244,7 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
   ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
        hipMemsetAsync(c->s.err, 0, 4, c->stream) == hipSuccess &&
-       hipMemsetAsync(c->s.last_now, 0, 8, c->stream) == hipSuccess &&
+       hipMemsetAsync(c->s.time_floor, 0, 8, c->stream) == hipSuccess &&
        hipMemsetAsync(c->s.counters, 0, 64, c->stream) == hipSuccess &&
        hipMemsetAsync(c->d_stem, 0, (size_t)cfg.max_stem_bytes + 64, c->stream) == hipSuccess &&
        hipStreamSynchronize(c->stream) == hipSuccess;
@@ -258,7 +259,7 @@ void rl_destroy(rl_ctx* c) {
   for (int i = 0; i < 4; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
   void* bufs[] = {c->slots, c->arena, c->s.hstem, c->s.keys[0], c->s.keys[1], c->s.vals[0], c->s.vals[1],
-                  c->s.hist, c->s.repid, c->s.err, c->s.last_now, c->s.counters, c->d_stem, c->d_off, c->d_now,
+                  c->s.hist, c->s.repid, c->s.err, c->s.time_floor, c->s.counters, c->d_stem, c->d_off, c->d_now,
                   c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_rem,
                   c->d_reset, c->d_stats};
   for (void* p : bufs)
@@ -386,11 +387,11 @@ int rl_sweep(rl_ctx* c, int64_t now, uint64_t* n_evicted) {
   if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
   if (now < 0 || now > (int64_t)NOW_MAX) return set_err(c, RL_E_TIME, "gpu: sweep time out of range");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  // later batches must not run at an earlier time than the sweep
+  // the sweep time becomes a floor: later requests may not be earlier
   int64_t last = 0;
-  HIPCHK(c, hipMemcpyAsync(&last, c->s.last_now, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&last, c->s.time_floor, 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (now > last) HIPCHK(c, hipMemcpyAsync(c->s.last_now, &now, 8, hipMemcpyHostToDevice, c->stream));
+  if (now > last) HIPCHK(c, hipMemcpyAsync(c->s.time_floor, &now, 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->s.counters, 0, 8, c->stream));
   launch_sweep(c->slots, c->nslots, (uint32_t)now, c->s.counters, c->stream);
   HIPCHK(c, hipGetLastError());

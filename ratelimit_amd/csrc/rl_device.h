@@ -145,6 +145,7 @@ enum : uint32_t {
   ERR_ARENA_FULL = 1u << 2,
   ERR_TIME = 1u << 3,
   ERR_COLLISIONS = 1u << 4,  // more than MAX_REPS distinct stems in one hash run
+  ERR_HISTORY = 1u << 5,     // a key's window is older than its (cur, prev) history
 };
 
 constexpr uint32_t NOW_MAX = 0xFFFFFFFFu - 2u * 86400u;  // now + 2*div must fit u32

@@ -55,7 +55,7 @@ struct Scratch {
   uint32_t* hist;
   uint8_t* repid;
   uint32_t* err;
-  int64_t* last_now;
+  int64_t* time_floor;  // requests earlier than the last sweep are rejected
   unsigned long long* counters;  // [0..3] sweep / info outputs
 };
 

@@ -8,7 +8,6 @@
 //                 exactly by byte compare): find-or-insert the (stem, unit)
 //                 slot in the HBM table and replay the run in order — the
 //                 reference's sequential INCRBY/EXPIRE/local-cache semantics
-//   k_finish      record the batch's last `now` (time must not go backwards)
 // plus k_sweep (epoch sweep = Redis EXPIRE), k_table_info, debug kernels.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -55,17 +54,16 @@ struct DwordReader {
 
 __global__ __launch_bounds__(256) void k_prepare(BatchDev b, uint64_t* __restrict__ hstem,
                                                  uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                 uint32_t* err, const int64_t* last_now, int check_order) {
+                                                 uint32_t* err, const int64_t* time_floor) {
   __shared__ uint32_t lds[HASH_LDS_BYTES / 4 + 4];
   const uint32_t tid = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + tid;
   uint32_t bad = 0;
 
-  // ---- per-request clock checks: now in [0, NOW_MAX], non-decreasing (also across batches)
+  // ---- per-request clock checks: now in [0, NOW_MAX] and not before the last sweep
   if (i < b.n_req) {
-    int64_t t = b.now[i];
-    int64_t prev = i ? b.now[i - 1] : *last_now;
-    if (t < 0 || t > (int64_t)NOW_MAX || (check_order && t < prev)) bad |= ERR_TIME;
+    const int64_t t = b.now[i];
+    if (t < 0 || t > (int64_t)NOW_MAX || t < *time_floor) bad |= ERR_TIME;
   }
 
   // ---- per-descriptor checks
@@ -367,35 +365,45 @@ struct SimpleState {
   }
 };
 
+// The record of window w in a slot's (cur, prev) pair: cur or prev when one of
+// them holds w; a newer window rolls cur into prev. Time may move back only to
+// the previous window of a (stem, unit): anything older is outside the table's
+// history (null -> RL_E_TIME), never silently wrong.
+__device__ inline Win* window_record(Win& cur, Win& prev, uint32_t w, uint32_t lc_init) {
+  if (cur.ws == w) return &cur;
+  if (prev.ws == w) return &prev;
+  if (cur.ws == WS_INVALID || w > cur.ws) {
+    prev = cur;
+    cur = Win{w, 0, 0, lc_init};
+    return &cur;
+  }
+  return nullptr;
+}
+
 __device__ inline void simple_step(const Params& P, const OutDev& o, StatAcc& acc, SimpleState& S, const Elem& x,
-                                   bool restore, uint8_t restore_lc) {
+                                   bool restore, uint8_t restore_lc, uint32_t* err) {
   if (x.req != S.cur_req) {
     S.apply_pending();
     S.cur_req = x.req;
   }
-  if (restore) {
-    if (S.cur.ws != x.w) {
-      S.prev = S.cur;
-      S.cur = Win{x.w, 0, 0, 0};
-    }
-    S.cur.count = x.h;
-    S.cur.expire = x.now + x.d;
-    if (restore_lc) S.cur.lc = x.now + x.d;
+  Win* R = window_record(S.cur, S.prev, x.w, 0);
+  if (!R) {
+    atomicOr(err, ERR_HISTORY);
     return;
   }
-  const bool lc_hit = P.lc_en && ((S.cur.ws == x.w && x.now < S.cur.lc) || (S.prev.ws == x.w && x.now < S.prev.lc));
+  if (restore) {
+    R->count = x.h;
+    R->expire = x.now + x.d;
+    if (restore_lc) R->lc = x.now + x.d;
+    return;
+  }
+  const bool lc_hit = P.lc_en && x.now < R->lc;  // freecache Get (hit while now < expireAt)
   uint32_t after = 0;
   if (!lc_hit) {
-    uint32_t v = 0;
-    if (S.cur.ws == x.w) {
-      if (x.now <= S.cur.expire) v = S.cur.count;
-    } else {
-      S.prev = S.cur;
-      S.cur = Win{x.w, 0, 0, 0};
-    }
-    S.cur.count = v + x.h;
-    S.cur.expire = x.now + x.d;
-    after = S.cur.count;
+    const uint32_t v = x.now <= R->expire ? R->count : 0u;  // a key past its EXPIRE reads as missing
+    R->count = v + x.h;                                      // INCRBY
+    R->expire = x.now + x.d;                                 // EXPIRE div (jitter draw 0)
+    after = R->count;
   }
   const Decision r = decide(after - x.h, after, lc_hit && !x.shadow, x.h, x.thr, P.ratio, x.shadow, P.lc_en);
   if (r.set_lc) {
@@ -430,7 +438,7 @@ __device__ inline void general_apply_pending(GeneralState& G) {
 }
 
 __device__ inline void general_step(const Params& P, const OutDev& o, StatAcc& acc, GeneralState& G, const Elem& x,
-                                    bool restore, uint8_t restore_lc) {
+                                    bool restore, uint8_t restore_lc, uint32_t* err) {
   if (x.req != G.cur_req) {
     general_apply_pending(G);
     G.cur_req = x.req;
@@ -459,9 +467,9 @@ __device__ inline void general_step(const Params& P, const OutDev& o, StatAcc& a
   if (!lc_hit) {
     const uint32_t nv = restore ? x.h : v + x.h;
     const uint32_t ex = x.now + x.d;
-    if (G.cur[ui].ws != x.w) {
-      G.prev[ui] = G.cur[ui];
-      G.cur[ui] = Win{x.w, 0, 0, lcw};
+    if (!window_record(G.cur[ui], G.prev[ui], x.w, lcw)) {
+      atomicOr(err, ERR_HISTORY);
+      return;
     }
     for (uint32_t k = 0; k < 4; k++) {  // Redis key stem‖w in this store: every alias record
       if (!(G.present >> k & 1) || ps_class(P, k) != ps_e) continue;
@@ -570,7 +578,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
           if (q != p && repid[q] != k) continue;
           if (q == p && k != 0) continue;
           const uint32_t e = svals[q];
-          simple_step(P, o, acc, S, load_elem(b, e, restore), restore, b.flags[e]);
+          simple_step(P, o, acc, S, load_elem(b, e, restore), restore, b.flags[e], err);
         }
         S.apply_pending();
         s->cur = S.cur;
@@ -597,7 +605,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
           if (q != p && repid[q] != k) continue;
           if (q == p && k != 0) continue;
           const uint32_t e = svals[q];
-          general_step(P, o, acc, G, load_elem(b, e, restore), restore, b.flags[e]);
+          general_step(P, o, acc, G, load_elem(b, e, restore), restore, b.flags[e], err);
         }
         general_apply_pending(G);
         const uint8_t fl = __popc(G.present) >= 2 ? SLOT_EXACT : 0;
@@ -618,10 +626,6 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
       if (v) atomicAdd(&o.stats[j], v);
     }
   }
-}
-
-__global__ void k_finish(const int64_t* now, uint32_t n_req, int64_t* last_now, const uint32_t* err) {
-  if (*err == 0 && n_req) *last_now = now[n_req - 1];
 }
 
 // ===========================================================================
@@ -712,7 +716,7 @@ void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, cons
                      int restore, hipStream_t st, hipEvent_t* ev) {
   const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
   if (ev) (void)hipEventRecord(ev[0], st);
-  if (g0) k_prepare<<<g0, 256, 0, st>>>(b, s.hstem, s.keys[0], s.vals[0], s.err, s.last_now, !restore);
+  if (g0) k_prepare<<<g0, 256, 0, st>>>(b, s.hstem, s.keys[0], s.vals[0], s.err, s.time_floor);
   if (ev) (void)hipEventRecord(ev[1], st);
   if (b.n) {
     const uint32_t ntiles = cdiv(b.n, RS_TILE);
@@ -727,7 +731,6 @@ void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, cons
   if (ev) (void)hipEventRecord(ev[2], st);
   if (b.n) k_runs<<<cdiv(b.n, 256), 256, 0, st>>>(b, o, t, P, s.keys[0], s.vals[0], s.hstem, s.repid, s.err, restore);
   if (ev) (void)hipEventRecord(ev[3], st);
-  if (!restore) k_finish<<<1, 1, 0, st>>>(b.now, b.n_req, s.last_now, s.err);
 }
 
 void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st) {

@@ -169,6 +169,33 @@ def test_gpu_aligned_window_key_sharing():
             assert stats == py_stats
 
 
+def test_gpu_time_moves_back_one_window():
+    """The reference's tests move the mocked clock backwards (fixed_cache_impl_test.go:
+    1000000 -> 1234). Per key the table keeps the previous window, so alternating
+    between two windows is exact; older windows fail loudly (RL_E_TIME)."""
+    reg = {}
+
+    def L(rpu, unit, key):
+        reg.setdefault(key, O.RateLimitStats(key))
+        return O.RateLimit(key, reg[key], O.Limit(rpu, unit))
+
+    t = 1_700_000_030
+    calls = []
+    for i, now in enumerate([t, t + 1, t, t + 1, t + 1, t, t + 61, t + 60, t + 61]):
+        calls.append((O.RateLimitRequest("d", [O.Descriptor([("k", "a")]), O.Descriptor([("k", "b")])], 2),
+                      [L(5, O.SECOND, "s"), L(9, O.MINUTE, "m")], now))
+    for lc in (False, True):
+        py_out, py_stats = streams.python_oracle_run(calls, 0.8, lc, "", False)
+        outs, stats = _gpu_stream_run(calls, 0.8, lc, "", False, [1, 2, 3, 1, 2])
+        assert [[G.status_tuple(s) for s in o] for o in outs] == [[s.as_tuple() for s in o] for o in py_out]
+        assert stats == py_stats
+    cache = GpuRateLimitCache(None, **SMALL)
+    cache.do_limit_batch(calls[:2])  # windows t, t+1 of the second-unit key
+    with pytest.raises(RedisError, match="RL_E_TIME"):
+        cache.do_limit_batch([(calls[0][0], calls[0][1], t - 1)])  # older than the previous window
+    cache.close()
+
+
 # --------------------------------------------------------------------------- packed streams vs C oracle
 def _compare_packed(batches, ratio=0.8, lc=False, ps=False, table_slots=1 << 22, max_batch=1 << 20):
     be = Backend(ratio, lc, ps, table_slots=table_slots, max_batch=max_batch, max_rules=64)
