@@ -45,7 +45,7 @@ def lib():
     L.rl_alloc_host.argtypes = [C.c_size_t]
     L.rl_free_host.argtypes = [C.c_void_p]
     L.rl_debug_keys.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.c_void_p, C.c_void_p, C.c_uint32]
-    L.rl_debug_decide.argtypes = [C.c_void_p, C.c_uint32] + [C.c_void_p] * 14
+    L.rl_debug_decide.argtypes = [C.c_void_p, C.c_uint32] + [C.c_void_p] * 13
     L.rl_profile.argtypes = [C.c_void_p, C.c_int]
     L.rl_profile_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_uint32, C.POINTER(C.c_uint64)]
     if L.rl_abi_version() != 1:

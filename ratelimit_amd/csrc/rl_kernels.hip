@@ -365,17 +365,25 @@ struct SimpleState {
   }
 };
 
-// The record of window w in a slot's (cur, prev) pair: cur or prev when one of
-// them holds w; a newer window rolls cur into prev. Time may move back only to
-// the previous window of a (stem, unit): anything older is outside the table's
-// history (null -> RL_E_TIME), never silently wrong.
-__device__ inline Win* window_record(Win& cur, Win& prev, uint32_t w, uint32_t lc_init) {
+// The record of window w in a slot's (cur, prev) pair. cur is the newest window
+// ever written for this (stem, unit), prev the newest before it, so a window
+// strictly between them was never written (a fresh key): it takes prev's place.
+// A newer window rolls cur into prev. A window older than prev is outside the
+// table's history: null -> RL_E_TIME, never silently wrong. With allow_back
+// false (multi-unit stems, where other units may alias the key) only the
+// current or a newer window is accepted.
+__device__ inline Win* window_record(Win& cur, Win& prev, uint32_t w, uint32_t lc_init, bool allow_back) {
   if (cur.ws == w) return &cur;
-  if (prev.ws == w) return &prev;
   if (cur.ws == WS_INVALID || w > cur.ws) {
     prev = cur;
     cur = Win{w, 0, 0, lc_init};
     return &cur;
+  }
+  if (!allow_back) return nullptr;
+  if (prev.ws == w) return &prev;
+  if (prev.ws == WS_INVALID || w > prev.ws) {
+    prev = Win{w, 0, 0, lc_init};
+    return &prev;
   }
   return nullptr;
 }
@@ -386,7 +394,7 @@ __device__ inline void simple_step(const Params& P, const OutDev& o, StatAcc& ac
     S.apply_pending();
     S.cur_req = x.req;
   }
-  Win* R = window_record(S.cur, S.prev, x.w, 0);
+  Win* R = window_record(S.cur, S.prev, x.w, 0, true);
   if (!R) {
     atomicOr(err, ERR_HISTORY);
     return;
@@ -467,7 +475,7 @@ __device__ inline void general_step(const Params& P, const OutDev& o, StatAcc& a
   if (!lc_hit) {
     const uint32_t nv = restore ? x.h : v + x.h;
     const uint32_t ex = x.now + x.d;
-    if (!window_record(G.cur[ui], G.prev[ui], x.w, lcw)) {
+    if (!window_record(G.cur[ui], G.prev[ui], x.w, lcw, false)) {
       atomicOr(err, ERR_HISTORY);
       return;
     }
