@@ -317,7 +317,8 @@ def test_gpu_errors_are_redis_errors():
     with pytest.raises(RedisError, match="RL_E_INVALID"):
         be.do_limit_arrays(bad, n, nq, nr)
     be.do_limit_arrays(a, n, nq, nr)  # the context is still usable
-    with pytest.raises(RedisError, match="RL_E_TIME"):
+    be.do_limit_arrays(*workloads.c1_batch(np.arange(4), workloads.NOW0 + 1))
+    with pytest.raises(RedisError, match="RL_E_TIME"):  # older than the keys' previous window
         be.do_limit_arrays(*workloads.c1_batch(np.arange(4), workloads.NOW0 - 5))
     be.close()
     tiny = Backend(table_slots=64, max_batch=1 << 10, max_rules=4)
