@@ -122,6 +122,7 @@ BatchDev dev_view(const rl_batch* in, uint32_t stem_cap) {
   b.n_req = in->n_requests;
   b.n_rules = in->n_rules;
   b.stem_cap = stem_cap;
+  b.stem_total = stem_cap;  // refined on the device from off[n]
   b.stem = in->stem_bytes;
   b.off = in->stem_off;
   b.now = in->now;
@@ -226,7 +227,11 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
     ok = ok && dalloc(&c->s.vals[i], n) == hipSuccess;
   }
   ok = ok && dalloc(&c->s.hist, 256ull * std::max(ntiles, 1u)) == hipSuccess;
+  ok = ok && dalloc(&c->s.hist_tot, 256) == hipSuccess;
   ok = ok && dalloc(&c->s.repid, n) == hipSuccess;
+  ok = ok && dalloc(&c->s.defer, n) == hipSuccess;
+  ok = ok && dalloc(&c->s.defer_n, 1) == hipSuccess;
+  ok = ok && dalloc(&c->s.stripes, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS) == hipSuccess;
   ok = ok && dalloc(&c->s.err, 1) == hipSuccess;
   ok = ok && dalloc(&c->s.time_floor, 1) == hipSuccess;
   ok = ok && dalloc(&c->s.counters, 8) == hipSuccess;
@@ -246,6 +251,8 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
        hipMemsetAsync(c->s.err, 0, 4, c->stream) == hipSuccess &&
        hipMemsetAsync(c->s.time_floor, 0, 8, c->stream) == hipSuccess &&
        hipMemsetAsync(c->s.counters, 0, 64, c->stream) == hipSuccess &&
+       hipMemsetAsync(c->s.stripes, 0, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS * 8, c->stream) ==
+           hipSuccess &&
        hipMemsetAsync(c->d_stem, 0, (size_t)cfg.max_stem_bytes + 64, c->stream) == hipSuccess &&
        hipStreamSynchronize(c->stream) == hipSuccess;
   if (!ok) return fail("gpu: device initialisation failed", c);
@@ -259,7 +266,7 @@ void rl_destroy(rl_ctx* c) {
   for (int i = 0; i < 4; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
   void* bufs[] = {c->slots, c->arena, c->s.hstem, c->s.keys[0], c->s.keys[1], c->s.vals[0], c->s.vals[1],
-                  c->s.hist, c->s.repid, c->s.err, c->s.time_floor, c->s.counters, c->d_stem, c->d_off, c->d_now,
+                  c->s.hist, c->s.hist_tot, c->s.repid, c->s.defer, c->s.defer_n, c->s.stripes, c->s.err, c->s.time_floor, c->s.counters, c->d_stem, c->d_off, c->d_now,
                   c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_rem,
                   c->d_reset, c->d_stats};
   for (void* p : bufs)

@@ -11,9 +11,12 @@ namespace rl {
 
 constexpr uint32_t RS_ITEMS = 16;
 constexpr uint32_t RS_TILE = 256 * RS_ITEMS;
+constexpr uint32_t STAT_STRIPES = 64;     // global partial stats tables
+constexpr uint32_t STAT_LDS_RULES = 512;  // rules aggregated in LDS (== LDS_RULES)
 
 struct BatchDev {
   uint32_t n, n_req, n_rules, stem_cap;
+  uint32_t stem_total;  // bytes of packed stems (off[n]); reads stay below it
   const uint8_t* stem;
   const uint32_t* off;
   const int64_t* now;
@@ -52,8 +55,12 @@ struct Scratch {
   uint64_t* hstem;
   uint32_t* keys[2];
   uint32_t* vals[2];
-  uint32_t* hist;
+  uint32_t* hist;      // 256 x ntiles, digit-major
+  uint32_t* hist_tot;  // 256 digit totals
   uint8_t* repid;
+  uint32_t* defer;                // runs deferred to k_runs_general
+  uint32_t* defer_n;
+  unsigned long long* stripes;    // STAT_STRIPES x STAT_LDS_RULES x RL_NUM_STATS
   uint32_t* err;
   int64_t* time_floor;  // requests earlier than the last sweep are rejected
   unsigned long long* counters;  // [0..3] sweep / info outputs

@@ -116,9 +116,8 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, uint64_t* __restric
 
 // ===========================================================================
 // Stable LSD radix sort of (u32 key, u32 value), 8-bit digits, 256-thread
-// tiles of RS_ITEMS x 256 elements. Per pass: tile histograms -> one exclusive
-// scan (digit-major) -> stable scatter. Ranks inside a wave come from 8
-// ballots (peer mask per digit); across the 4 waves of a tile from LDS counts.
+// tiles of RS_ITEMS x 256 elements. Per pass: tile histograms (digit-major) ->
+// per-digit row scans -> stable scatter.
 // ===========================================================================
 __global__ __launch_bounds__(256) void k_rs_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t shift,
                                                  uint32_t ntiles, uint32_t* __restrict__ hist, const uint32_t* err) {
@@ -137,103 +136,175 @@ __global__ __launch_bounds__(256) void k_rs_hist(const uint32_t* __restrict__ ke
   hist[tid * ntiles + blockIdx.x] = h[tid];
 }
 
-// Exclusive scan of len u32 in place, one 1024-thread block.
-__global__ __launch_bounds__(1024) void k_scan_u32(uint32_t* __restrict__ a, uint32_t len, const uint32_t* err) {
-  __shared__ uint32_t part[1024];
+// Row scan of the digit-major histogram: block d turns row d (ntiles tile
+// counts) into exclusive prefixes in place and writes the row total.
+__global__ __launch_bounds__(256) void k_rs_rowscan(uint32_t* __restrict__ hist, uint32_t ntiles,
+                                                    uint32_t* __restrict__ totals, const uint32_t* err) {
+  __shared__ uint32_t part[256];
   if (*err) return;
   const uint32_t tid = threadIdx.x;
-  const uint32_t chunk = (len + 1023) / 1024;
-  const uint32_t s = tid * chunk, e = min(s + chunk, len);
+  uint32_t* row = hist + (size_t)blockIdx.x * ntiles;
+  const uint32_t per = (ntiles + 255) / 256;
+  const uint32_t s0 = tid * per, s1 = min(s0 + per, ntiles);
   uint32_t sum = 0;
-  for (uint32_t j = s; j < e; j++) sum += a[j];
+  for (uint32_t j = s0; j < s1; j++) sum += row[j];
   part[tid] = sum;
   __syncthreads();
-  for (uint32_t off = 1; off < 1024; off <<= 1) {
-    uint32_t v = tid >= off ? part[tid - off] : 0;
+  for (uint32_t off = 1; off < 256; off <<= 1) {
+    const uint32_t v = tid >= off ? part[tid - off] : 0u;
     __syncthreads();
     part[tid] += v;
     __syncthreads();
   }
   uint32_t run = part[tid] - sum;
-  for (uint32_t j = s; j < e; j++) {
-    uint32_t v = a[j];
-    a[j] = run;
+  for (uint32_t j = s0; j < s1; j++) {
+    const uint32_t v = row[j];
+    row[j] = run;
     run += v;
   }
+  if (tid == 255) totals[blockIdx.x] = part[255];
 }
 
+// Stable scatter. Wave w of a tile owns elements [w*64*RS_ITEMS, (w+1)*64*RS_ITEMS)
+// of it, item-major: it ranks them with a ballot multisplit (8 ballots -> the
+// lanes sharing a digit) against a wave-private running count in LDS, keeps
+// keys/values/ranks in registers, and only then (one barrier) learns the
+// other waves' counts and the digit's global base.
 __global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                     uint32_t n, uint32_t shift, uint32_t ntiles,
-                                                    const uint32_t* __restrict__ hist, const uint32_t* err) {
-  __shared__ uint32_t gbase[256], lbase[256], wcnt[4][256];
+                                                    const uint32_t* __restrict__ hist,
+                                                    const uint32_t* __restrict__ totals, const uint32_t* err) {
+  __shared__ uint32_t wcnt[4][256];
+  __shared__ uint32_t dsum[256];
   if (*err) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  gbase[tid] = hist[tid * ntiles + blockIdx.x];
-  lbase[tid] = 0;
+  wcnt[0][tid] = 0; wcnt[1][tid] = 0; wcnt[2][tid] = 0; wcnt[3][tid] = 0;
+  dsum[tid] = totals[tid];
+  __syncthreads();
   const uint64_t lt_mask = (1ull << lane) - 1;
-  const uint32_t base = blockIdx.x * RS_TILE;
-  for (uint32_t c = 0; c < RS_ITEMS; c++) {
-    const uint32_t j = base + c * 256 + tid;
+  const uint32_t wbase = blockIdx.x * RS_TILE + wave * 64 * RS_ITEMS;
+  uint32_t kk[RS_ITEMS], vv[RS_ITEMS], pos[RS_ITEMS];
+#pragma unroll
+  for (uint32_t i = 0; i < RS_ITEMS; i++) {
+    const uint32_t j = wbase + i * 64 + lane;
     const bool valid = j < n;
-    const uint32_t k = valid ? kin[j] : 0u;
-    const uint32_t v = valid ? vin[j] : 0u;
-    const uint32_t d = (k >> shift) & 255u;
-    wcnt[0][tid] = 0; wcnt[1][tid] = 0; wcnt[2][tid] = 0; wcnt[3][tid] = 0;
-    __syncthreads();
+    kk[i] = valid ? kin[j] : 0xFFFFFFFFu;
+    vv[i] = valid ? vin[j] : 0u;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < RS_ITEMS; i++) {
+    const bool valid = wbase + i * 64 + lane < n;
+    const uint32_t d = (kk[i] >> shift) & 255u;
     uint64_t peers = __ballot(valid);
 #pragma unroll
     for (uint32_t bit = 0; bit < 8; bit++) {
-      const bool s = (d >> bit) & 1u;
-      const uint64_t bal = __ballot(s);
-      peers &= s ? bal : ~bal;
+      const bool sb = (d >> bit) & 1u;
+      const uint64_t bal = __ballot(sb);
+      peers &= sb ? bal : ~bal;
     }
     const uint32_t rank = __popcll(peers & lt_mask);
-    if (valid && rank == 0) wcnt[wave][d] = __popcll(peers);
+    const uint32_t leader = valid ? (uint32_t)(__ffsll((unsigned long long)peers) - 1) : lane;
+    uint32_t old = 0;
+    if (valid && rank == 0) {
+      old = wcnt[wave][d];
+      wcnt[wave][d] = old + __popcll(peers);
+    }
+    old = __shfl(old, leader);
+    pos[i] = old + rank;
+  }
+  __syncthreads();
+  {  // digit base for this tile = exclusive scan of the digit totals + row prefix
+    uint32_t x = dsum[tid];
     __syncthreads();
-    uint32_t tot = 0;
+    for (uint32_t off = 1; off < 256; off <<= 1) {
+      const uint32_t v = tid >= off ? dsum[tid - off] : 0u;
+      __syncthreads();
+      dsum[tid] += v;
+      __syncthreads();
+    }
+    uint32_t run = dsum[tid] - x + hist[(size_t)tid * ntiles + blockIdx.x];
 #pragma unroll
     for (uint32_t w = 0; w < 4; w++) {
-      uint32_t t = wcnt[w][tid];
-      wcnt[w][tid] = tot;
-      tot += t;
+      const uint32_t t = wcnt[w][tid];
+      wcnt[w][tid] = run;
+      run += t;
     }
-    __syncthreads();
-    if (valid) {
-      const uint32_t pos = gbase[d] + lbase[d] + wcnt[wave][d] + rank;
-      kout[pos] = k;
-      vout[pos] = v;
-    }
-    __syncthreads();
-    lbase[tid] += tot;
   }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t i = 0; i < RS_ITEMS; i++) {
+    if (wbase + i * 64 + lane < n) {
+      const uint32_t p = wcnt[wave][(kk[i] >> shift) & 255u] + pos[i];
+      kout[p] = kk[i];
+      vout[p] = vv[i];
+    }
+  }
+}
+
+// ===========================================================================
+// Stem bytes as dwords. Stems sit at arbitrary byte offsets of the packed
+// buffer; a StemRef reads them as aligned dwords and funnel-shifts
+// (v_alignbyte) so compares move 4 bytes per load. Dwords past the end of the
+// packed stems read as 0 (no access past the buffer).
+// ===========================================================================
+struct StemRef {
+  const uint32_t* p;  // dword-aligned base
+  uint32_t sh;        // byte offset of the stem's first byte in p[0]
+  uint32_t nw;        // readable dwords from p
+  __device__ inline uint32_t at(uint32_t i) const { return i < nw ? p[i] : 0u; }
+  __device__ inline uint32_t word(uint32_t k) const { return __builtin_amdgcn_alignbyte(at(k + 1), at(k), sh * 8); }
+};
+
+__device__ inline StemRef stem_ref(const BatchDev& b, uint32_t e) {
+  const uintptr_t a = (uintptr_t)(b.stem + b.off[e]);
+  const uintptr_t ab = a & ~uintptr_t(3);
+  const uintptr_t end = (uintptr_t)(b.stem + b.stem_total);
+  return StemRef{reinterpret_cast<const uint32_t*>(ab), (uint32_t)(a - ab), (uint32_t)((end - ab + 3) / 4)};
+}
+
+__device__ inline uint32_t tail_mask(uint32_t len) { return (len & 3) ? ((1u << ((len & 3) * 8)) - 1u) : 0u; }
+
+// bytes [4*w0, 4*w0 + len) of x and y equal (x at word offset w0 too)
+__device__ inline bool stem_words_equal(const StemRef& x, const StemRef& y, uint32_t len) {
+  uint32_t diff = 0;
+  const uint32_t nw = len >> 2;
+#pragma unroll 4
+  for (uint32_t k = 0; k < nw; k++) diff |= x.word(k) ^ y.word(k);
+  if (len & 3) diff |= (x.word(nw) ^ y.word(nw)) & tail_mask(len);
+  return diff == 0;
 }
 
 // ===========================================================================
 // HBM table probing.
 // ===========================================================================
-__device__ inline bool stems_equal(const uint8_t* a, const uint8_t* b, uint32_t len) {
-  for (uint32_t i = 0; i < len; i++)
-    if (a[i] != b[i]) return false;
-  return true;
-}
-
-__device__ inline bool slot_key_equal(const Slot* s, const uint8_t* stem, uint32_t len, const uint8_t* arena) {
+__device__ inline bool slot_key_equal(const Slot* s, const StemRef& st, uint32_t len, const uint8_t* arena) {
   if (s->key_len != len) return false;
+  const uint32_t* sk = reinterpret_cast<const uint32_t*>(s->key);
   const uint32_t il = len < INLINE_KEY ? len : INLINE_KEY;
-  if (!stems_equal(s->key, stem, il)) return false;
-  if (len > INLINE_KEY) return stems_equal(arena + (size_t)s->ext_off * 16, stem + INLINE_KEY, len - INLINE_KEY);
-  return true;
+  uint32_t diff = 0;
+  const uint32_t nw = il >> 2;
+#pragma unroll 4
+  for (uint32_t k = 0; k < nw; k++) diff |= sk[k] ^ st.word(k);
+  if (il & 3) diff |= (sk[nw] ^ st.word(nw)) & tail_mask(il);
+  if (len > INLINE_KEY) {
+    const uint32_t* ek = reinterpret_cast<const uint32_t*>(arena + (size_t)s->ext_off * 16);
+    const uint32_t rest = len - INLINE_KEY, rw = rest >> 2;
+    for (uint32_t k = 0; k < rw; k++) diff |= ek[k] ^ st.word(INLINE_KEY / 4 + k);
+    if (rest & 3) diff |= (ek[rw] ^ st.word(INLINE_KEY / 4 + rw)) & tail_mask(rest);
+  }
+  return diff == 0;
 }
 
-__device__ inline void slot_init(const TableDev& t, Slot* s, const uint8_t* stem, uint32_t len, uint32_t unit,
+__device__ inline void slot_init(const TableDev& t, Slot* s, const StemRef& st, uint32_t len, uint32_t unit,
                                  uint32_t* err) {
   s->key_len = (uint16_t)len;
   s->unit = (uint8_t)unit;
   s->flags = 0;
   s->ext_off = 0;
+  uint32_t* sk = reinterpret_cast<uint32_t*>(s->key);
   const uint32_t il = len < INLINE_KEY ? len : INLINE_KEY;
-  for (uint32_t i = 0; i < il; i++) s->key[i] = stem[i];
+  for (uint32_t k = 0; k < (il + 3) / 4; k++) sk[k] = st.word(k);
   if (len > INLINE_KEY) {
     const uint32_t n16 = (len - INLINE_KEY + 15) / 16;
     unsigned long long off = atomicAdd(t.arena_used16, (unsigned long long)n16);
@@ -241,8 +312,8 @@ __device__ inline void slot_init(const TableDev& t, Slot* s, const uint8_t* stem
       atomicOr(err, ERR_ARENA_FULL);
     } else {
       s->ext_off = (uint32_t)off;
-      uint8_t* dst = t.arena + off * 16;
-      for (uint32_t i = INLINE_KEY; i < len; i++) dst[i - INLINE_KEY] = stem[i];
+      uint32_t* ek = reinterpret_cast<uint32_t*>(t.arena + off * 16);
+      for (uint32_t k = 0; k < (len - INLINE_KEY + 3) / 4; k++) ek[k] = st.word(INLINE_KEY / 4 + k);
     }
   }
   s->cur = Win{WS_INVALID, 0, 0, 0};
@@ -250,8 +321,11 @@ __device__ inline void slot_init(const TableDev& t, Slot* s, const uint8_t* stem
 }
 
 // Find (and optionally insert) the slot of (stem, unit). Returns -1 when absent
-// and insert == false, or on a full table (error bit set).
-__device__ int64_t find_slot(const TableDev& t, uint64_t tag, const uint8_t* stem, uint32_t len, uint32_t unit,
+// and insert == false, or on a full table (error bit set). Linear probing over
+// 128-B slots; a tag match is confirmed by the full stem (collision-exact).
+// Inserts claim the slot with a 64-bit CAS on its tag; only one lane ever
+// handles a given (stem, unit) per batch (runs are grouped by stem).
+__device__ int64_t find_slot(const TableDev& t, uint64_t tag, const StemRef& stem, uint32_t len, uint32_t unit,
                              bool insert, bool* inserted, uint32_t* err) {
   uint64_t i = tag & t.mask;
   int64_t tomb = -1;
@@ -293,7 +367,74 @@ __device__ int64_t find_slot(const TableDev& t, uint64_t tag, const uint8_t* ste
 }
 
 // ===========================================================================
-// k_runs: replay each stem's descriptors in arrival order.
+// Per-rule stats. Each lane sums its run's deltas in registers (u64); at the
+// end the wave reduces lane sums rule by rule (butterfly shuffles) and one lane
+// adds them to the block's LDS table, which is flushed once per block into one
+// of STAT_STRIPES global partial tables (spreads same-address atomics), folded
+// into rl_result.stats by k_stats_fold. With more than LDS_RULES rules the
+// wave sums go straight to rl_result.stats.
+// ===========================================================================
+constexpr uint32_t LDS_RULES = 512;
+constexpr uint32_t MAX_REPS = 8;
+
+struct StatAcc {
+  unsigned long long* lds;   // LDS_RULES * RL_NUM_STATS, or null
+  unsigned long long* glob;  // rl_result.stats (no LDS)
+  __device__ inline void add(uint32_t rule, uint32_t which, unsigned long long v) {
+    if (!v) return;
+    if (lds) atomicAdd(&lds[rule * RL_NUM_STATS + which], v);
+    else atomicAdd(&glob[(size_t)rule * RL_NUM_STATS + which], v);
+  }
+};
+
+struct LaneStats {
+  uint32_t rule;
+  bool has;
+  unsigned long long v[RL_NUM_STATS];
+  __device__ inline void reset() {
+    has = false;
+#pragma unroll
+    for (int i = 0; i < RL_NUM_STATS; i++) v[i] = 0;
+  }
+  __device__ inline void add(StatAcc& acc, uint32_t r, const uint32_t d[RL_NUM_STATS]) {
+    if (has && rule != r) {  // rule changed inside this lane's run: flush directly
+#pragma unroll
+      for (int i = 0; i < RL_NUM_STATS; i++) acc.add(rule, i, v[i]);
+      reset();
+    }
+    rule = r;
+    has = true;
+#pragma unroll
+    for (int i = 0; i < RL_NUM_STATS; i++) v[i] += d[i];
+  }
+};
+
+__device__ inline unsigned long long wave_sum(unsigned long long x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m);
+  return x;
+}
+
+// All lanes of the wave must call this (converged).
+__device__ __attribute__((always_inline)) inline void wave_flush(LaneStats& L, StatAcc& acc) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t pending = __ballot(L.has);
+  while (pending) {
+    const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)pending) - 1);
+    const uint32_t r = __shfl(L.rule, leader);
+    const bool mine = L.has && L.rule == r;
+#pragma unroll
+    for (int i = 0; i < RL_NUM_STATS; i++) {
+      const unsigned long long s = wave_sum(mine ? L.v[i] : 0ull);
+      if (lane == leader) acc.add(r, i, s);
+    }
+    if (mine) L.has = false;
+    pending = __ballot(L.has);
+  }
+}
+
+// ===========================================================================
+// Replaying a stem's descriptors in arrival order.
 //
 // Per descriptor (fixed_cache_impl.go:33-113, base_limiter.go:45-197):
 //   h = max(1, HitsAddend); TotalHits += h
@@ -304,19 +445,6 @@ __device__ int64_t find_slot(const TableDev& t, uint64_t tag, const uint8_t* ste
 //   else          -> INCRBY (a key past its EXPIRE reads 0), EXPIRE = now+div
 //   status + stats (decide), localCache.Set(key, div) when over.
 // ===========================================================================
-constexpr uint32_t LDS_RULES = 512;
-constexpr uint32_t MAX_REPS = 8;
-
-struct StatAcc {
-  unsigned long long* lds;  // LDS_RULES * RL_NUM_STATS, or null
-  unsigned long long* glob;
-  __device__ inline void add(uint32_t rule, uint32_t which, uint32_t v) {
-    if (!v) return;
-    if (lds) atomicAdd(&lds[rule * RL_NUM_STATS + which], (unsigned long long)v);
-    else atomicAdd(&glob[(size_t)rule * RL_NUM_STATS + which], (unsigned long long)v);
-  }
-};
-
 struct Elem {
   uint32_t e, req, now, unit, d, w, h, thr, rule;
   bool shadow;
@@ -338,16 +466,37 @@ __device__ inline Elem load_elem(const BatchDev& b, uint32_t e, bool restore) {
   return x;
 }
 
-__device__ inline void emit(const OutDev& o, StatAcc& acc, const Elem& x, const Decision& r) {
+__device__ __attribute__((always_inline)) inline void emit(const OutDev& o, LaneStats& L, StatAcc& acc, const Elem& x, const Decision& r) {
   o.code[x.e] = r.code;
   o.rem[x.e] = r.remaining;
   o.reset[x.e] = x.d - x.now % x.d;  // utils.CalculateReset
-  acc.add(x.rule, RL_STAT_TOTAL_HITS, x.h);
-  acc.add(x.rule, RL_STAT_OVER_LIMIT, r.d_over);
-  acc.add(x.rule, RL_STAT_NEAR_LIMIT, r.d_near);
-  acc.add(x.rule, RL_STAT_OVER_LIMIT_WITH_LOCAL_CACHE, r.d_lc);
-  acc.add(x.rule, RL_STAT_WITHIN_LIMIT, r.d_within);
-  acc.add(x.rule, RL_STAT_SHADOW_MODE, r.d_shadow);
+  const uint32_t d[RL_NUM_STATS] = {x.h, r.d_over, r.d_near, r.d_lc, r.d_within, r.d_shadow};
+  L.add(acc, x.rule, d);
+}
+
+// The record of window w in a slot's (cur, prev) pair. cur is the newest window
+// ever written for this (stem, unit), prev the newest before it, so a window
+// strictly between them was never written (a fresh key): it takes prev's place.
+// A newer window rolls cur into prev. A window older than prev is outside the
+// table's history: null -> RL_E_TIME, never silently wrong. With allow_back
+// false (multi-unit stems, where other units may alias the key) only the
+// current or a newer window is accepted.
+// Returns 0 (cur), 1 (prev) or -1 (older than the history); may roll.
+__device__ __attribute__((always_inline)) inline int window_pick(Win& cur, Win& prev, uint32_t w, uint32_t lc_init,
+                                                                bool allow_back) {
+  if (cur.ws == w) return 0;
+  if (cur.ws == WS_INVALID || w > cur.ws) {
+    prev = cur;
+    cur = Win{w, 0, 0, lc_init};
+    return 0;
+  }
+  if (!allow_back) return -1;
+  if (prev.ws == w) return 1;
+  if (prev.ws == WS_INVALID || w > prev.ws) {
+    prev = Win{w, 0, 0, lc_init};
+    return 1;
+  }
+  return -1;
 }
 
 // ---- single (stem, unit) slot, stem never seen with another unit: registers only
@@ -365,61 +514,43 @@ struct SimpleState {
   }
 };
 
-// The record of window w in a slot's (cur, prev) pair. cur is the newest window
-// ever written for this (stem, unit), prev the newest before it, so a window
-// strictly between them was never written (a fresh key): it takes prev's place.
-// A newer window rolls cur into prev. A window older than prev is outside the
-// table's history: null -> RL_E_TIME, never silently wrong. With allow_back
-// false (multi-unit stems, where other units may alias the key) only the
-// current or a newer window is accepted.
-__device__ inline Win* window_record(Win& cur, Win& prev, uint32_t w, uint32_t lc_init, bool allow_back) {
-  if (cur.ws == w) return &cur;
-  if (cur.ws == WS_INVALID || w > cur.ws) {
-    prev = cur;
-    cur = Win{w, 0, 0, lc_init};
-    return &cur;
-  }
-  if (!allow_back) return nullptr;
-  if (prev.ws == w) return &prev;
-  if (prev.ws == WS_INVALID || w > prev.ws) {
-    prev = Win{w, 0, 0, lc_init};
-    return &prev;
-  }
-  return nullptr;
-}
-
-__device__ inline void simple_step(const Params& P, const OutDev& o, StatAcc& acc, SimpleState& S, const Elem& x,
-                                   bool restore, uint8_t restore_lc, uint32_t* err) {
+__device__ __attribute__((always_inline)) inline void simple_step(const Params& P, const OutDev& o, LaneStats& L, StatAcc& acc, SimpleState& S,
+                                   const Elem& x, bool restore, uint8_t restore_lc, uint32_t* err) {
   if (x.req != S.cur_req) {
     S.apply_pending();
     S.cur_req = x.req;
   }
-  Win* R = window_record(S.cur, S.prev, x.w, 0, true);
-  if (!R) {
+  const int which = window_pick(S.cur, S.prev, x.w, 0, true);
+  if (which < 0) {
     atomicOr(err, ERR_HISTORY);
     return;
   }
-  if (restore) {
-    R->count = x.h;
-    R->expire = x.now + x.d;
-    if (restore_lc) R->lc = x.now + x.d;
-    return;
-  }
-  const bool lc_hit = P.lc_en && x.now < R->lc;  // freecache Get (hit while now < expireAt)
+  Win R = which ? S.prev : S.cur;  // values, not pointers: the state stays in VGPRs
   uint32_t after = 0;
-  if (!lc_hit) {
-    const uint32_t v = x.now <= R->expire ? R->count : 0u;  // a key past its EXPIRE reads as missing
-    R->count = v + x.h;                                      // INCRBY
-    R->expire = x.now + x.d;                                 // EXPIRE div (jitter draw 0)
-    after = R->count;
+  bool lc_hit = false;
+  if (restore) {
+    R.count = x.h;
+    R.expire = x.now + x.d;
+    if (restore_lc) R.lc = x.now + x.d;
+  } else {
+    lc_hit = P.lc_en && x.now < R.lc;  // freecache Get (hit while now < expireAt)
+    if (!lc_hit) {
+      const uint32_t v = x.now <= R.expire ? R.count : 0u;  // a key past its EXPIRE reads as missing
+      R.count = v + x.h;                                     // INCRBY
+      R.expire = x.now + x.d;                                // EXPIRE div (jitter draw 0)
+      after = R.count;
+    }
   }
+  if (which) S.prev = R;
+  else S.cur = R;
+  if (restore) return;
   const Decision r = decide(after - x.h, after, lc_hit && !x.shadow, x.h, x.thr, P.ratio, x.shadow, P.lc_en);
   if (r.set_lc) {
     S.pend = true;
     S.pend_w = x.w;
     S.pend_e = x.now + x.d;
   }
-  emit(o, acc, x, r);
+  emit(o, L, acc, x, r);
 }
 
 // ---- general: every unit slot of the stem, Redis keys shared across units
@@ -445,8 +576,8 @@ __device__ inline void general_apply_pending(GeneralState& G) {
   G.npend = 0;
 }
 
-__device__ inline void general_step(const Params& P, const OutDev& o, StatAcc& acc, GeneralState& G, const Elem& x,
-                                    bool restore, uint8_t restore_lc, uint32_t* err) {
+__device__ inline void general_step(const Params& P, const OutDev& o, LaneStats& L, StatAcc& acc, GeneralState& G,
+                                    const Elem& x, bool restore, uint8_t restore_lc, uint32_t* err) {
   if (x.req != G.cur_req) {
     general_apply_pending(G);
     G.cur_req = x.req;
@@ -475,7 +606,7 @@ __device__ inline void general_step(const Params& P, const OutDev& o, StatAcc& a
   if (!lc_hit) {
     const uint32_t nv = restore ? x.h : v + x.h;
     const uint32_t ex = x.now + x.d;
-    if (!window_record(G.cur[ui], G.prev[ui], x.w, lcw, false)) {
+    if (window_pick(G.cur[ui], G.prev[ui], x.w, lcw, false) < 0) {
       atomicOr(err, ERR_HISTORY);
       return;
     }
@@ -504,28 +635,135 @@ __device__ inline void general_step(const Params& P, const OutDev& o, StatAcc& a
     G.pend_w[j] = x.w;
     G.pend_e[j] = x.now + x.d;
   }
-  emit(o, acc, x, r);
+  emit(o, L, acc, x, r);
 }
 
+// Replay elements [p, end) of a single-unit stem through its slot s0 (registers).
+__device__ __attribute__((always_inline)) inline void replay_simple(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P,
+                                     const uint32_t* svals, const uint8_t* repid, uint32_t p, uint32_t end, uint32_t k,
+                                     int64_t s0, LaneStats& L, StatAcc& acc, uint32_t* err, bool restore) {
+  Slot* s = &t.slots[s0];
+  SimpleState S;
+  S.cur = s->cur;
+  S.prev = s->prev;
+  S.cur_req = 0xFFFFFFFFu;
+  S.pend = false;
+  for (uint32_t q = p; q < end; q++) {
+    if (repid && ((q == p) ? 0u : repid[q]) != k) continue;
+    const uint32_t e = svals[q];
+    simple_step(P, o, L, acc, S, load_elem(b, e, restore), restore, b.flags[e], err);
+  }
+  S.apply_pending();
+  s->cur = S.cur;
+  s->prev = S.prev;
+}
+
+__device__ inline void stats_block_begin(unsigned long long* sacc, bool use_lds, uint32_t n_rules) {
+  if (use_lds)
+    for (uint32_t j = threadIdx.x; j < n_rules * RL_NUM_STATS; j += blockDim.x) sacc[j] = 0;
+  __syncthreads();
+}
+
+__device__ inline void stats_block_end(unsigned long long* sacc, bool use_lds, uint32_t n_rules,
+                                       unsigned long long* stripes) {
+  __syncthreads();
+  if (use_lds) {
+    unsigned long long* dst = stripes + (size_t)(blockIdx.x % STAT_STRIPES) * n_rules * RL_NUM_STATS;
+    for (uint32_t j = threadIdx.x; j < n_rules * RL_NUM_STATS; j += blockDim.x) {
+      const unsigned long long v = sacc[j];
+      if (v) atomicAdd(&dst[j], v);
+    }
+  }
+}
+
+// ---- k_runs: one lane per run of equal hash prefixes. The common case — one
+// stem, one unit, a slot not flagged multi-unit — is replayed here in
+// registers; anything else is deferred to k_runs_general.
 __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, Params P,
                                               const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ svals,
-                                              const uint64_t* __restrict__ hstem, uint8_t* __restrict__ repid,
-                                              uint32_t* err, int restore) {
+                                              const uint64_t* __restrict__ hstem, uint32_t* __restrict__ defer,
+                                              uint32_t* defer_n, unsigned long long* stripes, uint32_t* err,
+                                              int restore) {
   __shared__ unsigned long long sacc[LDS_RULES * RL_NUM_STATS];
   __shared__ uint32_t s_err;
   // err may change while this kernel runs (other blocks): read it once per block
   if (threadIdx.x == 0) s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (s_err) return;
+  b.stem_total = b.off[b.n];
   const bool use_lds = !restore && b.n_rules <= LDS_RULES;
-  if (use_lds) {
-    for (uint32_t j = threadIdx.x; j < b.n_rules * RL_NUM_STATS; j += 256) sacc[j] = 0;
-    __syncthreads();
-  }
+  stats_block_begin(sacc, use_lds, b.n_rules);
   StatAcc acc{use_lds ? sacc : nullptr, o.stats};
+  LaneStats L;
+  L.reset();
   const uint32_t p = blockIdx.x * 256 + threadIdx.x;
   const bool head = p < b.n && (p == 0 || skeys[p - 1] != skeys[p]);
   if (head) {
+    const uint32_t key = skeys[p];
+    uint32_t end = p + 1;
+    while (end < b.n && skeys[end] == key) end++;
+    const uint32_t e0 = svals[p];
+    const uint64_t h0 = hstem[e0];
+    const uint32_t u0 = b.unit[e0];
+    const uint32_t len0 = b.off[e0 + 1] - b.off[e0];
+    const StemRef st0 = stem_ref(b, e0);
+    bool ok = true;
+    for (uint32_t q = p + 1; q < end && ok; q++) {
+      const uint32_t e = svals[q];
+      ok = hstem[e] == h0 && b.unit[e] == u0 && b.off[e + 1] - b.off[e] == len0 &&
+           stem_words_equal(stem_ref(b, e), st0, len0);
+    }
+    int64_t s0 = -1;
+    if (ok) {
+      bool ins;
+      s0 = find_slot(t, slot_tag(h0, u0), st0, len0, u0, true, &ins, err);
+      if (s0 < 0) {
+        ok = false;
+      } else if (t.slots[s0].flags & SLOT_EXACT) {
+        ok = false;
+      } else if (ins) {  // new (stem, unit): the stem must not exist under another unit
+        for (uint32_t u = 1; u <= 4 && ok; u++) {
+          bool dummy;
+          if (u != u0 && find_slot(t, slot_tag(h0, u), st0, len0, u, false, &dummy, err) >= 0) ok = false;
+        }
+      }
+    }
+    if (ok) {
+      replay_simple(b, o, t, P, svals, nullptr, p, end, 0, s0, L, acc, err, restore);
+    } else if (!(s0 < 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_TABLE_FULL))) {
+      defer[atomicAdd(defer_n, 1u)] = p;
+    }
+  }
+  if (!restore) wave_flush(L, acc);
+  stats_block_end(sacc, use_lds, b.n_rules, stripes);
+}
+
+// ---- k_runs_general: deferred runs (hash-prefix collisions, multi-unit
+// stems). Splits the run into distinct stems, then replays each exactly.
+__global__ __launch_bounds__(256) void k_runs_general(BatchDev b, OutDev o, TableDev t, Params P,
+                                                      const uint32_t* __restrict__ skeys,
+                                                      const uint32_t* __restrict__ svals,
+                                                      const uint64_t* __restrict__ hstem,
+                                                      const uint32_t* __restrict__ defer, const uint32_t* defer_n,
+                                                      uint8_t* __restrict__ repid, unsigned long long* stripes,
+                                                      uint32_t* err, int restore) {
+  __shared__ unsigned long long sacc[LDS_RULES * RL_NUM_STATS];
+  __shared__ uint32_t s_err, s_n;
+  if (threadIdx.x == 0) {
+    s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_n = *defer_n;
+  }
+  __syncthreads();
+  if (s_err || blockIdx.x * 256 >= s_n) return;
+  b.stem_total = b.off[b.n];
+  const bool use_lds = !restore && b.n_rules <= LDS_RULES;
+  stats_block_begin(sacc, use_lds, b.n_rules);
+  StatAcc acc{use_lds ? sacc : nullptr, o.stats};
+  LaneStats L;
+  L.reset();
+  const uint32_t di = blockIdx.x * 256 + threadIdx.x;
+  if (di < s_n) {
+    const uint32_t p = defer[di];
     const uint32_t key = skeys[p];
     uint32_t end = p + 1;
     while (end < b.n && skeys[end] == key) end++;
@@ -539,11 +777,11 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
       const uint32_t e = svals[q];
       const uint64_t he = hstem[e];
       const uint32_t le = b.off[e + 1] - b.off[e];
+      const StemRef se = stem_ref(b, e);
       uint32_t k = 0;
       for (; k < nrep; k++) {
         const uint32_t r = rep[k];
-        if (hstem[r] == he && b.off[r + 1] - b.off[r] == le && stems_equal(b.stem + b.off[r], b.stem + b.off[e], le))
-          break;
+        if (hstem[r] == he && b.off[r + 1] - b.off[r] == le && stem_words_equal(stem_ref(b, r), se, le)) break;
       }
       if (k == nrep) {
         if (nrep == MAX_REPS) { atomicOr(err, ERR_COLLISIONS); k = 0; }
@@ -554,7 +792,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
     }
     for (uint32_t k = 0; k < nrep; k++) {
       const uint32_t r0 = rep[k];
-      const uint8_t* stem = b.stem + b.off[r0];
+      const StemRef stem = stem_ref(b, r0);
       const uint32_t len = b.off[r0 + 1] - b.off[r0];
       const uint64_t hs = hstem[r0];
       // ---- resolve the slot(s)
@@ -576,21 +814,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
         }
       }
       if (simple) {
-        Slot* s = &t.slots[s0];
-        SimpleState S;
-        S.cur = s->cur;
-        S.prev = s->prev;
-        S.cur_req = 0xFFFFFFFFu;
-        S.pend = false;
-        for (uint32_t q = p; q < end; q++) {
-          if (q != p && repid[q] != k) continue;
-          if (q == p && k != 0) continue;
-          const uint32_t e = svals[q];
-          simple_step(P, o, acc, S, load_elem(b, e, restore), restore, b.flags[e], err);
-        }
-        S.apply_pending();
-        s->cur = S.cur;
-        s->prev = S.prev;
+        replay_simple(b, o, t, P, svals, repid, p, end, k, s0, L, acc, err, restore);
       } else {
         GeneralState G;
         G.present = 0;
@@ -610,10 +834,9 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
         }
         if (fail) break;
         for (uint32_t q = p; q < end; q++) {
-          if (q != p && repid[q] != k) continue;
-          if (q == p && k != 0) continue;
+          if (((q == p) ? 0u : repid[q]) != k) continue;
           const uint32_t e = svals[q];
-          general_step(P, o, acc, G, load_elem(b, e, restore), restore, b.flags[e], err);
+          general_step(P, o, L, acc, G, load_elem(b, e, restore), restore, b.flags[e], err);
         }
         general_apply_pending(G);
         const uint8_t fl = __popc(G.present) >= 2 ? SLOT_EXACT : 0;
@@ -627,13 +850,22 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
       }
     }
   }
-  if (use_lds) {
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < b.n_rules * RL_NUM_STATS; j += 256) {
-      const unsigned long long v = sacc[j];
-      if (v) atomicAdd(&o.stats[j], v);
-    }
+  if (!restore) wave_flush(L, acc);
+  stats_block_end(sacc, use_lds, b.n_rules, stripes);
+}
+
+// Fold the striped per-block partial stats into rl_result.stats and clear them.
+__global__ __launch_bounds__(256) void k_stats_fold(unsigned long long* __restrict__ stripes, uint32_t n_rules,
+                                                    unsigned long long* __restrict__ stats, const uint32_t* err) {
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t m = n_rules * RL_NUM_STATS;
+  if (j >= m) return;
+  unsigned long long s = 0;
+  for (uint32_t k = 0; k < STAT_STRIPES; k++) {
+    s += stripes[(size_t)k * m + j];
+    stripes[(size_t)k * m + j] = 0;
   }
+  if (*err == 0) stats[j] += s;
 }
 
 // ===========================================================================
@@ -731,13 +963,21 @@ void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, cons
     for (uint32_t pass = 0; pass < 4; pass++) {
       const uint32_t src = pass & 1, dst = src ^ 1, shift = 8 * pass;
       k_rs_hist<<<ntiles, 256, 0, st>>>(s.keys[src], b.n, shift, ntiles, s.hist, s.err);
-      k_scan_u32<<<1, 1024, 0, st>>>(s.hist, 256 * ntiles, s.err);
+      k_rs_rowscan<<<256, 256, 0, st>>>(s.hist, ntiles, s.hist_tot, s.err);
       k_rs_scatter<<<ntiles, 256, 0, st>>>(s.keys[src], s.vals[src], s.keys[dst], s.vals[dst], b.n, shift, ntiles,
-                                           s.hist, s.err);
+                                           s.hist, s.hist_tot, s.err);
     }
   }
   if (ev) (void)hipEventRecord(ev[2], st);
-  if (b.n) k_runs<<<cdiv(b.n, 256), 256, 0, st>>>(b, o, t, P, s.keys[0], s.vals[0], s.hstem, s.repid, s.err, restore);
+  if (b.n) {
+    (void)hipMemsetAsync(s.defer_n, 0, sizeof(uint32_t), st);
+    k_runs<<<cdiv(b.n, 256), 256, 0, st>>>(b, o, t, P, s.keys[0], s.vals[0], s.hstem, s.defer, s.defer_n,
+                                           s.stripes, s.err, restore);
+    k_runs_general<<<cdiv(b.n, 256), 256, 0, st>>>(b, o, t, P, s.keys[0], s.vals[0], s.hstem, s.defer, s.defer_n,
+                                                   s.repid, s.stripes, s.err, restore);
+    if (!restore && b.n_rules <= LDS_RULES && b.n_rules)
+      k_stats_fold<<<cdiv(b.n_rules * RL_NUM_STATS, 256), 256, 0, st>>>(s.stripes, b.n_rules, o.stats, s.err);
+  }
   if (ev) (void)hipEventRecord(ev[3], st);
 }
 
