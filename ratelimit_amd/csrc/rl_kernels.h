@@ -11,6 +11,10 @@ namespace rl {
 
 constexpr uint32_t RS_ITEMS = 16;
 constexpr uint32_t RS_TILE = 256 * RS_ITEMS;
+constexpr uint32_t SEG_ITEMS = 16;
+constexpr uint32_t SEG_TILE = 256 * SEG_ITEMS;
+constexpr uint32_t LONG_RUN = 32;        // runs at least this long take the parallel path
+constexpr uint32_t RUN_SLOW = 1, RUN_FAST = 2;
 constexpr uint32_t STAT_STRIPES = 64;     // global partial stats tables
 constexpr uint32_t STAT_LDS_RULES = 512;  // rules aggregated in LDS (== LDS_RULES)
 
@@ -61,6 +65,15 @@ struct Scratch {
   uint32_t* defer;                // runs deferred to k_runs_general
   uint32_t* defer_n;
   unsigned long long* stripes;    // STAT_STRIPES x STAT_LDS_RULES x RL_NUM_STATS
+  // run segmentation (sorted order)
+  uint32_t *tile_f, *tile_s, *tile_h;  // per SEG_TILE tile
+  uint32_t* segsum;                    // [n] inclusive in-run sum of hits
+  uint32_t* rid;                       // [n] run id
+  uint32_t* run_start;                 // [n+1]
+  uint32_t* run_flags;                 // [n] RUN_*
+  uint4* run_state;                    // [n] {slot, c0, old lc, F | which<<1}
+  uint32_t* run_f;                     // [n] first over-limit position
+  uint32_t* num_runs;
   uint32_t* err;
   int64_t* time_floor;  // requests earlier than the last sweep are rejected
   unsigned long long* counters;  // [0..3] sweep / info outputs

@@ -253,7 +253,7 @@ struct StemRef {
   uint32_t sh;        // byte offset of the stem's first byte in p[0]
   uint32_t nw;        // readable dwords from p
   __device__ inline uint32_t at(uint32_t i) const { return i < nw ? p[i] : 0u; }
-  __device__ inline uint32_t word(uint32_t k) const { return __builtin_amdgcn_alignbyte(at(k + 1), at(k), sh * 8); }
+  __device__ inline uint32_t word(uint32_t k) const { return __builtin_amdgcn_alignbyte(at(k + 1), at(k), sh); }  // shift in BYTES
 };
 
 __device__ inline StemRef stem_ref(const BatchDev& b, uint32_t e) {
@@ -676,42 +676,245 @@ __device__ inline void stats_block_end(unsigned long long* sacc, bool use_lds, u
   }
 }
 
-// ---- k_runs: one lane per run of equal hash prefixes. The common case — one
-// stem, one unit, a slot not flagged multi-unit — is replayed here in
-// registers; anything else is deferred to k_runs_general.
-__global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, Params P,
-                                              const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ svals,
-                                              const uint64_t* __restrict__ hstem, uint32_t* __restrict__ defer,
-                                              uint32_t* defer_n, unsigned long long* stripes, uint32_t* err,
-                                              int restore) {
-  __shared__ unsigned long long sacc[LDS_RULES * RL_NUM_STATS];
-  __shared__ uint32_t s_err;
-  // err may change while this kernel runs (other blocks): read it once per block
-  if (threadIdx.x == 0) s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// ===========================================================================
+// Run segmentation of the sorted order (3 phases over tiles of SEG_TILE):
+// a run starts where the sort key changes. Produces, per sorted position q,
+// the run id and the inclusive in-run sum of max(1, hits) (u32, wrapping like
+// the sequential INCRBYs), and per run its start. Segmented-sum operator on
+// (head, sum): (f1,s1)+(f2,s2) = (f1|f2, f2 ? s2 : s1+s2).
+// ===========================================================================
+struct SegPair {
+  uint32_t f, s;
+};
+__device__ inline SegPair seg_op(SegPair a, SegPair b) { return SegPair{a.f | b.f, b.f ? b.s : a.s + b.s}; }
+
+// inclusive block scan of (pair, head count) over 256 threads
+__device__ inline void seg_block_scan(SegPair& v, uint32_t& hc, SegPair* sp, uint32_t* sh) {
+  const uint32_t tid = threadIdx.x;
+  sp[tid] = v;
+  sh[tid] = hc;
   __syncthreads();
-  if (s_err) return;
+  for (uint32_t off = 1; off < 256; off <<= 1) {
+    SegPair a = v;
+    uint32_t c = hc;
+    if (tid >= off) {
+      a = seg_op(sp[tid - off], v);
+      c = sh[tid - off] + hc;
+    }
+    __syncthreads();
+    v = a;
+    hc = c;
+    sp[tid] = v;
+    sh[tid] = hc;
+    __syncthreads();
+  }
+}
+
+__device__ inline void seg_load(const uint32_t* skeys, const uint32_t* svals, const uint32_t* hits, uint32_t n,
+                                uint32_t q, bool& valid, bool& head, uint32_t& h) {
+  valid = q < n;
+  head = valid && (q == 0 || skeys[q - 1] != skeys[q]);
+  const uint32_t hv = valid ? hits[svals[q]] : 0u;
+  h = valid ? (hv > 1 ? hv : 1u) : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_seg_reduce(const uint32_t* __restrict__ skeys,
+                                                    const uint32_t* __restrict__ svals,
+                                                    const uint32_t* __restrict__ hits, uint32_t n,
+                                                    uint32_t* __restrict__ tile_f, uint32_t* __restrict__ tile_s,
+                                                    uint32_t* __restrict__ tile_h, const uint32_t* err) {
+  __shared__ SegPair sp[256];
+  __shared__ uint32_t sh[256];
+  if (*err) return;
+  const uint32_t base = blockIdx.x * SEG_TILE + threadIdx.x * SEG_ITEMS;
+  SegPair v{0, 0};
+  uint32_t hc = 0;
+  for (uint32_t i = 0; i < SEG_ITEMS; i++) {
+    bool valid, head;
+    uint32_t h;
+    seg_load(skeys, svals, hits, n, base + i, valid, head, h);
+    if (!valid) break;
+    v = seg_op(v, SegPair{head ? 1u : 0u, h});
+    hc += head;
+  }
+  seg_block_scan(v, hc, sp, sh);
+  if (threadIdx.x == 255) {
+    tile_f[blockIdx.x] = v.f;
+    tile_s[blockIdx.x] = v.s;
+    tile_h[blockIdx.x] = hc;
+  }
+}
+
+// Exclusive scan over the tile aggregates (one block), in place.
+__global__ __launch_bounds__(1024) void k_seg_tiles(uint32_t* __restrict__ tile_f, uint32_t* __restrict__ tile_s,
+                                                    uint32_t* __restrict__ tile_h, uint32_t ntiles, const uint32_t* err) {
+  __shared__ SegPair sp[1024];
+  __shared__ uint32_t sh[1024];
+  if (*err) return;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t per = (ntiles + 1023) / 1024;
+  const uint32_t s0 = tid * per, s1 = min(s0 + per, ntiles);
+  SegPair v{0, 0};
+  uint32_t hc = 0;
+  for (uint32_t j = s0; j < s1; j++) {
+    v = seg_op(v, SegPair{tile_f[j], tile_s[j]});
+    hc += tile_h[j];
+  }
+  sp[tid] = v;
+  sh[tid] = hc;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    SegPair a = v;
+    uint32_t c = hc;
+    if (tid >= off) {
+      a = seg_op(sp[tid - off], v);
+      c = sh[tid - off] + hc;
+    }
+    __syncthreads();
+    v = a;
+    hc = c;
+    sp[tid] = v;
+    sh[tid] = hc;
+    __syncthreads();
+  }
+  SegPair run = tid ? sp[tid - 1] : SegPair{0, 0};
+  uint32_t hrun = tid ? sh[tid - 1] : 0u;
+  for (uint32_t j = s0; j < s1; j++) {
+    const SegPair x{tile_f[j], tile_s[j]};
+    const uint32_t xh = tile_h[j];
+    tile_f[j] = run.f;
+    tile_s[j] = run.s;
+    tile_h[j] = hrun;
+    run = seg_op(run, x);
+    hrun += xh;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_seg_apply(const uint32_t* __restrict__ skeys,
+                                                   const uint32_t* __restrict__ svals,
+                                                   const uint32_t* __restrict__ hits, uint32_t n,
+                                                   const uint32_t* __restrict__ tile_f,
+                                                   const uint32_t* __restrict__ tile_s,
+                                                   const uint32_t* __restrict__ tile_h, uint32_t* __restrict__ segsum,
+                                                   uint32_t* __restrict__ rid, uint32_t* __restrict__ run_start,
+                                                   uint32_t* __restrict__ run_flags, uint32_t* num_runs,
+                                                   const uint32_t* err) {
+  __shared__ SegPair sp[256];
+  __shared__ uint32_t sh[256];
+  if (*err) return;
+  const uint32_t base = blockIdx.x * SEG_TILE + threadIdx.x * SEG_ITEMS;
+  SegPair v{0, 0};
+  uint32_t hc = 0;
+  for (uint32_t i = 0; i < SEG_ITEMS; i++) {
+    bool valid, head;
+    uint32_t h;
+    seg_load(skeys, svals, hits, n, base + i, valid, head, h);
+    if (!valid) break;
+    v = seg_op(v, SegPair{head ? 1u : 0u, h});
+    hc += head;
+  }
+  const SegPair mine = v;
+  const uint32_t mine_h = hc;
+  seg_block_scan(v, hc, sp, sh);
+  // exclusive prefix of this thread = tile carry + block exclusive
+  SegPair run = SegPair{tile_f[blockIdx.x], tile_s[blockIdx.x]};
+  uint32_t hrun = tile_h[blockIdx.x];
+  if (threadIdx.x) {
+    run = seg_op(run, sp[threadIdx.x - 1]);
+    hrun += sh[threadIdx.x - 1];
+  }
+  (void)mine;
+  (void)mine_h;
+  for (uint32_t i = 0; i < SEG_ITEMS; i++) {
+    const uint32_t q = base + i;
+    bool valid, head;
+    uint32_t h;
+    seg_load(skeys, svals, hits, n, q, valid, head, h);
+    if (!valid) break;
+    run = seg_op(run, SegPair{head ? 1u : 0u, h});
+    hrun += head;
+    const uint32_t r = hrun - 1;
+    segsum[q] = run.s;
+    rid[q] = r;
+    if (head) {
+      run_start[r] = q;
+      run_flags[r] = 0;
+    }
+    if (q == n - 1) {
+      run_start[r + 1] = n;
+      *num_runs = r + 1;
+    }
+  }
+}
+
+// Long runs only: every element must share the head's stem, unit and window
+// for the parallel path; otherwise the run is replayed serially.
+__global__ __launch_bounds__(256) void k_run_check(BatchDev b, const uint32_t* __restrict__ svals,
+                                                   const uint64_t* __restrict__ hstem,
+                                                   const uint32_t* __restrict__ rid,
+                                                   const uint32_t* __restrict__ run_start,
+                                                   uint32_t* __restrict__ run_flags, const uint32_t* err) {
+  if (*err) return;
+  const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= b.n) return;
+  b.stem_total = b.off[b.n];
+  const uint32_t r = rid[q];
+  const uint32_t p = run_start[r];
+  if (q == p || run_start[r + 1] - p < LONG_RUN) return;
+  const uint32_t e0 = svals[p], e = svals[q];
+  const uint32_t len0 = b.off[e0 + 1] - b.off[e0];
+  bool same = hstem[e] == hstem[e0] && b.unit[e] == b.unit[e0] && b.off[e + 1] - b.off[e] == len0;
+  if (same) {
+    const uint32_t d = div_of(b.unit[e]);
+    const uint32_t n0 = (uint32_t)b.now[b.req[e0]], n1 = (uint32_t)b.now[b.req[e]];
+    same = n0 / d == n1 / d && stem_words_equal(stem_ref(b, e), stem_ref(b, e0), len0);
+  }
+  if (!same) atomicOr(&run_flags[r], RUN_SLOW);
+}
+
+// ---- k_runs: one lane per run. Short runs of one stem and one unit whose slot
+// is not flagged multi-unit are replayed here in registers; long uniform runs
+// are set up for the parallel path (k_fast_*); anything else is deferred to
+// k_runs_general.
+__global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, Params P,
+                                              const uint32_t* __restrict__ svals,
+                                              const uint64_t* __restrict__ hstem,
+                                              const uint32_t* __restrict__ run_start,
+                                              uint32_t* __restrict__ run_flags, uint4* __restrict__ run_state,
+                                              uint32_t* __restrict__ run_f, const uint32_t* num_runs,
+                                              uint32_t* __restrict__ defer, uint32_t* defer_n,
+                                              unsigned long long* stripes, uint32_t* err, int restore) {
+  __shared__ unsigned long long sacc[LDS_RULES * RL_NUM_STATS];
+  __shared__ uint32_t s_err, s_nr;
+  // err may change while this kernel runs (other blocks): read it once per block
+  if (threadIdx.x == 0) {
+    s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_nr = *num_runs;
+  }
+  __syncthreads();
+  if (s_err || blockIdx.x * 256 >= s_nr) return;
   b.stem_total = b.off[b.n];
   const bool use_lds = !restore && b.n_rules <= LDS_RULES;
   stats_block_begin(sacc, use_lds, b.n_rules);
   StatAcc acc{use_lds ? sacc : nullptr, o.stats};
   LaneStats L;
   L.reset();
-  const uint32_t p = blockIdx.x * 256 + threadIdx.x;
-  const bool head = p < b.n && (p == 0 || skeys[p - 1] != skeys[p]);
-  if (head) {
-    const uint32_t key = skeys[p];
-    uint32_t end = p + 1;
-    while (end < b.n && skeys[end] == key) end++;
+  const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+  if (r < s_nr) {
+    const uint32_t p = run_start[r], end = run_start[r + 1];
+    const bool long_run = !restore && end - p >= LONG_RUN && !(run_flags[r] & RUN_SLOW);
     const uint32_t e0 = svals[p];
     const uint64_t h0 = hstem[e0];
     const uint32_t u0 = b.unit[e0];
     const uint32_t len0 = b.off[e0 + 1] - b.off[e0];
     const StemRef st0 = stem_ref(b, e0);
     bool ok = true;
-    for (uint32_t q = p + 1; q < end && ok; q++) {
-      const uint32_t e = svals[q];
-      ok = hstem[e] == h0 && b.unit[e] == u0 && b.off[e + 1] - b.off[e] == len0 &&
-           stem_words_equal(stem_ref(b, e), st0, len0);
+    if (!long_run) {  // long uniform runs were checked in parallel (k_run_check)
+      for (uint32_t q = p + 1; q < end && ok; q++) {
+        const uint32_t e = svals[q];
+        ok = hstem[e] == h0 && b.unit[e] == u0 && b.off[e + 1] - b.off[e] == len0 &&
+             stem_words_equal(stem_ref(b, e), st0, len0);
+      }
     }
     int64_t s0 = -1;
     if (ok) {
@@ -722,19 +925,129 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
       } else if (t.slots[s0].flags & SLOT_EXACT) {
         ok = false;
       } else if (ins) {  // new (stem, unit): the stem must not exist under another unit
-        for (uint32_t u = 1; u <= 4 && ok; u++) {
+        for (uint32_t u = 1; u <= 4; u++) {
           bool dummy;
-          if (u != u0 && find_slot(t, slot_tag(h0, u), st0, len0, u, false, &dummy, err) >= 0) ok = false;
+          const int64_t so = u == u0 ? -1 : find_slot(t, slot_tag(h0, u), st0, len0, u, false, &dummy, err);
+          if (so >= 0) {  // multi-unit stem from now on: flag both before deferring
+            t.slots[so].flags |= SLOT_EXACT;
+            ok = false;
+          }
         }
+        if (!ok) t.slots[s0].flags |= SLOT_EXACT;
       }
     }
-    if (ok) {
+    if (ok && long_run) {
+      // Parallel path: pick the window record once; k_fast_* decide every element.
+      Slot* s = &t.slots[s0];
+      Win cur = s->cur, prev = s->prev;
+      const Elem x0 = load_elem(b, e0, false);
+      const int which = window_pick(cur, prev, x0.w, 0, true);
+      if (which < 0) {
+        atomicOr(err, ERR_HISTORY);
+      } else {
+        const Win R = which ? prev : cur;
+        // A record of window w was written inside w: its EXPIRE and local-cache
+        // TTL both end at or after w + div, so they hold for the whole run.
+        const uint32_t c0 = x0.now <= R.expire ? R.count : 0u;
+        const uint32_t F = (P.lc_en && x0.now < R.lc) ? 1u : 0u;
+        s->cur = cur;
+        s->prev = prev;
+        run_state[r] = make_uint4((uint32_t)s0, c0, R.lc, F | ((uint32_t)which << 1));
+        run_f[r] = 0xFFFFFFFFu;
+        run_flags[r] |= RUN_FAST;
+      }
+    } else if (ok) {
       replay_simple(b, o, t, P, svals, nullptr, p, end, 0, s0, L, acc, err, restore);
     } else if (!(s0 < 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_TABLE_FULL))) {
       defer[atomicAdd(defer_n, 1u)] = p;
     }
   }
   if (!restore) wave_flush(L, acc);
+  stats_block_end(sacc, use_lds, b.n_rules, stripes);
+}
+
+// ---- parallel path for long uniform runs (one stem, one unit, one window).
+// Sequential replay of such a run is: count a_j = c0 + Σ_{k<=j} h_k; with the
+// local cache on, the first element f with a_f > limit_f makes every element of
+// a LATER request a local-cache hit (Set happens after request q_f's statuses),
+// i.e. a suffix of the run, which therefore never increments.
+__global__ __launch_bounds__(256) void k_fast_over(BatchDev b, const uint32_t* __restrict__ svals,
+                                                   const uint32_t* __restrict__ segsum,
+                                                   const uint32_t* __restrict__ rid,
+                                                   const uint32_t* __restrict__ run_flags,
+                                                   const uint4* __restrict__ run_state, uint32_t* __restrict__ run_f,
+                                                   const uint32_t* err) {
+  if (*err) return;
+  const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;
+  bool cand = false;
+  uint32_t r = 0;
+  if (q < b.n) {
+    r = rid[q];
+    if (run_flags[r] & RUN_FAST) {
+      const uint4 st = run_state[r];
+      if (!(st.w & 1u)) cand = st.y + segsum[q] > b.limit[svals[q]];
+    }
+  }
+  uint64_t pending = __ballot(cand);
+  while (pending) {  // lowest candidate position per run in this wave
+    const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)pending) - 1);
+    const uint32_t rr = __shfl(r, leader);
+    if (lane == leader) atomicMin(&run_f[rr], q);
+    pending &= ~__ballot(cand && r == rr);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fast_emit(BatchDev b, OutDev o, TableDev t, Params P,
+                                                   const uint32_t* __restrict__ svals,
+                                                   const uint32_t* __restrict__ segsum,
+                                                   const uint32_t* __restrict__ rid,
+                                                   const uint32_t* __restrict__ run_start,
+                                                   const uint32_t* __restrict__ run_flags,
+                                                   const uint4* __restrict__ run_state,
+                                                   const uint32_t* __restrict__ run_f, unsigned long long* stripes,
+                                                   const uint32_t* err) {
+  __shared__ unsigned long long sacc[LDS_RULES * RL_NUM_STATS];
+  __shared__ uint32_t s_err;
+  if (threadIdx.x == 0) s_err = *err;
+  __syncthreads();
+  if (s_err) return;
+  const bool use_lds = b.n_rules <= LDS_RULES;
+  stats_block_begin(sacc, use_lds, b.n_rules);
+  StatAcc acc{use_lds ? sacc : nullptr, o.stats};
+  LaneStats L;
+  L.reset();
+  const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+  if (q < b.n) {
+    const uint32_t r = rid[q];
+    if (run_flags[r] & RUN_FAST) {
+      const uint4 st = run_state[r];
+      const uint32_t f = run_f[r];
+      const bool F = st.w & 1u;
+      const Elem x = load_elem(b, svals[q], false);
+      uint32_t req_f = 0xFFFFFFFFu;
+      if (P.lc_en && f != 0xFFFFFFFFu) req_f = b.req[svals[f]];
+      const bool masked = F || x.req > req_f;  // local-cache hit
+      const uint32_t after = masked ? 0u : st.y + segsum[q];
+      const Decision d = decide(after - x.h, after, masked && !x.shadow, x.h, x.thr, P.ratio, x.shadow, P.lc_en);
+      emit(o, L, acc, x, d);
+      if (!masked) {
+        const uint32_t nq = q + 1;
+        const bool last = nq == run_start[r + 1] || b.req[svals[nq]] > req_f;
+        if (last) {  // the last INCRBY of the run leaves the key's state
+          Win R;
+          R.ws = x.w;
+          R.count = after;
+          R.expire = x.now + x.d;
+          R.lc = (req_f != 0xFFFFFFFFu) ? (uint32_t)b.now[req_f] + x.d : st.z;
+          Slot* s = &t.slots[st.x];
+          if (st.w & 2u) s->prev = R;
+          else s->cur = R;
+        }
+      }
+    }
+  }
+  wave_flush(L, acc);
   stats_block_end(sacc, use_lds, b.n_rules, stripes);
 }
 
@@ -970,13 +1283,25 @@ void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, cons
   }
   if (ev) (void)hipEventRecord(ev[2], st);
   if (b.n) {
+    const uint32_t nt = cdiv(b.n, SEG_TILE), g = cdiv(b.n, 256);
+    k_seg_reduce<<<nt, 256, 0, st>>>(s.keys[0], s.vals[0], b.hits, b.n, s.tile_f, s.tile_s, s.tile_h, s.err);
+    k_seg_tiles<<<1, 1024, 0, st>>>(s.tile_f, s.tile_s, s.tile_h, nt, s.err);
+    k_seg_apply<<<nt, 256, 0, st>>>(s.keys[0], s.vals[0], b.hits, b.n, s.tile_f, s.tile_s, s.tile_h, s.segsum,
+                                    s.rid, s.run_start, s.run_flags, s.num_runs, s.err);
+    k_run_check<<<g, 256, 0, st>>>(b, s.vals[0], s.hstem, s.rid, s.run_start, s.run_flags, s.err);
     (void)hipMemsetAsync(s.defer_n, 0, sizeof(uint32_t), st);
-    k_runs<<<cdiv(b.n, 256), 256, 0, st>>>(b, o, t, P, s.keys[0], s.vals[0], s.hstem, s.defer, s.defer_n,
-                                           s.stripes, s.err, restore);
-    k_runs_general<<<cdiv(b.n, 256), 256, 0, st>>>(b, o, t, P, s.keys[0], s.vals[0], s.hstem, s.defer, s.defer_n,
-                                                   s.repid, s.stripes, s.err, restore);
-    if (!restore && b.n_rules <= LDS_RULES && b.n_rules)
-      k_stats_fold<<<cdiv(b.n_rules * RL_NUM_STATS, 256), 256, 0, st>>>(s.stripes, b.n_rules, o.stats, s.err);
+    k_runs<<<g, 256, 0, st>>>(b, o, t, P, s.vals[0], s.hstem, s.run_start, s.run_flags, s.run_state, s.run_f,
+                              s.num_runs, s.defer, s.defer_n, s.stripes, s.err, restore);
+    k_runs_general<<<g, 256, 0, st>>>(b, o, t, P, s.keys[0], s.vals[0], s.hstem, s.defer, s.defer_n, s.repid,
+                                      s.stripes, s.err, restore);
+    if (!restore) {
+      if (P.lc_en)
+        k_fast_over<<<g, 256, 0, st>>>(b, s.vals[0], s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.err);
+      k_fast_emit<<<g, 256, 0, st>>>(b, o, t, P, s.vals[0], s.segsum, s.rid, s.run_start, s.run_flags, s.run_state,
+                                     s.run_f, s.stripes, s.err);
+      if (b.n_rules <= LDS_RULES && b.n_rules)
+        k_stats_fold<<<cdiv(b.n_rules * RL_NUM_STATS, 256), 256, 0, st>>>(s.stripes, b.n_rules, o.stats, s.err);
+    }
   }
   if (ev) (void)hipEventRecord(ev[3], st);
 }
