@@ -158,7 +158,8 @@ int rl_do_limit(rl_ctx* ctx, const rl_batch* in, rl_result* out);
 
 /* Same, with every pointer in *in / *out in device memory of ctx's GPU,
  * enqueued on `stream` (a hipStream_t, NULL = ctx's own stream). Returns once
- * the work is enqueued; errors detected on the GPU surface at rl_synchronize. */
+ * the work is enqueued; errors detected on the GPU surface at rl_synchronize.
+ * stem_bytes must be 4-byte aligned (any hipMalloc / torch allocation is). */
 int rl_do_limit_async(rl_ctx* ctx, const rl_batch* in, rl_result* out, void* stream);
 int rl_synchronize(rl_ctx* ctx);
 

@@ -293,6 +293,7 @@ int rl_do_limit_async(rl_ctx* c, const rl_batch* in, rl_result* out, void* strea
   // kernels bound-check offsets against max_stem_bytes (stem_cap)
   int rc = check_sizes(c, in, 0);
   if (rc) return rc;
+  if ((uintptr_t)in->stem_bytes & 3u) return set_err(c, RL_E_INVALID, "gpu: stem_bytes must be 4-byte aligned");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   if (in->n_rules) HIPCHK(c, hipMemsetAsync(out->stats, 0, (size_t)in->n_rules * RL_NUM_STATS * 8, st));

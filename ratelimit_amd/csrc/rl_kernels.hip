@@ -84,14 +84,15 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, uint64_t* __restric
   const uint32_t b0 = blockIdx.x * 256;
   if (b0 >= b.n) return;  // whole block past the descriptors (request checks done)
   const uint32_t b1 = min(b0 + 256u, b.n);
-  uint32_t lo = b.off[b0], hi = b.off[b1];
-  bool range_ok = hi >= lo && hi <= b.stem_cap;
-  const uintptr_t base_addr = (uintptr_t)(b.stem + lo) & ~uintptr_t(3);
-  const uint32_t lead = (uint32_t)((uintptr_t)(b.stem + lo) - base_addr);
+  const uint32_t lo = b.off[b0], hi = b.off[b1];
+  const uint32_t total = b.off[b.n];
+  const bool range_ok = hi >= lo && hi <= b.stem_cap && total <= b.stem_cap;
+  const uint32_t* words = reinterpret_cast<const uint32_t*>(b.stem);  // 4-byte aligned base
+  const uint32_t lead = lo & 3u;
   const uint32_t nbytes = range_ok ? hi - lo + lead : 0;
   const bool use_lds = range_ok && nbytes + 8 <= HASH_LDS_BYTES;
   if (use_lds) {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(base_addr);
+    const uint32_t* src = words + (lo >> 2);
     const uint32_t nw = (nbytes + 3) / 4;
     for (uint32_t w = tid; w < nw; w += 256) lds[w] = src[w];
     if (tid < 4) lds[nw + tid] = 0;
@@ -99,14 +100,12 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, uint64_t* __restric
   __syncthreads();
   if (i >= b.n) return;
   uint64_t h = 0;
-  if (len) {
+  if (len && range_ok) {
     if (use_lds) {
       h = hash_stem(DwordReader{lds, HASH_LDS_BYTES / 4 + 4}, s0 - lo + lead, len);
     } else {
-      const uintptr_t a = (uintptr_t)(b.stem + s0);
-      const uintptr_t ab = a & ~uintptr_t(3);
-      const uint32_t nw = (uint32_t)(((uintptr_t)(b.stem + s0 + len) - ab + 3) / 4);
-      h = hash_stem(DwordReader{reinterpret_cast<const uint32_t*>(ab), nw}, (uint32_t)(a - ab), len);
+      const uint32_t nw = ((total + 3u) >> 2) - (s0 >> 2);
+      h = hash_stem(DwordReader{words + (s0 >> 2), nw}, s0 & 3u, len);
     }
   }
   hstem[i] = h;
@@ -256,11 +255,13 @@ struct StemRef {
   __device__ inline uint32_t word(uint32_t k) const { return __builtin_amdgcn_alignbyte(at(k + 1), at(k), sh); }  // shift in BYTES
 };
 
+// b.stem is 4-byte aligned (checked on the host). Pointers are derived from the
+// kernel argument by arithmetic only, so loads stay global_* (an integer
+// round trip would make them flat_*, which serialise vmcnt and lgkmcnt waits).
 __device__ inline StemRef stem_ref(const BatchDev& b, uint32_t e) {
-  const uintptr_t a = (uintptr_t)(b.stem + b.off[e]);
-  const uintptr_t ab = a & ~uintptr_t(3);
-  const uintptr_t end = (uintptr_t)(b.stem + b.stem_total);
-  return StemRef{reinterpret_cast<const uint32_t*>(ab), (uint32_t)(a - ab), (uint32_t)((end - ab + 3) / 4)};
+  const uint32_t o = b.off[e];
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(b.stem);
+  return StemRef{w + (o >> 2), o & 3u, ((b.stem_total + 3u) >> 2) - (o >> 2)};
 }
 
 __device__ inline uint32_t tail_mask(uint32_t len) { return (len & 3) ? ((1u << ((len & 3) * 8)) - 1u) : 0u; }
@@ -377,12 +378,15 @@ __device__ int64_t find_slot(const TableDev& t, uint64_t tag, const StemRef& ste
 constexpr uint32_t LDS_RULES = 512;
 constexpr uint32_t MAX_REPS = 8;
 
+// Block stats table in dynamic LDS (n_rules x RL_NUM_STATS u64, n_rules <= LDS_RULES).
+extern __shared__ unsigned long long rl_sacc[];
+
 struct StatAcc {
-  unsigned long long* lds;   // LDS_RULES * RL_NUM_STATS, or null
+  bool use_lds;
   unsigned long long* glob;  // rl_result.stats (no LDS)
   __device__ inline void add(uint32_t rule, uint32_t which, unsigned long long v) {
     if (!v) return;
-    if (lds) atomicAdd(&lds[rule * RL_NUM_STATS + which], v);
+    if (use_lds) atomicAdd(&rl_sacc[rule * RL_NUM_STATS + which], v);
     else atomicAdd(&glob[(size_t)rule * RL_NUM_STATS + which], v);
   }
 };
@@ -658,19 +662,18 @@ __device__ __attribute__((always_inline)) inline void replay_simple(const BatchD
   s->prev = S.prev;
 }
 
-__device__ inline void stats_block_begin(unsigned long long* sacc, bool use_lds, uint32_t n_rules) {
+__device__ inline void stats_block_begin(bool use_lds, uint32_t n_rules) {
   if (use_lds)
-    for (uint32_t j = threadIdx.x; j < n_rules * RL_NUM_STATS; j += blockDim.x) sacc[j] = 0;
+    for (uint32_t j = threadIdx.x; j < n_rules * RL_NUM_STATS; j += blockDim.x) rl_sacc[j] = 0;
   __syncthreads();
 }
 
-__device__ inline void stats_block_end(unsigned long long* sacc, bool use_lds, uint32_t n_rules,
-                                       unsigned long long* stripes) {
+__device__ inline void stats_block_end(bool use_lds, uint32_t n_rules, unsigned long long* stripes) {
   __syncthreads();
   if (use_lds) {
     unsigned long long* dst = stripes + (size_t)(blockIdx.x % STAT_STRIPES) * n_rules * RL_NUM_STATS;
     for (uint32_t j = threadIdx.x; j < n_rules * RL_NUM_STATS; j += blockDim.x) {
-      const unsigned long long v = sacc[j];
+      const unsigned long long v = rl_sacc[j];
       if (v) atomicAdd(&dst[j], v);
     }
   }
@@ -884,7 +887,6 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
                                               uint32_t* __restrict__ run_f, const uint32_t* num_runs,
                                               uint32_t* __restrict__ defer, uint32_t* defer_n,
                                               unsigned long long* stripes, uint32_t* err, int restore) {
-  __shared__ unsigned long long sacc[LDS_RULES * RL_NUM_STATS];
   __shared__ uint32_t s_err, s_nr;
   // err may change while this kernel runs (other blocks): read it once per block
   if (threadIdx.x == 0) {
@@ -895,8 +897,8 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
   if (s_err || blockIdx.x * 256 >= s_nr) return;
   b.stem_total = b.off[b.n];
   const bool use_lds = !restore && b.n_rules <= LDS_RULES;
-  stats_block_begin(sacc, use_lds, b.n_rules);
-  StatAcc acc{use_lds ? sacc : nullptr, o.stats};
+  stats_block_begin(use_lds, b.n_rules);
+  StatAcc acc{use_lds, o.stats};
   LaneStats L;
   L.reset();
   const uint32_t r = blockIdx.x * 256 + threadIdx.x;
@@ -963,7 +965,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
     }
   }
   if (!restore) wave_flush(L, acc);
-  stats_block_end(sacc, use_lds, b.n_rules, stripes);
+  stats_block_end(use_lds, b.n_rules, stripes);
 }
 
 // ---- parallel path for long uniform runs (one stem, one unit, one window).
@@ -1007,14 +1009,13 @@ __global__ __launch_bounds__(256) void k_fast_emit(BatchDev b, OutDev o, TableDe
                                                    const uint4* __restrict__ run_state,
                                                    const uint32_t* __restrict__ run_f, unsigned long long* stripes,
                                                    const uint32_t* err) {
-  __shared__ unsigned long long sacc[LDS_RULES * RL_NUM_STATS];
   __shared__ uint32_t s_err;
   if (threadIdx.x == 0) s_err = *err;
   __syncthreads();
   if (s_err) return;
   const bool use_lds = b.n_rules <= LDS_RULES;
-  stats_block_begin(sacc, use_lds, b.n_rules);
-  StatAcc acc{use_lds ? sacc : nullptr, o.stats};
+  stats_block_begin(use_lds, b.n_rules);
+  StatAcc acc{use_lds, o.stats};
   LaneStats L;
   L.reset();
   const uint32_t q = blockIdx.x * 256 + threadIdx.x;
@@ -1048,7 +1049,7 @@ __global__ __launch_bounds__(256) void k_fast_emit(BatchDev b, OutDev o, TableDe
     }
   }
   wave_flush(L, acc);
-  stats_block_end(sacc, use_lds, b.n_rules, stripes);
+  stats_block_end(use_lds, b.n_rules, stripes);
 }
 
 // ---- k_runs_general: deferred runs (hash-prefix collisions, multi-unit
@@ -1060,7 +1061,6 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, OutDev o, Tabl
                                                       const uint32_t* __restrict__ defer, const uint32_t* defer_n,
                                                       uint8_t* __restrict__ repid, unsigned long long* stripes,
                                                       uint32_t* err, int restore) {
-  __shared__ unsigned long long sacc[LDS_RULES * RL_NUM_STATS];
   __shared__ uint32_t s_err, s_n;
   if (threadIdx.x == 0) {
     s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1070,8 +1070,8 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, OutDev o, Tabl
   if (s_err || blockIdx.x * 256 >= s_n) return;
   b.stem_total = b.off[b.n];
   const bool use_lds = !restore && b.n_rules <= LDS_RULES;
-  stats_block_begin(sacc, use_lds, b.n_rules);
-  StatAcc acc{use_lds ? sacc : nullptr, o.stats};
+  stats_block_begin(use_lds, b.n_rules);
+  StatAcc acc{use_lds, o.stats};
   LaneStats L;
   L.reset();
   const uint32_t di = blockIdx.x * 256 + threadIdx.x;
@@ -1164,7 +1164,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, OutDev o, Tabl
     }
   }
   if (!restore) wave_flush(L, acc);
-  stats_block_end(sacc, use_lds, b.n_rules, stripes);
+  stats_block_end(use_lds, b.n_rules, stripes);
 }
 
 // Fold the striped per-block partial stats into rl_result.stats and clear them.
@@ -1290,14 +1290,15 @@ void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, cons
                                     s.rid, s.run_start, s.run_flags, s.num_runs, s.err);
     k_run_check<<<g, 256, 0, st>>>(b, s.vals[0], s.hstem, s.rid, s.run_start, s.run_flags, s.err);
     (void)hipMemsetAsync(s.defer_n, 0, sizeof(uint32_t), st);
-    k_runs<<<g, 256, 0, st>>>(b, o, t, P, s.vals[0], s.hstem, s.run_start, s.run_flags, s.run_state, s.run_f,
+    const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
+    k_runs<<<g, 256, lds, st>>>(b, o, t, P, s.vals[0], s.hstem, s.run_start, s.run_flags, s.run_state, s.run_f,
                               s.num_runs, s.defer, s.defer_n, s.stripes, s.err, restore);
-    k_runs_general<<<g, 256, 0, st>>>(b, o, t, P, s.keys[0], s.vals[0], s.hstem, s.defer, s.defer_n, s.repid,
+    k_runs_general<<<g, 256, lds, st>>>(b, o, t, P, s.keys[0], s.vals[0], s.hstem, s.defer, s.defer_n, s.repid,
                                       s.stripes, s.err, restore);
     if (!restore) {
       if (P.lc_en)
         k_fast_over<<<g, 256, 0, st>>>(b, s.vals[0], s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.err);
-      k_fast_emit<<<g, 256, 0, st>>>(b, o, t, P, s.vals[0], s.segsum, s.rid, s.run_start, s.run_flags, s.run_state,
+      k_fast_emit<<<g, 256, lds, st>>>(b, o, t, P, s.vals[0], s.segsum, s.rid, s.run_start, s.run_flags, s.run_state,
                                      s.run_f, s.stripes, s.err);
       if (b.n_rules <= LDS_RULES && b.n_rules)
         k_stats_fold<<<cdiv(b.n_rules * RL_NUM_STATS, 256), 256, 0, st>>>(s.stripes, b.n_rules, o.stats, s.err);
