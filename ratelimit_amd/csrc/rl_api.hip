@@ -221,7 +221,8 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
   ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess;
   ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess;
-  ok = ok && dalloc(&c->s.hstem, n) == hipSuccess;
+  ok = ok && dalloc(&c->s.rec, n) == hipSuccess && dalloc(&c->s.rec_s, n) == hipSuccess &&
+       dalloc(&c->s.res, n) == hipSuccess;
   for (int i = 0; i < 2; i++) {
     ok = ok && dalloc(&c->s.keys[i], n) == hipSuccess;
     ok = ok && dalloc(&c->s.vals[i], n) == hipSuccess;
@@ -274,7 +275,7 @@ void rl_destroy(rl_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (int i = 0; i < 4; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
-  void* bufs[] = {c->slots, c->arena, c->s.hstem, c->s.keys[0], c->s.keys[1], c->s.vals[0], c->s.vals[1],
+  void* bufs[] = {c->slots, c->arena, c->s.rec, c->s.rec_s, c->s.res, c->s.keys[0], c->s.keys[1], c->s.vals[0], c->s.vals[1],
                   c->s.hist, c->s.hist_tot, c->s.repid, c->s.defer, c->s.defer_n, c->s.stripes, c->s.tile_f, c->s.tile_s, c->s.tile_h, c->s.segsum, c->s.rid,
                   c->s.run_start, c->s.run_flags, c->s.run_state, c->s.run_f, c->s.num_runs, c->s.err, c->s.time_floor, c->s.counters, c->d_stem, c->d_off, c->d_now,
                   c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_rem,

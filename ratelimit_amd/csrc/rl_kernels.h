@@ -21,7 +21,7 @@ constexpr uint32_t STAT_LDS_RULES = 512;  // rules aggregated in LDS (== LDS_RUL
 struct BatchDev {
   uint32_t n, n_req, n_rules, stem_cap;
   uint32_t stem_total;  // bytes of packed stems (off[n]); reads stay below it
-  const uint8_t* stem;
+  const uint8_t* stem;  // 4-byte aligned
   const uint32_t* off;
   const int64_t* now;
   const uint32_t* req;
@@ -31,6 +31,25 @@ struct BatchDev {
   const uint32_t* hits;
   const uint32_t* rule;
 };
+
+// One descriptor, packed by k_prepare (arrival order) and gathered once into
+// sorted order, so the run kernels read one 32-B record per descriptor,
+// contiguously per run, instead of ~10 scattered fields.
+struct __attribute__((aligned(16))) Rec {
+  uint32_t hlo;    // low 32 bits of the stem hash (high 32 bits = sort key)
+  uint32_t off;    // stem byte offset
+  uint32_t lu;     // stem length (16) | unit << 16 | flags << 24
+  uint32_t rule;
+  uint32_t req;
+  uint32_t now;    // now[req] (validated to fit 32 bits)
+  uint32_t hits;   // raw HitsAddend (restore records: the count)
+  uint32_t limit;
+};
+static_assert(sizeof(Rec) == 32, "Rec is two dwordx4");
+
+__host__ __device__ inline uint32_t rec_len(const Rec& r) { return r.lu & 0xFFFFu; }
+__host__ __device__ inline uint32_t rec_unit(const Rec& r) { return (r.lu >> 16) & 0xFFu; }
+__host__ __device__ inline uint32_t rec_flags(const Rec& r) { return r.lu >> 24; }
 
 struct OutDev {
   uint8_t* code;
@@ -56,7 +75,9 @@ struct Params {
 
 // Per-batch scratch (device), sized for max_batch.
 struct Scratch {
-  uint64_t* hstem;
+  Rec* rec;                  // [n] arrival order
+  Rec* rec_s;                // [n] sorted order
+  unsigned long long* res;   // [n] packed result per descriptor (arrival order)
   uint32_t* keys[2];
   uint32_t* vals[2];
   uint32_t* hist;      // 256 x ntiles, digit-major
@@ -81,7 +102,7 @@ struct Scratch {
 
 // Launch the whole DoLimit pipeline (restore = 1: table seeding records).
 // ev (optional, 4 events): recorded before k_prepare, after it, after the
-// sort and after k_runs on stream st (per-stage timing, rl_profile).
+// sort and after the run kernels on stream st (per-stage timing, rl_profile).
 void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
                      int restore, hipStream_t st, hipEvent_t* ev = nullptr);
 void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st);

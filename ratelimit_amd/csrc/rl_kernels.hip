@@ -1,13 +1,19 @@
 // rl_kernels.hip — gfx950 kernels of the fixed-window rate-limit backend.
 //
-// Pipeline for one batch (all on one HIP stream, inputs already in HBM):
-//   k_prepare     validate the packed batch; hash every stem (LDS-staged bytes)
+// Pipeline for one batch (one HIP stream, inputs already in HBM):
+//   k_prepare     validate the packed batch; hash every stem (LDS-staged
+//                 bytes); pack each descriptor into a 32-B Rec
 //   radix sort    stable LSD sort of (hash[63:32], index): groups each stem's
 //                 descriptors together, in arrival (sequence) order
-//   k_runs        one lane per same-hash run = one stem (hash ties split
-//                 exactly by byte compare): find-or-insert the (stem, unit)
-//                 slot in the HBM table and replay the run in order — the
-//                 reference's sequential INCRBY/EXPIRE/local-cache semantics
+//   k_gather      Recs into sorted order (one random 32-B read each)
+//   k_seg_*       run ids + in-run prefix sums of hits (3-phase segmented scan)
+//   k_run_check   long runs: every element shares stem, unit and window?
+//   k_runs        one lane per run: find-or-insert the (stem, unit) slot of
+//                 the HBM table; replay short runs in registers, set up long
+//                 uniform runs for k_fast_*, defer the rest to k_runs_general
+//   k_fast_*      long uniform runs decided in parallel (scan + first-over)
+//   k_stats_fold  striped per-block stats -> rl_result.stats
+//   k_unpack      packed results -> code / limit_remaining / reset_s
 // plus k_sweep (epoch sweep = Redis EXPIRE), k_table_info, debug kernels.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -18,7 +24,7 @@
 namespace rl {
 
 // ===========================================================================
-// k_prepare: validation + stem hashing.
+// k_prepare: validation, stem hashing, record packing (arrival order).
 // Each 256-thread block stages the contiguous byte range of its 256 stems in
 // LDS with coalesced dword loads, then every lane hashes its own stem from LDS.
 // ===========================================================================
@@ -52,9 +58,9 @@ struct DwordReader {
   }
 };
 
-__global__ __launch_bounds__(256) void k_prepare(BatchDev b, uint64_t* __restrict__ hstem,
-                                                 uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                 uint32_t* err, const int64_t* time_floor) {
+__global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ rec, uint32_t* __restrict__ keys,
+                                                 uint32_t* __restrict__ vals, uint32_t* err,
+                                                 const int64_t* time_floor) {
   __shared__ uint32_t lds[HASH_LDS_BYTES / 4 + 4];
   const uint32_t tid = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + tid;
@@ -67,13 +73,14 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, uint64_t* __restric
   }
 
   // ---- per-descriptor checks
-  uint32_t s0 = 0, len = 0;
+  uint32_t s0 = 0, len = 0, u = 0, q = 0;
   if (i < b.n) {
     s0 = b.off[i];
-    uint32_t s1 = b.off[i + 1];
-    uint32_t u = b.unit[i];
-    if (u < 1 || u > 4 || b.rule[i] >= b.n_rules || b.req[i] >= b.n_req || (i && b.req[i - 1] > b.req[i]) ||
-        s1 < s0 || s1 > b.stem_cap || s1 - s0 == 0 || s1 - s0 > 65535)
+    const uint32_t s1 = b.off[i + 1];
+    u = b.unit[i];
+    q = b.req[i];
+    if (u < 1 || u > 4 || b.rule[i] >= b.n_rules || q >= b.n_req || (i && b.req[i - 1] > q) || s1 < s0 ||
+        s1 > b.stem_cap || s1 - s0 == 0 || s1 - s0 > 65535)
       bad |= ERR_INVALID;
     else
       len = s1 - s0;
@@ -108,9 +115,18 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, uint64_t* __restric
       h = hash_stem(DwordReader{words + (s0 >> 2), nw}, s0 & 3u, len);
     }
   }
-  hstem[i] = h;
   keys[i] = (uint32_t)(h >> 32);
   vals[i] = i;
+  Rec r;
+  r.hlo = (uint32_t)h;
+  r.off = s0;
+  r.lu = len | (u << 16) | ((uint32_t)b.flags[i] << 24);
+  r.rule = b.rule[i];
+  r.req = q;
+  r.now = (q < b.n_req) ? (uint32_t)b.now[q] : 0u;
+  r.hits = b.hits[i];
+  r.limit = b.limit[i];
+  rec[i] = r;
 }
 
 // ===========================================================================
@@ -241,6 +257,14 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t* __restrict__
   }
 }
 
+// Records into sorted order.
+__global__ __launch_bounds__(256) void k_gather(const Rec* __restrict__ rec, const uint32_t* __restrict__ svals,
+                                                uint32_t n, Rec* __restrict__ rec_s, const uint32_t* err) {
+  if (*err) return;
+  const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+  if (q < n) rec_s[q] = rec[svals[q]];
+}
+
 // ===========================================================================
 // Stem bytes as dwords. Stems sit at arbitrary byte offsets of the packed
 // buffer; a StemRef reads them as aligned dwords and funnel-shifts
@@ -252,21 +276,19 @@ struct StemRef {
   uint32_t sh;        // byte offset of the stem's first byte in p[0]
   uint32_t nw;        // readable dwords from p
   __device__ inline uint32_t at(uint32_t i) const { return i < nw ? p[i] : 0u; }
-  __device__ inline uint32_t word(uint32_t k) const { return __builtin_amdgcn_alignbyte(at(k + 1), at(k), sh); }  // shift in BYTES
+  __device__ inline uint32_t word(uint32_t k) const { return __builtin_amdgcn_alignbyte(at(k + 1), at(k), sh); }
 };
 
 // b.stem is 4-byte aligned (checked on the host). Pointers are derived from the
 // kernel argument by arithmetic only, so loads stay global_* (an integer
-// round trip would make them flat_*, which serialise vmcnt and lgkmcnt waits).
-__device__ inline StemRef stem_ref(const BatchDev& b, uint32_t e) {
-  const uint32_t o = b.off[e];
+// round trip would make them flat_*).
+__device__ inline StemRef stem_ref(const BatchDev& b, uint32_t o) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(b.stem);
   return StemRef{w + (o >> 2), o & 3u, ((b.stem_total + 3u) >> 2) - (o >> 2)};
 }
 
 __device__ inline uint32_t tail_mask(uint32_t len) { return (len & 3) ? ((1u << ((len & 3) * 8)) - 1u) : 0u; }
 
-// bytes [4*w0, 4*w0 + len) of x and y equal (x at word offset w0 too)
 __device__ inline bool stem_words_equal(const StemRef& x, const StemRef& y, uint32_t len) {
   uint32_t diff = 0;
   const uint32_t nw = len >> 2;
@@ -375,7 +397,7 @@ __device__ int64_t find_slot(const TableDev& t, uint64_t tag, const StemRef& ste
 // into rl_result.stats by k_stats_fold. With more than LDS_RULES rules the
 // wave sums go straight to rl_result.stats.
 // ===========================================================================
-constexpr uint32_t LDS_RULES = 512;
+constexpr uint32_t LDS_RULES = STAT_LDS_RULES;
 constexpr uint32_t MAX_REPS = 8;
 
 // Block stats table in dynamic LDS (n_rules x RL_NUM_STATS u64, n_rules <= LDS_RULES).
@@ -437,6 +459,23 @@ __device__ __attribute__((always_inline)) inline void wave_flush(LaneStats& L, S
   }
 }
 
+__device__ inline void stats_block_begin(bool use_lds, uint32_t n_rules) {
+  if (use_lds)
+    for (uint32_t j = threadIdx.x; j < n_rules * RL_NUM_STATS; j += blockDim.x) rl_sacc[j] = 0;
+  __syncthreads();
+}
+
+__device__ inline void stats_block_end(bool use_lds, uint32_t n_rules, unsigned long long* stripes) {
+  __syncthreads();
+  if (use_lds) {
+    unsigned long long* dst = stripes + (size_t)(blockIdx.x % STAT_STRIPES) * n_rules * RL_NUM_STATS;
+    for (uint32_t j = threadIdx.x; j < n_rules * RL_NUM_STATS; j += blockDim.x) {
+      const unsigned long long v = rl_sacc[j];
+      if (v) atomicAdd(&dst[j], v);
+    }
+  }
+}
+
 // ===========================================================================
 // Replaying a stem's descriptors in arrival order.
 //
@@ -452,40 +491,42 @@ __device__ __attribute__((always_inline)) inline void wave_flush(LaneStats& L, S
 struct Elem {
   uint32_t e, req, now, unit, d, w, h, thr, rule;
   bool shadow;
+  uint8_t flags;
 };
 
-__device__ inline Elem load_elem(const BatchDev& b, uint32_t e, bool restore) {
+__device__ inline Elem load_elem(const Rec& r, uint32_t e, bool restore) {
   Elem x;
   x.e = e;
-  x.req = b.req[e];
-  x.now = (uint32_t)b.now[x.req];
-  x.unit = b.unit[e];
+  x.req = r.req;
+  x.now = r.now;
+  x.unit = rec_unit(r);
   x.d = div_of(x.unit);
   x.w = x.now - x.now % x.d;
-  const uint32_t hv = b.hits[e];
-  x.h = restore ? hv : (hv > 1 ? hv : 1u);  // utils.Max(1, HitsAddend)
-  x.thr = b.limit[e];
-  x.rule = b.rule[e];
-  x.shadow = (b.flags[e] & RL_FLAG_SHADOW) != 0;
+  x.h = restore ? r.hits : (r.hits > 1 ? r.hits : 1u);  // utils.Max(1, HitsAddend)
+  x.thr = r.limit;
+  x.rule = r.rule;
+  x.flags = (uint8_t)rec_flags(r);
+  x.shadow = (x.flags & RL_FLAG_SHADOW) != 0;
   return x;
 }
 
-__device__ __attribute__((always_inline)) inline void emit(const OutDev& o, LaneStats& L, StatAcc& acc, const Elem& x, const Decision& r) {
-  o.code[x.e] = r.code;
-  o.rem[x.e] = r.remaining;
-  o.reset[x.e] = x.d - x.now % x.d;  // utils.CalculateReset
+// One 8-B store per descriptor: remaining | reset << 32 | code << 56 (k_unpack).
+__device__ __attribute__((always_inline)) inline void emit(unsigned long long* res, LaneStats& L, StatAcc& acc,
+                                                           const Elem& x, const Decision& r) {
+  const uint32_t reset = x.d - x.now % x.d;  // utils.CalculateReset
+  res[x.e] = (unsigned long long)r.remaining | ((unsigned long long)reset << 32) |
+             ((unsigned long long)r.code << 56);
   const uint32_t d[RL_NUM_STATS] = {x.h, r.d_over, r.d_near, r.d_lc, r.d_within, r.d_shadow};
   L.add(acc, x.rule, d);
 }
 
-// The record of window w in a slot's (cur, prev) pair. cur is the newest window
-// ever written for this (stem, unit), prev the newest before it, so a window
-// strictly between them was never written (a fresh key): it takes prev's place.
-// A newer window rolls cur into prev. A window older than prev is outside the
-// table's history: null -> RL_E_TIME, never silently wrong. With allow_back
-// false (multi-unit stems, where other units may alias the key) only the
-// current or a newer window is accepted.
-// Returns 0 (cur), 1 (prev) or -1 (older than the history); may roll.
+// The record of window w in a slot's (cur, prev) pair: 0 (cur), 1 (prev) or
+// -1. cur is the newest window ever written for this (stem, unit), prev the
+// newest before it, so a window strictly between them was never written (a
+// fresh key): it takes prev's place. A newer window rolls cur into prev. A
+// window older than prev is outside the table's history: -1 -> RL_E_TIME,
+// never silently wrong. With allow_back false (multi-unit stems, where other
+// units may alias the key) only the current or a newer window is accepted.
 __device__ __attribute__((always_inline)) inline int window_pick(Win& cur, Win& prev, uint32_t w, uint32_t lc_init,
                                                                 bool allow_back) {
   if (cur.ws == w) return 0;
@@ -518,8 +559,9 @@ struct SimpleState {
   }
 };
 
-__device__ __attribute__((always_inline)) inline void simple_step(const Params& P, const OutDev& o, LaneStats& L, StatAcc& acc, SimpleState& S,
-                                   const Elem& x, bool restore, uint8_t restore_lc, uint32_t* err) {
+__device__ __attribute__((always_inline)) inline void simple_step(const Params& P, unsigned long long* res,
+                                                                  LaneStats& L, StatAcc& acc, SimpleState& S,
+                                                                  const Elem& x, bool restore, uint32_t* err) {
   if (x.req != S.cur_req) {
     S.apply_pending();
     S.cur_req = x.req;
@@ -535,7 +577,7 @@ __device__ __attribute__((always_inline)) inline void simple_step(const Params& 
   if (restore) {
     R.count = x.h;
     R.expire = x.now + x.d;
-    if (restore_lc) R.lc = x.now + x.d;
+    if (x.flags) R.lc = x.now + x.d;  // restore records: flags = local-cache bit
   } else {
     lc_hit = P.lc_en && x.now < R.lc;  // freecache Get (hit while now < expireAt)
     if (!lc_hit) {
@@ -554,7 +596,7 @@ __device__ __attribute__((always_inline)) inline void simple_step(const Params& 
     S.pend_w = x.w;
     S.pend_e = x.now + x.d;
   }
-  emit(o, L, acc, x, r);
+  emit(res, L, acc, x, r);
 }
 
 // ---- general: every unit slot of the stem, Redis keys shared across units
@@ -580,8 +622,8 @@ __device__ inline void general_apply_pending(GeneralState& G) {
   G.npend = 0;
 }
 
-__device__ inline void general_step(const Params& P, const OutDev& o, LaneStats& L, StatAcc& acc, GeneralState& G,
-                                    const Elem& x, bool restore, uint8_t restore_lc, uint32_t* err) {
+__device__ inline void general_step(const Params& P, unsigned long long* res, LaneStats& L, StatAcc& acc,
+                                    GeneralState& G, const Elem& x, bool restore, uint32_t* err) {
   if (x.req != G.cur_req) {
     general_apply_pending(G);
     G.cur_req = x.req;
@@ -622,7 +664,7 @@ __device__ inline void general_step(const Params& P, const OutDev& o, LaneStats&
     after = nv;
   }
   if (restore) {
-    if (restore_lc) {
+    if (x.flags) {
       for (uint32_t k = 0; k < 4; k++) {
         if (!(G.present >> k & 1)) continue;
         if (G.cur[k].ws == x.w) G.cur[k].lc = x.now + x.d;
@@ -639,13 +681,17 @@ __device__ inline void general_step(const Params& P, const OutDev& o, LaneStats&
     G.pend_w[j] = x.w;
     G.pend_e[j] = x.now + x.d;
   }
-  emit(o, L, acc, x, r);
+  emit(res, L, acc, x, r);
 }
 
-// Replay elements [p, end) of a single-unit stem through its slot s0 (registers).
-__device__ __attribute__((always_inline)) inline void replay_simple(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P,
-                                     const uint32_t* svals, const uint8_t* repid, uint32_t p, uint32_t end, uint32_t k,
-                                     int64_t s0, LaneStats& L, StatAcc& acc, uint32_t* err, bool restore) {
+// Replay elements [p, end) (those of stem k when repid is given) through the
+// single-unit slot s0, in registers.
+__device__ __attribute__((always_inline)) inline void replay_simple(const Rec* rec_s, const uint32_t* svals,
+                                                                    unsigned long long* res, const TableDev& t,
+                                                                    const Params& P, const uint8_t* repid,
+                                                                    uint32_t p, uint32_t end, uint32_t k, int64_t s0,
+                                                                    LaneStats& L, StatAcc& acc, uint32_t* err,
+                                                                    bool restore) {
   Slot* s = &t.slots[s0];
   SimpleState S;
   S.cur = s->cur;
@@ -654,29 +700,11 @@ __device__ __attribute__((always_inline)) inline void replay_simple(const BatchD
   S.pend = false;
   for (uint32_t q = p; q < end; q++) {
     if (repid && ((q == p) ? 0u : repid[q]) != k) continue;
-    const uint32_t e = svals[q];
-    simple_step(P, o, L, acc, S, load_elem(b, e, restore), restore, b.flags[e], err);
+    simple_step(P, res, L, acc, S, load_elem(rec_s[q], svals[q], restore), restore, err);
   }
   S.apply_pending();
   s->cur = S.cur;
   s->prev = S.prev;
-}
-
-__device__ inline void stats_block_begin(bool use_lds, uint32_t n_rules) {
-  if (use_lds)
-    for (uint32_t j = threadIdx.x; j < n_rules * RL_NUM_STATS; j += blockDim.x) rl_sacc[j] = 0;
-  __syncthreads();
-}
-
-__device__ inline void stats_block_end(bool use_lds, uint32_t n_rules, unsigned long long* stripes) {
-  __syncthreads();
-  if (use_lds) {
-    unsigned long long* dst = stripes + (size_t)(blockIdx.x % STAT_STRIPES) * n_rules * RL_NUM_STATS;
-    for (uint32_t j = threadIdx.x; j < n_rules * RL_NUM_STATS; j += blockDim.x) {
-      const unsigned long long v = rl_sacc[j];
-      if (v) atomicAdd(&dst[j], v);
-    }
-  }
 }
 
 // ===========================================================================
@@ -713,19 +741,18 @@ __device__ inline void seg_block_scan(SegPair& v, uint32_t& hc, SegPair* sp, uin
   }
 }
 
-__device__ inline void seg_load(const uint32_t* skeys, const uint32_t* svals, const uint32_t* hits, uint32_t n,
-                                uint32_t q, bool& valid, bool& head, uint32_t& h) {
+__device__ inline void seg_load(const uint32_t* skeys, const Rec* rec_s, uint32_t n, uint32_t q, bool& valid,
+                                bool& head, uint32_t& h) {
   valid = q < n;
   head = valid && (q == 0 || skeys[q - 1] != skeys[q]);
-  const uint32_t hv = valid ? hits[svals[q]] : 0u;
+  const uint32_t hv = valid ? rec_s[q].hits : 0u;
   h = valid ? (hv > 1 ? hv : 1u) : 0u;
 }
 
-__global__ __launch_bounds__(256) void k_seg_reduce(const uint32_t* __restrict__ skeys,
-                                                    const uint32_t* __restrict__ svals,
-                                                    const uint32_t* __restrict__ hits, uint32_t n,
-                                                    uint32_t* __restrict__ tile_f, uint32_t* __restrict__ tile_s,
-                                                    uint32_t* __restrict__ tile_h, const uint32_t* err) {
+__global__ __launch_bounds__(256) void k_seg_reduce(const uint32_t* __restrict__ skeys, const Rec* __restrict__ rec_s,
+                                                    uint32_t n, uint32_t* __restrict__ tile_f,
+                                                    uint32_t* __restrict__ tile_s, uint32_t* __restrict__ tile_h,
+                                                    const uint32_t* err) {
   __shared__ SegPair sp[256];
   __shared__ uint32_t sh[256];
   if (*err) return;
@@ -735,7 +762,7 @@ __global__ __launch_bounds__(256) void k_seg_reduce(const uint32_t* __restrict__
   for (uint32_t i = 0; i < SEG_ITEMS; i++) {
     bool valid, head;
     uint32_t h;
-    seg_load(skeys, svals, hits, n, base + i, valid, head, h);
+    seg_load(skeys, rec_s, n, base + i, valid, head, h);
     if (!valid) break;
     v = seg_op(v, SegPair{head ? 1u : 0u, h});
     hc += head;
@@ -793,10 +820,8 @@ __global__ __launch_bounds__(1024) void k_seg_tiles(uint32_t* __restrict__ tile_
   }
 }
 
-__global__ __launch_bounds__(256) void k_seg_apply(const uint32_t* __restrict__ skeys,
-                                                   const uint32_t* __restrict__ svals,
-                                                   const uint32_t* __restrict__ hits, uint32_t n,
-                                                   const uint32_t* __restrict__ tile_f,
+__global__ __launch_bounds__(256) void k_seg_apply(const uint32_t* __restrict__ skeys, const Rec* __restrict__ rec_s,
+                                                   uint32_t n, const uint32_t* __restrict__ tile_f,
                                                    const uint32_t* __restrict__ tile_s,
                                                    const uint32_t* __restrict__ tile_h, uint32_t* __restrict__ segsum,
                                                    uint32_t* __restrict__ rid, uint32_t* __restrict__ run_start,
@@ -811,13 +836,11 @@ __global__ __launch_bounds__(256) void k_seg_apply(const uint32_t* __restrict__ 
   for (uint32_t i = 0; i < SEG_ITEMS; i++) {
     bool valid, head;
     uint32_t h;
-    seg_load(skeys, svals, hits, n, base + i, valid, head, h);
+    seg_load(skeys, rec_s, n, base + i, valid, head, h);
     if (!valid) break;
     v = seg_op(v, SegPair{head ? 1u : 0u, h});
     hc += head;
   }
-  const SegPair mine = v;
-  const uint32_t mine_h = hc;
   seg_block_scan(v, hc, sp, sh);
   // exclusive prefix of this thread = tile carry + block exclusive
   SegPair run = SegPair{tile_f[blockIdx.x], tile_s[blockIdx.x]};
@@ -826,13 +849,11 @@ __global__ __launch_bounds__(256) void k_seg_apply(const uint32_t* __restrict__ 
     run = seg_op(run, sp[threadIdx.x - 1]);
     hrun += sh[threadIdx.x - 1];
   }
-  (void)mine;
-  (void)mine_h;
   for (uint32_t i = 0; i < SEG_ITEMS; i++) {
     const uint32_t q = base + i;
     bool valid, head;
     uint32_t h;
-    seg_load(skeys, svals, hits, n, q, valid, head, h);
+    seg_load(skeys, rec_s, n, q, valid, head, h);
     if (!valid) break;
     run = seg_op(run, SegPair{head ? 1u : 0u, h});
     hrun += head;
@@ -852,25 +873,22 @@ __global__ __launch_bounds__(256) void k_seg_apply(const uint32_t* __restrict__ 
 
 // Long runs only: every element must share the head's stem, unit and window
 // for the parallel path; otherwise the run is replayed serially.
-__global__ __launch_bounds__(256) void k_run_check(BatchDev b, const uint32_t* __restrict__ svals,
-                                                   const uint64_t* __restrict__ hstem,
+__global__ __launch_bounds__(256) void k_run_check(BatchDev b, const Rec* __restrict__ rec_s,
                                                    const uint32_t* __restrict__ rid,
                                                    const uint32_t* __restrict__ run_start,
                                                    uint32_t* __restrict__ run_flags, const uint32_t* err) {
   if (*err) return;
   const uint32_t q = blockIdx.x * 256 + threadIdx.x;
   if (q >= b.n) return;
-  b.stem_total = b.off[b.n];
   const uint32_t r = rid[q];
   const uint32_t p = run_start[r];
   if (q == p || run_start[r + 1] - p < LONG_RUN) return;
-  const uint32_t e0 = svals[p], e = svals[q];
-  const uint32_t len0 = b.off[e0 + 1] - b.off[e0];
-  bool same = hstem[e] == hstem[e0] && b.unit[e] == b.unit[e0] && b.off[e + 1] - b.off[e] == len0;
+  b.stem_total = b.off[b.n];
+  const Rec x0 = rec_s[p], x = rec_s[q];
+  bool same = x.hlo == x0.hlo && (x.lu & 0xFFFFFFu) == (x0.lu & 0xFFFFFFu);  // hash, length, unit
   if (same) {
-    const uint32_t d = div_of(b.unit[e]);
-    const uint32_t n0 = (uint32_t)b.now[b.req[e0]], n1 = (uint32_t)b.now[b.req[e]];
-    same = n0 / d == n1 / d && stem_words_equal(stem_ref(b, e), stem_ref(b, e0), len0);
+    const uint32_t d = div_of(rec_unit(x));
+    same = x0.now / d == x.now / d && stem_words_equal(stem_ref(b, x.off), stem_ref(b, x0.off), rec_len(x0));
   }
   if (!same) atomicOr(&run_flags[r], RUN_SLOW);
 }
@@ -879,14 +897,15 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, const uint32_t* _
 // is not flagged multi-unit are replayed here in registers; long uniform runs
 // are set up for the parallel path (k_fast_*); anything else is deferred to
 // k_runs_general.
-__global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, Params P,
-                                              const uint32_t* __restrict__ svals,
-                                              const uint64_t* __restrict__ hstem,
+__global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, const Rec* __restrict__ rec_s,
+                                              const uint32_t* __restrict__ skeys,
+                                              const uint32_t* __restrict__ svals, unsigned long long* __restrict__ res,
                                               const uint32_t* __restrict__ run_start,
                                               uint32_t* __restrict__ run_flags, uint4* __restrict__ run_state,
                                               uint32_t* __restrict__ run_f, const uint32_t* num_runs,
                                               uint32_t* __restrict__ defer, uint32_t* defer_n,
-                                              unsigned long long* stripes, uint32_t* err, int restore) {
+                                              unsigned long long* stats, unsigned long long* stripes, uint32_t* err,
+                                              int restore) {
   __shared__ uint32_t s_err, s_nr;
   // err may change while this kernel runs (other blocks): read it once per block
   if (threadIdx.x == 0) {
@@ -898,24 +917,24 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
   b.stem_total = b.off[b.n];
   const bool use_lds = !restore && b.n_rules <= LDS_RULES;
   stats_block_begin(use_lds, b.n_rules);
-  StatAcc acc{use_lds, o.stats};
+  StatAcc acc{use_lds, stats};
   LaneStats L;
   L.reset();
   const uint32_t r = blockIdx.x * 256 + threadIdx.x;
   if (r < s_nr) {
     const uint32_t p = run_start[r], end = run_start[r + 1];
     const bool long_run = !restore && end - p >= LONG_RUN && !(run_flags[r] & RUN_SLOW);
-    const uint32_t e0 = svals[p];
-    const uint64_t h0 = hstem[e0];
-    const uint32_t u0 = b.unit[e0];
-    const uint32_t len0 = b.off[e0 + 1] - b.off[e0];
-    const StemRef st0 = stem_ref(b, e0);
+    const Rec x0 = rec_s[p];
+    const uint64_t h0 = ((uint64_t)skeys[p] << 32) | x0.hlo;
+    const uint32_t u0 = rec_unit(x0);
+    const uint32_t len0 = rec_len(x0);
+    const StemRef st0 = stem_ref(b, x0.off);
     bool ok = true;
     if (!long_run) {  // long uniform runs were checked in parallel (k_run_check)
       for (uint32_t q = p + 1; q < end && ok; q++) {
-        const uint32_t e = svals[q];
-        ok = hstem[e] == h0 && b.unit[e] == u0 && b.off[e + 1] - b.off[e] == len0 &&
-             stem_words_equal(stem_ref(b, e), st0, len0);
+        const Rec x = rec_s[q];
+        ok = x.hlo == x0.hlo && (x.lu & 0xFFFFFFu) == (x0.lu & 0xFFFFFFu) &&
+             stem_words_equal(stem_ref(b, x.off), st0, len0);
       }
     }
     int64_t s0 = -1;
@@ -942,16 +961,16 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
       // Parallel path: pick the window record once; k_fast_* decide every element.
       Slot* s = &t.slots[s0];
       Win cur = s->cur, prev = s->prev;
-      const Elem x0 = load_elem(b, e0, false);
-      const int which = window_pick(cur, prev, x0.w, 0, true);
+      const Elem e0 = load_elem(x0, svals[p], false);
+      const int which = window_pick(cur, prev, e0.w, 0, true);
       if (which < 0) {
         atomicOr(err, ERR_HISTORY);
       } else {
         const Win R = which ? prev : cur;
         // A record of window w was written inside w: its EXPIRE and local-cache
         // TTL both end at or after w + div, so they hold for the whole run.
-        const uint32_t c0 = x0.now <= R.expire ? R.count : 0u;
-        const uint32_t F = (P.lc_en && x0.now < R.lc) ? 1u : 0u;
+        const uint32_t c0 = e0.now <= R.expire ? R.count : 0u;
+        const uint32_t F = (P.lc_en && e0.now < R.lc) ? 1u : 0u;
         s->cur = cur;
         s->prev = prev;
         run_state[r] = make_uint4((uint32_t)s0, c0, R.lc, F | ((uint32_t)which << 1));
@@ -959,7 +978,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
         run_flags[r] |= RUN_FAST;
       }
     } else if (ok) {
-      replay_simple(b, o, t, P, svals, nullptr, p, end, 0, s0, L, acc, err, restore);
+      replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, L, acc, err, restore);
     } else if (!(s0 < 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_TABLE_FULL))) {
       defer[atomicAdd(defer_n, 1u)] = p;
     }
@@ -973,7 +992,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, OutDev o, TableDev t, 
 // local cache on, the first element f with a_f > limit_f makes every element of
 // a LATER request a local-cache hit (Set happens after request q_f's statuses),
 // i.e. a suffix of the run, which therefore never increments.
-__global__ __launch_bounds__(256) void k_fast_over(BatchDev b, const uint32_t* __restrict__ svals,
+__global__ __launch_bounds__(256) void k_fast_over(uint32_t n, const Rec* __restrict__ rec_s,
                                                    const uint32_t* __restrict__ segsum,
                                                    const uint32_t* __restrict__ rid,
                                                    const uint32_t* __restrict__ run_flags,
@@ -984,11 +1003,11 @@ __global__ __launch_bounds__(256) void k_fast_over(BatchDev b, const uint32_t* _
   const uint32_t lane = threadIdx.x & 63;
   bool cand = false;
   uint32_t r = 0;
-  if (q < b.n) {
+  if (q < n) {
     r = rid[q];
     if (run_flags[r] & RUN_FAST) {
       const uint4 st = run_state[r];
-      if (!(st.w & 1u)) cand = st.y + segsum[q] > b.limit[svals[q]];
+      if (!(st.w & 1u)) cand = st.y + segsum[q] > rec_s[q].limit;
     }
   }
   uint64_t pending = __ballot(cand);
@@ -1000,47 +1019,52 @@ __global__ __launch_bounds__(256) void k_fast_over(BatchDev b, const uint32_t* _
   }
 }
 
-__global__ __launch_bounds__(256) void k_fast_emit(BatchDev b, OutDev o, TableDev t, Params P,
-                                                   const uint32_t* __restrict__ svals,
+__global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules, TableDev t, Params P,
+                                                   const Rec* __restrict__ rec_s, const uint32_t* __restrict__ svals,
+                                                   unsigned long long* __restrict__ res,
                                                    const uint32_t* __restrict__ segsum,
                                                    const uint32_t* __restrict__ rid,
                                                    const uint32_t* __restrict__ run_start,
                                                    const uint32_t* __restrict__ run_flags,
                                                    const uint4* __restrict__ run_state,
-                                                   const uint32_t* __restrict__ run_f, unsigned long long* stripes,
-                                                   const uint32_t* err) {
+                                                   const uint32_t* __restrict__ run_f, unsigned long long* stats,
+                                                   unsigned long long* stripes, const uint32_t* err) {
   __shared__ uint32_t s_err;
   if (threadIdx.x == 0) s_err = *err;
   __syncthreads();
   if (s_err) return;
-  const bool use_lds = b.n_rules <= LDS_RULES;
-  stats_block_begin(use_lds, b.n_rules);
-  StatAcc acc{use_lds, o.stats};
+  const bool use_lds = n_rules <= LDS_RULES;
+  stats_block_begin(use_lds, n_rules);
+  StatAcc acc{use_lds, stats};
   LaneStats L;
   L.reset();
   const uint32_t q = blockIdx.x * 256 + threadIdx.x;
-  if (q < b.n) {
+  if (q < n) {
     const uint32_t r = rid[q];
     if (run_flags[r] & RUN_FAST) {
       const uint4 st = run_state[r];
       const uint32_t f = run_f[r];
       const bool F = st.w & 1u;
-      const Elem x = load_elem(b, svals[q], false);
-      uint32_t req_f = 0xFFFFFFFFu;
-      if (P.lc_en && f != 0xFFFFFFFFu) req_f = b.req[svals[f]];
+      const Elem x = load_elem(rec_s[q], svals[q], false);
+      uint32_t req_f = 0xFFFFFFFFu, now_f = 0;
+      if (P.lc_en && f != 0xFFFFFFFFu) {
+        const Rec xf = rec_s[f];
+        req_f = xf.req;
+        now_f = xf.now;
+      }
       const bool masked = F || x.req > req_f;  // local-cache hit
       const uint32_t after = masked ? 0u : st.y + segsum[q];
       const Decision d = decide(after - x.h, after, masked && !x.shadow, x.h, x.thr, P.ratio, x.shadow, P.lc_en);
-      emit(o, L, acc, x, d);
+      emit(res, L, acc, x, d);
       if (!masked) {
         const uint32_t nq = q + 1;
-        const bool last = nq == run_start[r + 1] || b.req[svals[nq]] > req_f;
+        const bool last = nq == run_start[r + 1] || rec_s[nq].req > req_f;
         if (last) {  // the last INCRBY of the run leaves the key's state
           Win R;
           R.ws = x.w;
           R.count = after;
           R.expire = x.now + x.d;
-          R.lc = (req_f != 0xFFFFFFFFu) ? (uint32_t)b.now[req_f] + x.d : st.z;
+          R.lc = (req_f != 0xFFFFFFFFu) ? now_f + x.d : st.z;
           Slot* s = &t.slots[st.x];
           if (st.w & 2u) s->prev = R;
           else s->cur = R;
@@ -1049,18 +1073,18 @@ __global__ __launch_bounds__(256) void k_fast_emit(BatchDev b, OutDev o, TableDe
     }
   }
   wave_flush(L, acc);
-  stats_block_end(use_lds, b.n_rules, stripes);
+  stats_block_end(use_lds, n_rules, stripes);
 }
 
 // ---- k_runs_general: deferred runs (hash-prefix collisions, multi-unit
 // stems). Splits the run into distinct stems, then replays each exactly.
-__global__ __launch_bounds__(256) void k_runs_general(BatchDev b, OutDev o, TableDev t, Params P,
+__global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Params P, const Rec* __restrict__ rec_s,
                                                       const uint32_t* __restrict__ skeys,
                                                       const uint32_t* __restrict__ svals,
-                                                      const uint64_t* __restrict__ hstem,
+                                                      unsigned long long* __restrict__ res,
                                                       const uint32_t* __restrict__ defer, const uint32_t* defer_n,
-                                                      uint8_t* __restrict__ repid, unsigned long long* stripes,
-                                                      uint32_t* err, int restore) {
+                                                      uint8_t* __restrict__ repid, unsigned long long* stats,
+                                                      unsigned long long* stripes, uint32_t* err, int restore) {
   __shared__ uint32_t s_err, s_n;
   if (threadIdx.x == 0) {
     s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1071,7 +1095,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, OutDev o, Tabl
   b.stem_total = b.off[b.n];
   const bool use_lds = !restore && b.n_rules <= LDS_RULES;
   stats_block_begin(use_lds, b.n_rules);
-  StatAcc acc{use_lds, o.stats};
+  StatAcc acc{use_lds, stats};
   LaneStats L;
   L.reset();
   const uint32_t di = blockIdx.x * 256 + threadIdx.x;
@@ -1084,30 +1108,29 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, OutDev o, Tabl
     uint32_t rep[MAX_REPS];
     uint32_t umask[MAX_REPS];
     uint32_t nrep = 1;
-    rep[0] = svals[p];
-    umask[0] = 1u << (b.unit[rep[0]] - 1);
+    rep[0] = p;
+    umask[0] = 1u << (rec_unit(rec_s[p]) - 1);
     for (uint32_t q = p + 1; q < end; q++) {
-      const uint32_t e = svals[q];
-      const uint64_t he = hstem[e];
-      const uint32_t le = b.off[e + 1] - b.off[e];
-      const StemRef se = stem_ref(b, e);
+      const Rec x = rec_s[q];
+      const StemRef se = stem_ref(b, x.off);
       uint32_t k = 0;
       for (; k < nrep; k++) {
-        const uint32_t r = rep[k];
-        if (hstem[r] == he && b.off[r + 1] - b.off[r] == le && stem_words_equal(stem_ref(b, r), se, le)) break;
+        const Rec y = rec_s[rep[k]];
+        if (y.hlo == x.hlo && rec_len(y) == rec_len(x) && stem_words_equal(stem_ref(b, y.off), se, rec_len(x)))
+          break;
       }
       if (k == nrep) {
         if (nrep == MAX_REPS) { atomicOr(err, ERR_COLLISIONS); k = 0; }
-        else { rep[nrep] = e; umask[nrep] = 0; nrep++; }
+        else { rep[nrep] = q; umask[nrep] = 0; nrep++; }
       }
       repid[q] = (uint8_t)k;
-      umask[k] |= 1u << (b.unit[e] - 1);
+      umask[k] |= 1u << (rec_unit(x) - 1);
     }
     for (uint32_t k = 0; k < nrep; k++) {
-      const uint32_t r0 = rep[k];
-      const StemRef stem = stem_ref(b, r0);
-      const uint32_t len = b.off[r0 + 1] - b.off[r0];
-      const uint64_t hs = hstem[r0];
+      const Rec y = rec_s[rep[k]];
+      const StemRef stem = stem_ref(b, y.off);
+      const uint32_t len = rec_len(y);
+      const uint64_t hs = ((uint64_t)key << 32) | y.hlo;
       // ---- resolve the slot(s)
       bool simple = false;
       int64_t s0 = -1;
@@ -1127,7 +1150,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, OutDev o, Tabl
         }
       }
       if (simple) {
-        replay_simple(b, o, t, P, svals, repid, p, end, k, s0, L, acc, err, restore);
+        replay_simple(rec_s, svals, res, t, P, repid, p, end, k, s0, L, acc, err, restore);
       } else {
         GeneralState G;
         G.present = 0;
@@ -1148,8 +1171,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, OutDev o, Tabl
         if (fail) break;
         for (uint32_t q = p; q < end; q++) {
           if (((q == p) ? 0u : repid[q]) != k) continue;
-          const uint32_t e = svals[q];
-          general_step(P, o, L, acc, G, load_elem(b, e, restore), restore, b.flags[e], err);
+          general_step(P, res, L, acc, G, load_elem(rec_s[q], svals[q], restore), restore, err);
         }
         general_apply_pending(G);
         const uint8_t fl = __popc(G.present) >= 2 ? SLOT_EXACT : 0;
@@ -1179,6 +1201,18 @@ __global__ __launch_bounds__(256) void k_stats_fold(unsigned long long* __restri
     stripes[(size_t)k * m + j] = 0;
   }
   if (*err == 0) stats[j] += s;
+}
+
+// Packed results -> the three rl_result arrays (arrival order, coalesced).
+__global__ __launch_bounds__(256) void k_unpack(const unsigned long long* __restrict__ res, uint32_t n, OutDev o,
+                                                const uint32_t* err) {
+  if (*err) return;
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long v = res[i];
+  o.code[i] = (uint8_t)(v >> 56);
+  o.rem[i] = (uint32_t)v;
+  o.reset[i] = (uint32_t)(v >> 32) & 0xFFFFFFu;
 }
 
 // ===========================================================================
@@ -1269,7 +1303,7 @@ void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, cons
                      int restore, hipStream_t st, hipEvent_t* ev) {
   const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
   if (ev) (void)hipEventRecord(ev[0], st);
-  if (g0) k_prepare<<<g0, 256, 0, st>>>(b, s.hstem, s.keys[0], s.vals[0], s.err, s.time_floor);
+  if (g0) k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.keys[0], s.vals[0], s.err, s.time_floor);
   if (ev) (void)hipEventRecord(ev[1], st);
   if (b.n) {
     const uint32_t ntiles = cdiv(b.n, RS_TILE);
@@ -1284,24 +1318,27 @@ void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, cons
   if (ev) (void)hipEventRecord(ev[2], st);
   if (b.n) {
     const uint32_t nt = cdiv(b.n, SEG_TILE), g = cdiv(b.n, 256);
-    k_seg_reduce<<<nt, 256, 0, st>>>(s.keys[0], s.vals[0], b.hits, b.n, s.tile_f, s.tile_s, s.tile_h, s.err);
-    k_seg_tiles<<<1, 1024, 0, st>>>(s.tile_f, s.tile_s, s.tile_h, nt, s.err);
-    k_seg_apply<<<nt, 256, 0, st>>>(s.keys[0], s.vals[0], b.hits, b.n, s.tile_f, s.tile_s, s.tile_h, s.segsum,
-                                    s.rid, s.run_start, s.run_flags, s.num_runs, s.err);
-    k_run_check<<<g, 256, 0, st>>>(b, s.vals[0], s.hstem, s.rid, s.run_start, s.run_flags, s.err);
-    (void)hipMemsetAsync(s.defer_n, 0, sizeof(uint32_t), st);
     const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
-    k_runs<<<g, 256, lds, st>>>(b, o, t, P, s.vals[0], s.hstem, s.run_start, s.run_flags, s.run_state, s.run_f,
-                              s.num_runs, s.defer, s.defer_n, s.stripes, s.err, restore);
-    k_runs_general<<<g, 256, lds, st>>>(b, o, t, P, s.keys[0], s.vals[0], s.hstem, s.defer, s.defer_n, s.repid,
-                                      s.stripes, s.err, restore);
+    k_gather<<<g, 256, 0, st>>>(s.rec, s.vals[0], b.n, s.rec_s, s.err);
+    k_seg_reduce<<<nt, 256, 0, st>>>(s.keys[0], s.rec_s, b.n, s.tile_f, s.tile_s, s.tile_h, s.err);
+    k_seg_tiles<<<1, 1024, 0, st>>>(s.tile_f, s.tile_s, s.tile_h, nt, s.err);
+    k_seg_apply<<<nt, 256, 0, st>>>(s.keys[0], s.rec_s, b.n, s.tile_f, s.tile_s, s.tile_h, s.segsum, s.rid,
+                                    s.run_start, s.run_flags, s.num_runs, s.err);
+    k_run_check<<<g, 256, 0, st>>>(b, s.rec_s, s.rid, s.run_start, s.run_flags, s.err);
+    (void)hipMemsetAsync(s.defer_n, 0, sizeof(uint32_t), st);
+    k_runs<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.keys[0], s.vals[0], s.res, s.run_start, s.run_flags,
+                                s.run_state, s.run_f, s.num_runs, s.defer, s.defer_n, o.stats, s.stripes, s.err,
+                                restore);
+    k_runs_general<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.keys[0], s.vals[0], s.res, s.defer, s.defer_n,
+                                        s.repid, o.stats, s.stripes, s.err, restore);
     if (!restore) {
       if (P.lc_en)
-        k_fast_over<<<g, 256, 0, st>>>(b, s.vals[0], s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.err);
-      k_fast_emit<<<g, 256, lds, st>>>(b, o, t, P, s.vals[0], s.segsum, s.rid, s.run_start, s.run_flags, s.run_state,
-                                     s.run_f, s.stripes, s.err);
+        k_fast_over<<<g, 256, 0, st>>>(b.n, s.rec_s, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.err);
+      k_fast_emit<<<g, 256, lds, st>>>(b.n, b.n_rules, t, P, s.rec_s, s.vals[0], s.res, s.segsum, s.rid,
+                                       s.run_start, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.err);
       if (b.n_rules <= LDS_RULES && b.n_rules)
         k_stats_fold<<<cdiv(b.n_rules * RL_NUM_STATS, 256), 256, 0, st>>>(s.stripes, b.n_rules, o.stats, s.err);
+      k_unpack<<<g, 256, 0, st>>>(s.res, b.n, o, s.err);
     }
   }
   if (ev) (void)hipEventRecord(ev[3], st);
