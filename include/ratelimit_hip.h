@@ -192,9 +192,10 @@ int rl_debug_decide(rl_ctx* ctx, uint32_t n, const uint32_t* before, const uint3
 
 /* Per-stage device timing (HIP events on the batch stream), for benchmarks.
  * rl_profile(ctx, 1) starts accumulating; rl_profile_read fills ms[0..n) with
- * the summed milliseconds of {prepare, sort, runs} and *batches with the number
- * of batches timed (it synchronises), then resets the sums. */
-#define RL_NUM_STAGES 3
+ * the summed milliseconds of the stages {prepare, sort, segment, runs, finish}
+ * and *batches with the number of batches timed (it synchronises), then resets
+ * the sums. "runs" brackets the single k_runs launch (the table kernel). */
+#define RL_NUM_STAGES 5
 int rl_profile(rl_ctx* ctx, int enable);
 int rl_profile_read(rl_ctx* ctx, double* ms, uint32_t n, uint64_t* batches);
 

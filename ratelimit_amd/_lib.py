@@ -9,7 +9,7 @@ import os
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libratelimit_hip.so")
+LIB_PATH = os.environ.get("RL_LIB_PATH") or os.path.join(HERE, "libratelimit_hip.so")  # override: profiling builds
 
 EXPORTS = ["rl_abi_version", "rl_create", "rl_destroy", "rl_last_error", "rl_do_limit", "rl_do_limit_async",
            "rl_synchronize", "rl_sweep", "rl_restore", "rl_table_info_get", "rl_alloc_host", "rl_free_host",

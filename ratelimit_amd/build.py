@@ -26,24 +26,26 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force=False, verbose=False):
-    if not force and not _stale():
+def build(force=False, verbose=False, out=None, defines=()):
+    """Compile and link; ``out``/``defines`` make side builds (e.g. RL_ABL ablations)."""
+    lib = out or LIB
+    if out is None and not force and not _stale():
         return LIB
     objs = []
     for s in SOURCES:
         o = os.path.join(CSRC, os.path.splitext(s)[0] + ".o")
-        cmd = [HIPCC] + FLAGS + ["-c", os.path.join(CSRC, s), "-o", o]
+        cmd = [HIPCC] + FLAGS + ["-D" + d for d in defines] + ["-c", os.path.join(CSRC, s), "-o", o]
         if verbose:
             print(" ".join(cmd))
         subprocess.check_call(cmd)
         objs.append(o)
-    cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB] + objs
+    cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", lib] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

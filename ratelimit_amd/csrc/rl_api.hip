@@ -38,8 +38,8 @@ struct rl_ctx {
   // rl_profile: events of the in-flight timed batch, accumulated stage sums
   bool prof = false;
   bool prof_pending = false;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  double stage_ms[RL_NUM_STAGES] = {0, 0, 0};
+  hipEvent_t ev[RL_NUM_STAGES + 1] = {};
+  double stage_ms[RL_NUM_STAGES] = {};
   uint64_t prof_batches = 0;
 };
 
@@ -53,7 +53,7 @@ int set_err(rl_ctx* c, int code, const std::string& msg);
 void prof_fold(rl_ctx* c) {
   if (!c->prof_pending) return;
   c->prof_pending = false;
-  if (hipEventSynchronize(c->ev[3]) != hipSuccess) return;
+  if (hipEventSynchronize(c->ev[RL_NUM_STAGES]) != hipSuccess) return;
   for (int i = 0; i < RL_NUM_STAGES; i++) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]) == hipSuccess) c->stage_ms[i] += ms;
@@ -143,6 +143,7 @@ TableDev table_view(rl_ctx* c) {
   t.arena_used16 = c->s.counters + 4;
   t.arena_cap16 = c->arena_cap16;
   t.max_probe = (uint32_t)std::min<uint64_t>(c->nslots, 1u << 16);
+  t.shift = 64u - (uint32_t)__builtin_ctzll(c->nslots);
   return t;
 }
 
@@ -221,6 +222,7 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
   ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess;
   ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess;
+  ok = ok && dalloc(&c->s.key, 4ull * n) == hipSuccess && dalloc(&c->s.key_s, 4ull * n) == hipSuccess;
   ok = ok && dalloc(&c->s.rec, n) == hipSuccess && dalloc(&c->s.rec_s, n) == hipSuccess &&
        dalloc(&c->s.res, n) == hipSuccess;
   for (int i = 0; i < 2; i++) {
@@ -273,9 +275,9 @@ void rl_destroy(rl_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->cfg.device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (int i = 0; i < 4; i++)
+  for (int i = 0; i <= RL_NUM_STAGES; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
-  void* bufs[] = {c->slots, c->arena, c->s.rec, c->s.rec_s, c->s.res, c->s.keys[0], c->s.keys[1], c->s.vals[0], c->s.vals[1],
+  void* bufs[] = {c->slots, c->arena, c->s.rec, c->s.rec_s, c->s.res, c->s.key, c->s.key_s, c->s.keys[0], c->s.keys[1], c->s.vals[0], c->s.vals[1],
                   c->s.hist, c->s.hist_tot, c->s.repid, c->s.defer, c->s.defer_n, c->s.stripes, c->s.tile_f, c->s.tile_s, c->s.tile_h, c->s.segsum, c->s.rid,
                   c->s.run_start, c->s.run_flags, c->s.run_state, c->s.run_f, c->s.num_runs, c->s.err, c->s.time_floor, c->s.counters, c->d_stem, c->d_off, c->d_now,
                   c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_rem,
@@ -311,7 +313,7 @@ int rl_profile(rl_ctx* c, int enable) {
   if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (enable && !c->ev[0])
-    for (int i = 0; i < 4; i++) HIPCHK(c, hipEventCreate(&c->ev[i]));
+    for (int i = 0; i <= RL_NUM_STAGES; i++) HIPCHK(c, hipEventCreate(&c->ev[i]));
   prof_fold(c);
   c->prof = enable != 0;
   return RL_OK;

@@ -15,6 +15,7 @@ constexpr uint32_t SEG_ITEMS = 16;
 constexpr uint32_t SEG_TILE = 256 * SEG_ITEMS;
 constexpr uint32_t LONG_RUN = 32;        // runs at least this long take the parallel path
 constexpr uint32_t RUN_SLOW = 1, RUN_FAST = 2;
+constexpr uint32_t KEY_HEAD = 64;         // stem bytes carried inline (zero-padded) per descriptor
 constexpr uint32_t STAT_STRIPES = 64;     // global partial stats tables
 constexpr uint32_t STAT_LDS_RULES = 512;  // rules aggregated in LDS (== LDS_RULES)
 
@@ -65,6 +66,7 @@ struct TableDev {
   unsigned long long* arena_used16;
   uint64_t arena_cap16;
   uint32_t max_probe;
+  uint32_t shift;  // home slot = stem hash >> shift (64 - log2 slots)
 };
 
 struct Params {
@@ -77,6 +79,8 @@ struct Params {
 struct Scratch {
   Rec* rec;                  // [n] arrival order
   Rec* rec_s;                // [n] sorted order
+  uint4* key;                // [n][4] 64-B stem heads, arrival order
+  uint4* key_s;              // [n][4] sorted order
   unsigned long long* res;   // [n] packed result per descriptor (arrival order)
   uint32_t* keys[2];
   uint32_t* vals[2];
@@ -101,8 +105,9 @@ struct Scratch {
 };
 
 // Launch the whole DoLimit pipeline (restore = 1: table seeding records).
-// ev (optional, 4 events): recorded before k_prepare, after it, after the
-// sort and after the run kernels on stream st (per-stage timing, rl_profile).
+// ev (optional, RL_NUM_STAGES + 1 events on stream st): recorded before
+// k_prepare, after it, after the sort, just before and just after k_runs, and
+// at the end (per-stage timing, rl_profile).
 void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
                      int restore, hipStream_t st, hipEvent_t* ev = nullptr);
 void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st);

@@ -21,6 +21,12 @@
 #include "rl_device.h"
 #include "rl_kernels.h"
 
+// Ablation switches for profiling builds only (RL_ABL bits; 0 in the product):
+// 1 = no table probe (slot = tag & mask), 2 = no replay body, 4 = no stats flush.
+#ifndef RL_ABL
+#define RL_ABL 0
+#endif
+
 namespace rl {
 
 // ===========================================================================
@@ -58,7 +64,8 @@ struct DwordReader {
   }
 };
 
-__global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ rec, uint32_t* __restrict__ keys,
+__global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ rec, uint4* __restrict__ key,
+                                                 uint32_t* __restrict__ keys,
                                                  uint32_t* __restrict__ vals, uint32_t* err,
                                                  const int64_t* time_floor) {
   __shared__ uint32_t lds[HASH_LDS_BYTES / 4 + 4];
@@ -117,6 +124,30 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   }
   keys[i] = (uint32_t)(h >> 32);
   vals[i] = i;
+  {  // zero-padded 64-B head of the stem: later compares read it as 4 x uint4
+    uint64_t w[8];
+    if (use_lds) {
+      const DwordReader rd{lds, HASH_LDS_BYTES / 4 + 4};
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) w[k] = rd(s0 - lo + lead + 8 * k);
+    } else {
+      const uint32_t nw = range_ok ? ((total + 3u) >> 2) - (s0 >> 2) : 0u;
+      const DwordReader rd{words + (s0 >> 2), nw};
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) w[k] = rd((s0 & 3u) + 8 * k);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+      const uint32_t c0 = 8 * k;
+      if (c0 >= len) w[k] = 0;
+      else if (c0 + 8 > len) w[k] &= (1ull << ((len - c0) * 8)) - 1;
+    }
+    uint4* dst = key + 4ull * i;
+#pragma unroll
+    for (uint32_t v = 0; v < 4; v++)
+      dst[v] = make_uint4((uint32_t)w[2 * v], (uint32_t)(w[2 * v] >> 32), (uint32_t)w[2 * v + 1],
+                          (uint32_t)(w[2 * v + 1] >> 32));
+  }
   Rec r;
   r.hlo = (uint32_t)h;
   r.off = s0;
@@ -258,11 +289,21 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t* __restrict__
 }
 
 // Records into sorted order.
-__global__ __launch_bounds__(256) void k_gather(const Rec* __restrict__ rec, const uint32_t* __restrict__ svals,
-                                                uint32_t n, Rec* __restrict__ rec_s, const uint32_t* err) {
+__global__ __launch_bounds__(256) void k_gather(const Rec* __restrict__ rec, const uint4* __restrict__ key,
+                                                const uint32_t* __restrict__ svals, uint32_t n, Rec* __restrict__ rec_s,
+                                                uint4* __restrict__ key_s, const uint32_t* err) {
   if (*err) return;
   const uint32_t q = blockIdx.x * 256 + threadIdx.x;
-  if (q < n) rec_s[q] = rec[svals[q]];
+  if (q >= n) return;
+  const uint32_t e = svals[q];
+  rec_s[q] = rec[e];
+  const uint4* src = key + 4ull * e;
+  uint4* dst = key_s + 4ull * q;
+  const uint4 a = src[0], b1 = src[1], c = src[2], d = src[3];
+  dst[0] = a;
+  dst[1] = b1;
+  dst[2] = c;
+  dst[3] = d;
 }
 
 // ===========================================================================
@@ -298,36 +339,86 @@ __device__ inline bool stem_words_equal(const StemRef& x, const StemRef& y, uint
   return diff == 0;
 }
 
+// A stem as the run kernels see it: its zero-padded 64-B head in sorted order
+// (coalesced uint4 loads) and, for stems longer than 64 B only, the rest in the
+// packed stem buffer.
+struct Key {
+  const uint4* k;  // 4 x uint4
+  StemRef st;      // full stem (bytes >= KEY_HEAD read from here)
+  uint32_t len;
+};
+
+__device__ inline Key key_at(const BatchDev& b, const uint4* key_s, const Rec* rec_s, uint32_t q) {
+  const Rec& r = rec_s[q];
+  return Key{key_s + 4ull * q, stem_ref(b, r.off), rec_len(r)};
+}
+
+__device__ inline uint32_t head_diff(const uint4* x, const uint4* y) {
+  uint32_t d = 0;
+#pragma unroll
+  for (uint32_t v = 0; v < 4; v++) {
+    const uint4 a = x[v], c = y[v];
+    d |= (a.x ^ c.x) | (a.y ^ c.y) | (a.z ^ c.z) | (a.w ^ c.w);
+  }
+  return d;
+}
+
+// bytes [64, len) of two stems (words 16.. of their StemRefs)
+__device__ inline uint32_t tail_diff(const StemRef& x, const StemRef& y, uint32_t len) {
+  uint32_t d = 0;
+  const uint32_t nw = len >> 2;
+  for (uint32_t k = KEY_HEAD / 4; k < nw; k++) d |= x.word(k) ^ y.word(k);
+  if (len & 3) d |= (x.word(nw) ^ y.word(nw)) & tail_mask(len);
+  return d;
+}
+
+// Same stem bytes (callers have compared hash and length).
+__device__ inline bool key_equal(const Key& x, const Key& y) {
+  uint32_t d = head_diff(x.k, y.k);
+  if (x.len > KEY_HEAD) d |= tail_diff(x.st, y.st, x.len);
+  return d == 0;
+}
+
 // ===========================================================================
 // HBM table probing.
 // ===========================================================================
-__device__ inline bool slot_key_equal(const Slot* s, const StemRef& st, uint32_t len, const uint8_t* arena) {
-  if (s->key_len != len) return false;
-  const uint32_t* sk = reinterpret_cast<const uint32_t*>(s->key);
-  const uint32_t il = len < INLINE_KEY ? len : INLINE_KEY;
-  uint32_t diff = 0;
-  const uint32_t nw = il >> 2;
-#pragma unroll 4
-  for (uint32_t k = 0; k < nw; k++) diff |= sk[k] ^ st.word(k);
-  if (il & 3) diff |= (sk[nw] ^ st.word(nw)) & tail_mask(il);
-  if (len > INLINE_KEY) {
-    const uint32_t* ek = reinterpret_cast<const uint32_t*>(arena + (size_t)s->ext_off * 16);
-    const uint32_t rest = len - INLINE_KEY, rw = rest >> 2;
-    for (uint32_t k = 0; k < rw; k++) diff |= ek[k] ^ st.word(INLINE_KEY / 4 + k);
-    if (rest & 3) diff |= (ek[rw] ^ st.word(INLINE_KEY / 4 + rw)) & tail_mask(rest);
+// Slot key bytes 0..63 were written from a zero-padded key head, so they
+// compare as whole uint4s; bytes 64..79 inline and the arena cover the rest.
+__device__ inline bool slot_key_equal(const Slot* s, const Key& key, const uint8_t* arena) {
+  if (s->key_len != key.len) return false;
+  const uint4* sk4 = reinterpret_cast<const uint4*>(s->key);
+  uint32_t diff = head_diff(sk4, key.k);
+  const uint32_t len = key.len;
+  if (len > KEY_HEAD) {
+    const uint32_t* sk = reinterpret_cast<const uint32_t*>(s->key);
+    const uint32_t il = len < INLINE_KEY ? len : INLINE_KEY;
+    const uint32_t nw = il >> 2;
+    for (uint32_t k = KEY_HEAD / 4; k < nw; k++) diff |= sk[k] ^ key.st.word(k);
+    if (il & 3) diff |= (sk[nw] ^ key.st.word(nw)) & tail_mask(il);
+    if (len > INLINE_KEY) {
+      const uint32_t* ek = reinterpret_cast<const uint32_t*>(arena + (size_t)s->ext_off * 16);
+      const uint32_t rest = len - INLINE_KEY, rw = rest >> 2;
+      for (uint32_t k = 0; k < rw; k++) diff |= ek[k] ^ key.st.word(INLINE_KEY / 4 + k);
+      if (rest & 3) diff |= (ek[rw] ^ key.st.word(INLINE_KEY / 4 + rw)) & tail_mask(rest);
+    }
   }
   return diff == 0;
 }
 
-__device__ inline void slot_init(const TableDev& t, Slot* s, const StemRef& st, uint32_t len, uint32_t unit,
-                                 uint32_t* err) {
+__device__ inline void slot_init(const TableDev& t, Slot* s, const Key& key, uint32_t unit, uint32_t* err) {
+  const uint32_t len = key.len;
   s->key_len = (uint16_t)len;
   s->unit = (uint8_t)unit;
   s->flags = 0;
   s->ext_off = 0;
-  uint32_t* sk = reinterpret_cast<uint32_t*>(s->key);
-  const uint32_t il = len < INLINE_KEY ? len : INLINE_KEY;
-  for (uint32_t k = 0; k < (il + 3) / 4; k++) sk[k] = st.word(k);
+  uint4* sk4 = reinterpret_cast<uint4*>(s->key);
+#pragma unroll
+  for (uint32_t v = 0; v < 4; v++) sk4[v] = key.k[v];
+  if (len > KEY_HEAD) {
+    uint32_t* sk = reinterpret_cast<uint32_t*>(s->key);
+    const uint32_t il = len < INLINE_KEY ? len : INLINE_KEY;
+    for (uint32_t k = KEY_HEAD / 4; k < (il + 3) / 4; k++) sk[k] = key.st.word(k);
+  }
   if (len > INLINE_KEY) {
     const uint32_t n16 = (len - INLINE_KEY + 15) / 16;
     unsigned long long off = atomicAdd(t.arena_used16, (unsigned long long)n16);
@@ -336,7 +427,7 @@ __device__ inline void slot_init(const TableDev& t, Slot* s, const StemRef& st, 
     } else {
       s->ext_off = (uint32_t)off;
       uint32_t* ek = reinterpret_cast<uint32_t*>(t.arena + off * 16);
-      for (uint32_t k = 0; k < (len - INLINE_KEY + 3) / 4; k++) ek[k] = st.word(INLINE_KEY / 4 + k);
+      for (uint32_t k = 0; k < (len - INLINE_KEY + 3) / 4; k++) ek[k] = key.st.word(INLINE_KEY / 4 + k);
     }
   }
   s->cur = Win{WS_INVALID, 0, 0, 0};
@@ -345,19 +436,21 @@ __device__ inline void slot_init(const TableDev& t, Slot* s, const StemRef& st, 
 
 // Find (and optionally insert) the slot of (stem, unit). Returns -1 when absent
 // and insert == false, or on a full table (error bit set). Linear probing over
-// 128-B slots; a tag match is confirmed by the full stem (collision-exact).
-// Inserts claim the slot with a 64-bit CAS on its tag; only one lane ever
-// handles a given (stem, unit) per batch (runs are grouped by stem).
-__device__ int64_t find_slot(const TableDev& t, uint64_t tag, const StemRef& stem, uint32_t len, uint32_t unit,
+// 128-B slots from the home slot = top bits of the stem hash, i.e. of the sort
+// key: consecutive runs probe increasing slots (page and TLB locality). A tag
+// match is confirmed by the full stem (collision-exact). Inserts claim the slot
+// with a 64-bit CAS on its tag; only one lane ever handles a given (stem, unit)
+// per batch (runs are grouped by stem).
+__device__ int64_t find_slot(const TableDev& t, uint64_t hstem, uint64_t tag, const Key& key, uint32_t unit,
                              bool insert, bool* inserted, uint32_t* err) {
-  uint64_t i = tag & t.mask;
+  uint64_t i = hstem >> t.shift;
   int64_t tomb = -1;
   *inserted = false;
   for (uint32_t p = 0; p < t.max_probe; p++, i = (i + 1) & t.mask) {
     Slot* s = &t.slots[i];
     const uint64_t st = __hip_atomic_load(&s->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (st == tag) {
-      if (slot_key_equal(s, stem, len, t.arena)) return (int64_t)i;
+      if (slot_key_equal(s, key, t.arena)) return (int64_t)i;
       continue;
     }
     if (st == TAG_TOMB) {
@@ -371,7 +464,7 @@ __device__ int64_t find_slot(const TableDev& t, uint64_t tag, const StemRef& ste
       Slot* ts = &t.slots[tomb];
       if (atomicCAS((unsigned long long*)&ts->tag, (unsigned long long)TAG_TOMB, (unsigned long long)tag) ==
           TAG_TOMB) {
-        slot_init(t, ts, stem, len, unit, err);
+        slot_init(t, ts, key, unit, err);
         *inserted = true;
         return tomb;
       }
@@ -379,7 +472,7 @@ __device__ int64_t find_slot(const TableDev& t, uint64_t tag, const StemRef& ste
     const unsigned long long prev =
         atomicCAS((unsigned long long*)&s->tag, (unsigned long long)TAG_EMPTY, (unsigned long long)tag);
     if (prev == TAG_EMPTY) {
-      slot_init(t, s, stem, len, unit, err);
+      slot_init(t, s, key, unit, err);
       *inserted = true;
       return (int64_t)i;
     }
@@ -568,7 +661,7 @@ __device__ __attribute__((always_inline)) inline void simple_step(const Params& 
   }
   const int which = window_pick(S.cur, S.prev, x.w, 0, true);
   if (which < 0) {
-    atomicOr(err, ERR_HISTORY);
+    if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
     return;
   }
   Win R = which ? S.prev : S.cur;  // values, not pointers: the state stays in VGPRs
@@ -653,7 +746,7 @@ __device__ inline void general_step(const Params& P, unsigned long long* res, La
     const uint32_t nv = restore ? x.h : v + x.h;
     const uint32_t ex = x.now + x.d;
     if (window_pick(G.cur[ui], G.prev[ui], x.w, lcw, false) < 0) {
-      atomicOr(err, ERR_HISTORY);
+      if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
       return;
     }
     for (uint32_t k = 0; k < 4; k++) {  // Redis key stem‖w in this store: every alias record
@@ -874,6 +967,7 @@ __global__ __launch_bounds__(256) void k_seg_apply(const uint32_t* __restrict__ 
 // Long runs only: every element must share the head's stem, unit and window
 // for the parallel path; otherwise the run is replayed serially.
 __global__ __launch_bounds__(256) void k_run_check(BatchDev b, const Rec* __restrict__ rec_s,
+                                                   const uint4* __restrict__ key_s,
                                                    const uint32_t* __restrict__ rid,
                                                    const uint32_t* __restrict__ run_start,
                                                    uint32_t* __restrict__ run_flags, const uint32_t* err) {
@@ -888,7 +982,7 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, const Rec* __rest
   bool same = x.hlo == x0.hlo && (x.lu & 0xFFFFFFu) == (x0.lu & 0xFFFFFFu);  // hash, length, unit
   if (same) {
     const uint32_t d = div_of(rec_unit(x));
-    same = x0.now / d == x.now / d && stem_words_equal(stem_ref(b, x.off), stem_ref(b, x0.off), rec_len(x0));
+    same = x0.now / d == x.now / d && key_equal(key_at(b, key_s, rec_s, q), key_at(b, key_s, rec_s, p));
   }
   if (!same) atomicOr(&run_flags[r], RUN_SLOW);
 }
@@ -898,6 +992,7 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, const Rec* __rest
 // are set up for the parallel path (k_fast_*); anything else is deferred to
 // k_runs_general.
 __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, const Rec* __restrict__ rec_s,
+                                              const uint4* __restrict__ key_s,
                                               const uint32_t* __restrict__ skeys,
                                               const uint32_t* __restrict__ svals, unsigned long long* __restrict__ res,
                                               const uint32_t* __restrict__ run_start,
@@ -927,20 +1022,20 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
     const Rec x0 = rec_s[p];
     const uint64_t h0 = ((uint64_t)skeys[p] << 32) | x0.hlo;
     const uint32_t u0 = rec_unit(x0);
-    const uint32_t len0 = rec_len(x0);
-    const StemRef st0 = stem_ref(b, x0.off);
+    const Key k0 = key_at(b, key_s, rec_s, p);
     bool ok = true;
     if (!long_run) {  // long uniform runs were checked in parallel (k_run_check)
       for (uint32_t q = p + 1; q < end && ok; q++) {
         const Rec x = rec_s[q];
-        ok = x.hlo == x0.hlo && (x.lu & 0xFFFFFFu) == (x0.lu & 0xFFFFFFu) &&
-             stem_words_equal(stem_ref(b, x.off), st0, len0);
+        ok = x.hlo == x0.hlo && (x.lu & 0xFFFFFFu) == (x0.lu & 0xFFFFFFu) && key_equal(key_at(b, key_s, rec_s, q), k0);
       }
     }
     int64_t s0 = -1;
-    if (ok) {
+    if (RL_ABL & 1) {
+      s0 = (int64_t)(h0 >> t.shift);
+    } else if (ok) {
       bool ins;
-      s0 = find_slot(t, slot_tag(h0, u0), st0, len0, u0, true, &ins, err);
+      s0 = find_slot(t, h0, slot_tag(h0, u0), k0, u0, true, &ins, err);
       if (s0 < 0) {
         ok = false;
       } else if (t.slots[s0].flags & SLOT_EXACT) {
@@ -948,7 +1043,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
       } else if (ins) {  // new (stem, unit): the stem must not exist under another unit
         for (uint32_t u = 1; u <= 4; u++) {
           bool dummy;
-          const int64_t so = u == u0 ? -1 : find_slot(t, slot_tag(h0, u), st0, len0, u, false, &dummy, err);
+          const int64_t so = u == u0 ? -1 : find_slot(t, h0, slot_tag(h0, u), k0, u, false, &dummy, err);
           if (so >= 0) {  // multi-unit stem from now on: flag both before deferring
             t.slots[so].flags |= SLOT_EXACT;
             ok = false;
@@ -964,7 +1059,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
       const Elem e0 = load_elem(x0, svals[p], false);
       const int which = window_pick(cur, prev, e0.w, 0, true);
       if (which < 0) {
-        atomicOr(err, ERR_HISTORY);
+        if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
       } else {
         const Win R = which ? prev : cur;
         // A record of window w was written inside w: its EXPIRE and local-cache
@@ -978,13 +1073,22 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
         run_flags[r] |= RUN_FAST;
       }
     } else if (ok) {
-      replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, L, acc, err, restore);
+      if (RL_ABL & 2) {
+        Slot* sl = &t.slots[s0];
+        Win c = sl->cur;
+        c.count += end - p;
+        sl->cur = c;
+      } else {
+        replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, L, acc, err, restore);
+      }
     } else if (!(s0 < 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_TABLE_FULL))) {
       defer[atomicAdd(defer_n, 1u)] = p;
     }
   }
-  if (!restore) wave_flush(L, acc);
-  stats_block_end(use_lds, b.n_rules, stripes);
+  if (!(RL_ABL & 4)) {
+    if (!restore) wave_flush(L, acc);
+    stats_block_end(use_lds, b.n_rules, stripes);
+  }
 }
 
 // ---- parallel path for long uniform runs (one stem, one unit, one window).
@@ -1079,6 +1183,7 @@ __global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules,
 // ---- k_runs_general: deferred runs (hash-prefix collisions, multi-unit
 // stems). Splits the run into distinct stems, then replays each exactly.
 __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Params P, const Rec* __restrict__ rec_s,
+                                                      const uint4* __restrict__ key_s,
                                                       const uint32_t* __restrict__ skeys,
                                                       const uint32_t* __restrict__ svals,
                                                       unsigned long long* __restrict__ res,
@@ -1112,12 +1217,11 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
     umask[0] = 1u << (rec_unit(rec_s[p]) - 1);
     for (uint32_t q = p + 1; q < end; q++) {
       const Rec x = rec_s[q];
-      const StemRef se = stem_ref(b, x.off);
+      const Key kx = key_at(b, key_s, rec_s, q);
       uint32_t k = 0;
       for (; k < nrep; k++) {
         const Rec y = rec_s[rep[k]];
-        if (y.hlo == x.hlo && rec_len(y) == rec_len(x) && stem_words_equal(stem_ref(b, y.off), se, rec_len(x)))
-          break;
+        if (y.hlo == x.hlo && rec_len(y) == rec_len(x) && key_equal(key_at(b, key_s, rec_s, rep[k]), kx)) break;
       }
       if (k == nrep) {
         if (nrep == MAX_REPS) { atomicOr(err, ERR_COLLISIONS); k = 0; }
@@ -1128,8 +1232,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
     }
     for (uint32_t k = 0; k < nrep; k++) {
       const Rec y = rec_s[rep[k]];
-      const StemRef stem = stem_ref(b, y.off);
-      const uint32_t len = rec_len(y);
+      const Key stem = key_at(b, key_s, rec_s, rep[k]);
       const uint64_t hs = ((uint64_t)key << 32) | y.hlo;
       // ---- resolve the slot(s)
       bool simple = false;
@@ -1137,14 +1240,14 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
       if (__popc(umask[k]) == 1) {
         const uint32_t u0 = __ffs(umask[k]);
         bool ins;
-        s0 = find_slot(t, slot_tag(hs, u0), stem, len, u0, true, &ins, err);
+        s0 = find_slot(t, hs, slot_tag(hs, u0), stem, u0, true, &ins, err);
         if (s0 < 0) break;
         if (!(t.slots[s0].flags & SLOT_EXACT)) {
           simple = true;
           if (ins) {  // new (stem, unit): the stem must not exist under another unit
             for (uint32_t u = 1; u <= 4 && simple; u++) {
               bool dummy;
-              if (u != u0 && find_slot(t, slot_tag(hs, u), stem, len, u, false, &dummy, err) >= 0) simple = false;
+              if (u != u0 && find_slot(t, hs, slot_tag(hs, u), stem, u, false, &dummy, err) >= 0) simple = false;
             }
           }
         }
@@ -1159,7 +1262,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
         bool fail = false;
         for (uint32_t u = 1; u <= 4; u++) {
           bool ins;
-          G.sidx[u - 1] = find_slot(t, slot_tag(hs, u), stem, len, u, (umask[k] >> (u - 1)) & 1, &ins, err);
+          G.sidx[u - 1] = find_slot(t, hs, slot_tag(hs, u), stem, u, (umask[k] >> (u - 1)) & 1, &ins, err);
           if (G.sidx[u - 1] >= 0) {
             G.present |= 1u << (u - 1);
             G.cur[u - 1] = t.slots[G.sidx[u - 1]].cur;
@@ -1303,7 +1406,7 @@ void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, cons
                      int restore, hipStream_t st, hipEvent_t* ev) {
   const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
   if (ev) (void)hipEventRecord(ev[0], st);
-  if (g0) k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.keys[0], s.vals[0], s.err, s.time_floor);
+  if (g0) k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.key, s.keys[0], s.vals[0], s.err, s.time_floor);
   if (ev) (void)hipEventRecord(ev[1], st);
   if (b.n) {
     const uint32_t ntiles = cdiv(b.n, RS_TILE);
@@ -1319,17 +1422,19 @@ void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, cons
   if (b.n) {
     const uint32_t nt = cdiv(b.n, SEG_TILE), g = cdiv(b.n, 256);
     const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
-    k_gather<<<g, 256, 0, st>>>(s.rec, s.vals[0], b.n, s.rec_s, s.err);
+    k_gather<<<g, 256, 0, st>>>(s.rec, s.key, s.vals[0], b.n, s.rec_s, s.key_s, s.err);
     k_seg_reduce<<<nt, 256, 0, st>>>(s.keys[0], s.rec_s, b.n, s.tile_f, s.tile_s, s.tile_h, s.err);
     k_seg_tiles<<<1, 1024, 0, st>>>(s.tile_f, s.tile_s, s.tile_h, nt, s.err);
     k_seg_apply<<<nt, 256, 0, st>>>(s.keys[0], s.rec_s, b.n, s.tile_f, s.tile_s, s.tile_h, s.segsum, s.rid,
                                     s.run_start, s.run_flags, s.num_runs, s.err);
-    k_run_check<<<g, 256, 0, st>>>(b, s.rec_s, s.rid, s.run_start, s.run_flags, s.err);
+    k_run_check<<<g, 256, 0, st>>>(b, s.rec_s, s.key_s, s.rid, s.run_start, s.run_flags, s.err);
     (void)hipMemsetAsync(s.defer_n, 0, sizeof(uint32_t), st);
-    k_runs<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.keys[0], s.vals[0], s.res, s.run_start, s.run_flags,
+    if (ev) (void)hipEventRecord(ev[3], st);
+    k_runs<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.key_s, s.keys[0], s.vals[0], s.res, s.run_start, s.run_flags,
                                 s.run_state, s.run_f, s.num_runs, s.defer, s.defer_n, o.stats, s.stripes, s.err,
                                 restore);
-    k_runs_general<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.keys[0], s.vals[0], s.res, s.defer, s.defer_n,
+    if (ev) (void)hipEventRecord(ev[4], st);
+    k_runs_general<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.key_s, s.keys[0], s.vals[0], s.res, s.defer, s.defer_n,
                                         s.repid, o.stats, s.stripes, s.err, restore);
     if (!restore) {
       if (P.lc_en)
@@ -1340,8 +1445,11 @@ void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, cons
         k_stats_fold<<<cdiv(b.n_rules * RL_NUM_STATS, 256), 256, 0, st>>>(s.stripes, b.n_rules, o.stats, s.err);
       k_unpack<<<g, 256, 0, st>>>(s.res, b.n, o, s.err);
     }
+  } else if (ev) {
+    (void)hipEventRecord(ev[3], st);
+    (void)hipEventRecord(ev[4], st);
   }
-  if (ev) (void)hipEventRecord(ev[3], st);
+  if (ev) (void)hipEventRecord(ev[5], st);
 }
 
 void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st) {

@@ -26,6 +26,9 @@ from ._lib import RedisError, check, lib
 from .packing import PackedBatch, RuleInterner, pack_calls
 from .types import OK, DescriptorStatus, Limit  # noqa: F401  (re-exported data model)
 
+# rl_profile stages (include/ratelimit_hip.h RL_NUM_STAGES)
+STAGES = ("prepare", "sort", "segment", "runs", "finish")
+
 __all__ = ["GpuRateLimitCache", "RedisError", "TimeSource"]
 
 
@@ -110,11 +113,11 @@ class Backend:
         check(self.ctx, lib().rl_profile(self.ctx, 1 if enable else 0))
 
     def profile_read(self):
-        """-> ({prepare, sort, runs} summed ms, batches timed); resets the sums."""
-        ms = (C.c_double * 3)()
+        """-> ({prepare, sort, segment, runs, finish} summed ms, batches timed); resets the sums."""
+        ms = (C.c_double * len(STAGES))()
         nb = C.c_uint64(0)
-        check(self.ctx, lib().rl_profile_read(self.ctx, ms, 3, C.byref(nb)))
-        return dict(zip(("prepare", "sort", "runs"), list(ms))), nb.value
+        check(self.ctx, lib().rl_profile_read(self.ctx, ms, len(STAGES), C.byref(nb)))
+        return dict(zip(STAGES, list(ms))), nb.value
 
     def synchronize(self):
         check(self.ctx, lib().rl_synchronize(self.ctx))
