@@ -237,6 +237,7 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
     const size_t nt = (n + SEG_TILE - 1) / SEG_TILE + 1;
     ok = ok && dalloc(&c->s.tile_f, nt) == hipSuccess && dalloc(&c->s.tile_s, nt) == hipSuccess &&
          dalloc(&c->s.tile_h, nt) == hipSuccess;
+    ok = ok && dalloc(&c->s.hits_s, n) == hipSuccess;
     ok = ok && dalloc(&c->s.segsum, n) == hipSuccess && dalloc(&c->s.rid, n) == hipSuccess &&
          dalloc(&c->s.run_start, (size_t)n + 1) == hipSuccess && dalloc(&c->s.run_flags, n) == hipSuccess &&
          dalloc(&c->s.run_state, n) == hipSuccess && dalloc(&c->s.run_f, n) == hipSuccess &&
@@ -278,7 +279,7 @@ void rl_destroy(rl_ctx* c) {
   for (int i = 0; i <= RL_NUM_STAGES; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
   void* bufs[] = {c->slots, c->arena, c->s.rec, c->s.rec_s, c->s.res, c->s.key, c->s.key_s, c->s.keys[0], c->s.keys[1], c->s.vals[0], c->s.vals[1],
-                  c->s.hist, c->s.hist_tot, c->s.repid, c->s.defer, c->s.defer_n, c->s.stripes, c->s.tile_f, c->s.tile_s, c->s.tile_h, c->s.segsum, c->s.rid,
+                  c->s.hist, c->s.hist_tot, c->s.repid, c->s.defer, c->s.defer_n, c->s.stripes, c->s.tile_f, c->s.tile_s, c->s.tile_h, c->s.hits_s, c->s.segsum, c->s.rid,
                   c->s.run_start, c->s.run_flags, c->s.run_state, c->s.run_f, c->s.num_runs, c->s.err, c->s.time_floor, c->s.counters, c->d_stem, c->d_off, c->d_now,
                   c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_rem,
                   c->d_reset, c->d_stats};

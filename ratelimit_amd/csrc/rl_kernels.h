@@ -92,6 +92,7 @@ struct Scratch {
   unsigned long long* stripes;    // STAT_STRIPES x STAT_LDS_RULES x RL_NUM_STATS
   // run segmentation (sorted order)
   uint32_t *tile_f, *tile_s, *tile_h;  // per SEG_TILE tile
+  uint32_t* hits_s;                    // [n] raw hits, sorted order
   uint32_t* segsum;                    // [n] inclusive in-run sum of hits
   uint32_t* rid;                       // [n] run id
   uint32_t* run_start;                 // [n+1]

@@ -291,12 +291,15 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t* __restrict__
 // Records into sorted order.
 __global__ __launch_bounds__(256) void k_gather(const Rec* __restrict__ rec, const uint4* __restrict__ key,
                                                 const uint32_t* __restrict__ svals, uint32_t n, Rec* __restrict__ rec_s,
-                                                uint4* __restrict__ key_s, const uint32_t* err) {
+                                                uint4* __restrict__ key_s, uint32_t* __restrict__ hits_s,
+                                                const uint32_t* err) {
   if (*err) return;
   const uint32_t q = blockIdx.x * 256 + threadIdx.x;
   if (q >= n) return;
   const uint32_t e = svals[q];
-  rec_s[q] = rec[e];
+  const Rec r = rec[e];
+  rec_s[q] = r;
+  hits_s[q] = r.hits;
   const uint4* src = key + 4ull * e;
   uint4* dst = key_s + 4ull * q;
   const uint4 a = src[0], b1 = src[1], c = src[2], d = src[3];
@@ -806,65 +809,96 @@ __device__ __attribute__((always_inline)) inline void replay_simple(const Rec* r
 // the run id and the inclusive in-run sum of max(1, hits) (u32, wrapping like
 // the sequential INCRBYs), and per run its start. Segmented-sum operator on
 // (head, sum): (f1,s1)+(f2,s2) = (f1|f2, f2 ? s2 : s1+s2).
+// Layout: each wave owns a strip of SEG_TILE/4 consecutive positions and walks
+// it in SEG_ITEMS chunks of 64 (one position per lane), so every load and
+// store is a coalesced 256-B wave access; scans are wave shuffles.
 // ===========================================================================
 struct SegPair {
   uint32_t f, s;
 };
 __device__ inline SegPair seg_op(SegPair a, SegPair b) { return SegPair{a.f | b.f, b.f ? b.s : a.s + b.s}; }
 
-// inclusive block scan of (pair, head count) over 256 threads
-__device__ inline void seg_block_scan(SegPair& v, uint32_t& hc, SegPair* sp, uint32_t* sh) {
-  const uint32_t tid = threadIdx.x;
-  sp[tid] = v;
-  sh[tid] = hc;
+constexpr uint32_t SEG_STRIP = SEG_TILE / 4;  // positions per wave
+static_assert(SEG_STRIP == SEG_ITEMS * 64, "4 waves x SEG_ITEMS chunks of 64");
+
+struct SegChunk {
+  uint64_t heads;  // ballot of run heads in the chunk
+  uint32_t h;      // this lane's max(1, hits) (0 past n)
+};
+
+__device__ inline SegChunk seg_chunk(const uint32_t* skeys, const uint32_t* hits_s, uint32_t n, uint32_t q) {
+  const bool valid = q < n;
+  const bool head = valid && (q == 0 || skeys[q - 1] != skeys[q]);
+  const uint32_t hv = valid ? hits_s[q] : 0u;
+  return SegChunk{(uint64_t)__ballot(head), valid ? (hv > 1 ? hv : 1u) : 0u};
+}
+
+// Inclusive segmented scan of a chunk (lane order). Plain prefix sum P, then
+// subtract the prefix before the lane's last head.
+__device__ inline SegPair seg_chunk_scan(const SegChunk& c, uint32_t lane) {
+  uint32_t P = c.h;
+#pragma unroll
+  for (uint32_t off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(P, off, 64);
+    if (lane >= off) P += y;
+  }
+  const uint64_t le = c.heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+  const uint32_t lh = le ? 63u - (uint32_t)__clzll((long long)le) : 0u;
+  const uint32_t Plh = __shfl(P, lh, 64), hlh = __shfl(c.h, lh, 64);
+  return le ? SegPair{1u, P - (Plh - hlh)} : SegPair{0u, P};
+}
+
+// Block-level combine of the 4 wave aggregates: returns this wave's exclusive
+// prefix within the tile (and the tile aggregate through *tot for lane 0 of
+// wave 0 callers).
+__device__ inline void seg_waves(SegPair agg, uint32_t hc, SegPair* sp, uint32_t* sh, SegPair& excl, uint32_t& hexcl,
+                                 SegPair& tot, uint32_t& htot) {
+  const uint32_t w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sp[w] = agg;
+    sh[w] = hc;
+  }
   __syncthreads();
-  for (uint32_t off = 1; off < 256; off <<= 1) {
-    SegPair a = v;
-    uint32_t c = hc;
-    if (tid >= off) {
-      a = seg_op(sp[tid - off], v);
-      c = sh[tid - off] + hc;
+  excl = SegPair{0, 0};
+  hexcl = 0;
+  tot = SegPair{0, 0};
+  htot = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    if (k == w) {
+      excl = tot;
+      hexcl = htot;
     }
-    __syncthreads();
-    v = a;
-    hc = c;
-    sp[tid] = v;
-    sh[tid] = hc;
-    __syncthreads();
+    tot = seg_op(tot, sp[k]);
+    htot += sh[k];
   }
 }
 
-__device__ inline void seg_load(const uint32_t* skeys, const Rec* rec_s, uint32_t n, uint32_t q, bool& valid,
-                                bool& head, uint32_t& h) {
-  valid = q < n;
-  head = valid && (q == 0 || skeys[q - 1] != skeys[q]);
-  const uint32_t hv = valid ? rec_s[q].hits : 0u;
-  h = valid ? (hv > 1 ? hv : 1u) : 0u;
-}
-
-__global__ __launch_bounds__(256) void k_seg_reduce(const uint32_t* __restrict__ skeys, const Rec* __restrict__ rec_s,
-                                                    uint32_t n, uint32_t* __restrict__ tile_f,
-                                                    uint32_t* __restrict__ tile_s, uint32_t* __restrict__ tile_h,
-                                                    const uint32_t* err) {
-  __shared__ SegPair sp[256];
-  __shared__ uint32_t sh[256];
+__global__ __launch_bounds__(256) void k_seg_reduce(const uint32_t* __restrict__ skeys,
+                                                    const uint32_t* __restrict__ hits_s, uint32_t n,
+                                                    uint32_t* __restrict__ tile_f, uint32_t* __restrict__ tile_s,
+                                                    uint32_t* __restrict__ tile_h, const uint32_t* err) {
+  __shared__ SegPair sp[4];
+  __shared__ uint32_t sh[4];
   if (*err) return;
-  const uint32_t base = blockIdx.x * SEG_TILE + threadIdx.x * SEG_ITEMS;
-  SegPair v{0, 0};
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t base = blockIdx.x * SEG_TILE + (threadIdx.x >> 6) * SEG_STRIP + lane;
+  SegPair agg{0, 0};
   uint32_t hc = 0;
-  for (uint32_t i = 0; i < SEG_ITEMS; i++) {
-    bool valid, head;
-    uint32_t h;
-    seg_load(skeys, rec_s, n, base + i, valid, head, h);
-    if (!valid) break;
-    v = seg_op(v, SegPair{head ? 1u : 0u, h});
-    hc += head;
+#pragma unroll 4
+  for (uint32_t c = 0; c < SEG_ITEMS; c++) {
+    const SegChunk ch = seg_chunk(skeys, hits_s, n, base + 64 * c);
+    const SegPair v = seg_chunk_scan(ch, lane);
+    agg = seg_op(agg, SegPair{__shfl(v.f, 63, 64), __shfl(v.s, 63, 64)});
+    hc += (uint32_t)__popcll(ch.heads);
   }
-  seg_block_scan(v, hc, sp, sh);
-  if (threadIdx.x == 255) {
-    tile_f[blockIdx.x] = v.f;
-    tile_s[blockIdx.x] = v.s;
-    tile_h[blockIdx.x] = hc;
+  SegPair excl, tot;
+  uint32_t hexcl, htot;
+  seg_waves(agg, hc, sp, sh, excl, hexcl, tot, htot);
+  if (threadIdx.x == 0) {
+    tile_f[blockIdx.x] = tot.f;
+    tile_s[blockIdx.x] = tot.s;
+    tile_h[blockIdx.x] = htot;
   }
 }
 
@@ -913,54 +947,61 @@ __global__ __launch_bounds__(1024) void k_seg_tiles(uint32_t* __restrict__ tile_
   }
 }
 
-__global__ __launch_bounds__(256) void k_seg_apply(const uint32_t* __restrict__ skeys, const Rec* __restrict__ rec_s,
-                                                   uint32_t n, const uint32_t* __restrict__ tile_f,
+__global__ __launch_bounds__(256) void k_seg_apply(const uint32_t* __restrict__ skeys,
+                                                   const uint32_t* __restrict__ hits_s, uint32_t n,
+                                                   const uint32_t* __restrict__ tile_f,
                                                    const uint32_t* __restrict__ tile_s,
                                                    const uint32_t* __restrict__ tile_h, uint32_t* __restrict__ segsum,
                                                    uint32_t* __restrict__ rid, uint32_t* __restrict__ run_start,
                                                    uint32_t* __restrict__ run_flags, uint32_t* num_runs,
                                                    const uint32_t* err) {
-  __shared__ SegPair sp[256];
-  __shared__ uint32_t sh[256];
+  __shared__ SegPair sp[4];
+  __shared__ uint32_t sh[4];
   if (*err) return;
-  const uint32_t base = blockIdx.x * SEG_TILE + threadIdx.x * SEG_ITEMS;
-  SegPair v{0, 0};
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t base = blockIdx.x * SEG_TILE + (threadIdx.x >> 6) * SEG_STRIP + lane;
+  // pass 1 (chunks kept in registers): this wave's aggregate
+  SegChunk ch[SEG_ITEMS];
+  SegPair agg{0, 0};
   uint32_t hc = 0;
-  for (uint32_t i = 0; i < SEG_ITEMS; i++) {
-    bool valid, head;
-    uint32_t h;
-    seg_load(skeys, rec_s, n, base + i, valid, head, h);
-    if (!valid) break;
-    v = seg_op(v, SegPair{head ? 1u : 0u, h});
-    hc += head;
+#pragma unroll
+  for (uint32_t c = 0; c < SEG_ITEMS; c++) {
+    ch[c] = seg_chunk(skeys, hits_s, n, base + 64 * c);
+    uint32_t t = ch[c].h;  // chunk total, segmented: sum after the last head
+    const uint32_t lh = ch[c].heads ? 63u - (uint32_t)__clzll((long long)ch[c].heads) : 0u;
+    if (ch[c].heads && lane < lh) t = 0;
+#pragma unroll
+    for (uint32_t off = 32; off; off >>= 1) t += __shfl_xor(t, off, 64);
+    agg = seg_op(agg, SegPair{ch[c].heads ? 1u : 0u, t});
+    hc += (uint32_t)__popcll(ch[c].heads);
   }
-  seg_block_scan(v, hc, sp, sh);
-  // exclusive prefix of this thread = tile carry + block exclusive
-  SegPair run = SegPair{tile_f[blockIdx.x], tile_s[blockIdx.x]};
-  uint32_t hrun = tile_h[blockIdx.x];
-  if (threadIdx.x) {
-    run = seg_op(run, sp[threadIdx.x - 1]);
-    hrun += sh[threadIdx.x - 1];
-  }
-  for (uint32_t i = 0; i < SEG_ITEMS; i++) {
-    const uint32_t q = base + i;
-    bool valid, head;
-    uint32_t h;
-    seg_load(skeys, rec_s, n, q, valid, head, h);
-    if (!valid) break;
-    run = seg_op(run, SegPair{head ? 1u : 0u, h});
-    hrun += head;
-    const uint32_t r = hrun - 1;
-    segsum[q] = run.s;
-    rid[q] = r;
-    if (head) {
-      run_start[r] = q;
-      run_flags[r] = 0;
+  SegPair excl, tot;
+  uint32_t hexcl, htot;
+  seg_waves(agg, hc, sp, sh, excl, hexcl, tot, htot);
+  // pass 2: exclusive prefix of the wave = tile carry + earlier waves
+  SegPair run = seg_op(SegPair{tile_f[blockIdx.x], tile_s[blockIdx.x]}, excl);
+  uint32_t hrun = tile_h[blockIdx.x] + hexcl;
+#pragma unroll
+  for (uint32_t c = 0; c < SEG_ITEMS; c++) {
+    const uint32_t q = base + 64 * c;
+    const SegPair v = seg_chunk_scan(ch[c], lane);
+    const SegPair in = seg_op(run, v);
+    const uint64_t heads = ch[c].heads;
+    const uint32_t r = hrun + (uint32_t)__popcll(heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1))) - 1;
+    if (q < n) {
+      segsum[q] = in.s;
+      rid[q] = r;
+      if ((heads >> lane) & 1) {
+        run_start[r] = q;
+        run_flags[r] = 0;
+      }
+      if (q == n - 1) {
+        run_start[r + 1] = n;
+        *num_runs = r + 1;
+      }
     }
-    if (q == n - 1) {
-      run_start[r + 1] = n;
-      *num_runs = r + 1;
-    }
+    run = seg_op(run, SegPair{__shfl(v.f, 63, 64), __shfl(v.s, 63, 64)});
+    hrun += (uint32_t)__popcll(heads);
   }
 }
 
@@ -1422,10 +1463,10 @@ void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, cons
   if (b.n) {
     const uint32_t nt = cdiv(b.n, SEG_TILE), g = cdiv(b.n, 256);
     const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
-    k_gather<<<g, 256, 0, st>>>(s.rec, s.key, s.vals[0], b.n, s.rec_s, s.key_s, s.err);
-    k_seg_reduce<<<nt, 256, 0, st>>>(s.keys[0], s.rec_s, b.n, s.tile_f, s.tile_s, s.tile_h, s.err);
+    k_gather<<<g, 256, 0, st>>>(s.rec, s.key, s.vals[0], b.n, s.rec_s, s.key_s, s.hits_s, s.err);
+    k_seg_reduce<<<nt, 256, 0, st>>>(s.keys[0], s.hits_s, b.n, s.tile_f, s.tile_s, s.tile_h, s.err);
     k_seg_tiles<<<1, 1024, 0, st>>>(s.tile_f, s.tile_s, s.tile_h, nt, s.err);
-    k_seg_apply<<<nt, 256, 0, st>>>(s.keys[0], s.rec_s, b.n, s.tile_f, s.tile_s, s.tile_h, s.segsum, s.rid,
+    k_seg_apply<<<nt, 256, 0, st>>>(s.keys[0], s.hits_s, b.n, s.tile_f, s.tile_s, s.tile_h, s.segsum, s.rid,
                                     s.run_start, s.run_flags, s.num_runs, s.err);
     k_run_check<<<g, 256, 0, st>>>(b, s.rec_s, s.key_s, s.rid, s.run_start, s.run_flags, s.err);
     (void)hipMemsetAsync(s.defer_n, 0, sizeof(uint32_t), st);

@@ -1,0 +1,14 @@
+#!/bin/bash
+# HBM traffic per kernel from rocprofv3 PMC counters: one pass per counter set
+# (FETCH_SIZE and WRITE_SIZE do not fit one pass), then a per-kernel summary.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+cfg=${CFG:-c1}
+for ctr in FETCH_SIZE WRITE_SIZE; do
+  mkdir -p gpurun_out/pmc_${cfg}_$ctr
+  timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc_${cfg}_$ctr -o run -- \
+    python -u bench.py --config $cfg --steps 10 --warmup 2 --latency-steps 2 --no-cpu-baseline \
+    > gpurun_out/pmc_${cfg}_$ctr.log 2>&1 || { tail -20 gpurun_out/pmc_${cfg}_$ctr.log; exit 1; }
+done
+python scripts/pmc_summary.py $cfg
