@@ -190,6 +190,41 @@ int rl_debug_decide(rl_ctx* ctx, uint32_t n, const uint32_t* before, const uint3
                     uint8_t* code, uint32_t* remaining, uint32_t* reset_s,
                     uint64_t* stat_deltas /* n * RL_NUM_STATS */, uint8_t* lc_set);
 
+/* ---- Multi-GPU routing (hash-sharded table; one rl_ctx per GPU) -----------
+ * the reference shards keys across Redis instances
+ * (src/redis/driver_impl.go:66-142 cluster/sentinel pools); here each GPU owns
+ * the keys whose stem hash maps to it, and every batch is exchanged once.
+ * Every pointer is device memory of ctx's GPU and work is enqueued on `stream`
+ * (a hipStream_t, NULL = ctx's stream). The exchange (two all_to_all calls over
+ * RCCL) is the caller's; ratelimit_amd/sharded.py is the reference driver.
+ *
+ * rl_route_pack (source side, synchronous): stable-partitions the batch `in`
+ * (device arrays, as rl_do_limit_async) by owner shard and writes, in owner
+ * order, one RL_WIRE_BYTES record per descriptor to send_rec and its stem bytes
+ * to send_stem (capacity: the batch's stem bytes). perm[j] = batch index of
+ * record j. counts_host[2*d], [2*d+1] = records / stem bytes for owner d. Request
+ * indices must be < 2^24; the global request label is src_rank << 24 | req_idx,
+ * so chunks concatenated in source-rank order are in global arrival order.
+ *
+ * rl_route_do_limit (owner side, asynchronous): DoLimit over the n records
+ * received from all sources (concatenated in source-rank order) with their stems
+ * (recv_stem, 4-byte aligned, recv_stem_bytes long; src_stem_base = host array
+ * of each source's chunk offset in recv_stem). ret[j] = remaining |
+ * reset_s << 32 | code << 56 for record j; stats = this owner's deltas
+ * (n_rules * RL_NUM_STATS, overwritten). Errors surface at rl_synchronize.
+ *
+ * rl_route_scatter (source side, asynchronous): results returned in record
+ * order (ret, n = the batch size) -> out (device SoA) in arrival order. */
+#define RL_WIRE_BYTES 32u
+#define RL_MAX_SHARDS 256u
+int rl_route_pack(rl_ctx* ctx, const rl_batch* in, uint32_t n_shards, uint32_t src_rank, void* send_rec,
+                  uint8_t* send_stem, uint32_t* perm, uint64_t* counts_host, void* stream);
+int rl_route_do_limit(rl_ctx* ctx, uint32_t n, const void* recv_rec, const uint8_t* recv_stem,
+                      uint64_t recv_stem_bytes, const uint64_t* src_stem_base, uint32_t n_shards,
+                      uint32_t n_rules, uint64_t* ret, uint64_t* stats, void* stream);
+int rl_route_scatter(rl_ctx* ctx, uint32_t n, const uint32_t* perm, const uint64_t* ret, rl_result* out,
+                     void* stream);
+
 /* Per-stage device timing (HIP events on the batch stream), for benchmarks.
  * rl_profile(ctx, 1) starts accumulating; rl_profile_read fills ms[0..n) with
  * the summed milliseconds of the stages {prepare, sort, segment, runs, finish}

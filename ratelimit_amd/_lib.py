@@ -13,7 +13,8 @@ LIB_PATH = os.environ.get("RL_LIB_PATH") or os.path.join(HERE, "libratelimit_hip
 
 EXPORTS = ["rl_abi_version", "rl_create", "rl_destroy", "rl_last_error", "rl_do_limit", "rl_do_limit_async",
            "rl_synchronize", "rl_sweep", "rl_restore", "rl_table_info_get", "rl_alloc_host", "rl_free_host",
-           "rl_debug_keys", "rl_debug_decide", "rl_profile", "rl_profile_read"]
+           "rl_debug_keys", "rl_debug_decide", "rl_profile", "rl_profile_read", "rl_route_pack",
+           "rl_route_do_limit", "rl_route_scatter"]
 
 _lib = None
 
@@ -48,6 +49,12 @@ def lib():
     L.rl_debug_decide.argtypes = [C.c_void_p, C.c_uint32] + [C.c_void_p] * 13
     L.rl_profile.argtypes = [C.c_void_p, C.c_int]
     L.rl_profile_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_uint32, C.POINTER(C.c_uint64)]
+    L.rl_route_pack.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
+                                C.c_void_p, C.c_void_p, C.c_void_p]
+    L.rl_route_do_limit.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                    C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.rl_route_scatter.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(abi.RlResult),
+                                   C.c_void_p]
     if L.rl_abi_version() != 1:
         raise RuntimeError("libratelimit_hip.so ABI mismatch")
     _lib = L

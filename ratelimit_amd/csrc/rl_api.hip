@@ -33,6 +33,7 @@ struct rl_ctx {
   unsigned long long* d_stats = nullptr;
   uint32_t* h_err = nullptr;  // pinned
   unsigned long long* h_counters = nullptr;
+  unsigned long long* h_route = nullptr;  // pinned route counts
   std::string last_error;
   uint64_t batches = 0, decisions = 0;
   // rl_profile: events of the in-flight timed batch, accumulated stage sums
@@ -99,11 +100,15 @@ int map_err(rl_ctx* c, uint32_t e) {
 }
 
 // Read (and clear) the sticky device error word; synchronises the stream.
-int collect(rl_ctx* c) {
-  HIPCHK(c, hipMemcpyAsync(c->h_err, c->s.err, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+int collect(rl_ctx* c, hipStream_t st = nullptr) {
+  if (!st) st = c->stream;
+  HIPCHK(c, hipMemcpyAsync(c->h_err, c->s.err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
   const uint32_t e = *c->h_err;
-  if (e) HIPCHK(c, hipMemsetAsync(c->s.err, 0, sizeof(uint32_t), c->stream));
+  if (e) {
+    HIPCHK(c, hipMemsetAsync(c->s.err, 0, sizeof(uint32_t), st));
+    HIPCHK(c, hipStreamSynchronize(st));
+  }
   return map_err(c, e);
 }
 
@@ -123,6 +128,7 @@ BatchDev dev_view(const rl_batch* in, uint32_t stem_cap) {
   b.n_rules = in->n_rules;
   b.stem_cap = stem_cap;
   b.stem_total = stem_cap;  // refined on the device from off[n]
+  b.now_desc = 0;
   b.stem = in->stem_bytes;
   b.off = in->stem_off;
   b.now = in->now;
@@ -248,6 +254,10 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && dalloc(&c->s.err, 1) == hipSuccess;
   ok = ok && dalloc(&c->s.time_floor, 1) == hipSuccess;
   ok = ok && dalloc(&c->s.counters, 8) == hipSuccess;
+  ok = ok && dalloc(&c->s.route_start, RL_MAX_SHARDS + 1) == hipSuccess &&
+       dalloc(&c->s.route_base, RL_MAX_SHARDS) == hipSuccess &&
+       dalloc(&c->s.route_counts, 2 * RL_MAX_SHARDS) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_route, 2 * RL_MAX_SHARDS * sizeof(unsigned long long)) == hipSuccess;
   ok = ok && dalloc(&c->d_stem, (size_t)cfg.max_stem_bytes + 64) == hipSuccess;
   ok = ok && dalloc(&c->d_off, (size_t)n + 1) == hipSuccess;
   ok = ok && dalloc(&c->d_now, cfg.max_requests) == hipSuccess;
@@ -282,11 +292,12 @@ void rl_destroy(rl_ctx* c) {
                   c->s.hist, c->s.hist_tot, c->s.repid, c->s.defer, c->s.defer_n, c->s.stripes, c->s.tile_f, c->s.tile_s, c->s.tile_h, c->s.hits_s, c->s.segsum, c->s.rid,
                   c->s.run_start, c->s.run_flags, c->s.run_state, c->s.run_f, c->s.num_runs, c->s.err, c->s.time_floor, c->s.counters, c->d_stem, c->d_off, c->d_now,
                   c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_rem,
-                  c->d_reset, c->d_stats};
+                  c->d_reset, c->d_stats, c->s.route_start, c->s.route_base, c->s.route_counts};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
+  if (c->h_route) (void)hipHostFree(c->h_route);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -307,6 +318,78 @@ int rl_do_limit_async(rl_ctx* c, const rl_batch* in, rl_result* out, void* strea
   HIPCHK(c, hipGetLastError());
   c->batches++;
   c->decisions += in->n;
+  return RL_OK;
+}
+
+int rl_route_pack(rl_ctx* c, const rl_batch* in, uint32_t n_shards, uint32_t src_rank, void* send_rec,
+                  uint8_t* send_stem, uint32_t* perm, uint64_t* counts_host, void* stream) {
+  if (!c || !in || !counts_host || (in->n && (!send_rec || !send_stem || !perm)))
+    return set_err(c, RL_E_INVALID, "gpu: null argument");
+  if (n_shards < 1 || n_shards > RL_MAX_SHARDS || src_rank >= n_shards)
+    return set_err(c, RL_E_INVALID, "gpu: n_shards must be 1..256 and src_rank < n_shards");
+  int rc = check_sizes(c, in, 0);
+  if (rc) return rc;
+  if ((uintptr_t)in->stem_bytes & 3u) return set_err(c, RL_E_INVALID, "gpu: stem_bytes must be 4-byte aligned");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  BatchDev b = dev_view(in, c->cfg.max_stem_bytes);
+  launch_route_pack(b, n_shards, src_rank, (Wire*)send_rec, send_stem, perm, c->s.route_counts, c->s, st);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->h_route, c->s.route_counts, 2ull * n_shards * 8, hipMemcpyDeviceToHost, st));
+  rc = collect(c, st);
+  for (uint32_t i = 0; i < 2 * n_shards; i++) counts_host[i] = rc ? 0 : c->h_route[i];
+  return rc;
+}
+
+int rl_route_do_limit(rl_ctx* c, uint32_t n, const void* recv_rec, const uint8_t* recv_stem, uint64_t recv_stem_bytes,
+                      const uint64_t* src_stem_base, uint32_t n_shards, uint32_t n_rules, uint64_t* ret,
+                      uint64_t* stats, void* stream) {
+  if (!c || !src_stem_base || (n && (!recv_rec || !recv_stem || !ret)) || (n_rules && !stats))
+    return set_err(c, RL_E_INVALID, "gpu: null argument");
+  if (n_shards < 1 || n_shards > RL_MAX_SHARDS) return set_err(c, RL_E_INVALID, "gpu: n_shards must be 1..256");
+  if (n > c->cfg.max_batch || n > c->cfg.max_requests || n_rules > c->cfg.max_rules ||
+      recv_stem_bytes > c->cfg.max_stem_bytes)
+    return set_err(c, RL_E_CAPACITY, "gpu: routed batch exceeds max_batch/max_requests/max_rules/max_stem_bytes");
+  if ((uintptr_t)recv_stem & 3u) return set_err(c, RL_E_INVALID, "gpu: recv_stem must be 4-byte aligned");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  HIPCHK(c, hipMemcpyAsync(c->s.route_base, src_stem_base, (size_t)n_shards * 8, hipMemcpyHostToDevice, st));
+  BatchOut bo{c->d_off, c->d_now, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule};
+  launch_route_unpack((const Wire*)recv_rec, n, c->s.route_base, n_shards, recv_stem_bytes, bo, c->s.err, st);
+  if (!n) HIPCHK(c, hipMemsetAsync(c->d_off, 0, sizeof(uint32_t), st));
+  if (n_rules) HIPCHK(c, hipMemsetAsync(stats, 0, (size_t)n_rules * RL_NUM_STATS * 8, st));
+  BatchDev b;
+  b.n = n;
+  b.n_req = n;
+  b.n_rules = n_rules;
+  b.stem_cap = (uint32_t)recv_stem_bytes;
+  b.stem_total = (uint32_t)recv_stem_bytes;
+  b.now_desc = 1;
+  b.stem = recv_stem;
+  b.off = c->d_off;
+  b.now = c->d_now;
+  b.req = c->d_req;
+  b.unit = c->d_unit;
+  b.flags = c->d_flags;
+  b.limit = c->d_limit;
+  b.hits = c->d_hits;
+  b.rule = c->d_rule;
+  OutDev o{c->d_code, c->d_rem, c->d_reset, (unsigned long long*)stats};
+  launch_do_limit(b, o, table_view(c), params(c), c->s, 0, st, prof_events(c));
+  if (n) HIPCHK(c, hipMemcpyAsync(ret, c->s.res, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
+  HIPCHK(c, hipGetLastError());
+  c->batches++;
+  c->decisions += n;
+  return RL_OK;
+}
+
+int rl_route_scatter(rl_ctx* c, uint32_t n, const uint32_t* perm, const uint64_t* ret, rl_result* out, void* stream) {
+  if (!c || !out || (n && (!perm || !ret))) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats};
+  launch_route_scatter(perm, (const unsigned long long*)ret, n, o, st);
+  HIPCHK(c, hipGetLastError());
   return RL_OK;
 }
 

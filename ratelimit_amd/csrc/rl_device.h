@@ -75,6 +75,35 @@ struct StemHasher {
   }
 };
 
+// 64-bit hash of the stem bytes [a, a+len) read through rd (8 bytes per call).
+template <typename Rd>
+__device__ inline uint64_t hash_stem(Rd rd, uint32_t a, uint32_t len) {
+  StemHasher hs(len);
+  uint32_t i = 0;
+  for (; i + 8 <= len; i += 8) hs.word(rd(a + i));
+  if (i < len) {
+    uint32_t rem = len - i;
+    uint64_t w = rd(a + i) & ((rem == 8) ? ~0ull : ((1ull << (rem * 8)) - 1));
+    hs.word(w);
+  }
+  return hs.finish();
+}
+
+// 8 bytes starting at byte address a of a dword array (little-endian); dwords
+// at index >= nw read as 0 (no access past the stem buffer).
+struct DwordReader {
+  const uint32_t* p;
+  uint32_t nw;
+  __device__ inline uint32_t at(uint32_t i) const { return i < nw ? p[i] : 0u; }
+  __device__ inline uint64_t operator()(uint32_t a) const {
+    uint32_t idx = a >> 2, sh = (a & 3) * 8;
+    uint64_t lo = at(idx), mid = at(idx + 1);
+    uint64_t x = lo | (mid << 32);
+    if (sh) x = (x >> sh) | (uint64_t(at(idx + 2)) << (64 - sh));
+    return x;
+  }
+};
+
 __host__ __device__ inline uint64_t slot_tag(uint64_t hstem, uint32_t unit) {
   uint64_t t = fmix64(hstem + uint64_t(unit) * 0x9E3779B97F4A7C15ull);
   return t < 2 ? t + 2 : t;

@@ -22,6 +22,7 @@ constexpr uint32_t STAT_LDS_RULES = 512;  // rules aggregated in LDS (== LDS_RUL
 struct BatchDev {
   uint32_t n, n_req, n_rules, stem_cap;
   uint32_t stem_total;  // bytes of packed stems (off[n]); reads stay below it
+  uint32_t now_desc;    // 1: now[] per descriptor and req[] an opaque non-decreasing label (routed batches)
   const uint8_t* stem;  // 4-byte aligned
   const uint32_t* off;
   const int64_t* now;
@@ -51,6 +52,32 @@ static_assert(sizeof(Rec) == 32, "Rec is two dwordx4");
 __host__ __device__ inline uint32_t rec_len(const Rec& r) { return r.lu & 0xFFFFu; }
 __host__ __device__ inline uint32_t rec_unit(const Rec& r) { return (r.lu >> 16) & 0xFFu; }
 __host__ __device__ inline uint32_t rec_flags(const Rec& r) { return r.lu >> 24; }
+
+// Multi-GPU routing wire record (rl_route.hip): one per routed descriptor.
+constexpr uint32_t ROUTE_REQ_BITS = 24;  // label = source rank << 24 | request index
+constexpr uint32_t ROUTE_MAX_REQ = 1u << ROUTE_REQ_BITS;
+struct __attribute__((aligned(8))) Wire {
+  uint32_t label;  // global request label (non-decreasing in global arrival order)
+  uint32_t off;    // stem byte offset inside the owner's chunk of this source
+  uint32_t lu;     // stem length (16) | unit << 16 | flags << 24
+  uint32_t limit;
+  uint32_t hits;
+  uint32_t rule;
+  int64_t now;
+};
+static_assert(sizeof(Wire) == RL_WIRE_BYTES, "wire record size is part of the ABI");
+
+// Batch arrays written by the owner-side unpack.
+struct BatchOut {
+  uint32_t* off;
+  int64_t* now;
+  uint32_t* req;
+  uint8_t* unit;
+  uint8_t* flags;
+  uint32_t* limit;
+  uint32_t* hits;
+  uint32_t* rule;
+};
 
 struct OutDev {
   uint8_t* code;
@@ -103,6 +130,10 @@ struct Scratch {
   uint32_t* err;
   int64_t* time_floor;  // requests earlier than the last sweep are rejected
   unsigned long long* counters;  // [0..3] sweep / info outputs
+  // multi-GPU routing
+  uint32_t* route_start;             // [RL_MAX_SHARDS + 1] stem chunk starts per owner
+  unsigned long long* route_base;    // [RL_MAX_SHARDS] received stem chunk starts per source
+  unsigned long long* route_counts;  // [2 * RL_MAX_SHARDS] records / stem bytes per owner
 };
 
 // Launch the whole DoLimit pipeline (restore = 1: table seeding records).
@@ -111,6 +142,18 @@ struct Scratch {
 // at the end (per-stage timing, rl_profile).
 void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
                      int restore, hipStream_t st, hipEvent_t* ev = nullptr);
+// One stable 8-bit counting pass on key bits [0, 8) (s.hist / s.hist_tot hold
+// the per-digit counts afterwards).
+void launch_partition(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, uint32_t n,
+                      const Scratch& s, hipStream_t st);
+// s.segsum[q] = inclusive sum of max(1, w) over the run of equal skeys holding q.
+void launch_run_sums(const uint32_t* skeys, const uint32_t* w, uint32_t n, const Scratch& s, hipStream_t st);
+void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
+                       uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st);
+void launch_route_unpack(const Wire* rec, uint32_t n, const unsigned long long* base, uint32_t n_shards,
+                         uint64_t stem_bytes, const BatchOut& bo, uint32_t* err, hipStream_t st);
+void launch_route_scatter(const uint32_t* perm, const unsigned long long* ret, uint32_t n, const OutDev& o,
+                          hipStream_t st);
 void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st);
 void launch_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out, hipStream_t st);
 void launch_debug_keys(const BatchDev& b, uint8_t* out, uint32_t* klen, hipStream_t st);

@@ -36,34 +36,6 @@ namespace rl {
 // ===========================================================================
 constexpr uint32_t HASH_LDS_BYTES = 16384;
 
-template <typename Rd>
-__device__ inline uint64_t hash_stem(Rd rd, uint32_t a, uint32_t len) {
-  StemHasher hs(len);
-  uint32_t i = 0;
-  for (; i + 8 <= len; i += 8) hs.word(rd(a + i));
-  if (i < len) {
-    uint32_t rem = len - i;
-    uint64_t w = rd(a + i) & ((rem == 8) ? ~0ull : ((1ull << (rem * 8)) - 1));
-    hs.word(w);
-  }
-  return hs.finish();
-}
-
-// 8 bytes starting at byte address a of a dword array (little-endian); dwords
-// at index >= nw read as 0 (no access past the stem buffer).
-struct DwordReader {
-  const uint32_t* p;
-  uint32_t nw;
-  __device__ inline uint32_t at(uint32_t i) const { return i < nw ? p[i] : 0u; }
-  __device__ inline uint64_t operator()(uint32_t a) const {
-    uint32_t idx = a >> 2, sh = (a & 3) * 8;
-    uint64_t lo = at(idx), mid = at(idx + 1);
-    uint64_t x = lo | (mid << 32);
-    if (sh) x = (x >> sh) | (uint64_t(at(idx + 2)) << (64 - sh));
-    return x;
-  }
-};
-
 __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ rec, uint4* __restrict__ key,
                                                  uint32_t* __restrict__ keys,
                                                  uint32_t* __restrict__ vals, uint32_t* err,
@@ -74,7 +46,7 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   uint32_t bad = 0;
 
   // ---- per-request clock checks: now in [0, NOW_MAX] and not before the last sweep
-  if (i < b.n_req) {
+  if (i < (b.now_desc ? b.n : b.n_req)) {
     const int64_t t = b.now[i];
     if (t < 0 || t > (int64_t)NOW_MAX || t < *time_floor) bad |= ERR_TIME;
   }
@@ -86,7 +58,7 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
     const uint32_t s1 = b.off[i + 1];
     u = b.unit[i];
     q = b.req[i];
-    if (u < 1 || u > 4 || b.rule[i] >= b.n_rules || q >= b.n_req || (i && b.req[i - 1] > q) || s1 < s0 ||
+    if (u < 1 || u > 4 || b.rule[i] >= b.n_rules || (!b.now_desc && q >= b.n_req) || (i && b.req[i - 1] > q) || s1 < s0 ||
         s1 > b.stem_cap || s1 - s0 == 0 || s1 - s0 > 65535)
       bad |= ERR_INVALID;
     else
@@ -154,7 +126,7 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   r.lu = len | (u << 16) | ((uint32_t)b.flags[i] << 24);
   r.rule = b.rule[i];
   r.req = q;
-  r.now = (q < b.n_req) ? (uint32_t)b.now[q] : 0u;
+  r.now = b.now_desc ? (uint32_t)b.now[i] : (q < b.n_req) ? (uint32_t)b.now[q] : 0u;
   r.hits = b.hits[i];
   r.limit = b.limit[i];
   rec[i] = r;
@@ -1491,6 +1463,24 @@ void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, cons
     (void)hipEventRecord(ev[4], st);
   }
   if (ev) (void)hipEventRecord(ev[5], st);
+}
+
+void launch_partition(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, uint32_t n,
+                      const Scratch& s, hipStream_t st) {
+  if (!n) return;
+  const uint32_t ntiles = cdiv(n, RS_TILE);
+  k_rs_hist<<<ntiles, 256, 0, st>>>(kin, n, 0, ntiles, s.hist, s.err);
+  k_rs_rowscan<<<256, 256, 0, st>>>(s.hist, ntiles, s.hist_tot, s.err);
+  k_rs_scatter<<<ntiles, 256, 0, st>>>(kin, vin, kout, vout, n, 0, ntiles, s.hist, s.hist_tot, s.err);
+}
+
+void launch_run_sums(const uint32_t* skeys, const uint32_t* w, uint32_t n, const Scratch& s, hipStream_t st) {
+  if (!n) return;
+  const uint32_t nt = cdiv(n, SEG_TILE);
+  k_seg_reduce<<<nt, 256, 0, st>>>(skeys, w, n, s.tile_f, s.tile_s, s.tile_h, s.err);
+  k_seg_tiles<<<1, 1024, 0, st>>>(s.tile_f, s.tile_s, s.tile_h, nt, s.err);
+  k_seg_apply<<<nt, 256, 0, st>>>(skeys, w, n, s.tile_f, s.tile_s, s.tile_h, s.segsum, s.rid, s.run_start,
+                                  s.run_flags, s.num_runs, s.err);
 }
 
 void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st) {

@@ -106,3 +106,20 @@ def pack_calls(calls, prefix: str, interner: RuleInterner, n_rules: Optional[int
     arrays = arrays_from_lists(stems, now_list, req_idx, unit, flags, limit, hits, rule_id)
     nr = len(interner.keys) if n_rules is None else n_rules
     return PackedBatch(arrays, len(stems), len(now_list), nr, origin)
+
+
+def slice_requests(arrays: Dict[str, np.ndarray], n: int, n_requests: int, r0: int, r1: int):
+    """Requests [r0, r1) of a packed batch as a packed batch of its own (request
+    indices and stem offsets rebased): how a node batcher hands each GPU rank a
+    contiguous slice of the arrival order (ratelimit_amd/sharded.py)."""
+    req = arrays["req_idx"][:n]
+    d0, d1 = (int(x) for x in np.searchsorted(req, [r0, r1], side="left"))
+    off = arrays["stem_off"]
+    s0, s1 = int(off[d0]), int(off[d1])
+    out = {"stem_bytes": np.ascontiguousarray(arrays["stem_bytes"][s0:s1]) if s1 > s0 else np.zeros(4, np.uint8),
+           "stem_off": (off[d0:d1 + 1].astype(np.int64) - s0).astype(np.uint32),
+           "now": np.ascontiguousarray(arrays["now"][r0:r1]) if r1 > r0 else np.zeros(1, np.int64),
+           "req_idx": (req[d0:d1].astype(np.int64) - r0).astype(np.uint32)}
+    for k in ("unit", "flags", "limit", "hits", "rule_id"):
+        out[k] = np.ascontiguousarray(arrays[k][d0:d1])
+    return out, d1 - d0, r1 - r0

@@ -1,0 +1,89 @@
+"""CPU stand-in for the device halves of the multi-GPU exchange (TEST ONLY).
+
+ratelimit_amd.sharded.ShardedRateLimitCache drives an `ops` object; on a GPU
+box that is DeviceRouteOps (rl_route_* kernels). Here the same protocol runs
+over gloo with numpy packing and the C oracle as each owner's table, so the
+host-side exchange (split sizes, ordering across ranks, inverse routing,
+stats all_reduce, error agreement) is tested without a GPU. The wire layout is
+the C ABI's (RL_WIRE_BYTES records: label, off, lu, limit, hits, rule, now).
+"""
+import zlib
+
+import numpy as np
+import torch
+
+from oracle.c_oracle import COracle
+from ratelimit_amd import abi
+from ratelimit_amd._lib import RedisError
+
+WIRE = np.dtype([("label", "<u4"), ("off", "<u4"), ("lu", "<u4"), ("limit", "<u4"), ("hits", "<u4"),
+                 ("rule", "<u4"), ("now", "<i8")])
+assert WIRE.itemsize == 32
+
+
+def owner_of(stem: bytes, world: int) -> int:
+    return (zlib.crc32(stem) * world) >> 32
+
+
+class CpuRouteOps:
+    def __init__(self, ratio=0.8, local_cache=False, per_second=False):
+        self.oracle = COracle(ratio, local_cache, per_second)
+
+    def pack(self, dev_in, n, n_requests, n_rules, world, rank, send_rec, send_stem, perm):
+        a = {k: v.numpy().view(abi.BATCH_DTYPES[k]) for k, v in dev_in.items()}
+        if n and (a["unit"][:n].min() < 1 or a["unit"][:n].max() > 4):
+            raise RedisError("gpu: malformed batch [RL_E_INVALID]")
+        off = a["stem_off"].astype(np.int64)
+        stems = [a["stem_bytes"][off[i]:off[i + 1]].tobytes() for i in range(n)]
+        dest = np.array([owner_of(s, world) for s in stems], np.int64)
+        order = np.argsort(dest, kind="stable")
+        rec = np.zeros(n, WIRE)
+        counts = np.zeros((world, 2), np.uint64)
+        chunk_off = np.zeros(world, np.int64)
+        blob = bytearray()
+        for j, e in enumerate(order):
+            d = dest[e]
+            s = stems[e]
+            q = int(a["req_idx"][e])
+            rec[j] = ((rank << 24) | q, chunk_off[d], len(s) | (int(a["unit"][e]) << 16) | (int(a["flags"][e]) << 24),
+                      a["limit"][e], a["hits"][e], a["rule_id"][e], a["now"][q])
+            chunk_off[d] += len(s)
+            counts[d, 0] += 1
+            counts[d, 1] += len(s)
+            blob += s
+        send_rec[:n * 32].copy_(torch.from_numpy(rec.view(np.uint8).copy()))
+        if blob:
+            send_stem[:len(blob)].copy_(torch.from_numpy(np.frombuffer(bytes(blob), np.uint8).copy()))
+        perm[:n].copy_(torch.from_numpy(order.astype(np.int32)))
+        return counts
+
+    def owner(self, n, recv_rec, recv_stem, stem_bytes, src_base, world, n_rules, ret, stats):
+        rec = recv_rec[:n * 32].numpy().view(WIRE)
+        blob = recv_stem[:stem_bytes].numpy()
+        src = rec["label"] >> 24
+        starts = np.asarray(src_base, np.int64)[src] + rec["off"]
+        lens = rec["lu"] & 0xFFFF
+        assert n == 0 or np.all(starts[1:] == starts[:-1] + lens[:-1]), "stems must abut"
+        labels, first, req = np.unique(rec["label"], return_index=True, return_inverse=True)
+        arrays = {"stem_bytes": blob.copy() if stem_bytes else np.zeros(4, np.uint8),
+                  "stem_off": np.concatenate([starts, [starts[-1] + lens[-1]]]).astype(np.uint32) if n else
+                  np.zeros(1, np.uint32),
+                  "now": rec["now"][first].copy() if n else np.zeros(1, np.int64),
+                  "req_idx": req.astype(np.uint32), "unit": ((rec["lu"] >> 16) & 0xFF).astype(np.uint8),
+                  "flags": (rec["lu"] >> 24).astype(np.uint8), "limit": rec["limit"].copy(),
+                  "hits": rec["hits"].copy(), "rule_id": rec["rule"].copy()}
+        out = self.oracle.do_limit(arrays, n, labels.size, n_rules)
+        packed = (out["limit_remaining"].astype(np.uint64) | (out["reset_s"].astype(np.uint64) << np.uint64(32)) |
+                  (out["code"].astype(np.uint64) << np.uint64(56)))
+        ret[:n].copy_(torch.from_numpy(packed.view(np.int64)))
+        stats[:n_rules * 6].copy_(torch.from_numpy(out["stats"].view(np.int64)))
+
+    def scatter(self, n, perm, back, dev_out):
+        p = perm[:n].numpy().astype(np.int64)
+        v = back[:n].numpy().view(np.uint64)
+        dev_out["code"][p] = torch.from_numpy((v >> np.uint64(56)).astype(np.uint8))
+        dev_out["limit_remaining"][p] = torch.from_numpy((v & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32))
+        dev_out["reset_s"][p] = torch.from_numpy(((v >> np.uint64(32)) & np.uint64(0xFFFFFF)).astype(np.int32))
+
+    def synchronize(self):
+        pass

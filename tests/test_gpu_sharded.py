@@ -1,0 +1,105 @@
+"""Multi-GPU routing through the C ABI (rl_route_*) on the GPU box.
+
+World size 1 (RCCL) and 2 (two ranks sharing cuda:0, gloo exchange staged
+through host memory; the 8-GPU RCCL run is the driver's) run
+ShardedRateLimitCache with DeviceRouteOps: hash -> owner partition, wire
+packing, owner-side unpack + the normal HIP pipeline, inverse routing. Results
+of all ranks' slices in rank order, and node-wide stats, must equal the C
+oracle over the whole stream.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from oracle.c_oracle import COracle
+from ratelimit_amd import abi, workloads as W
+from ratelimit_amd.packing import RuleInterner, pack_calls, slice_requests
+import streams
+from test_sharded_cpu import _free_port, _split_points
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+pytestmark = pytest.mark.gpu
+
+
+def _batches(kind, seed):
+    if kind == "random":
+        calls = streams.random_stream(seed, n_calls=480, zipf=True)
+        interner = RuleInterner()
+        pbs = [pack_calls(calls[k:k + 60], "", interner) for k in range(0, len(calls), 60)]
+        nr = max(len(interner.keys), 1)
+        return [(pb.arrays, pb.n, pb.n_requests, nr) for pb in pbs]
+    return list(W.c2_stream(seed=seed, n_tenants=20_000, requests_per_batch=6_000, batches=4))
+
+
+def _worker(rank, world, port, backend, batches, cfg, q):
+    sys.path.insert(0, HERE)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from ratelimit_amd.limiter import Backend
+    from ratelimit_amd.sharded import DeviceRouteOps, Exchange, ShardedRateLimitCache
+    try:
+        dist.init_process_group(backend, rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        be = Backend(*cfg, table_slots=1 << 18, max_batch=1 << 15, max_rules=64, device=0)
+        sc = ShardedRateLimitCache(DeviceRouteOps(be), Exchange(), max_batch=1 << 15, max_stem_bytes=1 << 21,
+                                   device=dev)
+        res = []
+        for k, (arrays, n, nq, n_rules) in enumerate(batches):
+            cuts = _split_points(nq, world, k)
+            sub, sn, snq = slice_requests(arrays, n, nq, cuts[rank], cuts[rank + 1])
+            dev_in = {key: torch.from_numpy(np.ascontiguousarray(v).view(
+                {np.dtype(np.uint32): np.int32}.get(v.dtype, v.dtype))).to(dev) for key, v in sub.items()}
+            dev_out = {"code": torch.zeros(max(sn, 1), dtype=torch.uint8, device=dev),
+                       "limit_remaining": torch.zeros(max(sn, 1), dtype=torch.int32, device=dev),
+                       "reset_s": torch.zeros(max(sn, 1), dtype=torch.int32, device=dev)}
+            stats = sc.do_limit(dev_in, sn, snq, n_rules, dev_out)
+            res.append((dev_out["code"][:sn].cpu().numpy(), dev_out["limit_remaining"][:sn].cpu().numpy().view(np.uint32),
+                        dev_out["reset_s"][:sn].cpu().numpy().view(np.uint32), stats.cpu().numpy().view(np.uint64)))
+        be.close()
+        q.put((rank, res, None))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+def _run(world, backend, batches, cfg):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, backend, batches, cfg, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            rank, res, err = q.get(timeout=100)
+            assert err is None, err
+            out[rank] = res
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    return out
+
+
+@pytest.mark.parametrize("world,backend,kind,local_cache", [(1, "nccl", "random", True), (2, "gloo", "random", True),
+                                                            (2, "gloo", "c2", False)])
+def test_gpu_sharded_matches_oracle(world, backend, kind, local_cache):
+    cfg = (0.8, local_cache, False)
+    batches = _batches(kind, 7)
+    out = _run(world, backend, batches, cfg)
+    co = COracle(*cfg)
+    for k, (arrays, n, nq, n_rules) in enumerate(batches):
+        exp = co.do_limit(arrays, n, nq, n_rules)
+        for f, i in (("code", 0), ("limit_remaining", 1), ("reset_s", 2)):
+            got = np.concatenate([out[r][k][i] for r in range(world)])
+            assert np.array_equal(got, exp[f]), (k, f)
+        for r in range(world):
+            assert np.array_equal(out[r][k][3], exp["stats"][:n_rules * abi.RL_NUM_STATS]), (k, r)
