@@ -6,9 +6,12 @@ A step is one DoLimit batch over device-resident packed input (BASELINE.json
 configs[1] = C1 by default: 10M tenant stems x {sec, min} per GPU, 500k
 requests = 1M descriptors per batch, uniform tenants, `now` +1 s per step).
 Before timing, every key is inserted ("warm-up inserts all 20M keys").
-N>1 (torch.distributed.run, one process per GPU): each rank owns a disjoint
-10M-tenant key range (hash-sharded by construction, weak scaling, no
-data-path collective); value = all ranks' decisions / max-over-ranks time.
+N>1 (torch.distributed.run, one process per GPU): the table is hash-sharded
+over the GPUs (10M tenants x 2 keys per GPU; --config c3: 62.5M, i.e. 1B keys
+on 8), each rank draws its 1M-descriptor slice from the whole node's tenant
+space, and every batch is routed to the owning GPUs and back with RCCL
+all_to_all (ratelimit_amd/sharded.py); weak scaling, value = all ranks'
+decisions / max-over-ranks time. --route runs the routed path at N=1.
 
 Besides the contract line, rank 0 reports:
   roofline      dominant kernel (k_runs) achieved GB/s on the canonical
@@ -37,15 +40,28 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c1", choices=["c1", "c2"])
+    ap.add_argument("--config", default="c1", choices=["c1", "c2", "c3"],
+                    help="c1 uniform / c2 Zipf(1.1), hits 1..8 / c3 = c1 at 62.5M tenants per GPU (1B keys on 8)")
     ap.add_argument("--requests", type=int, default=500_000, help="requests per batch per GPU (2 descriptors each)")
-    ap.add_argument("--tenants", type=int, default=10_000_000, help="tenants per GPU")
+    ap.add_argument("--tenants", type=int, default=0, help="tenants per GPU (default 10M; c3 62.5M)")
     ap.add_argument("--distinct-batches", type=int, default=4)
     ap.add_argument("--latency-steps", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fill", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--route", action="store_true", help="use the routed (all_to_all) path even at N=1")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo + --one-device: rehearse N ranks on one GPU (host-staged exchange)")
+    ap.add_argument("--one-device", action="store_true", help="every rank uses cuda:0 (rehearsal only)")
+    args = ap.parse_args()
+    if not args.tenants:
+        args.tenants = 62_500_000 if args.config == "c3" else 10_000_000
+    return args
+
+
+def to_dev(a, torch):
+    return {k: torch.from_numpy(np.ascontiguousarray(v).view(np.int32) if v.dtype == np.uint32
+                                else np.ascontiguousarray(v)).cuda() for k, v in a.items()}
 
 
 def main():
@@ -58,15 +74,24 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    routed = world > 1 or args.route
+    if routed:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29561")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     def barrier():
-        if world > 1:
+        if routed:
             dist.barrier()
 
     nq = args.requests
@@ -74,39 +99,53 @@ def main():
     T = args.tenants
     keys_per_gpu = 2 * T
     slots = 1 << max(16, int(np.ceil(np.log2(2 * keys_per_gpu))))
-    be = Backend(0.8, False, table_slots=slots, max_batch=n, max_rules=8, device=local)
-    base_t = rank * T  # this rank's tenant range (disjoint across ranks)
+    # a routed owner receives ~n descriptors (binomial spread across sources)
+    cap = n if not routed else int(n * 1.05) + 4096
+    be = Backend(0.8, False, table_slots=slots, max_batch=cap, max_rules=8, device=local,
+                 max_stem_bytes=64 * cap)
     now0 = W.NOW0
-
-    # ---- fill: insert every key of this rank's range (not timed)
-    t_fill = time.perf_counter()
-    if not args.no_fill:
-        for s0 in range(0, T, nq):
-            ids = np.arange(s0, min(s0 + nq, T), dtype=np.int64) + base_t
-            a, bn, bq, br = W.c1_batch(ids, now0 - 1)
-            be.do_limit_arrays(a, bn, bq, br)
-    t_fill = time.perf_counter() - t_fill
-
-    # ---- device-resident input batches + per-step clocks
-    rng = np.random.default_rng((0xC1 if args.config == "c1" else 0xC2) + 7919 * rank)
-    sampler = W.ZipfSampler(T, 1.1) if args.config == "c2" else None
-    dev_batches = []
-    for _ in range(args.distinct_batches):
-        if sampler is None:
-            a, bn, bq, br = W.c1_batch(rng.integers(0, T, nq) + base_t, now0)
-        else:
-            a, bn, bq, br = W.c1_batch(sampler.sample(rng, nq) + base_t, now0,
-                                       rng.integers(1, 9, nq).astype(np.uint32))
-        dev_batches.append({k: torch.from_numpy(np.ascontiguousarray(v).view(np.int32) if v.dtype == np.uint32
-                                                else np.ascontiguousarray(v)).cuda()
-                            for k, v in a.items() if k != "now"})
-    stem_len = 34
-    total_steps = args.warmup + args.steps + args.steps + args.latency_steps
-    nows = [torch.full((nq,), now0 + s, dtype=torch.int64, device="cuda") for s in range(total_steps)]
+    if routed:
+        from ratelimit_amd.sharded import DeviceRouteOps, Exchange, ShardedRateLimitCache
+        sc = ShardedRateLimitCache(DeviceRouteOps(be), Exchange(), max_batch=n, max_stem_bytes=64 * n,
+                                   device=torch.device("cuda", local), max_recv=cap, max_recv_stem=64 * cap)
     out = {"code": torch.empty(n, dtype=torch.uint8, device="cuda"),
            "limit_remaining": torch.empty(n, dtype=torch.int32, device="cuda"),
            "reset_s": torch.empty(n, dtype=torch.int32, device="cuda"),
            "stats": torch.zeros(2 * 6, dtype=torch.int64, device="cuda")}
+
+    def do_step(inp, bn, bq):
+        if routed:
+            sc.do_limit(inp, bn, bq, 2, out)
+        else:
+            be.do_limit_device(inp, out, bn, bq, 2)
+
+    # ---- fill: every key of the node's tenant space (rank r inserts tenants
+    # [r*T, (r+1)*T); routed batches land on their owners). Not timed.
+    t_fill = time.perf_counter()
+    if not args.no_fill:
+        for s0 in range(0, T, nq):
+            ids = np.arange(s0, min(s0 + nq, T), dtype=np.int64) + rank * T
+            a, bn, bq, br = W.c1_batch(ids, now0 - 1)
+            do_step(to_dev(a, torch), bn, bq)
+        be.synchronize()
+    t_fill = time.perf_counter() - t_fill
+
+    # ---- device-resident input batches + per-step clocks. Requests draw from
+    # the whole node's tenant space (world * T): with routing every rank talks
+    # to every owner.
+    rng = np.random.default_rng((0xC2 if args.config == "c2" else 0xC1) + 7919 * rank)
+    sampler = W.ZipfSampler(world * T, 1.1) if args.config == "c2" else None
+    dev_batches = []
+    for _ in range(args.distinct_batches):
+        if sampler is None:
+            a, bn, bq, br = W.c1_batch(rng.integers(0, world * T, nq), now0)
+        else:
+            a, bn, bq, br = W.c1_batch(sampler.sample(rng, nq), now0, rng.integers(1, 9, nq).astype(np.uint32))
+        a.pop("now")
+        dev_batches.append(to_dev(a, torch))
+    stem_len = 34
+    total_steps = args.warmup + args.steps + args.steps + args.latency_steps
+    nows = [torch.full((nq,), now0 + s, dtype=torch.int64, device="cuda") for s in range(total_steps)]
     torch.cuda.synchronize()
 
     step = [0]
@@ -115,7 +154,7 @@ def main():
         s = step[0]
         inp = dict(dev_batches[s % len(dev_batches)])
         inp["now"] = nows[s]
-        be.do_limit_device(inp, out, n, nq, 2)
+        do_step(inp, n, nq)
         step[0] += 1
 
     # ---- warmup
@@ -134,20 +173,23 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if routed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     value = world * n * args.steps / elapsed
 
     # ---- per-stage device times (HIP events on the library stream)
     be.profile(True)
+    recv = []
     for _ in range(args.steps):
         run_step()
+        recv.append(sc.last_recv if routed else n)
     be.synchronize()
     stage_ms, nb = be.profile_read()
     be.profile(False)
     stage_avg = {k: v / max(nb, 1) for k, v in stage_ms.items()}
+    n_owner = float(np.mean(recv))
 
     # ---- batch latency: submit -> outputs ready, one batch at a time
     lat = []
@@ -158,49 +200,57 @@ def main():
         lat.append((time.perf_counter() - t1) * 1e3)
     lat = np.array(lat) if lat else np.array([float("nan")])
     info = be.table_info()
+    if routed:
+        lt = torch.tensor([float(np.percentile(lat, 99))], dtype=torch.float64,
+                          device="cuda" if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(lt, op=dist.ReduceOp.MAX)
+        p99 = float(lt.item())
+    else:
+        p99 = float(np.percentile(lat, 99))
 
     if rank != 0:
-        if world > 1:
+        if routed:
             dist.destroy_process_group()
         return
 
     b_alg = stem_len + 10 + 16 + 12 + 64  # key = stem + 10-digit window
     runs_ms = stage_avg["runs"]
-    achieved = b_alg * n / (runs_ms * 1e-3) / 1e9 if runs_ms > 0 else None
+    achieved = b_alg * n_owner / (runs_ms * 1e-3) / 1e9 if runs_ms > 0 else None
     pipe_ms = sum(stage_avg.values())
     traffic = None
     tp = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
-    if os.path.exists(tp):
+    if os.path.exists(tp) and not routed:
         try:
             traffic = json.load(open(tp)).get("k_runs_bytes_per_launch")
         except Exception:
             traffic = None
     roofline = {"bound": "hbm", "kernel": "k_runs", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                "bytes_alg_per_decision": b_alg, "decisions_per_launch": n,
+                "bytes_alg_per_decision": b_alg, "decisions_per_launch": n_owner,
                 "stage_ms": {k: round(v, 4) for k, v in stage_avg.items()},
-                "pipeline_achieved": b_alg * n / (pipe_ms * 1e-3) / 1e9 if pipe_ms > 0 else None}
+                "pipeline_achieved": b_alg * n_owner / (pipe_ms * 1e-3) / 1e9 if pipe_ms > 0 else None}
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, W)
 
+    dist_desc = {"c1": "uniform", "c2": "Zipf(1.1), hits 1..8", "c3": "uniform"}[args.config]
     line = {
         "metric": METRIC, "value": value, "unit": "decisions/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-        "config": {"workload": "%s: %dM tenant stems x {sec,min} per GPU, %d-descriptor batches, %s tenants%s, "
-                               "now +1 s per batch, all keys pre-inserted" %
-                               (args.config.upper(), T // 1_000_000, n,
-                                "uniform" if args.config == "c1" else "Zipf(1.1)",
-                                "" if args.config == "c1" else ", hits 1..8"),
+        "config": {"workload": "%s: %.1fM tenant stems x {sec,min} per GPU (%d live keys node-wide), "
+                               "%d-descriptor batches per GPU, %s tenants, now +1 s per batch, all keys pre-inserted"
+                               % (args.config.upper(), T / 1e6, 2 * T * world, n, dist_desc),
                    "global_batch": world * n, "batch_per_gpu": n, "live_stem_slots_per_gpu": info["live_slots"],
-                   "table_slots": slots, "parallelism": "hash-sharded key ranges x%d (no data-path collective)" % world},
-        "p50_batch_ms": float(np.percentile(lat, 50)), "p99_batch_ms": float(np.percentile(lat, 99)),
+                   "table_slots": slots,
+                   "parallelism": ("hash-sharded table x%d, RCCL all_to_all routing" % world) if routed else
+                                  "single GPU"},
+        "p50_batch_ms": float(np.percentile(lat, 50)), "p99_batch_ms": p99,
         "roofline": roofline, "cpu_baseline": cpu, "fill_s": round(t_fill, 2),
     }
     print(json.dumps(line), flush=True)
-    if world > 1:
+    if routed:
         dist.destroy_process_group()
 
 
