@@ -29,6 +29,14 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libratelimit_hip.so not built (%s): run `python -m ratelimit_amd.build`" % LIB_PATH)
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7. Loaded
+    # first, it also serves this library (same soname); loaded after ours, torch
+    # would bring a second runtime that finds no GPU. Device tensors handed to
+    # the *_async / rl_route_* entry points must come from the same runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     L.rl_abi_version.restype = C.c_uint32
     L.rl_create.restype = C.c_void_p

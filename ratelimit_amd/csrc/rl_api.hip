@@ -1,6 +1,15 @@
 // rl_api.hip — the extern "C" boundary of libratelimit_hip.so
-// (include/ratelimit_hip.h). Owns the HBM table, per-batch scratch and the
-// HIP stream; every entry point maps a device error word to an rl_status.
+// (include/ratelimit_hip.h). Owns the HBM table, two sets of per-batch scratch
+// and the HIP streams; every entry point maps the device error words to an
+// rl_status.
+//
+// Batches submitted with rl_do_limit_async(stream = NULL) are pipelined: batch
+// t's table-free stage A (validate, hash, sort, segment) runs on scratch buffer
+// t % 2 and that buffer's stream while batch t-1's stage B (the table) still
+// runs. Stage B of every batch waits for the previous batch's stage B (an
+// event chain), so the table sees batches in submission order and every key
+// sees the reference's sequential INCRBY order. Every other call is serial and
+// ordered after all submitted batches.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -16,14 +25,19 @@ using namespace rl;
 
 struct rl_ctx {
   rl_config cfg;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // serial work (== pipe[0])
+  hipStream_t pipe[2] = {};       // one per scratch buffer
+  hipEvent_t b_done[2] = {};      // stage B of the last batch on each buffer is done
+  uint32_t next = 0, last = 1;    // buffer of the next / of the latest batch
   // table
   Slot* slots = nullptr;
   uint64_t nslots = 0;
   uint8_t* arena = nullptr;
   uint64_t arena_cap16 = 0;
-  // scratch
-  Scratch s{};
+  // scratch: s[k] per buffer; stripes, counters, time floor, routing and the
+  // table-stage error word are shared
+  Scratch s[2]{};
+  uint32_t* errw = nullptr;  // [0], [1] stage-A words of the buffers, [2] stage-B word
   // device staging for the host-buffer entry points
   uint8_t* d_stem = nullptr;
   uint32_t *d_off = nullptr, *d_req = nullptr, *d_limit = nullptr, *d_hits = nullptr, *d_rule = nullptr;
@@ -31,7 +45,7 @@ struct rl_ctx {
   uint8_t *d_unit = nullptr, *d_flags = nullptr, *d_code = nullptr;
   uint32_t *d_rem = nullptr, *d_reset = nullptr;
   unsigned long long* d_stats = nullptr;
-  uint32_t* h_err = nullptr;  // pinned
+  uint32_t* h_err = nullptr;  // pinned [4]
   unsigned long long* h_counters = nullptr;
   unsigned long long* h_route = nullptr;  // pinned route counts
   std::string last_error;
@@ -99,17 +113,52 @@ int map_err(rl_ctx* c, uint32_t e) {
   return set_err(c, RL_E_INTERNAL, "gpu: unknown device error");
 }
 
-// Read (and clear) the sticky device error word; synchronises the stream.
+// Order stream st after every batch submitted so far (their stage B, which
+// waited for all earlier ones).
+hipError_t after_batches(rl_ctx* c, hipStream_t st) { return hipStreamWaitEvent(st, c->b_done[c->last], 0); }
+
+// Read (and clear) the sticky device error words; synchronises the stream,
+// which must already be ordered after all submitted work.
 int collect(rl_ctx* c, hipStream_t st = nullptr) {
   if (!st) st = c->stream;
-  HIPCHK(c, hipMemcpyAsync(c->h_err, c->s.err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_err, c->errw, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
-  const uint32_t e = *c->h_err;
+  const uint32_t e = c->h_err[0] | c->h_err[1] | c->h_err[2];
   if (e) {
-    HIPCHK(c, hipMemsetAsync(c->s.err, 0, sizeof(uint32_t), st));
+    HIPCHK(c, hipMemsetAsync(c->errw, 0, 3 * sizeof(uint32_t), st));
     HIPCHK(c, hipStreamSynchronize(st));
   }
   return map_err(c, e);
+}
+
+TableDev table_view(rl_ctx* c);
+Params params(rl_ctx* c);
+
+// Enqueue one batch. Pipelined (ctx streams, profiling off): stage A on the
+// buffer's own stream as soon as the buffer is free, stage B after the
+// previous batch's stage B. Serial: both stages on `st` after all earlier work.
+uint32_t enqueue(rl_ctx* c, const BatchDev& b, const OutDev& o, int restore, hipStream_t st, bool pipelined) {
+  const uint32_t k = c->next;
+  c->next ^= 1u;
+  const TableDev t = table_view(c);
+  const Params P = params(c);
+  if (pipelined && !c->prof) {
+    hipStream_t a = c->pipe[k];
+    (void)hipStreamWaitEvent(a, c->b_done[k], 0);  // buffer k's previous batch is done
+    launch_stage_a(b, c->s[k], a);
+    (void)hipStreamWaitEvent(a, c->b_done[c->last], 0);  // table order
+    launch_stage_b(b, o, t, P, c->s[k], restore, a);
+    (void)hipEventRecord(c->b_done[k], a);
+  } else {
+    if (!st) st = c->stream;
+    (void)after_batches(c, st);
+    hipEvent_t* ev = prof_events(c);
+    launch_stage_a(b, c->s[k], st, ev);
+    launch_stage_b(b, o, t, P, c->s[k], restore, st, ev);
+    (void)hipEventRecord(c->b_done[k], st);
+  }
+  c->last = k;
+  return k;
 }
 
 int check_sizes(rl_ctx* c, const rl_batch* in, uint64_t stem_bytes) {
@@ -146,7 +195,7 @@ TableDev table_view(rl_ctx* c) {
   t.slots = c->slots;
   t.mask = c->nslots - 1;
   t.arena = c->arena;
-  t.arena_used16 = c->s.counters + 4;
+  t.arena_used16 = c->s[0].counters + 4;
   t.arena_cap16 = c->arena_cap16;
   t.max_probe = (uint32_t)std::min<uint64_t>(c->nslots, 1u << 16);
   t.shift = 64u - (uint32_t)__builtin_ctzll(c->nslots);
@@ -161,6 +210,33 @@ Params params(rl_ctx* c) {
   return P;
 }
 
+// Per-batch scratch of one pipeline buffer (sized for max_batch descriptors).
+bool alloc_buffer(Scratch& s, uint32_t n) {
+  const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
+  const size_t nt = (n + SEG_TILE - 1) / SEG_TILE + 1;
+  bool ok = dalloc(&s.key, 4ull * n) == hipSuccess && dalloc(&s.key_s, 4ull * n) == hipSuccess;
+  ok = ok && dalloc(&s.rec, n) == hipSuccess && dalloc(&s.rec_s, n) == hipSuccess && dalloc(&s.res, n) == hipSuccess;
+  for (int i = 0; i < 2; i++) ok = ok && dalloc(&s.keys[i], n) == hipSuccess && dalloc(&s.vals[i], n) == hipSuccess;
+  ok = ok && dalloc(&s.hist, 256ull * std::max(ntiles, 1u)) == hipSuccess && dalloc(&s.hist_tot, 256) == hipSuccess;
+  ok = ok && dalloc(&s.repid, n) == hipSuccess && dalloc(&s.defer, n) == hipSuccess &&
+       dalloc(&s.defer_n, 1) == hipSuccess;
+  ok = ok && dalloc(&s.tile_f, nt) == hipSuccess && dalloc(&s.tile_s, nt) == hipSuccess &&
+       dalloc(&s.tile_h, nt) == hipSuccess;
+  ok = ok && dalloc(&s.hits_s, n) == hipSuccess && dalloc(&s.segsum, n) == hipSuccess &&
+       dalloc(&s.rid, n) == hipSuccess && dalloc(&s.run_start, (size_t)n + 1) == hipSuccess &&
+       dalloc(&s.run_flags, n) == hipSuccess && dalloc(&s.run_state, n) == hipSuccess &&
+       dalloc(&s.run_f, n) == hipSuccess && dalloc(&s.num_runs, 1) == hipSuccess;
+  return ok;
+}
+
+void free_buffer(Scratch& s) {
+  void* bufs[] = {s.rec, s.rec_s, s.res, s.key, s.key_s, s.keys[0], s.keys[1], s.vals[0], s.vals[1], s.hist,
+                  s.hist_tot, s.repid, s.defer, s.defer_n, s.tile_f, s.tile_s, s.tile_h, s.hits_s, s.segsum, s.rid,
+                  s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+}
+
 // Copy a host batch into the staging buffers; returns the device view.
 int stage(rl_ctx* c, const rl_batch* in, BatchDev* out) {
   const uint32_t n = in->n, nq = in->n_requests;
@@ -168,6 +244,7 @@ int stage(rl_ctx* c, const rl_batch* in, BatchDev* out) {
   int rc = check_sizes(c, in, nb);
   if (rc) return rc;
   hipStream_t st = c->stream;
+  HIPCHK(c, after_batches(c, st));  // staging may still feed a routed batch
   if (nb) HIPCHK(c, hipMemcpyAsync(c->d_stem, in->stem_bytes, nb, hipMemcpyHostToDevice, st));
   HIPCHK(c, hipMemcpyAsync(c->d_off, in->stem_off, (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   if (nq) HIPCHK(c, hipMemcpyAsync(c->d_now, in->now, nq * sizeof(int64_t), hipMemcpyHostToDevice, st));
@@ -224,39 +301,31 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   c->nslots = cfg.table_slots;
   c->arena_cap16 = cfg.arena_bytes / 16;
   const uint32_t n = cfg.max_batch;
-  const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
-  bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
+  bool ok = hipStreamCreateWithFlags(&c->pipe[0], hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->pipe[1], hipStreamNonBlocking) == hipSuccess;
+  c->stream = c->pipe[0];
+  for (int k = 0; k < 2; k++) ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess;
   ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess;
   ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess;
-  ok = ok && dalloc(&c->s.key, 4ull * n) == hipSuccess && dalloc(&c->s.key_s, 4ull * n) == hipSuccess;
-  ok = ok && dalloc(&c->s.rec, n) == hipSuccess && dalloc(&c->s.rec_s, n) == hipSuccess &&
-       dalloc(&c->s.res, n) == hipSuccess;
-  for (int i = 0; i < 2; i++) {
-    ok = ok && dalloc(&c->s.keys[i], n) == hipSuccess;
-    ok = ok && dalloc(&c->s.vals[i], n) == hipSuccess;
+  for (int k = 0; k < 2; k++) ok = ok && alloc_buffer(c->s[k], n);
+  Scratch& s0 = c->s[0];
+  ok = ok && dalloc(&c->errw, 4) == hipSuccess;
+  ok = ok && dalloc(&s0.stripes, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS) == hipSuccess;
+  ok = ok && dalloc(&s0.time_floor, 1) == hipSuccess;
+  ok = ok && dalloc(&s0.counters, 8) == hipSuccess;
+  ok = ok && dalloc(&s0.route_start, RL_MAX_SHARDS + 1) == hipSuccess &&
+       dalloc(&s0.route_base, RL_MAX_SHARDS) == hipSuccess && dalloc(&s0.route_counts, 2 * RL_MAX_SHARDS) == hipSuccess;
+  for (int k = 0; k < 2; k++) {  // shared members
+    Scratch& sk = c->s[k];
+    sk.err = c->errw ? c->errw + k : nullptr;
+    sk.errb = c->errw ? c->errw + 2 : nullptr;
+    sk.stripes = s0.stripes;
+    sk.time_floor = s0.time_floor;
+    sk.counters = s0.counters;
+    sk.route_start = s0.route_start;
+    sk.route_base = s0.route_base;
+    sk.route_counts = s0.route_counts;
   }
-  ok = ok && dalloc(&c->s.hist, 256ull * std::max(ntiles, 1u)) == hipSuccess;
-  ok = ok && dalloc(&c->s.hist_tot, 256) == hipSuccess;
-  ok = ok && dalloc(&c->s.repid, n) == hipSuccess;
-  ok = ok && dalloc(&c->s.defer, n) == hipSuccess;
-  {
-    const size_t nt = (n + SEG_TILE - 1) / SEG_TILE + 1;
-    ok = ok && dalloc(&c->s.tile_f, nt) == hipSuccess && dalloc(&c->s.tile_s, nt) == hipSuccess &&
-         dalloc(&c->s.tile_h, nt) == hipSuccess;
-    ok = ok && dalloc(&c->s.hits_s, n) == hipSuccess;
-    ok = ok && dalloc(&c->s.segsum, n) == hipSuccess && dalloc(&c->s.rid, n) == hipSuccess &&
-         dalloc(&c->s.run_start, (size_t)n + 1) == hipSuccess && dalloc(&c->s.run_flags, n) == hipSuccess &&
-         dalloc(&c->s.run_state, n) == hipSuccess && dalloc(&c->s.run_f, n) == hipSuccess &&
-         dalloc(&c->s.num_runs, 1) == hipSuccess;
-  }
-  ok = ok && dalloc(&c->s.defer_n, 1) == hipSuccess;
-  ok = ok && dalloc(&c->s.stripes, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS) == hipSuccess;
-  ok = ok && dalloc(&c->s.err, 1) == hipSuccess;
-  ok = ok && dalloc(&c->s.time_floor, 1) == hipSuccess;
-  ok = ok && dalloc(&c->s.counters, 8) == hipSuccess;
-  ok = ok && dalloc(&c->s.route_start, RL_MAX_SHARDS + 1) == hipSuccess &&
-       dalloc(&c->s.route_base, RL_MAX_SHARDS) == hipSuccess &&
-       dalloc(&c->s.route_counts, 2 * RL_MAX_SHARDS) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_route, 2 * RL_MAX_SHARDS * sizeof(unsigned long long)) == hipSuccess;
   ok = ok && dalloc(&c->d_stem, (size_t)cfg.max_stem_bytes + 64) == hipSuccess;
   ok = ok && dalloc(&c->d_off, (size_t)n + 1) == hipSuccess;
@@ -267,16 +336,17 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && dalloc(&c->d_code, n) == hipSuccess && dalloc(&c->d_rem, n) == hipSuccess &&
        dalloc(&c->d_reset, n) == hipSuccess;
   ok = ok && dalloc(&c->d_stats, (size_t)cfg.max_rules * RL_NUM_STATS) == hipSuccess;
-  ok = ok && hipHostMalloc((void**)&c->h_err, sizeof(uint32_t)) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_err, 4 * sizeof(uint32_t)) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_counters, 8 * sizeof(unsigned long long)) == hipSuccess;
   if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
   ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
-       hipMemsetAsync(c->s.err, 0, 4, c->stream) == hipSuccess &&
-       hipMemsetAsync(c->s.time_floor, 0, 8, c->stream) == hipSuccess &&
-       hipMemsetAsync(c->s.counters, 0, 64, c->stream) == hipSuccess &&
-       hipMemsetAsync(c->s.stripes, 0, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS * 8, c->stream) ==
+       hipMemsetAsync(c->errw, 0, 16, c->stream) == hipSuccess &&
+       hipMemsetAsync(s0.time_floor, 0, 8, c->stream) == hipSuccess &&
+       hipMemsetAsync(s0.counters, 0, 64, c->stream) == hipSuccess &&
+       hipMemsetAsync(s0.stripes, 0, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS * 8, c->stream) ==
            hipSuccess &&
        hipMemsetAsync(c->d_stem, 0, (size_t)cfg.max_stem_bytes + 64, c->stream) == hipSuccess &&
+       hipEventRecord(c->b_done[0], c->stream) == hipSuccess && hipEventRecord(c->b_done[1], c->stream) == hipSuccess &&
        hipStreamSynchronize(c->stream) == hipSuccess;
   if (!ok) return fail("gpu: device initialisation failed", c);
   return c;
@@ -285,20 +355,25 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
 void rl_destroy(rl_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->cfg.device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (int k = 0; k < 2; k++)
+    if (c->pipe[k]) (void)hipStreamSynchronize(c->pipe[k]);
   for (int i = 0; i <= RL_NUM_STAGES; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
-  void* bufs[] = {c->slots, c->arena, c->s.rec, c->s.rec_s, c->s.res, c->s.key, c->s.key_s, c->s.keys[0], c->s.keys[1], c->s.vals[0], c->s.vals[1],
-                  c->s.hist, c->s.hist_tot, c->s.repid, c->s.defer, c->s.defer_n, c->s.stripes, c->s.tile_f, c->s.tile_s, c->s.tile_h, c->s.hits_s, c->s.segsum, c->s.rid,
-                  c->s.run_start, c->s.run_flags, c->s.run_state, c->s.run_f, c->s.num_runs, c->s.err, c->s.time_floor, c->s.counters, c->d_stem, c->d_off, c->d_now,
-                  c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_rem,
-                  c->d_reset, c->d_stats, c->s.route_start, c->s.route_base, c->s.route_counts};
+  for (int k = 0; k < 2; k++) {
+    free_buffer(c->s[k]);
+    if (c->b_done[k]) (void)hipEventDestroy(c->b_done[k]);
+  }
+  const Scratch& s0 = c->s[0];
+  void* bufs[] = {c->slots, c->arena, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
+                  c->d_now, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_rem,
+                  c->d_reset, c->d_stats, s0.route_start, s0.route_base, s0.route_counts};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
   if (c->h_route) (void)hipHostFree(c->h_route);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  for (int k = 0; k < 2; k++)
+    if (c->pipe[k]) (void)hipStreamDestroy(c->pipe[k]);
   delete c;
 }
 
@@ -310,11 +385,10 @@ int rl_do_limit_async(rl_ctx* c, const rl_batch* in, rl_result* out, void* strea
   if (rc) return rc;
   if ((uintptr_t)in->stem_bytes & 3u) return set_err(c, RL_E_INVALID, "gpu: stem_bytes must be 4-byte aligned");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-  if (in->n_rules) HIPCHK(c, hipMemsetAsync(out->stats, 0, (size_t)in->n_rules * RL_NUM_STATS * 8, st));
   BatchDev b = dev_view(in, c->cfg.max_stem_bytes);
   OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats};
-  launch_do_limit(b, o, table_view(c), params(c), c->s, 0, st, prof_events(c));
+  // NULL stream: pipelined on the ctx streams; otherwise serial on the caller's stream
+  enqueue(c, b, o, 0, (hipStream_t)stream, stream == nullptr);
   HIPCHK(c, hipGetLastError());
   c->batches++;
   c->decisions += in->n;
@@ -332,10 +406,11 @@ int rl_route_pack(rl_ctx* c, const rl_batch* in, uint32_t n_shards, uint32_t src
   if ((uintptr_t)in->stem_bytes & 3u) return set_err(c, RL_E_INVALID, "gpu: stem_bytes must be 4-byte aligned");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  HIPCHK(c, after_batches(c, st));  // the partition reuses buffer 0's scratch
   BatchDev b = dev_view(in, c->cfg.max_stem_bytes);
-  launch_route_pack(b, n_shards, src_rank, (Wire*)send_rec, send_stem, perm, c->s.route_counts, c->s, st);
+  launch_route_pack(b, n_shards, src_rank, (Wire*)send_rec, send_stem, perm, c->s[0].route_counts, c->s[0], st);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(c->h_route, c->s.route_counts, 2ull * n_shards * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_route, c->s[0].route_counts, 2ull * n_shards * 8, hipMemcpyDeviceToHost, st));
   rc = collect(c, st);
   for (uint32_t i = 0; i < 2 * n_shards; i++) counts_host[i] = rc ? 0 : c->h_route[i];
   return rc;
@@ -353,11 +428,13 @@ int rl_route_do_limit(rl_ctx* c, uint32_t n, const void* recv_rec, const uint8_t
   if ((uintptr_t)recv_stem & 3u) return set_err(c, RL_E_INVALID, "gpu: recv_stem must be 4-byte aligned");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-  HIPCHK(c, hipMemcpyAsync(c->s.route_base, src_stem_base, (size_t)n_shards * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(c, after_batches(c, st));  // the staging arrays below may still feed an earlier batch
+  HIPCHK(c, hipMemcpyAsync(c->s[0].route_base, src_stem_base, (size_t)n_shards * 8, hipMemcpyHostToDevice, st));
   BatchOut bo{c->d_off, c->d_now, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule};
-  launch_route_unpack((const Wire*)recv_rec, n, c->s.route_base, n_shards, recv_stem_bytes, bo, c->s.err, st);
+  // a malformed exchange poisons the table stage of this batch (sticky word)
+  launch_route_unpack((const Wire*)recv_rec, n, c->s[0].route_base, n_shards, recv_stem_bytes, bo, c->s[0].errb,
+                      st);
   if (!n) HIPCHK(c, hipMemsetAsync(c->d_off, 0, sizeof(uint32_t), st));
-  if (n_rules) HIPCHK(c, hipMemsetAsync(stats, 0, (size_t)n_rules * RL_NUM_STATS * 8, st));
   BatchDev b;
   b.n = n;
   b.n_req = n;
@@ -375,8 +452,8 @@ int rl_route_do_limit(rl_ctx* c, uint32_t n, const void* recv_rec, const uint8_t
   b.hits = c->d_hits;
   b.rule = c->d_rule;
   OutDev o{c->d_code, c->d_rem, c->d_reset, (unsigned long long*)stats};
-  launch_do_limit(b, o, table_view(c), params(c), c->s, 0, st, prof_events(c));
-  if (n) HIPCHK(c, hipMemcpyAsync(ret, c->s.res, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
+  const uint32_t k = enqueue(c, b, o, 0, st, false);
+  if (n) HIPCHK(c, hipMemcpyAsync(ret, c->s[k].res, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
   HIPCHK(c, hipGetLastError());
   c->batches++;
   c->decisions += n;
@@ -428,9 +505,8 @@ int rl_do_limit(rl_ctx* c, const rl_batch* in, rl_result* out) {
   int rc = stage(c, in, &b);
   if (rc) return rc;
   hipStream_t st = c->stream;
-  if (in->n_rules) HIPCHK(c, hipMemsetAsync(c->d_stats, 0, (size_t)in->n_rules * RL_NUM_STATS * 8, st));
   OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats};
-  launch_do_limit(b, o, table_view(c), params(c), c->s, 0, st, prof_events(c));
+  enqueue(c, b, o, 0, st, false);
   HIPCHK(c, hipGetLastError());
   const uint32_t n = in->n;
   if (n) {
@@ -478,7 +554,7 @@ int rl_restore(rl_ctx* c, const rl_restore_batch* r) {
   int rc = stage(c, &in, &b);
   if (!rc) {
     OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats};
-    launch_do_limit(b, o, table_view(c), params(c), c->s, 1, c->stream);
+    enqueue(c, b, o, 1, c->stream, false);
     hipError_t he = hipGetLastError();
     rc = he != hipSuccess ? set_err(c, RL_E_HIP, std::string("gpu: ") + hipGetErrorString(he)) : collect(c);
   }
@@ -494,13 +570,14 @@ int rl_sweep(rl_ctx* c, int64_t now, uint64_t* n_evicted) {
   HIPCHK(c, hipSetDevice(c->cfg.device));
   // the sweep time becomes a floor: later requests may not be earlier
   int64_t last = 0;
-  HIPCHK(c, hipMemcpyAsync(&last, c->s.time_floor, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, after_batches(c, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&last, c->s[0].time_floor, 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (now > last) HIPCHK(c, hipMemcpyAsync(c->s.time_floor, &now, 8, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemsetAsync(c->s.counters, 0, 8, c->stream));
-  launch_sweep(c->slots, c->nslots, (uint32_t)now, c->s.counters, c->stream);
+  if (now > last) HIPCHK(c, hipMemcpyAsync(c->s[0].time_floor, &now, 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->s[0].counters, 0, 8, c->stream));
+  launch_sweep(c->slots, c->nslots, (uint32_t)now, c->s[0].counters, c->stream);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s.counters, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (n_evicted) *n_evicted = c->h_counters[0];
   return RL_OK;
@@ -509,10 +586,11 @@ int rl_sweep(rl_ctx* c, int64_t now, uint64_t* n_evicted) {
 int rl_table_info_get(rl_ctx* c, rl_table_info* info) {
   if (!c || !info) return set_err(c, RL_E_INVALID, "gpu: null argument");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  HIPCHK(c, hipMemsetAsync(c->s.counters, 0, 24, c->stream));
-  launch_table_info(c->slots, c->nslots, c->s.counters, c->stream);
+  HIPCHK(c, after_batches(c, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->s[0].counters, 0, 24, c->stream));
+  launch_table_info(c->slots, c->nslots, c->s[0].counters, c->stream);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s.counters, 40, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 40, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   info->table_slots = c->nslots;
   info->live_slots = c->h_counters[0];

@@ -18,6 +18,7 @@ constexpr uint32_t RUN_SLOW = 1, RUN_FAST = 2;
 constexpr uint32_t KEY_HEAD = 64;         // stem bytes carried inline (zero-padded) per descriptor
 constexpr uint32_t STAT_STRIPES = 64;     // global partial stats tables
 constexpr uint32_t STAT_LDS_RULES = 512;  // rules aggregated in LDS (== LDS_RULES)
+constexpr uint32_t RUNS_GENERAL_BLOCKS = 64;  // grid of k_runs_general (grid-stride over deferrals)
 
 struct BatchDev {
   uint32_t n, n_req, n_rules, stem_cap;
@@ -127,7 +128,8 @@ struct Scratch {
   uint4* run_state;                    // [n] {slot, c0, old lc, F | which<<1}
   uint32_t* run_f;                     // [n] first over-limit position
   uint32_t* num_runs;
-  uint32_t* err;
+  uint32_t* err;   // validation word of this buffer's batch (stage A)
+  uint32_t* errb;  // sticky table-stage word (stage B), shared by both buffers
   int64_t* time_floor;  // requests earlier than the last sweep are rejected
   unsigned long long* counters;  // [0..3] sweep / info outputs
   // multi-GPU routing
@@ -136,6 +138,13 @@ struct Scratch {
   unsigned long long* route_counts;  // [2 * RL_MAX_SHARDS] records / stem bytes per owner
 };
 
+// The two stages of one batch. Stage A (validate, hash, sort, segment) touches
+// only the batch and this buffer's scratch, so it may overlap the previous
+// batch's stage B; stage B (table probe, replay, decisions, stats, results)
+// must run in batch order.
+void launch_stage_a(const BatchDev& b, const Scratch& s, hipStream_t st, hipEvent_t* ev = nullptr);
+void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
+                    int restore, hipStream_t st, hipEvent_t* ev = nullptr);
 // Launch the whole DoLimit pipeline (restore = 1: table seeding records).
 // ev (optional, RL_NUM_STAGES + 1 events on stream st): recorded before
 // k_prepare, after it, after the sort, just before and just after k_runs, and

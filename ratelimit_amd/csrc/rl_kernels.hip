@@ -1216,8 +1216,9 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
   StatAcc acc{use_lds, stats};
   LaneStats L;
   L.reset();
-  const uint32_t di = blockIdx.x * 256 + threadIdx.x;
-  if (di < s_n) {
+  // Grid-stride over the deferred runs: the grid is small and fixed (deferrals
+  // are rare), so an empty deferral list costs one short launch.
+  for (uint32_t di = blockIdx.x * 256 + threadIdx.x; di < s_n; di += gridDim.x * 256) {
     const uint32_t p = defer[di];
     const uint32_t key = skeys[p];
     uint32_t end = p + 1;
@@ -1303,6 +1304,21 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
   }
   if (!restore) wave_flush(L, acc);
   stats_block_end(use_lds, b.n_rules, stripes);
+}
+
+// First kernel of the table stage: merge this batch's validation errors into
+// the sticky table-stage word, clear the deferral counter and this call's
+// output stats (n_rules x RL_NUM_STATS).
+__global__ __launch_bounds__(256) void k_b_begin(const uint32_t* __restrict__ erra, uint32_t* errb,
+                                                 uint32_t* __restrict__ defer_n,
+                                                 unsigned long long* __restrict__ stats, uint32_t m) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i == 0) {
+    const uint32_t e = *erra;
+    if (e) atomicOr(errb, e);
+    *defer_n = 0;
+  }
+  for (uint32_t j = i; j < m; j += gridDim.x * 256) stats[j] = 0;
 }
 
 // Fold the striped per-block partial stats into rl_result.stats and clear them.
@@ -1415,8 +1431,9 @@ __global__ __launch_bounds__(256) void k_debug_decide(uint32_t n, const uint32_t
 // ===========================================================================
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
-void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                     int restore, hipStream_t st, hipEvent_t* ev) {
+// Stage A (table-free): validate, hash, sort, gather, segment. Uses only this
+// buffer's scratch and its validation word s.err.
+void launch_stage_a(const BatchDev& b, const Scratch& s, hipStream_t st, hipEvent_t* ev) {
   const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
   if (ev) (void)hipEventRecord(ev[0], st);
   if (g0) k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.key, s.keys[0], s.vals[0], s.err, s.time_floor);
@@ -1434,35 +1451,53 @@ void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, cons
   if (ev) (void)hipEventRecord(ev[2], st);
   if (b.n) {
     const uint32_t nt = cdiv(b.n, SEG_TILE), g = cdiv(b.n, 256);
-    const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
     k_gather<<<g, 256, 0, st>>>(s.rec, s.key, s.vals[0], b.n, s.rec_s, s.key_s, s.hits_s, s.err);
     k_seg_reduce<<<nt, 256, 0, st>>>(s.keys[0], s.hits_s, b.n, s.tile_f, s.tile_s, s.tile_h, s.err);
     k_seg_tiles<<<1, 1024, 0, st>>>(s.tile_f, s.tile_s, s.tile_h, nt, s.err);
     k_seg_apply<<<nt, 256, 0, st>>>(s.keys[0], s.hits_s, b.n, s.tile_f, s.tile_s, s.tile_h, s.segsum, s.rid,
                                     s.run_start, s.run_flags, s.num_runs, s.err);
     k_run_check<<<g, 256, 0, st>>>(b, s.rec_s, s.key_s, s.rid, s.run_start, s.run_flags, s.err);
-    (void)hipMemsetAsync(s.defer_n, 0, sizeof(uint32_t), st);
-    if (ev) (void)hipEventRecord(ev[3], st);
+  }
+}
+
+// Stage B (the table): runs strictly in batch order. Every kernel reads the
+// sticky table-stage word s.errb; k_b_begin folds this batch's validation
+// result into it first.
+void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
+                    int restore, hipStream_t st, hipEvent_t* ev) {
+  const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
+  const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
+  k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, s.defer_n, o.stats, m);
+  if (ev) (void)hipEventRecord(ev[3], st);
+  if (b.n) {
+    const uint32_t g = cdiv(b.n, 256);
+    const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
     k_runs<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.key_s, s.keys[0], s.vals[0], s.res, s.run_start, s.run_flags,
-                                s.run_state, s.run_f, s.num_runs, s.defer, s.defer_n, o.stats, s.stripes, s.err,
+                                s.run_state, s.run_f, s.num_runs, s.defer, s.defer_n, o.stats, s.stripes, s.errb,
                                 restore);
     if (ev) (void)hipEventRecord(ev[4], st);
-    k_runs_general<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.key_s, s.keys[0], s.vals[0], s.res, s.defer, s.defer_n,
-                                        s.repid, o.stats, s.stripes, s.err, restore);
+    k_runs_general<<<g < RUNS_GENERAL_BLOCKS ? g : RUNS_GENERAL_BLOCKS, 256, lds, st>>>(
+        b, t, P, s.rec_s, s.key_s, s.keys[0], s.vals[0], s.res, s.defer, s.defer_n, s.repid, o.stats, s.stripes,
+        s.errb, restore);
     if (!restore) {
       if (P.lc_en)
-        k_fast_over<<<g, 256, 0, st>>>(b.n, s.rec_s, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.err);
+        k_fast_over<<<g, 256, 0, st>>>(b.n, s.rec_s, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
       k_fast_emit<<<g, 256, lds, st>>>(b.n, b.n_rules, t, P, s.rec_s, s.vals[0], s.res, s.segsum, s.rid,
-                                       s.run_start, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.err);
+                                       s.run_start, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb);
       if (b.n_rules <= LDS_RULES && b.n_rules)
-        k_stats_fold<<<cdiv(b.n_rules * RL_NUM_STATS, 256), 256, 0, st>>>(s.stripes, b.n_rules, o.stats, s.err);
-      k_unpack<<<g, 256, 0, st>>>(s.res, b.n, o, s.err);
+        k_stats_fold<<<cdiv(b.n_rules * RL_NUM_STATS, 256), 256, 0, st>>>(s.stripes, b.n_rules, o.stats, s.errb);
+      k_unpack<<<g, 256, 0, st>>>(s.res, b.n, o, s.errb);
     }
   } else if (ev) {
-    (void)hipEventRecord(ev[3], st);
     (void)hipEventRecord(ev[4], st);
   }
   if (ev) (void)hipEventRecord(ev[5], st);
+}
+
+void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
+                     int restore, hipStream_t st, hipEvent_t* ev) {
+  launch_stage_a(b, s, st, ev);
+  launch_stage_b(b, o, t, P, s, restore, st, ev);
 }
 
 void launch_partition(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, uint32_t n,

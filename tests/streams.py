@@ -69,6 +69,72 @@ def random_stream(seed, n_calls=300, n_stems=12, start_now=1_700_000_035, max_st
     return calls
 
 
+def c4_stream(seed, n_calls=1500, start_now=1_700_000_037, end_now=1_700_000_043, p_override=0.01):
+    """BASELINE.json configs[4]: README Example 3/4-style nested
+    descriptors in domain "c4" (rules as config_impl.go:99-151 would load them):
+
+      service=<s> -> user (any value) -> method=<m> -> path (any value): SECOND 10
+                                                      -> path=/login: MINUTE 5, shadow_mode
+                                                      -> path=/health: unlimited (nil at DoLimit,
+                                                         ratelimit.go:140-143)
+      remote_address (any value): SECOND 10;  remote_address=50.0.0.5: SECOND 0
+
+    plus 1% per-request overrides (config_impl.go:254-265: a fresh RateLimit whose
+    stats key is descriptorKey, :300-312), duplicate descriptors inside one request,
+    hits_addend 1..8 and a non-decreasing clock stepping across the second and
+    minute boundaries (1_700_000_040 % 60 == 0). Wildcard rules share one stats key
+    for every value (config_test.go:110)."""
+    rng = random.Random(seed)
+    reg = {}
+
+    def rl(key, rpu, unit, shadow=False):
+        if key not in reg:
+            reg[key] = O.RateLimitStats(key)
+        return O.RateLimit(key, reg[key], O.Limit(rpu, unit), False, shadow)
+
+    dom = "c4"
+    services = ["svc%d" % i for i in range(3)]
+    users = ["u%03d" % i for i in range(24)]
+    methods = ["GET", "POST"]
+    paths = ["/login", "/health", "/api/a", "/api/b", "/static"]
+    ips = ["10.0.0.%d" % i for i in range(20)] + ["50.0.0.5"] * 2
+    nows = sorted(rng.randint(start_now, end_now) for _ in range(n_calls))
+    calls = []
+    for now in nows:
+        descs, limits = [], []
+        for _ in range(rng.randint(1, 4)):
+            if descs and rng.random() < 0.2:  # the same descriptor twice in one request
+                j = rng.randrange(len(descs))
+                descs.append(O.Descriptor(list(descs[j].entries), descs[j].limit))
+                limits.append(limits[j])
+                continue
+            if rng.random() < 0.7:
+                s, u, m, p = rng.choice(services), rng.choice(users), rng.choice(methods), rng.choice(paths)
+                entries = [("service", s), ("user", u), ("method", m), ("path", p)]
+                base = "%s.service_%s.user.method_%s" % (dom, s, m)
+                if p == "/login":
+                    lim = rl(base + ".path_/login", 5, O.MINUTE, True)
+                elif p == "/health":
+                    lim = None
+                else:
+                    lim = rl(base + ".path", 10, O.SECOND)
+            else:
+                ip = rng.choice(ips)
+                entries = [("remote_address", ip)]
+                lim = rl(dom + ".remote_address_50.0.0.5", 0, O.SECOND) if ip == "50.0.0.5" else \
+                    rl(dom + ".remote_address", 10, O.SECOND)
+            d = O.Descriptor(entries)
+            if rng.random() < p_override:
+                ou, ol = rng.choice([O.SECOND, O.MINUTE, O.HOUR]), rng.randint(0, 20)
+                d.limit = O.Limit(ol, ou)
+                key = dom + "." + ".".join(k + ("_" + v if v else "") for k, v in entries)
+                lim = rl(key, ol, ou)
+            descs.append(d)
+            limits.append(lim)
+        calls.append((O.RateLimitRequest(dom, descs, rng.randint(1, 8)), limits, now))
+    return calls
+
+
 def reset_stats(calls):
     seen = set()
     for _, limits, _ in calls:

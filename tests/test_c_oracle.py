@@ -98,3 +98,34 @@ def test_c_oracle_matches_python_oracle(seed, local_cache, per_second, prefix):
         i += k
     for key, v in py_stats.items():
         assert totals.get(key, (0,) * 6) == v, key
+
+
+@pytest.mark.parametrize("ratio,local_cache,prefix", [(0.8, False, ""), (0.8, True, "prefix:"), (0.9, True, ""),
+                                                      (0.9, False, "prefix:")])
+def test_c4_stream_c_oracle_matches_python_oracle(ratio, local_cache, prefix):
+    """C4 (nested 4-entry descriptors, shadow, unlimited, overrides, rollover):
+    the two restatements agree, so the GPU C4 test has a consistent checker."""
+    calls = streams.c4_stream(11, n_calls=1500)
+    assert any(l is None for _, ls, _ in calls for l in ls)              # unlimited -> nil
+    assert any(l is not None and l.shadow_mode for _, ls, _ in calls for l in ls)
+    assert any(d.limit is not None for r, _, _ in calls for d in r.descriptors)  # overrides
+    assert {now % 60 for _, _, now in calls} >= {59, 0, 1}                # minute rollover
+    py_out, py_stats = streams.python_oracle_run(calls, ratio, local_cache, prefix, False)
+    co = c_oracle.COracle(ratio, local_cache, False)
+    interner = RuleInterner()
+    totals = {}
+    i = 0
+    for k in (1, 7, 300, 64, 500, 628):
+        chunk = calls[i:i + k]
+        pb, res = run_packed(co, chunk, prefix, interner)
+        got = unpack_statuses(chunk, pb, res)
+        exp = [[s.as_tuple() for s in o] for o in py_out[i:i + k]]
+        assert got == exp, "mismatch in calls %d..%d" % (i, i + k)
+        st = res["stats"].reshape(-1, abi.RL_NUM_STATS)
+        for r, key in enumerate(interner.keys):
+            totals[key] = tuple(a + int(b) for a, b in zip(totals.get(key, (0,) * 6), st[r]))
+        i += k
+    assert i == len(calls)
+    for key, v in py_stats.items():
+        assert totals.get(key, (0,) * 6) == v, key
+    co.close()

@@ -339,3 +339,110 @@ def test_gpu_long_stems_use_arena():
     py_out, _ = streams.python_oracle_run(calls, 0.8, True, "", False)
     outs, _ = _gpu_stream_run(calls, 0.8, True, "", False, [10] * 5)
     assert [[G.status_tuple(s) for s in o] for o in outs] == [[s.as_tuple() for s in o] for o in py_out]
+
+
+# --------------------------------------------------------------------------- pipelined async submission
+def _dev(a):
+    import torch
+    return {k: torch.from_numpy(np.ascontiguousarray(v).view(np.int32) if v.dtype == np.uint32 else
+                                np.ascontiguousarray(v)).cuda() for k, v in a.items()}
+
+
+def _dev_out(n, nr):
+    import torch
+    return {"code": torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda"),
+            "limit_remaining": torch.zeros(max(n, 1), dtype=torch.int32, device="cuda"),
+            "reset_s": torch.zeros(max(n, 1), dtype=torch.int32, device="cuda"),
+            "stats": torch.zeros(max(nr, 1) * abi.RL_NUM_STATS, dtype=torch.int64, device="cuda")}
+
+
+def _host(o, n, nr):
+    return {"code": o["code"][:n].cpu().numpy(),
+            "limit_remaining": o["limit_remaining"][:n].cpu().numpy().view(np.uint32),
+            "reset_s": o["reset_s"][:n].cpu().numpy().view(np.uint32),
+            "stats": o["stats"][:nr * abi.RL_NUM_STATS].cpu().numpy().view(np.uint64)}
+
+
+@pytest.mark.parametrize("lc", [False, True])
+def test_gpu_async_pipeline_matches_oracle(lc):
+    """rl_do_limit_async(stream=NULL) overlaps batch t's sort/segment stage with
+    batch t-1's table stage. Batch by batch the results must equal the
+    sequential oracle, also with a synchronous call submitted mid-pipeline."""
+    import torch
+    z = workloads.ZipfSampler(20_000, 1.1)
+    batches = list(workloads.c2_stream(n_tenants=20_000, requests_per_batch=30_000, batches=7, sampler=z))
+    co = c_oracle.COracle(0.8, lc)
+    want = [co.do_limit(a, n, nq, nr) for a, n, nq, nr in batches]
+    co.close()
+    be = Backend(0.8, lc, table_slots=1 << 18, max_batch=1 << 17, max_rules=8)
+    dev_in = [_dev(a) for a, *_ in batches]
+    torch.cuda.synchronize()
+    got = []
+    for i, (a, n, nq, nr) in enumerate(batches):
+        if i == 4:  # synchronous call right behind three queued async batches
+            got.append(be.do_limit_arrays(a, n, nq, nr))
+            continue
+        o = _dev_out(n, nr)
+        be.do_limit_device(dev_in[i], o, n, nq, nr)
+        got.append((o, n, nr))
+    be.synchronize()
+    for i, (g, w) in enumerate(zip(got, want)):
+        if isinstance(g, tuple):
+            g = _host(*g)
+        for k in ("code", "limit_remaining", "reset_s", "stats"):
+            assert np.array_equal(g[k], w[k]), "batch %d: %s differs" % (i, k)
+    be.close()
+
+
+def test_gpu_async_invalid_batch_does_not_touch_its_predecessor():
+    """A batch that fails validation in the pipeline is reported at
+    rl_synchronize; the batch queued before it is still answered exactly."""
+    import torch
+    a0, n, nq, nr = workloads.c1_batch(np.arange(5000), workloads.NOW0)
+    a1, *_ = workloads.c1_batch(np.arange(5000), workloads.NOW0 + 1)
+    bad = dict(a1)
+    bad["unit"] = a1["unit"].copy()
+    bad["unit"][7] = 9
+    co = c_oracle.COracle(0.8, False)
+    want = co.do_limit(a0, n, nq, nr)
+    co.close()
+    be = Backend(0.8, False, **SMALL)
+    d0, d1 = _dev(a0), _dev(bad)
+    torch.cuda.synchronize()
+    o0, o1 = _dev_out(n, nr), _dev_out(n, nr)
+    be.do_limit_device(d0, o0, n, nq, nr)
+    be.do_limit_device(d1, o1, n, nq, nr)
+    with pytest.raises(RedisError, match="RL_E_INVALID"):
+        be.synchronize()
+    g = _host(o0, n, nr)
+    for k in ("code", "limit_remaining", "reset_s", "stats"):
+        assert np.array_equal(g[k], want[k]), k
+    # the context stays usable and the failed batch left the table untouched
+    g2 = be.do_limit_arrays(a1, n, nq, nr)
+    co = c_oracle.COracle(0.8, False)
+    co.do_limit(a0, n, nq, nr)
+    w2 = co.do_limit(a1, n, nq, nr)
+    co.close()
+    for k in ("code", "limit_remaining", "reset_s", "stats"):
+        assert np.array_equal(g2[k], w2[k]), k
+    be.close()
+
+
+# --------------------------------------------------------------------------- C4 (BASELINE configs[4])
+@pytest.mark.parametrize("ratio,lc,prefix", [(0.8, False, ""), (0.8, True, "prefix:"), (0.9, True, ""),
+                                             (0.9, False, "prefix:")])
+def test_gpu_c4_nested_shadow_unlimited_rollover(ratio, lc, prefix):
+    calls = streams.c4_stream(11, n_calls=1500)
+    py_out, py_stats = streams.python_oracle_run(calls, ratio, lc, prefix, False)
+    rng = np.random.default_rng(5)
+    chunks, left = [], len(calls)
+    while left:
+        k = int(min(left, rng.integers(1, 300)))
+        chunks.append(k)
+        left -= k
+    outs, stats = _gpu_stream_run(calls, ratio, lc, prefix, False, chunks)
+    got = [[G.status_tuple(s) for s in o] for o in outs]
+    exp = [[s.as_tuple() for s in o] for o in py_out]
+    for i, (g, e) in enumerate(zip(got, exp)):
+        assert g == e, "call %d: gpu %s oracle %s" % (i, g, e)
+    assert stats == py_stats
