@@ -28,6 +28,8 @@ struct rl_ctx {
   hipStream_t stream = nullptr;   // serial work (== pipe[0])
   hipStream_t pipe[2] = {};       // one per scratch buffer
   hipEvent_t b_done[2] = {};      // stage B of the last batch on each buffer is done
+  hipStream_t side = nullptr;     // k_runs_general beside k_runs (stage B)
+  hipEvent_t side_go = nullptr, side_done = nullptr;
   uint32_t next = 0, last = 1;    // buffer of the next / of the latest batch
   // table
   Slot* slots = nullptr;
@@ -147,14 +149,14 @@ uint32_t enqueue(rl_ctx* c, const BatchDev& b, const OutDev& o, int restore, hip
     (void)hipStreamWaitEvent(a, c->b_done[k], 0);  // buffer k's previous batch is done
     launch_stage_a(b, c->s[k], a);
     (void)hipStreamWaitEvent(a, c->b_done[c->last], 0);  // table order
-    launch_stage_b(b, o, t, P, c->s[k], restore, a);
+    launch_stage_b(b, o, t, P, c->s[k], restore, a, c->side, c->side_go, c->side_done);
     (void)hipEventRecord(c->b_done[k], a);
   } else {
     if (!st) st = c->stream;
     (void)after_batches(c, st);
     hipEvent_t* ev = prof_events(c);
     launch_stage_a(b, c->s[k], st, ev);
-    launch_stage_b(b, o, t, P, c->s[k], restore, st, ev);
+    launch_stage_b(b, o, t, P, c->s[k], restore, st, c->side, c->side_go, c->side_done, ev);
     (void)hipEventRecord(c->b_done[k], st);
   }
   c->last = k;
@@ -219,7 +221,8 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
   for (int i = 0; i < 2; i++) ok = ok && dalloc(&s.keys[i], n) == hipSuccess && dalloc(&s.vals[i], n) == hipSuccess;
   ok = ok && dalloc(&s.hist, 256ull * std::max(ntiles, 1u)) == hipSuccess && dalloc(&s.hist_tot, 256) == hipSuccess;
   ok = ok && dalloc(&s.repid, n) == hipSuccess && dalloc(&s.defer, n) == hipSuccess &&
-       dalloc(&s.defer_n, 1) == hipSuccess;
+       dalloc(&s.defer_n, 1) == hipSuccess && dalloc(&s.defer2, n) == hipSuccess &&
+       dalloc(&s.defer2_n, 1) == hipSuccess;
   ok = ok && dalloc(&s.tile_f, nt) == hipSuccess && dalloc(&s.tile_s, nt) == hipSuccess &&
        dalloc(&s.tile_h, nt) == hipSuccess;
   ok = ok && dalloc(&s.hits_s, n) == hipSuccess && dalloc(&s.segsum, n) == hipSuccess &&
@@ -231,7 +234,7 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
 
 void free_buffer(Scratch& s) {
   void* bufs[] = {s.rec, s.rec_s, s.res, s.key, s.key_s, s.keys[0], s.keys[1], s.vals[0], s.vals[1], s.hist,
-                  s.hist_tot, s.repid, s.defer, s.defer_n, s.tile_f, s.tile_s, s.tile_h, s.hits_s, s.segsum, s.rid,
+                  s.hist_tot, s.repid, s.defer, s.defer_n, s.defer2, s.defer2_n, s.tile_f, s.tile_s, s.tile_h, s.hits_s, s.segsum, s.rid,
                   s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -304,7 +307,10 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   bool ok = hipStreamCreateWithFlags(&c->pipe[0], hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithFlags(&c->pipe[1], hipStreamNonBlocking) == hipSuccess;
   c->stream = c->pipe[0];
+  ok = ok && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess;
   for (int k = 0; k < 2; k++) ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&c->side_go, hipEventDisableTiming) == hipSuccess &&
+       hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming) == hipSuccess;
   ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess;
   ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess;
   for (int k = 0; k < 2; k++) ok = ok && alloc_buffer(c->s[k], n);
@@ -357,6 +363,9 @@ void rl_destroy(rl_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   for (int k = 0; k < 2; k++)
     if (c->pipe[k]) (void)hipStreamSynchronize(c->pipe[k]);
+  if (c->side) (void)hipStreamSynchronize(c->side);
+  if (c->side_go) (void)hipEventDestroy(c->side_go);
+  if (c->side_done) (void)hipEventDestroy(c->side_done);
   for (int i = 0; i <= RL_NUM_STAGES; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
   for (int k = 0; k < 2; k++) {
@@ -374,6 +383,7 @@ void rl_destroy(rl_ctx* c) {
   if (c->h_route) (void)hipHostFree(c->h_route);
   for (int k = 0; k < 2; k++)
     if (c->pipe[k]) (void)hipStreamDestroy(c->pipe[k]);
+  if (c->side) (void)hipStreamDestroy(c->side);
   delete c;
 }
 

@@ -14,11 +14,12 @@ constexpr uint32_t RS_TILE = 256 * RS_ITEMS;
 constexpr uint32_t SEG_ITEMS = 16;
 constexpr uint32_t SEG_TILE = 256 * SEG_ITEMS;
 constexpr uint32_t LONG_RUN = 32;        // runs at least this long take the parallel path
-constexpr uint32_t RUN_SLOW = 1, RUN_FAST = 2;
+constexpr uint32_t RUN_SLOW = 1, RUN_FAST = 2, RUN_MULTI = 4;
 constexpr uint32_t KEY_HEAD = 64;         // stem bytes carried inline (zero-padded) per descriptor
 constexpr uint32_t STAT_STRIPES = 64;     // global partial stats tables
 constexpr uint32_t STAT_LDS_RULES = 512;  // rules aggregated in LDS (== LDS_RULES)
-constexpr uint32_t RUNS_GENERAL_BLOCKS = 64;  // grid of k_runs_general (grid-stride over deferrals)
+constexpr uint32_t RUNS_GENERAL_BLOCKS = 64;      // k_runs_general grids (grid-stride over deferrals):
+constexpr uint32_t RUNS_GENERAL_LATE_BLOCKS = 8;  //   RUN_MULTI runs beside k_runs / k_runs' deferrals after it
 
 struct BatchDev {
   uint32_t n, n_req, n_rules, stem_cap;
@@ -115,8 +116,10 @@ struct Scratch {
   uint32_t* hist;      // 256 x ntiles, digit-major
   uint32_t* hist_tot;  // 256 digit totals
   uint8_t* repid;
-  uint32_t* defer;                // runs deferred to k_runs_general
+  uint32_t* defer;                // RUN_MULTI runs (k_run_check), for k_runs_general beside k_runs
   uint32_t* defer_n;
+  uint32_t* defer2;               // runs k_runs found to need the exact path, for k_runs_general after it
+  uint32_t* defer2_n;
   unsigned long long* stripes;    // STAT_STRIPES x STAT_LDS_RULES x RL_NUM_STATS
   // run segmentation (sorted order)
   uint32_t *tile_f, *tile_s, *tile_h;  // per SEG_TILE tile
@@ -143,14 +146,14 @@ struct Scratch {
 // batch's stage B; stage B (table probe, replay, decisions, stats, results)
 // must run in batch order.
 void launch_stage_a(const BatchDev& b, const Scratch& s, hipStream_t st, hipEvent_t* ev = nullptr);
+// Stage B launches the RUN_MULTI runs' exact replay on `side` (ordered by the
+// events go / side_done) so that it overlaps k_runs.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                    int restore, hipStream_t st, hipEvent_t* ev = nullptr);
-// Launch the whole DoLimit pipeline (restore = 1: table seeding records).
+                    int restore, hipStream_t st, hipStream_t side, hipEvent_t go, hipEvent_t side_done,
+                    hipEvent_t* ev = nullptr);
 // ev (optional, RL_NUM_STAGES + 1 events on stream st): recorded before
 // k_prepare, after it, after the sort, just before and just after k_runs, and
 // at the end (per-stage timing, rl_profile).
-void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                     int restore, hipStream_t st, hipEvent_t* ev = nullptr);
 // One stable 8-bit counting pass on key bits [0, 8) (s.hist / s.hist_tot hold
 // the per-digit counts afterwards).
 void launch_partition(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, uint32_t n,

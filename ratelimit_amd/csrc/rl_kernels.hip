@@ -1,19 +1,22 @@
 // rl_kernels.hip — gfx950 kernels of the fixed-window rate-limit backend.
 //
-// Pipeline for one batch (one HIP stream, inputs already in HBM):
+// Pipeline for one batch (inputs already in HBM); stage A (table-free):
 //   k_prepare     validate the packed batch; hash every stem (LDS-staged
 //                 bytes); pack each descriptor into a 32-B Rec
 //   radix sort    stable LSD sort of (hash[63:32], index): groups each stem's
 //                 descriptors together, in arrival (sequence) order
 //   k_gather      Recs into sorted order (one random 32-B read each)
 //   k_seg_*       run ids + in-run prefix sums of hits (3-phase segmented scan)
-//   k_run_check   long runs: every element shares stem, unit and window?
-//   k_runs        one lane per run: find-or-insert the (stem, unit) slot of
-//                 the HBM table; replay short runs in registers, set up long
-//                 uniform runs for k_fast_*, defer the rest to k_runs_general
+//   k_run_check   every element shares its run's stem and unit (else the run
+//                 goes to k_runs_general); long runs: and its window?
+//   ---- stage B (the table; batch order) ----
+//   k_runs        one lane per run: probe/insert the (stem, unit) slot of the
+//                 HBM table (one 128-B line per probe); replay short runs in
+//                 registers, set up long uniform runs for k_fast_*
+//   k_runs_general multi-stem / multi-unit runs, exact (beside k_runs)
 //   k_fast_*      long uniform runs decided in parallel (scan + first-over)
-//   k_stats_fold  striped per-block stats -> rl_result.stats
-//   k_unpack      packed results -> code / limit_remaining / reset_s
+//   k_finish      packed results -> code / limit_remaining / reset_s, and the
+//                 striped per-block stats -> rl_result.stats
 // plus k_sweep (epoch sweep = Redis EXPIRE), k_table_info, debug kernels.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -39,11 +42,12 @@ constexpr uint32_t HASH_LDS_BYTES = 16384;
 __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ rec, uint4* __restrict__ key,
                                                  uint32_t* __restrict__ keys,
                                                  uint32_t* __restrict__ vals, uint32_t* err,
-                                                 const int64_t* time_floor) {
+                                                 const int64_t* time_floor, uint32_t* defer_n) {
   __shared__ uint32_t lds[HASH_LDS_BYTES / 4 + 4];
   const uint32_t tid = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + tid;
   uint32_t bad = 0;
+  if (i == 0) *defer_n = 0;  // k_run_check's RUN_MULTI queue
 
   // ---- per-request clock checks: now in [0, NOW_MAX] and not before the last sweep
   if (i < (b.now_desc ? b.n : b.n_req)) {
@@ -457,12 +461,105 @@ __device__ int64_t find_slot(const TableDev& t, uint64_t hstem, uint64_t tag, co
   return -1;
 }
 
+// A slot's whole 128-B line, loaded in one round trip (8 x dwordx4): [0] tag |
+// key_len, unit, flags | ext_off, [1] cur, [2] prev, [3..7] stem bytes 0..79.
+// The run kernel probes with it: tag, stem and both window records arrive
+// together instead of three dependent loads. Plain loads are enough: within a
+// launch only CAS inserts change tags, and a lane only ever looks for its own
+// stem, which no other lane inserts.
+struct SlotImg {
+  uint4 v[8];
+  __device__ inline uint64_t tag() const { return ((uint64_t)v[0].y << 32) | v[0].x; }
+  __device__ inline uint32_t key_len() const { return v[0].z & 0xFFFFu; }
+  __device__ inline uint32_t flags() const { return v[0].z >> 24; }
+  __device__ inline uint32_t ext_off() const { return v[0].w; }
+  __device__ inline Win cur() const { return Win{v[1].x, v[1].y, v[1].z, v[1].w}; }
+  __device__ inline Win prev() const { return Win{v[2].x, v[2].y, v[2].z, v[2].w}; }
+};
+
+__device__ inline void load_img(const Slot* s, SlotImg& im) {
+  const uint4* p = reinterpret_cast<const uint4*>(s);
+#pragma unroll
+  for (int j = 0; j < 8; j++) im.v[j] = p[j];
+}
+
+__device__ inline uint32_t u4w(const uint4& a, uint32_t j) { return j == 0 ? a.x : j == 1 ? a.y : j == 2 ? a.z : a.w; }
+
+// Stem of `key` (head kh = its zero-padded first 64 bytes) == the slot's stem?
+__device__ inline bool img_key_equal(const SlotImg& im, const uint4* kh, const Key& key, const uint8_t* arena) {
+  if (im.key_len() != key.len) return false;
+  uint32_t d = 0;
+#pragma unroll
+  for (uint32_t v = 0; v < 4; v++) {
+    const uint4 a = im.v[3 + v], c = kh[v];
+    d |= (a.x ^ c.x) | (a.y ^ c.y) | (a.z ^ c.z) | (a.w ^ c.w);
+  }
+  const uint32_t len = key.len;
+  if (len > KEY_HEAD) {
+    const uint32_t il = len < INLINE_KEY ? len : INLINE_KEY, nw = il >> 2;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      const uint32_t k = KEY_HEAD / 4 + j;
+      const uint32_t x = u4w(im.v[7], j) ^ key.st.word(k);
+      if (k < nw) d |= x;
+      else if (k == nw && (il & 3)) d |= x & tail_mask(il);
+    }
+    if (len > INLINE_KEY) {
+      const uint32_t* ek = reinterpret_cast<const uint32_t*>(arena + (size_t)im.ext_off() * 16);
+      const uint32_t rest = len - INLINE_KEY, rw = rest >> 2;
+      for (uint32_t k = 0; k < rw; k++) d |= ek[k] ^ key.st.word(INLINE_KEY / 4 + k);
+      if (rest & 3) d |= (ek[rw] ^ key.st.word(INLINE_KEY / 4 + rw)) & tail_mask(rest);
+    }
+  }
+  return d == 0;
+}
+
+// find_slot with insert, returning the slot's image (a fresh slot's image for
+// an insert: empty windows, no flags).
+__device__ int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint64_t tag, const Key& key, const uint4* kh,
+                                 uint32_t unit, bool* inserted, SlotImg& im, uint32_t* err) {
+  uint64_t i = hstem >> t.shift;
+  int64_t tomb = -1;
+  *inserted = false;
+  for (uint32_t p = 0; p < t.max_probe; p++, i = (i + 1) & t.mask) {
+    load_img(&t.slots[i], im);
+    const uint64_t st = im.tag();
+    if (st == tag) {
+      if (img_key_equal(im, kh, key, t.arena)) return (int64_t)i;
+      continue;
+    }
+    if (st == TAG_TOMB) {
+      if (tomb < 0) tomb = (int64_t)i;
+      continue;
+    }
+    if (st != TAG_EMPTY) continue;
+    int64_t at = -1;
+    if (tomb >= 0 && atomicCAS((unsigned long long*)&t.slots[tomb].tag, (unsigned long long)TAG_TOMB,
+                               (unsigned long long)tag) == TAG_TOMB)
+      at = tomb;
+    else if (atomicCAS((unsigned long long*)&t.slots[i].tag, (unsigned long long)TAG_EMPTY,
+                       (unsigned long long)tag) == TAG_EMPTY)
+      at = (int64_t)i;
+    if (at >= 0) {
+      slot_init(t, &t.slots[at], key, unit, err);
+      im.v[0] = make_uint4((uint32_t)tag, (uint32_t)(tag >> 32), key.len | (unit << 16), 0u);
+      im.v[1] = make_uint4(WS_INVALID, 0u, 0u, 0u);
+      im.v[2] = im.v[1];
+      *inserted = true;
+      return at;
+    }
+    // another stem claimed this slot concurrently: keep probing
+  }
+  atomicOr(err, ERR_TABLE_FULL);
+  return -1;
+}
+
 // ===========================================================================
 // Per-rule stats. Each lane sums its run's deltas in registers (u64); at the
 // end the wave reduces lane sums rule by rule (butterfly shuffles) and one lane
 // adds them to the block's LDS table, which is flushed once per block into one
 // of STAT_STRIPES global partial tables (spreads same-address atomics), folded
-// into rl_result.stats by k_stats_fold. With more than LDS_RULES rules the
+// into rl_result.stats by k_finish. With more than LDS_RULES rules the
 // wave sums go straight to rl_result.stats.
 // ===========================================================================
 constexpr uint32_t LDS_RULES = STAT_LDS_RULES;
@@ -578,7 +675,7 @@ __device__ inline Elem load_elem(const Rec& r, uint32_t e, bool restore) {
   return x;
 }
 
-// One 8-B store per descriptor: remaining | reset << 32 | code << 56 (k_unpack).
+// One 8-B store per descriptor: remaining | reset << 32 | code << 56 (k_finish).
 __device__ __attribute__((always_inline)) inline void emit(unsigned long long* res, LaneStats& L, StatAcc& acc,
                                                            const Elem& x, const Decision& r) {
   const uint32_t reset = x.d - x.now % x.d;  // utils.CalculateReset
@@ -758,12 +855,12 @@ __device__ __attribute__((always_inline)) inline void replay_simple(const Rec* r
                                                                     unsigned long long* res, const TableDev& t,
                                                                     const Params& P, const uint8_t* repid,
                                                                     uint32_t p, uint32_t end, uint32_t k, int64_t s0,
-                                                                    LaneStats& L, StatAcc& acc, uint32_t* err,
-                                                                    bool restore) {
+                                                                    Win cur0, Win prev0, LaneStats& L, StatAcc& acc,
+                                                                    uint32_t* err, bool restore) {
   Slot* s = &t.slots[s0];
   SimpleState S;
-  S.cur = s->cur;
-  S.prev = s->prev;
+  S.cur = cur0;
+  S.prev = prev0;
   S.cur_req = 0xFFFFFFFFu;
   S.pend = false;
   for (uint32_t q = p; q < end; q++) {
@@ -977,33 +1074,40 @@ __global__ __launch_bounds__(256) void k_seg_apply(const uint32_t* __restrict__ 
   }
 }
 
-// Long runs only: every element must share the head's stem, unit and window
-// for the parallel path; otherwise the run is replayed serially.
+// Every element of a run must have the head's stem and unit; a run that does
+// not (two stems sharing the 32-bit hash prefix, or one stem under several
+// units) is flagged RUN_MULTI and queued once for k_runs_general, which runs
+// beside k_runs. Long runs must also share the head's window for the parallel
+// path (RUN_SLOW otherwise: replayed serially).
 __global__ __launch_bounds__(256) void k_run_check(BatchDev b, const Rec* __restrict__ rec_s,
                                                    const uint4* __restrict__ key_s,
                                                    const uint32_t* __restrict__ rid,
                                                    const uint32_t* __restrict__ run_start,
-                                                   uint32_t* __restrict__ run_flags, const uint32_t* err) {
+                                                   uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
+                                                   uint32_t* defer_n, const uint32_t* err) {
   if (*err) return;
   const uint32_t q = blockIdx.x * 256 + threadIdx.x;
   if (q >= b.n) return;
   const uint32_t r = rid[q];
   const uint32_t p = run_start[r];
-  if (q == p || run_start[r + 1] - p < LONG_RUN) return;
+  if (q == p) return;
   b.stem_total = b.off[b.n];
   const Rec x0 = rec_s[p], x = rec_s[q];
-  bool same = x.hlo == x0.hlo && (x.lu & 0xFFFFFFu) == (x0.lu & 0xFFFFFFu);  // hash, length, unit
-  if (same) {
+  const bool same = x.hlo == x0.hlo && (x.lu & 0xFFFFFFu) == (x0.lu & 0xFFFFFFu) &&  // hash, length, unit
+                    key_equal(key_at(b, key_s, rec_s, q), key_at(b, key_s, rec_s, p));
+  if (!same) {
+    if (!(atomicOr(&run_flags[r], RUN_MULTI) & RUN_MULTI)) defer[atomicAdd(defer_n, 1u)] = p;
+  } else if (run_start[r + 1] - p >= LONG_RUN) {
     const uint32_t d = div_of(rec_unit(x));
-    same = x0.now / d == x.now / d && key_equal(key_at(b, key_s, rec_s, q), key_at(b, key_s, rec_s, p));
+    if (x0.now / d != x.now / d) atomicOr(&run_flags[r], RUN_SLOW);
   }
-  if (!same) atomicOr(&run_flags[r], RUN_SLOW);
 }
 
-// ---- k_runs: one lane per run. Short runs of one stem and one unit whose slot
-// is not flagged multi-unit are replayed here in registers; long uniform runs
-// are set up for the parallel path (k_fast_*); anything else is deferred to
-// k_runs_general.
+// ---- k_runs: one lane per run of one stem and one unit (k_run_check). Short
+// runs whose slot is not flagged multi-unit are replayed here in registers;
+// long uniform runs are set up for the parallel path (k_fast_*); a stem that
+// turns out to live in the table under another unit too is queued for the
+// exact path (defer2, k_runs_general after this kernel).
 __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, const Rec* __restrict__ rec_s,
                                               const uint4* __restrict__ key_s,
                                               const uint32_t* __restrict__ skeys,
@@ -1031,71 +1135,73 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
   const uint32_t r = blockIdx.x * 256 + threadIdx.x;
   if (r < s_nr) {
     const uint32_t p = run_start[r], end = run_start[r + 1];
-    const bool long_run = !restore && end - p >= LONG_RUN && !(run_flags[r] & RUN_SLOW);
+    const uint32_t fl = run_flags[r];
     const Rec x0 = rec_s[p];
     const uint64_t h0 = ((uint64_t)skeys[p] << 32) | x0.hlo;
     const uint32_t u0 = rec_unit(x0);
     const Key k0 = key_at(b, key_s, rec_s, p);
-    bool ok = true;
-    if (!long_run) {  // long uniform runs were checked in parallel (k_run_check)
-      for (uint32_t q = p + 1; q < end && ok; q++) {
-        const Rec x = rec_s[q];
-        ok = x.hlo == x0.hlo && (x.lu & 0xFFFFFFu) == (x0.lu & 0xFFFFFFu) && key_equal(key_at(b, key_s, rec_s, q), k0);
-      }
-    }
-    int64_t s0 = -1;
-    if (RL_ABL & 1) {
-      s0 = (int64_t)(h0 >> t.shift);
-    } else if (ok) {
-      bool ins;
-      s0 = find_slot(t, h0, slot_tag(h0, u0), k0, u0, true, &ins, err);
-      if (s0 < 0) {
-        ok = false;
-      } else if (t.slots[s0].flags & SLOT_EXACT) {
-        ok = false;
-      } else if (ins) {  // new (stem, unit): the stem must not exist under another unit
-        for (uint32_t u = 1; u <= 4; u++) {
-          bool dummy;
-          const int64_t so = u == u0 ? -1 : find_slot(t, h0, slot_tag(h0, u), k0, u, false, &dummy, err);
-          if (so >= 0) {  // multi-unit stem from now on: flag both before deferring
-            t.slots[so].flags |= SLOT_EXACT;
-            ok = false;
+    uint4 kh[4];
+#pragma unroll
+    for (uint32_t v = 0; v < 4; v++) kh[v] = k0.k[v];
+    if (!(fl & RUN_MULTI)) {  // RUN_MULTI runs belong to k_runs_general
+      const bool long_run = !restore && end - p >= LONG_RUN && !(fl & RUN_SLOW);
+      bool ok = true;
+      int64_t s0 = -1;
+      SlotImg im;
+      if (RL_ABL & 1) {
+        s0 = (int64_t)(h0 >> t.shift);
+        load_img(&t.slots[s0], im);
+      } else {
+        bool ins;
+        s0 = find_slot_img(t, h0, slot_tag(h0, u0), k0, kh, u0, &ins, im, err);
+        if (s0 < 0) {
+          ok = false;
+        } else if (im.flags() & SLOT_EXACT) {
+          ok = false;
+        } else if (ins) {  // new (stem, unit): the stem must not exist under another unit
+          for (uint32_t u = 1; u <= 4; u++) {
+            bool dummy;
+            const int64_t so = u == u0 ? -1 : find_slot(t, h0, slot_tag(h0, u), k0, u, false, &dummy, err);
+            if (so >= 0) {  // multi-unit stem from now on: flag both before deferring
+              t.slots[so].flags |= SLOT_EXACT;
+              ok = false;
+            }
           }
+          if (!ok) t.slots[s0].flags |= SLOT_EXACT;
         }
-        if (!ok) t.slots[s0].flags |= SLOT_EXACT;
       }
-    }
-    if (ok && long_run) {
-      // Parallel path: pick the window record once; k_fast_* decide every element.
-      Slot* s = &t.slots[s0];
-      Win cur = s->cur, prev = s->prev;
-      const Elem e0 = load_elem(x0, svals[p], false);
-      const int which = window_pick(cur, prev, e0.w, 0, true);
-      if (which < 0) {
-        if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
-      } else {
-        const Win R = which ? prev : cur;
-        // A record of window w was written inside w: its EXPIRE and local-cache
-        // TTL both end at or after w + div, so they hold for the whole run.
-        const uint32_t c0 = e0.now <= R.expire ? R.count : 0u;
-        const uint32_t F = (P.lc_en && e0.now < R.lc) ? 1u : 0u;
-        s->cur = cur;
-        s->prev = prev;
-        run_state[r] = make_uint4((uint32_t)s0, c0, R.lc, F | ((uint32_t)which << 1));
-        run_f[r] = 0xFFFFFFFFu;
-        run_flags[r] |= RUN_FAST;
+      if (ok && long_run) {
+        // Parallel path: pick the window record once; k_fast_* decide every element.
+        Slot* s = &t.slots[s0];
+        Win cur = im.cur(), prev = im.prev();
+        const Elem e0 = load_elem(x0, svals[p], false);
+        const int which = window_pick(cur, prev, e0.w, 0, true);
+        if (which < 0) {
+          if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
+        } else {
+          const Win R = which ? prev : cur;
+          // A record of window w was written inside w: its EXPIRE and local-cache
+          // TTL both end at or after w + div, so they hold for the whole run.
+          const uint32_t c0 = e0.now <= R.expire ? R.count : 0u;
+          const uint32_t F = (P.lc_en && e0.now < R.lc) ? 1u : 0u;
+          s->cur = cur;
+          s->prev = prev;
+          run_state[r] = make_uint4((uint32_t)s0, c0, R.lc, F | ((uint32_t)which << 1));
+          run_f[r] = 0xFFFFFFFFu;
+          run_flags[r] = fl | RUN_FAST;
+        }
+      } else if (ok) {
+        if (RL_ABL & 2) {
+          Slot* sl = &t.slots[s0];
+          Win c = im.cur();
+          c.count += end - p;
+          sl->cur = c;
+        } else {
+          replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, im.cur(), im.prev(), L, acc, err, restore);
+        }
+      } else if (!(s0 < 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_TABLE_FULL))) {
+        defer[atomicAdd(defer_n, 1u)] = p;
       }
-    } else if (ok) {
-      if (RL_ABL & 2) {
-        Slot* sl = &t.slots[s0];
-        Win c = sl->cur;
-        c.count += end - p;
-        sl->cur = c;
-      } else {
-        replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, L, acc, err, restore);
-      }
-    } else if (!(s0 < 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_TABLE_FULL))) {
-      defer[atomicAdd(defer_n, 1u)] = p;
     }
   }
   if (!(RL_ABL & 4)) {
@@ -1267,7 +1373,8 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
         }
       }
       if (simple) {
-        replay_simple(rec_s, svals, res, t, P, repid, p, end, k, s0, L, acc, err, restore);
+        replay_simple(rec_s, svals, res, t, P, repid, p, end, k, s0, t.slots[s0].cur, t.slots[s0].prev, L, acc, err,
+                      restore);
       } else {
         GeneralState G;
         G.present = 0;
@@ -1307,7 +1414,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
 }
 
 // First kernel of the table stage: merge this batch's validation errors into
-// the sticky table-stage word, clear the deferral counter and this call's
+// the sticky table-stage word, clear k_runs' deferral counter and this call's
 // output stats (n_rules x RL_NUM_STATS).
 __global__ __launch_bounds__(256) void k_b_begin(const uint32_t* __restrict__ erra, uint32_t* errb,
                                                  uint32_t* __restrict__ defer_n,
@@ -1321,26 +1428,25 @@ __global__ __launch_bounds__(256) void k_b_begin(const uint32_t* __restrict__ er
   for (uint32_t j = i; j < m; j += gridDim.x * 256) stats[j] = 0;
 }
 
-// Fold the striped per-block partial stats into rl_result.stats and clear them.
-__global__ __launch_bounds__(256) void k_stats_fold(unsigned long long* __restrict__ stripes, uint32_t n_rules,
-                                                    unsigned long long* __restrict__ stats, const uint32_t* err) {
-  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-  const uint32_t m = n_rules * RL_NUM_STATS;
-  if (j >= m) return;
-  unsigned long long s = 0;
-  for (uint32_t k = 0; k < STAT_STRIPES; k++) {
-    s += stripes[(size_t)k * m + j];
-    stripes[(size_t)k * m + j] = 0;
-  }
-  if (*err == 0) stats[j] += s;
-}
-
-// Packed results -> the three rl_result arrays (arrival order, coalesced).
-__global__ __launch_bounds__(256) void k_unpack(const unsigned long long* __restrict__ res, uint32_t n, OutDev o,
+// Last kernel of a batch: packed results -> the three rl_result arrays
+// (arrival order, coalesced), and the first n_fold x RL_NUM_STATS threads fold
+// the striped per-block stats into rl_result.stats (clearing the stripes even
+// when the batch failed, so nothing leaks into the next one).
+__global__ __launch_bounds__(256) void k_finish(const unsigned long long* __restrict__ res, uint32_t n, OutDev o,
+                                                unsigned long long* __restrict__ stripes, uint32_t n_fold,
                                                 const uint32_t* err) {
-  if (*err) return;
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
+  const bool ok = *err == 0;
+  const uint32_t m = n_fold * RL_NUM_STATS;
+  if (i < m) {
+    unsigned long long s = 0;
+    for (uint32_t k = 0; k < STAT_STRIPES; k++) {
+      s += stripes[(size_t)k * m + i];
+      stripes[(size_t)k * m + i] = 0;
+    }
+    if (ok) o.stats[i] += s;
+  }
+  if (!ok || i >= n) return;
   const unsigned long long v = res[i];
   o.code[i] = (uint8_t)(v >> 56);
   o.rem[i] = (uint32_t)v;
@@ -1436,7 +1542,7 @@ static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b -
 void launch_stage_a(const BatchDev& b, const Scratch& s, hipStream_t st, hipEvent_t* ev) {
   const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
   if (ev) (void)hipEventRecord(ev[0], st);
-  if (g0) k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.key, s.keys[0], s.vals[0], s.err, s.time_floor);
+  if (g0) k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.key, s.keys[0], s.vals[0], s.err, s.time_floor, s.defer_n);
   if (ev) (void)hipEventRecord(ev[1], st);
   if (b.n) {
     const uint32_t ntiles = cdiv(b.n, RS_TILE);
@@ -1456,7 +1562,8 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, hipStream_t st, hipEven
     k_seg_tiles<<<1, 1024, 0, st>>>(s.tile_f, s.tile_s, s.tile_h, nt, s.err);
     k_seg_apply<<<nt, 256, 0, st>>>(s.keys[0], s.hits_s, b.n, s.tile_f, s.tile_s, s.tile_h, s.segsum, s.rid,
                                     s.run_start, s.run_flags, s.num_runs, s.err);
-    k_run_check<<<g, 256, 0, st>>>(b, s.rec_s, s.key_s, s.rid, s.run_start, s.run_flags, s.err);
+    k_run_check<<<g, 256, 0, st>>>(b, s.rec_s, s.key_s, s.rid, s.run_start, s.run_flags, s.defer, s.defer_n,
+                                   s.err);
   }
 }
 
@@ -1464,40 +1571,45 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, hipStream_t st, hipEven
 // sticky table-stage word s.errb; k_b_begin folds this batch's validation
 // result into it first.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                    int restore, hipStream_t st, hipEvent_t* ev) {
+                    int restore, hipStream_t st, hipStream_t side, hipEvent_t go, hipEvent_t side_done,
+                    hipEvent_t* ev) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
-  k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, s.defer_n, o.stats, m);
-  if (ev) (void)hipEventRecord(ev[3], st);
+  k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, s.defer2_n, o.stats, m);
   if (b.n) {
     const uint32_t g = cdiv(b.n, 256);
     const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
-    k_runs<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.key_s, s.keys[0], s.vals[0], s.res, s.run_start, s.run_flags,
-                                s.run_state, s.run_f, s.num_runs, s.defer, s.defer_n, o.stats, s.stripes, s.errb,
-                                restore);
-    if (ev) (void)hipEventRecord(ev[4], st);
-    k_runs_general<<<g < RUNS_GENERAL_BLOCKS ? g : RUNS_GENERAL_BLOCKS, 256, lds, st>>>(
+    // RUN_MULTI runs (known since k_run_check) on the side stream, beside k_runs
+    (void)hipEventRecord(go, st);
+    (void)hipStreamWaitEvent(side, go, 0);
+    k_runs_general<<<g < RUNS_GENERAL_BLOCKS ? g : RUNS_GENERAL_BLOCKS, 256, lds, side>>>(
         b, t, P, s.rec_s, s.key_s, s.keys[0], s.vals[0], s.res, s.defer, s.defer_n, s.repid, o.stats, s.stripes,
         s.errb, restore);
+    (void)hipEventRecord(side_done, side);
+    if (ev) (void)hipEventRecord(ev[3], st);
+    k_runs<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.key_s, s.keys[0], s.vals[0], s.res, s.run_start, s.run_flags,
+                                s.run_state, s.run_f, s.num_runs, s.defer2, s.defer2_n, o.stats, s.stripes, s.errb,
+                                restore);
+    if (ev) (void)hipEventRecord(ev[4], st);
+    // stems k_runs found under several units in the table (rare)
+    k_runs_general<<<RUNS_GENERAL_LATE_BLOCKS, 256, lds, st>>>(b, t, P, s.rec_s, s.key_s, s.keys[0], s.vals[0],
+                                                                s.res, s.defer2, s.defer2_n, s.repid, o.stats,
+                                                                s.stripes, s.errb, restore);
+    (void)hipStreamWaitEvent(st, side_done, 0);
     if (!restore) {
       if (P.lc_en)
         k_fast_over<<<g, 256, 0, st>>>(b.n, s.rec_s, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
       k_fast_emit<<<g, 256, lds, st>>>(b.n, b.n_rules, t, P, s.rec_s, s.vals[0], s.res, s.segsum, s.rid,
                                        s.run_start, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb);
-      if (b.n_rules <= LDS_RULES && b.n_rules)
-        k_stats_fold<<<cdiv(b.n_rules * RL_NUM_STATS, 256), 256, 0, st>>>(s.stripes, b.n_rules, o.stats, s.errb);
-      k_unpack<<<g, 256, 0, st>>>(s.res, b.n, o, s.errb);
+      const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;
+      const uint32_t gf = cdiv(nf * RL_NUM_STATS > b.n ? nf * RL_NUM_STATS : b.n, 256);
+      k_finish<<<gf, 256, 0, st>>>(s.res, b.n, o, s.stripes, nf, s.errb);
     }
   } else if (ev) {
+    (void)hipEventRecord(ev[3], st);
     (void)hipEventRecord(ev[4], st);
   }
   if (ev) (void)hipEventRecord(ev[5], st);
-}
-
-void launch_do_limit(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                     int restore, hipStream_t st, hipEvent_t* ev) {
-  launch_stage_a(b, s, st, ev);
-  launch_stage_b(b, o, t, P, s, restore, st, ev);
 }
 
 void launch_partition(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, uint32_t n,
