@@ -31,6 +31,7 @@ struct rl_ctx {
   hipStream_t side = nullptr;     // k_runs_general beside k_runs (stage B)
   hipEvent_t side_go = nullptr, side_done = nullptr;
   uint32_t next = 0, last = 1;    // buffer of the next / of the latest batch
+  uint32_t epoch = 0;             // batches submitted (sort look-back tags)
   // table
   Slot* slots = nullptr;
   uint64_t nslots = 0;
@@ -142,12 +143,22 @@ Params params(rl_ctx* c);
 uint32_t enqueue(rl_ctx* c, const BatchDev& b, const OutDev& o, int restore, hipStream_t st, bool pipelined) {
   const uint32_t k = c->next;
   c->next ^= 1u;
+  c->epoch = (c->epoch + 1) & 0x0FFFFFFFu;
+  if (!c->epoch) {  // after 2^28 batches: clear the look-back granules once, so no old tag can alias
+    (void)hipDeviceSynchronize();
+    for (int j = 0; j < 2; j++)
+    {
+      (void)hipMemset(c->s[j].os_status, 0, 256ull * ((c->cfg.max_batch + RS_TILE - 1) / RS_TILE) * 8);
+      (void)hipMemset(c->s[j].seg_status, 0, 16ull * ((c->cfg.max_batch + SEG_TILE - 1) / SEG_TILE + 1));
+    }
+    c->epoch = 1;
+  }
   const TableDev t = table_view(c);
   const Params P = params(c);
   if (pipelined && !c->prof) {
     hipStream_t a = c->pipe[k];
     (void)hipStreamWaitEvent(a, c->b_done[k], 0);  // buffer k's previous batch is done
-    launch_stage_a(b, c->s[k], a);
+    launch_stage_a(b, c->s[k], c->epoch, a);
     (void)hipStreamWaitEvent(a, c->b_done[c->last], 0);  // table order
     launch_stage_b(b, o, t, P, c->s[k], restore, a, c->side, c->side_go, c->side_done);
     (void)hipEventRecord(c->b_done[k], a);
@@ -155,7 +166,7 @@ uint32_t enqueue(rl_ctx* c, const BatchDev& b, const OutDev& o, int restore, hip
     if (!st) st = c->stream;
     (void)after_batches(c, st);
     hipEvent_t* ev = prof_events(c);
-    launch_stage_a(b, c->s[k], st, ev);
+    launch_stage_a(b, c->s[k], c->epoch, st, ev);
     launch_stage_b(b, o, t, P, c->s[k], restore, st, c->side, c->side_go, c->side_done, ev);
     (void)hipEventRecord(c->b_done[k], st);
   }
@@ -216,7 +227,10 @@ Params params(rl_ctx* c) {
 bool alloc_buffer(Scratch& s, uint32_t n) {
   const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
   const size_t nt = (n + SEG_TILE - 1) / SEG_TILE + 1;
-  bool ok = dalloc(&s.key, 4ull * n) == hipSuccess && dalloc(&s.key_s, 4ull * n) == hipSuccess;
+  bool ok = dalloc(&s.seg_status, 2 * nt) == hipSuccess && hipMemset(s.seg_status, 0, 16 * nt) == hipSuccess;
+  ok = ok && dalloc(&s.os_ghist, 4 * 256) == hipSuccess && dalloc(&s.os_ctr, 8) == hipSuccess &&
+       dalloc(&s.os_status, 256ull * std::max(ntiles, 1u)) == hipSuccess &&
+       hipMemset(s.os_status, 0, 256ull * std::max(ntiles, 1u) * 8) == hipSuccess;
   ok = ok && dalloc(&s.rec, n) == hipSuccess && dalloc(&s.rec_s, n) == hipSuccess && dalloc(&s.res, n) == hipSuccess;
   for (int i = 0; i < 2; i++) ok = ok && dalloc(&s.keys[i], n) == hipSuccess && dalloc(&s.vals[i], n) == hipSuccess;
   ok = ok && dalloc(&s.hist, 256ull * std::max(ntiles, 1u)) == hipSuccess && dalloc(&s.hist_tot, 256) == hipSuccess;
@@ -233,7 +247,7 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
 }
 
 void free_buffer(Scratch& s) {
-  void* bufs[] = {s.rec, s.rec_s, s.res, s.key, s.key_s, s.keys[0], s.keys[1], s.vals[0], s.vals[1], s.hist,
+  void* bufs[] = {s.rec, s.rec_s, s.res, s.seg_status, s.os_ghist, s.os_ctr, s.os_status, s.keys[0], s.keys[1], s.vals[0], s.vals[1], s.hist,
                   s.hist_tot, s.repid, s.defer, s.defer_n, s.defer2, s.defer2_n, s.tile_f, s.tile_s, s.tile_h, s.hits_s, s.segsum, s.rid,
                   s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs};
   for (void* p : bufs)

@@ -108,13 +108,16 @@ struct Params {
 struct Scratch {
   Rec* rec;                  // [n] arrival order
   Rec* rec_s;                // [n] sorted order
-  uint4* key;                // [n][4] 64-B stem heads, arrival order
-  uint4* key_s;              // [n][4] sorted order
   unsigned long long* res;   // [n] packed result per descriptor (arrival order)
   uint32_t* keys[2];
   uint32_t* vals[2];
-  uint32_t* hist;      // 256 x ntiles, digit-major
+  uint32_t* hist;      // 256 x ntiles, digit-major (routing partition)
   uint32_t* hist_tot;  // 256 digit totals
+  // onesweep sort: digit totals of the 4 passes, tile tickets, look-back granules
+  uint32_t* os_ghist;               // [4 * 256]
+  uint32_t* os_ctr;                 // [5] tile tickets: sort passes 0..3, k_segment
+  unsigned long long* seg_status;   // [2 * seg tiles] k_segment look-back granules
+  unsigned long long* os_status;    // [ntiles * 256] {count, tag | flag}
   uint8_t* repid;
   uint32_t* defer;                // RUN_MULTI runs (k_run_check), for k_runs_general beside k_runs
   uint32_t* defer_n;
@@ -145,7 +148,9 @@ struct Scratch {
 // only the batch and this buffer's scratch, so it may overlap the previous
 // batch's stage B; stage B (table probe, replay, decisions, stats, results)
 // must run in batch order.
-void launch_stage_a(const BatchDev& b, const Scratch& s, hipStream_t st, hipEvent_t* ev = nullptr);
+// `epoch` (1..2^28-1, distinct for consecutive batches on one buffer) tags the
+// sort's look-back granules so they never need clearing.
+void launch_stage_a(const BatchDev& b, const Scratch& s, uint32_t epoch, hipStream_t st, hipEvent_t* ev = nullptr);
 // Stage B launches the RUN_MULTI runs' exact replay on `side` (ordered by the
 // events go / side_done) so that it overlaps k_runs.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,

@@ -39,15 +39,20 @@ namespace rl {
 // ===========================================================================
 constexpr uint32_t HASH_LDS_BYTES = 16384;
 
-__global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ rec, uint4* __restrict__ key,
-                                                 uint32_t* __restrict__ keys,
+__global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ rec, uint32_t* __restrict__ keys,
                                                  uint32_t* __restrict__ vals, uint32_t* err,
-                                                 const int64_t* time_floor, uint32_t* defer_n) {
+                                                 const int64_t* time_floor, uint32_t* defer_n,
+                                                 uint32_t* __restrict__ os_ghist, uint32_t* __restrict__ os_ctr) {
   __shared__ uint32_t lds[HASH_LDS_BYTES / 4 + 4];
   const uint32_t tid = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + tid;
   uint32_t bad = 0;
-  if (i == 0) *defer_n = 0;  // k_run_check's RUN_MULTI queue
+  if (blockIdx.x == 0) {  // per-batch counters: RUN_MULTI queue, sort digit totals and tile tickets
+    if (tid == 0) *defer_n = 0;
+    if (tid < 5) os_ctr[tid] = 0;  // [0..3] sort passes, [4] k_segment
+#pragma unroll
+    for (uint32_t p = 0; p < 4; p++) os_ghist[p * 256 + tid] = 0;
+  }
 
   // ---- per-request clock checks: now in [0, NOW_MAX] and not before the last sweep
   if (i < (b.now_desc ? b.n : b.n_req)) {
@@ -100,30 +105,6 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   }
   keys[i] = (uint32_t)(h >> 32);
   vals[i] = i;
-  {  // zero-padded 64-B head of the stem: later compares read it as 4 x uint4
-    uint64_t w[8];
-    if (use_lds) {
-      const DwordReader rd{lds, HASH_LDS_BYTES / 4 + 4};
-#pragma unroll
-      for (uint32_t k = 0; k < 8; k++) w[k] = rd(s0 - lo + lead + 8 * k);
-    } else {
-      const uint32_t nw = range_ok ? ((total + 3u) >> 2) - (s0 >> 2) : 0u;
-      const DwordReader rd{words + (s0 >> 2), nw};
-#pragma unroll
-      for (uint32_t k = 0; k < 8; k++) w[k] = rd((s0 & 3u) + 8 * k);
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < 8; k++) {
-      const uint32_t c0 = 8 * k;
-      if (c0 >= len) w[k] = 0;
-      else if (c0 + 8 > len) w[k] &= (1ull << ((len - c0) * 8)) - 1;
-    }
-    uint4* dst = key + 4ull * i;
-#pragma unroll
-    for (uint32_t v = 0; v < 4; v++)
-      dst[v] = make_uint4((uint32_t)w[2 * v], (uint32_t)(w[2 * v] >> 32), (uint32_t)w[2 * v + 1],
-                          (uint32_t)(w[2 * v + 1] >> 32));
-  }
   Rec r;
   r.hlo = (uint32_t)h;
   r.off = s0;
@@ -264,25 +245,179 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t* __restrict__
   }
 }
 
-// Records into sorted order.
-__global__ __launch_bounds__(256) void k_gather(const Rec* __restrict__ rec, const uint4* __restrict__ key,
-                                                const uint32_t* __restrict__ svals, uint32_t n, Rec* __restrict__ rec_s,
-                                                uint4* __restrict__ key_s, uint32_t* __restrict__ hits_s,
-                                                const uint32_t* err) {
+// ===========================================================================
+// Onesweep LSD radix sort of (u32 key, u32 value), 8-bit digits: one kernel
+// reads the keys once for all four digit histograms, then one kernel per pass.
+// A pass block takes the next tile ticket (so every earlier tile belongs to a
+// block that is already running), ranks its RS_TILE elements in LDS with the
+// wave ballot multisplit, publishes its per-digit counts and learns the counts
+// of all earlier tiles by decoupled look-back over 8-byte {count, tag} granules
+// (one agent-scope store / load each: untorn, no separate flag). The tag holds
+// the batch epoch and pass, so granules are never cleared.
+// ===========================================================================
+constexpr uint32_t OS_AGG = 1u, OS_INC = 2u;
+
+__host__ __device__ inline uint32_t os_tag(uint32_t epoch, uint32_t pass) { return (epoch << 4) | (pass << 2); }
+
+__global__ __launch_bounds__(256) void k_os_hist(const uint32_t* __restrict__ keys, uint32_t n,
+                                                 uint32_t* __restrict__ ghist, const uint32_t* err) {
+  __shared__ uint32_t h[4][256];
   if (*err) return;
-  const uint32_t q = blockIdx.x * 256 + threadIdx.x;
-  if (q >= n) return;
-  const uint32_t e = svals[q];
-  const Rec r = rec[e];
-  rec_s[q] = r;
-  hits_s[q] = r.hits;
-  const uint4* src = key + 4ull * e;
-  uint4* dst = key_s + 4ull * q;
-  const uint4 a = src[0], b1 = src[1], c = src[2], d = src[3];
-  dst[0] = a;
-  dst[1] = b1;
-  dst[2] = c;
-  dst[3] = d;
+  const uint32_t tid = threadIdx.x;
+#pragma unroll
+  for (uint32_t p = 0; p < 4; p++) h[p][tid] = 0;
+  __syncthreads();
+  for (uint32_t j = blockIdx.x * 256 + tid; j < n; j += gridDim.x * 256) {
+    const uint32_t k = keys[j];
+    atomicAdd(&h[0][k & 255u], 1u);
+    atomicAdd(&h[1][(k >> 8) & 255u], 1u);
+    atomicAdd(&h[2][(k >> 16) & 255u], 1u);
+    atomicAdd(&h[3][k >> 24], 1u);
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t p = 0; p < 4; p++) {
+    const uint32_t v = h[p][tid];
+    if (v) atomicAdd(&ghist[p * 256 + tid], v);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_os_pass(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                 uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, uint32_t n,
+                                                 uint32_t pass, const uint32_t* __restrict__ ghist,
+                                                 uint32_t* __restrict__ ctr, unsigned long long* status, uint32_t tag,
+                                                 const uint32_t* err) {
+  __shared__ uint32_t wcnt[4][256];
+  __shared__ uint32_t dbase[256];
+  __shared__ uint32_t gsum[4];
+  __shared__ uint32_t s_tile;
+  if (*err) return;  // the same for every block: no tile is left half-published
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_tile = atomicAdd(&ctr[pass], 1u);
+  wcnt[0][tid] = 0; wcnt[1][tid] = 0; wcnt[2][tid] = 0; wcnt[3][tid] = 0;
+  __syncthreads();
+  const uint32_t tile = s_tile, shift = 8 * pass;
+  const uint64_t lt_mask = (1ull << lane) - 1;
+  const uint32_t wbase = tile * RS_TILE + wave * 64 * RS_ITEMS;
+  uint32_t kk[RS_ITEMS], vv[RS_ITEMS], pos[RS_ITEMS];
+#pragma unroll
+  for (uint32_t i = 0; i < RS_ITEMS; i++) {
+    const uint32_t j = wbase + i * 64 + lane;
+    const bool valid = j < n;
+    kk[i] = valid ? kin[j] : 0xFFFFFFFFu;
+    vv[i] = valid ? vin[j] : 0u;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < RS_ITEMS; i++) {
+    const bool valid = wbase + i * 64 + lane < n;
+    const uint32_t d = (kk[i] >> shift) & 255u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (uint32_t bit = 0; bit < 8; bit++) {
+      const bool sb = (d >> bit) & 1u;
+      const uint64_t bal = __ballot(sb);
+      peers &= sb ? bal : ~bal;
+    }
+    const uint32_t rank = __popcll(peers & lt_mask);
+    const uint32_t leader = valid ? (uint32_t)(__ffsll((unsigned long long)peers) - 1) : lane;
+    uint32_t old = 0;
+    if (valid && rank == 0) {
+      old = wcnt[wave][d];
+      wcnt[wave][d] = old + __popcll(peers);
+    }
+    old = __shfl(old, leader);
+    pos[i] = old + rank;
+  }
+  __syncthreads();
+  // digit tid: this tile's count and the per-wave exclusive offsets
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < 4; w++) {
+    const uint32_t t = wcnt[w][tid];
+    wcnt[w][tid] = c;
+    c += t;
+  }
+  unsigned long long* mine = status + (size_t)tile * 256 + tid;
+  __hip_atomic_store(mine, (unsigned long long)c | ((unsigned long long)(tag | (tile ? OS_AGG : OS_INC)) << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // global exclusive base of digit tid: wave scans of the pass's digit totals
+  const uint32_t g = ghist[pass * 256 + tid];
+  uint32_t inc = g;
+#pragma unroll
+  for (uint32_t off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += y;
+  }
+  if (lane == 63) gsum[wave] = inc;
+  // decoupled look-back: add earlier tiles' counts until an inclusive prefix
+  uint32_t excl = 0;
+  if (tile) {
+    uint32_t j = tile - 1;
+    for (;;) {
+      const unsigned long long v =
+          __hip_atomic_load(status + (size_t)j * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t tg = (uint32_t)(v >> 32);
+      if ((tg & ~3u) != tag) {  // not yet published for this pass
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      excl += (uint32_t)v;
+      if (tg & OS_INC) break;
+      --j;  // tile 0 publishes an inclusive count, so j stays >= 0
+    }
+    __hip_atomic_store(mine, (unsigned long long)(excl + c) | ((unsigned long long)(tag | OS_INC) << 32),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();  // gsum
+  uint32_t wpre = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < 4; w++) wpre += w < wave ? gsum[w] : 0u;
+  dbase[tid] = wpre + inc - g + excl;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t i = 0; i < RS_ITEMS; i++) {
+    if (wbase + i * 64 + lane < n) {
+      const uint32_t d = (kk[i] >> shift) & 255u;
+      const uint32_t p = dbase[d] + wcnt[wave][d] + pos[i];
+      kout[p] = kk[i];
+      vout[p] = vv[i];
+    }
+  }
+}
+
+// The zero-padded first KEY_HEAD bytes of the stem at byte `off` of the packed
+// stems, as 4 x uint4: five aligned 16-B loads, then dword selects and funnel
+// shifts. Only chunks holding a byte of the head are loaded, so no load leaves
+// the 16-B blocks (hence the pages) the stem occupies.
+__device__ inline void load_head(const uint8_t* stem, uint32_t off, uint32_t len, uint4 out[4]) {
+  const uint32_t hl = len < KEY_HEAD ? len : KEY_HEAD;
+  const uint32_t mis = (uint32_t)((uintptr_t)stem & 15u);
+  const uint4* c16 = reinterpret_cast<const uint4*>(stem - mis);
+  const uint32_t a = off + mis;
+  const uint32_t c0 = a >> 4, last = (a + (hl ? hl : 1u) - 1u) >> 4;
+  uint32_t w[20];
+#pragma unroll
+  for (uint32_t j = 0; j < 5; j++) {
+    const uint4 v = c0 + j <= last ? c16[c0 + j] : make_uint4(0u, 0u, 0u, 0u);
+    w[4 * j] = v.x;
+    w[4 * j + 1] = v.y;
+    w[4 * j + 2] = v.z;
+    w[4 * j + 3] = v.w;
+  }
+  const uint32_t q = (a >> 2) & 3u, sb = a & 3u;
+  uint32_t x[17];
+#pragma unroll
+  for (uint32_t k = 0; k < 17; k++) x[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
+  uint32_t o[16];
+#pragma unroll
+  for (uint32_t k = 0; k < 16; k++) {
+    uint32_t v = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sb);
+    if (4 * k >= hl) v = 0;
+    else if (4 * k + 4 > hl) v &= (1u << ((hl - 4 * k) * 8)) - 1u;
+    o[k] = v;
+  }
+#pragma unroll
+  for (uint32_t v = 0; v < 4; v++) out[v] = make_uint4(o[4 * v], o[4 * v + 1], o[4 * v + 2], o[4 * v + 3]);
 }
 
 // ===========================================================================
@@ -318,19 +453,24 @@ __device__ inline bool stem_words_equal(const StemRef& x, const StemRef& y, uint
   return diff == 0;
 }
 
-// A stem as the run kernels see it: its zero-padded 64-B head in sorted order
-// (coalesced uint4 loads) and, for stems longer than 64 B only, the rest in the
-// packed stem buffer.
+// A stem as the run kernels see it: its zero-padded 64-B head in registers
+// (read from the packed stems with aligned 16-B loads) and, for stems longer
+// than 64 B only, the rest through a StemRef.
 struct Key {
-  const uint4* k;  // 4 x uint4
-  StemRef st;      // full stem (bytes >= KEY_HEAD read from here)
+  uint4 h[4];
+  StemRef st;  // full stem (bytes >= KEY_HEAD read from here)
   uint32_t len;
 };
 
-__device__ inline Key key_at(const BatchDev& b, const uint4* key_s, const Rec* rec_s, uint32_t q) {
-  const Rec& r = rec_s[q];
-  return Key{key_s + 4ull * q, stem_ref(b, r.off), rec_len(r)};
+__device__ inline Key key_of(const BatchDev& b, const Rec& r) {
+  Key k;
+  k.len = rec_len(r);
+  k.st = stem_ref(b, r.off);
+  load_head(b.stem, r.off, k.len, k.h);
+  return k;
 }
+
+__device__ inline Key key_at(const BatchDev& b, const Rec* rec_s, uint32_t q) { return key_of(b, rec_s[q]); }
 
 __device__ inline uint32_t head_diff(const uint4* x, const uint4* y) {
   uint32_t d = 0;
@@ -353,7 +493,7 @@ __device__ inline uint32_t tail_diff(const StemRef& x, const StemRef& y, uint32_
 
 // Same stem bytes (callers have compared hash and length).
 __device__ inline bool key_equal(const Key& x, const Key& y) {
-  uint32_t d = head_diff(x.k, y.k);
+  uint32_t d = head_diff(x.h, y.h);
   if (x.len > KEY_HEAD) d |= tail_diff(x.st, y.st, x.len);
   return d == 0;
 }
@@ -366,7 +506,7 @@ __device__ inline bool key_equal(const Key& x, const Key& y) {
 __device__ inline bool slot_key_equal(const Slot* s, const Key& key, const uint8_t* arena) {
   if (s->key_len != key.len) return false;
   const uint4* sk4 = reinterpret_cast<const uint4*>(s->key);
-  uint32_t diff = head_diff(sk4, key.k);
+  uint32_t diff = head_diff(sk4, key.h);
   const uint32_t len = key.len;
   if (len > KEY_HEAD) {
     const uint32_t* sk = reinterpret_cast<const uint32_t*>(s->key);
@@ -392,7 +532,7 @@ __device__ inline void slot_init(const TableDev& t, Slot* s, const Key& key, uin
   s->ext_off = 0;
   uint4* sk4 = reinterpret_cast<uint4*>(s->key);
 #pragma unroll
-  for (uint32_t v = 0; v < 4; v++) sk4[v] = key.k[v];
+  for (uint32_t v = 0; v < 4; v++) sk4[v] = key.h[v];
   if (len > KEY_HEAD) {
     uint32_t* sk = reinterpret_cast<uint32_t*>(s->key);
     const uint32_t il = len < INLINE_KEY ? len : INLINE_KEY;
@@ -485,8 +625,9 @@ __device__ inline void load_img(const Slot* s, SlotImg& im) {
 
 __device__ inline uint32_t u4w(const uint4& a, uint32_t j) { return j == 0 ? a.x : j == 1 ? a.y : j == 2 ? a.z : a.w; }
 
-// Stem of `key` (head kh = its zero-padded first 64 bytes) == the slot's stem?
-__device__ inline bool img_key_equal(const SlotImg& im, const uint4* kh, const Key& key, const uint8_t* arena) {
+// Stem of `key` == the slot's stem?
+__device__ inline bool img_key_equal(const SlotImg& im, const Key& key, const uint8_t* arena) {
+  const uint4* kh = key.h;
   if (im.key_len() != key.len) return false;
   uint32_t d = 0;
 #pragma unroll
@@ -516,8 +657,8 @@ __device__ inline bool img_key_equal(const SlotImg& im, const uint4* kh, const K
 
 // find_slot with insert, returning the slot's image (a fresh slot's image for
 // an insert: empty windows, no flags).
-__device__ int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint64_t tag, const Key& key, const uint4* kh,
-                                 uint32_t unit, bool* inserted, SlotImg& im, uint32_t* err) {
+__device__ int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint64_t tag, const Key& key, uint32_t unit,
+                                 bool* inserted, SlotImg& im, uint32_t* err) {
   uint64_t i = hstem >> t.shift;
   int64_t tomb = -1;
   *inserted = false;
@@ -525,7 +666,7 @@ __device__ int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint64_t tag
     load_img(&t.slots[i], im);
     const uint64_t st = im.tag();
     if (st == tag) {
-      if (img_key_equal(im, kh, key, t.arena)) return (int64_t)i;
+      if (img_key_equal(im, key, t.arena)) return (int64_t)i;
       continue;
     }
     if (st == TAG_TOMB) {
@@ -1074,13 +1215,153 @@ __global__ __launch_bounds__(256) void k_seg_apply(const uint32_t* __restrict__ 
   }
 }
 
+// ---- k_segment: gather + run segmentation in one pass over the sorted order,
+// tiles of SEG_TILE positions taken by ticket, decoupled look-back across
+// tiles. Per sorted position q: rec_s[q] = rec[svals[q]] (one random 32-B
+// read), head = q == 0 || skeys[q-1] != skeys[q], rid[q] = heads in [0, q] - 1,
+// segsum[q] = inclusive in-run sum of max(1, hits) (u32, wrapping like the
+// sequential INCRBYs); per run its start (flags cleared), and num_runs. A
+// tile's look-back state is (heads, segmented sum): two 8-B {value, tag}
+// granules that a reader accepts only when both carry the same tag and flag.
+__device__ inline SegPair seg_read(const unsigned long long* st, uint32_t j, uint32_t tag, bool& ready, bool& inc,
+                                   uint32_t& h) {
+  const unsigned long long g0 = __hip_atomic_load(st + 2 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long g1 = __hip_atomic_load(st + 2 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t t0 = (uint32_t)(g0 >> 32), t1 = (uint32_t)(g1 >> 32);
+  ready = (t0 & ~3u) == tag && t0 == t1;
+  inc = ready && (t0 & OS_INC);
+  h = (uint32_t)g1;
+  return SegPair{h ? 1u : 0u, (uint32_t)g0};
+}
+
+__device__ inline void seg_publish(unsigned long long* st, uint32_t j, uint32_t tag, SegPair v, uint32_t h) {
+  __hip_atomic_store(st + 2 * j, (unsigned long long)v.s | ((unsigned long long)tag << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(st + 2 * j + 1, (unsigned long long)h | ((unsigned long long)tag << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void k_segment(const Rec* __restrict__ rec, const uint32_t* __restrict__ skeys,
+                                                 const uint32_t* __restrict__ svals, uint32_t n,
+                                                 Rec* __restrict__ rec_s, uint32_t* __restrict__ segsum,
+                                                 uint32_t* __restrict__ rid, uint32_t* __restrict__ run_start,
+                                                 uint32_t* __restrict__ run_flags, uint32_t* num_runs,
+                                                 uint32_t* __restrict__ ctr, unsigned long long* status, uint32_t tag,
+                                                 const uint32_t* err) {
+  __shared__ SegPair sp[4];
+  __shared__ uint32_t sh[4];
+  __shared__ SegPair s_pre;
+  __shared__ uint32_t s_tile, s_preh;
+  if (*err) return;  // the same for every block
+  if (threadIdx.x == 0) s_tile = atomicAdd(ctr, 1u);
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t base = tile * SEG_TILE + wave * SEG_STRIP + lane;
+  // pass 1: records into sorted order; head flags and hits kept per chunk
+  SegChunk ch[SEG_ITEMS];
+  SegPair agg{0, 0};
+  uint32_t hc = 0;
+#pragma unroll
+  for (uint32_t c = 0; c < SEG_ITEMS; c++) {
+    const uint32_t q = base + 64 * c;
+    const bool valid = q < n;
+    bool head = false;
+    uint32_t hv = 0;
+    if (valid) {
+      head = q == 0 || skeys[q - 1] != skeys[q];
+      const Rec r = rec[svals[q]];
+      rec_s[q] = r;
+      hv = r.hits > 1 ? r.hits : 1u;
+    }
+    ch[c] = SegChunk{(uint64_t)__ballot(head), hv};
+    uint32_t t = hv;  // chunk total, segmented: sum after the last head
+    const uint32_t lh = ch[c].heads ? 63u - (uint32_t)__clzll((long long)ch[c].heads) : 0u;
+    if (ch[c].heads && lane < lh) t = 0;
+#pragma unroll
+    for (uint32_t off = 32; off; off >>= 1) t += __shfl_xor(t, off, 64);
+    agg = seg_op(agg, SegPair{ch[c].heads ? 1u : 0u, t});
+    hc += (uint32_t)__popcll(ch[c].heads);
+  }
+  SegPair excl, tot;
+  uint32_t hexcl, htot;
+  seg_waves(agg, hc, sp, sh, excl, hexcl, tot, htot);
+  // publish this tile's aggregate, look back for the prefix, publish the inclusive value
+  if (wave == 0) {
+    if (lane == 0) seg_publish(status, tile, tag | (tile ? OS_AGG : OS_INC), tot, htot);
+    SegPair acc{0, 0};
+    uint32_t acch = 0;
+    int32_t top = (int32_t)tile - 1;
+    while (top >= 0) {
+      const int32_t j = top - (int32_t)lane;
+      bool ready = true, inc = false;
+      uint32_t h = 0;
+      SegPair v{0, 0};
+      if (j >= 0) v = seg_read(status, (uint32_t)j, tag, ready, inc, h);
+      const uint64_t mi = __ballot(inc), mnr = __ballot(!ready);
+      const uint32_t fi = mi ? (uint32_t)(__ffsll((unsigned long long)mi) - 1) : 64u;
+      const uint64_t need = fi >= 63 ? ~0ull : ((2ull << fi) - 1);  // lanes 0..fi
+      if (mnr & need) {
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      // older tiles sit in higher lanes: x = x_63 (+) ... (+) x_0 over lanes 0..fi
+      SegPair x = lane <= fi ? v : SegPair{0, 0};
+      uint32_t xh = lane <= fi ? h : 0u;
+#pragma unroll
+      for (uint32_t off = 1; off < 64; off <<= 1) {
+        const SegPair y{__shfl_down(x.f, off, 64), __shfl_down(x.s, off, 64)};
+        const uint32_t yh = __shfl_down(xh, off, 64);
+        if (lane + off < 64) {
+          x = seg_op(y, x);
+          xh += yh;
+        }
+      }
+      acc = seg_op(SegPair{__shfl(x.f, 0, 64), __shfl(x.s, 0, 64)}, acc);
+      acch += __shfl(xh, 0, 64);
+      if (fi < 64) break;
+      top -= 64;
+    }
+    if (lane == 0) {
+      if (tile) seg_publish(status, tile, tag | OS_INC, seg_op(acc, tot), acch + htot);
+      s_pre = acc;
+      s_preh = acch;
+    }
+  }
+  __syncthreads();
+  // pass 2: exclusive prefix of the wave = tiles before + earlier waves
+  SegPair run = seg_op(s_pre, excl);
+  uint32_t hrun = s_preh + hexcl;
+#pragma unroll
+  for (uint32_t c = 0; c < SEG_ITEMS; c++) {
+    const uint32_t q = base + 64 * c;
+    const SegPair v = seg_chunk_scan(ch[c], lane);
+    const SegPair in = seg_op(run, v);
+    const uint64_t heads = ch[c].heads;
+    const uint32_t r = hrun + (uint32_t)__popcll(heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1))) - 1;
+    if (q < n) {
+      segsum[q] = in.s;
+      rid[q] = r;
+      if ((heads >> lane) & 1) {
+        run_start[r] = q;
+        run_flags[r] = 0;
+      }
+      if (q == n - 1) {
+        run_start[r + 1] = n;
+        *num_runs = r + 1;
+      }
+    }
+    run = seg_op(run, SegPair{__shfl(v.f, 63, 64), __shfl(v.s, 63, 64)});
+    hrun += (uint32_t)__popcll(heads);
+  }
+}
+
 // Every element of a run must have the head's stem and unit; a run that does
 // not (two stems sharing the 32-bit hash prefix, or one stem under several
 // units) is flagged RUN_MULTI and queued once for k_runs_general, which runs
 // beside k_runs. Long runs must also share the head's window for the parallel
 // path (RUN_SLOW otherwise: replayed serially).
 __global__ __launch_bounds__(256) void k_run_check(BatchDev b, const Rec* __restrict__ rec_s,
-                                                   const uint4* __restrict__ key_s,
                                                    const uint32_t* __restrict__ rid,
                                                    const uint32_t* __restrict__ run_start,
                                                    uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
@@ -1094,7 +1375,7 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, const Rec* __rest
   b.stem_total = b.off[b.n];
   const Rec x0 = rec_s[p], x = rec_s[q];
   const bool same = x.hlo == x0.hlo && (x.lu & 0xFFFFFFu) == (x0.lu & 0xFFFFFFu) &&  // hash, length, unit
-                    key_equal(key_at(b, key_s, rec_s, q), key_at(b, key_s, rec_s, p));
+                    key_equal(key_of(b, x), key_of(b, x0));
   if (!same) {
     if (!(atomicOr(&run_flags[r], RUN_MULTI) & RUN_MULTI)) defer[atomicAdd(defer_n, 1u)] = p;
   } else if (run_start[r + 1] - p >= LONG_RUN) {
@@ -1109,7 +1390,6 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, const Rec* __rest
 // turns out to live in the table under another unit too is queued for the
 // exact path (defer2, k_runs_general after this kernel).
 __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, const Rec* __restrict__ rec_s,
-                                              const uint4* __restrict__ key_s,
                                               const uint32_t* __restrict__ skeys,
                                               const uint32_t* __restrict__ svals, unsigned long long* __restrict__ res,
                                               const uint32_t* __restrict__ run_start,
@@ -1139,10 +1419,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
     const Rec x0 = rec_s[p];
     const uint64_t h0 = ((uint64_t)skeys[p] << 32) | x0.hlo;
     const uint32_t u0 = rec_unit(x0);
-    const Key k0 = key_at(b, key_s, rec_s, p);
-    uint4 kh[4];
-#pragma unroll
-    for (uint32_t v = 0; v < 4; v++) kh[v] = k0.k[v];
+    const Key k0 = key_of(b, x0);
     if (!(fl & RUN_MULTI)) {  // RUN_MULTI runs belong to k_runs_general
       const bool long_run = !restore && end - p >= LONG_RUN && !(fl & RUN_SLOW);
       bool ok = true;
@@ -1153,7 +1430,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
         load_img(&t.slots[s0], im);
       } else {
         bool ins;
-        s0 = find_slot_img(t, h0, slot_tag(h0, u0), k0, kh, u0, &ins, im, err);
+        s0 = find_slot_img(t, h0, slot_tag(h0, u0), k0, u0, &ins, im, err);
         if (s0 < 0) {
           ok = false;
         } else if (im.flags() & SLOT_EXACT) {
@@ -1302,7 +1579,6 @@ __global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules,
 // ---- k_runs_general: deferred runs (hash-prefix collisions, multi-unit
 // stems). Splits the run into distinct stems, then replays each exactly.
 __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Params P, const Rec* __restrict__ rec_s,
-                                                      const uint4* __restrict__ key_s,
                                                       const uint32_t* __restrict__ skeys,
                                                       const uint32_t* __restrict__ svals,
                                                       unsigned long long* __restrict__ res,
@@ -1337,11 +1613,11 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
     umask[0] = 1u << (rec_unit(rec_s[p]) - 1);
     for (uint32_t q = p + 1; q < end; q++) {
       const Rec x = rec_s[q];
-      const Key kx = key_at(b, key_s, rec_s, q);
+      const Key kx = key_of(b, x);
       uint32_t k = 0;
       for (; k < nrep; k++) {
         const Rec y = rec_s[rep[k]];
-        if (y.hlo == x.hlo && rec_len(y) == rec_len(x) && key_equal(key_at(b, key_s, rec_s, rep[k]), kx)) break;
+        if (y.hlo == x.hlo && rec_len(y) == rec_len(x) && key_equal(key_of(b, y), kx)) break;
       }
       if (k == nrep) {
         if (nrep == MAX_REPS) { atomicOr(err, ERR_COLLISIONS); k = 0; }
@@ -1352,7 +1628,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
     }
     for (uint32_t k = 0; k < nrep; k++) {
       const Rec y = rec_s[rep[k]];
-      const Key stem = key_at(b, key_s, rec_s, rep[k]);
+      const Key stem = key_at(b, rec_s, rep[k]);
       const uint64_t hs = ((uint64_t)key << 32) | y.hlo;
       // ---- resolve the slot(s)
       bool simple = false;
@@ -1539,30 +1815,28 @@ static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b -
 
 // Stage A (table-free): validate, hash, sort, gather, segment. Uses only this
 // buffer's scratch and its validation word s.err.
-void launch_stage_a(const BatchDev& b, const Scratch& s, hipStream_t st, hipEvent_t* ev) {
+void launch_stage_a(const BatchDev& b, const Scratch& s, uint32_t epoch, hipStream_t st, hipEvent_t* ev) {
   const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
   if (ev) (void)hipEventRecord(ev[0], st);
-  if (g0) k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.key, s.keys[0], s.vals[0], s.err, s.time_floor, s.defer_n);
+  if (g0)
+    k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.keys[0], s.vals[0], s.err, s.time_floor, s.defer_n, s.os_ghist,
+                                  s.os_ctr);
   if (ev) (void)hipEventRecord(ev[1], st);
   if (b.n) {
     const uint32_t ntiles = cdiv(b.n, RS_TILE);
+    k_os_hist<<<ntiles < 256 ? ntiles : 256, 256, 0, st>>>(s.keys[0], b.n, s.os_ghist, s.err);
     for (uint32_t pass = 0; pass < 4; pass++) {
-      const uint32_t src = pass & 1, dst = src ^ 1, shift = 8 * pass;
-      k_rs_hist<<<ntiles, 256, 0, st>>>(s.keys[src], b.n, shift, ntiles, s.hist, s.err);
-      k_rs_rowscan<<<256, 256, 0, st>>>(s.hist, ntiles, s.hist_tot, s.err);
-      k_rs_scatter<<<ntiles, 256, 0, st>>>(s.keys[src], s.vals[src], s.keys[dst], s.vals[dst], b.n, shift, ntiles,
-                                           s.hist, s.hist_tot, s.err);
+      const uint32_t src = pass & 1, dst = src ^ 1;
+      k_os_pass<<<ntiles, 256, 0, st>>>(s.keys[src], s.vals[src], s.keys[dst], s.vals[dst], b.n, pass, s.os_ghist,
+                                        s.os_ctr, s.os_status, os_tag(epoch, pass), s.err);
     }
   }
   if (ev) (void)hipEventRecord(ev[2], st);
   if (b.n) {
     const uint32_t nt = cdiv(b.n, SEG_TILE), g = cdiv(b.n, 256);
-    k_gather<<<g, 256, 0, st>>>(s.rec, s.key, s.vals[0], b.n, s.rec_s, s.key_s, s.hits_s, s.err);
-    k_seg_reduce<<<nt, 256, 0, st>>>(s.keys[0], s.hits_s, b.n, s.tile_f, s.tile_s, s.tile_h, s.err);
-    k_seg_tiles<<<1, 1024, 0, st>>>(s.tile_f, s.tile_s, s.tile_h, nt, s.err);
-    k_seg_apply<<<nt, 256, 0, st>>>(s.keys[0], s.hits_s, b.n, s.tile_f, s.tile_s, s.tile_h, s.segsum, s.rid,
-                                    s.run_start, s.run_flags, s.num_runs, s.err);
-    k_run_check<<<g, 256, 0, st>>>(b, s.rec_s, s.key_s, s.rid, s.run_start, s.run_flags, s.defer, s.defer_n,
+    k_segment<<<nt, 256, 0, st>>>(s.rec, s.keys[0], s.vals[0], b.n, s.rec_s, s.segsum, s.rid, s.run_start,
+                                  s.run_flags, s.num_runs, s.os_ctr + 4, s.seg_status, os_tag(epoch, 0), s.err);
+    k_run_check<<<g, 256, 0, st>>>(b, s.rec_s, s.rid, s.run_start, s.run_flags, s.defer, s.defer_n,
                                    s.err);
   }
 }
@@ -1583,16 +1857,16 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     (void)hipEventRecord(go, st);
     (void)hipStreamWaitEvent(side, go, 0);
     k_runs_general<<<g < RUNS_GENERAL_BLOCKS ? g : RUNS_GENERAL_BLOCKS, 256, lds, side>>>(
-        b, t, P, s.rec_s, s.key_s, s.keys[0], s.vals[0], s.res, s.defer, s.defer_n, s.repid, o.stats, s.stripes,
+        b, t, P, s.rec_s, s.keys[0], s.vals[0], s.res, s.defer, s.defer_n, s.repid, o.stats, s.stripes,
         s.errb, restore);
     (void)hipEventRecord(side_done, side);
     if (ev) (void)hipEventRecord(ev[3], st);
-    k_runs<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.key_s, s.keys[0], s.vals[0], s.res, s.run_start, s.run_flags,
+    k_runs<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.keys[0], s.vals[0], s.res, s.run_start, s.run_flags,
                                 s.run_state, s.run_f, s.num_runs, s.defer2, s.defer2_n, o.stats, s.stripes, s.errb,
                                 restore);
     if (ev) (void)hipEventRecord(ev[4], st);
     // stems k_runs found under several units in the table (rare)
-    k_runs_general<<<RUNS_GENERAL_LATE_BLOCKS, 256, lds, st>>>(b, t, P, s.rec_s, s.key_s, s.keys[0], s.vals[0],
+    k_runs_general<<<RUNS_GENERAL_LATE_BLOCKS, 256, lds, st>>>(b, t, P, s.rec_s, s.keys[0], s.vals[0],
                                                                 s.res, s.defer2, s.defer2_n, s.repid, o.stats,
                                                                 s.stripes, s.errb, restore);
     (void)hipStreamWaitEvent(st, side_done, 0);
