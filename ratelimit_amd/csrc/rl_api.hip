@@ -5,7 +5,7 @@
 //
 // Batches submitted with rl_do_limit_async(stream = NULL) are pipelined: batch
 // t's table-free stage A (validate, hash, sort, segment) runs on scratch buffer
-// t % 2 and that buffer's stream while batch t-1's stage B (the table) still
+// t % NBUF and that buffer's stream while batch t-1's stage B (the table) still
 // runs. Stage B of every batch waits for the previous batch's stage B (an
 // event chain), so the table sees batches in submission order and every key
 // sees the reference's sequential INCRBY order. Every other call is serial and
@@ -23,14 +23,21 @@
 
 using namespace rl;
 
+// Pipeline depth: scratch buffers (and streams) in flight. Stage A of up to
+// NBUF - 1 later batches may run while one batch's stage B holds the table.
+#ifndef RL_NBUF
+#define RL_NBUF 3
+#endif
+constexpr uint32_t NBUF = RL_NBUF;
+
 struct rl_ctx {
   rl_config cfg;
   hipStream_t stream = nullptr;   // serial work (== pipe[0])
-  hipStream_t pipe[2] = {};       // one per scratch buffer
-  hipEvent_t b_done[2] = {};      // stage B of the last batch on each buffer is done
+  hipStream_t pipe[NBUF] = {};    // one per scratch buffer
+  hipEvent_t b_done[NBUF] = {};   // stage B of the last batch on each buffer is done
   hipStream_t side = nullptr;     // k_runs_general beside k_runs (stage B)
   hipEvent_t side_go = nullptr, side_done = nullptr;
-  uint32_t next = 0, last = 1;    // buffer of the next / of the latest batch
+  uint32_t next = 0, last = NBUF - 1;  // buffer of the next / of the latest batch
   uint32_t epoch = 0;             // batches submitted (sort look-back tags)
   // table
   Slot* slots = nullptr;
@@ -39,8 +46,8 @@ struct rl_ctx {
   uint64_t arena_cap16 = 0;
   // scratch: s[k] per buffer; stripes, counters, time floor, routing and the
   // table-stage error word are shared
-  Scratch s[2]{};
-  uint32_t* errw = nullptr;  // [0], [1] stage-A words of the buffers, [2] stage-B word
+  Scratch s[NBUF]{};
+  uint32_t* errw = nullptr;  // [0, NBUF) stage-A words of the buffers, [NBUF] stage-B word
   // device staging for the host-buffer entry points
   uint8_t* d_stem = nullptr;
   uint32_t *d_off = nullptr, *d_req = nullptr, *d_limit = nullptr, *d_hits = nullptr, *d_rule = nullptr;
@@ -124,11 +131,12 @@ hipError_t after_batches(rl_ctx* c, hipStream_t st) { return hipStreamWaitEvent(
 // which must already be ordered after all submitted work.
 int collect(rl_ctx* c, hipStream_t st = nullptr) {
   if (!st) st = c->stream;
-  HIPCHK(c, hipMemcpyAsync(c->h_err, c->errw, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_err, c->errw, (NBUF + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
-  const uint32_t e = c->h_err[0] | c->h_err[1] | c->h_err[2];
+  uint32_t e = 0;
+  for (uint32_t j = 0; j <= NBUF; j++) e |= c->h_err[j];
   if (e) {
-    HIPCHK(c, hipMemsetAsync(c->errw, 0, 3 * sizeof(uint32_t), st));
+    HIPCHK(c, hipMemsetAsync(c->errw, 0, (NBUF + 1) * sizeof(uint32_t), st));
     HIPCHK(c, hipStreamSynchronize(st));
   }
   return map_err(c, e);
@@ -142,13 +150,13 @@ Params params(rl_ctx* c);
 // previous batch's stage B. Serial: both stages on `st` after all earlier work.
 uint32_t enqueue(rl_ctx* c, const BatchDev& b, const OutDev& o, int restore, hipStream_t st, bool pipelined) {
   const uint32_t k = c->next;
-  c->next ^= 1u;
+  c->next = (k + 1) % NBUF;
   c->epoch = (c->epoch + 1) & 0x0FFFFFFFu;
   if (!c->epoch) {  // after 2^28 batches: clear the look-back granules once, so no old tag can alias
     (void)hipDeviceSynchronize();
-    for (int j = 0; j < 2; j++)
+    for (uint32_t j = 0; j < NBUF; j++)
     {
-      (void)hipMemset(c->s[j].os_status, 0, 256ull * ((c->cfg.max_batch + RS_TILE - 1) / RS_TILE) * 8);
+      (void)hipMemset(c->s[j].os_status, 0, 256ull * ((c->cfg.max_batch + OS_TILE - 1) / OS_TILE) * 8);
       (void)hipMemset(c->s[j].seg_status, 0, 16ull * ((c->cfg.max_batch + SEG_TILE - 1) / SEG_TILE + 1));
     }
     c->epoch = 1;
@@ -225,12 +233,12 @@ Params params(rl_ctx* c) {
 
 // Per-batch scratch of one pipeline buffer (sized for max_batch descriptors).
 bool alloc_buffer(Scratch& s, uint32_t n) {
-  const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
+  const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE, os_tiles = (n + OS_TILE - 1) / OS_TILE;
   const size_t nt = (n + SEG_TILE - 1) / SEG_TILE + 1;
   bool ok = dalloc(&s.seg_status, 2 * nt) == hipSuccess && hipMemset(s.seg_status, 0, 16 * nt) == hipSuccess;
   ok = ok && dalloc(&s.os_ghist, 4 * 256) == hipSuccess && dalloc(&s.os_ctr, 8) == hipSuccess &&
-       dalloc(&s.os_status, 256ull * std::max(ntiles, 1u)) == hipSuccess &&
-       hipMemset(s.os_status, 0, 256ull * std::max(ntiles, 1u) * 8) == hipSuccess;
+       dalloc(&s.os_status, 256ull * std::max(os_tiles, 1u)) == hipSuccess &&
+       hipMemset(s.os_status, 0, 256ull * std::max(os_tiles, 1u) * 8) == hipSuccess;
   ok = ok && dalloc(&s.rec, n) == hipSuccess && dalloc(&s.rec_s, n) == hipSuccess && dalloc(&s.res, n) == hipSuccess;
   for (int i = 0; i < 2; i++) ok = ok && dalloc(&s.keys[i], n) == hipSuccess && dalloc(&s.vals[i], n) == hipSuccess;
   ok = ok && dalloc(&s.hist, 256ull * std::max(ntiles, 1u)) == hipSuccess && dalloc(&s.hist_tot, 256) == hipSuccess;
@@ -318,27 +326,28 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   c->nslots = cfg.table_slots;
   c->arena_cap16 = cfg.arena_bytes / 16;
   const uint32_t n = cfg.max_batch;
-  bool ok = hipStreamCreateWithFlags(&c->pipe[0], hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->pipe[1], hipStreamNonBlocking) == hipSuccess;
+  bool ok = true;
+  for (uint32_t k = 0; k < NBUF; k++) ok = ok && hipStreamCreateWithFlags(&c->pipe[k], hipStreamNonBlocking) == hipSuccess;
   c->stream = c->pipe[0];
   ok = ok && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess;
-  for (int k = 0; k < 2; k++) ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess;
+  for (uint32_t k = 0; k < NBUF; k++)
+    ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&c->side_go, hipEventDisableTiming) == hipSuccess &&
        hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming) == hipSuccess;
   ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess;
   ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess;
-  for (int k = 0; k < 2; k++) ok = ok && alloc_buffer(c->s[k], n);
+  for (uint32_t k = 0; k < NBUF; k++) ok = ok && alloc_buffer(c->s[k], n);
   Scratch& s0 = c->s[0];
-  ok = ok && dalloc(&c->errw, 4) == hipSuccess;
+  ok = ok && dalloc(&c->errw, NBUF + 1) == hipSuccess;
   ok = ok && dalloc(&s0.stripes, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS) == hipSuccess;
   ok = ok && dalloc(&s0.time_floor, 1) == hipSuccess;
   ok = ok && dalloc(&s0.counters, 8) == hipSuccess;
   ok = ok && dalloc(&s0.route_start, RL_MAX_SHARDS + 1) == hipSuccess &&
        dalloc(&s0.route_base, RL_MAX_SHARDS) == hipSuccess && dalloc(&s0.route_counts, 2 * RL_MAX_SHARDS) == hipSuccess;
-  for (int k = 0; k < 2; k++) {  // shared members
+  for (uint32_t k = 0; k < NBUF; k++) {  // shared members
     Scratch& sk = c->s[k];
     sk.err = c->errw ? c->errw + k : nullptr;
-    sk.errb = c->errw ? c->errw + 2 : nullptr;
+    sk.errb = c->errw ? c->errw + NBUF : nullptr;
     sk.stripes = s0.stripes;
     sk.time_floor = s0.time_floor;
     sk.counters = s0.counters;
@@ -356,18 +365,18 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && dalloc(&c->d_code, n) == hipSuccess && dalloc(&c->d_rem, n) == hipSuccess &&
        dalloc(&c->d_reset, n) == hipSuccess;
   ok = ok && dalloc(&c->d_stats, (size_t)cfg.max_rules * RL_NUM_STATS) == hipSuccess;
-  ok = ok && hipHostMalloc((void**)&c->h_err, 4 * sizeof(uint32_t)) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_err, (NBUF + 1) * sizeof(uint32_t)) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_counters, 8 * sizeof(unsigned long long)) == hipSuccess;
   if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
   ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
-       hipMemsetAsync(c->errw, 0, 16, c->stream) == hipSuccess &&
+       hipMemsetAsync(c->errw, 0, (NBUF + 1) * 4, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.time_floor, 0, 8, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.counters, 0, 64, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.stripes, 0, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS * 8, c->stream) ==
            hipSuccess &&
        hipMemsetAsync(c->d_stem, 0, (size_t)cfg.max_stem_bytes + 64, c->stream) == hipSuccess &&
-       hipEventRecord(c->b_done[0], c->stream) == hipSuccess && hipEventRecord(c->b_done[1], c->stream) == hipSuccess &&
        hipStreamSynchronize(c->stream) == hipSuccess;
+  for (uint32_t k = 0; k < NBUF; k++) ok = ok && hipEventRecord(c->b_done[k], c->stream) == hipSuccess;
   if (!ok) return fail("gpu: device initialisation failed", c);
   return c;
 }
@@ -375,14 +384,14 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
 void rl_destroy(rl_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->cfg.device);
-  for (int k = 0; k < 2; k++)
+  for (uint32_t k = 0; k < NBUF; k++)
     if (c->pipe[k]) (void)hipStreamSynchronize(c->pipe[k]);
   if (c->side) (void)hipStreamSynchronize(c->side);
   if (c->side_go) (void)hipEventDestroy(c->side_go);
   if (c->side_done) (void)hipEventDestroy(c->side_done);
   for (int i = 0; i <= RL_NUM_STAGES; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
-  for (int k = 0; k < 2; k++) {
+  for (uint32_t k = 0; k < NBUF; k++) {
     free_buffer(c->s[k]);
     if (c->b_done[k]) (void)hipEventDestroy(c->b_done[k]);
   }
@@ -395,7 +404,7 @@ void rl_destroy(rl_ctx* c) {
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
   if (c->h_route) (void)hipHostFree(c->h_route);
-  for (int k = 0; k < 2; k++)
+  for (uint32_t k = 0; k < NBUF; k++)
     if (c->pipe[k]) (void)hipStreamDestroy(c->pipe[k]);
   if (c->side) (void)hipStreamDestroy(c->side);
   delete c;

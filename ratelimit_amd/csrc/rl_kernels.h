@@ -9,8 +9,18 @@
 
 namespace rl {
 
-constexpr uint32_t RS_ITEMS = 16;
+constexpr uint32_t RS_ITEMS = 16;  // routing partition (k_rs_*): 256 threads x RS_ITEMS
 constexpr uint32_t RS_TILE = 256 * RS_ITEMS;
+// onesweep sort (k_os_pass): OS_WAVES waves x OS_ITEMS elements per lane per tile
+#ifndef RL_OS_ITEMS
+#define RL_OS_ITEMS 16
+#endif
+#ifndef RL_OS_WAVES
+#define RL_OS_WAVES 4
+#endif
+constexpr uint32_t OS_ITEMS = RL_OS_ITEMS, OS_WAVES = RL_OS_WAVES, OS_THREADS = 64 * OS_WAVES;
+constexpr uint32_t OS_TILE = OS_THREADS * OS_ITEMS;
+static_assert(OS_WAVES >= 4, "256 digits need at least 256 threads");
 constexpr uint32_t SEG_ITEMS = 16;
 constexpr uint32_t SEG_TILE = 256 * SEG_ITEMS;
 constexpr uint32_t LONG_RUN = 32;        // runs at least this long take the parallel path

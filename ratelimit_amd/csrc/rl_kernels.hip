@@ -3,12 +3,11 @@
 // Pipeline for one batch (inputs already in HBM); stage A (table-free):
 //   k_prepare     validate the packed batch; hash every stem (LDS-staged
 //                 bytes); pack each descriptor into a 32-B Rec
-//   radix sort    stable LSD sort of (hash[63:32], index): groups each stem's
-//                 descriptors together, in arrival (sequence) order
-//   k_gather      Recs into sorted order (one random 32-B read each)
-//   k_seg_*       run ids + in-run prefix sums of hits (3-phase segmented scan)
-//   k_run_check   every element shares its run's stem and unit (else the run
-//                 goes to k_runs_general); long runs: and its window?
+//   k_os_*        onesweep stable LSD sort of (hash[63:32], index): groups each
+//                 stem's descriptors together, in arrival (sequence) order
+//   k_segment     Recs into sorted order, run ids, in-run prefix sums of hits
+//                 (single pass, decoupled look-back), and the run checks: one
+//                 stem and one unit per run (else k_runs_general)
 //   ---- stage B (the table; batch order) ----
 //   k_runs        one lane per run: probe/insert the (stem, unit) slot of the
 //                 HBM table (one 128-B line per probe); replay short runs in
@@ -42,11 +41,13 @@ constexpr uint32_t HASH_LDS_BYTES = 16384;
 __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ rec, uint32_t* __restrict__ keys,
                                                  uint32_t* __restrict__ vals, uint32_t* err,
                                                  const int64_t* time_floor, uint32_t* defer_n,
-                                                 uint32_t* __restrict__ os_ghist, uint32_t* __restrict__ os_ctr) {
+                                                 uint32_t* __restrict__ os_ghist, uint32_t* __restrict__ os_ctr,
+                                                 uint32_t* __restrict__ run_flags) {
   __shared__ uint32_t lds[HASH_LDS_BYTES / 4 + 4];
   const uint32_t tid = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + tid;
   uint32_t bad = 0;
+  if (i < b.n) run_flags[i] = 0;  // k_segment ORs run flags in from any tile
   if (blockIdx.x == 0) {  // per-batch counters: RUN_MULTI queue, sort digit totals and tile tickets
     if (tid == 0) *defer_n = 0;
     if (tid < 5) os_ctr[tid] = 0;  // [0..3] sort passes, [4] k_segment
@@ -282,33 +283,42 @@ __global__ __launch_bounds__(256) void k_os_hist(const uint32_t* __restrict__ ke
   }
 }
 
-__global__ __launch_bounds__(256) void k_os_pass(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                 uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, uint32_t n,
-                                                 uint32_t pass, const uint32_t* __restrict__ ghist,
-                                                 uint32_t* __restrict__ ctr, unsigned long long* status, uint32_t tag,
-                                                 const uint32_t* err) {
-  __shared__ uint32_t wcnt[4][256];
+#ifdef RL_OS_PROF  // sortbench only: per-tile phase stamps of the last pass launched
+__device__ unsigned long long g_os_prof[8192 * 8];
+#define OS_STAMP(k) \
+  if (threadIdx.x == 0) g_os_prof[tile * 8 + (k)] = wall_clock64()
+#else
+#define OS_STAMP(k)
+#endif
+
+__global__ __launch_bounds__(OS_THREADS) void k_os_pass(const uint32_t* __restrict__ kin,
+                                                        const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
+                                                        uint32_t* __restrict__ vout, uint32_t n, uint32_t pass,
+                                                        const uint32_t* __restrict__ ghist, uint32_t* __restrict__ ctr,
+                                                        unsigned long long* status, uint32_t tag, const uint32_t* err) {
+  __shared__ uint32_t wcnt[OS_WAVES][256];
   __shared__ uint32_t dbase[256];
   __shared__ uint32_t gsum[4];
   __shared__ uint32_t s_tile;
   if (*err) return;  // the same for every block: no tile is left half-published
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) s_tile = atomicAdd(&ctr[pass], 1u);
-  wcnt[0][tid] = 0; wcnt[1][tid] = 0; wcnt[2][tid] = 0; wcnt[3][tid] = 0;
+  for (uint32_t j = tid; j < OS_WAVES * 256; j += OS_THREADS) (&wcnt[0][0])[j] = 0;
   __syncthreads();
   const uint32_t tile = s_tile, shift = 8 * pass;
+  OS_STAMP(0);
   const uint64_t lt_mask = (1ull << lane) - 1;
-  const uint32_t wbase = tile * RS_TILE + wave * 64 * RS_ITEMS;
-  uint32_t kk[RS_ITEMS], vv[RS_ITEMS], pos[RS_ITEMS];
+  const uint32_t wbase = tile * OS_TILE + wave * 64 * OS_ITEMS;
+  uint32_t kk[OS_ITEMS], vv[OS_ITEMS], pos[OS_ITEMS];
 #pragma unroll
-  for (uint32_t i = 0; i < RS_ITEMS; i++) {
+  for (uint32_t i = 0; i < OS_ITEMS; i++) {
     const uint32_t j = wbase + i * 64 + lane;
     const bool valid = j < n;
     kk[i] = valid ? kin[j] : 0xFFFFFFFFu;
     vv[i] = valid ? vin[j] : 0u;
   }
 #pragma unroll
-  for (uint32_t i = 0; i < RS_ITEMS; i++) {
+  for (uint32_t i = 0; i < OS_ITEMS; i++) {
     const bool valid = wbase + i * 64 + lane < n;
     const uint32_t d = (kk[i] >> shift) & 255u;
     uint64_t peers = __ballot(valid);
@@ -329,53 +339,60 @@ __global__ __launch_bounds__(256) void k_os_pass(const uint32_t* __restrict__ ki
     pos[i] = old + rank;
   }
   __syncthreads();
-  // digit tid: this tile's count and the per-wave exclusive offsets
-  uint32_t c = 0;
+  OS_STAMP(1);
+  if (tid < 256) {
+    // digit tid: this tile's count and the per-wave exclusive offsets
+    uint32_t c = 0;
 #pragma unroll
-  for (uint32_t w = 0; w < 4; w++) {
-    const uint32_t t = wcnt[w][tid];
-    wcnt[w][tid] = c;
-    c += t;
-  }
-  unsigned long long* mine = status + (size_t)tile * 256 + tid;
-  __hip_atomic_store(mine, (unsigned long long)c | ((unsigned long long)(tag | (tile ? OS_AGG : OS_INC)) << 32),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // global exclusive base of digit tid: wave scans of the pass's digit totals
-  const uint32_t g = ghist[pass * 256 + tid];
-  uint32_t inc = g;
-#pragma unroll
-  for (uint32_t off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(inc, off, 64);
-    if (lane >= off) inc += y;
-  }
-  if (lane == 63) gsum[wave] = inc;
-  // decoupled look-back: add earlier tiles' counts until an inclusive prefix
-  uint32_t excl = 0;
-  if (tile) {
-    uint32_t j = tile - 1;
-    for (;;) {
-      const unsigned long long v =
-          __hip_atomic_load(status + (size_t)j * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t tg = (uint32_t)(v >> 32);
-      if ((tg & ~3u) != tag) {  // not yet published for this pass
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      excl += (uint32_t)v;
-      if (tg & OS_INC) break;
-      --j;  // tile 0 publishes an inclusive count, so j stays >= 0
+    for (uint32_t w = 0; w < OS_WAVES; w++) {
+      const uint32_t t = wcnt[w][tid];
+      wcnt[w][tid] = c;
+      c += t;
     }
-    __hip_atomic_store(mine, (unsigned long long)(excl + c) | ((unsigned long long)(tag | OS_INC) << 32),
+    unsigned long long* mine = status + (size_t)tile * 256 + tid;
+    __hip_atomic_store(mine, (unsigned long long)c | ((unsigned long long)(tag | (tile ? OS_AGG : OS_INC)) << 32),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // global exclusive base of digit tid: wave scans of the pass's digit totals
+    const uint32_t g = ghist[pass * 256 + tid];
+    uint32_t inc = g;
+#pragma unroll
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(inc, off, 64);
+      if (lane >= off) inc += y;
+    }
+    if (lane == 63) gsum[wave] = inc;
+    // decoupled look-back: add earlier tiles' counts until an inclusive prefix
+    uint32_t excl = 0;
+    if (tile) {
+      uint32_t j = tile - 1;
+      for (;;) {
+        const unsigned long long v =
+            __hip_atomic_load(status + (size_t)j * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t tg = (uint32_t)(v >> 32);
+        if ((tg & ~3u) != tag) {  // not yet published for this pass
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        excl += (uint32_t)v;
+        if (tg & OS_INC) break;
+        --j;  // tile 0 publishes an inclusive count, so j stays >= 0
+      }
+      __hip_atomic_store(mine, (unsigned long long)(excl + c) | ((unsigned long long)(tag | OS_INC) << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    dbase[tid] = inc - g + excl;  // + earlier waves' digit totals, below
   }
-  __syncthreads();  // gsum
-  uint32_t wpre = 0;
+  __syncthreads();  // gsum, dbase
+  if (tid < 256) {
+    uint32_t wpre = 0;
 #pragma unroll
-  for (uint32_t w = 0; w < 4; w++) wpre += w < wave ? gsum[w] : 0u;
-  dbase[tid] = wpre + inc - g + excl;
+    for (uint32_t w = 0; w < 4; w++) wpre += w < wave ? gsum[w] : 0u;
+    dbase[tid] += wpre;
+  }
   __syncthreads();
+  OS_STAMP(2);
 #pragma unroll
-  for (uint32_t i = 0; i < RS_ITEMS; i++) {
+  for (uint32_t i = 0; i < OS_ITEMS; i++) {
     if (wbase + i * 64 + lane < n) {
       const uint32_t d = (kk[i] >> shift) & 255u;
       const uint32_t p = dbase[d] + wcnt[wave][d] + pos[i];
@@ -383,6 +400,7 @@ __global__ __launch_bounds__(256) void k_os_pass(const uint32_t* __restrict__ ki
       vout[p] = vv[i];
     }
   }
+  OS_STAMP(3);
 }
 
 // The zero-padded first KEY_HEAD bytes of the stem at byte `off` of the packed
@@ -1245,9 +1263,8 @@ __global__ __launch_bounds__(256) void k_segment(const Rec* __restrict__ rec, co
                                                  const uint32_t* __restrict__ svals, uint32_t n,
                                                  Rec* __restrict__ rec_s, uint32_t* __restrict__ segsum,
                                                  uint32_t* __restrict__ rid, uint32_t* __restrict__ run_start,
-                                                 uint32_t* __restrict__ run_flags, uint32_t* num_runs,
-                                                 uint32_t* __restrict__ ctr, unsigned long long* status, uint32_t tag,
-                                                 const uint32_t* err) {
+                                                 uint32_t* num_runs, uint32_t* __restrict__ ctr,
+                                                 unsigned long long* status, uint32_t tag, const uint32_t* err) {
   __shared__ SegPair sp[4];
   __shared__ uint32_t sh[4];
   __shared__ SegPair s_pre;
@@ -1344,7 +1361,6 @@ __global__ __launch_bounds__(256) void k_segment(const Rec* __restrict__ rec, co
       rid[q] = r;
       if ((heads >> lane) & 1) {
         run_start[r] = q;
-        run_flags[r] = 0;
       }
       if (q == n - 1) {
         run_start[r + 1] = n;
@@ -1356,31 +1372,28 @@ __global__ __launch_bounds__(256) void k_segment(const Rec* __restrict__ rec, co
   }
 }
 
-// Every element of a run must have the head's stem and unit; a run that does
-// not (two stems sharing the 32-bit hash prefix, or one stem under several
-// units) is flagged RUN_MULTI and queued once for k_runs_general, which runs
-// beside k_runs. Long runs must also share the head's window for the parallel
-// path (RUN_SLOW otherwise: replayed serially).
+// Run checks against the predecessor (equality chains): a run must hold one
+// stem under one unit, else it is flagged RUN_MULTI and queued once (by run
+// id) for k_runs_general; a window change within a run makes a long run
+// RUN_SLOW (serial replay). Run heads only compare two sort keys.
 __global__ __launch_bounds__(256) void k_run_check(BatchDev b, const Rec* __restrict__ rec_s,
+                                                   const uint32_t* __restrict__ skeys,
                                                    const uint32_t* __restrict__ rid,
-                                                   const uint32_t* __restrict__ run_start,
                                                    uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
                                                    uint32_t* defer_n, const uint32_t* err) {
   if (*err) return;
   const uint32_t q = blockIdx.x * 256 + threadIdx.x;
-  if (q >= b.n) return;
-  const uint32_t r = rid[q];
-  const uint32_t p = run_start[r];
-  if (q == p) return;
+  if (q == 0 || q >= b.n || skeys[q - 1] != skeys[q]) return;
   b.stem_total = b.off[b.n];
-  const Rec x0 = rec_s[p], x = rec_s[q];
-  const bool same = x.hlo == x0.hlo && (x.lu & 0xFFFFFFu) == (x0.lu & 0xFFFFFFu) &&  // hash, length, unit
-                    key_equal(key_of(b, x), key_of(b, x0));
+  const Rec x = rec_s[q], y = rec_s[q - 1];
+  const uint32_t r = rid[q];
+  const bool same = x.hlo == y.hlo && (x.lu & 0xFFFFFFu) == (y.lu & 0xFFFFFFu) &&  // hash, length, unit
+                    key_equal(key_of(b, x), key_of(b, y));
   if (!same) {
-    if (!(atomicOr(&run_flags[r], RUN_MULTI) & RUN_MULTI)) defer[atomicAdd(defer_n, 1u)] = p;
-  } else if (run_start[r + 1] - p >= LONG_RUN) {
+    if (!(atomicOr(&run_flags[r], RUN_MULTI) & RUN_MULTI)) defer[atomicAdd(defer_n, 1u)] = r;
+  } else {
     const uint32_t d = div_of(rec_unit(x));
-    if (x0.now / d != x.now / d) atomicOr(&run_flags[r], RUN_SLOW);
+    if (x.now / d != y.now / d) atomicOr(&run_flags[r], RUN_SLOW);
   }
 }
 
@@ -1477,7 +1490,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
           replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, im.cur(), im.prev(), L, acc, err, restore);
         }
       } else if (!(s0 < 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_TABLE_FULL))) {
-        defer[atomicAdd(defer_n, 1u)] = p;
+        defer[atomicAdd(defer_n, 1u)] = r;
       }
     }
   }
@@ -1582,6 +1595,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
                                                       const uint32_t* __restrict__ skeys,
                                                       const uint32_t* __restrict__ svals,
                                                       unsigned long long* __restrict__ res,
+                                                      const uint32_t* __restrict__ run_start,
                                                       const uint32_t* __restrict__ defer, const uint32_t* defer_n,
                                                       uint8_t* __restrict__ repid, unsigned long long* stats,
                                                       unsigned long long* stripes, uint32_t* err, int restore) {
@@ -1601,10 +1615,9 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
   // Grid-stride over the deferred runs: the grid is small and fixed (deferrals
   // are rare), so an empty deferral list costs one short launch.
   for (uint32_t di = blockIdx.x * 256 + threadIdx.x; di < s_n; di += gridDim.x * 256) {
-    const uint32_t p = defer[di];
+    const uint32_t rr = defer[di];  // run id
+    const uint32_t p = run_start[rr], end = run_start[rr + 1];
     const uint32_t key = skeys[p];
-    uint32_t end = p + 1;
-    while (end < b.n && skeys[end] == key) end++;
     // ---- split the run into distinct stems (hash, then bytes)
     uint32_t rep[MAX_REPS];
     uint32_t umask[MAX_REPS];
@@ -1820,24 +1833,24 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, uint32_t epoch, hipStre
   if (ev) (void)hipEventRecord(ev[0], st);
   if (g0)
     k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.keys[0], s.vals[0], s.err, s.time_floor, s.defer_n, s.os_ghist,
-                                  s.os_ctr);
+                                  s.os_ctr, s.run_flags);
   if (ev) (void)hipEventRecord(ev[1], st);
   if (b.n) {
-    const uint32_t ntiles = cdiv(b.n, RS_TILE);
+    const uint32_t ntiles = cdiv(b.n, OS_TILE);
     k_os_hist<<<ntiles < 256 ? ntiles : 256, 256, 0, st>>>(s.keys[0], b.n, s.os_ghist, s.err);
     for (uint32_t pass = 0; pass < 4; pass++) {
       const uint32_t src = pass & 1, dst = src ^ 1;
-      k_os_pass<<<ntiles, 256, 0, st>>>(s.keys[src], s.vals[src], s.keys[dst], s.vals[dst], b.n, pass, s.os_ghist,
+      k_os_pass<<<ntiles, OS_THREADS, 0, st>>>(s.keys[src], s.vals[src], s.keys[dst], s.vals[dst], b.n, pass, s.os_ghist,
                                         s.os_ctr, s.os_status, os_tag(epoch, pass), s.err);
     }
   }
   if (ev) (void)hipEventRecord(ev[2], st);
   if (b.n) {
-    const uint32_t nt = cdiv(b.n, SEG_TILE), g = cdiv(b.n, 256);
+    const uint32_t nt = cdiv(b.n, SEG_TILE);
     k_segment<<<nt, 256, 0, st>>>(s.rec, s.keys[0], s.vals[0], b.n, s.rec_s, s.segsum, s.rid, s.run_start,
-                                  s.run_flags, s.num_runs, s.os_ctr + 4, s.seg_status, os_tag(epoch, 0), s.err);
-    k_run_check<<<g, 256, 0, st>>>(b, s.rec_s, s.rid, s.run_start, s.run_flags, s.defer, s.defer_n,
-                                   s.err);
+                                  s.num_runs, s.os_ctr + 4, s.seg_status, os_tag(epoch, 0), s.err);
+    k_run_check<<<cdiv(b.n, 256), 256, 0, st>>>(b, s.rec_s, s.keys[0], s.rid, s.run_flags, s.defer, s.defer_n,
+                                                s.err);
   }
 }
 
@@ -1857,7 +1870,7 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     (void)hipEventRecord(go, st);
     (void)hipStreamWaitEvent(side, go, 0);
     k_runs_general<<<g < RUNS_GENERAL_BLOCKS ? g : RUNS_GENERAL_BLOCKS, 256, lds, side>>>(
-        b, t, P, s.rec_s, s.keys[0], s.vals[0], s.res, s.defer, s.defer_n, s.repid, o.stats, s.stripes,
+        b, t, P, s.rec_s, s.keys[0], s.vals[0], s.res, s.run_start, s.defer, s.defer_n, s.repid, o.stats, s.stripes,
         s.errb, restore);
     (void)hipEventRecord(side_done, side);
     if (ev) (void)hipEventRecord(ev[3], st);
@@ -1867,7 +1880,7 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     if (ev) (void)hipEventRecord(ev[4], st);
     // stems k_runs found under several units in the table (rare)
     k_runs_general<<<RUNS_GENERAL_LATE_BLOCKS, 256, lds, st>>>(b, t, P, s.rec_s, s.keys[0], s.vals[0],
-                                                                s.res, s.defer2, s.defer2_n, s.repid, o.stats,
+                                                                s.res, s.run_start, s.defer2, s.defer2_n, s.repid, o.stats,
                                                                 s.stripes, s.errb, restore);
     (void)hipStreamWaitEvent(st, side_done, 0);
     if (!restore) {
