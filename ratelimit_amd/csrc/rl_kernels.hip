@@ -674,14 +674,15 @@ __device__ inline bool img_key_equal(const SlotImg& im, const Key& key, const ui
 }
 
 // find_slot with insert, returning the slot's image (a fresh slot's image for
-// an insert: empty windows, no flags).
+// an insert: empty windows, no flags). `im` holds the home slot's image on
+// entry (the caller issues that load early, beside the stem's).
 __device__ int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint64_t tag, const Key& key, uint32_t unit,
                                  bool* inserted, SlotImg& im, uint32_t* err) {
   uint64_t i = hstem >> t.shift;
   int64_t tomb = -1;
   *inserted = false;
   for (uint32_t p = 0; p < t.max_probe; p++, i = (i + 1) & t.mask) {
-    load_img(&t.slots[i], im);
+    if (p) load_img(&t.slots[i], im);
     const uint64_t st = im.tag();
     if (st == tag) {
       if (img_key_equal(im, key, t.arena)) return (int64_t)i;
@@ -1014,16 +1015,18 @@ __device__ __attribute__((always_inline)) inline void replay_simple(const Rec* r
                                                                     unsigned long long* res, const TableDev& t,
                                                                     const Params& P, const uint8_t* repid,
                                                                     uint32_t p, uint32_t end, uint32_t k, int64_t s0,
-                                                                    Win cur0, Win prev0, LaneStats& L, StatAcc& acc,
-                                                                    uint32_t* err, bool restore) {
+                                                                    Win cur0, Win prev0, const Rec& x0, uint32_t e0,
+                                                                    LaneStats& L, StatAcc& acc, uint32_t* err,
+                                                                    bool restore) {
   Slot* s = &t.slots[s0];
   SimpleState S;
   S.cur = cur0;
   S.prev = prev0;
   S.cur_req = 0xFFFFFFFFu;
   S.pend = false;
-  for (uint32_t q = p; q < end; q++) {
-    if (repid && ((q == p) ? 0u : repid[q]) != k) continue;
+  simple_step(P, res, L, acc, S, load_elem(x0, e0, restore), restore, err);  // element p (always stem k)
+  for (uint32_t q = p + 1; q < end; q++) {
+    if (repid && repid[q] != k) continue;
     simple_step(P, res, L, acc, S, load_elem(rec_s[q], svals[q], restore), restore, err);
   }
   S.apply_pending();
@@ -1430,17 +1433,18 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
     const uint32_t p = run_start[r], end = run_start[r + 1];
     const uint32_t fl = run_flags[r];
     const Rec x0 = rec_s[p];
+    const uint32_t e0 = svals[p];
     const uint64_t h0 = ((uint64_t)skeys[p] << 32) | x0.hlo;
     const uint32_t u0 = rec_unit(x0);
+    SlotImg im;
+    load_img(&t.slots[h0 >> t.shift], im);  // home slot, in flight beside the stem
     const Key k0 = key_of(b, x0);
     if (!(fl & RUN_MULTI)) {  // RUN_MULTI runs belong to k_runs_general
       const bool long_run = !restore && end - p >= LONG_RUN && !(fl & RUN_SLOW);
       bool ok = true;
       int64_t s0 = -1;
-      SlotImg im;
       if (RL_ABL & 1) {
         s0 = (int64_t)(h0 >> t.shift);
-        load_img(&t.slots[s0], im);
       } else {
         bool ins;
         s0 = find_slot_img(t, h0, slot_tag(h0, u0), k0, u0, &ins, im, err);
@@ -1464,16 +1468,16 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
         // Parallel path: pick the window record once; k_fast_* decide every element.
         Slot* s = &t.slots[s0];
         Win cur = im.cur(), prev = im.prev();
-        const Elem e0 = load_elem(x0, svals[p], false);
-        const int which = window_pick(cur, prev, e0.w, 0, true);
+        const Elem el0 = load_elem(x0, e0, false);
+        const int which = window_pick(cur, prev, el0.w, 0, true);
         if (which < 0) {
           if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
         } else {
           const Win R = which ? prev : cur;
           // A record of window w was written inside w: its EXPIRE and local-cache
           // TTL both end at or after w + div, so they hold for the whole run.
-          const uint32_t c0 = e0.now <= R.expire ? R.count : 0u;
-          const uint32_t F = (P.lc_en && e0.now < R.lc) ? 1u : 0u;
+          const uint32_t c0 = el0.now <= R.expire ? R.count : 0u;
+          const uint32_t F = (P.lc_en && el0.now < R.lc) ? 1u : 0u;
           s->cur = cur;
           s->prev = prev;
           run_state[r] = make_uint4((uint32_t)s0, c0, R.lc, F | ((uint32_t)which << 1));
@@ -1487,7 +1491,8 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
           c.count += end - p;
           sl->cur = c;
         } else {
-          replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, im.cur(), im.prev(), L, acc, err, restore);
+          replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, im.cur(), im.prev(), x0, e0, L, acc, err,
+                        restore);
         }
       } else if (!(s0 < 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_TABLE_FULL))) {
         defer[atomicAdd(defer_n, 1u)] = r;
@@ -1662,8 +1667,9 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
         }
       }
       if (simple) {
-        replay_simple(rec_s, svals, res, t, P, repid, p, end, k, s0, t.slots[s0].cur, t.slots[s0].prev, L, acc, err,
-                      restore);
+        // (the run's stem k starts at rep[k], not necessarily at p)
+        replay_simple(rec_s, svals, res, t, P, repid, rep[k], end, k, s0, t.slots[s0].cur, t.slots[s0].prev,
+                      rec_s[rep[k]], svals[rep[k]], L, acc, err, restore);
       } else {
         GeneralState G;
         G.present = 0;
