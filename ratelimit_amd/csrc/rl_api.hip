@@ -251,13 +251,15 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
        dalloc(&s.rid, n) == hipSuccess && dalloc(&s.run_start, (size_t)n + 1) == hipSuccess &&
        dalloc(&s.run_flags, n) == hipSuccess && dalloc(&s.run_state, n) == hipSuccess &&
        dalloc(&s.run_f, n) == hipSuccess && dalloc(&s.num_runs, 1) == hipSuccess;
+  ok = ok && dalloc(&s.run_end, n) == hipSuccess &&
+       dalloc(&s.part_info, 256ull * std::max((n + PART_TILE - 1) / PART_TILE, 1u)) == hipSuccess;
   return ok;
 }
 
 void free_buffer(Scratch& s) {
   void* bufs[] = {s.rec, s.rec_s, s.res, s.seg_status, s.os_ghist, s.os_ctr, s.os_status, s.keys[0], s.keys[1], s.vals[0], s.vals[1], s.hist,
                   s.hist_tot, s.repid, s.defer, s.defer_n, s.defer2, s.defer2_n, s.tile_f, s.tile_s, s.tile_h, s.hits_s, s.segsum, s.rid,
-                  s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs};
+                  s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs, s.run_end, s.part_info};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
 }
@@ -316,6 +318,8 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   if (cfg.table_slots & (cfg.table_slots - 1)) return fail("gpu: table_slots must be a power of two", nullptr);
   if (!cfg.arena_bytes) cfg.arena_bytes = 64ull << 20;
   if (!cfg.max_batch) cfg.max_batch = 1u << 20;
+  if (cfg.max_batch > MAX_PART_TILES * PART_TILE)
+    return fail("gpu: max_batch must be at most 8388608 descriptors", nullptr);
   if (!cfg.max_requests) cfg.max_requests = cfg.max_batch;
   if (!cfg.max_rules) cfg.max_rules = 65536;
   if (!cfg.max_stem_bytes) cfg.max_stem_bytes = 128u * cfg.max_batch;

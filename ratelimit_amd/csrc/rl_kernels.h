@@ -21,8 +21,17 @@ constexpr uint32_t RS_TILE = 256 * RS_ITEMS;
 constexpr uint32_t OS_ITEMS = RL_OS_ITEMS, OS_WAVES = RL_OS_WAVES, OS_THREADS = 64 * OS_WAVES;
 constexpr uint32_t OS_TILE = OS_THREADS * OS_ITEMS;
 static_assert(OS_WAVES >= 4, "256 digits need at least 256 threads");
-constexpr uint32_t SEG_ITEMS = 16;
+#ifndef RL_OS_LB
+#define RL_OS_LB 8
+#endif
+constexpr uint32_t OS_LB = RL_OS_LB;  // look-back granules loaded per round trip
+#ifndef RL_SEG_ITEMS
+#define RL_SEG_ITEMS 16
+#endif
+constexpr uint32_t SEG_ITEMS = RL_SEG_ITEMS;  // 64-position chunks per wave (4 waves per tile)
 constexpr uint32_t SEG_TILE = 256 * SEG_ITEMS;
+constexpr uint32_t PART_ITEMS = 16, PART_TILE = 256 * PART_ITEMS;  // k_part: 256 threads x PART_ITEMS
+constexpr uint32_t MAX_PART_TILES = 2048;  // k_part tiles per batch (max_batch <= 2048 x 4096)
 constexpr uint32_t LONG_RUN = 32;        // runs at least this long take the parallel path
 constexpr uint32_t RUN_SLOW = 1, RUN_FAST = 2, RUN_MULTI = 4;
 constexpr uint32_t KEY_HEAD = 64;         // stem bytes carried inline (zero-padded) per descriptor
@@ -139,7 +148,9 @@ struct Scratch {
   uint32_t* hits_s;                    // [n] raw hits, sorted order
   uint32_t* segsum;                    // [n] inclusive in-run sum of hits
   uint32_t* rid;                       // [n] run id
-  uint32_t* run_start;                 // [n+1]
+  uint32_t* run_start;                 // [n] first sorted position of run r
+  uint32_t* run_end;                   // [n] one past its last
+  uint32_t* part_info;                 // [256 x part tiles] k_part: offset << 16 | count per digit and tile
   uint32_t* run_flags;                 // [n] RUN_*
   uint4* run_state;                    // [n] {slot, c0, old lc, F | which<<1}
   uint32_t* run_f;                     // [n] first over-limit position

@@ -42,14 +42,17 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
                                                  uint32_t* __restrict__ vals, uint32_t* err,
                                                  const int64_t* time_floor, uint32_t* defer_n,
                                                  uint32_t* __restrict__ os_ghist, uint32_t* __restrict__ os_ctr,
-                                                 uint32_t* __restrict__ run_flags) {
+                                                 uint32_t* __restrict__ run_flags, uint32_t* num_runs) {
   __shared__ uint32_t lds[HASH_LDS_BYTES / 4 + 4];
   const uint32_t tid = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + tid;
   uint32_t bad = 0;
-  if (i < b.n) run_flags[i] = 0;  // k_segment ORs run flags in from any tile
-  if (blockIdx.x == 0) {  // per-batch counters: RUN_MULTI queue, sort digit totals and tile tickets
-    if (tid == 0) *defer_n = 0;
+  if (i < b.n) run_flags[i] = 0;  // k_run_check ORs run flags in from any block
+  if (blockIdx.x == 0) {  // per-batch counters: RUN_MULTI queue, run ids, digit totals and tile tickets
+    if (tid == 0) {
+      *defer_n = 0;
+      *num_runs = 0;
+    }
     if (tid < 5) os_ctr[tid] = 0;  // [0..3] sort passes, [4] k_segment
 #pragma unroll
     for (uint32_t p = 0; p < 4; p++) os_ghist[p * 256 + tid] = 0;
@@ -361,21 +364,37 @@ __global__ __launch_bounds__(OS_THREADS) void k_os_pass(const uint32_t* __restri
       if (lane >= off) inc += y;
     }
     if (lane == 63) gsum[wave] = inc;
-    // decoupled look-back: add earlier tiles' counts until an inclusive prefix
+    // decoupled look-back: add earlier tiles' counts until an inclusive prefix.
+    // OS_LB granules (tiles j, j-1, ...) are loaded together per round trip;
+    // the ready prefix of them is consumed (an aggregate is a final tile count,
+    // so a partial window is exact) and the walk resumes below it.
     uint32_t excl = 0;
     if (tile) {
-      uint32_t j = tile - 1;
+      int32_t j = (int32_t)tile - 1;
       for (;;) {
-        const unsigned long long v =
-            __hip_atomic_load(status + (size_t)j * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t tg = (uint32_t)(v >> 32);
-        if ((tg & ~3u) != tag) {  // not yet published for this pass
-          __builtin_amdgcn_s_sleep(1);
-          continue;
+        unsigned long long v[OS_LB];
+#pragma unroll
+        for (uint32_t k = 0; k < OS_LB; k++)
+          v[k] = j - (int32_t)k >= 0 ? __hip_atomic_load(status + (size_t)(j - (int32_t)k) * 256 + tid,
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : 0ull;
+        uint32_t add = 0, used = 0;
+        bool stop = false, done = false;
+#pragma unroll
+        for (uint32_t k = 0; k < OS_LB; k++) {
+          const uint32_t tg = (uint32_t)(v[k] >> 32);
+          if (stop || (tg & ~3u) != tag) {  // not yet published for this pass
+            stop = true;
+            continue;
+          }
+          add += (uint32_t)v[k];
+          used++;
+          if (tg & OS_INC) stop = done = true;  // tile 0 is inclusive, so j never passes it
         }
-        excl += (uint32_t)v;
-        if (tg & OS_INC) break;
-        --j;  // tile 0 publishes an inclusive count, so j stays >= 0
+        excl += add;
+        if (done) break;
+        j -= (int32_t)used;
+        if (!used) __builtin_amdgcn_s_sleep(1);
       }
       __hip_atomic_store(mine, (unsigned long long)(excl + c) | ((unsigned long long)(tag | OS_INC) << 32),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1017,7 +1036,7 @@ __device__ __attribute__((always_inline)) inline void replay_simple(const Rec* r
                                                                     uint32_t p, uint32_t end, uint32_t k, int64_t s0,
                                                                     Win cur0, Win prev0, const Rec& x0, uint32_t e0,
                                                                     LaneStats& L, StatAcc& acc, uint32_t* err,
-                                                                    bool restore) {
+                                                                    bool restore, const SlotImg* img = nullptr) {
   Slot* s = &t.slots[s0];
   SimpleState S;
   S.cur = cur0;
@@ -1030,8 +1049,14 @@ __device__ __attribute__((always_inline)) inline void replay_simple(const Rec* r
     simple_step(P, res, L, acc, S, load_elem(rec_s[q], svals[q], restore), restore, err);
   }
   S.apply_pending();
-  s->cur = S.cur;
-  s->prev = S.prev;
+  if (img) {  // random writes are the costly part of the probe: store only records that changed
+    const uint4 c = img->v[1], q = img->v[2];
+    if (S.cur.ws != c.x || S.cur.count != c.y || S.cur.expire != c.z || S.cur.lc != c.w) s->cur = S.cur;
+    if (S.prev.ws != q.x || S.prev.count != q.y || S.prev.expire != q.z || S.prev.lc != q.w) s->prev = S.prev;
+  } else {
+    s->cur = S.cur;
+    s->prev = S.prev;
+  }
 }
 
 // ===========================================================================
@@ -1375,6 +1400,517 @@ __global__ __launch_bounds__(256) void k_segment(const Rec* __restrict__ rec, co
   }
 }
 
+// ===========================================================================
+// Grouping by MSD partition + per-bucket LDS sort (stage A).
+//
+// k_part: every PART_TILE tile of (sort key, index) pairs, in arrival order, is
+// stably partitioned by the key's top byte into its own tile region (one
+// wave-ballot multisplit rank, coalesced digit segments), and publishes per
+// digit its (offset, count) in the tile and the digit total. No look-back:
+// bucket d is the concatenation, in tile (= arrival) order, of every tile's
+// digit-d segment.
+// k_bucket: one 1024-thread workgroup per top byte. It gathers its bucket,
+// stably sorts it by key bits [0, 24) (three 8-bit multisplit passes in LDS;
+// buckets larger than BK_CAP run the same passes chunk by chunk through HBM),
+// so the batch ends up sorted by the full key with arrival order kept within
+// equal keys. It then segments the bucket in place (runs never cross buckets):
+// records into sorted order, in-run inclusive sums of max(1, hits), run ids
+// and [run_start, run_end). Run ids are allocated per bucket from one atomic
+// counter, contiguous and in sorted order within a bucket.
+// ===========================================================================
+constexpr uint32_t BK_WAVES = 16, BK_THREADS = 64 * BK_WAVES, BK_ITEMS = 8, BK_CAP = BK_THREADS * BK_ITEMS;
+constexpr uint32_t BK_STRIP = 64 * BK_ITEMS;  // positions per wave in a chunk
+
+// Wave-ballot multisplit: rank of each item among the wave's earlier items with
+// the same digit, against a wave-private running count row in LDS (item-major
+// order: item i of lane l precedes item i of lane l+1 and item i+1 of lane 0).
+template <uint32_t IT>
+__device__ inline void wave_multisplit(const uint32_t (&kk)[IT], uint32_t nvalid_base, uint32_t limit, uint32_t shift,
+                                       uint32_t* row, uint32_t (&pos)[IT]) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t lt_mask = (1ull << lane) - 1;
+  uint32_t leader[IT];
+  // The digit group leaders add to the row with returning LDS atomics, issued
+  // back to back for all items (LDS applies them in order), then every lane
+  // fetches its leader's old count.
+#pragma unroll
+  for (uint32_t i = 0; i < IT; i++) {
+    const bool valid = nvalid_base + i * 64 + lane < limit;
+    const uint32_t d = (kk[i] >> shift) & 255u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (uint32_t bit = 0; bit < 8; bit++) {
+      const bool sb = (d >> bit) & 1u;
+      const uint64_t bal = __ballot(sb);
+      peers &= sb ? bal : ~bal;
+    }
+    const uint32_t rank = __popcll(peers & lt_mask);
+    leader[i] = valid ? (uint32_t)(__ffsll((unsigned long long)peers) - 1) : lane;
+    pos[i] = (valid && rank == 0) ? atomicAdd(&row[d], (uint32_t)__popcll(peers)) : 0u;
+    pos[i] |= rank << 16;  // rank < 64; old counts < 2^16 (at most BK_CAP / PART_TILE)
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < IT; i++) pos[i] = __shfl(pos[i] & 0xFFFFu, leader[i]) + (pos[i] >> 16);
+}
+
+// Exclusive scan of one value per thread over threads [0, 256) (waves 0..3);
+// every thread of the block must call it. *total = sum of the 256 values.
+__device__ inline uint32_t scan256(uint32_t v, uint32_t* wsum4, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (uint32_t off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += y;
+  }
+  if (wave < 4 && lane == 63) wsum4[wave] = inc;
+  __syncthreads();
+  uint32_t pre = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < 4; w++) pre += w < wave ? wsum4[w] : 0u;
+  if (total) *total = wsum4[0] + wsum4[1] + wsum4[2] + wsum4[3];
+  __syncthreads();
+  return pre + inc - v;
+}
+
+__global__ __launch_bounds__(256) void k_part(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                              uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, uint32_t n,
+                                              uint32_t ntiles, uint32_t* __restrict__ info, uint32_t* __restrict__ tot,
+                                              const uint32_t* err) {
+  __shared__ uint32_t wcnt[4][256];
+  __shared__ uint32_t dbase[256];
+  __shared__ uint32_t wsum[4];
+  if (*err) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, tile = blockIdx.x;
+  wcnt[0][tid] = 0; wcnt[1][tid] = 0; wcnt[2][tid] = 0; wcnt[3][tid] = 0;
+  __syncthreads();
+  const uint32_t wbase = tile * PART_TILE + wave * 64 * PART_ITEMS;
+  uint32_t kk[PART_ITEMS], vv[PART_ITEMS], pos[PART_ITEMS];
+#pragma unroll
+  for (uint32_t i = 0; i < PART_ITEMS; i++) {
+    const uint32_t j = wbase + i * 64 + lane;
+    kk[i] = j < n ? kin[j] : 0xFFFFFFFFu;
+    vv[i] = j < n ? vin[j] : 0u;
+  }
+  wave_multisplit(kk, wbase, n, 24, wcnt[wave], pos);
+  __syncthreads();
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < 4; w++) {
+    const uint32_t t = wcnt[w][tid];
+    wcnt[w][tid] = c;
+    c += t;
+  }
+  const uint32_t excl = scan256(c, wsum, nullptr);
+  dbase[tid] = excl;
+  info[(size_t)tid * ntiles + tile] = (excl << 16) | c;
+  if (c) atomicAdd(&tot[tid], c);
+  __syncthreads();
+#pragma unroll
+  for (uint32_t i = 0; i < PART_ITEMS; i++) {
+    if (wbase + i * 64 + lane < n) {
+      const uint32_t d = kk[i] >> 24;
+      const uint32_t p = tile * PART_TILE + dbase[d] + wcnt[wave][d] + pos[i];
+      kout[p] = kk[i];
+      vout[p] = vv[i];
+    }
+  }
+}
+
+#ifdef RL_BK_PROF  // bucketbench only: per-bucket phase stamps
+__device__ unsigned long long g_bk_prof[256 * 16];
+#define BK_STAMP(k) \
+  if (threadIdx.x == 0) g_bk_prof[blockIdx.x * 16 + (k)] = wall_clock64()
+#else
+#define BK_STAMP(k)
+#endif
+
+// LDS of one k_bucket workgroup.
+struct BucketLds {
+  uint32_t k[BK_CAP], v[BK_CAP];      // the bucket (fast path) in sorted order
+  uint32_t wcnt[BK_WAVES][256];       // multisplit rows
+  uint32_t seg[MAX_PART_TILES + 1];   // bucket position where each tile's segment starts
+  uint32_t src[MAX_PART_TILES];       // tile-layout index of a segment's element = src[t] + position
+  uint32_t base[256];                 // digit offsets: chunk-local (fast) / running in the bucket (slow)
+  uint32_t roff[3][256];              // slow path: running digit offsets per pass
+  uint32_t dtot[256];
+  uint32_t gsum[4][256];              // bucket_rank: digit counts per group of 4 waves
+  uint32_t wsum[BK_WAVES];
+  SegPair sp[BK_WAVES];
+  uint32_t sh[BK_WAVES];
+  SegPair carry;
+  uint32_t hcarry, rb, nruns;
+};
+
+// Bucket positions -> indices in the tile layout: for each item the last tile
+// t with seg[t] <= p (a segment holding p), by a fixed-depth search whose
+// levels visit all items together (independent LDS reads in flight).
+template <uint32_t IT>
+__device__ inline void bucket_src(const BucketLds& L, uint32_t ntiles, const uint32_t (&p)[IT], uint32_t (&j)[IT]) {
+  uint32_t lo[IT];
+#pragma unroll
+  for (uint32_t i = 0; i < IT; i++) lo[i] = 0;
+#pragma unroll
+  for (uint32_t step = MAX_PART_TILES / 2; step; step >>= 1) {
+#pragma unroll
+    for (uint32_t i = 0; i < IT; i++) {
+      const uint32_t m = lo[i] + step;
+      if (m < ntiles && L.seg[m] <= p[i]) lo[i] = m;
+    }
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < IT; i++) j[i] = L.src[lo[i]] + p[i];
+}
+
+// Rank one chunk (BK_ITEMS per lane, wave-strip layout) by digit [shift, shift+8):
+// pos = L.base[d] + (earlier waves' count of d) + rank in the wave. With
+// chunk_scan, L.base becomes the chunk's own exclusive digit offsets first.
+// L.dtot = the chunk's digit counts. Ends with a barrier.
+__device__ inline void bucket_rank(BucketLds& L, const uint32_t (&kk)[BK_ITEMS], uint32_t strip0, uint32_t limit,
+                                   uint32_t shift, bool chunk_scan, uint32_t (&pos)[BK_ITEMS]) {
+  const uint32_t tid = threadIdx.x, wave = tid >> 6;
+  for (uint32_t j = tid; j < BK_WAVES * 256; j += BK_THREADS) (&L.wcnt[0][0])[j] = 0;
+  __syncthreads();
+  if (shift == 0 && chunk_scan) BK_STAMP(8);
+  uint32_t local[BK_ITEMS];
+  wave_multisplit(kk, strip0, limit, shift, L.wcnt[wave], local);
+  __syncthreads();
+  if (shift == 0 && chunk_scan) BK_STAMP(9);
+  // per digit, exclusive offsets over the 16 wave rows: thread (g, d) scans rows
+  // 4g..4g+3 of digit d, then adds the totals of the groups before g
+  constexpr uint32_t G = BK_WAVES / 4;
+  const uint32_t dg = tid & 255u, g = tid >> 8;
+  uint32_t r[G], c = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < G; w++) r[w] = L.wcnt[g * G + w][dg];
+#pragma unroll
+  for (uint32_t w = 0; w < G; w++) {
+    const uint32_t t = r[w];
+    r[w] = c;
+    c += t;
+  }
+  L.gsum[g][dg] = c;
+  __syncthreads();
+  uint32_t pre = 0, all = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) {
+    const uint32_t t = L.gsum[q][dg];
+    pre += q < g ? t : 0u;
+    all += t;
+  }
+#pragma unroll
+  for (uint32_t w = 0; w < G; w++) L.wcnt[g * G + w][dg] = r[w] + pre;
+  if (tid < 256) L.dtot[tid] = all;
+  const uint32_t excl = scan256(tid < 256 ? all : 0u, L.wsum, nullptr);
+  if (chunk_scan && tid < 256) L.base[tid] = excl;
+  __syncthreads();
+  if (shift == 0 && chunk_scan) BK_STAMP(10);
+#pragma unroll
+  for (uint32_t i = 0; i < BK_ITEMS; i++) {
+    const uint32_t d = (kk[i] >> shift) & 255u;
+    pos[i] = L.base[d] + L.wcnt[wave][d] + local[i];
+  }
+  __syncthreads();
+  if (shift == 0 && chunk_scan) BK_STAMP(11);
+}
+
+// Wave-sum of v over the block (all threads call); result in every thread.
+__device__ inline uint32_t block_sum(BucketLds& L, uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (uint32_t off = 32; off; off >>= 1) v += __shfl_xor(v, off, 64);
+  if (lane == 0) L.wsum[wave] = v;
+  __syncthreads();
+  uint32_t s = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < BK_WAVES; w++) s += L.wsum[w];
+  __syncthreads();
+  return s;
+}
+
+// Segment the sorted bucket [0, S) (keys/values from LDS or from the sorted
+// global arrays at base): records into sorted order, in-run sums, run ids and
+// run bounds. Chunks of BK_CAP positions; each wave walks its strip of the
+// chunk in 64-position pieces, and the 16 wave aggregates plus the carry of
+// the earlier chunks give every wave its exclusive prefix.
+template <bool FROM_LDS>
+__device__ inline void bucket_segment(BucketLds& L, uint32_t S, uint32_t base, const uint32_t* __restrict__ sk,
+                                      const uint32_t* __restrict__ sv, const Rec* __restrict__ rec,
+                                      Rec* __restrict__ rec_s, uint32_t* __restrict__ segsum,
+                                      uint32_t* __restrict__ rid, uint32_t* __restrict__ run_start,
+                                      uint32_t* __restrict__ run_end, uint32_t* num_runs) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  auto key = [&](uint32_t p) -> uint32_t { return FROM_LDS ? L.k[p] : sk[base + p]; };
+  auto val = [&](uint32_t p) -> uint32_t { return FROM_LDS ? L.v[p] : sv[base + p]; };
+  // runs of the bucket -> run id base
+  uint32_t nh = 0;
+  for (uint32_t c0 = 0; c0 < S; c0 += BK_CAP) {
+    uint32_t a[BK_ITEMS], b[BK_ITEMS];
+#pragma unroll
+    for (uint32_t i = 0; i < BK_ITEMS; i++) {  // loads first, BK_ITEMS pairs in flight
+      const uint32_t p = c0 + i * BK_THREADS + tid;
+      a[i] = p < S && p ? key(p - 1) : 0u;
+      b[i] = p < S && p ? key(p) : 1u;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < BK_ITEMS; i++) nh += (c0 + i * BK_THREADS + tid < S && a[i] != b[i]) ? 1u : 0u;
+  }
+  nh = block_sum(L, nh);
+  BK_STAMP(4);
+  if (tid == 0) {
+    L.rb = atomicAdd(num_runs, nh);
+    L.nruns = nh;
+    L.carry = SegPair{0, 0};
+    L.hcarry = 0;
+  }
+  __syncthreads();
+  const uint32_t rb = L.rb;
+  for (uint32_t c0 = 0; c0 < S; c0 += BK_CAP) {
+    const uint32_t s0 = c0 + wave * BK_STRIP;
+    SegChunk ch[BK_ITEMS];
+    SegPair agg{0, 0};
+    uint32_t hc = 0;
+    bool hd[BK_ITEMS];
+    uint32_t hvs[BK_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < BK_ITEMS; j++) {  // gathers first (all in flight), scans after
+      const uint32_t q = s0 + 64 * j + lane;
+      hd[j] = false;
+      hvs[j] = 0;
+      if (q < S) {
+        const uint32_t kq = key(q);
+        hd[j] = q == 0 || key(q - 1) != kq;
+        const Rec r = rec[val(q)];
+        rec_s[base + q] = r;
+        hvs[j] = r.hits > 1 ? r.hits : 1u;
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < BK_ITEMS; j++) {
+      const bool head = hd[j];
+      const uint32_t hv = hvs[j];
+      ch[j] = SegChunk{(uint64_t)__ballot(head), hv};
+      uint32_t t = hv;  // piece total, segmented: sum after the last head
+      const uint32_t lh = ch[j].heads ? 63u - (uint32_t)__clzll((long long)ch[j].heads) : 0u;
+      if (ch[j].heads && lane < lh) t = 0;
+#pragma unroll
+      for (uint32_t off = 32; off; off >>= 1) t += __shfl_xor(t, off, 64);
+      agg = seg_op(agg, SegPair{ch[j].heads ? 1u : 0u, t});
+      hc += (uint32_t)__popcll(ch[j].heads);
+    }
+    if (lane == 0) {
+      L.sp[wave] = agg;
+      L.sh[wave] = hc;
+    }
+    __syncthreads();
+    SegPair run = L.carry;
+    uint32_t hrun = L.hcarry;
+    SegPair tot = run;
+    uint32_t htot = hrun;
+    for (uint32_t w = 0; w < BK_WAVES; w++) {
+      if (w == wave) {
+        run = tot;
+        hrun = htot;
+      }
+      tot = seg_op(tot, L.sp[w]);
+      htot += L.sh[w];
+    }
+    __syncthreads();
+    if (tid == 0) {
+      L.carry = tot;
+      L.hcarry = htot;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < BK_ITEMS; j++) {
+      const uint32_t q = s0 + 64 * j + lane;
+      const SegPair v = seg_chunk_scan(ch[j], lane);
+      const SegPair in = seg_op(run, v);
+      const uint64_t heads = ch[j].heads;
+      const uint32_t r = hrun + (uint32_t)__popcll(heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1))) - 1;
+      if (q < S) {
+        segsum[base + q] = in.s;
+        rid[base + q] = rb + r;
+        if ((heads >> lane) & 1) {
+          run_start[rb + r] = base + q;
+          if (r) run_end[rb + r - 1] = base + q;
+        }
+      }
+      run = seg_op(run, SegPair{__shfl(v.f, 63, 64), __shfl(v.s, 63, 64)});
+      hrun += (uint32_t)__popcll(heads);
+    }
+    __syncthreads();  // carry
+  }
+  if (tid == 0 && S) run_end[rb + L.nruns - 1] = base + S;
+}
+
+__global__ __launch_bounds__(BK_THREADS) void k_bucket(const uint32_t* __restrict__ pk, const uint32_t* __restrict__ pv,
+                                                       const uint32_t* __restrict__ info,
+                                                       const uint32_t* __restrict__ tot, uint32_t ntiles,
+                                                       const Rec* __restrict__ rec, uint32_t* __restrict__ sk,
+                                                       uint32_t* __restrict__ sv, Rec* __restrict__ rec_s,
+                                                       uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
+                                                       uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end,
+                                                       uint32_t* num_runs, const uint32_t* err) {
+  __shared__ BucketLds L;
+  __shared__ uint32_t s_base, s_S;
+  if (*err) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, d = blockIdx.x;
+  BK_STAMP(0);
+  {  // bucket position in the sorted batch
+    const uint32_t v = tid < 256 ? tot[tid] : 0u;
+    const uint32_t excl = scan256(v, L.wsum, nullptr);
+    if (tid == d) {
+      s_base = excl;
+      s_S = v;
+    }
+    __syncthreads();
+  }
+  const uint32_t base = s_base, S = s_S;
+  if (!S) return;
+  // tile segments of the bucket: starts (exclusive scan of the counts) and sources
+  for (uint32_t t0 = 0; t0 < ntiles; t0 += BK_THREADS) {
+    const uint32_t t = t0 + tid;
+    const uint32_t e = t < ntiles ? info[(size_t)d * ntiles + t] : 0u;
+    const uint32_t cnt = e & 0xFFFFu;
+    uint32_t inc = cnt;
+#pragma unroll
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(inc, off, 64);
+      if (lane >= off) inc += y;
+    }
+    if (lane == 63) L.wsum[wave] = inc;
+    __syncthreads();
+    uint32_t pre = t0 ? L.seg[t0] : 0u;  // carried from the previous round
+    for (uint32_t w = 0; w < wave; w++) pre += L.wsum[w];
+    if (t < ntiles) {
+      const uint32_t st = pre + inc - cnt;
+      L.seg[t] = st;
+      L.src[t] = t * PART_TILE + (e >> 16) - st;
+    }
+    __syncthreads();
+    if (tid == BK_THREADS - 1 && t0 + BK_THREADS < ntiles) L.seg[t0 + BK_THREADS] = pre + inc;  // next round's carry
+    __syncthreads();
+  }
+  if (tid == 0) L.seg[ntiles] = S;
+  __syncthreads();
+  BK_STAMP(1);
+  uint32_t kk[BK_ITEMS], vv[BK_ITEMS], pos[BK_ITEMS];
+  if (S <= BK_CAP) {
+    // ---- fast path: the bucket lives in registers / LDS for all three passes
+    const uint32_t strip0 = wave * BK_STRIP;
+    uint32_t pp[BK_ITEMS], jj[BK_ITEMS];
+#pragma unroll
+    for (uint32_t i = 0; i < BK_ITEMS; i++) pp[i] = min(strip0 + i * 64 + lane, S - 1);
+    bucket_src(L, ntiles, pp, jj);
+#pragma unroll
+    for (uint32_t i = 0; i < BK_ITEMS; i++) {
+      const bool in = strip0 + i * 64 + lane < S;
+      kk[i] = in ? pk[jj[i]] : 0xFFFFFFFFu;
+      vv[i] = in ? pv[jj[i]] : 0u;
+    }
+    BK_STAMP(2);
+    for (uint32_t pass = 0; pass < 3; pass++) {
+      bucket_rank(L, kk, strip0, S, 8 * pass, true, pos);
+#pragma unroll
+      for (uint32_t i = 0; i < BK_ITEMS; i++) {
+        if (strip0 + i * 64 + lane < S) {
+          L.k[pos[i]] = kk[i];
+          L.v[pos[i]] = vv[i];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t i = 0; i < BK_ITEMS; i++) {
+        const uint32_t p = strip0 + i * 64 + lane;
+        if (p < S) {
+          kk[i] = L.k[p];
+          vv[i] = L.v[p];
+        }
+      }
+      if (pass == 0) BK_STAMP(12);
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < BK_ITEMS; i++) {
+      const uint32_t p = strip0 + i * 64 + lane;
+      if (p < S) {
+        sk[base + p] = kk[i];
+        sv[base + p] = vv[i];
+      }
+    }
+    __syncthreads();
+    BK_STAMP(3);
+    bucket_segment<true>(L, S, base, sk, sv, rec, rec_s, segsum, rid, run_start, run_end, num_runs);
+    BK_STAMP(5);
+    return;
+  }
+  // ---- large bucket: the same three stable passes, chunk by chunk through HBM
+  // (tile layout -> sk -> temp -> sk; temp = this bucket's rid / segsum ranges,
+  // which the segmentation overwrites afterwards). Running digit offsets per
+  // pass come from one histogram sweep.
+  for (uint32_t j = tid; j < 3 * 256; j += BK_THREADS) (&L.roff[0][0])[j] = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < S; c0 += BK_CAP) {
+    uint32_t pp[BK_ITEMS], jj[BK_ITEMS];
+#pragma unroll
+    for (uint32_t i = 0; i < BK_ITEMS; i++) pp[i] = min(c0 + i * BK_THREADS + tid, S - 1);
+    bucket_src(L, ntiles, pp, jj);
+#pragma unroll
+    for (uint32_t i = 0; i < BK_ITEMS; i++) kk[i] = pk[jj[i]];  // loads first, BK_ITEMS in flight
+#pragma unroll
+    for (uint32_t i = 0; i < BK_ITEMS; i++) {
+      if (c0 + i * BK_THREADS + tid < S) {
+        atomicAdd(&L.roff[0][kk[i] & 255u], 1u);
+        atomicAdd(&L.roff[1][(kk[i] >> 8) & 255u], 1u);
+        atomicAdd(&L.roff[2][(kk[i] >> 16) & 255u], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t pass = 0; pass < 3; pass++) {
+    const uint32_t v = tid < 256 ? L.roff[pass][tid] : 0u;
+    const uint32_t excl = scan256(v, L.wsum, nullptr);
+    if (tid < 256) L.roff[pass][tid] = excl;
+  }
+  __syncthreads();
+  for (uint32_t pass = 0; pass < 3; pass++) {
+    const uint32_t* ik = pass == 0 ? pk : pass == 1 ? sk + base : rid + base;
+    const uint32_t* iv = pass == 0 ? pv : pass == 1 ? sv + base : segsum + base;
+    uint32_t* ok = pass == 1 ? rid + base : sk + base;
+    uint32_t* ov = pass == 1 ? segsum + base : sv + base;
+    for (uint32_t c0 = 0; c0 < S; c0 += BK_CAP) {
+      const uint32_t strip0 = c0 + wave * BK_STRIP;
+      uint32_t pp[BK_ITEMS], jj[BK_ITEMS];
+#pragma unroll
+      for (uint32_t i = 0; i < BK_ITEMS; i++) pp[i] = min(strip0 + i * 64 + lane, S - 1);
+      if (pass == 0) {
+        bucket_src(L, ntiles, pp, jj);
+      } else {
+#pragma unroll
+        for (uint32_t i = 0; i < BK_ITEMS; i++) jj[i] = pp[i];
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < BK_ITEMS; i++) {
+        const bool in = strip0 + i * 64 + lane < S;
+        kk[i] = in ? ik[jj[i]] : 0xFFFFFFFFu;
+        vv[i] = in ? iv[jj[i]] : 0u;
+      }
+      if (tid < 256) L.base[tid] = L.roff[pass][tid];
+      bucket_rank(L, kk, strip0, S, 8 * pass, false, pos);
+      if (tid < 256) L.roff[pass][tid] += L.dtot[tid];
+#pragma unroll
+      for (uint32_t i = 0; i < BK_ITEMS; i++) {
+        if (strip0 + i * 64 + lane < S) {
+          ok[pos[i]] = kk[i];
+          ov[pos[i]] = vv[i];
+        }
+      }
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
+  bucket_segment<false>(L, S, base, sk, sv, rec, rec_s, segsum, rid, run_start, run_end, num_runs);
+}
+
 // Run checks against the predecessor (equality chains): a run must hold one
 // stem under one unit, else it is flagged RUN_MULTI and queued once (by run
 // id) for k_runs_general; a window change within a run makes a long run
@@ -1409,6 +1945,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
                                               const uint32_t* __restrict__ skeys,
                                               const uint32_t* __restrict__ svals, unsigned long long* __restrict__ res,
                                               const uint32_t* __restrict__ run_start,
+                                              const uint32_t* __restrict__ run_end,
                                               uint32_t* __restrict__ run_flags, uint4* __restrict__ run_state,
                                               uint32_t* __restrict__ run_f, const uint32_t* num_runs,
                                               uint32_t* __restrict__ defer, uint32_t* defer_n,
@@ -1430,7 +1967,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
   L.reset();
   const uint32_t r = blockIdx.x * 256 + threadIdx.x;
   if (r < s_nr) {
-    const uint32_t p = run_start[r], end = run_start[r + 1];
+    const uint32_t p = run_start[r], end = run_end[r];
     const uint32_t fl = run_flags[r];
     const Rec x0 = rec_s[p];
     const uint32_t e0 = svals[p];
@@ -1443,10 +1980,10 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
       const bool long_run = !restore && end - p >= LONG_RUN && !(fl & RUN_SLOW);
       bool ok = true;
       int64_t s0 = -1;
+      bool ins = false;
       if (RL_ABL & 1) {
         s0 = (int64_t)(h0 >> t.shift);
       } else {
-        bool ins;
         s0 = find_slot_img(t, h0, slot_tag(h0, u0), k0, u0, &ins, im, err);
         if (s0 < 0) {
           ok = false;
@@ -1492,7 +2029,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
           sl->cur = c;
         } else {
           replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, im.cur(), im.prev(), x0, e0, L, acc, err,
-                        restore);
+                        restore, ins ? nullptr : &im);
         }
       } else if (!(s0 < 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_TABLE_FULL))) {
         defer[atomicAdd(defer_n, 1u)] = r;
@@ -1543,6 +2080,7 @@ __global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules,
                                                    const uint32_t* __restrict__ segsum,
                                                    const uint32_t* __restrict__ rid,
                                                    const uint32_t* __restrict__ run_start,
+                                                   const uint32_t* __restrict__ run_end,
                                                    const uint32_t* __restrict__ run_flags,
                                                    const uint4* __restrict__ run_state,
                                                    const uint32_t* __restrict__ run_f, unsigned long long* stats,
@@ -1576,7 +2114,7 @@ __global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules,
       emit(res, L, acc, x, d);
       if (!masked) {
         const uint32_t nq = q + 1;
-        const bool last = nq == run_start[r + 1] || rec_s[nq].req > req_f;
+        const bool last = nq == run_end[r] || rec_s[nq].req > req_f;
         if (last) {  // the last INCRBY of the run leaves the key's state
           Win R;
           R.ws = x.w;
@@ -1601,6 +2139,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
                                                       const uint32_t* __restrict__ svals,
                                                       unsigned long long* __restrict__ res,
                                                       const uint32_t* __restrict__ run_start,
+                                                      const uint32_t* __restrict__ run_end,
                                                       const uint32_t* __restrict__ defer, const uint32_t* defer_n,
                                                       uint8_t* __restrict__ repid, unsigned long long* stats,
                                                       unsigned long long* stripes, uint32_t* err, int restore) {
@@ -1621,7 +2160,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
   // are rare), so an empty deferral list costs one short launch.
   for (uint32_t di = blockIdx.x * 256 + threadIdx.x; di < s_n; di += gridDim.x * 256) {
     const uint32_t rr = defer[di];  // run id
-    const uint32_t p = run_start[rr], end = run_start[rr + 1];
+    const uint32_t p = run_start[rr], end = run_end[rr];
     const uint32_t key = skeys[p];
     // ---- split the run into distinct stems (hash, then bytes)
     uint32_t rep[MAX_REPS];
@@ -1839,22 +2378,16 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, uint32_t epoch, hipStre
   if (ev) (void)hipEventRecord(ev[0], st);
   if (g0)
     k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.keys[0], s.vals[0], s.err, s.time_floor, s.defer_n, s.os_ghist,
-                                  s.os_ctr, s.run_flags);
+                                  s.os_ctr, s.run_flags, s.num_runs);
   if (ev) (void)hipEventRecord(ev[1], st);
-  if (b.n) {
-    const uint32_t ntiles = cdiv(b.n, OS_TILE);
-    k_os_hist<<<ntiles < 256 ? ntiles : 256, 256, 0, st>>>(s.keys[0], b.n, s.os_ghist, s.err);
-    for (uint32_t pass = 0; pass < 4; pass++) {
-      const uint32_t src = pass & 1, dst = src ^ 1;
-      k_os_pass<<<ntiles, OS_THREADS, 0, st>>>(s.keys[src], s.vals[src], s.keys[dst], s.vals[dst], b.n, pass, s.os_ghist,
-                                        s.os_ctr, s.os_status, os_tag(epoch, pass), s.err);
-    }
-  }
+  const uint32_t ptiles = cdiv(b.n, PART_TILE);
+  if (b.n) k_part<<<ptiles, 256, 0, st>>>(s.keys[0], s.vals[0], s.keys[1], s.vals[1], b.n, ptiles, s.part_info,
+                                         s.os_ghist, s.err);
   if (ev) (void)hipEventRecord(ev[2], st);
   if (b.n) {
-    const uint32_t nt = cdiv(b.n, SEG_TILE);
-    k_segment<<<nt, 256, 0, st>>>(s.rec, s.keys[0], s.vals[0], b.n, s.rec_s, s.segsum, s.rid, s.run_start,
-                                  s.num_runs, s.os_ctr + 4, s.seg_status, os_tag(epoch, 0), s.err);
+    k_bucket<<<256, BK_THREADS, 0, st>>>(s.keys[1], s.vals[1], s.part_info, s.os_ghist, ptiles, s.rec, s.keys[0],
+                                         s.vals[0], s.rec_s, s.segsum, s.rid, s.run_start, s.run_end, s.num_runs,
+                                         s.err);
     k_run_check<<<cdiv(b.n, 256), 256, 0, st>>>(b, s.rec_s, s.keys[0], s.rid, s.run_flags, s.defer, s.defer_n,
                                                 s.err);
   }
@@ -1876,24 +2409,24 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     (void)hipEventRecord(go, st);
     (void)hipStreamWaitEvent(side, go, 0);
     k_runs_general<<<g < RUNS_GENERAL_BLOCKS ? g : RUNS_GENERAL_BLOCKS, 256, lds, side>>>(
-        b, t, P, s.rec_s, s.keys[0], s.vals[0], s.res, s.run_start, s.defer, s.defer_n, s.repid, o.stats, s.stripes,
+        b, t, P, s.rec_s, s.keys[0], s.vals[0], s.res, s.run_start, s.run_end, s.defer, s.defer_n, s.repid, o.stats, s.stripes,
         s.errb, restore);
     (void)hipEventRecord(side_done, side);
     if (ev) (void)hipEventRecord(ev[3], st);
-    k_runs<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.keys[0], s.vals[0], s.res, s.run_start, s.run_flags,
+    k_runs<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.keys[0], s.vals[0], s.res, s.run_start, s.run_end, s.run_flags,
                                 s.run_state, s.run_f, s.num_runs, s.defer2, s.defer2_n, o.stats, s.stripes, s.errb,
                                 restore);
     if (ev) (void)hipEventRecord(ev[4], st);
     // stems k_runs found under several units in the table (rare)
     k_runs_general<<<RUNS_GENERAL_LATE_BLOCKS, 256, lds, st>>>(b, t, P, s.rec_s, s.keys[0], s.vals[0],
-                                                                s.res, s.run_start, s.defer2, s.defer2_n, s.repid, o.stats,
+                                                                s.res, s.run_start, s.run_end, s.defer2, s.defer2_n, s.repid, o.stats,
                                                                 s.stripes, s.errb, restore);
     (void)hipStreamWaitEvent(st, side_done, 0);
     if (!restore) {
       if (P.lc_en)
         k_fast_over<<<g, 256, 0, st>>>(b.n, s.rec_s, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
       k_fast_emit<<<g, 256, lds, st>>>(b.n, b.n_rules, t, P, s.rec_s, s.vals[0], s.res, s.segsum, s.rid,
-                                       s.run_start, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb);
+                                       s.run_start, s.run_end, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb);
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;
       const uint32_t gf = cdiv(nf * RL_NUM_STATS > b.n ? nf * RL_NUM_STATS : b.n, 256);
       k_finish<<<gf, 256, 0, st>>>(s.res, b.n, o, s.stripes, nf, s.errb);
