@@ -38,7 +38,6 @@ struct rl_ctx {
   hipStream_t side = nullptr;     // k_runs_general beside k_runs (stage B)
   hipEvent_t side_go = nullptr, side_done = nullptr;
   uint32_t next = 0, last = NBUF - 1;  // buffer of the next / of the latest batch
-  uint32_t epoch = 0;             // batches submitted (sort look-back tags)
   // table
   Slot* slots = nullptr;
   uint64_t nslots = 0;
@@ -151,22 +150,12 @@ Params params(rl_ctx* c);
 uint32_t enqueue(rl_ctx* c, const BatchDev& b, const OutDev& o, int restore, hipStream_t st, bool pipelined) {
   const uint32_t k = c->next;
   c->next = (k + 1) % NBUF;
-  c->epoch = (c->epoch + 1) & 0x0FFFFFFFu;
-  if (!c->epoch) {  // after 2^28 batches: clear the look-back granules once, so no old tag can alias
-    (void)hipDeviceSynchronize();
-    for (uint32_t j = 0; j < NBUF; j++)
-    {
-      (void)hipMemset(c->s[j].os_status, 0, 256ull * ((c->cfg.max_batch + OS_TILE - 1) / OS_TILE) * 8);
-      (void)hipMemset(c->s[j].seg_status, 0, 16ull * ((c->cfg.max_batch + SEG_TILE - 1) / SEG_TILE + 1));
-    }
-    c->epoch = 1;
-  }
   const TableDev t = table_view(c);
   const Params P = params(c);
   if (pipelined && !c->prof) {
     hipStream_t a = c->pipe[k];
     (void)hipStreamWaitEvent(a, c->b_done[k], 0);  // buffer k's previous batch is done
-    launch_stage_a(b, c->s[k], c->epoch, a);
+    launch_stage_a(b, c->s[k], a);
     (void)hipStreamWaitEvent(a, c->b_done[c->last], 0);  // table order
     launch_stage_b(b, o, t, P, c->s[k], restore, a, c->side, c->side_go, c->side_done);
     (void)hipEventRecord(c->b_done[k], a);
@@ -174,7 +163,7 @@ uint32_t enqueue(rl_ctx* c, const BatchDev& b, const OutDev& o, int restore, hip
     if (!st) st = c->stream;
     (void)after_batches(c, st);
     hipEvent_t* ev = prof_events(c);
-    launch_stage_a(b, c->s[k], c->epoch, st, ev);
+    launch_stage_a(b, c->s[k], st, ev);
     launch_stage_b(b, o, t, P, c->s[k], restore, st, c->side, c->side_go, c->side_done, ev);
     (void)hipEventRecord(c->b_done[k], st);
   }
@@ -233,13 +222,13 @@ Params params(rl_ctx* c) {
 
 // Per-batch scratch of one pipeline buffer (sized for max_batch descriptors).
 bool alloc_buffer(Scratch& s, uint32_t n) {
-  const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE, os_tiles = (n + OS_TILE - 1) / OS_TILE;
+  const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
   const size_t nt = (n + SEG_TILE - 1) / SEG_TILE + 1;
-  bool ok = dalloc(&s.seg_status, 2 * nt) == hipSuccess && hipMemset(s.seg_status, 0, 16 * nt) == hipSuccess;
-  ok = ok && dalloc(&s.os_ghist, 4 * 256) == hipSuccess && dalloc(&s.os_ctr, 8) == hipSuccess &&
-       dalloc(&s.os_status, 256ull * std::max(os_tiles, 1u)) == hipSuccess &&
-       hipMemset(s.os_status, 0, 256ull * std::max(os_tiles, 1u) * 8) == hipSuccess;
-  ok = ok && dalloc(&s.rec, n) == hipSuccess && dalloc(&s.rec_s, n) == hipSuccess && dalloc(&s.res, n) == hipSuccess;
+  const size_t items = (size_t)n / (64 * 4 * 8) + 1 + PART_DIGITS;  // BIG_CHUNK-position work items
+  bool ok = dalloc(&s.big_meta, PART_DIGITS) == hipSuccess && dalloc(&s.big_n, 1) == hipSuccess &&
+            dalloc(&s.big_work, items) == hipSuccess && dalloc(&s.work_n, 1) == hipSuccess &&
+            dalloc(&s.big_cnt, items * (1 + 2 * BIG_HEAVY)) == hipSuccess;
+  ok = ok && dalloc(&s.rec, n) == hipSuccess && dalloc(&s.res, n) == hipSuccess;
   for (int i = 0; i < 2; i++) ok = ok && dalloc(&s.keys[i], n) == hipSuccess && dalloc(&s.vals[i], n) == hipSuccess;
   ok = ok && dalloc(&s.hist, 256ull * std::max(ntiles, 1u)) == hipSuccess && dalloc(&s.hist_tot, 256) == hipSuccess;
   ok = ok && dalloc(&s.repid, n) == hipSuccess && dalloc(&s.defer, n) == hipSuccess &&
@@ -251,15 +240,17 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
        dalloc(&s.rid, n) == hipSuccess && dalloc(&s.run_start, (size_t)n + 1) == hipSuccess &&
        dalloc(&s.run_flags, n) == hipSuccess && dalloc(&s.run_state, n) == hipSuccess &&
        dalloc(&s.run_f, n) == hipSuccess && dalloc(&s.num_runs, 1) == hipSuccess;
+  ok = ok && dalloc(&s.hit_a, n) == hipSuccess && dalloc(&s.hit_p, n) == hipSuccess &&
+       dalloc(&s.hit_t, n) == hipSuccess;
   ok = ok && dalloc(&s.run_end, n) == hipSuccess &&
-       dalloc(&s.part_info, 256ull * std::max((n + PART_TILE - 1) / PART_TILE, 1u)) == hipSuccess;
+       dalloc(&s.part_info, (size_t)PART_DIGITS * std::max((n + PART_TILE - 1) / PART_TILE, 1u)) == hipSuccess;
   return ok;
 }
 
 void free_buffer(Scratch& s) {
-  void* bufs[] = {s.rec, s.rec_s, s.res, s.seg_status, s.os_ghist, s.os_ctr, s.os_status, s.keys[0], s.keys[1], s.vals[0], s.vals[1], s.hist,
+  void* bufs[] = {s.rec, s.res, s.big_meta, s.big_n, s.big_work, s.work_n, s.big_cnt, s.keys[0], s.keys[1], s.vals[0], s.vals[1], s.hist,
                   s.hist_tot, s.repid, s.defer, s.defer_n, s.defer2, s.defer2_n, s.tile_f, s.tile_s, s.tile_h, s.hits_s, s.segsum, s.rid,
-                  s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs, s.run_end, s.part_info};
+                  s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs, s.run_end, s.part_info, s.hit_a, s.hit_p, s.hit_t};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
 }

@@ -11,26 +11,22 @@ namespace rl {
 
 constexpr uint32_t RS_ITEMS = 16;  // routing partition (k_rs_*): 256 threads x RS_ITEMS
 constexpr uint32_t RS_TILE = 256 * RS_ITEMS;
-// onesweep sort (k_os_pass): OS_WAVES waves x OS_ITEMS elements per lane per tile
-#ifndef RL_OS_ITEMS
-#define RL_OS_ITEMS 16
-#endif
-#ifndef RL_OS_WAVES
-#define RL_OS_WAVES 4
-#endif
-constexpr uint32_t OS_ITEMS = RL_OS_ITEMS, OS_WAVES = RL_OS_WAVES, OS_THREADS = 64 * OS_WAVES;
-constexpr uint32_t OS_TILE = OS_THREADS * OS_ITEMS;
-static_assert(OS_WAVES >= 4, "256 digits need at least 256 threads");
-#ifndef RL_OS_LB
-#define RL_OS_LB 8
-#endif
-constexpr uint32_t OS_LB = RL_OS_LB;  // look-back granules loaded per round trip
 #ifndef RL_SEG_ITEMS
 #define RL_SEG_ITEMS 16
 #endif
 constexpr uint32_t SEG_ITEMS = RL_SEG_ITEMS;  // 64-position chunks per wave (4 waves per tile)
 constexpr uint32_t SEG_TILE = 256 * SEG_ITEMS;
 constexpr uint32_t PART_ITEMS = 16, PART_TILE = 256 * PART_ITEMS;  // k_part: 256 threads x PART_ITEMS
+constexpr uint32_t PART_BITS = 10, PART_DIGITS = 1u << PART_BITS;   // buckets = top key bits
+constexpr uint32_t BIG_BLOCKS = 64;                                 // k_bucket_big workgroups
+constexpr uint32_t BIG_ITEM_BLOCKS = 512;                           // k_big_count / k_big_place workgroups
+constexpr uint32_t BIG_HEAVY = 4;                                   // hot keys peeled off a large bucket
+
+// A bucket too large for k_bucket's LDS, queued with its sampled hot keys.
+struct BigMeta {
+  uint32_t d, S, base, nchunks, item0, r, rb_heavy, pad;
+  uint32_t heavy[BIG_HEAVY];
+};
 constexpr uint32_t MAX_PART_TILES = 2048;  // k_part tiles per batch (max_batch <= 2048 x 4096)
 constexpr uint32_t LONG_RUN = 32;        // runs at least this long take the parallel path
 constexpr uint32_t RUN_SLOW = 1, RUN_FAST = 2, RUN_MULTI = 4;
@@ -69,6 +65,15 @@ struct __attribute__((aligned(16))) Rec {
   uint32_t limit;
 };
 static_assert(sizeof(Rec) == 32, "Rec is two dwordx4");
+
+// A descriptor's record by sorted position: records stay in arrival order
+// (k_prepare) and the sorted order is the permutation svals (one gather per
+// access, no sorted copy of the records).
+struct SRec {
+  const Rec* rec;
+  const uint32_t* sv;
+  __device__ inline Rec operator[](uint32_t q) const { return rec[sv[q]]; }
+};
 
 __host__ __device__ inline uint32_t rec_len(const Rec& r) { return r.lu & 0xFFFFu; }
 __host__ __device__ inline uint32_t rec_unit(const Rec& r) { return (r.lu >> 16) & 0xFFu; }
@@ -126,17 +131,16 @@ struct Params {
 // Per-batch scratch (device), sized for max_batch.
 struct Scratch {
   Rec* rec;                  // [n] arrival order
-  Rec* rec_s;                // [n] sorted order
   unsigned long long* res;   // [n] packed result per descriptor (arrival order)
   uint32_t* keys[2];
   uint32_t* vals[2];
   uint32_t* hist;      // 256 x ntiles, digit-major (routing partition)
   uint32_t* hist_tot;  // 256 digit totals
-  // onesweep sort: digit totals of the 4 passes, tile tickets, look-back granules
-  uint32_t* os_ghist;               // [4 * 256]
-  uint32_t* os_ctr;                 // [5] tile tickets: sort passes 0..3, k_segment
-  unsigned long long* seg_status;   // [2 * seg tiles] k_segment look-back granules
-  unsigned long long* os_status;    // [ntiles * 256] {count, tag | flag}
+  BigMeta* big_meta;                 // [PART_DIGITS] buckets queued for the large-bucket kernels
+  uint32_t* big_n;
+  uint32_t* big_work;                // [n / BIG_CHUNK + PART_DIGITS] chunk work items (bucket << 16 | chunk)
+  uint32_t* work_n;
+  uint32_t* big_cnt;                 // [work items x (1 + 2 x BIG_HEAVY)] k_big_count per chunk
   uint8_t* repid;
   uint32_t* defer;                // RUN_MULTI runs (k_run_check), for k_runs_general beside k_runs
   uint32_t* defer_n;
@@ -146,6 +150,9 @@ struct Scratch {
   // run segmentation (sorted order)
   uint32_t *tile_f, *tile_s, *tile_h;  // per SEG_TILE tile
   uint32_t* hits_s;                    // [n] raw hits, sorted order
+  uint32_t* hit_a;                     // [n] raw hits, arrival order (k_prepare)
+  uint32_t* hit_p;                     // [n] raw hits, k_part tile layout
+  uint32_t* hit_t;                     // [n] k_bucket large-bucket temp
   uint32_t* segsum;                    // [n] inclusive in-run sum of hits
   uint32_t* rid;                       // [n] run id
   uint32_t* run_start;                 // [n] first sorted position of run r
@@ -169,9 +176,7 @@ struct Scratch {
 // only the batch and this buffer's scratch, so it may overlap the previous
 // batch's stage B; stage B (table probe, replay, decisions, stats, results)
 // must run in batch order.
-// `epoch` (1..2^28-1, distinct for consecutive batches on one buffer) tags the
-// sort's look-back granules so they never need clearing.
-void launch_stage_a(const BatchDev& b, const Scratch& s, uint32_t epoch, hipStream_t st, hipEvent_t* ev = nullptr);
+void launch_stage_a(const BatchDev& b, const Scratch& s, hipStream_t st, hipEvent_t* ev = nullptr);
 // Stage B launches the RUN_MULTI runs' exact replay on `side` (ordered by the
 // events go / side_done) so that it overlaps k_runs.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,

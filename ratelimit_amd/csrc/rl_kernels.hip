@@ -2,12 +2,14 @@
 //
 // Pipeline for one batch (inputs already in HBM); stage A (table-free):
 //   k_prepare     validate the packed batch; hash every stem (LDS-staged
-//                 bytes); pack each descriptor into a 32-B Rec
-//   k_os_*        onesweep stable LSD sort of (hash[63:32], index): groups each
-//                 stem's descriptors together, in arrival (sequence) order
-//   k_segment     Recs into sorted order, run ids, in-run prefix sums of hits
-//                 (single pass, decoupled look-back), and the run checks: one
-//                 stem and one unit per run (else k_runs_general)
+//                 bytes); pack each descriptor into a 32-B Rec (arrival order)
+//   k_part        stable partition of (hash[63:32], index, hits) by the top
+//                 byte, tile by tile (no look-back)
+//   k_bucket      one workgroup per top byte: gather the bucket, stable LDS
+//                 sort by the remaining 24 bits (hot keys of a large bucket
+//                 peeled off), run ids, run bounds and in-run prefix sums of
+//                 hits: each stem's descriptors together, in arrival order
+//   k_run_check   one stem and one unit per run (else k_runs_general)
 //   ---- stage B (the table; batch order) ----
 //   k_runs        one lane per run: probe/insert the (stem, unit) slot of the
 //                 HBM table (one 128-B line per probe); replay short runs in
@@ -41,21 +43,19 @@ constexpr uint32_t HASH_LDS_BYTES = 16384;
 __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ rec, uint32_t* __restrict__ keys,
                                                  uint32_t* __restrict__ vals, uint32_t* err,
                                                  const int64_t* time_floor, uint32_t* defer_n,
-                                                 uint32_t* __restrict__ os_ghist, uint32_t* __restrict__ os_ctr,
-                                                 uint32_t* __restrict__ run_flags, uint32_t* num_runs) {
+                                                 uint32_t* big_n, uint32_t* work_n, uint32_t* __restrict__ run_flags,
+                                                 uint32_t* num_runs,
+                                                 uint32_t* __restrict__ hit_a) {
   __shared__ uint32_t lds[HASH_LDS_BYTES / 4 + 4];
   const uint32_t tid = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + tid;
   uint32_t bad = 0;
   if (i < b.n) run_flags[i] = 0;  // k_run_check ORs run flags in from any block
-  if (blockIdx.x == 0) {  // per-batch counters: RUN_MULTI queue, run ids, digit totals and tile tickets
-    if (tid == 0) {
-      *defer_n = 0;
-      *num_runs = 0;
-    }
-    if (tid < 5) os_ctr[tid] = 0;  // [0..3] sort passes, [4] k_segment
-#pragma unroll
-    for (uint32_t p = 0; p < 4; p++) os_ghist[p * 256 + tid] = 0;
+  if (blockIdx.x == 0 && tid == 0) {  // per-batch counters: RUN_MULTI queue, run ids, large buckets
+    *defer_n = 0;
+    *num_runs = 0;
+    *big_n = 0;
+    *work_n = 0;
   }
 
   // ---- per-request clock checks: now in [0, NOW_MAX] and not before the last sweep
@@ -119,6 +119,7 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   r.hits = b.hits[i];
   r.limit = b.limit[i];
   rec[i] = r;
+  hit_a[i] = r.hits;
 }
 
 // ===========================================================================
@@ -249,179 +250,6 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t* __restrict__
   }
 }
 
-// ===========================================================================
-// Onesweep LSD radix sort of (u32 key, u32 value), 8-bit digits: one kernel
-// reads the keys once for all four digit histograms, then one kernel per pass.
-// A pass block takes the next tile ticket (so every earlier tile belongs to a
-// block that is already running), ranks its RS_TILE elements in LDS with the
-// wave ballot multisplit, publishes its per-digit counts and learns the counts
-// of all earlier tiles by decoupled look-back over 8-byte {count, tag} granules
-// (one agent-scope store / load each: untorn, no separate flag). The tag holds
-// the batch epoch and pass, so granules are never cleared.
-// ===========================================================================
-constexpr uint32_t OS_AGG = 1u, OS_INC = 2u;
-
-__host__ __device__ inline uint32_t os_tag(uint32_t epoch, uint32_t pass) { return (epoch << 4) | (pass << 2); }
-
-__global__ __launch_bounds__(256) void k_os_hist(const uint32_t* __restrict__ keys, uint32_t n,
-                                                 uint32_t* __restrict__ ghist, const uint32_t* err) {
-  __shared__ uint32_t h[4][256];
-  if (*err) return;
-  const uint32_t tid = threadIdx.x;
-#pragma unroll
-  for (uint32_t p = 0; p < 4; p++) h[p][tid] = 0;
-  __syncthreads();
-  for (uint32_t j = blockIdx.x * 256 + tid; j < n; j += gridDim.x * 256) {
-    const uint32_t k = keys[j];
-    atomicAdd(&h[0][k & 255u], 1u);
-    atomicAdd(&h[1][(k >> 8) & 255u], 1u);
-    atomicAdd(&h[2][(k >> 16) & 255u], 1u);
-    atomicAdd(&h[3][k >> 24], 1u);
-  }
-  __syncthreads();
-#pragma unroll
-  for (uint32_t p = 0; p < 4; p++) {
-    const uint32_t v = h[p][tid];
-    if (v) atomicAdd(&ghist[p * 256 + tid], v);
-  }
-}
-
-#ifdef RL_OS_PROF  // sortbench only: per-tile phase stamps of the last pass launched
-__device__ unsigned long long g_os_prof[8192 * 8];
-#define OS_STAMP(k) \
-  if (threadIdx.x == 0) g_os_prof[tile * 8 + (k)] = wall_clock64()
-#else
-#define OS_STAMP(k)
-#endif
-
-__global__ __launch_bounds__(OS_THREADS) void k_os_pass(const uint32_t* __restrict__ kin,
-                                                        const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
-                                                        uint32_t* __restrict__ vout, uint32_t n, uint32_t pass,
-                                                        const uint32_t* __restrict__ ghist, uint32_t* __restrict__ ctr,
-                                                        unsigned long long* status, uint32_t tag, const uint32_t* err) {
-  __shared__ uint32_t wcnt[OS_WAVES][256];
-  __shared__ uint32_t dbase[256];
-  __shared__ uint32_t gsum[4];
-  __shared__ uint32_t s_tile;
-  if (*err) return;  // the same for every block: no tile is left half-published
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) s_tile = atomicAdd(&ctr[pass], 1u);
-  for (uint32_t j = tid; j < OS_WAVES * 256; j += OS_THREADS) (&wcnt[0][0])[j] = 0;
-  __syncthreads();
-  const uint32_t tile = s_tile, shift = 8 * pass;
-  OS_STAMP(0);
-  const uint64_t lt_mask = (1ull << lane) - 1;
-  const uint32_t wbase = tile * OS_TILE + wave * 64 * OS_ITEMS;
-  uint32_t kk[OS_ITEMS], vv[OS_ITEMS], pos[OS_ITEMS];
-#pragma unroll
-  for (uint32_t i = 0; i < OS_ITEMS; i++) {
-    const uint32_t j = wbase + i * 64 + lane;
-    const bool valid = j < n;
-    kk[i] = valid ? kin[j] : 0xFFFFFFFFu;
-    vv[i] = valid ? vin[j] : 0u;
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < OS_ITEMS; i++) {
-    const bool valid = wbase + i * 64 + lane < n;
-    const uint32_t d = (kk[i] >> shift) & 255u;
-    uint64_t peers = __ballot(valid);
-#pragma unroll
-    for (uint32_t bit = 0; bit < 8; bit++) {
-      const bool sb = (d >> bit) & 1u;
-      const uint64_t bal = __ballot(sb);
-      peers &= sb ? bal : ~bal;
-    }
-    const uint32_t rank = __popcll(peers & lt_mask);
-    const uint32_t leader = valid ? (uint32_t)(__ffsll((unsigned long long)peers) - 1) : lane;
-    uint32_t old = 0;
-    if (valid && rank == 0) {
-      old = wcnt[wave][d];
-      wcnt[wave][d] = old + __popcll(peers);
-    }
-    old = __shfl(old, leader);
-    pos[i] = old + rank;
-  }
-  __syncthreads();
-  OS_STAMP(1);
-  if (tid < 256) {
-    // digit tid: this tile's count and the per-wave exclusive offsets
-    uint32_t c = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < OS_WAVES; w++) {
-      const uint32_t t = wcnt[w][tid];
-      wcnt[w][tid] = c;
-      c += t;
-    }
-    unsigned long long* mine = status + (size_t)tile * 256 + tid;
-    __hip_atomic_store(mine, (unsigned long long)c | ((unsigned long long)(tag | (tile ? OS_AGG : OS_INC)) << 32),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // global exclusive base of digit tid: wave scans of the pass's digit totals
-    const uint32_t g = ghist[pass * 256 + tid];
-    uint32_t inc = g;
-#pragma unroll
-    for (uint32_t off = 1; off < 64; off <<= 1) {
-      const uint32_t y = __shfl_up(inc, off, 64);
-      if (lane >= off) inc += y;
-    }
-    if (lane == 63) gsum[wave] = inc;
-    // decoupled look-back: add earlier tiles' counts until an inclusive prefix.
-    // OS_LB granules (tiles j, j-1, ...) are loaded together per round trip;
-    // the ready prefix of them is consumed (an aggregate is a final tile count,
-    // so a partial window is exact) and the walk resumes below it.
-    uint32_t excl = 0;
-    if (tile) {
-      int32_t j = (int32_t)tile - 1;
-      for (;;) {
-        unsigned long long v[OS_LB];
-#pragma unroll
-        for (uint32_t k = 0; k < OS_LB; k++)
-          v[k] = j - (int32_t)k >= 0 ? __hip_atomic_load(status + (size_t)(j - (int32_t)k) * 256 + tid,
-                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                     : 0ull;
-        uint32_t add = 0, used = 0;
-        bool stop = false, done = false;
-#pragma unroll
-        for (uint32_t k = 0; k < OS_LB; k++) {
-          const uint32_t tg = (uint32_t)(v[k] >> 32);
-          if (stop || (tg & ~3u) != tag) {  // not yet published for this pass
-            stop = true;
-            continue;
-          }
-          add += (uint32_t)v[k];
-          used++;
-          if (tg & OS_INC) stop = done = true;  // tile 0 is inclusive, so j never passes it
-        }
-        excl += add;
-        if (done) break;
-        j -= (int32_t)used;
-        if (!used) __builtin_amdgcn_s_sleep(1);
-      }
-      __hip_atomic_store(mine, (unsigned long long)(excl + c) | ((unsigned long long)(tag | OS_INC) << 32),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    dbase[tid] = inc - g + excl;  // + earlier waves' digit totals, below
-  }
-  __syncthreads();  // gsum, dbase
-  if (tid < 256) {
-    uint32_t wpre = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < 4; w++) wpre += w < wave ? gsum[w] : 0u;
-    dbase[tid] += wpre;
-  }
-  __syncthreads();
-  OS_STAMP(2);
-#pragma unroll
-  for (uint32_t i = 0; i < OS_ITEMS; i++) {
-    if (wbase + i * 64 + lane < n) {
-      const uint32_t d = (kk[i] >> shift) & 255u;
-      const uint32_t p = dbase[d] + wcnt[wave][d] + pos[i];
-      kout[p] = kk[i];
-      vout[p] = vv[i];
-    }
-  }
-  OS_STAMP(3);
-}
-
 // The zero-padded first KEY_HEAD bytes of the stem at byte `off` of the packed
 // stems, as 4 x uint4: five aligned 16-B loads, then dword selects and funnel
 // shifts. Only chunks holding a byte of the head are loaded, so no load leaves
@@ -507,7 +335,7 @@ __device__ inline Key key_of(const BatchDev& b, const Rec& r) {
   return k;
 }
 
-__device__ inline Key key_at(const BatchDev& b, const Rec* rec_s, uint32_t q) { return key_of(b, rec_s[q]); }
+__device__ inline Key key_at(const BatchDev& b, SRec rec_s, uint32_t q) { return key_of(b, rec_s[q]); }
 
 __device__ inline uint32_t head_diff(const uint4* x, const uint4* y) {
   uint32_t d = 0;
@@ -1030,7 +858,7 @@ __device__ inline void general_step(const Params& P, unsigned long long* res, La
 
 // Replay elements [p, end) (those of stem k when repid is given) through the
 // single-unit slot s0, in registers.
-__device__ __attribute__((always_inline)) inline void replay_simple(const Rec* rec_s, const uint32_t* svals,
+__device__ __attribute__((always_inline)) inline void replay_simple(SRec rec_s, const uint32_t* svals,
                                                                     unsigned long long* res, const TableDev& t,
                                                                     const Params& P, const uint8_t* repid,
                                                                     uint32_t p, uint32_t end, uint32_t k, int64_t s0,
@@ -1261,185 +1089,70 @@ __global__ __launch_bounds__(256) void k_seg_apply(const uint32_t* __restrict__ 
   }
 }
 
-// ---- k_segment: gather + run segmentation in one pass over the sorted order,
-// tiles of SEG_TILE positions taken by ticket, decoupled look-back across
-// tiles. Per sorted position q: rec_s[q] = rec[svals[q]] (one random 32-B
-// read), head = q == 0 || skeys[q-1] != skeys[q], rid[q] = heads in [0, q] - 1,
-// segsum[q] = inclusive in-run sum of max(1, hits) (u32, wrapping like the
-// sequential INCRBYs); per run its start (flags cleared), and num_runs. A
-// tile's look-back state is (heads, segmented sum): two 8-B {value, tag}
-// granules that a reader accepts only when both carry the same tag and flag.
-__device__ inline SegPair seg_read(const unsigned long long* st, uint32_t j, uint32_t tag, bool& ready, bool& inc,
-                                   uint32_t& h) {
-  const unsigned long long g0 = __hip_atomic_load(st + 2 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long g1 = __hip_atomic_load(st + 2 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t t0 = (uint32_t)(g0 >> 32), t1 = (uint32_t)(g1 >> 32);
-  ready = (t0 & ~3u) == tag && t0 == t1;
-  inc = ready && (t0 & OS_INC);
-  h = (uint32_t)g1;
-  return SegPair{h ? 1u : 0u, (uint32_t)g0};
-}
-
-__device__ inline void seg_publish(unsigned long long* st, uint32_t j, uint32_t tag, SegPair v, uint32_t h) {
-  __hip_atomic_store(st + 2 * j, (unsigned long long)v.s | ((unsigned long long)tag << 32), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(st + 2 * j + 1, (unsigned long long)h | ((unsigned long long)tag << 32), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ __launch_bounds__(256) void k_segment(const Rec* __restrict__ rec, const uint32_t* __restrict__ skeys,
-                                                 const uint32_t* __restrict__ svals, uint32_t n,
-                                                 Rec* __restrict__ rec_s, uint32_t* __restrict__ segsum,
-                                                 uint32_t* __restrict__ rid, uint32_t* __restrict__ run_start,
-                                                 uint32_t* num_runs, uint32_t* __restrict__ ctr,
-                                                 unsigned long long* status, uint32_t tag, const uint32_t* err) {
-  __shared__ SegPair sp[4];
-  __shared__ uint32_t sh[4];
-  __shared__ SegPair s_pre;
-  __shared__ uint32_t s_tile, s_preh;
-  if (*err) return;  // the same for every block
-  if (threadIdx.x == 0) s_tile = atomicAdd(ctr, 1u);
-  __syncthreads();
-  const uint32_t tile = s_tile;
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t base = tile * SEG_TILE + wave * SEG_STRIP + lane;
-  // pass 1: records into sorted order; head flags and hits kept per chunk
-  SegChunk ch[SEG_ITEMS];
-  SegPair agg{0, 0};
-  uint32_t hc = 0;
-#pragma unroll
-  for (uint32_t c = 0; c < SEG_ITEMS; c++) {
-    const uint32_t q = base + 64 * c;
-    const bool valid = q < n;
-    bool head = false;
-    uint32_t hv = 0;
-    if (valid) {
-      head = q == 0 || skeys[q - 1] != skeys[q];
-      const Rec r = rec[svals[q]];
-      rec_s[q] = r;
-      hv = r.hits > 1 ? r.hits : 1u;
-    }
-    ch[c] = SegChunk{(uint64_t)__ballot(head), hv};
-    uint32_t t = hv;  // chunk total, segmented: sum after the last head
-    const uint32_t lh = ch[c].heads ? 63u - (uint32_t)__clzll((long long)ch[c].heads) : 0u;
-    if (ch[c].heads && lane < lh) t = 0;
-#pragma unroll
-    for (uint32_t off = 32; off; off >>= 1) t += __shfl_xor(t, off, 64);
-    agg = seg_op(agg, SegPair{ch[c].heads ? 1u : 0u, t});
-    hc += (uint32_t)__popcll(ch[c].heads);
-  }
-  SegPair excl, tot;
-  uint32_t hexcl, htot;
-  seg_waves(agg, hc, sp, sh, excl, hexcl, tot, htot);
-  // publish this tile's aggregate, look back for the prefix, publish the inclusive value
-  if (wave == 0) {
-    if (lane == 0) seg_publish(status, tile, tag | (tile ? OS_AGG : OS_INC), tot, htot);
-    SegPair acc{0, 0};
-    uint32_t acch = 0;
-    int32_t top = (int32_t)tile - 1;
-    while (top >= 0) {
-      const int32_t j = top - (int32_t)lane;
-      bool ready = true, inc = false;
-      uint32_t h = 0;
-      SegPair v{0, 0};
-      if (j >= 0) v = seg_read(status, (uint32_t)j, tag, ready, inc, h);
-      const uint64_t mi = __ballot(inc), mnr = __ballot(!ready);
-      const uint32_t fi = mi ? (uint32_t)(__ffsll((unsigned long long)mi) - 1) : 64u;
-      const uint64_t need = fi >= 63 ? ~0ull : ((2ull << fi) - 1);  // lanes 0..fi
-      if (mnr & need) {
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      // older tiles sit in higher lanes: x = x_63 (+) ... (+) x_0 over lanes 0..fi
-      SegPair x = lane <= fi ? v : SegPair{0, 0};
-      uint32_t xh = lane <= fi ? h : 0u;
-#pragma unroll
-      for (uint32_t off = 1; off < 64; off <<= 1) {
-        const SegPair y{__shfl_down(x.f, off, 64), __shfl_down(x.s, off, 64)};
-        const uint32_t yh = __shfl_down(xh, off, 64);
-        if (lane + off < 64) {
-          x = seg_op(y, x);
-          xh += yh;
-        }
-      }
-      acc = seg_op(SegPair{__shfl(x.f, 0, 64), __shfl(x.s, 0, 64)}, acc);
-      acch += __shfl(xh, 0, 64);
-      if (fi < 64) break;
-      top -= 64;
-    }
-    if (lane == 0) {
-      if (tile) seg_publish(status, tile, tag | OS_INC, seg_op(acc, tot), acch + htot);
-      s_pre = acc;
-      s_preh = acch;
-    }
-  }
-  __syncthreads();
-  // pass 2: exclusive prefix of the wave = tiles before + earlier waves
-  SegPair run = seg_op(s_pre, excl);
-  uint32_t hrun = s_preh + hexcl;
-#pragma unroll
-  for (uint32_t c = 0; c < SEG_ITEMS; c++) {
-    const uint32_t q = base + 64 * c;
-    const SegPair v = seg_chunk_scan(ch[c], lane);
-    const SegPair in = seg_op(run, v);
-    const uint64_t heads = ch[c].heads;
-    const uint32_t r = hrun + (uint32_t)__popcll(heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1))) - 1;
-    if (q < n) {
-      segsum[q] = in.s;
-      rid[q] = r;
-      if ((heads >> lane) & 1) {
-        run_start[r] = q;
-      }
-      if (q == n - 1) {
-        run_start[r + 1] = n;
-        *num_runs = r + 1;
-      }
-    }
-    run = seg_op(run, SegPair{__shfl(v.f, 63, 64), __shfl(v.s, 63, 64)});
-    hrun += (uint32_t)__popcll(heads);
-  }
-}
-
 // ===========================================================================
 // Grouping by MSD partition + per-bucket LDS sort (stage A).
 //
-// k_part: every PART_TILE tile of (sort key, index) pairs, in arrival order, is
-// stably partitioned by the key's top byte into its own tile region (one
-// wave-ballot multisplit rank, coalesced digit segments), and publishes per
-// digit its (offset, count) in the tile and the digit total. No look-back:
-// bucket d is the concatenation, in tile (= arrival) order, of every tile's
-// digit-d segment.
-// k_bucket: one 1024-thread workgroup per top byte. It gathers its bucket,
-// stably sorts it by key bits [0, 24) (three 8-bit multisplit passes in LDS;
-// buckets larger than BK_CAP run the same passes chunk by chunk through HBM),
-// so the batch ends up sorted by the full key with arrival order kept within
-// equal keys. It then segments the bucket in place (runs never cross buckets):
-// records into sorted order, in-run inclusive sums of max(1, hits), run ids
-// and [run_start, run_end). Run ids are allocated per bucket from one atomic
-// counter, contiguous and in sorted order within a bucket.
+// k_part: every PART_TILE tile of (sort key, index, hits), in arrival order,
+// is stably partitioned by the key's top PART_BITS bits into its own tile
+// region (one wave-ballot multisplit rank, digit segments), and records per
+// digit its (offset, count) in the tile. No look-back and no atomics: bucket d
+// is the concatenation, in tile (= arrival) order, of every tile's digit-d
+// segment; its size is the sum of the counts and its place in the sorted batch
+// the sum of the offsets (each offset counts the tile's smaller digits).
+// k_bucket: one 4-wave workgroup per bucket (several per CU, so one group's
+// barriers overlap another's work). It gathers the bucket, stably sorts it by
+// the remaining 22 key bits (three multisplit passes in LDS), so the batch ends
+// up sorted by the full key with arrival order kept within equal keys, and
+// segments it in place (runs never cross buckets): in-run inclusive sums of
+// max(1, hits), run ids and [run_start, run_end). Run ids are allocated per
+// bucket from one atomic counter, contiguous and in sorted order within a
+// bucket. Buckets larger than its LDS capacity are queued for k_bucket_big.
+// k_bucket_big: 8-wave workgroups (register budget for 16 items per lane)
+// over the queued buckets: the hot keys of a large bucket are peeled off
+// (sampled, then moved as whole blocks in arrival order) and the rest sorted
+// in LDS; failing that, the three passes run chunk by chunk through HBM.
 // ===========================================================================
-constexpr uint32_t BK_WAVES = 16, BK_THREADS = 64 * BK_WAVES, BK_ITEMS = 8, BK_CAP = BK_THREADS * BK_ITEMS;
-constexpr uint32_t BK_STRIP = 64 * BK_ITEMS;  // positions per wave in a chunk
+constexpr uint32_t BK_HEAVY = BIG_HEAVY;  // heavy keys peeled off a large bucket
+constexpr uint32_t BK_HEAVY_MIN = 3;  // ... seen at least this often among 64 samples
 
-// Wave-ballot multisplit: rank of each item among the wave's earlier items with
-// the same digit, against a wave-private running count row in LDS (item-major
-// order: item i of lane l precedes item i of lane l+1 and item i+1 of lane 0).
-template <uint32_t IT>
+template <uint32_t W, uint32_t IT>
+struct BkShape {
+  static constexpr uint32_t WAVES = W, ITEMS = IT, THREADS = 64 * W, CAP = 64 * W * IT, STRIP = 64 * IT;
+};
+using BkSmall = BkShape<4, 8>;   // k_bucket: 2048 elements in LDS
+using BkBig = BkShape<8, 16>;    // k_bucket_big: 8192 elements per chunk
+
+#ifdef RL_BK_PROF  // bucketbench only: per-bucket phase stamps
+__device__ unsigned long long g_bk_prof[PART_DIGITS * 16];
+__device__ uint32_t g_bk_peel[PART_DIGITS * 16];  // peel state per bucket
+#define BK_STAMP(d, k) \
+  if (threadIdx.x == 0) g_bk_prof[(d) * 16 + (k)] = wall_clock64()
+#else
+#define BK_STAMP(d, k)
+#endif
+
+// Wave-ballot multisplit on the BITS-bit digit at `shift`: rank of each item
+// among the wave's earlier items with the same digit, against a wave-private
+// running count row in LDS (item-major order: item i of lane l precedes item i
+// of lane l+1 and item i+1 of lane 0). The digit group leaders add to the row
+// with returning LDS atomics, issued back to back for all items (LDS applies
+// them in order), then every lane fetches its leader's old count.
+template <uint32_t IT, uint32_t BITS>
 __device__ inline void wave_multisplit(const uint32_t (&kk)[IT], uint32_t nvalid_base, uint32_t limit, uint32_t shift,
                                        uint32_t* row, uint32_t (&pos)[IT]) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t lt_mask = (1ull << lane) - 1;
   uint32_t leader[IT];
-  // The digit group leaders add to the row with returning LDS atomics, issued
-  // back to back for all items (LDS applies them in order), then every lane
-  // fetches its leader's old count.
 #pragma unroll
   for (uint32_t i = 0; i < IT; i++) {
+    leader[i] = lane;
+    pos[i] = 0;
+    if (nvalid_base + i * 64 >= limit) continue;  // wave-uniform: no item of the wave left
     const bool valid = nvalid_base + i * 64 + lane < limit;
-    const uint32_t d = (kk[i] >> shift) & 255u;
+    const uint32_t d = (kk[i] >> shift) & ((1u << BITS) - 1u);
     uint64_t peers = __ballot(valid);
 #pragma unroll
-    for (uint32_t bit = 0; bit < 8; bit++) {
+    for (uint32_t bit = 0; bit < BITS; bit++) {
       const bool sb = (d >> bit) & 1u;
       const uint64_t bal = __ballot(sb);
       peers &= sb ? bal : ~bal;
@@ -1447,7 +1160,7 @@ __device__ inline void wave_multisplit(const uint32_t (&kk)[IT], uint32_t nvalid
     const uint32_t rank = __popcll(peers & lt_mask);
     leader[i] = valid ? (uint32_t)(__ffsll((unsigned long long)peers) - 1) : lane;
     pos[i] = (valid && rank == 0) ? atomicAdd(&row[d], (uint32_t)__popcll(peers)) : 0u;
-    pos[i] |= rank << 16;  // rank < 64; old counts < 2^16 (at most BK_CAP / PART_TILE)
+    pos[i] |= rank << 16;  // rank < 64; old counts < 2^16 (at most a chunk / a tile)
   }
 #pragma unroll
   for (uint32_t i = 0; i < IT; i++) pos[i] = __shfl(pos[i] & 0xFFFFu, leader[i]) + (pos[i] >> 16);
@@ -1474,117 +1187,196 @@ __device__ inline uint32_t scan256(uint32_t v, uint32_t* wsum4, uint32_t* total)
 }
 
 __global__ __launch_bounds__(256) void k_part(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                              uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, uint32_t n,
-                                              uint32_t ntiles, uint32_t* __restrict__ info, uint32_t* __restrict__ tot,
-                                              const uint32_t* err) {
-  __shared__ uint32_t wcnt[4][256];
-  __shared__ uint32_t dbase[256];
+                                              const uint32_t* __restrict__ hin, uint32_t* __restrict__ kout,
+                                              uint32_t* __restrict__ vout, uint32_t* __restrict__ hout, uint32_t n,
+                                              uint32_t ntiles, uint32_t* __restrict__ info, const uint32_t* err) {
+  constexpr uint32_t DPT = PART_DIGITS / 256;  // digits per thread
+  __shared__ uint32_t wcnt[4][PART_DIGITS];
   __shared__ uint32_t wsum[4];
   if (*err) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, tile = blockIdx.x;
-  wcnt[0][tid] = 0; wcnt[1][tid] = 0; wcnt[2][tid] = 0; wcnt[3][tid] = 0;
+  for (uint32_t j = tid; j < 4 * PART_DIGITS; j += 256) (&wcnt[0][0])[j] = 0;
   __syncthreads();
   const uint32_t wbase = tile * PART_TILE + wave * 64 * PART_ITEMS;
-  uint32_t kk[PART_ITEMS], vv[PART_ITEMS], pos[PART_ITEMS];
+  uint32_t kk[PART_ITEMS], vv[PART_ITEMS], hh[PART_ITEMS], pos[PART_ITEMS];
 #pragma unroll
   for (uint32_t i = 0; i < PART_ITEMS; i++) {
-    const uint32_t j = wbase + i * 64 + lane;
-    kk[i] = j < n ? kin[j] : 0xFFFFFFFFu;
-    vv[i] = j < n ? vin[j] : 0u;
+    const uint32_t j = min(wbase + i * 64 + lane, n - 1);  // unconditional loads, all in flight
+    kk[i] = kin[j];
+    vv[i] = vin[j];
+    hh[i] = hin[j];
   }
-  wave_multisplit(kk, wbase, n, 24, wcnt[wave], pos);
+  wave_multisplit<PART_ITEMS, PART_BITS>(kk, wbase, n, 32 - PART_BITS, wcnt[wave], pos);
   __syncthreads();
-  uint32_t c = 0;
+  // digits tid*DPT .. tid*DPT+DPT-1: per-wave exclusive offsets and counts,
+  // then the tile's exclusive digit offsets (scan over threads)
+  uint32_t c[DPT], tsum = 0;
 #pragma unroll
-  for (uint32_t w = 0; w < 4; w++) {
-    const uint32_t t = wcnt[w][tid];
-    wcnt[w][tid] = c;
-    c += t;
+  for (uint32_t j = 0; j < DPT; j++) {
+    const uint32_t d = tid * DPT + j;
+    uint32_t acc = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 4; w++) {
+      const uint32_t t = wcnt[w][d];
+      wcnt[w][d] = acc;
+      acc += t;
+    }
+    c[j] = acc;
+    tsum += acc;
   }
-  const uint32_t excl = scan256(c, wsum, nullptr);
-  dbase[tid] = excl;
-  info[(size_t)tid * ntiles + tile] = (excl << 16) | c;
-  if (c) atomicAdd(&tot[tid], c);
+  uint32_t excl = scan256(tsum, wsum, nullptr);
+#pragma unroll
+  for (uint32_t j = 0; j < DPT; j++) {
+    const uint32_t d = tid * DPT + j;
+    info[(size_t)d * ntiles + tile] = (excl << 16) | c[j];
+#pragma unroll
+    for (uint32_t w = 0; w < 4; w++) wcnt[w][d] += excl;  // rows now hold tile-relative bases
+    excl += c[j];
+  }
   __syncthreads();
 #pragma unroll
   for (uint32_t i = 0; i < PART_ITEMS; i++) {
     if (wbase + i * 64 + lane < n) {
-      const uint32_t d = kk[i] >> 24;
-      const uint32_t p = tile * PART_TILE + dbase[d] + wcnt[wave][d] + pos[i];
+      const uint32_t d = kk[i] >> (32 - PART_BITS);
+      const uint32_t p = tile * PART_TILE + wcnt[wave][d] + pos[i];
       kout[p] = kk[i];
       vout[p] = vv[i];
+      hout[p] = hh[i];
     }
   }
 }
 
-#ifdef RL_BK_PROF  // bucketbench only: per-bucket phase stamps
-__device__ unsigned long long g_bk_prof[256 * 16];
-#define BK_STAMP(k) \
-  if (threadIdx.x == 0) g_bk_prof[blockIdx.x * 16 + (k)] = wall_clock64()
-#else
-#define BK_STAMP(k)
-#endif
-
-// LDS of one k_bucket workgroup.
+// LDS of one bucket workgroup (the tile segment table is in dynamic LDS).
+template <typename B>
 struct BucketLds {
-  uint32_t k[BK_CAP], v[BK_CAP];      // the bucket (fast path) in sorted order
-  uint32_t wcnt[BK_WAVES][256];       // multisplit rows
-  uint32_t seg[MAX_PART_TILES + 1];   // bucket position where each tile's segment starts
-  uint32_t src[MAX_PART_TILES];       // tile-layout index of a segment's element = src[t] + position
-  uint32_t base[256];                 // digit offsets: chunk-local (fast) / running in the bucket (slow)
-  uint32_t roff[3][256];              // slow path: running digit offsets per pass
+  uint32_t k[B::CAP], v[B::CAP], h[B::CAP];  // a bucket / chunk in sorted order: key, index, hits
+  uint32_t wcnt[B::WAVES][256];             // multisplit rows
+  uint32_t gsum[B::WAVES / 4][256];         // digit counts per group of 4 waves
+  uint32_t base[256];                       // digit offsets: chunk-local / running in the bucket
+  uint32_t roff[3][256];                    // large buckets: running digit offsets per pass
   uint32_t dtot[256];
-  uint32_t gsum[4][256];              // bucket_rank: digit counts per group of 4 waves
-  uint32_t wsum[BK_WAVES];
-  SegPair sp[BK_WAVES];
-  uint32_t sh[BK_WAVES];
+  uint32_t wsum[B::WAVES];
+  SegPair sp[B::WAVES];
+  uint32_t sh[B::WAVES];
   SegPair carry;
-  uint32_t hcarry, rb, nruns;
+  uint32_t hcarry, rb, nruns, S, base_pos;
+  // large buckets: heavy keys peeled off (bucket_peel)
+  uint32_t heavy[BK_HEAVY];           // sampled heavy keys (class c)
+  uint32_t hcnt[BK_HEAVY];            // elements per class
+  uint32_t hstart[BK_HEAVY];          // first bucket position of each class's block
+  uint32_t hrun[BK_HEAVY];            // elements of the class placed so far
+  uint32_t hw[B::WAVES][BK_HEAVY];    // per-wave class counts of a chunk
+  uint32_t hsw[B::WAVES][BK_HEAVY];   // per-wave class sums of max(1, hits) of a chunk
+  uint32_t acc[1 + 2 * BK_HEAVY];     // k_big_place: sums over the bucket's earlier chunks
+  uint32_t lw[B::WAVES];              // per-wave light counts of a chunk
+  uint32_t nheavy, nlight;
 };
+
+extern __shared__ uint32_t bk_seg[];  // [ntiles + 1] segment starts, then [ntiles] sources
 
 // Bucket positions -> indices in the tile layout: for each item the last tile
 // t with seg[t] <= p (a segment holding p), by a fixed-depth search whose
 // levels visit all items together (independent LDS reads in flight).
 template <uint32_t IT>
-__device__ inline void bucket_src(const BucketLds& L, uint32_t ntiles, const uint32_t (&p)[IT], uint32_t (&j)[IT]) {
+__device__ inline void bucket_src(uint32_t ntiles, const uint32_t (&p)[IT], uint32_t (&j)[IT]) {
+  const uint32_t* seg = bk_seg;
+  const uint32_t* src = bk_seg + ntiles + 1;
   uint32_t lo[IT];
 #pragma unroll
   for (uint32_t i = 0; i < IT; i++) lo[i] = 0;
 #pragma unroll
   for (uint32_t step = MAX_PART_TILES / 2; step; step >>= 1) {
+    if (step >= ntiles) continue;  // uniform
 #pragma unroll
     for (uint32_t i = 0; i < IT; i++) {
       const uint32_t m = lo[i] + step;
-      if (m < ntiles && L.seg[m] <= p[i]) lo[i] = m;
+      if (m < ntiles && seg[m] <= p[i]) lo[i] = m;
     }
   }
 #pragma unroll
-  for (uint32_t i = 0; i < IT; i++) j[i] = L.src[lo[i]] + p[i];
+  for (uint32_t i = 0; i < IT; i++) j[i] = src[lo[i]] + p[i];
 }
 
-// Rank one chunk (BK_ITEMS per lane, wave-strip layout) by digit [shift, shift+8):
-// pos = L.base[d] + (earlier waves' count of d) + rank in the wave. With
-// chunk_scan, L.base becomes the chunk's own exclusive digit offsets first.
-// L.dtot = the chunk's digit counts. Ends with a barrier.
-__device__ inline void bucket_rank(BucketLds& L, const uint32_t (&kk)[BK_ITEMS], uint32_t strip0, uint32_t limit,
-                                   uint32_t shift, bool chunk_scan, uint32_t (&pos)[BK_ITEMS]) {
+// Wave-sum of v over the block (all threads call); result in every thread.
+template <typename B>
+__device__ inline uint32_t block_sum(BucketLds<B>& L, uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (uint32_t off = 32; off; off >>= 1) v += __shfl_xor(v, off, 64);
+  if (lane == 0) L.wsum[wave] = v;
+  __syncthreads();
+  uint32_t s = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < B::WAVES; w++) s += L.wsum[w];
+  __syncthreads();
+  return s;
+}
+
+// Bucket d's size, its first position in the sorted batch and its tile
+// segment table (starts = exclusive scan of the tile counts) in bk_seg.
+template <typename B>
+__device__ inline void bucket_setup(BucketLds<B>& L, const uint32_t* __restrict__ info, uint32_t ntiles, uint32_t d) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t* seg = bk_seg;
+  uint32_t* src = bk_seg + ntiles + 1;
+  uint32_t carry = 0, offs = 0;
+  for (uint32_t t0 = 0; t0 < ntiles; t0 += B::THREADS) {
+    const uint32_t t = t0 + tid;
+    const uint32_t e = t < ntiles ? info[(size_t)d * ntiles + t] : 0u;
+    const uint32_t cnt = e & 0xFFFFu;
+    offs += e >> 16;
+    uint32_t inc = cnt;
+#pragma unroll
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(inc, off, 64);
+      if (lane >= off) inc += y;
+    }
+    if (lane == 63) L.wsum[wave] = inc;
+    __syncthreads();
+    uint32_t pre = carry, all = carry;
+    for (uint32_t w = 0; w < B::WAVES; w++) {
+      pre += w < wave ? L.wsum[w] : 0u;
+      all += L.wsum[w];
+    }
+    if (t < ntiles) {
+      const uint32_t st = pre + inc - cnt;
+      seg[t] = st;
+      src[t] = t * PART_TILE + (e >> 16) - st;
+    }
+    carry = all;
+    __syncthreads();
+  }
+  const uint32_t bp = block_sum(L, offs);
+  if (tid == 0) {
+    seg[ntiles] = carry;
+    L.S = carry;
+    L.base_pos = bp;
+  }
+  __syncthreads();
+}
+
+// Rank one chunk (IT items per lane, wave-strip layout) by the BITS-bit digit
+// at `shift`: pos = L.base[d] + (earlier waves' count of d) + rank in the
+// wave. With chunk_scan, L.base becomes the chunk's own exclusive digit
+// offsets first. L.dtot = the chunk's digit counts. Ends with a barrier.
+template <typename B, uint32_t BITS>
+__device__ inline void bucket_rank(BucketLds<B>& L, const uint32_t (&kk)[B::ITEMS], uint32_t strip0, uint32_t limit,
+                                   uint32_t shift, bool chunk_scan, uint32_t (&pos)[B::ITEMS]) {
   const uint32_t tid = threadIdx.x, wave = tid >> 6;
-  for (uint32_t j = tid; j < BK_WAVES * 256; j += BK_THREADS) (&L.wcnt[0][0])[j] = 0;
+  for (uint32_t j = tid; j < B::WAVES * 256; j += B::THREADS) (&L.wcnt[0][0])[j] = 0;
   __syncthreads();
-  if (shift == 0 && chunk_scan) BK_STAMP(8);
-  uint32_t local[BK_ITEMS];
-  wave_multisplit(kk, strip0, limit, shift, L.wcnt[wave], local);
+  uint32_t local[B::ITEMS];
+  wave_multisplit<B::ITEMS, BITS>(kk, strip0, limit, shift, L.wcnt[wave], local);
   __syncthreads();
-  if (shift == 0 && chunk_scan) BK_STAMP(9);
-  // per digit, exclusive offsets over the 16 wave rows: thread (g, d) scans rows
+  // per digit, exclusive offsets over the wave rows: thread (g, d) scans rows
   // 4g..4g+3 of digit d, then adds the totals of the groups before g
-  constexpr uint32_t G = BK_WAVES / 4;
+  constexpr uint32_t NG = B::WAVES / 4;
   const uint32_t dg = tid & 255u, g = tid >> 8;
-  uint32_t r[G], c = 0;
+  uint32_t r[4], c = 0;
 #pragma unroll
-  for (uint32_t w = 0; w < G; w++) r[w] = L.wcnt[g * G + w][dg];
+  for (uint32_t w = 0; w < 4; w++) r[w] = L.wcnt[g * 4 + w][dg];
 #pragma unroll
-  for (uint32_t w = 0; w < G; w++) {
+  for (uint32_t w = 0; w < 4; w++) {
     const uint32_t t = r[w];
     r[w] = c;
     c += t;
@@ -1593,70 +1385,95 @@ __device__ inline void bucket_rank(BucketLds& L, const uint32_t (&kk)[BK_ITEMS],
   __syncthreads();
   uint32_t pre = 0, all = 0;
 #pragma unroll
-  for (uint32_t q = 0; q < 4; q++) {
+  for (uint32_t q = 0; q < NG; q++) {
     const uint32_t t = L.gsum[q][dg];
     pre += q < g ? t : 0u;
     all += t;
   }
 #pragma unroll
-  for (uint32_t w = 0; w < G; w++) L.wcnt[g * G + w][dg] = r[w] + pre;
+  for (uint32_t w = 0; w < 4; w++) L.wcnt[g * 4 + w][dg] = r[w] + pre;
   if (tid < 256) L.dtot[tid] = all;
   const uint32_t excl = scan256(tid < 256 ? all : 0u, L.wsum, nullptr);
   if (chunk_scan && tid < 256) L.base[tid] = excl;
   __syncthreads();
-  if (shift == 0 && chunk_scan) BK_STAMP(10);
 #pragma unroll
-  for (uint32_t i = 0; i < BK_ITEMS; i++) {
-    const uint32_t d = (kk[i] >> shift) & 255u;
+  for (uint32_t i = 0; i < B::ITEMS; i++) {
+    const uint32_t d = (kk[i] >> shift) & ((1u << BITS) - 1u);
     pos[i] = L.base[d] + L.wcnt[wave][d] + local[i];
   }
   __syncthreads();
-  if (shift == 0 && chunk_scan) BK_STAMP(11);
 }
 
-// Wave-sum of v over the block (all threads call); result in every thread.
-__device__ inline uint32_t block_sum(BucketLds& L, uint32_t v) {
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// Stable sort of n <= CAP (key, value, hits) triples held in wave-strip
+// order in registers by key bits [0, 32 - PART_BITS): passes of 8, 8 and 6
+// bits, each ranked in LDS and scattered through L.k / L.v / L.h. On return
+// L.k / L.v / L.h and kk / vv / hh hold the sorted triples.
+template <typename B>
+__device__ inline void lds_sort3(BucketLds<B>& L, uint32_t (&kk)[B::ITEMS], uint32_t (&vv)[B::ITEMS],
+                                 uint32_t (&hh)[B::ITEMS], uint32_t n) {
+  static_assert(32 - PART_BITS == 22, "passes of 8 + 8 + 6 bits");
+  const uint32_t lane = threadIdx.x & 63, strip0 = (threadIdx.x >> 6) * B::STRIP;
+  uint32_t pos[B::ITEMS];
+#pragma unroll 1
+  for (uint32_t pass = 0; pass < 3; pass++) {
+    if (pass < 2) bucket_rank<B, 8>(L, kk, strip0, n, 8 * pass, true, pos);
+    else bucket_rank<B, 6>(L, kk, strip0, n, 16, true, pos);
 #pragma unroll
-  for (uint32_t off = 32; off; off >>= 1) v += __shfl_xor(v, off, 64);
-  if (lane == 0) L.wsum[wave] = v;
-  __syncthreads();
-  uint32_t s = 0;
+    for (uint32_t i = 0; i < B::ITEMS; i++) {
+      if (strip0 + i * 64 + lane < n) {
+        L.k[pos[i]] = kk[i];
+        L.v[pos[i]] = vv[i];
+        L.h[pos[i]] = hh[i];
+      }
+    }
+    __syncthreads();
 #pragma unroll
-  for (uint32_t w = 0; w < BK_WAVES; w++) s += L.wsum[w];
-  __syncthreads();
-  return s;
+    for (uint32_t i = 0; i < B::ITEMS; i++) {
+      const uint32_t p = strip0 + i * 64 + lane;
+      if (p < n) {
+        kk[i] = L.k[p];
+        vv[i] = L.v[p];
+        hh[i] = L.h[p];
+      }
+    }
+  }
 }
 
-// Segment the sorted bucket [0, S) (keys/values from LDS or from the sorted
-// global arrays at base): records into sorted order, in-run sums, run ids and
-// run bounds. Chunks of BK_CAP positions; each wave walks its strip of the
-// chunk in 64-position pieces, and the 16 wave aggregates plus the carry of
-// the earlier chunks give every wave its exclusive prefix.
-template <bool FROM_LDS>
-__device__ inline void bucket_segment(BucketLds& L, uint32_t S, uint32_t base, const uint32_t* __restrict__ sk,
-                                      const uint32_t* __restrict__ sv, const Rec* __restrict__ rec,
-                                      Rec* __restrict__ rec_s, uint32_t* __restrict__ segsum,
-                                      uint32_t* __restrict__ rid, uint32_t* __restrict__ run_start,
-                                      uint32_t* __restrict__ run_end, uint32_t* num_runs) {
+// Segment the sorted bucket [0, S) (keys / hits from LDS or from the sorted
+// global arrays at base): in-run sums, run ids and run bounds. Chunks of CAP
+// positions; each wave walks its strip of the chunk in 64-position pieces, and
+// the wave aggregates plus the carry of the earlier chunks give every wave its
+// exclusive prefix. Every gather is an unconditional load at a clamped
+// position, issued in a straight-line loop before any use, so all of a lane's
+// loads are in flight together (a load under a branch is waited for on the spot).
+template <typename B, bool FROM_LDS>
+__device__ inline void bucket_segment(BucketLds<B>& L, uint32_t d, uint32_t S, uint32_t base,
+                                      const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sh,
+                                      uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
+                                      uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end,
+                                      uint32_t* num_runs) {
+  constexpr uint32_t IT = B::ITEMS;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   auto key = [&](uint32_t p) -> uint32_t { return FROM_LDS ? L.k[p] : sk[base + p]; };
-  auto val = [&](uint32_t p) -> uint32_t { return FROM_LDS ? L.v[p] : sv[base + p]; };
+  auto hit = [&](uint32_t p) -> uint32_t { return FROM_LDS ? L.h[p] : sh[base + p]; };
   // runs of the bucket -> run id base
   uint32_t nh = 0;
-  for (uint32_t c0 = 0; c0 < S; c0 += BK_CAP) {
-    uint32_t a[BK_ITEMS], b[BK_ITEMS];
+  for (uint32_t c0 = 0; c0 < S; c0 += B::CAP) {
+    uint32_t a[IT], b[IT];
 #pragma unroll
-    for (uint32_t i = 0; i < BK_ITEMS; i++) {  // loads first, BK_ITEMS pairs in flight
-      const uint32_t p = c0 + i * BK_THREADS + tid;
-      a[i] = p < S && p ? key(p - 1) : 0u;
-      b[i] = p < S && p ? key(p) : 1u;
+    for (uint32_t i = 0; i < IT; i++) {
+      const uint32_t p = min(c0 + i * B::THREADS + tid, S - 1);
+      a[i] = key(p ? p - 1 : 0);
+      b[i] = key(p);
     }
 #pragma unroll
-    for (uint32_t i = 0; i < BK_ITEMS; i++) nh += (c0 + i * BK_THREADS + tid < S && a[i] != b[i]) ? 1u : 0u;
+    for (uint32_t i = 0; i < IT; i++) {
+      const uint32_t p = c0 + i * B::THREADS + tid;
+      nh += (p < S && (p == 0 || a[i] != b[i])) ? 1u : 0u;
+    }
   }
   nh = block_sum(L, nh);
-  BK_STAMP(4);
+  BK_STAMP(d, 4);
   if (tid == 0) {
     L.rb = atomicAdd(num_runs, nh);
     L.nruns = nh;
@@ -1665,31 +1482,33 @@ __device__ inline void bucket_segment(BucketLds& L, uint32_t S, uint32_t base, c
   }
   __syncthreads();
   const uint32_t rb = L.rb;
-  for (uint32_t c0 = 0; c0 < S; c0 += BK_CAP) {
-    const uint32_t s0 = c0 + wave * BK_STRIP;
-    SegChunk ch[BK_ITEMS];
+  for (uint32_t c0 = 0; c0 < S; c0 += B::CAP) {
+    const uint32_t s0 = c0 + wave * B::STRIP;
+    const uint32_t ni = s0 >= S ? 0u : min(IT, (S - s0 + 63) / 64);  // items of this wave in the bucket
+    SegChunk ch[IT];
     SegPair agg{0, 0};
     uint32_t hc = 0;
-    bool hd[BK_ITEMS];
-    uint32_t hvs[BK_ITEMS];
+    uint32_t kp[IT], kq[IT], hq[IT];
 #pragma unroll
-    for (uint32_t j = 0; j < BK_ITEMS; j++) {  // gathers first (all in flight), scans after
+    for (uint32_t j = 0; j < IT; j++) {
+      const uint32_t q = min(s0 + 64 * j + lane, S - 1);
+      kp[j] = key(q ? q - 1 : 0);
+      kq[j] = key(q);
+      hq[j] = hit(q);
+    }
+    uint32_t hd = 0;  // head flags, bit j
+#pragma unroll
+    for (uint32_t j = 0; j < IT; j++) {
       const uint32_t q = s0 + 64 * j + lane;
-      hd[j] = false;
-      hvs[j] = 0;
-      if (q < S) {
-        const uint32_t kq = key(q);
-        hd[j] = q == 0 || key(q - 1) != kq;
-        const Rec r = rec[val(q)];
-        rec_s[base + q] = r;
-        hvs[j] = r.hits > 1 ? r.hits : 1u;
-      }
+      hd |= (q < S && (q == 0 || kp[j] != kq[j])) ? 1u << j : 0u;
     }
 #pragma unroll
-    for (uint32_t j = 0; j < BK_ITEMS; j++) {
-      const bool head = hd[j];
-      const uint32_t hv = hvs[j];
-      ch[j] = SegChunk{(uint64_t)__ballot(head), hv};
+    for (uint32_t j = 0; j < IT; j++) {
+      ch[j] = SegChunk{0, 0};
+      if (j >= ni) continue;  // wave-uniform
+      // max(1, HitsAddend) (utils.Max, fixed_cache_impl.go:41); 0 past the bucket
+      const uint32_t hv = s0 + 64 * j + lane < S ? (hq[j] > 1 ? hq[j] : 1u) : 0u;
+      ch[j] = SegChunk{(uint64_t)__ballot((hd >> j) & 1u), hv};
       uint32_t t = hv;  // piece total, segmented: sum after the last head
       const uint32_t lh = ch[j].heads ? 63u - (uint32_t)__clzll((long long)ch[j].heads) : 0u;
       if (ch[j].heads && lane < lh) t = 0;
@@ -1707,7 +1526,7 @@ __device__ inline void bucket_segment(BucketLds& L, uint32_t S, uint32_t base, c
     uint32_t hrun = L.hcarry;
     SegPair tot = run;
     uint32_t htot = hrun;
-    for (uint32_t w = 0; w < BK_WAVES; w++) {
+    for (uint32_t w = 0; w < B::WAVES; w++) {
       if (w == wave) {
         run = tot;
         hrun = htot;
@@ -1721,7 +1540,8 @@ __device__ inline void bucket_segment(BucketLds& L, uint32_t S, uint32_t base, c
       L.hcarry = htot;
     }
 #pragma unroll
-    for (uint32_t j = 0; j < BK_ITEMS; j++) {
+    for (uint32_t j = 0; j < IT; j++) {
+      if (j >= ni) continue;  // wave-uniform
       const uint32_t q = s0 + 64 * j + lane;
       const SegPair v = seg_chunk_scan(ch[j], lane);
       const SegPair in = seg_op(run, v);
@@ -1743,125 +1563,354 @@ __device__ inline void bucket_segment(BucketLds& L, uint32_t S, uint32_t base, c
   if (tid == 0 && S) run_end[rb + L.nruns - 1] = base + S;
 }
 
-__global__ __launch_bounds__(BK_THREADS) void k_bucket(const uint32_t* __restrict__ pk, const uint32_t* __restrict__ pv,
-                                                       const uint32_t* __restrict__ info,
-                                                       const uint32_t* __restrict__ tot, uint32_t ntiles,
-                                                       const Rec* __restrict__ rec, uint32_t* __restrict__ sk,
-                                                       uint32_t* __restrict__ sv, Rec* __restrict__ rec_s,
-                                                       uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
-                                                       uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end,
-                                                       uint32_t* num_runs, const uint32_t* err) {
-  __shared__ BucketLds L;
-  __shared__ uint32_t s_base, s_S;
+constexpr uint32_t BIG_CHUNK = BkSmall::CAP;
+constexpr uint32_t BIG_LIGHT_CAP = BkBig::CAP;
+constexpr uint32_t BIG_CNT = 1 + 2 * BK_HEAVY;  // per work item: light count, class counts, class hit sums
+
+// Hot keys of a large bucket: 64 evenly spaced positions are sampled by wave
+// 0; keys seen at least BK_HEAVY_MIN times become L.heavy[0..L.nheavy).
+template <typename B>
+__device__ inline void sample_heavy(BucketLds<B>& L, uint32_t S, uint32_t ntiles, const uint32_t* __restrict__ pk) {
+  const uint32_t lane = threadIdx.x & 63;
+  if ((threadIdx.x >> 6) == 0) {
+    uint32_t p[1] = {(uint32_t)(((uint64_t)(2 * lane + 1) * S) >> 7)}, j[1];
+    bucket_src(ntiles, p, j);
+    const uint32_t ks = pk[j[0]];
+    uint32_t cnt = 0;
+    bool first = true;
+    for (uint32_t q = 0; q < 64; q++) {
+      const uint32_t kq = __shfl(ks, q, 64);
+      cnt += kq == ks ? 1u : 0u;
+      if (q < lane && kq == ks) first = false;
+    }
+    const bool cand = first && cnt >= BK_HEAVY_MIN;
+    const uint64_t b = __ballot(cand);
+    const uint32_t rank = __popcll(b & ((1ull << lane) - 1));
+    if (cand && rank < BK_HEAVY) L.heavy[rank] = ks;
+    if (lane == 0) L.nheavy = min((uint32_t)__popcll(b), BK_HEAVY);
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
+    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ pv, const uint32_t* __restrict__ ph,
+    const uint32_t* __restrict__ info, uint32_t ntiles, uint32_t* __restrict__ sk, uint32_t* __restrict__ sv,
+    uint32_t* __restrict__ sh, uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
+    uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end, uint32_t* num_runs,
+    BigMeta* __restrict__ meta, uint32_t* big_n, uint32_t* __restrict__ work, uint32_t* work_n,
+    const uint32_t* err) {
+  using B = BkSmall;
+  __shared__ BucketLds<B> L;
   if (*err) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, d = blockIdx.x;
-  BK_STAMP(0);
-  {  // bucket position in the sorted batch
-    const uint32_t v = tid < 256 ? tot[tid] : 0u;
-    const uint32_t excl = scan256(v, L.wsum, nullptr);
-    if (tid == d) {
-      s_base = excl;
-      s_S = v;
-    }
-    __syncthreads();
-  }
-  const uint32_t base = s_base, S = s_S;
+  BK_STAMP(d, 0);
+  bucket_setup(L, info, ntiles, d);
+  const uint32_t S = L.S, base = L.base_pos;
   if (!S) return;
-  // tile segments of the bucket: starts (exclusive scan of the counts) and sources
-  for (uint32_t t0 = 0; t0 < ntiles; t0 += BK_THREADS) {
-    const uint32_t t = t0 + tid;
-    const uint32_t e = t < ntiles ? info[(size_t)d * ntiles + t] : 0u;
-    const uint32_t cnt = e & 0xFFFFu;
-    uint32_t inc = cnt;
-#pragma unroll
-    for (uint32_t off = 1; off < 64; off <<= 1) {
-      const uint32_t y = __shfl_up(inc, off, 64);
-      if (lane >= off) inc += y;
-    }
-    if (lane == 63) L.wsum[wave] = inc;
-    __syncthreads();
-    uint32_t pre = t0 ? L.seg[t0] : 0u;  // carried from the previous round
-    for (uint32_t w = 0; w < wave; w++) pre += L.wsum[w];
-    if (t < ntiles) {
-      const uint32_t st = pre + inc - cnt;
-      L.seg[t] = st;
-      L.src[t] = t * PART_TILE + (e >> 16) - st;
-    }
-    __syncthreads();
-    if (tid == BK_THREADS - 1 && t0 + BK_THREADS < ntiles) L.seg[t0 + BK_THREADS] = pre + inc;  // next round's carry
-    __syncthreads();
-  }
-  if (tid == 0) L.seg[ntiles] = S;
-  __syncthreads();
-  BK_STAMP(1);
-  uint32_t kk[BK_ITEMS], vv[BK_ITEMS], pos[BK_ITEMS];
-  if (S <= BK_CAP) {
-    // ---- fast path: the bucket lives in registers / LDS for all three passes
-    const uint32_t strip0 = wave * BK_STRIP;
-    uint32_t pp[BK_ITEMS], jj[BK_ITEMS];
-#pragma unroll
-    for (uint32_t i = 0; i < BK_ITEMS; i++) pp[i] = min(strip0 + i * 64 + lane, S - 1);
-    bucket_src(L, ntiles, pp, jj);
-#pragma unroll
-    for (uint32_t i = 0; i < BK_ITEMS; i++) {
-      const bool in = strip0 + i * 64 + lane < S;
-      kk[i] = in ? pk[jj[i]] : 0xFFFFFFFFu;
-      vv[i] = in ? pv[jj[i]] : 0u;
-    }
-    BK_STAMP(2);
-    for (uint32_t pass = 0; pass < 3; pass++) {
-      bucket_rank(L, kk, strip0, S, 8 * pass, true, pos);
-#pragma unroll
-      for (uint32_t i = 0; i < BK_ITEMS; i++) {
-        if (strip0 + i * 64 + lane < S) {
-          L.k[pos[i]] = kk[i];
-          L.v[pos[i]] = vv[i];
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (uint32_t i = 0; i < BK_ITEMS; i++) {
-        const uint32_t p = strip0 + i * 64 + lane;
-        if (p < S) {
-          kk[i] = L.k[p];
-          vv[i] = L.v[p];
-        }
-      }
-      if (pass == 0) BK_STAMP(12);
-    }
-#pragma unroll
-    for (uint32_t i = 0; i < BK_ITEMS; i++) {
-      const uint32_t p = strip0 + i * 64 + lane;
-      if (p < S) {
-        sk[base + p] = kk[i];
-        sv[base + p] = vv[i];
-      }
+  if (S > B::CAP) {  // queued: hot keys sampled, their run ids and the chunk work items allocated
+    sample_heavy(L, S, ntiles, pk);
+    if (tid == 0) {
+      BigMeta M;
+      M.d = d;
+      M.S = S;
+      M.base = base;
+      M.r = L.nheavy;
+      M.nchunks = M.r ? (S + BIG_CHUNK - 1) / BIG_CHUNK : 0u;
+      M.item0 = M.nchunks ? atomicAdd(work_n, M.nchunks) : 0u;
+      M.rb_heavy = M.r ? atomicAdd(num_runs, M.r) : 0u;
+      M.pad = 0;
+      for (uint32_t c = 0; c < BK_HEAVY; c++) M.heavy[c] = c < M.r ? L.heavy[c] : 0u;
+      const uint32_t b = atomicAdd(big_n, 1u);
+      meta[b] = M;
+      L.rb = b;
+      L.nruns = M.item0;
+      L.hcarry = M.nchunks;
     }
     __syncthreads();
-    BK_STAMP(3);
-    bucket_segment<true>(L, S, base, sk, sv, rec, rec_s, segsum, rid, run_start, run_end, num_runs);
-    BK_STAMP(5);
+    for (uint32_t t = tid; t < L.hcarry; t += B::THREADS) work[L.nruns + t] = (L.rb << 16) | t;
     return;
   }
-  // ---- large bucket: the same three stable passes, chunk by chunk through HBM
-  // (tile layout -> sk -> temp -> sk; temp = this bucket's rid / segsum ranges,
-  // which the segmentation overwrites afterwards). Running digit offsets per
-  // pass come from one histogram sweep.
-  for (uint32_t j = tid; j < 3 * 256; j += BK_THREADS) (&L.roff[0][0])[j] = 0;
+  BK_STAMP(d, 1);
+  uint32_t kk[B::ITEMS], vv[B::ITEMS], hh[B::ITEMS];
+  const uint32_t strip0 = wave * B::STRIP;
+  uint32_t pp[B::ITEMS], jj[B::ITEMS];
+#pragma unroll
+  for (uint32_t i = 0; i < B::ITEMS; i++) pp[i] = min(strip0 + i * 64 + lane, S - 1);
+  bucket_src(ntiles, pp, jj);
+#pragma unroll
+  for (uint32_t i = 0; i < B::ITEMS; i++) {
+    kk[i] = pk[jj[i]];
+    vv[i] = pv[jj[i]];
+    hh[i] = ph[jj[i]];
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < B::ITEMS; i++)
+    if (strip0 + i * 64 + lane >= S) kk[i] = 0xFFFFFFFFu;
+  BK_STAMP(d, 2);
+  lds_sort3(L, kk, vv, hh, S);
+#pragma unroll
+  for (uint32_t i = 0; i < B::ITEMS; i++) {
+    const uint32_t p = strip0 + i * 64 + lane;
+    if (p < S) {
+      sk[base + p] = kk[i];
+      sv[base + p] = vv[i];
+    }
+  }
+  BK_STAMP(d, 3);
+  bucket_segment<B, true>(L, d, S, base, sk, sh, segsum, rid, run_start, run_end, num_runs);
+  BK_STAMP(d, 5);
+}
+
+// Large bucket dominated by a few keys (hot tenants): sample 64 positions;
+// keys seen at least BK_HEAVY_MIN times are "heavy". Pass A compacts the light
+// elements (arrival order) into LDS and counts each heavy key; the light ones
+// are sorted in LDS; each heavy key's elements then form one block, placed
+// between the light keys by key order, filled in arrival order by pass B.
+// Returns false (nothing written) when no key is heavy or the light elements
+// do not fit in LDS.
+template <typename B>
+__device__ inline bool bucket_peel(BucketLds<B>& L, uint32_t d, uint32_t S, uint32_t base, uint32_t ntiles,
+                                   const uint32_t* __restrict__ pk, const uint32_t* __restrict__ pv,
+                                   const uint32_t* __restrict__ ph, uint32_t* __restrict__ sk,
+                                   uint32_t* __restrict__ sv, uint32_t* __restrict__ sh) {
+  constexpr uint32_t IT = B::ITEMS;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t lt_mask = (1ull << lane) - 1;
+  if (wave == 0) {
+    uint32_t p[1] = {(uint32_t)(((uint64_t)(2 * lane + 1) * S) >> 7)}, j[1];
+    bucket_src(ntiles, p, j);
+    const uint32_t ks = pk[j[0]];
+    uint32_t cnt = 0;
+    bool first = true;
+    for (uint32_t q = 0; q < 64; q++) {
+      const uint32_t kq = __shfl(ks, q, 64);
+      cnt += kq == ks ? 1u : 0u;
+      if (q < lane && kq == ks) first = false;
+    }
+    const bool cand = first && cnt >= BK_HEAVY_MIN;
+    const uint64_t b = __ballot(cand);
+    const uint32_t rank = __popcll(b & lt_mask);
+    if (cand && rank < BK_HEAVY) L.heavy[rank] = ks;
+    if (lane < BK_HEAVY) {
+      L.hcnt[lane] = 0;
+      L.hrun[lane] = 0;
+    }
+    if (lane == 0) {
+      L.nheavy = min((uint32_t)__popcll(b), BK_HEAVY);
+      L.nlight = 0;
+    }
+  }
   __syncthreads();
-  for (uint32_t c0 = 0; c0 < S; c0 += BK_CAP) {
-    uint32_t pp[BK_ITEMS], jj[BK_ITEMS];
+  const uint32_t r = L.nheavy;
+  if (!r) return false;
+  uint32_t hk[BK_HEAVY];
 #pragma unroll
-    for (uint32_t i = 0; i < BK_ITEMS; i++) pp[i] = min(c0 + i * BK_THREADS + tid, S - 1);
-    bucket_src(L, ntiles, pp, jj);
+  for (uint32_t c = 0; c < BK_HEAVY; c++) hk[c] = __builtin_amdgcn_readfirstlane(c < r ? L.heavy[c] : 0u);
+  uint32_t kk[IT], vv[IT], hh[IT], cls[IT];
+  // ---- pass A: light elements -> L.k / L.v / L.h (arrival order), class counts
+  for (uint32_t c0 = 0; c0 < S; c0 += B::CAP) {
+    const uint32_t strip0 = c0 + wave * B::STRIP;
+    uint32_t pp[IT], jj[IT];
 #pragma unroll
-    for (uint32_t i = 0; i < BK_ITEMS; i++) kk[i] = pk[jj[i]];  // loads first, BK_ITEMS in flight
+    for (uint32_t i = 0; i < IT; i++) pp[i] = min(strip0 + i * 64 + lane, S - 1);
+    bucket_src(ntiles, pp, jj);
 #pragma unroll
-    for (uint32_t i = 0; i < BK_ITEMS; i++) {
-      if (c0 + i * BK_THREADS + tid < S) {
+    for (uint32_t i = 0; i < IT; i++) {
+      kk[i] = pk[jj[i]];
+      vv[i] = pv[jj[i]];
+      hh[i] = ph[jj[i]];
+    }
+    uint32_t wl = 0, lr[IT];
+    uint32_t wc[BK_HEAVY];
+#pragma unroll
+    for (uint32_t c = 0; c < BK_HEAVY; c++) wc[c] = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < IT; i++) {
+      const bool in = strip0 + i * 64 + lane < S;
+      cls[i] = in ? r : 0xFFu;  // light: class r (<= BK_HEAVY); past the bucket: 0xFF
+#pragma unroll
+      for (uint32_t c = 0; c < BK_HEAVY; c++)
+        if (in && c < r && kk[i] == hk[c]) cls[i] = c;
+      const uint64_t bl = __ballot(cls[i] == r);
+      lr[i] = wl + __popcll(bl & lt_mask);
+      wl += __popcll(bl);
+#pragma unroll
+      for (uint32_t c = 0; c < BK_HEAVY; c++) wc[c] += c < r ? __popcll(__ballot(cls[i] == c)) : 0u;
+    }
+    if (lane == 0) {
+      L.lw[wave] = wl;
+#pragma unroll
+      for (uint32_t c = 0; c < BK_HEAVY; c++) L.hw[wave][c] = wc[c];
+    }
+    __syncthreads();
+    uint32_t pre = L.nlight, tl = 0;
+    for (uint32_t w = 0; w < B::WAVES; w++) {
+      pre += w < wave ? L.lw[w] : 0u;
+      tl += L.lw[w];
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < IT; i++) {
+      const uint32_t at = pre + lr[i];
+      if (cls[i] == r && at < B::CAP) {
+        L.k[at] = kk[i];
+        L.v[at] = vv[i];
+        L.h[at] = hh[i];
+      }
+    }
+    __syncthreads();
+    if (tid < BK_HEAVY) {
+      uint32_t t = 0;
+      for (uint32_t w = 0; w < B::WAVES; w++) t += L.hw[w][tid];
+      L.hcnt[tid] += t;
+    }
+    if (tid == 0) L.nlight += tl;
+    __syncthreads();
+  }
+  const uint32_t nl = L.nlight;
+  if (nl > B::CAP) return false;
+  BK_STAMP(d, 13);
+  // ---- sort the light elements in LDS
+  const uint32_t strip0 = wave * B::STRIP;
+#pragma unroll
+  for (uint32_t i = 0; i < IT; i++) {
+    const uint32_t p = strip0 + i * 64 + lane;
+    kk[i] = p < nl ? L.k[p] : 0xFFFFFFFFu;
+    vv[i] = p < nl ? L.v[p] : 0u;
+    hh[i] = p < nl ? L.h[p] : 0u;
+  }
+  if (nl) lds_sort3(L, kk, vv, hh, nl);
+  // ---- block starts: light keys below the heavy key + heavy blocks of smaller keys
+  if (tid < r) {
+    const uint32_t K = hk[tid];
+    uint32_t lo = 0, hi = nl;  // first light index with key >= K
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (L.k[mid] < K) lo = mid + 1;
+      else hi = mid;
+    }
+    uint32_t st = lo;
+    for (uint32_t c = 0; c < r; c++) st += hk[c] < K ? L.hcnt[c] : 0u;
+    L.hstart[tid] = st;
+  }
+#ifdef RL_BK_PROF
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t* g = g_bk_peel + d * 16;
+    g[0] = r;
+    g[1] = nl;
+    for (uint32_t c = 0; c < BK_HEAVY; c++) {
+      g[2 + c] = hk[c];
+      g[6 + c] = L.hcnt[c];
+      g[10 + c] = L.hstart[c];
+    }
+    g[14] = S;
+  }
+#endif
+  // light elements to their final positions (shifted past smaller heavy blocks)
+#pragma unroll
+  for (uint32_t i = 0; i < IT; i++) {
+    const uint32_t p = strip0 + i * 64 + lane;
+    if (p < nl) {
+      uint32_t at = p;
+#pragma unroll
+      for (uint32_t c = 0; c < BK_HEAVY; c++) at += (c < r && hk[c] < kk[i]) ? L.hcnt[c] : 0u;
+      sk[base + at] = kk[i];
+      sv[base + at] = vv[i];
+      sh[base + at] = hh[i];
+    }
+  }
+  __syncthreads();
+  BK_STAMP(d, 14);
+  // ---- pass B: heavy elements, in arrival order within each block
+  for (uint32_t c0 = 0; c0 < S; c0 += B::CAP) {
+    const uint32_t s0 = c0 + wave * B::STRIP;
+    uint32_t pp[IT], jj[IT];
+#pragma unroll
+    for (uint32_t i = 0; i < IT; i++) pp[i] = min(s0 + i * 64 + lane, S - 1);
+    bucket_src(ntiles, pp, jj);
+#pragma unroll
+    for (uint32_t i = 0; i < IT; i++) {
+      kk[i] = pk[jj[i]];
+      vv[i] = pv[jj[i]];
+      hh[i] = ph[jj[i]];
+    }
+    uint32_t hr[IT], wc[BK_HEAVY];
+#pragma unroll
+    for (uint32_t c = 0; c < BK_HEAVY; c++) wc[c] = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < IT; i++) {
+      const bool in = s0 + i * 64 + lane < S;
+      cls[i] = BK_HEAVY;
+#pragma unroll
+      for (uint32_t c = 0; c < BK_HEAVY; c++)
+        if (in && c < r && kk[i] == hk[c]) cls[i] = c;
+      hr[i] = 0;
+#pragma unroll
+      for (uint32_t c = 0; c < BK_HEAVY; c++) {
+        if (c >= r) continue;
+        const uint64_t b = __ballot(cls[i] == c);
+        if (cls[i] == c) hr[i] = wc[c] + __popcll(b & lt_mask);
+        wc[c] += __popcll(b);
+      }
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (uint32_t c = 0; c < BK_HEAVY; c++) L.hw[wave][c] = wc[c];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t i = 0; i < IT; i++) {
+      const uint32_t c = cls[i];
+      if (c < BK_HEAVY) {
+        uint32_t at = L.hstart[c] + L.hrun[c] + hr[i];
+        for (uint32_t w = 0; w < wave; w++) at += L.hw[w][c];
+        sk[base + at] = kk[i];
+        sv[base + at] = vv[i];
+        sh[base + at] = hh[i];
+      }
+    }
+    __syncthreads();
+    if (tid < r) {
+      uint32_t t = 0;
+      for (uint32_t w = 0; w < B::WAVES; w++) t += L.hw[w][tid];
+      L.hrun[tid] += t;
+    }
+    __syncthreads();
+  }
+  __threadfence_block();
+  __syncthreads();
+  BK_STAMP(d, 15);
+  return true;
+}
+
+// Large bucket without (enough) hot keys: the three stable passes chunk by
+// chunk through HBM (tile layout -> sk -> temp -> sk; temp = this bucket's rid
+// / segsum / ht ranges, which the segmentation overwrites or ignores
+// afterwards). Running digit offsets per pass come from one histogram sweep.
+template <typename B>
+__device__ inline void bucket_lsd(BucketLds<B>& L, uint32_t S, uint32_t base, uint32_t ntiles,
+                                  const uint32_t* __restrict__ pk, const uint32_t* __restrict__ pv,
+                                  const uint32_t* __restrict__ ph, uint32_t* __restrict__ sk,
+                                  uint32_t* __restrict__ sv, uint32_t* __restrict__ sh, uint32_t* __restrict__ ht,
+                                  uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid) {
+  constexpr uint32_t IT = B::ITEMS;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t kk[IT], vv[IT], hh[IT], pos[IT];
+  for (uint32_t j = tid; j < 3 * 256; j += B::THREADS) (&L.roff[0][0])[j] = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < S; c0 += B::CAP) {
+    uint32_t pp[IT], jj[IT];
+#pragma unroll
+    for (uint32_t i = 0; i < IT; i++) pp[i] = min(c0 + i * B::THREADS + tid, S - 1);
+    bucket_src(ntiles, pp, jj);
+#pragma unroll
+    for (uint32_t i = 0; i < IT; i++) kk[i] = pk[jj[i]];  // loads first, all in flight
+#pragma unroll
+    for (uint32_t i = 0; i < IT; i++) {
+      if (c0 + i * B::THREADS + tid < S) {
         atomicAdd(&L.roff[0][kk[i] & 255u], 1u);
         atomicAdd(&L.roff[1][(kk[i] >> 8) & 255u], 1u);
-        atomicAdd(&L.roff[2][(kk[i] >> 16) & 255u], 1u);
+        atomicAdd(&L.roff[2][(kk[i] >> 16) & 63u], 1u);
       }
     }
   }
@@ -1875,47 +1924,339 @@ __global__ __launch_bounds__(BK_THREADS) void k_bucket(const uint32_t* __restric
   for (uint32_t pass = 0; pass < 3; pass++) {
     const uint32_t* ik = pass == 0 ? pk : pass == 1 ? sk + base : rid + base;
     const uint32_t* iv = pass == 0 ? pv : pass == 1 ? sv + base : segsum + base;
+    const uint32_t* ih = pass == 0 ? ph : pass == 1 ? sh + base : ht + base;
     uint32_t* ok = pass == 1 ? rid + base : sk + base;
     uint32_t* ov = pass == 1 ? segsum + base : sv + base;
-    for (uint32_t c0 = 0; c0 < S; c0 += BK_CAP) {
-      const uint32_t strip0 = c0 + wave * BK_STRIP;
-      uint32_t pp[BK_ITEMS], jj[BK_ITEMS];
+    uint32_t* oh = pass == 1 ? ht + base : sh + base;
+    for (uint32_t c0 = 0; c0 < S; c0 += B::CAP) {
+      const uint32_t strip0 = c0 + wave * B::STRIP;
+      uint32_t pp[IT], jj[IT];
 #pragma unroll
-      for (uint32_t i = 0; i < BK_ITEMS; i++) pp[i] = min(strip0 + i * 64 + lane, S - 1);
+      for (uint32_t i = 0; i < IT; i++) pp[i] = min(strip0 + i * 64 + lane, S - 1);
       if (pass == 0) {
-        bucket_src(L, ntiles, pp, jj);
+        bucket_src(ntiles, pp, jj);
       } else {
 #pragma unroll
-        for (uint32_t i = 0; i < BK_ITEMS; i++) jj[i] = pp[i];
+        for (uint32_t i = 0; i < IT; i++) jj[i] = pp[i];
       }
 #pragma unroll
-      for (uint32_t i = 0; i < BK_ITEMS; i++) {
-        const bool in = strip0 + i * 64 + lane < S;
-        kk[i] = in ? ik[jj[i]] : 0xFFFFFFFFu;
-        vv[i] = in ? iv[jj[i]] : 0u;
+      for (uint32_t i = 0; i < IT; i++) {
+        kk[i] = ik[jj[i]];
+        vv[i] = iv[jj[i]];
+        hh[i] = ih[jj[i]];
       }
+#pragma unroll
+      for (uint32_t i = 0; i < IT; i++)
+        if (strip0 + i * 64 + lane >= S) kk[i] = 0xFFFFFFFFu;
       if (tid < 256) L.base[tid] = L.roff[pass][tid];
-      bucket_rank(L, kk, strip0, S, 8 * pass, false, pos);
+      if (pass < 2) bucket_rank<B, 8>(L, kk, strip0, S, 8 * pass, false, pos);
+      else bucket_rank<B, 6>(L, kk, strip0, S, 16, false, pos);
       if (tid < 256) L.roff[pass][tid] += L.dtot[tid];
 #pragma unroll
-      for (uint32_t i = 0; i < BK_ITEMS; i++) {
+      for (uint32_t i = 0; i < IT; i++) {
         if (strip0 + i * 64 + lane < S) {
           ok[pos[i]] = kk[i];
           ov[pos[i]] = vv[i];
+          oh[pos[i]] = hh[i];
         }
       }
     }
     __threadfence_block();
     __syncthreads();
   }
-  bucket_segment<false>(L, S, base, sk, sv, rec, rec_s, segsum, rid, run_start, run_end, num_runs);
+}
+
+// ---- Large buckets, chunk-parallel. k_bucket samples a queued bucket's hot
+// keys, allocates their run ids and one work item per BIG_CHUNK positions.
+// k_big_count classifies every chunk (light / hot key c) and counts;
+// k_big_place writes each hot key's elements straight to its block (after the
+// bucket's light part, in arrival order: positions, in-run hit sums, run id)
+// and compacts the light elements, in arrival order, into the front of the
+// bucket; k_bucket_big then sorts and segments the light part in LDS (or, for
+// a bucket without hot keys or with too many light elements, runs the whole
+// single-workgroup path).
+__device__ inline uint32_t wave_sum32(uint32_t x) {
+#pragma unroll
+  for (uint32_t m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+  return x;
+}
+
+// Load one chunk of a queued bucket (BkSmall shape) and classify it: cls =
+// hot key index c < r, r for a light element, 0xFF past the bucket.
+__device__ inline void big_chunk_load(const BigMeta& M, uint32_t j, uint32_t ntiles, const uint32_t* __restrict__ pk,
+                                      const uint32_t* __restrict__ pv, const uint32_t* __restrict__ ph,
+                                      uint32_t (&kk)[BkSmall::ITEMS], uint32_t (&vv)[BkSmall::ITEMS],
+                                      uint32_t (&hh)[BkSmall::ITEMS], uint32_t (&cls)[BkSmall::ITEMS], bool values) {
+  using B = BkSmall;
+  const uint32_t lane = threadIdx.x & 63, s0 = j * BIG_CHUNK + (threadIdx.x >> 6) * B::STRIP;
+  uint32_t pp[B::ITEMS], jj[B::ITEMS];
+#pragma unroll
+  for (uint32_t i = 0; i < B::ITEMS; i++) pp[i] = min(s0 + i * 64 + lane, M.S - 1);
+  bucket_src(ntiles, pp, jj);
+#pragma unroll
+  for (uint32_t i = 0; i < B::ITEMS; i++) {
+    kk[i] = pk[jj[i]];
+    hh[i] = ph[jj[i]];
+    vv[i] = values ? pv[jj[i]] : 0u;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < B::ITEMS; i++) {
+    cls[i] = s0 + i * 64 + lane < M.S ? M.r : 0xFFu;
+#pragma unroll
+    for (uint32_t c = 0; c < BK_HEAVY; c++)
+      if (cls[i] != 0xFFu && c < M.r && kk[i] == M.heavy[c]) cls[i] = c;
+  }
+}
+
+__global__ __launch_bounds__(BkSmall::THREADS) void k_big_count(const uint32_t* __restrict__ pk,
+                                                                const uint32_t* __restrict__ ph,
+                                                                const uint32_t* __restrict__ info, uint32_t ntiles,
+                                                                const BigMeta* __restrict__ meta,
+                                                                const uint32_t* __restrict__ work,
+                                                                const uint32_t* work_n, uint32_t* __restrict__ cnt,
+                                                                const uint32_t* err) {
+  using B = BkSmall;
+  __shared__ BucketLds<B> L;
+  if (*err) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = *work_n;
+  for (uint32_t it = blockIdx.x; it < nw; it += gridDim.x) {
+    const uint32_t w = work[it];
+    const BigMeta M = meta[w >> 16];
+    bucket_setup(L, info, ntiles, M.d);
+    uint32_t kk[B::ITEMS], vv[B::ITEMS], hh[B::ITEMS], cls[B::ITEMS];
+    big_chunk_load(M, w & 0xFFFFu, ntiles, pk, nullptr, ph, kk, vv, hh, cls, false);
+    uint32_t nl = 0, nc[BK_HEAVY], hs[BK_HEAVY];
+#pragma unroll
+    for (uint32_t c = 0; c < BK_HEAVY; c++) nc[c] = hs[c] = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < B::ITEMS; i++) {
+      const uint32_t hv = hh[i] > 1 ? hh[i] : 1u;
+      nl += cls[i] == M.r ? 1u : 0u;
+#pragma unroll
+      for (uint32_t c = 0; c < BK_HEAVY; c++) {
+        nc[c] += cls[i] == c ? 1u : 0u;
+        hs[c] += cls[i] == c ? hv : 0u;
+      }
+    }
+    nl = wave_sum32(nl);
+#pragma unroll
+    for (uint32_t c = 0; c < BK_HEAVY; c++) {
+      nc[c] = wave_sum32(nc[c]);
+      hs[c] = wave_sum32(hs[c]);
+    }
+    if (lane == 0) {
+      L.lw[wave] = nl;
+#pragma unroll
+      for (uint32_t c = 0; c < BK_HEAVY; c++) {
+        L.hw[wave][c] = nc[c];
+        L.hsw[wave][c] = hs[c];
+      }
+    }
+    __syncthreads();
+    if (tid < BIG_CNT) {
+      uint32_t t = 0;
+      for (uint32_t v = 0; v < B::WAVES; v++)
+        t += tid == 0 ? L.lw[v] : tid <= BK_HEAVY ? L.hw[v][tid - 1] : L.hsw[v][tid - 1 - BK_HEAVY];
+      cnt[(size_t)it * BIG_CNT + tid] = t;
+    }
+    __syncthreads();  // L is reused by the next item
+  }
+}
+
+__global__ __launch_bounds__(BkSmall::THREADS) void k_big_place(
+    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ pv, const uint32_t* __restrict__ ph,
+    const uint32_t* __restrict__ info, uint32_t ntiles, const BigMeta* __restrict__ meta,
+    const uint32_t* __restrict__ work, const uint32_t* work_n, const uint32_t* __restrict__ cnt,
+    uint32_t* __restrict__ sk, uint32_t* __restrict__ sv, uint32_t* __restrict__ sh, uint32_t* __restrict__ segsum,
+    uint32_t* __restrict__ rid, uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end,
+    const uint32_t* err) {
+  using B = BkSmall;
+  __shared__ BucketLds<B> L;
+  if (*err) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = *work_n;
+  const uint64_t lt_mask = (1ull << lane) - 1;
+  for (uint32_t it = blockIdx.x; it < nw; it += gridDim.x) {
+    const uint32_t w = work[it], j = w & 0xFFFFu;
+    const BigMeta M = meta[w >> 16];
+    // sums over the bucket's earlier chunks (prefix) and all chunks (totals)
+    if (tid < BIG_CNT) L.acc[tid] = 0;
+    uint32_t tot[BIG_CNT];
+#pragma unroll
+    for (uint32_t k = 0; k < BIG_CNT; k++) tot[k] = 0;
+    __syncthreads();
+    for (uint32_t t = tid; t < M.nchunks; t += B::THREADS) {
+      const uint32_t* ct = cnt + (size_t)(M.item0 + t) * BIG_CNT;
+#pragma unroll
+      for (uint32_t k = 0; k < BIG_CNT; k++) {
+        const uint32_t v = ct[k];
+        tot[k] += v;
+        if (t < j) atomicAdd(&L.acc[k], v);
+      }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 1 + BK_HEAVY; k++) tot[k] = block_sum(L, tot[k]);  // light and class totals
+    bucket_setup(L, info, ntiles, M.d);  // (barriers: L.acc complete)
+    const uint32_t NL = tot[0];
+    if (NL > BIG_LIGHT_CAP) continue;  // k_bucket_big runs the whole bucket
+    uint32_t hstart[BK_HEAVY];  // hot key blocks after the light part, in class order
+    uint32_t st = NL;
+#pragma unroll
+    for (uint32_t c = 0; c < BK_HEAVY; c++) {
+      hstart[c] = st;
+      st += c < M.r ? tot[1 + c] : 0u;
+    }
+    if (j == 0 && tid < M.r) {
+      run_start[M.rb_heavy + tid] = M.base + hstart[tid];
+      run_end[M.rb_heavy + tid] = M.base + hstart[tid] + tot[1 + tid];
+    }
+    uint32_t kk[B::ITEMS], vv[B::ITEMS], hh[B::ITEMS], cls[B::ITEMS];
+    big_chunk_load(M, j, ntiles, pk, pv, ph, kk, vv, hh, cls, true);
+    // ranks in the chunk (item-major within the wave strip = arrival order):
+    // light rank, and per hot key: rank and inclusive sum of max(1, hits)
+    uint32_t rk[B::ITEMS], hp[B::ITEMS], wl = 0, wc[BK_HEAVY], wh[BK_HEAVY];
+#pragma unroll
+    for (uint32_t c = 0; c < BK_HEAVY; c++) wc[c] = wh[c] = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < B::ITEMS; i++) {
+      const uint64_t bl = __ballot(cls[i] == M.r);
+      rk[i] = wl + __popcll(bl & lt_mask);
+      wl += __popcll(bl);
+      hp[i] = 0;
+      const uint32_t hv = hh[i] > 1 ? hh[i] : 1u;
+#pragma unroll
+      for (uint32_t c = 0; c < BK_HEAVY; c++) {
+        if (c >= M.r) continue;  // uniform
+        const bool mine = cls[i] == c;
+        const uint64_t b = __ballot(mine);
+        uint32_t x = mine ? hv : 0u;  // inclusive scan of the class's hits over the lanes
+#pragma unroll
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+          const uint32_t y = __shfl_up(x, off, 64);
+          if (lane >= off) x += y;
+        }
+        if (mine) {
+          rk[i] = wc[c] + __popcll(b & lt_mask);
+          hp[i] = wh[c] + x;
+        }
+        wc[c] += __popcll(b);
+        wh[c] += __shfl(x, 63, 64);
+      }
+    }
+    if (lane == 0) {
+      L.lw[wave] = wl;
+#pragma unroll
+      for (uint32_t c = 0; c < BK_HEAVY; c++) {
+        L.hw[wave][c] = wc[c];
+        L.hsw[wave][c] = wh[c];
+      }
+    }
+    __syncthreads();
+    uint32_t lpre = L.acc[0], cpre[BK_HEAVY], hpre[BK_HEAVY];
+#pragma unroll
+    for (uint32_t c = 0; c < BK_HEAVY; c++) {
+      cpre[c] = L.acc[1 + c];
+      hpre[c] = L.acc[1 + BK_HEAVY + c];
+    }
+    for (uint32_t v = 0; v < wave; v++) {
+      lpre += L.lw[v];
+#pragma unroll
+      for (uint32_t c = 0; c < BK_HEAVY; c++) {
+        cpre[c] += L.hw[v][c];
+        hpre[c] += L.hsw[v][c];
+      }
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < B::ITEMS; i++) {
+      const uint32_t c = cls[i];
+      if (c == M.r) {  // light: compacted in arrival order into [0, NL)
+        const uint32_t at = M.base + lpre + rk[i];
+        sk[at] = kk[i];
+        sv[at] = vv[i];
+        sh[at] = hh[i];
+      } else if (c < BK_HEAVY) {  // hot key c: final position, run sums, run id
+        uint32_t cp = 0, hq = 0, hs0 = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < BK_HEAVY; q++)
+          if (q == c) {
+            cp = cpre[q];
+            hq = hpre[q];
+            hs0 = hstart[q];
+          }
+        const uint32_t at = M.base + hs0 + cp + rk[i];
+        sk[at] = kk[i];
+        sv[at] = vv[i];
+        segsum[at] = hq + hp[i];
+        rid[at] = M.rb_heavy + c;
+      }
+    }
+    __syncthreads();  // L is reused by the next item
+  }
+}
+
+__global__ __launch_bounds__(BkBig::THREADS) void k_bucket_big(
+    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ pv, const uint32_t* __restrict__ ph,
+    const uint32_t* __restrict__ info, uint32_t ntiles, uint32_t* __restrict__ sk, uint32_t* __restrict__ sv,
+    uint32_t* __restrict__ sh, uint32_t* __restrict__ ht, uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
+    uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end, uint32_t* num_runs,
+    const BigMeta* __restrict__ meta, const uint32_t* big_n, const uint32_t* __restrict__ cnt,
+    const uint32_t* err) {
+  using B = BkBig;
+  __shared__ BucketLds<B> L;
+  if (*err) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nb = *big_n;
+  for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
+    const BigMeta M = meta[bi];
+    const uint32_t d = M.d, S = M.S, base = M.base;
+    BK_STAMP(d, 0);
+    uint32_t nl = 0;
+    for (uint32_t t = tid; t < M.nchunks; t += B::THREADS) nl += cnt[(size_t)(M.item0 + t) * BIG_CNT];
+    nl = block_sum(L, nl);
+    if (M.r && nl <= BIG_LIGHT_CAP) {
+      // hot keys placed by k_big_place; the light part [0, nl), compacted in
+      // arrival order, is sorted and segmented here
+      uint32_t kk[B::ITEMS], vv[B::ITEMS], hh[B::ITEMS];
+      const uint32_t strip0 = wave * B::STRIP;
+#pragma unroll
+      for (uint32_t i = 0; i < B::ITEMS; i++) {
+        const uint32_t p = min(strip0 + i * 64 + lane, nl ? nl - 1 : 0u);
+        kk[i] = sk[base + p];
+        vv[i] = sv[base + p];
+        hh[i] = sh[base + p];
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < B::ITEMS; i++)
+        if (strip0 + i * 64 + lane >= nl) kk[i] = 0xFFFFFFFFu;
+      if (nl) {
+        lds_sort3(L, kk, vv, hh, nl);
+#pragma unroll
+        for (uint32_t i = 0; i < B::ITEMS; i++) {
+          const uint32_t p = strip0 + i * 64 + lane;
+          if (p < nl) {
+            sk[base + p] = kk[i];
+            sv[base + p] = vv[i];
+          }
+        }
+        __syncthreads();
+        bucket_segment<B, true>(L, d, nl, base, sk, sh, segsum, rid, run_start, run_end, num_runs);
+      }
+    } else {
+      if (tid < M.r) run_start[M.rb_heavy + tid] = run_end[M.rb_heavy + tid] = 0;  // hot-key runs left empty
+      bucket_setup(L, info, ntiles, d);
+      BK_STAMP(d, 1);
+      if (!bucket_peel(L, d, S, base, ntiles, pk, pv, ph, sk, sv, sh))
+        bucket_lsd(L, S, base, ntiles, pk, pv, ph, sk, sv, sh, ht, segsum, rid);
+      bucket_segment<B, false>(L, d, S, base, sk, sh, segsum, rid, run_start, run_end, num_runs);
+    }
+    BK_STAMP(d, 7);
+    __syncthreads();  // L is reused by the next bucket
+  }
 }
 
 // Run checks against the predecessor (equality chains): a run must hold one
 // stem under one unit, else it is flagged RUN_MULTI and queued once (by run
 // id) for k_runs_general; a window change within a run makes a long run
 // RUN_SLOW (serial replay). Run heads only compare two sort keys.
-__global__ __launch_bounds__(256) void k_run_check(BatchDev b, const Rec* __restrict__ rec_s,
+__global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
                                                    const uint32_t* __restrict__ skeys,
                                                    const uint32_t* __restrict__ rid,
                                                    uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
@@ -1941,7 +2282,7 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, const Rec* __rest
 // long uniform runs are set up for the parallel path (k_fast_*); a stem that
 // turns out to live in the table under another unit too is queued for the
 // exact path (defer2, k_runs_general after this kernel).
-__global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, const Rec* __restrict__ rec_s,
+__global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, SRec rec_s,
                                               const uint32_t* __restrict__ skeys,
                                               const uint32_t* __restrict__ svals, unsigned long long* __restrict__ res,
                                               const uint32_t* __restrict__ run_start,
@@ -1966,8 +2307,8 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
   LaneStats L;
   L.reset();
   const uint32_t r = blockIdx.x * 256 + threadIdx.x;
-  if (r < s_nr) {
-    const uint32_t p = run_start[r], end = run_end[r];
+  const uint32_t p = r < s_nr ? run_start[r] : 0u, end = r < s_nr ? run_end[r] : 0u;
+  if (p < end) {  // (a large bucket's hot-key run left to its fallback path is empty)
     const uint32_t fl = run_flags[r];
     const Rec x0 = rec_s[p];
     const uint32_t e0 = svals[p];
@@ -2047,7 +2388,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
 // local cache on, the first element f with a_f > limit_f makes every element of
 // a LATER request a local-cache hit (Set happens after request q_f's statuses),
 // i.e. a suffix of the run, which therefore never increments.
-__global__ __launch_bounds__(256) void k_fast_over(uint32_t n, const Rec* __restrict__ rec_s,
+__global__ __launch_bounds__(256) void k_fast_over(uint32_t n, SRec rec_s,
                                                    const uint32_t* __restrict__ segsum,
                                                    const uint32_t* __restrict__ rid,
                                                    const uint32_t* __restrict__ run_flags,
@@ -2075,7 +2416,7 @@ __global__ __launch_bounds__(256) void k_fast_over(uint32_t n, const Rec* __rest
 }
 
 __global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules, TableDev t, Params P,
-                                                   const Rec* __restrict__ rec_s, const uint32_t* __restrict__ svals,
+                                                   SRec rec_s, const uint32_t* __restrict__ svals,
                                                    unsigned long long* __restrict__ res,
                                                    const uint32_t* __restrict__ segsum,
                                                    const uint32_t* __restrict__ rid,
@@ -2134,7 +2475,7 @@ __global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules,
 
 // ---- k_runs_general: deferred runs (hash-prefix collisions, multi-unit
 // stems). Splits the run into distinct stems, then replays each exactly.
-__global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Params P, const Rec* __restrict__ rec_s,
+__global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Params P, SRec rec_s,
                                                       const uint32_t* __restrict__ skeys,
                                                       const uint32_t* __restrict__ svals,
                                                       unsigned long long* __restrict__ res,
@@ -2373,22 +2714,35 @@ static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b -
 
 // Stage A (table-free): validate, hash, sort, gather, segment. Uses only this
 // buffer's scratch and its validation word s.err.
-void launch_stage_a(const BatchDev& b, const Scratch& s, uint32_t epoch, hipStream_t st, hipEvent_t* ev) {
+void launch_stage_a(const BatchDev& b, const Scratch& s, hipStream_t st, hipEvent_t* ev) {
   const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
   if (ev) (void)hipEventRecord(ev[0], st);
   if (g0)
-    k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.keys[0], s.vals[0], s.err, s.time_floor, s.defer_n, s.os_ghist,
-                                  s.os_ctr, s.run_flags, s.num_runs);
+    k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.keys[0], s.vals[0], s.err, s.time_floor, s.defer_n, s.big_n,
+                                  s.work_n, s.run_flags, s.num_runs, s.hit_a);
   if (ev) (void)hipEventRecord(ev[1], st);
   const uint32_t ptiles = cdiv(b.n, PART_TILE);
-  if (b.n) k_part<<<ptiles, 256, 0, st>>>(s.keys[0], s.vals[0], s.keys[1], s.vals[1], b.n, ptiles, s.part_info,
-                                         s.os_ghist, s.err);
+  if (b.n)
+    k_part<<<ptiles, 256, 0, st>>>(s.keys[0], s.vals[0], s.hit_a, s.keys[1], s.vals[1], s.hit_p, b.n, ptiles,
+                                   s.part_info, s.err);
   if (ev) (void)hipEventRecord(ev[2], st);
   if (b.n) {
-    k_bucket<<<256, BK_THREADS, 0, st>>>(s.keys[1], s.vals[1], s.part_info, s.os_ghist, ptiles, s.rec, s.keys[0],
-                                         s.vals[0], s.rec_s, s.segsum, s.rid, s.run_start, s.run_end, s.num_runs,
-                                         s.err);
-    k_run_check<<<cdiv(b.n, 256), 256, 0, st>>>(b, s.rec_s, s.keys[0], s.rid, s.run_flags, s.defer, s.defer_n,
+    const size_t seg_lds = (2ull * ptiles + 1) * 4;
+    k_bucket<<<PART_DIGITS, BkSmall::THREADS, seg_lds, st>>>(s.keys[1], s.vals[1], s.hit_p, s.part_info, ptiles,
+                                                             s.keys[0], s.vals[0], s.hits_s, s.segsum, s.rid,
+                                                             s.run_start, s.run_end, s.num_runs, s.big_meta, s.big_n,
+                                                             s.big_work, s.work_n, s.err);
+    k_big_count<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds, st>>>(s.keys[1], s.hit_p, s.part_info, ptiles,
+                                                                    s.big_meta, s.big_work, s.work_n, s.big_cnt,
+                                                                    s.err);
+    k_big_place<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds, st>>>(
+        s.keys[1], s.vals[1], s.hit_p, s.part_info, ptiles, s.big_meta, s.big_work, s.work_n, s.big_cnt, s.keys[0],
+        s.vals[0], s.hits_s, s.segsum, s.rid, s.run_start, s.run_end, s.err);
+    k_bucket_big<<<BIG_BLOCKS, BkBig::THREADS, seg_lds, st>>>(s.keys[1], s.vals[1], s.hit_p, s.part_info, ptiles,
+                                                              s.keys[0], s.vals[0], s.hits_s, s.hit_t, s.segsum,
+                                                              s.rid, s.run_start, s.run_end, s.num_runs, s.big_meta,
+                                                              s.big_n, s.big_cnt, s.err);
+    k_run_check<<<cdiv(b.n, 256), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[0], s.rid, s.run_flags, s.defer, s.defer_n,
                                                 s.err);
   }
 }
@@ -2409,23 +2763,23 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     (void)hipEventRecord(go, st);
     (void)hipStreamWaitEvent(side, go, 0);
     k_runs_general<<<g < RUNS_GENERAL_BLOCKS ? g : RUNS_GENERAL_BLOCKS, 256, lds, side>>>(
-        b, t, P, s.rec_s, s.keys[0], s.vals[0], s.res, s.run_start, s.run_end, s.defer, s.defer_n, s.repid, o.stats, s.stripes,
+        b, t, P, SRec{s.rec, s.vals[0]}, s.keys[0], s.vals[0], s.res, s.run_start, s.run_end, s.defer, s.defer_n, s.repid, o.stats, s.stripes,
         s.errb, restore);
     (void)hipEventRecord(side_done, side);
     if (ev) (void)hipEventRecord(ev[3], st);
-    k_runs<<<g, 256, lds, st>>>(b, t, P, s.rec_s, s.keys[0], s.vals[0], s.res, s.run_start, s.run_end, s.run_flags,
+    k_runs<<<g, 256, lds, st>>>(b, t, P, SRec{s.rec, s.vals[0]}, s.keys[0], s.vals[0], s.res, s.run_start, s.run_end, s.run_flags,
                                 s.run_state, s.run_f, s.num_runs, s.defer2, s.defer2_n, o.stats, s.stripes, s.errb,
                                 restore);
     if (ev) (void)hipEventRecord(ev[4], st);
     // stems k_runs found under several units in the table (rare)
-    k_runs_general<<<RUNS_GENERAL_LATE_BLOCKS, 256, lds, st>>>(b, t, P, s.rec_s, s.keys[0], s.vals[0],
+    k_runs_general<<<RUNS_GENERAL_LATE_BLOCKS, 256, lds, st>>>(b, t, P, SRec{s.rec, s.vals[0]}, s.keys[0], s.vals[0],
                                                                 s.res, s.run_start, s.run_end, s.defer2, s.defer2_n, s.repid, o.stats,
                                                                 s.stripes, s.errb, restore);
     (void)hipStreamWaitEvent(st, side_done, 0);
     if (!restore) {
       if (P.lc_en)
-        k_fast_over<<<g, 256, 0, st>>>(b.n, s.rec_s, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
-      k_fast_emit<<<g, 256, lds, st>>>(b.n, b.n_rules, t, P, s.rec_s, s.vals[0], s.res, s.segsum, s.rid,
+        k_fast_over<<<g, 256, 0, st>>>(b.n, SRec{s.rec, s.vals[0]}, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
+      k_fast_emit<<<g, 256, lds, st>>>(b.n, b.n_rules, t, P, SRec{s.rec, s.vals[0]}, s.vals[0], s.res, s.segsum, s.rid,
                                        s.run_start, s.run_end, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb);
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;
       const uint32_t gf = cdiv(nf * RL_NUM_STATS > b.n ? nf * RL_NUM_STATS : b.n, 256);

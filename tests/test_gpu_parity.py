@@ -224,6 +224,15 @@ def test_gpu_c2_zipf_hits_vs_c_oracle(lc):
                                              sampler=z)), lc=lc)
 
 
+def test_gpu_c2_hot_keys_large_buckets_vs_c_oracle():
+    """Bench-scale skew: hot tenants put tens of thousands of descriptors of one
+    key into a single bucket (k_bucket_big: heavy keys peeled off over several
+    chunks), consecutive 1M-descriptor batches with time advancing."""
+    z = workloads.ZipfSampler(2_000_000, 1.1)
+    _compare_packed(list(workloads.c2_stream(n_tenants=2_000_000, requests_per_batch=500_000, batches=3,
+                                             sampler=z)), table_slots=1 << 23)
+
+
 def test_gpu_c0_vs_c_oracle():
     _compare_packed(list(workloads.c0_stream(n_requests=300_000, per_batch=100_000)), lc=True)
 
