@@ -29,6 +29,7 @@ using namespace rl;
 #define RL_NBUF 3
 #endif
 constexpr uint32_t NBUF = RL_NBUF;
+constexpr uint32_t PROF_RING = 8;  // timed batches in flight (> NBUF)
 
 struct rl_ctx {
   rl_config cfg;
@@ -59,10 +60,13 @@ struct rl_ctx {
   unsigned long long* h_route = nullptr;  // pinned route counts
   std::string last_error;
   uint64_t batches = 0, decisions = 0;
-  // rl_profile: events of the in-flight timed batch, accumulated stage sums
+  // rl_profile: a ring of per-batch event sets (stage boundaries, recorded on
+  // the batch's own stream, so pipelined batches are timed as they run),
+  // folded into the stage sums when a set is reused or read
   bool prof = false;
-  bool prof_pending = false;
-  hipEvent_t ev[RL_NUM_STAGES + 1] = {};
+  bool prof_pending[PROF_RING] = {};
+  uint32_t prof_next = 0;
+  hipEvent_t ev[PROF_RING][RL_NUM_STAGES + 1] = {};
   double stage_ms[RL_NUM_STAGES] = {};
   uint64_t prof_batches = 0;
 };
@@ -73,23 +77,29 @@ thread_local std::string g_err;
 
 int set_err(rl_ctx* c, int code, const std::string& msg);
 
-// Fold the previous timed batch's events into the stage sums (waits for it).
-void prof_fold(rl_ctx* c) {
-  if (!c->prof_pending) return;
-  c->prof_pending = false;
-  if (hipEventSynchronize(c->ev[RL_NUM_STAGES]) != hipSuccess) return;
+// Fold event set k (a timed batch) into the stage sums; waits for the batch.
+void prof_fold(rl_ctx* c, uint32_t k) {
+  if (!c->prof_pending[k]) return;
+  c->prof_pending[k] = false;
+  if (hipEventSynchronize(c->ev[k][RL_NUM_STAGES]) != hipSuccess) return;
   for (int i = 0; i < RL_NUM_STAGES; i++) {
     float ms = 0;
-    if (hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]) == hipSuccess) c->stage_ms[i] += ms;
+    if (hipEventElapsedTime(&ms, c->ev[k][i], c->ev[k][i + 1]) == hipSuccess) c->stage_ms[i] += ms;
   }
   c->prof_batches++;
 }
 
+void prof_fold_all(rl_ctx* c) {
+  for (uint32_t k = 0; k < PROF_RING; k++) prof_fold(c, (c->prof_next + k) % PROF_RING);
+}
+
 hipEvent_t* prof_events(rl_ctx* c) {
   if (!c->prof) return nullptr;
-  prof_fold(c);  // one batch in flight at a time per event set
-  c->prof_pending = true;
-  return c->ev;
+  const uint32_t k = c->prof_next;
+  c->prof_next = (k + 1) % PROF_RING;
+  prof_fold(c, k);  // the batch that used this set PROF_RING batches ago
+  c->prof_pending[k] = true;
+  return c->ev[k];
 }
 
 int set_err(rl_ctx* c, int code, const std::string& msg) {
@@ -144,20 +154,22 @@ int collect(rl_ctx* c, hipStream_t st = nullptr) {
 TableDev table_view(rl_ctx* c);
 Params params(rl_ctx* c);
 
-// Enqueue one batch. Pipelined (ctx streams, profiling off): stage A on the
-// buffer's own stream as soon as the buffer is free, stage B after the
-// previous batch's stage B. Serial: both stages on `st` after all earlier work.
+// Enqueue one batch. Pipelined (ctx streams): stage A on the buffer's own
+// stream as soon as the buffer is free, stage B after the previous batch's
+// stage B. Serial: both stages on `st` after all earlier work. With rl_profile
+// on, the stage boundaries are recorded on the batch's stream either way.
 uint32_t enqueue(rl_ctx* c, const BatchDev& b, const OutDev& o, int restore, hipStream_t st, bool pipelined) {
   const uint32_t k = c->next;
   c->next = (k + 1) % NBUF;
   const TableDev t = table_view(c);
   const Params P = params(c);
-  if (pipelined && !c->prof) {
+  if (pipelined) {
     hipStream_t a = c->pipe[k];
+    hipEvent_t* ev = prof_events(c);
     (void)hipStreamWaitEvent(a, c->b_done[k], 0);  // buffer k's previous batch is done
-    launch_stage_a(b, c->s[k], a);
+    launch_stage_a(b, c->s[k], a, ev);
     (void)hipStreamWaitEvent(a, c->b_done[c->last], 0);  // table order
-    launch_stage_b(b, o, t, P, c->s[k], restore, a, c->side, c->side_go, c->side_done);
+    launch_stage_b(b, o, t, P, c->s[k], restore, a, c->side, c->side_go, c->side_done, ev);
     (void)hipEventRecord(c->b_done[k], a);
   } else {
     if (!st) st = c->stream;
@@ -384,8 +396,9 @@ void rl_destroy(rl_ctx* c) {
   if (c->side) (void)hipStreamSynchronize(c->side);
   if (c->side_go) (void)hipEventDestroy(c->side_go);
   if (c->side_done) (void)hipEventDestroy(c->side_done);
-  for (int i = 0; i <= RL_NUM_STAGES; i++)
-    if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+  for (uint32_t k = 0; k < PROF_RING; k++)
+    for (int i = 0; i <= RL_NUM_STAGES; i++)
+      if (c->ev[k][i]) (void)hipEventDestroy(c->ev[k][i]);
   for (uint32_t k = 0; k < NBUF; k++) {
     free_buffer(c->s[k]);
     if (c->b_done[k]) (void)hipEventDestroy(c->b_done[k]);
@@ -501,9 +514,10 @@ int rl_route_scatter(rl_ctx* c, uint32_t n, const uint32_t* perm, const uint64_t
 int rl_profile(rl_ctx* c, int enable) {
   if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  if (enable && !c->ev[0])
-    for (int i = 0; i <= RL_NUM_STAGES; i++) HIPCHK(c, hipEventCreate(&c->ev[i]));
-  prof_fold(c);
+  if (enable && !c->ev[0][0])
+    for (uint32_t k = 0; k < PROF_RING; k++)
+      for (int i = 0; i <= RL_NUM_STAGES; i++) HIPCHK(c, hipEventCreate(&c->ev[k][i]));
+  prof_fold_all(c);
   c->prof = enable != 0;
   return RL_OK;
 }
@@ -511,7 +525,7 @@ int rl_profile(rl_ctx* c, int enable) {
 int rl_profile_read(rl_ctx* c, double* ms, uint32_t n, uint64_t* batches) {
   if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  prof_fold(c);
+  prof_fold_all(c);
   for (uint32_t i = 0; i < n && i < RL_NUM_STAGES; i++) ms[i] = c->stage_ms[i];
   if (batches) *batches = c->prof_batches;
   for (int i = 0; i < RL_NUM_STAGES; i++) c->stage_ms[i] = 0;
