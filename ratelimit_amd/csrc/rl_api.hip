@@ -252,7 +252,7 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
        dalloc(&s.rid, n) == hipSuccess && dalloc(&s.run_start, (size_t)n + 1) == hipSuccess &&
        dalloc(&s.run_flags, n) == hipSuccess && dalloc(&s.run_state, n) == hipSuccess &&
        dalloc(&s.run_f, n) == hipSuccess && dalloc(&s.num_runs, 1) == hipSuccess;
-  ok = ok && dalloc(&s.hit_a, n) == hipSuccess && dalloc(&s.hit_p, n) == hipSuccess &&
+  ok = ok && dalloc(&s.hit_a, n) == hipSuccess && dalloc(&s.tile, n) == hipSuccess &&
        dalloc(&s.hit_t, n) == hipSuccess;
   ok = ok && dalloc(&s.run_end, n) == hipSuccess &&
        dalloc(&s.part_info, (size_t)PART_DIGITS * std::max((n + PART_TILE - 1) / PART_TILE, 1u)) == hipSuccess;
@@ -262,7 +262,7 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
 void free_buffer(Scratch& s) {
   void* bufs[] = {s.rec, s.res, s.big_meta, s.big_n, s.big_work, s.work_n, s.big_cnt, s.keys[0], s.keys[1], s.vals[0], s.vals[1], s.hist,
                   s.hist_tot, s.repid, s.defer, s.defer_n, s.defer2, s.defer2_n, s.tile_f, s.tile_s, s.tile_h, s.hits_s, s.segsum, s.rid,
-                  s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs, s.run_end, s.part_info, s.hit_a, s.hit_p, s.hit_t};
+                  s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
 }

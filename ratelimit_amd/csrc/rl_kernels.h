@@ -151,7 +151,7 @@ struct Scratch {
   uint32_t *tile_f, *tile_s, *tile_h;  // per SEG_TILE tile
   uint32_t* hits_s;                    // [n] raw hits, sorted order
   uint32_t* hit_a;                     // [n] raw hits, arrival order (k_prepare)
-  uint32_t* hit_p;                     // [n] raw hits, k_part tile layout
+  uint4* tile;                         // [n] k_part tile layout: {sort key, index, hits, 0}
   uint32_t* hit_t;                     // [n] k_bucket large-bucket temp
   uint32_t* segsum;                    // [n] inclusive in-run sum of hits
   uint32_t* rid;                       // [n] run id

@@ -41,7 +41,7 @@ namespace rl {
 constexpr uint32_t HASH_LDS_BYTES = 16384;
 
 __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ rec, uint32_t* __restrict__ keys,
-                                                 uint32_t* __restrict__ vals, uint32_t* err,
+                                                 uint32_t* err,
                                                  const int64_t* time_floor, uint32_t* defer_n,
                                                  uint32_t* big_n, uint32_t* work_n, uint32_t* __restrict__ run_flags,
                                                  uint32_t* num_runs,
@@ -108,7 +108,6 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
     }
   }
   keys[i] = (uint32_t)(h >> 32);
-  vals[i] = i;
   Rec r;
   r.hlo = (uint32_t)h;
   r.off = s0;
@@ -1186,10 +1185,9 @@ __device__ inline uint32_t scan256(uint32_t v, uint32_t* wsum4, uint32_t* total)
   return pre + inc - v;
 }
 
-__global__ __launch_bounds__(256) void k_part(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                              const uint32_t* __restrict__ hin, uint32_t* __restrict__ kout,
-                                              uint32_t* __restrict__ vout, uint32_t* __restrict__ hout, uint32_t n,
-                                              uint32_t ntiles, uint32_t* __restrict__ info, const uint32_t* err) {
+__global__ __launch_bounds__(256) void k_part(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ hin,
+                                              uint4* __restrict__ out, uint32_t n, uint32_t ntiles,
+                                              uint32_t* __restrict__ info, const uint32_t* err) {
   constexpr uint32_t DPT = PART_DIGITS / 256;  // digits per thread
   __shared__ uint32_t wcnt[4][PART_DIGITS];
   __shared__ uint32_t wsum[4];
@@ -1203,7 +1201,7 @@ __global__ __launch_bounds__(256) void k_part(const uint32_t* __restrict__ kin, 
   for (uint32_t i = 0; i < PART_ITEMS; i++) {
     const uint32_t j = min(wbase + i * 64 + lane, n - 1);  // unconditional loads, all in flight
     kk[i] = kin[j];
-    vv[i] = vin[j];
+    vv[i] = j;  // the descriptor index
     hh[i] = hin[j];
   }
   wave_multisplit<PART_ITEMS, PART_BITS>(kk, wbase, n, 32 - PART_BITS, wcnt[wave], pos);
@@ -1238,10 +1236,7 @@ __global__ __launch_bounds__(256) void k_part(const uint32_t* __restrict__ kin, 
   for (uint32_t i = 0; i < PART_ITEMS; i++) {
     if (wbase + i * 64 + lane < n) {
       const uint32_t d = kk[i] >> (32 - PART_BITS);
-      const uint32_t p = tile * PART_TILE + wcnt[wave][d] + pos[i];
-      kout[p] = kk[i];
-      vout[p] = vv[i];
-      hout[p] = hh[i];
+      out[tile * PART_TILE + wcnt[wave][d] + pos[i]] = make_uint4(kk[i], vv[i], hh[i], 0u);  // one 16-B record
     }
   }
 }
@@ -1570,12 +1565,12 @@ constexpr uint32_t BIG_CNT = 1 + 2 * BK_HEAVY;  // per work item: light count, c
 // Hot keys of a large bucket: 64 evenly spaced positions are sampled by wave
 // 0; keys seen at least BK_HEAVY_MIN times become L.heavy[0..L.nheavy).
 template <typename B>
-__device__ inline void sample_heavy(BucketLds<B>& L, uint32_t S, uint32_t ntiles, const uint32_t* __restrict__ pk) {
+__device__ inline void sample_heavy(BucketLds<B>& L, uint32_t S, uint32_t ntiles, const uint4* __restrict__ pt) {
   const uint32_t lane = threadIdx.x & 63;
   if ((threadIdx.x >> 6) == 0) {
     uint32_t p[1] = {(uint32_t)(((uint64_t)(2 * lane + 1) * S) >> 7)}, j[1];
     bucket_src(ntiles, p, j);
-    const uint32_t ks = pk[j[0]];
+    const uint32_t ks = pt[j[0]].x;
     uint32_t cnt = 0;
     bool first = true;
     for (uint32_t q = 0; q < 64; q++) {
@@ -1593,7 +1588,7 @@ __device__ inline void sample_heavy(BucketLds<B>& L, uint32_t S, uint32_t ntiles
 }
 
 __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
-    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ pv, const uint32_t* __restrict__ ph,
+    const uint4* __restrict__ pt,
     const uint32_t* __restrict__ info, uint32_t ntiles, uint32_t* __restrict__ sk, uint32_t* __restrict__ sv,
     uint32_t* __restrict__ sh, uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
     uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end, uint32_t* num_runs,
@@ -1608,7 +1603,7 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
   const uint32_t S = L.S, base = L.base_pos;
   if (!S) return;
   if (S > B::CAP) {  // queued: hot keys sampled, their run ids and the chunk work items allocated
-    sample_heavy(L, S, ntiles, pk);
+    sample_heavy(L, S, ntiles, pt);
     if (tid == 0) {
       BigMeta M;
       M.d = d;
@@ -1639,9 +1634,10 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
   bucket_src(ntiles, pp, jj);
 #pragma unroll
   for (uint32_t i = 0; i < B::ITEMS; i++) {
-    kk[i] = pk[jj[i]];
-    vv[i] = pv[jj[i]];
-    hh[i] = ph[jj[i]];
+    const uint4 e = pt[jj[i]];
+    kk[i] = e.x;
+    vv[i] = e.y;
+    hh[i] = e.z;
   }
 #pragma unroll
   for (uint32_t i = 0; i < B::ITEMS; i++)
@@ -1670,8 +1666,8 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
 // do not fit in LDS.
 template <typename B>
 __device__ inline bool bucket_peel(BucketLds<B>& L, uint32_t d, uint32_t S, uint32_t base, uint32_t ntiles,
-                                   const uint32_t* __restrict__ pk, const uint32_t* __restrict__ pv,
-                                   const uint32_t* __restrict__ ph, uint32_t* __restrict__ sk,
+                                   const uint4* __restrict__ pt,
+                                   uint32_t* __restrict__ sk,
                                    uint32_t* __restrict__ sv, uint32_t* __restrict__ sh) {
   constexpr uint32_t IT = B::ITEMS;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1679,7 +1675,7 @@ __device__ inline bool bucket_peel(BucketLds<B>& L, uint32_t d, uint32_t S, uint
   if (wave == 0) {
     uint32_t p[1] = {(uint32_t)(((uint64_t)(2 * lane + 1) * S) >> 7)}, j[1];
     bucket_src(ntiles, p, j);
-    const uint32_t ks = pk[j[0]];
+    const uint32_t ks = pt[j[0]].x;
     uint32_t cnt = 0;
     bool first = true;
     for (uint32_t q = 0; q < 64; q++) {
@@ -1716,9 +1712,10 @@ __device__ inline bool bucket_peel(BucketLds<B>& L, uint32_t d, uint32_t S, uint
     bucket_src(ntiles, pp, jj);
 #pragma unroll
     for (uint32_t i = 0; i < IT; i++) {
-      kk[i] = pk[jj[i]];
-      vv[i] = pv[jj[i]];
-      hh[i] = ph[jj[i]];
+      const uint4 e = pt[jj[i]];
+      kk[i] = e.x;
+      vv[i] = e.y;
+      hh[i] = e.z;
     }
     uint32_t wl = 0, lr[IT];
     uint32_t wc[BK_HEAVY];
@@ -1830,9 +1827,10 @@ __device__ inline bool bucket_peel(BucketLds<B>& L, uint32_t d, uint32_t S, uint
     bucket_src(ntiles, pp, jj);
 #pragma unroll
     for (uint32_t i = 0; i < IT; i++) {
-      kk[i] = pk[jj[i]];
-      vv[i] = pv[jj[i]];
-      hh[i] = ph[jj[i]];
+      const uint4 e = pt[jj[i]];
+      kk[i] = e.x;
+      vv[i] = e.y;
+      hh[i] = e.z;
     }
     uint32_t hr[IT], wc[BK_HEAVY];
 #pragma unroll
@@ -1889,8 +1887,8 @@ __device__ inline bool bucket_peel(BucketLds<B>& L, uint32_t d, uint32_t S, uint
 // afterwards). Running digit offsets per pass come from one histogram sweep.
 template <typename B>
 __device__ inline void bucket_lsd(BucketLds<B>& L, uint32_t S, uint32_t base, uint32_t ntiles,
-                                  const uint32_t* __restrict__ pk, const uint32_t* __restrict__ pv,
-                                  const uint32_t* __restrict__ ph, uint32_t* __restrict__ sk,
+                                  const uint4* __restrict__ pt,
+                                  uint32_t* __restrict__ sk,
                                   uint32_t* __restrict__ sv, uint32_t* __restrict__ sh, uint32_t* __restrict__ ht,
                                   uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid) {
   constexpr uint32_t IT = B::ITEMS;
@@ -1904,7 +1902,7 @@ __device__ inline void bucket_lsd(BucketLds<B>& L, uint32_t S, uint32_t base, ui
     for (uint32_t i = 0; i < IT; i++) pp[i] = min(c0 + i * B::THREADS + tid, S - 1);
     bucket_src(ntiles, pp, jj);
 #pragma unroll
-    for (uint32_t i = 0; i < IT; i++) kk[i] = pk[jj[i]];  // loads first, all in flight
+    for (uint32_t i = 0; i < IT; i++) kk[i] = pt[jj[i]].x;  // loads first, all in flight
 #pragma unroll
     for (uint32_t i = 0; i < IT; i++) {
       if (c0 + i * B::THREADS + tid < S) {
@@ -1922,9 +1920,9 @@ __device__ inline void bucket_lsd(BucketLds<B>& L, uint32_t S, uint32_t base, ui
   }
   __syncthreads();
   for (uint32_t pass = 0; pass < 3; pass++) {
-    const uint32_t* ik = pass == 0 ? pk : pass == 1 ? sk + base : rid + base;
-    const uint32_t* iv = pass == 0 ? pv : pass == 1 ? sv + base : segsum + base;
-    const uint32_t* ih = pass == 0 ? ph : pass == 1 ? sh + base : ht + base;
+    const uint32_t* ik = pass == 1 ? sk + base : rid + base;  // passes 1, 2 (pass 0 reads the tile layout)
+    const uint32_t* iv = pass == 1 ? sv + base : segsum + base;
+    const uint32_t* ih = pass == 1 ? sh + base : ht + base;
     uint32_t* ok = pass == 1 ? rid + base : sk + base;
     uint32_t* ov = pass == 1 ? segsum + base : sv + base;
     uint32_t* oh = pass == 1 ? ht + base : sh + base;
@@ -1939,11 +1937,21 @@ __device__ inline void bucket_lsd(BucketLds<B>& L, uint32_t S, uint32_t base, ui
 #pragma unroll
         for (uint32_t i = 0; i < IT; i++) jj[i] = pp[i];
       }
+      if (pass == 0) {
 #pragma unroll
-      for (uint32_t i = 0; i < IT; i++) {
-        kk[i] = ik[jj[i]];
-        vv[i] = iv[jj[i]];
-        hh[i] = ih[jj[i]];
+        for (uint32_t i = 0; i < IT; i++) {
+          const uint4 e = pt[jj[i]];
+          kk[i] = e.x;
+          vv[i] = e.y;
+          hh[i] = e.z;
+        }
+      } else {
+#pragma unroll
+        for (uint32_t i = 0; i < IT; i++) {
+          kk[i] = ik[jj[i]];
+          vv[i] = iv[jj[i]];
+          hh[i] = ih[jj[i]];
+        }
       }
 #pragma unroll
       for (uint32_t i = 0; i < IT; i++)
@@ -1983,8 +1991,7 @@ __device__ inline uint32_t wave_sum32(uint32_t x) {
 
 // Load one chunk of a queued bucket (BkSmall shape) and classify it: cls =
 // hot key index c < r, r for a light element, 0xFF past the bucket.
-__device__ inline void big_chunk_load(const BigMeta& M, uint32_t j, uint32_t ntiles, const uint32_t* __restrict__ pk,
-                                      const uint32_t* __restrict__ pv, const uint32_t* __restrict__ ph,
+__device__ inline void big_chunk_load(const BigMeta& M, uint32_t j, uint32_t ntiles, const uint4* __restrict__ pt,
                                       uint32_t (&kk)[BkSmall::ITEMS], uint32_t (&vv)[BkSmall::ITEMS],
                                       uint32_t (&hh)[BkSmall::ITEMS], uint32_t (&cls)[BkSmall::ITEMS], bool values) {
   using B = BkSmall;
@@ -1995,9 +2002,10 @@ __device__ inline void big_chunk_load(const BigMeta& M, uint32_t j, uint32_t nti
   bucket_src(ntiles, pp, jj);
 #pragma unroll
   for (uint32_t i = 0; i < B::ITEMS; i++) {
-    kk[i] = pk[jj[i]];
-    hh[i] = ph[jj[i]];
-    vv[i] = values ? pv[jj[i]] : 0u;
+    const uint4 e = pt[jj[i]];
+    kk[i] = e.x;
+    hh[i] = e.z;
+    vv[i] = values ? e.y : 0u;
   }
 #pragma unroll
   for (uint32_t i = 0; i < B::ITEMS; i++) {
@@ -2008,8 +2016,7 @@ __device__ inline void big_chunk_load(const BigMeta& M, uint32_t j, uint32_t nti
   }
 }
 
-__global__ __launch_bounds__(BkSmall::THREADS) void k_big_count(const uint32_t* __restrict__ pk,
-                                                                const uint32_t* __restrict__ ph,
+__global__ __launch_bounds__(BkSmall::THREADS) void k_big_count(const uint4* __restrict__ pt,
                                                                 const uint32_t* __restrict__ info, uint32_t ntiles,
                                                                 const BigMeta* __restrict__ meta,
                                                                 const uint32_t* __restrict__ work,
@@ -2024,7 +2031,7 @@ __global__ __launch_bounds__(BkSmall::THREADS) void k_big_count(const uint32_t* 
     const BigMeta M = meta[w >> 16];
     bucket_setup(L, info, ntiles, M.d);
     uint32_t kk[B::ITEMS], vv[B::ITEMS], hh[B::ITEMS], cls[B::ITEMS];
-    big_chunk_load(M, w & 0xFFFFu, ntiles, pk, nullptr, ph, kk, vv, hh, cls, false);
+    big_chunk_load(M, w & 0xFFFFu, ntiles, pt, kk, vv, hh, cls, false);
     uint32_t nl = 0, nc[BK_HEAVY], hs[BK_HEAVY];
 #pragma unroll
     for (uint32_t c = 0; c < BK_HEAVY; c++) nc[c] = hs[c] = 0;
@@ -2064,7 +2071,7 @@ __global__ __launch_bounds__(BkSmall::THREADS) void k_big_count(const uint32_t* 
 }
 
 __global__ __launch_bounds__(BkSmall::THREADS) void k_big_place(
-    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ pv, const uint32_t* __restrict__ ph,
+    const uint4* __restrict__ pt,
     const uint32_t* __restrict__ info, uint32_t ntiles, const BigMeta* __restrict__ meta,
     const uint32_t* __restrict__ work, const uint32_t* work_n, const uint32_t* __restrict__ cnt,
     uint32_t* __restrict__ sk, uint32_t* __restrict__ sv, uint32_t* __restrict__ sh, uint32_t* __restrict__ segsum,
@@ -2110,7 +2117,7 @@ __global__ __launch_bounds__(BkSmall::THREADS) void k_big_place(
       run_end[M.rb_heavy + tid] = M.base + hstart[tid] + tot[1 + tid];
     }
     uint32_t kk[B::ITEMS], vv[B::ITEMS], hh[B::ITEMS], cls[B::ITEMS];
-    big_chunk_load(M, j, ntiles, pk, pv, ph, kk, vv, hh, cls, true);
+    big_chunk_load(M, j, ntiles, pt, kk, vv, hh, cls, true);
     // ranks in the chunk (item-major within the wave strip = arrival order):
     // light rank, and per hot key: rank and inclusive sum of max(1, hits)
     uint32_t rk[B::ITEMS], hp[B::ITEMS], wl = 0, wc[BK_HEAVY], wh[BK_HEAVY];
@@ -2194,7 +2201,7 @@ __global__ __launch_bounds__(BkSmall::THREADS) void k_big_place(
 }
 
 __global__ __launch_bounds__(BkBig::THREADS) void k_bucket_big(
-    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ pv, const uint32_t* __restrict__ ph,
+    const uint4* __restrict__ pt,
     const uint32_t* __restrict__ info, uint32_t ntiles, uint32_t* __restrict__ sk, uint32_t* __restrict__ sv,
     uint32_t* __restrict__ sh, uint32_t* __restrict__ ht, uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
     uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end, uint32_t* num_runs,
@@ -2243,8 +2250,8 @@ __global__ __launch_bounds__(BkBig::THREADS) void k_bucket_big(
       if (tid < M.r) run_start[M.rb_heavy + tid] = run_end[M.rb_heavy + tid] = 0;  // hot-key runs left empty
       bucket_setup(L, info, ntiles, d);
       BK_STAMP(d, 1);
-      if (!bucket_peel(L, d, S, base, ntiles, pk, pv, ph, sk, sv, sh))
-        bucket_lsd(L, S, base, ntiles, pk, pv, ph, sk, sv, sh, ht, segsum, rid);
+      if (!bucket_peel(L, d, S, base, ntiles, pt, sk, sv, sh))
+        bucket_lsd(L, S, base, ntiles, pt, sk, sv, sh, ht, segsum, rid);
       bucket_segment<B, false>(L, d, S, base, sk, sh, segsum, rid, run_start, run_end, num_runs);
     }
     BK_STAMP(d, 7);
@@ -2718,27 +2725,26 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, hipStream_t st, hipEven
   const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
   if (ev) (void)hipEventRecord(ev[0], st);
   if (g0)
-    k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.keys[0], s.vals[0], s.err, s.time_floor, s.defer_n, s.big_n,
+    k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.keys[0], s.err, s.time_floor, s.defer_n, s.big_n,
                                   s.work_n, s.run_flags, s.num_runs, s.hit_a);
   if (ev) (void)hipEventRecord(ev[1], st);
   const uint32_t ptiles = cdiv(b.n, PART_TILE);
   if (b.n)
-    k_part<<<ptiles, 256, 0, st>>>(s.keys[0], s.vals[0], s.hit_a, s.keys[1], s.vals[1], s.hit_p, b.n, ptiles,
-                                   s.part_info, s.err);
+    k_part<<<ptiles, 256, 0, st>>>(s.keys[0], s.hit_a, s.tile, b.n, ptiles, s.part_info, s.err);
   if (ev) (void)hipEventRecord(ev[2], st);
   if (b.n) {
     const size_t seg_lds = (2ull * ptiles + 1) * 4;
-    k_bucket<<<PART_DIGITS, BkSmall::THREADS, seg_lds, st>>>(s.keys[1], s.vals[1], s.hit_p, s.part_info, ptiles,
+    k_bucket<<<PART_DIGITS, BkSmall::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
                                                              s.keys[0], s.vals[0], s.hits_s, s.segsum, s.rid,
                                                              s.run_start, s.run_end, s.num_runs, s.big_meta, s.big_n,
                                                              s.big_work, s.work_n, s.err);
-    k_big_count<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds, st>>>(s.keys[1], s.hit_p, s.part_info, ptiles,
+    k_big_count<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
                                                                     s.big_meta, s.big_work, s.work_n, s.big_cnt,
                                                                     s.err);
     k_big_place<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds, st>>>(
-        s.keys[1], s.vals[1], s.hit_p, s.part_info, ptiles, s.big_meta, s.big_work, s.work_n, s.big_cnt, s.keys[0],
+        s.tile, s.part_info, ptiles, s.big_meta, s.big_work, s.work_n, s.big_cnt, s.keys[0],
         s.vals[0], s.hits_s, s.segsum, s.rid, s.run_start, s.run_end, s.err);
-    k_bucket_big<<<BIG_BLOCKS, BkBig::THREADS, seg_lds, st>>>(s.keys[1], s.vals[1], s.hit_p, s.part_info, ptiles,
+    k_bucket_big<<<BIG_BLOCKS, BkBig::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
                                                               s.keys[0], s.vals[0], s.hits_s, s.hit_t, s.segsum,
                                                               s.rid, s.run_start, s.run_end, s.num_runs, s.big_meta,
                                                               s.big_n, s.big_cnt, s.err);

@@ -40,6 +40,7 @@ int main(int argc, char** argv) {
     hv[i] = i;
     hh[i] = i % 7;
   }
+  uint4* tl;
   uint32_t *kp[2], *vp[2], *hp[3], *info, *big_n, *work, *work_n, *cnt, *segsum, *rid, *rs, *re, *nr, *err, *ht;
   BigMeta* meta;
   for (int i = 0; i < 2; i++) {
@@ -48,6 +49,7 @@ int main(int argc, char** argv) {
   }
   for (int i = 0; i < 3; i++) CK(hipMalloc(&hp[i], n * 4));
   CK(hipMalloc(&ht, n * 4));
+  CK(hipMalloc(&tl, n * 16));
   CK(hipMalloc(&info, (size_t)PART_DIGITS * ptiles * 4));
   const size_t items = n / BIG_CHUNK + 1 + PART_DIGITS;
   CK(hipMalloc(&meta, PART_DIGITS * sizeof(BigMeta)));
@@ -74,14 +76,14 @@ int main(int argc, char** argv) {
     CK(hipMemset(work_n, 0, 4));
     CK(hipMemset(nr, 0, 4));
     CK(hipEventRecord(ev[0], 0));
-    k_part<<<ptiles, 256>>>(kp[0], vp[0], hp[0], kp[1], vp[1], hp[1], n, ptiles, info, err);
+    k_part<<<ptiles, 256>>>(kp[0], hp[0], tl, n, ptiles, info, err);
     CK(hipEventRecord(ev[1], 0));
-    k_bucket<<<PART_DIGITS, BkSmall::THREADS, seg_lds>>>(kp[1], vp[1], hp[1], info, ptiles, kp[0], vp[0], hp[2], segsum,
+    k_bucket<<<PART_DIGITS, BkSmall::THREADS, seg_lds>>>(tl, info, ptiles, kp[0], vp[0], hp[2], segsum,
                                                          rid, rs, re, nr, meta, big_n, work, work_n, err);
-    k_big_count<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds>>>(kp[1], hp[1], info, ptiles, meta, work, work_n, cnt, err);
-    k_big_place<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds>>>(kp[1], vp[1], hp[1], info, ptiles, meta, work, work_n, cnt,
+    k_big_count<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds>>>(tl, info, ptiles, meta, work, work_n, cnt, err);
+    k_big_place<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds>>>(tl, info, ptiles, meta, work, work_n, cnt,
                                                                 kp[0], vp[0], hp[2], segsum, rid, rs, re, err);
-    k_bucket_big<<<BIG_BLOCKS, BkBig::THREADS, seg_lds>>>(kp[1], vp[1], hp[1], info, ptiles, kp[0], vp[0], hp[2], ht,
+    k_bucket_big<<<BIG_BLOCKS, BkBig::THREADS, seg_lds>>>(tl, info, ptiles, kp[0], vp[0], hp[2], ht,
                                                           segsum, rid, rs, re, nr, meta, big_n, cnt, err);
     CK(hipEventRecord(ev[2], 0));
     CK(hipDeviceSynchronize());
