@@ -38,7 +38,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c1", choices=["c1", "c2", "c3"],
                     help="c1 uniform / c2 Zipf(1.1), hits 1..8 / c3 = c1 at 62.5M tenants per GPU (1B keys on 8)")

@@ -3,6 +3,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/ratelimit_hip.h"
@@ -27,23 +28,35 @@ constexpr uint64_t TAG_TOMB = 1;
 constexpr uint32_t INLINE_KEY = 80;           // stem bytes stored in the slot
 constexpr uint8_t SLOT_EXACT = 0x1;           // stem has >1 unit slot: exact (serial) path
 
-struct __attribute__((aligned(16))) Win {
+struct Win {
   uint32_t ws;      // window start (Redis key suffix); WS_INVALID = no record
   uint32_t count;   // INCRBY value (u32, radix decodes into *uint32)
   uint32_t expire;  // Redis key live while now <= expire (EXPIRE = now + div)
   uint32_t lc;      // freecache entry live while now < lc (Set ttl = div)
 };
 
+// One 128-B line. The first 64-B sector holds everything a probe of a stem of
+// at most KEY_LO bytes needs (tag, length, the current window, the stem), so
+// such a probe reads one sector; `prev`, the arena offset and stem bytes
+// KEY_LO..79 are in the second sector, read only when needed (longer stems,
+// time moving back to the previous window).
+constexpr uint32_t KEY_LO = 36;               // stem bytes in the first sector
 struct __attribute__((aligned(128))) Slot {
   uint64_t tag;       // TAG_EMPTY / TAG_TOMB / mix(hash(stem), unit) >= 2
   uint16_t key_len;   // stem length
   uint8_t unit;       // rl_unit
   uint8_t flags;      // SLOT_EXACT
+  Win cur;            // bytes 12..27
+  uint8_t key0[KEY_LO];               // stem bytes 0..35 (28..63)
+  Win prev;                           // 64..79
   uint32_t ext_off;   // arena offset in 16-B units for bytes >= INLINE_KEY
-  Win cur;
-  Win prev;
-  uint8_t key[INLINE_KEY];
+  uint8_t key1[INLINE_KEY - KEY_LO];  // stem bytes 36..79 (84..127)
 };
+static_assert(offsetof(Slot, cur) == 12 && offsetof(Slot, key0) == 28 && offsetof(Slot, prev) == 64 &&
+                  offsetof(Slot, ext_off) == 80 && offsetof(Slot, key1) == 84,
+              "slot layout");
+// dword of the slot holding stem dword k (k < 20)
+__host__ __device__ constexpr uint32_t slot_key_dw(uint32_t k) { return k < KEY_LO / 4 ? 7 + k : 12 + k; }
 static_assert(sizeof(Slot) == 128, "slot must be one 128-B line");
 
 __host__ __device__ inline uint32_t div_of(uint32_t unit) {  // utils.UnitToDivider

@@ -365,42 +365,49 @@ __device__ inline bool key_equal(const Key& x, const Key& y) {
 // ===========================================================================
 // HBM table probing.
 // ===========================================================================
-// Slot key bytes 0..63 were written from a zero-padded key head, so they
-// compare as whole uint4s; bytes 64..79 inline and the arena cover the rest.
+__device__ inline uint32_t u4w(const uint4& a, uint32_t j) { return j == 0 ? a.x : j == 1 ? a.y : j == 2 ? a.z : a.w; }
+
+// Stem dword k (static in unrolled loops): the zero-padded head, then the packed stems.
+__device__ inline uint32_t key_dw(const Key& key, uint32_t k) {
+  return k < KEY_HEAD / 4 ? u4w(key.h[k >> 2], k & 3) : key.st.word(k);
+}
+
+// Stem bytes [INLINE_KEY, len) of `key` against the arena copy at ext_off.
+__device__ inline uint32_t arena_diff(const uint8_t* arena, uint32_t ext_off, const Key& key) {
+  const uint32_t* ek = reinterpret_cast<const uint32_t*>(arena + (size_t)ext_off * 16);
+  const uint32_t rest = key.len - INLINE_KEY, rw = rest >> 2;
+  uint32_t d = 0;
+  for (uint32_t k = 0; k < rw; k++) d |= ek[k] ^ key.st.word(INLINE_KEY / 4 + k);
+  if (rest & 3) d |= (ek[rw] ^ key.st.word(INLINE_KEY / 4 + rw)) & tail_mask(rest);
+  return d;
+}
+
+// Slot stem == `key`? Only the stem's own dwords are read (the last one masked).
 __device__ inline bool slot_key_equal(const Slot* s, const Key& key, const uint8_t* arena) {
   if (s->key_len != key.len) return false;
-  const uint4* sk4 = reinterpret_cast<const uint4*>(s->key);
-  uint32_t diff = head_diff(sk4, key.h);
-  const uint32_t len = key.len;
-  if (len > KEY_HEAD) {
-    const uint32_t* sk = reinterpret_cast<const uint32_t*>(s->key);
-    const uint32_t il = len < INLINE_KEY ? len : INLINE_KEY;
-    const uint32_t nw = il >> 2;
-    for (uint32_t k = KEY_HEAD / 4; k < nw; k++) diff |= sk[k] ^ key.st.word(k);
-    if (il & 3) diff |= (sk[nw] ^ key.st.word(nw)) & tail_mask(il);
-    if (len > INLINE_KEY) {
-      const uint32_t* ek = reinterpret_cast<const uint32_t*>(arena + (size_t)s->ext_off * 16);
-      const uint32_t rest = len - INLINE_KEY, rw = rest >> 2;
-      for (uint32_t k = 0; k < rw; k++) diff |= ek[k] ^ key.st.word(INLINE_KEY / 4 + k);
-      if (rest & 3) diff |= (ek[rw] ^ key.st.word(INLINE_KEY / 4 + rw)) & tail_mask(rest);
-    }
+  const uint32_t* sd = reinterpret_cast<const uint32_t*>(s);
+  const uint32_t len = key.len, il = len < INLINE_KEY ? len : INLINE_KEY, nw = il >> 2;
+  uint32_t diff = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < INLINE_KEY / 4; k++) {
+    if (k < nw) diff |= sd[slot_key_dw(k)] ^ key_dw(key, k);
+    else if (k == nw && (il & 3)) diff |= (sd[slot_key_dw(k)] ^ key_dw(key, k)) & tail_mask(il);
   }
+  if (len > INLINE_KEY) diff |= arena_diff(arena, s->ext_off, key);
   return diff == 0;
 }
 
 __device__ inline void slot_init(const TableDev& t, Slot* s, const Key& key, uint32_t unit, uint32_t* err) {
-  const uint32_t len = key.len;
+  const uint32_t len = key.len, il = len < INLINE_KEY ? len : INLINE_KEY, nw = il >> 2;
   s->key_len = (uint16_t)len;
   s->unit = (uint8_t)unit;
   s->flags = 0;
   s->ext_off = 0;
-  uint4* sk4 = reinterpret_cast<uint4*>(s->key);
+  uint32_t* sd = reinterpret_cast<uint32_t*>(s);
 #pragma unroll
-  for (uint32_t v = 0; v < 4; v++) sk4[v] = key.h[v];
-  if (len > KEY_HEAD) {
-    uint32_t* sk = reinterpret_cast<uint32_t*>(s->key);
-    const uint32_t il = len < INLINE_KEY ? len : INLINE_KEY;
-    for (uint32_t k = KEY_HEAD / 4; k < (il + 3) / 4; k++) sk[k] = key.st.word(k);
+  for (uint32_t k = 0; k < INLINE_KEY / 4; k++) {
+    if (k < nw) sd[slot_key_dw(k)] = key_dw(key, k);
+    else if (k == nw && (il & 3)) sd[slot_key_dw(k)] = key_dw(key, k) & tail_mask(il);
   }
   if (len > INLINE_KEY) {
     const uint32_t n16 = (len - INLINE_KEY + 15) / 16;
@@ -465,73 +472,73 @@ __device__ int64_t find_slot(const TableDev& t, uint64_t hstem, uint64_t tag, co
   return -1;
 }
 
-// A slot's whole 128-B line, loaded in one round trip (8 x dwordx4): [0] tag |
-// key_len, unit, flags | ext_off, [1] cur, [2] prev, [3..7] stem bytes 0..79.
-// The run kernel probes with it: tag, stem and both window records arrive
-// together instead of three dependent loads. Plain loads are enough: within a
-// launch only CAS inserts change tags, and a lane only ever looks for its own
-// stem, which no other lane inserts.
+// A slot image for probing: the first 64-B sector (tag, length, flags, cur,
+// stem bytes 0..35) always, the second (prev, arena offset, stem bytes 36..79)
+// only when needed (hi). Plain loads are enough: within a launch only CAS
+// inserts change tags, and a lane only ever looks for its own stem, which no
+// other lane inserts.
 struct SlotImg {
-  uint4 v[8];
+  uint4 v[4];   // first sector
+  uint4 pv;     // prev (valid when hi)
+  bool hi;
+  __device__ inline uint32_t dw(uint32_t k) const { return u4w(v[k >> 2], k & 3); }
   __device__ inline uint64_t tag() const { return ((uint64_t)v[0].y << 32) | v[0].x; }
   __device__ inline uint32_t key_len() const { return v[0].z & 0xFFFFu; }
   __device__ inline uint32_t flags() const { return v[0].z >> 24; }
-  __device__ inline uint32_t ext_off() const { return v[0].w; }
-  __device__ inline Win cur() const { return Win{v[1].x, v[1].y, v[1].z, v[1].w}; }
-  __device__ inline Win prev() const { return Win{v[2].x, v[2].y, v[2].z, v[2].w}; }
+  __device__ inline Win cur() const { return Win{v[0].w, v[1].x, v[1].y, v[1].z}; }
+  __device__ inline Win prev() const { return Win{pv.x, pv.y, pv.z, pv.w}; }
 };
 
-__device__ inline void load_img(const Slot* s, SlotImg& im) {
+__device__ inline void load_img_lo(const Slot* s, SlotImg& im) {
   const uint4* p = reinterpret_cast<const uint4*>(s);
 #pragma unroll
-  for (int j = 0; j < 8; j++) im.v[j] = p[j];
+  for (int j = 0; j < 4; j++) im.v[j] = p[j];
+  im.hi = false;
 }
 
-__device__ inline uint32_t u4w(const uint4& a, uint32_t j) { return j == 0 ? a.x : j == 1 ? a.y : j == 2 ? a.z : a.w; }
+__device__ inline void load_img_hi(const Slot* s, SlotImg& im) {
+  if (im.hi) return;
+  im.pv = reinterpret_cast<const uint4*>(s)[4];
+  im.hi = true;
+}
 
-// Stem of `key` == the slot's stem?
-__device__ inline bool img_key_equal(const SlotImg& im, const Key& key, const uint8_t* arena) {
-  const uint4* kh = key.h;
+// Stem of `key` == the slot's stem? Stem bytes beyond the first sector (stems
+// longer than KEY_LO) are read from the slot line directly.
+__device__ inline bool img_key_equal(const Slot* s, const SlotImg& im, const Key& key, const uint8_t* arena) {
   if (im.key_len() != key.len) return false;
+  const uint32_t len = key.len, il = len < INLINE_KEY ? len : INLINE_KEY, nw = il >> 2;
   uint32_t d = 0;
 #pragma unroll
-  for (uint32_t v = 0; v < 4; v++) {
-    const uint4 a = im.v[3 + v], c = kh[v];
-    d |= (a.x ^ c.x) | (a.y ^ c.y) | (a.z ^ c.z) | (a.w ^ c.w);
+  for (uint32_t k = 0; k < KEY_LO / 4; k++) {
+    if (k < nw) d |= im.dw(slot_key_dw(k)) ^ key_dw(key, k);
+    else if (k == nw && (il & 3)) d |= (im.dw(slot_key_dw(k)) ^ key_dw(key, k)) & tail_mask(il);
   }
-  const uint32_t len = key.len;
-  if (len > KEY_HEAD) {
-    const uint32_t il = len < INLINE_KEY ? len : INLINE_KEY, nw = il >> 2;
+  if (len > KEY_LO) {
+    const uint32_t* sd = reinterpret_cast<const uint32_t*>(s);
 #pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-      const uint32_t k = KEY_HEAD / 4 + j;
-      const uint32_t x = u4w(im.v[7], j) ^ key.st.word(k);
-      if (k < nw) d |= x;
-      else if (k == nw && (il & 3)) d |= x & tail_mask(il);
+    for (uint32_t k = KEY_LO / 4; k < INLINE_KEY / 4; k++) {
+      if (k < nw) d |= sd[slot_key_dw(k)] ^ key_dw(key, k);
+      else if (k == nw && (il & 3)) d |= (sd[slot_key_dw(k)] ^ key_dw(key, k)) & tail_mask(il);
     }
-    if (len > INLINE_KEY) {
-      const uint32_t* ek = reinterpret_cast<const uint32_t*>(arena + (size_t)im.ext_off() * 16);
-      const uint32_t rest = len - INLINE_KEY, rw = rest >> 2;
-      for (uint32_t k = 0; k < rw; k++) d |= ek[k] ^ key.st.word(INLINE_KEY / 4 + k);
-      if (rest & 3) d |= (ek[rw] ^ key.st.word(INLINE_KEY / 4 + rw)) & tail_mask(rest);
-    }
+    if (len > INLINE_KEY) d |= arena_diff(arena, s->ext_off, key);
   }
   return d == 0;
 }
 
 // find_slot with insert, returning the slot's image (a fresh slot's image for
-// an insert: empty windows, no flags). `im` holds the home slot's image on
-// entry (the caller issues that load early, beside the stem's).
+// an insert: empty windows, no flags, second sector included). `im` holds the
+// home slot's first sector on entry (the caller issues that load early,
+// beside the stem's).
 __device__ int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint64_t tag, const Key& key, uint32_t unit,
                                  bool* inserted, SlotImg& im, uint32_t* err) {
   uint64_t i = hstem >> t.shift;
   int64_t tomb = -1;
   *inserted = false;
   for (uint32_t p = 0; p < t.max_probe; p++, i = (i + 1) & t.mask) {
-    if (p) load_img(&t.slots[i], im);
+    if (p) load_img_lo(&t.slots[i], im);
     const uint64_t st = im.tag();
     if (st == tag) {
-      if (img_key_equal(im, key, t.arena)) return (int64_t)i;
+      if (img_key_equal(&t.slots[i], im, key, t.arena)) return (int64_t)i;
       continue;
     }
     if (st == TAG_TOMB) {
@@ -548,9 +555,10 @@ __device__ int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint64_t tag
       at = (int64_t)i;
     if (at >= 0) {
       slot_init(t, &t.slots[at], key, unit, err);
-      im.v[0] = make_uint4((uint32_t)tag, (uint32_t)(tag >> 32), key.len | (unit << 16), 0u);
-      im.v[1] = make_uint4(WS_INVALID, 0u, 0u, 0u);
-      im.v[2] = im.v[1];
+      im.v[0] = make_uint4((uint32_t)tag, (uint32_t)(tag >> 32), key.len | (unit << 16), WS_INVALID);
+      im.v[1] = make_uint4(0u, 0u, 0u, 0u);
+      im.pv = make_uint4(WS_INVALID, 0u, 0u, 0u);
+      im.hi = true;
       *inserted = true;
       return at;
     }
@@ -718,13 +726,21 @@ __device__ __attribute__((always_inline)) inline int window_pick(Win& cur, Win& 
 // ---- single (stem, unit) slot, stem never seen with another unit: registers only
 struct SimpleState {
   Win cur, prev;
+  const Slot* slot;     // prev is read from here on first need (have_prev false)
+  bool have_prev;
+  bool cur_dirty, prev_dirty;
   uint32_t cur_req;
   bool pend;
   uint32_t pend_w, pend_e;
   __device__ inline void apply_pending() {
     if (pend) {
-      if (cur.ws == pend_w) cur.lc = pend_e;
-      else if (prev.ws == pend_w) prev.lc = pend_e;
+      if (cur.ws == pend_w) {
+        cur.lc = pend_e;
+        cur_dirty = true;
+      } else if (prev.ws == pend_w) {
+        prev.lc = pend_e;
+        prev_dirty = true;
+      }
       pend = false;
     }
   }
@@ -737,10 +753,20 @@ __device__ __attribute__((always_inline)) inline void simple_step(const Params& 
     S.apply_pending();
     S.cur_req = x.req;
   }
+  // window_pick reads prev only for a window older than cur (time moved back)
+  if (!S.have_prev && S.cur.ws != WS_INVALID && x.w < S.cur.ws) {
+    S.prev = S.slot->prev;
+    S.have_prev = true;
+  }
+  const uint32_t ws0 = S.cur.ws;
   const int which = window_pick(S.cur, S.prev, x.w, 0, true);
   if (which < 0) {
     if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
     return;
+  }
+  if (S.cur.ws != ws0) {  // rolled: the old cur became prev
+    S.have_prev = true;
+    S.prev_dirty = true;
   }
   Win R = which ? S.prev : S.cur;  // values, not pointers: the state stays in VGPRs
   uint32_t after = 0;
@@ -758,8 +784,13 @@ __device__ __attribute__((always_inline)) inline void simple_step(const Params& 
       after = R.count;
     }
   }
-  if (which) S.prev = R;
-  else S.cur = R;
+  if (which) {
+    S.prev = R;
+    S.prev_dirty = true;
+  } else {
+    S.cur = R;
+    S.cur_dirty = true;
+  }
   if (restore) return;
   const Decision r = decide(after - x.h, after, lc_hit && !x.shadow, x.h, x.thr, P.ratio, x.shadow, P.lc_en);
   if (r.set_lc) {
@@ -861,13 +892,16 @@ __device__ __attribute__((always_inline)) inline void replay_simple(SRec rec_s, 
                                                                     unsigned long long* res, const TableDev& t,
                                                                     const Params& P, const uint8_t* repid,
                                                                     uint32_t p, uint32_t end, uint32_t k, int64_t s0,
-                                                                    Win cur0, Win prev0, const Rec& x0, uint32_t e0,
-                                                                    LaneStats& L, StatAcc& acc, uint32_t* err,
-                                                                    bool restore, const SlotImg* img = nullptr) {
+                                                                    Win cur0, Win prev0, bool have_prev,
+                                                                    const Rec& x0, uint32_t e0, LaneStats& L,
+                                                                    StatAcc& acc, uint32_t* err, bool restore) {
   Slot* s = &t.slots[s0];
   SimpleState S;
   S.cur = cur0;
-  S.prev = prev0;
+  S.prev = have_prev ? prev0 : Win{WS_INVALID, 0, 0, 0};  // (never matches a pending window)
+  S.slot = s;
+  S.have_prev = have_prev;
+  S.cur_dirty = S.prev_dirty = false;
   S.cur_req = 0xFFFFFFFFu;
   S.pend = false;
   simple_step(P, res, L, acc, S, load_elem(x0, e0, restore), restore, err);  // element p (always stem k)
@@ -876,14 +910,9 @@ __device__ __attribute__((always_inline)) inline void replay_simple(SRec rec_s, 
     simple_step(P, res, L, acc, S, load_elem(rec_s[q], svals[q], restore), restore, err);
   }
   S.apply_pending();
-  if (img) {  // random writes are the costly part of the probe: store only records that changed
-    const uint4 c = img->v[1], q = img->v[2];
-    if (S.cur.ws != c.x || S.cur.count != c.y || S.cur.expire != c.z || S.cur.lc != c.w) s->cur = S.cur;
-    if (S.prev.ws != q.x || S.prev.count != q.y || S.prev.expire != q.z || S.prev.lc != q.w) s->prev = S.prev;
-  } else {
-    s->cur = S.cur;
-    s->prev = S.prev;
-  }
+  // random writes are the costly part of the probe: store only records that changed
+  if (S.cur_dirty) s->cur = S.cur;
+  if (S.prev_dirty) s->prev = S.prev;
 }
 
 // ===========================================================================
@@ -2322,7 +2351,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
     const uint64_t h0 = ((uint64_t)skeys[p] << 32) | x0.hlo;
     const uint32_t u0 = rec_unit(x0);
     SlotImg im;
-    load_img(&t.slots[h0 >> t.shift], im);  // home slot, in flight beside the stem
+    load_img_lo(&t.slots[h0 >> t.shift], im);  // home slot's first sector, in flight beside the stem
     const Key k0 = key_of(b, x0);
     if (!(fl & RUN_MULTI)) {  // RUN_MULTI runs belong to k_runs_general
       const bool long_run = !restore && end - p >= LONG_RUN && !(fl & RUN_SLOW);
@@ -2352,8 +2381,11 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
       if (ok && long_run) {
         // Parallel path: pick the window record once; k_fast_* decide every element.
         Slot* s = &t.slots[s0];
-        Win cur = im.cur(), prev = im.prev();
         const Elem el0 = load_elem(x0, e0, false);
+        Win cur = im.cur();
+        if (cur.ws != WS_INVALID && el0.w < cur.ws) load_img_hi(s, im);  // prev only for an older window
+        Win prev = im.hi ? im.prev() : Win{WS_INVALID, 0, 0, 0};
+        const uint32_t ws0 = cur.ws;
         const int which = window_pick(cur, prev, el0.w, 0, true);
         if (which < 0) {
           if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
@@ -2363,8 +2395,12 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
           // TTL both end at or after w + div, so they hold for the whole run.
           const uint32_t c0 = el0.now <= R.expire ? R.count : 0u;
           const uint32_t F = (P.lc_en && el0.now < R.lc) ? 1u : 0u;
-          s->cur = cur;
-          s->prev = prev;
+          if (cur.ws != ws0) {  // rolled: cur is new, prev is the old cur
+            s->cur = cur;
+            s->prev = prev;
+          } else if (which) {  // an older window: prev found or started afresh
+            s->prev = prev;
+          }
           run_state[r] = make_uint4((uint32_t)s0, c0, R.lc, F | ((uint32_t)which << 1));
           run_f[r] = 0xFFFFFFFFu;
           run_flags[r] = fl | RUN_FAST;
@@ -2376,8 +2412,8 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
           c.count += end - p;
           sl->cur = c;
         } else {
-          replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, im.cur(), im.prev(), x0, e0, L, acc, err,
-                        restore, ins ? nullptr : &im);
+          replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, im.cur(), im.prev(), im.hi, x0, e0, L, acc,
+                        err, restore);
         }
       } else if (!(s0 < 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_TABLE_FULL))) {
         defer[atomicAdd(defer_n, 1u)] = r;
@@ -2555,7 +2591,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
       }
       if (simple) {
         // (the run's stem k starts at rep[k], not necessarily at p)
-        replay_simple(rec_s, svals, res, t, P, repid, rep[k], end, k, s0, t.slots[s0].cur, t.slots[s0].prev,
+        replay_simple(rec_s, svals, res, t, P, repid, rep[k], end, k, s0, t.slots[s0].cur, t.slots[s0].prev, true,
                       rec_s[rep[k]], svals[rep[k]], L, acc, err, restore);
       } else {
         GeneralState G;
