@@ -225,6 +225,94 @@ int rl_route_do_limit(rl_ctx* ctx, uint32_t n, const void* recv_rec, const uint8
 int rl_route_scatter(rl_ctx* ctx, uint32_t n, const uint32_t* perm, const uint64_t* ret, rl_result* out,
                      void* stream);
 
+/* ---- Config match on the GPU (the caller side of DoLimit) ---
+ * The service's constructLimitsToCheck (src/service/ratelimit.go:104-143) calls
+ * rateLimitConfigImpl.GetLimit (src/config/config_impl.go:243-298) once per
+ * descriptor, then DoLimit, then maps unlimited descriptors to
+ * {OK, LimitRemaining = MaxUint32} (ratelimit.go:176-183). rl_do_limit_requests
+ * does all three on the device for a batch of raw requests: the host only
+ * copies domain / entry bytes; the config trie is walked per descriptor on the
+ * GPU and the matched descriptors are compacted into the DoLimit pipeline.
+ *
+ * rl_config_load replaces the loaded config (GetCurrentConfig snapshot,
+ * ratelimit.go:105) with a flattened trie: one rl_config_node per domain root
+ * and per descriptor config node (rateLimitDescriptor, config_impl.go:45-48),
+ * parents before children. A node's key is the domain name for a root, else
+ * its finalKey: key, or key ‖ '_' ‖ value (config_impl.go:106-109). Host
+ * buffers; (parent, key) pairs must be unique (RL_E_INVALID otherwise).
+ * cache_key_prefix is CACHE_KEY_PREFIX (cache_key.go:62, settings.go). */
+typedef struct rl_config_node {
+  int32_t parent;             /* index of the parent node; -1: a domain root */
+  uint32_t key_off;           /* key bytes in rl_config_tree.key_bytes */
+  uint32_t key_len;
+  uint32_t requests_per_unit; /* RateLimit.Limit.RequestsPerUnit */
+  uint32_t rule_id;           /* dense id of the rule's Stats.Key (its full key path, config_impl.go:111,139) */
+  uint8_t unit;               /* rl_unit (0 for unlimited) */
+  uint8_t has_limit;          /* the node has a rate_limit block (rateLimitDescriptor.limit != nil) */
+  uint8_t unlimited;          /* RateLimit.Unlimited */
+  uint8_t shadow_mode;        /* RateLimit.ShadowMode */
+} rl_config_node;
+
+typedef struct rl_config_tree {
+  uint32_t n_nodes;
+  uint32_t cache_key_prefix_len;
+  const rl_config_node* nodes;
+  const uint8_t* key_bytes;
+  uint64_t key_bytes_len;
+  const uint8_t* cache_key_prefix;
+} rl_config_tree;
+
+int rl_config_load(rl_ctx* ctx, const rl_config_tree* tree);
+
+/* Raw requests (RateLimitRequest, arrival order). Descriptor d belongs to
+ * request req_idx[d] (non-decreasing); its entries are
+ * [entry_first[d], entry_first[d+1]), and its bytes
+ * desc_bytes[desc_off[d], desc_off[d+1]) are Σ(key ‖ '_' ‖ value ‖ '_') over its
+ * entries (the stem tail of cache_key.go:65-70), with key_len / value_len per
+ * entry. Overrides (RateLimitDescriptor.Limit, config_impl.go:255-266):
+ * override_flags[d] bit 0 = present, with override_rpu / override_unit and
+ * override_rule = dense id of descriptorKey(domain, descriptor) (interned
+ * host-side: the one per-override string the caller builds). The three
+ * override arrays may be NULL when no descriptor carries one. Host buffers. */
+typedef struct rl_request_batch {
+  uint32_t n_requests;
+  uint32_t n_descriptors;
+  uint32_t n_entries;
+  uint32_t n_rules;               /* every rule id (config and override) < n_rules */
+  const uint8_t* domain_bytes;    /* RateLimitRequest.Domain, concatenated */
+  const uint32_t* domain_off;     /* [n_requests + 1] */
+  const int64_t* now;             /* [n_requests] UnixNow() of each request */
+  const uint32_t* hits;           /* [n_requests] HitsAddend */
+  const uint32_t* req_idx;        /* [n_descriptors] */
+  const uint32_t* entry_first;    /* [n_descriptors + 1] */
+  const uint32_t* desc_off;       /* [n_descriptors + 1] */
+  const uint8_t* desc_bytes;
+  const uint16_t* key_len;        /* [n_entries] */
+  const uint16_t* value_len;      /* [n_entries] */
+  const uint8_t* override_flags;  /* [n_descriptors] or NULL */
+  const uint32_t* override_rpu;   /* [n_descriptors] or NULL */
+  const uint8_t* override_unit;   /* [n_descriptors] or NULL (pb_type.RateLimitUnit) */
+  const uint32_t* override_rule;  /* [n_descriptors] or NULL */
+} rl_request_batch;
+
+/* Per descriptor, what the service answers (ratelimit.go:158-190). */
+enum rl_match { RL_MATCH_NONE = 0, RL_MATCH_UNLIMITED = 1, RL_MATCH_LIMIT = 2 };
+typedef struct rl_request_result {
+  uint8_t* code;               /* [n_descriptors] rl_code */
+  uint32_t* limit_remaining;   /* [n_descriptors]; MaxUint32 for unlimited */
+  uint32_t* reset_s;           /* [n_descriptors]; 0 = no DurationUntilReset (nil limit) */
+  uint8_t* match;              /* [n_descriptors] rl_match */
+  uint32_t* rule_id;           /* [n_descriptors] matched rule (RL_MATCH_LIMIT / UNLIMITED) */
+  uint32_t* requests_per_unit; /* [n_descriptors] CurrentLimit.RequestsPerUnit (RL_MATCH_LIMIT) */
+  uint8_t* unit;               /* [n_descriptors] CurrentLimit.Unit (RL_MATCH_LIMIT) */
+  uint64_t* stats;             /* [n_rules * RL_NUM_STATS], this call's deltas */
+} rl_request_result;
+
+/* GetLimit + DoLimit + the unlimited mapping for a batch of raw requests.
+ * Synchronous. A descriptor whose override or config unit is not 1..4 fails
+ * the batch with RL_E_INVALID (the reference panics in UnitToDivider). */
+int rl_do_limit_requests(rl_ctx* ctx, const rl_request_batch* in, rl_request_result* out);
+
 /* Per-stage device timing (HIP events on the batch stream), for benchmarks.
  * rl_profile(ctx, 1) starts accumulating; rl_profile_read fills ms[0..n) with
  * the summed milliseconds of the stages {prepare, sort, segment, runs, finish}

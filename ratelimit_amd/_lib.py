@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("RL_LIB_PATH") or os.path.join(HERE, "libratelimit_hip
 EXPORTS = ["rl_abi_version", "rl_create", "rl_destroy", "rl_last_error", "rl_do_limit", "rl_do_limit_async",
            "rl_synchronize", "rl_sweep", "rl_restore", "rl_table_info_get", "rl_alloc_host", "rl_free_host",
            "rl_debug_keys", "rl_debug_decide", "rl_profile", "rl_profile_read", "rl_route_pack",
-           "rl_route_do_limit", "rl_route_scatter"]
+           "rl_route_do_limit", "rl_route_scatter", "rl_config_load", "rl_do_limit_requests"]
 
 _lib = None
 
@@ -63,6 +63,8 @@ def lib():
                                     C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
     L.rl_route_scatter.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(abi.RlResult),
                                    C.c_void_p]
+    L.rl_config_load.argtypes = [C.c_void_p, C.POINTER(abi.RlConfigTree)]
+    L.rl_do_limit_requests.argtypes = [C.c_void_p, C.POINTER(abi.RlRequestBatch), C.POINTER(abi.RlRequestResult)]
     if L.rl_abi_version() != 1:
         raise RuntimeError("libratelimit_hip.so ABI mismatch")
     _lib = L

@@ -46,6 +46,47 @@ class RlTableInfo(C.Structure):
                 ("batches", C.c_uint64), ("decisions", C.c_uint64)]
 
 
+class RlConfigNode(C.Structure):
+    _fields_ = [("parent", C.c_int32), ("key_off", C.c_uint32), ("key_len", C.c_uint32),
+                ("requests_per_unit", C.c_uint32), ("rule_id", C.c_uint32), ("unit", C.c_uint8),
+                ("has_limit", C.c_uint8), ("unlimited", C.c_uint8), ("shadow_mode", C.c_uint8)]
+
+
+# numpy view of rl_config_node (24 B), for building the node array in one go
+CONFIG_NODE_DTYPE = np.dtype([("parent", np.int32), ("key_off", np.uint32), ("key_len", np.uint32),
+                              ("requests_per_unit", np.uint32), ("rule_id", np.uint32), ("unit", np.uint8),
+                              ("has_limit", np.uint8), ("unlimited", np.uint8), ("shadow_mode", np.uint8)])
+
+
+class RlConfigTree(C.Structure):
+    _fields_ = [("n_nodes", C.c_uint32), ("cache_key_prefix_len", C.c_uint32), ("nodes", P),
+                ("key_bytes", P), ("key_bytes_len", C.c_uint64), ("cache_key_prefix", P)]
+
+
+class RlRequestBatch(C.Structure):
+    _fields_ = [("n_requests", C.c_uint32), ("n_descriptors", C.c_uint32), ("n_entries", C.c_uint32),
+                ("n_rules", C.c_uint32), ("domain_bytes", P), ("domain_off", P), ("now", P), ("hits", P),
+                ("req_idx", P), ("entry_first", P), ("desc_off", P), ("desc_bytes", P), ("key_len", P),
+                ("value_len", P), ("override_flags", P), ("override_rpu", P), ("override_unit", P),
+                ("override_rule", P)]
+
+
+class RlRequestResult(C.Structure):
+    _fields_ = [("code", P), ("limit_remaining", P), ("reset_s", P), ("match", P), ("rule_id", P),
+                ("requests_per_unit", P), ("unit", P), ("stats", P)]
+
+
+RL_MATCH_NONE, RL_MATCH_UNLIMITED, RL_MATCH_LIMIT = 0, 1, 2
+REQUEST_ARRAYS = ("domain_bytes", "domain_off", "now", "hits", "req_idx", "entry_first", "desc_off", "desc_bytes",
+                  "key_len", "value_len", "override_flags", "override_rpu", "override_unit", "override_rule")
+REQUEST_DTYPES = {"domain_bytes": np.uint8, "domain_off": np.uint32, "now": np.int64, "hits": np.uint32,
+                  "req_idx": np.uint32, "entry_first": np.uint32, "desc_off": np.uint32, "desc_bytes": np.uint8,
+                  "key_len": np.uint16, "value_len": np.uint16, "override_flags": np.uint8,
+                  "override_rpu": np.uint32, "override_unit": np.uint8, "override_rule": np.uint32}
+REQUEST_RESULT_DTYPES = {"code": np.uint8, "limit_remaining": np.uint32, "reset_s": np.uint32, "match": np.uint8,
+                         "rule_id": np.uint32, "requests_per_unit": np.uint32, "unit": np.uint8}
+
+
 def ptr(a):
     """Address of a numpy array (host) or a torch tensor (device) as c_void_p."""
     if a is None:

@@ -10,8 +10,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libratelimit_hip.so")
-SOURCES = ["rl_kernels.hip", "rl_route.hip", "rl_api.hip"]
-HEADERS = ["rl_device.h", "rl_kernels.h", os.path.join("..", "..", "include", "ratelimit_hip.h")]
+SOURCES = ["rl_kernels.hip", "rl_route.hip", "rl_match.hip", "rl_api.hip"]
+HEADERS = ["rl_device.h", "rl_kernels.h", "rl_match.h", os.path.join("..", "..", "include", "ratelimit_hip.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RL_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-ffp-contract=off",

@@ -16,10 +16,12 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/ratelimit_hip.h"
 #include "rl_device.h"
 #include "rl_kernels.h"
+#include "rl_match.h"
 
 using namespace rl;
 
@@ -69,6 +71,16 @@ struct rl_ctx {
   hipEvent_t ev[PROF_RING][RL_NUM_STAGES + 1] = {};
   double stage_ms[RL_NUM_STAGES] = {};
   uint64_t prof_batches = 0;
+  // config match (rl_config_load / rl_do_limit_requests): the device trie and
+  // one growable device buffer carved per call for the raw requests
+  CfgNode* cfg_nodes = nullptr;
+  uint8_t* cfg_keys = nullptr;
+  unsigned long long* cfg_index = nullptr;
+  CfgDev cfg_dev{};
+  bool cfg_loaded = false;
+  uint8_t* mbuf = nullptr;
+  size_t mbuf_cap = 0;
+  uint32_t* h_match = nullptr;  // pinned [4]: matched count, stem bytes, error bits
 };
 
 namespace {
@@ -412,6 +424,9 @@ void rl_destroy(rl_ctx* c) {
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
   if (c->h_route) (void)hipHostFree(c->h_route);
+  for (void* p : {(void*)c->cfg_nodes, (void*)c->cfg_keys, (void*)c->cfg_index, (void*)c->mbuf})
+    if (p) (void)hipFree(p);
+  if (c->h_match) (void)hipHostFree(c->h_match);
   for (uint32_t k = 0; k < NBUF; k++)
     if (c->pipe[k]) (void)hipStreamDestroy(c->pipe[k]);
   if (c->side) (void)hipStreamDestroy(c->side);
@@ -740,4 +755,216 @@ int rl_debug_decide(rl_ctx* c, uint32_t n, const uint32_t* before, const uint32_
   return RL_OK;
 }
 
+// ---- config match: GetLimit on the device (rl_match.hip) -------------------
+
+int rl_config_load(rl_ctx* c, const rl_config_tree* t) {
+  if (!c || !t || (t->n_nodes && (!t->nodes || (t->key_bytes_len && !t->key_bytes))) ||
+      (t->cache_key_prefix_len && !t->cache_key_prefix))
+    return set_err(c, RL_E_INVALID, "gpu: null config tree");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const uint32_t n = t->n_nodes;
+  std::vector<CfgNode> nodes(n);
+  for (uint32_t i = 0; i < n; i++) {
+    const rl_config_node& x = t->nodes[i];
+    if (x.parent < -1 || x.parent >= (int32_t)i || (uint64_t)x.key_off + x.key_len > t->key_bytes_len)
+      return set_err(c, RL_E_INVALID, "gpu: config node " + std::to_string(i) + ": bad parent or key range");
+    if (x.has_limit && !x.unlimited && (x.unit < RL_UNIT_SECOND || x.unit > RL_UNIT_DAY))
+      return set_err(c, RL_E_INVALID, "gpu: config node " + std::to_string(i) + ": invalid rate limit unit");
+    if (x.has_limit && x.rule_id >= c->cfg.max_rules)
+      return set_err(c, RL_E_INVALID, "gpu: config node " + std::to_string(i) + ": rule id >= max_rules");
+    CfgNode& d = nodes[i];
+    d = CfgNode{};
+    d.parent = x.parent;
+    d.key_off = t->cache_key_prefix_len + x.key_off;  // the prefix is stored first
+    d.key_len = x.key_len;
+    d.rpu = x.requests_per_unit;
+    d.rule = x.rule_id;
+    d.unit = x.unit;
+    d.has_limit = x.has_limit ? 1 : 0;
+    d.unlimited = x.unlimited ? 1 : 0;
+    d.shadow = x.shadow_mode ? 1 : 0;
+    if (x.parent >= 0) nodes[x.parent].n_children++;
+  }
+  uint32_t size = 16;
+  while (size < 2 * n) size <<= 1;
+  std::vector<unsigned long long> index(size, 0);
+  const uint8_t* kb = t->key_bytes;
+  for (uint32_t i = 0; i < n; i++) {
+    const rl_config_node& x = t->nodes[i];
+    const uint64_t h = cfg_hash(x.parent, kb + x.key_off, x.key_len);
+    uint32_t pos = (uint32_t)h & (size - 1);
+    for (;; pos = (pos + 1) & (size - 1)) {
+      const unsigned long long e = index[pos];
+      if (!e) break;
+      const rl_config_node& y = t->nodes[(uint32_t)(e >> 32) - 1];
+      if (y.parent == x.parent && y.key_len == x.key_len && !memcmp(kb + y.key_off, kb + x.key_off, x.key_len))
+        return set_err(c, RL_E_INVALID, "gpu: duplicate config key under one parent (node " + std::to_string(i) + ")");
+    }
+    index[pos] = (unsigned long long)(uint32_t)(h >> 32) | (unsigned long long)(i + 1) << 32;
+  }
+  const uint64_t nkeys = t->cache_key_prefix_len + t->key_bytes_len;
+  HIPCHK(c, after_batches(c, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (void* p : {(void*)c->cfg_nodes, (void*)c->cfg_keys, (void*)c->cfg_index})
+    if (p) (void)hipFree(p);
+  c->cfg_nodes = nullptr;
+  c->cfg_keys = nullptr;
+  c->cfg_index = nullptr;
+  c->cfg_loaded = false;
+  HIPCHK(c, dalloc(&c->cfg_nodes, n));
+  HIPCHK(c, dalloc(&c->cfg_keys, nkeys));
+  HIPCHK(c, dalloc(&c->cfg_index, size));
+  if (!c->h_match) HIPCHK(c, hipHostMalloc((void**)&c->h_match, 16, hipHostMallocDefault));
+  if (n) HIPCHK(c, hipMemcpy(c->cfg_nodes, nodes.data(), n * sizeof(CfgNode), hipMemcpyHostToDevice));
+  if (t->cache_key_prefix_len)
+    HIPCHK(c, hipMemcpy(c->cfg_keys, t->cache_key_prefix, t->cache_key_prefix_len, hipMemcpyHostToDevice));
+  if (t->key_bytes_len)
+    HIPCHK(c, hipMemcpy(c->cfg_keys + t->cache_key_prefix_len, kb, t->key_bytes_len, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->cfg_index, index.data(), size * 8ull, hipMemcpyHostToDevice));
+  c->cfg_dev = CfgDev{c->cfg_nodes, c->cfg_keys, c->cfg_index, size - 1, n, c->cfg_keys, t->cache_key_prefix_len};
+  c->cfg_loaded = true;
+  return RL_OK;
+}
+
+int rl_do_limit_requests(rl_ctx* c, const rl_request_batch* in, rl_request_result* out) {
+  if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  // checkServiceErr(snappedConfig != nil, ...) (ratelimit.go:106)
+  if (!c->cfg_loaded) return set_err(c, RL_E_INVALID, "gpu: no rate limit configuration loaded");
+  const uint32_t n = in->n_descriptors, nq = in->n_requests, ne = in->n_entries;
+  if (n > c->cfg.max_batch || nq > c->cfg.max_requests || in->n_rules > c->cfg.max_rules)
+    return set_err(c, RL_E_CAPACITY, "gpu: request batch exceeds configured max_batch/max_requests/max_rules");
+  if (n && !nq) return set_err(c, RL_E_INVALID, "gpu: descriptors without requests");
+  if (!in->domain_off || !in->entry_first || !in->desc_off || (nq && (!in->now || !in->hits)) ||
+      (n && !in->req_idx) || (ne && (!in->key_len || !in->value_len)))
+    return set_err(c, RL_E_INVALID, "gpu: null request batch array");
+  const bool ovr = in->override_flags != nullptr;
+  if (ovr && (!in->override_rpu || !in->override_unit || !in->override_rule))
+    return set_err(c, RL_E_INVALID, "gpu: override_flags without override_rpu/unit/rule");
+  if (in->entry_first[0] != 0 || in->entry_first[n] != ne || in->desc_off[0] != 0 || in->domain_off[0] != 0)
+    return set_err(c, RL_E_INVALID, "gpu: request batch offsets must start at 0 and end at n_entries");
+  const uint64_t dom_bytes = in->domain_off[nq], desc_bytes = in->desc_off[n];
+  if ((dom_bytes && !in->domain_bytes) || (desc_bytes && !in->desc_bytes))
+    return set_err(c, RL_E_INVALID, "gpu: null request byte array");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  // one device buffer, carved (256-B aligned pieces)
+  const size_t scan = n ? match_scan_bytes(n) : 0;
+  size_t need = 0;
+  auto piece = [&need](size_t bytes) {
+    const size_t o = need;
+    need += (std::max<size_t>(bytes, 1) + 255) & ~(size_t)255;
+    return o;
+  };
+  const size_t o_dom = piece(dom_bytes), o_domoff = piece((nq + 1) * 4ull), o_hits = piece(nq * 4ull),
+               o_req = piece(n * 4ull), o_ent = piece((n + 1) * 4ull), o_doff = piece((n + 1) * 4ull),
+               o_desc = piece(desc_bytes), o_kl = piece(ne * 2ull), o_vl = piece(ne * 2ull),
+               o_ovf = piece(ovr ? n : 0), o_ovr = piece(ovr ? n * 4ull : 0), o_ovu = piece(ovr ? n : 0),
+               o_ovrule = piece(ovr ? n * 4ull : 0), o_v = piece(n * 16ull), o_kind = piece(n * 4ull),
+               o_rpu = piece(n * 4ull), o_rule = piece(n * 4ull), o_cnt = piece(16), o_code = piece(n),
+               o_rem = piece(n * 4ull), o_reset = piece(n * 4ull), o_match = piece(n), o_orule = piece(n * 4ull),
+               o_orpu = piece(n * 4ull), o_ounit = piece(n), o_tmp = piece(scan);
+  hipStream_t st = c->stream;
+  HIPCHK(c, after_batches(c, st));
+  if (need > c->mbuf_cap) {
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (c->mbuf) (void)hipFree(c->mbuf);
+    c->mbuf = nullptr;
+    c->mbuf_cap = 0;
+    HIPCHK(c, hipMalloc((void**)&c->mbuf, need));
+    c->mbuf_cap = need;
+  }
+  uint8_t* B = c->mbuf;
+  auto h2d = [&](size_t off, const void* src, size_t bytes) {
+    return bytes ? hipMemcpyAsync(B + off, src, bytes, hipMemcpyHostToDevice, st) : hipSuccess;
+  };
+  HIPCHK(c, h2d(o_dom, in->domain_bytes, dom_bytes));
+  HIPCHK(c, h2d(o_domoff, in->domain_off, (nq + 1) * 4ull));
+  HIPCHK(c, h2d(o_hits, in->hits, nq * 4ull));
+  HIPCHK(c, h2d(o_req, in->req_idx, n * 4ull));
+  HIPCHK(c, h2d(o_ent, in->entry_first, (n + 1) * 4ull));
+  HIPCHK(c, h2d(o_doff, in->desc_off, (n + 1) * 4ull));
+  HIPCHK(c, h2d(o_desc, in->desc_bytes, desc_bytes));
+  HIPCHK(c, h2d(o_kl, in->key_len, ne * 2ull));
+  HIPCHK(c, h2d(o_vl, in->value_len, ne * 2ull));
+  if (ovr) {
+    HIPCHK(c, h2d(o_ovf, in->override_flags, n));
+    HIPCHK(c, h2d(o_ovr, in->override_rpu, n * 4ull));
+    HIPCHK(c, h2d(o_ovu, in->override_unit, n));
+    HIPCHK(c, h2d(o_ovrule, in->override_rule, n * 4ull));
+  }
+  if (nq) HIPCHK(c, hipMemcpyAsync(c->d_now, in->now, nq * 8ull, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemsetAsync(B + o_cnt, 0, 16, st));
+  ReqDev r;
+  r.n_req = nq;
+  r.n_desc = n;
+  r.n_ent = ne;
+  r.dom_total = (uint32_t)dom_bytes;
+  r.desc_total = (uint32_t)desc_bytes;
+  r.dom = B + o_dom;
+  r.dom_off = (const uint32_t*)(B + o_domoff);
+  r.hits = (const uint32_t*)(B + o_hits);
+  r.req = (const uint32_t*)(B + o_req);
+  r.ent_first = (const uint32_t*)(B + o_ent);
+  r.desc_off = (const uint32_t*)(B + o_doff);
+  r.desc = B + o_desc;
+  r.klen = (const uint16_t*)(B + o_kl);
+  r.vlen = (const uint16_t*)(B + o_vl);
+  r.ovf = ovr ? B + o_ovf : nullptr;
+  r.ov_rpu = ovr ? (const uint32_t*)(B + o_ovr) : nullptr;
+  r.ov_unit = ovr ? B + o_ovu : nullptr;
+  r.ov_rule = ovr ? (const uint32_t*)(B + o_ovrule) : nullptr;
+  MatchBuf m{(unsigned long long*)(B + o_v), (uint32_t*)(B + o_kind), (uint32_t*)(B + o_rpu),
+             (uint32_t*)(B + o_rule), (uint32_t*)(B + o_cnt)};
+  // the matched descriptors become an ordinary DoLimit batch in the staging buffers
+  PackOut po{c->d_stem, c->d_off, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule,
+             c->cfg.max_stem_bytes};
+  launch_match(c->cfg_dev, r, m, po, B + o_tmp, scan, st);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->h_match, B + o_cnt, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  if (c->h_match[2] & MATCH_ERR_REQ)
+    return set_err(c, RL_E_INVALID, "gpu: malformed request batch (request index or entry byte layout)");
+  if (c->h_match[2] & MATCH_ERR_CAP)
+    return set_err(c, RL_E_CAPACITY, "gpu: matched stems exceed max_stem_bytes");
+  const uint32_t nm = n ? c->h_match[0] : 0;
+  if (!n) {  // off[0] of the empty batch
+    HIPCHK(c, hipMemsetAsync(c->d_off, 0, 4, st));
+  }
+  rl_batch pb{};
+  pb.n = nm;
+  pb.n_requests = nq;
+  pb.n_rules = in->n_rules;
+  pb.stem_bytes = c->d_stem;
+  pb.stem_off = c->d_off;
+  pb.now = c->d_now;
+  pb.req_idx = c->d_req;
+  pb.unit = c->d_unit;
+  pb.flags = c->d_flags;
+  pb.limit = c->d_limit;
+  pb.hits = c->d_hits;
+  pb.rule_id = c->d_rule;
+  BatchDev b = dev_view(&pb, c->cfg.max_stem_bytes);
+  OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats};
+  enqueue(c, b, o, 0, st, false);
+  ReqOutDev ro{B + o_code, (uint32_t*)(B + o_rem), (uint32_t*)(B + o_reset), B + o_match,
+               (uint32_t*)(B + o_orule), (uint32_t*)(B + o_orpu), B + o_ounit};
+  launch_match_expand(r, m, c->d_code, c->d_rem, c->d_reset, ro, st);
+  HIPCHK(c, hipGetLastError());
+  auto d2h = [&](void* dst, size_t off, size_t bytes) {
+    return (bytes && dst) ? hipMemcpyAsync(dst, B + off, bytes, hipMemcpyDeviceToHost, st) : hipSuccess;
+  };
+  HIPCHK(c, d2h(out->code, o_code, n));
+  HIPCHK(c, d2h(out->limit_remaining, o_rem, n * 4ull));
+  HIPCHK(c, d2h(out->reset_s, o_reset, n * 4ull));
+  HIPCHK(c, d2h(out->match, o_match, n));
+  HIPCHK(c, d2h(out->rule_id, o_orule, n * 4ull));
+  HIPCHK(c, d2h(out->requests_per_unit, o_orpu, n * 4ull));
+  HIPCHK(c, d2h(out->unit, o_ounit, n));
+  if (in->n_rules && out->stats)
+    HIPCHK(c, hipMemcpyAsync(out->stats, c->d_stats, (size_t)in->n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost, st));
+  c->batches++;
+  c->decisions += nm;
+  return collect(c);
+}
+
 }  // extern "C"
+

@@ -29,7 +29,7 @@ from .types import OK, DescriptorStatus, Limit  # noqa: F401  (re-exported data 
 # rl_profile stages (include/ratelimit_hip.h RL_NUM_STAGES)
 STAGES = ("prepare", "sort", "segment", "runs", "finish")
 
-__all__ = ["GpuRateLimitCache", "RedisError", "TimeSource"]
+__all__ = ["GpuRateLimitCache", "GpuRateLimitService", "RedisError", "TimeSource"]
 
 
 class TimeSource:
@@ -108,6 +108,36 @@ class Backend:
         r = abi.make_result_struct(dev_out)
         check(self.ctx, lib().rl_do_limit_async(self.ctx, C.byref(b), C.byref(r),
                                                 C.c_void_p(stream) if stream else None))
+
+    # ---- config match + DoLimit on raw requests (rl_match.hip)
+    def load_config(self, tree) -> None:
+        """rl_config_load: ``tree`` is a ratelimit_amd.config.ConfigTree."""
+        nodes, kb, pre = tree.arrays()
+        t = abi.RlConfigTree()
+        t.n_nodes = len(nodes)
+        t.cache_key_prefix_len = len(tree.prefix.encode())
+        t.nodes = C.c_void_p(nodes.ctypes.data)
+        t.key_bytes = abi.ptr(kb)
+        t.key_bytes_len = sum(len(k) for k in tree.keys)
+        t.cache_key_prefix = abi.ptr(pre)
+        check(self.ctx, lib().rl_config_load(self.ctx, C.byref(t)))
+
+    def do_limit_requests(self, arrays: dict, n_rules: int) -> dict:
+        """rl_do_limit_requests on pack_requests() arrays -> per-descriptor results + stats."""
+        n = len(arrays["req_idx"])
+        b = abi.RlRequestBatch()
+        b.n_requests, b.n_descriptors, b.n_entries, b.n_rules = len(arrays["hits"]), n, len(arrays["key_len"]), n_rules
+        for k in abi.REQUEST_ARRAYS:
+            setattr(b, k, abi.ptr(arrays[k]))
+        out = {k: np.zeros(max(n, 1), dt) for k, dt in abi.REQUEST_RESULT_DTYPES.items()}
+        out["stats"] = np.zeros(max(n_rules, 1) * abi.RL_NUM_STATS, np.uint64)
+        r = abi.RlRequestResult()
+        for k in out:
+            setattr(r, k, abi.ptr(out[k]))
+        check(self.ctx, lib().rl_do_limit_requests(self.ctx, C.byref(b), C.byref(r)))
+        res = {k: v[:n] for k, v in out.items() if k != "stats"}
+        res["stats"] = out["stats"][:n_rules * abi.RL_NUM_STATS]
+        return res
 
     def profile(self, enable: bool):
         check(self.ctx, lib().rl_profile(self.ctx, 1 if enable else 0))
@@ -213,3 +243,64 @@ class GpuRateLimitCache:
     def flush(self):
         """Flush(): nothing is asynchronous on the host path."""
         return None
+
+
+class GpuRateLimitService:
+    """The service step around DoLimit with the config lookup on the GPU:
+    constructLimitsToCheck + DoLimit + shouldRateLimitWorker's statuses
+    (src/service/ratelimit.go:104-208; no custom headers) for many requests at
+    once through ``rl_do_limit_requests``. Config is YAML text as
+    ``NewRateLimitConfigImpl`` takes it (src/config/config_impl.go:318-330)."""
+
+    def __init__(self, config_files, near_limit_ratio: float = 0.8, local_cache: bool = False,
+                 cache_key_prefix: str = "", per_second: bool = False, global_shadow_mode: bool = False,
+                 **backend_kw):
+        from .config import ConfigTree
+        self.interner = RuleInterner()
+        self.tree = ConfigTree.from_yaml(config_files, cache_key_prefix, self.interner)
+        self.global_shadow_mode = global_shadow_mode
+        self.backend = Backend(near_limit_ratio, local_cache, per_second, **backend_kw)
+        self.backend.load_config(self.tree)
+        self.stats = {}  # stats key -> [6 counters] (the gostats store)
+
+    def close(self):
+        self.backend.close()
+
+    def should_rate_limit_batch(self, requests, nows):
+        """-> [(overall code, [DescriptorStatus])] per request, arrival order."""
+        from .config import pack_requests
+        for r in requests:  # checkServiceErr (ratelimit.go:151-152)
+            if r.domain == "":
+                raise ValueError("rate limit domain must not be empty")
+            if not r.descriptors:
+                raise ValueError("rate limit descriptor list must not be empty")
+        a = pack_requests(requests, nows, self.interner)
+        n_rules = max(len(self.interner.keys), 1)
+        res = self.backend.do_limit_requests(a, n_rules)
+        st = res["stats"].reshape(-1, abi.RL_NUM_STATS)
+        for i in np.nonzero(st.any(axis=1))[0]:
+            row = self.stats.setdefault(self.interner.keys[i], [0] * abi.RL_NUM_STATS)
+            for j in range(abi.RL_NUM_STATS):
+                row[j] += int(st[i, j])
+        out = []
+        d = 0
+        OVER = 2
+        for r in requests:
+            sts = []
+            final = OK
+            for _ in r.descriptors:
+                m = int(res["match"][d])
+                if m == abi.RL_MATCH_LIMIT:
+                    s_ = DescriptorStatus(int(res["code"][d]),
+                                          Limit(int(res["requests_per_unit"][d]), int(res["unit"][d])),
+                                          int(res["limit_remaining"][d]), int(res["reset_s"][d]))
+                    if s_.code == OVER:
+                        final = OVER
+                else:  # nil limit {OK, nil, 0}; unlimited {OK, nil, MaxUint32}
+                    s_ = DescriptorStatus(OK, None, int(res["limit_remaining"][d]), None)
+                sts.append(s_)
+                d += 1
+            if final == OVER and self.global_shadow_mode:
+                final = OK
+            out.append((final, sts))
+        return out
