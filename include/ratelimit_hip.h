@@ -267,7 +267,7 @@ int rl_config_load(rl_ctx* ctx, const rl_config_tree* tree);
 /* Raw requests (RateLimitRequest, arrival order). Descriptor d belongs to
  * request req_idx[d] (non-decreasing); its entries are
  * [entry_first[d], entry_first[d+1]), and its bytes
- * desc_bytes[desc_off[d], desc_off[d+1]) are Σ(key ‖ '_' ‖ value ‖ '_') over its
+ * desc_bytes[desc_off[d], desc_off[d+1]) (all offsets non-decreasing) are Σ(key ‖ '_' ‖ value ‖ '_') over its
  * entries (the stem tail of cache_key.go:65-70), with key_len / value_len per
  * entry. Overrides (RateLimitDescriptor.Limit, config_impl.go:255-266):
  * override_flags[d] bit 0 = present, with override_rpu / override_unit and

@@ -73,9 +73,7 @@ struct rl_ctx {
   uint64_t prof_batches = 0;
   // config match (rl_config_load / rl_do_limit_requests): the device trie and
   // one growable device buffer carved per call for the raw requests
-  CfgNode* cfg_nodes = nullptr;
-  uint8_t* cfg_keys = nullptr;
-  unsigned long long* cfg_index = nullptr;
+  uint8_t* cfg_blob = nullptr;  // [nodes | index | prefix ‖ keys]
   CfgDev cfg_dev{};
   bool cfg_loaded = false;
   uint8_t* mbuf = nullptr;
@@ -424,7 +422,7 @@ void rl_destroy(rl_ctx* c) {
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
   if (c->h_route) (void)hipHostFree(c->h_route);
-  for (void* p : {(void*)c->cfg_nodes, (void*)c->cfg_keys, (void*)c->cfg_index, (void*)c->mbuf})
+  for (void* p : {(void*)c->cfg_blob, (void*)c->mbuf})
     if (p) (void)hipFree(p);
   if (c->h_match) (void)hipHostFree(c->h_match);
   for (uint32_t k = 0; k < NBUF; k++)
@@ -775,7 +773,7 @@ int rl_config_load(rl_ctx* c, const rl_config_tree* t) {
     CfgNode& d = nodes[i];
     d = CfgNode{};
     d.parent = x.parent;
-    d.key_off = t->cache_key_prefix_len + x.key_off;  // the prefix is stored first
+    d.key_off = x.key_off;
     d.key_len = x.key_len;
     d.rpu = x.requests_per_unit;
     d.rule = x.rule_id;
@@ -802,26 +800,37 @@ int rl_config_load(rl_ctx* c, const rl_config_tree* t) {
     }
     index[pos] = (unsigned long long)(uint32_t)(h >> 32) | (unsigned long long)(i + 1) << 32;
   }
+  // one blob [nodes | index | prefix ‖ keys], so a small config is staged into LDS in one copy
   const uint64_t nkeys = t->cache_key_prefix_len + t->key_bytes_len;
+  const uint64_t idx_off = (uint64_t)n * sizeof(CfgNode), key_off = idx_off + size * 8ull;
+  const uint64_t blob = (key_off + nkeys + 3) & ~3ull;
+  std::vector<uint8_t> host(blob, 0);
+  if (n) memcpy(host.data(), nodes.data(), n * sizeof(CfgNode));
+  memcpy(host.data() + idx_off, index.data(), size * 8ull);
+  if (t->cache_key_prefix_len) memcpy(host.data() + key_off, t->cache_key_prefix, t->cache_key_prefix_len);
+  if (t->key_bytes_len) memcpy(host.data() + key_off + t->cache_key_prefix_len, kb, t->key_bytes_len);
   HIPCHK(c, after_batches(c, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  for (void* p : {(void*)c->cfg_nodes, (void*)c->cfg_keys, (void*)c->cfg_index})
-    if (p) (void)hipFree(p);
-  c->cfg_nodes = nullptr;
-  c->cfg_keys = nullptr;
-  c->cfg_index = nullptr;
+  if (c->cfg_blob) (void)hipFree(c->cfg_blob);
+  c->cfg_blob = nullptr;
   c->cfg_loaded = false;
-  HIPCHK(c, dalloc(&c->cfg_nodes, n));
-  HIPCHK(c, dalloc(&c->cfg_keys, nkeys));
-  HIPCHK(c, dalloc(&c->cfg_index, size));
+  HIPCHK(c, dalloc(&c->cfg_blob, blob));
   if (!c->h_match) HIPCHK(c, hipHostMalloc((void**)&c->h_match, 16, hipHostMallocDefault));
-  if (n) HIPCHK(c, hipMemcpy(c->cfg_nodes, nodes.data(), n * sizeof(CfgNode), hipMemcpyHostToDevice));
-  if (t->cache_key_prefix_len)
-    HIPCHK(c, hipMemcpy(c->cfg_keys, t->cache_key_prefix, t->cache_key_prefix_len, hipMemcpyHostToDevice));
-  if (t->key_bytes_len)
-    HIPCHK(c, hipMemcpy(c->cfg_keys + t->cache_key_prefix_len, kb, t->key_bytes_len, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->cfg_index, index.data(), size * 8ull, hipMemcpyHostToDevice));
-  c->cfg_dev = CfgDev{c->cfg_nodes, c->cfg_keys, c->cfg_index, size - 1, n, c->cfg_keys, t->cache_key_prefix_len};
+  HIPCHK(c, hipMemcpy(c->cfg_blob, host.data(), blob, hipMemcpyHostToDevice));
+  uint8_t* B = c->cfg_blob;
+  CfgDev d{};
+  d.nodes = (const CfgNode*)B;
+  d.index = (const unsigned long long*)(B + idx_off);
+  d.keys = B + key_off + t->cache_key_prefix_len;
+  d.mask = size - 1;
+  d.n_nodes = n;
+  d.prefix = B + key_off;
+  d.prefix_len = t->cache_key_prefix_len;
+  d.blob = B;
+  d.blob_words = blob / 4 <= CFG_LDS_WORDS ? (uint32_t)(blob / 4) : 0u;
+  d.idx_word = (uint32_t)(idx_off / 4);
+  d.key_word = (uint32_t)(key_off / 4);
+  c->cfg_dev = d;
   c->cfg_loaded = true;
   return RL_OK;
 }

@@ -29,7 +29,12 @@ struct CfgDev {
   uint32_t n_nodes;
   const uint8_t* prefix;
   uint32_t prefix_len;
+  // the whole config as one blob [nodes | index | prefix ‖ keys]; staged into
+  // LDS by k_match when blob_words != 0 (it fits CFG_LDS_WORDS)
+  const uint8_t* blob;
+  uint32_t blob_words, idx_word, key_word;
 };
+constexpr uint32_t CFG_LDS_WORDS = 12288 / 4;
 
 // Raw request batch on the device (rl_request_batch).
 struct ReqDev {

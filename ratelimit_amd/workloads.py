@@ -145,3 +145,50 @@ def concat_batches(batches):
     res["stem_off"] = np.append(res["stem_off"], base).astype(np.uint32)
     res["req_idx"] = res["req_idx"].astype(np.uint32)
     return res, n, nq, n_rules
+
+
+# C1 as a config file: the rules c1_batch packs by hand (rule ids 0, 1 in load order)
+C1_CONFIG_YAML = """\
+domain: bench
+descriptors:
+  - key: tenant
+    descriptors:
+      - key: tier
+        value: sec
+        rate_limit:
+          unit: second
+          requests_per_unit: 100
+      - key: tier
+        value: min
+        rate_limit:
+          unit: minute
+          requests_per_unit: 3000
+"""
+
+
+def c1_requests(tenants, now, hits=None):
+    """One C1/C2 batch as raw requests (rl_request_batch arrays): request q is
+    domain ``bench`` with descriptors [(tenant, t), (tier, sec)] and
+    [(tenant, t), (tier, min)]; matched through C1_CONFIG_YAML it is c1_batch."""
+    tenants = np.asarray(tenants, np.int64)
+    nq = tenants.size
+    n = 2 * nq
+    sec, L = _fixed_stems(b"tenant_t", tenants, 10, b"_tier_sec_")
+    mn, _ = _fixed_stems(b"tenant_t", tenants, 10, b"_tier_min_")
+    rec = np.empty((n, L), np.uint8)
+    rec[0::2] = sec
+    rec[1::2] = mn
+    h = np.ones(nq, np.uint32) if hits is None else np.asarray(hits, np.uint32)
+    return {
+        "domain_bytes": np.tile(np.frombuffer(b"bench", np.uint8), nq),
+        "domain_off": (np.arange(nq + 1, dtype=np.uint64) * 5).astype(np.uint32),
+        "now": np.full(nq, now, np.int64) if np.ndim(now) == 0 else np.asarray(now, np.int64),
+        "hits": h,
+        "req_idx": np.repeat(np.arange(nq, dtype=np.uint32), 2),
+        "entry_first": (np.arange(n + 1, dtype=np.uint64) * 2).astype(np.uint32),
+        "desc_off": (np.arange(n + 1, dtype=np.uint64) * L).astype(np.uint32),
+        "desc_bytes": rec.reshape(-1),
+        "key_len": np.tile(np.array([6, 4], np.uint16), n),
+        "value_len": np.tile(np.array([11, 3], np.uint16), n),
+        "override_flags": None, "override_rpu": None, "override_unit": None, "override_rule": None,
+    }

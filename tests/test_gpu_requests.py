@@ -205,3 +205,32 @@ def test_gpu_requests_errors():
         assert ok2["limit_remaining"][0] == ok["limit_remaining"][0] - 1
     finally:
         be.close()
+
+
+def test_gpu_request_long_entries_take_global_paths():
+    """Entry bytes beyond a workgroup's LDS staging (16 KB) and stems beyond its
+    assembly buffer (24 KB) take the global-memory paths of k_match /
+    k_match_emit; stems > 80 B also go through the table's overflow arena."""
+    rng = random.Random(99)
+    reqs, nows = [], []
+    vals = ["v" + "x_" * rng.randint(40, 150) + str(i) for i in range(40)]
+    for i in range(1500):
+        descs = [O.Descriptor([("tenant", rng.choice(vals))]),
+                 O.Descriptor([("tenant", rng.choice(vals)), ("tier", "x_y")]),
+                 O.Descriptor([("remote_address", rng.choice(vals))])]
+        reqs.append(O.RateLimitRequest("c4", descs, rng.randint(1, 3)))
+        nows.append(1_700_000_038 + i // 500)
+    svc = GpuRateLimitService(FILES, 0.8, True, "prefix:", table_slots=1 << 16, max_batch=1 << 14,
+                              max_rules=1 << 10, max_stem_bytes=1 << 22)
+    store = StatsStore()
+    osvc = OracleService(RateLimitConfig(FILES, store), O.OracleFixedRateLimitCache(0.8, True, "prefix:"))
+    try:
+        got = svc.should_rate_limit_batch(reqs, nows)
+        for r, now, (gcode, gsts) in zip(reqs, nows, got):
+            ocode, osts, _ = osvc.should_rate_limit(r, now)
+            assert gcode == ocode
+            assert [st_tuple(s) for s in gsts] == [st_tuple(s) for s in osts]
+        want = {k: list(v.as_tuple()) for k, v in store.by_key.items() if any(v.as_tuple())}
+        assert svc.stats == want
+    finally:
+        svc.close()
