@@ -210,7 +210,7 @@ int rl_debug_decide(rl_ctx* ctx, uint32_t n, const uint32_t* before, const uint3
  * received from all sources (concatenated in source-rank order) with their stems
  * (recv_stem, 4-byte aligned, recv_stem_bytes long; src_stem_base = host array
  * of each source's chunk offset in recv_stem). ret[j] = remaining |
- * reset_s << 32 | code << 56 for record j; stats = this owner's deltas
+ * reset_s << 32 | code << 56 | local-cache hit << 62 for record j; stats = this owner's deltas
  * (n_rules * RL_NUM_STATS, overwritten). Errors surface at rl_synchronize.
  *
  * rl_route_scatter (source side, asynchronous): results returned in record
@@ -312,6 +312,33 @@ typedef struct rl_request_result {
  * Synchronous. A descriptor whose override or config unit is not 1..4 fails
  * the batch with RL_E_INVALID (the reference panics in UnitToDivider). */
 int rl_do_limit_requests(rl_ctx* ctx, const rl_request_batch* in, rl_request_result* out);
+
+/* ---- Observability and restart -----------------------
+ * rl_local_cache_info_get: the local over-limit cache gauges of
+ * limiter.localCacheStats (src/limiter/local_cache_stats.go:20-43):
+ * lookup_count = Get calls (one per descriptor with a limit while the local cache
+ * is enabled, fixed_cache_impl.go:57-67), hit_count, miss_count, and
+ * entry_count = keys whose local-cache TTL has not passed at `now`. Counts are
+ * cumulative since rl_create over the single-GPU batch path (rl_do_limit*,
+ * rl_do_limit_requests). freecache's eviction/overwrite gauges have no
+ * counterpart: entries live in the table's window records and are never evicted. */
+typedef struct rl_local_cache_info {
+  uint64_t entry_count;
+  uint64_t lookup_count;
+  uint64_t hit_count;
+  uint64_t miss_count;
+} rl_local_cache_info;
+int rl_local_cache_info_get(rl_ctx* ctx, int64_t now, rl_local_cache_info* info);
+
+/* Table snapshot / restore (Redis RDB-style restart): an exact image of the
+ * counter table, the long-stem arena, the local-cache state and the sweep time
+ * floor. rl_snapshot_size gives the bytes rl_snapshot_save writes into `host`;
+ * rl_snapshot_load accepts an image from a ctx with the same table_slots and an
+ * arena at least as large (RL_E_INVALID otherwise). Both order after every
+ * submitted batch. */
+int rl_snapshot_size(rl_ctx* ctx, uint64_t* bytes);
+int rl_snapshot_save(rl_ctx* ctx, void* host, uint64_t bytes);
+int rl_snapshot_load(rl_ctx* ctx, const void* host, uint64_t bytes);
 
 /* Per-stage device timing (HIP events on the batch stream), for benchmarks.
  * rl_profile(ctx, 1) starts accumulating; rl_profile_read fills ms[0..n) with

@@ -260,6 +260,10 @@ class FakeFreecache:
     def set(self, key: str, ttl: int, now: int) -> None:
         self.data[key] = now + ttl
 
+    def entry_count(self, now: int) -> int:
+        """Entries whose TTL has not passed at ``now`` (the live part of EntryCount)."""
+        return sum(1 for e in self.data.values() if now < e)
+
     def purge(self, now: int) -> None:
         for k in [k for k, e in self.data.items() if e <= now]:
             del self.data[k]

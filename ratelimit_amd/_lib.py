@@ -14,7 +14,8 @@ LIB_PATH = os.environ.get("RL_LIB_PATH") or os.path.join(HERE, "libratelimit_hip
 EXPORTS = ["rl_abi_version", "rl_create", "rl_destroy", "rl_last_error", "rl_do_limit", "rl_do_limit_async",
            "rl_synchronize", "rl_sweep", "rl_restore", "rl_table_info_get", "rl_alloc_host", "rl_free_host",
            "rl_debug_keys", "rl_debug_decide", "rl_profile", "rl_profile_read", "rl_route_pack",
-           "rl_route_do_limit", "rl_route_scatter", "rl_config_load", "rl_do_limit_requests"]
+           "rl_route_do_limit", "rl_route_scatter", "rl_config_load", "rl_do_limit_requests",
+           "rl_local_cache_info_get", "rl_snapshot_size", "rl_snapshot_save", "rl_snapshot_load"]
 
 _lib = None
 
@@ -65,6 +66,10 @@ def lib():
                                    C.c_void_p]
     L.rl_config_load.argtypes = [C.c_void_p, C.POINTER(abi.RlConfigTree)]
     L.rl_do_limit_requests.argtypes = [C.c_void_p, C.POINTER(abi.RlRequestBatch), C.POINTER(abi.RlRequestResult)]
+    L.rl_local_cache_info_get.argtypes = [C.c_void_p, C.c_int64, C.POINTER(abi.RlLocalCacheInfo)]
+    L.rl_snapshot_size.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+    L.rl_snapshot_save.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+    L.rl_snapshot_load.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
     if L.rl_abi_version() != 1:
         raise RuntimeError("libratelimit_hip.so ABI mismatch")
     _lib = L

@@ -76,6 +76,11 @@ class RlRequestResult(C.Structure):
                 ("requests_per_unit", P), ("unit", P), ("stats", P)]
 
 
+class RlLocalCacheInfo(C.Structure):
+    _fields_ = [("entry_count", C.c_uint64), ("lookup_count", C.c_uint64), ("hit_count", C.c_uint64),
+                ("miss_count", C.c_uint64)]
+
+
 RL_MATCH_NONE, RL_MATCH_UNLIMITED, RL_MATCH_LIMIT = 0, 1, 2
 REQUEST_ARRAYS = ("domain_bytes", "domain_off", "now", "hits", "req_idx", "entry_first", "desc_off", "desc_bytes",
                   "key_len", "value_len", "override_flags", "override_rpu", "override_unit", "override_rule")

@@ -975,5 +975,95 @@ int rl_do_limit_requests(rl_ctx* c, const rl_request_batch* in, rl_request_resul
   return collect(c);
 }
 
+// ---- observability and restart ---------------------------------------------
+
+int rl_local_cache_info_get(rl_ctx* c, int64_t now, rl_local_cache_info* info) {
+  if (!c || !info) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  if (now < 0 || now > (int64_t)NOW_MAX) return set_err(c, RL_E_TIME, "gpu: now out of range");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, after_batches(c, c->stream));
+  unsigned long long* ctr = c->s[0].counters;
+  HIPCHK(c, hipMemsetAsync(ctr + 7, 0, 8, c->stream));
+  launch_lc_count(c->slots, c->nslots, (uint32_t)now, ctr + 7, c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->h_counters, ctr, 64, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  info->entry_count = c->h_counters[7];
+  info->lookup_count = c->h_counters[5];
+  info->hit_count = c->h_counters[6];
+  info->miss_count = c->h_counters[5] - c->h_counters[6];
+  return RL_OK;
+}
+
+namespace {
+constexpr uint64_t SNAP_MAGIC = 0x31304150414e534cull;  // "LSNAPA01"
+struct SnapHeader {
+  uint64_t magic, nslots, arena_used16, reserved0;
+  int64_t time_floor;
+  uint64_t reserved[3];
+};
+static_assert(sizeof(SnapHeader) == 64, "snapshot header");
+
+int snap_state(rl_ctx* c, uint64_t* arena_used16, int64_t* floor) {
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, after_batches(c, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 64, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(floor, c->s[0].time_floor, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *arena_used16 = std::min<uint64_t>(c->h_counters[4], c->arena_cap16);
+  return RL_OK;
+}
+}  // namespace
+
+int rl_snapshot_size(rl_ctx* c, uint64_t* bytes) {
+  if (!c || !bytes) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  uint64_t au = 0;
+  int64_t fl = 0;
+  int rc = snap_state(c, &au, &fl);
+  if (rc) return rc;
+  *bytes = sizeof(SnapHeader) + c->nslots * sizeof(Slot) + au * 16;
+  return RL_OK;
+}
+
+int rl_snapshot_save(rl_ctx* c, void* host, uint64_t bytes) {
+  if (!c || !host) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  SnapHeader h{};
+  int rc = snap_state(c, &h.arena_used16, &h.time_floor);
+  if (rc) return rc;
+  h.magic = SNAP_MAGIC;
+  h.nslots = c->nslots;
+  const uint64_t need = sizeof(SnapHeader) + c->nslots * sizeof(Slot) + h.arena_used16 * 16;
+  if (bytes < need) return set_err(c, RL_E_CAPACITY, "gpu: snapshot buffer smaller than rl_snapshot_size");
+  uint8_t* p = (uint8_t*)host;
+  memcpy(p, &h, sizeof h);
+  HIPCHK(c, hipMemcpy(p + sizeof h, c->slots, c->nslots * sizeof(Slot), hipMemcpyDeviceToHost));
+  if (h.arena_used16)
+    HIPCHK(c, hipMemcpy(p + sizeof h + c->nslots * sizeof(Slot), c->arena, h.arena_used16 * 16, hipMemcpyDeviceToHost));
+  return RL_OK;
+}
+
+int rl_snapshot_load(rl_ctx* c, const void* host, uint64_t bytes) {
+  if (!c || !host) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  SnapHeader h;
+  if (bytes < sizeof h) return set_err(c, RL_E_INVALID, "gpu: snapshot too short");
+  memcpy(&h, host, sizeof h);
+  if (h.magic != SNAP_MAGIC) return set_err(c, RL_E_INVALID, "gpu: not a table snapshot");
+  if (h.nslots != c->nslots) return set_err(c, RL_E_INVALID, "gpu: snapshot table_slots differ from this ctx");
+  if (h.arena_used16 > c->arena_cap16) return set_err(c, RL_E_INVALID, "gpu: snapshot arena larger than this ctx's");
+  if (bytes < sizeof h + h.nslots * sizeof(Slot) + h.arena_used16 * 16)
+    return set_err(c, RL_E_INVALID, "gpu: snapshot truncated");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, after_batches(c, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint8_t* p = (const uint8_t*)host;
+  HIPCHK(c, hipMemcpy(c->slots, p + sizeof h, c->nslots * sizeof(Slot), hipMemcpyHostToDevice));
+  if (h.arena_used16)
+    HIPCHK(c, hipMemcpy(c->arena, p + sizeof h + c->nslots * sizeof(Slot), h.arena_used16 * 16, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->s[0].counters + 4, &h.arena_used16, 8, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->s[0].time_floor, &h.time_floor, 8, hipMemcpyHostToDevice));
+  return RL_OK;
+}
+
 }  // extern "C"
+
 

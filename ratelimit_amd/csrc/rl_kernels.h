@@ -198,6 +198,7 @@ void launch_route_unpack(const Wire* rec, uint32_t n, const unsigned long long* 
 void launch_route_scatter(const uint32_t* perm, const unsigned long long* ret, uint32_t n, const OutDev& o,
                           hipStream_t st);
 void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st);
+void launch_lc_count(const Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* out, hipStream_t st);
 void launch_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out, hipStream_t st);
 void launch_debug_keys(const BatchDev& b, uint8_t* out, uint32_t* klen, hipStream_t st);
 void launch_debug_decide(uint32_t n, const uint32_t* before, const uint32_t* after, const uint8_t* lc_hit,

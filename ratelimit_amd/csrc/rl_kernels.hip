@@ -689,12 +689,13 @@ __device__ inline Elem load_elem(const Rec& r, uint32_t e, bool restore) {
   return x;
 }
 
-// One 8-B store per descriptor: remaining | reset << 32 | code << 56 (k_finish).
+// One 8-B store per descriptor: remaining | reset << 32 | code << 56, bit 62 =
+// the local-cache Get hit (k_finish counts them for the hitCount gauge).
 __device__ __attribute__((always_inline)) inline void emit(unsigned long long* res, LaneStats& L, StatAcc& acc,
-                                                           const Elem& x, const Decision& r) {
+                                                           const Elem& x, const Decision& r, bool lc_get) {
   const uint32_t reset = x.d - x.now % x.d;  // utils.CalculateReset
   res[x.e] = (unsigned long long)r.remaining | ((unsigned long long)reset << 32) |
-             ((unsigned long long)r.code << 56);
+             ((unsigned long long)r.code << 56) | ((unsigned long long)lc_get << 62);
   const uint32_t d[RL_NUM_STATS] = {x.h, r.d_over, r.d_near, r.d_lc, r.d_within, r.d_shadow};
   L.add(acc, x.rule, d);
 }
@@ -798,7 +799,7 @@ __device__ __attribute__((always_inline)) inline void simple_step(const Params& 
     S.pend_w = x.w;
     S.pend_e = x.now + x.d;
   }
-  emit(res, L, acc, x, r);
+  emit(res, L, acc, x, r, lc_hit);
 }
 
 // ---- general: every unit slot of the stem, Redis keys shared across units
@@ -883,7 +884,7 @@ __device__ inline void general_step(const Params& P, unsigned long long* res, La
     G.pend_w[j] = x.w;
     G.pend_e[j] = x.now + x.d;
   }
-  emit(res, L, acc, x, r);
+  emit(res, L, acc, x, r, lc_hit);
 }
 
 // Replay elements [p, end) (those of stem k when repid is given) through the
@@ -2495,7 +2496,7 @@ __global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules,
       const bool masked = F || x.req > req_f;  // local-cache hit
       const uint32_t after = masked ? 0u : st.y + segsum[q];
       const Decision d = decide(after - x.h, after, masked && !x.shadow, x.h, x.thr, P.ratio, x.shadow, P.lc_en);
-      emit(res, L, acc, x, d);
+      emit(res, L, acc, x, d, masked);
       if (!masked) {
         const uint32_t nq = q + 1;
         const bool last = nq == run_end[r] || rec_s[nq].req > req_f;
@@ -2652,7 +2653,7 @@ __global__ __launch_bounds__(256) void k_b_begin(const uint32_t* __restrict__ er
 // when the batch failed, so nothing leaks into the next one).
 __global__ __launch_bounds__(256) void k_finish(const unsigned long long* __restrict__ res, uint32_t n, OutDev o,
                                                 unsigned long long* __restrict__ stripes, uint32_t n_fold,
-                                                const uint32_t* err) {
+                                                const uint32_t* err, unsigned long long* lc_ctr) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   const bool ok = *err == 0;
   const uint32_t m = n_fold * RL_NUM_STATS;
@@ -2664,11 +2665,32 @@ __global__ __launch_bounds__(256) void k_finish(const unsigned long long* __rest
     }
     if (ok) o.stats[i] += s;
   }
-  if (!ok || i >= n) return;
-  const unsigned long long v = res[i];
-  o.code[i] = (uint8_t)(v >> 56);
-  o.rem[i] = (uint32_t)v;
-  o.reset[i] = (uint32_t)(v >> 32) & 0xFFFFFFu;
+  bool hit = false;
+  if (ok && i < n) {
+    const unsigned long long v = res[i];
+    o.code[i] = (uint8_t)((v >> 56) & 0x3Fu);
+    o.rem[i] = (uint32_t)v;
+    o.reset[i] = (uint32_t)(v >> 32) & 0xFFFFFFu;
+    hit = (v >> 62) & 1u;
+  }
+  if (lc_ctr && ok) {  // freecache LookupCount / HitCount (local_cache_stats.go:36-43)
+    const unsigned long long w = __ballot(hit);
+    if ((threadIdx.x & 63u) == 0 && w) atomicAdd(&lc_ctr[1], (unsigned long long)__popcll(w));
+    if (i == 0) atomicAdd(&lc_ctr[0], (unsigned long long)n);
+  }
+}
+
+// Keys in the local over-limit cache at `now` (freecache EntryCount of live
+// entries): window records whose local-cache TTL has not passed.
+__global__ __launch_bounds__(256) void k_lc_count(const Slot* slots, uint64_t nslots, uint32_t now,
+                                                  unsigned long long* out) {
+  uint32_t live = 0;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * 256) {
+    const Slot& s = slots[i];
+    if (s.tag < 2) continue;
+    live += (s.cur.ws != WS_INVALID && now < s.cur.lc) + (s.prev.ws != WS_INVALID && now < s.prev.lc);
+  }
+  if (live) atomicAdd(out, (unsigned long long)live);
 }
 
 // ===========================================================================
@@ -2825,7 +2847,7 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
                                        s.run_start, s.run_end, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb);
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;
       const uint32_t gf = cdiv(nf * RL_NUM_STATS > b.n ? nf * RL_NUM_STATS : b.n, 256);
-      k_finish<<<gf, 256, 0, st>>>(s.res, b.n, o, s.stripes, nf, s.errb);
+      k_finish<<<gf, 256, 0, st>>>(s.res, b.n, o, s.stripes, nf, s.errb, P.lc_en ? s.counters + 5 : nullptr);
     }
   } else if (ev) {
     (void)hipEventRecord(ev[3], st);
@@ -2854,6 +2876,10 @@ void launch_run_sums(const uint32_t* skeys, const uint32_t* w, uint32_t n, const
 
 void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st) {
   k_sweep<<<2048, 256, 0, st>>>(slots, nslots, now, evicted);
+}
+
+void launch_lc_count(const Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* out, hipStream_t st) {
+  k_lc_count<<<2048, 256, 0, st>>>(slots, nslots, now, out);
 }
 
 void launch_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out, hipStream_t st) {

@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void k_route_scatter(const uint32_t* __restric
   if (j >= n) return;
   const uint32_t e = perm[j];
   const unsigned long long v = ret[j];
-  o.code[e] = (uint8_t)(v >> 56);
+  o.code[e] = (uint8_t)((v >> 56) & 0x3Fu);
   o.rem[e] = (uint32_t)v;
   o.reset[e] = (uint32_t)(v >> 32) & 0xFFFFFFu;
 }

@@ -175,6 +175,24 @@ class Backend:
         check(self.ctx, lib().rl_table_info_get(self.ctx, C.byref(info)))
         return {f: getattr(info, f) for f, _ in abi.RlTableInfo._fields_}
 
+    def local_cache_info(self, now: int) -> dict:
+        """localCacheStats gauges (src/limiter/local_cache_stats.go:20-43)."""
+        info = abi.RlLocalCacheInfo()
+        check(self.ctx, lib().rl_local_cache_info_get(self.ctx, now, C.byref(info)))
+        return {f: getattr(info, f) for f, _ in abi.RlLocalCacheInfo._fields_}
+
+    def snapshot(self) -> np.ndarray:
+        """Exact table image (counters, local cache, arena, time floor) as host bytes."""
+        nb = C.c_uint64(0)
+        check(self.ctx, lib().rl_snapshot_size(self.ctx, C.byref(nb)))
+        buf = np.empty(nb.value, np.uint8)
+        check(self.ctx, lib().rl_snapshot_save(self.ctx, abi.ptr(buf), nb.value))
+        return buf
+
+    def load_snapshot(self, buf: np.ndarray) -> None:
+        buf = np.ascontiguousarray(buf, np.uint8)
+        check(self.ctx, lib().rl_snapshot_load(self.ctx, abi.ptr(buf), buf.size))
+
     def debug_keys(self, pb: PackedBatch) -> List[str]:
         cap = int(pb.arrays["stem_off"][-1]) + 24 * pb.n + 1
         buf = np.zeros(cap, np.uint8)

@@ -111,6 +111,7 @@ LAYOUT_C = r'''
 int main(void) {
   printf("rl_config_node %zu\nrl_config_tree %zu\nrl_request_batch %zu\nrl_request_result %zu\n",
          sizeof(rl_config_node), sizeof(rl_config_tree), sizeof(rl_request_batch), sizeof(rl_request_result));
+  printf("rl_local_cache_info %zu\n", sizeof(rl_local_cache_info));
   P(rl_config_node, rule_id) P(rl_config_node, unit) P(rl_config_node, shadow_mode)
   P(rl_config_tree, nodes) P(rl_config_tree, key_bytes_len) P(rl_config_tree, cache_key_prefix)
   P(rl_request_batch, domain_bytes) P(rl_request_batch, override_rule)
@@ -127,7 +128,8 @@ def test_request_struct_layouts_match_c_compiler(tmp_path):
     subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
     got = dict(l.split() for l in subprocess.check_output([str(exe)]).decode().splitlines())
     py = {"rl_config_node": C.sizeof(abi.RlConfigNode), "rl_config_tree": C.sizeof(abi.RlConfigTree),
-          "rl_request_batch": C.sizeof(abi.RlRequestBatch), "rl_request_result": C.sizeof(abi.RlRequestResult)}
+          "rl_request_batch": C.sizeof(abi.RlRequestBatch), "rl_request_result": C.sizeof(abi.RlRequestResult),
+          "rl_local_cache_info": C.sizeof(abi.RlLocalCacheInfo)}
     for k, v in py.items():
         assert int(got[k]) == v, k
     assert abi.CONFIG_NODE_DTYPE.itemsize == C.sizeof(abi.RlConfigNode)
