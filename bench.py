@@ -17,8 +17,8 @@ Besides the contract line, rank 0 reports:
   roofline      dominant kernel (k_runs) achieved GB/s on the canonical
                 B_alg = key_len + 16 + 12 + 64 B per decision,
                 from HIP events on the library's stream;
-  cpu_baseline  the C restatement oracle (sequential, 1 core) on a bounded
-                sample of the same C1 stream.
+  cpu_baseline  the C restatement oracle, key-sharded over the host's cores
+                (and on 1 core), on a bounded sample of the same stream.
 """
 import argparse
 import json
@@ -254,29 +254,42 @@ def main():
 
 
 def cpu_baseline(args, W):
-    """The C restatement oracle (sequential, 1 thread) on a bounded sample of the same stream."""
-    from oracle.c_oracle import COracle
-    co = COracle(0.8, False, False)
-    rng = np.random.default_rng(0xC1 + 1)
-    sampler = W.ZipfSampler(args.tenants, 1.1) if args.config == "c2" else None
-    done = 0
-    spent = 0.0
-    k = 0
-    while spent < args.cpu_seconds and k < 40:
-        if sampler is None:
-            a, n, nq, nr = W.c1_batch(rng.integers(0, args.tenants, args.requests), W.NOW0 + k)
-        else:
-            a, n, nq, nr = W.c1_batch(sampler.sample(rng, args.requests), W.NOW0 + k,
-                                      rng.integers(1, 9, args.requests).astype(np.uint32))
-        t = time.perf_counter()
-        co.do_limit(a, n, nq, nr)
-        spent += time.perf_counter() - t
-        done += n
-        k += 1
-    co.close()
-    return {"value": done / spent, "unit": "decisions/s", "cores": 1, "kind": "port",
-            "sample": "%d consecutive %s batches x %d descriptors (%.1f s of CPU work), C restatement oracle, "
-                      "sequential" % (k, args.config.upper(), 2 * args.requests, spent)}
+    """The C restatement oracle on a bounded sample of the same stream, sharded by
+    stem hash over the host's cores (SURVEY.md §8d CPU baseline (i): independent
+    in-process stores, one thread each; bit-equal to the sequential replay,
+    tests/test_c_oracle.py), plus the single-thread rate on a shorter sample."""
+    from oracle.c_oracle import COracle, COracleMT
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    threads = max(1, min(16, ncpu, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+
+    def run(co, seconds, seed):
+        rng = np.random.default_rng(seed)
+        sampler = W.ZipfSampler(args.tenants, 1.1) if args.config == "c2" else None
+        done, spent, k = 0, 0.0, 0
+        while spent < seconds and k < 40:
+            if sampler is None:
+                a, n, nq, nr = W.c1_batch(rng.integers(0, args.tenants, args.requests), W.NOW0 + k)
+            else:
+                a, n, nq, nr = W.c1_batch(sampler.sample(rng, args.requests), W.NOW0 + k,
+                                          rng.integers(1, 9, args.requests).astype(np.uint32))
+            t = time.perf_counter()
+            co.do_limit(a, n, nq, nr)
+            spent += time.perf_counter() - t
+            done += n
+            k += 1
+        co.close()
+        return done / spent, k, spent
+
+    v1, k1, s1 = run(COracle(0.8, False, False), args.cpu_seconds / 3, 0xC1 + 1)
+    vt, kt, st = run(COracleMT(0.8, False, False, threads), args.cpu_seconds, 0xC1 + 2)
+    return {"value": vt, "unit": "decisions/s", "cores": threads, "kind": "port",
+            "value_1_core": v1,
+            "sample": "%d consecutive %s batches x %d descriptors (%.1f s wall), C restatement oracle sharded by "
+                      "stem hash over %d threads (one store each); 1 thread: %d batches (%.1f s)"
+                      % (kt, args.config.upper(), 2 * args.requests, st, threads, k1, s1)}
 
 
 if __name__ == "__main__":

@@ -29,6 +29,10 @@ def lib():
         L.rlo_create.restype = C.c_void_p
         L.rlo_create.argtypes = [C.c_float, C.c_int, C.c_int]
         L.rlo_destroy.argtypes = [C.c_void_p]
+        L.rlo_mt_create.restype = C.c_void_p
+        L.rlo_mt_create.argtypes = [C.c_float, C.c_int, C.c_int, C.c_int]
+        L.rlo_mt_destroy.argtypes = [C.c_void_p]
+        L.rlo_mt_do_limit.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.POINTER(abi.RlResult)]
         L.rlo_do_limit.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.POINTER(abi.RlResult)]
         L.rlo_restore.argtypes = [C.c_void_p, C.POINTER(abi.RlRestoreBatch)]
         L.rlo_keys.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.c_void_p, C.c_void_p, C.c_uint32]
@@ -94,3 +98,30 @@ class COracle:
 
 def near_threshold(limit, ratio):
     return lib().rlo_near_threshold(limit, ratio)
+
+
+class COracleMT:
+    """The C restatement sharded by stem hash over `threads` independent stores,
+    one thread per shard (the multi-core CPU baseline; equal to COracle)."""
+
+    def __init__(self, near_limit_ratio=0.8, local_cache=False, per_second=False, threads=1):
+        self.threads = threads
+        self.h = lib().rlo_mt_create(near_limit_ratio, int(local_cache), int(per_second), threads)
+
+    def close(self):
+        if self.h:
+            lib().rlo_mt_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def do_limit(self, arrays, n, n_requests, n_rules):
+        b = abi.make_batch_struct(arrays, n, n_requests, n_rules)
+        out = {"code": np.zeros(max(n, 1), np.uint8), "limit_remaining": np.zeros(max(n, 1), np.uint32),
+               "reset_s": np.zeros(max(n, 1), np.uint32),
+               "stats": np.zeros(max(n_rules, 1) * abi.RL_NUM_STATS, np.uint64)}
+        r = abi.make_result_struct(out)
+        rc = lib().rlo_mt_do_limit(self.h, C.byref(b), C.byref(r))
+        if rc:
+            raise RuntimeError("oracle rlo_mt_do_limit: %s" % abi.STATUS_NAMES.get(rc, rc))
+        return {k: v[:n] if k != "stats" else v[:n_rules * abi.RL_NUM_STATS] for k, v in out.items()}

@@ -19,6 +19,7 @@
  * Pinned against tests/golden (see tests/test_c_oracle.py).
  */
 #include <math.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -208,52 +209,58 @@ static dec_t decide(uint32_t before, uint32_t after, int lc_hit, uint32_t h, uin
   return r;
 }
 
-static uint64_t* stat_row(const rl_result* o, uint32_t rule) { return o->stats + (uint64_t)rule * RL_NUM_STATS; }
-
-int rlo_do_limit(rlo_ctx* c, const rl_batch* b, rl_result* o) {
-  if (b->n_rules) memset(o->stats, 0, sizeof(uint64_t) * RL_NUM_STATS * b->n_rules);
+/* DoLimit over the descriptors idx[0..m) of batch b (all of b when idx is
+ * NULL), in that order; results at their batch positions, stats deltas added
+ * into `stats` (n_rules x RL_NUM_STATS). Requests are the runs of equal req_idx. */
+static int do_limit_idx(rlo_ctx* c, const rl_batch* b, const uint32_t* idx, uint32_t m, rl_result* o,
+                        uint64_t* stats) {
+#define AT(j) (idx ? idx[j] : (j))
   uint32_t i = 0;
-  uint32_t* after = (uint32_t*)malloc(sizeof(uint32_t) * (b->n ? b->n : 1));
-  uint8_t* lcf = (uint8_t*)malloc(b->n ? b->n : 1);
-  while (i < b->n) {
-    uint32_t q = b->req_idx[i], a = i, e = i;
-    while (e < b->n && b->req_idx[e] == q) e++;
+  uint32_t* after = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1));
+  uint8_t* lcf = (uint8_t*)malloc(m ? m : 1);
+  while (i < m) {
+    uint32_t q = b->req_idx[AT(i)], a = i, e = i;
+    while (e < m && b->req_idx[AT(e)] == q) e++;
     int64_t now = b->now[q];
     /* GenerateCacheKeys: TotalHits (base_limiter.go:55-57) */
-    for (uint32_t k = a; k < e; k++) {
+    for (uint32_t j = a; j < e; j++) {
+      uint32_t k = AT(j);
       if (!unit_to_divider(b->unit[k]) || b->rule_id[k] >= b->n_rules) { free(after); free(lcf); return RL_E_INVALID; }
       uint32_t h = b->hits[k] > 1 ? b->hits[k] : 1;
-      stat_row(o, b->rule_id[k])[RL_STAT_TOTAL_HITS] += h;
+      stats[(uint64_t)b->rule_id[k] * RL_NUM_STATS + RL_STAT_TOTAL_HITS] += h;
     }
     /* local cache check for every key first (fixed_cache_impl.go:51-67) */
-    for (uint32_t k = a; k < e; k++) {
-      lcf[k] = 0; after[k] = 0;
+    for (uint32_t j = a; j < e; j++) {
+      uint32_t k = AT(j);
+      lcf[j] = 0; after[j] = 0;
       if (!c->lc_enabled) continue;
       uint32_t kl; const char* key = build_key(c, b, k, now, &kl);
       ent_t* le = smap_get(&c->lc, key, kl);
-      if (le && now < le->expire) lcf[k] = (b->flags[k] & RL_FLAG_SHADOW) ? 2 : 1; /* 2: skip, not marked */
+      if (le && now < le->expire) lcf[j] = (b->flags[k] & RL_FLAG_SHADOW) ? 2 : 1; /* 2: skip, not marked */
     }
     /* PipeDo: main pipeline in order, then the per-second pipeline (:90-95) */
     for (int pass = 0; pass < 2; pass++) {
-      for (uint32_t k = a; k < e; k++) {
-        if (lcf[k]) continue;
+      for (uint32_t j = a; j < e; j++) {
+        uint32_t k = AT(j);
+        if (lcf[j]) continue;
         int ps = c->per_second && b->unit[k] == RL_UNIT_SECOND;
         if (ps != pass) continue;
-        smap_t* m = ps ? &c->redis_ps : &c->redis;
+        smap_t* mp = ps ? &c->redis_ps : &c->redis;
         uint32_t kl; const char* key = build_key(c, b, k, now, &kl);
         uint32_t h = b->hits[k] > 1 ? b->hits[k] : 1;
-        int created; ent_t* re = smap_upsert(m, key, kl, now, &created);
-        if (!live(m, re, now)) { re->count = 0; re->expire = -1; }
+        int created; ent_t* re = smap_upsert(mp, key, kl, now, &created);
+        if (!live(mp, re, now)) { re->count = 0; re->expire = -1; }
         re->count += h;                                   /* INCRBY */
         re->expire = now + unit_to_divider(b->unit[k]);   /* EXPIRE (jitter draw 0) */
-        after[k] = re->count;
+        after[j] = re->count;
       }
     }
     /* statuses (fixed_cache_impl.go:100-110) */
-    for (uint32_t k = a; k < e; k++) {
+    for (uint32_t j = a; j < e; j++) {
+      uint32_t k = AT(j);
       uint32_t h = b->hits[k] > 1 ? b->hits[k] : 1;
       int64_t d = unit_to_divider(b->unit[k]);
-      dec_t r = decide(after[k] - h, after[k], lcf[k] == 1, h, b->limit[k], c->ratio,
+      dec_t r = decide(after[j] - h, after[j], lcf[j] == 1, h, b->limit[k], c->ratio,
                        (b->flags[k] & RL_FLAG_SHADOW) != 0, c->lc_enabled);
       if (r.set_lc) { /* localCache.Set(key, ttl = divider) */
         uint32_t kl; const char* key = build_key(c, b, k, now, &kl);
@@ -262,7 +269,7 @@ int rlo_do_limit(rlo_ctx* c, const rl_batch* b, rl_result* o) {
       }
       o->code[k] = r.code; o->limit_remaining[k] = r.rem;
       o->reset_s[k] = (uint32_t)(d - now % d); /* CalculateReset */
-      uint64_t* s = stat_row(o, b->rule_id[k]);
+      uint64_t* s = stats + (uint64_t)b->rule_id[k] * RL_NUM_STATS;
       s[RL_STAT_OVER_LIMIT] += r.over; s[RL_STAT_NEAR_LIMIT] += r.near;
       s[RL_STAT_OVER_LIMIT_WITH_LOCAL_CACHE] += r.lcs; s[RL_STAT_WITHIN_LIMIT] += r.within;
       s[RL_STAT_SHADOW_MODE] += r.shadow;
@@ -271,6 +278,90 @@ int rlo_do_limit(rlo_ctx* c, const rl_batch* b, rl_result* o) {
   }
   free(after); free(lcf);
   return RL_OK;
+#undef AT
+}
+
+int rlo_do_limit(rlo_ctx* c, const rl_batch* b, rl_result* o) {
+  if (b->n_rules) memset(o->stats, 0, sizeof(uint64_t) * RL_NUM_STATS * b->n_rules);
+  return do_limit_idx(c, b, NULL, b->n, o, o->stats);
+}
+
+/* ------------------------------------------------- key-sharded, multi-threaded
+ * The CPU baseline of SURVEY.md §8d (i): T independent stores ("Redis" + local
+ * cache), descriptors routed by a hash of their stem (so a key, and both units
+ * of a stem, always land in one shard), each shard replaying its descriptors in
+ * arrival order on its own thread. Keys never interact, so the results equal
+ * the sequential replay's bit for bit (tests/test_c_oracle.py checks that). */
+typedef struct rlo_mt {
+  int T;
+  rlo_ctx** sh;
+} rlo_mt;
+
+rlo_mt* rlo_mt_create(float near_limit_ratio, int local_cache, int per_second, int threads) {
+  if (threads < 1) threads = 1;
+  rlo_mt* m = (rlo_mt*)calloc(1, sizeof(rlo_mt));
+  m->T = threads;
+  m->sh = (rlo_ctx**)calloc(threads, sizeof(rlo_ctx*));
+  for (int t = 0; t < threads; t++) m->sh[t] = rlo_create(near_limit_ratio, local_cache, per_second);
+  return m;
+}
+
+void rlo_mt_destroy(rlo_mt* m) {
+  if (!m) return;
+  for (int t = 0; t < m->T; t++) rlo_destroy(m->sh[t]);
+  free(m->sh); free(m);
+}
+
+typedef struct {
+  rlo_mt* m; const rl_batch* b; rl_result* o;
+  uint16_t* shard; int t, phase, rc;
+  uint64_t* stats;
+} mt_job;
+
+static void* mt_worker(void* arg) {
+  mt_job* j = (mt_job*)arg;
+  const rl_batch* b = j->b;
+  const int T = j->m->T;
+  if (j->phase == 0) { /* shard of every descriptor in this thread's slice */
+    uint32_t a = (uint32_t)((uint64_t)b->n * j->t / T), e = (uint32_t)((uint64_t)b->n * (j->t + 1) / T);
+    for (uint32_t i = a; i < e; i++) {
+      uint32_t s0 = b->stem_off[i];
+      j->shard[i] = (uint16_t)(hash_bytes((const char*)b->stem_bytes + s0, b->stem_off[i + 1] - s0) % (uint64_t)T);
+    }
+    return NULL;
+  }
+  uint32_t cnt = 0;
+  for (uint32_t i = 0; i < b->n; i++) cnt += j->shard[i] == j->t;
+  uint32_t* idx = (uint32_t*)malloc(sizeof(uint32_t) * (cnt ? cnt : 1));
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < b->n; i++) if (j->shard[i] == j->t) idx[k++] = i;
+  j->stats = (uint64_t*)calloc((size_t)(b->n_rules ? b->n_rules : 1) * RL_NUM_STATS, sizeof(uint64_t));
+  j->rc = do_limit_idx(j->m->sh[j->t], b, idx, cnt, j->o, j->stats);
+  free(idx);
+  return NULL;
+}
+
+int rlo_mt_do_limit(rlo_mt* m, const rl_batch* b, rl_result* o) {
+  const int T = m->T;
+  uint16_t* shard = (uint16_t*)malloc(sizeof(uint16_t) * (b->n ? b->n : 1));
+  mt_job* jobs = (mt_job*)calloc(T, sizeof(mt_job));
+  pthread_t* th = (pthread_t*)calloc(T, sizeof(pthread_t));
+  int rc = RL_OK;
+  for (int phase = 0; phase < 2; phase++) {
+    for (int t = 0; t < T; t++) {
+      jobs[t] = (mt_job){m, b, o, shard, t, phase, RL_OK, jobs[t].stats};
+      pthread_create(&th[t], NULL, mt_worker, &jobs[t]);
+    }
+    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+  }
+  if (b->n_rules) memset(o->stats, 0, sizeof(uint64_t) * RL_NUM_STATS * b->n_rules);
+  for (int t = 0; t < T; t++) {
+    if (jobs[t].rc) rc = jobs[t].rc;
+    for (uint64_t i = 0; i < (uint64_t)b->n_rules * RL_NUM_STATS; i++) o->stats[i] += jobs[t].stats[i];
+    free(jobs[t].stats);
+  }
+  free(th); free(jobs); free(shard);
+  return rc;
 }
 
 int rlo_restore(rlo_ctx* c, const rl_restore_batch* r) {

@@ -129,3 +129,31 @@ def test_c4_stream_c_oracle_matches_python_oracle(ratio, local_cache, prefix):
     for key, v in py_stats.items():
         assert totals.get(key, (0,) * 6) == v, key
     co.close()
+
+
+@pytest.mark.parametrize("threads", [2, 7])
+@pytest.mark.parametrize("local_cache,per_second,prefix", [(False, False, ""), (True, False, "p:"),
+                                                           (True, True, "")])
+def test_sharded_multithreaded_oracle_equals_sequential(threads, local_cache, per_second, prefix):
+    """The multi-core CPU baseline (key-sharded stores, one thread each) replays
+    exactly what the sequential restatement does: random structured streams
+    (shared keys across units, shadow, per-second split) and a Zipf C2 stream."""
+    from ratelimit_amd import workloads as W
+    seq = c_oracle.COracle(0.8, local_cache, per_second)
+    mt = c_oracle.COracleMT(0.8, local_cache, per_second, threads)
+    interner = RuleInterner()
+    calls = streams.random_stream(threads, n_calls=400, zipf=True)
+    for i in range(0, len(calls), 50):
+        pb = pack_calls(calls[i:i + 50], prefix, interner)
+        a = seq.do_limit(pb.arrays, pb.n, pb.n_requests, pb.n_rules)
+        b = mt.do_limit(pb.arrays, pb.n, pb.n_requests, pb.n_rules)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), k
+    z = W.ZipfSampler(5000, 1.1)
+    for arr, n, nq, nr in W.c2_stream(n_tenants=5000, requests_per_batch=20000, batches=3, sampler=z):
+        a = seq.do_limit(arr, n, nq, nr)
+        b = mt.do_limit(arr, n, nq, nr)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), k
+    seq.close()
+    mt.close()
