@@ -313,6 +313,26 @@ typedef struct rl_request_result {
  * the batch with RL_E_INVALID (the reference panics in UnitToDivider). */
 int rl_do_limit_requests(rl_ctx* ctx, const rl_request_batch* in, rl_request_result* out);
 
+/* ---- Host packer -------------------------------------
+ * Serialized envoy.service.ratelimit.v3.RateLimitRequest messages (the gRPC
+ * payloads: msgs[msg_off[i], msg_off[i+1]), n + 1 offsets) with each request's
+ * UnixNow() -> an rl_request_batch for rl_do_limit_requests, without building
+ * per-descriptor objects. Replaces the per-descriptor Go work of
+ * constructLimitsToCheck's caller side (src/service/ratelimit.go:104-143) and the
+ * proto unmarshalling of the request. Override stats keys (descriptorKey,
+ * src/config/config_impl.go:300-312) are interned to rule ids from
+ * first_override_rule up (config rules take the ids below it);
+ * rl_packer_rule_key names them. The batch's arrays are owned by the packer and
+ * valid until its next rl_packer_pack. Host code; no GPU needed. */
+typedef struct rl_packer rl_packer;
+rl_packer* rl_packer_create(uint32_t first_override_rule);
+void rl_packer_destroy(rl_packer* packer);
+int rl_packer_pack(rl_packer* packer, const uint8_t* msgs, const uint64_t* msg_off, uint32_t n,
+                   const int64_t* now, rl_request_batch* out);
+uint32_t rl_packer_rules(const rl_packer* packer);  /* first_override_rule + interned override keys */
+const char* rl_packer_rule_key(const rl_packer* packer, uint32_t rule_id);  /* NULL below first_override_rule */
+const char* rl_packer_last_error(const rl_packer* packer);
+
 /* ---- Observability and restart -----------------------
  * rl_local_cache_info_get: the local over-limit cache gauges of
  * limiter.localCacheStats (src/limiter/local_cache_stats.go:20-43):

@@ -15,7 +15,9 @@ EXPORTS = ["rl_abi_version", "rl_create", "rl_destroy", "rl_last_error", "rl_do_
            "rl_synchronize", "rl_sweep", "rl_restore", "rl_table_info_get", "rl_alloc_host", "rl_free_host",
            "rl_debug_keys", "rl_debug_decide", "rl_profile", "rl_profile_read", "rl_route_pack",
            "rl_route_do_limit", "rl_route_scatter", "rl_config_load", "rl_do_limit_requests",
-           "rl_local_cache_info_get", "rl_snapshot_size", "rl_snapshot_save", "rl_snapshot_load"]
+           "rl_local_cache_info_get", "rl_snapshot_size", "rl_snapshot_save", "rl_snapshot_load",
+           "rl_packer_create", "rl_packer_destroy", "rl_packer_pack", "rl_packer_rules", "rl_packer_rule_key",
+           "rl_packer_last_error"]
 
 _lib = None
 
@@ -70,6 +72,17 @@ def lib():
     L.rl_snapshot_size.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     L.rl_snapshot_save.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
     L.rl_snapshot_load.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+    L.rl_packer_create.restype = C.c_void_p
+    L.rl_packer_create.argtypes = [C.c_uint32]
+    L.rl_packer_destroy.argtypes = [C.c_void_p]
+    L.rl_packer_pack.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                 C.POINTER(abi.RlRequestBatch)]
+    L.rl_packer_rules.restype = C.c_uint32
+    L.rl_packer_rules.argtypes = [C.c_void_p]
+    L.rl_packer_rule_key.restype = C.c_char_p
+    L.rl_packer_rule_key.argtypes = [C.c_void_p, C.c_uint32]
+    L.rl_packer_last_error.restype = C.c_char_p
+    L.rl_packer_last_error.argtypes = [C.c_void_p]
     if L.rl_abi_version() != 1:
         raise RuntimeError("libratelimit_hip.so ABI mismatch")
     _lib = L

@@ -193,3 +193,66 @@ def pack_requests(requests, nows, interner: RuleInterner) -> Dict[str, np.ndarra
     else:
         a.update(override_flags=None, override_rpu=None, override_unit=None, override_rule=None)
     return a
+
+
+class RequestPacker:
+    """rl_packer: serialized RateLimitRequest messages -> rl_request_batch
+    (native, no per-descriptor Python objects). Override stats keys get rule
+    ids from ``first_override_rule`` up (config rules take the ids below)."""
+
+    def __init__(self, first_override_rule: int):
+        import ctypes as C
+        from ._lib import lib
+        self._C, self._lib = C, lib()
+        self.h = self._lib.rl_packer_create(first_override_rule)
+        self._keep = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._lib.rl_packer_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def pack(self, messages, nows) -> "abi.RlRequestBatch":
+        """-> an RlRequestBatch over packer-owned arrays (valid until the next pack)."""
+        from ._lib import RedisError
+        C = self._C
+        buf = np.frombuffer(b"".join(messages) or b"\0", np.uint8)
+        off = np.zeros(len(messages) + 1, np.uint64)
+        off[1:] = np.cumsum([len(m) for m in messages])
+        now = np.ascontiguousarray(nows, np.int64)
+        self._keep = (buf, off, now)
+        b = abi.RlRequestBatch()
+        rc = self._lib.rl_packer_pack(self.h, abi.ptr(buf), abi.ptr(off), len(messages), abi.ptr(now), C.byref(b))
+        if rc:
+            raise RedisError(self._lib.rl_packer_last_error(self.h).decode())
+        return b
+
+    def rules(self) -> int:
+        return self._lib.rl_packer_rules(self.h)
+
+    def rule_key(self, rule_id: int):
+        k = self._lib.rl_packer_rule_key(self.h, rule_id)
+        return None if k is None else k.decode()
+
+
+def batch_arrays(b) -> Dict[str, np.ndarray]:
+    """Copy an RlRequestBatch's arrays into numpy (tests and inspection)."""
+    import ctypes as C
+    n, nq, ne = b.n_descriptors, b.n_requests, b.n_entries
+
+    def arr(p, count, dt):
+        if not p or count == 0:
+            return np.zeros(0, dt)
+        return np.ctypeslib.as_array((C.c_uint8 * (count * np.dtype(dt).itemsize)).from_address(p)).view(dt).copy()
+
+    dom_off = arr(b.domain_off, nq + 1, np.uint32)
+    desc_off = arr(b.desc_off, n + 1, np.uint32)
+    return {"domain_off": dom_off, "domain_bytes": arr(b.domain_bytes, int(dom_off[-1]) if nq else 0, np.uint8),
+            "now": arr(b.now, nq, np.int64), "hits": arr(b.hits, nq, np.uint32), "req_idx": arr(b.req_idx, n, np.uint32),
+            "entry_first": arr(b.entry_first, n + 1, np.uint32), "desc_off": desc_off,
+            "desc_bytes": arr(b.desc_bytes, int(desc_off[-1]) if n else 0, np.uint8),
+            "key_len": arr(b.key_len, ne, np.uint16), "value_len": arr(b.value_len, ne, np.uint16),
+            "override_flags": arr(b.override_flags, n, np.uint8), "override_rpu": arr(b.override_rpu, n, np.uint32),
+            "override_unit": arr(b.override_unit, n, np.uint8), "override_rule": arr(b.override_rule, n, np.uint32)}

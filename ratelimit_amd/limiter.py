@@ -129,6 +129,11 @@ class Backend:
         b.n_requests, b.n_descriptors, b.n_entries, b.n_rules = len(arrays["hits"]), n, len(arrays["key_len"]), n_rules
         for k in abi.REQUEST_ARRAYS:
             setattr(b, k, abi.ptr(arrays[k]))
+        return self.do_limit_request_batch(b)
+
+    def do_limit_request_batch(self, b) -> dict:
+        """rl_do_limit_requests on a filled RlRequestBatch (e.g. from RequestPacker.pack)."""
+        n, n_rules = b.n_descriptors, b.n_rules
         out = {k: np.zeros(max(n, 1), dt) for k, dt in abi.REQUEST_RESULT_DTYPES.items()}
         out["stats"] = np.zeros(max(n_rules, 1) * abi.RL_NUM_STATS, np.uint64)
         r = abi.RlRequestResult()

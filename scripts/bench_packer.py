@@ -1,0 +1,47 @@
+"""Host packer throughput (rl_packer, one thread): C1-shaped gRPC payloads
+(serialized RateLimitRequest: domain "bench", descriptors [(tenant, t), (tier,
+sec)] and [(tenant, t), (tier, min)], hits 1) -> rl_request_batch. CPU only.
+
+    python scripts/bench_packer.py [--requests N] [--reps K]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import pbwire  # noqa: E402
+from ratelimit_amd.config import RequestPacker  # noqa: E402
+from ratelimit_amd.types import Descriptor, RateLimitRequest  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--requests", type=int, default=500_000)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    rng = np.random.default_rng(0xC1)
+    tenants = rng.integers(0, 10_000_000, a.requests)
+    msgs = [pbwire.encode_request(RateLimitRequest("bench", [
+        Descriptor([("tenant", "t%010d" % t), ("tier", "sec")]),
+        Descriptor([("tenant", "t%010d" % t), ("tier", "min")])], 1)) for t in tenants]
+    nows = np.full(a.requests, 1_700_000_000, np.int64)
+    pk = RequestPacker(2)
+    pk.pack(msgs, nows)  # warm the packer's buffers
+    t0 = time.perf_counter()
+    for _ in range(a.reps):
+        b = pk.pack(msgs, nows)
+    dt = (time.perf_counter() - t0) / a.reps
+    print(json.dumps({"path": "rl_packer_pack (1 thread, includes joining the payloads)", "requests": a.requests,
+                      "descriptors": int(b.n_descriptors), "payload_bytes_per_request": sum(map(len, msgs)) / a.requests,
+                      "ms_per_batch": dt * 1e3, "descriptors_per_s": b.n_descriptors / dt}))
+    pk.close()
+
+
+if __name__ == "__main__":
+    main()

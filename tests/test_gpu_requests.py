@@ -234,3 +234,47 @@ def test_gpu_request_long_entries_take_global_paths():
         assert svc.stats == want
     finally:
         svc.close()
+
+
+def test_gpu_serialized_requests_through_native_packer():
+    """gRPC payloads (serialized RateLimitRequest) -> rl_packer -> rl_do_limit_requests:
+    statuses and stats equal the oracle service's; override stats keys come back
+    by name from the packer."""
+    import pbwire
+    from ratelimit_amd.config import ConfigTree, RequestPacker
+    from ratelimit_amd.packing import RuleInterner
+    reqs, nows = gen_requests(21, 1500)
+    it = RuleInterner()
+    tree = ConfigTree.from_yaml(FILES, "", it)
+    be = Backend(0.8, True, **SMALL)
+    be.load_config(tree)
+    pk = RequestPacker(len(it.keys))
+    store = StatsStore()
+    osvc = OracleService(RateLimitConfig(FILES, store), O.OracleFixedRateLimitCache(0.8, True, ""))
+    totals = {}
+    try:
+        for i in range(0, len(reqs), 250):
+            part, pn = reqs[i:i + 250], nows[i:i + 250]
+            b = pk.pack([pbwire.encode_request(r) for r in part], pn)
+            res = be.do_limit_request_batch(b)
+            d = 0
+            for r, now in zip(part, pn):
+                _, osts, _ = osvc.should_rate_limit(r, now)
+                for s in osts:
+                    m = int(res["match"][d])
+                    cl = (int(res["requests_per_unit"][d]), int(res["unit"][d])) if m == abi.RL_MATCH_LIMIT else None
+                    got = (int(res["code"][d]), cl, int(res["limit_remaining"][d]),
+                           int(res["reset_s"][d]) if m == abi.RL_MATCH_LIMIT else None)
+                    assert got == st_tuple(s)
+                    d += 1
+            st = res["stats"].reshape(-1, abi.RL_NUM_STATS)
+            for rid in np.nonzero(st.any(axis=1))[0]:
+                name = it.keys[rid] if rid < len(it.keys) else pk.rule_key(int(rid))
+                row = totals.setdefault(name, [0] * abi.RL_NUM_STATS)
+                for j in range(abi.RL_NUM_STATS):
+                    row[j] += int(st[rid, j])
+        want = {k: list(v.as_tuple()) for k, v in store.by_key.items() if any(v.as_tuple())}
+        assert totals == want
+    finally:
+        pk.close()
+        be.close()
