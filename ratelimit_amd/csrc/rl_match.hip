@@ -26,8 +26,8 @@ namespace rl {
 namespace {
 
 constexpr uint32_t MT = 256;                // descriptors per workgroup
-constexpr uint32_t IN_WORDS = 16384 / 4;    // entry bytes staged per workgroup (LDS)
-constexpr uint32_t OUT_WORDS = 24576 / 4;   // stem bytes assembled per workgroup (LDS)
+constexpr uint32_t IN_WORDS = 8192 / 4;     // entry bytes staged per workgroup (LDS; 32 B per descriptor)
+constexpr uint32_t OUT_WORDS = 12288 / 4;   // stem bytes assembled per workgroup (LDS; 48 B per descriptor)
 constexpr unsigned long long M40 = (1ull << 40) - 1;
 
 // Byte sources for the walk: the workgroup's entry bytes staged in LDS
@@ -114,7 +114,7 @@ __device__ __forceinline__ bool fits(uint32_t a, uint32_t b, uint32_t total, uin
 
 __global__ __launch_bounds__(MT) void k_match(CfgDev cg, ReqDev r, MatchBuf m) {
   __shared__ uint32_t s_in[IN_WORDS];
-  __shared__ __attribute__((aligned(16))) uint32_t s_cfg[CFG_LDS_WORDS];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_cfg[];  // cg.blob_words (dynamic: only what the config needs)
   const uint32_t d0 = blockIdx.x * MT, d1 = min(d0 + MT, r.n_desc);
   const uint32_t ba = r.desc_off[d0], bb = r.desc_off[d1];
   const bool staged = fits(ba, bb, r.desc_total, IN_WORDS);
@@ -290,7 +290,7 @@ void launch_match(const CfgDev& cfg, const ReqDev& r, const MatchBuf& m, const P
                   size_t tmp_bytes, hipStream_t st) {
   if (!r.n_desc) return;
   const uint32_t g = (r.n_desc + 255) / 256;
-  k_match<<<g, MT, 0, st>>>(cfg, r, m);
+  k_match<<<g, MT, (size_t)cfg.blob_words * 4, st>>>(cfg, r, m);
   (void)hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, m.v, m.v + r.n_desc, (int)r.n_desc, st);
   k_match_emit<<<g, MT, 0, st>>>(cfg, r, m, m.v + r.n_desc, o);
 }
