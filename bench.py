@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--latency-steps", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--prof-every", type=int, default=8,
+                    help="time every k-th batch's stages with HIP events (k_runs' live time for the roofline)")
     ap.add_argument("--no-fill", action="store_true")
     ap.add_argument("--route", action="store_true", help="use the routed (all_to_all) path even at N=1")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -166,7 +168,7 @@ def main():
     # ---- timed region: exactly K steps. The library records HIP events at the
     # stage boundaries on each batch's own stream (pipelined batches are timed
     # as they run, k_runs included: the roofline's kernel time).
-    be.profile(True)
+    be.profile(True, args.prof_every)
     be.profile_read()
     recv = []
     barrier()

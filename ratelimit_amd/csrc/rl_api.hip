@@ -66,6 +66,7 @@ struct rl_ctx {
   // the batch's own stream, so pipelined batches are timed as they run),
   // folded into the stage sums when a set is reused or read
   bool prof = false;
+  uint32_t prof_every = 1, prof_skip = 0;  // time every prof_every-th batch
   bool prof_pending[PROF_RING] = {};
   uint32_t prof_next = 0;
   hipEvent_t ev[PROF_RING][RL_NUM_STAGES + 1] = {};
@@ -105,6 +106,11 @@ void prof_fold_all(rl_ctx* c) {
 
 hipEvent_t* prof_events(rl_ctx* c) {
   if (!c->prof) return nullptr;
+  if (c->prof_skip) {
+    c->prof_skip--;
+    return nullptr;
+  }
+  c->prof_skip = c->prof_every - 1;
   const uint32_t k = c->prof_next;
   c->prof_next = (k + 1) % PROF_RING;
   prof_fold(c, k);  // the batch that used this set PROF_RING batches ago
@@ -531,7 +537,9 @@ int rl_profile(rl_ctx* c, int enable) {
     for (uint32_t k = 0; k < PROF_RING; k++)
       for (int i = 0; i <= RL_NUM_STAGES; i++) HIPCHK(c, hipEventCreate(&c->ev[k][i]));
   prof_fold_all(c);
-  c->prof = enable != 0;
+  c->prof = enable > 0;
+  c->prof_every = enable > 0 ? (uint32_t)enable : 1u;
+  c->prof_skip = 0;
   return RL_OK;
 }
 

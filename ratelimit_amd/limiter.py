@@ -144,8 +144,9 @@ class Backend:
         res["stats"] = out["stats"][:n_rules * abi.RL_NUM_STATS]
         return res
 
-    def profile(self, enable: bool):
-        check(self.ctx, lib().rl_profile(self.ctx, 1 if enable else 0))
+    def profile(self, enable: bool, every: int = 1):
+        """Time every ``every``-th batch's stages with HIP events (rl_profile)."""
+        check(self.ctx, lib().rl_profile(self.ctx, max(int(every), 1) if enable else 0))
 
     def profile_read(self):
         """-> ({prepare, sort, segment, runs, finish} summed ms, batches timed); resets the sums."""
