@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--latency-steps", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--prof-every", type=int, default=8,
+    ap.add_argument("--prof-every", type=int, default=7,
                     help="time every k-th batch's stages with HIP events (k_runs' live time for the roofline)")
     ap.add_argument("--no-fill", action="store_true")
     ap.add_argument("--route", action="store_true", help="use the routed (all_to_all) path even at N=1")

@@ -33,7 +33,10 @@ constexpr uint32_t RUN_SLOW = 1, RUN_FAST = 2, RUN_MULTI = 4;
 constexpr uint32_t KEY_HEAD = 64;         // stem bytes carried inline (zero-padded) per descriptor
 constexpr uint32_t STAT_STRIPES = 64;     // global partial stats tables
 constexpr uint32_t STAT_LDS_RULES = 512;  // rules aggregated in LDS (== LDS_RULES)
-constexpr uint32_t RUNS_GENERAL_BLOCKS = 64;      // k_runs_general grids (grid-stride over deferrals):
+#ifndef RL_RG_BLOCKS
+#define RL_RG_BLOCKS 64
+#endif
+constexpr uint32_t RUNS_GENERAL_BLOCKS = RL_RG_BLOCKS;  // k_runs_general grids (grid-stride over deferrals):
 constexpr uint32_t RUNS_GENERAL_LATE_BLOCKS = 8;  //   RUN_MULTI runs beside k_runs / k_runs' deferrals after it
 
 struct BatchDev {

@@ -106,3 +106,29 @@ def test_gpu_snapshot_restore_continues_exactly():
             small.close()
     finally:
         b.close()
+
+
+def test_gpu_profile_sampling_counts_and_leaves_results_unchanged():
+    """rl_profile(ctx, k) times every k-th batch (bench --prof-every) and does
+    not change any decision."""
+    calls = stream(11, n_calls=1400)
+    oc = O.OracleFixedRateLimitCache(0.8, True)
+    cache = GpuRateLimitCache(FixedTimeSource(0), 0.8, True, **SMALL)
+    try:
+        cache.backend.profile(True, 3)
+        cache.backend.profile_read()
+        n_batches = 0
+        for i in range(0, len(calls), 200):
+            part = calls[i:i + 200]
+            want = [oc.do_limit(r, l, now) for r, l, now in part]
+            got = cache.do_limit_batch(part)
+            assert [[st(s) for s in g] for g in got] == [[st(s) for s in w] for w in want]
+            n_batches += 1
+        ms, nb = cache.backend.profile_read()
+        assert nb == (n_batches + 2) // 3
+        assert all(v >= 0.0 for v in ms.values()) and ms["runs"] > 0.0
+        cache.backend.profile(False)
+        cache.do_limit_batch(calls[-10:])
+        assert cache.backend.profile_read()[1] == 0
+    finally:
+        cache.close()
