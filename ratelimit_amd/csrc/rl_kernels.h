@@ -149,6 +149,7 @@ struct Scratch {
   uint32_t* defer_n;
   uint32_t* defer2;               // runs k_runs found to need the exact path, for k_runs_general after it
   uint32_t* defer2_n;
+  uint32_t* fast_blk;             // bit per 256-descriptor block holding a RUN_FAST run (k_runs -> k_fast_emit)
   unsigned long long* stripes;    // STAT_STRIPES x STAT_LDS_RULES x RL_NUM_STATS
   // run segmentation (sorted order)
   uint32_t *tile_f, *tile_s, *tile_h;  // per SEG_TILE tile

@@ -2328,7 +2328,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
                                               uint32_t* __restrict__ run_f, const uint32_t* num_runs,
                                               uint32_t* __restrict__ defer, uint32_t* defer_n,
                                               unsigned long long* stats, unsigned long long* stripes, uint32_t* err,
-                                              int restore) {
+                                              int restore, uint32_t* __restrict__ fast_blk) {
   __shared__ uint32_t s_err, s_nr;
   // err may change while this kernel runs (other blocks): read it once per block
   if (threadIdx.x == 0) {
@@ -2405,6 +2405,12 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
           run_state[r] = make_uint4((uint32_t)s0, c0, R.lc, F | ((uint32_t)which << 1));
           run_f[r] = 0xFFFFFFFFu;
           run_flags[r] = fl | RUN_FAST;
+          // mark the 256-descriptor blocks of k_fast_emit this run spans
+          const uint32_t b0 = p >> 8, b1 = (end - 1) >> 8;
+          for (uint32_t w = b0 >> 5; w <= b1 >> 5; w++) {
+            const uint32_t lo = w == (b0 >> 5) ? (b0 & 31) : 0u, hi = w == (b1 >> 5) ? (b1 & 31) : 31u;
+            atomicOr(&fast_blk[w], (0xFFFFFFFFu >> (31 - hi)) & (0xFFFFFFFFu << lo));
+          }
         }
       } else if (ok) {
         if (RL_ABL & 2) {
@@ -2469,11 +2475,15 @@ __global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules,
                                                    const uint32_t* __restrict__ run_flags,
                                                    const uint4* __restrict__ run_state,
                                                    const uint32_t* __restrict__ run_f, unsigned long long* stats,
-                                                   unsigned long long* stripes, const uint32_t* err) {
-  __shared__ uint32_t s_err;
-  if (threadIdx.x == 0) s_err = *err;
+                                                   unsigned long long* stripes, const uint32_t* err,
+                                                   const uint32_t* __restrict__ fast_blk) {
+  __shared__ uint32_t s_err, s_fast;
+  if (threadIdx.x == 0) {
+    s_err = *err;
+    s_fast = (fast_blk[blockIdx.x >> 5] >> (blockIdx.x & 31)) & 1u;
+  }
   __syncthreads();
-  if (s_err) return;
+  if (s_err || !s_fast) return;  // no RUN_FAST descriptor in this block (k_runs' bitmap)
   const bool use_lds = n_rules <= LDS_RULES;
   stats_block_begin(use_lds, n_rules);
   StatAcc acc{use_lds, stats};
@@ -2637,7 +2647,8 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
 // output stats (n_rules x RL_NUM_STATS).
 __global__ __launch_bounds__(256) void k_b_begin(const uint32_t* __restrict__ erra, uint32_t* errb,
                                                  uint32_t* __restrict__ defer_n,
-                                                 unsigned long long* __restrict__ stats, uint32_t m) {
+                                                 unsigned long long* __restrict__ stats, uint32_t m,
+                                                 uint32_t* __restrict__ fast_blk, uint32_t nw) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i == 0) {
     const uint32_t e = *erra;
@@ -2645,6 +2656,7 @@ __global__ __launch_bounds__(256) void k_b_begin(const uint32_t* __restrict__ er
     *defer_n = 0;
   }
   for (uint32_t j = i; j < m; j += gridDim.x * 256) stats[j] = 0;
+  for (uint32_t j = i; j < nw; j += gridDim.x * 256) fast_blk[j] = 0;
 }
 
 // Last kernel of a batch: packed results -> the three rl_result arrays
@@ -2819,7 +2831,7 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
                     hipEvent_t* ev) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
-  k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, s.defer2_n, o.stats, m);
+  k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, s.defer2_n, o.stats, m, s.fast_blk, cdiv(b.n, 256 * 32));
   if (b.n) {
     const uint32_t g = cdiv(b.n, 256);
     const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
@@ -2833,7 +2845,7 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     if (ev) (void)hipEventRecord(ev[3], st);
     k_runs<<<g, 256, lds, st>>>(b, t, P, SRec{s.rec, s.vals[0]}, s.keys[0], s.vals[0], s.res, s.run_start, s.run_end, s.run_flags,
                                 s.run_state, s.run_f, s.num_runs, s.defer2, s.defer2_n, o.stats, s.stripes, s.errb,
-                                restore);
+                                restore, s.fast_blk);
     if (ev) (void)hipEventRecord(ev[4], st);
     // stems k_runs found under several units in the table (rare)
     k_runs_general<<<RUNS_GENERAL_LATE_BLOCKS, 256, lds, st>>>(b, t, P, SRec{s.rec, s.vals[0]}, s.keys[0], s.vals[0],
@@ -2844,7 +2856,8 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
       if (P.lc_en)
         k_fast_over<<<g, 256, 0, st>>>(b.n, SRec{s.rec, s.vals[0]}, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
       k_fast_emit<<<g, 256, lds, st>>>(b.n, b.n_rules, t, P, SRec{s.rec, s.vals[0]}, s.vals[0], s.res, s.segsum, s.rid,
-                                       s.run_start, s.run_end, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb);
+                                       s.run_start, s.run_end, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb,
+                                       s.fast_blk);
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;
       const uint32_t gf = cdiv(nf * RL_NUM_STATS > b.n ? nf * RL_NUM_STATS : b.n, 256);
       k_finish<<<gf, 256, 0, st>>>(s.res, b.n, o, s.stripes, nf, s.errb, P.lc_en ? s.counters + 5 : nullptr);
