@@ -103,7 +103,14 @@ def main():
     slots = 1 << max(16, int(np.ceil(np.log2(2 * keys_per_gpu))))
     # a routed owner receives ~n descriptors (binomial spread across sources)
     cap = n if not routed else int(n * 1.05) + 4096
-    be = Backend(0.8, False, table_slots=slots, max_batch=cap, max_rules=8, device=local,
+    seed = 0
+    if routed:  # every shard of one table hashes stems under one key: rank 0 draws it
+        import secrets
+        t = torch.tensor([secrets.randbits(62) + 1 if rank == 0 else 0], dtype=torch.int64,
+                         device="cpu" if args.dist_backend == "gloo" else "cuda")
+        dist.broadcast(t, 0)
+        seed = int(t.item())
+    be = Backend(0.8, False, table_slots=slots, max_batch=cap, max_rules=8, device=local, hash_seed=seed,
                  max_stem_bytes=64 * cap)
     now0 = W.NOW0
     if routed:
@@ -126,9 +133,9 @@ def main():
     t_fill = time.perf_counter()
     if not args.no_fill:
         for s0 in range(0, T, nq):
-            ids = np.arange(s0, min(s0 + nq, T), dtype=np.int64) + rank * T
-            a, bn, bq, br = W.c1_batch(ids, now0 - 1)
-            do_step(to_dev(a, torch), bn, bq)
+            ids = torch.arange(s0, min(s0 + nq, T), dtype=torch.int64, device="cuda") + rank * T
+            a, bn, bq, br = W.c1_batch_dev(ids, now0 - 1)
+            do_step(a, bn, bq)
         be.synchronize()
     t_fill = time.perf_counter() - t_fill
 

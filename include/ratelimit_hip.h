@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 1u
+#define RL_ABI_VERSION 2u
 
 /* Status codes. */
 enum rl_status {
@@ -40,7 +40,8 @@ enum rl_status {
   RL_E_HIP = 4,        /* HIP runtime error */
   RL_E_CAPACITY = 5,   /* batch larger than rl_config.max_* */
   RL_E_TIME = 6,       /* now outside [0, 2^32 - 2*86400], before the last sweep, or
-                          moved back more than one window on one key */
+                          moved back more than one window on one key. Note: the reference's
+                          clock is int64 (utils.TimeSource); this backend's is 32-bit */
   RL_E_COMM = 7,       /* multi-GPU routing (RCCL) error */
   RL_E_INTERNAL = 8
 };
@@ -79,6 +80,13 @@ typedef struct rl_config {
   int32_t device;               /* HIP device ordinal */
   int64_t expiration_jitter_max_seconds; /* EXPIRATION_JITTER_MAX_SECONDS: accepted; the
                                             backend fixes the draw at 0 */
+  uint64_t hash_seed;        /* key of the stem hash (SipHash-1-3); 0 = drawn at random per ctx.
+                                Descriptor values are client-controlled: keep it secret. */
+  uint32_t n_shards;         /* hash shards of the table held by this ctx (0 = 1); see rl_do_limit */
+  uint32_t debug_hash_bits;  /* tests only: keep the top N bits of the hash's high word (0 = all 32),
+                                so that many stems share one sort key and one home region */
+  int32_t shard_device[16];  /* HIP device of shard k < n_shards (shards may share a device);
+                                unused when n_shards <= 1 (cfg.device) */
   int32_t reserved[8];
 } rl_config;
 
@@ -99,7 +107,9 @@ typedef struct rl_batch {
   uint32_t reserved;
   const uint8_t* stem_bytes;  /* concatenated stems */
   const uint32_t* stem_off;   /* n+1 offsets into stem_bytes, stem_off[0] == 0 */
-  const int64_t* now;         /* [n_requests] UnixNow() of each request (seconds) */
+  const int64_t* now;         /* [n_requests] UnixNow() of each request (seconds). The reference's
+                                 clock is int64; here it must lie in [0, 2^32 - 172800] (the table
+                                 stores 32-bit times) and not before the last rl_sweep: else RL_E_TIME */
   const uint32_t* req_idx;    /* [n] request of each descriptor */
   const uint8_t* unit;        /* [n] rl_unit of the descriptor's limit */
   const uint8_t* flags;       /* [n] RL_FLAG_* */
@@ -116,6 +126,16 @@ typedef struct rl_result {
   uint32_t* limit_remaining;  /* [n] LimitRemaining */
   uint32_t* reset_s;          /* [n] DurationUntilReset.Seconds (1..86400) */
   uint64_t* stats;            /* [n_rules * RL_NUM_STATS] */
+  uint8_t* status;            /* [n] or NULL. Non-NULL: per-descriptor failure isolation. A
+                                 descriptor that cannot be answered (bad unit / rule id / stem length:
+                                 RL_E_INVALID; clock: RL_E_TIME; no slot: RL_E_TABLE_FULL /
+                                 RL_E_ARENA_FULL) gets that rl_status here, code 0 and no stats; the
+                                 rest of the batch is answered and the call returns RL_OK. The adapter
+                                 fails only the RPCs holding a failed descriptor, as the reference's
+                                 per-call checkError does (fixed_cache_impl.go:90-95,
+                                 ratelimit.go:252-256). NULL: any such failure fails the whole call
+                                 (and the batch leaves the table untouched). A malformed batch
+                                 layout (offsets, request order) always fails the call. */
 } rl_result;
 
 /* Table restore / seed records: set the fixed-window counter of key
@@ -209,8 +229,8 @@ int rl_debug_decide(rl_ctx* ctx, uint32_t n, const uint32_t* before, const uint3
  * rl_route_do_limit (owner side, asynchronous): DoLimit over the n records
  * received from all sources (concatenated in source-rank order) with their stems
  * (recv_stem, 4-byte aligned, recv_stem_bytes long; src_stem_base = host array
- * of each source's chunk offset in recv_stem). ret[j] = remaining |
- * reset_s << 32 | code << 56 | local-cache hit << 62 for record j; stats = this owner's deltas
+ * of each source's chunk offset in recv_stem). ret[j] = the packed result of record j
+ * (bits 0-31 remaining, 32-51 reset_s, 52-55 status, 56-61 code, 62 local-cache hit); stats = this owner's deltas
  * (n_rules * RL_NUM_STATS, overwritten). Errors surface at rl_synchronize.
  *
  * rl_route_scatter (source side, asynchronous): results returned in record

@@ -83,7 +83,7 @@ def lib():
     L.rl_packer_rule_key.argtypes = [C.c_void_p, C.c_uint32]
     L.rl_packer_last_error.restype = C.c_char_p
     L.rl_packer_last_error.argtypes = [C.c_void_p]
-    if L.rl_abi_version() != 1:
+    if L.rl_abi_version() != abi.ABI_VERSION:
         raise RuntimeError("libratelimit_hip.so ABI mismatch")
     _lib = L
     return L

@@ -21,7 +21,9 @@ class RlConfig(C.Structure):
                 ("max_rules", C.c_uint32), ("max_stem_bytes", C.c_uint32),
                 ("near_limit_ratio", C.c_float), ("local_cache_enabled", C.c_int32),
                 ("per_second_split", C.c_int32), ("device", C.c_int32),
-                ("expiration_jitter_max_seconds", C.c_int64), ("reserved", C.c_int32 * 8)]
+                ("expiration_jitter_max_seconds", C.c_int64), ("hash_seed", C.c_uint64),
+                ("n_shards", C.c_uint32), ("debug_hash_bits", C.c_uint32), ("shard_device", C.c_int32 * 16),
+                ("reserved", C.c_int32 * 8)]
 
 
 class RlBatch(C.Structure):
@@ -32,7 +34,7 @@ class RlBatch(C.Structure):
 
 
 class RlResult(C.Structure):
-    _fields_ = [("code", P), ("limit_remaining", P), ("reset_s", P), ("stats", P)]
+    _fields_ = [("code", P), ("limit_remaining", P), ("reset_s", P), ("stats", P), ("status", P)]
 
 
 class RlRestoreBatch(C.Structure):
@@ -106,7 +108,9 @@ BATCH_ARRAYS = ("stem_bytes", "stem_off", "now", "req_idx", "unit", "flags", "li
 BATCH_DTYPES = {"stem_bytes": np.uint8, "stem_off": np.uint32, "now": np.int64, "req_idx": np.uint32,
                 "unit": np.uint8, "flags": np.uint8, "limit": np.uint32, "hits": np.uint32,
                 "rule_id": np.uint32}
-RESULT_DTYPES = {"code": np.uint8, "limit_remaining": np.uint32, "reset_s": np.uint32, "stats": np.uint64}
+RESULT_DTYPES = {"code": np.uint8, "limit_remaining": np.uint32, "reset_s": np.uint32, "stats": np.uint64,
+                 "status": np.uint8}
+ABI_VERSION = 2
 
 
 def make_batch_struct(arrays, n, n_requests, n_rules):
@@ -119,6 +123,6 @@ def make_batch_struct(arrays, n, n_requests, n_rules):
 
 def make_result_struct(arrays):
     r = RlResult()
-    for k in ("code", "limit_remaining", "reset_s", "stats"):
-        setattr(r, k, ptr(arrays[k]))
+    for k in ("code", "limit_remaining", "reset_s", "stats", "status"):
+        setattr(r, k, ptr(arrays.get(k)))
     return r

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <random>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -41,20 +42,23 @@ struct rl_ctx {
   hipStream_t side = nullptr;     // k_runs_general beside k_runs (stage B)
   hipEvent_t side_go = nullptr, side_done = nullptr;
   uint32_t next = 0, last = NBUF - 1;  // buffer of the next / of the latest batch
+  uint64_t hash_seed = 0;
+  HashKey hk{};
   // table
   Slot* slots = nullptr;
   uint64_t nslots = 0;
   uint8_t* arena = nullptr;
+  uint8_t* arena2 = nullptr;  // compaction target (rl_sweep), swapped with arena
   uint64_t arena_cap16 = 0;
   // scratch: s[k] per buffer; stripes, counters, time floor, routing and the
   // table-stage error word are shared
   Scratch s[NBUF]{};
-  uint32_t* errw = nullptr;  // [0, NBUF) stage-A words of the buffers, [NBUF] stage-B word
+  uint32_t* errw = nullptr;  // [0, NBUF) stage-A words of the buffers, [NBUF] stage-B word, [NBUF+1] soft word
   // device staging for the host-buffer entry points
   uint8_t* d_stem = nullptr;
   uint32_t *d_off = nullptr, *d_req = nullptr, *d_limit = nullptr, *d_hits = nullptr, *d_rule = nullptr;
   int64_t* d_now = nullptr;
-  uint8_t *d_unit = nullptr, *d_flags = nullptr, *d_code = nullptr;
+  uint8_t *d_unit = nullptr, *d_flags = nullptr, *d_code = nullptr, *d_status = nullptr;
   uint32_t *d_rem = nullptr, *d_reset = nullptr;
   unsigned long long* d_stats = nullptr;
   uint32_t* h_err = nullptr;  // pinned [4]
@@ -144,7 +148,6 @@ int map_err(rl_ctx* c, uint32_t e) {
   if (e & ERR_INVALID) return set_err(c, RL_E_INVALID, "gpu: malformed batch (unit, rule id, request index or stem offsets)");
   if (e & ERR_TABLE_FULL) return set_err(c, RL_E_TABLE_FULL, "gpu: counter table full (raise table_slots or sweep)");
   if (e & ERR_ARENA_FULL) return set_err(c, RL_E_ARENA_FULL, "gpu: long-stem arena full (raise arena_bytes)");
-  if (e & ERR_COLLISIONS) return set_err(c, RL_E_INTERNAL, "gpu: too many stems share one 32-bit hash prefix");
   return set_err(c, RL_E_INTERNAL, "gpu: unknown device error");
 }
 
@@ -154,21 +157,22 @@ hipError_t after_batches(rl_ctx* c, hipStream_t st) { return hipStreamWaitEvent(
 
 // Read (and clear) the sticky device error words; synchronises the stream,
 // which must already be ordered after all submitted work.
+// The soft word (descriptor errors answered by statuses) is cleared, not reported.
 int collect(rl_ctx* c, hipStream_t st = nullptr) {
   if (!st) st = c->stream;
-  HIPCHK(c, hipMemcpyAsync(c->h_err, c->errw, (NBUF + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_err, c->errw, (NBUF + 2) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
   uint32_t e = 0;
   for (uint32_t j = 0; j <= NBUF; j++) e |= c->h_err[j];
-  if (e) {
-    HIPCHK(c, hipMemsetAsync(c->errw, 0, (NBUF + 1) * sizeof(uint32_t), st));
+  if (e || c->h_err[NBUF + 1]) {
+    HIPCHK(c, hipMemsetAsync(c->errw, 0, (NBUF + 2) * sizeof(uint32_t), st));
     HIPCHK(c, hipStreamSynchronize(st));
   }
   return map_err(c, e);
 }
 
 TableDev table_view(rl_ctx* c);
-Params params(rl_ctx* c);
+Params params(rl_ctx* c, int isolate = 0);
 
 // Enqueue one batch. Pipelined (ctx streams): stage A on the buffer's own
 // stream as soon as the buffer is free, stage B after the previous batch's
@@ -178,12 +182,13 @@ uint32_t enqueue(rl_ctx* c, const BatchDev& b, const OutDev& o, int restore, hip
   const uint32_t k = c->next;
   c->next = (k + 1) % NBUF;
   const TableDev t = table_view(c);
-  const Params P = params(c);
+  const int isolate = (!restore && o.status) ? 1 : 0;
+  const Params P = params(c, isolate);
   if (pipelined) {
     hipStream_t a = c->pipe[k];
     hipEvent_t* ev = prof_events(c);
     (void)hipStreamWaitEvent(a, c->b_done[k], 0);  // buffer k's previous batch is done
-    launch_stage_a(b, c->s[k], a, ev);
+    launch_stage_a(b, c->s[k], isolate, a, ev);
     (void)hipStreamWaitEvent(a, c->b_done[c->last], 0);  // table order
     launch_stage_b(b, o, t, P, c->s[k], restore, a, c->side, c->side_go, c->side_done, ev);
     (void)hipEventRecord(c->b_done[k], a);
@@ -191,7 +196,7 @@ uint32_t enqueue(rl_ctx* c, const BatchDev& b, const OutDev& o, int restore, hip
     if (!st) st = c->stream;
     (void)after_batches(c, st);
     hipEvent_t* ev = prof_events(c);
-    launch_stage_a(b, c->s[k], st, ev);
+    launch_stage_a(b, c->s[k], isolate, st, ev);
     launch_stage_b(b, o, t, P, c->s[k], restore, st, c->side, c->side_go, c->side_done, ev);
     (void)hipEventRecord(c->b_done[k], st);
   }
@@ -208,8 +213,9 @@ int check_sizes(rl_ctx* c, const rl_batch* in, uint64_t stem_bytes) {
   return RL_OK;
 }
 
-BatchDev dev_view(const rl_batch* in, uint32_t stem_cap) {
+BatchDev dev_view(const rl_ctx* c, const rl_batch* in, uint32_t stem_cap) {
   BatchDev b;
+  b.hk = c->hk;
   b.n = in->n;
   b.n_req = in->n_requests;
   b.n_rules = in->n_rules;
@@ -240,11 +246,12 @@ TableDev table_view(rl_ctx* c) {
   return t;
 }
 
-Params params(rl_ctx* c) {
+Params params(rl_ctx* c, int isolate) {
   Params P;
   P.ratio = c->cfg.near_limit_ratio;
   P.lc_en = c->cfg.local_cache_enabled != 0;
   P.per_second = c->cfg.per_second_split != 0;
+  P.isolate = isolate;
   return P;
 }
 
@@ -259,7 +266,8 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
   ok = ok && dalloc(&s.rec, n) == hipSuccess && dalloc(&s.res, n) == hipSuccess;
   for (int i = 0; i < 2; i++) ok = ok && dalloc(&s.keys[i], n) == hipSuccess && dalloc(&s.vals[i], n) == hipSuccess;
   ok = ok && dalloc(&s.hist, 256ull * std::max(ntiles, 1u)) == hipSuccess && dalloc(&s.hist_tot, 256) == hipSuccess;
-  ok = ok && dalloc(&s.repid, n) == hipSuccess && dalloc(&s.defer, n) == hipSuccess &&
+  ok = ok && dalloc(&s.grp, n) == hipSuccess && dalloc(&s.lead, n) == hipSuccess && dalloc(&s.gmask, n) == hipSuccess &&
+       dalloc(&s.defer, n) == hipSuccess &&
        dalloc(&s.defer_n, 1) == hipSuccess && dalloc(&s.defer2, n) == hipSuccess &&
        dalloc(&s.defer2_n, 1) == hipSuccess && dalloc(&s.fast_blk, (size_t)n / (256 * 32) + 1) == hipSuccess;
   ok = ok && dalloc(&s.tile_f, nt) == hipSuccess && dalloc(&s.tile_s, nt) == hipSuccess &&
@@ -277,7 +285,7 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
 
 void free_buffer(Scratch& s) {
   void* bufs[] = {s.rec, s.res, s.big_meta, s.big_n, s.big_work, s.work_n, s.big_cnt, s.keys[0], s.keys[1], s.vals[0], s.vals[1], s.hist,
-                  s.hist_tot, s.repid, s.defer, s.defer_n, s.defer2, s.defer2_n, s.fast_blk, s.tile_f, s.tile_s, s.tile_h, s.hits_s, s.segsum, s.rid,
+                  s.hist_tot, s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.fast_blk, s.tile_f, s.tile_s, s.tile_h, s.hits_s, s.segsum, s.rid,
                   s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -312,7 +320,7 @@ int stage(rl_ctx* c, const rl_batch* in, BatchDev* out) {
   d.limit = c->d_limit;
   d.hits = c->d_hits;
   d.rule_id = c->d_rule;
-  *out = dev_view(&d, c->cfg.max_stem_bytes);
+  *out = dev_view(c, &d, c->cfg.max_stem_bytes);
   return RL_OK;
 }
 
@@ -346,6 +354,13 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
 
   rl_ctx* c = new rl_ctx();
   c->cfg = cfg;
+  c->hash_seed = cfg.hash_seed;
+  while (!c->hash_seed) {  // a secret per-ctx key unless the caller shares one (multi-shard tables)
+    std::random_device rd;
+    c->hash_seed = ((uint64_t)rd() << 32) ^ rd();
+  }
+  c->cfg.hash_seed = c->hash_seed;
+  c->hk = hash_key_of(c->hash_seed, cfg.debug_hash_bits);
   c->nslots = cfg.table_slots;
   c->arena_cap16 = cfg.arena_bytes / 16;
   const uint32_t n = cfg.max_batch;
@@ -358,10 +373,10 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && hipEventCreateWithFlags(&c->side_go, hipEventDisableTiming) == hipSuccess &&
        hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming) == hipSuccess;
   ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess;
-  ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess;
+  ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess && dalloc(&c->arena2, cfg.arena_bytes) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++) ok = ok && alloc_buffer(c->s[k], n);
   Scratch& s0 = c->s[0];
-  ok = ok && dalloc(&c->errw, NBUF + 1) == hipSuccess;
+  ok = ok && dalloc(&c->errw, NBUF + 2) == hipSuccess;
   ok = ok && dalloc(&s0.stripes, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS) == hipSuccess;
   ok = ok && dalloc(&s0.time_floor, 1) == hipSuccess;
   ok = ok && dalloc(&s0.counters, 8) == hipSuccess;
@@ -371,6 +386,7 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
     Scratch& sk = c->s[k];
     sk.err = c->errw ? c->errw + k : nullptr;
     sk.errb = c->errw ? c->errw + NBUF : nullptr;
+    sk.errs = c->errw ? c->errw + NBUF + 1 : nullptr;
     sk.stripes = s0.stripes;
     sk.time_floor = s0.time_floor;
     sk.counters = s0.counters;
@@ -385,14 +401,15 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && dalloc(&c->d_req, n) == hipSuccess && dalloc(&c->d_unit, n) == hipSuccess &&
        dalloc(&c->d_flags, n) == hipSuccess && dalloc(&c->d_limit, n) == hipSuccess &&
        dalloc(&c->d_hits, n) == hipSuccess && dalloc(&c->d_rule, n) == hipSuccess;
-  ok = ok && dalloc(&c->d_code, n) == hipSuccess && dalloc(&c->d_rem, n) == hipSuccess &&
+  ok = ok && dalloc(&c->d_code, n) == hipSuccess && dalloc(&c->d_status, n) == hipSuccess &&
+       dalloc(&c->d_rem, n) == hipSuccess &&
        dalloc(&c->d_reset, n) == hipSuccess;
   ok = ok && dalloc(&c->d_stats, (size_t)cfg.max_rules * RL_NUM_STATS) == hipSuccess;
-  ok = ok && hipHostMalloc((void**)&c->h_err, (NBUF + 1) * sizeof(uint32_t)) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_err, (NBUF + 2) * sizeof(uint32_t)) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_counters, 8 * sizeof(unsigned long long)) == hipSuccess;
   if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
   ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
-       hipMemsetAsync(c->errw, 0, (NBUF + 1) * 4, c->stream) == hipSuccess &&
+       hipMemsetAsync(c->errw, 0, (NBUF + 2) * 4, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.time_floor, 0, 8, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.counters, 0, 64, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.stripes, 0, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS * 8, c->stream) ==
@@ -420,8 +437,9 @@ void rl_destroy(rl_ctx* c) {
     if (c->b_done[k]) (void)hipEventDestroy(c->b_done[k]);
   }
   const Scratch& s0 = c->s[0];
-  void* bufs[] = {c->slots, c->arena, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
-                  c->d_now, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_rem,
+  void* bufs[] = {c->slots, c->arena, c->arena2, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
+                  c->d_now, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_status,
+                  c->d_rem,
                   c->d_reset, c->d_stats, s0.route_start, s0.route_base, s0.route_counts};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -445,8 +463,8 @@ int rl_do_limit_async(rl_ctx* c, const rl_batch* in, rl_result* out, void* strea
   if (rc) return rc;
   if ((uintptr_t)in->stem_bytes & 3u) return set_err(c, RL_E_INVALID, "gpu: stem_bytes must be 4-byte aligned");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  BatchDev b = dev_view(in, c->cfg.max_stem_bytes);
-  OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats};
+  BatchDev b = dev_view(c, in, c->cfg.max_stem_bytes);
+  OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats, out->status};
   // NULL stream: pipelined on the ctx streams; otherwise serial on the caller's stream
   enqueue(c, b, o, 0, (hipStream_t)stream, stream == nullptr);
   HIPCHK(c, hipGetLastError());
@@ -467,7 +485,7 @@ int rl_route_pack(rl_ctx* c, const rl_batch* in, uint32_t n_shards, uint32_t src
   HIPCHK(c, hipSetDevice(c->cfg.device));
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   HIPCHK(c, after_batches(c, st));  // the partition reuses buffer 0's scratch
-  BatchDev b = dev_view(in, c->cfg.max_stem_bytes);
+  BatchDev b = dev_view(c, in, c->cfg.max_stem_bytes);
   launch_route_pack(b, n_shards, src_rank, (Wire*)send_rec, send_stem, perm, c->s[0].route_counts, c->s[0], st);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(c->h_route, c->s[0].route_counts, 2ull * n_shards * 8, hipMemcpyDeviceToHost, st));
@@ -496,6 +514,7 @@ int rl_route_do_limit(rl_ctx* c, uint32_t n, const void* recv_rec, const uint8_t
                       st);
   if (!n) HIPCHK(c, hipMemsetAsync(c->d_off, 0, sizeof(uint32_t), st));
   BatchDev b;
+  b.hk = c->hk;
   b.n = n;
   b.n_req = n;
   b.n_rules = n_rules;
@@ -511,7 +530,7 @@ int rl_route_do_limit(rl_ctx* c, uint32_t n, const void* recv_rec, const uint8_t
   b.limit = c->d_limit;
   b.hits = c->d_hits;
   b.rule = c->d_rule;
-  OutDev o{c->d_code, c->d_rem, c->d_reset, (unsigned long long*)stats};
+  OutDev o{c->d_code, c->d_rem, c->d_reset, (unsigned long long*)stats, nullptr};
   const uint32_t k = enqueue(c, b, o, 0, st, false);
   if (n) HIPCHK(c, hipMemcpyAsync(ret, c->s[k].res, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
   HIPCHK(c, hipGetLastError());
@@ -524,7 +543,7 @@ int rl_route_scatter(rl_ctx* c, uint32_t n, const uint32_t* perm, const uint64_t
   if (!c || !out || (n && (!perm || !ret))) return set_err(c, RL_E_INVALID, "gpu: null argument");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-  OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats};
+  OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats, out->status};
   launch_route_scatter(perm, (const unsigned long long*)ret, n, o, st);
   HIPCHK(c, hipGetLastError());
   return RL_OK;
@@ -568,11 +587,12 @@ int rl_do_limit(rl_ctx* c, const rl_batch* in, rl_result* out) {
   int rc = stage(c, in, &b);
   if (rc) return rc;
   hipStream_t st = c->stream;
-  OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats};
+  OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats, out->status ? c->d_status : nullptr};
   enqueue(c, b, o, 0, st, false);
   HIPCHK(c, hipGetLastError());
   const uint32_t n = in->n;
   if (n) {
+    if (out->status) HIPCHK(c, hipMemcpyAsync(out->status, c->d_status, n, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(out->code, c->d_code, n, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(out->limit_remaining, c->d_rem, n * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(out->reset_s, c->d_reset, n * 4, hipMemcpyDeviceToHost, st));
@@ -616,7 +636,7 @@ int rl_restore(rl_ctx* c, const rl_restore_batch* r) {
   BatchDev b;
   int rc = stage(c, &in, &b);
   if (!rc) {
-    OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats};
+    OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats, nullptr};
     enqueue(c, b, o, 1, c->stream, false);
     hipError_t he = hipGetLastError();
     rc = he != hipSuccess ? set_err(c, RL_E_HIP, std::string("gpu: ") + hipGetErrorString(he)) : collect(c);
@@ -640,9 +660,18 @@ int rl_sweep(rl_ctx* c, int64_t now, uint64_t* n_evicted) {
   HIPCHK(c, hipMemsetAsync(c->s[0].counters, 0, 8, c->stream));
   launch_sweep(c->slots, c->nslots, (uint32_t)now, c->s[0].counters, c->stream);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 40, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (n_evicted) *n_evicted = c->h_counters[0];
+  if (c->h_counters[0] && c->h_counters[4]) {
+    // reclaim the long-stem arena: live slots' overflow bytes move to the spare
+    // arena, packed from 0, and the two swap (counters[4] = the arena cursor)
+    HIPCHK(c, hipMemsetAsync(c->s[0].counters + 4, 0, 8, c->stream));
+    launch_arena_compact(c->slots, c->nslots, c->arena, c->arena2, c->s[0].counters + 4, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::swap(c->arena, c->arena2);
+  }
   return RL_OK;
 }
 
@@ -959,8 +988,8 @@ int rl_do_limit_requests(rl_ctx* c, const rl_request_batch* in, rl_request_resul
   pb.limit = c->d_limit;
   pb.hits = c->d_hits;
   pb.rule_id = c->d_rule;
-  BatchDev b = dev_view(&pb, c->cfg.max_stem_bytes);
-  OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats};
+  BatchDev b = dev_view(c, &pb, c->cfg.max_stem_bytes);
+  OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats, nullptr};
   enqueue(c, b, o, 0, st, false);
   ReqOutDev ro{B + o_code, (uint32_t*)(B + o_rem), (uint32_t*)(B + o_reset), B + o_match,
                (uint32_t*)(B + o_orule), (uint32_t*)(B + o_orpu), B + o_ounit};
@@ -1004,9 +1033,9 @@ int rl_local_cache_info_get(rl_ctx* c, int64_t now, rl_local_cache_info* info) {
 }
 
 namespace {
-constexpr uint64_t SNAP_MAGIC = 0x31304150414e534cull;  // "LSNAPA01"
+constexpr uint64_t SNAP_MAGIC = 0x32304150414e534cull;  // "LSNAPA02" (keyed hash)
 struct SnapHeader {
-  uint64_t magic, nslots, arena_used16, reserved0;
+  uint64_t magic, nslots, arena_used16, hash_seed;  // slots are placed by the keyed hash: restore adopts its key
   int64_t time_floor;
   uint64_t reserved[3];
 };
@@ -1040,6 +1069,7 @@ int rl_snapshot_save(rl_ctx* c, void* host, uint64_t bytes) {
   if (rc) return rc;
   h.magic = SNAP_MAGIC;
   h.nslots = c->nslots;
+  h.hash_seed = c->hash_seed;
   const uint64_t need = sizeof(SnapHeader) + c->nslots * sizeof(Slot) + h.arena_used16 * 16;
   if (bytes < need) return set_err(c, RL_E_CAPACITY, "gpu: snapshot buffer smaller than rl_snapshot_size");
   uint8_t* p = (uint8_t*)host;
@@ -1069,6 +1099,9 @@ int rl_snapshot_load(rl_ctx* c, const void* host, uint64_t bytes) {
     HIPCHK(c, hipMemcpy(c->arena, p + sizeof h + c->nslots * sizeof(Slot), h.arena_used16 * 16, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->s[0].counters + 4, &h.arena_used16, 8, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->s[0].time_floor, &h.time_floor, 8, hipMemcpyHostToDevice));
+  c->hash_seed = h.hash_seed;
+  c->cfg.hash_seed = h.hash_seed;
+  c->hk = hash_key_of(h.hash_seed, c->cfg.debug_hash_bits);
   return RL_OK;
 }
 

@@ -72,34 +72,72 @@ __host__ __device__ inline uint64_t fmix64(uint64_t k) {
   return k;
 }
 
-// 64-bit stem hash: one 8-byte little-endian word per round (bytes past the end = 0).
+// Keyed 64-bit stem hash: SipHash-1-3 (one compression round per 8-byte
+// little-endian word, three finalisation rounds) under a 128-bit key drawn per
+// rl_ctx (rl_config.hash_seed; random when 0). Descriptor values are
+// client-controlled; with a secret key an attacker cannot aim stems at one
+// sort key or one home slot. Correctness never depends on the hash: every
+// match is confirmed on the full stem bytes, and any number of stems sharing a
+// sort key takes the exact path.
+struct HashKey {
+  uint64_t k0, k1;
+  uint32_t hi_bits;  // test knob: keep only the top hi_bits of the high word (32 = all)
+};
+
+__host__ __device__ inline HashKey hash_key_of(uint64_t seed, uint32_t hi_bits) {
+  return HashKey{fmix64(seed ^ 0x243F6A8885A308D3ull), fmix64(seed + 0x13198A2E03707344ull),
+                 hi_bits == 0 || hi_bits > 32 ? 32u : hi_bits};
+}
+
 struct StemHasher {
-  uint64_t h;
-  __host__ __device__ explicit StemHasher(uint32_t len) : h(0x9E3779B97F4A7C15ull ^ (uint64_t(len) * 0xC2B2AE3D27D4EB4Full)) {}
-  __host__ __device__ inline void word(uint64_t w) {
-    uint64_t k = w * 0x87c37b91114253d5ull;
-    k = rotl64(k, 31) * 0x4cf5ad432745937full;
-    h ^= k;
-    h = rotl64(h, 27) * 5 + 0x52dce729ull;
+  uint64_t v0, v1, v2, v3, b;
+  __host__ __device__ inline StemHasher(const HashKey& k, uint32_t len)
+      : v0(k.k0 ^ 0x736f6d6570736575ull), v1(k.k1 ^ 0x646f72616e646f6dull), v2(k.k0 ^ 0x6c7967656e657261ull),
+        v3(k.k1 ^ 0x7465646279746573ull), b(uint64_t(len) << 56) {}
+  __host__ __device__ inline void round() {
+    v0 += v1; v1 = rotl64(v1, 13); v1 ^= v0; v0 = rotl64(v0, 32);
+    v2 += v3; v3 = rotl64(v3, 16); v3 ^= v2;
+    v0 += v3; v3 = rotl64(v3, 21); v3 ^= v0;
+    v2 += v1; v1 = rotl64(v1, 17); v1 ^= v2; v2 = rotl64(v2, 32);
   }
-  __host__ __device__ inline uint64_t finish() const {
-    uint64_t x = fmix64(h);
+  __host__ __device__ inline void word(uint64_t m) {
+    v3 ^= m;
+    round();
+    v0 ^= m;
+  }
+  // tail = the last len % 8 bytes (little-endian, zero above them)
+  __host__ __device__ inline uint64_t finish(uint64_t tail, uint32_t hi_bits) {
+    word(b | tail);
+    v2 ^= 0xff;
+    round(); round(); round();
+    uint64_t x = v0 ^ v1 ^ v2 ^ v3;
+    if (hi_bits < 32) x &= ~(((1ull << (32 - hi_bits)) - 1) << 32);
     return x ? x : 1;
   }
 };
 
 // 64-bit hash of the stem bytes [a, a+len) read through rd (8 bytes per call).
 template <typename Rd>
-__device__ inline uint64_t hash_stem(Rd rd, uint32_t a, uint32_t len) {
-  StemHasher hs(len);
+__device__ inline uint64_t hash_stem(const HashKey& key, Rd rd, uint32_t a, uint32_t len) {
+  StemHasher hs(key, len);
   uint32_t i = 0;
   for (; i + 8 <= len; i += 8) hs.word(rd(a + i));
-  if (i < len) {
-    uint32_t rem = len - i;
-    uint64_t w = rd(a + i) & ((rem == 8) ? ~0ull : ((1ull << (rem * 8)) - 1));
-    hs.word(w);
-  }
-  return hs.finish();
+  uint64_t tail = 0;
+  if (i < len) tail = rd(a + i) & ((1ull << ((len - i) * 8)) - 1);
+  return hs.finish(tail, key.hi_bits);
+}
+
+// Host reference of the same hash (tests, tools).
+__host__ inline uint64_t hash_stem_host(const HashKey& key, const uint8_t* s, uint32_t len) {
+  StemHasher hs(key, len);
+  uint32_t i = 0;
+  auto rd = [&](uint32_t at, uint32_t nb) {
+    uint64_t w = 0;
+    for (uint32_t j = 0; j < nb; j++) w |= uint64_t(s[at + j]) << (8 * j);
+    return w;
+  };
+  for (; i + 8 <= len; i += 8) hs.word(rd(i, 8));
+  return hs.finish(i < len ? rd(i, len - i) : 0, key.hi_bits);
 }
 
 // 8 bytes starting at byte address a of a dword array (little-endian); dwords
@@ -180,15 +218,39 @@ __host__ __device__ inline Decision decide(uint32_t before, uint32_t after, bool
   return r;
 }
 
-// Device error word bits (mapped to rl_status by the host).
+// Device error word bits (mapped to rl_status by the host). Without per-descriptor
+// statuses every bit fails the batch; with them (rl_result.status) only
+// ERR_INVALID from a malformed batch layout does, and the others become the
+// statuses of the descriptors they concern, collected in a soft word.
 enum : uint32_t {
   ERR_INVALID = 1u << 0,
   ERR_TABLE_FULL = 1u << 1,
   ERR_ARENA_FULL = 1u << 2,
   ERR_TIME = 1u << 3,
-  ERR_COLLISIONS = 1u << 4,  // more than MAX_REPS distinct stems in one hash run
   ERR_HISTORY = 1u << 5,     // a key's window is older than its (cur, prev) history
 };
+
+// Packed 8-B result of one descriptor (k_finish / the route exchange unpack it):
+//   bits  0..31 LimitRemaining, 32..51 DurationUntilReset (<= 86400),
+//   52..55 rl_status of the descriptor (0 = answered), 56..61 code,
+//   62 the local-cache Get hit (localCacheStats hitCount).
+__host__ __device__ inline unsigned long long pack_res(uint32_t rem, uint32_t reset, uint32_t code, bool lc_hit) {
+  return (unsigned long long)rem | ((unsigned long long)(reset & 0xFFFFFu) << 32) |
+         ((unsigned long long)code << 56) | ((unsigned long long)lc_hit << 62);
+}
+__host__ __device__ inline unsigned long long pack_fail(uint32_t status) {
+  return (unsigned long long)(status & 0xFu) << 52;
+}
+__host__ __device__ inline uint32_t res_rem(unsigned long long v) { return (uint32_t)v; }
+__host__ __device__ inline uint32_t res_reset(unsigned long long v) { return (uint32_t)(v >> 32) & 0xFFFFFu; }
+__host__ __device__ inline uint32_t res_status(unsigned long long v) { return (uint32_t)(v >> 52) & 0xFu; }
+__host__ __device__ inline uint32_t res_code(unsigned long long v) { return (uint32_t)(v >> 56) & 0x3Fu; }
+__host__ __device__ inline bool res_lc_hit(unsigned long long v) { return (v >> 62) & 1u; }
+
+// Rec / wire flags byte: bit 0 = RL_FLAG_SHADOW (ABI); bit 7 = the descriptor
+// failed (its status is already in its packed result): every table kernel
+// leaves it alone.
+constexpr uint32_t FLAG_SKIP = 0x80;
 
 constexpr uint32_t NOW_MAX = 0xFFFFFFFFu - 2u * 86400u;  // now + 2*div must fit u32
 

@@ -43,6 +43,7 @@ struct BatchDev {
   uint32_t n, n_req, n_rules, stem_cap;
   uint32_t stem_total;  // bytes of packed stems (off[n]); reads stay below it
   uint32_t now_desc;    // 1: now[] per descriptor and req[] an opaque non-decreasing label (routed batches)
+  HashKey hk;           // the ctx's stem-hash key
   const uint8_t* stem;  // 4-byte aligned
   const uint32_t* off;
   const int64_t* now;
@@ -113,6 +114,7 @@ struct OutDev {
   uint32_t* rem;
   uint32_t* reset;
   unsigned long long* stats;
+  uint8_t* status;  // per-descriptor rl_status (isolate mode), or null
 };
 
 struct TableDev {
@@ -129,6 +131,7 @@ struct Params {
   float ratio;
   int lc_en;
   int per_second;
+  int isolate;  // per-descriptor statuses (rl_result.status): descriptor errors do not fail the batch
 };
 
 // Per-batch scratch (device), sized for max_batch.
@@ -144,7 +147,9 @@ struct Scratch {
   uint32_t* big_work;                // [n / BIG_CHUNK + PART_DIGITS] chunk work items (bucket << 16 | chunk)
   uint32_t* work_n;
   uint32_t* big_cnt;                 // [work items x (1 + 2 x BIG_HEAVY)] k_big_count per chunk
-  uint8_t* repid;
+  uint32_t* grp;                  // k_runs_general: stem group of each position of a deferred run
+  uint32_t* lead;                 //   first position of each group (stored from the run's start)
+  uint8_t* gmask;                 //   units seen per group
   uint32_t* defer;                // RUN_MULTI runs (k_run_check), for k_runs_general beside k_runs
   uint32_t* defer_n;
   uint32_t* defer2;               // runs k_runs found to need the exact path, for k_runs_general after it
@@ -168,6 +173,7 @@ struct Scratch {
   uint32_t* num_runs;
   uint32_t* err;   // validation word of this buffer's batch (stage A)
   uint32_t* errb;  // sticky table-stage word (stage B), shared by both buffers
+  uint32_t* errs;  // soft word: descriptor errors answered by statuses (isolate mode)
   int64_t* time_floor;  // requests earlier than the last sweep are rejected
   unsigned long long* counters;  // [0..3] sweep / info outputs
   // multi-GPU routing
@@ -180,7 +186,7 @@ struct Scratch {
 // only the batch and this buffer's scratch, so it may overlap the previous
 // batch's stage B; stage B (table probe, replay, decisions, stats, results)
 // must run in batch order.
-void launch_stage_a(const BatchDev& b, const Scratch& s, hipStream_t st, hipEvent_t* ev = nullptr);
+void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_t st, hipEvent_t* ev = nullptr);
 // Stage B launches the RUN_MULTI runs' exact replay on `side` (ordered by the
 // events go / side_done) so that it overlaps k_runs.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
@@ -202,6 +208,8 @@ void launch_route_unpack(const Wire* rec, uint32_t n, const unsigned long long* 
 void launch_route_scatter(const uint32_t* perm, const unsigned long long* ret, uint32_t n, const OutDev& o,
                           hipStream_t st);
 void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st);
+void launch_arena_compact(Slot* slots, uint64_t nslots, const uint8_t* from, uint8_t* to, unsigned long long* used16,
+                          hipStream_t st);
 void launch_lc_count(const Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* out, hipStream_t st);
 void launch_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out, hipStream_t st);
 void launch_debug_keys(const BatchDev& b, uint8_t* out, uint32_t* klen, hipStream_t st);

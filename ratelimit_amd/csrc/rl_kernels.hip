@@ -41,11 +41,11 @@ namespace rl {
 constexpr uint32_t HASH_LDS_BYTES = 16384;
 
 __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ rec, uint32_t* __restrict__ keys,
-                                                 uint32_t* err,
+                                                 uint32_t* err, uint32_t* errs, int isolate,
                                                  const int64_t* time_floor, uint32_t* defer_n,
                                                  uint32_t* big_n, uint32_t* work_n, uint32_t* __restrict__ run_flags,
-                                                 uint32_t* num_runs,
-                                                 uint32_t* __restrict__ hit_a) {
+                                                 uint32_t* num_runs, uint32_t* __restrict__ hit_a,
+                                                 unsigned long long* __restrict__ res) {
   __shared__ uint32_t lds[HASH_LDS_BYTES / 4 + 4];
   const uint32_t tid = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + tid;
@@ -57,25 +57,30 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
     *big_n = 0;
     *work_n = 0;
   }
+  const int64_t floor = *time_floor;
+  auto time_bad = [&](int64_t t) { return t < 0 || t > (int64_t)NOW_MAX || t < floor; };
 
-  // ---- per-request clock checks: now in [0, NOW_MAX] and not before the last sweep
-  if (i < (b.now_desc ? b.n : b.n_req)) {
-    const int64_t t = b.now[i];
-    if (t < 0 || t > (int64_t)NOW_MAX || t < *time_floor) bad |= ERR_TIME;
-  }
+  // ---- per-request clock checks (whole-batch mode): now in [0, NOW_MAX], not before the last sweep
+  if (!isolate && i < (b.now_desc ? b.n : b.n_req) && time_bad(b.now[i])) bad |= ERR_TIME;
 
-  // ---- per-descriptor checks
-  uint32_t s0 = 0, len = 0, u = 0, q = 0;
+  // ---- per-descriptor checks. The batch layout (request order, offsets) is
+  // fatal; a bad unit / rule / stem length or clock is the descriptor's own
+  // error: with isolate it becomes its status (FLAG_SKIP), else it fails the batch.
+  uint32_t s0 = 0, len = 0, u = 0, q = 0, dstat = 0;
   if (i < b.n) {
     s0 = b.off[i];
     const uint32_t s1 = b.off[i + 1];
     u = b.unit[i];
     q = b.req[i];
-    if (u < 1 || u > 4 || b.rule[i] >= b.n_rules || (!b.now_desc && q >= b.n_req) || (i && b.req[i - 1] > q) || s1 < s0 ||
-        s1 > b.stem_cap || s1 - s0 == 0 || s1 - s0 > 65535)
+    if ((!b.now_desc && q >= b.n_req) || (i && b.req[i - 1] > q) || s1 < s0 || s1 > b.stem_cap) {
       bad |= ERR_INVALID;
-    else
+    } else {
       len = s1 - s0;
+      if (u < 1 || u > 4 || b.rule[i] >= b.n_rules || len == 0 || len > 65535) dstat = RL_E_INVALID;
+      else if (isolate && time_bad(b.now_desc ? b.now[i] : b.now[q])) dstat = RL_E_TIME;
+      if (len > 65535) len = 0;
+    }
+    if (dstat && !isolate) bad |= ERR_INVALID;
   }
   if (bad) atomicOr(err, bad);
 
@@ -99,19 +104,19 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   __syncthreads();
   if (i >= b.n) return;
   uint64_t h = 0;
-  if (len && range_ok) {
+  if (len && range_ok && s0 + len <= total) {
     if (use_lds) {
-      h = hash_stem(DwordReader{lds, HASH_LDS_BYTES / 4 + 4}, s0 - lo + lead, len);
+      h = hash_stem(b.hk, DwordReader{lds, HASH_LDS_BYTES / 4 + 4}, s0 - lo + lead, len);
     } else {
       const uint32_t nw = ((total + 3u) >> 2) - (s0 >> 2);
-      h = hash_stem(DwordReader{words + (s0 >> 2), nw}, s0 & 3u, len);
+      h = hash_stem(b.hk, DwordReader{words + (s0 >> 2), nw}, s0 & 3u, len);
     }
   }
   keys[i] = (uint32_t)(h >> 32);
   Rec r;
   r.hlo = (uint32_t)h;
   r.off = s0;
-  r.lu = len | (u << 16) | ((uint32_t)b.flags[i] << 24);
+  r.lu = len | (u << 16) | ((uint32_t)((b.flags[i] & 0x7Fu) | (dstat ? FLAG_SKIP : 0u)) << 24);
   r.rule = b.rule[i];
   r.req = q;
   r.now = b.now_desc ? (uint32_t)b.now[i] : (q < b.n_req) ? (uint32_t)b.now[q] : 0u;
@@ -119,6 +124,10 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   r.limit = b.limit[i];
   rec[i] = r;
   hit_a[i] = r.hits;
+  if (dstat && isolate) {  // answered here: the table kernels skip it
+    res[i] = pack_fail(dstat);
+    atomicOr(errs, dstat == RL_E_TIME ? ERR_TIME : ERR_INVALID);
+  }
 }
 
 // ===========================================================================
@@ -397,41 +406,74 @@ __device__ inline bool slot_key_equal(const Slot* s, const Key& key, const uint8
   return diff == 0;
 }
 
-__device__ inline void slot_init(const TableDev& t, Slot* s, const Key& key, uint32_t unit, uint32_t* err) {
+// Claim n16 16-B units of the long-stem arena; the cursor never moves past the
+// cap (a failed claim leaves it alone). rl_sweep compacts the arena.
+__device__ __attribute__((always_inline)) inline bool arena_claim(const TableDev& t, uint32_t n16, unsigned long long* off) {
+  unsigned long long cur = __hip_atomic_load(t.arena_used16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    if (cur + n16 > t.arena_cap16) return false;
+    const unsigned long long prev = atomicCAS(t.arena_used16, cur, cur + n16);
+    if (prev == cur) {
+      *off = cur;
+      return true;
+    }
+    cur = prev;
+  }
+}
+
+// Fill a freshly claimed slot. False when the arena cannot take the stem's
+// tail: the caller returns the slot to the table as a tombstone.
+__device__ __attribute__((always_inline)) inline bool slot_init(const TableDev& t, Slot* s, const Key& key, uint32_t unit) {
   const uint32_t len = key.len, il = len < INLINE_KEY ? len : INLINE_KEY, nw = il >> 2;
+  s->ext_off = 0;
+  if (len > INLINE_KEY) {
+    const uint32_t n16 = (len - INLINE_KEY + 15) / 16;
+    unsigned long long off;
+    if (!arena_claim(t, n16, &off)) return false;
+    s->ext_off = (uint32_t)off;
+    uint32_t* ek = reinterpret_cast<uint32_t*>(t.arena + off * 16);
+    for (uint32_t k = 0; k < (len - INLINE_KEY + 3) / 4; k++) ek[k] = key.st.word(INLINE_KEY / 4 + k);
+  }
   s->key_len = (uint16_t)len;
   s->unit = (uint8_t)unit;
   s->flags = 0;
-  s->ext_off = 0;
   uint32_t* sd = reinterpret_cast<uint32_t*>(s);
 #pragma unroll
   for (uint32_t k = 0; k < INLINE_KEY / 4; k++) {
     if (k < nw) sd[slot_key_dw(k)] = key_dw(key, k);
     else if (k == nw && (il & 3)) sd[slot_key_dw(k)] = key_dw(key, k) & tail_mask(il);
   }
-  if (len > INLINE_KEY) {
-    const uint32_t n16 = (len - INLINE_KEY + 15) / 16;
-    unsigned long long off = atomicAdd(t.arena_used16, (unsigned long long)n16);
-    if (off + n16 > t.arena_cap16) {
-      atomicOr(err, ERR_ARENA_FULL);
-    } else {
-      s->ext_off = (uint32_t)off;
-      uint32_t* ek = reinterpret_cast<uint32_t*>(t.arena + off * 16);
-      for (uint32_t k = 0; k < (len - INLINE_KEY + 3) / 4; k++) ek[k] = key.st.word(INLINE_KEY / 4 + k);
-    }
-  }
   s->cur = Win{WS_INVALID, 0, 0, 0};
   s->prev = Win{WS_INVALID, 0, 0, 0};
+  return true;
 }
 
-// Find (and optionally insert) the slot of (stem, unit). Returns -1 when absent
-// and insert == false, or on a full table (error bit set). Linear probing over
-// 128-B slots from the home slot = top bits of the stem hash, i.e. of the sort
-// key: consecutive runs probe increasing slots (page and TLB locality). A tag
-// match is confirmed by the full stem (collision-exact). Inserts claim the slot
-// with a 64-bit CAS on its tag; only one lane ever handles a given (stem, unit)
-// per batch (runs are grouped by stem).
-__device__ int64_t find_slot(const TableDev& t, uint64_t hstem, uint64_t tag, const Key& key, uint32_t unit,
+// find_slot* results below 0.
+constexpr int64_t SLOT_ABSENT = -1, SLOT_TABLE_FULL = -2, SLOT_ARENA_FULL = -3;
+__device__ inline uint32_t slot_fail_status(int64_t r) {
+  return r == SLOT_ARENA_FULL ? (uint32_t)RL_E_ARENA_FULL : (uint32_t)RL_E_TABLE_FULL;
+}
+
+// Claim slot i (expected tag `from`) for (stem, unit) and initialise it.
+// 1: claimed, 0: lost the race, -1: the arena is full (the slot is a tombstone again).
+__device__ __attribute__((always_inline)) inline int slot_claim(const TableDev& t, uint64_t i, uint64_t from, uint64_t tag, const Key& key,
+                                 uint32_t unit) {
+  Slot* s = &t.slots[i];
+  if (atomicCAS((unsigned long long*)&s->tag, (unsigned long long)from, (unsigned long long)tag) != from) return 0;
+  if (slot_init(t, s, key, unit)) return 1;
+  __hip_atomic_store(&s->tag, TAG_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return -1;
+}
+
+// Find (and optionally insert) the slot of (stem, unit). Returns SLOT_ABSENT
+// when absent and insert == false, SLOT_TABLE_FULL / SLOT_ARENA_FULL (error
+// bit set in *err) when it cannot be inserted. Linear probing over 128-B slots
+// from the home slot = top bits of the stem hash, i.e. of the sort key:
+// consecutive runs probe increasing slots (page and TLB locality). A tag
+// match is confirmed by the full stem (collision-exact). Inserts claim the
+// slot with a 64-bit CAS on its tag; only one lane ever handles a given
+// (stem, unit) per batch (runs are grouped by stem).
+__device__ __attribute__((always_inline)) inline int64_t find_slot(const TableDev& t, uint64_t hstem, uint64_t tag, const Key& key, uint32_t unit,
                              bool insert, bool* inserted, uint32_t* err) {
   uint64_t i = hstem >> t.shift;
   int64_t tomb = -1;
@@ -449,27 +491,25 @@ __device__ int64_t find_slot(const TableDev& t, uint64_t hstem, uint64_t tag, co
     }
     if (st != TAG_EMPTY) continue;
     // (stem, unit) is absent: claim the first tombstone on the path, else this slot.
-    if (!insert) return -1;
-    if (tomb >= 0) {
-      Slot* ts = &t.slots[tomb];
-      if (atomicCAS((unsigned long long*)&ts->tag, (unsigned long long)TAG_TOMB, (unsigned long long)tag) ==
-          TAG_TOMB) {
-        slot_init(t, ts, key, unit, err);
-        *inserted = true;
-        return tomb;
-      }
+    if (!insert) return SLOT_ABSENT;
+    int c = tomb >= 0 ? slot_claim(t, (uint64_t)tomb, TAG_TOMB, tag, key, unit) : 0;
+    if (c > 0) {
+      *inserted = true;
+      return tomb;
     }
-    const unsigned long long prev =
-        atomicCAS((unsigned long long*)&s->tag, (unsigned long long)TAG_EMPTY, (unsigned long long)tag);
-    if (prev == TAG_EMPTY) {
-      slot_init(t, s, key, unit, err);
+    if (c == 0) c = slot_claim(t, i, TAG_EMPTY, tag, key, unit);
+    if (c > 0) {
       *inserted = true;
       return (int64_t)i;
+    }
+    if (c < 0) {
+      atomicOr(err, ERR_ARENA_FULL);
+      return SLOT_ARENA_FULL;
     }
     // another stem claimed this slot concurrently: keep probing
   }
   atomicOr(err, ERR_TABLE_FULL);
-  return -1;
+  return SLOT_TABLE_FULL;
 }
 
 // A slot image for probing: the first 64-B sector (tag, length, flags, cur,
@@ -529,7 +569,7 @@ __device__ inline bool img_key_equal(const Slot* s, const SlotImg& im, const Key
 // an insert: empty windows, no flags, second sector included). `im` holds the
 // home slot's first sector on entry (the caller issues that load early,
 // beside the stem's).
-__device__ int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint64_t tag, const Key& key, uint32_t unit,
+__device__ __attribute__((always_inline)) inline int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint64_t tag, const Key& key, uint32_t unit,
                                  bool* inserted, SlotImg& im, uint32_t* err) {
   uint64_t i = hstem >> t.shift;
   int64_t tomb = -1;
@@ -547,14 +587,15 @@ __device__ int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint64_t tag
     }
     if (st != TAG_EMPTY) continue;
     int64_t at = -1;
-    if (tomb >= 0 && atomicCAS((unsigned long long*)&t.slots[tomb].tag, (unsigned long long)TAG_TOMB,
-                               (unsigned long long)tag) == TAG_TOMB)
-      at = tomb;
-    else if (atomicCAS((unsigned long long*)&t.slots[i].tag, (unsigned long long)TAG_EMPTY,
-                       (unsigned long long)tag) == TAG_EMPTY)
-      at = (int64_t)i;
+    int c = tomb >= 0 ? slot_claim(t, (uint64_t)tomb, TAG_TOMB, tag, key, unit) : 0;
+    if (c > 0) at = tomb;
+    if (c == 0) c = slot_claim(t, i, TAG_EMPTY, tag, key, unit);
+    if (c > 0 && at < 0) at = (int64_t)i;
+    if (c < 0) {
+      atomicOr(err, ERR_ARENA_FULL);
+      return SLOT_ARENA_FULL;
+    }
     if (at >= 0) {
-      slot_init(t, &t.slots[at], key, unit, err);
       im.v[0] = make_uint4((uint32_t)tag, (uint32_t)(tag >> 32), key.len | (unit << 16), WS_INVALID);
       im.v[1] = make_uint4(0u, 0u, 0u, 0u);
       im.pv = make_uint4(WS_INVALID, 0u, 0u, 0u);
@@ -565,7 +606,7 @@ __device__ int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint64_t tag
     // another stem claimed this slot concurrently: keep probing
   }
   atomicOr(err, ERR_TABLE_FULL);
-  return -1;
+  return SLOT_TABLE_FULL;
 }
 
 // ===========================================================================
@@ -577,7 +618,6 @@ __device__ int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint64_t tag
 // wave sums go straight to rl_result.stats.
 // ===========================================================================
 constexpr uint32_t LDS_RULES = STAT_LDS_RULES;
-constexpr uint32_t MAX_REPS = 8;
 
 // Block stats table in dynamic LDS (n_rules x RL_NUM_STATS u64, n_rules <= LDS_RULES).
 extern __shared__ unsigned long long rl_sacc[];
@@ -689,13 +729,12 @@ __device__ inline Elem load_elem(const Rec& r, uint32_t e, bool restore) {
   return x;
 }
 
-// One 8-B store per descriptor: remaining | reset << 32 | code << 56, bit 62 =
-// the local-cache Get hit (k_finish counts them for the hitCount gauge).
+// One 8-B store per descriptor (pack_res): remaining, reset, code and the
+// local-cache Get hit (k_finish counts them for the hitCount gauge).
 __device__ __attribute__((always_inline)) inline void emit(unsigned long long* res, LaneStats& L, StatAcc& acc,
                                                            const Elem& x, const Decision& r, bool lc_get) {
   const uint32_t reset = x.d - x.now % x.d;  // utils.CalculateReset
-  res[x.e] = (unsigned long long)r.remaining | ((unsigned long long)reset << 32) |
-             ((unsigned long long)r.code << 56) | ((unsigned long long)lc_get << 62);
+  res[x.e] = pack_res(r.remaining, reset, r.code, lc_get);
   const uint32_t d[RL_NUM_STATS] = {x.h, r.d_over, r.d_near, r.d_lc, r.d_within, r.d_shadow};
   L.add(acc, x.rule, d);
 }
@@ -761,7 +800,8 @@ __device__ __attribute__((always_inline)) inline void simple_step(const Params& 
   }
   const uint32_t ws0 = S.cur.ws;
   const int which = window_pick(S.cur, S.prev, x.w, 0, true);
-  if (which < 0) {
+  if (which < 0) {  // older than the table's history: this descriptor's RL_E_TIME
+    if (P.isolate) res[x.e] = pack_fail(RL_E_TIME);
     if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
     return;
   }
@@ -856,6 +896,7 @@ __device__ inline void general_step(const Params& P, unsigned long long* res, La
     const uint32_t nv = restore ? x.h : v + x.h;
     const uint32_t ex = x.now + x.d;
     if (window_pick(G.cur[ui], G.prev[ui], x.w, lcw, false) < 0) {
+      if (P.isolate) res[x.e] = pack_fail(RL_E_TIME);
       if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
       return;
     }
@@ -887,11 +928,11 @@ __device__ inline void general_step(const Params& P, unsigned long long* res, La
   emit(res, L, acc, x, r, lc_hit);
 }
 
-// Replay elements [p, end) (those of stem k when repid is given) through the
+// Replay elements [p, end) (those of group k when grp is given) through the
 // single-unit slot s0, in registers.
 __device__ __attribute__((always_inline)) inline void replay_simple(SRec rec_s, const uint32_t* svals,
                                                                     unsigned long long* res, const TableDev& t,
-                                                                    const Params& P, const uint8_t* repid,
+                                                                    const Params& P, const uint32_t* grp,
                                                                     uint32_t p, uint32_t end, uint32_t k, int64_t s0,
                                                                     Win cur0, Win prev0, bool have_prev,
                                                                     const Rec& x0, uint32_t e0, LaneStats& L,
@@ -907,7 +948,7 @@ __device__ __attribute__((always_inline)) inline void replay_simple(SRec rec_s, 
   S.pend = false;
   simple_step(P, res, L, acc, S, load_elem(x0, e0, restore), restore, err);  // element p (always stem k)
   for (uint32_t q = p + 1; q < end; q++) {
-    if (repid && repid[q] != k) continue;
+    if (grp && grp[q] != k) continue;
     simple_step(P, res, L, acc, S, load_elem(rec_s[q], svals[q], restore), restore, err);
   }
   S.apply_pending();
@@ -2304,7 +2345,9 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
   b.stem_total = b.off[b.n];
   const Rec x = rec_s[q], y = rec_s[q - 1];
   const uint32_t r = rid[q];
-  const bool same = x.hlo == y.hlo && (x.lu & 0xFFFFFFu) == (y.lu & 0xFFFFFFu) &&  // hash, length, unit
+  // a failed descriptor (FLAG_SKIP) makes its run exact-path: k_runs_general leaves it out
+  const bool same = !((rec_flags(x) | rec_flags(y)) & FLAG_SKIP) && x.hlo == y.hlo &&
+                    (x.lu & 0xFFFFFFu) == (y.lu & 0xFFFFFFu) &&  // hash, length, unit
                     key_equal(key_of(b, x), key_of(b, y));
   if (!same) {
     if (!(atomicOr(&run_flags[r], RUN_MULTI) & RUN_MULTI)) defer[atomicAdd(defer_n, 1u)] = r;
@@ -2319,6 +2362,12 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
 // long uniform runs are set up for the parallel path (k_fast_*); a stem that
 // turns out to live in the table under another unit too is queued for the
 // exact path (defer2, k_runs_general after this kernel).
+// Every element of sorted positions [p, end) gets status st (isolate mode).
+__device__ inline void fail_range(unsigned long long* res, const uint32_t* svals, uint32_t p, uint32_t end,
+                                  uint32_t st) {
+  for (uint32_t q = p; q < end; q++) res[svals[q]] = pack_fail(st);
+}
+
 __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, SRec rec_s,
                                               const uint32_t* __restrict__ skeys,
                                               const uint32_t* __restrict__ svals, unsigned long long* __restrict__ res,
@@ -2328,7 +2377,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
                                               uint32_t* __restrict__ run_f, const uint32_t* num_runs,
                                               uint32_t* __restrict__ defer, uint32_t* defer_n,
                                               unsigned long long* stats, unsigned long long* stripes, uint32_t* err,
-                                              int restore, uint32_t* __restrict__ fast_blk) {
+                                              uint32_t* errs, int restore, uint32_t* __restrict__ fast_blk) {
   __shared__ uint32_t s_err, s_nr;
   // err may change while this kernel runs (other blocks): read it once per block
   if (threadIdx.x == 0) {
@@ -2338,6 +2387,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
   __syncthreads();
   if (s_err || blockIdx.x * 256 >= s_nr) return;
   b.stem_total = b.off[b.n];
+  uint32_t* ferr = P.isolate ? errs : err;  // descriptor-level failures: soft word with statuses
   const bool use_lds = !restore && b.n_rules <= LDS_RULES;
   stats_block_begin(use_lds, b.n_rules);
   StatAcc acc{use_lds, stats};
@@ -2354,7 +2404,8 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
     SlotImg im;
     load_img_lo(&t.slots[h0 >> t.shift], im);  // home slot's first sector, in flight beside the stem
     const Key k0 = key_of(b, x0);
-    if (!(fl & RUN_MULTI)) {  // RUN_MULTI runs belong to k_runs_general
+    // RUN_MULTI runs belong to k_runs_general; a run of one failed descriptor is done
+    if (!(fl & RUN_MULTI) && !(rec_flags(x0) & FLAG_SKIP)) {
       const bool long_run = !restore && end - p >= LONG_RUN && !(fl & RUN_SLOW);
       bool ok = true;
       int64_t s0 = -1;
@@ -2362,7 +2413,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
       if (RL_ABL & 1) {
         s0 = (int64_t)(h0 >> t.shift);
       } else {
-        s0 = find_slot_img(t, h0, slot_tag(h0, u0), k0, u0, &ins, im, err);
+        s0 = find_slot_img(t, h0, slot_tag(h0, u0), k0, u0, &ins, im, ferr);
         if (s0 < 0) {
           ok = false;
         } else if (im.flags() & SLOT_EXACT) {
@@ -2370,7 +2421,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
         } else if (ins) {  // new (stem, unit): the stem must not exist under another unit
           for (uint32_t u = 1; u <= 4; u++) {
             bool dummy;
-            const int64_t so = u == u0 ? -1 : find_slot(t, h0, slot_tag(h0, u), k0, u, false, &dummy, err);
+            const int64_t so = u == u0 ? -1 : find_slot(t, h0, slot_tag(h0, u), k0, u, false, &dummy, ferr);
             if (so >= 0) {  // multi-unit stem from now on: flag both before deferring
               t.slots[so].flags |= SLOT_EXACT;
               ok = false;
@@ -2388,8 +2439,11 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
         Win prev = im.hi ? im.prev() : Win{WS_INVALID, 0, 0, 0};
         const uint32_t ws0 = cur.ws;
         const int which = window_pick(cur, prev, el0.w, 0, true);
+        bool fast = true;
         if (which < 0) {
-          if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
+          if (!(RL_ABL & 1)) atomicOr(ferr, ERR_HISTORY);  // (ablation builds probe garbage slots)
+          fast = P.isolate != 0;  // every element of the run: RL_E_TIME (k_fast_emit)
+          if (fast) run_state[r] = make_uint4((uint32_t)s0, 0u, 0u, 4u);
         } else {
           const Win R = which ? prev : cur;
           // A record of window w was written inside w: its EXPIRE and local-cache
@@ -2403,6 +2457,8 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
             s->prev = prev;
           }
           run_state[r] = make_uint4((uint32_t)s0, c0, R.lc, F | ((uint32_t)which << 1));
+        }
+        if (fast) {
           run_f[r] = 0xFFFFFFFFu;
           run_flags[r] = fl | RUN_FAST;
           // mark the 256-descriptor blocks of k_fast_emit this run spans
@@ -2420,9 +2476,11 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
           sl->cur = c;
         } else {
           replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, im.cur(), im.prev(), im.hi, x0, e0, L, acc,
-                        err, restore);
+                        ferr, restore);
         }
-      } else if (!(s0 < 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_TABLE_FULL))) {
+      } else if (s0 == SLOT_TABLE_FULL || s0 == SLOT_ARENA_FULL) {
+        if (P.isolate) fail_range(res, svals, p, end, slot_fail_status(s0));  // else the batch fails
+      } else {
         defer[atomicAdd(defer_n, 1u)] = r;
       }
     }
@@ -2453,7 +2511,7 @@ __global__ __launch_bounds__(256) void k_fast_over(uint32_t n, SRec rec_s,
     r = rid[q];
     if (run_flags[r] & RUN_FAST) {
       const uint4 st = run_state[r];
-      if (!(st.w & 1u)) cand = st.y + segsum[q] > rec_s[q].limit;
+      if (!(st.w & 5u)) cand = st.y + segsum[q] > rec_s[q].limit;  // (not for a local-cache hit or failed run)
     }
   }
   uint64_t pending = __ballot(cand);
@@ -2490,10 +2548,12 @@ __global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules,
   LaneStats L;
   L.reset();
   const uint32_t q = blockIdx.x * 256 + threadIdx.x;
-  if (q < n) {
-    const uint32_t r = rid[q];
-    if (run_flags[r] & RUN_FAST) {
-      const uint4 st = run_state[r];
+  const uint32_t r = q < n ? rid[q] : 0u;
+  if (q < n && (run_flags[r] & RUN_FAST)) {
+    const uint4 st = run_state[r];
+    if (st.w & 4u) {  // the run's window is older than the key's history (isolate): RL_E_TIME
+      res[svals[q]] = pack_fail(RL_E_TIME);
+    } else {
       const uint32_t f = run_f[r];
       const bool F = st.w & 1u;
       const Elem x = load_elem(rec_s[q], svals[q], false);
@@ -2528,7 +2588,20 @@ __global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules,
 }
 
 // ---- k_runs_general: deferred runs (hash-prefix collisions, multi-unit
-// stems). Splits the run into distinct stems, then replays each exactly.
+// stems, failed descriptors). Splits the run into its distinct stems by the
+// full bytes (any number of them: correctness never depends on the hash; a
+// secret hash key keeps the count small), then replays each stem exactly.
+// Group g of run [p, end) is recorded in grp[q] for its positions; its first
+// position in lead[p + g] and its units in gmask[p + g] (a run owns its range
+// of these arrays).
+constexpr uint32_t GRP_NONE = 0xFFFFFFFFu;
+
+__device__ inline void fail_group(unsigned long long* res, const uint32_t* svals, const uint32_t* grp, uint32_t p,
+                                  uint32_t end, uint32_t g, uint32_t st) {
+  for (uint32_t q = p; q < end; q++)
+    if (grp[q] == g) res[svals[q]] = pack_fail(st);
+}
+
 __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Params P, SRec rec_s,
                                                       const uint32_t* __restrict__ skeys,
                                                       const uint32_t* __restrict__ svals,
@@ -2536,8 +2609,10 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
                                                       const uint32_t* __restrict__ run_start,
                                                       const uint32_t* __restrict__ run_end,
                                                       const uint32_t* __restrict__ defer, const uint32_t* defer_n,
-                                                      uint8_t* __restrict__ repid, unsigned long long* stats,
-                                                      unsigned long long* stripes, uint32_t* err, int restore) {
+                                                      uint32_t* __restrict__ grp, uint32_t* __restrict__ lead,
+                                                      uint8_t* __restrict__ gmask, unsigned long long* stats,
+                                                      unsigned long long* stripes, uint32_t* err, uint32_t* errs,
+                                                      int restore) {
   __shared__ uint32_t s_err, s_n;
   if (threadIdx.x == 0) {
     s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2546,6 +2621,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
   __syncthreads();
   if (s_err || blockIdx.x * 256 >= s_n) return;
   b.stem_total = b.off[b.n];
+  uint32_t* ferr = P.isolate ? errs : err;
   const bool use_lds = !restore && b.n_rules <= LDS_RULES;
   stats_block_begin(use_lds, b.n_rules);
   StatAcc acc{use_lds, stats};
@@ -2557,84 +2633,91 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
     const uint32_t rr = defer[di];  // run id
     const uint32_t p = run_start[rr], end = run_end[rr];
     const uint32_t key = skeys[p];
-    // ---- split the run into distinct stems (hash, then bytes)
-    uint32_t rep[MAX_REPS];
-    uint32_t umask[MAX_REPS];
-    uint32_t nrep = 1;
-    rep[0] = p;
-    umask[0] = 1u << (rec_unit(rec_s[p]) - 1);
-    for (uint32_t q = p + 1; q < end; q++) {
+    // ---- split the run into distinct stems (hash, length, then bytes)
+    uint32_t ng = 0;
+    for (uint32_t q = p; q < end; q++) {
       const Rec x = rec_s[q];
+      if (rec_flags(x) & FLAG_SKIP) {  // failed in validation: answered already
+        grp[q] = GRP_NONE;
+        continue;
+      }
       const Key kx = key_of(b, x);
-      uint32_t k = 0;
-      for (; k < nrep; k++) {
-        const Rec y = rec_s[rep[k]];
+      uint32_t g = 0;
+      for (; g < ng; g++) {
+        const Rec y = rec_s[lead[p + g]];
         if (y.hlo == x.hlo && rec_len(y) == rec_len(x) && key_equal(key_of(b, y), kx)) break;
       }
-      if (k == nrep) {
-        if (nrep == MAX_REPS) { atomicOr(err, ERR_COLLISIONS); k = 0; }
-        else { rep[nrep] = q; umask[nrep] = 0; nrep++; }
+      if (g == ng) {
+        lead[p + ng] = q;
+        gmask[p + ng] = 0;
+        ng++;
       }
-      repid[q] = (uint8_t)k;
-      umask[k] |= 1u << (rec_unit(x) - 1);
+      grp[q] = g;
+      gmask[p + g] |= (uint8_t)(1u << (rec_unit(x) - 1));
     }
-    for (uint32_t k = 0; k < nrep; k++) {
-      const Rec y = rec_s[rep[k]];
-      const Key stem = key_at(b, rec_s, rep[k]);
+    for (uint32_t g = 0; g < ng; g++) {
+      const uint32_t q0 = lead[p + g], um = gmask[p + g];
+      const Rec y = rec_s[q0];
+      const Key stem = key_at(b, rec_s, q0);
       const uint64_t hs = ((uint64_t)key << 32) | y.hlo;
       // ---- resolve the slot(s)
       bool simple = false;
       int64_t s0 = -1;
-      if (__popc(umask[k]) == 1) {
-        const uint32_t u0 = __ffs(umask[k]);
+      if (__popc(um) == 1) {
+        const uint32_t u0 = __ffs(um);
         bool ins;
-        s0 = find_slot(t, hs, slot_tag(hs, u0), stem, u0, true, &ins, err);
-        if (s0 < 0) break;
+        s0 = find_slot(t, hs, slot_tag(hs, u0), stem, u0, true, &ins, ferr);
+        if (s0 < 0) {
+          if (P.isolate) fail_group(res, svals, grp, q0, end, g, slot_fail_status(s0));
+          continue;
+        }
         if (!(t.slots[s0].flags & SLOT_EXACT)) {
           simple = true;
           if (ins) {  // new (stem, unit): the stem must not exist under another unit
             for (uint32_t u = 1; u <= 4 && simple; u++) {
               bool dummy;
-              if (u != u0 && find_slot(t, hs, slot_tag(hs, u), stem, u, false, &dummy, err) >= 0) simple = false;
+              if (u != u0 && find_slot(t, hs, slot_tag(hs, u), stem, u, false, &dummy, ferr) >= 0) simple = false;
             }
           }
         }
       }
       if (simple) {
-        // (the run's stem k starts at rep[k], not necessarily at p)
-        replay_simple(rec_s, svals, res, t, P, repid, rep[k], end, k, s0, t.slots[s0].cur, t.slots[s0].prev, true,
-                      rec_s[rep[k]], svals[rep[k]], L, acc, err, restore);
-      } else {
-        GeneralState G;
-        G.present = 0;
-        G.cur_req = 0xFFFFFFFFu;
-        G.npend = 0;
-        bool fail = false;
-        for (uint32_t u = 1; u <= 4; u++) {
-          bool ins;
-          G.sidx[u - 1] = find_slot(t, hs, slot_tag(hs, u), stem, u, (umask[k] >> (u - 1)) & 1, &ins, err);
-          if (G.sidx[u - 1] >= 0) {
-            G.present |= 1u << (u - 1);
-            G.cur[u - 1] = t.slots[G.sidx[u - 1]].cur;
-            G.prev[u - 1] = t.slots[G.sidx[u - 1]].prev;
-          } else if ((umask[k] >> (u - 1)) & 1) {
-            fail = true;
-          }
+        replay_simple(rec_s, svals, res, t, P, grp, q0, end, g, s0, t.slots[s0].cur, t.slots[s0].prev, true, y,
+                      svals[q0], L, acc, ferr, restore);
+        continue;
+      }
+      GeneralState G;
+      G.present = 0;
+      G.cur_req = 0xFFFFFFFFu;
+      G.npend = 0;
+      int64_t fail = 0;
+      for (uint32_t u = 1; u <= 4; u++) {
+        bool ins;
+        G.sidx[u - 1] = find_slot(t, hs, slot_tag(hs, u), stem, u, (um >> (u - 1)) & 1, &ins, ferr);
+        if (G.sidx[u - 1] >= 0) {
+          G.present |= 1u << (u - 1);
+          G.cur[u - 1] = t.slots[G.sidx[u - 1]].cur;
+          G.prev[u - 1] = t.slots[G.sidx[u - 1]].prev;
+        } else if ((um >> (u - 1)) & 1) {
+          fail = G.sidx[u - 1];
         }
-        if (fail) break;
-        for (uint32_t q = p; q < end; q++) {
-          if (((q == p) ? 0u : repid[q]) != k) continue;
-          general_step(P, res, L, acc, G, load_elem(rec_s[q], svals[q], restore), restore, err);
-        }
-        general_apply_pending(G);
-        const uint8_t fl = __popc(G.present) >= 2 ? SLOT_EXACT : 0;
-        for (uint32_t u = 0; u < 4; u++) {
-          if (!(G.present >> u & 1)) continue;
-          Slot* s = &t.slots[G.sidx[u]];
-          s->cur = G.cur[u];
-          s->prev = G.prev[u];
-          s->flags |= fl;
-        }
+      }
+      if (fail) {
+        if (P.isolate) fail_group(res, svals, grp, q0, end, g, slot_fail_status(fail));
+        continue;
+      }
+      for (uint32_t q = q0; q < end; q++) {
+        if (grp[q] != g) continue;
+        general_step(P, res, L, acc, G, load_elem(rec_s[q], svals[q], restore), restore, ferr);
+      }
+      general_apply_pending(G);
+      const uint8_t fl = __popc(G.present) >= 2 ? SLOT_EXACT : 0;
+      for (uint32_t u = 0; u < 4; u++) {
+        if (!(G.present >> u & 1)) continue;
+        Slot* s = &t.slots[G.sidx[u]];
+        s->cur = G.cur[u];
+        s->prev = G.prev[u];
+        s->flags |= fl;
       }
     }
   }
@@ -2680,10 +2763,11 @@ __global__ __launch_bounds__(256) void k_finish(const unsigned long long* __rest
   bool hit = false;
   if (ok && i < n) {
     const unsigned long long v = res[i];
-    o.code[i] = (uint8_t)((v >> 56) & 0x3Fu);
-    o.rem[i] = (uint32_t)v;
-    o.reset[i] = (uint32_t)(v >> 32) & 0xFFFFFFu;
-    hit = (v >> 62) & 1u;
+    o.code[i] = (uint8_t)res_code(v);
+    o.rem[i] = res_rem(v);
+    o.reset[i] = res_reset(v);
+    if (o.status) o.status[i] = (uint8_t)res_status(v);
+    hit = res_lc_hit(v);
   }
   if (lc_ctr && ok) {  // freecache LookupCount / HitCount (local_cache_stats.go:36-43)
     const unsigned long long w = __ballot(hit);
@@ -2725,6 +2809,24 @@ __global__ __launch_bounds__(256) void k_sweep(Slot* slots, uint64_t nslots, uin
     }
   }
   if (local) atomicAdd(evicted, (unsigned long long)local);
+}
+
+// Long-stem arena compaction (rl_sweep, after k_sweep): every live slot's
+// overflow bytes move to a fresh arena, packed from offset 0, so the space of
+// swept slots is reclaimed. Order inside the new arena does not matter (a slot
+// keeps its own offset), so a bump counter replaces a scan.
+__global__ __launch_bounds__(256) void k_arena_compact(Slot* slots, uint64_t nslots, const uint8_t* __restrict__ from,
+                                                       uint8_t* __restrict__ to, unsigned long long* used16) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * 256) {
+    Slot* s = &slots[i];
+    if (s->tag < 2 || s->key_len <= INLINE_KEY) continue;
+    const uint32_t n16 = (s->key_len - INLINE_KEY + 15) / 16;
+    const unsigned long long off = atomicAdd(used16, (unsigned long long)n16);
+    const uint4* src = reinterpret_cast<const uint4*>(from + (size_t)s->ext_off * 16);
+    uint4* dst = reinterpret_cast<uint4*>(to + off * 16);
+    for (uint32_t k = 0; k < n16; k++) dst[k] = src[k];
+    s->ext_off = (uint32_t)off;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out) {
@@ -2791,12 +2893,12 @@ static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b -
 
 // Stage A (table-free): validate, hash, sort, gather, segment. Uses only this
 // buffer's scratch and its validation word s.err.
-void launch_stage_a(const BatchDev& b, const Scratch& s, hipStream_t st, hipEvent_t* ev) {
+void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_t st, hipEvent_t* ev) {
   const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
   if (ev) (void)hipEventRecord(ev[0], st);
   if (g0)
-    k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.keys[0], s.err, s.time_floor, s.defer_n, s.big_n,
-                                  s.work_n, s.run_flags, s.num_runs, s.hit_a);
+    k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.keys[0], s.err, s.errs, isolate, s.time_floor, s.defer_n, s.big_n,
+                                  s.work_n, s.run_flags, s.num_runs, s.hit_a, s.res);
   if (ev) (void)hipEventRecord(ev[1], st);
   const uint32_t ptiles = cdiv(b.n, PART_TILE);
   if (b.n)
@@ -2839,18 +2941,18 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     (void)hipEventRecord(go, st);
     (void)hipStreamWaitEvent(side, go, 0);
     k_runs_general<<<g < RUNS_GENERAL_BLOCKS ? g : RUNS_GENERAL_BLOCKS, 256, lds, side>>>(
-        b, t, P, SRec{s.rec, s.vals[0]}, s.keys[0], s.vals[0], s.res, s.run_start, s.run_end, s.defer, s.defer_n, s.repid, o.stats, s.stripes,
-        s.errb, restore);
+        b, t, P, SRec{s.rec, s.vals[0]}, s.keys[0], s.vals[0], s.res, s.run_start, s.run_end, s.defer, s.defer_n, s.grp,
+        s.lead, s.gmask, o.stats, s.stripes, s.errb, s.errs, restore);
     (void)hipEventRecord(side_done, side);
     if (ev) (void)hipEventRecord(ev[3], st);
     k_runs<<<g, 256, lds, st>>>(b, t, P, SRec{s.rec, s.vals[0]}, s.keys[0], s.vals[0], s.res, s.run_start, s.run_end, s.run_flags,
                                 s.run_state, s.run_f, s.num_runs, s.defer2, s.defer2_n, o.stats, s.stripes, s.errb,
-                                restore, s.fast_blk);
+                                s.errs, restore, s.fast_blk);
     if (ev) (void)hipEventRecord(ev[4], st);
     // stems k_runs found under several units in the table (rare)
     k_runs_general<<<RUNS_GENERAL_LATE_BLOCKS, 256, lds, st>>>(b, t, P, SRec{s.rec, s.vals[0]}, s.keys[0], s.vals[0],
-                                                                s.res, s.run_start, s.run_end, s.defer2, s.defer2_n, s.repid, o.stats,
-                                                                s.stripes, s.errb, restore);
+                                                                s.res, s.run_start, s.run_end, s.defer2, s.defer2_n, s.grp, s.lead,
+                                                                s.gmask, o.stats, s.stripes, s.errb, s.errs, restore);
     (void)hipStreamWaitEvent(st, side_done, 0);
     if (!restore) {
       if (P.lc_en)
@@ -2889,6 +2991,11 @@ void launch_run_sums(const uint32_t* skeys, const uint32_t* w, uint32_t n, const
 
 void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st) {
   k_sweep<<<2048, 256, 0, st>>>(slots, nslots, now, evicted);
+}
+
+void launch_arena_compact(Slot* slots, uint64_t nslots, const uint8_t* from, uint8_t* to, unsigned long long* used16,
+                          hipStream_t st) {
+  k_arena_compact<<<2048, 256, 0, st>>>(slots, nslots, from, to, used16);
 }
 
 void launch_lc_count(const Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* out, hipStream_t st) {

@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void k_route_prep(BatchDev b, uint32_t n_shard
     atomicOr(err, ERR_INVALID);
   } else {
     const uint32_t* words = reinterpret_cast<const uint32_t*>(b.stem);
-    h = hash_stem(DwordReader{words + (s0 >> 2), ((total + 3u) >> 2) - (s0 >> 2)}, s0 & 3u, s1 - s0);
+    h = hash_stem(b.hk, DwordReader{words + (s0 >> 2), ((total + 3u) >> 2) - (s0 >> 2)}, s0 & 3u, s1 - s0);
   }
   dest[i] = bad ? 0u : owner_of(h, n_shards);
   idx[i] = i;
@@ -114,9 +114,10 @@ __global__ __launch_bounds__(256) void k_route_scatter(const uint32_t* __restric
   if (j >= n) return;
   const uint32_t e = perm[j];
   const unsigned long long v = ret[j];
-  o.code[e] = (uint8_t)((v >> 56) & 0x3Fu);
-  o.rem[e] = (uint32_t)v;
-  o.reset[e] = (uint32_t)(v >> 32) & 0xFFFFFFu;
+  o.code[e] = (uint8_t)res_code(v);
+  o.rem[e] = res_rem(v);
+  o.reset[e] = res_reset(v);
+  if (o.status) o.status[e] = (uint8_t)res_status(v);
 }
 
 // ---- owner side -----------------------------------------------------------

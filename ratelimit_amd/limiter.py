@@ -48,7 +48,7 @@ class FixedTimeSource(TimeSource):
 
 
 def _config(near_limit_ratio, local_cache, per_second, jitter, table_slots, max_batch, max_rules, device,
-            arena_bytes, max_stem_bytes):
+            arena_bytes, max_stem_bytes, hash_seed=0, debug_hash_bits=0):
     cfg = abi.RlConfig()
     cfg.table_slots = table_slots
     cfg.arena_bytes = arena_bytes
@@ -61,6 +61,8 @@ def _config(near_limit_ratio, local_cache, per_second, jitter, table_slots, max_
     cfg.per_second_split = 1 if per_second else 0
     cfg.device = device
     cfg.expiration_jitter_max_seconds = jitter
+    cfg.hash_seed = hash_seed
+    cfg.debug_hash_bits = debug_hash_bits
     return cfg
 
 
@@ -69,11 +71,11 @@ class Backend:
 
     def __init__(self, near_limit_ratio=0.8, local_cache=False, per_second=False, jitter=0,
                  table_slots=1 << 20, max_batch=1 << 16, max_rules=1 << 12, device=0, arena_bytes=0,
-                 max_stem_bytes=0):
+                 max_stem_bytes=0, hash_seed=0, debug_hash_bits=0):
         L = lib()
         err = C.create_string_buffer(512)
         self.cfg = _config(near_limit_ratio, local_cache, per_second, jitter, table_slots, max_batch, max_rules,
-                           device, arena_bytes, max_stem_bytes)
+                           device, arena_bytes, max_stem_bytes, hash_seed, debug_hash_bits)
         self.ctx = L.rl_create(C.byref(self.cfg), err, 512)
         if not self.ctx:
             raise RedisError(err.value.decode())
@@ -90,17 +92,22 @@ class Backend:
             pass
 
     # ---- raw packed-batch entry points
-    def do_limit_packed(self, pb: PackedBatch):
-        out = pb.alloc_result()
+    def do_limit_packed(self, pb: PackedBatch, isolate: bool = False):
+        """rl_do_limit. isolate: per-descriptor statuses (result "status"): a
+        descriptor that cannot be answered fails alone instead of the batch."""
+        out = pb.alloc_result(isolate)
         b = pb.batch_struct()
         r = abi.make_result_struct(out)
         check(self.ctx, lib().rl_do_limit(self.ctx, C.byref(b), C.byref(r)))
         n, nr = pb.n, pb.n_rules
-        return {"code": out["code"][:n], "limit_remaining": out["limit_remaining"][:n],
-                "reset_s": out["reset_s"][:n], "stats": out["stats"][:nr * abi.RL_NUM_STATS]}
+        res = {"code": out["code"][:n], "limit_remaining": out["limit_remaining"][:n],
+               "reset_s": out["reset_s"][:n], "stats": out["stats"][:nr * abi.RL_NUM_STATS]}
+        if isolate:
+            res["status"] = out["status"][:n]
+        return res
 
-    def do_limit_arrays(self, arrays, n, n_requests, n_rules):
-        return self.do_limit_packed(PackedBatch(arrays, n, n_requests, n_rules))
+    def do_limit_arrays(self, arrays, n, n_requests, n_rules, isolate: bool = False):
+        return self.do_limit_packed(PackedBatch(arrays, n, n_requests, n_rules), isolate)
 
     def do_limit_device(self, dev_in: dict, dev_out: dict, n, n_requests, n_rules, stream=None):
         """All arrays are torch CUDA tensors (device memory); asynchronous."""
@@ -241,15 +248,26 @@ class GpuRateLimitCache:
         """fixedRateLimitCacheImpl.DoLimit semantics for one request."""
         return self.do_limit_batch([(request, limits, self.time_source.unix_now())])[0]
 
-    def do_limit_batch(self, calls) -> List[List[DescriptorStatus]]:
-        """Many in-flight DoLimit calls (request, limits, now) as one GPU batch, in arrival order."""
+    def do_limit_batch(self, calls, isolate: bool = False) -> list:
+        """Many in-flight DoLimit calls (request, limits, now) as one GPU batch, in arrival order.
+
+        isolate=False: any failure raises RedisError for the whole batch.
+        isolate=True: a call holding a descriptor the backend could not answer
+        gets a RedisError object in place of its statuses (the batcher panics
+        that RPC only, as checkError does per DoLimit, fixed_cache_impl.go:90-95);
+        every other call is answered."""
         pb = pack_calls(calls, self.prefix, self.interner)
-        res = self.backend.do_limit_packed(pb)
+        res = self.backend.do_limit_packed(pb, isolate)
         outs = [[DescriptorStatus(OK, None, 0, None) for _ in req.descriptors] for req, _, _ in calls]
         code, rem, rst = res["code"], res["limit_remaining"], res["reset_s"]
+        failed = {}
         for j, (c, i) in enumerate(pb.origin):
             lim = calls[c][1][i]
+            if isolate and res["status"][j]:
+                failed.setdefault(c, int(res["status"][j]))
             outs[c][i] = DescriptorStatus(int(code[j]), lim.limit, int(rem[j]), int(rst[j]))
+        for c, st in failed.items():
+            outs[c] = RedisError("gpu: descriptor failed [%s]" % abi.STATUS_NAMES.get(st, st))
         st = res["stats"].reshape(-1, abi.RL_NUM_STATS)
         # apply the per-rule deltas to the gostats counters (limit.Stats)
         seen = {}

@@ -52,11 +52,14 @@ class PackedBatch:
     def batch_struct(self):
         return abi.make_batch_struct(self.arrays, self.n, self.n_requests, self.n_rules)
 
-    def alloc_result(self):
-        return {"code": np.zeros(max(self.n, 1), np.uint8),
-                "limit_remaining": np.zeros(max(self.n, 1), np.uint32),
-                "reset_s": np.zeros(max(self.n, 1), np.uint32),
-                "stats": np.zeros(max(self.n_rules, 1) * abi.RL_NUM_STATS, np.uint64)}
+    def alloc_result(self, isolate: bool = False):
+        out = {"code": np.zeros(max(self.n, 1), np.uint8),
+               "limit_remaining": np.zeros(max(self.n, 1), np.uint32),
+               "reset_s": np.zeros(max(self.n, 1), np.uint32),
+               "stats": np.zeros(max(self.n_rules, 1) * abi.RL_NUM_STATS, np.uint64)}
+        if isolate:
+            out["status"] = np.zeros(max(self.n, 1), np.uint8)
+        return out
 
 
 def arrays_from_lists(stems: List[bytes], now: Sequence[int], req_idx, unit, flags, limit, hits,

@@ -64,6 +64,8 @@ class DeviceRouteOps:
     """The device halves of the exchange, through the C ABI (rl_route_*)."""
 
     def __init__(self, backend):
+        if not backend.cfg.hash_seed:
+            raise ValueError("a sharded table needs an explicit hash_seed shared by every shard (owner = stem hash)")
         self.be = backend
         self.device = torch.device("cuda", backend.cfg.device)
         # One explicit stream for the library kernels AND the collectives (a NULL

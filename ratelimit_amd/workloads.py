@@ -77,6 +77,45 @@ def c1_batch(tenants, now, hits=None):
 C1_RULES = ["bench.tenant.tier_sec", "bench.tenant.tier_min"]
 
 
+def c1_batch_dev(tenants, now, hits=None, device="cuda"):
+    """c1_batch built on the GPU with torch (same bytes, same arrays): used to
+    fill 10^8-key tables (BASELINE C3) without host-side generation. ``tenants``
+    is an int64 tensor (or array); uint32 arrays come back as int32 tensors of
+    the same bits, ready for Backend.do_limit_device."""
+    import torch
+    t = torch.as_tensor(tenants, dtype=torch.int64, device=device)
+    nq = t.numel()
+    n = 2 * nq
+    pre = torch.tensor(list(b"bench_tenant_t"), dtype=torch.uint8, device=device)
+    sec = torch.tensor(list(b"_tier_sec_"), dtype=torch.uint8, device=device)
+    mn = torch.tensor(list(b"_tier_min_"), dtype=torch.uint8, device=device)
+    L = pre.numel() + 10 + sec.numel()
+    dig = torch.empty((nq, 10), dtype=torch.uint8, device=device)
+    v = t.clone()
+    for k in range(9, -1, -1):
+        dig[:, k] = (v % 10 + 48).to(torch.uint8)
+        v = v // 10
+    rec = torch.empty((nq, 2, L), dtype=torch.uint8, device=device)
+    rec[:, :, :pre.numel()] = pre
+    rec[:, :, pre.numel():pre.numel() + 10] = dig[:, None, :]
+    rec[:, 0, pre.numel() + 10:] = sec
+    rec[:, 1, pre.numel() + 10:] = mn
+    i32 = dict(dtype=torch.int32, device=device)
+    h = torch.ones(nq, **i32) if hits is None else torch.as_tensor(hits, device=device).to(torch.int32)
+    return {
+        "stem_bytes": rec.reshape(-1),
+        "stem_off": torch.arange(n + 1, **i32) * L,
+        "now": (torch.full((nq,), int(now), dtype=torch.int64, device=device) if np.ndim(now) == 0
+                else torch.as_tensor(now, dtype=torch.int64, device=device)),
+        "req_idx": torch.arange(nq, **i32).repeat_interleave(2),
+        "unit": torch.tensor([1, 2], dtype=torch.uint8, device=device).repeat(nq),
+        "flags": torch.zeros(n, dtype=torch.uint8, device=device),
+        "limit": torch.tensor([100, 3000], **i32).repeat(nq),
+        "hits": h.repeat_interleave(2),
+        "rule_id": torch.tensor([0, 1], **i32).repeat(nq),
+    }, n, nq, 2
+
+
 def c1_stream(seed=0xC1, n_tenants=10_000_000, requests_per_batch=500_000, batches=4, now0=NOW0):
     rng = np.random.default_rng(seed)
     for k in range(batches):

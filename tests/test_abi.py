@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
     for f in declared_functions():
         assert hasattr(lib, f), f
     lib.rl_abi_version.restype = C.c_uint32
-    assert lib.rl_abi_version() == 1
+    assert lib.rl_abi_version() == abi.ABI_VERSION
 
 
 def test_product_loader_lists_all_exports():
@@ -47,9 +47,9 @@ def test_product_loader_lists_all_exports():
 
 def test_struct_layout_matches_header():
     # sizes as laid out by the C compiler for include/ratelimit_hip.h (x86-64 / gfx950 host)
-    assert C.sizeof(abi.RlConfig) == 8 + 8 + 4 * 4 + 4 + 4 * 3 + 8 + 4 * 8
+    assert C.sizeof(abi.RlConfig) == 8 + 8 + 4 * 4 + 4 + 4 * 3 + 8 + 8 + 4 + 4 + 4 * 16 + 4 * 8
     assert C.sizeof(abi.RlBatch) == 16 + 9 * 8
-    assert C.sizeof(abi.RlResult) == 4 * 8
+    assert C.sizeof(abi.RlResult) == 5 * 8
     assert C.sizeof(abi.RlRestoreBatch) == 8 + 6 * 8
 
 
@@ -87,6 +87,19 @@ def test_c1_workload_shape():
     s = bytes(a["stem_bytes"][a["stem_off"][3]:a["stem_off"][4]])
     assert s == b"bench_tenant_t0000000007_tier_min_"
     assert list(a["unit"]) == [1, 2, 1, 2] and list(a["req_idx"]) == [0, 0, 1, 1]
+
+
+def test_c1_device_generator_equals_host_generator():
+    """c1_batch_dev (torch, used to fill C3-sized tables on the GPU) builds the
+    same bytes and arrays as c1_batch; checked here on the CPU device."""
+    t = np.array([0, 1234, 9_999_999_999, 62_499_999], np.int64)
+    h = np.array([1, 2, 3, 8], np.uint32)
+    a, n, nq, nr = workloads.c1_batch(t, 1_700_000_000, h)
+    d, dn, dq, dr = workloads.c1_batch_dev(t, 1_700_000_000, h, device="cpu")
+    assert (n, nq, nr) == (dn, dq, dr)
+    for k, v in a.items():
+        got = d[k].numpy()
+        assert np.array_equal(got.view(v.dtype) if got.dtype != v.dtype else got, v), k
 
 
 def test_concat_batches_rebases():

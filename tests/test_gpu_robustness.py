@@ -1,0 +1,234 @@
+"""GPU robustness: correctness never depends on the stem hash; one descriptor
+the backend cannot answer fails alone (per-descriptor statuses); the long-stem
+arena is reclaimed by the sweep; the hash key travels with snapshots.
+
+* Hash collisions: the test knob debug_hash_bits keeps only the top few bits of
+  the hash's high word, so hundreds of distinct stems share one 32-bit sort key
+  and one home region of the table. Answers must equal the oracle's.
+* Failure isolation (rl_result.status): in the reference an error fails only the
+  DoLimit call that hit it (checkError per call, src/redis/fixed_cache_impl.go:
+  90-95; panic mapped per RPC, src/service/ratelimit.go:252-256). A bad unit,
+  rule id or clock, or a window older than a key's history, must leave every
+  other answer of the batch oracle-exact.
+"""
+import numpy as np
+import pytest
+
+from oracle import c_oracle
+from ratelimit_amd import abi, workloads
+from ratelimit_amd.limiter import Backend, GpuRateLimitCache, RedisError
+import golden_util as G
+import streams
+
+pytestmark = pytest.mark.gpu
+
+SMALL = dict(table_slots=1 << 16, max_batch=1 << 15, max_rules=1 << 10)
+
+
+def _run(calls, chunks, **kw):
+    streams.reset_stats(calls)
+    cache = GpuRateLimitCache(None, 0.8, kw.pop("lc", False), "", kw.pop("ps", False), **kw)
+    outs = []
+    try:
+        i = 0
+        for k in chunks:
+            outs += cache.do_limit_batch(calls[i:i + k])
+            i += k
+    finally:
+        cache.close()
+    stats = {}
+    for _, limits, _ in calls:
+        for l in limits:
+            if l is not None:
+                stats[l.stats.key] = tuple(getattr(l.stats, f) for f in abi.STAT_FIELDS)
+    return outs, stats
+
+
+@pytest.mark.parametrize("bits", [1, 4, 9])
+@pytest.mark.parametrize("lc", [False, True])
+def test_gpu_colliding_sort_keys_vs_python_oracle(bits, lc):
+    calls = streams.random_stream(100 + bits, n_calls=500, n_stems=300, zipf=True)
+    py_out, py_stats = streams.python_oracle_run(calls, 0.8, lc, "", False)
+    outs, stats = _run(calls, [100, 1, 150, 249], lc=lc, debug_hash_bits=bits, **SMALL)
+    got = [[G.status_tuple(s) for s in o] for o in outs]
+    exp = [[s.as_tuple() for s in o] for o in py_out]
+    for i, (g, e) in enumerate(zip(got, exp)):
+        assert g == e, "call %d: gpu %s oracle %s" % (i, g, e)
+    assert stats == py_stats
+
+
+def test_gpu_colliding_sort_keys_c2_vs_c_oracle():
+    """Zipf batches where ~40 distinct stems share each of 1024 sort keys (runs
+    with hot keys AND many colliding stems: the exact path at scale)."""
+    z = workloads.ZipfSampler(20_000, 1.1)
+    batches = list(workloads.c2_stream(n_tenants=20_000, requests_per_batch=10_000, batches=3, sampler=z))
+    for lc in (False, True):
+        be = Backend(0.8, lc, table_slots=1 << 17, max_batch=1 << 15, max_rules=8, debug_hash_bits=10)
+        co = c_oracle.COracle(0.8, lc)
+        for a, n, nq, nr in batches:
+            g = be.do_limit_arrays(a, n, nq, nr)
+            o = co.do_limit(a, n, nq, nr)
+            for k in ("code", "limit_remaining", "reset_s", "stats"):
+                assert np.array_equal(g[k], o[k]), k
+        be.close()
+        co.close()
+
+
+def test_gpu_hash_seed_does_not_change_answers_and_travels_with_snapshots():
+    z = workloads.ZipfSampler(5_000, 1.1)
+    batches = list(workloads.c2_stream(n_tenants=5_000, requests_per_batch=4_000, batches=4, sampler=z))
+    co = c_oracle.COracle(0.8, True)
+    want = [co.do_limit(*b) for b in batches]
+    co.close()
+    a1 = Backend(0.8, True, hash_seed=1, **SMALL)
+    a2 = Backend(0.8, True, hash_seed=0xDEADBEEF12345, **SMALL)
+    for b, w in zip(batches[:2], want[:2]):
+        for be in (a1, a2):
+            g = be.do_limit_arrays(*b)
+            for k in w:
+                assert np.array_equal(g[k], w[k]), k
+    snap = a1.snapshot()
+    a3 = Backend(0.8, True, hash_seed=7, **SMALL)  # adopts the snapshot's key
+    a3.load_snapshot(snap)
+    for b, w in zip(batches[2:], want[2:]):
+        g = a3.do_limit_arrays(*b)
+        for k in w:
+            assert np.array_equal(g[k], w[k]), k
+    for be in (a1, a2, a3):
+        be.close()
+
+
+# --------------------------------------------------------------------------- failure isolation
+def _drop(a, n, nq, keep):
+    """The packed batch without the descriptors where keep is False."""
+    idx = np.nonzero(keep[:n])[0]
+    off = a["stem_off"]
+    stems = [a["stem_bytes"][off[i]:off[i + 1]] for i in idx]
+    o = np.zeros(idx.size + 1, np.uint32)
+    o[1:] = np.cumsum([s.size for s in stems])
+    out = {"stem_bytes": np.concatenate(stems) if stems else np.zeros(4, np.uint8), "stem_off": o,
+           "now": a["now"]}
+    for k in ("req_idx", "unit", "flags", "limit", "hits", "rule_id"):
+        out[k] = a[k][idx]
+    return out, idx.size, nq
+
+
+@pytest.mark.parametrize("lc", [False, True])
+def test_gpu_one_bad_descriptor_fails_alone(lc):
+    z = workloads.ZipfSampler(3_000, 1.1)
+    (a, n, nq, nr), = workloads.c2_stream(n_tenants=3_000, requests_per_batch=4_000, batches=1, sampler=z)
+    bad = {k: v.copy() for k, v in a.items()}
+    bad["unit"][7] = 9                          # unknown unit
+    bad["rule_id"][1001] = 99                   # rule id >= n_rules
+    bad["now"][2500] = -5                       # clock out of range: both descriptors of request 2500
+    be = Backend(0.8, lc, **SMALL)
+    with pytest.raises(RedisError, match="RL_E_(INVALID|TIME)"):  # without statuses the batch fails
+        be.do_limit_arrays(bad, n, nq, nr)
+    g = be.do_limit_arrays(bad, n, nq, nr, isolate=True)
+    failed = np.zeros(n, bool)
+    failed[[7, 1001, 5000, 5001]] = True
+    st = g["status"]
+    assert st[7] == abi.RL_E_INVALID and st[1001] == abi.RL_E_INVALID
+    assert st[5000] == abi.RL_E_TIME and st[5001] == abi.RL_E_TIME
+    assert (st[~failed] == 0).all() and (g["code"][failed] == 0).all()
+    co = c_oracle.COracle(0.8, lc)
+    o = co.do_limit(*_drop(bad, n, nq, ~failed), nr)
+    co.close()
+    for k in ("code", "limit_remaining", "reset_s"):
+        assert np.array_equal(g[k][~failed], o[k]), k
+    assert np.array_equal(g["stats"], o["stats"])
+    be.close()
+
+
+def test_gpu_history_miss_fails_alone():
+    """Per (stem, unit) the table keeps two windows; a request older than both
+    gets RL_E_TIME for that descriptor only: on a short run, on a long run
+    (the parallel path), and through the per-call API."""
+    be = Backend(0.8, False, **SMALL)
+    co = c_oracle.COracle(0.8, False)
+    t0 = workloads.NOW0
+    for k in (0, 1):  # SECOND windows t0, t0+1 of tenants 0..99
+        b = workloads.c1_batch(np.arange(100), t0 + k)
+        be.do_limit_arrays(*b, isolate=True)
+        co.do_limit(*b)
+    # tenants 0 (x1) and 1 (x40: a long run) at t0 - 1, among fresh tenants at t0 + 1
+    ten = np.r_[np.arange(200, 300), [0], np.full(40, 1), np.arange(300, 400)]
+    now = np.r_[np.full(100, t0 + 1), np.full(41, t0 - 1), np.full(100, t0 + 1)]
+    a, n, nq, nr = workloads.c1_batch(ten, now)
+    g = be.do_limit_arrays(a, n, nq, nr, isolate=True)
+    failed = np.zeros(n, bool)
+    failed[200:282:2] = True  # the SECOND descriptors of requests 100..140
+    assert (g["status"][failed] == abi.RL_E_TIME).all() and (g["status"][~failed] == 0).all()
+    o = co.do_limit(*_drop(a, n, nq, ~failed), nr)
+    for k in ("code", "limit_remaining", "reset_s"):
+        assert np.array_equal(g[k][~failed], o[k]), k
+    assert np.array_equal(g["stats"], o["stats"])
+    be.close()
+    co.close()
+
+
+def test_gpu_cache_isolates_failed_calls():
+    from oracle import oracle as O
+    reg = {}
+
+    def L(rpu, unit, key):
+        reg.setdefault(key, O.RateLimitStats(key))
+        return O.RateLimit(key, reg[key], O.Limit(rpu, unit))
+
+    t = 1_700_000_030
+    mk = lambda v, now: (O.RateLimitRequest("d", [O.Descriptor([("k", v)])], 1), [L(5, O.SECOND, "s")], now)
+    cache = GpuRateLimitCache(None, **SMALL)
+    cache.do_limit_batch([mk("a", t), mk("a", t + 1)])
+    outs = cache.do_limit_batch([mk("b", t + 1), mk("a", t - 1), mk("a", t + 1)], isolate=True)
+    # b@t+1: first hit; a@t-1: older than a's windows {t, t+1}: its call alone fails; a@t+1: second hit
+    assert isinstance(outs[1], RedisError) and "RL_E_TIME" in str(outs[1])
+    assert outs[0][0].code == 1 and outs[0][0].limit_remaining == 4
+    assert outs[2][0].code == 1 and outs[2][0].limit_remaining == 3
+    cache.close()
+
+
+# --------------------------------------------------------------------------- arena and fast-path blocks
+def test_gpu_arena_reclaimed_by_sweep():
+    """stems longer than 80 B take arena space; the sweep's
+    compaction must return it, so inserting, sweeping and re-inserting far more
+    long stems than the arena holds never fails."""
+    from oracle import oracle as O
+    be = Backend(0.8, False, table_slots=1 << 14, max_batch=1 << 12, max_rules=4, arena_bytes=64 << 10)
+    reg = {"r": O.RateLimitStats("r")}
+    cache_prefix = "x" * 150
+    t = 1_700_000_000
+    for rnd in range(8):  # 8 x 400 stems x 5 units of 16 B = 4x the 64 KiB arena
+        calls = [(O.RateLimitRequest(cache_prefix, [O.Descriptor([("k", "r%d_%d" % (rnd, i))])], 1),
+                  [O.RateLimit("r", reg["r"], O.Limit(5, O.SECOND))], t) for i in range(400)]
+        from ratelimit_amd.packing import RuleInterner, pack_calls
+        pb = pack_calls(calls, "", RuleInterner())
+        g = be.do_limit_packed(pb)
+        assert (g["limit_remaining"] == 4).all()
+        lens = np.diff(pb.arrays["stem_off"].astype(np.int64))
+        assert be.table_info()["arena_bytes_used"] == int(((lens - 80 + 15) // 16 * 16).sum())
+        t += 5
+        assert be.sweep(t) == 400
+        assert be.table_info()["arena_bytes_used"] == 0
+    be.close()
+
+
+def test_gpu_long_runs_across_fast_blocks_vs_c_oracle():
+    """k_fast_emit skips 256-position blocks without a long run (a
+    bitmap set by k_runs). Hundreds of long runs (33..120 descriptors) among
+    singletons land across 256-block and 32-block-word boundaries."""
+    rng = np.random.default_rng(3)
+    hot = np.repeat(np.arange(300), rng.integers(33, 121, 300))
+    for seed in range(3):
+        r = np.random.default_rng(seed)
+        ten = r.permutation(np.r_[hot, 1000 + r.integers(0, 1_000_000, 20_000)])
+        batches = [workloads.c1_batch(ten, workloads.NOW0 + k) for k in range(2)]
+        for lc in (False, True):
+            be = Backend(0.8, lc, table_slots=1 << 18, max_batch=1 << 17, max_rules=8)
+            co = c_oracle.COracle(0.8, lc)
+            for b in batches:
+                g = be.do_limit_arrays(*b)
+                o = co.do_limit(*b)
+                for k in ("code", "limit_remaining", "reset_s", "stats"):
+                    assert np.array_equal(g[k], o[k]), (seed, lc, k)
+            be.close()
+            co.close()

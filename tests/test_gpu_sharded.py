@@ -44,7 +44,7 @@ def _worker(rank, world, port, backend, batches, cfg, q):
         dist.init_process_group(backend, rank=rank, world_size=world)
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        be = Backend(*cfg, table_slots=1 << 18, max_batch=1 << 15, max_rules=64, device=0)
+        be = Backend(*cfg, table_slots=1 << 18, max_batch=1 << 15, max_rules=64, device=0, hash_seed=0x5EED)
         sc = ShardedRateLimitCache(DeviceRouteOps(be), Exchange(), max_batch=1 << 15, max_stem_bytes=1 << 21,
                                    device=dev)
         res = []
