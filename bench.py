@@ -51,10 +51,13 @@ def parse():
     ap.add_argument("--prof-every", type=int, default=7,
                     help="time every k-th batch's stages with HIP events (k_runs' live time for the roofline)")
     ap.add_argument("--no-fill", action="store_true")
+    ap.add_argument("--slots-per-key", type=float, default=4.0, help="table slots per live key (power of 2 above)")
     ap.add_argument("--route", action="store_true", help="use the routed (all_to_all) path even at N=1")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + --one-device: rehearse N ranks on one GPU (host-staged exchange)")
     ap.add_argument("--one-device", action="store_true", help="every rank uses cuda:0 (rehearsal only)")
+    ap.add_argument("--serial", action="store_true",
+                    help="submit every batch on one stream, unpipelined (isolated per-kernel times for profiling)")
     args = ap.parse_args()
     if not args.tenants:
         args.tenants = 62_500_000 if args.config == "c3" else 10_000_000
@@ -100,7 +103,9 @@ def main():
     n = 2 * nq
     T = args.tenants
     keys_per_gpu = 2 * T
-    slots = 1 << max(16, int(np.ceil(np.log2(2 * keys_per_gpu))))
+    # Table at <= 25% load: HBM is plentiful (288 GB) and every extra linear
+    # probe is one more random 64-B sector read (tools/slotprobe.hip).
+    slots = 1 << max(16, int(np.ceil(np.log2(args.slots_per_key * keys_per_gpu))))
     # a routed owner receives ~n descriptors (binomial spread across sources)
     cap = n if not routed else int(n * 1.05) + 4096
     seed = 0
@@ -122,11 +127,14 @@ def main():
            "reset_s": torch.empty(n, dtype=torch.int32, device="cuda"),
            "stats": torch.zeros(2 * 6, dtype=torch.int64, device="cuda")}
 
+    serial_torch_stream = torch.cuda.Stream() if args.serial else None  # (the default stream's handle is NULL)
+    serial_stream = serial_torch_stream.cuda_stream if args.serial else None
+
     def do_step(inp, bn, bq):
         if routed:
             sc.do_limit(inp, bn, bq, 2, out)
         else:
-            be.do_limit_device(inp, out, bn, bq, 2)
+            be.do_limit_device(inp, out, bn, bq, 2, stream=serial_stream)
 
     # ---- fill: every key of the node's tenant space (rank r inserts tenants
     # [r*T, (r+1)*T); routed batches land on their owners). Not timed.
@@ -175,7 +183,7 @@ def main():
     # ---- timed region: exactly K steps. The library records HIP events at the
     # stage boundaries on each batch's own stream (pipelined batches are timed
     # as they run, k_runs included: the roofline's kernel time).
-    be.profile(True, args.prof_every)
+    be.profile(args.prof_every > 0, args.prof_every)
     be.profile_read()
     recv = []
     barrier()

@@ -269,13 +269,15 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
   ok = ok && dalloc(&s.grp, n) == hipSuccess && dalloc(&s.lead, n) == hipSuccess && dalloc(&s.gmask, n) == hipSuccess &&
        dalloc(&s.defer, n) == hipSuccess &&
        dalloc(&s.defer_n, 1) == hipSuccess && dalloc(&s.defer2, n) == hipSuccess &&
+       dalloc(&s.defer1, n) == hipSuccess && dalloc(&s.defer1_n, 1) == hipSuccess &&
        dalloc(&s.defer2_n, 1) == hipSuccess && dalloc(&s.fast_blk, (size_t)n / (256 * 32) + 1) == hipSuccess;
   ok = ok && dalloc(&s.tile_f, nt) == hipSuccess && dalloc(&s.tile_s, nt) == hipSuccess &&
        dalloc(&s.tile_h, nt) == hipSuccess;
   ok = ok && dalloc(&s.hits_s, n) == hipSuccess && dalloc(&s.segsum, n) == hipSuccess &&
        dalloc(&s.rid, n) == hipSuccess && dalloc(&s.run_start, (size_t)n + 1) == hipSuccess &&
        dalloc(&s.run_flags, n) == hipSuccess && dalloc(&s.run_state, n) == hipSuccess &&
-       dalloc(&s.run_f, n) == hipSuccess && dalloc(&s.num_runs, 1) == hipSuccess;
+       dalloc(&s.run_f, n) == hipSuccess && dalloc(&s.num_runs, 1) == hipSuccess &&
+       dalloc(&s.runs64, 1) == hipSuccess && dalloc(&s.drun, (size_t)n / 2 + BIG_HEAVY * PART_DIGITS) == hipSuccess;
   ok = ok && dalloc(&s.hit_a, n) == hipSuccess && dalloc(&s.tile, n) == hipSuccess &&
        dalloc(&s.hit_t, n) == hipSuccess;
   ok = ok && dalloc(&s.run_end, n) == hipSuccess &&
@@ -285,8 +287,8 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
 
 void free_buffer(Scratch& s) {
   void* bufs[] = {s.rec, s.res, s.big_meta, s.big_n, s.big_work, s.work_n, s.big_cnt, s.keys[0], s.keys[1], s.vals[0], s.vals[1], s.hist,
-                  s.hist_tot, s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.fast_blk, s.tile_f, s.tile_s, s.tile_h, s.hits_s, s.segsum, s.rid,
-                  s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t};
+                  s.hist_tot, s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1, s.defer1_n, s.fast_blk, s.tile_f, s.tile_s, s.tile_h, s.hits_s, s.segsum, s.rid,
+                  s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs, s.runs64, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
 }

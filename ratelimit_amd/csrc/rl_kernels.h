@@ -24,7 +24,7 @@ constexpr uint32_t BIG_HEAVY = 4;                                   // hot keys 
 
 // A bucket too large for k_bucket's LDS, queued with its sampled hot keys.
 struct BigMeta {
-  uint32_t d, S, base, nchunks, item0, r, rb_heavy, pad;
+  uint32_t d, S, base, nchunks, item0, r, rb_heavy, db_heavy;
   uint32_t heavy[BIG_HEAVY];
 };
 constexpr uint32_t MAX_PART_TILES = 2048;  // k_part tiles per batch (max_batch <= 2048 x 4096)
@@ -154,6 +154,8 @@ struct Scratch {
   uint32_t* defer_n;
   uint32_t* defer2;               // runs k_runs found to need the exact path, for k_runs_general after it
   uint32_t* defer2_n;
+  uint32_t* defer1;               // singletons k_unique found to need the exact path (arrival indices)
+  uint32_t* defer1_n;
   uint32_t* fast_blk;             // bit per 256-descriptor block holding a RUN_FAST run (k_runs -> k_fast_emit)
   unsigned long long* stripes;    // STAT_STRIPES x STAT_LDS_RULES x RL_NUM_STATS
   // run segmentation (sorted order)
@@ -170,7 +172,9 @@ struct Scratch {
   uint32_t* run_flags;                 // [n] RUN_*
   uint4* run_state;                    // [n] {slot, c0, old lc, F | which<<1}
   uint32_t* run_f;                     // [n] first over-limit position
-  uint32_t* num_runs;
+  uint32_t* num_runs;                  // routing partition (launch_run_sums)
+  unsigned long long* runs64;          // bucket path: runs | runs of two or more << 32
+  uint32_t* drun;                      // [n/2 + BIG_HEAVY x PART_DIGITS] ids of the runs of two or more
   uint32_t* err;   // validation word of this buffer's batch (stage A)
   uint32_t* errb;  // sticky table-stage word (stage B), shared by both buffers
   uint32_t* errs;  // soft word: descriptor errors answered by statuses (isolate mode)

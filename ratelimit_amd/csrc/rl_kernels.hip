@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
                                                  uint32_t* err, uint32_t* errs, int isolate,
                                                  const int64_t* time_floor, uint32_t* defer_n,
                                                  uint32_t* big_n, uint32_t* work_n, uint32_t* __restrict__ run_flags,
-                                                 uint32_t* num_runs, uint32_t* __restrict__ hit_a,
+                                                 unsigned long long* num_runs, uint32_t* __restrict__ hit_a,
                                                  unsigned long long* __restrict__ res) {
   __shared__ uint32_t lds[HASH_LDS_BYTES / 4 + 4];
   const uint32_t tid = threadIdx.x;
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   Rec r;
   r.hlo = (uint32_t)h;
   r.off = s0;
-  r.lu = len | (u << 16) | ((uint32_t)((b.flags[i] & 0x7Fu) | (dstat ? FLAG_SKIP : 0u)) << 24);
+  r.lu = len | (u << 16) | ((uint32_t)((b.flags[i] & RL_FLAG_SHADOW) | (dstat ? FLAG_SKIP : 0u)) << 24);
   r.rule = b.rule[i];
   r.req = q;
   r.now = b.now_desc ? (uint32_t)b.now[i] : (q < b.n_req) ? (uint32_t)b.now[q] : 0u;
@@ -724,7 +724,7 @@ __device__ inline Elem load_elem(const Rec& r, uint32_t e, bool restore) {
   x.h = restore ? r.hits : (r.hits > 1 ? r.hits : 1u);  // utils.Max(1, HitsAddend)
   x.thr = r.limit;
   x.rule = r.rule;
-  x.flags = (uint8_t)rec_flags(r);
+  x.flags = (uint8_t)(rec_flags(r) & RL_FLAG_SHADOW);  // (restore records: the local-cache bit)
   x.shadow = (x.flags & RL_FLAG_SHADOW) != 0;
   return x;
 }
@@ -1325,7 +1325,7 @@ struct BucketLds {
   SegPair sp[B::WAVES];
   uint32_t sh[B::WAVES];
   SegPair carry;
-  uint32_t hcarry, rb, nruns, S, base_pos;
+  uint32_t hcarry, rb, nruns, S, base_pos, db, dcnt;
   // large buckets: heavy keys peeled off (bucket_peel)
   uint32_t heavy[BK_HEAVY];           // sampled heavy keys (class c)
   uint32_t hcnt[BK_HEAVY];            // elements per class
@@ -1517,31 +1517,38 @@ __device__ inline void bucket_segment(BucketLds<B>& L, uint32_t d, uint32_t S, u
                                       const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sh,
                                       uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
                                       uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end,
-                                      uint32_t* num_runs) {
+                                      unsigned long long* num_runs, uint32_t* __restrict__ drun) {
   constexpr uint32_t IT = B::ITEMS;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   auto key = [&](uint32_t p) -> uint32_t { return FROM_LDS ? L.k[p] : sk[base + p]; };
   auto hit = [&](uint32_t p) -> uint32_t { return FROM_LDS ? L.h[p] : sh[base + p]; };
-  // runs of the bucket -> run id base
-  uint32_t nh = 0;
+  // runs of the bucket -> run id base; runs of two or more (counted at their
+  // second element) -> their place in the dup-run list k_runs works through
+  uint32_t nh = 0, nd = 0;
   for (uint32_t c0 = 0; c0 < S; c0 += B::CAP) {
-    uint32_t a[IT], b[IT];
+    uint32_t a[IT], b[IT], c[IT];
 #pragma unroll
     for (uint32_t i = 0; i < IT; i++) {
       const uint32_t p = min(c0 + i * B::THREADS + tid, S - 1);
       a[i] = key(p ? p - 1 : 0);
       b[i] = key(p);
+      c[i] = key(p > 1 ? p - 2 : 0);
     }
 #pragma unroll
     for (uint32_t i = 0; i < IT; i++) {
       const uint32_t p = c0 + i * B::THREADS + tid;
       nh += (p < S && (p == 0 || a[i] != b[i])) ? 1u : 0u;
+      nd += (p < S && p >= 1 && a[i] == b[i] && (p == 1 || c[i] != a[i])) ? 1u : 0u;
     }
   }
   nh = block_sum(L, nh);
+  nd = block_sum(L, nd);
   BK_STAMP(d, 4);
   if (tid == 0) {
-    L.rb = atomicAdd(num_runs, nh);
+    const unsigned long long old = atomicAdd(num_runs, ((unsigned long long)nd << 32) | nh);
+    L.rb = (uint32_t)old;
+    L.db = (uint32_t)(old >> 32);
+    L.dcnt = 0;
     L.nruns = nh;
     L.carry = SegPair{0, 0};
     L.hcarry = 0;
@@ -1554,19 +1561,21 @@ __device__ inline void bucket_segment(BucketLds<B>& L, uint32_t d, uint32_t S, u
     SegChunk ch[IT];
     SegPair agg{0, 0};
     uint32_t hc = 0;
-    uint32_t kp[IT], kq[IT], hq[IT];
+    uint32_t kp[IT], kq[IT], hq[IT], kpp[IT];
 #pragma unroll
     for (uint32_t j = 0; j < IT; j++) {
       const uint32_t q = min(s0 + 64 * j + lane, S - 1);
       kp[j] = key(q ? q - 1 : 0);
       kq[j] = key(q);
       hq[j] = hit(q);
+      kpp[j] = key(q > 1 ? q - 2 : 0);
     }
-    uint32_t hd = 0;  // head flags, bit j
+    uint32_t hd = 0, sd = 0;  // head flags / second-element flags, bit j
 #pragma unroll
     for (uint32_t j = 0; j < IT; j++) {
       const uint32_t q = s0 + 64 * j + lane;
       hd |= (q < S && (q == 0 || kp[j] != kq[j])) ? 1u << j : 0u;
+      sd |= (q < S && q >= 1 && kp[j] == kq[j] && (q == 1 || kpp[j] != kp[j])) ? 1u << j : 0u;
     }
 #pragma unroll
     for (uint32_t j = 0; j < IT; j++) {
@@ -1620,6 +1629,7 @@ __device__ inline void bucket_segment(BucketLds<B>& L, uint32_t d, uint32_t S, u
           run_start[rb + r] = base + q;
           if (r) run_end[rb + r - 1] = base + q;
         }
+        if ((sd >> j) & 1) drun[L.db + atomicAdd(&L.dcnt, 1u)] = rb + r;  // (any order)
       }
       run = seg_op(run, SegPair{__shfl(v.f, 63, 64), __shfl(v.s, 63, 64)});
       hrun += (uint32_t)__popcll(heads);
@@ -1662,9 +1672,9 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
     const uint4* __restrict__ pt,
     const uint32_t* __restrict__ info, uint32_t ntiles, uint32_t* __restrict__ sk, uint32_t* __restrict__ sv,
     uint32_t* __restrict__ sh, uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
-    uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end, uint32_t* num_runs,
-    BigMeta* __restrict__ meta, uint32_t* big_n, uint32_t* __restrict__ work, uint32_t* work_n,
-    const uint32_t* err) {
+    uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end, unsigned long long* num_runs,
+    uint32_t* __restrict__ drun, BigMeta* __restrict__ meta, uint32_t* big_n, uint32_t* __restrict__ work,
+    uint32_t* work_n, const uint32_t* err) {
   using B = BkSmall;
   __shared__ BucketLds<B> L;
   if (*err) return;
@@ -1683,8 +1693,10 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
       M.r = L.nheavy;
       M.nchunks = M.r ? (S + BIG_CHUNK - 1) / BIG_CHUNK : 0u;
       M.item0 = M.nchunks ? atomicAdd(work_n, M.nchunks) : 0u;
-      M.rb_heavy = M.r ? atomicAdd(num_runs, M.r) : 0u;
-      M.pad = 0;
+      const unsigned long long old =
+          M.r ? atomicAdd(num_runs, ((unsigned long long)M.r << 32) | M.r) : 0ull;  // hot keys: runs of >= 3
+      M.rb_heavy = (uint32_t)old;
+      M.db_heavy = (uint32_t)(old >> 32);
       for (uint32_t c = 0; c < BK_HEAVY; c++) M.heavy[c] = c < M.r ? L.heavy[c] : 0u;
       const uint32_t b = atomicAdd(big_n, 1u);
       meta[b] = M;
@@ -1724,7 +1736,7 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
     }
   }
   BK_STAMP(d, 3);
-  bucket_segment<B, true>(L, d, S, base, sk, sh, segsum, rid, run_start, run_end, num_runs);
+  bucket_segment<B, true>(L, d, S, base, sk, sh, segsum, rid, run_start, run_end, num_runs, drun);
   BK_STAMP(d, 5);
 }
 
@@ -2147,7 +2159,7 @@ __global__ __launch_bounds__(BkSmall::THREADS) void k_big_place(
     const uint32_t* __restrict__ work, const uint32_t* work_n, const uint32_t* __restrict__ cnt,
     uint32_t* __restrict__ sk, uint32_t* __restrict__ sv, uint32_t* __restrict__ sh, uint32_t* __restrict__ segsum,
     uint32_t* __restrict__ rid, uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end,
-    const uint32_t* err) {
+    uint32_t* __restrict__ drun, const uint32_t* err) {
   using B = BkSmall;
   __shared__ BucketLds<B> L;
   if (*err) return;
@@ -2186,6 +2198,7 @@ __global__ __launch_bounds__(BkSmall::THREADS) void k_big_place(
     if (j == 0 && tid < M.r) {
       run_start[M.rb_heavy + tid] = M.base + hstart[tid];
       run_end[M.rb_heavy + tid] = M.base + hstart[tid] + tot[1 + tid];
+      drun[M.db_heavy + tid] = M.rb_heavy + tid;
     }
     uint32_t kk[B::ITEMS], vv[B::ITEMS], hh[B::ITEMS], cls[B::ITEMS];
     big_chunk_load(M, j, ntiles, pt, kk, vv, hh, cls, true);
@@ -2275,9 +2288,9 @@ __global__ __launch_bounds__(BkBig::THREADS) void k_bucket_big(
     const uint4* __restrict__ pt,
     const uint32_t* __restrict__ info, uint32_t ntiles, uint32_t* __restrict__ sk, uint32_t* __restrict__ sv,
     uint32_t* __restrict__ sh, uint32_t* __restrict__ ht, uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
-    uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end, uint32_t* num_runs,
-    const BigMeta* __restrict__ meta, const uint32_t* big_n, const uint32_t* __restrict__ cnt,
-    const uint32_t* err) {
+    uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end, unsigned long long* num_runs,
+    uint32_t* __restrict__ drun, const BigMeta* __restrict__ meta, const uint32_t* big_n,
+    const uint32_t* __restrict__ cnt, const uint32_t* err) {
   using B = BkBig;
   __shared__ BucketLds<B> L;
   if (*err) return;
@@ -2315,7 +2328,7 @@ __global__ __launch_bounds__(BkBig::THREADS) void k_bucket_big(
           }
         }
         __syncthreads();
-        bucket_segment<B, true>(L, d, nl, base, sk, sh, segsum, rid, run_start, run_end, num_runs);
+        bucket_segment<B, true>(L, d, nl, base, sk, sh, segsum, rid, run_start, run_end, num_runs, drun);
       }
     } else {
       if (tid < M.r) run_start[M.rb_heavy + tid] = run_end[M.rb_heavy + tid] = 0;  // hot-key runs left empty
@@ -2323,7 +2336,7 @@ __global__ __launch_bounds__(BkBig::THREADS) void k_bucket_big(
       BK_STAMP(d, 1);
       if (!bucket_peel(L, d, S, base, ntiles, pt, sk, sv, sh))
         bucket_lsd(L, S, base, ntiles, pt, sk, sv, sh, ht, segsum, rid);
-      bucket_segment<B, false>(L, d, S, base, sk, sh, segsum, rid, run_start, run_end, num_runs);
+      bucket_segment<B, false>(L, d, S, base, sk, sh, segsum, rid, run_start, run_end, num_runs, drun);
     }
     BK_STAMP(d, 7);
     __syncthreads();  // L is reused by the next bucket
@@ -2334,27 +2347,141 @@ __global__ __launch_bounds__(BkBig::THREADS) void k_bucket_big(
 // stem under one unit, else it is flagged RUN_MULTI and queued once (by run
 // id) for k_runs_general; a window change within a run makes a long run
 // RUN_SLOW (serial replay). Run heads only compare two sort keys.
+// ---------------------------------------------------------------------------
+// Sparse work, densely. Where only some positions of a range need the random
+// table / record accesses (the runs of two or more at C1, the keys seen once at
+// C2), spreading them one per lane over the whole grid makes nearly every wave
+// pay a full chain of dependent random loads for one or two active lanes. A
+// block instead scans a CHUNK of positions with coalesced reads, compacts the
+// active ones into LDS (any order: the items are independent) and works
+// through them with all its lanes.
+// ---------------------------------------------------------------------------
+constexpr uint32_t CHUNK = 1024;
+
+template <typename Pred>
+__device__ __attribute__((always_inline)) inline uint32_t block_compact(uint32_t lo, uint32_t hi, uint32_t* list,
+                                                                        uint32_t* count, Pred pred) {
+  const uint32_t lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) *count = 0;
+  __syncthreads();
+  for (uint32_t i0 = lo; i0 < hi; i0 += blockDim.x) {
+    const uint32_t i = i0 + threadIdx.x;
+    const bool take = i < hi && pred(i);
+    const uint64_t m = __ballot(take);
+    uint32_t base = 0;
+    if (lane == 0 && m) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = __shfl(base, 0);
+    if (take) list[base + __popcll(m & ((1ull << lane) - 1))] = i;
+  }
+  __syncthreads();
+  return *count;
+}
+
+// k_run_check marks every descriptor whose sort key occurs twice or more in the
+// batch (FLAG_DUP in its record, one plain store per descriptor: the thread of
+// sorted position q marks q, and the run's head when q is its second element).
+// k_unique answers the unmarked ones in arrival order; k_runs the runs.
 __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
                                                    const uint32_t* __restrict__ skeys,
                                                    const uint32_t* __restrict__ rid,
                                                    uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
                                                    uint32_t* defer_n, const uint32_t* err) {
+  __shared__ uint32_t s_list[CHUNK], s_cnt;
   if (*err) return;
-  const uint32_t q = blockIdx.x * 256 + threadIdx.x;
-  if (q == 0 || q >= b.n || skeys[q - 1] != skeys[q]) return;
+  const uint32_t lo = max(blockIdx.x * CHUNK, 1u), hi = min(blockIdx.x * CHUNK + CHUNK, b.n);
+  if (lo >= hi) return;
+  // non-head positions (the second and later descriptors of a run)
+  const uint32_t cnt = block_compact(lo, hi, s_list, &s_cnt, [&](uint32_t q) { return skeys[q - 1] == skeys[q]; });
   b.stem_total = b.off[b.n];
-  const Rec x = rec_s[q], y = rec_s[q - 1];
-  const uint32_t r = rid[q];
-  // a failed descriptor (FLAG_SKIP) makes its run exact-path: k_runs_general leaves it out
-  const bool same = !((rec_flags(x) | rec_flags(y)) & FLAG_SKIP) && x.hlo == y.hlo &&
-                    (x.lu & 0xFFFFFFu) == (y.lu & 0xFFFFFFu) &&  // hash, length, unit
-                    key_equal(key_of(b, x), key_of(b, y));
-  if (!same) {
-    if (!(atomicOr(&run_flags[r], RUN_MULTI) & RUN_MULTI)) defer[atomicAdd(defer_n, 1u)] = r;
-  } else {
-    const uint32_t d = div_of(rec_unit(x));
-    if (x.now / d != y.now / d) atomicOr(&run_flags[r], RUN_SLOW);
+  Rec* rec = const_cast<Rec*>(rec_s.rec);
+#pragma unroll 1
+  for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
+    const uint32_t q = s_list[j];
+    const Rec x = rec_s[q], y = rec_s[q - 1];
+    const uint32_t r = rid[q];
+    rec[rec_s.sv[q]].lu = x.lu | (FLAG_DUP << 24);
+    if (q == 1 || skeys[q - 2] != skeys[q]) rec[rec_s.sv[q - 1]].lu = y.lu | (FLAG_DUP << 24);  // the run's head
+    // a failed descriptor (FLAG_SKIP) makes its run exact-path: k_runs_general leaves it out
+    const bool same = !((rec_flags(x) | rec_flags(y)) & FLAG_SKIP) && x.hlo == y.hlo &&
+                      (x.lu & 0xFFFFFFu) == (y.lu & 0xFFFFFFu) &&  // hash, length, unit
+                      key_equal(key_of(b, x), key_of(b, y));
+    if (!same) {
+      if (!(atomicOr(&run_flags[r], RUN_MULTI) & RUN_MULTI)) defer[atomicAdd(defer_n, 1u)] = r;
+    } else {
+      const uint32_t d = div_of(rec_unit(x));
+      if (x.now / d != y.now / d) atomicOr(&run_flags[r], RUN_SLOW);
+    }
   }
+}
+
+// ---- k_unique: descriptors whose sort key occurs once in the batch (no
+// FLAG_DUP), one lane each in ARRIVAL order: the record, the sort key and
+// the stem are coalesced wave reads (consecutive descriptors sit side by side
+// in the packed batch), the result a coalesced store; only the slot's first
+// sector (and the changed window record) is a random access. Such a stem has
+// no other descriptor in the batch, so the lanes are independent and this
+// kernel commutes with the sorted path (k_runs). A stem that lives in the
+// table under another unit too is left to k_runs_general (defer1).
+__global__ __launch_bounds__(256) void k_unique(BatchDev b, TableDev t, Params P, const Rec* __restrict__ rec,
+                                                const uint32_t* __restrict__ keys0, unsigned long long* __restrict__ res,
+                                                uint32_t* __restrict__ defer1, uint32_t* defer1_n,
+                                                unsigned long long* stats, unsigned long long* stripes, uint32_t* err,
+                                                uint32_t* errs, int restore) {
+  __shared__ uint32_t s_err, s_cnt, s_list[256];
+  if (threadIdx.x == 0) s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const uint32_t lo = blockIdx.x * 256, hi = min(lo + 256, b.n);
+  if (s_err || lo >= hi) return;
+  b.stem_total = b.off[b.n];
+  uint32_t* ferr = P.isolate ? errs : err;
+  const bool use_lds = !restore && b.n_rules <= LDS_RULES;
+  stats_block_begin(use_lds, b.n_rules);
+  StatAcc acc{use_lds, stats};
+  LaneStats L;
+  L.reset();
+  // not a duplicated key (the sorted path's), not failed (answered already)
+  const uint32_t cnt = block_compact(lo, hi, s_list, &s_cnt,
+                                     [&](uint32_t i) { return !((rec[i].lu >> 24) & (FLAG_SKIP | FLAG_DUP)); });
+  if (threadIdx.x < cnt) {
+    const uint32_t j = threadIdx.x;
+    const uint32_t i = s_list[j];
+    const uint32_t key = keys0[i];
+    const Rec x = rec[i];
+    {
+      const uint64_t h0 = ((uint64_t)key << 32) | x.hlo;
+      const uint32_t u0 = rec_unit(x);
+      SlotImg im;
+      load_img_lo(&t.slots[h0 >> t.shift], im);  // home slot's first sector, in flight beside the stem
+      const Key k0 = key_of(b, x);
+      bool ins = false, ok = true;
+      const int64_t s0 = find_slot_img(t, h0, slot_tag(h0, u0), k0, u0, &ins, im, ferr);
+      if (s0 < 0) {
+        ok = false;
+      } else if (im.flags() & SLOT_EXACT) {
+        ok = false;
+      } else if (ins) {  // new (stem, unit): the stem must not exist under another unit
+        for (uint32_t u = 1; u <= 4; u++) {
+          bool dummy;
+          const int64_t so = u == u0 ? -1 : find_slot(t, h0, slot_tag(h0, u), k0, u, false, &dummy, ferr);
+          if (so >= 0) {
+            t.slots[so].flags |= SLOT_EXACT;
+            ok = false;
+          }
+        }
+        if (!ok) t.slots[s0].flags |= SLOT_EXACT;
+      }
+      if (ok) {
+        replay_simple(SRec{rec, nullptr}, nullptr, res, t, P, nullptr, 0, 1, 0, s0, im.cur(), im.prev(), im.hi, x, i,
+                      L, acc, ferr, restore);
+      } else if (s0 == SLOT_TABLE_FULL || s0 == SLOT_ARENA_FULL) {
+        if (P.isolate) res[i] = pack_fail(slot_fail_status(s0));  // else the batch fails
+      } else {
+        defer1[atomicAdd(defer1_n, 1u)] = i;
+      }
+    }
+  }
+  if (!restore) wave_flush(L, acc);
+  stats_block_end(use_lds, b.n_rules, stripes);
 }
 
 // ---- k_runs: one lane per run of one stem and one unit (k_run_check). Short
@@ -2374,28 +2501,38 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
                                               const uint32_t* __restrict__ run_start,
                                               const uint32_t* __restrict__ run_end,
                                               uint32_t* __restrict__ run_flags, uint4* __restrict__ run_state,
-                                              uint32_t* __restrict__ run_f, const uint32_t* num_runs,
+                                              uint32_t* __restrict__ run_f, const unsigned long long* num_runs,
+                                              const uint32_t* __restrict__ drun,
                                               uint32_t* __restrict__ defer, uint32_t* defer_n,
                                               unsigned long long* stats, unsigned long long* stripes, uint32_t* err,
                                               uint32_t* errs, int restore, uint32_t* __restrict__ fast_blk) {
-  __shared__ uint32_t s_err, s_nr;
+  __shared__ uint32_t s_err, s_nr, s_cnt, s_list[256];
   // err may change while this kernel runs (other blocks): read it once per block
   if (threadIdx.x == 0) {
     s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_nr = *num_runs;
+    s_nr = (uint32_t)(*num_runs >> 32);  // runs of two or more (drun)
   }
   __syncthreads();
-  if (s_err || blockIdx.x * 256 >= s_nr) return;
+  const uint32_t lo = blockIdx.x * 256, hi = min(lo + 256, s_nr);
+  if (s_err || lo >= hi) return;
   b.stem_total = b.off[b.n];
   uint32_t* ferr = P.isolate ? errs : err;  // descriptor-level failures: soft word with statuses
-  const bool use_lds = !restore && b.n_rules <= LDS_RULES;
-  stats_block_begin(use_lds, b.n_rules);
-  StatAcc acc{use_lds, stats};
+  // the dup-run list, compacted once more (a large bucket's hot-key run left
+  // to its fallback path is empty)
+  const uint32_t cnt =
+      block_compact(lo, hi, s_list, &s_cnt, [&](uint32_t j) { return run_end[drun[j]] - run_start[drun[j]] >= 2; });
+  // Waves without a run leave at once (no block barrier after this point):
+  // stats go wave by wave to this block's stripe (or straight to the output
+  // past LDS_RULES rules), not through a block-wide LDS table.
+  if ((threadIdx.x & ~63u) >= cnt) return;
+  StatAcc acc{false, b.n_rules <= LDS_RULES && !restore
+                         ? stripes + (size_t)(blockIdx.x % STAT_STRIPES) * b.n_rules * RL_NUM_STATS : stats};
   LaneStats L;
   L.reset();
-  const uint32_t r = blockIdx.x * 256 + threadIdx.x;
-  const uint32_t p = r < s_nr ? run_start[r] : 0u, end = r < s_nr ? run_end[r] : 0u;
-  if (p < end) {  // (a large bucket's hot-key run left to its fallback path is empty)
+  if (threadIdx.x < cnt) {
+    const uint32_t j = threadIdx.x;
+    const uint32_t r = drun[s_list[j]];
+    const uint32_t p = run_start[r], end = run_end[r];
     const uint32_t fl = run_flags[r];
     const Rec x0 = rec_s[p];
     const uint32_t e0 = svals[p];
@@ -2485,10 +2622,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
       }
     }
   }
-  if (!(RL_ABL & 4)) {
-    if (!restore) wave_flush(L, acc);
-    stats_block_end(use_lds, b.n_rules, stripes);
-  }
+  if (!(RL_ABL & 4) && !restore) wave_flush(L, acc);
 }
 
 // ---- parallel path for long uniform runs (one stem, one unit, one window).
@@ -2602,6 +2736,45 @@ __device__ inline void fail_group(unsigned long long* res, const uint32_t* svals
     if (grp[q] == g) res[svals[q]] = pack_fail(st);
 }
 
+// Exact replay of one stem's descriptors over every unit slot it has (Redis
+// keys shared across units: general_step). visit(f) calls f(Elem) for each of
+// the stem's descriptors in arrival order.
+template <typename Visit>
+__device__ inline void stem_exact(const TableDev& t, const Params& P, unsigned long long* res, LaneStats& L,
+                                  StatAcc& acc, uint32_t* ferr, int restore, uint64_t hs, const Key& stem, uint32_t um,
+                                  Visit visit) {
+  GeneralState G;
+  G.present = 0;
+  G.cur_req = 0xFFFFFFFFu;
+  G.npend = 0;
+  int64_t fail = 0;
+  for (uint32_t u = 1; u <= 4; u++) {
+    bool ins;
+    G.sidx[u - 1] = find_slot(t, hs, slot_tag(hs, u), stem, u, (um >> (u - 1)) & 1, &ins, ferr);
+    if (G.sidx[u - 1] >= 0) {
+      G.present |= 1u << (u - 1);
+      G.cur[u - 1] = t.slots[G.sidx[u - 1]].cur;
+      G.prev[u - 1] = t.slots[G.sidx[u - 1]].prev;
+    } else if ((um >> (u - 1)) & 1) {
+      fail = G.sidx[u - 1];
+    }
+  }
+  if (fail) {
+    if (P.isolate) visit([&](const Elem& x) { res[x.e] = pack_fail(slot_fail_status(fail)); });
+    return;
+  }
+  visit([&](const Elem& x) { general_step(P, res, L, acc, G, x, restore, ferr); });
+  general_apply_pending(G);
+  const uint8_t fl = __popc(G.present) >= 2 ? SLOT_EXACT : 0;
+  for (uint32_t u = 0; u < 4; u++) {
+    if (!(G.present >> u & 1)) continue;
+    Slot* s = &t.slots[G.sidx[u]];
+    s->cur = G.cur[u];
+    s->prev = G.prev[u];
+    s->flags |= fl;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Params P, SRec rec_s,
                                                       const uint32_t* __restrict__ skeys,
                                                       const uint32_t* __restrict__ svals,
@@ -2610,16 +2783,18 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
                                                       const uint32_t* __restrict__ run_end,
                                                       const uint32_t* __restrict__ defer, const uint32_t* defer_n,
                                                       uint32_t* __restrict__ grp, uint32_t* __restrict__ lead,
-                                                      uint8_t* __restrict__ gmask, unsigned long long* stats,
-                                                      unsigned long long* stripes, uint32_t* err, uint32_t* errs,
-                                                      int restore) {
-  __shared__ uint32_t s_err, s_n;
+                                                      uint8_t* __restrict__ gmask, const uint32_t* __restrict__ keys0,
+                                                      const uint32_t* __restrict__ defer1, const uint32_t* defer1_n,
+                                                      unsigned long long* stats, unsigned long long* stripes,
+                                                      uint32_t* err, uint32_t* errs, int restore) {
+  __shared__ uint32_t s_err, s_n, s_n1;
   if (threadIdx.x == 0) {
     s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_n = *defer_n;
+    s_n1 = defer1_n ? *defer1_n : 0u;
   }
   __syncthreads();
-  if (s_err || blockIdx.x * 256 >= s_n) return;
+  if (s_err || (blockIdx.x * 256 >= s_n && blockIdx.x * 256 >= s_n1)) return;
   b.stem_total = b.off[b.n];
   uint32_t* ferr = P.isolate ? errs : err;
   const bool use_lds = !restore && b.n_rules <= LDS_RULES;
@@ -2686,40 +2861,19 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
                       svals[q0], L, acc, ferr, restore);
         continue;
       }
-      GeneralState G;
-      G.present = 0;
-      G.cur_req = 0xFFFFFFFFu;
-      G.npend = 0;
-      int64_t fail = 0;
-      for (uint32_t u = 1; u <= 4; u++) {
-        bool ins;
-        G.sidx[u - 1] = find_slot(t, hs, slot_tag(hs, u), stem, u, (um >> (u - 1)) & 1, &ins, ferr);
-        if (G.sidx[u - 1] >= 0) {
-          G.present |= 1u << (u - 1);
-          G.cur[u - 1] = t.slots[G.sidx[u - 1]].cur;
-          G.prev[u - 1] = t.slots[G.sidx[u - 1]].prev;
-        } else if ((um >> (u - 1)) & 1) {
-          fail = G.sidx[u - 1];
-        }
-      }
-      if (fail) {
-        if (P.isolate) fail_group(res, svals, grp, q0, end, g, slot_fail_status(fail));
-        continue;
-      }
-      for (uint32_t q = q0; q < end; q++) {
-        if (grp[q] != g) continue;
-        general_step(P, res, L, acc, G, load_elem(rec_s[q], svals[q], restore), restore, ferr);
-      }
-      general_apply_pending(G);
-      const uint8_t fl = __popc(G.present) >= 2 ? SLOT_EXACT : 0;
-      for (uint32_t u = 0; u < 4; u++) {
-        if (!(G.present >> u & 1)) continue;
-        Slot* s = &t.slots[G.sidx[u]];
-        s->cur = G.cur[u];
-        s->prev = G.prev[u];
-        s->flags |= fl;
-      }
+      stem_exact(t, P, res, L, acc, ferr, restore, hs, stem, um, [&](auto&& f) {
+        for (uint32_t q = q0; q < end; q++)
+          if (grp[q] == g) f(load_elem(rec_s[q], svals[q], restore));
+      });
     }
+  }
+  // singletons k_unique found under several units (arrival indices)
+  for (uint32_t di = blockIdx.x * 256 + threadIdx.x; di < s_n1; di += gridDim.x * 256) {
+    const uint32_t e = defer1[di];
+    const Rec x = rec_s.rec[e];
+    const uint64_t hs = ((uint64_t)keys0[e] << 32) | x.hlo;
+    stem_exact(t, P, res, L, acc, ferr, restore, hs, key_of(b, x), 1u << (rec_unit(x) - 1),
+               [&](auto&& f) { f(load_elem(x, e, restore)); });
   }
   if (!restore) wave_flush(L, acc);
   stats_block_end(use_lds, b.n_rules, stripes);
@@ -2729,7 +2883,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
 // the sticky table-stage word, clear k_runs' deferral counter and this call's
 // output stats (n_rules x RL_NUM_STATS).
 __global__ __launch_bounds__(256) void k_b_begin(const uint32_t* __restrict__ erra, uint32_t* errb,
-                                                 uint32_t* __restrict__ defer_n,
+                                                 uint32_t* __restrict__ defer_n, uint32_t* __restrict__ defer1_n,
                                                  unsigned long long* __restrict__ stats, uint32_t m,
                                                  uint32_t* __restrict__ fast_blk, uint32_t nw) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
@@ -2737,6 +2891,7 @@ __global__ __launch_bounds__(256) void k_b_begin(const uint32_t* __restrict__ er
     const uint32_t e = *erra;
     if (e) atomicOr(errb, e);
     *defer_n = 0;
+    *defer1_n = 0;
   }
   for (uint32_t j = i; j < m; j += gridDim.x * 256) stats[j] = 0;
   for (uint32_t j = i; j < nw; j += gridDim.x * 256) fast_blk[j] = 0;
@@ -2891,14 +3046,21 @@ __global__ __launch_bounds__(256) void k_debug_decide(uint32_t n, const uint32_t
 // ===========================================================================
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
-// Stage A (table-free): validate, hash, sort, gather, segment. Uses only this
-// buffer's scratch and its validation word s.err.
+#ifndef RL_RUNS_SIDE
+#define RL_RUNS_SIDE 0
+#endif
+#define RL_RUNS_STREAM (RL_RUNS_SIDE ? side : st)
+
+// Stage A (table-free): validate, hash, sort, segment, and mark the descriptors
+// whose sort key occurs more than once. Uses only this buffer's scratch and its
+// validation word s.err. Sorted keys go to keys[1] (keys[0] keeps the arrival
+// order for k_unique), the sort permutation to vals[0].
 void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_t st, hipEvent_t* ev) {
   const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
   if (ev) (void)hipEventRecord(ev[0], st);
   if (g0)
     k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.keys[0], s.err, s.errs, isolate, s.time_floor, s.defer_n, s.big_n,
-                                  s.work_n, s.run_flags, s.num_runs, s.hit_a, s.res);
+                                  s.work_n, s.run_flags, s.runs64, s.hit_a, s.res);
   if (ev) (void)hipEventRecord(ev[1], st);
   const uint32_t ptiles = cdiv(b.n, PART_TILE);
   if (b.n)
@@ -2907,58 +3069,65 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
   if (b.n) {
     const size_t seg_lds = (2ull * ptiles + 1) * 4;
     k_bucket<<<PART_DIGITS, BkSmall::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
-                                                             s.keys[0], s.vals[0], s.hits_s, s.segsum, s.rid,
-                                                             s.run_start, s.run_end, s.num_runs, s.big_meta, s.big_n,
+                                                             s.keys[1], s.vals[0], s.hits_s, s.segsum, s.rid,
+                                                             s.run_start, s.run_end, s.runs64, s.drun, s.big_meta, s.big_n,
                                                              s.big_work, s.work_n, s.err);
     k_big_count<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
                                                                     s.big_meta, s.big_work, s.work_n, s.big_cnt,
                                                                     s.err);
     k_big_place<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds, st>>>(
-        s.tile, s.part_info, ptiles, s.big_meta, s.big_work, s.work_n, s.big_cnt, s.keys[0],
-        s.vals[0], s.hits_s, s.segsum, s.rid, s.run_start, s.run_end, s.err);
+        s.tile, s.part_info, ptiles, s.big_meta, s.big_work, s.work_n, s.big_cnt, s.keys[1],
+        s.vals[0], s.hits_s, s.segsum, s.rid, s.run_start, s.run_end, s.drun, s.err);
     k_bucket_big<<<BIG_BLOCKS, BkBig::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
-                                                              s.keys[0], s.vals[0], s.hits_s, s.hit_t, s.segsum,
-                                                              s.rid, s.run_start, s.run_end, s.num_runs, s.big_meta,
+                                                              s.keys[1], s.vals[0], s.hits_s, s.hit_t, s.segsum,
+                                                              s.rid, s.run_start, s.run_end, s.runs64, s.drun, s.big_meta,
                                                               s.big_n, s.big_cnt, s.err);
-    k_run_check<<<cdiv(b.n, 256), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[0], s.rid, s.run_flags, s.defer, s.defer_n,
-                                                s.err);
+    k_run_check<<<cdiv(b.n, CHUNK), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[1], s.rid, s.run_flags, s.defer,
+                                                s.defer_n, s.err);
   }
 }
 
 // Stage B (the table): runs strictly in batch order. Every kernel reads the
 // sticky table-stage word s.errb; k_b_begin folds this batch's validation
-// result into it first.
+// result into it first. k_unique (keys seen once) and the sorted path (k_runs
+// and its exact / parallel companions) touch disjoint stems.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
                     int restore, hipStream_t st, hipStream_t side, hipEvent_t go, hipEvent_t side_done,
                     hipEvent_t* ev) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
-  k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, s.defer2_n, o.stats, m, s.fast_blk, cdiv(b.n, 256 * 32));
+  k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, s.defer2_n, s.defer1_n, o.stats, m, s.fast_blk, cdiv(b.n, 256 * 32));
   if (b.n) {
     const uint32_t g = cdiv(b.n, 256);
     const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
-    // RUN_MULTI runs (known since k_run_check) on the side stream, beside k_runs
+    const SRec rs{s.rec, s.vals[0]};
+    // Side stream: the RUN_MULTI runs (known since k_run_check); main stream:
+    // the runs of two or more (k_runs), then the keys seen once (k_unique).
+    // The three touch disjoint stems. (The order and stream split were chosen
+    // by A/B on the pipelined C1/C2 benches)
     (void)hipEventRecord(go, st);
     (void)hipStreamWaitEvent(side, go, 0);
     k_runs_general<<<g < RUNS_GENERAL_BLOCKS ? g : RUNS_GENERAL_BLOCKS, 256, lds, side>>>(
-        b, t, P, SRec{s.rec, s.vals[0]}, s.keys[0], s.vals[0], s.res, s.run_start, s.run_end, s.defer, s.defer_n, s.grp,
-        s.lead, s.gmask, o.stats, s.stripes, s.errb, s.errs, restore);
+        b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer, s.defer_n, s.grp, s.lead, s.gmask,
+        s.keys[0], nullptr, nullptr, o.stats, s.stripes, s.errb, s.errs, restore);
+    k_runs<<<cdiv(b.n / 2 + BIG_HEAVY * PART_DIGITS, 256), 256, 0, RL_RUNS_STREAM>>>(
+        b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.run_flags, s.run_state, s.run_f, s.runs64,
+        s.drun, s.defer2, s.defer2_n, o.stats, s.stripes, s.errb, s.errs, restore, s.fast_blk);
     (void)hipEventRecord(side_done, side);
     if (ev) (void)hipEventRecord(ev[3], st);
-    k_runs<<<g, 256, lds, st>>>(b, t, P, SRec{s.rec, s.vals[0]}, s.keys[0], s.vals[0], s.res, s.run_start, s.run_end, s.run_flags,
-                                s.run_state, s.run_f, s.num_runs, s.defer2, s.defer2_n, o.stats, s.stripes, s.errb,
-                                s.errs, restore, s.fast_blk);
+    k_unique<<<cdiv(b.n, 256), 256, lds, st>>>(b, t, P, s.rec, s.keys[0], s.res, s.defer1, s.defer1_n, o.stats,
+                                               s.stripes, s.errb, s.errs, restore);
     if (ev) (void)hipEventRecord(ev[4], st);
-    // stems k_runs found under several units in the table (rare)
-    k_runs_general<<<RUNS_GENERAL_LATE_BLOCKS, 256, lds, st>>>(b, t, P, SRec{s.rec, s.vals[0]}, s.keys[0], s.vals[0],
-                                                                s.res, s.run_start, s.run_end, s.defer2, s.defer2_n, s.grp, s.lead,
-                                                                s.gmask, o.stats, s.stripes, s.errb, s.errs, restore);
     (void)hipStreamWaitEvent(st, side_done, 0);
+    // stems k_unique / k_runs found under several units in the table (rare)
+    k_runs_general<<<RUNS_GENERAL_LATE_BLOCKS, 256, lds, st>>>(
+        b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer2, s.defer2_n, s.grp, s.lead, s.gmask,
+        s.keys[0], s.defer1, s.defer1_n, o.stats, s.stripes, s.errb, s.errs, restore);
     if (!restore) {
       if (P.lc_en)
-        k_fast_over<<<g, 256, 0, st>>>(b.n, SRec{s.rec, s.vals[0]}, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
-      k_fast_emit<<<g, 256, lds, st>>>(b.n, b.n_rules, t, P, SRec{s.rec, s.vals[0]}, s.vals[0], s.res, s.segsum, s.rid,
-                                       s.run_start, s.run_end, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb,
+        k_fast_over<<<g, 256, 0, st>>>(b.n, rs, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
+      k_fast_emit<<<g, 256, lds, st>>>(b.n, b.n_rules, t, P, rs, s.vals[0], s.res, s.segsum, s.rid, s.run_start,
+                                       s.run_end, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb,
                                        s.fast_blk);
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;
       const uint32_t gf = cdiv(nf * RL_NUM_STATS > b.n ? nf * RL_NUM_STATS : b.n, 256);
