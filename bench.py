@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--no-fill", action="store_true")
     ap.add_argument("--slots-per-key", type=float, default=4.0, help="table slots per live key (power of 2 above)")
     ap.add_argument("--route", action="store_true", help="use the routed (all_to_all) path even at N=1")
+    ap.add_argument("--route-impl", default="lib", choices=["lib", "python"],
+                    help="routed step: inside the library over RCCL (lib) or collectives from Python")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + --one-device: rehearse N ranks on one GPU (host-staged exchange)")
     ap.add_argument("--one-device", action="store_true", help="every rank uses cuda:0 (rehearsal only)")
@@ -115,13 +117,23 @@ def main():
                          device="cpu" if args.dist_backend == "gloo" else "cuda")
         dist.broadcast(t, 0)
         seed = int(t.item())
-    be = Backend(0.8, False, table_slots=slots, max_batch=cap, max_rules=8, device=local, hash_seed=seed,
-                 max_stem_bytes=64 * cap)
+    # a routed owner attributes stats per source rank: world x n_rules rule slots
+    be = Backend(0.8, False, table_slots=slots, max_batch=cap, max_rules=max(8, 2 * world), device=local,
+                 hash_seed=seed, max_stem_bytes=64 * cap)
     now0 = W.NOW0
-    if routed:
+    py_route = routed and (args.route_impl == "python" or args.dist_backend == "gloo")
+    if routed and not py_route:
+        # the routed step inside the library: RCCL send/recv over xGMI (rl_comm.hip)
+        from ratelimit_amd.sharded import RcclRouter
+        sc = RcclRouter(be)
+    elif routed:
         from ratelimit_amd.sharded import DeviceRouteOps, Exchange, ShardedRateLimitCache
+        # forward and return collectives on two groups: batch t+1's forward
+        # exchange overlaps batch t's owner pipeline and return exchange
+        ret_group = dist.new_group(backend=args.dist_backend)
         sc = ShardedRateLimitCache(DeviceRouteOps(be), Exchange(), max_batch=n, max_stem_bytes=64 * n,
-                                   device=torch.device("cuda", local), max_recv=cap, max_recv_stem=64 * cap)
+                                   device=torch.device("cuda", local), max_recv=cap, max_recv_stem=64 * cap,
+                                   ret_exchange=Exchange(ret_group))
     out = {"code": torch.empty(n, dtype=torch.uint8, device="cuda"),
            "limit_remaining": torch.empty(n, dtype=torch.int32, device="cuda"),
            "reset_s": torch.empty(n, dtype=torch.int32, device="cuda"),
@@ -132,9 +144,15 @@ def main():
 
     def do_step(inp, bn, bq):
         if routed:
-            sc.do_limit(inp, bn, bq, 2, out)
+            sc.submit(inp, bn, bq, 2, out)
         else:
             be.do_limit_device(inp, out, bn, bq, 2, stream=serial_stream)
+
+    def sync():
+        if routed:
+            sc.finish()
+        else:
+            be.synchronize()
 
     # ---- fill: every key of the node's tenant space (rank r inserts tenants
     # [r*T, (r+1)*T); routed batches land on their owners). Not timed.
@@ -144,7 +162,7 @@ def main():
             ids = torch.arange(s0, min(s0 + nq, T), dtype=torch.int64, device="cuda") + rank * T
             a, bn, bq, br = W.c1_batch_dev(ids, now0 - 1)
             do_step(a, bn, bq)
-        be.synchronize()
+        sync()
     t_fill = time.perf_counter() - t_fill
 
     # ---- device-resident input batches + per-step clocks. Requests draw from
@@ -177,7 +195,7 @@ def main():
     # ---- warmup
     for _ in range(args.warmup):
         run_step()
-    be.synchronize()
+    sync()
     torch.cuda.synchronize()
 
     # ---- timed region: exactly K steps. The library records HIP events at the
@@ -186,17 +204,25 @@ def main():
     be.profile(args.prof_every > 0, args.prof_every)
     be.profile_read()
     recv = []
+    if py_route:
+        for k in sc.host_s:
+            sc.host_s[k] = 0.0
+    info0 = be.table_info()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run_step()
-        if routed:
+        if py_route:
             recv.append(sc.last_recv)
-    be.synchronize()
+    sync()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
+    route_host = {k: round(v / args.steps * 1e3, 4) for k, v in sc.host_s.items()} if py_route else None
+    info1 = be.table_info()
+    if routed and not recv:  # decisions this rank's table answered per owner batch
+        recv = [(info1["decisions"] - info0["decisions"]) / max(info1["batches"] - info0["batches"], 1)]
     stage_ms, nb = be.profile_read()
     be.profile(False)
     stage_avg = {k: v / max(nb, 1) for k, v in stage_ms.items()}
@@ -212,7 +238,7 @@ def main():
     for _ in range(args.latency_steps):
         t1 = time.perf_counter()
         run_step()
-        be.synchronize()
+        sync()
         lat.append((time.perf_counter() - t1) * 1e3)
     lat = np.array(lat) if lat else np.array([float("nan")])
     info = be.table_info()
@@ -260,10 +286,13 @@ def main():
                                % (args.config.upper(), T / 1e6, 2 * T * world, n, dist_desc),
                    "global_batch": world * n, "batch_per_gpu": n, "live_stem_slots_per_gpu": info["live_slots"],
                    "table_slots": slots,
-                   "parallelism": ("hash-sharded table x%d, RCCL all_to_all routing" % world) if routed else
+                   "parallelism": ("hash-sharded table x%d, %s" % (
+                                      world, "RCCL send/recv routing inside the library" if not py_route else
+                                      "all_to_all routing from Python (%s)" % args.dist_backend)) if routed else
                                   "single GPU"},
         "p50_batch_ms": float(np.percentile(lat, 50)), "p99_batch_ms": p99,
         "roofline": roofline, "cpu_baseline": cpu, "fill_s": round(t_fill, 2),
+        **({"route_host_ms_per_step": route_host} if py_route else {}),
     }
     print(json.dumps(line), flush=True)
     if routed:

@@ -173,12 +173,20 @@ void rl_destroy(rl_ctx* ctx);
 const char* rl_last_error(const rl_ctx* ctx);
 
 /* DoLimit for a whole batch. Host buffers (pinned via rl_alloc_host is fastest).
- * Synchronous: returns after results are in *out. */
+ * Synchronous: returns after results are in *out.
+ * Multi-GPU (rl_config.n_shards > 1): the table is hash-sharded over
+ * shard_device[0..n_shards) inside this one ctx (the reference's single service
+ * process scaled out over a Redis cluster, src/redis/driver_impl.go:108-126).
+ * Every batch is partitioned by owner on shard 0's device, each owner's chunk
+ * goes to its GPU over xGMI (peer copies), owners run their pipelines, and the
+ * results come back in arrival order, stats summed. Same call, same answers. */
 int rl_do_limit(rl_ctx* ctx, const rl_batch* in, rl_result* out);
 
-/* Same, with every pointer in *in / *out in device memory of ctx's GPU,
- * enqueued on `stream` (a hipStream_t, NULL = ctx's own stream). Returns once
- * the work is enqueued; errors detected on the GPU surface at rl_synchronize.
+/* Same, with every pointer in *in / *out in device memory of ctx's GPU
+ * (shard_device[0] when n_shards > 1), enqueued on `stream` (a hipStream_t,
+ * NULL = ctx's own streams, pipelined). Returns once the work is enqueued (a
+ * multi-shard ctx first waits for this batch's owner partition, never for the
+ * owners' pipelines); errors detected on the GPU surface at rl_synchronize.
  * stem_bytes must be 4-byte aligned (any hipMalloc / torch allocation is). */
 int rl_do_limit_async(rl_ctx* ctx, const rl_batch* in, rl_result* out, void* stream);
 int rl_synchronize(rl_ctx* ctx);
@@ -191,7 +199,8 @@ int rl_sweep(rl_ctx* ctx, int64_t now, uint64_t* n_evicted);
 /* Seed / restore counters (host buffers). */
 int rl_restore(rl_ctx* ctx, const rl_restore_batch* in);
 
-int rl_table_info_get(rl_ctx* ctx, rl_table_info* info);
+int rl_table_info_get(rl_ctx* ctx, rl_table_info* info);  /* summed over shards */
+int rl_table_info_shard(rl_ctx* ctx, uint32_t shard, rl_table_info* info);
 
 /* Pinned host memory for the packed buffers (hipHostMalloc). */
 void* rl_alloc_host(size_t bytes);
@@ -210,40 +219,70 @@ int rl_debug_decide(rl_ctx* ctx, uint32_t n, const uint32_t* before, const uint3
                     uint8_t* code, uint32_t* remaining, uint32_t* reset_s,
                     uint64_t* stat_deltas /* n * RL_NUM_STATS */, uint8_t* lc_set);
 
-/* ---- Multi-GPU routing (hash-sharded table; one rl_ctx per GPU) -----------
- * the reference shards keys across Redis instances
- * (src/redis/driver_impl.go:66-142 cluster/sentinel pools); here each GPU owns
- * the keys whose stem hash maps to it, and every batch is exchanged once.
- * Every pointer is device memory of ctx's GPU and work is enqueued on `stream`
- * (a hipStream_t, NULL = ctx's stream). The exchange (two all_to_all calls over
- * RCCL) is the caller's; ratelimit_amd/sharded.py is the reference driver.
+/* ---- Multi-GPU routing across processes (one single-shard rl_ctx per GPU) ---
+ * SURVEY.md §8e. For one process per GPU (torch.distributed / RCCL), each rank
+ * routes its slice of the node's requests; the collectives are the caller's
+ * (ratelimit_amd/sharded.py). Every pointer is device memory of ctx's GPU, work
+ * is enqueued on `stream` (a hipStream_t, NULL = ctx's stream) and never waits
+ * on the host; errors surface at rl_synchronize. Every rank's ctx must share
+ * rl_config.hash_seed (owner = stem hash).
  *
- * rl_route_pack (source side, synchronous): stable-partitions the batch `in`
- * (device arrays, as rl_do_limit_async) by owner shard and writes, in owner
- * order, one RL_WIRE_BYTES record per descriptor to send_rec and its stem bytes
- * to send_stem (capacity: the batch's stem bytes). perm[j] = batch index of
- * record j. counts_host[2*d], [2*d+1] = records / stem bytes for owner d. Request
+ * rl_route_pack (source side): stable-partitions the batch `in` by owner shard
+ * and writes, in owner order, one RL_WIRE_BYTES record per descriptor to
+ * send_rec and its stem bytes to send_stem (capacity: the batch's stem bytes).
+ * perm[j] = batch index of record j. counts[2*d], [2*d+1] (device memory) =
+ * records / stem bytes for owner d (all zero when the batch is malformed). Request
  * indices must be < 2^24; the global request label is src_rank << 24 | req_idx,
  * so chunks concatenated in source-rank order are in global arrival order.
  *
- * rl_route_do_limit (owner side, asynchronous): DoLimit over the n records
- * received from all sources (concatenated in source-rank order) with their stems
- * (recv_stem, 4-byte aligned, recv_stem_bytes long; src_stem_base = host array
- * of each source's chunk offset in recv_stem). ret[j] = the packed result of record j
- * (bits 0-31 remaining, 32-51 reset_s, 52-55 status, 56-61 code, 62 local-cache hit); stats = this owner's deltas
- * (n_rules * RL_NUM_STATS, overwritten). Errors surface at rl_synchronize.
+ * rl_route_do_limit (owner side): DoLimit over the n records received from all
+ * sources (concatenated in source-rank order) with their stems (recv_stem,
+ * 4-byte aligned, recv_stem_bytes long; src_stem_base = host array of each
+ * source's chunk offset in recv_stem), pipelined on the ctx's streams once the
+ * work already on `stream` is done; then, on `stream`, ret[j] = the packed
+ * result of record j (bits 0-31 remaining, 32-51 reset_s, 52-55 status, 56-61
+ * code, 62 local-cache hit). stats: rule_stride == 0: n_rules x RL_NUM_STATS
+ * deltas; rule_stride > 0: per source rank, n_shards blocks of rule_stride x
+ * RL_NUM_STATS (the deltas of each source's own requests). isolate != 0:
+ * per-descriptor statuses (rl_result.status semantics) in ret.
  *
- * rl_route_scatter (source side, asynchronous): results returned in record
- * order (ret, n = the batch size) -> out (device SoA) in arrival order. */
+ * rl_route_scatter (source side): results returned in record order (ret, n =
+ * the batch size) -> out (device SoA, status optional) in arrival order. */
 #define RL_WIRE_BYTES 32u
 #define RL_MAX_SHARDS 256u
 int rl_route_pack(rl_ctx* ctx, const rl_batch* in, uint32_t n_shards, uint32_t src_rank, void* send_rec,
-                  uint8_t* send_stem, uint32_t* perm, uint64_t* counts_host, void* stream);
+                  uint8_t* send_stem, uint32_t* perm, uint64_t* counts, void* stream);
 int rl_route_do_limit(rl_ctx* ctx, uint32_t n, const void* recv_rec, const uint8_t* recv_stem,
-                      uint64_t recv_stem_bytes, const uint64_t* src_stem_base, uint32_t n_shards,
-                      uint32_t n_rules, uint64_t* ret, uint64_t* stats, void* stream);
+                      uint64_t recv_stem_bytes, const uint64_t* src_stem_base, uint32_t n_shards, uint32_t n_rules,
+                      uint32_t rule_stride, uint64_t* ret, uint64_t* stats, int isolate, void* stream);
 int rl_route_scatter(rl_ctx* ctx, uint32_t n, const uint32_t* perm, const uint64_t* ret, rl_result* out,
                      void* stream);
+
+/* ---- Multi-process routing over RCCL, inside the library ------------------
+ * SURVEY.md §8e with the exchange itself in the library (rl_comm.hip): one
+ * process per GPU, each with one single-shard ctx, every ctx created with the
+ * same rl_config.hash_seed.
+ *
+ * rl_comm_unique_id (one rank) fills RL_COMM_ID_BYTES bytes (an ncclUniqueId)
+ * that the caller hands to every rank (e.g. a torch.distributed broadcast);
+ * rl_comm_init (collective: every rank, the same id) joins ctx to the world as
+ * `rank`. RCCL is loaded at this point (dlopen), not at library load.
+ *
+ * rl_do_limit_routed_async (collective: every rank calls it the same number of
+ * times in the same order; n may be 0) answers this rank's slice of the node
+ * batch. Rank r's slice precedes rank r+1's in the global order (the order the
+ * sequential INCRBY contract is kept in). Device arrays and the stream
+ * semantics of rl_do_limit_async; the only host wait is for this batch's
+ * partition counts. out->stats = the deltas of THIS rank's requests (summed
+ * over ranks: the node's). Needs max_rules >= world x n_rules (an owner keeps
+ * stats per source). A descriptor whose owner batch failed gets that
+ * rl_status in out->status; without out->status it fails this rank's batch at
+ * rl_synchronize. Replaces the Redis cluster client's key-slot routing inside
+ * one service process (src/redis/driver_impl.go:108-126). */
+#define RL_COMM_ID_BYTES 128u
+int rl_comm_unique_id(uint8_t* id);
+int rl_comm_init(rl_ctx* ctx, uint32_t world, uint32_t rank, const uint8_t* id);
+int rl_do_limit_routed_async(rl_ctx* ctx, const rl_batch* in, rl_result* out, void* stream);
 
 /* ---- Config match on the GPU (the caller side of DoLimit) ---
  * The service's constructLimitsToCheck (src/service/ratelimit.go:104-143) calls

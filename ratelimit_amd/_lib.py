@@ -12,12 +12,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RL_LIB_PATH") or os.path.join(HERE, "libratelimit_hip.so")  # override: profiling builds
 
 EXPORTS = ["rl_abi_version", "rl_create", "rl_destroy", "rl_last_error", "rl_do_limit", "rl_do_limit_async",
-           "rl_synchronize", "rl_sweep", "rl_restore", "rl_table_info_get", "rl_alloc_host", "rl_free_host",
+           "rl_synchronize", "rl_sweep", "rl_restore", "rl_table_info_get", "rl_table_info_shard", "rl_alloc_host",
+           "rl_free_host",
            "rl_debug_keys", "rl_debug_decide", "rl_profile", "rl_profile_read", "rl_route_pack",
            "rl_route_do_limit", "rl_route_scatter", "rl_config_load", "rl_do_limit_requests",
            "rl_local_cache_info_get", "rl_snapshot_size", "rl_snapshot_save", "rl_snapshot_load",
            "rl_packer_create", "rl_packer_destroy", "rl_packer_pack", "rl_packer_rules", "rl_packer_rule_key",
-           "rl_packer_last_error"]
+           "rl_packer_last_error", "rl_comm_unique_id", "rl_comm_init", "rl_do_limit_routed_async"]
 
 _lib = None
 
@@ -53,6 +54,7 @@ def lib():
     L.rl_sweep.argtypes = [C.c_void_p, C.c_int64, C.POINTER(C.c_uint64)]
     L.rl_restore.argtypes = [C.c_void_p, C.POINTER(abi.RlRestoreBatch)]
     L.rl_table_info_get.argtypes = [C.c_void_p, C.POINTER(abi.RlTableInfo)]
+    L.rl_table_info_shard.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(abi.RlTableInfo)]
     L.rl_alloc_host.restype = C.c_void_p
     L.rl_alloc_host.argtypes = [C.c_size_t]
     L.rl_free_host.argtypes = [C.c_void_p]
@@ -63,9 +65,12 @@ def lib():
     L.rl_route_pack.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
                                 C.c_void_p, C.c_void_p, C.c_void_p]
     L.rl_route_do_limit.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
-                                    C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+                                    C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
     L.rl_route_scatter.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(abi.RlResult),
                                    C.c_void_p]
+    L.rl_comm_unique_id.argtypes = [C.c_void_p]
+    L.rl_comm_init.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+    L.rl_do_limit_routed_async.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.POINTER(abi.RlResult), C.c_void_p]
     L.rl_config_load.argtypes = [C.c_void_p, C.POINTER(abi.RlConfigTree)]
     L.rl_do_limit_requests.argtypes = [C.c_void_p, C.POINTER(abi.RlRequestBatch), C.POINTER(abi.RlRequestResult)]
     L.rl_local_cache_info_get.argtypes = [C.c_void_p, C.c_int64, C.POINTER(abi.RlLocalCacheInfo)]

@@ -111,6 +111,7 @@ BATCH_DTYPES = {"stem_bytes": np.uint8, "stem_off": np.uint32, "now": np.int64, 
 RESULT_DTYPES = {"code": np.uint8, "limit_remaining": np.uint32, "reset_s": np.uint32, "stats": np.uint64,
                  "status": np.uint8}
 ABI_VERSION = 2
+RL_COMM_ID_BYTES = 128  # include/ratelimit_hip.h
 
 
 def make_batch_struct(arrays, n, n_requests, n_rules):

@@ -10,8 +10,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libratelimit_hip.so")
-SOURCES = ["rl_kernels.hip", "rl_route.hip", "rl_match.hip", "rl_api.hip", "rl_pack.cpp"]
-HEADERS = ["rl_device.h", "rl_kernels.h", "rl_match.h", os.path.join("..", "..", "include", "ratelimit_hip.h")]
+SOURCES = ["rl_kernels.hip", "rl_route.hip", "rl_match.hip", "rl_engine.hip", "rl_comm.hip", "rl_api.hip",
+           "rl_pack.cpp"]
+HEADERS = ["rl_device.h", "rl_kernels.h", "rl_match.h", "rl_engine.h", "rl_comm.h",
+           os.path.join("..", "..", "include", "ratelimit_hip.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RL_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-ffp-contract=off",
@@ -31,15 +33,20 @@ def build(force=False, verbose=False, out=None, defines=()):
     lib = out or LIB
     if out is None and not force and not _stale():
         return LIB
-    objs = []
-    for s in SOURCES:
-        o = os.path.join(CSRC, os.path.splitext(s)[0] + ".o")
+    objs, procs = [], []
+    tag = "" if out is None else "_%x" % (hash(lib) & 0xFFFFFF)
+    for s in SOURCES:  # (compiled side by side: one hipcc per source)
+        o = os.path.join(CSRC, os.path.splitext(s)[0] + tag + ".o")
         cmd = [HIPCC] + FLAGS + ["-D" + d for d in defines] + ["-c", os.path.join(CSRC, s), "-o", o]
         if verbose:
             print(" ".join(cmd))
-        subprocess.check_call(cmd)
+        procs.append((subprocess.Popen(cmd), cmd))
         objs.append(o)
-    cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", lib] + objs
+    for p, cmd in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
+    # RCCL is dlopen'ed by rl_comm.hip (libdl), never linked
+    cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", lib] + objs + ["-ldl"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

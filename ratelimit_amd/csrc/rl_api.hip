@@ -1,138 +1,107 @@
 // rl_api.hip — the extern "C" boundary of libratelimit_hip.so
-// (include/ratelimit_hip.h). Owns the HBM table, two sets of per-batch scratch
-// and the HIP streams; every entry point maps the device error words to an
-// rl_status.
+// (include/ratelimit_hip.h).
 //
-// Batches submitted with rl_do_limit_async(stream = NULL) are pipelined: batch
-// t's table-free stage A (validate, hash, sort, segment) runs on scratch buffer
-// t % NBUF and that buffer's stream while batch t-1's stage B (the table) still
-// runs. Stage B of every batch waits for the previous batch's stage B (an
-// event chain), so the table sees batches in submission order and every key
-// sees the reference's sequential INCRBY order. Every other call is serial and
-// ordered after all submitted batches.
+// A ctx holds one engine per table shard (rl_engine.h: HBM table, pipeline
+// buffers, streams). With one shard every entry point is the engine's own.
+// With rl_config.n_shards > 1 the table is hash-sharded over the shards'
+// devices inside this one process (the reference's single service process
+// scaled out over a Redis cluster, src/redis/driver_impl.go:108-126; here the
+// cgo adapter still drives one ctx), and every batch is routed:
+//
+//   shard 0's device (the source): partition the batch by owner (stem hash)
+//     into wire records + stem bytes, on the forward stream;
+//   host: read the per-owner counts (the one wait per batch: the partition
+//     only, never the owners' pipelines);
+//   forward stream: copy each owner's chunk to its device (xGMI peer copies;
+//     a plain device copy when shards share a device);
+//   each owner: the normal pipelined DoLimit over its chunk (eng_route_owner);
+//   return stream: copy the packed results and stats deltas back, scatter the
+//     results to arrival order, sum the stats.
+//
+// Batch t's partition and copies run while earlier batches' owner pipelines
+// still hold the tables; RSLOTS batches may be in flight.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
-#include <random>
 #include <cstring>
+#include <random>
 #include <string>
 #include <vector>
 
 #include "../../include/ratelimit_hip.h"
+#include "rl_comm.h"
 #include "rl_device.h"
+#include "rl_engine.h"
 #include "rl_kernels.h"
-#include "rl_match.h"
 
 using namespace rl;
 
-// Pipeline depth: scratch buffers (and streams) in flight. Stage A of up to
-// NBUF - 1 later batches may run while one batch's stage B holds the table.
-#ifndef RL_NBUF
-#define RL_NBUF 3
-#endif
-constexpr uint32_t NBUF = RL_NBUF;
-constexpr uint32_t PROF_RING = 8;  // timed batches in flight (> NBUF)
+namespace {
+
+constexpr uint32_t MAX_LOCAL_SHARDS = 16;
+constexpr uint32_t RSLOTS = 3;
+
+struct RouteSlot {
+  Wire* send_rec = nullptr;              // dev0: wire records in owner order
+  uint8_t* send_stem = nullptr;          // dev0: their stems
+  uint32_t* perm = nullptr;              // dev0: record -> batch index
+  unsigned long long* counts = nullptr;  // dev0: [2 x n] records / stem bytes per owner
+  unsigned long long* back = nullptr;    // dev0: packed results, record order
+  unsigned long long* stats_stage = nullptr;  // dev0: [n][max_rules x RL_NUM_STATS] owners' deltas
+  Wire* recv_rec[MAX_LOCAL_SHARDS] = {};      // owner devices: received records
+  uint8_t* recv_stem[MAX_LOCAL_SHARDS] = {};
+  unsigned long long* ostats[MAX_LOCAL_SHARDS] = {};
+  uint32_t k[MAX_LOCAL_SHARDS] = {};     // owner engine buffer of this slot's batch
+  hipEvent_t packed = nullptr;           // forward stream: partition + counts copy done
+  hipEvent_t done = nullptr;             // return stream: results and stats complete
+};
+
+}  // namespace
 
 struct rl_ctx {
   rl_config cfg;
-  hipStream_t stream = nullptr;   // serial work (== pipe[0])
-  hipStream_t pipe[NBUF] = {};    // one per scratch buffer
-  hipEvent_t b_done[NBUF] = {};   // stage B of the last batch on each buffer is done
-  hipStream_t side = nullptr;     // k_runs_general beside k_runs (stage B)
-  hipEvent_t side_go = nullptr, side_done = nullptr;
-  uint32_t next = 0, last = NBUF - 1;  // buffer of the next / of the latest batch
-  uint64_t hash_seed = 0;
-  HashKey hk{};
-  // table
-  Slot* slots = nullptr;
-  uint64_t nslots = 0;
-  uint8_t* arena = nullptr;
-  uint8_t* arena2 = nullptr;  // compaction target (rl_sweep), swapped with arena
-  uint64_t arena_cap16 = 0;
-  // scratch: s[k] per buffer; stripes, counters, time floor, routing and the
-  // table-stage error word are shared
-  Scratch s[NBUF]{};
-  uint32_t* errw = nullptr;  // [0, NBUF) stage-A words of the buffers, [NBUF] stage-B word, [NBUF+1] soft word
-  // device staging for the host-buffer entry points
+  uint32_t n = 1;
+  Engine* e[MAX_LOCAL_SHARDS] = {};
+  CommRouter* comm = nullptr;  // rl_comm_init: multi-process routing (single-shard ctx)
+  std::string last_error;
+  // router (n > 1), on shard 0's device
+  int dev0 = 0;
+  hipStream_t fwd = nullptr, ret = nullptr;
+  hipEvent_t fwd_ready = nullptr, in_ready = nullptr;
+  RouteSlot slot[RSLOTS];
+  uint32_t next_slot = 0;
+  unsigned long long* h_counts = nullptr;  // pinned [RSLOTS][2 x MAX_LOCAL_SHARDS]
+  // staging for the host-buffer entry point (dev0)
   uint8_t* d_stem = nullptr;
   uint32_t *d_off = nullptr, *d_req = nullptr, *d_limit = nullptr, *d_hits = nullptr, *d_rule = nullptr;
   int64_t* d_now = nullptr;
   uint8_t *d_unit = nullptr, *d_flags = nullptr, *d_code = nullptr, *d_status = nullptr;
   uint32_t *d_rem = nullptr, *d_reset = nullptr;
   unsigned long long* d_stats = nullptr;
-  uint32_t* h_err = nullptr;  // pinned [4]
-  unsigned long long* h_counters = nullptr;
-  unsigned long long* h_route = nullptr;  // pinned route counts
-  std::string last_error;
-  uint64_t batches = 0, decisions = 0;
-  // rl_profile: a ring of per-batch event sets (stage boundaries, recorded on
-  // the batch's own stream, so pipelined batches are timed as they run),
-  // folded into the stage sums when a set is reused or read
-  bool prof = false;
-  uint32_t prof_every = 1, prof_skip = 0;  // time every prof_every-th batch
-  bool prof_pending[PROF_RING] = {};
-  uint32_t prof_next = 0;
-  hipEvent_t ev[PROF_RING][RL_NUM_STAGES + 1] = {};
-  double stage_ms[RL_NUM_STAGES] = {};
-  uint64_t prof_batches = 0;
-  // config match (rl_config_load / rl_do_limit_requests): the device trie and
-  // one growable device buffer carved per call for the raw requests
-  uint8_t* cfg_blob = nullptr;  // [nodes | index | prefix ‖ keys]
-  CfgDev cfg_dev{};
-  bool cfg_loaded = false;
-  uint8_t* mbuf = nullptr;
-  size_t mbuf_cap = 0;
-  uint32_t* h_match = nullptr;  // pinned [4]: matched count, stem bytes, error bits
 };
 
 namespace {
 
-thread_local std::string g_err;
+thread_local std::string g_api_err;
 
-int set_err(rl_ctx* c, int code, const std::string& msg);
-
-// Fold event set k (a timed batch) into the stage sums; waits for the batch.
-void prof_fold(rl_ctx* c, uint32_t k) {
-  if (!c->prof_pending[k]) return;
-  c->prof_pending[k] = false;
-  if (hipEventSynchronize(c->ev[k][RL_NUM_STAGES]) != hipSuccess) return;
-  for (int i = 0; i < RL_NUM_STAGES; i++) {
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, c->ev[k][i], c->ev[k][i + 1]) == hipSuccess) c->stage_ms[i] += ms;
-  }
-  c->prof_batches++;
-}
-
-void prof_fold_all(rl_ctx* c) {
-  for (uint32_t k = 0; k < PROF_RING; k++) prof_fold(c, (c->prof_next + k) % PROF_RING);
-}
-
-hipEvent_t* prof_events(rl_ctx* c) {
-  if (!c->prof) return nullptr;
-  if (c->prof_skip) {
-    c->prof_skip--;
-    return nullptr;
-  }
-  c->prof_skip = c->prof_every - 1;
-  const uint32_t k = c->prof_next;
-  c->prof_next = (k + 1) % PROF_RING;
-  prof_fold(c, k);  // the batch that used this set PROF_RING batches ago
-  c->prof_pending[k] = true;
-  return c->ev[k];
-}
-
-int set_err(rl_ctx* c, int code, const std::string& msg) {
+int fail(rl_ctx* c, int code, const std::string& msg) {
   if (c) c->last_error = msg;
-  else g_err = msg;
+  else g_api_err = msg;
   return code;
 }
 
-#define HIPCHK(c, expr)                                                                        \
-  do {                                                                                         \
-    hipError_t _e = (expr);                                                                    \
-    if (_e != hipSuccess)                                                                      \
-      return set_err((c), RL_E_HIP, std::string("gpu: ") + #expr + ": " + hipGetErrorString(_e)); \
+// An engine's failure, surfaced through the ctx.
+int from_engine(rl_ctx* c, Engine* e, int rc) {
+  if (rc && c->n > 1) c->last_error = eng_last_error(e);
+  return rc;
+}
+
+#define API_HIP(c, expr)                                                                        \
+  do {                                                                                          \
+    hipError_t _e = (expr);                                                                     \
+    if (_e != hipSuccess)                                                                       \
+      return fail((c), RL_E_HIP, std::string("gpu: ") + #expr + ": " + hipGetErrorString(_e));  \
   } while (0)
 
 template <typename T>
@@ -140,177 +109,284 @@ hipError_t dalloc(T** p, size_t count) {
   return hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T));
 }
 
-int map_err(rl_ctx* c, uint32_t e) {
-  if (!e) return RL_OK;
-  if (e & ERR_TIME) return set_err(c, RL_E_TIME, "gpu: now outside [0, 2^32-172800] or before the last sweep");
-  if (e & ERR_HISTORY)
-    return set_err(c, RL_E_TIME, "gpu: time moved back beyond the previous window of a key (table keeps 2 windows)");
-  if (e & ERR_INVALID) return set_err(c, RL_E_INVALID, "gpu: malformed batch (unit, rule id, request index or stem offsets)");
-  if (e & ERR_TABLE_FULL) return set_err(c, RL_E_TABLE_FULL, "gpu: counter table full (raise table_slots or sweep)");
-  if (e & ERR_ARENA_FULL) return set_err(c, RL_E_ARENA_FULL, "gpu: long-stem arena full (raise arena_bytes)");
-  return set_err(c, RL_E_INTERNAL, "gpu: unknown device error");
-}
+uint32_t owner_of_host(uint64_t h, uint32_t n) { return (uint32_t)(((uint64_t)(uint32_t)h * n) >> 32); }
 
-// Order stream st after every batch submitted so far (their stage B, which
-// waited for all earlier ones).
-hipError_t after_batches(rl_ctx* c, hipStream_t st) { return hipStreamWaitEvent(st, c->b_done[c->last], 0); }
-
-// Read (and clear) the sticky device error words; synchronises the stream,
-// which must already be ordered after all submitted work.
-// The soft word (descriptor errors answered by statuses) is cleared, not reported.
-int collect(rl_ctx* c, hipStream_t st = nullptr) {
-  if (!st) st = c->stream;
-  HIPCHK(c, hipMemcpyAsync(c->h_err, c->errw, (NBUF + 2) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipStreamSynchronize(st));
-  uint32_t e = 0;
-  for (uint32_t j = 0; j <= NBUF; j++) e |= c->h_err[j];
-  if (e || c->h_err[NBUF + 1]) {
-    HIPCHK(c, hipMemsetAsync(c->errw, 0, (NBUF + 2) * sizeof(uint32_t), st));
-    HIPCHK(c, hipStreamSynchronize(st));
+void free_router(rl_ctx* c) {
+  for (uint32_t s = 0; s < RSLOTS; s++) {
+    RouteSlot& S = c->slot[s];
+    void* dev0_bufs[] = {S.send_rec, S.send_stem, S.perm, S.counts, S.back, S.stats_stage};
+    (void)hipSetDevice(c->dev0);
+    for (void* p : dev0_bufs)
+      if (p) (void)hipFree(p);
+    for (uint32_t j = 0; j < c->n; j++) {
+      (void)hipSetDevice(c->cfg.shard_device[j]);
+      for (void* p : {(void*)S.recv_rec[j], (void*)S.recv_stem[j], (void*)S.ostats[j]})
+        if (p) (void)hipFree(p);
+    }
+    (void)hipSetDevice(c->dev0);
+    if (S.packed) (void)hipEventDestroy(S.packed);
+    if (S.done) (void)hipEventDestroy(S.done);
   }
-  return map_err(c, e);
+  (void)hipSetDevice(c->dev0);
+  void* bufs[] = {c->d_stem, c->d_off, c->d_req, c->d_limit, c->d_hits, c->d_rule, c->d_now, c->d_unit,
+                  c->d_flags, c->d_code, c->d_status, c->d_rem, c->d_reset, c->d_stats};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+  if (c->h_counts) (void)hipHostFree(c->h_counts);
+  for (hipEvent_t ev : {c->fwd_ready, c->in_ready})
+    if (ev) (void)hipEventDestroy(ev);
+  for (hipStream_t st : {c->fwd, c->ret})
+    if (st) (void)hipStreamDestroy(st);
 }
 
-TableDev table_view(rl_ctx* c);
-Params params(rl_ctx* c, int isolate = 0);
-
-// Enqueue one batch. Pipelined (ctx streams): stage A on the buffer's own
-// stream as soon as the buffer is free, stage B after the previous batch's
-// stage B. Serial: both stages on `st` after all earlier work. With rl_profile
-// on, the stage boundaries are recorded on the batch's stream either way.
-uint32_t enqueue(rl_ctx* c, const BatchDev& b, const OutDev& o, int restore, hipStream_t st, bool pipelined) {
-  const uint32_t k = c->next;
-  c->next = (k + 1) % NBUF;
-  const TableDev t = table_view(c);
-  const int isolate = (!restore && o.status) ? 1 : 0;
-  const Params P = params(c, isolate);
-  if (pipelined) {
-    hipStream_t a = c->pipe[k];
-    hipEvent_t* ev = prof_events(c);
-    (void)hipStreamWaitEvent(a, c->b_done[k], 0);  // buffer k's previous batch is done
-    launch_stage_a(b, c->s[k], isolate, a, ev);
-    (void)hipStreamWaitEvent(a, c->b_done[c->last], 0);  // table order
-    launch_stage_b(b, o, t, P, c->s[k], restore, a, c->side, c->side_go, c->side_done, ev);
-    (void)hipEventRecord(c->b_done[k], a);
-  } else {
-    if (!st) st = c->stream;
-    (void)after_batches(c, st);
-    hipEvent_t* ev = prof_events(c);
-    launch_stage_a(b, c->s[k], isolate, st, ev);
-    launch_stage_b(b, o, t, P, c->s[k], restore, st, c->side, c->side_go, c->side_done, ev);
-    (void)hipEventRecord(c->b_done[k], st);
+bool alloc_router(rl_ctx* c) {
+  const rl_config& g = c->cfg;
+  const uint32_t n = g.max_batch, sb = g.max_stem_bytes, m = g.max_rules * RL_NUM_STATS;
+  // every pair of distinct shard devices talks directly over xGMI
+  for (uint32_t i = 0; i < c->n; i++)
+    for (uint32_t j = 0; j < c->n; j++) {
+      const int di = g.shard_device[i], dj = g.shard_device[j];
+      if (di == dj) continue;
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, di, dj) == hipSuccess && can) {
+        (void)hipSetDevice(di);
+        const hipError_t e = hipDeviceEnablePeerAccess(dj, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return false;
+        (void)hipGetLastError();
+      }
+    }
+  if (hipSetDevice(c->dev0) != hipSuccess) return false;
+  bool ok = hipStreamCreateWithFlags(&c->fwd, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->ret, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&c->fwd_ready, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->in_ready, hipEventDisableTiming) == hipSuccess &&
+            hipHostMalloc((void**)&c->h_counts, RSLOTS * 2 * MAX_LOCAL_SHARDS * 8) == hipSuccess;
+  for (uint32_t s = 0; s < RSLOTS && ok; s++) {
+    RouteSlot& S = c->slot[s];
+    ok = dalloc(&S.send_rec, n) == hipSuccess && dalloc(&S.send_stem, (size_t)sb + 64) == hipSuccess &&
+         dalloc(&S.perm, n) == hipSuccess && dalloc(&S.counts, 2 * RL_MAX_SHARDS) == hipSuccess &&
+         dalloc(&S.back, n) == hipSuccess && dalloc(&S.stats_stage, (size_t)c->n * m) == hipSuccess &&
+         hipEventCreateWithFlags(&S.packed, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&S.done, hipEventDisableTiming) == hipSuccess &&
+         hipEventRecord(S.done, c->ret) == hipSuccess;
+    for (uint32_t j = 0; j < c->n && ok; j++) {
+      ok = hipSetDevice(g.shard_device[j]) == hipSuccess && dalloc(&S.recv_rec[j], n) == hipSuccess &&
+           dalloc(&S.recv_stem[j], (size_t)sb + 64) == hipSuccess && dalloc(&S.ostats[j], m) == hipSuccess;
+    }
+    ok = ok && hipSetDevice(c->dev0) == hipSuccess;
   }
-  c->last = k;
-  return k;
-}
-
-int check_sizes(rl_ctx* c, const rl_batch* in, uint64_t stem_bytes) {
-  if (!in) return set_err(c, RL_E_INVALID, "gpu: null batch");
-  if (in->n > c->cfg.max_batch || in->n_requests > c->cfg.max_requests || in->n_rules > c->cfg.max_rules ||
-      stem_bytes > c->cfg.max_stem_bytes)
-    return set_err(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_rules/max_stem_bytes");
-  if (in->n && in->n_requests == 0) return set_err(c, RL_E_INVALID, "gpu: descriptors without requests");
-  return RL_OK;
-}
-
-BatchDev dev_view(const rl_ctx* c, const rl_batch* in, uint32_t stem_cap) {
-  BatchDev b;
-  b.hk = c->hk;
-  b.n = in->n;
-  b.n_req = in->n_requests;
-  b.n_rules = in->n_rules;
-  b.stem_cap = stem_cap;
-  b.stem_total = stem_cap;  // refined on the device from off[n]
-  b.now_desc = 0;
-  b.stem = in->stem_bytes;
-  b.off = in->stem_off;
-  b.now = in->now;
-  b.req = in->req_idx;
-  b.unit = in->unit;
-  b.flags = in->flags;
-  b.limit = in->limit;
-  b.hits = in->hits;
-  b.rule = in->rule_id;
-  return b;
-}
-
-TableDev table_view(rl_ctx* c) {
-  TableDev t;
-  t.slots = c->slots;
-  t.mask = c->nslots - 1;
-  t.arena = c->arena;
-  t.arena_used16 = c->s[0].counters + 4;
-  t.arena_cap16 = c->arena_cap16;
-  t.max_probe = (uint32_t)std::min<uint64_t>(c->nslots, 1u << 16);
-  t.shift = 64u - (uint32_t)__builtin_ctzll(c->nslots);
-  return t;
-}
-
-Params params(rl_ctx* c, int isolate) {
-  Params P;
-  P.ratio = c->cfg.near_limit_ratio;
-  P.lc_en = c->cfg.local_cache_enabled != 0;
-  P.per_second = c->cfg.per_second_split != 0;
-  P.isolate = isolate;
-  return P;
-}
-
-// Per-batch scratch of one pipeline buffer (sized for max_batch descriptors).
-bool alloc_buffer(Scratch& s, uint32_t n) {
-  const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
-  const size_t nt = (n + SEG_TILE - 1) / SEG_TILE + 1;
-  const size_t items = (size_t)n / (64 * 4 * 8) + 1 + PART_DIGITS;  // BIG_CHUNK-position work items
-  bool ok = dalloc(&s.big_meta, PART_DIGITS) == hipSuccess && dalloc(&s.big_n, 1) == hipSuccess &&
-            dalloc(&s.big_work, items) == hipSuccess && dalloc(&s.work_n, 1) == hipSuccess &&
-            dalloc(&s.big_cnt, items * (1 + 2 * BIG_HEAVY)) == hipSuccess;
-  ok = ok && dalloc(&s.rec, n) == hipSuccess && dalloc(&s.res, n) == hipSuccess;
-  for (int i = 0; i < 2; i++) ok = ok && dalloc(&s.keys[i], n) == hipSuccess && dalloc(&s.vals[i], n) == hipSuccess;
-  ok = ok && dalloc(&s.hist, 256ull * std::max(ntiles, 1u)) == hipSuccess && dalloc(&s.hist_tot, 256) == hipSuccess;
-  ok = ok && dalloc(&s.grp, n) == hipSuccess && dalloc(&s.lead, n) == hipSuccess && dalloc(&s.gmask, n) == hipSuccess &&
-       dalloc(&s.defer, n) == hipSuccess &&
-       dalloc(&s.defer_n, 1) == hipSuccess && dalloc(&s.defer2, n) == hipSuccess &&
-       dalloc(&s.defer1, n) == hipSuccess && dalloc(&s.defer1_n, 1) == hipSuccess &&
-       dalloc(&s.defer2_n, 1) == hipSuccess && dalloc(&s.fast_blk, (size_t)n / (256 * 32) + 1) == hipSuccess;
-  ok = ok && dalloc(&s.tile_f, nt) == hipSuccess && dalloc(&s.tile_s, nt) == hipSuccess &&
-       dalloc(&s.tile_h, nt) == hipSuccess;
-  ok = ok && dalloc(&s.hits_s, n) == hipSuccess && dalloc(&s.segsum, n) == hipSuccess &&
-       dalloc(&s.rid, n) == hipSuccess && dalloc(&s.run_start, (size_t)n + 1) == hipSuccess &&
-       dalloc(&s.run_flags, n) == hipSuccess && dalloc(&s.run_state, n) == hipSuccess &&
-       dalloc(&s.run_f, n) == hipSuccess && dalloc(&s.num_runs, 1) == hipSuccess &&
-       dalloc(&s.runs64, 1) == hipSuccess && dalloc(&s.drun, (size_t)n / 2 + BIG_HEAVY * PART_DIGITS) == hipSuccess;
-  ok = ok && dalloc(&s.hit_a, n) == hipSuccess && dalloc(&s.tile, n) == hipSuccess &&
-       dalloc(&s.hit_t, n) == hipSuccess;
-  ok = ok && dalloc(&s.run_end, n) == hipSuccess &&
-       dalloc(&s.part_info, (size_t)PART_DIGITS * std::max((n + PART_TILE - 1) / PART_TILE, 1u)) == hipSuccess;
+  ok = ok && dalloc(&c->d_stem, (size_t)sb + 64) == hipSuccess && dalloc(&c->d_off, (size_t)n + 1) == hipSuccess &&
+       dalloc(&c->d_req, n) == hipSuccess && dalloc(&c->d_limit, n) == hipSuccess &&
+       dalloc(&c->d_hits, n) == hipSuccess && dalloc(&c->d_rule, n) == hipSuccess &&
+       dalloc(&c->d_now, g.max_requests) == hipSuccess && dalloc(&c->d_unit, n) == hipSuccess &&
+       dalloc(&c->d_flags, n) == hipSuccess && dalloc(&c->d_code, n) == hipSuccess &&
+       dalloc(&c->d_status, n) == hipSuccess && dalloc(&c->d_rem, n) == hipSuccess &&
+       dalloc(&c->d_reset, n) == hipSuccess && dalloc(&c->d_stats, m) == hipSuccess;
+  ok = ok && hipStreamSynchronize(c->ret) == hipSuccess;
   return ok;
 }
 
-void free_buffer(Scratch& s) {
-  void* bufs[] = {s.rec, s.res, s.big_meta, s.big_n, s.big_work, s.work_n, s.big_cnt, s.keys[0], s.keys[1], s.vals[0], s.vals[1], s.hist,
-                  s.hist_tot, s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1, s.defer1_n, s.fast_blk, s.tile_f, s.tile_s, s.tile_h, s.hits_s, s.segsum, s.rid,
-                  s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs, s.runs64, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t};
-  for (void* p : bufs)
-    if (p) (void)hipFree(p);
+// One routed batch (device arrays on dev0; see the file comment).
+int routed_async(rl_ctx* c, const rl_batch* in, rl_result* out, hipStream_t caller) {
+  const uint32_t n = in->n, N = c->n;
+  if (n > c->cfg.max_batch || in->n_requests > c->cfg.max_requests || in->n_rules > c->cfg.max_rules)
+    return fail(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_rules");
+  const uint32_t s = c->next_slot;
+  c->next_slot = (s + 1) % RSLOTS;
+  RouteSlot& S = c->slot[s];
+  Engine* e0 = c->e[0];
+  API_HIP(c, hipSetDevice(c->dev0));
+  API_HIP(c, hipStreamWaitEvent(c->fwd, S.done, 0));  // the slot's previous batch is complete
+  if (caller) {
+    API_HIP(c, hipEventRecord(c->in_ready, caller));
+    API_HIP(c, hipStreamWaitEvent(c->fwd, c->in_ready, 0));
+  }
+  int rc = eng_route_pack(e0, in, N, 0, S.send_rec, S.send_stem, S.perm, (uint64_t*)S.counts, c->fwd);
+  if (rc) return from_engine(c, e0, rc);
+  unsigned long long* hc = c->h_counts + (size_t)s * 2 * MAX_LOCAL_SHARDS;
+  API_HIP(c, hipMemcpyAsync(hc, S.counts, 2ull * N * 8, hipMemcpyDeviceToHost, c->fwd));
+  API_HIP(c, hipEventRecord(S.packed, c->fwd));
+  API_HIP(c, hipEventSynchronize(S.packed));  // the one host wait: this batch's partition
+  uint64_t roff[MAX_LOCAL_SHARDS], soff[MAX_LOCAL_SHARDS], acc_r = 0, acc_s = 0;
+  for (uint32_t j = 0; j < N; j++) {
+    roff[j] = acc_r;
+    soff[j] = acc_s;
+    acc_r += hc[2 * j];
+    acc_s += hc[2 * j + 1];
+  }
+  if (acc_r != (n ? n : 0) && acc_r != 0) return fail(c, RL_E_INTERNAL, "gpu: routing counts do not add up");
+  for (uint32_t j = 0; j < N; j++) {
+    const int dj = c->cfg.shard_device[j];
+    if (hc[2 * j])
+      API_HIP(c, hipMemcpyPeerAsync(S.recv_rec[j], dj, S.send_rec + roff[j], c->dev0, hc[2 * j] * sizeof(Wire),
+                                    c->fwd));
+    if (hc[2 * j + 1])
+      API_HIP(c, hipMemcpyPeerAsync(S.recv_stem[j], dj, S.send_stem + soff[j], c->dev0, hc[2 * j + 1], c->fwd));
+  }
+  API_HIP(c, hipEventRecord(c->fwd_ready, c->fwd));
+  const int isolate = out->status ? 1 : 0;
+  const uint64_t zero = 0;
+  for (uint32_t j = 0; j < N; j++) {
+    rc = eng_route_owner(c->e[j], (uint32_t)hc[2 * j], S.recv_rec[j], S.recv_stem[j], hc[2 * j + 1], &zero, 1,
+                         in->n_rules, 0, S.ostats[j], isolate, c->fwd_ready, &S.k[j]);
+    if (rc) return from_engine(c, c->e[j], rc);
+  }
+  API_HIP(c, hipSetDevice(c->dev0));
+  const uint32_t m = in->n_rules * RL_NUM_STATS;
+  for (uint32_t j = 0; j < N; j++) {
+    Engine* ej = c->e[j];
+    const uint32_t k = S.k[j];
+    const int dj = c->cfg.shard_device[j];
+    API_HIP(c, hipStreamWaitEvent(c->ret, ej->b_done[k], 0));
+    if (hc[2 * j])
+      API_HIP(c, hipMemcpyPeerAsync(S.back + roff[j], c->dev0, ej->s[k].res, dj, hc[2 * j] * 8, c->ret));
+    if (m) API_HIP(c, hipMemcpyPeerAsync(S.stats_stage + (size_t)j * m, c->dev0, S.ostats[j], dj, (size_t)m * 8, c->ret));
+    API_HIP(c, hipEventRecord(ej->consumed[k], c->ret));
+  }
+  OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats, out->status};
+  launch_route_scatter(S.perm, S.back, n, o, c->ret);
+  if (m && out->stats) launch_stats_sum(S.stats_stage, N, m, (unsigned long long*)out->stats, c->ret);
+  API_HIP(c, hipGetLastError());
+  API_HIP(c, hipEventRecord(S.done, c->ret));
+  if (caller) API_HIP(c, hipStreamWaitEvent(caller, S.done, 0));
+  return RL_OK;
 }
 
-// Copy a host batch into the staging buffers; returns the device view.
-int stage(rl_ctx* c, const rl_batch* in, BatchDev* out) {
+int synchronize_all(rl_ctx* c) {
+  if (c->comm) {
+    const int rc = comm_synchronize(c->comm, c->e[0]);
+    if (rc) return rc;
+  }
+  if (c->n > 1) {
+    API_HIP(c, hipSetDevice(c->dev0));
+    API_HIP(c, hipStreamSynchronize(c->fwd));
+    API_HIP(c, hipStreamSynchronize(c->ret));
+  }
+  int first = RL_OK;
+  for (uint32_t j = 0; j < c->n; j++) {
+    const int rc = from_engine(c, c->e[j], eng_synchronize(c->e[j]));
+    if (rc && !first) first = rc;
+  }
+  if (first && c->n > 1) {  // keep the first failing shard's message
+    for (uint32_t j = 0; j < c->n; j++)
+      if (*eng_last_error(c->e[j])) {
+        c->last_error = eng_last_error(c->e[j]);
+        break;
+      }
+  }
+  return first;
+}
+
+constexpr uint64_t MSNAP_MAGIC = 0x31304853414e534cull;  // "LSNASH01": one image per shard
+
+}  // namespace
+
+extern "C" {
+
+uint32_t rl_abi_version(void) { return RL_ABI_VERSION; }
+
+const char* rl_last_error(const rl_ctx* c) {
+  if (!c) return g_api_err.c_str();
+  return c->n == 1 ? eng_last_error(c->e[0]) : c->last_error.c_str();
+}
+
+rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
+  auto bad = [&](const std::string& m) -> rl_ctx* {
+    if (err && errlen) snprintf(err, errlen, "%s", m.c_str());
+    g_api_err = m;
+    return nullptr;
+  };
+  if (!cfg_in) return bad("gpu: null config");
+  rl_config cfg = *cfg_in;
+  const uint32_t n = cfg.n_shards ? cfg.n_shards : 1;
+  if (n > MAX_LOCAL_SHARDS) return bad("gpu: n_shards must be at most 16");
+  rl_ctx* c = new rl_ctx();
+  if (n == 1) {
+    cfg.n_shards = 1;
+    c->e[0] = eng_create(&cfg, err, errlen);
+    if (!c->e[0]) {
+      delete c;
+      return nullptr;
+    }
+    c->cfg = c->e[0]->cfg;
+    return c;
+  }
+  // one key for every shard: the owner of a stem is a function of its hash
+  while (!cfg.hash_seed) {
+    std::random_device rd;
+    cfg.hash_seed = ((uint64_t)rd() << 32) ^ rd();
+  }
+  if (!cfg.max_batch) cfg.max_batch = 1u << 20;
+  if (!cfg.max_requests) cfg.max_requests = cfg.max_batch;
+  if (!cfg.max_rules) cfg.max_rules = 65536;
+  if (!cfg.max_stem_bytes) cfg.max_stem_bytes = 128u * cfg.max_batch;
+  c->n = n;
+  c->cfg = cfg;
+  c->dev0 = cfg.shard_device[0];
+  for (uint32_t j = 0; j < n; j++) {
+    rl_config ec = cfg;
+    ec.n_shards = 1;
+    ec.device = cfg.shard_device[j];
+    c->e[j] = eng_create(&ec, err, errlen);
+    if (!c->e[j]) {
+      const std::string m = g_api_err = (err && errlen) ? std::string(err) : std::string("gpu: shard creation failed");
+      rl_destroy(c);
+      return bad(m);
+    }
+  }
+  c->cfg = c->e[0]->cfg;
+  c->cfg.n_shards = n;
+  for (uint32_t j = 0; j < MAX_LOCAL_SHARDS; j++) c->cfg.shard_device[j] = cfg.shard_device[j];
+  if (!alloc_router(c)) {
+    rl_destroy(c);
+    return bad("gpu: router allocation failed (peer access or device memory)");
+  }
+  return c;
+}
+
+void rl_destroy(rl_ctx* c) {
+  if (!c) return;
+  if (c->comm) comm_destroy(c->comm);
+  if (c->n > 1) {
+    (void)hipSetDevice(c->dev0);
+    if (c->fwd) (void)hipStreamSynchronize(c->fwd);
+    if (c->ret) (void)hipStreamSynchronize(c->ret);
+    free_router(c);
+  }
+  for (uint32_t j = 0; j < c->n; j++)
+    if (c->e[j]) eng_destroy(c->e[j]);
+  delete c;
+}
+
+int rl_do_limit_async(rl_ctx* c, const rl_batch* in, rl_result* out, void* stream) {
+  if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (c->n == 1) return eng_do_limit_async(c->e[0], in, out, stream);
+  if ((uintptr_t)in->stem_bytes & 3u) return fail(c, RL_E_INVALID, "gpu: stem_bytes must be 4-byte aligned");
+  return routed_async(c, in, out, (hipStream_t)stream);
+}
+
+int rl_do_limit(rl_ctx* c, const rl_batch* in, rl_result* out) {
+  if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (c->n == 1) return eng_do_limit(c->e[0], in, out);
   const uint32_t n = in->n, nq = in->n_requests;
   const uint64_t nb = n ? in->stem_off[n] : 0;
-  int rc = check_sizes(c, in, nb);
-  if (rc) return rc;
-  hipStream_t st = c->stream;
-  HIPCHK(c, after_batches(c, st));  // staging may still feed a routed batch
-  if (nb) HIPCHK(c, hipMemcpyAsync(c->d_stem, in->stem_bytes, nb, hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(c->d_off, in->stem_off, (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-  if (nq) HIPCHK(c, hipMemcpyAsync(c->d_now, in->now, nq * sizeof(int64_t), hipMemcpyHostToDevice, st));
+  if (n > c->cfg.max_batch || nq > c->cfg.max_requests || in->n_rules > c->cfg.max_rules ||
+      nb > c->cfg.max_stem_bytes)
+    return fail(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_rules/max_stem_bytes");
+  if (n && !nq) return fail(c, RL_E_INVALID, "gpu: descriptors without requests");
+  API_HIP(c, hipSetDevice(c->dev0));
+  hipStream_t st = c->fwd;
+  API_HIP(c, hipStreamWaitEvent(st, c->slot[(c->next_slot + RSLOTS - 1) % RSLOTS].done, 0));  // staging is free
+  if (nb) API_HIP(c, hipMemcpyAsync(c->d_stem, in->stem_bytes, nb, hipMemcpyHostToDevice, st));
+  API_HIP(c, hipMemcpyAsync(c->d_off, in->stem_off, (n + 1) * 4ull, hipMemcpyHostToDevice, st));
+  if (nq) API_HIP(c, hipMemcpyAsync(c->d_now, in->now, nq * 8ull, hipMemcpyHostToDevice, st));
   if (n) {
-    HIPCHK(c, hipMemcpyAsync(c->d_req, in->req_idx, n * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(c, hipMemcpyAsync(c->d_unit, in->unit, n, hipMemcpyHostToDevice, st));
-    HIPCHK(c, hipMemcpyAsync(c->d_flags, in->flags, n, hipMemcpyHostToDevice, st));
-    HIPCHK(c, hipMemcpyAsync(c->d_limit, in->limit, n * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(c, hipMemcpyAsync(c->d_hits, in->hits, n * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(c, hipMemcpyAsync(c->d_rule, in->rule_id, n * 4, hipMemcpyHostToDevice, st));
+    API_HIP(c, hipMemcpyAsync(c->d_req, in->req_idx, n * 4ull, hipMemcpyHostToDevice, st));
+    API_HIP(c, hipMemcpyAsync(c->d_unit, in->unit, n, hipMemcpyHostToDevice, st));
+    API_HIP(c, hipMemcpyAsync(c->d_flags, in->flags, n, hipMemcpyHostToDevice, st));
+    API_HIP(c, hipMemcpyAsync(c->d_limit, in->limit, n * 4ull, hipMemcpyHostToDevice, st));
+    API_HIP(c, hipMemcpyAsync(c->d_hits, in->hits, n * 4ull, hipMemcpyHostToDevice, st));
+    API_HIP(c, hipMemcpyAsync(c->d_rule, in->rule_id, n * 4ull, hipMemcpyHostToDevice, st));
   }
   rl_batch d = *in;
   d.stem_bytes = c->d_stem;
@@ -322,378 +398,264 @@ int stage(rl_ctx* c, const rl_batch* in, BatchDev* out) {
   d.limit = c->d_limit;
   d.hits = c->d_hits;
   d.rule_id = c->d_rule;
-  *out = dev_view(c, &d, c->cfg.max_stem_bytes);
-  return RL_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-uint32_t rl_abi_version(void) { return RL_ABI_VERSION; }
-
-const char* rl_last_error(const rl_ctx* c) { return c ? c->last_error.c_str() : g_err.c_str(); }
-
-rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
-  auto fail = [&](const std::string& m, rl_ctx* c) -> rl_ctx* {
-    if (err && errlen) snprintf(err, errlen, "%s", m.c_str());
-    g_err = m;
-    if (c) rl_destroy(c);
-    return nullptr;
-  };
-  if (!cfg_in) return fail("gpu: null config", nullptr);
-  rl_config cfg = *cfg_in;
-  if (!cfg.table_slots) cfg.table_slots = 1ull << 24;
-  if (cfg.table_slots & (cfg.table_slots - 1)) return fail("gpu: table_slots must be a power of two", nullptr);
-  if (!cfg.arena_bytes) cfg.arena_bytes = 64ull << 20;
-  if (!cfg.max_batch) cfg.max_batch = 1u << 20;
-  if (cfg.max_batch > MAX_PART_TILES * PART_TILE)
-    return fail("gpu: max_batch must be at most 8388608 descriptors", nullptr);
-  if (!cfg.max_requests) cfg.max_requests = cfg.max_batch;
-  if (!cfg.max_rules) cfg.max_rules = 65536;
-  if (!cfg.max_stem_bytes) cfg.max_stem_bytes = 128u * cfg.max_batch;
-  if (hipSetDevice(cfg.device) != hipSuccess) return fail("gpu: hipSetDevice failed", nullptr);
-
-  rl_ctx* c = new rl_ctx();
-  c->cfg = cfg;
-  c->hash_seed = cfg.hash_seed;
-  while (!c->hash_seed) {  // a secret per-ctx key unless the caller shares one (multi-shard tables)
-    std::random_device rd;
-    c->hash_seed = ((uint64_t)rd() << 32) ^ rd();
-  }
-  c->cfg.hash_seed = c->hash_seed;
-  c->hk = hash_key_of(c->hash_seed, cfg.debug_hash_bits);
-  c->nslots = cfg.table_slots;
-  c->arena_cap16 = cfg.arena_bytes / 16;
-  const uint32_t n = cfg.max_batch;
-  bool ok = true;
-  for (uint32_t k = 0; k < NBUF; k++) ok = ok && hipStreamCreateWithFlags(&c->pipe[k], hipStreamNonBlocking) == hipSuccess;
-  c->stream = c->pipe[0];
-  ok = ok && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess;
-  for (uint32_t k = 0; k < NBUF; k++)
-    ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess;
-  ok = ok && hipEventCreateWithFlags(&c->side_go, hipEventDisableTiming) == hipSuccess &&
-       hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming) == hipSuccess;
-  ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess;
-  ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess && dalloc(&c->arena2, cfg.arena_bytes) == hipSuccess;
-  for (uint32_t k = 0; k < NBUF; k++) ok = ok && alloc_buffer(c->s[k], n);
-  Scratch& s0 = c->s[0];
-  ok = ok && dalloc(&c->errw, NBUF + 2) == hipSuccess;
-  ok = ok && dalloc(&s0.stripes, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS) == hipSuccess;
-  ok = ok && dalloc(&s0.time_floor, 1) == hipSuccess;
-  ok = ok && dalloc(&s0.counters, 8) == hipSuccess;
-  ok = ok && dalloc(&s0.route_start, RL_MAX_SHARDS + 1) == hipSuccess &&
-       dalloc(&s0.route_base, RL_MAX_SHARDS) == hipSuccess && dalloc(&s0.route_counts, 2 * RL_MAX_SHARDS) == hipSuccess;
-  for (uint32_t k = 0; k < NBUF; k++) {  // shared members
-    Scratch& sk = c->s[k];
-    sk.err = c->errw ? c->errw + k : nullptr;
-    sk.errb = c->errw ? c->errw + NBUF : nullptr;
-    sk.errs = c->errw ? c->errw + NBUF + 1 : nullptr;
-    sk.stripes = s0.stripes;
-    sk.time_floor = s0.time_floor;
-    sk.counters = s0.counters;
-    sk.route_start = s0.route_start;
-    sk.route_base = s0.route_base;
-    sk.route_counts = s0.route_counts;
-  }
-  ok = ok && hipHostMalloc((void**)&c->h_route, 2 * RL_MAX_SHARDS * sizeof(unsigned long long)) == hipSuccess;
-  ok = ok && dalloc(&c->d_stem, (size_t)cfg.max_stem_bytes + 64) == hipSuccess;
-  ok = ok && dalloc(&c->d_off, (size_t)n + 1) == hipSuccess;
-  ok = ok && dalloc(&c->d_now, cfg.max_requests) == hipSuccess;
-  ok = ok && dalloc(&c->d_req, n) == hipSuccess && dalloc(&c->d_unit, n) == hipSuccess &&
-       dalloc(&c->d_flags, n) == hipSuccess && dalloc(&c->d_limit, n) == hipSuccess &&
-       dalloc(&c->d_hits, n) == hipSuccess && dalloc(&c->d_rule, n) == hipSuccess;
-  ok = ok && dalloc(&c->d_code, n) == hipSuccess && dalloc(&c->d_status, n) == hipSuccess &&
-       dalloc(&c->d_rem, n) == hipSuccess &&
-       dalloc(&c->d_reset, n) == hipSuccess;
-  ok = ok && dalloc(&c->d_stats, (size_t)cfg.max_rules * RL_NUM_STATS) == hipSuccess;
-  ok = ok && hipHostMalloc((void**)&c->h_err, (NBUF + 2) * sizeof(uint32_t)) == hipSuccess;
-  ok = ok && hipHostMalloc((void**)&c->h_counters, 8 * sizeof(unsigned long long)) == hipSuccess;
-  if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
-  ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
-       hipMemsetAsync(c->errw, 0, (NBUF + 2) * 4, c->stream) == hipSuccess &&
-       hipMemsetAsync(s0.time_floor, 0, 8, c->stream) == hipSuccess &&
-       hipMemsetAsync(s0.counters, 0, 64, c->stream) == hipSuccess &&
-       hipMemsetAsync(s0.stripes, 0, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS * 8, c->stream) ==
-           hipSuccess &&
-       hipMemsetAsync(c->d_stem, 0, (size_t)cfg.max_stem_bytes + 64, c->stream) == hipSuccess &&
-       hipStreamSynchronize(c->stream) == hipSuccess;
-  for (uint32_t k = 0; k < NBUF; k++) ok = ok && hipEventRecord(c->b_done[k], c->stream) == hipSuccess;
-  if (!ok) return fail("gpu: device initialisation failed", c);
-  return c;
-}
-
-void rl_destroy(rl_ctx* c) {
-  if (!c) return;
-  (void)hipSetDevice(c->cfg.device);
-  for (uint32_t k = 0; k < NBUF; k++)
-    if (c->pipe[k]) (void)hipStreamSynchronize(c->pipe[k]);
-  if (c->side) (void)hipStreamSynchronize(c->side);
-  if (c->side_go) (void)hipEventDestroy(c->side_go);
-  if (c->side_done) (void)hipEventDestroy(c->side_done);
-  for (uint32_t k = 0; k < PROF_RING; k++)
-    for (int i = 0; i <= RL_NUM_STAGES; i++)
-      if (c->ev[k][i]) (void)hipEventDestroy(c->ev[k][i]);
-  for (uint32_t k = 0; k < NBUF; k++) {
-    free_buffer(c->s[k]);
-    if (c->b_done[k]) (void)hipEventDestroy(c->b_done[k]);
-  }
-  const Scratch& s0 = c->s[0];
-  void* bufs[] = {c->slots, c->arena, c->arena2, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
-                  c->d_now, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_status,
-                  c->d_rem,
-                  c->d_reset, c->d_stats, s0.route_start, s0.route_base, s0.route_counts};
-  for (void* p : bufs)
-    if (p) (void)hipFree(p);
-  if (c->h_err) (void)hipHostFree(c->h_err);
-  if (c->h_counters) (void)hipHostFree(c->h_counters);
-  if (c->h_route) (void)hipHostFree(c->h_route);
-  for (void* p : {(void*)c->cfg_blob, (void*)c->mbuf})
-    if (p) (void)hipFree(p);
-  if (c->h_match) (void)hipHostFree(c->h_match);
-  for (uint32_t k = 0; k < NBUF; k++)
-    if (c->pipe[k]) (void)hipStreamDestroy(c->pipe[k]);
-  if (c->side) (void)hipStreamDestroy(c->side);
-  delete c;
-}
-
-int rl_do_limit_async(rl_ctx* c, const rl_batch* in, rl_result* out, void* stream) {
-  if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
-  // device pointers: the total stem size is only known on the device; the
-  // kernels bound-check offsets against max_stem_bytes (stem_cap)
-  int rc = check_sizes(c, in, 0);
+  rl_result r{c->d_code, c->d_rem, c->d_reset, (uint64_t*)c->d_stats, out->status ? c->d_status : nullptr};
+  int rc = routed_async(c, &d, &r, nullptr);
   if (rc) return rc;
-  if ((uintptr_t)in->stem_bytes & 3u) return set_err(c, RL_E_INVALID, "gpu: stem_bytes must be 4-byte aligned");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  BatchDev b = dev_view(c, in, c->cfg.max_stem_bytes);
-  OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats, out->status};
-  // NULL stream: pipelined on the ctx streams; otherwise serial on the caller's stream
-  enqueue(c, b, o, 0, (hipStream_t)stream, stream == nullptr);
-  HIPCHK(c, hipGetLastError());
-  c->batches++;
-  c->decisions += in->n;
+  hipStream_t rs = c->ret;
+  if (n) {
+    API_HIP(c, hipMemcpyAsync(out->code, c->d_code, n, hipMemcpyDeviceToHost, rs));
+    API_HIP(c, hipMemcpyAsync(out->limit_remaining, c->d_rem, n * 4ull, hipMemcpyDeviceToHost, rs));
+    API_HIP(c, hipMemcpyAsync(out->reset_s, c->d_reset, n * 4ull, hipMemcpyDeviceToHost, rs));
+    if (out->status) API_HIP(c, hipMemcpyAsync(out->status, c->d_status, n, hipMemcpyDeviceToHost, rs));
+  }
+  if (in->n_rules && out->stats)
+    API_HIP(c, hipMemcpyAsync(out->stats, c->d_stats, (size_t)in->n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost,
+                              rs));
+  return synchronize_all(c);
+}
+
+int rl_comm_unique_id(uint8_t* id) {
+  if (!id) return fail(nullptr, RL_E_INVALID, "gpu: null argument");
+  std::string err;
+  const int rc = comm_unique_id(id, &err);
+  if (rc) return fail(nullptr, rc, err);
   return RL_OK;
 }
 
-int rl_route_pack(rl_ctx* c, const rl_batch* in, uint32_t n_shards, uint32_t src_rank, void* send_rec,
-                  uint8_t* send_stem, uint32_t* perm, uint64_t* counts_host, void* stream) {
-  if (!c || !in || !counts_host || (in->n && (!send_rec || !send_stem || !perm)))
-    return set_err(c, RL_E_INVALID, "gpu: null argument");
-  if (n_shards < 1 || n_shards > RL_MAX_SHARDS || src_rank >= n_shards)
-    return set_err(c, RL_E_INVALID, "gpu: n_shards must be 1..256 and src_rank < n_shards");
-  int rc = check_sizes(c, in, 0);
-  if (rc) return rc;
-  if ((uintptr_t)in->stem_bytes & 3u) return set_err(c, RL_E_INVALID, "gpu: stem_bytes must be 4-byte aligned");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-  HIPCHK(c, after_batches(c, st));  // the partition reuses buffer 0's scratch
-  BatchDev b = dev_view(c, in, c->cfg.max_stem_bytes);
-  launch_route_pack(b, n_shards, src_rank, (Wire*)send_rec, send_stem, perm, c->s[0].route_counts, c->s[0], st);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(c->h_route, c->s[0].route_counts, 2ull * n_shards * 8, hipMemcpyDeviceToHost, st));
-  rc = collect(c, st);
-  for (uint32_t i = 0; i < 2 * n_shards; i++) counts_host[i] = rc ? 0 : c->h_route[i];
-  return rc;
-}
-
-int rl_route_do_limit(rl_ctx* c, uint32_t n, const void* recv_rec, const uint8_t* recv_stem, uint64_t recv_stem_bytes,
-                      const uint64_t* src_stem_base, uint32_t n_shards, uint32_t n_rules, uint64_t* ret,
-                      uint64_t* stats, void* stream) {
-  if (!c || !src_stem_base || (n && (!recv_rec || !recv_stem || !ret)) || (n_rules && !stats))
-    return set_err(c, RL_E_INVALID, "gpu: null argument");
-  if (n_shards < 1 || n_shards > RL_MAX_SHARDS) return set_err(c, RL_E_INVALID, "gpu: n_shards must be 1..256");
-  if (n > c->cfg.max_batch || n > c->cfg.max_requests || n_rules > c->cfg.max_rules ||
-      recv_stem_bytes > c->cfg.max_stem_bytes)
-    return set_err(c, RL_E_CAPACITY, "gpu: routed batch exceeds max_batch/max_requests/max_rules/max_stem_bytes");
-  if ((uintptr_t)recv_stem & 3u) return set_err(c, RL_E_INVALID, "gpu: recv_stem must be 4-byte aligned");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-  HIPCHK(c, after_batches(c, st));  // the staging arrays below may still feed an earlier batch
-  HIPCHK(c, hipMemcpyAsync(c->s[0].route_base, src_stem_base, (size_t)n_shards * 8, hipMemcpyHostToDevice, st));
-  BatchOut bo{c->d_off, c->d_now, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule};
-  // a malformed exchange poisons the table stage of this batch (sticky word)
-  launch_route_unpack((const Wire*)recv_rec, n, c->s[0].route_base, n_shards, recv_stem_bytes, bo, c->s[0].errb,
-                      st);
-  if (!n) HIPCHK(c, hipMemsetAsync(c->d_off, 0, sizeof(uint32_t), st));
-  BatchDev b;
-  b.hk = c->hk;
-  b.n = n;
-  b.n_req = n;
-  b.n_rules = n_rules;
-  b.stem_cap = (uint32_t)recv_stem_bytes;
-  b.stem_total = (uint32_t)recv_stem_bytes;
-  b.now_desc = 1;
-  b.stem = recv_stem;
-  b.off = c->d_off;
-  b.now = c->d_now;
-  b.req = c->d_req;
-  b.unit = c->d_unit;
-  b.flags = c->d_flags;
-  b.limit = c->d_limit;
-  b.hits = c->d_hits;
-  b.rule = c->d_rule;
-  OutDev o{c->d_code, c->d_rem, c->d_reset, (unsigned long long*)stats, nullptr};
-  const uint32_t k = enqueue(c, b, o, 0, st, false);
-  if (n) HIPCHK(c, hipMemcpyAsync(ret, c->s[k].res, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
-  HIPCHK(c, hipGetLastError());
-  c->batches++;
-  c->decisions += n;
+int rl_comm_init(rl_ctx* c, uint32_t world, uint32_t rank, const uint8_t* id) {
+  if (!c || !id) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (c->n > 1) return fail(c, RL_E_INVALID, "gpu: rl_comm_init needs a single-shard ctx (one per process and GPU)");
+  if (c->comm) return eng_fail(c->e[0], RL_E_INVALID, "gpu: ctx already joined a communicator");
+  if (!c->cfg.hash_seed)
+    return eng_fail(c->e[0], RL_E_INVALID, "gpu: a routed table needs an explicit hash_seed shared by every rank");
+  std::string err;
+  c->comm = comm_create(c->e[0], world, rank, id, &err);
+  if (!c->comm) return eng_fail(c->e[0], RL_E_COMM, err);
   return RL_OK;
 }
 
-int rl_route_scatter(rl_ctx* c, uint32_t n, const uint32_t* perm, const uint64_t* ret, rl_result* out, void* stream) {
-  if (!c || !out || (n && (!perm || !ret))) return set_err(c, RL_E_INVALID, "gpu: null argument");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-  OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats, out->status};
-  launch_route_scatter(perm, (const unsigned long long*)ret, n, o, st);
-  HIPCHK(c, hipGetLastError());
-  return RL_OK;
-}
-
-int rl_profile(rl_ctx* c, int enable) {
-  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  if (enable && !c->ev[0][0])
-    for (uint32_t k = 0; k < PROF_RING; k++)
-      for (int i = 0; i <= RL_NUM_STAGES; i++) HIPCHK(c, hipEventCreate(&c->ev[k][i]));
-  prof_fold_all(c);
-  c->prof = enable > 0;
-  c->prof_every = enable > 0 ? (uint32_t)enable : 1u;
-  c->prof_skip = 0;
-  return RL_OK;
-}
-
-int rl_profile_read(rl_ctx* c, double* ms, uint32_t n, uint64_t* batches) {
-  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  prof_fold_all(c);
-  for (uint32_t i = 0; i < n && i < RL_NUM_STAGES; i++) ms[i] = c->stage_ms[i];
-  if (batches) *batches = c->prof_batches;
-  for (int i = 0; i < RL_NUM_STAGES; i++) c->stage_ms[i] = 0;
-  c->prof_batches = 0;
-  return RL_OK;
+int rl_do_limit_routed_async(rl_ctx* c, const rl_batch* in, rl_result* out, void* stream) {
+  if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (!c->comm) return fail(c, RL_E_INVALID, "gpu: ctx has no communicator (rl_comm_init)");
+  return comm_do_limit(c->comm, c->e[0], in, out, (hipStream_t)stream);
 }
 
 int rl_synchronize(rl_ctx* c) {
-  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  HIPCHK(c, hipDeviceSynchronize());
-  return collect(c);
-}
-
-int rl_do_limit(rl_ctx* c, const rl_batch* in, rl_result* out) {
-  if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  BatchDev b;
-  int rc = stage(c, in, &b);
-  if (rc) return rc;
-  hipStream_t st = c->stream;
-  OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats, out->status ? c->d_status : nullptr};
-  enqueue(c, b, o, 0, st, false);
-  HIPCHK(c, hipGetLastError());
-  const uint32_t n = in->n;
-  if (n) {
-    if (out->status) HIPCHK(c, hipMemcpyAsync(out->status, c->d_status, n, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(out->code, c->d_code, n, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(out->limit_remaining, c->d_rem, n * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(out->reset_s, c->d_reset, n * 4, hipMemcpyDeviceToHost, st));
-  }
-  if (in->n_rules)
-    HIPCHK(c, hipMemcpyAsync(out->stats, c->d_stats, (size_t)in->n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost, st));
-  c->batches++;
-  c->decisions += n;
-  return collect(c);
-}
-
-int rl_restore(rl_ctx* c, const rl_restore_batch* r) {
-  if (!c || !r) return set_err(c, RL_E_INVALID, "gpu: null argument");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  if (!r->n) return RL_OK;
-  // A restore batch is a batch of SET records: req = record index, hits = count,
-  // flags = local-cache bit. It runs through the same grouping pipeline.
-  std::string* e = &c->last_error;
-  (void)e;
-  const uint32_t n = r->n;
-  uint32_t* req = new uint32_t[n];
-  uint32_t* zero = new uint32_t[n]();
-  uint8_t* lcf = new uint8_t[n]();
-  for (uint32_t i = 0; i < n; i++) {
-    req[i] = i;
-    if (r->lc) lcf[i] = r->lc[i] ? 1 : 0;
-  }
-  rl_batch in{};
-  in.n = n;
-  in.n_requests = n;
-  in.n_rules = 1;
-  in.stem_bytes = r->stem_bytes;
-  in.stem_off = r->stem_off;
-  in.now = r->now;
-  in.req_idx = req;
-  in.unit = r->unit;
-  in.flags = lcf;
-  in.limit = zero;
-  in.hits = r->count;
-  in.rule_id = zero;
-  BatchDev b;
-  int rc = stage(c, &in, &b);
-  if (!rc) {
-    OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats, nullptr};
-    enqueue(c, b, o, 1, c->stream, false);
-    hipError_t he = hipGetLastError();
-    rc = he != hipSuccess ? set_err(c, RL_E_HIP, std::string("gpu: ") + hipGetErrorString(he)) : collect(c);
-  }
-  delete[] req;
-  delete[] zero;
-  delete[] lcf;
-  return rc;
+  if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
+  return synchronize_all(c);
 }
 
 int rl_sweep(rl_ctx* c, int64_t now, uint64_t* n_evicted) {
-  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
-  if (now < 0 || now > (int64_t)NOW_MAX) return set_err(c, RL_E_TIME, "gpu: sweep time out of range");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  // the sweep time becomes a floor: later requests may not be earlier
-  int64_t last = 0;
-  HIPCHK(c, after_batches(c, c->stream));
-  HIPCHK(c, hipMemcpyAsync(&last, c->s[0].time_floor, 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (now > last) HIPCHK(c, hipMemcpyAsync(c->s[0].time_floor, &now, 8, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemsetAsync(c->s[0].counters, 0, 8, c->stream));
-  launch_sweep(c->slots, c->nslots, (uint32_t)now, c->s[0].counters, c->stream);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 40, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (n_evicted) *n_evicted = c->h_counters[0];
-  if (c->h_counters[0] && c->h_counters[4]) {
-    // reclaim the long-stem arena: live slots' overflow bytes move to the spare
-    // arena, packed from 0, and the two swap (counters[4] = the arena cursor)
-    HIPCHK(c, hipMemsetAsync(c->s[0].counters + 4, 0, 8, c->stream));
-    launch_arena_compact(c->slots, c->nslots, c->arena, c->arena2, c->s[0].counters + 4, c->stream);
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    std::swap(c->arena, c->arena2);
+  if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
+  if (c->n > 1) {
+    int rc = synchronize_all(c);
+    if (rc) return rc;
+  }
+  uint64_t total = 0;
+  for (uint32_t j = 0; j < c->n; j++) {
+    uint64_t ev = 0;
+    const int rc = from_engine(c, c->e[j], eng_sweep(c->e[j], now, &ev));
+    if (rc) return rc;
+    total += ev;
+  }
+  if (n_evicted) *n_evicted = total;
+  return RL_OK;
+}
+
+int rl_restore(rl_ctx* c, const rl_restore_batch* r) {
+  if (!c || !r) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (c->n == 1) return eng_restore(c->e[0], r);
+  // route the SET records by owner on the host (restores are rare)
+  const uint32_t N = c->n;
+  std::vector<std::vector<uint32_t>> idx(N);
+  for (uint32_t i = 0; i < r->n; i++) {
+    const uint32_t a = r->stem_off[i], b = r->stem_off[i + 1];
+    if (b < a) return fail(c, RL_E_INVALID, "gpu: restore stem offsets");
+    idx[owner_of_host(hash_stem_host(c->e[0]->hk, r->stem_bytes + a, b - a), N)].push_back(i);
+  }
+  for (uint32_t j = 0; j < N; j++) {
+    if (idx[j].empty()) continue;
+    std::vector<uint8_t> stems, unit, lc;
+    std::vector<uint32_t> off{0}, count;
+    std::vector<int64_t> now;
+    for (uint32_t i : idx[j]) {
+      stems.insert(stems.end(), r->stem_bytes + r->stem_off[i], r->stem_bytes + r->stem_off[i + 1]);
+      off.push_back((uint32_t)stems.size());
+      unit.push_back(r->unit[i]);
+      now.push_back(r->now[i]);
+      count.push_back(r->count[i]);
+      lc.push_back(r->lc ? r->lc[i] : 0);
+    }
+    rl_restore_batch sub{};
+    sub.n = (uint32_t)idx[j].size();
+    sub.stem_bytes = stems.data();
+    sub.stem_off = off.data();
+    sub.unit = unit.data();
+    sub.now = now.data();
+    sub.count = count.data();
+    sub.lc = lc.data();
+    const int rc = from_engine(c, c->e[j], eng_restore(c->e[j], &sub));
+    if (rc) return rc;
   }
   return RL_OK;
 }
 
 int rl_table_info_get(rl_ctx* c, rl_table_info* info) {
-  if (!c || !info) return set_err(c, RL_E_INVALID, "gpu: null argument");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  HIPCHK(c, after_batches(c, c->stream));
-  HIPCHK(c, hipMemsetAsync(c->s[0].counters, 0, 24, c->stream));
-  launch_table_info(c->slots, c->nslots, c->s[0].counters, c->stream);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 40, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  info->table_slots = c->nslots;
-  info->live_slots = c->h_counters[0];
-  info->tombstones = c->h_counters[1];
-  info->exact_stems = c->h_counters[2];
-  info->arena_bytes_used = c->h_counters[4] * 16;
-  info->batches = c->batches;
-  info->decisions = c->decisions;
+  if (!c || !info) return fail(c, RL_E_INVALID, "gpu: null argument");
+  rl_table_info sum{};
+  for (uint32_t j = 0; j < c->n; j++) {
+    rl_table_info x{};
+    const int rc = from_engine(c, c->e[j], eng_table_info_get(c->e[j], &x));
+    if (rc) return rc;
+    sum.table_slots += x.table_slots;
+    sum.live_slots += x.live_slots;
+    sum.tombstones += x.tombstones;
+    sum.arena_bytes_used += x.arena_bytes_used;
+    sum.exact_stems += x.exact_stems;
+    sum.decisions += x.decisions;
+    sum.batches = std::max(sum.batches, x.batches);
+  }
+  *info = sum;
   return RL_OK;
+}
+
+int rl_local_cache_info_get(rl_ctx* c, int64_t now, rl_local_cache_info* info) {
+  if (!c || !info) return fail(c, RL_E_INVALID, "gpu: null argument");
+  rl_local_cache_info sum{};
+  for (uint32_t j = 0; j < c->n; j++) {
+    rl_local_cache_info x{};
+    const int rc = from_engine(c, c->e[j], eng_local_cache_info_get(c->e[j], now, &x));
+    if (rc) return rc;
+    sum.entry_count += x.entry_count;
+    sum.lookup_count += x.lookup_count;
+    sum.hit_count += x.hit_count;
+    sum.miss_count += x.miss_count;
+  }
+  *info = sum;
+  return RL_OK;
+}
+
+int rl_snapshot_size(rl_ctx* c, uint64_t* bytes) {
+  if (!c || !bytes) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (c->n == 1) return eng_snapshot_size(c->e[0], bytes);
+  uint64_t total = 8 * (2 + c->n);  // magic, n, per-shard sizes
+  for (uint32_t j = 0; j < c->n; j++) {
+    uint64_t b = 0;
+    const int rc = from_engine(c, c->e[j], eng_snapshot_size(c->e[j], &b));
+    if (rc) return rc;
+    total += b;
+  }
+  *bytes = total;
+  return RL_OK;
+}
+
+int rl_snapshot_save(rl_ctx* c, void* host, uint64_t bytes) {
+  if (!c || !host) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (c->n == 1) return eng_snapshot_save(c->e[0], host, bytes);
+  uint64_t* h = (uint64_t*)host;
+  const uint64_t head = 8 * (2 + c->n);
+  if (bytes < head) return fail(c, RL_E_CAPACITY, "gpu: snapshot buffer smaller than rl_snapshot_size");
+  h[0] = MSNAP_MAGIC;
+  h[1] = c->n;
+  uint64_t pos = head;
+  for (uint32_t j = 0; j < c->n; j++) {
+    uint64_t b = 0;
+    int rc = from_engine(c, c->e[j], eng_snapshot_size(c->e[j], &b));
+    if (rc) return rc;
+    if (pos + b > bytes) return fail(c, RL_E_CAPACITY, "gpu: snapshot buffer smaller than rl_snapshot_size");
+    rc = from_engine(c, c->e[j], eng_snapshot_save(c->e[j], (uint8_t*)host + pos, b));
+    if (rc) return rc;
+    h[2 + j] = b;
+    pos += b;
+  }
+  return RL_OK;
+}
+
+int rl_snapshot_load(rl_ctx* c, const void* host, uint64_t bytes) {
+  if (!c || !host) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (c->n == 1) return eng_snapshot_load(c->e[0], host, bytes);
+  const uint64_t* h = (const uint64_t*)host;
+  if (bytes < 16 || h[0] != MSNAP_MAGIC || h[1] != c->n || bytes < 8 * (2 + c->n))
+    return fail(c, RL_E_INVALID, "gpu: not a snapshot of a ctx with this many shards");
+  uint64_t pos = 8 * (2 + c->n);
+  for (uint32_t j = 0; j < c->n; j++) {
+    if (pos + h[2 + j] > bytes) return fail(c, RL_E_INVALID, "gpu: snapshot truncated");
+    const int rc = from_engine(c, c->e[j], eng_snapshot_load(c->e[j], (const uint8_t*)host + pos, h[2 + j]));
+    if (rc) return rc;
+    pos += h[2 + j];
+  }
+  return RL_OK;
+}
+
+int rl_config_load(rl_ctx* c, const rl_config_tree* t) {
+  if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
+  for (uint32_t j = 0; j < c->n; j++) {
+    const int rc = from_engine(c, c->e[j], eng_config_load(c->e[j], t));
+    if (rc) return rc;
+  }
+  return RL_OK;
+}
+
+int rl_do_limit_requests(rl_ctx* c, const rl_request_batch* in, rl_request_result* out) {
+  if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
+  if (c->n > 1) return fail(c, RL_E_INVALID, "gpu: rl_do_limit_requests runs on a single-shard ctx");
+  return eng_do_limit_requests(c->e[0], in, out);
+}
+
+// Diagnostics, profiling and the per-rank routing halves act on shard 0.
+int rl_table_info_shard(rl_ctx* c, uint32_t shard, rl_table_info* info) {
+  if (!c || !info || shard >= c->n) return fail(c, RL_E_INVALID, "gpu: bad shard");
+  return from_engine(c, c->e[shard], eng_table_info_get(c->e[shard], info));
+}
+
+int rl_debug_keys(rl_ctx* c, const rl_batch* in, uint8_t* out_bytes, uint32_t* out_off, uint32_t out_cap) {
+  if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
+  return from_engine(c, c->e[0], eng_debug_keys(c->e[0], in, out_bytes, out_off, out_cap));
+}
+
+int rl_debug_decide(rl_ctx* c, uint32_t n, const uint32_t* before, const uint32_t* after, const uint8_t* lc_hit,
+                    const uint32_t* hits, const uint32_t* limit, const uint8_t* unit, const uint8_t* flags,
+                    const int64_t* now, uint8_t* code, uint32_t* remaining, uint32_t* reset_s,
+                    uint64_t* stat_deltas, uint8_t* lc_set) {
+  if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
+  return from_engine(c, c->e[0], eng_debug_decide(c->e[0], n, before, after, lc_hit, hits, limit, unit, flags, now,
+                                                   code, remaining, reset_s, stat_deltas, lc_set));
+}
+
+int rl_profile(rl_ctx* c, int enable) {
+  if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
+  for (uint32_t j = 0; j < c->n; j++) {
+    const int rc = from_engine(c, c->e[j], eng_profile(c->e[j], enable));
+    if (rc) return rc;
+  }
+  return RL_OK;
+}
+
+int rl_profile_read(rl_ctx* c, double* ms, uint32_t n, uint64_t* batches) {
+  if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
+  return from_engine(c, c->e[0], eng_profile_read(c->e[0], ms, n, batches));
+}
+
+int rl_route_pack(rl_ctx* c, const rl_batch* in, uint32_t n_shards, uint32_t src_rank, void* send_rec,
+                  uint8_t* send_stem, uint32_t* perm, uint64_t* counts, void* stream) {
+  if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
+  if (c->n > 1) return fail(c, RL_E_INVALID, "gpu: per-rank routing needs a single-shard ctx");
+  return eng_route_pack(c->e[0], in, n_shards, src_rank, send_rec, send_stem, perm, counts, stream);
+}
+
+int rl_route_do_limit(rl_ctx* c, uint32_t n, const void* recv_rec, const uint8_t* recv_stem, uint64_t recv_stem_bytes,
+                      const uint64_t* src_stem_base, uint32_t n_shards, uint32_t n_rules, uint32_t rule_stride,
+                      uint64_t* ret, uint64_t* stats, int isolate, void* stream) {
+  if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
+  if (c->n > 1) return fail(c, RL_E_INVALID, "gpu: per-rank routing needs a single-shard ctx");
+  return eng_route_do_limit(c->e[0], n, recv_rec, recv_stem, recv_stem_bytes, src_stem_base, n_shards, n_rules,
+                            rule_stride, ret, stats, isolate, stream);
+}
+
+int rl_route_scatter(rl_ctx* c, uint32_t n, const uint32_t* perm, const uint64_t* ret, rl_result* out, void* stream) {
+  if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
+  if (c->n > 1) return fail(c, RL_E_INVALID, "gpu: per-rank routing needs a single-shard ctx");
+  return eng_route_scatter(c->e[0], n, perm, ret, out, stream);
 }
 
 void* rl_alloc_host(size_t bytes) {
@@ -706,407 +668,4 @@ void rl_free_host(void* p) {
   if (p) (void)hipHostFree(p);
 }
 
-int rl_debug_keys(rl_ctx* c, const rl_batch* in, uint8_t* out_bytes, uint32_t* out_off, uint32_t out_cap) {
-  if (!c || !in || !out_off) return set_err(c, RL_E_INVALID, "gpu: null argument");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  BatchDev b;
-  int rc = stage(c, in, &b);
-  if (rc) return rc;
-  const uint32_t n = in->n;
-  const size_t cap = (size_t)(n ? in->stem_off[n] : 0) + 24ull * n + 1;
-  uint8_t* d_out = nullptr;
-  uint32_t* d_len = nullptr;
-  HIPCHK(c, dalloc(&d_out, cap));
-  HIPCHK(c, dalloc(&d_len, (size_t)n + 1));
-  launch_debug_keys(b, d_out, d_len, c->stream);
-  uint8_t* h_out = new uint8_t[cap];
-  uint32_t* h_len = new uint32_t[n + 1];
-  hipError_t e1 = hipMemcpyAsync(h_out, d_out, cap, hipMemcpyDeviceToHost, c->stream);
-  hipError_t e2 = hipMemcpyAsync(h_len, d_len, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream);
-  hipError_t e3 = hipStreamSynchronize(c->stream);
-  (void)hipFree(d_out);
-  (void)hipFree(d_len);
-  rc = (e1 || e2 || e3) ? set_err(c, RL_E_HIP, "gpu: debug_keys copy failed") : RL_OK;
-  uint32_t pos = 0;
-  out_off[0] = 0;
-  for (uint32_t i = 0; i < n && rc == RL_OK; i++) {
-    if (pos + h_len[i] > out_cap) {
-      rc = set_err(c, RL_E_CAPACITY, "gpu: debug_keys output buffer too small");
-      break;
-    }
-    memcpy(out_bytes + pos, h_out + in->stem_off[i] + 24ull * i, h_len[i]);
-    pos += h_len[i];
-    out_off[i + 1] = pos;
-  }
-  delete[] h_out;
-  delete[] h_len;
-  return rc;
-}
-
-int rl_debug_decide(rl_ctx* c, uint32_t n, const uint32_t* before, const uint32_t* after, const uint8_t* lc_hit,
-                    const uint32_t* hits, const uint32_t* limit, const uint8_t* unit, const uint8_t* flags,
-                    const int64_t* now, uint8_t* code, uint32_t* remaining, uint32_t* reset_s,
-                    uint64_t* stat_deltas, uint8_t* lc_set) {
-  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
-  if (!n) return RL_OK;
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  for (uint32_t i = 0; i < n; i++)
-    if (unit[i] < 1 || unit[i] > 4) return set_err(c, RL_E_INVALID, "gpu: unit out of range");
-  uint32_t *d_b, *d_a, *d_h, *d_l, *d_rem, *d_rs;
-  uint8_t *d_lc, *d_u, *d_f, *d_code, *d_set;
-  int64_t* d_now;
-  unsigned long long* d_del;
-  HIPCHK(c, dalloc(&d_b, n));
-  HIPCHK(c, dalloc(&d_a, n));
-  HIPCHK(c, dalloc(&d_h, n));
-  HIPCHK(c, dalloc(&d_l, n));
-  HIPCHK(c, dalloc(&d_rem, n));
-  HIPCHK(c, dalloc(&d_rs, n));
-  HIPCHK(c, dalloc(&d_lc, n));
-  HIPCHK(c, dalloc(&d_u, n));
-  HIPCHK(c, dalloc(&d_f, n));
-  HIPCHK(c, dalloc(&d_code, n));
-  HIPCHK(c, dalloc(&d_set, n));
-  HIPCHK(c, dalloc(&d_now, n));
-  HIPCHK(c, dalloc(&d_del, (size_t)n * RL_NUM_STATS));
-  hipStream_t st = c->stream;
-  HIPCHK(c, hipMemcpyAsync(d_b, before, n * 4, hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(d_a, after, n * 4, hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(d_h, hits, n * 4, hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(d_l, limit, n * 4, hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(d_lc, lc_hit, n, hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(d_u, unit, n, hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(d_f, flags, n, hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(d_now, now, n * 8, hipMemcpyHostToDevice, st));
-  launch_debug_decide(n, d_b, d_a, d_lc, d_h, d_l, d_u, d_f, d_now, c->cfg.near_limit_ratio,
-                      c->cfg.local_cache_enabled, d_code, d_rem, d_rs, d_del, d_set, st);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(code, d_code, n, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(remaining, d_rem, n * 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(reset_s, d_rs, n * 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(stat_deltas, d_del, (size_t)n * RL_NUM_STATS * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipMemcpyAsync(lc_set, d_set, n, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipStreamSynchronize(st));
-  void* bufs[] = {d_b, d_a, d_h, d_l, d_rem, d_rs, d_lc, d_u, d_f, d_code, d_set, d_now, d_del};
-  for (void* p : bufs) (void)hipFree(p);
-  return RL_OK;
-}
-
-// ---- config match: GetLimit on the device (rl_match.hip) -------------------
-
-int rl_config_load(rl_ctx* c, const rl_config_tree* t) {
-  if (!c || !t || (t->n_nodes && (!t->nodes || (t->key_bytes_len && !t->key_bytes))) ||
-      (t->cache_key_prefix_len && !t->cache_key_prefix))
-    return set_err(c, RL_E_INVALID, "gpu: null config tree");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  const uint32_t n = t->n_nodes;
-  std::vector<CfgNode> nodes(n);
-  for (uint32_t i = 0; i < n; i++) {
-    const rl_config_node& x = t->nodes[i];
-    if (x.parent < -1 || x.parent >= (int32_t)i || (uint64_t)x.key_off + x.key_len > t->key_bytes_len)
-      return set_err(c, RL_E_INVALID, "gpu: config node " + std::to_string(i) + ": bad parent or key range");
-    if (x.has_limit && !x.unlimited && (x.unit < RL_UNIT_SECOND || x.unit > RL_UNIT_DAY))
-      return set_err(c, RL_E_INVALID, "gpu: config node " + std::to_string(i) + ": invalid rate limit unit");
-    if (x.has_limit && x.rule_id >= c->cfg.max_rules)
-      return set_err(c, RL_E_INVALID, "gpu: config node " + std::to_string(i) + ": rule id >= max_rules");
-    CfgNode& d = nodes[i];
-    d = CfgNode{};
-    d.parent = x.parent;
-    d.key_off = x.key_off;
-    d.key_len = x.key_len;
-    d.rpu = x.requests_per_unit;
-    d.rule = x.rule_id;
-    d.unit = x.unit;
-    d.has_limit = x.has_limit ? 1 : 0;
-    d.unlimited = x.unlimited ? 1 : 0;
-    d.shadow = x.shadow_mode ? 1 : 0;
-    if (x.parent >= 0) nodes[x.parent].n_children++;
-  }
-  uint32_t size = 16;
-  while (size < 2 * n) size <<= 1;
-  std::vector<unsigned long long> index(size, 0);
-  const uint8_t* kb = t->key_bytes;
-  for (uint32_t i = 0; i < n; i++) {
-    const rl_config_node& x = t->nodes[i];
-    const uint64_t h = cfg_hash(x.parent, kb + x.key_off, x.key_len);
-    uint32_t pos = (uint32_t)h & (size - 1);
-    for (;; pos = (pos + 1) & (size - 1)) {
-      const unsigned long long e = index[pos];
-      if (!e) break;
-      const rl_config_node& y = t->nodes[(uint32_t)(e >> 32) - 1];
-      if (y.parent == x.parent && y.key_len == x.key_len && !memcmp(kb + y.key_off, kb + x.key_off, x.key_len))
-        return set_err(c, RL_E_INVALID, "gpu: duplicate config key under one parent (node " + std::to_string(i) + ")");
-    }
-    index[pos] = (unsigned long long)(uint32_t)(h >> 32) | (unsigned long long)(i + 1) << 32;
-  }
-  // one blob [nodes | index | prefix ‖ keys], so a small config is staged into LDS in one copy
-  const uint64_t nkeys = t->cache_key_prefix_len + t->key_bytes_len;
-  const uint64_t idx_off = (uint64_t)n * sizeof(CfgNode), key_off = idx_off + size * 8ull;
-  const uint64_t blob = (key_off + nkeys + 3) & ~3ull;
-  std::vector<uint8_t> host(blob, 0);
-  if (n) memcpy(host.data(), nodes.data(), n * sizeof(CfgNode));
-  memcpy(host.data() + idx_off, index.data(), size * 8ull);
-  if (t->cache_key_prefix_len) memcpy(host.data() + key_off, t->cache_key_prefix, t->cache_key_prefix_len);
-  if (t->key_bytes_len) memcpy(host.data() + key_off + t->cache_key_prefix_len, kb, t->key_bytes_len);
-  HIPCHK(c, after_batches(c, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (c->cfg_blob) (void)hipFree(c->cfg_blob);
-  c->cfg_blob = nullptr;
-  c->cfg_loaded = false;
-  HIPCHK(c, dalloc(&c->cfg_blob, blob));
-  if (!c->h_match) HIPCHK(c, hipHostMalloc((void**)&c->h_match, 16, hipHostMallocDefault));
-  HIPCHK(c, hipMemcpy(c->cfg_blob, host.data(), blob, hipMemcpyHostToDevice));
-  uint8_t* B = c->cfg_blob;
-  CfgDev d{};
-  d.nodes = (const CfgNode*)B;
-  d.index = (const unsigned long long*)(B + idx_off);
-  d.keys = B + key_off + t->cache_key_prefix_len;
-  d.mask = size - 1;
-  d.n_nodes = n;
-  d.prefix = B + key_off;
-  d.prefix_len = t->cache_key_prefix_len;
-  d.blob = B;
-  d.blob_words = blob / 4 <= CFG_LDS_WORDS ? (uint32_t)(blob / 4) : 0u;
-  d.idx_word = (uint32_t)(idx_off / 4);
-  d.key_word = (uint32_t)(key_off / 4);
-  c->cfg_dev = d;
-  c->cfg_loaded = true;
-  return RL_OK;
-}
-
-int rl_do_limit_requests(rl_ctx* c, const rl_request_batch* in, rl_request_result* out) {
-  if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
-  // checkServiceErr(snappedConfig != nil, ...) (ratelimit.go:106)
-  if (!c->cfg_loaded) return set_err(c, RL_E_INVALID, "gpu: no rate limit configuration loaded");
-  const uint32_t n = in->n_descriptors, nq = in->n_requests, ne = in->n_entries;
-  if (n > c->cfg.max_batch || nq > c->cfg.max_requests || in->n_rules > c->cfg.max_rules)
-    return set_err(c, RL_E_CAPACITY, "gpu: request batch exceeds configured max_batch/max_requests/max_rules");
-  if (n && !nq) return set_err(c, RL_E_INVALID, "gpu: descriptors without requests");
-  if (!in->domain_off || !in->entry_first || !in->desc_off || (nq && (!in->now || !in->hits)) ||
-      (n && !in->req_idx) || (ne && (!in->key_len || !in->value_len)))
-    return set_err(c, RL_E_INVALID, "gpu: null request batch array");
-  const bool ovr = in->override_flags != nullptr;
-  if (ovr && (!in->override_rpu || !in->override_unit || !in->override_rule))
-    return set_err(c, RL_E_INVALID, "gpu: override_flags without override_rpu/unit/rule");
-  if (in->entry_first[0] != 0 || in->entry_first[n] != ne || in->desc_off[0] != 0 || in->domain_off[0] != 0)
-    return set_err(c, RL_E_INVALID, "gpu: request batch offsets must start at 0 and end at n_entries");
-  const uint64_t dom_bytes = in->domain_off[nq], desc_bytes = in->desc_off[n];
-  if ((dom_bytes && !in->domain_bytes) || (desc_bytes && !in->desc_bytes))
-    return set_err(c, RL_E_INVALID, "gpu: null request byte array");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  // one device buffer, carved (256-B aligned pieces)
-  const size_t scan = n ? match_scan_bytes(n) : 0;
-  size_t need = 0;
-  auto piece = [&need](size_t bytes) {
-    const size_t o = need;
-    need += (std::max<size_t>(bytes, 1) + 255) & ~(size_t)255;
-    return o;
-  };
-  const size_t o_dom = piece(dom_bytes), o_domoff = piece((nq + 1) * 4ull), o_hits = piece(nq * 4ull),
-               o_req = piece(n * 4ull), o_ent = piece((n + 1) * 4ull), o_doff = piece((n + 1) * 4ull),
-               o_desc = piece(desc_bytes), o_kl = piece(ne * 2ull), o_vl = piece(ne * 2ull),
-               o_ovf = piece(ovr ? n : 0), o_ovr = piece(ovr ? n * 4ull : 0), o_ovu = piece(ovr ? n : 0),
-               o_ovrule = piece(ovr ? n * 4ull : 0), o_v = piece(n * 16ull), o_kind = piece(n * 4ull),
-               o_rpu = piece(n * 4ull), o_rule = piece(n * 4ull), o_cnt = piece(16), o_code = piece(n),
-               o_rem = piece(n * 4ull), o_reset = piece(n * 4ull), o_match = piece(n), o_orule = piece(n * 4ull),
-               o_orpu = piece(n * 4ull), o_ounit = piece(n), o_tmp = piece(scan);
-  hipStream_t st = c->stream;
-  HIPCHK(c, after_batches(c, st));
-  if (need > c->mbuf_cap) {
-    HIPCHK(c, hipStreamSynchronize(st));
-    if (c->mbuf) (void)hipFree(c->mbuf);
-    c->mbuf = nullptr;
-    c->mbuf_cap = 0;
-    HIPCHK(c, hipMalloc((void**)&c->mbuf, need));
-    c->mbuf_cap = need;
-  }
-  uint8_t* B = c->mbuf;
-  auto h2d = [&](size_t off, const void* src, size_t bytes) {
-    return bytes ? hipMemcpyAsync(B + off, src, bytes, hipMemcpyHostToDevice, st) : hipSuccess;
-  };
-  HIPCHK(c, h2d(o_dom, in->domain_bytes, dom_bytes));
-  HIPCHK(c, h2d(o_domoff, in->domain_off, (nq + 1) * 4ull));
-  HIPCHK(c, h2d(o_hits, in->hits, nq * 4ull));
-  HIPCHK(c, h2d(o_req, in->req_idx, n * 4ull));
-  HIPCHK(c, h2d(o_ent, in->entry_first, (n + 1) * 4ull));
-  HIPCHK(c, h2d(o_doff, in->desc_off, (n + 1) * 4ull));
-  HIPCHK(c, h2d(o_desc, in->desc_bytes, desc_bytes));
-  HIPCHK(c, h2d(o_kl, in->key_len, ne * 2ull));
-  HIPCHK(c, h2d(o_vl, in->value_len, ne * 2ull));
-  if (ovr) {
-    HIPCHK(c, h2d(o_ovf, in->override_flags, n));
-    HIPCHK(c, h2d(o_ovr, in->override_rpu, n * 4ull));
-    HIPCHK(c, h2d(o_ovu, in->override_unit, n));
-    HIPCHK(c, h2d(o_ovrule, in->override_rule, n * 4ull));
-  }
-  if (nq) HIPCHK(c, hipMemcpyAsync(c->d_now, in->now, nq * 8ull, hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemsetAsync(B + o_cnt, 0, 16, st));
-  ReqDev r;
-  r.n_req = nq;
-  r.n_desc = n;
-  r.n_ent = ne;
-  r.dom_total = (uint32_t)dom_bytes;
-  r.desc_total = (uint32_t)desc_bytes;
-  r.dom = B + o_dom;
-  r.dom_off = (const uint32_t*)(B + o_domoff);
-  r.hits = (const uint32_t*)(B + o_hits);
-  r.req = (const uint32_t*)(B + o_req);
-  r.ent_first = (const uint32_t*)(B + o_ent);
-  r.desc_off = (const uint32_t*)(B + o_doff);
-  r.desc = B + o_desc;
-  r.klen = (const uint16_t*)(B + o_kl);
-  r.vlen = (const uint16_t*)(B + o_vl);
-  r.ovf = ovr ? B + o_ovf : nullptr;
-  r.ov_rpu = ovr ? (const uint32_t*)(B + o_ovr) : nullptr;
-  r.ov_unit = ovr ? B + o_ovu : nullptr;
-  r.ov_rule = ovr ? (const uint32_t*)(B + o_ovrule) : nullptr;
-  MatchBuf m{(unsigned long long*)(B + o_v), (uint32_t*)(B + o_kind), (uint32_t*)(B + o_rpu),
-             (uint32_t*)(B + o_rule), (uint32_t*)(B + o_cnt)};
-  // the matched descriptors become an ordinary DoLimit batch in the staging buffers
-  PackOut po{c->d_stem, c->d_off, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule,
-             c->cfg.max_stem_bytes};
-  launch_match(c->cfg_dev, r, m, po, B + o_tmp, scan, st);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(c->h_match, B + o_cnt, 16, hipMemcpyDeviceToHost, st));
-  HIPCHK(c, hipStreamSynchronize(st));
-  if (c->h_match[2] & MATCH_ERR_REQ)
-    return set_err(c, RL_E_INVALID, "gpu: malformed request batch (request index or entry byte layout)");
-  if (c->h_match[2] & MATCH_ERR_CAP)
-    return set_err(c, RL_E_CAPACITY, "gpu: matched stems exceed max_stem_bytes");
-  const uint32_t nm = n ? c->h_match[0] : 0;
-  if (!n) {  // off[0] of the empty batch
-    HIPCHK(c, hipMemsetAsync(c->d_off, 0, 4, st));
-  }
-  rl_batch pb{};
-  pb.n = nm;
-  pb.n_requests = nq;
-  pb.n_rules = in->n_rules;
-  pb.stem_bytes = c->d_stem;
-  pb.stem_off = c->d_off;
-  pb.now = c->d_now;
-  pb.req_idx = c->d_req;
-  pb.unit = c->d_unit;
-  pb.flags = c->d_flags;
-  pb.limit = c->d_limit;
-  pb.hits = c->d_hits;
-  pb.rule_id = c->d_rule;
-  BatchDev b = dev_view(c, &pb, c->cfg.max_stem_bytes);
-  OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats, nullptr};
-  enqueue(c, b, o, 0, st, false);
-  ReqOutDev ro{B + o_code, (uint32_t*)(B + o_rem), (uint32_t*)(B + o_reset), B + o_match,
-               (uint32_t*)(B + o_orule), (uint32_t*)(B + o_orpu), B + o_ounit};
-  launch_match_expand(r, m, c->d_code, c->d_rem, c->d_reset, ro, st);
-  HIPCHK(c, hipGetLastError());
-  auto d2h = [&](void* dst, size_t off, size_t bytes) {
-    return (bytes && dst) ? hipMemcpyAsync(dst, B + off, bytes, hipMemcpyDeviceToHost, st) : hipSuccess;
-  };
-  HIPCHK(c, d2h(out->code, o_code, n));
-  HIPCHK(c, d2h(out->limit_remaining, o_rem, n * 4ull));
-  HIPCHK(c, d2h(out->reset_s, o_reset, n * 4ull));
-  HIPCHK(c, d2h(out->match, o_match, n));
-  HIPCHK(c, d2h(out->rule_id, o_orule, n * 4ull));
-  HIPCHK(c, d2h(out->requests_per_unit, o_orpu, n * 4ull));
-  HIPCHK(c, d2h(out->unit, o_ounit, n));
-  if (in->n_rules && out->stats)
-    HIPCHK(c, hipMemcpyAsync(out->stats, c->d_stats, (size_t)in->n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost, st));
-  c->batches++;
-  c->decisions += nm;
-  return collect(c);
-}
-
-// ---- observability and restart ---------------------------------------------
-
-int rl_local_cache_info_get(rl_ctx* c, int64_t now, rl_local_cache_info* info) {
-  if (!c || !info) return set_err(c, RL_E_INVALID, "gpu: null argument");
-  if (now < 0 || now > (int64_t)NOW_MAX) return set_err(c, RL_E_TIME, "gpu: now out of range");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  HIPCHK(c, after_batches(c, c->stream));
-  unsigned long long* ctr = c->s[0].counters;
-  HIPCHK(c, hipMemsetAsync(ctr + 7, 0, 8, c->stream));
-  launch_lc_count(c->slots, c->nslots, (uint32_t)now, ctr + 7, c->stream);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(c->h_counters, ctr, 64, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  info->entry_count = c->h_counters[7];
-  info->lookup_count = c->h_counters[5];
-  info->hit_count = c->h_counters[6];
-  info->miss_count = c->h_counters[5] - c->h_counters[6];
-  return RL_OK;
-}
-
-namespace {
-constexpr uint64_t SNAP_MAGIC = 0x32304150414e534cull;  // "LSNAPA02" (keyed hash)
-struct SnapHeader {
-  uint64_t magic, nslots, arena_used16, hash_seed;  // slots are placed by the keyed hash: restore adopts its key
-  int64_t time_floor;
-  uint64_t reserved[3];
-};
-static_assert(sizeof(SnapHeader) == 64, "snapshot header");
-
-int snap_state(rl_ctx* c, uint64_t* arena_used16, int64_t* floor) {
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  HIPCHK(c, after_batches(c, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 64, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(floor, c->s[0].time_floor, 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  *arena_used16 = std::min<uint64_t>(c->h_counters[4], c->arena_cap16);
-  return RL_OK;
-}
-}  // namespace
-
-int rl_snapshot_size(rl_ctx* c, uint64_t* bytes) {
-  if (!c || !bytes) return set_err(c, RL_E_INVALID, "gpu: null argument");
-  uint64_t au = 0;
-  int64_t fl = 0;
-  int rc = snap_state(c, &au, &fl);
-  if (rc) return rc;
-  *bytes = sizeof(SnapHeader) + c->nslots * sizeof(Slot) + au * 16;
-  return RL_OK;
-}
-
-int rl_snapshot_save(rl_ctx* c, void* host, uint64_t bytes) {
-  if (!c || !host) return set_err(c, RL_E_INVALID, "gpu: null argument");
-  SnapHeader h{};
-  int rc = snap_state(c, &h.arena_used16, &h.time_floor);
-  if (rc) return rc;
-  h.magic = SNAP_MAGIC;
-  h.nslots = c->nslots;
-  h.hash_seed = c->hash_seed;
-  const uint64_t need = sizeof(SnapHeader) + c->nslots * sizeof(Slot) + h.arena_used16 * 16;
-  if (bytes < need) return set_err(c, RL_E_CAPACITY, "gpu: snapshot buffer smaller than rl_snapshot_size");
-  uint8_t* p = (uint8_t*)host;
-  memcpy(p, &h, sizeof h);
-  HIPCHK(c, hipMemcpy(p + sizeof h, c->slots, c->nslots * sizeof(Slot), hipMemcpyDeviceToHost));
-  if (h.arena_used16)
-    HIPCHK(c, hipMemcpy(p + sizeof h + c->nslots * sizeof(Slot), c->arena, h.arena_used16 * 16, hipMemcpyDeviceToHost));
-  return RL_OK;
-}
-
-int rl_snapshot_load(rl_ctx* c, const void* host, uint64_t bytes) {
-  if (!c || !host) return set_err(c, RL_E_INVALID, "gpu: null argument");
-  SnapHeader h;
-  if (bytes < sizeof h) return set_err(c, RL_E_INVALID, "gpu: snapshot too short");
-  memcpy(&h, host, sizeof h);
-  if (h.magic != SNAP_MAGIC) return set_err(c, RL_E_INVALID, "gpu: not a table snapshot");
-  if (h.nslots != c->nslots) return set_err(c, RL_E_INVALID, "gpu: snapshot table_slots differ from this ctx");
-  if (h.arena_used16 > c->arena_cap16) return set_err(c, RL_E_INVALID, "gpu: snapshot arena larger than this ctx's");
-  if (bytes < sizeof h + h.nslots * sizeof(Slot) + h.arena_used16 * 16)
-    return set_err(c, RL_E_INVALID, "gpu: snapshot truncated");
-  HIPCHK(c, hipSetDevice(c->cfg.device));
-  HIPCHK(c, after_batches(c, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  const uint8_t* p = (const uint8_t*)host;
-  HIPCHK(c, hipMemcpy(c->slots, p + sizeof h, c->nslots * sizeof(Slot), hipMemcpyHostToDevice));
-  if (h.arena_used16)
-    HIPCHK(c, hipMemcpy(c->arena, p + sizeof h + c->nslots * sizeof(Slot), h.arena_used16 * 16, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->s[0].counters + 4, &h.arena_used16, 8, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->s[0].time_floor, &h.time_floor, 8, hipMemcpyHostToDevice));
-  c->hash_seed = h.hash_seed;
-  c->cfg.hash_seed = h.hash_seed;
-  c->hk = hash_key_of(h.hash_seed, c->cfg.debug_hash_bits);
-  return RL_OK;
-}
-
 }  // extern "C"
-
-

@@ -1,0 +1,27 @@
+// rl_comm.h — multi-process routing over RCCL inside the library
+// (rl_comm_* / rl_do_limit_routed_async, include/ratelimit_hip.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "../../include/ratelimit_hip.h"
+#include "rl_engine.h"
+
+namespace rl {
+
+struct CommRouter;
+
+// ncclGetUniqueId through the RCCL library loaded in the process (dlopen).
+int comm_unique_id(uint8_t* id, std::string* err);
+// Collective over `world` processes: joins engine e (one GPU) to the
+// communicator `id` as `rank`. Null + *err on failure.
+CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t* id, std::string* err);
+void comm_destroy(CommRouter* r);
+// One routed batch: this rank's slice (device arrays) -> out in arrival order.
+int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, hipStream_t caller);
+// Wait for the router's streams (then the engine's own synchronize reports errors).
+int comm_synchronize(CommRouter* r, Engine* e);
+
+}  // namespace rl

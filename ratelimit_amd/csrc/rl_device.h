@@ -230,6 +230,20 @@ enum : uint32_t {
   ERR_HISTORY = 1u << 5,     // a key's window is older than its (cur, prev) history
 };
 
+// rl_status of a batch that failed with device error bits e (the host's
+// map_err order), and the error bit that reports a descriptor status.
+__host__ __device__ inline uint32_t err_status(uint32_t e) {
+  return (e & (ERR_TIME | ERR_HISTORY)) ? (uint32_t)RL_E_TIME
+         : (e & ERR_INVALID)            ? (uint32_t)RL_E_INVALID
+         : (e & ERR_TABLE_FULL)         ? (uint32_t)RL_E_TABLE_FULL
+         : (e & ERR_ARENA_FULL)         ? (uint32_t)RL_E_ARENA_FULL
+                                        : (uint32_t)RL_E_INTERNAL;
+}
+__host__ __device__ inline uint32_t status_err(uint32_t st) {
+  return st == RL_E_TIME ? ERR_TIME : st == RL_E_TABLE_FULL ? ERR_TABLE_FULL : st == RL_E_ARENA_FULL ? ERR_ARENA_FULL
+                                                                                                       : ERR_INVALID;
+}
+
 // Packed 8-B result of one descriptor (k_finish / the route exchange unpack it):
 //   bits  0..31 LimitRemaining, 32..51 DurationUntilReset (<= 86400),
 //   52..55 rl_status of the descriptor (0 = answered), 56..61 code,

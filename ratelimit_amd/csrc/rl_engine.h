@@ -1,0 +1,134 @@
+// rl_engine.h — one table shard on one GPU: the HBM table, the per-batch
+// scratch of the pipeline buffers, and the HIP streams and events that order
+// them (rl_engine.hip). The C ABI (rl_api.hip) drives one engine per shard; a
+// ctx with one shard is one engine.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "../../include/ratelimit_hip.h"
+#include "rl_device.h"
+#include "rl_kernels.h"
+#include "rl_match.h"
+
+namespace rl {
+
+// Pipeline depth: scratch buffers (and streams) in flight. Stage A of up to
+// NBUF - 1 later batches may run while one batch's stage B holds the table.
+#ifndef RL_NBUF
+#define RL_NBUF 3
+#endif
+constexpr uint32_t NBUF = RL_NBUF;
+constexpr uint32_t PROF_RING = 8;  // timed batches in flight (> NBUF)
+
+struct Engine {
+  rl_config cfg;
+  hipStream_t stream = nullptr;   // serial work (== pipe[0])
+  hipStream_t pipe[NBUF] = {};    // one per scratch buffer
+  hipEvent_t b_done[NBUF] = {};   // stage B of the last batch on each buffer is done
+  hipEvent_t consumed[NBUF] = {}; // a routed owner batch's packed results (s[k].res) have been read
+  hipEvent_t route_ready = nullptr;  // eng_route_do_limit: the caller's received buffers are ready
+  hipStream_t side = nullptr;     // k_runs_general beside k_runs (stage B)
+  hipEvent_t side_go = nullptr, side_done = nullptr;
+  uint32_t next = 0, last = NBUF - 1;  // buffer of the next / of the latest batch
+  uint64_t hash_seed = 0;
+  HashKey hk{};
+  // table
+  Slot* slots = nullptr;
+  uint64_t nslots = 0;
+  uint8_t* arena = nullptr;
+  uint8_t* arena2 = nullptr;  // compaction target (rl_sweep), swapped with arena
+  uint64_t arena_cap16 = 0;
+  // scratch: s[k] per buffer; stripes, counters, time floor, routing and the
+  // table-stage error word are shared
+  Scratch s[NBUF]{};
+  Scratch rs{};                 // routing partition (eng_route_pack), allocated on first use
+  bool rs_ready = false;
+  unsigned long long* h_base = nullptr;  // pinned [NBUF][RL_MAX_SHARDS] routed chunk bases
+  uint32_t* errw = nullptr;  // [0, NBUF) stage-A words of the buffers, [NBUF] stage-B word, [NBUF+1] soft word
+  // device staging for the host-buffer entry points
+  uint8_t* d_stem = nullptr;
+  uint32_t *d_off = nullptr, *d_req = nullptr, *d_limit = nullptr, *d_hits = nullptr, *d_rule = nullptr;
+  int64_t* d_now = nullptr;
+  uint8_t *d_unit = nullptr, *d_flags = nullptr, *d_code = nullptr, *d_status = nullptr;
+  uint32_t *d_rem = nullptr, *d_reset = nullptr;
+  unsigned long long* d_stats = nullptr;
+  uint32_t* h_err = nullptr;  // pinned [4]
+  unsigned long long* h_counters = nullptr;
+  unsigned long long* h_route = nullptr;  // pinned route counts
+  std::string last_error;
+  uint64_t batches = 0, decisions = 0;
+  // rl_profile: a ring of per-batch event sets (stage boundaries, recorded on
+  // the batch's own stream, so pipelined batches are timed as they run),
+  // folded into the stage sums when a set is reused or read
+  bool prof = false;
+  uint32_t prof_every = 1, prof_skip = 0;  // time every prof_every-th batch
+  bool prof_pending[PROF_RING] = {};
+  uint32_t prof_next = 0;
+  hipEvent_t ev[PROF_RING][RL_NUM_STAGES + 1] = {};
+  double stage_ms[RL_NUM_STAGES] = {};
+  uint64_t prof_batches = 0;
+  // config match (rl_config_load / rl_do_limit_requests): the device trie and
+  // one growable device buffer carved per call for the raw requests
+  uint8_t* cfg_blob = nullptr;  // [nodes | index | prefix ‖ keys]
+  CfgDev cfg_dev{};
+  bool cfg_loaded = false;
+  uint8_t* mbuf = nullptr;
+  size_t mbuf_cap = 0;
+  uint32_t* h_match = nullptr;  // pinned [4]: matched count, stem bytes, error bits
+};
+
+// Engine entry points (rl_engine.hip): the single-shard implementations of
+// the C ABI functions of the same name (rl_x -> eng_x).
+Engine* eng_create(const rl_config* cfg, char* err, size_t errlen);
+void eng_destroy(Engine* c);
+const char* eng_last_error(const Engine* c);
+int eng_do_limit(Engine* c, const rl_batch* in, rl_result* out);
+int eng_do_limit_async(Engine* c, const rl_batch* in, rl_result* out, void* stream);
+int eng_synchronize(Engine* c);
+int eng_sweep(Engine* c, int64_t now, uint64_t* n_evicted);
+int eng_restore(Engine* c, const rl_restore_batch* in);
+int eng_table_info_get(Engine* c, rl_table_info* info);
+int eng_debug_keys(Engine* c, const rl_batch* in, uint8_t* out_bytes, uint32_t* out_off, uint32_t out_cap);
+int eng_debug_decide(Engine* c, uint32_t n, const uint32_t* before, const uint32_t* after, const uint8_t* lc_hit,
+                     const uint32_t* hits, const uint32_t* limit, const uint8_t* unit, const uint8_t* flags,
+                     const int64_t* now, uint8_t* code, uint32_t* remaining, uint32_t* reset_s, uint64_t* stat_deltas,
+                     uint8_t* lc_set);
+int eng_route_pack(Engine* c, const rl_batch* in, uint32_t n_shards, uint32_t src_rank, void* send_rec,
+                   uint8_t* send_stem, uint32_t* perm, uint64_t* counts, void* stream);
+int eng_route_do_limit(Engine* c, uint32_t n, const void* recv_rec, const uint8_t* recv_stem, uint64_t recv_stem_bytes,
+                       const uint64_t* src_stem_base, uint32_t n_shards, uint32_t n_rules, uint32_t rule_stride,
+                       uint64_t* ret, uint64_t* stats, int isolate, void* stream);
+int eng_route_scatter(Engine* c, uint32_t n, const uint32_t* perm, const uint64_t* ret, rl_result* out, void* stream);
+int eng_profile(Engine* c, int enable);
+int eng_profile_read(Engine* c, double* ms, uint32_t n, uint64_t* batches);
+int eng_config_load(Engine* c, const rl_config_tree* tree);
+int eng_do_limit_requests(Engine* c, const rl_request_batch* in, rl_request_result* out);
+int eng_local_cache_info_get(Engine* c, int64_t now, rl_local_cache_info* info);
+int eng_snapshot_size(Engine* c, uint64_t* bytes);
+int eng_snapshot_save(Engine* c, void* host, uint64_t bytes);
+int eng_snapshot_load(Engine* c, const void* host, uint64_t bytes);
+
+// Owner side of a routed batch, pipelined on the engine's streams like
+// eng_do_limit_async: unpack the n received wire records (chunks of n_src
+// sources, concatenated in source order, stems in recv_stem) and enqueue the
+// DoLimit pipeline once `ready` (an event of any device, or null) has fired.
+// rule_stride > 0 attributes stats per source: rule' = source x rule_stride +
+// rule (stats then holds n_src blocks of rule_stride x RL_NUM_STATS). The
+// packed results land in s[*slot].res (record order); b_done[*slot] marks
+// them complete and the reader must record consumed[*slot] once it has copied
+// them (the buffer is not reused before).
+int eng_route_owner(Engine* c, uint32_t n, const Wire* recv_rec, const uint8_t* recv_stem, uint64_t recv_stem_bytes,
+                    const uint64_t* src_stem_base, uint32_t n_src, uint32_t n_rules, uint32_t rule_stride,
+                    unsigned long long* stats, int isolate, hipEvent_t ready, uint32_t* slot);
+
+// Record an error on the engine (its rl_last_error) and return code.
+int eng_fail(Engine* c, int code, const std::string& msg);
+
+// Per-batch scratch arrays (rl_engine.hip), for the router's own partition.
+bool scratch_alloc(Scratch& s, uint32_t n);
+void scratch_free(Scratch& s);
+
+}  // namespace rl

@@ -1,0 +1,1118 @@
+// rl_api.hip — the extern "C" boundary of libratelimit_hip.so
+// (include/ratelimit_hip.h). Owns the HBM table, two sets of per-batch scratch
+// and the HIP streams; every entry point maps the device error words to an
+// rl_status.
+//
+// Batches submitted with eng_do_limit_async(stream = NULL) are pipelined: batch
+// t's table-free stage A (validate, hash, sort, segment) runs on scratch buffer
+// t % NBUF and that buffer's stream while batch t-1's stage B (the table) still
+// runs. Stage B of every batch waits for the previous batch's stage B (an
+// event chain), so the table sees batches in submission order and every key
+// sees the reference's sequential INCRBY order. Every other call is serial and
+// ordered after all submitted batches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <random>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ratelimit_hip.h"
+#include "rl_device.h"
+#include "rl_kernels.h"
+#include "rl_match.h"
+#include "rl_engine.h"
+
+using namespace rl;
+
+
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(Engine* c, int code, const std::string& msg);
+
+// Fold event set k (a timed batch) into the stage sums; waits for the batch.
+void prof_fold(Engine* c, uint32_t k) {
+  if (!c->prof_pending[k]) return;
+  c->prof_pending[k] = false;
+  if (hipEventSynchronize(c->ev[k][RL_NUM_STAGES]) != hipSuccess) return;
+  for (int i = 0; i < RL_NUM_STAGES; i++) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->ev[k][i], c->ev[k][i + 1]) == hipSuccess) c->stage_ms[i] += ms;
+  }
+  c->prof_batches++;
+}
+
+void prof_fold_all(Engine* c) {
+  for (uint32_t k = 0; k < PROF_RING; k++) prof_fold(c, (c->prof_next + k) % PROF_RING);
+}
+
+hipEvent_t* prof_events(Engine* c) {
+  if (!c->prof) return nullptr;
+  if (c->prof_skip) {
+    c->prof_skip--;
+    return nullptr;
+  }
+  c->prof_skip = c->prof_every - 1;
+  const uint32_t k = c->prof_next;
+  c->prof_next = (k + 1) % PROF_RING;
+  prof_fold(c, k);  // the batch that used this set PROF_RING batches ago
+  c->prof_pending[k] = true;
+  return c->ev[k];
+}
+
+int set_err(Engine* c, int code, const std::string& msg) {
+  if (c) c->last_error = msg;
+  else g_err = msg;
+  return code;
+}
+
+#define HIPCHK(c, expr)                                                                        \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess)                                                                      \
+      return set_err((c), RL_E_HIP, std::string("gpu: ") + #expr + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+template <typename T>
+hipError_t dalloc(T** p, size_t count) {
+  return hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T));
+}
+
+int map_err(Engine* c, uint32_t e) {
+  if (!e) return RL_OK;
+  if (e & ERR_TIME) return set_err(c, RL_E_TIME, "gpu: now outside [0, 2^32-172800] or before the last sweep");
+  if (e & ERR_HISTORY)
+    return set_err(c, RL_E_TIME, "gpu: time moved back beyond the previous window of a key (table keeps 2 windows)");
+  if (e & ERR_INVALID) return set_err(c, RL_E_INVALID, "gpu: malformed batch (unit, rule id, request index or stem offsets)");
+  if (e & ERR_TABLE_FULL) return set_err(c, RL_E_TABLE_FULL, "gpu: counter table full (raise table_slots or sweep)");
+  if (e & ERR_ARENA_FULL) return set_err(c, RL_E_ARENA_FULL, "gpu: long-stem arena full (raise arena_bytes)");
+  return set_err(c, RL_E_INTERNAL, "gpu: unknown device error");
+}
+
+// Order stream st after every batch submitted so far (their stage B, which
+// waited for all earlier ones).
+hipError_t after_batches(Engine* c, hipStream_t st) { return hipStreamWaitEvent(st, c->b_done[c->last], 0); }
+
+// Read (and clear) the sticky device error words; synchronises the stream,
+// which must already be ordered after all submitted work.
+// The soft word (descriptor errors answered by statuses) is cleared, not reported.
+int collect(Engine* c, hipStream_t st = nullptr) {
+  if (!st) st = c->stream;
+  HIPCHK(c, hipMemcpyAsync(c->h_err, c->errw, (NBUF + 3) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  uint32_t e = c->h_err[NBUF + 2];  // the routing partition's word
+  for (uint32_t j = 0; j <= NBUF; j++) e |= c->h_err[j];
+  if (e || c->h_err[NBUF + 1]) {
+    HIPCHK(c, hipMemsetAsync(c->errw, 0, (NBUF + 3) * sizeof(uint32_t), st));
+    HIPCHK(c, hipStreamSynchronize(st));
+  }
+  return map_err(c, e);
+}
+
+TableDev table_view(Engine* c);
+Params params(Engine* c, int isolate = 0);
+
+// Enqueue one batch. Pipelined (ctx streams): stage A on the buffer's own
+// stream as soon as the buffer is free, stage B after the previous batch's
+// stage B. Serial: both stages on `st` after all earlier work. With rl_profile
+// on, the stage boundaries are recorded on the batch's stream either way.
+uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hipStream_t st, bool pipelined) {
+  const uint32_t k = c->next;
+  c->next = (k + 1) % NBUF;
+  const TableDev t = table_view(c);
+  const int isolate = (!restore && o.status) ? 1 : 0;
+  const Params P = params(c, isolate);
+  if (pipelined) {
+    hipStream_t a = c->pipe[k];
+    hipEvent_t* ev = prof_events(c);
+    (void)hipStreamWaitEvent(a, c->b_done[k], 0);    // buffer k's previous batch is done
+    (void)hipStreamWaitEvent(a, c->consumed[k], 0);  // ... and its routed results were read
+    launch_stage_a(b, c->s[k], isolate, a, ev);
+    (void)hipStreamWaitEvent(a, c->b_done[c->last], 0);  // table order
+    launch_stage_b(b, o, t, P, c->s[k], restore, a, c->side, c->side_go, c->side_done, ev);
+    (void)hipEventRecord(c->b_done[k], a);
+  } else {
+    if (!st) st = c->stream;
+    (void)after_batches(c, st);
+    hipEvent_t* ev = prof_events(c);
+    launch_stage_a(b, c->s[k], isolate, st, ev);
+    launch_stage_b(b, o, t, P, c->s[k], restore, st, c->side, c->side_go, c->side_done, ev);
+    (void)hipEventRecord(c->b_done[k], st);
+  }
+  c->last = k;
+  return k;
+}
+
+int check_sizes(Engine* c, const rl_batch* in, uint64_t stem_bytes) {
+  if (!in) return set_err(c, RL_E_INVALID, "gpu: null batch");
+  if (in->n > c->cfg.max_batch || in->n_requests > c->cfg.max_requests || in->n_rules > c->cfg.max_rules ||
+      stem_bytes > c->cfg.max_stem_bytes)
+    return set_err(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_rules/max_stem_bytes");
+  if (in->n && in->n_requests == 0) return set_err(c, RL_E_INVALID, "gpu: descriptors without requests");
+  return RL_OK;
+}
+
+BatchDev dev_view(const Engine* c, const rl_batch* in, uint32_t stem_cap) {
+  BatchDev b;
+  b.hk = c->hk;
+  b.n = in->n;
+  b.n_req = in->n_requests;
+  b.n_rules = in->n_rules;
+  b.stem_cap = stem_cap;
+  b.stem_total = stem_cap;  // refined on the device from off[n]
+  b.now_desc = 0;
+  b.stem = in->stem_bytes;
+  b.off = in->stem_off;
+  b.now = in->now;
+  b.req = in->req_idx;
+  b.unit = in->unit;
+  b.flags = in->flags;
+  b.limit = in->limit;
+  b.hits = in->hits;
+  b.rule = in->rule_id;
+  return b;
+}
+
+TableDev table_view(Engine* c) {
+  TableDev t;
+  t.slots = c->slots;
+  t.mask = c->nslots - 1;
+  t.arena = c->arena;
+  t.arena_used16 = c->s[0].counters + 4;
+  t.arena_cap16 = c->arena_cap16;
+  t.max_probe = (uint32_t)std::min<uint64_t>(c->nslots, 1u << 16);
+  t.shift = 64u - (uint32_t)__builtin_ctzll(c->nslots);
+  return t;
+}
+
+Params params(Engine* c, int isolate) {
+  Params P;
+  P.ratio = c->cfg.near_limit_ratio;
+  P.lc_en = c->cfg.local_cache_enabled != 0;
+  P.per_second = c->cfg.per_second_split != 0;
+  P.isolate = isolate;
+  return P;
+}
+
+// Per-batch scratch of one pipeline buffer (sized for max_batch descriptors).
+bool alloc_buffer(Scratch& s, uint32_t n) {
+  const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
+  const size_t nt = (n + SEG_TILE - 1) / SEG_TILE + 1;
+  const size_t items = (size_t)n / (64 * 4 * 8) + 1 + PART_DIGITS;  // BIG_CHUNK-position work items
+  bool ok = dalloc(&s.big_meta, PART_DIGITS) == hipSuccess && dalloc(&s.big_n, 1) == hipSuccess &&
+            dalloc(&s.big_work, items) == hipSuccess && dalloc(&s.work_n, 1) == hipSuccess &&
+            dalloc(&s.big_cnt, items * (1 + 2 * BIG_HEAVY)) == hipSuccess;
+  ok = ok && dalloc(&s.rec, n) == hipSuccess && dalloc(&s.res, n) == hipSuccess;
+  for (int i = 0; i < 2; i++) ok = ok && dalloc(&s.keys[i], n) == hipSuccess && dalloc(&s.vals[i], n) == hipSuccess;
+  ok = ok && dalloc(&s.hist, 256ull * std::max(ntiles, 1u)) == hipSuccess && dalloc(&s.hist_tot, 256) == hipSuccess;
+  ok = ok && dalloc(&s.grp, n) == hipSuccess && dalloc(&s.lead, n) == hipSuccess && dalloc(&s.gmask, n) == hipSuccess &&
+       dalloc(&s.defer, n) == hipSuccess &&
+       dalloc(&s.defer_n, 1) == hipSuccess && dalloc(&s.defer2, n) == hipSuccess &&
+       dalloc(&s.defer1, n) == hipSuccess && dalloc(&s.defer1_n, 1) == hipSuccess &&
+       dalloc(&s.defer2_n, 1) == hipSuccess && dalloc(&s.fast_blk, (size_t)n / (256 * 32) + 1) == hipSuccess;
+  ok = ok && dalloc(&s.tile_f, nt) == hipSuccess && dalloc(&s.tile_s, nt) == hipSuccess &&
+       dalloc(&s.tile_h, nt) == hipSuccess;
+  ok = ok && dalloc(&s.hits_s, n) == hipSuccess && dalloc(&s.segsum, n) == hipSuccess &&
+       dalloc(&s.rid, n) == hipSuccess && dalloc(&s.run_start, (size_t)n + 1) == hipSuccess &&
+       dalloc(&s.run_flags, n) == hipSuccess && dalloc(&s.run_state, n) == hipSuccess &&
+       dalloc(&s.run_f, n) == hipSuccess && dalloc(&s.num_runs, 1) == hipSuccess &&
+       dalloc(&s.runs64, 1) == hipSuccess && dalloc(&s.drun, (size_t)n / 2 + BIG_HEAVY * PART_DIGITS) == hipSuccess;
+  ok = ok && dalloc(&s.hit_a, n) == hipSuccess && dalloc(&s.tile, n) == hipSuccess &&
+       dalloc(&s.hit_t, n) == hipSuccess;
+  ok = ok && dalloc(&s.run_end, n) == hipSuccess &&
+       dalloc(&s.part_info, (size_t)PART_DIGITS * std::max((n + PART_TILE - 1) / PART_TILE, 1u)) == hipSuccess;
+  ok = ok && dalloc(&s.r_off, (size_t)n + 1) == hipSuccess && dalloc(&s.r_req, n) == hipSuccess &&
+       dalloc(&s.r_limit, n) == hipSuccess && dalloc(&s.r_hits, n) == hipSuccess && dalloc(&s.r_rule, n) == hipSuccess &&
+       dalloc(&s.r_now, n) == hipSuccess && dalloc(&s.r_unit, n) == hipSuccess && dalloc(&s.r_flags, n) == hipSuccess &&
+       dalloc(&s.r_base, RL_MAX_SHARDS) == hipSuccess;
+  return ok;
+}
+
+void free_buffer(Scratch& s) {
+  void* bufs[] = {s.rec, s.res, s.big_meta, s.big_n, s.big_work, s.work_n, s.big_cnt, s.keys[0], s.keys[1], s.vals[0], s.vals[1], s.hist,
+                  s.hist_tot, s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1, s.defer1_n, s.fast_blk, s.tile_f, s.tile_s, s.tile_h, s.hits_s, s.segsum, s.rid,
+                  s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs, s.runs64, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t,
+                  s.r_off, s.r_req, s.r_limit, s.r_hits, s.r_rule, s.r_now, s.r_unit, s.r_flags, s.r_base};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+}
+
+// Copy a host batch into the staging buffers; returns the device view.
+int stage(Engine* c, const rl_batch* in, BatchDev* out) {
+  const uint32_t n = in->n, nq = in->n_requests;
+  const uint64_t nb = n ? in->stem_off[n] : 0;
+  int rc = check_sizes(c, in, nb);
+  if (rc) return rc;
+  hipStream_t st = c->stream;
+  HIPCHK(c, after_batches(c, st));  // staging may still feed a routed batch
+  if (nb) HIPCHK(c, hipMemcpyAsync(c->d_stem, in->stem_bytes, nb, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->d_off, in->stem_off, (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  if (nq) HIPCHK(c, hipMemcpyAsync(c->d_now, in->now, nq * sizeof(int64_t), hipMemcpyHostToDevice, st));
+  if (n) {
+    HIPCHK(c, hipMemcpyAsync(c->d_req, in->req_idx, n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->d_unit, in->unit, n, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->d_flags, in->flags, n, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->d_limit, in->limit, n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->d_hits, in->hits, n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(c->d_rule, in->rule_id, n * 4, hipMemcpyHostToDevice, st));
+  }
+  rl_batch d = *in;
+  d.stem_bytes = c->d_stem;
+  d.stem_off = c->d_off;
+  d.now = c->d_now;
+  d.req_idx = c->d_req;
+  d.unit = c->d_unit;
+  d.flags = c->d_flags;
+  d.limit = c->d_limit;
+  d.hits = c->d_hits;
+  d.rule_id = c->d_rule;
+  *out = dev_view(c, &d, c->cfg.max_stem_bytes);
+  return RL_OK;
+}
+
+}  // namespace
+
+namespace rl {
+
+const char* eng_last_error(const Engine* c) { return c ? c->last_error.c_str() : g_err.c_str(); }
+
+Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
+  auto fail = [&](const std::string& m, Engine* c) -> Engine* {
+    if (err && errlen) snprintf(err, errlen, "%s", m.c_str());
+    g_err = m;
+    if (c) eng_destroy(c);
+    return nullptr;
+  };
+  if (!cfg_in) return fail("gpu: null config", nullptr);
+  rl_config cfg = *cfg_in;
+  if (!cfg.table_slots) cfg.table_slots = 1ull << 24;
+  if (cfg.table_slots & (cfg.table_slots - 1)) return fail("gpu: table_slots must be a power of two", nullptr);
+  if (!cfg.arena_bytes) cfg.arena_bytes = 64ull << 20;
+  if (!cfg.max_batch) cfg.max_batch = 1u << 20;
+  if (cfg.max_batch > MAX_PART_TILES * PART_TILE)
+    return fail("gpu: max_batch must be at most 8388608 descriptors", nullptr);
+  if (!cfg.max_requests) cfg.max_requests = cfg.max_batch;
+  if (!cfg.max_rules) cfg.max_rules = 65536;
+  if (!cfg.max_stem_bytes) cfg.max_stem_bytes = 128u * cfg.max_batch;
+  if (hipSetDevice(cfg.device) != hipSuccess) return fail("gpu: hipSetDevice failed", nullptr);
+
+  Engine* c = new Engine();
+  c->cfg = cfg;
+  c->hash_seed = cfg.hash_seed;
+  while (!c->hash_seed) {  // a secret per-ctx key unless the caller shares one (multi-shard tables)
+    std::random_device rd;
+    c->hash_seed = ((uint64_t)rd() << 32) ^ rd();
+  }
+  c->cfg.hash_seed = c->hash_seed;
+  c->hk = hash_key_of(c->hash_seed, cfg.debug_hash_bits);
+  c->nslots = cfg.table_slots;
+  c->arena_cap16 = cfg.arena_bytes / 16;
+  const uint32_t n = cfg.max_batch;
+  bool ok = true;
+  for (uint32_t k = 0; k < NBUF; k++) ok = ok && hipStreamCreateWithFlags(&c->pipe[k], hipStreamNonBlocking) == hipSuccess;
+  c->stream = c->pipe[0];
+  ok = ok && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess;
+  for (uint32_t k = 0; k < NBUF; k++)
+    ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&c->side_go, hipEventDisableTiming) == hipSuccess &&
+       hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming) == hipSuccess;
+  ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess;
+  ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess && dalloc(&c->arena2, cfg.arena_bytes) == hipSuccess;
+  for (uint32_t k = 0; k < NBUF; k++) ok = ok && alloc_buffer(c->s[k], n);
+  Scratch& s0 = c->s[0];
+  ok = ok && dalloc(&c->errw, NBUF + 3) == hipSuccess;
+  for (uint32_t k = 0; k < NBUF; k++)
+    ok = ok && hipEventCreateWithFlags(&c->consumed[k], hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&c->route_ready, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_base, (size_t)NBUF * RL_MAX_SHARDS * 8) == hipSuccess;
+  ok = ok && dalloc(&s0.stripes, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS) == hipSuccess;
+  ok = ok && dalloc(&s0.time_floor, 1) == hipSuccess;
+  ok = ok && dalloc(&s0.counters, 8) == hipSuccess;
+  ok = ok && dalloc(&s0.route_start, RL_MAX_SHARDS + 1) == hipSuccess &&
+       dalloc(&s0.route_base, RL_MAX_SHARDS) == hipSuccess && dalloc(&s0.route_counts, 2 * RL_MAX_SHARDS) == hipSuccess;
+  for (uint32_t k = 0; k < NBUF; k++) {  // shared members
+    Scratch& sk = c->s[k];
+    sk.err = c->errw ? c->errw + k : nullptr;
+    sk.errb = c->errw ? c->errw + NBUF : nullptr;
+    sk.errs = c->errw ? c->errw + NBUF + 1 : nullptr;
+    sk.stripes = s0.stripes;
+    sk.time_floor = s0.time_floor;
+    sk.counters = s0.counters;
+    sk.route_start = s0.route_start;
+    sk.route_base = s0.route_base;
+    sk.route_counts = s0.route_counts;
+  }
+  ok = ok && hipHostMalloc((void**)&c->h_route, 2 * RL_MAX_SHARDS * sizeof(unsigned long long)) == hipSuccess;
+  ok = ok && dalloc(&c->d_stem, (size_t)cfg.max_stem_bytes + 64) == hipSuccess;
+  ok = ok && dalloc(&c->d_off, (size_t)n + 1) == hipSuccess;
+  ok = ok && dalloc(&c->d_now, cfg.max_requests) == hipSuccess;
+  ok = ok && dalloc(&c->d_req, n) == hipSuccess && dalloc(&c->d_unit, n) == hipSuccess &&
+       dalloc(&c->d_flags, n) == hipSuccess && dalloc(&c->d_limit, n) == hipSuccess &&
+       dalloc(&c->d_hits, n) == hipSuccess && dalloc(&c->d_rule, n) == hipSuccess;
+  ok = ok && dalloc(&c->d_code, n) == hipSuccess && dalloc(&c->d_status, n) == hipSuccess &&
+       dalloc(&c->d_rem, n) == hipSuccess &&
+       dalloc(&c->d_reset, n) == hipSuccess;
+  ok = ok && dalloc(&c->d_stats, (size_t)cfg.max_rules * RL_NUM_STATS) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_err, (NBUF + 3) * sizeof(uint32_t)) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_counters, 8 * sizeof(unsigned long long)) == hipSuccess;
+  if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
+  ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
+       hipMemsetAsync(c->errw, 0, (NBUF + 3) * 4, c->stream) == hipSuccess &&
+       hipMemsetAsync(s0.time_floor, 0, 8, c->stream) == hipSuccess &&
+       hipMemsetAsync(s0.counters, 0, 64, c->stream) == hipSuccess &&
+       hipMemsetAsync(s0.stripes, 0, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS * 8, c->stream) ==
+           hipSuccess &&
+       hipMemsetAsync(c->d_stem, 0, (size_t)cfg.max_stem_bytes + 64, c->stream) == hipSuccess &&
+       hipStreamSynchronize(c->stream) == hipSuccess;
+  for (uint32_t k = 0; k < NBUF; k++)
+    ok = ok && hipEventRecord(c->b_done[k], c->stream) == hipSuccess &&
+         hipEventRecord(c->consumed[k], c->stream) == hipSuccess;
+  if (!ok) return fail("gpu: device initialisation failed", c);
+  return c;
+}
+
+void eng_destroy(Engine* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->cfg.device);
+  for (uint32_t k = 0; k < NBUF; k++)
+    if (c->pipe[k]) (void)hipStreamSynchronize(c->pipe[k]);
+  if (c->side) (void)hipStreamSynchronize(c->side);
+  if (c->side_go) (void)hipEventDestroy(c->side_go);
+  if (c->side_done) (void)hipEventDestroy(c->side_done);
+  for (uint32_t k = 0; k < PROF_RING; k++)
+    for (int i = 0; i <= RL_NUM_STAGES; i++)
+      if (c->ev[k][i]) (void)hipEventDestroy(c->ev[k][i]);
+  for (uint32_t k = 0; k < NBUF; k++) {
+    free_buffer(c->s[k]);
+    if (c->b_done[k]) (void)hipEventDestroy(c->b_done[k]);
+    if (c->consumed[k]) (void)hipEventDestroy(c->consumed[k]);
+  }
+  if (c->rs_ready) {
+    c->rs.err = nullptr;  // (a word of errw)
+    scratch_free(c->rs);
+  }
+  if (c->route_ready) (void)hipEventDestroy(c->route_ready);
+  if (c->h_base) (void)hipHostFree(c->h_base);
+  const Scratch& s0 = c->s[0];
+  void* bufs[] = {c->slots, c->arena, c->arena2, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
+                  c->d_now, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_status,
+                  c->d_rem,
+                  c->d_reset, c->d_stats, s0.route_start, s0.route_base, s0.route_counts};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+  if (c->h_err) (void)hipHostFree(c->h_err);
+  if (c->h_counters) (void)hipHostFree(c->h_counters);
+  if (c->h_route) (void)hipHostFree(c->h_route);
+  for (void* p : {(void*)c->cfg_blob, (void*)c->mbuf})
+    if (p) (void)hipFree(p);
+  if (c->h_match) (void)hipHostFree(c->h_match);
+  for (uint32_t k = 0; k < NBUF; k++)
+    if (c->pipe[k]) (void)hipStreamDestroy(c->pipe[k]);
+  if (c->side) (void)hipStreamDestroy(c->side);
+  delete c;
+}
+
+int eng_do_limit_async(Engine* c, const rl_batch* in, rl_result* out, void* stream) {
+  if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  // device pointers: the total stem size is only known on the device; the
+  // kernels bound-check offsets against max_stem_bytes (stem_cap)
+  int rc = check_sizes(c, in, 0);
+  if (rc) return rc;
+  if ((uintptr_t)in->stem_bytes & 3u) return set_err(c, RL_E_INVALID, "gpu: stem_bytes must be 4-byte aligned");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  BatchDev b = dev_view(c, in, c->cfg.max_stem_bytes);
+  OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats, out->status};
+  // NULL stream: pipelined on the ctx streams; otherwise serial on the caller's stream
+  enqueue(c, b, o, 0, (hipStream_t)stream, stream == nullptr);
+  HIPCHK(c, hipGetLastError());
+  c->batches++;
+  c->decisions += in->n;
+  return RL_OK;
+}
+
+bool scratch_alloc(Scratch& s, uint32_t n) {
+  s = Scratch{};
+  bool ok = alloc_buffer(s, n);
+  ok = ok && dalloc(&s.err, 1) == hipSuccess && dalloc(&s.route_start, RL_MAX_SHARDS + 1) == hipSuccess &&
+       dalloc(&s.route_base, RL_MAX_SHARDS) == hipSuccess && dalloc(&s.route_counts, 2 * RL_MAX_SHARDS) == hipSuccess;
+  ok = ok && hipMemset(s.err, 0, 4) == hipSuccess;
+  return ok;
+}
+
+void scratch_free(Scratch& s) {
+  free_buffer(s);
+  for (void* p : {(void*)s.err, (void*)s.route_start, (void*)s.route_base, (void*)s.route_counts})
+    if (p) (void)hipFree(p);
+  s = Scratch{};
+}
+
+// The routing partition runs on its own scratch (c->rs), so it never waits
+// for, or disturbs, the pipeline buffers; its validation word is the ctx's
+// errw[NBUF + 2] (reported at rl_synchronize). counts = device memory.
+int eng_route_pack(Engine* c, const rl_batch* in, uint32_t n_shards, uint32_t src_rank, void* send_rec,
+                   uint8_t* send_stem, uint32_t* perm, uint64_t* counts, void* stream) {
+  if (!c || !in || !counts || (in->n && (!send_rec || !send_stem || !perm)))
+    return set_err(c, RL_E_INVALID, "gpu: null argument");
+  if (n_shards < 1 || n_shards > RL_MAX_SHARDS || src_rank >= n_shards)
+    return set_err(c, RL_E_INVALID, "gpu: n_shards must be 1..256 and src_rank < n_shards");
+  int rc = check_sizes(c, in, 0);
+  if (rc) return rc;
+  if ((uintptr_t)in->stem_bytes & 3u) return set_err(c, RL_E_INVALID, "gpu: stem_bytes must be 4-byte aligned");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (!c->rs_ready) {
+    HIPCHK(c, after_batches(c, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!scratch_alloc(c->rs, c->cfg.max_batch)) {
+      scratch_free(c->rs);
+      return set_err(c, RL_E_HIP, "gpu: routing scratch allocation failed");
+    }
+    (void)hipFree(c->rs.err);
+    c->rs.err = c->errw + NBUF + 2;
+    c->rs_ready = true;
+  }
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  BatchDev b = dev_view(c, in, c->cfg.max_stem_bytes);
+  launch_route_pack(b, n_shards, src_rank, (Wire*)send_rec, send_stem, perm, (unsigned long long*)counts, c->rs, st);
+  HIPCHK(c, hipGetLastError());
+  return RL_OK;
+}
+
+int eng_route_owner(Engine* c, uint32_t n, const Wire* recv_rec, const uint8_t* recv_stem, uint64_t recv_stem_bytes,
+                    const uint64_t* src_stem_base, uint32_t n_src, uint32_t n_rules, uint32_t rule_stride,
+                    unsigned long long* stats, int isolate, hipEvent_t ready, uint32_t* slot) {
+  const uint32_t rules_eff = rule_stride ? n_src * rule_stride : n_rules;
+  if (!c || !src_stem_base || (n && (!recv_rec || !recv_stem)) || (rules_eff && !stats))
+    return set_err(c, RL_E_INVALID, "gpu: null argument");
+  if (n_src < 1 || n_src > RL_MAX_SHARDS) return set_err(c, RL_E_INVALID, "gpu: n_shards must be 1..256");
+  if (rule_stride && n_rules > rule_stride) return set_err(c, RL_E_INVALID, "gpu: n_rules exceeds the rule stride");
+  // (the received stems are the caller's buffer: only 32-bit offsets bound them)
+  if (n > c->cfg.max_batch || rules_eff > c->cfg.max_rules || recv_stem_bytes >= (1ull << 32))
+    return set_err(c, RL_E_CAPACITY, "gpu: routed batch exceeds max_batch/max_rules or 4 GiB of stems");
+  if ((uintptr_t)recv_stem & 3u) return set_err(c, RL_E_INVALID, "gpu: recv_stem must be 4-byte aligned");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  // the buffer this batch will take (enqueue advances c->next the same way)
+  const uint32_t k = c->next;
+  Scratch& sk = c->s[k];
+  hipStream_t a = c->pipe[k];
+  HIPCHK(c, hipStreamWaitEvent(a, c->b_done[k], 0));
+  HIPCHK(c, hipStreamWaitEvent(a, c->consumed[k], 0));
+  if (ready) HIPCHK(c, hipStreamWaitEvent(a, ready, 0));
+  unsigned long long* hb = c->h_base + (size_t)k * RL_MAX_SHARDS;
+  HIPCHK(c, hipEventSynchronize(c->b_done[k]));  // (the pinned bases of buffer k's previous batch were read)
+  for (uint32_t j = 0; j < n_src; j++) hb[j] = src_stem_base[j];
+  HIPCHK(c, hipMemcpyAsync(sk.r_base, hb, (size_t)n_src * 8, hipMemcpyHostToDevice, a));
+  BatchOut bo{sk.r_off, sk.r_now, sk.r_req, sk.r_unit, sk.r_flags, sk.r_limit, sk.r_hits, sk.r_rule};
+  // a malformed exchange poisons this batch's validation word (fails the batch)
+  launch_route_unpack(recv_rec, n, sk.r_base, n_src, recv_stem_bytes, rule_stride, bo, sk.err, a);
+  if (!n) HIPCHK(c, hipMemsetAsync(sk.r_off, 0, sizeof(uint32_t), a));
+  BatchDev b;
+  b.hk = c->hk;
+  b.n = n;
+  b.n_req = n;
+  b.n_rules = rules_eff;
+  b.stem_cap = (uint32_t)recv_stem_bytes;
+  b.stem_total = (uint32_t)recv_stem_bytes;
+  b.now_desc = 1;
+  b.stem = recv_stem;
+  b.off = sk.r_off;
+  b.now = sk.r_now;
+  b.req = sk.r_req;
+  b.unit = sk.r_unit;
+  b.flags = sk.r_flags;
+  b.limit = sk.r_limit;
+  b.hits = sk.r_hits;
+  b.rule = sk.r_rule;
+  OutDev o{nullptr, nullptr, nullptr, stats, isolate ? c->d_status : nullptr};
+  const uint32_t kk = enqueue(c, b, o, 0, nullptr, true);
+  HIPCHK(c, hipGetLastError());
+  c->batches++;
+  c->decisions += n;
+  *slot = kk;
+  return RL_OK;
+}
+
+// The per-rank owner step of the multi-process exchange (sharded.py): the
+// pipelined owner batch, then on `stream` its packed results copied to ret.
+int eng_route_do_limit(Engine* c, uint32_t n, const void* recv_rec, const uint8_t* recv_stem, uint64_t recv_stem_bytes,
+                       const uint64_t* src_stem_base, uint32_t n_shards, uint32_t n_rules, uint32_t rule_stride,
+                       uint64_t* ret, uint64_t* stats, int isolate, void* stream) {
+  if (!c || (n && !ret)) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  HIPCHK(c, hipEventRecord(c->route_ready, st));  // the received buffers are ordered on the caller's stream
+  uint32_t k = 0;
+  const int rc = eng_route_owner(c, n, (const Wire*)recv_rec, recv_stem, recv_stem_bytes, src_stem_base, n_shards,
+                                 n_rules, rule_stride, (unsigned long long*)stats, isolate, c->route_ready, &k);
+  if (rc) return rc;
+  HIPCHK(c, hipStreamWaitEvent(st, c->b_done[k], 0));
+  if (n) HIPCHK(c, hipMemcpyAsync(ret, c->s[k].res, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
+  HIPCHK(c, hipEventRecord(c->consumed[k], st));
+  return RL_OK;
+}
+
+int eng_fail(Engine* c, int code, const std::string& msg) { return set_err(c, code, msg); }
+
+int eng_route_scatter(Engine* c, uint32_t n, const uint32_t* perm, const uint64_t* ret, rl_result* out, void* stream) {
+  if (!c || !out || (n && (!perm || !ret))) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats, out->status};
+  launch_route_scatter(perm, (const unsigned long long*)ret, n, o, st);
+  HIPCHK(c, hipGetLastError());
+  return RL_OK;
+}
+
+int eng_profile(Engine* c, int enable) {
+  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (enable && !c->ev[0][0])
+    for (uint32_t k = 0; k < PROF_RING; k++)
+      for (int i = 0; i <= RL_NUM_STAGES; i++) HIPCHK(c, hipEventCreate(&c->ev[k][i]));
+  prof_fold_all(c);
+  c->prof = enable > 0;
+  c->prof_every = enable > 0 ? (uint32_t)enable : 1u;
+  c->prof_skip = 0;
+  return RL_OK;
+}
+
+int eng_profile_read(Engine* c, double* ms, uint32_t n, uint64_t* batches) {
+  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  prof_fold_all(c);
+  for (uint32_t i = 0; i < n && i < RL_NUM_STAGES; i++) ms[i] = c->stage_ms[i];
+  if (batches) *batches = c->prof_batches;
+  for (int i = 0; i < RL_NUM_STAGES; i++) c->stage_ms[i] = 0;
+  c->prof_batches = 0;
+  return RL_OK;
+}
+
+int eng_synchronize(Engine* c) {
+  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, hipDeviceSynchronize());
+  return collect(c);
+}
+
+int eng_do_limit(Engine* c, const rl_batch* in, rl_result* out) {
+  if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  BatchDev b;
+  int rc = stage(c, in, &b);
+  if (rc) return rc;
+  hipStream_t st = c->stream;
+  OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats, out->status ? c->d_status : nullptr};
+  enqueue(c, b, o, 0, st, false);
+  HIPCHK(c, hipGetLastError());
+  const uint32_t n = in->n;
+  if (n) {
+    if (out->status) HIPCHK(c, hipMemcpyAsync(out->status, c->d_status, n, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(out->code, c->d_code, n, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(out->limit_remaining, c->d_rem, n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(out->reset_s, c->d_reset, n * 4, hipMemcpyDeviceToHost, st));
+  }
+  if (in->n_rules)
+    HIPCHK(c, hipMemcpyAsync(out->stats, c->d_stats, (size_t)in->n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost, st));
+  c->batches++;
+  c->decisions += n;
+  return collect(c);
+}
+
+int eng_restore(Engine* c, const rl_restore_batch* r) {
+  if (!c || !r) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (!r->n) return RL_OK;
+  // A restore batch is a batch of SET records: req = record index, hits = count,
+  // flags = local-cache bit. It runs through the same grouping pipeline.
+  std::string* e = &c->last_error;
+  (void)e;
+  const uint32_t n = r->n;
+  uint32_t* req = new uint32_t[n];
+  uint32_t* zero = new uint32_t[n]();
+  uint8_t* lcf = new uint8_t[n]();
+  for (uint32_t i = 0; i < n; i++) {
+    req[i] = i;
+    if (r->lc) lcf[i] = r->lc[i] ? 1 : 0;
+  }
+  rl_batch in{};
+  in.n = n;
+  in.n_requests = n;
+  in.n_rules = 1;
+  in.stem_bytes = r->stem_bytes;
+  in.stem_off = r->stem_off;
+  in.now = r->now;
+  in.req_idx = req;
+  in.unit = r->unit;
+  in.flags = lcf;
+  in.limit = zero;
+  in.hits = r->count;
+  in.rule_id = zero;
+  BatchDev b;
+  int rc = stage(c, &in, &b);
+  if (!rc) {
+    OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats, nullptr};
+    enqueue(c, b, o, 1, c->stream, false);
+    hipError_t he = hipGetLastError();
+    rc = he != hipSuccess ? set_err(c, RL_E_HIP, std::string("gpu: ") + hipGetErrorString(he)) : collect(c);
+  }
+  delete[] req;
+  delete[] zero;
+  delete[] lcf;
+  return rc;
+}
+
+int eng_sweep(Engine* c, int64_t now, uint64_t* n_evicted) {
+  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
+  if (now < 0 || now > (int64_t)NOW_MAX) return set_err(c, RL_E_TIME, "gpu: sweep time out of range");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  // the sweep time becomes a floor: later requests may not be earlier
+  int64_t last = 0;
+  HIPCHK(c, after_batches(c, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&last, c->s[0].time_floor, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (now > last) HIPCHK(c, hipMemcpyAsync(c->s[0].time_floor, &now, 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->s[0].counters, 0, 8, c->stream));
+  launch_sweep(c->slots, c->nslots, (uint32_t)now, c->s[0].counters, c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 40, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (n_evicted) *n_evicted = c->h_counters[0];
+  if (c->h_counters[0] && c->h_counters[4]) {
+    // reclaim the long-stem arena: live slots' overflow bytes move to the spare
+    // arena, packed from 0, and the two swap (counters[4] = the arena cursor)
+    HIPCHK(c, hipMemsetAsync(c->s[0].counters + 4, 0, 8, c->stream));
+    launch_arena_compact(c->slots, c->nslots, c->arena, c->arena2, c->s[0].counters + 4, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::swap(c->arena, c->arena2);
+  }
+  return RL_OK;
+}
+
+int eng_table_info_get(Engine* c, rl_table_info* info) {
+  if (!c || !info) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, after_batches(c, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->s[0].counters, 0, 24, c->stream));
+  launch_table_info(c->slots, c->nslots, c->s[0].counters, c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 40, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  info->table_slots = c->nslots;
+  info->live_slots = c->h_counters[0];
+  info->tombstones = c->h_counters[1];
+  info->exact_stems = c->h_counters[2];
+  info->arena_bytes_used = c->h_counters[4] * 16;
+  info->batches = c->batches;
+  info->decisions = c->decisions;
+  return RL_OK;
+}
+
+int eng_debug_keys(Engine* c, const rl_batch* in, uint8_t* out_bytes, uint32_t* out_off, uint32_t out_cap) {
+  if (!c || !in || !out_off) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  BatchDev b;
+  int rc = stage(c, in, &b);
+  if (rc) return rc;
+  const uint32_t n = in->n;
+  const size_t cap = (size_t)(n ? in->stem_off[n] : 0) + 24ull * n + 1;
+  uint8_t* d_out = nullptr;
+  uint32_t* d_len = nullptr;
+  HIPCHK(c, dalloc(&d_out, cap));
+  HIPCHK(c, dalloc(&d_len, (size_t)n + 1));
+  launch_debug_keys(b, d_out, d_len, c->stream);
+  uint8_t* h_out = new uint8_t[cap];
+  uint32_t* h_len = new uint32_t[n + 1];
+  hipError_t e1 = hipMemcpyAsync(h_out, d_out, cap, hipMemcpyDeviceToHost, c->stream);
+  hipError_t e2 = hipMemcpyAsync(h_len, d_len, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream);
+  hipError_t e3 = hipStreamSynchronize(c->stream);
+  (void)hipFree(d_out);
+  (void)hipFree(d_len);
+  rc = (e1 || e2 || e3) ? set_err(c, RL_E_HIP, "gpu: debug_keys copy failed") : RL_OK;
+  uint32_t pos = 0;
+  out_off[0] = 0;
+  for (uint32_t i = 0; i < n && rc == RL_OK; i++) {
+    if (pos + h_len[i] > out_cap) {
+      rc = set_err(c, RL_E_CAPACITY, "gpu: debug_keys output buffer too small");
+      break;
+    }
+    memcpy(out_bytes + pos, h_out + in->stem_off[i] + 24ull * i, h_len[i]);
+    pos += h_len[i];
+    out_off[i + 1] = pos;
+  }
+  delete[] h_out;
+  delete[] h_len;
+  return rc;
+}
+
+int eng_debug_decide(Engine* c, uint32_t n, const uint32_t* before, const uint32_t* after, const uint8_t* lc_hit,
+                    const uint32_t* hits, const uint32_t* limit, const uint8_t* unit, const uint8_t* flags,
+                    const int64_t* now, uint8_t* code, uint32_t* remaining, uint32_t* reset_s,
+                    uint64_t* stat_deltas, uint8_t* lc_set) {
+  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
+  if (!n) return RL_OK;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  for (uint32_t i = 0; i < n; i++)
+    if (unit[i] < 1 || unit[i] > 4) return set_err(c, RL_E_INVALID, "gpu: unit out of range");
+  uint32_t *d_b, *d_a, *d_h, *d_l, *d_rem, *d_rs;
+  uint8_t *d_lc, *d_u, *d_f, *d_code, *d_set;
+  int64_t* d_now;
+  unsigned long long* d_del;
+  HIPCHK(c, dalloc(&d_b, n));
+  HIPCHK(c, dalloc(&d_a, n));
+  HIPCHK(c, dalloc(&d_h, n));
+  HIPCHK(c, dalloc(&d_l, n));
+  HIPCHK(c, dalloc(&d_rem, n));
+  HIPCHK(c, dalloc(&d_rs, n));
+  HIPCHK(c, dalloc(&d_lc, n));
+  HIPCHK(c, dalloc(&d_u, n));
+  HIPCHK(c, dalloc(&d_f, n));
+  HIPCHK(c, dalloc(&d_code, n));
+  HIPCHK(c, dalloc(&d_set, n));
+  HIPCHK(c, dalloc(&d_now, n));
+  HIPCHK(c, dalloc(&d_del, (size_t)n * RL_NUM_STATS));
+  hipStream_t st = c->stream;
+  HIPCHK(c, hipMemcpyAsync(d_b, before, n * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(d_a, after, n * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(d_h, hits, n * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(d_l, limit, n * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(d_lc, lc_hit, n, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(d_u, unit, n, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(d_f, flags, n, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(d_now, now, n * 8, hipMemcpyHostToDevice, st));
+  launch_debug_decide(n, d_b, d_a, d_lc, d_h, d_l, d_u, d_f, d_now, c->cfg.near_limit_ratio,
+                      c->cfg.local_cache_enabled, d_code, d_rem, d_rs, d_del, d_set, st);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(code, d_code, n, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(remaining, d_rem, n * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(reset_s, d_rs, n * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(stat_deltas, d_del, (size_t)n * RL_NUM_STATS * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(lc_set, d_set, n, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  void* bufs[] = {d_b, d_a, d_h, d_l, d_rem, d_rs, d_lc, d_u, d_f, d_code, d_set, d_now, d_del};
+  for (void* p : bufs) (void)hipFree(p);
+  return RL_OK;
+}
+
+// ---- config match: GetLimit on the device (rl_match.hip) -------------------
+
+int eng_config_load(Engine* c, const rl_config_tree* t) {
+  if (!c || !t || (t->n_nodes && (!t->nodes || (t->key_bytes_len && !t->key_bytes))) ||
+      (t->cache_key_prefix_len && !t->cache_key_prefix))
+    return set_err(c, RL_E_INVALID, "gpu: null config tree");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const uint32_t n = t->n_nodes;
+  std::vector<CfgNode> nodes(n);
+  for (uint32_t i = 0; i < n; i++) {
+    const rl_config_node& x = t->nodes[i];
+    if (x.parent < -1 || x.parent >= (int32_t)i || (uint64_t)x.key_off + x.key_len > t->key_bytes_len)
+      return set_err(c, RL_E_INVALID, "gpu: config node " + std::to_string(i) + ": bad parent or key range");
+    if (x.has_limit && !x.unlimited && (x.unit < RL_UNIT_SECOND || x.unit > RL_UNIT_DAY))
+      return set_err(c, RL_E_INVALID, "gpu: config node " + std::to_string(i) + ": invalid rate limit unit");
+    if (x.has_limit && x.rule_id >= c->cfg.max_rules)
+      return set_err(c, RL_E_INVALID, "gpu: config node " + std::to_string(i) + ": rule id >= max_rules");
+    CfgNode& d = nodes[i];
+    d = CfgNode{};
+    d.parent = x.parent;
+    d.key_off = x.key_off;
+    d.key_len = x.key_len;
+    d.rpu = x.requests_per_unit;
+    d.rule = x.rule_id;
+    d.unit = x.unit;
+    d.has_limit = x.has_limit ? 1 : 0;
+    d.unlimited = x.unlimited ? 1 : 0;
+    d.shadow = x.shadow_mode ? 1 : 0;
+    if (x.parent >= 0) nodes[x.parent].n_children++;
+  }
+  uint32_t size = 16;
+  while (size < 2 * n) size <<= 1;
+  std::vector<unsigned long long> index(size, 0);
+  const uint8_t* kb = t->key_bytes;
+  for (uint32_t i = 0; i < n; i++) {
+    const rl_config_node& x = t->nodes[i];
+    const uint64_t h = cfg_hash(x.parent, kb + x.key_off, x.key_len);
+    uint32_t pos = (uint32_t)h & (size - 1);
+    for (;; pos = (pos + 1) & (size - 1)) {
+      const unsigned long long e = index[pos];
+      if (!e) break;
+      const rl_config_node& y = t->nodes[(uint32_t)(e >> 32) - 1];
+      if (y.parent == x.parent && y.key_len == x.key_len && !memcmp(kb + y.key_off, kb + x.key_off, x.key_len))
+        return set_err(c, RL_E_INVALID, "gpu: duplicate config key under one parent (node " + std::to_string(i) + ")");
+    }
+    index[pos] = (unsigned long long)(uint32_t)(h >> 32) | (unsigned long long)(i + 1) << 32;
+  }
+  // one blob [nodes | index | prefix ‖ keys], so a small config is staged into LDS in one copy
+  const uint64_t nkeys = t->cache_key_prefix_len + t->key_bytes_len;
+  const uint64_t idx_off = (uint64_t)n * sizeof(CfgNode), key_off = idx_off + size * 8ull;
+  const uint64_t blob = (key_off + nkeys + 3) & ~3ull;
+  std::vector<uint8_t> host(blob, 0);
+  if (n) memcpy(host.data(), nodes.data(), n * sizeof(CfgNode));
+  memcpy(host.data() + idx_off, index.data(), size * 8ull);
+  if (t->cache_key_prefix_len) memcpy(host.data() + key_off, t->cache_key_prefix, t->cache_key_prefix_len);
+  if (t->key_bytes_len) memcpy(host.data() + key_off + t->cache_key_prefix_len, kb, t->key_bytes_len);
+  HIPCHK(c, after_batches(c, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->cfg_blob) (void)hipFree(c->cfg_blob);
+  c->cfg_blob = nullptr;
+  c->cfg_loaded = false;
+  HIPCHK(c, dalloc(&c->cfg_blob, blob));
+  if (!c->h_match) HIPCHK(c, hipHostMalloc((void**)&c->h_match, 16, hipHostMallocDefault));
+  HIPCHK(c, hipMemcpy(c->cfg_blob, host.data(), blob, hipMemcpyHostToDevice));
+  uint8_t* B = c->cfg_blob;
+  CfgDev d{};
+  d.nodes = (const CfgNode*)B;
+  d.index = (const unsigned long long*)(B + idx_off);
+  d.keys = B + key_off + t->cache_key_prefix_len;
+  d.mask = size - 1;
+  d.n_nodes = n;
+  d.prefix = B + key_off;
+  d.prefix_len = t->cache_key_prefix_len;
+  d.blob = B;
+  d.blob_words = blob / 4 <= CFG_LDS_WORDS ? (uint32_t)(blob / 4) : 0u;
+  d.idx_word = (uint32_t)(idx_off / 4);
+  d.key_word = (uint32_t)(key_off / 4);
+  c->cfg_dev = d;
+  c->cfg_loaded = true;
+  return RL_OK;
+}
+
+int eng_do_limit_requests(Engine* c, const rl_request_batch* in, rl_request_result* out) {
+  if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  // checkServiceErr(snappedConfig != nil, ...) (ratelimit.go:106)
+  if (!c->cfg_loaded) return set_err(c, RL_E_INVALID, "gpu: no rate limit configuration loaded");
+  const uint32_t n = in->n_descriptors, nq = in->n_requests, ne = in->n_entries;
+  if (n > c->cfg.max_batch || nq > c->cfg.max_requests || in->n_rules > c->cfg.max_rules)
+    return set_err(c, RL_E_CAPACITY, "gpu: request batch exceeds configured max_batch/max_requests/max_rules");
+  if (n && !nq) return set_err(c, RL_E_INVALID, "gpu: descriptors without requests");
+  if (!in->domain_off || !in->entry_first || !in->desc_off || (nq && (!in->now || !in->hits)) ||
+      (n && !in->req_idx) || (ne && (!in->key_len || !in->value_len)))
+    return set_err(c, RL_E_INVALID, "gpu: null request batch array");
+  const bool ovr = in->override_flags != nullptr;
+  if (ovr && (!in->override_rpu || !in->override_unit || !in->override_rule))
+    return set_err(c, RL_E_INVALID, "gpu: override_flags without override_rpu/unit/rule");
+  if (in->entry_first[0] != 0 || in->entry_first[n] != ne || in->desc_off[0] != 0 || in->domain_off[0] != 0)
+    return set_err(c, RL_E_INVALID, "gpu: request batch offsets must start at 0 and end at n_entries");
+  const uint64_t dom_bytes = in->domain_off[nq], desc_bytes = in->desc_off[n];
+  if ((dom_bytes && !in->domain_bytes) || (desc_bytes && !in->desc_bytes))
+    return set_err(c, RL_E_INVALID, "gpu: null request byte array");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  // one device buffer, carved (256-B aligned pieces)
+  const size_t scan = n ? match_scan_bytes(n) : 0;
+  size_t need = 0;
+  auto piece = [&need](size_t bytes) {
+    const size_t o = need;
+    need += (std::max<size_t>(bytes, 1) + 255) & ~(size_t)255;
+    return o;
+  };
+  const size_t o_dom = piece(dom_bytes), o_domoff = piece((nq + 1) * 4ull), o_hits = piece(nq * 4ull),
+               o_req = piece(n * 4ull), o_ent = piece((n + 1) * 4ull), o_doff = piece((n + 1) * 4ull),
+               o_desc = piece(desc_bytes), o_kl = piece(ne * 2ull), o_vl = piece(ne * 2ull),
+               o_ovf = piece(ovr ? n : 0), o_ovr = piece(ovr ? n * 4ull : 0), o_ovu = piece(ovr ? n : 0),
+               o_ovrule = piece(ovr ? n * 4ull : 0), o_v = piece(n * 16ull), o_kind = piece(n * 4ull),
+               o_rpu = piece(n * 4ull), o_rule = piece(n * 4ull), o_cnt = piece(16), o_code = piece(n),
+               o_rem = piece(n * 4ull), o_reset = piece(n * 4ull), o_match = piece(n), o_orule = piece(n * 4ull),
+               o_orpu = piece(n * 4ull), o_ounit = piece(n), o_tmp = piece(scan);
+  hipStream_t st = c->stream;
+  HIPCHK(c, after_batches(c, st));
+  if (need > c->mbuf_cap) {
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (c->mbuf) (void)hipFree(c->mbuf);
+    c->mbuf = nullptr;
+    c->mbuf_cap = 0;
+    HIPCHK(c, hipMalloc((void**)&c->mbuf, need));
+    c->mbuf_cap = need;
+  }
+  uint8_t* B = c->mbuf;
+  auto h2d = [&](size_t off, const void* src, size_t bytes) {
+    return bytes ? hipMemcpyAsync(B + off, src, bytes, hipMemcpyHostToDevice, st) : hipSuccess;
+  };
+  HIPCHK(c, h2d(o_dom, in->domain_bytes, dom_bytes));
+  HIPCHK(c, h2d(o_domoff, in->domain_off, (nq + 1) * 4ull));
+  HIPCHK(c, h2d(o_hits, in->hits, nq * 4ull));
+  HIPCHK(c, h2d(o_req, in->req_idx, n * 4ull));
+  HIPCHK(c, h2d(o_ent, in->entry_first, (n + 1) * 4ull));
+  HIPCHK(c, h2d(o_doff, in->desc_off, (n + 1) * 4ull));
+  HIPCHK(c, h2d(o_desc, in->desc_bytes, desc_bytes));
+  HIPCHK(c, h2d(o_kl, in->key_len, ne * 2ull));
+  HIPCHK(c, h2d(o_vl, in->value_len, ne * 2ull));
+  if (ovr) {
+    HIPCHK(c, h2d(o_ovf, in->override_flags, n));
+    HIPCHK(c, h2d(o_ovr, in->override_rpu, n * 4ull));
+    HIPCHK(c, h2d(o_ovu, in->override_unit, n));
+    HIPCHK(c, h2d(o_ovrule, in->override_rule, n * 4ull));
+  }
+  if (nq) HIPCHK(c, hipMemcpyAsync(c->d_now, in->now, nq * 8ull, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemsetAsync(B + o_cnt, 0, 16, st));
+  ReqDev r;
+  r.n_req = nq;
+  r.n_desc = n;
+  r.n_ent = ne;
+  r.dom_total = (uint32_t)dom_bytes;
+  r.desc_total = (uint32_t)desc_bytes;
+  r.dom = B + o_dom;
+  r.dom_off = (const uint32_t*)(B + o_domoff);
+  r.hits = (const uint32_t*)(B + o_hits);
+  r.req = (const uint32_t*)(B + o_req);
+  r.ent_first = (const uint32_t*)(B + o_ent);
+  r.desc_off = (const uint32_t*)(B + o_doff);
+  r.desc = B + o_desc;
+  r.klen = (const uint16_t*)(B + o_kl);
+  r.vlen = (const uint16_t*)(B + o_vl);
+  r.ovf = ovr ? B + o_ovf : nullptr;
+  r.ov_rpu = ovr ? (const uint32_t*)(B + o_ovr) : nullptr;
+  r.ov_unit = ovr ? B + o_ovu : nullptr;
+  r.ov_rule = ovr ? (const uint32_t*)(B + o_ovrule) : nullptr;
+  MatchBuf m{(unsigned long long*)(B + o_v), (uint32_t*)(B + o_kind), (uint32_t*)(B + o_rpu),
+             (uint32_t*)(B + o_rule), (uint32_t*)(B + o_cnt)};
+  // the matched descriptors become an ordinary DoLimit batch in the staging buffers
+  PackOut po{c->d_stem, c->d_off, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule,
+             c->cfg.max_stem_bytes};
+  launch_match(c->cfg_dev, r, m, po, B + o_tmp, scan, st);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->h_match, B + o_cnt, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  if (c->h_match[2] & MATCH_ERR_REQ)
+    return set_err(c, RL_E_INVALID, "gpu: malformed request batch (request index or entry byte layout)");
+  if (c->h_match[2] & MATCH_ERR_CAP)
+    return set_err(c, RL_E_CAPACITY, "gpu: matched stems exceed max_stem_bytes");
+  const uint32_t nm = n ? c->h_match[0] : 0;
+  if (!n) {  // off[0] of the empty batch
+    HIPCHK(c, hipMemsetAsync(c->d_off, 0, 4, st));
+  }
+  rl_batch pb{};
+  pb.n = nm;
+  pb.n_requests = nq;
+  pb.n_rules = in->n_rules;
+  pb.stem_bytes = c->d_stem;
+  pb.stem_off = c->d_off;
+  pb.now = c->d_now;
+  pb.req_idx = c->d_req;
+  pb.unit = c->d_unit;
+  pb.flags = c->d_flags;
+  pb.limit = c->d_limit;
+  pb.hits = c->d_hits;
+  pb.rule_id = c->d_rule;
+  BatchDev b = dev_view(c, &pb, c->cfg.max_stem_bytes);
+  OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats, nullptr};
+  enqueue(c, b, o, 0, st, false);
+  ReqOutDev ro{B + o_code, (uint32_t*)(B + o_rem), (uint32_t*)(B + o_reset), B + o_match,
+               (uint32_t*)(B + o_orule), (uint32_t*)(B + o_orpu), B + o_ounit};
+  launch_match_expand(r, m, c->d_code, c->d_rem, c->d_reset, ro, st);
+  HIPCHK(c, hipGetLastError());
+  auto d2h = [&](void* dst, size_t off, size_t bytes) {
+    return (bytes && dst) ? hipMemcpyAsync(dst, B + off, bytes, hipMemcpyDeviceToHost, st) : hipSuccess;
+  };
+  HIPCHK(c, d2h(out->code, o_code, n));
+  HIPCHK(c, d2h(out->limit_remaining, o_rem, n * 4ull));
+  HIPCHK(c, d2h(out->reset_s, o_reset, n * 4ull));
+  HIPCHK(c, d2h(out->match, o_match, n));
+  HIPCHK(c, d2h(out->rule_id, o_orule, n * 4ull));
+  HIPCHK(c, d2h(out->requests_per_unit, o_orpu, n * 4ull));
+  HIPCHK(c, d2h(out->unit, o_ounit, n));
+  if (in->n_rules && out->stats)
+    HIPCHK(c, hipMemcpyAsync(out->stats, c->d_stats, (size_t)in->n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost, st));
+  c->batches++;
+  c->decisions += nm;
+  return collect(c);
+}
+
+// ---- observability and restart ---------------------------------------------
+
+int eng_local_cache_info_get(Engine* c, int64_t now, rl_local_cache_info* info) {
+  if (!c || !info) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  if (now < 0 || now > (int64_t)NOW_MAX) return set_err(c, RL_E_TIME, "gpu: now out of range");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, after_batches(c, c->stream));
+  unsigned long long* ctr = c->s[0].counters;
+  HIPCHK(c, hipMemsetAsync(ctr + 7, 0, 8, c->stream));
+  launch_lc_count(c->slots, c->nslots, (uint32_t)now, ctr + 7, c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->h_counters, ctr, 64, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  info->entry_count = c->h_counters[7];
+  info->lookup_count = c->h_counters[5];
+  info->hit_count = c->h_counters[6];
+  info->miss_count = c->h_counters[5] - c->h_counters[6];
+  return RL_OK;
+}
+
+namespace {
+constexpr uint64_t SNAP_MAGIC = 0x32304150414e534cull;  // "LSNAPA02" (keyed hash)
+struct SnapHeader {
+  uint64_t magic, nslots, arena_used16, hash_seed;  // slots are placed by the keyed hash: restore adopts its key
+  int64_t time_floor;
+  uint64_t reserved[3];
+};
+static_assert(sizeof(SnapHeader) == 64, "snapshot header");
+
+int snap_state(Engine* c, uint64_t* arena_used16, int64_t* floor) {
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, after_batches(c, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 64, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(floor, c->s[0].time_floor, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *arena_used16 = std::min<uint64_t>(c->h_counters[4], c->arena_cap16);
+  return RL_OK;
+}
+}  // namespace
+
+int eng_snapshot_size(Engine* c, uint64_t* bytes) {
+  if (!c || !bytes) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  uint64_t au = 0;
+  int64_t fl = 0;
+  int rc = snap_state(c, &au, &fl);
+  if (rc) return rc;
+  *bytes = sizeof(SnapHeader) + c->nslots * sizeof(Slot) + au * 16;
+  return RL_OK;
+}
+
+int eng_snapshot_save(Engine* c, void* host, uint64_t bytes) {
+  if (!c || !host) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  SnapHeader h{};
+  int rc = snap_state(c, &h.arena_used16, &h.time_floor);
+  if (rc) return rc;
+  h.magic = SNAP_MAGIC;
+  h.nslots = c->nslots;
+  h.hash_seed = c->hash_seed;
+  const uint64_t need = sizeof(SnapHeader) + c->nslots * sizeof(Slot) + h.arena_used16 * 16;
+  if (bytes < need) return set_err(c, RL_E_CAPACITY, "gpu: snapshot buffer smaller than rl_snapshot_size");
+  uint8_t* p = (uint8_t*)host;
+  memcpy(p, &h, sizeof h);
+  HIPCHK(c, hipMemcpy(p + sizeof h, c->slots, c->nslots * sizeof(Slot), hipMemcpyDeviceToHost));
+  if (h.arena_used16)
+    HIPCHK(c, hipMemcpy(p + sizeof h + c->nslots * sizeof(Slot), c->arena, h.arena_used16 * 16, hipMemcpyDeviceToHost));
+  return RL_OK;
+}
+
+int eng_snapshot_load(Engine* c, const void* host, uint64_t bytes) {
+  if (!c || !host) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  SnapHeader h;
+  if (bytes < sizeof h) return set_err(c, RL_E_INVALID, "gpu: snapshot too short");
+  memcpy(&h, host, sizeof h);
+  if (h.magic != SNAP_MAGIC) return set_err(c, RL_E_INVALID, "gpu: not a table snapshot");
+  if (h.nslots != c->nslots) return set_err(c, RL_E_INVALID, "gpu: snapshot table_slots differ from this ctx");
+  if (h.arena_used16 > c->arena_cap16) return set_err(c, RL_E_INVALID, "gpu: snapshot arena larger than this ctx's");
+  if (bytes < sizeof h + h.nslots * sizeof(Slot) + h.arena_used16 * 16)
+    return set_err(c, RL_E_INVALID, "gpu: snapshot truncated");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, after_batches(c, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint8_t* p = (const uint8_t*)host;
+  HIPCHK(c, hipMemcpy(c->slots, p + sizeof h, c->nslots * sizeof(Slot), hipMemcpyHostToDevice));
+  if (h.arena_used16)
+    HIPCHK(c, hipMemcpy(c->arena, p + sizeof h + c->nslots * sizeof(Slot), h.arena_used16 * 16, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->s[0].counters + 4, &h.arena_used16, 8, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->s[0].time_floor, &h.time_floor, 8, hipMemcpyHostToDevice));
+  c->hash_seed = h.hash_seed;
+  c->cfg.hash_seed = h.hash_seed;
+  c->hk = hash_key_of(h.hash_seed, c->cfg.debug_hash_bits);
+  return RL_OK;
+}
+
+}  // namespace rl
+
+

@@ -184,6 +184,11 @@ struct Scratch {
   uint32_t* route_start;             // [RL_MAX_SHARDS + 1] stem chunk starts per owner
   unsigned long long* route_base;    // [RL_MAX_SHARDS] received stem chunk starts per source
   unsigned long long* route_counts;  // [2 * RL_MAX_SHARDS] records / stem bytes per owner
+  // routed owner batches (eng_route_owner): this buffer's unpacked batch arrays
+  uint32_t *r_off, *r_req, *r_limit, *r_hits, *r_rule;
+  int64_t* r_now;
+  uint8_t *r_unit, *r_flags;
+  unsigned long long* r_base;        // [RL_MAX_SHARDS] received stem chunk starts per source
 };
 
 // The two stages of one batch. Stage A (validate, hash, sort, segment) touches
@@ -208,9 +213,17 @@ void launch_run_sums(const uint32_t* skeys, const uint32_t* w, uint32_t n, const
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
                        uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st);
 void launch_route_unpack(const Wire* rec, uint32_t n, const unsigned long long* base, uint32_t n_shards,
-                         uint64_t stem_bytes, const BatchOut& bo, uint32_t* err, hipStream_t st);
+                         uint64_t stem_bytes, uint32_t rule_stride, const BatchOut& bo, uint32_t* err, hipStream_t st);
+// src_err (optional): without o.status, a returned failure status sets its
+// error bit there (the source's batch then fails at rl_synchronize).
 void launch_route_scatter(const uint32_t* perm, const unsigned long long* ret, uint32_t n, const OutDev& o,
-                          hipStream_t st);
+                          hipStream_t st, uint32_t* src_err = nullptr);
+// Owner side: ret[i] = res[i], or every record failed with the status of
+// *errb when the batch's table stage failed.
+void launch_route_ret(const unsigned long long* res, uint32_t n, const uint32_t* errb, unsigned long long* ret,
+                      hipStream_t st);
+void launch_stats_sum(const unsigned long long* stage, uint32_t n_blocks, uint32_t m, unsigned long long* out,
+                      hipStream_t st);
 void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st);
 void launch_arena_compact(Slot* slots, uint64_t nslots, const uint8_t* from, uint8_t* to, unsigned long long* used16,
                           hipStream_t st);

@@ -2918,10 +2918,12 @@ __global__ __launch_bounds__(256) void k_finish(const unsigned long long* __rest
   bool hit = false;
   if (ok && i < n) {
     const unsigned long long v = res[i];
-    o.code[i] = (uint8_t)res_code(v);
-    o.rem[i] = res_rem(v);
-    o.reset[i] = res_reset(v);
-    if (o.status) o.status[i] = (uint8_t)res_status(v);
+    if (o.code) {  // (routed owner batches keep the packed results only)
+      o.code[i] = (uint8_t)res_code(v);
+      o.rem[i] = res_rem(v);
+      o.reset[i] = res_reset(v);
+      if (o.status) o.status[i] = (uint8_t)res_status(v);
+    }
     hit = res_lc_hit(v);
   }
   if (lc_ctr && ok) {  // freecache LookupCount / HitCount (local_cache_stats.go:36-43)

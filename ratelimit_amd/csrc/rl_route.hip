@@ -35,8 +35,10 @@ __global__ __launch_bounds__(256) void k_route_prep(BatchDev b, uint32_t n_shard
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= b.n) return;
   const uint32_t s0 = b.off[i], s1 = b.off[i + 1], total = b.off[b.n];
-  const uint32_t u = b.unit[i], q = b.req[i];
-  const bool bad = u < 1 || u > 4 || q >= ROUTE_MAX_REQ || (i && b.req[i - 1] > q) || s1 <= s0 ||
+  // Only a malformed layout fails the partition; a bad unit, rule id or clock
+  // is the owner's to judge (per-descriptor status, or the batch's error).
+  const uint32_t q = b.req[i];
+  const bool bad = q >= ROUTE_MAX_REQ || (i && b.req[i - 1] > q) || s1 <= s0 ||
                    s1 - s0 > 65535 || total > b.stem_cap || s1 > total || q >= b.n_req;
   uint64_t h = 0;
   if (bad) {
@@ -109,7 +111,7 @@ __global__ __launch_bounds__(256) void k_route_pack(BatchDev b, const uint32_t* 
 
 __global__ __launch_bounds__(256) void k_route_scatter(const uint32_t* __restrict__ perm,
                                                        const unsigned long long* __restrict__ ret, uint32_t n,
-                                                       OutDev o) {
+                                                       OutDev o, uint32_t* src_err) {
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
   const uint32_t e = perm[j];
@@ -118,16 +120,26 @@ __global__ __launch_bounds__(256) void k_route_scatter(const uint32_t* __restric
   o.rem[e] = res_rem(v);
   o.reset[e] = res_reset(v);
   if (o.status) o.status[e] = (uint8_t)res_status(v);
+  else if (src_err && res_status(v)) atomicOr(src_err, status_err(res_status(v)));
+}
+
+__global__ __launch_bounds__(256) void k_route_ret(const unsigned long long* __restrict__ res, uint32_t n,
+                                                   const uint32_t* errb, unsigned long long* __restrict__ ret) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t e = *errb;
+  ret[i] = e ? pack_fail(err_status(e)) : res[i];
 }
 
 // ---- owner side -----------------------------------------------------------
 // Received records -> batch arrays. Chunks arrive in source-rank order, each
 // with its stems contiguous in record order, so consecutive records' stems
 // must abut (checked: a malformed exchange is RL_E_INVALID, never a wrong key).
+// rule_stride > 0: per-source stats, rule' = source x rule_stride + rule.
 __global__ __launch_bounds__(256) void k_route_unpack(const Wire* __restrict__ rec, uint32_t n,
                                                       const unsigned long long* __restrict__ base,
-                                                      uint32_t n_shards, uint64_t stem_bytes, BatchOut bo,
-                                                      uint32_t* err) {
+                                                      uint32_t n_shards, uint64_t stem_bytes, uint32_t rule_stride,
+                                                      BatchOut bo, uint32_t* err) {
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
   const Wire w = rec[j];
@@ -150,10 +162,26 @@ __global__ __launch_bounds__(256) void k_route_unpack(const Wire* __restrict__ r
   bo.flags[j] = (uint8_t)(w.lu >> 24);
   bo.limit[j] = w.limit;
   bo.hits[j] = w.hits;
-  bo.rule[j] = w.rule;
+  // (a rule id past the stride stays out of range for the owner's validation)
+  bo.rule[j] = !rule_stride ? w.rule : w.rule >= rule_stride ? 0xFFFFFFFFu : (bad ? 0u : src) * rule_stride + w.rule;
+}
+
+// Per-rule stats deltas of several owners (blocks of m counters) summed into out.
+__global__ __launch_bounds__(256) void k_stats_sum(const unsigned long long* __restrict__ stage, uint32_t n_blocks,
+                                                   uint32_t m, unsigned long long* __restrict__ out) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= m) return;
+  unsigned long long s = 0;
+  for (uint32_t b = 0; b < n_blocks; b++) s += stage[(size_t)b * m + i];
+  out[i] = s;
 }
 
 }  // namespace
+
+void launch_stats_sum(const unsigned long long* stage, uint32_t n_blocks, uint32_t m, unsigned long long* out,
+                      hipStream_t st) {
+  if (m) k_stats_sum<<<cdiv(m, 256), 256, 0, st>>>(stage, n_blocks, m, out);
+}
 
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
                        uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st) {
@@ -173,13 +201,18 @@ void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, 
 }
 
 void launch_route_unpack(const Wire* rec, uint32_t n, const unsigned long long* base, uint32_t n_shards,
-                         uint64_t stem_bytes, const BatchOut& bo, uint32_t* err, hipStream_t st) {
-  if (n) k_route_unpack<<<cdiv(n, 256), 256, 0, st>>>(rec, n, base, n_shards, stem_bytes, bo, err);
+                         uint64_t stem_bytes, uint32_t rule_stride, const BatchOut& bo, uint32_t* err, hipStream_t st) {
+  if (n) k_route_unpack<<<cdiv(n, 256), 256, 0, st>>>(rec, n, base, n_shards, stem_bytes, rule_stride, bo, err);
 }
 
 void launch_route_scatter(const uint32_t* perm, const unsigned long long* ret, uint32_t n, const OutDev& o,
-                          hipStream_t st) {
-  if (n) k_route_scatter<<<cdiv(n, 256), 256, 0, st>>>(perm, ret, n, o);
+                          hipStream_t st, uint32_t* src_err) {
+  if (n) k_route_scatter<<<cdiv(n, 256), 256, 0, st>>>(perm, ret, n, o, src_err);
+}
+
+void launch_route_ret(const unsigned long long* res, uint32_t n, const uint32_t* errb, unsigned long long* ret,
+                      hipStream_t st) {
+  if (n) k_route_ret<<<cdiv(n, 256), 256, 0, st>>>(res, n, errb, ret);
 }
 
 }  // namespace rl

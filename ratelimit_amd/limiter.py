@@ -48,7 +48,7 @@ class FixedTimeSource(TimeSource):
 
 
 def _config(near_limit_ratio, local_cache, per_second, jitter, table_slots, max_batch, max_rules, device,
-            arena_bytes, max_stem_bytes, hash_seed=0, debug_hash_bits=0):
+            arena_bytes, max_stem_bytes, hash_seed=0, debug_hash_bits=0, n_shards=1, shard_devices=None):
     cfg = abi.RlConfig()
     cfg.table_slots = table_slots
     cfg.arena_bytes = arena_bytes
@@ -63,6 +63,12 @@ def _config(near_limit_ratio, local_cache, per_second, jitter, table_slots, max_
     cfg.expiration_jitter_max_seconds = jitter
     cfg.hash_seed = hash_seed
     cfg.debug_hash_bits = debug_hash_bits
+    cfg.n_shards = n_shards
+    devs = list(shard_devices) if shard_devices is not None else [device] * n_shards
+    if len(devs) != n_shards or n_shards > 16:
+        raise ValueError("shard_devices must name n_shards (<= 16) devices")
+    for j, d in enumerate(devs):
+        cfg.shard_device[j] = d
     return cfg
 
 
@@ -71,11 +77,13 @@ class Backend:
 
     def __init__(self, near_limit_ratio=0.8, local_cache=False, per_second=False, jitter=0,
                  table_slots=1 << 20, max_batch=1 << 16, max_rules=1 << 12, device=0, arena_bytes=0,
-                 max_stem_bytes=0, hash_seed=0, debug_hash_bits=0):
+                 max_stem_bytes=0, hash_seed=0, debug_hash_bits=0, n_shards=1, shard_devices=None):
+        """n_shards > 1: one ctx hash-shards its table over shard_devices (default:
+        all on `device`) and routes every batch between them (rl_config.n_shards)."""
         L = lib()
         err = C.create_string_buffer(512)
         self.cfg = _config(near_limit_ratio, local_cache, per_second, jitter, table_slots, max_batch, max_rules,
-                           device, arena_bytes, max_stem_bytes, hash_seed, debug_hash_bits)
+                           device, arena_bytes, max_stem_bytes, hash_seed, debug_hash_bits, n_shards, shard_devices)
         self.ctx = L.rl_create(C.byref(self.cfg), err, 512)
         if not self.ctx:
             raise RedisError(err.value.decode())
@@ -183,9 +191,13 @@ class Backend:
         check(self.ctx, lib().rl_sweep(self.ctx, now, C.byref(ev)))
         return ev.value
 
-    def table_info(self) -> dict:
+    def table_info(self, shard=None) -> dict:
+        """Table counters summed over shards (or of one shard)."""
         info = abi.RlTableInfo()
-        check(self.ctx, lib().rl_table_info_get(self.ctx, C.byref(info)))
+        if shard is None:
+            check(self.ctx, lib().rl_table_info_get(self.ctx, C.byref(info)))
+        else:
+            check(self.ctx, lib().rl_table_info_shard(self.ctx, shard, C.byref(info)))
         return {f: getattr(info, f) for f, _ in abi.RlTableInfo._fields_}
 
     def local_cache_info(self, now: int) -> dict:

@@ -29,7 +29,7 @@ class CpuRouteOps:
     def __init__(self, ratio=0.8, local_cache=False, per_second=False):
         self.oracle = COracle(ratio, local_cache, per_second)
 
-    def pack(self, dev_in, n, n_requests, n_rules, world, rank, send_rec, send_stem, perm):
+    def pack(self, dev_in, n, n_requests, n_rules, world, rank, send_rec, send_stem, perm, counts_out):
         a = {k: v.numpy().view(abi.BATCH_DTYPES[k]) for k, v in dev_in.items()}
         if n and (a["unit"][:n].min() < 1 or a["unit"][:n].max() > 4):
             raise RedisError("gpu: malformed batch [RL_E_INVALID]")
@@ -55,9 +55,10 @@ class CpuRouteOps:
         if blob:
             send_stem[:len(blob)].copy_(torch.from_numpy(np.frombuffer(bytes(blob), np.uint8).copy()))
         perm[:n].copy_(torch.from_numpy(order.astype(np.int32)))
-        return counts
+        counts_out.copy_(torch.from_numpy(counts.reshape(-1).astype(np.int64)))
 
-    def owner(self, n, recv_rec, recv_stem, stem_bytes, src_base, world, n_rules, ret, stats):
+    def owner(self, n, recv_rec, recv_stem, stem_bytes, src_base, world, n_rules, ret, stats, isolate, slot):
+        assert not isolate, "per-descriptor statuses: GPU tests only"
         rec = recv_rec[:n * 32].numpy().view(WIRE)
         blob = recv_stem[:stem_bytes].numpy()
         src = rec["label"] >> 24
@@ -71,12 +72,14 @@ class CpuRouteOps:
                   "now": rec["now"][first].copy() if n else np.zeros(1, np.int64),
                   "req_idx": req.astype(np.uint32), "unit": ((rec["lu"] >> 16) & 0xFF).astype(np.uint8),
                   "flags": (rec["lu"] >> 24).astype(np.uint8), "limit": rec["limit"].copy(),
-                  "hits": rec["hits"].copy(), "rule_id": rec["rule"].copy()}
-        out = self.oracle.do_limit(arrays, n, labels.size, n_rules)
+                  "hits": rec["hits"].copy(),
+                # per-source stats (rule_stride = n_rules): rule' = source x n_rules + rule
+                "rule_id": (src * n_rules + rec["rule"]).astype(np.uint32)}
+        out = self.oracle.do_limit(arrays, n, labels.size, world * n_rules)
         packed = (out["limit_remaining"].astype(np.uint64) | (out["reset_s"].astype(np.uint64) << np.uint64(32)) |
                   (out["code"].astype(np.uint64) << np.uint64(56)))
         ret[:n].copy_(torch.from_numpy(packed.view(np.int64)))
-        stats[:n_rules * 6].copy_(torch.from_numpy(out["stats"].view(np.int64)))
+        stats[:world * n_rules * 6].copy_(torch.from_numpy(out["stats"][:world * n_rules * 6].view(np.int64)))
 
     def scatter(self, n, perm, back, dev_out):
         p = perm[:n].numpy().astype(np.int64)

@@ -3,7 +3,7 @@
 World sizes 2 and 3 run ShardedRateLimitCache with the CPU stand-in ops
 (tests/route_cpu.py: numpy packing + the C oracle as each owner's table). The
 per-descriptor results of every rank's slice, concatenated in rank order, and
-the node-wide stats must equal one sequential oracle over the whole batch
+the sum of the ranks' per-source stats must equal one sequential oracle over the whole batch
 sequence: the routing preserves the global arrival order per key.
 """
 import os
@@ -48,7 +48,7 @@ def _split_points(nq, world, k):
     return cuts
 
 
-def _worker(rank, world, port, batches, cfg, q, poison_rank=-1):
+def _worker(rank, world, port, batches, cfg, q, poison_rank=-1, pipelined=False):
     sys.path.insert(0, HERE)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
@@ -59,9 +59,11 @@ def _worker(rank, world, port, batches, cfg, q, poison_rank=-1):
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         ops = CpuRouteOps(*cfg)
+        rx = Exchange(dist.new_group(backend="gloo")) if pipelined else None
         sc = ShardedRateLimitCache(ops, Exchange(), max_batch=4096, max_stem_bytes=1 << 18,
-                                   device=torch.device("cpu"))
+                                   device=torch.device("cpu"), ret_exchange=rx)
         res = []
+        pending = []
         for k, (arrays, n, nq, n_rules) in enumerate(batches):
             cuts = _split_points(nq, world, k)
             sub, sn, snq = slice_requests(arrays, n, nq, cuts[rank], cuts[rank + 1])
@@ -73,6 +75,9 @@ def _worker(rank, world, port, batches, cfg, q, poison_rank=-1):
             dev_out = {"code": torch.zeros(max(sn, 1), dtype=torch.uint8),
                        "limit_remaining": torch.zeros(max(sn, 1), dtype=torch.int32),
                        "reset_s": torch.zeros(max(sn, 1), dtype=torch.int32)}
+            if pipelined:  # submit everything, one finish at the end
+                pending.append((sn, dev_out, sc.submit(dev_in, sn, snq, n_rules, dev_out)))
+                continue
             try:
                 stats = sc.do_limit(dev_in, sn, snq, n_rules, dev_out)
             except RedisError as e:
@@ -82,6 +87,13 @@ def _worker(rank, world, port, batches, cfg, q, poison_rank=-1):
                         dev_out["limit_remaining"][:sn].numpy().view(np.uint32).copy(),
                         dev_out["reset_s"][:sn].numpy().view(np.uint32).copy(),
                         stats.numpy().view(np.uint64).copy()))
+        if pipelined:
+            sc.finish()
+            for sn, dev_out, stats in pending:
+                res.append((dev_out["code"][:sn].numpy().copy(),
+                            dev_out["limit_remaining"][:sn].numpy().view(np.uint32).copy(),
+                            dev_out["reset_s"][:sn].numpy().view(np.uint32).copy(),
+                            stats.numpy().view(np.uint64).copy()))
         q.put((rank, res, None))
         dist.destroy_process_group()
     except Exception as e:  # report instead of hanging the parent
@@ -89,12 +101,12 @@ def _worker(rank, world, port, batches, cfg, q, poison_rank=-1):
         q.put((rank, None, traceback.format_exc()))
 
 
-def _run(world, batches, cfg, poison_rank=-1):
+def _run(world, batches, cfg, poison_rank=-1, pipelined=False):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, batches, cfg, q, poison_rank)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, batches, cfg, q, poison_rank, pipelined)) for r in range(world)]
     for p in ps:
         p.start()
     out = {}
@@ -107,12 +119,12 @@ def _run(world, batches, cfg, poison_rank=-1):
     return out
 
 
-@pytest.mark.parametrize("world,seed,local_cache,per_second", [(2, 1, False, False), (2, 2, True, False),
-                                                                (3, 3, True, True)])
-def test_sharded_exchange_matches_sequential_oracle(world, seed, local_cache, per_second):
+@pytest.mark.parametrize("world,seed,local_cache,per_second,pipelined", [
+    (2, 1, False, False, False), (2, 2, True, False, False), (3, 3, True, True, False), (3, 4, True, False, True)])
+def test_sharded_exchange_matches_sequential_oracle(world, seed, local_cache, per_second, pipelined):
     cfg = (0.8, local_cache, per_second)
     batches = _batches(seed, local_cache=local_cache)
-    out = _run(world, batches, cfg)
+    out = _run(world, batches, cfg, pipelined=pipelined)
     co = COracle(*cfg)
     for k, (arrays, n, nq, n_rules) in enumerate(batches):
         exp = co.do_limit(arrays, n, nq, n_rules)
@@ -122,8 +134,9 @@ def test_sharded_exchange_matches_sequential_oracle(world, seed, local_cache, pe
         assert np.array_equal(got_code, exp["code"]), k
         assert np.array_equal(got_rem, exp["limit_remaining"]), k
         assert np.array_equal(got_reset, exp["reset_s"]), k
-        for r in range(world):  # node-wide stats on every rank
-            assert np.array_equal(out[r][k][3], exp["stats"][:n_rules * abi.RL_NUM_STATS]), (k, r)
+        # per-source stats: each rank counts its own requests; the sum is the node's
+        tot = sum(out[r][k][3].astype(np.uint64) for r in range(world))
+        assert np.array_equal(tot, exp["stats"][:n_rules * abi.RL_NUM_STATS]), k
 
 
 def test_sharded_error_on_one_rank_fails_the_batch_everywhere():
