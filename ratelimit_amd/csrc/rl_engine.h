@@ -57,7 +57,6 @@ struct Engine {
   unsigned long long* d_stats = nullptr;
   uint32_t* h_err = nullptr;  // pinned [4]
   unsigned long long* h_counters = nullptr;
-  unsigned long long* h_route = nullptr;  // pinned route counts
   std::string last_error;
   uint64_t batches = 0, decisions = 0;
   // rl_profile: a ring of per-batch event sets (stage boundaries, recorded on

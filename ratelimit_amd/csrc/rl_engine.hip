@@ -158,7 +158,7 @@ int check_sizes(Engine* c, const rl_batch* in, uint64_t stem_bytes) {
 }
 
 BatchDev dev_view(const Engine* c, const rl_batch* in, uint32_t stem_cap) {
-  BatchDev b;
+  BatchDev b{};
   b.hk = c->hk;
   b.n = in->n;
   b.n_req = in->n_requests;
@@ -201,43 +201,35 @@ Params params(Engine* c, int isolate) {
 
 // Per-batch scratch of one pipeline buffer (sized for max_batch descriptors).
 bool alloc_buffer(Scratch& s, uint32_t n) {
-  const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
-  const size_t nt = (n + SEG_TILE - 1) / SEG_TILE + 1;
   const size_t items = (size_t)n / (64 * 4 * 8) + 1 + PART_DIGITS;  // BIG_CHUNK-position work items
   bool ok = dalloc(&s.big_meta, PART_DIGITS) == hipSuccess && dalloc(&s.big_n, 1) == hipSuccess &&
             dalloc(&s.big_work, items) == hipSuccess && dalloc(&s.work_n, 1) == hipSuccess &&
             dalloc(&s.big_cnt, items * (1 + 2 * BIG_HEAVY)) == hipSuccess;
   ok = ok && dalloc(&s.rec, n) == hipSuccess && dalloc(&s.res, n) == hipSuccess;
   for (int i = 0; i < 2; i++) ok = ok && dalloc(&s.keys[i], n) == hipSuccess && dalloc(&s.vals[i], n) == hipSuccess;
-  ok = ok && dalloc(&s.hist, 256ull * std::max(ntiles, 1u)) == hipSuccess && dalloc(&s.hist_tot, 256) == hipSuccess;
   ok = ok && dalloc(&s.grp, n) == hipSuccess && dalloc(&s.lead, n) == hipSuccess && dalloc(&s.gmask, n) == hipSuccess &&
        dalloc(&s.defer, n) == hipSuccess &&
        dalloc(&s.defer_n, 1) == hipSuccess && dalloc(&s.defer2, n) == hipSuccess &&
        dalloc(&s.defer1, n) == hipSuccess && dalloc(&s.defer1_n, 1) == hipSuccess &&
        dalloc(&s.defer2_n, 1) == hipSuccess && dalloc(&s.fast_blk, (size_t)n / (256 * 32) + 1) == hipSuccess;
-  ok = ok && dalloc(&s.tile_f, nt) == hipSuccess && dalloc(&s.tile_s, nt) == hipSuccess &&
-       dalloc(&s.tile_h, nt) == hipSuccess;
   ok = ok && dalloc(&s.hits_s, n) == hipSuccess && dalloc(&s.segsum, n) == hipSuccess &&
        dalloc(&s.rid, n) == hipSuccess && dalloc(&s.run_start, (size_t)n + 1) == hipSuccess &&
        dalloc(&s.run_flags, n) == hipSuccess && dalloc(&s.run_state, n) == hipSuccess &&
-       dalloc(&s.run_f, n) == hipSuccess && dalloc(&s.num_runs, 1) == hipSuccess &&
+       dalloc(&s.run_f, n) == hipSuccess &&
        dalloc(&s.runs64, 1) == hipSuccess && dalloc(&s.drun, (size_t)n / 2 + BIG_HEAVY * PART_DIGITS) == hipSuccess;
   ok = ok && dalloc(&s.hit_a, n) == hipSuccess && dalloc(&s.tile, n) == hipSuccess &&
        dalloc(&s.hit_t, n) == hipSuccess;
   ok = ok && dalloc(&s.run_end, n) == hipSuccess &&
        dalloc(&s.part_info, (size_t)PART_DIGITS * std::max((n + PART_TILE - 1) / PART_TILE, 1u)) == hipSuccess;
-  ok = ok && dalloc(&s.r_off, (size_t)n + 1) == hipSuccess && dalloc(&s.r_req, n) == hipSuccess &&
-       dalloc(&s.r_limit, n) == hipSuccess && dalloc(&s.r_hits, n) == hipSuccess && dalloc(&s.r_rule, n) == hipSuccess &&
-       dalloc(&s.r_now, n) == hipSuccess && dalloc(&s.r_unit, n) == hipSuccess && dalloc(&s.r_flags, n) == hipSuccess &&
-       dalloc(&s.r_base, RL_MAX_SHARDS) == hipSuccess;
+  ok = ok && dalloc(&s.r_base, RL_MAX_SHARDS) == hipSuccess;
   return ok;
 }
 
 void free_buffer(Scratch& s) {
-  void* bufs[] = {s.rec, s.res, s.big_meta, s.big_n, s.big_work, s.work_n, s.big_cnt, s.keys[0], s.keys[1], s.vals[0], s.vals[1], s.hist,
-                  s.hist_tot, s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1, s.defer1_n, s.fast_blk, s.tile_f, s.tile_s, s.tile_h, s.hits_s, s.segsum, s.rid,
-                  s.run_start, s.run_flags, s.run_state, s.run_f, s.num_runs, s.runs64, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t,
-                  s.r_off, s.r_req, s.r_limit, s.r_hits, s.r_rule, s.r_now, s.r_unit, s.r_flags, s.r_base};
+  void* bufs[] = {s.rec, s.res, s.big_meta, s.big_n, s.big_work, s.work_n, s.big_cnt, s.keys[0], s.keys[1],
+                  s.vals[0], s.vals[1], s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1,
+                  s.defer1_n, s.fast_blk, s.hits_s, s.segsum, s.rid, s.run_start, s.run_flags, s.run_state, s.run_f,
+                  s.runs64, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t, s.r_base};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
 }
@@ -333,8 +325,6 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && dalloc(&s0.stripes, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS) == hipSuccess;
   ok = ok && dalloc(&s0.time_floor, 1) == hipSuccess;
   ok = ok && dalloc(&s0.counters, 8) == hipSuccess;
-  ok = ok && dalloc(&s0.route_start, RL_MAX_SHARDS + 1) == hipSuccess &&
-       dalloc(&s0.route_base, RL_MAX_SHARDS) == hipSuccess && dalloc(&s0.route_counts, 2 * RL_MAX_SHARDS) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++) {  // shared members
     Scratch& sk = c->s[k];
     sk.err = c->errw ? c->errw + k : nullptr;
@@ -343,11 +333,7 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
     sk.stripes = s0.stripes;
     sk.time_floor = s0.time_floor;
     sk.counters = s0.counters;
-    sk.route_start = s0.route_start;
-    sk.route_base = s0.route_base;
-    sk.route_counts = s0.route_counts;
   }
-  ok = ok && hipHostMalloc((void**)&c->h_route, 2 * RL_MAX_SHARDS * sizeof(unsigned long long)) == hipSuccess;
   ok = ok && dalloc(&c->d_stem, (size_t)cfg.max_stem_bytes + 64) == hipSuccess;
   ok = ok && dalloc(&c->d_off, (size_t)n + 1) == hipSuccess;
   ok = ok && dalloc(&c->d_now, cfg.max_requests) == hipSuccess;
@@ -402,12 +388,11 @@ void eng_destroy(Engine* c) {
   void* bufs[] = {c->slots, c->arena, c->arena2, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
                   c->d_now, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_status,
                   c->d_rem,
-                  c->d_reset, c->d_stats, s0.route_start, s0.route_base, s0.route_counts};
+                  c->d_reset, c->d_stats};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
-  if (c->h_route) (void)hipHostFree(c->h_route);
   for (void* p : {(void*)c->cfg_blob, (void*)c->mbuf})
     if (p) (void)hipFree(p);
   if (c->h_match) (void)hipHostFree(c->h_match);
@@ -438,15 +423,16 @@ int eng_do_limit_async(Engine* c, const rl_batch* in, rl_result* out, void* stre
 bool scratch_alloc(Scratch& s, uint32_t n) {
   s = Scratch{};
   bool ok = alloc_buffer(s, n);
-  ok = ok && dalloc(&s.err, 1) == hipSuccess && dalloc(&s.route_start, RL_MAX_SHARDS + 1) == hipSuccess &&
-       dalloc(&s.route_base, RL_MAX_SHARDS) == hipSuccess && dalloc(&s.route_counts, 2 * RL_MAX_SHARDS) == hipSuccess;
+  ok = ok && dalloc(&s.err, 1) == hipSuccess && dalloc(&s.route_start, 2 * RL_MAX_SHARDS + 1) == hipSuccess &&
+       dalloc(&s.route_dest, n) == hipSuccess &&
+       dalloc(&s.route_hist, 2ull * RL_MAX_SHARDS * ((n + ROUTE_TILE - 1) / ROUTE_TILE)) == hipSuccess;
   ok = ok && hipMemset(s.err, 0, 4) == hipSuccess;
   return ok;
 }
 
 void scratch_free(Scratch& s) {
   free_buffer(s);
-  for (void* p : {(void*)s.err, (void*)s.route_start, (void*)s.route_base, (void*)s.route_counts})
+  for (void* p : {(void*)s.err, (void*)s.route_start, (void*)s.route_dest, (void*)s.route_hist})
     if (p) (void)hipFree(p);
   s = Scratch{};
 }
@@ -506,11 +492,9 @@ int eng_route_owner(Engine* c, uint32_t n, const Wire* recv_rec, const uint8_t* 
   HIPCHK(c, hipEventSynchronize(c->b_done[k]));  // (the pinned bases of buffer k's previous batch were read)
   for (uint32_t j = 0; j < n_src; j++) hb[j] = src_stem_base[j];
   HIPCHK(c, hipMemcpyAsync(sk.r_base, hb, (size_t)n_src * 8, hipMemcpyHostToDevice, a));
-  BatchOut bo{sk.r_off, sk.r_now, sk.r_req, sk.r_unit, sk.r_flags, sk.r_limit, sk.r_hits, sk.r_rule};
-  // a malformed exchange poisons this batch's validation word (fails the batch)
-  launch_route_unpack(recv_rec, n, sk.r_base, n_src, recv_stem_bytes, rule_stride, bo, sk.err, a);
-  if (!n) HIPCHK(c, hipMemsetAsync(sk.r_off, 0, sizeof(uint32_t), a));
-  BatchDev b;
+  // k_prepare reads the wire records in place (a malformed exchange fails
+  // the batch's validation word)
+  BatchDev b{};
   b.hk = c->hk;
   b.n = n;
   b.n_req = n;
@@ -519,14 +503,10 @@ int eng_route_owner(Engine* c, uint32_t n, const Wire* recv_rec, const uint8_t* 
   b.stem_total = (uint32_t)recv_stem_bytes;
   b.now_desc = 1;
   b.stem = recv_stem;
-  b.off = sk.r_off;
-  b.now = sk.r_now;
-  b.req = sk.r_req;
-  b.unit = sk.r_unit;
-  b.flags = sk.r_flags;
-  b.limit = sk.r_limit;
-  b.hits = sk.r_hits;
-  b.rule = sk.r_rule;
+  b.wire = recv_rec;
+  b.wbase = sk.r_base;
+  b.n_src = n_src;
+  b.rule_stride = rule_stride;
   OutDev o{nullptr, nullptr, nullptr, stats, isolate ? c->d_status : nullptr};
   const uint32_t kk = enqueue(c, b, o, 0, nullptr, true);
   HIPCHK(c, hipGetLastError());
@@ -601,7 +581,7 @@ int eng_synchronize(Engine* c) {
 int eng_do_limit(Engine* c, const rl_batch* in, rl_result* out) {
   if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  BatchDev b;
+  BatchDev b{};
   int rc = stage(c, in, &b);
   if (rc) return rc;
   hipStream_t st = c->stream;
@@ -651,7 +631,7 @@ int eng_restore(Engine* c, const rl_restore_batch* r) {
   in.limit = zero;
   in.hits = r->count;
   in.rule_id = zero;
-  BatchDev b;
+  BatchDev b{};
   int rc = stage(c, &in, &b);
   if (!rc) {
     OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats, nullptr};
@@ -715,7 +695,7 @@ int eng_table_info_get(Engine* c, rl_table_info* info) {
 int eng_debug_keys(Engine* c, const rl_batch* in, uint8_t* out_bytes, uint32_t* out_off, uint32_t out_cap) {
   if (!c || !in || !out_off) return set_err(c, RL_E_INVALID, "gpu: null argument");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  BatchDev b;
+  BatchDev b{};
   int rc = stage(c, in, &b);
   if (rc) return rc;
   const uint32_t n = in->n;

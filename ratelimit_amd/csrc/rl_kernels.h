@@ -9,13 +9,6 @@
 
 namespace rl {
 
-constexpr uint32_t RS_ITEMS = 16;  // routing partition (k_rs_*): 256 threads x RS_ITEMS
-constexpr uint32_t RS_TILE = 256 * RS_ITEMS;
-#ifndef RL_SEG_ITEMS
-#define RL_SEG_ITEMS 16
-#endif
-constexpr uint32_t SEG_ITEMS = RL_SEG_ITEMS;  // 64-position chunks per wave (4 waves per tile)
-constexpr uint32_t SEG_TILE = 256 * SEG_ITEMS;
 constexpr uint32_t PART_ITEMS = 16, PART_TILE = 256 * PART_ITEMS;  // k_part: 256 threads x PART_ITEMS
 constexpr uint32_t PART_BITS = 10, PART_DIGITS = 1u << PART_BITS;   // buckets = top key bits
 constexpr uint32_t BIG_BLOCKS = 64;                                 // k_bucket_big workgroups
@@ -39,6 +32,7 @@ constexpr uint32_t STAT_LDS_RULES = 512;  // rules aggregated in LDS (== LDS_RUL
 constexpr uint32_t RUNS_GENERAL_BLOCKS = RL_RG_BLOCKS;  // k_runs_general grids (grid-stride over deferrals):
 constexpr uint32_t RUNS_GENERAL_LATE_BLOCKS = 8;  //   RUN_MULTI runs beside k_runs / k_runs' deferrals after it
 
+struct Wire;
 struct BatchDev {
   uint32_t n, n_req, n_rules, stem_cap;
   uint32_t stem_total;  // bytes of packed stems (off[n]); reads stay below it
@@ -53,6 +47,12 @@ struct BatchDev {
   const uint32_t* limit;
   const uint32_t* hits;
   const uint32_t* rule;
+  // routed owner batch (eng_route_owner): the received wire records replace
+  // the arrays above (off, now, req, unit, flags, limit, hits, rule = null);
+  // the stem of record j starts at wbase[source] + wire[j].off
+  const Wire* wire;
+  const unsigned long long* wbase;  // [n_src] chunk offset of each source in stem
+  uint32_t n_src, rule_stride;
 };
 
 // One descriptor, packed by k_prepare (arrival order) and gathered once into
@@ -86,6 +86,7 @@ __host__ __device__ inline uint32_t rec_flags(const Rec& r) { return r.lu >> 24;
 // Multi-GPU routing wire record (rl_route.hip): one per routed descriptor.
 constexpr uint32_t ROUTE_REQ_BITS = 24;  // label = source rank << 24 | request index
 constexpr uint32_t ROUTE_MAX_REQ = 1u << ROUTE_REQ_BITS;
+constexpr uint32_t ROUTE_TILE = 512;  // descriptors per partition tile (rl_route.hip RP_TILE)
 struct __attribute__((aligned(8))) Wire {
   uint32_t label;  // global request label (non-decreasing in global arrival order)
   uint32_t off;    // stem byte offset inside the owner's chunk of this source
@@ -96,18 +97,6 @@ struct __attribute__((aligned(8))) Wire {
   int64_t now;
 };
 static_assert(sizeof(Wire) == RL_WIRE_BYTES, "wire record size is part of the ABI");
-
-// Batch arrays written by the owner-side unpack.
-struct BatchOut {
-  uint32_t* off;
-  int64_t* now;
-  uint32_t* req;
-  uint8_t* unit;
-  uint8_t* flags;
-  uint32_t* limit;
-  uint32_t* hits;
-  uint32_t* rule;
-};
 
 struct OutDev {
   uint8_t* code;
@@ -140,8 +129,6 @@ struct Scratch {
   unsigned long long* res;   // [n] packed result per descriptor (arrival order)
   uint32_t* keys[2];
   uint32_t* vals[2];
-  uint32_t* hist;      // 256 x ntiles, digit-major (routing partition)
-  uint32_t* hist_tot;  // 256 digit totals
   BigMeta* big_meta;                 // [PART_DIGITS] buckets queued for the large-bucket kernels
   uint32_t* big_n;
   uint32_t* big_work;                // [n / BIG_CHUNK + PART_DIGITS] chunk work items (bucket << 16 | chunk)
@@ -159,7 +146,6 @@ struct Scratch {
   uint32_t* fast_blk;             // bit per 256-descriptor block holding a RUN_FAST run (k_runs -> k_fast_emit)
   unsigned long long* stripes;    // STAT_STRIPES x STAT_LDS_RULES x RL_NUM_STATS
   // run segmentation (sorted order)
-  uint32_t *tile_f, *tile_s, *tile_h;  // per SEG_TILE tile
   uint32_t* hits_s;                    // [n] raw hits, sorted order
   uint32_t* hit_a;                     // [n] raw hits, arrival order (k_prepare)
   uint4* tile;                         // [n] k_part tile layout: {sort key, index, hits, 0}
@@ -172,7 +158,6 @@ struct Scratch {
   uint32_t* run_flags;                 // [n] RUN_*
   uint4* run_state;                    // [n] {slot, c0, old lc, F | which<<1}
   uint32_t* run_f;                     // [n] first over-limit position
-  uint32_t* num_runs;                  // routing partition (launch_run_sums)
   unsigned long long* runs64;          // bucket path: runs | runs of two or more << 32
   uint32_t* drun;                      // [n/2 + BIG_HEAVY x PART_DIGITS] ids of the runs of two or more
   uint32_t* err;   // validation word of this buffer's batch (stage A)
@@ -181,13 +166,10 @@ struct Scratch {
   int64_t* time_floor;  // requests earlier than the last sweep are rejected
   unsigned long long* counters;  // [0..3] sweep / info outputs
   // multi-GPU routing
-  uint32_t* route_start;             // [RL_MAX_SHARDS + 1] stem chunk starts per owner
-  unsigned long long* route_base;    // [RL_MAX_SHARDS] received stem chunk starts per source
-  unsigned long long* route_counts;  // [2 * RL_MAX_SHARDS] records / stem bytes per owner
-  // routed owner batches (eng_route_owner): this buffer's unpacked batch arrays
-  uint32_t *r_off, *r_req, *r_limit, *r_hits, *r_rule;
-  int64_t* r_now;
-  uint8_t *r_unit, *r_flags;
+  uint32_t* route_start;             // [2 x RL_MAX_SHARDS + 1] records / stem bytes per owner (partition)
+  uint8_t* route_dest;               // [n] owner of each descriptor (routing scratch only)
+  uint32_t* route_hist;              // [2 x RL_MAX_SHARDS x tiles] per-tile counts (routing scratch only)
+  // routed owner batches (eng_route_owner)
   unsigned long long* r_base;        // [RL_MAX_SHARDS] received stem chunk starts per source
 };
 
@@ -204,16 +186,8 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
 // ev (optional, RL_NUM_STAGES + 1 events on stream st): recorded before
 // k_prepare, after it, after the sort, just before and just after k_runs, and
 // at the end (per-stage timing, rl_profile).
-// One stable 8-bit counting pass on key bits [0, 8) (s.hist / s.hist_tot hold
-// the per-digit counts afterwards).
-void launch_partition(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, uint32_t n,
-                      const Scratch& s, hipStream_t st);
-// s.segsum[q] = inclusive sum of max(1, w) over the run of equal skeys holding q.
-void launch_run_sums(const uint32_t* skeys, const uint32_t* w, uint32_t n, const Scratch& s, hipStream_t st);
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
                        uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st);
-void launch_route_unpack(const Wire* rec, uint32_t n, const unsigned long long* base, uint32_t n_shards,
-                         uint64_t stem_bytes, uint32_t rule_stride, const BatchOut& bo, uint32_t* err, hipStream_t st);
 // src_err (optional): without o.status, a returned failure status sets its
 // error bit there (the source's batch then fails at rl_synchronize).
 void launch_route_scatter(const uint32_t* perm, const unsigned long long* ret, uint32_t n, const OutDev& o,

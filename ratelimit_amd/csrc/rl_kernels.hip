@@ -60,24 +60,68 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   const int64_t floor = *time_floor;
   auto time_bad = [&](int64_t t) { return t < 0 || t > (int64_t)NOW_MAX || t < floor; };
 
+  // ---- the descriptor: packed arrays, or (routed owner batch) its wire
+  // record, whose stem sits at its source's chunk base + off; chunks arrive in
+  // source order, so consecutive records' stems must abut (a malformed
+  // exchange fails the batch, never a wrong key). rule_stride > 0 attributes
+  // stats per source (rule' = source x rule_stride + rule).
+  uint32_t s0 = 0, s1 = 0, u = 0, q = 0, fl = 0, rule = 0, hits = 0, limit = 0, dstat = 0, len = 0;
+  int64_t tnow = 0;
+  bool layout_bad = false;
+  if (i < b.n) {
+    if (b.wire) {
+      const Wire w = b.wire[i];
+      const uint32_t src = w.label >> ROUTE_REQ_BITS;
+      const uint32_t wl = w.lu & 0xFFFFu;
+      layout_bad = src >= b.n_src;
+      s0 = (uint32_t)((layout_bad ? 0ull : b.wbase[src]) + w.off);
+      s1 = s0 + wl;
+      if (i + 1 < b.n) {
+        const Wire x = b.wire[i + 1];
+        const uint32_t s2 = x.label >> ROUTE_REQ_BITS;
+        layout_bad = layout_bad || s2 >= b.n_src || b.wbase[s2] + x.off != (unsigned long long)s1 || x.label < w.label;
+      }
+      layout_bad = layout_bad || s1 > b.stem_total;
+      u = (w.lu >> 16) & 0xFFu;
+      fl = w.lu >> 24;
+      q = w.label;
+      tnow = w.now;
+      rule = !b.rule_stride ? w.rule : w.rule >= b.rule_stride ? 0xFFFFFFFFu : src * b.rule_stride + w.rule;
+      hits = w.hits;
+      limit = w.limit;
+    } else {
+      s0 = b.off[i];
+      s1 = b.off[i + 1];
+      u = b.unit[i];
+      q = b.req[i];
+      fl = b.flags[i];
+      rule = b.rule[i];
+      hits = b.hits[i];
+      limit = b.limit[i];
+      layout_bad = (!b.now_desc && q >= b.n_req) || (i && b.req[i - 1] > q);
+      tnow = b.now_desc ? b.now[i] : (q < b.n_req ? b.now[q] : 0);
+    }
+    layout_bad = layout_bad || s1 < s0 || s1 > b.stem_cap;
+  }
   // ---- per-request clock checks (whole-batch mode): now in [0, NOW_MAX], not before the last sweep
-  if (!isolate && i < (b.now_desc ? b.n : b.n_req) && time_bad(b.now[i])) bad |= ERR_TIME;
+  if (!isolate) {
+    if (b.wire) {
+      if (i < b.n && time_bad(tnow)) bad |= ERR_TIME;
+    } else if (i < (b.now_desc ? b.n : b.n_req) && time_bad(b.now[i])) {
+      bad |= ERR_TIME;
+    }
+  }
 
   // ---- per-descriptor checks. The batch layout (request order, offsets) is
   // fatal; a bad unit / rule / stem length or clock is the descriptor's own
   // error: with isolate it becomes its status (FLAG_SKIP), else it fails the batch.
-  uint32_t s0 = 0, len = 0, u = 0, q = 0, dstat = 0;
   if (i < b.n) {
-    s0 = b.off[i];
-    const uint32_t s1 = b.off[i + 1];
-    u = b.unit[i];
-    q = b.req[i];
-    if ((!b.now_desc && q >= b.n_req) || (i && b.req[i - 1] > q) || s1 < s0 || s1 > b.stem_cap) {
+    if (layout_bad) {
       bad |= ERR_INVALID;
     } else {
       len = s1 - s0;
-      if (u < 1 || u > 4 || b.rule[i] >= b.n_rules || len == 0 || len > 65535) dstat = RL_E_INVALID;
-      else if (isolate && time_bad(b.now_desc ? b.now[i] : b.now[q])) dstat = RL_E_TIME;
+      if (u < 1 || u > 4 || rule >= b.n_rules || len == 0 || len > 65535) dstat = RL_E_INVALID;
+      else if (isolate && time_bad(tnow)) dstat = RL_E_TIME;
       if (len > 65535) len = 0;
     }
     if (dstat && !isolate) bad |= ERR_INVALID;
@@ -88,8 +132,22 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   const uint32_t b0 = blockIdx.x * 256;
   if (b0 >= b.n) return;  // whole block past the descriptors (request checks done)
   const uint32_t b1 = min(b0 + 256u, b.n);
-  const uint32_t lo = b.off[b0], hi = b.off[b1];
-  const uint32_t total = b.off[b.n];
+  uint32_t lo, hi, total;
+  if (b.wire) {  // (stems abut: the block's range runs from its first record's to the next block's)
+    total = b.stem_total;
+    const Wire w0 = b.wire[b0];
+    lo = (uint32_t)(((w0.label >> ROUTE_REQ_BITS) < b.n_src ? b.wbase[w0.label >> ROUTE_REQ_BITS] : 0ull) + w0.off);
+    if (b1 < b.n) {
+      const Wire w1 = b.wire[b1];
+      hi = (uint32_t)(((w1.label >> ROUTE_REQ_BITS) < b.n_src ? b.wbase[w1.label >> ROUTE_REQ_BITS] : 0ull) + w1.off);
+    } else {
+      hi = total;
+    }
+  } else {
+    lo = b.off[b0];
+    hi = b.off[b1];
+    total = b.off[b.n];
+  }
   const bool range_ok = hi >= lo && hi <= b.stem_cap && total <= b.stem_cap;
   const uint32_t* words = reinterpret_cast<const uint32_t*>(b.stem);  // 4-byte aligned base
   const uint32_t lead = lo & 3u;
@@ -104,157 +162,32 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   __syncthreads();
   if (i >= b.n) return;
   uint64_t h = 0;
-  if (len && range_ok && s0 + len <= total) {
+  if (len && range_ok && s0 + len <= total && s0 >= lo && s0 + len <= hi) {
     if (use_lds) {
       h = hash_stem(b.hk, DwordReader{lds, HASH_LDS_BYTES / 4 + 4}, s0 - lo + lead, len);
     } else {
       const uint32_t nw = ((total + 3u) >> 2) - (s0 >> 2);
       h = hash_stem(b.hk, DwordReader{words + (s0 >> 2), nw}, s0 & 3u, len);
     }
+  } else if (len && range_ok && s0 + len <= total) {
+    const uint32_t nw = ((total + 3u) >> 2) - (s0 >> 2);
+    h = hash_stem(b.hk, DwordReader{words + (s0 >> 2), nw}, s0 & 3u, len);
   }
   keys[i] = (uint32_t)(h >> 32);
   Rec r;
   r.hlo = (uint32_t)h;
   r.off = s0;
-  r.lu = len | (u << 16) | ((uint32_t)((b.flags[i] & RL_FLAG_SHADOW) | (dstat ? FLAG_SKIP : 0u)) << 24);
-  r.rule = b.rule[i];
+  r.lu = len | (u << 16) | ((uint32_t)((fl & RL_FLAG_SHADOW) | (dstat ? FLAG_SKIP : 0u)) << 24);
+  r.rule = rule;
   r.req = q;
-  r.now = b.now_desc ? (uint32_t)b.now[i] : (q < b.n_req) ? (uint32_t)b.now[q] : 0u;
-  r.hits = b.hits[i];
-  r.limit = b.limit[i];
+  r.now = (uint32_t)tnow;
+  r.hits = hits;
+  r.limit = limit;
   rec[i] = r;
   hit_a[i] = r.hits;
   if (dstat && isolate) {  // answered here: the table kernels skip it
     res[i] = pack_fail(dstat);
     atomicOr(errs, dstat == RL_E_TIME ? ERR_TIME : ERR_INVALID);
-  }
-}
-
-// ===========================================================================
-// Stable LSD radix sort of (u32 key, u32 value), 8-bit digits, 256-thread
-// tiles of RS_ITEMS x 256 elements. Per pass: tile histograms (digit-major) ->
-// per-digit row scans -> stable scatter.
-// ===========================================================================
-__global__ __launch_bounds__(256) void k_rs_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t shift,
-                                                 uint32_t ntiles, uint32_t* __restrict__ hist, const uint32_t* err) {
-  __shared__ uint32_t h[256];
-  if (*err) return;
-  const uint32_t tid = threadIdx.x;
-  h[tid] = 0;
-  __syncthreads();
-  const uint32_t base = blockIdx.x * RS_TILE;
-#pragma unroll 4
-  for (uint32_t c = 0; c < RS_ITEMS; c++) {
-    uint32_t j = base + c * 256 + tid;
-    if (j < n) atomicAdd(&h[(keys[j] >> shift) & 255u], 1u);
-  }
-  __syncthreads();
-  hist[tid * ntiles + blockIdx.x] = h[tid];
-}
-
-// Row scan of the digit-major histogram: block d turns row d (ntiles tile
-// counts) into exclusive prefixes in place and writes the row total.
-__global__ __launch_bounds__(256) void k_rs_rowscan(uint32_t* __restrict__ hist, uint32_t ntiles,
-                                                    uint32_t* __restrict__ totals, const uint32_t* err) {
-  __shared__ uint32_t part[256];
-  if (*err) return;
-  const uint32_t tid = threadIdx.x;
-  uint32_t* row = hist + (size_t)blockIdx.x * ntiles;
-  const uint32_t per = (ntiles + 255) / 256;
-  const uint32_t s0 = tid * per, s1 = min(s0 + per, ntiles);
-  uint32_t sum = 0;
-  for (uint32_t j = s0; j < s1; j++) sum += row[j];
-  part[tid] = sum;
-  __syncthreads();
-  for (uint32_t off = 1; off < 256; off <<= 1) {
-    const uint32_t v = tid >= off ? part[tid - off] : 0u;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
-  }
-  uint32_t run = part[tid] - sum;
-  for (uint32_t j = s0; j < s1; j++) {
-    const uint32_t v = row[j];
-    row[j] = run;
-    run += v;
-  }
-  if (tid == 255) totals[blockIdx.x] = part[255];
-}
-
-// Stable scatter. Wave w of a tile owns elements [w*64*RS_ITEMS, (w+1)*64*RS_ITEMS)
-// of it, item-major: it ranks them with a ballot multisplit (8 ballots -> the
-// lanes sharing a digit) against a wave-private running count in LDS, keeps
-// keys/values/ranks in registers, and only then (one barrier) learns the
-// other waves' counts and the digit's global base.
-__global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                    uint32_t n, uint32_t shift, uint32_t ntiles,
-                                                    const uint32_t* __restrict__ hist,
-                                                    const uint32_t* __restrict__ totals, const uint32_t* err) {
-  __shared__ uint32_t wcnt[4][256];
-  __shared__ uint32_t dsum[256];
-  if (*err) return;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  wcnt[0][tid] = 0; wcnt[1][tid] = 0; wcnt[2][tid] = 0; wcnt[3][tid] = 0;
-  dsum[tid] = totals[tid];
-  __syncthreads();
-  const uint64_t lt_mask = (1ull << lane) - 1;
-  const uint32_t wbase = blockIdx.x * RS_TILE + wave * 64 * RS_ITEMS;
-  uint32_t kk[RS_ITEMS], vv[RS_ITEMS], pos[RS_ITEMS];
-#pragma unroll
-  for (uint32_t i = 0; i < RS_ITEMS; i++) {
-    const uint32_t j = wbase + i * 64 + lane;
-    const bool valid = j < n;
-    kk[i] = valid ? kin[j] : 0xFFFFFFFFu;
-    vv[i] = valid ? vin[j] : 0u;
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < RS_ITEMS; i++) {
-    const bool valid = wbase + i * 64 + lane < n;
-    const uint32_t d = (kk[i] >> shift) & 255u;
-    uint64_t peers = __ballot(valid);
-#pragma unroll
-    for (uint32_t bit = 0; bit < 8; bit++) {
-      const bool sb = (d >> bit) & 1u;
-      const uint64_t bal = __ballot(sb);
-      peers &= sb ? bal : ~bal;
-    }
-    const uint32_t rank = __popcll(peers & lt_mask);
-    const uint32_t leader = valid ? (uint32_t)(__ffsll((unsigned long long)peers) - 1) : lane;
-    uint32_t old = 0;
-    if (valid && rank == 0) {
-      old = wcnt[wave][d];
-      wcnt[wave][d] = old + __popcll(peers);
-    }
-    old = __shfl(old, leader);
-    pos[i] = old + rank;
-  }
-  __syncthreads();
-  {  // digit base for this tile = exclusive scan of the digit totals + row prefix
-    uint32_t x = dsum[tid];
-    __syncthreads();
-    for (uint32_t off = 1; off < 256; off <<= 1) {
-      const uint32_t v = tid >= off ? dsum[tid - off] : 0u;
-      __syncthreads();
-      dsum[tid] += v;
-      __syncthreads();
-    }
-    uint32_t run = dsum[tid] - x + hist[(size_t)tid * ntiles + blockIdx.x];
-#pragma unroll
-    for (uint32_t w = 0; w < 4; w++) {
-      const uint32_t t = wcnt[w][tid];
-      wcnt[w][tid] = run;
-      run += t;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (uint32_t i = 0; i < RS_ITEMS; i++) {
-    if (wbase + i * 64 + lane < n) {
-      const uint32_t p = wcnt[wave][(kk[i] >> shift) & 255u] + pos[i];
-      kout[p] = kk[i];
-      vout[p] = vv[i];
-    }
   }
 }
 
@@ -972,23 +905,11 @@ struct SegPair {
 };
 __device__ inline SegPair seg_op(SegPair a, SegPair b) { return SegPair{a.f | b.f, b.f ? b.s : a.s + b.s}; }
 
-constexpr uint32_t SEG_STRIP = SEG_TILE / 4;  // positions per wave
-static_assert(SEG_STRIP == SEG_ITEMS * 64, "4 waves x SEG_ITEMS chunks of 64");
-
 struct SegChunk {
   uint64_t heads;  // ballot of run heads in the chunk
   uint32_t h;      // this lane's max(1, hits) (0 past n)
 };
 
-__device__ inline SegChunk seg_chunk(const uint32_t* skeys, const uint32_t* hits_s, uint32_t n, uint32_t q) {
-  const bool valid = q < n;
-  const bool head = valid && (q == 0 || skeys[q - 1] != skeys[q]);
-  const uint32_t hv = valid ? hits_s[q] : 0u;
-  return SegChunk{(uint64_t)__ballot(head), valid ? (hv > 1 ? hv : 1u) : 0u};
-}
-
-// Inclusive segmented scan of a chunk (lane order). Plain prefix sum P, then
-// subtract the prefix before the lane's last head.
 __device__ inline SegPair seg_chunk_scan(const SegChunk& c, uint32_t lane) {
   uint32_t P = c.h;
 #pragma unroll
@@ -1005,160 +926,6 @@ __device__ inline SegPair seg_chunk_scan(const SegChunk& c, uint32_t lane) {
 // Block-level combine of the 4 wave aggregates: returns this wave's exclusive
 // prefix within the tile (and the tile aggregate through *tot for lane 0 of
 // wave 0 callers).
-__device__ inline void seg_waves(SegPair agg, uint32_t hc, SegPair* sp, uint32_t* sh, SegPair& excl, uint32_t& hexcl,
-                                 SegPair& tot, uint32_t& htot) {
-  const uint32_t w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    sp[w] = agg;
-    sh[w] = hc;
-  }
-  __syncthreads();
-  excl = SegPair{0, 0};
-  hexcl = 0;
-  tot = SegPair{0, 0};
-  htot = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < 4; k++) {
-    if (k == w) {
-      excl = tot;
-      hexcl = htot;
-    }
-    tot = seg_op(tot, sp[k]);
-    htot += sh[k];
-  }
-}
-
-__global__ __launch_bounds__(256) void k_seg_reduce(const uint32_t* __restrict__ skeys,
-                                                    const uint32_t* __restrict__ hits_s, uint32_t n,
-                                                    uint32_t* __restrict__ tile_f, uint32_t* __restrict__ tile_s,
-                                                    uint32_t* __restrict__ tile_h, const uint32_t* err) {
-  __shared__ SegPair sp[4];
-  __shared__ uint32_t sh[4];
-  if (*err) return;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t base = blockIdx.x * SEG_TILE + (threadIdx.x >> 6) * SEG_STRIP + lane;
-  SegPair agg{0, 0};
-  uint32_t hc = 0;
-#pragma unroll 4
-  for (uint32_t c = 0; c < SEG_ITEMS; c++) {
-    const SegChunk ch = seg_chunk(skeys, hits_s, n, base + 64 * c);
-    const SegPair v = seg_chunk_scan(ch, lane);
-    agg = seg_op(agg, SegPair{__shfl(v.f, 63, 64), __shfl(v.s, 63, 64)});
-    hc += (uint32_t)__popcll(ch.heads);
-  }
-  SegPair excl, tot;
-  uint32_t hexcl, htot;
-  seg_waves(agg, hc, sp, sh, excl, hexcl, tot, htot);
-  if (threadIdx.x == 0) {
-    tile_f[blockIdx.x] = tot.f;
-    tile_s[blockIdx.x] = tot.s;
-    tile_h[blockIdx.x] = htot;
-  }
-}
-
-// Exclusive scan over the tile aggregates (one block), in place.
-__global__ __launch_bounds__(1024) void k_seg_tiles(uint32_t* __restrict__ tile_f, uint32_t* __restrict__ tile_s,
-                                                    uint32_t* __restrict__ tile_h, uint32_t ntiles, const uint32_t* err) {
-  __shared__ SegPair sp[1024];
-  __shared__ uint32_t sh[1024];
-  if (*err) return;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t per = (ntiles + 1023) / 1024;
-  const uint32_t s0 = tid * per, s1 = min(s0 + per, ntiles);
-  SegPair v{0, 0};
-  uint32_t hc = 0;
-  for (uint32_t j = s0; j < s1; j++) {
-    v = seg_op(v, SegPair{tile_f[j], tile_s[j]});
-    hc += tile_h[j];
-  }
-  sp[tid] = v;
-  sh[tid] = hc;
-  __syncthreads();
-  for (uint32_t off = 1; off < 1024; off <<= 1) {
-    SegPair a = v;
-    uint32_t c = hc;
-    if (tid >= off) {
-      a = seg_op(sp[tid - off], v);
-      c = sh[tid - off] + hc;
-    }
-    __syncthreads();
-    v = a;
-    hc = c;
-    sp[tid] = v;
-    sh[tid] = hc;
-    __syncthreads();
-  }
-  SegPair run = tid ? sp[tid - 1] : SegPair{0, 0};
-  uint32_t hrun = tid ? sh[tid - 1] : 0u;
-  for (uint32_t j = s0; j < s1; j++) {
-    const SegPair x{tile_f[j], tile_s[j]};
-    const uint32_t xh = tile_h[j];
-    tile_f[j] = run.f;
-    tile_s[j] = run.s;
-    tile_h[j] = hrun;
-    run = seg_op(run, x);
-    hrun += xh;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_seg_apply(const uint32_t* __restrict__ skeys,
-                                                   const uint32_t* __restrict__ hits_s, uint32_t n,
-                                                   const uint32_t* __restrict__ tile_f,
-                                                   const uint32_t* __restrict__ tile_s,
-                                                   const uint32_t* __restrict__ tile_h, uint32_t* __restrict__ segsum,
-                                                   uint32_t* __restrict__ rid, uint32_t* __restrict__ run_start,
-                                                   uint32_t* __restrict__ run_flags, uint32_t* num_runs,
-                                                   const uint32_t* err) {
-  __shared__ SegPair sp[4];
-  __shared__ uint32_t sh[4];
-  if (*err) return;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t base = blockIdx.x * SEG_TILE + (threadIdx.x >> 6) * SEG_STRIP + lane;
-  // pass 1 (chunks kept in registers): this wave's aggregate
-  SegChunk ch[SEG_ITEMS];
-  SegPair agg{0, 0};
-  uint32_t hc = 0;
-#pragma unroll
-  for (uint32_t c = 0; c < SEG_ITEMS; c++) {
-    ch[c] = seg_chunk(skeys, hits_s, n, base + 64 * c);
-    uint32_t t = ch[c].h;  // chunk total, segmented: sum after the last head
-    const uint32_t lh = ch[c].heads ? 63u - (uint32_t)__clzll((long long)ch[c].heads) : 0u;
-    if (ch[c].heads && lane < lh) t = 0;
-#pragma unroll
-    for (uint32_t off = 32; off; off >>= 1) t += __shfl_xor(t, off, 64);
-    agg = seg_op(agg, SegPair{ch[c].heads ? 1u : 0u, t});
-    hc += (uint32_t)__popcll(ch[c].heads);
-  }
-  SegPair excl, tot;
-  uint32_t hexcl, htot;
-  seg_waves(agg, hc, sp, sh, excl, hexcl, tot, htot);
-  // pass 2: exclusive prefix of the wave = tile carry + earlier waves
-  SegPair run = seg_op(SegPair{tile_f[blockIdx.x], tile_s[blockIdx.x]}, excl);
-  uint32_t hrun = tile_h[blockIdx.x] + hexcl;
-#pragma unroll
-  for (uint32_t c = 0; c < SEG_ITEMS; c++) {
-    const uint32_t q = base + 64 * c;
-    const SegPair v = seg_chunk_scan(ch[c], lane);
-    const SegPair in = seg_op(run, v);
-    const uint64_t heads = ch[c].heads;
-    const uint32_t r = hrun + (uint32_t)__popcll(heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1))) - 1;
-    if (q < n) {
-      segsum[q] = in.s;
-      rid[q] = r;
-      if ((heads >> lane) & 1) {
-        run_start[r] = q;
-        run_flags[r] = 0;
-      }
-      if (q == n - 1) {
-        run_start[r + 1] = n;
-        *num_runs = r + 1;
-      }
-    }
-    run = seg_op(run, SegPair{__shfl(v.f, 63, 64), __shfl(v.s, 63, 64)});
-    hrun += (uint32_t)__popcll(heads);
-  }
-}
-
 // ===========================================================================
 // Grouping by MSD partition + per-bucket LDS sort (stage A).
 //
@@ -2392,7 +2159,7 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
   if (lo >= hi) return;
   // non-head positions (the second and later descriptors of a run)
   const uint32_t cnt = block_compact(lo, hi, s_list, &s_cnt, [&](uint32_t q) { return skeys[q - 1] == skeys[q]; });
-  b.stem_total = b.off[b.n];
+  if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
   Rec* rec = const_cast<Rec*>(rec_s.rec);
 #pragma unroll 1
   for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
@@ -2432,7 +2199,7 @@ __global__ __launch_bounds__(256) void k_unique(BatchDev b, TableDev t, Params P
   __syncthreads();
   const uint32_t lo = blockIdx.x * 256, hi = min(lo + 256, b.n);
   if (s_err || lo >= hi) return;
-  b.stem_total = b.off[b.n];
+  if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
   uint32_t* ferr = P.isolate ? errs : err;
   const bool use_lds = !restore && b.n_rules <= LDS_RULES;
   stats_block_begin(use_lds, b.n_rules);
@@ -2515,7 +2282,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
   __syncthreads();
   const uint32_t lo = blockIdx.x * 256, hi = min(lo + 256, s_nr);
   if (s_err || lo >= hi) return;
-  b.stem_total = b.off[b.n];
+  if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
   uint32_t* ferr = P.isolate ? errs : err;  // descriptor-level failures: soft word with statuses
   // the dup-run list, compacted once more (a large bucket's hot-key run left
   // to its fallback path is empty)
@@ -2795,7 +2562,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
   }
   __syncthreads();
   if (s_err || (blockIdx.x * 256 >= s_n && blockIdx.x * 256 >= s_n1)) return;
-  b.stem_total = b.off[b.n];
+  if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
   uint32_t* ferr = P.isolate ? errs : err;
   const bool use_lds = !restore && b.n_rules <= LDS_RULES;
   stats_block_begin(use_lds, b.n_rules);
@@ -3142,23 +2909,6 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
   if (ev) (void)hipEventRecord(ev[5], st);
 }
 
-void launch_partition(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, uint32_t n,
-                      const Scratch& s, hipStream_t st) {
-  if (!n) return;
-  const uint32_t ntiles = cdiv(n, RS_TILE);
-  k_rs_hist<<<ntiles, 256, 0, st>>>(kin, n, 0, ntiles, s.hist, s.err);
-  k_rs_rowscan<<<256, 256, 0, st>>>(s.hist, ntiles, s.hist_tot, s.err);
-  k_rs_scatter<<<ntiles, 256, 0, st>>>(kin, vin, kout, vout, n, 0, ntiles, s.hist, s.hist_tot, s.err);
-}
-
-void launch_run_sums(const uint32_t* skeys, const uint32_t* w, uint32_t n, const Scratch& s, hipStream_t st) {
-  if (!n) return;
-  const uint32_t nt = cdiv(n, SEG_TILE);
-  k_seg_reduce<<<nt, 256, 0, st>>>(skeys, w, n, s.tile_f, s.tile_s, s.tile_h, s.err);
-  k_seg_tiles<<<1, 1024, 0, st>>>(s.tile_f, s.tile_s, s.tile_h, nt, s.err);
-  k_seg_apply<<<nt, 256, 0, st>>>(skeys, w, n, s.tile_f, s.tile_s, s.tile_h, s.segsum, s.rid, s.run_start,
-                                  s.run_flags, s.num_runs, s.err);
-}
 
 void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st) {
   k_sweep<<<2048, 256, 0, st>>>(slots, nslots, now, evicted);

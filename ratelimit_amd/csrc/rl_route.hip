@@ -1,14 +1,15 @@
 // rl_route.hip — multi-GPU routing of a batch to the GPUs that own its keys
-// (hash-sharded table). The exchange itself is two RCCL
-// all_to_all calls issued by the host (ratelimit_amd/sharded.py); these
-// kernels do the device-side halves around it:
+// (hash-sharded table). The exchange itself is driven by
+// rl_comm.hip (RCCL send/recv inside the library), rl_api.hip (shards of one
+// ctx: peer copies) or ratelimit_amd/sharded.py (collectives from Python);
+// these kernels are the device-side halves around it:
 //
-//   source: hash -> owner, stable partition by owner (one 8-bit counting
-//           pass), per-owner stem offsets (segmented sums), pack 32-B wire
-//           records + stem bytes in owner order;
-//   owner:  unpack the received chunks (concatenated in source-rank order =
-//           global arrival order) into a batch with per-descriptor `now` and
-//           request labels, run the normal DoLimit pipeline;
+//   source: hash -> owner, stable partition by owner, 32-B wire records +
+//           stem bytes in owner order (k_rp_count / k_rp_scan / k_rp_pack);
+//   owner:  the received chunks (concatenated in source-rank order = global
+//           arrival order) feed the normal DoLimit pipeline directly: its
+//           k_prepare reads the wire records (BatchDev.wire);
+//           k_route_ret hands the packed results (or the batch's failure) back;
 //   source: scatter the returned packed results to arrival order.
 //
 // Owner of a stem = (low 32 bits of its 64-bit hash x n_shards) >> 32: the
@@ -30,83 +31,284 @@ __device__ inline uint32_t owner_of(uint64_t h, uint32_t n_shards) {
 }
 
 // ---- source side ----------------------------------------------------------
-__global__ __launch_bounds__(256) void k_route_prep(BatchDev b, uint32_t n_shards, uint32_t* __restrict__ dest,
-                                                    uint32_t* __restrict__ idx, uint32_t* err) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= b.n) return;
-  const uint32_t s0 = b.off[i], s1 = b.off[i + 1], total = b.off[b.n];
-  // Only a malformed layout fails the partition; a bad unit, rule id or clock
-  // is the owner's to judge (per-descriptor status, or the batch's error).
-  const uint32_t q = b.req[i];
-  const bool bad = q >= ROUTE_MAX_REQ || (i && b.req[i - 1] > q) || s1 <= s0 ||
-                   s1 - s0 > 65535 || total > b.stem_cap || s1 > total || q >= b.n_req;
-  uint64_t h = 0;
-  if (bad) {
-    atomicOr(err, ERR_INVALID);
-  } else {
-    const uint32_t* words = reinterpret_cast<const uint32_t*>(b.stem);
-    h = hash_stem(b.hk, DwordReader{words + (s0 >> 2), ((total + 3u) >> 2) - (s0 >> 2)}, s0 & 3u, s1 - s0);
+// Partition of a slice by owner, in three launches over tiles of RP_TILE
+// descriptors (all HBM-streaming; the byte moves go through LDS):
+//   k_rp_count  hash -> owner per descriptor (dest, u8), per-tile record and
+//               stem-byte counts per owner;
+//   k_rp_scan   per owner: exclusive scan of the tile counts, the totals
+//               (= the exchange counts);
+//   k_rp_pack   stable rank of each descriptor inside its tile and owner
+//               (wave ballots), its 32-B wire record and perm entry, and its
+//               stem bytes staged in LDS so that each owner's run of stems
+//               leaves the tile as whole dwords.
+constexpr uint32_t RP_ITEMS = 2;
+constexpr uint32_t RP_TILE = 256 * RP_ITEMS;
+static_assert(RP_TILE == ROUTE_TILE, "scratch sizing");
+constexpr uint32_t RP_WAVE = RP_TILE / 4;       // consecutive descriptors per wave
+constexpr uint32_t RP_STAGE = 24 * 1024;        // LDS bytes for a tile's stems (else direct byte copies)
+
+__device__ inline uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// Inclusive prefix sum over the 64 lanes of a wave.
+__device__ inline uint32_t wave_incl(uint32_t v) {
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(v, o, 64);
+    if (lane_id() >= o) v += y;
   }
-  dest[i] = bad ? 0u : owner_of(h, n_shards);
-  idx[i] = i;
+  return v;
 }
 
-__global__ __launch_bounds__(256) void k_route_lens(const uint32_t* __restrict__ off,
-                                                    const uint32_t* __restrict__ perm, uint32_t n,
-                                                    uint32_t* __restrict__ lens_s, const uint32_t* err) {
+// Exclusive prefix over the 256 threads of a block of (a, b); returns the
+// block totals. tmp: 8 shared words.
+__device__ inline void block_excl2(uint32_t& a, uint32_t& b, uint32_t& ta, uint32_t& tb, uint32_t* tmp) {
+  const uint32_t ia = wave_incl(a), ib = wave_incl(b), w = threadIdx.x >> 6;
+  if (lane_id() == 63) {
+    tmp[w] = ia;
+    tmp[4 + w] = ib;
+  }
+  __syncthreads();
+  uint32_t pa = 0, pb = 0;
+  for (uint32_t k = 0; k < w; k++) {
+    pa += tmp[k];
+    pb += tmp[4 + k];
+  }
+  ta = tmp[0] + tmp[1] + tmp[2] + tmp[3];
+  tb = tmp[4] + tmp[5] + tmp[6] + tmp[7];
+  a = pa + ia - a;
+  b = pb + ib - b;
+  __syncthreads();
+}
+
+// A descriptor the partition cannot route: malformed layout only (a bad
+// unit, rule id or clock is the owner's to judge).
+__device__ inline bool rp_bad(const BatchDev& b, uint32_t i, uint32_t total) {
+  const uint32_t s0 = b.off[i], s1 = b.off[i + 1], q = b.req[i];
+  return q >= ROUTE_MAX_REQ || (i && b.req[i - 1] > q) || s1 <= s0 || s1 - s0 > 65535 || total > b.stem_cap ||
+         s1 > total || q >= b.n_req;
+}
+
+__global__ __launch_bounds__(256) void k_rp_count(BatchDev b, uint32_t n_shards, uint32_t ntiles,
+                                                  uint8_t* __restrict__ dest, uint32_t* __restrict__ hist,
+                                                  uint32_t* err) {
+  __shared__ uint32_t cr[RL_MAX_SHARDS], cb[RL_MAX_SHARDS];
+  for (uint32_t d = threadIdx.x; d < n_shards; d += 256) cr[d] = cb[d] = 0;
+  __syncthreads();
+  const uint32_t total = b.off[b.n];
+  const uint32_t* words = reinterpret_cast<const uint32_t*>(b.stem);
+  const uint32_t nw = (total + 3u) >> 2;
+  bool bad = false;
+#pragma unroll
+  for (uint32_t t = 0; t < RP_ITEMS; t++) {
+    const uint32_t i = blockIdx.x * RP_TILE + t * 256 + threadIdx.x;
+    if (i >= b.n) continue;
+    uint32_t d = 0, len = 0;
+    if (rp_bad(b, i, total)) {
+      bad = true;
+    } else {
+      const uint32_t s0 = b.off[i];
+      len = b.off[i + 1] - s0;
+      const uint64_t h = hash_stem(b.hk, DwordReader{words + (s0 >> 2), nw - (s0 >> 2)}, s0 & 3u, len);
+      d = owner_of(h, n_shards);
+    }
+    dest[i] = (uint8_t)d;
+    atomicAdd(&cr[d], 1u);
+    atomicAdd(&cb[d], len);
+  }
+  if (bad) atomicOr(err, ERR_INVALID);
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < n_shards; d += 256) {
+    hist[(size_t)d * ntiles + blockIdx.x] = cr[d];
+    hist[((size_t)n_shards + d) * ntiles + blockIdx.x] = cb[d];
+  }
+}
+
+// One block per owner d: exclusive scans of its row of tile counts (records,
+// bytes); counts[2d], [2d+1] = the totals (zero when the slice is malformed,
+// so the exchange stays well-formed); tot[d], tot[n_shards + d] too.
+__global__ __launch_bounds__(256) void k_rp_scan(uint32_t* __restrict__ hist, uint32_t n_shards, uint32_t ntiles,
+                                                 unsigned long long* __restrict__ counts,
+                                                 uint32_t* __restrict__ tot, const uint32_t* err) {
+  __shared__ uint32_t tmp[8];
+  const uint32_t d = blockIdx.x;
+  uint32_t* rr = hist + (size_t)d * ntiles;
+  uint32_t* rb = hist + ((size_t)n_shards + d) * ntiles;
+  uint32_t ca = 0, cb = 0;
+  for (uint32_t base = 0; base < ntiles; base += 256) {
+    const uint32_t j = base + threadIdx.x;
+    uint32_t a = j < ntiles ? rr[j] : 0u, bb = j < ntiles ? rb[j] : 0u, ta, tb;
+    block_excl2(a, bb, ta, tb, tmp);
+    if (j < ntiles) {
+      rr[j] = ca + a;
+      rb[j] = cb + bb;
+    }
+    ca += ta;
+    cb += tb;
+  }
+  if (threadIdx.x == 0) {
+    const bool ok = *err == 0;
+    counts[2 * d] = ok ? ca : 0u;
+    counts[2 * d + 1] = ok ? cb : 0u;
+    tot[d] = ca;
+    tot[n_shards + d] = cb;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, uint32_t ntiles, uint32_t src_rank,
+                                                 const uint8_t* __restrict__ dest, const uint32_t* __restrict__ hist,
+                                                 const uint32_t* __restrict__ tot, Wire* __restrict__ out,
+                                                 uint8_t* __restrict__ out_stem, uint32_t* __restrict__ perm,
+                                                 const uint32_t* err) {
+  __shared__ uint32_t wr[4][RL_MAX_SHARDS], wb[4][RL_MAX_SHARDS];  // per wave, then wave bases
+  __shared__ uint32_t gr[RL_MAX_SHARDS], gb[RL_MAX_SHARDS];        // tile's first record / chunk byte per owner
+  __shared__ uint32_t sb[RL_MAX_SHARDS], lo[RL_MAX_SHARDS], tb[RL_MAX_SHARDS];
+  __shared__ uint32_t tmp[8];
+  __shared__ uint8_t stage[RP_STAGE];
   if (*err) return;
-  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= n) return;
-  const uint32_t e = perm[j];
-  lens_s[j] = off[e + 1] - off[e];
-}
-
-// Per owner: record count (partition digit totals) and stem bytes (the in-run
-// sum at the owner's last record); stem_start = exclusive prefix of the bytes.
-// All zero when the batch failed validation, so the exchange stays well-formed.
-__global__ void k_route_counts(const uint32_t* __restrict__ digit_tot, const uint32_t* __restrict__ segsum,
-                               uint32_t n_shards, uint32_t* __restrict__ stem_start,
-                               unsigned long long* __restrict__ counts, const uint32_t* err) {
-  if (threadIdx.x != 0) return;
-  const bool ok = *err == 0;
-  uint32_t rec = 0, sb = 0;
+  const uint32_t tile = blockIdx.x, w = threadIdx.x >> 6, lane = lane_id();
+  for (uint32_t d = threadIdx.x; d < n_shards; d += 256) {
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) wr[k][d] = wb[k][d] = 0;
+  }
+  // owners' first record (global) and stem byte (send buffer): exclusive
+  // scans of the totals over owners
+  {
+    uint32_t ra = 0, rb = 0, sa = 0, sbb = 0;
+    const uint32_t d = threadIdx.x;  // (n_shards <= 256)
+    if (d < n_shards) {
+      ra = tot[d];
+      rb = tot[n_shards + d];
+    }
+    sa = ra;
+    sbb = rb;
+    uint32_t ta, tbb;
+    block_excl2(sa, sbb, ta, tbb, tmp);
+    if (d < n_shards) {
+      gr[d] = sa + hist[(size_t)d * ntiles + tile];
+      sb[d] = sbb;
+      gb[d] = hist[((size_t)n_shards + d) * ntiles + tile];
+    }
+  }
+  __syncthreads();
+  // stable rank inside (tile, owner): wave w takes RP_WAVE consecutive
+  // descriptors, 64 per round, grouping lanes by owner with ballots
+  const uint32_t i0 = tile * RP_TILE + w * RP_WAVE;
+  uint32_t my_d[RP_ITEMS], my_r[RP_ITEMS], my_b[RP_ITEMS], my_len[RP_ITEMS];
+  const uint64_t lt = (lane ? ~0ull >> (64 - lane) : 0ull);
+#pragma unroll
+  for (uint32_t t = 0; t < RP_ITEMS; t++) {
+    const uint32_t i = i0 + t * 64 + lane;
+    const bool valid = i < b.n;
+    const uint32_t d = valid ? dest[i] : 0xFFFFu;
+    const uint32_t len = valid ? b.off[i + 1] - b.off[i] : 0u;
+    uint64_t todo = __ballot(valid);
+    uint32_t r = 0, bp = 0;
+    while (todo) {
+      const uint32_t leader = __ffsll((unsigned long long)todo) - 1;
+      const uint32_t dl = __shfl(d, leader, 64);
+      const bool mine = valid && d == dl;
+      const uint64_t mask = __ballot(mine);
+      const uint32_t incl = wave_incl(mine ? len : 0u);
+      const uint32_t gbytes = __shfl(incl, 63, 64);
+      const uint32_t br = wr[w][dl], bb = wb[w][dl];  // (one wave: read before the leader's update)
+      if (mine) {
+        r = br + (uint32_t)__popcll(mask & lt);
+        bp = bb + incl - len;
+      }
+      if (lane == leader) {
+        wr[w][dl] = br + (uint32_t)__popcll(mask);
+        wb[w][dl] = bb + gbytes;
+      }
+      todo &= ~mask;
+    }
+    my_d[t] = d;
+    my_r[t] = r;
+    my_b[t] = bp;
+    my_len[t] = len;
+  }
+  __syncthreads();
+  // wave bases inside the tile, the tile's bytes per owner, LDS segments
+  {
+    const uint32_t d = threadIdx.x;
+    uint32_t byt = 0;
+    if (d < n_shards) {
+      uint32_t ar = 0, ab = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t xr = wr[k][d], xb = wb[k][d];
+        wr[k][d] = ar;
+        wb[k][d] = ab;
+        ar += xr;
+        ab += xb;
+      }
+      tb[d] = ab;
+      byt = ab;
+    }
+    uint32_t dummy = 0, t1, t2;
+    block_excl2(byt, dummy, t1, t2, tmp);
+    if (d < n_shards) lo[d] = byt;
+    if (d == 0) tmp[0] = t1;  // the tile's stem bytes
+  }
+  __syncthreads();
+  const bool staged = tmp[0] <= RP_STAGE;
+  const uint32_t* words = reinterpret_cast<const uint32_t*>(b.stem);
+  const uint32_t nw = (b.off[b.n] + 3u) >> 2;
+#pragma unroll
+  for (uint32_t t = 0; t < RP_ITEMS; t++) {
+    const uint32_t i = i0 + t * 64 + lane;
+    if (i >= b.n) continue;
+    const uint32_t d = my_d[t], len = my_len[t];
+    const uint32_t j = gr[d] + wr[w][d] + my_r[t];      // record index in the send buffer
+    const uint32_t local = gb[d] + wb[w][d] + my_b[t];  // byte offset inside owner d's chunk
+    const uint32_t q = b.req[i];
+    Wire x;
+    x.label = (src_rank << ROUTE_REQ_BITS) | q;
+    x.off = local;
+    x.lu = len | ((uint32_t)b.unit[i] << 16) | ((uint32_t)b.flags[i] << 24);
+    x.limit = b.limit[i];
+    x.hits = b.hits[i];
+    x.rule = b.rule[i];
+    x.now = b.now[q];
+    out[j] = x;
+    perm[j] = i;
+    const uint32_t s0 = b.off[i];
+    if (staged) {
+      uint8_t* dst = stage + lo[d] + wb[w][d] + my_b[t];
+      for (uint32_t k = 0; k < len; k += 4) {
+        const uint32_t a = s0 + k, wi = a >> 2, sh = (a & 3u) * 8;
+        uint32_t v = words[wi];
+        if (sh) v = (v >> sh) | ((wi + 1 < nw ? words[wi + 1] : 0u) << (32 - sh));
+        const uint32_t m = len - k < 4 ? len - k : 4u;
+        for (uint32_t z = 0; z < m; z++) dst[k + z] = (uint8_t)(v >> (8 * z));
+      }
+    } else {
+      uint8_t* dst = out_stem + sb[d] + local;
+      for (uint32_t k = 0; k < len; k++) dst[k] = b.stem[s0 + k];
+    }
+  }
+  if (!staged) return;
+  __syncthreads();
+  // each owner's run of stems leaves the tile as dwords (bytes at its ends:
+  // the neighbouring tiles own the rest of those dwords)
   for (uint32_t d = 0; d < n_shards; d++) {
-    const uint32_t c = ok ? digit_tot[d] : 0u;
-    const uint32_t bytes = c ? segsum[rec + c - 1] : 0u;
-    counts[2 * d] = c;
-    counts[2 * d + 1] = bytes;
-    stem_start[d] = sb;
-    rec += c;
-    sb += bytes;
+    const uint32_t T = tb[d];
+    if (!T) continue;
+    const uint32_t G = sb[d] + gb[d], L = lo[d];
+    const uint32_t A0 = G & ~3u, nd = (((G + T + 3u) & ~3u) - A0) >> 2;
+    for (uint32_t k = threadIdx.x; k < nd; k += 256) {
+      const uint32_t A = A0 + 4 * k;
+      if (A >= G && A + 4 <= G + T) {
+        const uint8_t* p = stage + L + (A - G);
+        *reinterpret_cast<uint32_t*>(out_stem + A) =
+            (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+      } else {
+        for (uint32_t z = 0; z < 4; z++) {
+          const uint32_t a = A + z;
+          if (a >= G && a < G + T) out_stem[a] = stage[L + (a - G)];
+        }
+      }
+    }
   }
-  stem_start[n_shards] = sb;
-}
-
-__global__ __launch_bounds__(256) void k_route_pack(BatchDev b, const uint32_t* __restrict__ perm,
-                                                    const uint32_t* __restrict__ sdest,
-                                                    const uint32_t* __restrict__ segsum,
-                                                    const uint32_t* __restrict__ lens_s,
-                                                    const uint32_t* __restrict__ stem_start, uint32_t src_rank,
-                                                    Wire* __restrict__ out, uint8_t* __restrict__ out_stem,
-                                                    const uint32_t* err) {
-  if (*err) return;
-  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= b.n) return;
-  const uint32_t e = perm[j], len = lens_s[j];
-  const uint32_t local = segsum[j] - len;  // byte offset inside the owner's chunk
-  const uint32_t q = b.req[e];
-  Wire w;
-  w.label = (src_rank << ROUTE_REQ_BITS) | q;
-  w.off = local;
-  w.lu = len | ((uint32_t)b.unit[e] << 16) | ((uint32_t)b.flags[e] << 24);
-  w.limit = b.limit[e];
-  w.hits = b.hits[e];
-  w.rule = b.rule[e];
-  w.now = b.now[q];
-  out[j] = w;
-  const uint8_t* src = b.stem + b.off[e];
-  uint8_t* dst = out_stem + stem_start[sdest[j]] + local;
-  for (uint32_t k = 0; k < len; k++) dst[k] = src[k];
 }
 
 __global__ __launch_bounds__(256) void k_route_scatter(const uint32_t* __restrict__ perm,
@@ -131,41 +333,6 @@ __global__ __launch_bounds__(256) void k_route_ret(const unsigned long long* __r
   ret[i] = e ? pack_fail(err_status(e)) : res[i];
 }
 
-// ---- owner side -----------------------------------------------------------
-// Received records -> batch arrays. Chunks arrive in source-rank order, each
-// with its stems contiguous in record order, so consecutive records' stems
-// must abut (checked: a malformed exchange is RL_E_INVALID, never a wrong key).
-// rule_stride > 0: per-source stats, rule' = source x rule_stride + rule.
-__global__ __launch_bounds__(256) void k_route_unpack(const Wire* __restrict__ rec, uint32_t n,
-                                                      const unsigned long long* __restrict__ base,
-                                                      uint32_t n_shards, uint64_t stem_bytes, uint32_t rule_stride,
-                                                      BatchOut bo, uint32_t* err) {
-  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= n) return;
-  const Wire w = rec[j];
-  const uint32_t src = w.label >> ROUTE_REQ_BITS, len = w.lu & 0xFFFFu;
-  bool bad = src >= n_shards;
-  const uint64_t o = (bad ? 0ull : base[src]) + w.off;
-  if (j + 1 < n) {
-    const Wire x = rec[j + 1];
-    const uint32_t s2 = x.label >> ROUTE_REQ_BITS;
-    bad = bad || s2 >= n_shards || (s2 >= n_shards ? true : base[s2] + x.off != o + len) || x.label < w.label;
-  } else {
-    bad = bad || o + len > stem_bytes;
-    bo.off[n] = (uint32_t)(o + len);
-  }
-  if (bad) atomicOr(err, ERR_INVALID);
-  bo.off[j] = (uint32_t)o;
-  bo.now[j] = w.now;
-  bo.req[j] = w.label;
-  bo.unit[j] = (uint8_t)(w.lu >> 16);
-  bo.flags[j] = (uint8_t)(w.lu >> 24);
-  bo.limit[j] = w.limit;
-  bo.hits[j] = w.hits;
-  // (a rule id past the stride stays out of range for the owner's validation)
-  bo.rule[j] = !rule_stride ? w.rule : w.rule >= rule_stride ? 0xFFFFFFFFu : (bad ? 0u : src) * rule_stride + w.rule;
-}
-
 // Per-rule stats deltas of several owners (blocks of m counters) summed into out.
 __global__ __launch_bounds__(256) void k_stats_sum(const unsigned long long* __restrict__ stage, uint32_t n_blocks,
                                                    uint32_t m, unsigned long long* __restrict__ out) {
@@ -185,24 +352,12 @@ void launch_stats_sum(const unsigned long long* stage, uint32_t n_blocks, uint32
 
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
                        uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st) {
-  const uint32_t g = cdiv(b.n, 256);
-  if (b.n) {
-    k_route_prep<<<g, 256, 0, st>>>(b, n_shards, s.keys[0], s.vals[0], s.err);
-    launch_partition(s.keys[0], s.vals[0], s.keys[1], perm, b.n, s, st);
-    k_route_lens<<<g, 256, 0, st>>>(b.off, perm, b.n, s.hits_s, s.err);
-    launch_run_sums(s.keys[1], s.hits_s, b.n, s, st);
-  } else {
-    (void)hipMemsetAsync(s.hist_tot, 0, 256 * sizeof(uint32_t), st);
-  }
-  k_route_counts<<<1, 64, 0, st>>>(s.hist_tot, s.segsum, n_shards, s.route_start, counts, s.err);
+  const uint32_t ntiles = b.n ? cdiv(b.n, RP_TILE) : 0u;
+  if (b.n) k_rp_count<<<ntiles, 256, 0, st>>>(b, n_shards, ntiles, s.route_dest, s.route_hist, s.err);
+  k_rp_scan<<<n_shards, 256, 0, st>>>(s.route_hist, n_shards, ntiles, counts, s.route_start, s.err);
   if (b.n)
-    k_route_pack<<<g, 256, 0, st>>>(b, perm, s.keys[1], s.segsum, s.hits_s, s.route_start, src_rank, out, out_stem,
-                                    s.err);
-}
-
-void launch_route_unpack(const Wire* rec, uint32_t n, const unsigned long long* base, uint32_t n_shards,
-                         uint64_t stem_bytes, uint32_t rule_stride, const BatchOut& bo, uint32_t* err, hipStream_t st) {
-  if (n) k_route_unpack<<<cdiv(n, 256), 256, 0, st>>>(rec, n, base, n_shards, stem_bytes, rule_stride, bo, err);
+    k_rp_pack<<<ntiles, 256, 0, st>>>(b, n_shards, ntiles, src_rank, s.route_dest, s.route_hist, s.route_start, out,
+                                      out_stem, perm, s.err);
 }
 
 void launch_route_scatter(const uint32_t* perm, const unsigned long long* ret, uint32_t n, const OutDev& o,

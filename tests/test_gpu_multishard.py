@@ -182,3 +182,38 @@ def test_gpu_multishard_bad_config():
         Backend(0.8, False, **SMALL, n_shards=17, shard_devices=[0] * 17)
     with pytest.raises(ValueError):
         Backend(0.8, False, **SMALL, n_shards=2, shard_devices=[0])
+
+
+def test_gpu_multishard_long_and_ragged_stems_vs_c_oracle():
+    """Stems of 1..300 bytes, Zipf-repeated: partition tiles whose stems do not
+    fit the LDS staging area take the direct byte-copy path, short ones the
+    staged dword path; unaligned chunk boundaries on every owner."""
+    from ratelimit_amd.packing import arrays_from_lists
+    rng = np.random.default_rng(9)
+    pool = [bytes(rng.integers(33, 127, int(L)).astype(np.uint8)) for L in
+            np.r_[rng.integers(1, 40, 2000), rng.integers(80, 300, 2000)]]
+    z = workloads.ZipfSampler(len(pool), 1.1)
+    batches = []
+    for k in range(3):
+        nq = 5000
+        ids = z.sample(rng, nq)
+        if k == 1:  # one tile of only long stems, one of only short ones
+            ids[:512] = rng.integers(2000, 4000, 512)
+            ids[512:1024] = rng.integers(0, 2000, 512)
+        stems = [pool[i] for i in ids]
+        a = arrays_from_lists(stems, np.full(nq, workloads.NOW0 + k, np.int64), np.arange(nq),
+                              rng.integers(1, 5, nq), np.zeros(nq), rng.integers(1, 50, nq), rng.integers(1, 4, nq),
+                              rng.integers(0, 4, nq))
+        pad = (-a["stem_bytes"].size) % 4  # (device stems: 4-byte aligned, whole dwords)
+        a["stem_bytes"] = np.r_[a["stem_bytes"], np.zeros(pad + 4, np.uint8)]
+        batches.append((a, nq, nq, 4))
+    for n_shards in (1, 3):
+        be = Backend(0.8, True, table_slots=1 << 16, max_batch=1 << 14, max_rules=16, hash_seed=3,
+                     **_shards(n_shards))
+        co = c_oracle.COracle(0.8, True)
+        for b in batches:
+            g, o = be.do_limit_arrays(*b), co.do_limit(*b)
+            for key in ("code", "limit_remaining", "reset_s", "stats"):
+                assert np.array_equal(g[key], o[key]), (n_shards, key)
+        be.close()
+        co.close()
