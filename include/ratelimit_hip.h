@@ -228,7 +228,8 @@ int rl_debug_decide(rl_ctx* ctx, uint32_t n, const uint32_t* before, const uint3
  * rl_config.hash_seed (owner = stem hash).
  *
  * rl_route_pack (source side): stable-partitions the batch `in` by owner shard
- * and writes, in owner order, one RL_WIRE_BYTES record per descriptor to
+ * and writes, in owner order, one RL_WIRE_BYTES record per descriptor (its
+ * fields and keyed 64-bit stem hash, so owners never rehash) to
  * send_rec and its stem bytes to send_stem (capacity: the batch's stem bytes).
  * perm[j] = batch index of record j. counts[2*d], [2*d+1] (device memory) =
  * records / stem bytes for owner d (all zero when the batch is malformed). Request
@@ -248,7 +249,7 @@ int rl_debug_decide(rl_ctx* ctx, uint32_t n, const uint32_t* before, const uint3
  *
  * rl_route_scatter (source side): results returned in record order (ret, n =
  * the batch size) -> out (device SoA, status optional) in arrival order. */
-#define RL_WIRE_BYTES 32u
+#define RL_WIRE_BYTES 40u
 #define RL_MAX_SHARDS 256u
 int rl_route_pack(rl_ctx* ctx, const rl_batch* in, uint32_t n_shards, uint32_t src_rank, void* send_rec,
                   uint8_t* send_stem, uint32_t* perm, uint64_t* counts, void* stream);

@@ -424,7 +424,7 @@ bool scratch_alloc(Scratch& s, uint32_t n) {
   s = Scratch{};
   bool ok = alloc_buffer(s, n);
   ok = ok && dalloc(&s.err, 1) == hipSuccess && dalloc(&s.route_start, 2 * RL_MAX_SHARDS + 1) == hipSuccess &&
-       dalloc(&s.route_dest, n) == hipSuccess &&
+       dalloc(&s.route_dest, n) == hipSuccess && dalloc(&s.route_hash, n) == hipSuccess &&
        dalloc(&s.route_hist, 2ull * RL_MAX_SHARDS * ((n + ROUTE_TILE - 1) / ROUTE_TILE)) == hipSuccess;
   ok = ok && hipMemset(s.err, 0, 4) == hipSuccess;
   return ok;
@@ -432,7 +432,7 @@ bool scratch_alloc(Scratch& s, uint32_t n) {
 
 void scratch_free(Scratch& s) {
   free_buffer(s);
-  for (void* p : {(void*)s.err, (void*)s.route_start, (void*)s.route_dest, (void*)s.route_hist})
+  for (void* p : {(void*)s.err, (void*)s.route_start, (void*)s.route_dest, (void*)s.route_hash, (void*)s.route_hist})
     if (p) (void)hipFree(p);
   s = Scratch{};
 }

@@ -95,6 +95,7 @@ struct __attribute__((aligned(8))) Wire {
   uint32_t hits;
   uint32_t rule;
   int64_t now;
+  unsigned long long hash;  // keyed stem hash (source side): the owner's sort key and slot tag
 };
 static_assert(sizeof(Wire) == RL_WIRE_BYTES, "wire record size is part of the ABI");
 
@@ -168,6 +169,7 @@ struct Scratch {
   // multi-GPU routing
   uint32_t* route_start;             // [2 x RL_MAX_SHARDS + 1] records / stem bytes per owner (partition)
   uint8_t* route_dest;               // [n] owner of each descriptor (routing scratch only)
+  unsigned long long* route_hash;    // [n] its stem hash (routing scratch only)
   uint32_t* route_hist;              // [2 x RL_MAX_SHARDS x tiles] per-tile counts (routing scratch only)
   // routed owner batches (eng_route_owner)
   unsigned long long* r_base;        // [RL_MAX_SHARDS] received stem chunk starts per source

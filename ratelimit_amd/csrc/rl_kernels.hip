@@ -67,6 +67,7 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   // stats per source (rule' = source x rule_stride + rule).
   uint32_t s0 = 0, s1 = 0, u = 0, q = 0, fl = 0, rule = 0, hits = 0, limit = 0, dstat = 0, len = 0;
   int64_t tnow = 0;
+  unsigned long long whash = 0;
   bool layout_bad = false;
   if (i < b.n) {
     if (b.wire) {
@@ -89,6 +90,7 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
       rule = !b.rule_stride ? w.rule : w.rule >= b.rule_stride ? 0xFFFFFFFFu : src * b.rule_stride + w.rule;
       hits = w.hits;
       limit = w.limit;
+      whash = w.hash;
     } else {
       s0 = b.off[i];
       s1 = b.off[i + 1];
@@ -128,26 +130,35 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   }
   if (bad) atomicOr(err, bad);
 
+  auto emit_rec = [&](uint64_t h) {
+    keys[i] = (uint32_t)(h >> 32);
+    Rec r;
+    r.hlo = (uint32_t)h;
+    r.off = s0;
+    r.lu = len | (u << 16) | ((uint32_t)((fl & RL_FLAG_SHADOW) | (dstat ? FLAG_SKIP : 0u)) << 24);
+    r.rule = rule;
+    r.req = q;
+    r.now = (uint32_t)tnow;
+    r.hits = hits;
+    r.limit = limit;
+    rec[i] = r;
+    hit_a[i] = r.hits;
+    if (dstat && isolate) {  // answered here: the table kernels skip it
+      res[i] = pack_fail(dstat);
+      atomicOr(errs, dstat == RL_E_TIME ? ERR_TIME : ERR_INVALID);
+    }
+  };
+  // ---- a routed owner batch carries the sources' stem hashes: no stem read
+  if (b.wire) {
+    if (i < b.n) emit_rec(len ? whash : 0ull);
+    return;
+  }
+
   // ---- stage this block's stem bytes in LDS (uniform decision per block)
   const uint32_t b0 = blockIdx.x * 256;
   if (b0 >= b.n) return;  // whole block past the descriptors (request checks done)
   const uint32_t b1 = min(b0 + 256u, b.n);
-  uint32_t lo, hi, total;
-  if (b.wire) {  // (stems abut: the block's range runs from its first record's to the next block's)
-    total = b.stem_total;
-    const Wire w0 = b.wire[b0];
-    lo = (uint32_t)(((w0.label >> ROUTE_REQ_BITS) < b.n_src ? b.wbase[w0.label >> ROUTE_REQ_BITS] : 0ull) + w0.off);
-    if (b1 < b.n) {
-      const Wire w1 = b.wire[b1];
-      hi = (uint32_t)(((w1.label >> ROUTE_REQ_BITS) < b.n_src ? b.wbase[w1.label >> ROUTE_REQ_BITS] : 0ull) + w1.off);
-    } else {
-      hi = total;
-    }
-  } else {
-    lo = b.off[b0];
-    hi = b.off[b1];
-    total = b.off[b.n];
-  }
+  const uint32_t lo = b.off[b0], hi = b.off[b1], total = b.off[b.n];
   const bool range_ok = hi >= lo && hi <= b.stem_cap && total <= b.stem_cap;
   const uint32_t* words = reinterpret_cast<const uint32_t*>(b.stem);  // 4-byte aligned base
   const uint32_t lead = lo & 3u;
@@ -162,33 +173,15 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   __syncthreads();
   if (i >= b.n) return;
   uint64_t h = 0;
-  if (len && range_ok && s0 + len <= total && s0 >= lo && s0 + len <= hi) {
+  if (len && range_ok && s0 + len <= total) {
     if (use_lds) {
       h = hash_stem(b.hk, DwordReader{lds, HASH_LDS_BYTES / 4 + 4}, s0 - lo + lead, len);
     } else {
       const uint32_t nw = ((total + 3u) >> 2) - (s0 >> 2);
       h = hash_stem(b.hk, DwordReader{words + (s0 >> 2), nw}, s0 & 3u, len);
     }
-  } else if (len && range_ok && s0 + len <= total) {
-    const uint32_t nw = ((total + 3u) >> 2) - (s0 >> 2);
-    h = hash_stem(b.hk, DwordReader{words + (s0 >> 2), nw}, s0 & 3u, len);
   }
-  keys[i] = (uint32_t)(h >> 32);
-  Rec r;
-  r.hlo = (uint32_t)h;
-  r.off = s0;
-  r.lu = len | (u << 16) | ((uint32_t)((fl & RL_FLAG_SHADOW) | (dstat ? FLAG_SKIP : 0u)) << 24);
-  r.rule = rule;
-  r.req = q;
-  r.now = (uint32_t)tnow;
-  r.hits = hits;
-  r.limit = limit;
-  rec[i] = r;
-  hit_a[i] = r.hits;
-  if (dstat && isolate) {  // answered here: the table kernels skip it
-    res[i] = pack_fail(dstat);
-    atomicOr(errs, dstat == RL_E_TIME ? ERR_TIME : ERR_INVALID);
-  }
+  emit_rec(h);
 }
 
 // The zero-padded first KEY_HEAD bytes of the stem at byte `off` of the packed

@@ -33,14 +33,18 @@ __device__ inline uint32_t owner_of(uint64_t h, uint32_t n_shards) {
 // ---- source side ----------------------------------------------------------
 // Partition of a slice by owner, in three launches over tiles of RP_TILE
 // descriptors (all HBM-streaming; the byte moves go through LDS):
-//   k_rp_count  hash -> owner per descriptor (dest, u8), per-tile record and
-//               stem-byte counts per owner;
+//   k_rp_count  keyed stem hash (kept for the wire record: owners never
+//               rehash) -> owner per descriptor (dest, u8), per-tile record
+//               and stem-byte counts per owner;
 //   k_rp_scan   per owner: exclusive scan of the tile counts, the totals
 //               (= the exchange counts);
 //   k_rp_pack   stable rank of each descriptor inside its tile and owner
 //               (wave ballots), its 32-B wire record and perm entry, and its
 //               stem bytes staged in LDS so that each owner's run of stems
 //               leaves the tile as whole dwords.
+#ifndef RL_RP_ABL
+#define RL_RP_ABL 0  // measurement builds: 1 = no stem moves, 2 = no record stores
+#endif
 constexpr uint32_t RP_ITEMS = 2;
 constexpr uint32_t RP_TILE = 256 * RP_ITEMS;
 static_assert(RP_TILE == ROUTE_TILE, "scratch sizing");
@@ -59,22 +63,28 @@ __device__ inline uint32_t wave_incl(uint32_t v) {
   return v;
 }
 
-// Exclusive prefix over the 256 threads of a block of (a, b); returns the
-// block totals. tmp: 8 shared words.
+// Exclusive prefix over the NW x 64 threads of a block of (a, b); returns the
+// block totals. tmp: 2 x NW shared words.
+template <uint32_t NW>
 __device__ inline void block_excl2(uint32_t& a, uint32_t& b, uint32_t& ta, uint32_t& tb, uint32_t* tmp) {
   const uint32_t ia = wave_incl(a), ib = wave_incl(b), w = threadIdx.x >> 6;
   if (lane_id() == 63) {
     tmp[w] = ia;
-    tmp[4 + w] = ib;
+    tmp[NW + w] = ib;
   }
   __syncthreads();
   uint32_t pa = 0, pb = 0;
-  for (uint32_t k = 0; k < w; k++) {
-    pa += tmp[k];
-    pb += tmp[4 + k];
+  ta = tb = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < NW; k++) {
+    const uint32_t xa = tmp[k], xb = tmp[NW + k];
+    if (k < w) {
+      pa += xa;
+      pb += xb;
+    }
+    ta += xa;
+    tb += xb;
   }
-  ta = tmp[0] + tmp[1] + tmp[2] + tmp[3];
-  tb = tmp[4] + tmp[5] + tmp[6] + tmp[7];
   a = pa + ia - a;
   b = pb + ib - b;
   __syncthreads();
@@ -89,8 +99,8 @@ __device__ inline bool rp_bad(const BatchDev& b, uint32_t i, uint32_t total) {
 }
 
 __global__ __launch_bounds__(256) void k_rp_count(BatchDev b, uint32_t n_shards, uint32_t ntiles,
-                                                  uint8_t* __restrict__ dest, uint32_t* __restrict__ hist,
-                                                  uint32_t* err) {
+                                                  uint8_t* __restrict__ dest, unsigned long long* __restrict__ hash,
+                                                  uint32_t* __restrict__ hist, uint32_t* err) {
   __shared__ uint32_t cr[RL_MAX_SHARDS], cb[RL_MAX_SHARDS];
   for (uint32_t d = threadIdx.x; d < n_shards; d += 256) cr[d] = cb[d] = 0;
   __syncthreads();
@@ -101,19 +111,34 @@ __global__ __launch_bounds__(256) void k_rp_count(BatchDev b, uint32_t n_shards,
 #pragma unroll
   for (uint32_t t = 0; t < RP_ITEMS; t++) {
     const uint32_t i = blockIdx.x * RP_TILE + t * 256 + threadIdx.x;
-    if (i >= b.n) continue;
+    const bool valid = i < b.n;
     uint32_t d = 0, len = 0;
-    if (rp_bad(b, i, total)) {
-      bad = true;
-    } else {
-      const uint32_t s0 = b.off[i];
-      len = b.off[i + 1] - s0;
-      const uint64_t h = hash_stem(b.hk, DwordReader{words + (s0 >> 2), nw - (s0 >> 2)}, s0 & 3u, len);
-      d = owner_of(h, n_shards);
+    if (valid) {
+      if (rp_bad(b, i, total)) {
+        bad = true;
+      } else {
+        const uint32_t s0 = b.off[i];
+        len = b.off[i + 1] - s0;
+        const uint64_t h = hash_stem(b.hk, DwordReader{words + (s0 >> 2), nw - (s0 >> 2)}, s0 & 3u, len);
+        d = owner_of(h, n_shards);
+        hash[i] = h;
+      }
+      dest[i] = (uint8_t)d;
     }
-    dest[i] = (uint8_t)d;
-    atomicAdd(&cr[d], 1u);
-    atomicAdd(&cb[d], len);
+    // one LDS add per owner present in the wave (few owners: few adds)
+    uint64_t todo = __ballot(valid);
+    while (todo) {
+      const uint32_t leader = __ffsll((unsigned long long)todo) - 1;
+      const uint32_t dl = __shfl(d, leader, 64);
+      const bool mine = valid && d == dl;
+      const uint64_t mask = __ballot(mine);
+      const uint32_t bytes = wave_incl(mine ? len : 0u);
+      if (lane_id() == 63) {
+        atomicAdd(&cr[dl], (uint32_t)__popcll(mask));
+        atomicAdd(&cb[dl], bytes);
+      }
+      todo &= ~mask;
+    }
   }
   if (bad) atomicOr(err, ERR_INVALID);
   __syncthreads();
@@ -126,18 +151,18 @@ __global__ __launch_bounds__(256) void k_rp_count(BatchDev b, uint32_t n_shards,
 // One block per owner d: exclusive scans of its row of tile counts (records,
 // bytes); counts[2d], [2d+1] = the totals (zero when the slice is malformed,
 // so the exchange stays well-formed); tot[d], tot[n_shards + d] too.
-__global__ __launch_bounds__(256) void k_rp_scan(uint32_t* __restrict__ hist, uint32_t n_shards, uint32_t ntiles,
-                                                 unsigned long long* __restrict__ counts,
-                                                 uint32_t* __restrict__ tot, const uint32_t* err) {
-  __shared__ uint32_t tmp[8];
+__global__ __launch_bounds__(1024) void k_rp_scan(uint32_t* __restrict__ hist, uint32_t n_shards, uint32_t ntiles,
+                                                  unsigned long long* __restrict__ counts,
+                                                  uint32_t* __restrict__ tot, const uint32_t* err) {
+  __shared__ uint32_t tmp[32];
   const uint32_t d = blockIdx.x;
   uint32_t* rr = hist + (size_t)d * ntiles;
   uint32_t* rb = hist + ((size_t)n_shards + d) * ntiles;
   uint32_t ca = 0, cb = 0;
-  for (uint32_t base = 0; base < ntiles; base += 256) {
+  for (uint32_t base = 0; base < ntiles; base += 1024) {
     const uint32_t j = base + threadIdx.x;
     uint32_t a = j < ntiles ? rr[j] : 0u, bb = j < ntiles ? rb[j] : 0u, ta, tb;
-    block_excl2(a, bb, ta, tb, tmp);
+    block_excl2<16>(a, bb, ta, tb, tmp);
     if (j < ntiles) {
       rr[j] = ca + a;
       rb[j] = cb + bb;
@@ -155,7 +180,9 @@ __global__ __launch_bounds__(256) void k_rp_scan(uint32_t* __restrict__ hist, ui
 }
 
 __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, uint32_t ntiles, uint32_t src_rank,
-                                                 const uint8_t* __restrict__ dest, const uint32_t* __restrict__ hist,
+                                                 const uint8_t* __restrict__ dest,
+                                                 const unsigned long long* __restrict__ hash,
+                                                 const uint32_t* __restrict__ hist,
                                                  const uint32_t* __restrict__ tot, Wire* __restrict__ out,
                                                  uint8_t* __restrict__ out_stem, uint32_t* __restrict__ perm,
                                                  const uint32_t* err) {
@@ -182,7 +209,7 @@ __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, 
     sa = ra;
     sbb = rb;
     uint32_t ta, tbb;
-    block_excl2(sa, sbb, ta, tbb, tmp);
+    block_excl2<4>(sa, sbb, ta, tbb, tmp);
     if (d < n_shards) {
       gr[d] = sa + hist[(size_t)d * ntiles + tile];
       sb[d] = sbb;
@@ -245,7 +272,7 @@ __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, 
       byt = ab;
     }
     uint32_t dummy = 0, t1, t2;
-    block_excl2(byt, dummy, t1, t2, tmp);
+    block_excl2<4>(byt, dummy, t1, t2, tmp);
     if (d < n_shards) lo[d] = byt;
     if (d == 0) tmp[0] = t1;  // the tile's stem bytes
   }
@@ -269,9 +296,15 @@ __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, 
     x.hits = b.hits[i];
     x.rule = b.rule[i];
     x.now = b.now[q];
+    x.hash = hash[i];
+#if !(RL_RP_ABL & 2)
     out[j] = x;
     perm[j] = i;
+#endif
     const uint32_t s0 = b.off[i];
+#if RL_RP_ABL & 1
+    continue;
+#endif
     if (staged) {
       uint8_t* dst = stage + lo[d] + wb[w][d] + my_b[t];
       for (uint32_t k = 0; k < len; k += 4) {
@@ -353,10 +386,11 @@ void launch_stats_sum(const unsigned long long* stage, uint32_t n_blocks, uint32
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
                        uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st) {
   const uint32_t ntiles = b.n ? cdiv(b.n, RP_TILE) : 0u;
-  if (b.n) k_rp_count<<<ntiles, 256, 0, st>>>(b, n_shards, ntiles, s.route_dest, s.route_hist, s.err);
-  k_rp_scan<<<n_shards, 256, 0, st>>>(s.route_hist, n_shards, ntiles, counts, s.route_start, s.err);
+  if (b.n) k_rp_count<<<ntiles, 256, 0, st>>>(b, n_shards, ntiles, s.route_dest, s.route_hash, s.route_hist, s.err);
+  k_rp_scan<<<n_shards, 1024, 0, st>>>(s.route_hist, n_shards, ntiles, counts, s.route_start, s.err);
   if (b.n)
-    k_rp_pack<<<ntiles, 256, 0, st>>>(b, n_shards, ntiles, src_rank, s.route_dest, s.route_hist, s.route_start, out,
+    k_rp_pack<<<ntiles, 256, 0, st>>>(b, n_shards, ntiles, src_rank, s.route_dest, s.route_hash, s.route_hist,
+                                      s.route_start, out,
                                       out_stem, perm, s.err);
 }
 

@@ -5,7 +5,8 @@ box that is DeviceRouteOps (rl_route_* kernels). Here the same protocol runs
 over gloo with numpy packing and the C oracle as each owner's table, so the
 host-side exchange (split sizes, ordering across ranks, inverse routing,
 stats all_reduce, error agreement) is tested without a GPU. The wire layout is
-the C ABI's (RL_WIRE_BYTES records: label, off, lu, limit, hits, rule, now).
+the C ABI's (RL_WIRE_BYTES records: label, off, lu, limit, hits, rule, now,
+stem hash; the CPU owners here do not read the hash and it is left 0).
 """
 import zlib
 
@@ -17,8 +18,8 @@ from ratelimit_amd import abi
 from ratelimit_amd._lib import RedisError
 
 WIRE = np.dtype([("label", "<u4"), ("off", "<u4"), ("lu", "<u4"), ("limit", "<u4"), ("hits", "<u4"),
-                 ("rule", "<u4"), ("now", "<i8")])
-assert WIRE.itemsize == 32
+                 ("rule", "<u4"), ("now", "<i8"), ("hash", "<u8")])
+assert WIRE.itemsize == 40
 
 
 def owner_of(stem: bytes, world: int) -> int:
@@ -46,12 +47,12 @@ class CpuRouteOps:
             s = stems[e]
             q = int(a["req_idx"][e])
             rec[j] = ((rank << 24) | q, chunk_off[d], len(s) | (int(a["unit"][e]) << 16) | (int(a["flags"][e]) << 24),
-                      a["limit"][e], a["hits"][e], a["rule_id"][e], a["now"][q])
+                      a["limit"][e], a["hits"][e], a["rule_id"][e], a["now"][q], 0)
             chunk_off[d] += len(s)
             counts[d, 0] += 1
             counts[d, 1] += len(s)
             blob += s
-        send_rec[:n * 32].copy_(torch.from_numpy(rec.view(np.uint8).copy()))
+        send_rec[:n * WIRE.itemsize].copy_(torch.from_numpy(rec.view(np.uint8).copy()))
         if blob:
             send_stem[:len(blob)].copy_(torch.from_numpy(np.frombuffer(bytes(blob), np.uint8).copy()))
         perm[:n].copy_(torch.from_numpy(order.astype(np.int32)))
@@ -59,7 +60,7 @@ class CpuRouteOps:
 
     def owner(self, n, recv_rec, recv_stem, stem_bytes, src_base, world, n_rules, ret, stats, isolate, slot):
         assert not isolate, "per-descriptor statuses: GPU tests only"
-        rec = recv_rec[:n * 32].numpy().view(WIRE)
+        rec = recv_rec[:n * WIRE.itemsize].numpy().view(WIRE)
         blob = recv_stem[:stem_bytes].numpy()
         src = rec["label"] >> 24
         starts = np.asarray(src_base, np.int64)[src] + rec["off"]
