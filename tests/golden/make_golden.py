@@ -136,9 +136,35 @@ lc.append({
     "expect_stats": {"key4_value4": stats(total_hits=4, over_limit=2, over_limit_with_local_cache=1,
                                           near_limit=1, within_limit=2)},
 })
+# localCacheStats gauges after each step (testLocalCacheStats(hit, miss, lookup,
+# expired, entry), fixed_cache_impl_test.go:218,239,260,279). freecache v1.1.0
+# (go.mod:9, not vendored) counts LookupCount = HitCount + MissCount, and every
+# DoLimit of a non-empty key makes one Get (IsOverLimitWithLocalCache,
+# base_limiter.go:63-72). The vector at :260, (0, 2, 3, 0, 1), is not reachable:
+# its lookup 3 needs hit + miss = 3, and :279's (1, 3, 4) needs miss 3 already.
+# testLocalCacheStats returns a func(*testing.T) that the test never runs
+# (:143-145), so the reference never checks it; the executed semantics give
+# (0, 3, 3, 0, 1), kept here with the transcribed vector beside it.
+# expiredCount is freecache's own bookkeeping (entries found stale on access),
+# 0 in every vector; the backend reports entry/lookup/hit/miss.
+KEY4_GAUGES = [((0, 1, 1, 0, 0), None), ((0, 2, 2, 0, 0), None), ((0, 3, 3, 0, 1), (0, 2, 3, 0, 1)),
+               ((1, 3, 4, 0, 1), None)]
+
+
+def with_gauges(steps, lines):
+    for step, ((h, m, lk, ex, en), ref), line in zip(steps, KEY4_GAUGES, lines):
+        g = {"hit_count": h, "miss_count": m, "lookup_count": lk, "entry_count": en, "source_line": line}
+        if ref is not None:
+            g["reference_vector"] = list(ref)
+            g["note"] = "unreachable as transcribed (lookup != hit + miss); never executed by the reference"
+        step["expect_gauges"] = g
+    return steps
+
+
 fixtures["ref_over_limit_with_local_cache"] = {
     "source": "test/redis/fixed_cache_impl_test.go:179-280", "kind": "do_limit",
-    "config": cfg(local_cache=True), "steps": lc}
+    "config": cfg(local_cache=True),
+    "steps": with_gauges(lc, ["fixed_cache_impl_test.go:%d" % x for x in (218, 239, 260, 279)])}
 
 lcs = key4_steps(True, True)
 # :569-586: shadow rule in the local cache: INCRBY skipped, result 0 -> OK with the full limit
@@ -153,7 +179,8 @@ lcs.append({
 })
 fixtures["ref_over_limit_with_local_cache_shadow_rule"] = {
     "source": "test/redis/fixed_cache_impl_test.go:485-590", "kind": "do_limit",
-    "config": cfg(local_cache=True), "steps": lcs}
+    "config": cfg(local_cache=True),
+    "steps": with_gauges(lcs, ["fixed_cache_impl_test.go:%d" % x for x in (524, 545, 567, 589)])}
 
 # ---------------------------------------------------------------- near limit
 nl = key4_steps(False, False)
@@ -279,12 +306,15 @@ def integration_steps(local_cache):
     s = []
     # :383-393 unknown domain "foo" -> nil limit
     s.append({"now": now, "seed": [], "request": req("foo", [[["hello", "world"]]], 1), "limits": [None],
-              "expect_statuses": [st(OK, None, 0, None)], "expect_stats": {}})
+              "expect_statuses": [st(OK, None, 0, None)], "expect_stats": {},
+              "expect_gauges": {"hit_count": 0, "miss_count": 0, "source_line": "integration_test.go:397-401"}})
     # :405-420 basic/key1 (second, 50)
     s.append({"now": now, "seed": [], "request": req("basic", [[["key1", "foo"]]], 1),
               "limits": [lim(50, SEC, "basic.key1")],
               "expect_statuses": [st(OK, [50, SEC], 49, reset(SEC, now))],
-              "expect_stats": {"basic.key1": stats(total_hits=1)}})
+              "expect_stats": {"basic.key1": stats(total_hits=1)},
+              "expect_gauges": {"hit_count": 0, "miss_count": 1 if local_cache else 0,
+                                "source_line": "integration_test.go:425-433"}})
     # :434-496 25x another/key2 (minute, 20)
     for i in range(25):
         code, rem = (OVER, 0) if i >= 20 else (OK, 20 - (i + 1))
@@ -293,7 +323,10 @@ def integration_steps(local_cache):
         s.append({"now": now, "seed": [], "request": req("another", [[["key2", "rand1"]]], 1),
                   "limits": [lim(20, MIN, "another.key2")],
                   "expect_statuses": [st(code, [20, MIN], rem, reset(MIN, now))],
-                  "expect_stats": {"another.key2": e}})
+                  "expect_stats": {"another.key2": e},
+                  "expect_gauges": {"hit_count": (i - 20) if (local_cache and i >= 20) else 0,
+                                    "miss_count": ((i + 2) if i < 20 else 22) if local_cache else 0,
+                                    "source_line": "integration_test.go:479-495"}})
     # :498-583 15x another/{key2 (minute, 20), key3 (hour, 10)}
     for i in range(15):
         code3, rem3 = (OVER, 0) if i >= 10 else (OK, 10 - (i + 1))
@@ -306,7 +339,10 @@ def integration_steps(local_cache):
                       "another.key2": stats(total_hits=i + 26, over_limit=5,
                                             over_limit_with_local_cache=4 if local_cache else 0),
                       "another.key3": stats(total_hits=i + 1, over_limit=(i - 9) if i >= 10 else 0,
-                                            over_limit_with_local_cache=(i - 10) if (local_cache and i >= 10) else 0)}})
+                                            over_limit_with_local_cache=(i - 10) if (local_cache and i >= 10) else 0)},
+                  "expect_gauges": {"hit_count": ((4 if i < 10 else i - 6) if local_cache else 0),
+                                    "miss_count": ((i * 2 + 24 if i < 10 else i + 34) if local_cache else 0),
+                                    "source_line": "integration_test.go:559-582"}})
     # :585-596 DurationUntilReset decreases between two hits 2 s apart (day unit, 20)
     s.append({"now": now, "seed": [], "request": req("another", [[["key4", "durTest"]]], 1),
               "limits": [lim(20, DAY, "another.key4")],

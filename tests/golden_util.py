@@ -67,3 +67,21 @@ def check_stats(reg, expect_stats):
         st = reg.get(key)
         for f, v in fields.items():
             assert getattr(st, f) == v, "%s.%s = %d, expected %d" % (key, f, getattr(st, f), v)
+
+
+GAUGES = ("hit_count", "miss_count", "lookup_count", "entry_count")
+
+
+def check_gauges(got, expect):
+    """localCacheStats gauges (local_cache_stats.go:36-43) against a step's expect_gauges."""
+    for g in GAUGES:
+        if g in expect:
+            assert got[g] == expect[g], "%s = %d, expected %d (%s)" % (g, got[g], expect[g], expect["source_line"])
+
+
+def oracle_gauges(cache, now):
+    lc = cache.local_cache
+    if lc is None:
+        return dict.fromkeys(GAUGES, 0)
+    return {"hit_count": lc.hit_count, "miss_count": lc.miss_count, "lookup_count": lc.hit_count + lc.miss_count,
+            "entry_count": lc.entry_count(now)}

@@ -53,6 +53,8 @@ def test_gpu_golden_do_limit(name):
             out = cache.do_limit(None, req, limits)
             assert [G.status_tuple(s) for s in out] == [G.expect_tuple(e) for e in step["expect_statuses"]]
             G.check_stats(reg, step["expect_stats"])
+            if "expect_gauges" in step:  # rl_local_cache_info_get (localCacheStats gauges)
+                G.check_gauges(cache.backend.local_cache_info(step["now"]), step["expect_gauges"])
     finally:
         cache.close()
 

@@ -33,6 +33,8 @@ def test_oracle_do_limit_fixture(name):
         out = cache.do_limit(req, limits, step["now"])
         assert [G.status_tuple(s) for s in out] == [G.expect_tuple(e) for e in step["expect_statuses"]]
         G.check_stats(reg, step["expect_stats"])
+        if "expect_gauges" in step:
+            G.check_gauges(G.oracle_gauges(cache, step["now"]), step["expect_gauges"])
         for client_name, cmds in step.get("expect_commands", {}).items():
             client = cache.client if client_name == "main" else cache.per_second_client
             assert [list(x) for x in client.log] == cmds
@@ -82,3 +84,22 @@ def test_oracle_near_threshold():
 def test_oracle_unknown_unit_panics():
     with pytest.raises(RuntimeError):
         O.unit_to_divider(O.UNIT_UNKNOWN)
+
+
+def test_gauge_vectors_present_and_the_unreachable_one_explained():
+    """integration_test.go:397-582 and fixed_cache_impl_test.go:218-279 / :524-589
+    are transcribed; the one vector that breaks lookup = hit + miss keeps its
+    transcription beside the executed value."""
+    n = 0
+    for name in G.names("do_limit"):
+        for step in G.load(name)["steps"]:
+            g = step.get("expect_gauges")
+            if g is None:
+                continue
+            n += 1
+            if "lookup_count" in g:
+                assert g["lookup_count"] == g["hit_count"] + g["miss_count"]
+            if "reference_vector" in g:
+                h, m, lk = g["reference_vector"][:3]
+                assert lk != h + m and g["source_line"].endswith((":260", ":567"))
+    assert n == 5 * 42 + 2 * 4
