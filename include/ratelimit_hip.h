@@ -272,9 +272,13 @@ int rl_route_scatter(rl_ctx* ctx, uint32_t n, const uint32_t* perm, const uint64
  * rl_do_limit_routed_async (collective: every rank calls it the same number of
  * times in the same order; n may be 0) answers this rank's slice of the node
  * batch. Rank r's slice precedes rank r+1's in the global order (the order the
- * sequential INCRBY contract is kept in). Device arrays and the stream
- * semantics of rl_do_limit_async; the only host wait is for this batch's
- * partition counts. out->stats = the deltas of THIS rank's requests (summed
+ * sequential INCRBY contract is kept in). Device arrays. A call enqueues its
+ * batch's partition and counts exchange and completes the PREVIOUS batch, so
+ * the host never waits for work it just issued: the inputs may be reused once
+ * the work the call leaves on `stream` has run, the outputs of a batch are
+ * ready on `stream` after the NEXT call's work, or after rl_synchronize
+ * (collective too on such a ctx: it completes the last batch). Keep `out`
+ * valid until then. out->stats = the deltas of THIS rank's requests (summed
  * over ranks: the node's). Needs max_rules >= world x n_rules (an owner keeps
  * stats per source). A descriptor whose owner batch failed gets that
  * rl_status in out->status; without out->status it fails this rank's batch at

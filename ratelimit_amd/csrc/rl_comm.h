@@ -20,8 +20,10 @@ int comm_unique_id(uint8_t* id, std::string* err);
 CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t* id, std::string* err);
 void comm_destroy(CommRouter* r);
 // One routed batch: this rank's slice (device arrays) -> out in arrival order.
+// Enqueues the batch's first half and runs the previous batch's second half.
 int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, hipStream_t caller);
-// Wait for the router's streams (then the engine's own synchronize reports errors).
+// Completes the pending batch (collective) and waits for the router's streams
+// (then the engine's own synchronize reports errors).
 int comm_synchronize(CommRouter* r, Engine* e);
 
 }  // namespace rl
