@@ -251,6 +251,7 @@ def main():
         p99 = float(np.percentile(lat, 99))
 
     if rank != 0:
+        be.close()
         if routed:
             dist.destroy_process_group()
         return
@@ -295,6 +296,7 @@ def main():
         **({"route_host_ms_per_step": route_host} if py_route else {}),
     }
     print(json.dumps(line), flush=True)
+    be.close()
     if routed:
         dist.destroy_process_group()
 

@@ -31,6 +31,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -44,7 +46,7 @@ namespace rl {
 
 namespace {
 
-constexpr uint32_t RSLOTS = 3;
+constexpr uint32_t RSLOTS = 3;  // batches a router keeps in flight (slot reuse waits for the batch RSLOTS back)
 
 struct Rccl {
   bool ok = false;
@@ -131,7 +133,15 @@ struct CommRouter {
   unsigned long long* h_cnt = nullptr;  // pinned [RSLOTS][4 x world]
   std::vector<uint64_t> base;           // received chunk offsets in recv_stem (host)
   std::vector<uint64_t> so_r, so_b, ro_r;  // per-peer send / receive offsets (host)
+  // host seconds per phase (printed at destroy when RL_DEBUG_ROUTE_TIMING is set)
+  bool timing = false;
+  double t_first = 0, t_wait_counts = 0, t_owner = 0, t_second = 0;
+  uint64_t n_steps = 0;
 };
+
+inline double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 namespace {
 
@@ -229,7 +239,10 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, hipStream_t c
   const uint32_t W = r->world, me = r->rank, n = S.n, nr = S.n_rules;
   const uint32_t m = nr * RL_NUM_STATS;
   unsigned long long* h = r->h_cnt + (size_t)s * 4 * W;
+  const double t0 = now_s();
   CHK_HIP(e, hipEventSynchronize(S.packed));  // (issued one call ago)
+  const double t1 = now_s();
+  r->t_wait_counts += t1 - t0;
   h[2 * W + 2 * me] = h[2 * me];  // (own chunk)
   h[2 * W + 2 * me + 1] = h[2 * me + 1];
   uint64_t n_send = 0, n_recv = 0, b_recv = 0;
@@ -299,9 +312,12 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, hipStream_t c
   const uint32_t parts = (uint32_t)cut.size() - 1;
   if (parts > S.cap_parts) CHK_HIP(e, grow(r, S, 0, 0, parts));
   unsigned long long* ret_send = r->alias ? S.back : S.ret_send;  // (world 1: results land in place)
+  // world 1, one part: the scatter reads the owner batch's results directly
+  const bool direct = r->alias && parts == 1;
   const int isolate = S.out.status ? 1 : 0;
   S.k.assign(parts, 0);
   const size_t blk = (size_t)W * m;  // one part's per-source stats
+  const double t2 = now_s();
   for (uint32_t q = 0; q < parts; q++) {
     const uint64_t a = cut[q], b = cut[q + 1];
     const int rc = eng_route_owner(e, (uint32_t)(b - a), recv_rec + a, recv_stem, b_recv, r->base.data(), W, nr,
@@ -311,9 +327,12 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, hipStream_t c
     const uint32_t k = S.k[q];
     CHK_HIP(e, hipSetDevice(r->dev));
     CHK_HIP(e, hipStreamWaitEvent(r->ret, e->b_done[k], 0));
+    if (direct) break;
     launch_route_ret(e->s[k].res, (uint32_t)(b - a), e->s[k].errb, ret_send + a, r->ret);
     CHK_HIP(e, hipEventRecord(e->consumed[k], r->ret));
   }
+  const double t3 = now_s();
+  r->t_owner += t3 - t2;
   // results and per-source stats back to their sources
   if (parts > 1 && m) launch_stats_sum(S.ostats, parts, (uint32_t)blk, S.ostats, r->ret);
   const unsigned long long* stats_in = S.ostats;  // (world 1: this rank's block is the owner's)
@@ -340,11 +359,20 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, hipStream_t c
   }
   const rl_result& out = S.out;
   OutDev o{out.code, out.limit_remaining, out.reset_s, (unsigned long long*)out.stats, out.status};
-  launch_route_scatter(S.perm, S.back, n, o, r->ret, isolate ? nullptr : e->errw + NBUF + 2);
+  uint32_t* src_err = isolate ? nullptr : e->errw + NBUF + 2;
+  if (direct) {
+    const uint32_t k = S.k[0];
+    launch_route_scatter(S.perm, e->s[k].res, n, o, r->ret, src_err, e->s[k].errb);
+    CHK_HIP(e, hipEventRecord(e->consumed[k], r->ret));
+  } else {
+    launch_route_scatter(S.perm, S.back, n, o, r->ret, src_err);
+  }
   if (m && out.stats) launch_stats_sum(stats_in, W, m, (unsigned long long*)out.stats, r->ret);
   CHK_HIP(e, hipGetLastError());
   CHK_HIP(e, hipEventRecord(S.done, r->ret));
   if (caller) CHK_HIP(e, hipStreamWaitEvent(caller, S.done, 0));
+  r->t_second += now_s() - t1;
+  r->n_steps++;
   return RL_OK;
 }
 
@@ -385,6 +413,7 @@ CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t*
   const rl_config& g = e->cfg;
   r->part_max = g.max_batch;
   r->alias = world == 1 && !getenv("RL_DEBUG_ROUTE_NOALIAS");
+  r->timing = getenv("RL_DEBUG_ROUTE_TIMING") != nullptr;
   if (const char* pm = getenv("RL_DEBUG_OWNER_PART"))
     r->part_max = std::max<uint32_t>(1, std::min<uint32_t>(g.max_batch, (uint32_t)atoi(pm)));
   bool ok = hipSetDevice(r->dev) == hipSuccess;
@@ -428,6 +457,11 @@ CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t*
 
 void comm_destroy(CommRouter* r) {
   if (!r) return;
+  if (r->timing && r->n_steps)
+    fprintf(stderr, "{\"route_host_us\": {\"first_half\": %.1f, \"wait_counts\": %.1f, \"owner_enqueue\": %.1f, "
+                    "\"second_half\": %.1f, \"batches\": %llu}}\n",
+            r->t_first / r->n_steps * 1e6, r->t_wait_counts / r->n_steps * 1e6, r->t_owner / r->n_steps * 1e6,
+            r->t_second / r->n_steps * 1e6, (unsigned long long)r->n_steps);
   (void)hipSetDevice(r->dev);
   for (hipStream_t st : {r->cs, r->fwd, r->ret})
     if (st) (void)hipStreamSynchronize(st);
@@ -468,7 +502,9 @@ int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, 
   S.out = *out;
   S.n = n;
   S.n_rules = nr;
+  const double t0 = now_s();
   int rc = first_half(r, e, S, s, in, caller);
+  r->t_first += now_s() - t0;
   if (rc) return rc;
   // the previous batch: its counts had a whole call to arrive
   if (r->pending >= 0) {

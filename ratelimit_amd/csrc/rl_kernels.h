@@ -191,9 +191,11 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
                        uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st);
 // src_err (optional): without o.status, a returned failure status sets its
-// error bit there (the source's batch then fails at rl_synchronize).
+// error bit there (the source's batch then fails at rl_synchronize). errb
+// (optional): ret is an owner batch's own results; a failed batch (*errb)
+// answers every record with its status, as k_route_ret does.
 void launch_route_scatter(const uint32_t* perm, const unsigned long long* ret, uint32_t n, const OutDev& o,
-                          hipStream_t st, uint32_t* src_err = nullptr);
+                          hipStream_t st, uint32_t* src_err = nullptr, const uint32_t* errb = nullptr);
 // Owner side: ret[i] = res[i], or every record failed with the status of
 // *errb when the batch's table stage failed.
 void launch_route_ret(const unsigned long long* res, uint32_t n, const uint32_t* errb, unsigned long long* ret,

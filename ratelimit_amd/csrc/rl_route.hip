@@ -346,11 +346,12 @@ __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, 
 
 __global__ __launch_bounds__(256) void k_route_scatter(const uint32_t* __restrict__ perm,
                                                        const unsigned long long* __restrict__ ret, uint32_t n,
-                                                       OutDev o, uint32_t* src_err) {
+                                                       OutDev o, uint32_t* src_err, const uint32_t* errb) {
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
   const uint32_t e = perm[j];
-  const unsigned long long v = ret[j];
+  const uint32_t fail = errb ? *errb : 0u;  // (results straight from an owner batch: k_route_ret's check)
+  const unsigned long long v = fail ? pack_fail(err_status(fail)) : ret[j];
   o.code[e] = (uint8_t)res_code(v);
   o.rem[e] = res_rem(v);
   o.reset[e] = res_reset(v);
@@ -395,8 +396,8 @@ void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, 
 }
 
 void launch_route_scatter(const uint32_t* perm, const unsigned long long* ret, uint32_t n, const OutDev& o,
-                          hipStream_t st, uint32_t* src_err) {
-  if (n) k_route_scatter<<<cdiv(n, 256), 256, 0, st>>>(perm, ret, n, o, src_err);
+                          hipStream_t st, uint32_t* src_err, const uint32_t* errb) {
+  if (n) k_route_scatter<<<cdiv(n, 256), 256, 0, st>>>(perm, ret, n, o, src_err, errb);
 }
 
 void launch_route_ret(const unsigned long long* res, uint32_t n, const uint32_t* errb, unsigned long long* ret,
