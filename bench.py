@@ -171,11 +171,15 @@ def main():
     rng = np.random.default_rng((0xC2 if args.config == "c2" else 0xC1) + 7919 * rank)
     sampler = W.ZipfSampler(world * T, 1.1) if args.config == "c2" else None
     dev_batches = []
+    uniq = []  # descriptors whose key occurs once in the batch (k_unique's share)
     for _ in range(args.distinct_batches):
+        ten = rng.integers(0, world * T, nq) if sampler is None else sampler.sample(rng, nq)
         if sampler is None:
-            a, bn, bq, br = W.c1_batch(rng.integers(0, world * T, nq), now0)
+            a, bn, bq, br = W.c1_batch(ten, now0)
         else:
-            a, bn, bq, br = W.c1_batch(sampler.sample(rng, nq), now0, rng.integers(1, 9, nq).astype(np.uint32))
+            a, bn, bq, br = W.c1_batch(ten, now0, rng.integers(1, 9, nq).astype(np.uint32))
+        _, cnt = np.unique(ten, return_counts=True)
+        uniq.append(2 * int((cnt == 1).sum()))  # (both units of a tenant seen once)
         a.pop("now")
         dev_batches.append(to_dev(a, torch))
     stem_len = 34
@@ -226,6 +230,7 @@ def main():
     stage_ms, nb = be.profile_read()
     be.profile(False)
     stage_avg = {k: v / max(nb, 1) for k, v in stage_ms.items()}
+    n_unique = float(np.mean(uniq)) if world == 1 else None  # (routed: each owner's share is not tracked)
     n_owner = float(np.mean(recv)) if recv else float(n)
     if routed:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
@@ -256,20 +261,24 @@ def main():
             dist.destroy_process_group()
         return
 
-    b_alg = stem_len + 10 + 16 + 12 + 64  # key = stem + 10-digit window
-    runs_ms = stage_avg["runs"]
-    achieved = b_alg * n_owner / (runs_ms * 1e-3) / 1e9 if runs_ms > 0 else None
+    # k_unique answers the keys seen once in the batch (FLAG_DUP clear): the
+    # bulk of C1/C3, a share of C2. SURVEY §8(d): 136 B per decision (key =
+    # stem + 10-digit window, slot 64 B read, 16 B window write-back, 12 B out).
+    b_alg = stem_len + 10 + 16 + 12 + 64
+    uniq_ms = stage_avg["unique"]
+    achieved = b_alg * n_unique / (uniq_ms * 1e-3) / 1e9 if (uniq_ms > 0 and n_unique) else None
     pipe_ms = elapsed / args.steps * 1e3
     traffic = None
     tp = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
     if os.path.exists(tp) and not routed:
         try:
-            traffic = json.load(open(tp)).get("k_runs_bytes_per_launch")
+            traffic = json.load(open(tp)).get("k_unique_bytes_per_launch")
         except Exception:
             traffic = None
-    roofline = {"bound": "hbm", "kernel": "k_runs", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    roofline = {"bound": "hbm", "kernel": "k_unique", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                "bytes_alg_per_decision": b_alg, "decisions_per_launch": n_owner,
+                "bytes_alg_per_decision": b_alg, "decisions_per_launch": n_unique,
+                "descriptors_per_batch": n_owner,
                 "stage_ms": {k: round(v, 4) for k, v in stage_avg.items()},
                 "pipeline_achieved": b_alg * n_owner / (pipe_ms * 1e-3) / 1e9 if pipe_ms > 0 else None}
 

@@ -22,11 +22,21 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A bindable port below the ephemeral range: an OS-assigned port could be
+    handed to another socket (RCCL's bootstrap binds ephemeral ones) between
+    this probe and the rendezvous store's bind."""
+    import random
+    for _ in range(200):
+        p = random.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
+    raise RuntimeError("no free port")
 
 
 def _batches(seed, n_batches=6, calls_per_batch=40, local_cache=False):
