@@ -268,15 +268,20 @@ def main():
     uniq_ms = stage_avg["unique"]
     achieved = b_alg * n_unique / (uniq_ms * 1e-3) / 1e9 if (uniq_ms > 0 and n_unique) else None
     pipe_ms = elapsed / args.steps * 1e3
-    traffic = None
+    traffic, traffic_cal = None, None
     tp = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
     if os.path.exists(tp) and not routed:
         try:
-            traffic = json.load(open(tp)).get("k_unique_bytes_per_launch")
+            tj = json.load(open(tp))
+            traffic = tj.get("k_unique_bytes_per_launch")  # 2 x FETCH_SIZE + WRITE_SIZE (guide)
+            rb = tj.get("k_unique_read_bytes_bounds")       # probe-calibrated reads (tools/pmcprobe.hip)
+            wr = tj["kernels"]["rl::k_unique"]["write_size_bytes"]
+            traffic_cal = [rb[0] + wr, rb[1] + wr] if rb else None
         except Exception:
-            traffic = None
+            traffic, traffic_cal = None, None
     roofline = {"bound": "hbm", "kernel": "k_unique", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                "traffic_calibrated_bounds": traffic_cal,
                 "bytes_alg_per_decision": b_alg, "decisions_per_launch": n_unique,
                 "descriptors_per_batch": n_owner,
                 "stage_ms": {k: round(v, 4) for k, v in stage_avg.items()},

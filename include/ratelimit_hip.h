@@ -183,8 +183,10 @@ const char* rl_last_error(const rl_ctx* ctx);
 int rl_do_limit(rl_ctx* ctx, const rl_batch* in, rl_result* out);
 
 /* Same, with every pointer in *in / *out in device memory of ctx's GPU
- * (shard_device[0] when n_shards > 1), enqueued on `stream` (a hipStream_t,
- * NULL = ctx's own streams, pipelined). Returns once the work is enqueued (a
+ * (shard_device[0] when n_shards > 1), enqueued on `stream` (a hipStream_t),
+ * or with NULL on the ctx's own streams, pipelined, after the work already on
+ * the default (null) stream; then read *out after rl_synchronize. Returns once
+ * the work is enqueued (a
  * multi-shard ctx first waits for this batch's owner partition, never for the
  * owners' pipelines); errors detected on the GPU surface at rl_synchronize.
  * stem_bytes must be 4-byte aligned (any hipMalloc / torch allocation is). */

@@ -320,7 +320,8 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && dalloc(&c->errw, NBUF + 3) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++)
     ok = ok && hipEventCreateWithFlags(&c->consumed[k], hipEventDisableTiming) == hipSuccess;
-  ok = ok && hipEventCreateWithFlags(&c->route_ready, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&c->route_ready, hipEventDisableTiming) == hipSuccess &&
+       hipEventCreateWithFlags(&c->caller_ready, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_base, (size_t)NBUF * RL_MAX_SHARDS * 8) == hipSuccess;
   ok = ok && dalloc(&s0.stripes, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS) == hipSuccess;
   ok = ok && dalloc(&s0.time_floor, 1) == hipSuccess;
@@ -383,6 +384,7 @@ void eng_destroy(Engine* c) {
     scratch_free(c->rs);
   }
   if (c->route_ready) (void)hipEventDestroy(c->route_ready);
+  if (c->caller_ready) (void)hipEventDestroy(c->caller_ready);
   if (c->h_base) (void)hipHostFree(c->h_base);
   const Scratch& s0 = c->s[0];
   void* bufs[] = {c->slots, c->arena, c->arena2, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
@@ -412,7 +414,13 @@ int eng_do_limit_async(Engine* c, const rl_batch* in, rl_result* out, void* stre
   HIPCHK(c, hipSetDevice(c->cfg.device));
   BatchDev b = dev_view(c, in, c->cfg.max_stem_bytes);
   OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats, out->status};
-  // NULL stream: pipelined on the ctx streams; otherwise serial on the caller's stream
+  // NULL stream: pipelined on the ctx streams, after the work already on the
+  // default (null) stream (the inputs' producer, e.g. torch's default stream);
+  // otherwise serial on the caller's stream
+  if (!stream) {
+    HIPCHK(c, hipEventRecord(c->caller_ready, nullptr));
+    HIPCHK(c, hipStreamWaitEvent(c->pipe[c->next], c->caller_ready, 0));
+  }
   enqueue(c, b, o, 0, (hipStream_t)stream, stream == nullptr);
   HIPCHK(c, hipGetLastError());
   c->batches++;
