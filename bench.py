@@ -85,6 +85,11 @@ def main():
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
     torch.cuda.set_device(local)
+    # every torch op and library call of the benchmark on one non-default
+    # stream: the library orders each batch after the work that produced its
+    # inputs on it (the default stream's handle is NULL: unordered)
+    main_stream = torch.cuda.Stream()
+    torch.cuda.set_stream(main_stream)
     routed = world > 1 or args.route
     if routed:
         if world == 1:
@@ -117,6 +122,8 @@ def main():
                          device="cpu" if args.dist_backend == "gloo" else "cuda")
         dist.broadcast(t, 0)
         seed = int(t.item())
+    if args.serial:  # isolated kernel timings: each batch's stages serially on the bench stream
+        os.environ["RL_DEBUG_SERIAL"] = "1"
     # a routed owner attributes stats per source rank: world x n_rules rule slots
     be = Backend(0.8, False, table_slots=slots, max_batch=cap, max_rules=max(8, 2 * world), device=local,
                  hash_seed=seed, max_stem_bytes=64 * cap)
@@ -139,14 +146,13 @@ def main():
            "reset_s": torch.empty(n, dtype=torch.int32, device="cuda"),
            "stats": torch.zeros(2 * 6, dtype=torch.int64, device="cuda")}
 
-    serial_torch_stream = torch.cuda.Stream() if args.serial else None  # (the default stream's handle is NULL)
-    serial_stream = serial_torch_stream.cuda_stream if args.serial else None
+    serial_stream = main_stream.cuda_stream
 
     def do_step(inp, bn, bq):
         if routed:
             sc.submit(inp, bn, bq, 2, out)
         else:
-            be.do_limit_device(inp, out, bn, bq, 2, stream=serial_stream)
+            be.do_limit_device(inp, out, bn, bq, 2, stream=serial_stream)  # (pipelined; --serial: RL_DEBUG_SERIAL)
 
     def sync():
         if routed:

@@ -183,10 +183,12 @@ const char* rl_last_error(const rl_ctx* ctx);
 int rl_do_limit(rl_ctx* ctx, const rl_batch* in, rl_result* out);
 
 /* Same, with every pointer in *in / *out in device memory of ctx's GPU
- * (shard_device[0] when n_shards > 1), enqueued on `stream` (a hipStream_t),
- * or with NULL on the ctx's own streams, pipelined, after the work already on
- * the default (null) stream; then read *out after rl_synchronize. Returns once
- * the work is enqueued (a
+ * (shard_device[0] when n_shards > 1), pipelined on the ctx's own streams.
+ * With `stream` (a hipStream_t) the batch starts after the work already on it
+ * (the inputs' producer); with NULL the inputs must be complete at the call.
+ * *out is read after rl_synchronize (the caller's stream is never made to wait
+ * for a batch, which would chain the next batch's inputs behind it and
+ * serialise the pipeline). Returns once the work is enqueued (a
  * multi-shard ctx first waits for this batch's owner partition, never for the
  * owners' pipelines); errors detected on the GPU surface at rl_synchronize.
  * stem_bytes must be 4-byte aligned (any hipMalloc / torch allocation is). */
@@ -274,13 +276,14 @@ int rl_route_scatter(rl_ctx* ctx, uint32_t n, const uint32_t* perm, const uint64
  * rl_do_limit_routed_async (collective: every rank calls it the same number of
  * times in the same order; n may be 0) answers this rank's slice of the node
  * batch. Rank r's slice precedes rank r+1's in the global order (the order the
- * sequential INCRBY contract is kept in). Device arrays. A call enqueues its
- * batch's partition and counts exchange and completes the PREVIOUS batch, so
- * the host never waits for work it just issued: the inputs may be reused once
- * the work the call leaves on `stream` has run, the outputs of a batch are
- * ready on `stream` after the NEXT call's work, or after rl_synchronize
- * (collective too on such a ctx: it completes the last batch). Keep `out`
- * valid until then. out->stats = the deltas of THIS rank's requests (summed
+ * sequential INCRBY contract is kept in). Device arrays; the batch starts
+ * after the work already on `stream` (NULL: inputs complete at the call). A
+ * call enqueues its batch's partition and counts exchange and completes the
+ * PREVIOUS batch, so the host never waits for work it just issued: a batch's
+ * inputs may be reused once the next call has returned, its outputs are read
+ * after rl_synchronize (collective too on such a ctx: it completes the last
+ * batch). Keep `out` valid until then. out->stats = the deltas of
+ * THIS rank's requests (summed
  * over ranks: the node's). Needs max_rules >= world x n_rules (an owner keeps
  * stats per source). A descriptor whose owner batch failed gets that
  * rl_status in out->status; without out->status it fails this rank's batch at

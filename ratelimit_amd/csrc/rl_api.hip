@@ -197,9 +197,10 @@ int routed_async(rl_ctx* c, const rl_batch* in, rl_result* out, hipStream_t call
   Engine* e0 = c->e[0];
   API_HIP(c, hipSetDevice(c->dev0));
   API_HIP(c, hipStreamWaitEvent(c->fwd, S.done, 0));  // the slot's previous batch is complete
-  // the inputs' producer: the caller's stream, or the default (null) stream
-  API_HIP(c, hipEventRecord(c->in_ready, caller));
-  API_HIP(c, hipStreamWaitEvent(c->fwd, c->in_ready, 0));
+  if (caller && hipStreamQuery(caller) == hipErrorNotReady) {  // the inputs' producer (still running)
+    API_HIP(c, hipEventRecord(c->in_ready, caller));
+    API_HIP(c, hipStreamWaitEvent(c->fwd, c->in_ready, 0));
+  }
   int rc = eng_route_pack(e0, in, N, 0, S.send_rec, S.send_stem, S.perm, (uint64_t*)S.counts, c->fwd);
   if (rc) return from_engine(c, e0, rc);
   unsigned long long* hc = c->h_counts + (size_t)s * 2 * MAX_LOCAL_SHARDS;
@@ -246,8 +247,7 @@ int routed_async(rl_ctx* c, const rl_batch* in, rl_result* out, hipStream_t call
   launch_route_scatter(S.perm, S.back, n, o, c->ret);
   if (m && out->stats) launch_stats_sum(S.stats_stage, N, m, (unsigned long long*)out->stats, c->ret);
   API_HIP(c, hipGetLastError());
-  API_HIP(c, hipEventRecord(S.done, c->ret));
-  if (caller) API_HIP(c, hipStreamWaitEvent(caller, S.done, 0));
+  API_HIP(c, hipEventRecord(S.done, c->ret));  // (outputs: read after rl_synchronize)
   return RL_OK;
 }
 

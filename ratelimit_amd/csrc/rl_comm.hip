@@ -203,12 +203,13 @@ hipError_t grow(CommRouter* r, CommSlot& S, uint64_t n_rec, uint64_t n_stem, uin
 }
 
 // First half of a batch (slot s): partition, counts exchange, counts to the
-// host. The caller's stream waits until the partition has read the inputs.
+// host. (The next call's second half waits on the host for this partition:
+// from then on the inputs may be reused.)
 int first_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, const rl_batch* in, hipStream_t caller) {
   Rccl& R = rccl();
   const uint32_t W = r->world, me = r->rank;
   CHK_HIP(e, hipStreamWaitEvent(r->cs, S.done, 0));  // the slot's previous batch is complete
-  if (caller) {
+  if (caller && hipStreamQuery(caller) == hipErrorNotReady) {  // the inputs' producer (still running)
     CHK_HIP(e, hipEventRecord(r->in_ready, caller));
     CHK_HIP(e, hipStreamWaitEvent(r->cs, r->in_ready, 0));
   }
@@ -227,14 +228,12 @@ int first_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, const rl_batch
   }
   CHK_HIP(e, hipMemcpyAsync(r->h_cnt + (size_t)s * 4 * W, S.cnt, 4ull * W * 8, hipMemcpyDeviceToHost, r->cs));
   CHK_HIP(e, hipEventRecord(S.packed, r->cs));
-  if (caller) CHK_HIP(e, hipStreamWaitEvent(caller, S.packed, 0));  // (inputs consumed)
   return RL_OK;
 }
 
 // Second half (slot s): records and stems to their owners, the owner
-// pipeline, results and per-source stats back, scatter. The caller's stream
-// then waits for the batch's outputs.
-int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, hipStream_t caller) {
+// pipeline, results and per-source stats back, scatter.
+int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
   Rccl& R = rccl();
   const uint32_t W = r->world, me = r->rank, n = S.n, nr = S.n_rules;
   const uint32_t m = nr * RL_NUM_STATS;
@@ -369,8 +368,7 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, hipStream_t c
   }
   if (m && out.stats) launch_stats_sum(stats_in, W, m, (unsigned long long*)out.stats, r->ret);
   CHK_HIP(e, hipGetLastError());
-  CHK_HIP(e, hipEventRecord(S.done, r->ret));
-  if (caller) CHK_HIP(e, hipStreamWaitEvent(caller, S.done, 0));
+  CHK_HIP(e, hipEventRecord(S.done, r->ret));  // (outputs: read after rl_synchronize)
   r->t_second += now_s() - t1;
   r->n_steps++;
   return RL_OK;
@@ -482,7 +480,7 @@ int comm_synchronize(CommRouter* r, Engine* e) {
   if (r->pending >= 0) {
     const uint32_t p = (uint32_t)r->pending;
     r->pending = -1;
-    const int rc = second_half(r, e, r->slot[p], p, nullptr);
+    const int rc = second_half(r, e, r->slot[p], p);
     if (rc) return rc;
   }
   for (hipStream_t st : {r->cs, r->fwd, r->ret}) CHK_HIP(e, hipStreamSynchronize(st));
@@ -510,7 +508,7 @@ int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, 
   if (r->pending >= 0) {
     const uint32_t p = (uint32_t)r->pending;
     r->pending = -1;
-    rc = second_half(r, e, r->slot[p], p, caller);
+    rc = second_half(r, e, r->slot[p], p);
     if (rc) return rc;
   }
   r->pending = (int)s;

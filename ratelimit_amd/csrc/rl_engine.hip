@@ -322,6 +322,7 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
     ok = ok && hipEventCreateWithFlags(&c->consumed[k], hipEventDisableTiming) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&c->route_ready, hipEventDisableTiming) == hipSuccess &&
        hipEventCreateWithFlags(&c->caller_ready, hipEventDisableTiming) == hipSuccess;
+  c->serial_debug = getenv("RL_DEBUG_SERIAL") != nullptr;
   ok = ok && hipHostMalloc((void**)&c->h_base, (size_t)NBUF * RL_MAX_SHARDS * 8) == hipSuccess;
   ok = ok && dalloc(&s0.stripes, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS) == hipSuccess;
   ok = ok && dalloc(&s0.time_floor, 1) == hipSuccess;
@@ -414,14 +415,24 @@ int eng_do_limit_async(Engine* c, const rl_batch* in, rl_result* out, void* stre
   HIPCHK(c, hipSetDevice(c->cfg.device));
   BatchDev b = dev_view(c, in, c->cfg.max_stem_bytes);
   OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats, out->status};
-  // NULL stream: pipelined on the ctx streams, after the work already on the
-  // default (null) stream (the inputs' producer, e.g. torch's default stream);
-  // otherwise serial on the caller's stream
-  if (!stream) {
-    HIPCHK(c, hipEventRecord(c->caller_ready, nullptr));
-    HIPCHK(c, hipStreamWaitEvent(c->pipe[c->next], c->caller_ready, 0));
+  // Pipelined on the ctx streams. With a caller stream, after the work already
+  // on it (the inputs' producer); NULL: the caller completes the inputs first.
+  // Either way *out is read after rl_synchronize: ordering the caller's stream
+  // after each batch would chain the next batch's inputs behind this batch's
+  // stage B and serialise the pipeline. RL_DEBUG_SERIAL: every stage on the
+  // caller's stream, one batch at a time (isolated kernel timings).
+  hipStream_t st = (hipStream_t)stream;
+  if (st && c->serial_debug) {
+    enqueue(c, b, o, 0, st, false);
+  } else {
+    // (an idle caller stream needs no event: a cross-stream wait can stall
+    // behind whatever shares the caller's hardware queue)
+    if (st && hipStreamQuery(st) == hipErrorNotReady) {
+      HIPCHK(c, hipEventRecord(c->caller_ready, st));
+      HIPCHK(c, hipStreamWaitEvent(c->pipe[c->next], c->caller_ready, 0));
+    }
+    enqueue(c, b, o, 0, nullptr, true);
   }
-  enqueue(c, b, o, 0, (hipStream_t)stream, stream == nullptr);
   HIPCHK(c, hipGetLastError());
   c->batches++;
   c->decisions += in->n;

@@ -118,7 +118,15 @@ class Backend:
         return self.do_limit_packed(PackedBatch(arrays, n, n_requests, n_rules), isolate)
 
     def do_limit_device(self, dev_in: dict, dev_out: dict, n, n_requests, n_rules, stream=None):
-        """All arrays are torch CUDA tensors (device memory); asynchronous."""
+        """All arrays are torch CUDA tensors (device memory); asynchronous and
+        pipelined; dev_out is read after synchronize(). `stream` (a hipStream_t
+        handle; default: torch's current stream) orders the batch after the
+        work producing its inputs. torch's default stream has the NULL handle,
+        which the library cannot order against cheaply: under it, the inputs
+        must be complete at the call."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream().cuda_stream
         b = abi.make_batch_struct(dev_in, n, n_requests, n_rules)
         r = abi.make_result_struct(dev_out)
         check(self.ctx, lib().rl_do_limit_async(self.ctx, C.byref(b), C.byref(r),

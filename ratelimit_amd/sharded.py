@@ -68,10 +68,9 @@ class RcclRouter:
     its slice (device tensors, the rl_batch / rl_result layout; a rank may
     pass n = 0). Results land in dev_out in arrival order; dev_out["stats"]
     (optional) receives the deltas of this rank's requests. A submit completes
-    the previous batch (the library never waits for work it just issued), so a
-    batch's dev_out is final after the next submit's work on the current stream
-    or after finish(), which every rank calls together: it completes the last
-    batch and raises RedisError if one failed on this rank.
+    the previous batch (the library never waits for work it just issued);
+    dev_out is final after finish(), which every rank calls together: it
+    completes the last batch and raises RedisError if one failed on this rank.
     """
 
     def __init__(self, backend, group=None):
