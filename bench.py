@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--prof-every", type=int, default=7,
                     help="time every k-th batch's stages with HIP events (k_runs' live time for the roofline)")
     ap.add_argument("--no-fill", action="store_true")
+    ap.add_argument("--pcie-steps", type=int, default=60, help="host-fed (PCIe) batches timed after the device phase")
     ap.add_argument("--slots-per-key", type=float, default=4.0, help="table slots per live key (power of 2 above)")
     ap.add_argument("--route", action="store_true", help="use the routed (all_to_all) path even at N=1")
     ap.add_argument("--route-impl", default="lib", choices=["lib", "python"],
@@ -178,6 +179,7 @@ def main():
     sampler = W.ZipfSampler(world * T, 1.1) if args.config == "c2" else None
     dev_batches = []
     uniq = []  # descriptors whose key occurs once in the batch (k_unique's share)
+    host_batches = []
     for _ in range(args.distinct_batches):
         ten = rng.integers(0, world * T, nq) if sampler is None else sampler.sample(rng, nq)
         if sampler is None:
@@ -187,6 +189,7 @@ def main():
         _, cnt = np.unique(ten, return_counts=True)
         uniq.append(2 * int((cnt == 1).sum()))  # (both units of a tenant seen once)
         a.pop("now")
+        host_batches.append((a, bn, bq))
         dev_batches.append(to_dev(a, torch))
     stem_len = 34
     total_steps = args.warmup + args.steps + args.steps + args.latency_steps
@@ -252,6 +255,7 @@ def main():
         sync()
         lat.append((time.perf_counter() - t1) * 1e3)
     lat = np.array(lat) if lat else np.array([float("nan")])
+    pcie = None if (routed or args.pcie_steps <= 0) else pcie_fed(args, be, host_batches, now0 + total_steps)
     info = be.table_info()
     if routed:
         lt = torch.tensor([float(np.percentile(lat, 99))], dtype=torch.float64,
@@ -311,7 +315,7 @@ def main():
                                       world, "RCCL send/recv routing inside the library" if not py_route else
                                       "all_to_all routing from Python (%s)" % args.dist_backend)) if routed else
                                   "single GPU"},
-        "p50_batch_ms": float(np.percentile(lat, 50)), "p99_batch_ms": p99,
+        "p50_batch_ms": float(np.percentile(lat, 50)), "p99_batch_ms": p99, "pcie_fed": pcie,
         "roofline": roofline, "cpu_baseline": cpu, "fill_s": round(t_fill, 2),
         **({"route_host_ms_per_step": route_host} if py_route else {}),
     }
@@ -319,6 +323,69 @@ def main():
     be.close()
     if routed:
         dist.destroy_process_group()
+
+
+def pcie_fed(args, be, host_batches, now):
+    """The same batches fed from page-locked host memory (rl_do_limit_host_async):
+    inputs cross PCIe while earlier batches compute, outputs come back
+    (code, remaining, reset). SURVEY §8(d): with requests arriving in host
+    memory, PCIe is the honest bound. Rate over args.pcie_steps queued batches,
+    then per-batch latency (submit -> outputs on the host)."""
+    from ratelimit_amd.limiter import PinnedArena
+    from ratelimit_amd.packing import PackedBatch
+    arena = PinnedArena()
+    fed = []
+    for a, bn, bq in host_batches:
+        arr = {k: arena.like(v) for k, v in a.items()}
+        arr["now"] = arena.like(np.full(bq, now, np.int64))  # (time holds: one second for the whole phase)
+        fed.append(PackedBatch(arr, bn, bq, 2))
+    outs = [{k: arena.like(v) for k, v in fed[0].alloc_result().items()} for _ in range(4)]
+    n = fed[0].n
+    bytes_in = sum(int(v.nbytes) for k, v in fed[0].arrays.items() if k != "stem_bytes") + \
+        int(fed[0].arrays["stem_off"][n])
+    bytes_out = n * 9
+    keep = []
+
+    def submit(s):
+        keep.append(be.do_limit_host_async(fed[s % len(fed)], outs[s % len(outs)]))
+
+    for s in range(3):
+        submit(s)
+    be.synchronize()
+    keep.clear()
+    t0 = time.perf_counter()
+    for s in range(args.pcie_steps):
+        submit(s)
+    be.synchronize()
+    el = time.perf_counter() - t0
+    keep.clear()
+    lat = []
+    for s in range(20):
+        t1 = time.perf_counter()
+        submit(s)
+        be.synchronize()
+        lat.append((time.perf_counter() - t1) * 1e3)
+        keep.clear()
+    # the link's own rate for one large page-locked copy, the bound to read h2d_GBps against
+    import torch
+    big = arena.array(256 << 20, np.uint8)
+    dst = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
+    src = torch.from_numpy(big)
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(5):
+        dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    peak = 5 * (256 << 20) / (time.perf_counter() - t1) / 1e9
+    del dst, src
+    arena.close()
+    return {"value": n * args.pcie_steps / el, "unit": "decisions/s", "ms_per_step": el / args.pcie_steps * 1e3,
+            "h2d_peak_GBps": peak, "frac_of_h2d_peak": bytes_in * args.pcie_steps / el / 1e9 / peak,
+            "p50_batch_ms": float(np.percentile(lat, 50)), "p99_batch_ms": float(np.percentile(lat, 99)),
+            "h2d_bytes_per_decision": bytes_in / n, "d2h_bytes_per_decision": bytes_out / n,
+            "h2d_GBps": bytes_in * args.pcie_steps / el / 1e9, "steps": args.pcie_steps,
+            "buffers": "page-locked (rl_alloc_host); now constant over the phase"}
 
 
 def cpu_baseline(args, W):

@@ -193,6 +193,14 @@ int rl_do_limit(rl_ctx* ctx, const rl_batch* in, rl_result* out);
  * owners' pipelines); errors detected on the GPU surface at rl_synchronize.
  * stem_bytes must be 4-byte aligned (any hipMalloc / torch allocation is). */
 int rl_do_limit_async(rl_ctx* ctx, const rl_batch* in, rl_result* out, void* stream);
+
+/* Host buffers in and out, like rl_do_limit, without waiting: the batch's
+ * inputs cross PCIe into one of the ctx's device staging slots while earlier
+ * batches compute, its outputs cross back when it is done; *out is read after
+ * rl_synchronize, and the host buffers of a batch stay untouched until then.
+ * Pinned buffers (rl_alloc_host) make the copies asynchronous. The fed path of
+ * a batcher whose requests arrive in host memory (single-shard ctx). */
+int rl_do_limit_host_async(rl_ctx* ctx, const rl_batch* in, rl_result* out);
 int rl_synchronize(rl_ctx* ctx);
 
 /* Epoch sweep (replaces Redis EXPIRE): tombstones every slot whose counter

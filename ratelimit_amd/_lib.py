@@ -18,7 +18,8 @@ EXPORTS = ["rl_abi_version", "rl_create", "rl_destroy", "rl_last_error", "rl_do_
            "rl_route_do_limit", "rl_route_scatter", "rl_config_load", "rl_do_limit_requests",
            "rl_local_cache_info_get", "rl_snapshot_size", "rl_snapshot_save", "rl_snapshot_load",
            "rl_packer_create", "rl_packer_destroy", "rl_packer_pack", "rl_packer_rules", "rl_packer_rule_key",
-           "rl_packer_last_error", "rl_comm_unique_id", "rl_comm_init", "rl_do_limit_routed_async"]
+           "rl_packer_last_error", "rl_comm_unique_id", "rl_comm_init", "rl_do_limit_routed_async",
+           "rl_do_limit_host_async"]
 
 _lib = None
 
@@ -50,6 +51,7 @@ def lib():
     L.rl_last_error.argtypes = [C.c_void_p]
     L.rl_do_limit.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.POINTER(abi.RlResult)]
     L.rl_do_limit_async.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.POINTER(abi.RlResult), C.c_void_p]
+    L.rl_do_limit_host_async.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.POINTER(abi.RlResult)]
     L.rl_synchronize.argtypes = [C.c_void_p]
     L.rl_sweep.argtypes = [C.c_void_p, C.c_int64, C.POINTER(C.c_uint64)]
     L.rl_restore.argtypes = [C.c_void_p, C.POINTER(abi.RlRestoreBatch)]

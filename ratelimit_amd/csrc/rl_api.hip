@@ -364,6 +364,12 @@ int rl_do_limit_async(rl_ctx* c, const rl_batch* in, rl_result* out, void* strea
   return routed_async(c, in, out, (hipStream_t)stream);
 }
 
+int rl_do_limit_host_async(rl_ctx* c, const rl_batch* in, rl_result* out) {
+  if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (c->n > 1) return fail(c, RL_E_INVALID, "gpu: rl_do_limit_host_async runs on a single-shard ctx");
+  return eng_do_limit_host_async(c->e[0], in, out);
+}
+
 int rl_do_limit(rl_ctx* c, const rl_batch* in, rl_result* out) {
   if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
   if (c->n == 1) return eng_do_limit(c->e[0], in, out);

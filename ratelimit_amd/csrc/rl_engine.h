@@ -23,6 +23,19 @@ namespace rl {
 constexpr uint32_t NBUF = RL_NBUF;
 constexpr uint32_t PROF_RING = 8;  // timed batches in flight (> NBUF)
 
+// Device staging of one host-fed batch in flight (eng_do_limit_host_async).
+struct HostSlot {
+  uint8_t* stem = nullptr;
+  uint32_t *off = nullptr, *req = nullptr, *limit = nullptr, *hits = nullptr, *rule = nullptr;
+  int64_t* now = nullptr;
+  uint8_t *unit = nullptr, *flags = nullptr;
+  uint8_t *code = nullptr, *status = nullptr;
+  uint32_t *rem = nullptr, *reset = nullptr;
+  unsigned long long* stats = nullptr;
+  hipEvent_t in_done = nullptr;   // its inputs are on the device
+  hipEvent_t out_done = nullptr;  // its outputs are back on the host (the slot is free)
+};
+
 struct Engine {
   rl_config cfg;
   hipStream_t stream = nullptr;   // serial work (== pipe[0])
@@ -79,6 +92,13 @@ struct Engine {
   uint8_t* mbuf = nullptr;
   size_t mbuf_cap = 0;
   uint32_t* h_match = nullptr;  // pinned [4]: matched count, stem bytes, error bits
+  // host-fed async batches: NBUF staging slots and two copy streams, so that
+  // batch t+1's inputs cross PCIe and batch t-1's outputs come back while
+  // batch t's kernels run (allocated on first use)
+  HostSlot hs[NBUF]{};
+  hipStream_t h2d = nullptr, d2h = nullptr;
+  uint32_t hnext = 0;
+  bool hs_ready = false;
 };
 
 // Engine entry points (rl_engine.hip): the single-shard implementations of
@@ -88,6 +108,7 @@ void eng_destroy(Engine* c);
 const char* eng_last_error(const Engine* c);
 int eng_do_limit(Engine* c, const rl_batch* in, rl_result* out);
 int eng_do_limit_async(Engine* c, const rl_batch* in, rl_result* out, void* stream);
+int eng_do_limit_host_async(Engine* c, const rl_batch* in, rl_result* out);
 int eng_synchronize(Engine* c);
 int eng_sweep(Engine* c, int64_t now, uint64_t* n_evicted);
 int eng_restore(Engine* c, const rl_restore_batch* in);

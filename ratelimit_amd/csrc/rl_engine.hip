@@ -364,9 +364,29 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   return c;
 }
 
+void free_host_slots(Engine* c) {
+  for (HostSlot& h : c->hs) {
+    void* bufs[] = {h.stem, h.off, h.req, h.limit, h.hits, h.rule, h.now, h.unit, h.flags, h.code, h.status, h.rem,
+                    h.reset, h.stats};
+    for (void* p : bufs)
+      if (p) (void)hipFree(p);
+    if (h.in_done) (void)hipEventDestroy(h.in_done);
+    if (h.out_done) (void)hipEventDestroy(h.out_done);
+    h = HostSlot{};
+  }
+  for (hipStream_t st : {c->h2d, c->d2h})
+    if (st) (void)hipStreamDestroy(st);
+  c->h2d = c->d2h = nullptr;
+  c->hs_ready = false;
+}
+
 void eng_destroy(Engine* c) {
   if (!c) return;
   (void)hipSetDevice(c->cfg.device);
+  if (c->hs_ready) {
+    (void)hipDeviceSynchronize();
+    free_host_slots(c);
+  }
   for (uint32_t k = 0; k < NBUF; k++)
     if (c->pipe[k]) (void)hipStreamSynchronize(c->pipe[k]);
   if (c->side) (void)hipStreamSynchronize(c->side);
@@ -595,6 +615,93 @@ int eng_synchronize(Engine* c) {
   HIPCHK(c, hipSetDevice(c->cfg.device));
   HIPCHK(c, hipDeviceSynchronize());
   return collect(c);
+}
+
+// Host buffers in and out, nothing waited for: the inputs cross PCIe on the
+// h2d stream into a staging slot, the batch is pipelined on the ctx streams
+// once they have landed, its outputs cross back on the d2h stream; the caller
+// reads *out after rl_synchronize. Pinned host buffers (rl_alloc_host) make
+// the copies truly asynchronous; the host buffers of a batch must stay
+// untouched until then.
+int eng_do_limit_host_async(Engine* c, const rl_batch* in, rl_result* out) {
+  if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  const uint32_t n = in->n, nq = in->n_requests;
+  if (n && (!in->stem_off || !out->code || !out->limit_remaining || !out->reset_s))
+    return set_err(c, RL_E_INVALID, "gpu: null argument");
+  const uint64_t nb = n ? in->stem_off[n] : 0;
+  int rc = check_sizes(c, in, nb);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (!c->hs_ready) {
+    const rl_config& g = c->cfg;
+    bool ok = hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) == hipSuccess;
+    for (HostSlot& h : c->hs) {
+      ok = ok && dalloc(&h.stem, (size_t)g.max_stem_bytes + 64) == hipSuccess &&
+           dalloc(&h.off, (size_t)g.max_batch + 1) == hipSuccess && dalloc(&h.req, g.max_batch) == hipSuccess &&
+           dalloc(&h.limit, g.max_batch) == hipSuccess && dalloc(&h.hits, g.max_batch) == hipSuccess &&
+           dalloc(&h.rule, g.max_batch) == hipSuccess && dalloc(&h.now, g.max_requests) == hipSuccess &&
+           dalloc(&h.unit, g.max_batch) == hipSuccess && dalloc(&h.flags, g.max_batch) == hipSuccess &&
+           dalloc(&h.code, g.max_batch) == hipSuccess && dalloc(&h.status, g.max_batch) == hipSuccess &&
+           dalloc(&h.rem, g.max_batch) == hipSuccess && dalloc(&h.reset, g.max_batch) == hipSuccess &&
+           dalloc(&h.stats, (size_t)g.max_rules * RL_NUM_STATS) == hipSuccess &&
+           hipEventCreateWithFlags(&h.in_done, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&h.out_done, hipEventDisableTiming) == hipSuccess &&
+           hipEventRecord(h.out_done, c->d2h) == hipSuccess;
+    }
+    if (!ok) {
+      free_host_slots(c);
+      return set_err(c, RL_E_HIP, "gpu: host-fed staging allocation failed");
+    }
+    c->hs_ready = true;
+  }
+  const uint32_t j = c->hnext;
+  c->hnext = (j + 1) % NBUF;
+  HostSlot& h = c->hs[j];
+  hipStream_t up = c->h2d, down = c->d2h;
+  HIPCHK(c, hipStreamWaitEvent(up, h.out_done, 0));  // the slot's previous batch is drained
+  if (nb) HIPCHK(c, hipMemcpyAsync(h.stem, in->stem_bytes, nb, hipMemcpyHostToDevice, up));
+  HIPCHK(c, hipMemcpyAsync(h.off, in->stem_off, (n + 1) * 4ull, hipMemcpyHostToDevice, up));
+  if (nq) HIPCHK(c, hipMemcpyAsync(h.now, in->now, nq * 8ull, hipMemcpyHostToDevice, up));
+  if (n) {
+    HIPCHK(c, hipMemcpyAsync(h.req, in->req_idx, n * 4ull, hipMemcpyHostToDevice, up));
+    HIPCHK(c, hipMemcpyAsync(h.unit, in->unit, n, hipMemcpyHostToDevice, up));
+    HIPCHK(c, hipMemcpyAsync(h.flags, in->flags, n, hipMemcpyHostToDevice, up));
+    HIPCHK(c, hipMemcpyAsync(h.limit, in->limit, n * 4ull, hipMemcpyHostToDevice, up));
+    HIPCHK(c, hipMemcpyAsync(h.hits, in->hits, n * 4ull, hipMemcpyHostToDevice, up));
+    HIPCHK(c, hipMemcpyAsync(h.rule, in->rule_id, n * 4ull, hipMemcpyHostToDevice, up));
+  }
+  HIPCHK(c, hipEventRecord(h.in_done, up));
+  rl_batch d = *in;
+  d.stem_bytes = h.stem;
+  d.stem_off = h.off;
+  d.now = h.now;
+  d.req_idx = h.req;
+  d.unit = h.unit;
+  d.flags = h.flags;
+  d.limit = h.limit;
+  d.hits = h.hits;
+  d.rule_id = h.rule;
+  BatchDev b = dev_view(c, &d, c->cfg.max_stem_bytes);
+  b.stem_total = (uint32_t)nb;
+  OutDev o{h.code, h.rem, h.reset, in->n_rules ? h.stats : nullptr, out->status ? h.status : nullptr};
+  HIPCHK(c, hipStreamWaitEvent(c->pipe[c->next], h.in_done, 0));
+  const uint32_t k = enqueue(c, b, o, 0, nullptr, true);
+  HIPCHK(c, hipStreamWaitEvent(down, c->b_done[k], 0));
+  if (n) {
+    HIPCHK(c, hipMemcpyAsync(out->code, h.code, n, hipMemcpyDeviceToHost, down));
+    HIPCHK(c, hipMemcpyAsync(out->limit_remaining, h.rem, n * 4ull, hipMemcpyDeviceToHost, down));
+    HIPCHK(c, hipMemcpyAsync(out->reset_s, h.reset, n * 4ull, hipMemcpyDeviceToHost, down));
+    if (out->status) HIPCHK(c, hipMemcpyAsync(out->status, h.status, n, hipMemcpyDeviceToHost, down));
+  }
+  if (in->n_rules && out->stats)
+    HIPCHK(c, hipMemcpyAsync(out->stats, h.stats, (size_t)in->n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost,
+                             down));
+  HIPCHK(c, hipEventRecord(h.out_done, down));
+  HIPCHK(c, hipGetLastError());
+  c->batches++;
+  c->decisions += n;
+  return RL_OK;
 }
 
 int eng_do_limit(Engine* c, const rl_batch* in, rl_result* out) {

@@ -72,6 +72,34 @@ def _config(near_limit_ratio, local_cache, per_second, jitter, table_slots, max_
     return cfg
 
 
+class PinnedArena:
+    """Page-locked host arrays from the library (rl_alloc_host): numpy views
+    whose PCIe copies run asynchronously (rl_do_limit_host_async)."""
+
+    def __init__(self):
+        self.ptrs = []
+
+    def array(self, n: int, dtype) -> np.ndarray:
+        dt = np.dtype(dtype)
+        nbytes = max(int(n), 1) * dt.itemsize
+        p = lib().rl_alloc_host(nbytes)
+        if not p:
+            raise MemoryError("rl_alloc_host(%d) failed" % nbytes)
+        self.ptrs.append(p)
+        buf = (C.c_uint8 * nbytes).from_address(p)
+        return np.frombuffer(buf, dtype=dt, count=max(int(n), 1))
+
+    def like(self, a: np.ndarray) -> np.ndarray:
+        out = self.array(a.size, a.dtype)
+        out[:a.size] = a
+        return out
+
+    def close(self):
+        for p in self.ptrs:
+            lib().rl_free_host(p)
+        self.ptrs = []
+
+
 class Backend:
     """Owns one rl_ctx (one GPU's table)."""
 
@@ -131,6 +159,17 @@ class Backend:
         r = abi.make_result_struct(dev_out)
         check(self.ctx, lib().rl_do_limit_async(self.ctx, C.byref(b), C.byref(r),
                                                 C.c_void_p(stream) if stream else None))
+
+    def do_limit_host_async(self, pb: PackedBatch, out: dict):
+        """rl_do_limit_host_async: host arrays in (pb) and out (dict of numpy
+        arrays: code, limit_remaining, reset_s, stats[, status]), nothing waited
+        for; out is final after synchronize(). Both must stay alive and
+        untouched until then; pinned arrays (PinnedArena) make the copies
+        asynchronous."""
+        b = pb.batch_struct()
+        r = abi.make_result_struct(out)
+        check(self.ctx, lib().rl_do_limit_host_async(self.ctx, C.byref(b), C.byref(r)))
+        return b, r  # (the structs the call read; kept by the caller with the arrays)
 
     # ---- config match + DoLimit on raw requests (rl_match.hip)
     def load_config(self, tree) -> None:

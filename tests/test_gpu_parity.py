@@ -405,6 +405,45 @@ def test_gpu_async_pipeline_matches_oracle(lc):
     be.close()
 
 
+@pytest.mark.parametrize("pinned,lc", [(True, False), (True, True), (False, True)])
+def test_gpu_host_fed_async_pipeline_matches_oracle(pinned, lc):
+    """rl_do_limit_host_async: host batches copied in on one stream while the
+    previous ones compute, outputs copied back on another; every batch queued
+    before one synchronize (pinned buffers from rl_alloc_host, or plain numpy),
+    with a synchronous call and a per-descriptor-status batch mid-stream."""
+    from ratelimit_amd.limiter import PinnedArena
+    from ratelimit_amd.packing import PackedBatch
+    z = workloads.ZipfSampler(20_000, 1.1)
+    batches = list(workloads.c2_stream(n_tenants=20_000, requests_per_batch=30_000, batches=7, sampler=z))
+    co = c_oracle.COracle(0.8, lc)
+    want = [co.do_limit(a, n, nq, nr) for a, n, nq, nr in batches]
+    co.close()
+    be = Backend(0.8, lc, table_slots=1 << 18, max_batch=1 << 17, max_rules=8)
+    arena = PinnedArena()
+    keep, got = [], []
+    for i, (a, n, nq, nr) in enumerate(batches):
+        if i == 3:
+            got.append(be.do_limit_arrays(a, n, nq, nr))
+            continue
+        arr = {k: arena.like(v) for k, v in a.items()} if pinned else a
+        pb = PackedBatch(arr, n, nq, nr)
+        out = pb.alloc_result(isolate=(i == 5))
+        if pinned:
+            out = {k: arena.like(v) for k, v in out.items()}
+        keep.append((pb, out, be.do_limit_host_async(pb, out)))
+        got.append(out)
+    be.synchronize()
+    for i, (g, w) in enumerate(zip(got, want)):
+        n, nr = batches[i][1], batches[i][3]
+        for k in ("code", "limit_remaining", "reset_s"):
+            assert np.array_equal(g[k][:n], w[k]), "batch %d: %s differs" % (i, k)
+        assert np.array_equal(g["stats"][:nr * abi.RL_NUM_STATS], w["stats"]), i
+        if "status" in g:
+            assert (g["status"][:n] == 0).all()
+    be.close()
+    arena.close()
+
+
 def test_gpu_async_invalid_batch_does_not_touch_its_predecessor():
     """A batch that fails validation in the pipeline is reported at
     rl_synchronize; the batch queued before it is still answered exactly."""
