@@ -84,3 +84,34 @@ def test_packer_rejects_malformed_messages():
         assert b.n_requests == 2 and b.n_descriptors == 1
     finally:
         pk.close()
+
+
+@pytest.mark.parametrize("where", ["request", "descriptor", "entry", "override"])
+def test_packer_rejects_field_numbers_outside_protobuf_range(where):
+    """field number 0 and numbers past 2^29 - 1 are invalid protobuf
+    keys at every nesting level; a valid unknown field (2^29 - 1) is skipped."""
+    ok_unknown = pbwire.varint((2 ** 29 - 1) << 3) + pbwire.varint(7)
+    for tag, valid in ((0, False), ((2 ** 29) << 3, False), (ok_unknown, True)):
+        junk = tag if isinstance(tag, bytes) else pbwire.varint(tag) + pbwire.varint(7)
+        entry = pbwire.field_bytes(1, b"k") + pbwire.field_bytes(2, b"v")
+        over = pbwire.field_varint(1, 5) + pbwire.field_varint(2, 1)
+        if where == "entry":
+            entry += junk
+        if where == "override":
+            over += junk
+        desc = pbwire.field_bytes(1, entry) + pbwire.field_bytes(2, over)
+        if where == "descriptor":
+            desc += junk
+        msg = pbwire.field_bytes(1, b"d") + pbwire.field_bytes(2, desc) + pbwire.field_varint(3, 1)
+        if where == "request":
+            msg += junk
+        pk = RequestPacker(0)
+        try:
+            if valid:
+                b = pk.pack([msg], [0])
+                assert b.n_descriptors == 1
+            else:
+                with pytest.raises(RedisError, match="malformed"):
+                    pk.pack([msg], [0])
+        finally:
+            pk.close()
