@@ -40,7 +40,7 @@ enum rl_status {
   RL_E_HIP = 4,        /* HIP runtime error */
   RL_E_CAPACITY = 5,   /* batch larger than rl_config.max_* */
   RL_E_TIME = 6,       /* now outside [0, 2^32 - 2*86400], before the last sweep, or
-                          moved back more than one window on one key. Note: the reference's
+                          moved back more than 8 windows on one key. Note: the reference's
                           clock is int64 (utils.TimeSource); this backend's is 32-bit */
   RL_E_COMM = 7,       /* multi-GPU routing (RCCL) error */
   RL_E_INTERNAL = 8
@@ -95,8 +95,10 @@ typedef struct rl_config {
  * base_limiter.go:78-81); unlimited rules are nil by then (ratelimit.go:140-143).
  * Descriptors appear in arrival order: request-major, descriptor order inside
  * the request; req_idx is non-decreasing. now[] may move backwards (the
- * reference's tests do, on different keys); per (stem, unit) it may return to
- * the previous window but not older (RL_E_TIME).
+ * reference's tests do, on different keys); per (stem, unit) the table keeps
+ * the 8 windows below the newest one written (Redis keeps a key div + jitter
+ * seconds after its last hit, fixed_cache_impl.go:71-74): a request up to 8
+ * windows back is answered exactly, an older one gets RL_E_TIME.
  * The stem is the cache key without its window suffix:
  *   prefix ‖ domain ‖ '_' ‖ Σ(key ‖ '_' ‖ value ‖ '_')   (cache_key.go:62-71)
  * The full key is stem ‖ decimal((now/div)*div) (cache_key.go:73-74). */

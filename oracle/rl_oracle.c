@@ -33,7 +33,16 @@ typedef struct {
   uint32_t len;
   uint32_t count;
   int64_t expire;  /* redis: -1 = no TTL; lc: expireAt */
+  int64_t slack;   /* GC_WINDOWS windows of the largest unit that wrote the key */
 } ent_t;
+
+/* Garbage collection (smap_rebuild) drops an entry only once it is dead for
+ * any request up to GC_WINDOWS windows of its unit behind the request that
+ * triggers the rebuild. Liveness is judged against each request's own clock
+ * (lazy expiry), so with time moving backwards an entry dead at one request
+ * is live again for an earlier one; the slack keeps every entry a request
+ * within that lag can read (the GPU table's ring reaches as far, HIST_W). */
+#define GC_WINDOWS 8
 
 typedef struct {
   ent_t* e;
@@ -77,7 +86,7 @@ static ent_t* smap_find(smap_t* m, const char* k, uint32_t n, uint64_t h) {
 static void smap_rebuild(smap_t* m, int64_t now) {
   uint64_t live_n = 0;
   for (uint64_t i = 0; i < m->cap; i++)
-    if (m->e[i].h && live(m, &m->e[i], now)) live_n++;
+    if (m->e[i].h && live(m, &m->e[i], now - m->e[i].slack)) live_n++;
   uint64_t ncap = m->cap;
   while (live_n * 4 > ncap) ncap *= 2;
   ent_t* old = m->e; uint64_t ocap = m->cap; char* oar = m->arena;
@@ -86,7 +95,7 @@ static void smap_rebuild(smap_t* m, int64_t now) {
   m->arena = (char*)malloc(m->arena_cap); m->arena_used = 0;
   for (uint64_t i = 0; i < ocap; i++) {
     ent_t* o = &old[i];
-    if (!o->h || !live(m, o, now)) continue;
+    if (!o->h || !live(m, o, now - o->slack)) continue;
     ent_t* e = smap_find(m, oar + o->off, o->len, o->h);
     *e = *o; e->off = m->arena_used;
     memcpy(m->arena + m->arena_used, oar + o->off, o->len); m->arena_used += o->len;
@@ -97,14 +106,17 @@ static void smap_rebuild(smap_t* m, int64_t now) {
 
 /* Find or create the entry for key k (a dead entry is returned as is: the
  * caller decides liveness). */
-static ent_t* smap_upsert(smap_t* m, const char* k, uint32_t n, int64_t now, int* created) {
+static ent_t* smap_upsert(smap_t* m, const char* k, uint32_t n, int64_t now, int64_t div, int* created) {
   uint64_t h = hash_bytes(k, n);
   ent_t* e = smap_find(m, k, n, h);
   *created = 0;
-  if (e->h) return e;
+  if (e->h) {
+    if (e->slack < GC_WINDOWS * div) e->slack = GC_WINDOWS * div;
+    return e;
+  }
   if ((m->used + 1) * 2 > m->cap) { smap_rebuild(m, now); e = smap_find(m, k, n, h); }
   while (m->arena_used + n > m->arena_cap) { m->arena_cap *= 2; m->arena = (char*)realloc(m->arena, m->arena_cap); }
-  e->h = h; e->off = m->arena_used; e->len = n; e->count = 0; e->expire = -1;
+  e->h = h; e->off = m->arena_used; e->len = n; e->count = 0; e->expire = -1; e->slack = GC_WINDOWS * div;
   memcpy(m->arena + m->arena_used, k, n); m->arena_used += n; m->used++;
   *created = 1;
   return e;
@@ -248,7 +260,7 @@ static int do_limit_idx(rlo_ctx* c, const rl_batch* b, const uint32_t* idx, uint
         smap_t* mp = ps ? &c->redis_ps : &c->redis;
         uint32_t kl; const char* key = build_key(c, b, k, now, &kl);
         uint32_t h = b->hits[k] > 1 ? b->hits[k] : 1;
-        int created; ent_t* re = smap_upsert(mp, key, kl, now, &created);
+        int created; ent_t* re = smap_upsert(mp, key, kl, now, unit_to_divider(b->unit[k]), &created);
         if (!live(mp, re, now)) { re->count = 0; re->expire = -1; }
         re->count += h;                                   /* INCRBY */
         re->expire = now + unit_to_divider(b->unit[k]);   /* EXPIRE (jitter draw 0) */
@@ -264,7 +276,7 @@ static int do_limit_idx(rlo_ctx* c, const rl_batch* b, const uint32_t* idx, uint
                        (b->flags[k] & RL_FLAG_SHADOW) != 0, c->lc_enabled);
       if (r.set_lc) { /* localCache.Set(key, ttl = divider) */
         uint32_t kl; const char* key = build_key(c, b, k, now, &kl);
-        int created; ent_t* le = smap_upsert(&c->lc, key, kl, now, &created);
+        int created; ent_t* le = smap_upsert(&c->lc, key, kl, now, d, &created);
         le->expire = now + d;
       }
       o->code[k] = r.code; o->limit_remaining[k] = r.rem;
@@ -374,9 +386,9 @@ int rlo_restore(rlo_ctx* c, const rl_restore_batch* r) {
     memcpy(buf, r->stem_bytes + s0, sl);
     uint32_t kl = sl + fmt_i64(buf + sl, (r->now[i] / d) * d);
     smap_t* m = (c->per_second && r->unit[i] == RL_UNIT_SECOND) ? &c->redis_ps : &c->redis;
-    int created; ent_t* e = smap_upsert(m, buf, kl, r->now[i], &created);
+    int created; ent_t* e = smap_upsert(m, buf, kl, r->now[i], d, &created);
     e->count = r->count[i]; e->expire = r->now[i] + d;
-    if (r->lc && r->lc[i]) { ent_t* le = smap_upsert(&c->lc, buf, kl, r->now[i], &created); le->expire = r->now[i] + d; }
+    if (r->lc && r->lc[i]) { ent_t* le = smap_upsert(&c->lc, buf, kl, r->now[i], d, &created); le->expire = r->now[i] + d; }
   }
   return RL_OK;
 }

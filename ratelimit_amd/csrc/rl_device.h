@@ -15,18 +15,26 @@ namespace rl {
 //
 // One slot per (stem, unit). The Redis key of the reference is
 // stem ‖ decimal(windowStart) (cache_key.go:62-74); a slot holds the state of
-// the last two window keys of its (stem, unit): `cur` and `prev`.  For a stem
-// used with a single unit the current window is the only live key, so the slot
-// is recycled in place when the window advances (no insert per window, no
-// EXPIRE traffic).  `prev` exists so that a stem later seen with a second unit
-// (only possible through per-request overrides, config_impl.go:254-265) can
-// reproduce Redis key sharing exactly (DESIGN.md §"Exact key identity").
+// the newest window key of its (stem, unit), `cur`, and a ring beside the
+// table (`Hist`, one 128-B line per slot) holds the HIST_W windows before it:
+// window w < cur at position (w / div) % HIST_W. For a stem used with a
+// single unit the current window is the only live key while time moves
+// forward, so the slot is recycled in place when the window advances (no
+// insert per window, no EXPIRE traffic) and the old record moves to the ring
+// with one write. The ring answers requests whose time moved back: Redis keeps
+// a key div + jitter seconds after its last hit (fixed_cache_impl.go:71-74),
+// so a request that waited in a batcher finds its window's count. A window
+// more than HIST_W windows back is RL_E_TIME for that descriptor, never a
+// silently wrong count. The ring also keeps the records a stem later seen with
+// a second unit shares with it (only possible through per-request overrides,
+// config_impl.go:254-265; DESIGN.md §"Exact key identity").
 // ---------------------------------------------------------------------------
 constexpr uint32_t WS_INVALID = 0xFFFFFFFFu;  // record never written
 constexpr uint64_t TAG_EMPTY = 0;
 constexpr uint64_t TAG_TOMB = 1;
 constexpr uint32_t INLINE_KEY = 80;           // stem bytes stored in the slot
 constexpr uint8_t SLOT_EXACT = 0x1;           // stem has >1 unit slot: exact (serial) path
+constexpr uint32_t HIST_W = 8;                // ring records per slot: windows 1..HIST_W back from cur
 
 struct Win {
   uint32_t ws;      // window start (Redis key suffix); WS_INVALID = no record
@@ -37,9 +45,8 @@ struct Win {
 
 // One 128-B line. The first 64-B sector holds everything a probe of a stem of
 // at most KEY_LO bytes needs (tag, length, the current window, the stem), so
-// such a probe reads one sector; `prev`, the arena offset and stem bytes
-// KEY_LO..79 are in the second sector, read only when needed (longer stems,
-// time moving back to the previous window).
+// such a probe reads one sector; the arena offset and stem bytes KEY_LO..79
+// are in the second sector, read only for longer stems.
 constexpr uint32_t KEY_LO = 36;               // stem bytes in the first sector
 struct __attribute__((aligned(128))) Slot {
   uint64_t tag;       // TAG_EMPTY / TAG_TOMB / mix(hash(stem), unit) >= 2
@@ -48,16 +55,29 @@ struct __attribute__((aligned(128))) Slot {
   uint8_t flags;      // SLOT_EXACT
   Win cur;            // bytes 12..27
   uint8_t key0[KEY_LO];               // stem bytes 0..35 (28..63)
-  Win prev;                           // 64..79
+  uint32_t spare[4];                  // 64..79 (unused)
   uint32_t ext_off;   // arena offset in 16-B units for bytes >= INLINE_KEY
   uint8_t key1[INLINE_KEY - KEY_LO];  // stem bytes 36..79 (84..127)
 };
-static_assert(offsetof(Slot, cur) == 12 && offsetof(Slot, key0) == 28 && offsetof(Slot, prev) == 64 &&
+static_assert(offsetof(Slot, cur) == 12 && offsetof(Slot, key0) == 28 && offsetof(Slot, spare) == 64 &&
                   offsetof(Slot, ext_off) == 80 && offsetof(Slot, key1) == 84,
               "slot layout");
 // dword of the slot holding stem dword k (k < 20)
 __host__ __device__ constexpr uint32_t slot_key_dw(uint32_t k) { return k < KEY_LO / 4 ? 7 + k : 12 + k; }
 static_assert(sizeof(Slot) == 128, "slot must be one 128-B line");
+
+// The window records of slot i below its cur: one 128-B line (table-parallel
+// array; line i belongs to slot i).
+struct __attribute__((aligned(128))) Hist {
+  Win w[HIST_W];
+};
+static_assert(sizeof(Hist) == 128, "ring must be one 128-B line");
+__host__ __device__ inline uint32_t hist_pos(uint32_t ws, uint32_t d) { return (ws / d) % HIST_W; }
+// Window w < cur_ws is within the ring's reach (windows 1..HIST_W back). Within
+// it, the ring record at hist_pos(w) either is w's or w was never written
+// (every later write to that position is of an older window, which is out of
+// reach and therefore never written once w is in the ring).
+__host__ __device__ inline bool hist_reach(uint32_t w, uint32_t cur_ws, uint32_t d) { return cur_ws - w <= HIST_W * d; }
 
 __host__ __device__ inline uint32_t div_of(uint32_t unit) {  // utils.UnitToDivider
   return unit == RL_UNIT_SECOND ? 1u : unit == RL_UNIT_MINUTE ? 60u : unit == RL_UNIT_HOUR ? 3600u : 86400u;
@@ -227,7 +247,7 @@ enum : uint32_t {
   ERR_TABLE_FULL = 1u << 1,
   ERR_ARENA_FULL = 1u << 2,
   ERR_TIME = 1u << 3,
-  ERR_HISTORY = 1u << 5,     // a key's window is older than its (cur, prev) history
+  ERR_HISTORY = 1u << 5,     // a key's window is older than its ring reaches (HIST_W windows)
 };
 
 // rl_status of a batch that failed with device error bits e (the host's

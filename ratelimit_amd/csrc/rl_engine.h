@@ -52,6 +52,7 @@ struct Engine {
   HashKey hk{};
   // table
   Slot* slots = nullptr;
+  Hist* hist = nullptr;  // [nslots] ring lines (window records below cur)
   uint64_t nslots = 0;
   uint8_t* arena = nullptr;
   uint8_t* arena2 = nullptr;  // compaction target (rl_sweep), swapped with arena

@@ -87,7 +87,7 @@ int map_err(Engine* c, uint32_t e) {
   if (!e) return RL_OK;
   if (e & ERR_TIME) return set_err(c, RL_E_TIME, "gpu: now outside [0, 2^32-172800] or before the last sweep");
   if (e & ERR_HISTORY)
-    return set_err(c, RL_E_TIME, "gpu: time moved back beyond the previous window of a key (table keeps 2 windows)");
+    return set_err(c, RL_E_TIME, "gpu: time moved back more than 8 windows on a key (the window ring's reach)");
   if (e & ERR_INVALID) return set_err(c, RL_E_INVALID, "gpu: malformed batch (unit, rule id, request index or stem offsets)");
   if (e & ERR_TABLE_FULL) return set_err(c, RL_E_TABLE_FULL, "gpu: counter table full (raise table_slots or sweep)");
   if (e & ERR_ARENA_FULL) return set_err(c, RL_E_ARENA_FULL, "gpu: long-stem arena full (raise arena_bytes)");
@@ -181,6 +181,7 @@ BatchDev dev_view(const Engine* c, const rl_batch* in, uint32_t stem_cap) {
 TableDev table_view(Engine* c) {
   TableDev t;
   t.slots = c->slots;
+  t.hist = c->hist;
   t.mask = c->nslots - 1;
   t.arena = c->arena;
   t.arena_used16 = c->s[0].counters + 4;
@@ -313,7 +314,7 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
     ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&c->side_go, hipEventDisableTiming) == hipSuccess &&
        hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming) == hipSuccess;
-  ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess;
+  ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess && dalloc(&c->hist, c->nslots) == hipSuccess;
   ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess && dalloc(&c->arena2, cfg.arena_bytes) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++) ok = ok && alloc_buffer(c->s[k], n);
   Scratch& s0 = c->s[0];
@@ -350,6 +351,7 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && hipHostMalloc((void**)&c->h_counters, 8 * sizeof(unsigned long long)) == hipSuccess;
   if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
   ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
+       hipMemsetAsync(c->hist, 0xFF, c->nslots * sizeof(Hist), c->stream) == hipSuccess &&  // ws = WS_INVALID
        hipMemsetAsync(c->errw, 0, (NBUF + 3) * 4, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.time_floor, 0, 8, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.counters, 0, 64, c->stream) == hipSuccess &&
@@ -408,7 +410,7 @@ void eng_destroy(Engine* c) {
   if (c->caller_ready) (void)hipEventDestroy(c->caller_ready);
   if (c->h_base) (void)hipHostFree(c->h_base);
   const Scratch& s0 = c->s[0];
-  void* bufs[] = {c->slots, c->arena, c->arena2, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
+  void* bufs[] = {c->slots, c->hist, c->arena, c->arena2, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
                   c->d_now, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_status,
                   c->d_rem,
                   c->d_reset, c->d_stats};
@@ -782,7 +784,7 @@ int eng_sweep(Engine* c, int64_t now, uint64_t* n_evicted) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (now > last) HIPCHK(c, hipMemcpyAsync(c->s[0].time_floor, &now, 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->s[0].counters, 0, 8, c->stream));
-  launch_sweep(c->slots, c->nslots, (uint32_t)now, c->s[0].counters, c->stream);
+  launch_sweep(c->slots, c->hist, c->nslots, (uint32_t)now, c->s[0].counters, c->stream);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 40, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1135,7 +1137,7 @@ int eng_local_cache_info_get(Engine* c, int64_t now, rl_local_cache_info* info) 
   HIPCHK(c, after_batches(c, c->stream));
   unsigned long long* ctr = c->s[0].counters;
   HIPCHK(c, hipMemsetAsync(ctr + 7, 0, 8, c->stream));
-  launch_lc_count(c->slots, c->nslots, (uint32_t)now, ctr + 7, c->stream);
+  launch_lc_count(c->slots, c->hist, c->nslots, (uint32_t)now, ctr + 7, c->stream);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(c->h_counters, ctr, 64, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1147,7 +1149,7 @@ int eng_local_cache_info_get(Engine* c, int64_t now, rl_local_cache_info* info) 
 }
 
 namespace {
-constexpr uint64_t SNAP_MAGIC = 0x32304150414e534cull;  // "LSNAPA02" (keyed hash)
+constexpr uint64_t SNAP_MAGIC = 0x33304150414e534cull;  // "LSNAPA03" (keyed hash, window ring)
 struct SnapHeader {
   uint64_t magic, nslots, arena_used16, hash_seed;  // slots are placed by the keyed hash: restore adopts its key
   int64_t time_floor;
@@ -1172,7 +1174,7 @@ int eng_snapshot_size(Engine* c, uint64_t* bytes) {
   int64_t fl = 0;
   int rc = snap_state(c, &au, &fl);
   if (rc) return rc;
-  *bytes = sizeof(SnapHeader) + c->nslots * sizeof(Slot) + au * 16;
+  *bytes = sizeof(SnapHeader) + c->nslots * (sizeof(Slot) + sizeof(Hist)) + au * 16;
   return RL_OK;
 }
 
@@ -1184,13 +1186,15 @@ int eng_snapshot_save(Engine* c, void* host, uint64_t bytes) {
   h.magic = SNAP_MAGIC;
   h.nslots = c->nslots;
   h.hash_seed = c->hash_seed;
-  const uint64_t need = sizeof(SnapHeader) + c->nslots * sizeof(Slot) + h.arena_used16 * 16;
+  const uint64_t tb = c->nslots * sizeof(Slot), hb = c->nslots * sizeof(Hist);
+  const uint64_t need = sizeof(SnapHeader) + tb + hb + h.arena_used16 * 16;
   if (bytes < need) return set_err(c, RL_E_CAPACITY, "gpu: snapshot buffer smaller than rl_snapshot_size");
   uint8_t* p = (uint8_t*)host;
   memcpy(p, &h, sizeof h);
-  HIPCHK(c, hipMemcpy(p + sizeof h, c->slots, c->nslots * sizeof(Slot), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(p + sizeof h, c->slots, tb, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(p + sizeof h + tb, c->hist, hb, hipMemcpyDeviceToHost));
   if (h.arena_used16)
-    HIPCHK(c, hipMemcpy(p + sizeof h + c->nslots * sizeof(Slot), c->arena, h.arena_used16 * 16, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(p + sizeof h + tb + hb, c->arena, h.arena_used16 * 16, hipMemcpyDeviceToHost));
   return RL_OK;
 }
 
@@ -1202,15 +1206,16 @@ int eng_snapshot_load(Engine* c, const void* host, uint64_t bytes) {
   if (h.magic != SNAP_MAGIC) return set_err(c, RL_E_INVALID, "gpu: not a table snapshot");
   if (h.nslots != c->nslots) return set_err(c, RL_E_INVALID, "gpu: snapshot table_slots differ from this ctx");
   if (h.arena_used16 > c->arena_cap16) return set_err(c, RL_E_INVALID, "gpu: snapshot arena larger than this ctx's");
-  if (bytes < sizeof h + h.nslots * sizeof(Slot) + h.arena_used16 * 16)
-    return set_err(c, RL_E_INVALID, "gpu: snapshot truncated");
+  const uint64_t tb = h.nslots * sizeof(Slot), hb = h.nslots * sizeof(Hist);
+  if (bytes < sizeof h + tb + hb + h.arena_used16 * 16) return set_err(c, RL_E_INVALID, "gpu: snapshot truncated");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   HIPCHK(c, after_batches(c, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const uint8_t* p = (const uint8_t*)host;
-  HIPCHK(c, hipMemcpy(c->slots, p + sizeof h, c->nslots * sizeof(Slot), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->slots, p + sizeof h, tb, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->hist, p + sizeof h + tb, hb, hipMemcpyHostToDevice));
   if (h.arena_used16)
-    HIPCHK(c, hipMemcpy(c->arena, p + sizeof h + c->nslots * sizeof(Slot), h.arena_used16 * 16, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->arena, p + sizeof h + tb + hb, h.arena_used16 * 16, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->s[0].counters + 4, &h.arena_used16, 8, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->s[0].time_floor, &h.time_floor, 8, hipMemcpyHostToDevice));
   c->hash_seed = h.hash_seed;

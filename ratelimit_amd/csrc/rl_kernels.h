@@ -109,6 +109,7 @@ struct OutDev {
 
 struct TableDev {
   Slot* slots;
+  Hist* hist;  // [slots] window records below each slot's cur
   uint64_t mask;
   uint8_t* arena;
   unsigned long long* arena_used16;
@@ -202,10 +203,10 @@ void launch_route_ret(const unsigned long long* res, uint32_t n, const uint32_t*
                       hipStream_t st);
 void launch_stats_sum(const unsigned long long* stage, uint32_t n_blocks, uint32_t m, unsigned long long* out,
                       hipStream_t st);
-void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st);
+void launch_sweep(Slot* slots, const Hist* hist, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st);
 void launch_arena_compact(Slot* slots, uint64_t nslots, const uint8_t* from, uint8_t* to, unsigned long long* used16,
                           hipStream_t st);
-void launch_lc_count(const Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* out, hipStream_t st);
+void launch_lc_count(const Slot* slots, const Hist* hist, uint64_t nslots, uint32_t now, unsigned long long* out, hipStream_t st);
 void launch_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out, hipStream_t st);
 void launch_debug_keys(const BatchDev& b, uint8_t* out, uint32_t* klen, hipStream_t st);
 void launch_debug_decide(uint32_t n, const uint32_t* before, const uint32_t* after, const uint8_t* lc_hit,

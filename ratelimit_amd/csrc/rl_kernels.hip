@@ -370,7 +370,10 @@ __device__ __attribute__((always_inline)) inline bool slot_init(const TableDev& 
     else if (k == nw && (il & 3)) sd[slot_key_dw(k)] = key_dw(key, k) & tail_mask(il);
   }
   s->cur = Win{WS_INVALID, 0, 0, 0};
-  s->prev = Win{WS_INVALID, 0, 0, 0};
+  // the ring may hold a swept key's records: one full-line write clears it
+  uint4* ring = reinterpret_cast<uint4*>(&t.hist[s - t.slots]);
+#pragma unroll
+  for (uint32_t j = 0; j < HIST_W; j++) ring[j] = make_uint4(WS_INVALID, 0u, 0u, 0u);
   return true;
 }
 
@@ -439,33 +442,22 @@ __device__ __attribute__((always_inline)) inline int64_t find_slot(const TableDe
 }
 
 // A slot image for probing: the first 64-B sector (tag, length, flags, cur,
-// stem bytes 0..35) always, the second (prev, arena offset, stem bytes 36..79)
-// only when needed (hi). Plain loads are enough: within a launch only CAS
+// stem bytes 0..35). Plain loads are enough: within a launch only CAS
 // inserts change tags, and a lane only ever looks for its own stem, which no
 // other lane inserts.
 struct SlotImg {
   uint4 v[4];   // first sector
-  uint4 pv;     // prev (valid when hi)
-  bool hi;
   __device__ inline uint32_t dw(uint32_t k) const { return u4w(v[k >> 2], k & 3); }
   __device__ inline uint64_t tag() const { return ((uint64_t)v[0].y << 32) | v[0].x; }
   __device__ inline uint32_t key_len() const { return v[0].z & 0xFFFFu; }
   __device__ inline uint32_t flags() const { return v[0].z >> 24; }
   __device__ inline Win cur() const { return Win{v[0].w, v[1].x, v[1].y, v[1].z}; }
-  __device__ inline Win prev() const { return Win{pv.x, pv.y, pv.z, pv.w}; }
 };
 
 __device__ inline void load_img_lo(const Slot* s, SlotImg& im) {
   const uint4* p = reinterpret_cast<const uint4*>(s);
 #pragma unroll
   for (int j = 0; j < 4; j++) im.v[j] = p[j];
-  im.hi = false;
-}
-
-__device__ inline void load_img_hi(const Slot* s, SlotImg& im) {
-  if (im.hi) return;
-  im.pv = reinterpret_cast<const uint4*>(s)[4];
-  im.hi = true;
 }
 
 // Stem of `key` == the slot's stem? Stem bytes beyond the first sector (stems
@@ -492,7 +484,7 @@ __device__ inline bool img_key_equal(const Slot* s, const SlotImg& im, const Key
 }
 
 // find_slot with insert, returning the slot's image (a fresh slot's image for
-// an insert: empty windows, no flags, second sector included). `im` holds the
+// an insert: no window, no flags). `im` holds the
 // home slot's first sector on entry (the caller issues that load early,
 // beside the stem's).
 __device__ __attribute__((always_inline)) inline int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint64_t tag, const Key& key, uint32_t unit,
@@ -524,8 +516,6 @@ __device__ __attribute__((always_inline)) inline int64_t find_slot_img(const Tab
     if (at >= 0) {
       im.v[0] = make_uint4((uint32_t)tag, (uint32_t)(tag >> 32), key.len | (unit << 16), WS_INVALID);
       im.v[1] = make_uint4(0u, 0u, 0u, 0u);
-      im.pv = make_uint4(WS_INVALID, 0u, 0u, 0u);
-      im.hi = true;
       *inserted = true;
       return at;
     }
@@ -665,36 +655,13 @@ __device__ __attribute__((always_inline)) inline void emit(unsigned long long* r
   L.add(acc, x.rule, d);
 }
 
-// The record of window w in a slot's (cur, prev) pair: 0 (cur), 1 (prev) or
-// -1. cur is the newest window ever written for this (stem, unit), prev the
-// newest before it, so a window strictly between them was never written (a
-// fresh key): it takes prev's place. A newer window rolls cur into prev. A
-// window older than prev is outside the table's history: -1 -> RL_E_TIME,
-// never silently wrong. With allow_back false (multi-unit stems, where other
-// units may alias the key) only the current or a newer window is accepted.
-__device__ __attribute__((always_inline)) inline int window_pick(Win& cur, Win& prev, uint32_t w, uint32_t lc_init,
-                                                                bool allow_back) {
-  if (cur.ws == w) return 0;
-  if (cur.ws == WS_INVALID || w > cur.ws) {
-    prev = cur;
-    cur = Win{w, 0, 0, lc_init};
-    return 0;
-  }
-  if (!allow_back) return -1;
-  if (prev.ws == w) return 1;
-  if (prev.ws == WS_INVALID || w > prev.ws) {
-    prev = Win{w, 0, 0, lc_init};
-    return 1;
-  }
-  return -1;
-}
-
-// ---- single (stem, unit) slot, stem never seen with another unit: registers only
+// ---- single (stem, unit) slot, stem never seen with another unit: registers
+// only. cur is the slot's newest window; `old` caches one ring record (that of
+// the last older window touched), written back when another one is needed.
 struct SimpleState {
-  Win cur, prev;
-  const Slot* slot;     // prev is read from here on first need (have_prev false)
-  bool have_prev;
-  bool cur_dirty, prev_dirty;
+  Win cur, old;
+  Win* ring;  // the slot's HIST_W ring records (t.hist)
+  bool cur_dirty, old_dirty;
   uint32_t cur_req;
   bool pend;
   uint32_t pend_w, pend_e;
@@ -703,14 +670,41 @@ struct SimpleState {
       if (cur.ws == pend_w) {
         cur.lc = pend_e;
         cur_dirty = true;
-      } else if (prev.ws == pend_w) {
-        prev.lc = pend_e;
-        prev_dirty = true;
+      } else if (old.ws == pend_w) {
+        old.lc = pend_e;
+        old_dirty = true;
       }
       pend = false;
     }
   }
 };
+
+// The record of window w: 0 = cur (rolled forward when w is newer: the old cur
+// moves to the ring with one write, no read), 1 = S.old, the ring record of w
+// (loaded, or started afresh when w was never written), -1 = w is more than
+// HIST_W windows back (RL_E_TIME, never a silently wrong count).
+__device__ __attribute__((always_inline)) inline int simple_pick(SimpleState& S, uint32_t w, uint32_t d) {
+  if (S.cur.ws == w) return 0;
+  if (S.cur.ws == WS_INVALID || w > S.cur.ws) {
+    if (S.cur.ws != WS_INVALID) {
+      // the cached record goes back first, unless the old cur takes its
+      // position (then it is out of the ring's reach from the new cur)
+      if (S.old_dirty && hist_pos(S.old.ws, d) != hist_pos(S.cur.ws, d)) S.ring[hist_pos(S.old.ws, d)] = S.old;
+      S.old = S.cur;
+      S.old_dirty = true;
+    }
+    S.cur = Win{w, 0, 0, 0};
+    return 0;
+  }
+  if (!hist_reach(w, S.cur.ws, d)) return -1;
+  if (S.old.ws != w) {
+    if (S.old_dirty) S.ring[hist_pos(S.old.ws, d)] = S.old;
+    const Win r = S.ring[hist_pos(w, d)];
+    S.old = r.ws == w ? r : Win{w, 0, 0, 0};
+    S.old_dirty = false;
+  }
+  return 1;
+}
 
 __device__ __attribute__((always_inline)) inline void simple_step(const Params& P, unsigned long long* res,
                                                                   LaneStats& L, StatAcc& acc, SimpleState& S,
@@ -719,23 +713,13 @@ __device__ __attribute__((always_inline)) inline void simple_step(const Params& 
     S.apply_pending();
     S.cur_req = x.req;
   }
-  // window_pick reads prev only for a window older than cur (time moved back)
-  if (!S.have_prev && S.cur.ws != WS_INVALID && x.w < S.cur.ws) {
-    S.prev = S.slot->prev;
-    S.have_prev = true;
-  }
-  const uint32_t ws0 = S.cur.ws;
-  const int which = window_pick(S.cur, S.prev, x.w, 0, true);
-  if (which < 0) {  // older than the table's history: this descriptor's RL_E_TIME
+  const int which = simple_pick(S, x.w, x.d);
+  if (which < 0) {  // older than the ring reaches: this descriptor's RL_E_TIME
     if (P.isolate) res[x.e] = pack_fail(RL_E_TIME);
     if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
     return;
   }
-  if (S.cur.ws != ws0) {  // rolled: the old cur became prev
-    S.have_prev = true;
-    S.prev_dirty = true;
-  }
-  Win R = which ? S.prev : S.cur;  // values, not pointers: the state stays in VGPRs
+  Win R = which ? S.old : S.cur;  // values, not pointers: the state stays in VGPRs
   uint32_t after = 0;
   bool lc_hit = false;
   if (restore) {
@@ -752,8 +736,8 @@ __device__ __attribute__((always_inline)) inline void simple_step(const Params& 
     }
   }
   if (which) {
-    S.prev = R;
-    S.prev_dirty = true;
+    S.old = R;
+    S.old_dirty = true;
   } else {
     S.cur = R;
     S.cur_dirty = true;
@@ -768,10 +752,12 @@ __device__ __attribute__((always_inline)) inline void simple_step(const Params& 
   emit(res, L, acc, x, r, lc_hit);
 }
 
-// ---- general: every unit slot of the stem, Redis keys shared across units
+// ---- general: every unit slot of the stem, Redis keys shared across units.
+// Each unit's cur lives in registers; ring records are read and written in
+// place (the exact path is rare).
 struct GeneralState {
   int64_t sidx[4];
-  Win cur[4], prev[4];
+  Win cur[4];
   uint32_t present;  // bit u-1
   uint32_t cur_req;
   uint32_t npend;
@@ -780,56 +766,85 @@ struct GeneralState {
 
 __device__ inline bool ps_class(const Params& P, uint32_t k) { return P.per_second && k == 0; }
 
-__device__ inline void general_apply_pending(GeneralState& G) {
+// The record of window w in unit slot k (present): its cur, its ring record,
+// or null when unit k never wrote w. *lost: w may have been written but is
+// out of the ring's reach.
+__device__ inline Win* gen_rec(const TableDev& t, GeneralState& G, uint32_t k, uint32_t w, bool* lost) {
+  const uint32_t d = div_of(k + 1);
+  Win& c = G.cur[k];
+  if (c.ws == w) return &c;
+  if (c.ws == WS_INVALID || w > c.ws || w % d) return nullptr;  // (unit k's keys are multiples of its div)
+  Win* r = &t.hist[G.sidx[k]].w[hist_pos(w, d)];
+  if (r->ws == w) return r;
+  if (lost && !hist_reach(w, c.ws, d)) *lost = true;
+  return nullptr;
+}
+
+__device__ inline void general_apply_pending(const TableDev& t, GeneralState& G) {
   for (uint32_t j = 0; j < G.npend; j++) {
     for (uint32_t k = 0; k < 4; k++) {
       if (!(G.present >> k & 1)) continue;
-      if (G.cur[k].ws == G.pend_w[j]) G.cur[k].lc = G.pend_e[j];
-      if (G.prev[k].ws == G.pend_w[j]) G.prev[k].lc = G.pend_e[j];
+      Win* R = gen_rec(t, G, k, G.pend_w[j], nullptr);
+      if (R) R->lc = G.pend_e[j];
     }
   }
   G.npend = 0;
 }
 
-__device__ inline void general_step(const Params& P, unsigned long long* res, LaneStats& L, StatAcc& acc,
-                                    GeneralState& G, const Elem& x, bool restore, uint32_t* err) {
+__device__ inline void general_step(const TableDev& t, const Params& P, unsigned long long* res, LaneStats& L,
+                                    StatAcc& acc, GeneralState& G, const Elem& x, bool restore, uint32_t* err) {
   if (x.req != G.cur_req) {
-    general_apply_pending(G);
+    general_apply_pending(t, G);
     G.cur_req = x.req;
   }
   const uint32_t ui = x.unit - 1;
   const bool ps_e = ps_class(P, ui);
-  bool lc_hit = false;
+  bool lc_hit = false, lost = false;
   uint32_t v = 0, lcw = 0;
   bool vfound = false;
   for (uint32_t k = 0; k < 4; k++) {
     if (!(G.present >> k & 1)) continue;
-    const Win* recs[2] = {&G.cur[k], &G.prev[k]};
-    for (uint32_t r = 0; r < 2; r++) {
-      const Win& R = *recs[r];
-      if (R.ws != x.w) continue;
-      if (x.now < R.lc) lc_hit = true;
-      lcw = R.lc > lcw ? R.lc : lcw;
-      if (ps_class(P, k) == ps_e && !vfound && x.now <= R.expire) {
-        v = R.count;
-        vfound = true;
-      }
+    bool lk = false;
+    const Win* R = gen_rec(t, G, k, x.w, &lk);
+    // A record of w that unit k wrote lives at most 2 divs past w (EXPIRE and
+    // local-cache TTL = div after a hit inside w); one lost from the ring
+    // while it could still be live cannot be answered: RL_E_TIME.
+    if (lk && x.now - x.w < 2u * div_of(k + 1)) lost = true;
+    if (!R) continue;
+    if (x.now < R->lc) lc_hit = true;
+    lcw = R->lc > lcw ? R->lc : lcw;
+    if (ps_class(P, k) == ps_e && !vfound && x.now <= R->expire) {
+      v = R->count;
+      vfound = true;
     }
+  }
+  if (lost) {
+    if (P.isolate) res[x.e] = pack_fail(RL_E_TIME);
+    atomicOr(err, ERR_HISTORY);
+    return;
   }
   lc_hit = lc_hit && P.lc_en && !restore;
   uint32_t after = 0;
   if (!lc_hit) {
     const uint32_t nv = restore ? x.h : v + x.h;
     const uint32_t ex = x.now + x.d;
-    if (window_pick(G.cur[ui], G.prev[ui], x.w, lcw, false) < 0) {
-      if (P.isolate) res[x.e] = pack_fail(RL_E_TIME);
-      if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
-      return;
+    Win& c = G.cur[ui];  // this unit's record of w: cur, a roll, or its ring record (in reach: checked above)
+    if (c.ws != x.w) {
+      if (c.ws == WS_INVALID || x.w > c.ws) {
+        if (c.ws != WS_INVALID) t.hist[G.sidx[ui]].w[hist_pos(c.ws, x.d)] = c;
+        c = Win{x.w, 0, 0, lcw};
+      } else {
+        Win* r = &t.hist[G.sidx[ui]].w[hist_pos(x.w, x.d)];
+        if (r->ws != x.w) *r = Win{x.w, 0, 0, lcw};
+      }
     }
     for (uint32_t k = 0; k < 4; k++) {  // Redis key stem‖w in this store: every alias record
       if (!(G.present >> k & 1) || ps_class(P, k) != ps_e) continue;
-      if (G.cur[k].ws == x.w) { G.cur[k].count = nv; G.cur[k].expire = ex; }
-      if (G.prev[k].ws == x.w) { G.prev[k].count = nv; G.prev[k].expire = ex; }
+      Win* R = gen_rec(t, G, k, x.w, nullptr);
+      if (R) {
+        R->count = nv;
+        R->expire = ex;
+      }
     }
     after = nv;
   }
@@ -837,8 +852,8 @@ __device__ inline void general_step(const Params& P, unsigned long long* res, La
     if (x.flags) {
       for (uint32_t k = 0; k < 4; k++) {
         if (!(G.present >> k & 1)) continue;
-        if (G.cur[k].ws == x.w) G.cur[k].lc = x.now + x.d;
-        if (G.prev[k].ws == x.w) G.prev[k].lc = x.now + x.d;
+        Win* R = gen_rec(t, G, k, x.w, nullptr);
+        if (R) R->lc = x.now + x.d;
       }
     }
     return;
@@ -860,16 +875,14 @@ __device__ __attribute__((always_inline)) inline void replay_simple(SRec rec_s, 
                                                                     unsigned long long* res, const TableDev& t,
                                                                     const Params& P, const uint32_t* grp,
                                                                     uint32_t p, uint32_t end, uint32_t k, int64_t s0,
-                                                                    Win cur0, Win prev0, bool have_prev,
-                                                                    const Rec& x0, uint32_t e0, LaneStats& L,
+                                                                    Win cur0, const Rec& x0, uint32_t e0, LaneStats& L,
                                                                     StatAcc& acc, uint32_t* err, bool restore) {
   Slot* s = &t.slots[s0];
   SimpleState S;
   S.cur = cur0;
-  S.prev = have_prev ? prev0 : Win{WS_INVALID, 0, 0, 0};  // (never matches a pending window)
-  S.slot = s;
-  S.have_prev = have_prev;
-  S.cur_dirty = S.prev_dirty = false;
+  S.old = Win{WS_INVALID, 0, 0, 0};  // (never matches a pending window)
+  S.ring = t.hist[s0].w;
+  S.cur_dirty = S.old_dirty = false;
   S.cur_req = 0xFFFFFFFFu;
   S.pend = false;
   simple_step(P, res, L, acc, S, load_elem(x0, e0, restore), restore, err);  // element p (always stem k)
@@ -880,7 +893,7 @@ __device__ __attribute__((always_inline)) inline void replay_simple(SRec rec_s, 
   S.apply_pending();
   // random writes are the costly part of the probe: store only records that changed
   if (S.cur_dirty) s->cur = S.cur;
-  if (S.prev_dirty) s->prev = S.prev;
+  if (S.old_dirty) S.ring[hist_pos(S.old.ws, div_of(rec_unit(x0)))] = S.old;
 }
 
 // ===========================================================================
@@ -2231,8 +2244,8 @@ __global__ __launch_bounds__(256) void k_unique(BatchDev b, TableDev t, Params P
         if (!ok) t.slots[s0].flags |= SLOT_EXACT;
       }
       if (ok) {
-        replay_simple(SRec{rec, nullptr}, nullptr, res, t, P, nullptr, 0, 1, 0, s0, im.cur(), im.prev(), im.hi, x, i,
-                      L, acc, ferr, restore);
+        replay_simple(SRec{rec, nullptr}, nullptr, res, t, P, nullptr, 0, 1, 0, s0, im.cur(), x, i, L, acc, ferr,
+                      restore);
       } else if (s0 == SLOT_TABLE_FULL || s0 == SLOT_ARENA_FULL) {
         if (P.isolate) res[i] = pack_fail(slot_fail_status(s0));  // else the batch fails
       } else {
@@ -2331,28 +2344,37 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
         // Parallel path: pick the window record once; k_fast_* decide every element.
         Slot* s = &t.slots[s0];
         const Elem el0 = load_elem(x0, e0, false);
-        Win cur = im.cur();
-        if (cur.ws != WS_INVALID && el0.w < cur.ws) load_img_hi(s, im);  // prev only for an older window
-        Win prev = im.hi ? im.prev() : Win{WS_INVALID, 0, 0, 0};
-        const uint32_t ws0 = cur.ws;
-        const int which = window_pick(cur, prev, el0.w, 0, true);
+        const Win cur = im.cur();
+        Win* ring = t.hist[s0].w;
+        // the record of el0.w: cur, a roll (the old cur moves to the ring), or a ring record
+        int which = 0;
+        Win R = cur;
+        if (cur.ws != el0.w) {
+          if (cur.ws == WS_INVALID || el0.w > cur.ws) {
+            if (cur.ws != WS_INVALID) ring[hist_pos(cur.ws, el0.d)] = cur;
+            R = Win{el0.w, 0, 0, 0};
+            s->cur = R;
+          } else if (hist_reach(el0.w, cur.ws, el0.d)) {
+            which = 1;
+            R = ring[hist_pos(el0.w, el0.d)];
+            if (R.ws != el0.w) {  // never written: started afresh
+              R = Win{el0.w, 0, 0, 0};
+              ring[hist_pos(el0.w, el0.d)] = R;
+            }
+          } else {
+            which = -1;
+          }
+        }
         bool fast = true;
         if (which < 0) {
           if (!(RL_ABL & 1)) atomicOr(ferr, ERR_HISTORY);  // (ablation builds probe garbage slots)
           fast = P.isolate != 0;  // every element of the run: RL_E_TIME (k_fast_emit)
           if (fast) run_state[r] = make_uint4((uint32_t)s0, 0u, 0u, 4u);
         } else {
-          const Win R = which ? prev : cur;
           // A record of window w was written inside w: its EXPIRE and local-cache
           // TTL both end at or after w + div, so they hold for the whole run.
           const uint32_t c0 = el0.now <= R.expire ? R.count : 0u;
           const uint32_t F = (P.lc_en && el0.now < R.lc) ? 1u : 0u;
-          if (cur.ws != ws0) {  // rolled: cur is new, prev is the old cur
-            s->cur = cur;
-            s->prev = prev;
-          } else if (which) {  // an older window: prev found or started afresh
-            s->prev = prev;
-          }
           run_state[r] = make_uint4((uint32_t)s0, c0, R.lc, F | ((uint32_t)which << 1));
         }
         if (fast) {
@@ -2372,8 +2394,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
           c.count += end - p;
           sl->cur = c;
         } else {
-          replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, im.cur(), im.prev(), im.hi, x0, e0, L, acc,
-                        ferr, restore);
+          replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, im.cur(), x0, e0, L, acc, ferr, restore);
         }
       } else if (s0 == SLOT_TABLE_FULL || s0 == SLOT_ARENA_FULL) {
         if (P.isolate) fail_range(res, svals, p, end, slot_fail_status(s0));  // else the batch fails
@@ -2470,9 +2491,8 @@ __global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules,
           R.count = after;
           R.expire = x.now + x.d;
           R.lc = (req_f != 0xFFFFFFFFu) ? now_f + x.d : st.z;
-          Slot* s = &t.slots[st.x];
-          if (st.w & 2u) s->prev = R;
-          else s->cur = R;
+          if (st.w & 2u) t.hist[st.x].w[hist_pos(x.w, x.d)] = R;  // a ring record
+          else t.slots[st.x].cur = R;
         }
       }
     }
@@ -2514,7 +2534,6 @@ __device__ inline void stem_exact(const TableDev& t, const Params& P, unsigned l
     if (G.sidx[u - 1] >= 0) {
       G.present |= 1u << (u - 1);
       G.cur[u - 1] = t.slots[G.sidx[u - 1]].cur;
-      G.prev[u - 1] = t.slots[G.sidx[u - 1]].prev;
     } else if ((um >> (u - 1)) & 1) {
       fail = G.sidx[u - 1];
     }
@@ -2523,14 +2542,13 @@ __device__ inline void stem_exact(const TableDev& t, const Params& P, unsigned l
     if (P.isolate) visit([&](const Elem& x) { res[x.e] = pack_fail(slot_fail_status(fail)); });
     return;
   }
-  visit([&](const Elem& x) { general_step(P, res, L, acc, G, x, restore, ferr); });
-  general_apply_pending(G);
+  visit([&](const Elem& x) { general_step(t, P, res, L, acc, G, x, restore, ferr); });
+  general_apply_pending(t, G);
   const uint8_t fl = __popc(G.present) >= 2 ? SLOT_EXACT : 0;
   for (uint32_t u = 0; u < 4; u++) {
     if (!(G.present >> u & 1)) continue;
     Slot* s = &t.slots[G.sidx[u]];
     s->cur = G.cur[u];
-    s->prev = G.prev[u];
     s->flags |= fl;
   }
 }
@@ -2617,8 +2635,8 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
         }
       }
       if (simple) {
-        replay_simple(rec_s, svals, res, t, P, grp, q0, end, g, s0, t.slots[s0].cur, t.slots[s0].prev, true, y,
-                      svals[q0], L, acc, ferr, restore);
+        replay_simple(rec_s, svals, res, t, P, grp, q0, end, g, s0, t.slots[s0].cur, y, svals[q0], L, acc, ferr,
+                      restore);
         continue;
       }
       stem_exact(t, P, res, L, acc, ferr, restore, hs, stem, um, [&](auto&& f) {
@@ -2695,13 +2713,17 @@ __global__ __launch_bounds__(256) void k_finish(const unsigned long long* __rest
 
 // Keys in the local over-limit cache at `now` (freecache EntryCount of live
 // entries): window records whose local-cache TTL has not passed.
-__global__ __launch_bounds__(256) void k_lc_count(const Slot* slots, uint64_t nslots, uint32_t now,
-                                                  unsigned long long* out) {
+__global__ __launch_bounds__(256) void k_lc_count(const Slot* slots, const Hist* hist, uint64_t nslots,
+                                                  uint32_t now, unsigned long long* out) {
   uint32_t live = 0;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * 256) {
     const Slot& s = slots[i];
     if (s.tag < 2) continue;
-    live += (s.cur.ws != WS_INVALID && now < s.cur.lc) + (s.prev.ws != WS_INVALID && now < s.prev.lc);
+    live += s.cur.ws != WS_INVALID && now < s.cur.lc;
+    for (uint32_t j = 0; j < HIST_W; j++) {
+      const Win& w = hist[i].w[j];
+      live += w.ws != WS_INVALID && now < w.lc;
+    }
   }
   if (live) atomicAdd(out, (unsigned long long)live);
 }
@@ -2714,13 +2736,15 @@ __device__ inline bool win_alive(const Win& w, uint32_t now) {
   return w.ws != WS_INVALID && (now <= w.expire || now < w.lc);
 }
 
-__global__ __launch_bounds__(256) void k_sweep(Slot* slots, uint64_t nslots, uint32_t now,
+__global__ __launch_bounds__(256) void k_sweep(Slot* slots, const Hist* hist, uint64_t nslots, uint32_t now,
                                                unsigned long long* evicted) {
   uint32_t local = 0;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * 256) {
     Slot* s = &slots[i];
     if (s->tag < 2) continue;
-    if (!win_alive(s->cur, now) && !win_alive(s->prev, now)) {
+    bool alive = win_alive(s->cur, now);
+    for (uint32_t j = 0; j < HIST_W && !alive; j++) alive = win_alive(hist[i].w[j], now);
+    if (!alive) {
       s->tag = TAG_TOMB;
       local++;
     }
@@ -2903,8 +2927,9 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
 }
 
 
-void launch_sweep(Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st) {
-  k_sweep<<<2048, 256, 0, st>>>(slots, nslots, now, evicted);
+void launch_sweep(Slot* slots, const Hist* hist, uint64_t nslots, uint32_t now, unsigned long long* evicted,
+                  hipStream_t st) {
+  k_sweep<<<2048, 256, 0, st>>>(slots, hist, nslots, now, evicted);
 }
 
 void launch_arena_compact(Slot* slots, uint64_t nslots, const uint8_t* from, uint8_t* to, unsigned long long* used16,
@@ -2912,8 +2937,9 @@ void launch_arena_compact(Slot* slots, uint64_t nslots, const uint8_t* from, uin
   k_arena_compact<<<2048, 256, 0, st>>>(slots, nslots, from, to, used16);
 }
 
-void launch_lc_count(const Slot* slots, uint64_t nslots, uint32_t now, unsigned long long* out, hipStream_t st) {
-  k_lc_count<<<2048, 256, 0, st>>>(slots, nslots, now, out);
+void launch_lc_count(const Slot* slots, const Hist* hist, uint64_t nslots, uint32_t now, unsigned long long* out,
+                     hipStream_t st) {
+  k_lc_count<<<2048, 256, 0, st>>>(slots, hist, nslots, now, out);
 }
 
 void launch_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out, hipStream_t st) {

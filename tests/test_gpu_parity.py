@@ -173,8 +173,9 @@ def test_gpu_aligned_window_key_sharing():
 
 def test_gpu_time_moves_back_one_window():
     """The reference's tests move the mocked clock backwards (fixed_cache_impl_test.go:
-    1000000 -> 1234). Per key the table keeps the previous window, so alternating
-    between two windows is exact; older windows fail loudly (RL_E_TIME)."""
+    1000000 -> 1234). Per key the ring keeps the 8 windows below the newest, so
+    alternating between windows is exact; older windows fail loudly (RL_E_TIME;
+    test_gpu_history.py covers windows 2-8 back)."""
     reg = {}
 
     def L(rpu, unit, key):
@@ -194,7 +195,7 @@ def test_gpu_time_moves_back_one_window():
     cache = GpuRateLimitCache(None, **SMALL)
     cache.do_limit_batch(calls[:2])  # windows t, t+1 of the second-unit key
     with pytest.raises(RedisError, match="RL_E_TIME"):
-        cache.do_limit_batch([(calls[0][0], calls[0][1], t - 1)])  # older than the previous window
+        cache.do_limit_batch([(calls[0][0], calls[0][1], t - 8)])  # 9 windows below the newest
     cache.close()
 
 
@@ -329,8 +330,8 @@ def test_gpu_errors_are_redis_errors():
         be.do_limit_arrays(bad, n, nq, nr)
     be.do_limit_arrays(a, n, nq, nr)  # the context is still usable
     be.do_limit_arrays(*workloads.c1_batch(np.arange(4), workloads.NOW0 + 1))
-    with pytest.raises(RedisError, match="RL_E_TIME"):  # older than the keys' previous window
-        be.do_limit_arrays(*workloads.c1_batch(np.arange(4), workloads.NOW0 - 5))
+    with pytest.raises(RedisError, match="RL_E_TIME"):  # 9 windows below the keys' newest
+        be.do_limit_arrays(*workloads.c1_batch(np.arange(4), workloads.NOW0 - 8))
     be.close()
     tiny = Backend(table_slots=64, max_batch=1 << 10, max_rules=4)
     with pytest.raises(RedisError, match="RL_E_TABLE_FULL"):

@@ -141,9 +141,9 @@ def test_gpu_one_bad_descriptor_fails_alone(lc):
 
 
 def test_gpu_history_miss_fails_alone():
-    """Per (stem, unit) the table keeps two windows; a request older than both
-    gets RL_E_TIME for that descriptor only: on a short run, on a long run
-    (the parallel path), and through the per-call API."""
+    """Per (stem, unit) the ring keeps the 8 windows below the newest; a request
+    older than that gets RL_E_TIME for that descriptor only: on a short run, on
+    a long run (the parallel path), and through the per-call API."""
     be = Backend(0.8, False, **SMALL)
     co = c_oracle.COracle(0.8, False)
     t0 = workloads.NOW0
@@ -151,9 +151,9 @@ def test_gpu_history_miss_fails_alone():
         b = workloads.c1_batch(np.arange(100), t0 + k)
         be.do_limit_arrays(*b, isolate=True)
         co.do_limit(*b)
-    # tenants 0 (x1) and 1 (x40: a long run) at t0 - 1, among fresh tenants at t0 + 1
+    # tenants 0 (x1) and 1 (x40: a long run) at t0 - 8 (9 back), among fresh tenants at t0 + 1
     ten = np.r_[np.arange(200, 300), [0], np.full(40, 1), np.arange(300, 400)]
-    now = np.r_[np.full(100, t0 + 1), np.full(41, t0 - 1), np.full(100, t0 + 1)]
+    now = np.r_[np.full(100, t0 + 1), np.full(41, t0 - 8), np.full(100, t0 + 1)]
     a, n, nq, nr = workloads.c1_batch(ten, now)
     g = be.do_limit_arrays(a, n, nq, nr, isolate=True)
     failed = np.zeros(n, bool)
@@ -179,8 +179,8 @@ def test_gpu_cache_isolates_failed_calls():
     mk = lambda v, now: (O.RateLimitRequest("d", [O.Descriptor([("k", v)])], 1), [L(5, O.SECOND, "s")], now)
     cache = GpuRateLimitCache(None, **SMALL)
     cache.do_limit_batch([mk("a", t), mk("a", t + 1)])
-    outs = cache.do_limit_batch([mk("b", t + 1), mk("a", t - 1), mk("a", t + 1)], isolate=True)
-    # b@t+1: first hit; a@t-1: older than a's windows {t, t+1}: its call alone fails; a@t+1: second hit
+    outs = cache.do_limit_batch([mk("b", t + 1), mk("a", t - 8), mk("a", t + 1)], isolate=True)
+    # b@t+1: first hit; a@t-8: 9 windows below a's newest (t+1): its call alone fails; a@t+1: second hit
     assert isinstance(outs[1], RedisError) and "RL_E_TIME" in str(outs[1])
     assert outs[0][0].code == 1 and outs[0][0].limit_remaining == 4
     assert outs[2][0].code == 1 and outs[2][0].limit_remaining == 3
