@@ -14,7 +14,7 @@ all_to_all (ratelimit_amd/sharded.py); weak scaling, value = all ranks'
 decisions / max-over-ranks time. --route runs the routed path at N=1.
 
 Besides the contract line, rank 0 reports:
-  roofline      dominant kernel (k_runs) achieved GB/s on the canonical
+  roofline      dominant kernel (k_table) achieved GB/s on the canonical
                 B_alg = key_len + 16 + 12 + 64 B per decision,
                 from HIP events on the library's stream;
   cpu_baseline  the C restatement oracle, key-sharded over the host's cores
@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "rate-limit decisions/sec (whole node) at 10M/1B keys; p99 batch latency"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+LONG_RUN = 32  # rl_kernels.h: runs at least this long take the parallel path (k_late)
 
 
 def parse():
@@ -49,7 +50,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--prof-every", type=int, default=7,
-                    help="time every k-th batch's stages with HIP events (k_runs' live time for the roofline)")
+                    help="time every k-th batch's stages with HIP events (k_table's live time for the roofline)")
     ap.add_argument("--no-fill", action="store_true")
     ap.add_argument("--pcie-steps", type=int, default=60, help="host-fed (PCIe) batches timed after the device phase")
     ap.add_argument("--slots-per-key", type=float, default=4.0, help="table slots per live key (power of 2 above)")
@@ -178,7 +179,7 @@ def main():
     rng = np.random.default_rng((0xC2 if args.config == "c2" else 0xC1) + 7919 * rank)
     sampler = W.ZipfSampler(world * T, 1.1) if args.config == "c2" else None
     dev_batches = []
-    uniq = []  # descriptors whose key occurs once in the batch (k_unique's share)
+    uniq = []  # descriptors k_table answers: keys seen once + runs shorter than LONG_RUN (the rest: k_late)
     host_batches = []
     for _ in range(args.distinct_batches):
         ten = rng.integers(0, world * T, nq) if sampler is None else sampler.sample(rng, nq)
@@ -187,7 +188,7 @@ def main():
         else:
             a, bn, bq, br = W.c1_batch(ten, now0, rng.integers(1, 9, nq).astype(np.uint32))
         _, cnt = np.unique(ten, return_counts=True)
-        uniq.append(2 * int((cnt == 1).sum()))  # (both units of a tenant seen once)
+        uniq.append(2 * int(cnt[cnt < LONG_RUN].sum()))  # (a tenant's two stems: one per unit)
         a.pop("now")
         host_batches.append((a, bn, bq))
         dev_batches.append(to_dev(a, torch))
@@ -213,7 +214,7 @@ def main():
 
     # ---- timed region: exactly K steps. The library records HIP events at the
     # stage boundaries on each batch's own stream (pipelined batches are timed
-    # as they run, k_runs included: the roofline's kernel time).
+    # as they run, k_table included: the roofline's kernel time).
     be.profile(args.prof_every > 0, args.prof_every)
     be.profile_read()
     recv = []
@@ -271,11 +272,13 @@ def main():
             dist.destroy_process_group()
         return
 
-    # k_unique answers the keys seen once in the batch (FLAG_DUP clear): the
-    # bulk of C1/C3, a share of C2. SURVEY §8(d): 136 B per decision (key =
-    # stem + 10-digit window, slot 64 B read, 16 B window write-back, 12 B out).
+    # k_table answers the keys seen once in the batch and the runs shorter than
+    # LONG_RUN (replayed in registers): all of C1/C3 but the ~100 hash-prefix
+    # collisions, most of C2 but its hot keys' long runs. SURVEY §8(d): 136 B per
+    # decision (key = stem + 10-digit window, slot 64 B read, 16 B window
+    # write-back, 12 B out).
     b_alg = stem_len + 10 + 16 + 12 + 64
-    uniq_ms = stage_avg["unique"]
+    uniq_ms = stage_avg["table"]
     achieved = b_alg * n_unique / (uniq_ms * 1e-3) / 1e9 if (uniq_ms > 0 and n_unique) else None
     pipe_ms = elapsed / args.steps * 1e3
     traffic, traffic_cal = None, None
@@ -283,13 +286,13 @@ def main():
     if os.path.exists(tp) and not routed:
         try:
             tj = json.load(open(tp))
-            traffic = tj.get("k_unique_bytes_per_launch")  # 2 x FETCH_SIZE + WRITE_SIZE (guide)
-            rb = tj.get("k_unique_read_bytes_bounds")       # probe-calibrated reads (tools/pmcprobe.hip)
-            wr = tj["kernels"]["rl::k_unique"]["write_size_bytes"]
+            traffic = tj.get("k_table_bytes_per_launch")  # 2 x FETCH_SIZE + WRITE_SIZE (guide)
+            rb = tj.get("k_table_read_bytes_bounds")       # probe-calibrated reads (tools/pmcprobe.hip)
+            wr = tj["kernels"]["rl::k_table"]["write_size_bytes"]
             traffic_cal = [rb[0] + wr, rb[1] + wr] if rb else None
         except Exception:
             traffic, traffic_cal = None, None
-    roofline = {"bound": "hbm", "kernel": "k_unique", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    roofline = {"bound": "hbm", "kernel": "k_table", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                 "traffic_calibrated_bounds": traffic_cal,
                 "bytes_alg_per_decision": b_alg, "decisions_per_launch": n_unique,

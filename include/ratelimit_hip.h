@@ -444,11 +444,12 @@ int rl_snapshot_load(rl_ctx* ctx, const void* host, uint64_t bytes);
  * (1 = every batch; the event markers cost stage B a few microseconds per
  * batch, so a sparse sample keeps the timed pipeline unchanged), 0 stops;
  * rl_profile_read fills ms[0..n) with
- * the summed milliseconds of the stages {prepare, sort, segment, unique, finish}
+ * the summed milliseconds of the stages {prepare, sort, segment, table, finish}
  * and *batches with the number of batches timed (it synchronises), then resets
- * the sums. "segment" runs up to the start of k_unique (the runs of repeated
- * keys included), "unique" brackets the single k_unique launch (the keys seen
- * once in the batch: the bulk of the table work on uniform batches). */
+ * the sums. "segment" runs up to the start of k_table (the table stage's
+ * wait for the previous batch included), "table" brackets the single k_table
+ * launch (the keys seen once and the short runs: the bulk of the table work),
+ * "finish" the rest (deferrals, long runs, outputs). */
 #define RL_NUM_STAGES 5
 int rl_profile(rl_ctx* ctx, int enable);
 int rl_profile_read(rl_ctx* ctx, double* ms, uint32_t n, uint64_t* batches);

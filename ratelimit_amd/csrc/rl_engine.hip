@@ -134,14 +134,14 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     (void)hipStreamWaitEvent(a, c->consumed[k], 0);  // ... and its routed results were read
     launch_stage_a(b, c->s[k], isolate, a, ev);
     (void)hipStreamWaitEvent(a, c->b_done[c->last], 0);  // table order
-    launch_stage_b(b, o, t, P, c->s[k], restore, a, c->side, c->side_go, c->side_done, ev);
+    launch_stage_b(b, o, t, P, c->s[k], restore, a, c->side, c->side_go, c->side_tab, c->side_done, ev);
     (void)hipEventRecord(c->b_done[k], a);
   } else {
     if (!st) st = c->stream;
     (void)after_batches(c, st);
     hipEvent_t* ev = prof_events(c);
     launch_stage_a(b, c->s[k], isolate, st, ev);
-    launch_stage_b(b, o, t, P, c->s[k], restore, st, c->side, c->side_go, c->side_done, ev);
+    launch_stage_b(b, o, t, P, c->s[k], restore, st, c->side, c->side_go, c->side_tab, c->side_done, ev);
     (void)hipEventRecord(c->b_done[k], st);
   }
   c->last = k;
@@ -313,6 +313,7 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   for (uint32_t k = 0; k < NBUF; k++)
     ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&c->side_go, hipEventDisableTiming) == hipSuccess &&
+       hipEventCreateWithFlags(&c->side_tab, hipEventDisableTiming) == hipSuccess &&
        hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming) == hipSuccess;
   ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess && dalloc(&c->hist, c->nslots) == hipSuccess;
   ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess && dalloc(&c->arena2, cfg.arena_bytes) == hipSuccess;
@@ -394,6 +395,7 @@ void eng_destroy(Engine* c) {
   if (c->side) (void)hipStreamSynchronize(c->side);
   if (c->side_go) (void)hipEventDestroy(c->side_go);
   if (c->side_done) (void)hipEventDestroy(c->side_done);
+  if (c->side_tab) (void)hipEventDestroy(c->side_tab);
   for (uint32_t k = 0; k < PROF_RING; k++)
     for (int i = 0; i <= RL_NUM_STAGES; i++)
       if (c->ev[k][i]) (void)hipEventDestroy(c->ev[k][i]);

@@ -30,7 +30,7 @@ constexpr uint32_t STAT_LDS_RULES = 512;  // rules aggregated in LDS (== LDS_RUL
 #define RL_RG_BLOCKS 64
 #endif
 constexpr uint32_t RUNS_GENERAL_BLOCKS = RL_RG_BLOCKS;  // k_runs_general grids (grid-stride over deferrals):
-constexpr uint32_t RUNS_GENERAL_LATE_BLOCKS = 8;  //   RUN_MULTI runs beside k_runs / k_runs' deferrals after it
+constexpr uint32_t RUNS_GENERAL_LATE_BLOCKS = 8;  //   RUN_MULTI runs beside k_table / k_table's deferrals after it
 
 struct Wire;
 struct BatchDev {
@@ -181,13 +181,14 @@ struct Scratch {
 // batch's stage B; stage B (table probe, replay, decisions, stats, results)
 // must run in batch order.
 void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_t st, hipEvent_t* ev = nullptr);
-// Stage B launches the RUN_MULTI runs' exact replay on `side` (ordered by the
-// events go / side_done) so that it overlaps k_runs.
+// Stage B launches the exact path (k_runs_general) on `side`: the RUN_MULTI
+// runs beside k_table (after event go), k_table's deferrals after it (event
+// tab); the stream st waits for side_done before k_finish.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                    int restore, hipStream_t st, hipStream_t side, hipEvent_t go, hipEvent_t side_done,
-                    hipEvent_t* ev = nullptr);
+                    int restore, hipStream_t st, hipStream_t side, hipEvent_t go, hipEvent_t tab,
+                    hipEvent_t side_done, hipEvent_t* ev = nullptr);
 // ev (optional, RL_NUM_STAGES + 1 events on stream st): recorded before
-// k_prepare, after it, after the sort, just before and just after k_runs, and
+// k_prepare, after it, after the sort, just before and just after k_table, and
 // at the end (per-stage timing, rl_profile).
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
                        uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st);

@@ -1035,6 +1035,8 @@ __global__ __launch_bounds__(256) void k_part(const uint32_t* __restrict__ kin, 
   constexpr uint32_t DPT = PART_DIGITS / 256;  // digits per thread
   __shared__ uint32_t wcnt[4][PART_DIGITS];
   __shared__ uint32_t wsum[4];
+  // the tile in partitioned order (key, index, hits), written out as whole lines
+  __shared__ uint32_t sk[PART_TILE], sv[PART_TILE], sh[PART_TILE];
   if (*err) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, tile = blockIdx.x;
   for (uint32_t j = tid; j < 4 * PART_DIGITS; j += 256) (&wcnt[0][0])[j] = 0;
@@ -1076,12 +1078,26 @@ __global__ __launch_bounds__(256) void k_part(const uint32_t* __restrict__ kin, 
     excl += c[j];
   }
   __syncthreads();
+  // Scatter into LDS, then stream the tile out with consecutive 16-B stores:
+  // scattering straight to HBM left ~4 records per digit segment, i.e. partial
+  // 64-B lines (3.8x write amplification, profiles/r02/traffic_c1.json).
 #pragma unroll
   for (uint32_t i = 0; i < PART_ITEMS; i++) {
     if (wbase + i * 64 + lane < n) {
       const uint32_t d = kk[i] >> (32 - PART_BITS);
-      out[tile * PART_TILE + wcnt[wave][d] + pos[i]] = make_uint4(kk[i], vv[i], hh[i], 0u);  // one 16-B record
+      const uint32_t q = wcnt[wave][d] + pos[i];
+      sk[q] = kk[i];
+      sv[q] = vv[i];
+      sh[q] = hh[i];
     }
+  }
+  __syncthreads();
+  const uint32_t cnt = min(PART_TILE, n - tile * PART_TILE);
+  uint4* o = out + (size_t)tile * PART_TILE;
+#pragma unroll
+  for (uint32_t i = 0; i < PART_ITEMS; i++) {
+    const uint32_t q = i * 256 + tid;
+    if (q < cnt) o[q] = make_uint4(sk[q], sv[q], sh[q], 0u);  // one 16-B record
   }
 }
 
@@ -2153,10 +2169,16 @@ __device__ __attribute__((always_inline)) inline uint32_t block_compact(uint32_t
 // k_run_check marks every descriptor whose sort key occurs twice or more in the
 // batch (FLAG_DUP in its record, one plain store per descriptor: the thread of
 // sorted position q marks q, and the run's head when q is its second element).
-// k_unique answers the unmarked ones in arrival order; k_runs the runs.
+// k_table answers the unmarked ones in arrival order and the runs in sorted
+// order. A run must hold one stem under one unit and one window: every
+// non-head element is compared with the run's HEAD (equivalent to comparing
+// neighbours, and the head's record and stem are shared by the whole run, so
+// they stay in cache: one random record and stem read per element instead of
+// two, which matters for the hot keys' long runs).
 __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
                                                    const uint32_t* __restrict__ skeys,
                                                    const uint32_t* __restrict__ rid,
+                                                   const uint32_t* __restrict__ run_start,
                                                    uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
                                                    uint32_t* defer_n, const uint32_t* err) {
   __shared__ uint32_t s_list[CHUNK], s_cnt;
@@ -2170,10 +2192,12 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
 #pragma unroll 1
   for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
     const uint32_t q = s_list[j];
-    const Rec x = rec_s[q], y = rec_s[q - 1];
     const uint32_t r = rid[q];
-    rec[rec_s.sv[q]].lu = x.lu | (FLAG_DUP << 24);
-    if (q == 1 || skeys[q - 2] != skeys[q]) rec[rec_s.sv[q - 1]].lu = y.lu | (FLAG_DUP << 24);  // the run's head
+    const uint32_t p = run_start[r];
+    const uint32_t eq = rec_s.sv[q], ep = rec_s.sv[p];
+    const Rec x = rec[eq], y = rec[ep];
+    rec[eq].lu = x.lu | (FLAG_DUP << 24);
+    if (q == p + 1) rec[ep].lu = y.lu | (FLAG_DUP << 24);  // the run's head
     // a failed descriptor (FLAG_SKIP) makes its run exact-path: k_runs_general leaves it out
     const bool same = !((rec_flags(x) | rec_flags(y)) & FLAG_SKIP) && x.hlo == y.hlo &&
                       (x.lu & 0xFFFFFFu) == (y.lu & 0xFFFFFFu) &&  // hash, length, unit
@@ -2195,7 +2219,7 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
 // no other descriptor in the batch, so the lanes are independent and this
 // kernel commutes with the sorted path (k_runs). A stem that lives in the
 // table under another unit too is left to k_runs_general (defer1).
-__global__ __launch_bounds__(256) void k_unique(BatchDev b, TableDev t, Params P, const Rec* __restrict__ rec,
+__device__ __attribute__((always_inline)) inline void unique_body(uint32_t blk, BatchDev b, TableDev t, Params P, const Rec* __restrict__ rec,
                                                 const uint32_t* __restrict__ keys0, unsigned long long* __restrict__ res,
                                                 uint32_t* __restrict__ defer1, uint32_t* defer1_n,
                                                 unsigned long long* stats, unsigned long long* stripes, uint32_t* err,
@@ -2203,7 +2227,7 @@ __global__ __launch_bounds__(256) void k_unique(BatchDev b, TableDev t, Params P
   __shared__ uint32_t s_err, s_cnt, s_list[256];
   if (threadIdx.x == 0) s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  const uint32_t lo = blockIdx.x * 256, hi = min(lo + 256, b.n);
+  const uint32_t lo = blk * 256, hi = min(lo + 256, b.n);
   if (s_err || lo >= hi) return;
   if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
   uint32_t* ferr = P.isolate ? errs : err;
@@ -2268,7 +2292,7 @@ __device__ inline void fail_range(unsigned long long* res, const uint32_t* svals
   for (uint32_t q = p; q < end; q++) res[svals[q]] = pack_fail(st);
 }
 
-__global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, SRec rec_s,
+__device__ __attribute__((always_inline)) inline void runs_body(uint32_t blk, BatchDev b, TableDev t, Params P, SRec rec_s,
                                               const uint32_t* __restrict__ skeys,
                                               const uint32_t* __restrict__ svals, unsigned long long* __restrict__ res,
                                               const uint32_t* __restrict__ run_start,
@@ -2286,7 +2310,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
     s_nr = (uint32_t)(*num_runs >> 32);  // runs of two or more (drun)
   }
   __syncthreads();
-  const uint32_t lo = blockIdx.x * 256, hi = min(lo + 256, s_nr);
+  const uint32_t lo = blk * 256, hi = min(lo + 256, s_nr);
   if (s_err || lo >= hi) return;
   if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
   uint32_t* ferr = P.isolate ? errs : err;  // descriptor-level failures: soft word with statuses
@@ -2299,7 +2323,7 @@ __global__ __launch_bounds__(256) void k_runs(BatchDev b, TableDev t, Params P, 
   // past LDS_RULES rules), not through a block-wide LDS table.
   if ((threadIdx.x & ~63u) >= cnt) return;
   StatAcc acc{false, b.n_rules <= LDS_RULES && !restore
-                         ? stripes + (size_t)(blockIdx.x % STAT_STRIPES) * b.n_rules * RL_NUM_STATS : stats};
+                         ? stripes + (size_t)(blk % STAT_STRIPES) * b.n_rules * RL_NUM_STATS : stats};
   LaneStats L;
   L.reset();
   if (threadIdx.x < cnt) {
@@ -2438,7 +2462,7 @@ __global__ __launch_bounds__(256) void k_fast_over(uint32_t n, SRec rec_s,
   }
 }
 
-__global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules, TableDev t, Params P,
+__device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t blk, uint32_t n, uint32_t n_rules, TableDev t, Params P,
                                                    SRec rec_s, const uint32_t* __restrict__ svals,
                                                    unsigned long long* __restrict__ res,
                                                    const uint32_t* __restrict__ segsum,
@@ -2453,7 +2477,7 @@ __global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules,
   __shared__ uint32_t s_err, s_fast;
   if (threadIdx.x == 0) {
     s_err = *err;
-    s_fast = (fast_blk[blockIdx.x >> 5] >> (blockIdx.x & 31)) & 1u;
+    s_fast = (fast_blk[blk >> 5] >> (blk & 31)) & 1u;
   }
   __syncthreads();
   if (s_err || !s_fast) return;  // no RUN_FAST descriptor in this block (k_runs' bitmap)
@@ -2462,7 +2486,7 @@ __global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules,
   StatAcc acc{use_lds, stats};
   LaneStats L;
   L.reset();
-  const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t q = blk * 256 + threadIdx.x;
   const uint32_t r = q < n ? rid[q] : 0u;
   if (q < n && (run_flags[r] & RUN_FAST)) {
     const uint4 st = run_state[r];
@@ -2553,7 +2577,7 @@ __device__ inline void stem_exact(const TableDev& t, const Params& P, unsigned l
   }
 }
 
-__global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Params P, SRec rec_s,
+__device__ __attribute__((always_inline)) inline void general_body(uint32_t blk, uint32_t nblk, BatchDev b, TableDev t, Params P, SRec rec_s,
                                                       const uint32_t* __restrict__ skeys,
                                                       const uint32_t* __restrict__ svals,
                                                       unsigned long long* __restrict__ res,
@@ -2572,7 +2596,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
     s_n1 = defer1_n ? *defer1_n : 0u;
   }
   __syncthreads();
-  if (s_err || (blockIdx.x * 256 >= s_n && blockIdx.x * 256 >= s_n1)) return;
+  if (s_err || (blk * 256 >= s_n && blk * 256 >= s_n1)) return;
   if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
   uint32_t* ferr = P.isolate ? errs : err;
   const bool use_lds = !restore && b.n_rules <= LDS_RULES;
@@ -2582,7 +2606,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
   L.reset();
   // Grid-stride over the deferred runs: the grid is small and fixed (deferrals
   // are rare), so an empty deferral list costs one short launch.
-  for (uint32_t di = blockIdx.x * 256 + threadIdx.x; di < s_n; di += gridDim.x * 256) {
+  for (uint32_t di = blk * 256 + threadIdx.x; di < s_n; di += nblk * 256) {
     const uint32_t rr = defer[di];  // run id
     const uint32_t p = run_start[rr], end = run_end[rr];
     const uint32_t key = skeys[p];
@@ -2646,7 +2670,7 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
     }
   }
   // singletons k_unique found under several units (arrival indices)
-  for (uint32_t di = blockIdx.x * 256 + threadIdx.x; di < s_n1; di += gridDim.x * 256) {
+  for (uint32_t di = blk * 256 + threadIdx.x; di < s_n1; di += nblk * 256) {
     const uint32_t e = defer1[di];
     const Rec x = rec_s.rec[e];
     const uint64_t hs = ((uint64_t)keys0[e] << 32) | x.hlo;
@@ -2655,6 +2679,70 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
   }
   if (!restore) wave_flush(L, acc);
   stats_block_end(use_lds, b.n_rules, stripes);
+}
+
+// ---- stage B grids. Each combines parts that touch disjoint stems, so they
+// share the GPU instead of queueing one behind the other on the table stage's
+// critical path.
+//
+// k_table: the runs of two or more (runs_body, blocks [0, g_runs)) and the keys
+// seen once (unique_body, the rest).
+__global__ __launch_bounds__(256) void k_table(uint32_t g_runs, BatchDev b, TableDev t, Params P, SRec rec_s,
+                                               const uint32_t* __restrict__ skeys,
+                                               const uint32_t* __restrict__ svals,
+                                               unsigned long long* __restrict__ res,
+                                               const uint32_t* __restrict__ run_start,
+                                               const uint32_t* __restrict__ run_end, uint32_t* __restrict__ run_flags,
+                                               uint4* __restrict__ run_state, uint32_t* __restrict__ run_f,
+                                               const unsigned long long* num_runs, const uint32_t* __restrict__ drun,
+                                               uint32_t* __restrict__ defer2, uint32_t* defer2_n,
+                                               const uint32_t* __restrict__ keys0, uint32_t* __restrict__ defer1,
+                                               uint32_t* defer1_n, unsigned long long* stats,
+                                               unsigned long long* stripes, uint32_t* err, uint32_t* errs, int restore,
+                                               uint32_t* __restrict__ fast_blk) {
+  if (blockIdx.x < g_runs)
+    runs_body(blockIdx.x, b, t, P, rec_s, skeys, svals, res, run_start, run_end, run_flags, run_state, run_f,
+              num_runs, drun, defer2, defer2_n, stats, stripes, err, errs, restore, fast_blk);
+  else
+    unique_body(blockIdx.x - g_runs, b, t, P, rec_s.rec, keys0, res, defer1, defer1_n, stats, stripes, err, errs,
+                restore);
+}
+
+// k_runs_general (side stream): beside k_table, the RUN_MULTI runs (defer);
+// after it, the stems k_table found under several units in the table (defer:
+// its runs, defer1: keys seen once).
+__global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Params P, SRec rec_s,
+                                                      const uint32_t* __restrict__ skeys,
+                                                      const uint32_t* __restrict__ svals,
+                                                      unsigned long long* __restrict__ res,
+                                                      const uint32_t* __restrict__ run_start,
+                                                      const uint32_t* __restrict__ run_end,
+                                                      const uint32_t* __restrict__ defer, const uint32_t* defer_n,
+                                                      uint32_t* __restrict__ grp, uint32_t* __restrict__ lead,
+                                                      uint8_t* __restrict__ gmask, const uint32_t* __restrict__ keys0,
+                                                      const uint32_t* __restrict__ defer1, const uint32_t* defer1_n,
+                                                      unsigned long long* stats, unsigned long long* stripes,
+                                                      uint32_t* err, uint32_t* errs, int restore) {
+  general_body(blockIdx.x, gridDim.x, b, t, P, rec_s, skeys, svals, res, run_start, run_end, defer, defer_n, grp, lead,
+               gmask, keys0, defer1, defer1_n, stats, stripes, err, errs, restore);
+}
+
+// k_fast_emit (after k_table, and k_fast_over with the local cache on): the
+// long runs' elements.
+__global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules, TableDev t, Params P, SRec rec_s,
+                                                   const uint32_t* __restrict__ svals,
+                                                   unsigned long long* __restrict__ res,
+                                                   const uint32_t* __restrict__ segsum,
+                                                   const uint32_t* __restrict__ rid,
+                                                   const uint32_t* __restrict__ run_start,
+                                                   const uint32_t* __restrict__ run_end,
+                                                   const uint32_t* __restrict__ run_flags,
+                                                   const uint4* __restrict__ run_state,
+                                                   const uint32_t* __restrict__ run_f, unsigned long long* stats,
+                                                   unsigned long long* stripes, const uint32_t* err,
+                                                   const uint32_t* __restrict__ fast_blk) {
+  fast_emit_body(blockIdx.x, n, n_rules, t, P, rec_s, svals, res, segsum, rid, run_start, run_end, run_flags,
+                 run_state, run_f, stats, stripes, err, fast_blk);
 }
 
 // First kernel of the table stage: merge this batch's validation errors into
@@ -2832,11 +2920,6 @@ __global__ __launch_bounds__(256) void k_debug_decide(uint32_t n, const uint32_t
 // ===========================================================================
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
-#ifndef RL_RUNS_SIDE
-#define RL_RUNS_SIDE 0
-#endif
-#define RL_RUNS_STREAM (RL_RUNS_SIDE ? side : st)
-
 // Stage A (table-free): validate, hash, sort, segment, and mark the descriptors
 // whose sort key occurs more than once. Uses only this buffer's scratch and its
 // validation word s.err. Sorted keys go to keys[1] (keys[0] keeps the arrival
@@ -2868,8 +2951,8 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
                                                               s.keys[1], s.vals[0], s.hits_s, s.hit_t, s.segsum,
                                                               s.rid, s.run_start, s.run_end, s.runs64, s.drun, s.big_meta,
                                                               s.big_n, s.big_cnt, s.err);
-    k_run_check<<<cdiv(b.n, CHUNK), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[1], s.rid, s.run_flags, s.defer,
-                                                s.defer_n, s.err);
+    k_run_check<<<cdiv(b.n, CHUNK), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[1], s.rid, s.run_start,
+                                                s.run_flags, s.defer, s.defer_n, s.err);
   }
 }
 
@@ -2878,8 +2961,8 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
 // result into it first. k_unique (keys seen once) and the sorted path (k_runs
 // and its exact / parallel companions) touch disjoint stems.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                    int restore, hipStream_t st, hipStream_t side, hipEvent_t go, hipEvent_t side_done,
-                    hipEvent_t* ev) {
+                    int restore, hipStream_t st, hipStream_t side, hipEvent_t go, hipEvent_t tab,
+                    hipEvent_t side_done, hipEvent_t* ev) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
   k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, s.defer2_n, s.defer1_n, o.stats, m, s.fast_blk, cdiv(b.n, 256 * 32));
@@ -2887,34 +2970,38 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     const uint32_t g = cdiv(b.n, 256);
     const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
     const SRec rs{s.rec, s.vals[0]};
-    // Side stream: the RUN_MULTI runs (known since k_run_check); main stream:
-    // the runs of two or more (k_runs), then the keys seen once (k_unique).
-    // The three touch disjoint stems. (The order and stream split were chosen
-    // by A/B on the pipelined C1/C2 benches)
+    // Side stream: the RUN_MULTI runs (known since k_run_check) beside k_table,
+    // then k_table's deferrals. Main stream: k_table (the runs of two or more
+    // and the keys seen once), then the long runs' elements (k_fast_*). All
+    // these grids touch disjoint stems; k_finish waits for both streams.
     (void)hipEventRecord(go, st);
     (void)hipStreamWaitEvent(side, go, 0);
-    k_runs_general<<<g < RUNS_GENERAL_BLOCKS ? g : RUNS_GENERAL_BLOCKS, 256, lds, side>>>(
-        b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer, s.defer_n, s.grp, s.lead, s.gmask,
-        s.keys[0], nullptr, nullptr, o.stats, s.stripes, s.errb, s.errs, restore);
-    k_runs<<<cdiv(b.n / 2 + BIG_HEAVY * PART_DIGITS, 256), 256, 0, RL_RUNS_STREAM>>>(
-        b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.run_flags, s.run_state, s.run_f, s.runs64,
-        s.drun, s.defer2, s.defer2_n, o.stats, s.stripes, s.errb, s.errs, restore, s.fast_blk);
-    (void)hipEventRecord(side_done, side);
+    const uint32_t gs = g < RUNS_GENERAL_BLOCKS ? g : RUNS_GENERAL_BLOCKS;
+    k_runs_general<<<gs, 256, lds, side>>>(b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer,
+                                           s.defer_n, s.grp, s.lead, s.gmask, nullptr, nullptr, nullptr, o.stats,
+                                           s.stripes, s.errb, s.errs, restore);
     if (ev) (void)hipEventRecord(ev[3], st);
-    k_unique<<<cdiv(b.n, 256), 256, lds, st>>>(b, t, P, s.rec, s.keys[0], s.res, s.defer1, s.defer1_n, o.stats,
-                                               s.stripes, s.errb, s.errs, restore);
+    const uint32_t g_runs = cdiv(b.n / 2 + BIG_HEAVY * PART_DIGITS, 256);
+    k_table<<<g_runs + g, 256, lds, st>>>(g_runs, b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end,
+                                         s.run_flags, s.run_state, s.run_f, s.runs64, s.drun, s.defer2, s.defer2_n,
+                                         s.keys[0], s.defer1, s.defer1_n, o.stats, s.stripes, s.errb, s.errs, restore,
+                                         s.fast_blk);
     if (ev) (void)hipEventRecord(ev[4], st);
-    (void)hipStreamWaitEvent(st, side_done, 0);
-    // stems k_unique / k_runs found under several units in the table (rare)
-    k_runs_general<<<RUNS_GENERAL_LATE_BLOCKS, 256, lds, st>>>(
+    (void)hipEventRecord(tab, st);
+    (void)hipStreamWaitEvent(side, tab, 0);
+    k_runs_general<<<RUNS_GENERAL_LATE_BLOCKS, 256, lds, side>>>(
         b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer2, s.defer2_n, s.grp, s.lead, s.gmask,
         s.keys[0], s.defer1, s.defer1_n, o.stats, s.stripes, s.errb, s.errs, restore);
+    (void)hipEventRecord(side_done, side);
     if (!restore) {
       if (P.lc_en)
         k_fast_over<<<g, 256, 0, st>>>(b.n, rs, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
       k_fast_emit<<<g, 256, lds, st>>>(b.n, b.n_rules, t, P, rs, s.vals[0], s.res, s.segsum, s.rid, s.run_start,
                                        s.run_end, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb,
                                        s.fast_blk);
+    }
+    (void)hipStreamWaitEvent(st, side_done, 0);
+    if (!restore) {
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;
       const uint32_t gf = cdiv(nf * RL_NUM_STATS > b.n ? nf * RL_NUM_STATS : b.n, 256);
       k_finish<<<gf, 256, 0, st>>>(s.res, b.n, o, s.stripes, nf, s.errb, P.lc_en ? s.counters + 5 : nullptr);

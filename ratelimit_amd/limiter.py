@@ -27,7 +27,7 @@ from .packing import PackedBatch, RuleInterner, pack_calls
 from .types import OK, DescriptorStatus, Limit  # noqa: F401  (re-exported data model)
 
 # rl_profile stages (include/ratelimit_hip.h RL_NUM_STAGES)
-STAGES = ("prepare", "sort", "segment", "unique", "finish")
+STAGES = ("prepare", "sort", "segment", "table", "finish")
 
 __all__ = ["GpuRateLimitCache", "GpuRateLimitService", "RedisError", "TimeSource"]
 

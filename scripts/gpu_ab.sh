@@ -10,7 +10,7 @@ for lib in "" build_abl/lib_*.so; do
     tag=$(basename "${lib:-cur}" .so)_${cfg}_$rep
     RL_LIB_PATH=${lib:+$PWD/$lib} timeout -k 10 200 python -u bench.py --config $cfg --no-cpu-baseline --steps 200 --latency-steps 5 \
       > gpurun_out/ab_$tag.log 2>&1 || { tail -5 gpurun_out/ab_$tag.log; exit 1; }
-    python -c "import json; d=json.loads(open('gpurun_out/ab_$tag.log').read().strip().splitlines()[-1]); print('$tag', round(d['value']/1e9,3), 'G/s', round(d['ms_per_step'],4), 'ms unique', d['roofline']['stage_ms']['unique'])"
+    python -c "import json; d=json.loads(open('gpurun_out/ab_$tag.log').read().strip().splitlines()[-1]); print('$tag', round(d['value']/1e9,3), 'G/s', round(d['ms_per_step'],4), 'ms table', d['roofline']['stage_ms']['table'])"
   done
 done
 done

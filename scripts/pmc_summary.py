@@ -9,7 +9,7 @@ after table fill and warm-up). The guide leaves other access widths
 uncalibrated, so gpurun_out/pmc_probe_* (tools/pmcprobe.hip, known byte
 counts) give the measured bytes-per-counted-byte of random 64-B sector reads
 and of 64-B-per-lane streaming reads; both are recorded beside the per-kernel
-figures, and the k_unique line is bracketed by them (its reads are part
+figures, and the k_table line is bracketed by them (its reads are part
 streamed records, part random slot sectors).
 """
 import csv
@@ -73,15 +73,15 @@ def main():
                  "random64_read_bytes_per_fetch_byte": rd / (pfk["k_rand64"] * 1024.0),
                  "seq64_read_bytes_per_fetch_byte": rd / (pfk["k_seq"] * 1024.0),
                  "random64_write_bytes_per_write_byte": wr / max(pwk["k_rand64"] * 1024.0, 1.0)}
-    ku = kernels.get("rl::k_unique", {})
+    ku = kernels.get("rl::k_table", {})
     res = {"config": cfg, "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate runs; median of the "
                                     "last %d dispatches per kernel; read = 2 x FETCH_SIZE (gfx950 correction)" % tail,
            "calibration": calib,
            "kernels": kernels,
-           "k_unique_bytes_per_launch": ku.get("traffic_bytes")}
+           "k_table_bytes_per_launch": ku.get("traffic_bytes")}
     if calib and ku:
         f = ku["fetch_size_bytes"]
-        res["k_unique_read_bytes_bounds"] = sorted([f * calib["random64_read_bytes_per_fetch_byte"],
+        res["k_table_read_bytes_bounds"] = sorted([f * calib["random64_read_bytes_per_fetch_byte"],
                                                     f * calib["seq64_read_bytes_per_fetch_byte"]])
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     p = os.path.join(ROOT, "profiles", "traffic_%s.json" % cfg)

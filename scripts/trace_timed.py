@@ -1,4 +1,4 @@
-"""k_unique duration from a rocprofv3 kernel trace of one bench.py run, split by
+"""k_table duration from a rocprofv3 kernel trace of one bench.py run, split by
 phase: fill + warmup launches, the K timed launches, the latency launches.
 The timed-region average is what bench.py's HIP events (roofline.achieved)
 must agree with; the whole-run kernel_stats average also holds the fill
@@ -16,14 +16,14 @@ def main():
     d = json.loads([l for l in open(bench) if l.startswith('{"metric')][-1])
     k = d["steps"]
     lat = 50 if len(sys.argv) < 5 else int(sys.argv[4])
-    rows = [r for r in csv.DictReader(open(trace)) if r["Kernel_Name"].startswith("rl::k_unique(")]
+    rows = [r for r in csv.DictReader(open(trace)) if r["Kernel_Name"].startswith("rl::k_table(")]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     us = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
     timed = us[len(us) - lat - k:len(us) - lat]
     out = {
-        "kernel": "k_unique", "launches": len(us), "timed_launches": len(timed),
+        "kernel": "k_table", "launches": len(us), "timed_launches": len(timed),
         "trace_timed_avg_us": round(sum(timed) / len(timed), 1),
-        "events_unique_avg_us": round(d["roofline"]["stage_ms"]["unique"] * 1e3, 1),
+        "events_table_avg_us": round(d["roofline"]["stage_ms"]["table"] * 1e3, 1),
         "trace_other_avg_us": round((sum(us) - sum(timed)) / max(1, len(us) - len(timed)), 1),
         "trace_all_avg_us": round(sum(us) / len(us), 1),
     }
