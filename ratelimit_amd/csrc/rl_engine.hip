@@ -134,14 +134,14 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     (void)hipStreamWaitEvent(a, c->consumed[k], 0);  // ... and its routed results were read
     launch_stage_a(b, c->s[k], isolate, a, ev);
     (void)hipStreamWaitEvent(a, c->b_done[c->last], 0);  // table order
-    launch_stage_b(b, o, t, P, c->s[k], restore, a, c->side, c->side_go, c->side_tab, c->side_done, ev);
+    launch_stage_b(b, o, t, P, c->s[k], restore, a, c->side, c->side_go, c->side_done, ev);
     (void)hipEventRecord(c->b_done[k], a);
   } else {
     if (!st) st = c->stream;
     (void)after_batches(c, st);
     hipEvent_t* ev = prof_events(c);
     launch_stage_a(b, c->s[k], isolate, st, ev);
-    launch_stage_b(b, o, t, P, c->s[k], restore, st, c->side, c->side_go, c->side_tab, c->side_done, ev);
+    launch_stage_b(b, o, t, P, c->s[k], restore, st, c->side, c->side_go, c->side_done, ev);
     (void)hipEventRecord(c->b_done[k], st);
   }
   c->last = k;
@@ -217,7 +217,7 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
        dalloc(&s.rid, n) == hipSuccess && dalloc(&s.run_start, (size_t)n + 1) == hipSuccess &&
        dalloc(&s.run_flags, n) == hipSuccess && dalloc(&s.run_state, n) == hipSuccess &&
        dalloc(&s.run_f, n) == hipSuccess &&
-       dalloc(&s.runs64, 1) == hipSuccess && dalloc(&s.drun, (size_t)n / 2 + BIG_HEAVY * PART_DIGITS) == hipSuccess;
+       dalloc(&s.runs64, 1) == hipSuccess && dalloc(&s.split, 2) == hipSuccess && dalloc(&s.drun, (size_t)n / 2 + BIG_HEAVY * PART_DIGITS) == hipSuccess;
   ok = ok && dalloc(&s.hit_a, n) == hipSuccess && dalloc(&s.tile, n) == hipSuccess &&
        dalloc(&s.hit_t, n) == hipSuccess;
   ok = ok && dalloc(&s.run_end, n) == hipSuccess &&
@@ -230,7 +230,7 @@ void free_buffer(Scratch& s) {
   void* bufs[] = {s.rec, s.res, s.big_meta, s.big_n, s.big_work, s.work_n, s.big_cnt, s.keys[0], s.keys[1],
                   s.vals[0], s.vals[1], s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1,
                   s.defer1_n, s.fast_blk, s.hits_s, s.segsum, s.rid, s.run_start, s.run_flags, s.run_state, s.run_f,
-                  s.runs64, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t, s.r_base};
+                  s.runs64, s.split, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t, s.r_base};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
 }
@@ -313,7 +313,6 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   for (uint32_t k = 0; k < NBUF; k++)
     ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&c->side_go, hipEventDisableTiming) == hipSuccess &&
-       hipEventCreateWithFlags(&c->side_tab, hipEventDisableTiming) == hipSuccess &&
        hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming) == hipSuccess;
   ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess && dalloc(&c->hist, c->nslots) == hipSuccess;
   ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess && dalloc(&c->arena2, cfg.arena_bytes) == hipSuccess;
@@ -395,7 +394,6 @@ void eng_destroy(Engine* c) {
   if (c->side) (void)hipStreamSynchronize(c->side);
   if (c->side_go) (void)hipEventDestroy(c->side_go);
   if (c->side_done) (void)hipEventDestroy(c->side_done);
-  if (c->side_tab) (void)hipEventDestroy(c->side_tab);
   for (uint32_t k = 0; k < PROF_RING; k++)
     for (int i = 0; i <= RL_NUM_STAGES; i++)
       if (c->ev[k][i]) (void)hipEventDestroy(c->ev[k][i]);

@@ -161,6 +161,7 @@ struct Scratch {
   uint4* run_state;                    // [n] {slot, c0, old lc, F | which<<1}
   uint32_t* run_f;                     // [n] first over-limit position
   unsigned long long* runs64;          // bucket path: runs | runs of two or more << 32
+  unsigned long long* split;           // k_split: [0] reservations (ids | dup-run entries << 32), [1] runs64 before it
   uint32_t* drun;                      // [n/2 + BIG_HEAVY x PART_DIGITS] ids of the runs of two or more
   uint32_t* err;   // validation word of this buffer's batch (stage A)
   uint32_t* errb;  // sticky table-stage word (stage B), shared by both buffers
@@ -181,12 +182,12 @@ struct Scratch {
 // batch's stage B; stage B (table probe, replay, decisions, stats, results)
 // must run in batch order.
 void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_t st, hipEvent_t* ev = nullptr);
-// Stage B launches the exact path (k_runs_general) on `side`: the RUN_MULTI
-// runs beside k_table (after event go), k_table's deferrals after it (event
-// tab); the stream st waits for side_done before k_finish.
+// Stage B launches the RUN_MULTI runs' exact path (k_runs_general) on `side`
+// beside k_table (after event go); the stream st waits for side_done before
+// k_finish.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                    int restore, hipStream_t st, hipStream_t side, hipEvent_t go, hipEvent_t tab,
-                    hipEvent_t side_done, hipEvent_t* ev = nullptr);
+                    int restore, hipStream_t st, hipStream_t side, hipEvent_t go, hipEvent_t side_done,
+                    hipEvent_t* ev = nullptr);
 // ev (optional, RL_NUM_STAGES + 1 events on stream st): recorded before
 // k_prepare, after it, after the sort, just before and just after k_table, and
 // at the end (per-stage timing, rl_profile).

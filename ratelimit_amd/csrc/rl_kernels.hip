@@ -2180,8 +2180,13 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
                                                    const uint32_t* __restrict__ rid,
                                                    const uint32_t* __restrict__ run_start,
                                                    uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
-                                                   uint32_t* defer_n, const uint32_t* err) {
+                                                   uint32_t* defer_n, const uint32_t* err,
+                                                   const unsigned long long* num_runs, unsigned long long* split) {
   __shared__ uint32_t s_list[CHUNK], s_cnt;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // k_split's reservations start from the bucket kernels' count
+    split[0] = 0;
+    split[1] = *num_runs;
+  }
   if (*err) return;
   const uint32_t lo = max(blockIdx.x * CHUNK, 1u), hi = min(blockIdx.x * CHUNK + CHUNK, b.n);
   if (lo >= hi) return;
@@ -2208,6 +2213,187 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
       const uint32_t d = div_of(rec_unit(x));
       if (x.now / d != y.now / d) atomicOr(&run_flags[r], RUN_SLOW);
     }
+  }
+}
+
+// ---- k_split: hash-prefix collisions. A run is defined by the 32-bit sort
+// key; k_run_check flags it RUN_MULTI when its elements do not all share the
+// head's stem and unit. When they form at most SPLIT_MAXG distinct stems, each
+// under one unit (the usual case: unrelated keys whose hashes agree in 32
+// bits, ~100 runs per 1M batch at C1), the run is reordered stably by stem
+// into consecutive sub-runs with their own run ids, in-run sums and flags, and
+// k_table answers them like any other run (a sub-run of one element becomes a
+// key seen once) instead of the one-lane exact path, whose chain of dependent
+// table accesses outlasted k_table. Anything else (a stem under several
+// units, a 64-bit hash collision, a failed descriptor, more than SPLIT_CAP
+// elements, or no room left in the dup-run list) stays on the exact path.
+constexpr uint32_t SPLIT_CAP = 1024, SPLIT_MAXG = 8, SPLIT_BLOCKS = 128;
+constexpr uint32_t DEFER_DONE = 0xFFFFFFFFu;  // a deferral k_split resolved
+
+__global__ __launch_bounds__(256) void k_split(BatchDev b, SRec rec_s, uint32_t* __restrict__ svals,
+                                               uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
+                                               uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end,
+                                               uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
+                                               const uint32_t* defer_n, unsigned long long* num_runs,
+                                               unsigned long long* split, uint32_t* __restrict__ drun,
+                                               uint32_t drun_cap, const uint32_t* err) {
+  __shared__ uint32_t s_e[SPLIT_CAP], s_hlo[SPLIT_CAP], s_lu[SPLIT_CAP], s_now[SPLIT_CAP], s_h[SPLIT_CAP];
+  __shared__ uint32_t s_nh[SPLIT_CAP];           // max(1, hits) in the new order
+  __shared__ uint16_t s_pos[SPLIT_CAP];          // rank inside the element's sub-run
+  __shared__ uint8_t s_g[SPLIT_CAP], s_ng[SPLIT_CAP];  // sub-run of each element / of each new position
+  __shared__ uint32_t s_cnt[SPLIT_MAXG], s_base[SPLIT_MAXG], s_id[SPLIT_MAXG], s_fl[SPLIT_MAXG];
+  __shared__ uint32_t s_lnow[SPLIT_MAXG], s_lunit[SPLIT_MAXG];
+  __shared__ uint32_t s_bad, s_lead;
+  if (*err) return;
+  if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t nd = *defer_n;
+  Rec* rec = const_cast<Rec*>(rec_s.rec);
+  for (uint32_t j = blockIdx.x; j < nd; j += gridDim.x) {
+    const uint32_t r = defer[j];
+    const uint32_t p = run_start[r], L = run_end[r] - p;
+    if (L > SPLIT_CAP) continue;  // (uniform)
+    __syncthreads();  // the previous run's shared state has been read
+    if (tid == 0) s_bad = 0;
+    for (uint32_t k = tid; k < L; k += 256) {
+      const uint32_t e = rec_s.sv[p + k];
+      const Rec x = rec[e];
+      s_e[k] = e;
+      s_hlo[k] = x.hlo;
+      s_lu[k] = x.lu;
+      s_now[k] = x.now;
+      s_h[k] = x.hits > 1 ? x.hits : 1u;
+      s_g[k] = 0xFF;
+    }
+    __syncthreads();
+    for (uint32_t k = tid; k < L; k += 256)
+      if ((s_lu[k] >> 24) & FLAG_SKIP) s_bad = 1;
+    // sub-runs: repeatedly the first unassigned element leads, and every
+    // element with its stem (hash, length, then bytes) joins
+    uint32_t G = 0;
+    for (;;) {
+      if (tid == 0) s_lead = 0xFFFFFFFFu;
+      __syncthreads();
+      for (uint32_t k = tid; k < L; k += 256)
+        if (s_g[k] == 0xFF) atomicMin(&s_lead, k);
+      __syncthreads();
+      const uint32_t ld = s_lead;
+      if (ld == 0xFFFFFFFFu || s_bad || G == SPLIT_MAXG) break;  // (uniform)
+      const Rec y = rec[s_e[ld]];
+      const Key ky = key_of(b, y);
+      if (tid == 0) {
+        s_lnow[G] = y.now;
+        s_lunit[G] = rec_unit(y);
+      }
+      for (uint32_t k = tid; k < L; k += 256) {
+        if (s_g[k] != 0xFF || s_hlo[k] != y.hlo || (s_lu[k] & 0xFFFFu) != (y.lu & 0xFFFFu)) continue;
+        if (!key_equal(key_of(b, rec[s_e[k]]), ky)) {
+          s_bad = 1;  // equal 64-bit hash, different stem
+        } else {
+          if (((s_lu[k] >> 16) & 0xFFu) != rec_unit(y)) s_bad = 1;  // one stem, several units
+          s_g[k] = (uint8_t)G;
+        }
+      }
+      G++;
+      __syncthreads();
+    }
+    if (s_lead != 0xFFFFFFFFu) s_bad = 1;  // more than SPLIT_MAXG stems (or stopped early)
+    __syncthreads();
+    if (s_bad || G < 2) continue;  // (uniform) the exact path keeps it
+    // stable ranks inside the sub-runs (wave 0 walks the run in arrival order)
+    if (tid < 64) {
+      uint32_t cnt[SPLIT_MAXG];
+#pragma unroll
+      for (uint32_t g = 0; g < SPLIT_MAXG; g++) cnt[g] = 0;
+      const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+      for (uint32_t c0 = 0; c0 < L; c0 += 64) {
+        const uint32_t k = c0 + lane;
+        const uint32_t gk = k < L ? s_g[k] : 0xFFu;
+#pragma unroll
+        for (uint32_t g = 0; g < SPLIT_MAXG; g++) {
+          const uint64_t m = __ballot(gk == g);
+          if (gk == g) s_pos[k] = (uint16_t)(cnt[g] + __popcll(m & lt));
+          cnt[g] += __popcll(m);
+        }
+      }
+      if (lane == 0) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (uint32_t g = 0; g < SPLIT_MAXG; g++) {
+          s_cnt[g] = cnt[g];
+          s_base[g] = acc;
+          s_fl[g] = 0;
+          acc += cnt[g];
+        }
+        // run ids: sub-run 0 keeps r, the others are new; the dup-run list
+        // (k_table's runs part) takes the new ones of two or more elements
+        uint32_t nd2 = 0;
+        for (uint32_t g = 1; g < G; g++) nd2 += cnt[g] >= 2 ? 1u : 0u;
+        // room: a reservation (one fetch-add; a CAS loop on the shared
+        // counter serialised ~100 blocks) is checked against the bucket
+        // kernels' count plus every reservation before it, so the successful
+        // ones, the only ones added to num_runs, always fit
+        const unsigned long long add = ((unsigned long long)nd2 << 32) | (unsigned long long)(G - 1);
+        const unsigned long long rs = atomicAdd(&split[0], add), base = split[1];
+        const bool room = (uint32_t)(base >> 32) + (uint32_t)(rs >> 32) + nd2 <= drun_cap &&
+                          (uint32_t)base + (uint32_t)rs + (G - 1) <= b.n;
+        unsigned long long old = 0;
+        if (!room) s_bad = 1;
+        else old = atomicAdd(num_runs, add);
+        if (!s_bad) {
+          s_id[0] = r;
+          uint32_t di = (uint32_t)(old >> 32);
+          for (uint32_t g = 1; g < G; g++) {
+            s_id[g] = (uint32_t)old + g - 1;
+            if (cnt[g] >= 2) drun[di++] = s_id[g];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (s_bad) continue;  // (uniform) no room in the dup-run list: the exact path keeps it
+    for (uint32_t k = tid; k < L; k += 256) {
+      const uint32_t g = s_g[k], np = s_base[g] + s_pos[k];
+      svals[p + np] = s_e[k];
+      rid[p + np] = s_id[g];
+      s_nh[np] = s_h[k];
+      s_ng[np] = (uint8_t)g;
+      const uint32_t d = div_of(s_lunit[g]);
+      if (s_now[k] / d != s_lnow[g] / d) atomicOr(&s_fl[g], RUN_SLOW);
+      // a sub-run of one element is a key seen once (k_table's singleton part)
+      if (s_cnt[g] == 1) rec[s_e[k]].lu = s_lu[k] & ~(FLAG_DUP << 24);
+    }
+    __syncthreads();
+    // inclusive sums of max(1, hits) inside each sub-run, in the new order
+    // (wave 0; the sub-runs are consecutive): segmented wave scans + carry
+    if (tid < 64) {
+      uint32_t carry = 0;
+      for (uint32_t c0 = 0; c0 < L; c0 += 64) {
+        const uint32_t k = c0 + lane;
+        const bool in = k < L;
+        uint32_t v = in ? s_nh[k] : 0u;
+        bool f = in && (k == 0 || s_ng[k - 1] != s_ng[k]);  // a sub-run starts here
+#pragma unroll
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+          const uint32_t y = __shfl_up(v, off, 64);
+          const bool yf = __shfl_up(f ? 1 : 0, off, 64) != 0;
+          if (lane >= off) {
+            if (!f) v += y;
+            f = f || yf;
+          }
+        }
+        if (!f) v += carry;  // no sub-run start since the chunk began
+        if (in) segsum[p + k] = v;
+        carry = __shfl(v, 63, 64);
+      }
+    }
+    if (tid < G) {
+      const uint32_t id = s_id[tid];
+      run_start[id] = p + s_base[tid];
+      run_end[id] = p + s_base[tid] + s_cnt[tid];
+      run_flags[id] = s_fl[tid];
+    }
+    if (tid == 0) defer[j] = DEFER_DONE;
   }
 }
 
@@ -2608,6 +2794,7 @@ __device__ __attribute__((always_inline)) inline void general_body(uint32_t blk,
   // are rare), so an empty deferral list costs one short launch.
   for (uint32_t di = blk * 256 + threadIdx.x; di < s_n; di += nblk * 256) {
     const uint32_t rr = defer[di];  // run id
+    if (rr == DEFER_DONE) continue;  // split into ordinary runs (k_split)
     const uint32_t p = run_start[rr], end = run_end[rr];
     const uint32_t key = skeys[p];
     // ---- split the run into distinct stems (hash, length, then bytes)
@@ -2727,22 +2914,34 @@ __global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Pa
                gmask, keys0, defer1, defer1_n, stats, stripes, err, errs, restore);
 }
 
-// k_fast_emit (after k_table, and k_fast_over with the local cache on): the
-// long runs' elements.
-__global__ __launch_bounds__(256) void k_fast_emit(uint32_t n, uint32_t n_rules, TableDev t, Params P, SRec rec_s,
-                                                   const uint32_t* __restrict__ svals,
-                                                   unsigned long long* __restrict__ res,
-                                                   const uint32_t* __restrict__ segsum,
-                                                   const uint32_t* __restrict__ rid,
-                                                   const uint32_t* __restrict__ run_start,
-                                                   const uint32_t* __restrict__ run_end,
-                                                   const uint32_t* __restrict__ run_flags,
-                                                   const uint4* __restrict__ run_state,
-                                                   const uint32_t* __restrict__ run_f, unsigned long long* stats,
-                                                   unsigned long long* stripes, const uint32_t* err,
-                                                   const uint32_t* __restrict__ fast_blk) {
-  fast_emit_body(blockIdx.x, n, n_rules, t, P, rec_s, svals, res, segsum, rid, run_start, run_end, run_flags,
-                 run_state, run_f, stats, stripes, err, fast_blk);
+// k_late (after k_table, and k_fast_over with the local cache on): the stems
+// k_table found under several units in the table (general_body, blocks
+// [0, RUNS_GENERAL_LATE_BLOCKS): defer2 = its runs, defer1 = keys seen once)
+// and the long runs' elements (fast_emit_body, the rest). The two touch
+// disjoint stems. At least 8 waves per SIMD caps the grid at 64 VGPRs: the
+// rare exact path spills to scratch instead of lowering the streaming part's
+// occupancy (uncapped, the exact path's 88 VGPRs slowed the long-run part
+// 55 -> 85 us at C2).
+__global__ __launch_bounds__(256, 8) void k_late(BatchDev b, TableDev t, Params P, SRec rec_s,
+                                                 const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ svals,
+                                                 unsigned long long* __restrict__ res,
+                                                 const uint32_t* __restrict__ run_start,
+                                                 const uint32_t* __restrict__ run_end,
+                                                 const uint32_t* __restrict__ defer2, const uint32_t* defer2_n,
+                                                 uint32_t* __restrict__ grp, uint32_t* __restrict__ lead,
+                                                 uint8_t* __restrict__ gmask, const uint32_t* __restrict__ keys0,
+                                                 const uint32_t* __restrict__ defer1, const uint32_t* defer1_n,
+                                                 const uint32_t* __restrict__ segsum, const uint32_t* __restrict__ rid,
+                                                 const uint32_t* __restrict__ run_flags,
+                                                 const uint4* __restrict__ run_state, const uint32_t* __restrict__ run_f,
+                                                 unsigned long long* stats, unsigned long long* stripes, uint32_t* err,
+                                                 uint32_t* errs, int restore, const uint32_t* __restrict__ fast_blk) {
+  if (blockIdx.x < RUNS_GENERAL_LATE_BLOCKS)
+    general_body(blockIdx.x, RUNS_GENERAL_LATE_BLOCKS, b, t, P, rec_s, skeys, svals, res, run_start, run_end, defer2,
+                 defer2_n, grp, lead, gmask, keys0, defer1, defer1_n, stats, stripes, err, errs, restore);
+  else if (!restore)
+    fast_emit_body(blockIdx.x - RUNS_GENERAL_LATE_BLOCKS, b.n, b.n_rules, t, P, rec_s, svals, res, segsum, rid,
+                   run_start, run_end, run_flags, run_state, run_f, stats, stripes, err, fast_blk);
 }
 
 // First kernel of the table stage: merge this batch's validation errors into
@@ -2952,7 +3151,10 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
                                                               s.rid, s.run_start, s.run_end, s.runs64, s.drun, s.big_meta,
                                                               s.big_n, s.big_cnt, s.err);
     k_run_check<<<cdiv(b.n, CHUNK), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[1], s.rid, s.run_start,
-                                                s.run_flags, s.defer, s.defer_n, s.err);
+                                                s.run_flags, s.defer, s.defer_n, s.err, s.runs64, s.split);
+    k_split<<<SPLIT_BLOCKS, 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.vals[0], s.segsum, s.rid, s.run_start,
+                                          s.run_end, s.run_flags, s.defer, s.defer_n, s.runs64, s.split, s.drun,
+                                          b.n / 2 + BIG_HEAVY * PART_DIGITS, s.err);
   }
 }
 
@@ -2961,8 +3163,8 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
 // result into it first. k_unique (keys seen once) and the sorted path (k_runs
 // and its exact / parallel companions) touch disjoint stems.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                    int restore, hipStream_t st, hipStream_t side, hipEvent_t go, hipEvent_t tab,
-                    hipEvent_t side_done, hipEvent_t* ev) {
+                    int restore, hipStream_t st, hipStream_t side, hipEvent_t go, hipEvent_t side_done,
+                    hipEvent_t* ev) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
   k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, s.defer2_n, s.defer1_n, o.stats, m, s.fast_blk, cdiv(b.n, 256 * 32));
@@ -2970,16 +3172,17 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     const uint32_t g = cdiv(b.n, 256);
     const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
     const SRec rs{s.rec, s.vals[0]};
-    // Side stream: the RUN_MULTI runs (known since k_run_check) beside k_table,
-    // then k_table's deferrals. Main stream: k_table (the runs of two or more
-    // and the keys seen once), then the long runs' elements (k_fast_*). All
-    // these grids touch disjoint stems; k_finish waits for both streams.
+    // Side stream: the RUN_MULTI runs (known since k_run_check) beside k_table.
+    // Main stream: k_table (the runs of two or more and the keys seen once),
+    // then k_late (k_table's deferrals and the long runs' elements). All these
+    // grids touch disjoint stems; k_finish waits for both streams.
     (void)hipEventRecord(go, st);
     (void)hipStreamWaitEvent(side, go, 0);
     const uint32_t gs = g < RUNS_GENERAL_BLOCKS ? g : RUNS_GENERAL_BLOCKS;
     k_runs_general<<<gs, 256, lds, side>>>(b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer,
                                            s.defer_n, s.grp, s.lead, s.gmask, nullptr, nullptr, nullptr, o.stats,
                                            s.stripes, s.errb, s.errs, restore);
+    (void)hipEventRecord(side_done, side);
     if (ev) (void)hipEventRecord(ev[3], st);
     const uint32_t g_runs = cdiv(b.n / 2 + BIG_HEAVY * PART_DIGITS, 256);
     k_table<<<g_runs + g, 256, lds, st>>>(g_runs, b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end,
@@ -2987,19 +3190,12 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
                                          s.keys[0], s.defer1, s.defer1_n, o.stats, s.stripes, s.errb, s.errs, restore,
                                          s.fast_blk);
     if (ev) (void)hipEventRecord(ev[4], st);
-    (void)hipEventRecord(tab, st);
-    (void)hipStreamWaitEvent(side, tab, 0);
-    k_runs_general<<<RUNS_GENERAL_LATE_BLOCKS, 256, lds, side>>>(
+    if (!restore && P.lc_en)
+      k_fast_over<<<g, 256, 0, st>>>(b.n, rs, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
+    k_late<<<RUNS_GENERAL_LATE_BLOCKS + (restore ? 0u : g), 256, lds, st>>>(
         b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer2, s.defer2_n, s.grp, s.lead, s.gmask,
-        s.keys[0], s.defer1, s.defer1_n, o.stats, s.stripes, s.errb, s.errs, restore);
-    (void)hipEventRecord(side_done, side);
-    if (!restore) {
-      if (P.lc_en)
-        k_fast_over<<<g, 256, 0, st>>>(b.n, rs, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
-      k_fast_emit<<<g, 256, lds, st>>>(b.n, b.n_rules, t, P, rs, s.vals[0], s.res, s.segsum, s.rid, s.run_start,
-                                       s.run_end, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb,
-                                       s.fast_blk);
-    }
+        s.keys[0], s.defer1, s.defer1_n, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb,
+        s.errs, restore, s.fast_blk);
     (void)hipStreamWaitEvent(st, side_done, 0);
     if (!restore) {
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;

@@ -16,6 +16,7 @@ def main():
     d = json.loads([l for l in open(bench) if l.startswith('{"metric')][-1])
     k = d["steps"]
     lat = 50 if len(sys.argv) < 5 else int(sys.argv[4])
+    lat += (d.get("pcie_fed") or {}).get("steps", 0)  # the host-fed phase runs after the latency steps
     rows = [r for r in csv.DictReader(open(trace)) if r["Kernel_Name"].startswith("rl::k_table(")]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     us = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]

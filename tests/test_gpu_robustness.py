@@ -44,7 +44,7 @@ def _run(calls, chunks, **kw):
     return outs, stats
 
 
-@pytest.mark.parametrize("bits", [1, 4, 9])
+@pytest.mark.parametrize("bits", [1, 4, 7, 9])
 @pytest.mark.parametrize("lc", [False, True])
 def test_gpu_colliding_sort_keys_vs_python_oracle(bits, lc):
     calls = streams.random_stream(100 + bits, n_calls=500, n_stems=300, zipf=True)
@@ -55,6 +55,25 @@ def test_gpu_colliding_sort_keys_vs_python_oracle(bits, lc):
     for i, (g, e) in enumerate(zip(got, exp)):
         assert g == e, "call %d: gpu %s oracle %s" % (i, g, e)
     assert stats == py_stats
+
+
+@pytest.mark.parametrize("bits", [13, 15])
+def test_gpu_split_colliding_runs_c2_vs_c_oracle(bits):
+    """A few distinct stems per sort key (40k stems over 2^13 / 2^15 keys):
+    k_split reorders such runs into per-stem sub-runs (hot keys included, up to
+    its 1024-element cap; longer runs and the rest stay exact)."""
+    z = workloads.ZipfSampler(20_000, 1.1)
+    batches = list(workloads.c2_stream(n_tenants=20_000, requests_per_batch=10_000, batches=3, sampler=z))
+    for lc in (False, True):
+        be = Backend(0.8, lc, table_slots=1 << 17, max_batch=1 << 15, max_rules=8, debug_hash_bits=bits)
+        co = c_oracle.COracle(0.8, lc)
+        for a, n, nq, nr in batches:
+            g = be.do_limit_arrays(a, n, nq, nr)
+            o = co.do_limit(a, n, nq, nr)
+            for k in ("code", "limit_remaining", "reset_s", "stats"):
+                assert np.array_equal(g[k], o[k]), k
+        be.close()
+        co.close()
 
 
 def test_gpu_colliding_sort_keys_c2_vs_c_oracle():
