@@ -5,7 +5,7 @@
 #   2. the default bench (C1) under rocprofv3 --kernel-trace --stats: the bench
 #      line (k_table's live HIP-event time) and the trace of the same command,
 #      compared over the timed launches (scripts/trace_timed.py);
-#   3. C2 and C3 bench lines;
+#   3. C2 and C3 bench lines, the routed path at N = 1;
 #   4. PMC FETCH_SIZE / WRITE_SIZE passes for C1 (scripts/gpu_pmc.sh).
 # Outputs under gpurun_out/ev_*.
 set -o pipefail
@@ -26,5 +26,8 @@ for cfg in c2 c3; do
     || { tail -20 gpurun_out/ev_bench_$cfg.log; exit 1; }
   tail -1 gpurun_out/ev_bench_$cfg.log | cut -c1-300
 done
+timeout -k 10 300 python -u bench.py --route --no-cpu-baseline --pcie-steps 0 > gpurun_out/ev_bench_route.log 2>&1 \
+  || { tail -20 gpurun_out/ev_bench_route.log; exit 1; }
+tail -1 gpurun_out/ev_bench_route.log | cut -c1-300
 CFG=c1 bash scripts/gpu_pmc.sh > gpurun_out/ev_pmc.log 2>&1 || { tail -20 gpurun_out/ev_pmc.log; exit 1; }
 tail -14 gpurun_out/ev_pmc.log
