@@ -46,7 +46,11 @@ namespace rl {
 
 namespace {
 
-constexpr uint32_t RSLOTS = 3;  // batches a router keeps in flight (slot reuse waits for the batch RSLOTS back)
+// batches a router keeps in flight: a slot's partition waits for the batch
+// RSLOTS back to complete (its buffers are reused). With 3, the partition of
+// batch t waited for batch t-3's owner pipeline and return, and the host then
+// waited ~140 us per step for those counts (RL_DEBUG_ROUTE_TIMING).
+constexpr uint32_t RSLOTS = 6;
 
 struct Rccl {
   bool ok = false;

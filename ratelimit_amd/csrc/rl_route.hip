@@ -190,7 +190,8 @@ __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, 
   __shared__ uint32_t gr[RL_MAX_SHARDS], gb[RL_MAX_SHARDS];        // tile's first record / chunk byte per owner
   __shared__ uint32_t sb[RL_MAX_SHARDS], lo[RL_MAX_SHARDS], tb[RL_MAX_SHARDS];
   __shared__ uint32_t tmp[8];
-  __shared__ uint8_t stage[RP_STAGE];
+  __shared__ uint32_t stage32[RP_STAGE / 4];
+  uint8_t* stage = reinterpret_cast<uint8_t*>(stage32);
   if (*err) return;
   const uint32_t tile = blockIdx.x, w = threadIdx.x >> 6, lane = lane_id();
   for (uint32_t d = threadIdx.x; d < n_shards; d += 256) {
@@ -269,12 +270,14 @@ __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, 
         ab += xb;
       }
       tb[d] = ab;
-      byt = ab;
+      byt = ab ? ab + 3u : 0u;  // (room to align the segment, below)
     }
     uint32_t dummy = 0, t1, t2;
     block_excl2<4>(byt, dummy, t1, t2, tmp);
-    if (d < n_shards) lo[d] = byt;
-    if (d == 0) tmp[0] = t1;  // the tile's stem bytes
+    // owner d's LDS segment starts at the same offset mod 4 as its bytes in
+    // the send buffer (sb + gb), so the segment leaves as aligned dwords
+    if (d < n_shards) lo[d] = byt + ((sb[d] + gb[d] - byt) & 3u);
+    if (d == 0) tmp[0] = t1;  // the tile's stem bytes (+ alignment room)
   }
   __syncthreads();
   const bool staged = tmp[0] <= RP_STAGE;
@@ -306,13 +309,21 @@ __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, 
     continue;
 #endif
     if (staged) {
-      uint8_t* dst = stage + lo[d] + wb[w][d] + my_b[t];
-      for (uint32_t k = 0; k < len; k += 4) {
-        const uint32_t a = s0 + k, wi = a >> 2, sh = (a & 3u) * 8;
-        uint32_t v = words[wi];
-        if (sh) v = (v >> sh) | ((wi + 1 < nw ? words[wi + 1] : 0u) << (32 - sh));
-        const uint32_t m = len - k < 4 ? len - k : 4u;
-        for (uint32_t z = 0; z < m; z++) dst[k + z] = (uint8_t)(v >> (8 * z));
+      // whole LDS dwords of the destination from funnel-shifted source dwords;
+      // single bytes only at the two ends (shared with the neighbours' stems)
+      const uint32_t D = lo[d] + wb[w][d] + my_b[t];
+      auto src4 = [&](uint32_t a) {  // stem bytes a..a+3 of the packed batch
+        const uint32_t wi = a >> 2, sh = (a & 3u) * 8;
+        const uint32_t v = words[wi];
+        return sh ? (v >> sh) | ((wi + 1 < nw ? words[wi + 1] : 0u) << (32 - sh)) : v;
+      };
+      const uint32_t A0 = (D + 3u) & ~3u, A1 = (D + len) & ~3u;
+      if (A0 >= A1) {
+        for (uint32_t k = 0; k < len; k++) stage[D + k] = b.stem[s0 + k];
+      } else {
+        for (uint32_t a = D; a < A0; a++) stage[a] = b.stem[s0 + (a - D)];
+        for (uint32_t a = A0; a < A1; a += 4) reinterpret_cast<uint32_t*>(stage)[a >> 2] = src4(s0 + (a - D));
+        for (uint32_t a = A1; a < D + len; a++) stage[a] = b.stem[s0 + (a - D)];
       }
     } else {
       uint8_t* dst = out_stem + sb[d] + local;
@@ -331,9 +342,7 @@ __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, 
     for (uint32_t k = threadIdx.x; k < nd; k += 256) {
       const uint32_t A = A0 + 4 * k;
       if (A >= G && A + 4 <= G + T) {
-        const uint8_t* p = stage + L + (A - G);
-        *reinterpret_cast<uint32_t*>(out_stem + A) =
-            (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+        *reinterpret_cast<uint32_t*>(out_stem + A) = reinterpret_cast<const uint32_t*>(stage)[(L + (A - G)) >> 2];
       } else {
         for (uint32_t z = 0; z < 4; z++) {
           const uint32_t a = A + z;
