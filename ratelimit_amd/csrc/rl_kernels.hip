@@ -2423,11 +2423,22 @@ __device__ __attribute__((always_inline)) inline void unique_body(uint32_t blk, 
   LaneStats L;
   L.reset();
   // not a duplicated key (the sorted path's), not failed (answered already)
-  const uint32_t cnt = block_compact(lo, hi, s_list, &s_cnt,
-                                     [&](uint32_t i) { return !((rec[i].lu >> 24) & (FLAG_SKIP | FLAG_DUP)); });
-  if (threadIdx.x < cnt) {
-    const uint32_t j = threadIdx.x;
-    const uint32_t i = s_list[j];
+  auto single = [&](uint32_t i) { return !((rec[i].lu >> 24) & (FLAG_SKIP | FLAG_DUP)); };
+  const uint32_t i0 = lo + threadIdx.x;
+  const bool own = i0 < hi && single(i0);
+  // A dense block (the bulk at C1/C3) answers in place, lane by lane; a sparse
+  // one (hot-key batches) compacts its keys seen once onto the first lanes.
+  bool act;
+  uint32_t i;
+  if (__syncthreads_count(own) >= 192) {
+    act = own;
+    i = i0;
+  } else {
+    const uint32_t cnt = block_compact(lo, hi, s_list, &s_cnt, single);
+    act = threadIdx.x < cnt;
+    i = act ? s_list[threadIdx.x] : 0u;
+  }
+  if (act) {
     const uint32_t key = keys0[i];
     const Rec x = rec[i];
     {
