@@ -286,7 +286,7 @@ __host__ __device__ inline bool res_lc_hit(unsigned long long v) { return (v >> 
 // leaves it alone.
 constexpr uint32_t FLAG_SKIP = 0x80;
 // bit 6 = the descriptor's sort key occurs more than once in the batch
-// (k_run_check): the sorted path answers it, not k_unique.
+// (k_run_check): the sorted path answers it, not the keys-seen-once part.
 constexpr uint32_t FLAG_DUP = 0x40;
 
 constexpr uint32_t NOW_MAX = 0xFFFFFFFFu - 2u * 86400u;  // now + 2*div must fit u32

@@ -139,13 +139,13 @@ struct Scratch {
   uint32_t* grp;                  // k_runs_general: stem group of each position of a deferred run
   uint32_t* lead;                 //   first position of each group (stored from the run's start)
   uint8_t* gmask;                 //   units seen per group
-  uint32_t* defer;                // RUN_MULTI runs (k_run_check), for k_runs_general beside k_runs
+  uint32_t* defer;                // RUN_MULTI runs (k_run_check), for k_runs_general beside k_table
   uint32_t* defer_n;
-  uint32_t* defer2;               // runs k_runs found to need the exact path, for k_runs_general after it
+  uint32_t* defer2;               // runs k_table found to need the exact path (k_late)
   uint32_t* defer2_n;
-  uint32_t* defer1;               // singletons k_unique found to need the exact path (arrival indices)
+  uint32_t* defer1;               // keys seen once k_table found to need the exact path (arrival indices)
   uint32_t* defer1_n;
-  uint32_t* fast_blk;             // bit per 256-descriptor block holding a RUN_FAST run (k_runs -> k_fast_emit)
+  uint32_t* fast_blk;             // bit per 256-descriptor block holding a RUN_FAST run (k_table -> k_late)
   unsigned long long* stripes;    // STAT_STRIPES x STAT_LDS_RULES x RL_NUM_STATS
   // run segmentation (sorted order)
   uint32_t* hits_s;                    // [n] raw hits, sorted order

@@ -4,18 +4,22 @@
 //   k_prepare     validate the packed batch; hash every stem (LDS-staged
 //                 bytes); pack each descriptor into a 32-B Rec (arrival order)
 //   k_part        stable partition of (hash[63:32], index, hits) by the top
-//                 byte, tile by tile (no look-back)
-//   k_bucket      one workgroup per top byte: gather the bucket, stable LDS
-//                 sort by the remaining 24 bits (hot keys of a large bucket
-//                 peeled off), run ids, run bounds and in-run prefix sums of
+//                 10 bits, tile by tile (no look-back; tiles leave via LDS)
+//   k_bucket      one workgroup per bucket: gather it, stable LDS sort by the
+//                 remaining 22 bits (hot keys of a large bucket: k_big_*,
+//                 k_bucket_big), run ids, run bounds and in-run prefix sums of
 //                 hits: each stem's descriptors together, in arrival order
-//   k_run_check   one stem and one unit per run (else k_runs_general)
+//   k_run_check   one stem and one unit per run (else RUN_MULTI); marks the
+//                 descriptors of runs (FLAG_DUP)
+//   k_split       RUN_MULTI runs of a few single-unit stems -> per-stem runs
 //   ---- stage B (the table; batch order) ----
-//   k_runs        one lane per run: probe/insert the (stem, unit) slot of the
-//                 HBM table (one 128-B line per probe); replay short runs in
-//                 registers, set up long uniform runs for k_fast_*
-//   k_runs_general multi-stem / multi-unit runs, exact (beside k_runs)
-//   k_fast_*      long uniform runs decided in parallel (scan + first-over)
+//   k_table       keys seen once (arrival order) and runs of two or more (one
+//                 lane per run): probe/insert the (stem, unit) slot of the HBM
+//                 table; replay short runs in registers, set up long uniform
+//                 runs for the parallel path
+//   k_runs_general the exact path (side stream): RUN_MULTI runs left
+//   k_late        k_table's exact-path deferrals + long runs decided in
+//                 parallel (k_fast_over first with the local cache on)
 //   k_finish      packed results -> code / limit_remaining / reset_s, and the
 //                 striped per-block stats -> rl_result.stats
 // plus k_sweep (epoch sweep = Redis EXPIRE), k_table_info, debug kernels.
@@ -963,7 +967,7 @@ struct BkShape {
   static constexpr uint32_t WAVES = W, ITEMS = IT, THREADS = 64 * W, CAP = 64 * W * IT, STRIP = 64 * IT;
 };
 using BkSmall = BkShape<4, 8>;   // k_bucket: 2048 elements in LDS
-using BkBig = BkShape<8, 16>;    // k_bucket_big: 8192 elements per chunk
+using BkBig = BkShape<8, 8>;     // k_bucket_big: 4096 elements per chunk (~62 KB of LDS: 2 workgroups per CU)
 
 #ifdef RL_BK_PROF  // bucketbench only: per-bucket phase stamps
 __device__ unsigned long long g_bk_prof[PART_DIGITS * 16];
@@ -1312,7 +1316,7 @@ __device__ inline void bucket_segment(BucketLds<B>& L, uint32_t d, uint32_t S, u
   auto key = [&](uint32_t p) -> uint32_t { return FROM_LDS ? L.k[p] : sk[base + p]; };
   auto hit = [&](uint32_t p) -> uint32_t { return FROM_LDS ? L.h[p] : sh[base + p]; };
   // runs of the bucket -> run id base; runs of two or more (counted at their
-  // second element) -> their place in the dup-run list k_runs works through
+  // second element) -> their place in the dup-run list k_table works through
   uint32_t nh = 0, nd = 0;
   for (uint32_t c0 = 0; c0 < S; c0 += B::CAP) {
     uint32_t a[IT], b[IT], c[IT];
@@ -2397,13 +2401,13 @@ __global__ __launch_bounds__(256) void k_split(BatchDev b, SRec rec_s, uint32_t*
   }
 }
 
-// ---- k_unique: descriptors whose sort key occurs once in the batch (no
+// ---- k_table, keys seen once (unique_body): sort key once in the batch (no
 // FLAG_DUP), one lane each in ARRIVAL order: the record, the sort key and
 // the stem are coalesced wave reads (consecutive descriptors sit side by side
 // in the packed batch), the result a coalesced store; only the slot's first
 // sector (and the changed window record) is a random access. Such a stem has
 // no other descriptor in the batch, so the lanes are independent and this
-// kernel commutes with the sorted path (k_runs). A stem that lives in the
+// part commutes with the sorted path (runs_body). A stem that lives in the
 // table under another unit too is left to k_runs_general (defer1).
 __device__ __attribute__((always_inline)) inline void unique_body(uint32_t blk, BatchDev b, TableDev t, Params P, const Rec* __restrict__ rec,
                                                 const uint32_t* __restrict__ keys0, unsigned long long* __restrict__ res,
@@ -2478,7 +2482,7 @@ __device__ __attribute__((always_inline)) inline void unique_body(uint32_t blk, 
   stats_block_end(use_lds, b.n_rules, stripes);
 }
 
-// ---- k_runs: one lane per run of one stem and one unit (k_run_check). Short
+// ---- k_table, runs (runs_body): one lane per run of one stem and one unit. Short
 // runs whose slot is not flagged multi-unit are replayed here in registers;
 // long uniform runs are set up for the parallel path (k_fast_*); a stem that
 // turns out to live in the table under another unit too is queued for the
@@ -2677,7 +2681,7 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
     s_fast = (fast_blk[blk >> 5] >> (blk & 31)) & 1u;
   }
   __syncthreads();
-  if (s_err || !s_fast) return;  // no RUN_FAST descriptor in this block (k_runs' bitmap)
+  if (s_err || !s_fast) return;  // no RUN_FAST descriptor in this block (k_table's bitmap)
   const bool use_lds = n_rules <= LDS_RULES;
   stats_block_begin(use_lds, n_rules);
   StatAcc acc{use_lds, stats};
@@ -2867,7 +2871,7 @@ __device__ __attribute__((always_inline)) inline void general_body(uint32_t blk,
       });
     }
   }
-  // singletons k_unique found under several units (arrival indices)
+  // keys seen once that k_table found under several units (arrival indices)
   for (uint32_t di = blk * 256 + threadIdx.x; di < s_n1; di += nblk * 256) {
     const uint32_t e = defer1[di];
     const Rec x = rec_s.rec[e];
@@ -2956,7 +2960,7 @@ __global__ __launch_bounds__(256, 8) void k_late(BatchDev b, TableDev t, Params 
 }
 
 // First kernel of the table stage: merge this batch's validation errors into
-// the sticky table-stage word, clear k_runs' deferral counter and this call's
+// the sticky table-stage word, clear k_table's deferral counters and this call's
 // output stats (n_rules x RL_NUM_STATS).
 __global__ __launch_bounds__(256) void k_b_begin(const uint32_t* __restrict__ erra, uint32_t* errb,
                                                  uint32_t* __restrict__ defer_n, uint32_t* __restrict__ defer1_n,
@@ -3133,7 +3137,7 @@ static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b -
 // Stage A (table-free): validate, hash, sort, segment, and mark the descriptors
 // whose sort key occurs more than once. Uses only this buffer's scratch and its
 // validation word s.err. Sorted keys go to keys[1] (keys[0] keeps the arrival
-// order for k_unique), the sort permutation to vals[0].
+// order for k_table's keys seen once), the sort permutation to vals[0].
 void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_t st, hipEvent_t* ev) {
   const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
   if (ev) (void)hipEventRecord(ev[0], st);
@@ -3171,7 +3175,7 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
 
 // Stage B (the table): runs strictly in batch order. Every kernel reads the
 // sticky table-stage word s.errb; k_b_begin folds this batch's validation
-// result into it first. k_unique (keys seen once) and the sorted path (k_runs
+// result into it first. The keys seen once and the sorted path (runs
 // and its exact / parallel companions) touch disjoint stems.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
                     int restore, hipStream_t st, hipStream_t side, hipEvent_t go, hipEvent_t side_done,
