@@ -12,7 +12,7 @@ namespace rl {
 constexpr uint32_t PART_ITEMS = 16, PART_TILE = 256 * PART_ITEMS;  // k_part: 256 threads x PART_ITEMS
 constexpr uint32_t PART_BITS = 10, PART_DIGITS = 1u << PART_BITS;   // buckets = top key bits
 constexpr uint32_t BIG_BLOCKS = 64;                                 // k_bucket_big workgroups
-constexpr uint32_t BIG_ITEM_BLOCKS = 512;                           // k_big_count / k_big_place workgroups
+constexpr uint32_t BIG_ITEM_BLOCKS = 256;                           // k_big_count / k_big_place workgroups
 constexpr uint32_t BIG_HEAVY = 4;                                   // hot keys peeled off a large bucket
 
 // A bucket too large for k_bucket's LDS, queued with its sampled hot keys.
