@@ -9,9 +9,11 @@ Before timing, every key is inserted ("warm-up inserts all 20M keys").
 N>1 (torch.distributed.run, one process per GPU): the table is hash-sharded
 over the GPUs (10M tenants x 2 keys per GPU; --config c3: 62.5M, i.e. 1B keys
 on 8), each rank draws its 1M-descriptor slice from the whole node's tenant
-space, and every batch is routed to the owning GPUs and back with RCCL
-all_to_all (ratelimit_amd/sharded.py); weak scaling, value = all ranks'
-decisions / max-over-ranks time. --route runs the routed path at N=1.
+space, and every batch is routed to the owning GPUs and back over RCCL by the
+library itself (rl_comm_init / rl_do_limit_routed_async, send/recv over xGMI;
+--route-impl python: the collectives from ratelimit_amd/sharded.py); weak
+scaling, value = all ranks' decisions / max-over-ranks time. --route runs the
+routed path at N=1.
 
 Besides the contract line, rank 0 reports:
   roofline      dominant kernel (k_table) achieved GB/s on the canonical
