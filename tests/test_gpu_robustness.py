@@ -132,15 +132,16 @@ def _drop(a, n, nq, keep):
     return out, idx.size, nq
 
 
+@pytest.mark.parametrize("bits", [0, 12])  # 12: ~1.5 stems per sort key (k_split beside failed descriptors)
 @pytest.mark.parametrize("lc", [False, True])
-def test_gpu_one_bad_descriptor_fails_alone(lc):
+def test_gpu_one_bad_descriptor_fails_alone(lc, bits):
     z = workloads.ZipfSampler(3_000, 1.1)
     (a, n, nq, nr), = workloads.c2_stream(n_tenants=3_000, requests_per_batch=4_000, batches=1, sampler=z)
     bad = {k: v.copy() for k, v in a.items()}
     bad["unit"][7] = 9                          # unknown unit
     bad["rule_id"][1001] = 99                   # rule id >= n_rules
     bad["now"][2500] = -5                       # clock out of range: both descriptors of request 2500
-    be = Backend(0.8, lc, **SMALL)
+    be = Backend(0.8, lc, debug_hash_bits=bits, **SMALL)
     with pytest.raises(RedisError, match="RL_E_(INVALID|TIME)"):  # without statuses the batch fails
         be.do_limit_arrays(bad, n, nq, nr)
     g = be.do_limit_arrays(bad, n, nq, nr, isolate=True)
