@@ -47,9 +47,10 @@ namespace rl {
 namespace {
 
 // batches a router keeps in flight: a slot's partition waits for the batch
-// RSLOTS back to complete (its buffers are reused). With 3, the partition of
-// batch t waited for batch t-3's owner pipeline and return, and the host then
-// waited ~140 us per step for those counts (RL_DEBUG_ROUTE_TIMING).
+// RSLOTS back to complete (its buffers are reused). 6 rather than 3 so that
+// this wait never binds (routed N=1 3.33-3.36 vs 3.22-3.30 G); the host's
+// remaining ~150 us wait per step for the counts is the partition waiting for
+// GPU capacity beside the owner pipelines (RL_DEBUG_ROUTE_TIMING).
 constexpr uint32_t RSLOTS = 6;
 
 struct Rccl {
