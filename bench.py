@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--no-fill", action="store_true")
     ap.add_argument("--pcie-steps", type=int, default=60, help="host-fed (PCIe) batches timed after the device phase")
     ap.add_argument("--slots-per-key", type=float, default=4.0, help="table slots per live key (power of 2 above)")
+    ap.add_argument("--hash-seed", type=int, default=0, help="stem hash key (0: drawn at random per run; reported)")
     ap.add_argument("--route", action="store_true", help="use the routed (all_to_all) path even at N=1")
     ap.add_argument("--route-impl", default="lib", choices=["lib", "python"],
                     help="routed step: inside the library over RCCL (lib) or collectives from Python")
@@ -119,8 +120,11 @@ def main():
     slots = 1 << max(16, int(np.ceil(np.log2(args.slots_per_key * keys_per_gpu))))
     # a routed owner receives ~n descriptors (binomial spread across sources)
     cap = n if not routed else int(n * 1.05) + 4096
-    seed = 0
-    if routed:  # every shard of one table hashes stems under one key: rank 0 draws it
+    seed = args.hash_seed
+    if not seed and not routed:  # a random key per run, as the library would draw; reported in the line
+        import secrets
+        seed = secrets.randbits(62) + 1
+    if routed and not seed:  # every shard of one table hashes stems under one key: rank 0 draws it
         import secrets
         t = torch.tensor([secrets.randbits(62) + 1 if rank == 0 else 0], dtype=torch.int64,
                          device="cpu" if args.dist_backend == "gloo" else "cuda")
@@ -315,7 +319,7 @@ def main():
                                "%d-descriptor batches per GPU, %s tenants, now +1 s per batch, all keys pre-inserted"
                                % (args.config.upper(), T / 1e6, 2 * T * world, n, dist_desc),
                    "global_batch": world * n, "batch_per_gpu": n, "live_stem_slots_per_gpu": info["live_slots"],
-                   "table_slots": slots,
+                   "table_slots": slots, "hash_seed": seed,
                    "parallelism": ("hash-sharded table x%d, %s" % (
                                       world, "RCCL send/recv routing inside the library" if not py_route else
                                       "all_to_all routing from Python (%s)" % args.dist_backend)) if routed else
