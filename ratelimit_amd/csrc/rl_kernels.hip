@@ -2229,10 +2229,211 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
 // k_table answers them like any other run (a sub-run of one element becomes a
 // key seen once) instead of the one-lane exact path, whose chain of dependent
 // table accesses outlasted k_table. Anything else (a stem under several
-// units, a 64-bit hash collision, a failed descriptor, more than SPLIT_CAP
-// elements, or no room left in the dup-run list) stays on the exact path.
+// units, a 64-bit hash collision, a failed descriptor, or no room left in the
+// dup-run list) stays on the exact path. Runs over SPLIT_CAP elements take
+// split_long_body (global-memory scratch instead of LDS).
 constexpr uint32_t SPLIT_CAP = 1024, SPLIT_MAXG = 8, SPLIT_BLOCKS = 128;
 constexpr uint32_t DEFER_DONE = 0xFFFFFFFFu;  // a deferral k_split resolved
+
+// ---- split_long (k_split's blocks, for RUN_MULTI runs over SPLIT_CAP
+// elements): the same reordering. Under an unlucky hash key a hot stem (tens
+// of thousands of descriptors per batch at C2) shares its sort key with
+// another stem, and the one-lane exact path replayed the whole run: 1.3 ms per
+// batch on average at C2 under seed 5 (profiles/r02/seed_sweep/). Split, the
+// hot stem is an ordinary long run for the parallel path. The per-element
+// state lives in global scratch owned by the run's range: grp (the sub-run)
+// and lead (the rank inside it) are the exact path's per-position scratch,
+// which it never reads for a run it does not see, and segsum holds the
+// permutation's source until the in-run sums overwrite it. (A kernel of its
+// own with 1024-lane blocks cost every batch 4-6 us of launch on the critical
+// path, 1-3 %, profiles/r02/ab/long_*.)
+constexpr uint32_t SPLIT_UNROLL = 8;
+
+template <uint32_t NT>
+__device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j, uint32_t r, uint32_t p, uint32_t L, BatchDev b,
+                                                          SRec rec_s, uint32_t* svals, uint32_t* segsum,
+                                                          uint32_t* __restrict__ rid, uint32_t* __restrict__ run_start,
+                                                          uint32_t* __restrict__ run_end,
+                                                          uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
+                                                          unsigned long long* num_runs, unsigned long long* split,
+                                                          uint32_t* __restrict__ drun, uint32_t drun_cap, uint32_t* grp,
+                                                          uint32_t* rank) {
+  constexpr uint32_t NW = NT / 64;
+  __shared__ uint32_t s_w[NW][SPLIT_MAXG], s_ws[NW];
+  __shared__ uint32_t s_cnt[SPLIT_MAXG], s_base[SPLIT_MAXG], s_id[SPLIT_MAXG], s_fl[SPLIT_MAXG], s_off[SPLIT_MAXG];
+  __shared__ uint32_t s_lnow[SPLIT_MAXG], s_lunit[SPLIT_MAXG];
+  __shared__ uint32_t s_bad, s_lead, s_carry;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  Rec* rec = const_cast<Rec*>(rec_s.rec);
+  {
+    __syncthreads();  // the previous run's shared state has been read
+    if (tid == 0) s_bad = 0;
+    __syncthreads();
+    for (uint32_t k = tid; k < L; k += NT) {
+      const uint32_t e = rec_s.sv[p + k];
+      segsum[p + k] = e;
+      grp[p + k] = 0xFFu;
+      if ((rec[e].lu >> 24) & FLAG_SKIP) s_bad = 1;
+    }
+    // sub-runs, as in k_split: the first unassigned element leads, and every
+    // element with its stem joins (records read SPLIT_UNROLL at a time: the
+    // scan is a chain of random reads)
+    uint32_t G = 0;
+    for (;;) {
+      if (tid == 0) s_lead = 0xFFFFFFFFu;
+      __syncthreads();
+      for (uint32_t k = tid; k < L; k += NT)
+        if (grp[p + k] == 0xFFu) {
+          atomicMin(&s_lead, k);  // this lane's first is its smallest
+          break;
+        }
+      __syncthreads();
+      const uint32_t ld = s_lead;
+      if (ld == 0xFFFFFFFFu || s_bad || G == SPLIT_MAXG) break;  // (uniform)
+      const Rec y = rec[segsum[p + ld]];
+      const Key ky = key_of(b, y);
+      if (tid == 0) {
+        s_lnow[G] = y.now;
+        s_lunit[G] = rec_unit(y);
+      }
+      for (uint32_t k0 = tid; k0 < L; k0 += NT * SPLIT_UNROLL) {
+        Rec x[SPLIT_UNROLL];
+        bool act[SPLIT_UNROLL];
+#pragma unroll
+        for (uint32_t u = 0; u < SPLIT_UNROLL; u++) {
+          const uint32_t k = k0 + u * NT;
+          act[u] = k < L && grp[p + k] == 0xFFu;
+          if (act[u]) x[u] = rec[segsum[p + k]];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < SPLIT_UNROLL; u++) {
+          if (!act[u] || x[u].hlo != y.hlo || (x[u].lu & 0xFFFFu) != (y.lu & 0xFFFFu)) continue;
+          if (!key_equal(key_of(b, x[u]), ky)) {
+            s_bad = 1;  // equal 64-bit hash, different stem
+          } else {
+            if (rec_unit(x[u]) != rec_unit(y)) s_bad = 1;  // one stem, several units
+            grp[p + k0 + u * NT] = G;
+          }
+        }
+      }
+      G++;
+      __syncthreads();
+    }
+    if (tid == 0 && s_lead != 0xFFFFFFFFu) s_bad = 1;  // more than SPLIT_MAXG stems
+    __syncthreads();
+    if (s_bad || G < 2) return;  // (uniform) the exact path keeps it
+    // stable ranks inside the sub-runs: per NT-element chunk, wave ballots,
+    // then the waves before this one and the chunks before this one
+    if (tid < SPLIT_MAXG) s_cnt[tid] = 0;
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < L; c0 += NT) {
+      const uint32_t k = c0 + tid;
+      const uint32_t gk = k < L ? grp[p + k] : 0xFFu;
+      uint32_t mine = 0;
+#pragma unroll
+      for (uint32_t g = 0; g < SPLIT_MAXG; g++) {
+        const uint64_t m = __ballot(gk == g);
+        if (gk == g) mine = __popcll(m & lt);
+        if (lane == 0) s_w[wv][g] = __popcll(m);
+      }
+      __syncthreads();
+      if (gk < SPLIT_MAXG) {
+        uint32_t pre = s_cnt[gk];
+        for (uint32_t w = 0; w < wv; w++) pre += s_w[w][gk];
+        rank[p + k] = pre + mine;
+      }
+      __syncthreads();
+      if (tid < SPLIT_MAXG) {
+        uint32_t a = 0;
+        for (uint32_t w = 0; w < NW; w++) a += s_w[w][tid];
+        s_cnt[tid] += a;
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {  // run ids and room, exactly as k_split
+      uint32_t acc = 0, nd2 = 0;
+      for (uint32_t g = 0; g < SPLIT_MAXG; g++) {
+        s_base[g] = acc;
+        s_fl[g] = 0;
+        acc += s_cnt[g];
+        if (g >= 1 && g < G && s_cnt[g] >= 2) nd2++;
+      }
+      const unsigned long long add = ((unsigned long long)nd2 << 32) | (unsigned long long)(G - 1);
+      const unsigned long long rs = atomicAdd(&split[0], add), base = split[1];
+      const bool room = (uint32_t)(base >> 32) + (uint32_t)(rs >> 32) + nd2 <= drun_cap &&
+                        (uint32_t)base + (uint32_t)rs + (G - 1) <= b.n;
+      if (!room) {
+        s_bad = 1;
+      } else {
+        const unsigned long long old = atomicAdd(num_runs, add);
+        s_id[0] = r;
+        uint32_t di = (uint32_t)(old >> 32);
+        for (uint32_t g = 1; g < G; g++) {
+          s_id[g] = (uint32_t)old + g - 1;
+          if (s_cnt[g] >= 2) drun[di++] = s_id[g];
+        }
+      }
+    }
+    __syncthreads();
+    if (s_bad) return;  // (uniform) no room in the dup-run list: the exact path keeps it
+    for (uint32_t k = tid; k < L; k += NT) {
+      const uint32_t g = grp[p + k], np = s_base[g] + rank[p + k], e = segsum[p + k];
+      svals[p + np] = e;
+      rid[p + np] = s_id[g];
+      const Rec x = rec[e];
+      const uint32_t d = div_of(s_lunit[g]);
+      if (x.now / d != s_lnow[g] / d) atomicOr(&s_fl[g], RUN_SLOW);
+      // a sub-run of one element is a key seen once (k_table's singleton part)
+      if (s_cnt[g] == 1) rec[e].lu = x.lu & ~(FLAG_DUP << 24);
+    }
+    if (tid == 0) s_carry = 0;
+    __syncthreads();
+    // in-run sums of max(1, hits) in the new order: one inclusive scan over the
+    // whole run (mod 2^32, like the bucket kernels' sums), then each sub-run
+    // subtracts the total before its start
+    for (uint32_t c0 = 0; c0 < L; c0 += NT) {
+      const uint32_t k = c0 + tid;
+      uint32_t v = 0;
+      if (k < L) {
+        const uint32_t h = rec[svals[p + k]].hits;
+        v = h > 1 ? h : 1u;
+      }
+#pragma unroll
+      for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(v, off, 64);
+        if (lane >= off) v += y;
+      }
+      if (lane == 63) s_ws[wv] = v;
+      __syncthreads();
+      uint32_t pre = s_carry;
+      for (uint32_t w = 0; w < wv; w++) pre += s_ws[w];
+      if (k < L) segsum[p + k] = v + pre;
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t a = 0;
+        for (uint32_t w = 0; w < NW; w++) a += s_ws[w];
+        s_carry += a;
+      }
+      __syncthreads();
+    }
+    if (tid < SPLIT_MAXG) s_off[tid] = (tid < G && s_base[tid]) ? segsum[p + s_base[tid] - 1] : 0u;
+    __syncthreads();
+    for (uint32_t k = tid; k < L; k += NT) {
+      uint32_t g = 0;
+      while (g + 1 < G && k >= s_base[g + 1]) g++;
+      if (s_off[g]) segsum[p + k] -= s_off[g];
+    }
+    if (tid < G) {
+      const uint32_t id = s_id[tid];
+      run_start[id] = p + s_base[tid];
+      run_end[id] = p + s_base[tid] + s_cnt[tid];
+      run_flags[id] = s_fl[tid];
+    }
+    if (tid == 0) defer[j] = DEFER_DONE;
+  }
+}
+
 
 __global__ __launch_bounds__(256) void k_split(BatchDev b, SRec rec_s, uint32_t* __restrict__ svals,
                                                uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
@@ -2240,7 +2441,8 @@ __global__ __launch_bounds__(256) void k_split(BatchDev b, SRec rec_s, uint32_t*
                                                uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
                                                const uint32_t* defer_n, unsigned long long* num_runs,
                                                unsigned long long* split, uint32_t* __restrict__ drun,
-                                               uint32_t drun_cap, const uint32_t* err) {
+                                               uint32_t drun_cap, uint32_t* grp, uint32_t* rank,
+                                               const uint32_t* err) {
   __shared__ uint32_t s_e[SPLIT_CAP], s_hlo[SPLIT_CAP], s_lu[SPLIT_CAP], s_now[SPLIT_CAP], s_h[SPLIT_CAP];
   __shared__ uint32_t s_nh[SPLIT_CAP];           // max(1, hits) in the new order
   __shared__ uint16_t s_pos[SPLIT_CAP];          // rank inside the element's sub-run
@@ -2256,7 +2458,11 @@ __global__ __launch_bounds__(256) void k_split(BatchDev b, SRec rec_s, uint32_t*
   for (uint32_t j = blockIdx.x; j < nd; j += gridDim.x) {
     const uint32_t r = defer[j];
     const uint32_t p = run_start[r], L = run_end[r] - p;
-    if (L > SPLIT_CAP) continue;  // (uniform)
+    if (L > SPLIT_CAP) {  // (uniform)
+      split_long_body<256>(j, r, p, L, b, rec_s, svals, segsum, rid, run_start, run_end, run_flags, defer, num_runs,
+                           split, drun, drun_cap, grp, rank);
+      continue;
+    }
     __syncthreads();  // the previous run's shared state has been read
     if (tid == 0) s_bad = 0;
     for (uint32_t k = tid; k < L; k += 256) {
@@ -3169,7 +3375,7 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
                                                 s.run_flags, s.defer, s.defer_n, s.err, s.runs64, s.split);
     k_split<<<SPLIT_BLOCKS, 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.vals[0], s.segsum, s.rid, s.run_start,
                                           s.run_end, s.run_flags, s.defer, s.defer_n, s.runs64, s.split, s.drun,
-                                          b.n / 2 + BIG_HEAVY * PART_DIGITS, s.err);
+                                          b.n / 2 + BIG_HEAVY * PART_DIGITS, s.grp, s.lead, s.err);
   }
 }
 

@@ -60,8 +60,8 @@ def test_gpu_colliding_sort_keys_vs_python_oracle(bits, lc):
 @pytest.mark.parametrize("bits", [13, 15])
 def test_gpu_split_colliding_runs_c2_vs_c_oracle(bits):
     """A few distinct stems per sort key (40k stems over 2^13 / 2^15 keys):
-    k_split reorders such runs into per-stem sub-runs (hot keys included, up to
-    its 1024-element cap; longer runs and the rest stay exact)."""
+    k_split reorders such runs into per-stem sub-runs (hot keys included; runs
+    of more than 8 stems stay exact)."""
     z = workloads.ZipfSampler(20_000, 1.1)
     batches = list(workloads.c2_stream(n_tenants=20_000, requests_per_batch=10_000, batches=3, sampler=z))
     for lc in (False, True):
@@ -74,6 +74,53 @@ def test_gpu_split_colliding_runs_c2_vs_c_oracle(bits):
                 assert np.array_equal(g[k], o[k]), k
         be.close()
         co.close()
+
+
+@pytest.mark.parametrize("tenants", [1, 2, 4, 5])
+def test_gpu_split_long_colliding_run_vs_c_oracle(tenants):
+    """Every descriptor under one sort key (debug_hash_bits=0): one run of
+    ~2 x 6000 elements from 2 x `tenants` stems (a stem per tenant and unit).
+    Up to 8 stems k_split (split_long_body) reorders it into per-stem long runs for the
+    parallel path (the hot-stem collision that made C2 collapse under some
+    hash keys); 10 stems stay on the exact path. Hits vary (1..8) and the
+    clock moves by a second between batches."""
+    z = workloads.ZipfSampler(tenants, 1.1)
+    batches = list(workloads.c2_stream(seed=tenants, n_tenants=tenants, requests_per_batch=6_000, batches=3,
+                                       sampler=z))
+    for lc in (False, True):
+        be = Backend(0.8, lc, table_slots=1 << 16, max_batch=1 << 14, max_rules=8, debug_hash_bits=0)
+        co = c_oracle.COracle(0.8, lc)
+        for a, n, nq, nr in batches:
+            g = be.do_limit_arrays(a, n, nq, nr)
+            o = co.do_limit(a, n, nq, nr)
+            for k in ("code", "limit_remaining", "reset_s", "stats"):
+                assert np.array_equal(g[k], o[k]), k
+        be.close()
+        co.close()
+
+
+@pytest.mark.parametrize("lc", [False, True])
+def test_gpu_split_long_run_singletons_and_window_change(lc):
+    """One sort key again: a hot tenant (3000 requests), one request of a
+    second tenant (one-element sub-runs: keys seen once) and one of a third
+    that falls between the hot tenant's requests; the clock moves by a second
+    every 700 requests inside the batch (window changes inside the long
+    sub-runs: RUN_SLOW)."""
+    t = np.zeros(3002, np.int64)
+    t[1500] = 1
+    t[3001] = 2
+    now = workloads.NOW0 + np.arange(t.size) // 700
+    h = (np.arange(t.size) % 5 + 1).astype(np.uint32)
+    batches = [workloads.c1_batch(t, now, h), workloads.c1_batch(t[::-1].copy(), now + 10, h)]
+    be = Backend(0.8, lc, table_slots=1 << 16, max_batch=1 << 14, max_rules=8, debug_hash_bits=0)
+    co = c_oracle.COracle(0.8, lc)
+    for a, n, nq, nr in batches:
+        g = be.do_limit_arrays(a, n, nq, nr)
+        o = co.do_limit(a, n, nq, nr)
+        for k in ("code", "limit_remaining", "reset_s", "stats"):
+            assert np.array_equal(g[k], o[k]), k
+    be.close()
+    co.close()
 
 
 def test_gpu_colliding_sort_keys_c2_vs_c_oracle():
