@@ -76,19 +76,22 @@ def test_gpu_split_colliding_runs_c2_vs_c_oracle(bits):
         co.close()
 
 
-@pytest.mark.parametrize("tenants", [1, 2, 4, 5])
+@pytest.mark.parametrize("tenants", [2, 3, 4, 12])
 def test_gpu_split_long_colliding_run_vs_c_oracle(tenants):
-    """Every descriptor under one sort key (debug_hash_bits=0): one run of
-    ~2 x 6000 elements from 2 x `tenants` stems (a stem per tenant and unit).
-    Up to 8 stems k_split (split_long_body) reorders it into per-stem long runs for the
+    """Two sort keys for the whole batch (debug_hash_bits=1): 2 x `tenants`
+    stems (a stem per tenant and unit) in two runs of thousands of elements,
+    at least one holding two or more stems. Up to 8 stems k_split
+    (split_long_body) reorders such a run into per-stem long runs for the
     parallel path (the hot-stem collision that made C2 collapse under some
-    hash keys); 10 stems stay on the exact path. Hits vary (1..8) and the
-    clock moves by a second between batches."""
+    hash keys); with 12 tenants at least one run holds 12 or more stems and
+    stays on the exact path. Hits vary (1..8) and the clock moves by a second
+    between batches. Fixed hash keys keep the layout reproducible."""
     z = workloads.ZipfSampler(tenants, 1.1)
     batches = list(workloads.c2_stream(seed=tenants, n_tenants=tenants, requests_per_batch=6_000, batches=3,
                                        sampler=z))
-    for lc in (False, True):
-        be = Backend(0.8, lc, table_slots=1 << 16, max_batch=1 << 14, max_rules=8, debug_hash_bits=0)
+    for lc, seed in ((False, 11), (True, 12)):
+        be = Backend(0.8, lc, table_slots=1 << 16, max_batch=1 << 14, max_rules=8, debug_hash_bits=1,
+                     hash_seed=seed)
         co = c_oracle.COracle(0.8, lc)
         for a, n, nq, nr in batches:
             g = be.do_limit_arrays(a, n, nq, nr)
@@ -101,9 +104,9 @@ def test_gpu_split_long_colliding_run_vs_c_oracle(tenants):
 
 @pytest.mark.parametrize("lc", [False, True])
 def test_gpu_split_long_run_singletons_and_window_change(lc):
-    """One sort key again: a hot tenant (3000 requests), one request of a
-    second tenant (one-element sub-runs: keys seen once) and one of a third
-    that falls between the hot tenant's requests; the clock moves by a second
+    """Two sort keys again (6 stems: at least one run of two or more stems):
+    a hot tenant (3000 requests), one request of a second tenant (one-element
+    sub-runs: keys seen once) and one of a third; the clock moves by a second
     every 700 requests inside the batch (window changes inside the long
     sub-runs: RUN_SLOW)."""
     t = np.zeros(3002, np.int64)
@@ -112,15 +115,17 @@ def test_gpu_split_long_run_singletons_and_window_change(lc):
     now = workloads.NOW0 + np.arange(t.size) // 700
     h = (np.arange(t.size) % 5 + 1).astype(np.uint32)
     batches = [workloads.c1_batch(t, now, h), workloads.c1_batch(t[::-1].copy(), now + 10, h)]
-    be = Backend(0.8, lc, table_slots=1 << 16, max_batch=1 << 14, max_rules=8, debug_hash_bits=0)
-    co = c_oracle.COracle(0.8, lc)
-    for a, n, nq, nr in batches:
-        g = be.do_limit_arrays(a, n, nq, nr)
-        o = co.do_limit(a, n, nq, nr)
-        for k in ("code", "limit_remaining", "reset_s", "stats"):
-            assert np.array_equal(g[k], o[k]), k
-    be.close()
-    co.close()
+    for seed in (21, 22, 23):
+        be = Backend(0.8, lc, table_slots=1 << 16, max_batch=1 << 14, max_rules=8, debug_hash_bits=1,
+                     hash_seed=seed)
+        co = c_oracle.COracle(0.8, lc)
+        for a, n, nq, nr in batches:
+            g = be.do_limit_arrays(a, n, nq, nr)
+            o = co.do_limit(a, n, nq, nr)
+            for k in ("code", "limit_remaining", "reset_s", "stats"):
+                assert np.array_equal(g[k], o[k]), k
+        be.close()
+        co.close()
 
 
 def test_gpu_colliding_sort_keys_c2_vs_c_oracle():
