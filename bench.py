@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--one-device", action="store_true", help="every rank uses cuda:0 (rehearsal only)")
     ap.add_argument("--serial", action="store_true",
                     help="submit every batch on one stream, unpipelined (isolated per-kernel times for profiling)")
+    ap.add_argument("--loopback", type=int, default=0,
+                    help="W > 0: W ranks of the library router as threads of this process, all on cuda:0, "
+                         "exchanging through the in-process loopback transport (the W-rank protocol on one GPU)")
     args = ap.parse_args()
     if not args.tenants:
         args.tenants = 62_500_000 if args.config == "c3" else 10_000_000
@@ -78,6 +81,8 @@ def to_dev(a, torch):
 
 def main():
     args = parse()
+    if args.loopback:
+        return loopback_main(args)
     import torch
     import torch.distributed as dist
 
@@ -332,6 +337,101 @@ def main():
     be.close()
     if routed:
         dist.destroy_process_group()
+
+
+def loopback_main(args):
+    """--loopback W: the routed step of an W-GPU node (rl_comm.hip: partition,
+    counts, records and stems, owner pipelines, results and stats, scatter)
+    with every rank a thread of this process on cuda:0 and the exchanges
+    through the loopback transport. Each rank owns `tenants` tenants x {sec,
+    min} (all pre-inserted) and submits --requests requests per step drawn
+    from the whole world's tenant space. value = W x descriptors per step /
+    max-over-ranks time: one GPU does every rank's work, so this measures the
+    protocol's cost on the GPU, not scaling."""
+    import secrets
+    import threading
+
+    import torch
+
+    from ratelimit_amd import workloads as W
+    from ratelimit_amd.limiter import Backend
+    from ratelimit_amd.sharded import LibRouter, loopback_id
+    R = args.loopback
+    nq, n, T = args.requests, 2 * args.requests, args.tenants
+    slots = 1 << max(16, int(np.ceil(np.log2(args.slots_per_key * 2 * T))))
+    cap = int(n * 1.05) + 4096
+    seed = args.hash_seed or secrets.randbits(62) + 1
+    torch.cuda.set_device(0)
+    uid = loopback_id()
+    bes = [Backend(0.8, False, table_slots=slots, max_batch=cap, max_rules=max(8, 2 * R), device=0, hash_seed=seed,
+                   max_stem_bytes=64 * cap) for _ in range(R)]
+    routers = [LibRouter(be, R, r, uid) for r, be in enumerate(bes)]
+    gate = threading.Barrier(R)
+    times, fills, errs = [0.0] * R, [0.0] * R, [None] * R
+
+    def body(r):
+        try:
+            torch.cuda.set_device(0)
+            torch.cuda.set_stream(torch.cuda.Stream())
+            out = {"code": torch.empty(n, dtype=torch.uint8, device="cuda"),
+                   "limit_remaining": torch.empty(n, dtype=torch.int32, device="cuda"),
+                   "reset_s": torch.empty(n, dtype=torch.int32, device="cuda"),
+                   "stats": torch.zeros(2 * 6, dtype=torch.int64, device="cuda")}
+            rt = routers[r]
+            t = time.perf_counter()
+            if not args.no_fill:
+                for s0 in range(0, T, nq):
+                    ids = torch.arange(s0, min(s0 + nq, T), dtype=torch.int64, device="cuda") + r * T
+                    a, bn, bq, _ = W.c1_batch_dev(ids, W.NOW0 - 1)
+                    rt.submit(a, bn, bq, 2, out)
+                rt.finish()
+            fills[r] = time.perf_counter() - t
+            rng = np.random.default_rng(0xC1 + 7919 * r)
+            batches = []
+            for _ in range(args.distinct_batches):
+                a, _, _, _ = W.c1_batch(rng.integers(0, R * T, nq), W.NOW0)
+                a.pop("now")
+                batches.append(to_dev(a, torch))
+            total = args.warmup + args.steps
+            nows = [torch.full((nq,), W.NOW0 + s, dtype=torch.int64, device="cuda") for s in range(total)]
+            for s in range(args.warmup):
+                rt.submit(dict(batches[s % len(batches)], now=nows[s]), n, nq, 2, out)
+            rt.finish()
+            torch.cuda.synchronize()
+            gate.wait()
+            t = time.perf_counter()
+            for s in range(args.warmup, total):
+                rt.submit(dict(batches[s % len(batches)], now=nows[s]), n, nq, 2, out)
+            rt.finish()
+            torch.cuda.synchronize()
+            times[r] = time.perf_counter() - t
+        except Exception as e:  # (a failed rank's peers time out in the loopback transport)
+            errs[r] = repr(e)
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(R)]
+    for th in ts:
+        th.start()
+    for th in ts:
+        th.join()
+    if any(errs):
+        raise SystemExit("loopback bench failed: %s" % errs)
+    info = [be.table_info() for be in bes]
+    for be in bes:
+        be.close()
+    elapsed = max(times)
+    line = {
+        "metric": METRIC, "value": R * n * args.steps / elapsed, "unit": "decisions/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "C1 routed: %d loopback ranks on one GPU, %.1fM tenants x {sec,min} per rank, "
+                               "%d-descriptor slices per rank per step, uniform over all ranks' tenants"
+                               % (R, T / 1e6, n),
+                   "global_batch": R * n, "batch_per_rank": n, "table_slots_per_rank": slots, "hash_seed": seed,
+                   "live_stem_slots": sum(i["live_slots"] for i in info),
+                   "parallelism": "hash-sharded table x%d, library router over the loopback transport" % R},
+        "fill_s": round(max(fills), 2),
+    }
+    print(json.dumps(line), flush=True)
 
 
 def pcie_fed(args, be, host_batches, now):

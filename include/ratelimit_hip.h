@@ -273,15 +273,22 @@ int rl_route_do_limit(rl_ctx* ctx, uint32_t n, const void* recv_rec, const uint8
 int rl_route_scatter(rl_ctx* ctx, uint32_t n, const uint32_t* perm, const uint64_t* ret, rl_result* out,
                      void* stream);
 
-/* ---- Multi-process routing over RCCL, inside the library ------------------
+/* ---- Multi-rank routing inside the library (RCCL or in-process loopback) ---
  * SURVEY.md §8e with the exchange itself in the library (rl_comm.hip): one
- * process per GPU, each with one single-shard ctx, every ctx created with the
- * same rl_config.hash_seed.
+ * rank per table shard, each with one single-shard ctx, every ctx created with
+ * the same rl_config.hash_seed.
  *
  * rl_comm_unique_id (one rank) fills RL_COMM_ID_BYTES bytes (an ncclUniqueId)
- * that the caller hands to every rank (e.g. a torch.distributed broadcast);
+ * that the caller hands to every rank (e.g. a torch.distributed broadcast):
+ * one process per GPU, exchanges over RCCL (xGMI). RCCL is loaded then
+ * (dlopen), not at library load.
+ * rl_comm_loopback_id fills the id of an in-process world instead: its ranks
+ * are threads of THIS process, one ctx each (any devices; several may share
+ * one GPU, which RCCL refuses), exchanging by device copies with the same
+ * protocol. A rank whose peers never arrive fails with RL_E_COMM after
+ * RL_LOOPBACK_TIMEOUT_S seconds (default 120) instead of waiting forever.
  * rl_comm_init (collective: every rank, the same id) joins ctx to the world as
- * `rank`. RCCL is loaded at this point (dlopen), not at library load.
+ * `rank`.
  *
  * rl_do_limit_routed_async (collective: every rank calls it the same number of
  * times in the same order; n may be 0) answers this rank's slice of the node
@@ -293,14 +300,25 @@ int rl_route_scatter(rl_ctx* ctx, uint32_t n, const uint32_t* perm, const uint64
  * inputs may be reused once the next call has returned, its outputs are read
  * after rl_synchronize (collective too on such a ctx: it completes the last
  * batch). Keep `out` valid until then. out->stats = the deltas of
- * THIS rank's requests (summed
- * over ranks: the node's). Needs max_rules >= world x n_rules (an owner keeps
- * stats per source). A descriptor whose owner batch failed gets that
- * rl_status in out->status; without out->status it fails this rank's batch at
- * rl_synchronize. Replaces the Redis cluster client's key-slot routing inside
- * one service process (src/redis/driver_impl.go:108-126). */
+ * THIS rank's requests (summed over ranks: the node's). Ranks may pass
+ * different n_rules; every owner keeps stats per source with the largest
+ * n_rules of the batch as stride, so it needs max_rules >= world x that. If
+ * any rank passes out->status, owners answer per descriptor (isolation) for
+ * the whole batch.
+ * Errors never leave a peer waiting: a slice this rank rejects (sizes, null
+ * outputs) takes part in the exchange with no records and fails this rank's
+ * batch at rl_synchronize; an owner that cannot run what it received answers
+ * every such record with its rl_status (in out->status, or failing the
+ * source's batch at rl_synchronize). Only a HIP / transport runtime failure
+ * leaves the ctx's router unusable (RL_E_COMM / RL_E_HIP from every later
+ * call). Replaces the Redis cluster client's key-slot routing inside one
+ * service process (src/redis/driver_impl.go:108-126).
+ * On a routed ctx rl_synchronize, rl_sweep, rl_restore, rl_table_info_get,
+ * rl_local_cache_info_get and rl_snapshot_save / _load first complete the
+ * pending batch, so they are collective like the batches. */
 #define RL_COMM_ID_BYTES 128u
 int rl_comm_unique_id(uint8_t* id);
+int rl_comm_loopback_id(uint8_t* id);
 int rl_comm_init(rl_ctx* ctx, uint32_t world, uint32_t rank, const uint8_t* id);
 int rl_do_limit_routed_async(rl_ctx* ctx, const rl_batch* in, rl_result* out, void* stream);
 

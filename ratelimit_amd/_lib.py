@@ -18,7 +18,7 @@ EXPORTS = ["rl_abi_version", "rl_create", "rl_destroy", "rl_last_error", "rl_do_
            "rl_route_do_limit", "rl_route_scatter", "rl_config_load", "rl_do_limit_requests",
            "rl_local_cache_info_get", "rl_snapshot_size", "rl_snapshot_save", "rl_snapshot_load",
            "rl_packer_create", "rl_packer_destroy", "rl_packer_pack", "rl_packer_rules", "rl_packer_rule_key",
-           "rl_packer_last_error", "rl_comm_unique_id", "rl_comm_init", "rl_do_limit_routed_async",
+           "rl_packer_last_error", "rl_comm_unique_id", "rl_comm_loopback_id", "rl_comm_init", "rl_do_limit_routed_async",
            "rl_do_limit_host_async"]
 
 _lib = None
@@ -71,6 +71,7 @@ def lib():
     L.rl_route_scatter.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(abi.RlResult),
                                    C.c_void_p]
     L.rl_comm_unique_id.argtypes = [C.c_void_p]
+    L.rl_comm_loopback_id.argtypes = [C.c_void_p]
     L.rl_comm_init.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
     L.rl_do_limit_routed_async.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.POINTER(abi.RlResult), C.c_void_p]
     L.rl_config_load.argtypes = [C.c_void_p, C.POINTER(abi.RlConfigTree)]

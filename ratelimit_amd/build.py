@@ -10,9 +10,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libratelimit_hip.so")
-SOURCES = ["rl_kernels.hip", "rl_route.hip", "rl_match.hip", "rl_engine.hip", "rl_comm.hip", "rl_api.hip",
+SOURCES = ["rl_kernels.hip", "rl_route.hip", "rl_match.hip", "rl_engine.hip", "rl_transport.hip", "rl_comm.hip",
+           "rl_api.hip",
            "rl_pack.cpp"]
-HEADERS = ["rl_device.h", "rl_kernels.h", "rl_match.h", "rl_engine.h", "rl_comm.h",
+HEADERS = ["rl_device.h", "rl_kernels.h", "rl_match.h", "rl_engine.h", "rl_comm.h", "rl_transport.h",
            os.path.join("..", "..", "include", "ratelimit_hip.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RL_OFFLOAD_ARCH", "gfx950")

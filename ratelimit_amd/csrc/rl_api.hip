@@ -252,9 +252,17 @@ int routed_async(rl_ctx* c, const rl_batch* in, rl_result* out, hipStream_t call
 }
 
 int synchronize_all(rl_ctx* c) {
-  if (c->comm) {
-    const int rc = comm_synchronize(c->comm, c->e[0]);
-    if (rc) return rc;
+  int comm_rc = RL_OK;
+  std::string comm_msg;
+  if (c->comm) {  // (collective on a routed ctx: it completes the pending batch)
+    comm_rc = comm_synchronize(c->comm, c->e[0]);
+    if (comm_rc) comm_msg = eng_last_error(c->e[0]);
+  }
+  if (comm_rc) {
+    // the engine's own words are collected (and cleared) too; the router's
+    // failure is the one reported
+    (void)eng_synchronize(c->e[0]);
+    return eng_fail(c->e[0], comm_rc, comm_msg);
   }
   if (c->n > 1) {
     API_HIP(c, hipSetDevice(c->dev0));
@@ -277,6 +285,11 @@ int synchronize_all(rl_ctx* c) {
 }
 
 constexpr uint64_t MSNAP_MAGIC = 0x31304853414e534cull;  // "LSNASH01": one image per shard
+
+// Calls that read or change the table order after every submitted batch: on a
+// multi-shard or routed ctx the batches still in the router first complete
+// (on a routed ctx this makes the call collective, like rl_synchronize).
+int settle(rl_ctx* c) { return (c->comm || c->n > 1) ? synchronize_all(c) : RL_OK; }
 
 }  // namespace
 
@@ -427,6 +440,14 @@ int rl_comm_unique_id(uint8_t* id) {
   return RL_OK;
 }
 
+int rl_comm_loopback_id(uint8_t* id) {
+  if (!id) return fail(nullptr, RL_E_INVALID, "gpu: null argument");
+  std::string err;
+  const int rc = comm_loopback_id(id, &err);
+  if (rc) return fail(nullptr, rc, err);
+  return RL_OK;
+}
+
 int rl_comm_init(rl_ctx* c, uint32_t world, uint32_t rank, const uint8_t* id) {
   if (!c || !id) return fail(c, RL_E_INVALID, "gpu: null argument");
   if (c->n > 1) return fail(c, RL_E_INVALID, "gpu: rl_comm_init needs a single-shard ctx (one per process and GPU)");
@@ -452,14 +473,12 @@ int rl_synchronize(rl_ctx* c) {
 
 int rl_sweep(rl_ctx* c, int64_t now, uint64_t* n_evicted) {
   if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
-  if (c->n > 1) {
-    int rc = synchronize_all(c);
-    if (rc) return rc;
-  }
+  int rc = settle(c);
+  if (rc) return rc;
   uint64_t total = 0;
   for (uint32_t j = 0; j < c->n; j++) {
     uint64_t ev = 0;
-    const int rc = from_engine(c, c->e[j], eng_sweep(c->e[j], now, &ev));
+    rc = from_engine(c, c->e[j], eng_sweep(c->e[j], now, &ev));
     if (rc) return rc;
     total += ev;
   }
@@ -469,6 +488,7 @@ int rl_sweep(rl_ctx* c, int64_t now, uint64_t* n_evicted) {
 
 int rl_restore(rl_ctx* c, const rl_restore_batch* r) {
   if (!c || !r) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (const int src = settle(c)) return src;
   if (c->n == 1) return eng_restore(c->e[0], r);
   // route the SET records by owner on the host (restores are rare)
   const uint32_t N = c->n;
@@ -507,6 +527,7 @@ int rl_restore(rl_ctx* c, const rl_restore_batch* r) {
 
 int rl_table_info_get(rl_ctx* c, rl_table_info* info) {
   if (!c || !info) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (const int src = settle(c)) return src;
   rl_table_info sum{};
   for (uint32_t j = 0; j < c->n; j++) {
     rl_table_info x{};
@@ -526,6 +547,7 @@ int rl_table_info_get(rl_ctx* c, rl_table_info* info) {
 
 int rl_local_cache_info_get(rl_ctx* c, int64_t now, rl_local_cache_info* info) {
   if (!c || !info) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (const int src = settle(c)) return src;
   rl_local_cache_info sum{};
   for (uint32_t j = 0; j < c->n; j++) {
     rl_local_cache_info x{};
@@ -556,6 +578,7 @@ int rl_snapshot_size(rl_ctx* c, uint64_t* bytes) {
 
 int rl_snapshot_save(rl_ctx* c, void* host, uint64_t bytes) {
   if (!c || !host) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (const int src = settle(c)) return src;
   if (c->n == 1) return eng_snapshot_save(c->e[0], host, bytes);
   uint64_t* h = (uint64_t*)host;
   const uint64_t head = 8 * (2 + c->n);
@@ -578,6 +601,7 @@ int rl_snapshot_save(rl_ctx* c, void* host, uint64_t bytes) {
 
 int rl_snapshot_load(rl_ctx* c, const void* host, uint64_t bytes) {
   if (!c || !host) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (const int src = settle(c)) return src;
   if (c->n == 1) return eng_snapshot_load(c->e[0], host, bytes);
   const uint64_t* h = (const uint64_t*)host;
   if (bytes < 16 || h[0] != MSNAP_MAGIC || h[1] != c->n || bytes < 8 * (2 + c->n))

@@ -1,46 +1,55 @@
-// rl_comm.hip — the multi-process routed DoLimit step over RCCL, driven
-// entirely by the library.
+// rl_comm.hip — the multi-rank routed DoLimit step, driven entirely by the
+// library.
 //
-// One process per GPU, one single-shard engine per process; every rank calls
-// comm_do_limit once per node batch with its own slice. Per batch:
+// One single-shard engine per rank; every rank calls comm_do_limit once per
+// node batch with its own slice. The exchanges go through a Transport
+// (rl_transport.h): RCCL between processes (one per GPU, the 8-GPU node), or
+// the in-process loopback (several ranks as host threads, e.g. on one GPU).
+// Per batch:
 //
 //   cnt stream:  rl_route_pack partition of the slice by owner (stem hash);
-//                counts exchange (2 u64 per peer, grouped send/recv);
+//                counts exchange (channel 0): per peer {records, stem bytes,
+//                n_rules, flags};
 //   host:        read the counts (the one wait per batch, one call later);
-//   fwd stream:  records + stem bytes exchange (one grouped send/recv over
-//                xGMI: each peer pair uses its own link);
+//   fwd stream:  records + stem bytes to their owners (channel 1; each peer
+//                pair uses its own xGMI link);
 //   engine:      the owner pipeline over the received chunks, concatenated in
 //                source-rank order (= global arrival order), in parts of at
-//                most max_batch records; stats attributed per source rank;
-//   ret stream:  packed results (a failed owner batch returns its status for
-//                every record) and each source's stats block go back (grouped
-//                send/recv); scatter to arrival order, sum the stats blocks.
+//                most max_batch records; stats attributed per source rank
+//                (rule stride = the largest n_rules any rank sent);
+//   ret stream:  packed results (a failed owner batch answers its status for
+//                every record) and each source's stats block go back (channel
+//                2); scatter to arrival order, sum the stats blocks.
 //
 // A call enqueues its batch's partition and counts exchange and then
 // completes the PREVIOUS batch (whose counts have had a whole call to arrive):
 // the host never waits for work it just issued, batch t's partition runs
 // beside batch t-1's owner pipeline, and rl_synchronize completes the last
-// one. Three communicators, one per direction of traffic (counts, records,
-// results), each on its own stream, so that no exchange waits in RCCL's
-// per-communicator order behind another kind. RSLOTS batches may be in
-// flight. RCCL is loaded with dlopen, preferring an instance already in the
-// process (torch's, which shares the HIP runtime this library binds to), so
-// the library loads and runs single-GPU without RCCL present.
-#include <dlfcn.h>
+// one. RSLOTS batches may be in flight.
+//
+// Failures never break the exchange. A slice the host rejects (sizes, null
+// outputs, a bad n_rules) sends zero counts with the FAILED flag and still
+// takes part in every group; its rank's batch fails at rl_synchronize. An
+// owner that cannot run what it received (stats stride or stems beyond its
+// capacity) answers every received record with the failure status, which
+// each source reports per descriptor (rl_result.status) or at rl_synchronize.
+// Only a runtime failure of HIP or the transport itself leaves the router
+// broken (every later call fails; RCCL peers may then wait forever, loopback
+// peers time out).
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "rl_comm.h"
 #include "rl_kernels.h"
+#include "rl_transport.h"
 
 namespace rl {
 
@@ -53,47 +62,10 @@ namespace {
 // GPU capacity beside the owner pipelines (RL_DEBUG_ROUTE_TIMING).
 constexpr uint32_t RSLOTS = 6;
 
-struct Rccl {
-  bool ok = false;
-  std::string err;
-  decltype(&ncclGetUniqueId) get_id = nullptr;
-  decltype(&ncclCommInitRank) init = nullptr;
-  decltype(&ncclCommSplit) split = nullptr;
-  decltype(&ncclCommDestroy) destroy = nullptr;
-  decltype(&ncclGroupStart) gstart = nullptr;
-  decltype(&ncclGroupEnd) gend = nullptr;
-  decltype(&ncclSend) send = nullptr;
-  decltype(&ncclRecv) recv = nullptr;
-  decltype(&ncclGetErrorString) estr = nullptr;
-};
-
-Rccl& rccl() {
-  static Rccl r;
-  static std::once_flag once;
-  std::call_once(once, [] {
-    void* h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);  // torch's copy, if loaded
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!h) {
-      const char* e = dlerror();
-      r.err = std::string("gpu: RCCL not loadable: ") + (e ? e : "?");
-      return;
-    }
-    r.get_id = (decltype(r.get_id))dlsym(h, "ncclGetUniqueId");
-    r.init = (decltype(r.init))dlsym(h, "ncclCommInitRank");
-    r.split = (decltype(r.split))dlsym(h, "ncclCommSplit");
-    r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
-    r.gstart = (decltype(r.gstart))dlsym(h, "ncclGroupStart");
-    r.gend = (decltype(r.gend))dlsym(h, "ncclGroupEnd");
-    r.send = (decltype(r.send))dlsym(h, "ncclSend");
-    r.recv = (decltype(r.recv))dlsym(h, "ncclRecv");
-    r.estr = (decltype(r.estr))dlsym(h, "ncclGetErrorString");
-    r.ok = r.get_id && r.init && r.split && r.destroy && r.gstart && r.gend && r.send && r.recv && r.estr;
-    if (!r.ok) r.err = "gpu: RCCL library lacks a required symbol";
-  });
-  return r;
-}
+// The counts message: CNT_W u64 per peer.
+constexpr uint32_t CNT_W = 4;                 // records, stem bytes, n_rules, flags
+constexpr uint64_t CNT_ISOLATE = 1;           // the sender wants per-descriptor statuses
+constexpr uint64_t CNT_FAILED = 2;            // the sender's slice failed on its host (nothing sent)
 
 template <typename T>
 hipError_t dalloc(T** p, size_t count) {
@@ -106,7 +78,7 @@ struct CommSlot {
   Wire* send_rec = nullptr;                // partition of this rank's slice, owner order
   uint8_t* send_stem = nullptr;
   uint32_t* perm = nullptr;                // record -> slice index
-  unsigned long long* cnt = nullptr;       // [4 x world]: sent (records, bytes) per peer, then received
+  unsigned long long* cnt = nullptr;       // [2 x CNT_W x world]: sent per peer, then received
   Wire* recv_rec = nullptr;                // chunks of every source, rank order
   uint8_t* recv_stem = nullptr;
   unsigned long long* ret_send = nullptr;  // packed results of the received records
@@ -121,10 +93,12 @@ struct CommSlot {
   // the batch between its two halves
   rl_result out{};
   uint32_t n = 0, n_rules = 0;
+  int err = RL_OK;                         // the slice failed on the host: it sent nothing
+  std::string errmsg;
 };
 
 struct CommRouter {
-  ncclComm_t comm_c = nullptr, comm_f = nullptr, comm_r = nullptr;  // counts, records, results
+  std::unique_ptr<Transport> tr;
   uint32_t world = 1, rank = 0;
   int dev = 0;
   uint32_t m_max = 0;
@@ -135,9 +109,16 @@ struct CommRouter {
   CommSlot slot[RSLOTS];
   uint32_t next = 0;
   int pending = -1;                     // slot whose second half is still to run
-  unsigned long long* h_cnt = nullptr;  // pinned [RSLOTS][4 x world]
+  unsigned long long* h_cnt = nullptr;  // pinned [RSLOTS][2 x CNT_W x world]
   std::vector<uint64_t> base;           // received chunk offsets in recv_stem (host)
   std::vector<uint64_t> so_r, so_b, ro_r;  // per-peer send / receive offsets (host)
+  std::vector<Xfer> ops;
+  // the first batch failure since the last synchronize (reported there)
+  int sticky = RL_OK;
+  std::string sticky_msg;
+  // a HIP / transport runtime failure: the router is unusable
+  int broken = RL_OK;
+  std::string broken_msg;
   // host seconds per phase (printed at destroy when RL_DEBUG_ROUTE_TIMING is set)
   bool timing = false;
   double t_first = 0, t_wait_counts = 0, t_owner = 0, t_second = 0;
@@ -150,17 +131,27 @@ inline double now_s() {
 
 namespace {
 
-#define CHK_HIP(e, expr)                                                                         \
-  do {                                                                                           \
-    hipError_t _h = (expr);                                                                      \
-    if (_h != hipSuccess) return eng_fail((e), RL_E_HIP, std::string("gpu: ") + #expr + ": " + hipGetErrorString(_h)); \
+// A runtime failure: the router stops here.
+int breaks(CommRouter* r, Engine* e, int code, const std::string& msg) {
+  if (!r->broken) {
+    r->broken = code;
+    r->broken_msg = msg;
+  }
+  return eng_fail(e, code, msg);
+}
+
+#define CHK_HIP(e, expr)                                                                                  \
+  do {                                                                                                    \
+    hipError_t _h = (expr);                                                                               \
+    if (_h != hipSuccess) return breaks(r, (e), RL_E_HIP, std::string("gpu: ") + #expr + ": " + hipGetErrorString(_h)); \
   } while (0)
 
-#define CHK_NCCL(e, expr)                                                                        \
-  do {                                                                                           \
-    ncclResult_t _r = (expr);                                                                    \
-    if (_r != ncclSuccess) return eng_fail((e), RL_E_COMM, std::string("gpu: ") + #expr + ": " + rccl().estr(_r)); \
-  } while (0)
+int run_group(CommRouter* r, Engine* e, uint32_t ch, hipStream_t st) {
+  std::string err;
+  const int rc = r->tr->group(ch, r->ops, st, &err);
+  if (rc) return breaks(r, e, rc, err);
+  return RL_OK;
+}
 
 void free_slot(CommSlot& S) {
   void* bufs[] = {S.send_rec, S.send_stem, S.perm, S.cnt, S.recv_rec, S.recv_stem, S.ret_send, S.back, S.ostats,
@@ -208,30 +199,39 @@ hipError_t grow(CommRouter* r, CommSlot& S, uint64_t n_rec, uint64_t n_stem, uin
 }
 
 // First half of a batch (slot s): partition, counts exchange, counts to the
-// host. (The next call's second half waits on the host for this partition:
-// from then on the inputs may be reused.)
-int first_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, const rl_batch* in, hipStream_t caller) {
-  Rccl& R = rccl();
+// host. `hostrc` != RL_OK: the slice was rejected before the partition; it
+// sends zero counts. (The next call's second half waits on the host for this
+// partition: from then on the inputs may be reused.)
+int first_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, const rl_batch* in, hipStream_t caller,
+               int hostrc) {
   const uint32_t W = r->world, me = r->rank;
   CHK_HIP(e, hipStreamWaitEvent(r->cs, S.done, 0));  // the slot's previous batch is complete
   if (caller && hipStreamQuery(caller) == hipErrorNotReady) {  // the inputs' producer (still running)
     CHK_HIP(e, hipEventRecord(r->in_ready, caller));
     CHK_HIP(e, hipStreamWaitEvent(r->cs, r->in_ready, 0));
   }
-  // a malformed slice sends nothing (zero counts) and fails this rank's batch
-  // at rl_synchronize
-  const int rc = eng_route_pack(e, in, W, me, S.send_rec, S.send_stem, S.perm, (uint64_t*)S.cnt, r->cs);
-  if (rc) return rc;
+  const uint64_t flags = S.out.status ? CNT_ISOLATE : 0;
+  int rc = hostrc;
+  if (!rc)
+    rc = eng_route_pack(e, in, W, me, S.send_rec, S.send_stem, S.perm, (uint64_t*)S.cnt, r->cs, CNT_W, S.n_rules,
+                        flags);
+  if (rc) {  // (a device-side malformation zeroes the counts itself and fails at rl_synchronize)
+    S.err = rc;
+    S.errmsg = eng_last_error(e);
+    launch_cnt_fill(S.cnt, W, CNT_W, 0, flags | CNT_FAILED, r->cs);
+  }
   if (!r->alias) {
-    CHK_NCCL(e, R.gstart());
+    r->ops.clear();
     for (uint32_t p = 0; p < W; p++) {
       if (p == me) continue;
-      CHK_NCCL(e, R.send(S.cnt + 2 * p, 2, ncclUint64, (int)p, r->comm_c, r->cs));
-      CHK_NCCL(e, R.recv(S.cnt + 2 * W + 2 * p, 2, ncclUint64, (int)p, r->comm_c, r->cs));
+      r->ops.push_back({S.cnt + (size_t)CNT_W * p, CNT_W * 8ull, p, true});
+      r->ops.push_back({S.cnt + (size_t)CNT_W * (W + p), CNT_W * 8ull, p, false});
     }
-    CHK_NCCL(e, R.gend());
+    const int g = run_group(r, e, 0, r->cs);
+    if (g) return g;
   }
-  CHK_HIP(e, hipMemcpyAsync(r->h_cnt + (size_t)s * 4 * W, S.cnt, 4ull * W * 8, hipMemcpyDeviceToHost, r->cs));
+  CHK_HIP(e, hipMemcpyAsync(r->h_cnt + (size_t)s * 2 * CNT_W * W, S.cnt, 2ull * CNT_W * W * 8, hipMemcpyDeviceToHost,
+                            r->cs));
   CHK_HIP(e, hipEventRecord(S.packed, r->cs));
   return RL_OK;
 }
@@ -239,34 +239,48 @@ int first_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, const rl_batch
 // Second half (slot s): records and stems to their owners, the owner
 // pipeline, results and per-source stats back, scatter.
 int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
-  Rccl& R = rccl();
-  const uint32_t W = r->world, me = r->rank, n = S.n, nr = S.n_rules;
-  const uint32_t m = nr * RL_NUM_STATS;
-  unsigned long long* h = r->h_cnt + (size_t)s * 4 * W;
+  const uint32_t W = r->world, me = r->rank, n = S.n;
+  unsigned long long* h = r->h_cnt + (size_t)s * 2 * CNT_W * W;
+  unsigned long long* hr = h + (size_t)CNT_W * W;  // received
   const double t0 = now_s();
   CHK_HIP(e, hipEventSynchronize(S.packed));  // (issued one call ago)
   const double t1 = now_s();
   r->t_wait_counts += t1 - t0;
-  h[2 * W + 2 * me] = h[2 * me];  // (own chunk)
-  h[2 * W + 2 * me + 1] = h[2 * me + 1];
-  uint64_t n_send = 0, n_recv = 0, b_recv = 0;
+  for (uint32_t k = 0; k < CNT_W; k++) hr[CNT_W * me + k] = h[CNT_W * me + k];  // (own chunk)
+  uint64_t n_send = 0, n_recv = 0, b_recv = 0, M = 0, iso = 0;
   for (uint32_t p = 0; p < W; p++) {
-    n_send += h[2 * p];
+    n_send += h[CNT_W * p];
     r->base[p] = b_recv;
-    n_recv += h[2 * W + 2 * p];
-    b_recv += h[2 * W + 2 * p + 1];
+    n_recv += hr[CNT_W * p];
+    b_recv += hr[CNT_W * p + 1];
+    M = std::max<uint64_t>(M, hr[CNT_W * p + 2]);
+    iso |= hr[CNT_W * p + 3] & CNT_ISOLATE;
   }
-  if (n_send != n && n_send != 0) return eng_fail(e, RL_E_INTERNAL, "gpu: routing counts do not add up");
+  if (!S.err && n_send != n && n_send != 0) {  // (0: the device rejected the slice, below)
+    S.err = eng_fail(e, RL_E_INTERNAL, "gpu: routing counts do not add up");
+    S.errmsg = eng_last_error(e);
+  }
+  // what this rank cannot run as an owner fails every record it received
+  int owner_fail = RL_OK;
+  if (b_recv >= (1ull << 32)) {
+    owner_fail = RL_E_CAPACITY;
+  } else if ((uint64_t)W * M > e->cfg.max_rules) {
+    owner_fail = RL_E_CAPACITY;  // (per-source stats: an owner needs world x n_rules rule slots)
+  }
+  if (owner_fail && !r->sticky) {
+    r->sticky = owner_fail;
+    r->sticky_msg = "gpu: routed owner capacity exceeded (4 GiB of stems, or max_rules < world x n_rules)";
+  }
+  const uint32_t m = (uint32_t)M * RL_NUM_STATS;  // one source's stats block
   const uint32_t mb = r->part_max;
-  if (b_recv >= (1ull << 32)) return eng_fail(e, RL_E_CAPACITY, "gpu: more than 4 GiB of stems routed to one owner");
   // per-peer offsets: so_* into the send buffers, ro_* into the receive ones
   r->so_r.assign(W + 1, 0);
   r->so_b.assign(W + 1, 0);
   r->ro_r.assign(W + 1, 0);
   for (uint32_t p = 0; p < W; p++) {
-    r->so_r[p + 1] = r->so_r[p] + h[2 * p];
-    r->so_b[p + 1] = r->so_b[p] + h[2 * p + 1];
-    r->ro_r[p + 1] = r->ro_r[p] + h[2 * W + 2 * p];
+    r->so_r[p + 1] = r->so_r[p] + h[CNT_W * p];
+    r->so_b[p + 1] = r->so_b[p] + h[CNT_W * p + 1];
+    r->ro_r[p + 1] = r->ro_r[p] + hr[CNT_W * p];
   }
   CHK_HIP(e, hipStreamWaitEvent(r->fwd, S.packed, 0));
   if (!r->alias) CHK_HIP(e, grow(r, S, n_recv, b_recv, 1));
@@ -275,21 +289,22 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
   const uint8_t* recv_stem = r->alias ? S.send_stem : S.recv_stem;
   if (!r->alias) {
     // records and stems to their owners; this rank's own chunk by device copy
-    CHK_NCCL(e, R.gstart());
+    r->ops.clear();
     for (uint32_t p = 0; p < W; p++) {
-      const uint64_t sn = h[2 * p], sb = h[2 * p + 1], rn = h[2 * W + 2 * p], rb = h[2 * W + 2 * p + 1];
       if (p == me) continue;
-      if (sn) CHK_NCCL(e, R.send(S.send_rec + r->so_r[p], sn * sizeof(Wire), ncclUint8, (int)p, r->comm_f, r->fwd));
-      if (sb) CHK_NCCL(e, R.send(S.send_stem + r->so_b[p], sb, ncclUint8, (int)p, r->comm_f, r->fwd));
-      if (rn) CHK_NCCL(e, R.recv(S.recv_rec + r->ro_r[p], rn * sizeof(Wire), ncclUint8, (int)p, r->comm_f, r->fwd));
-      if (rb) CHK_NCCL(e, R.recv(S.recv_stem + r->base[p], rb, ncclUint8, (int)p, r->comm_f, r->fwd));
+      const uint64_t sn = h[CNT_W * p], sb = h[CNT_W * p + 1], rn = hr[CNT_W * p], rb = hr[CNT_W * p + 1];
+      r->ops.push_back({S.send_rec + r->so_r[p], sn * sizeof(Wire), p, true});
+      r->ops.push_back({S.send_stem + r->so_b[p], sb, p, true});
+      r->ops.push_back({S.recv_rec + r->ro_r[p], rn * sizeof(Wire), p, false});
+      r->ops.push_back({S.recv_stem + r->base[p], rb, p, false});
     }
-    CHK_NCCL(e, R.gend());
-    if (h[2 * me])
-      CHK_HIP(e, hipMemcpyAsync(S.recv_rec + r->ro_r[me], S.send_rec + r->so_r[me], h[2 * me] * sizeof(Wire),
+    const int g = run_group(r, e, 1, r->fwd);
+    if (g) return g;
+    if (h[CNT_W * me])
+      CHK_HIP(e, hipMemcpyAsync(S.recv_rec + r->ro_r[me], S.send_rec + r->so_r[me], h[CNT_W * me] * sizeof(Wire),
                                 hipMemcpyDeviceToDevice, r->fwd));
-    if (h[2 * me + 1])
-      CHK_HIP(e, hipMemcpyAsync(S.recv_stem + r->base[me], S.send_stem + r->so_b[me], h[2 * me + 1],
+    if (h[CNT_W * me + 1])
+      CHK_HIP(e, hipMemcpyAsync(S.recv_stem + r->base[me], S.send_stem + r->so_b[me], h[CNT_W * me + 1],
                                 hipMemcpyDeviceToDevice, r->fwd));
   }
   CHK_HIP(e, hipEventRecord(S.sent, r->fwd));
@@ -300,7 +315,7 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
   // the received labels.
   std::vector<uint64_t>& cut = S.cut;
   cut.assign(1, 0);
-  if (n_recv > mb) {
+  if (n_recv > mb && !owner_fail) {
     std::vector<uint32_t> lab(n_recv);
     CHK_HIP(e, hipStreamSynchronize(r->fwd));
     CHK_HIP(e, hipMemcpy2D(lab.data(), 4, recv_rec, sizeof(Wire), 4, n_recv, hipMemcpyDeviceToHost));
@@ -317,61 +332,75 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
   if (parts > S.cap_parts) CHK_HIP(e, grow(r, S, 0, 0, parts));
   unsigned long long* ret_send = r->alias ? S.back : S.ret_send;  // (world 1: results land in place)
   // world 1, one part: the scatter reads the owner batch's results directly
-  const bool direct = r->alias && parts == 1;
-  const int isolate = S.out.status ? 1 : 0;
+  const bool direct = r->alias && parts == 1 && !owner_fail;
   S.k.assign(parts, 0);
   const size_t blk = (size_t)W * m;  // one part's per-source stats
   const double t2 = now_s();
-  for (uint32_t q = 0; q < parts; q++) {
-    const uint64_t a = cut[q], b = cut[q + 1];
-    const int rc = eng_route_owner(e, (uint32_t)(b - a), recv_rec + a, recv_stem, b_recv, r->base.data(), W, nr,
-                                   nr, S.ostats + q * blk, isolate, S.sent, &S.k[q]);
-    if (rc) return rc;
-    // its packed results, before a later part can take the same engine buffer
-    const uint32_t k = S.k[q];
-    CHK_HIP(e, hipSetDevice(r->dev));
-    CHK_HIP(e, hipStreamWaitEvent(r->ret, e->b_done[k], 0));
-    if (direct) break;
-    launch_route_ret(e->s[k].res, (uint32_t)(b - a), e->s[k].errb, ret_send + a, r->ret);
-    CHK_HIP(e, hipEventRecord(e->consumed[k], r->ret));
+  if (owner_fail) {
+    CHK_HIP(e, hipStreamWaitEvent(r->ret, S.sent, 0));
+    launch_route_fail(ret_send, (uint32_t)n_recv, (uint32_t)owner_fail, r->ret);
+    if (blk) CHK_HIP(e, hipMemsetAsync(S.ostats, 0, blk * 8, r->ret));
+  } else {
+    for (uint32_t q = 0; q < parts; q++) {
+      const uint64_t a = cut[q], b = cut[q + 1];
+      const int rc = eng_route_owner(e, (uint32_t)(b - a), recv_rec + a, recv_stem, b_recv, r->base.data(), W,
+                                     (uint32_t)M, (uint32_t)M, S.ostats + q * blk, iso ? 1 : 0, S.sent, &S.k[q]);
+      if (rc) return breaks(r, e, rc, eng_last_error(e));  // (argument checks only: the sizes were checked above)
+      // its packed results, before a later part can take the same engine buffer
+      const uint32_t k = S.k[q];
+      CHK_HIP(e, hipSetDevice(r->dev));
+      CHK_HIP(e, hipStreamWaitEvent(r->ret, e->b_done[k], 0));
+      if (direct) break;
+      launch_route_ret(e->s[k].res, (uint32_t)(b - a), e->s[k].errb, ret_send + a, r->ret);
+      CHK_HIP(e, hipEventRecord(e->consumed[k], r->ret));
+    }
   }
   const double t3 = now_s();
   r->t_owner += t3 - t2;
   // results and per-source stats back to their sources
-  if (parts > 1 && m) launch_stats_sum(S.ostats, parts, (uint32_t)blk, S.ostats, r->ret);
+  if (parts > 1 && m && !owner_fail) launch_stats_sum(S.ostats, parts, (uint32_t)blk, S.ostats, r->ret);
   const unsigned long long* stats_in = S.ostats;  // (world 1: this rank's block is the owner's)
   if (!r->alias) {
-    CHK_NCCL(e, R.gstart());
+    r->ops.clear();
     for (uint32_t p = 0; p < W; p++) {
-      const uint64_t sn = h[2 * p], rn = h[2 * W + 2 * p];
       if (p == me) continue;
-      if (rn) CHK_NCCL(e, R.send(S.ret_send + r->ro_r[p], rn, ncclUint64, (int)p, r->comm_r, r->ret));
-      if (sn) CHK_NCCL(e, R.recv(S.back + r->so_r[p], sn, ncclUint64, (int)p, r->comm_r, r->ret));
-      if (m) {
-        CHK_NCCL(e, R.send(S.ostats + (size_t)p * m, m, ncclUint64, (int)p, r->comm_r, r->ret));
-        CHK_NCCL(e, R.recv(S.stats_stage + (size_t)p * m, m, ncclUint64, (int)p, r->comm_r, r->ret));
-      }
+      const uint64_t sn = h[CNT_W * p], rn = hr[CNT_W * p];
+      r->ops.push_back({S.ret_send + r->ro_r[p], rn * 8, p, true});
+      r->ops.push_back({S.back + r->so_r[p], sn * 8, p, false});
+      r->ops.push_back({S.ostats + (size_t)p * m, (uint64_t)m * 8, p, true});
+      r->ops.push_back({S.stats_stage + (size_t)p * m, (uint64_t)m * 8, p, false});
     }
-    CHK_NCCL(e, R.gend());
-    if (h[2 * me])
-      CHK_HIP(e, hipMemcpyAsync(S.back + r->so_r[me], S.ret_send + r->ro_r[me], h[2 * me] * 8,
+    const int g = run_group(r, e, 2, r->ret);
+    if (g) return g;
+    if (h[CNT_W * me])
+      CHK_HIP(e, hipMemcpyAsync(S.back + r->so_r[me], S.ret_send + r->ro_r[me], h[CNT_W * me] * 8,
                                 hipMemcpyDeviceToDevice, r->ret));
     if (m)
       CHK_HIP(e, hipMemcpyAsync(S.stats_stage + (size_t)me * m, S.ostats + (size_t)me * m, (size_t)m * 8,
                                 hipMemcpyDeviceToDevice, r->ret));
     stats_in = S.stats_stage;
   }
-  const rl_result& out = S.out;
-  OutDev o{out.code, out.limit_remaining, out.reset_s, (unsigned long long*)out.stats, out.status};
-  uint32_t* src_err = isolate ? nullptr : e->errw + NBUF + 2;
-  if (direct) {
-    const uint32_t k = S.k[0];
-    launch_route_scatter(S.perm, e->s[k].res, n, o, r->ret, src_err, e->s[k].errb);
-    CHK_HIP(e, hipEventRecord(e->consumed[k], r->ret));
-  } else {
-    launch_route_scatter(S.perm, S.back, n, o, r->ret, src_err);
+  if (!S.err && n && n_send != n) {
+    // the partition rejected the slice on the device (zero counts; its error
+    // word fails the batch at rl_synchronize): perm was never written, so
+    // nothing is scattered
+  } else if (!S.err) {
+    const rl_result& out = S.out;
+    const uint32_t mine = S.n_rules * RL_NUM_STATS;  // (<= m: M is the largest n_rules sent)
+    OutDev o{out.code, out.limit_remaining, out.reset_s, (unsigned long long*)out.stats, out.status};
+    uint32_t* src_err = out.status ? nullptr : e->errw + NBUF + 2;
+    if (direct) {
+      const uint32_t k = S.k[0];
+      launch_route_scatter(S.perm, e->s[k].res, n, o, r->ret, src_err, e->s[k].errb);
+      CHK_HIP(e, hipEventRecord(e->consumed[k], r->ret));
+    } else {
+      launch_route_scatter(S.perm, S.back, n, o, r->ret, src_err);
+    }
+    if (mine && out.stats) launch_stats_sum(stats_in, W, mine, (unsigned long long*)out.stats, r->ret, m);
+  } else if (!r->sticky) {
+    r->sticky = S.err;
+    r->sticky_msg = S.errmsg;
   }
-  if (m && out.stats) launch_stats_sum(stats_in, W, m, (unsigned long long*)out.stats, r->ret);
   CHK_HIP(e, hipGetLastError());
   CHK_HIP(e, hipEventRecord(S.done, r->ret));  // (outputs: read after rl_synchronize)
   r->t_second += now_s() - t1;
@@ -381,29 +410,11 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
 
 }  // namespace
 
-int comm_unique_id(uint8_t* id, std::string* err) {
-  Rccl& R = rccl();
-  if (!R.ok) {
-    *err = R.err;
-    return RL_E_COMM;
-  }
-  static_assert(sizeof(ncclUniqueId) == RL_COMM_ID_BYTES, "RL_COMM_ID_BYTES");
-  ncclUniqueId u;
-  const ncclResult_t rc = R.get_id(&u);
-  if (rc != ncclSuccess) {
-    *err = std::string("gpu: ncclGetUniqueId: ") + R.estr(rc);
-    return RL_E_COMM;
-  }
-  memcpy(id, &u, sizeof(u));
-  return RL_OK;
-}
+int comm_unique_id(uint8_t* id, std::string* err) { return rccl_unique_id(id, err); }
+
+int comm_loopback_id(uint8_t* id, std::string* err) { return loopback_new_id(id, err); }
 
 CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t* id, std::string* err) {
-  Rccl& R = rccl();
-  if (!R.ok) {
-    *err = R.err;
-    return nullptr;
-  }
   if (world < 1 || world > RL_MAX_SHARDS || rank >= world) {
     *err = "gpu: world must be 1..256 and rank < world";
     return nullptr;
@@ -419,27 +430,21 @@ CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t*
   r->timing = getenv("RL_DEBUG_ROUTE_TIMING") != nullptr;
   if (const char* pm = getenv("RL_DEBUG_OWNER_PART"))
     r->part_max = std::max<uint32_t>(1, std::min<uint32_t>(g.max_batch, (uint32_t)atoi(pm)));
-  bool ok = hipSetDevice(r->dev) == hipSuccess;
-  ncclUniqueId u;
-  memcpy(&u, id, sizeof(u));
-  // one communicator per direction of traffic (collective: every rank splits alike)
-  ncclResult_t nr = ok ? R.init(&r->comm_c, (int)world, u, (int)rank) : ncclSuccess;
-  if (nr == ncclSuccess && ok) nr = R.split(r->comm_c, 0, (int)rank, &r->comm_f, nullptr);
-  if (nr == ncclSuccess && ok) nr = R.split(r->comm_c, 0, (int)rank, &r->comm_r, nullptr);
-  if (nr != ncclSuccess) {
-    *err = std::string("gpu: RCCL communicator setup: ") + R.estr(nr);
+  r->tr.reset(loopback_id(id) ? loopback_join(id, world, rank, err) : rccl_join(id, world, rank, r->dev, err));
+  if (!r->tr) {
     comm_destroy(r);
     return nullptr;
   }
-  ok = ok && hipStreamCreateWithFlags(&r->cs, hipStreamNonBlocking) == hipSuccess &&
-       hipStreamCreateWithFlags(&r->fwd, hipStreamNonBlocking) == hipSuccess &&
-       hipStreamCreateWithFlags(&r->ret, hipStreamNonBlocking) == hipSuccess &&
-       hipEventCreateWithFlags(&r->in_ready, hipEventDisableTiming) == hipSuccess &&
-       hipHostMalloc((void**)&r->h_cnt, (size_t)RSLOTS * 4 * world * 8) == hipSuccess;
+  bool ok = hipSetDevice(r->dev) == hipSuccess &&
+            hipStreamCreateWithFlags(&r->cs, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&r->fwd, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&r->ret, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&r->in_ready, hipEventDisableTiming) == hipSuccess &&
+            hipHostMalloc((void**)&r->h_cnt, (size_t)RSLOTS * 2 * CNT_W * world * 8) == hipSuccess;
   for (uint32_t s = 0; s < RSLOTS && ok; s++) {
     CommSlot& S = r->slot[s];
     ok = dalloc(&S.send_rec, g.max_batch) == hipSuccess && dalloc(&S.send_stem, (size_t)g.max_stem_bytes + 64) == hipSuccess &&
-         dalloc(&S.perm, g.max_batch) == hipSuccess && dalloc(&S.cnt, 4 * (size_t)world) == hipSuccess &&
+         dalloc(&S.perm, g.max_batch) == hipSuccess && dalloc(&S.cnt, 2 * CNT_W * (size_t)world) == hipSuccess &&
          dalloc(&S.back, g.max_batch) == hipSuccess &&
          dalloc(&S.stats_stage, (size_t)world * r->m_max) == hipSuccess &&
          hipEventCreateWithFlags(&S.packed, hipEventDisableTiming) == hipSuccess &&
@@ -458,6 +463,8 @@ CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t*
   return r;
 }
 
+const char* comm_kind(const CommRouter* r) { return r && r->tr ? r->tr->kind() : ""; }
+
 void comm_destroy(CommRouter* r) {
   if (!r) return;
   if (r->timing && r->n_steps)
@@ -468,8 +475,7 @@ void comm_destroy(CommRouter* r) {
   (void)hipSetDevice(r->dev);
   for (hipStream_t st : {r->cs, r->fwd, r->ret})
     if (st) (void)hipStreamSynchronize(st);
-  for (ncclComm_t c : {r->comm_r, r->comm_f, r->comm_c})
-    if (c) (void)rccl().destroy(c);
+  r->tr.reset();
   for (CommSlot& S : r->slot) free_slot(S);
   if (r->h_cnt) (void)hipHostFree(r->h_cnt);
   if (r->in_ready) (void)hipEventDestroy(r->in_ready);
@@ -478,9 +484,11 @@ void comm_destroy(CommRouter* r) {
   delete r;
 }
 
-// Completes the pending batch (collective, like every routed step), then
-// waits for the router's streams.
+// Completes the pending batch (collective, like every routed step), waits for
+// the router's streams, then reports the first batch failure since the last
+// call.
 int comm_synchronize(CommRouter* r, Engine* e) {
+  if (r->broken) return eng_fail(e, r->broken, r->broken_msg);
   CHK_HIP(e, hipSetDevice(r->dev));
   if (r->pending >= 0) {
     const uint32_t p = (uint32_t)r->pending;
@@ -489,15 +497,18 @@ int comm_synchronize(CommRouter* r, Engine* e) {
     if (rc) return rc;
   }
   for (hipStream_t st : {r->cs, r->fwd, r->ret}) CHK_HIP(e, hipStreamSynchronize(st));
+  if (r->sticky) {
+    const int rc = eng_fail(e, r->sticky, r->sticky_msg);
+    r->sticky = RL_OK;
+    r->sticky_msg.clear();
+    return rc;
+  }
   return RL_OK;
 }
 
 int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, hipStream_t caller) {
-  const uint32_t W = r->world, n = in->n, nr = in->n_rules;
-  if ((uint64_t)W * nr > e->cfg.max_rules)
-    return eng_fail(e, RL_E_CAPACITY, "gpu: routed batches need max_rules >= world x n_rules (per-source stats)");
-  if (n && (!out->code || !out->limit_remaining || !out->reset_s))
-    return eng_fail(e, RL_E_INVALID, "gpu: null result array");
+  if (r->broken) return eng_fail(e, r->broken, r->broken_msg);
+  const uint32_t n = in->n, nr = in->n_rules;
   CHK_HIP(e, hipSetDevice(r->dev));
   const uint32_t s = r->next;
   r->next = (s + 1) % RSLOTS;
@@ -505,8 +516,19 @@ int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, 
   S.out = *out;
   S.n = n;
   S.n_rules = nr;
+  S.err = RL_OK;
+  S.errmsg.clear();
+  // checks the partition does not make: a failure here still takes part in
+  // the exchange (zero counts) and fails this rank's batch at rl_synchronize
+  int hostrc = RL_OK;
+  if (n && (!out->code || !out->limit_remaining || !out->reset_s)) {
+    hostrc = eng_fail(e, RL_E_INVALID, "gpu: null result array");
+  } else if ((uint64_t)r->world * nr > e->cfg.max_rules) {
+    hostrc = eng_fail(e, RL_E_CAPACITY, "gpu: routed batches need max_rules >= world x n_rules (per-source stats)");
+  }
+  if (hostrc) S.n_rules = 0;  // (a failed slice must not widen every owner's stats stride)
   const double t0 = now_s();
-  int rc = first_half(r, e, S, s, in, caller);
+  int rc = first_half(r, e, S, s, in, caller, hostrc);
   r->t_first += now_s() - t0;
   if (rc) return rc;
   // the previous batch: its counts had a whole call to arrive

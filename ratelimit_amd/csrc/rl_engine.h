@@ -119,8 +119,11 @@ int eng_debug_decide(Engine* c, uint32_t n, const uint32_t* before, const uint32
                      const uint32_t* hits, const uint32_t* limit, const uint8_t* unit, const uint8_t* flags,
                      const int64_t* now, uint8_t* code, uint32_t* remaining, uint32_t* reset_s, uint64_t* stat_deltas,
                      uint8_t* lc_set);
+// counts: cstride u64 per owner (records, stem bytes[, meta0, meta1]: the
+// in-library router's counts message).
 int eng_route_pack(Engine* c, const rl_batch* in, uint32_t n_shards, uint32_t src_rank, void* send_rec,
-                   uint8_t* send_stem, uint32_t* perm, uint64_t* counts, void* stream);
+                   uint8_t* send_stem, uint32_t* perm, uint64_t* counts, void* stream, uint32_t cstride = 2,
+                   uint64_t meta0 = 0, uint64_t meta1 = 0);
 int eng_route_do_limit(Engine* c, uint32_t n, const void* recv_rec, const uint8_t* recv_stem, uint64_t recv_stem_bytes,
                        const uint64_t* src_stem_base, uint32_t n_shards, uint32_t n_rules, uint32_t rule_stride,
                        uint64_t* ret, uint64_t* stats, int isolate, void* stream);

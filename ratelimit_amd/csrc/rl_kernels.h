@@ -191,8 +191,15 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
 // ev (optional, RL_NUM_STAGES + 1 events on stream st): recorded before
 // k_prepare, after it, after the sort, just before and just after k_table, and
 // at the end (per-stage timing, rl_profile).
+// counts: cstride u64 per owner (records, stem bytes[, meta0, meta1]).
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
-                       uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st);
+                       uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st,
+                       uint32_t cstride = 2, unsigned long long meta0 = 0, unsigned long long meta1 = 0);
+// The counts of a slice that failed on the host (zero records and bytes, meta words set).
+void launch_cnt_fill(unsigned long long* cnt, uint32_t n_peers, uint32_t cstride, unsigned long long meta0,
+                     unsigned long long meta1, hipStream_t st);
+// ret[0, n) = a failed record's packed result with rl_status `status`.
+void launch_route_fail(unsigned long long* ret, uint32_t n, uint32_t status, hipStream_t st);
 // src_err (optional): without o.status, a returned failure status sets its
 // error bit there (the source's batch then fails at rl_synchronize). errb
 // (optional): ret is an owner batch's own results; a failed batch (*errb)
@@ -203,8 +210,9 @@ void launch_route_scatter(const uint32_t* perm, const unsigned long long* ret, u
 // *errb when the batch's table stage failed.
 void launch_route_ret(const unsigned long long* res, uint32_t n, const uint32_t* errb, unsigned long long* ret,
                       hipStream_t st);
+// out[i] = sum over blocks b of stage[b * stride + i], i < m (stride 0: m).
 void launch_stats_sum(const unsigned long long* stage, uint32_t n_blocks, uint32_t m, unsigned long long* out,
-                      hipStream_t st);
+                      hipStream_t st, uint32_t stride = 0);
 void launch_sweep(Slot* slots, const Hist* hist, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st);
 void launch_arena_compact(Slot* slots, uint64_t nslots, const uint8_t* from, uint8_t* to, unsigned long long* used16,
                           hipStream_t st);

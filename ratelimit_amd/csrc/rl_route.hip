@@ -149,10 +149,12 @@ __global__ __launch_bounds__(256) void k_rp_count(BatchDev b, uint32_t n_shards,
 }
 
 // One block per owner d: exclusive scans of its row of tile counts (records,
-// bytes); counts[2d], [2d+1] = the totals (zero when the slice is malformed,
-// so the exchange stays well-formed); tot[d], tot[n_shards + d] too.
+// bytes); counts[cstride d], [cstride d + 1] = the totals (zero when the slice
+// is malformed, so the exchange stays well-formed); tot[d], tot[n_shards + d]
+// too.
 __global__ __launch_bounds__(1024) void k_rp_scan(uint32_t* __restrict__ hist, uint32_t n_shards, uint32_t ntiles,
-                                                  unsigned long long* __restrict__ counts,
+                                                  unsigned long long* __restrict__ counts, uint32_t cstride,
+                                                  unsigned long long meta0, unsigned long long meta1,
                                                   uint32_t* __restrict__ tot, const uint32_t* err) {
   __shared__ uint32_t tmp[32];
   const uint32_t d = blockIdx.x;
@@ -172,8 +174,12 @@ __global__ __launch_bounds__(1024) void k_rp_scan(uint32_t* __restrict__ hist, u
   }
   if (threadIdx.x == 0) {
     const bool ok = *err == 0;
-    counts[2 * d] = ok ? ca : 0u;
-    counts[2 * d + 1] = ok ? cb : 0u;
+    counts[(size_t)cstride * d] = ok ? ca : 0u;
+    counts[(size_t)cstride * d + 1] = ok ? cb : 0u;
+    if (cstride >= 4) {  // (the in-library router's counts message: n_rules, flags)
+      counts[(size_t)cstride * d + 2] = meta0;
+      counts[(size_t)cstride * d + 3] = meta1;
+    }
     tot[d] = ca;
     tot[n_shards + d] = cb;
   }
@@ -297,7 +303,7 @@ __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, 
     x.lu = len | ((uint32_t)b.unit[i] << 16) | ((uint32_t)b.flags[i] << 24);
     x.limit = b.limit[i];
     x.hits = b.hits[i];
-    x.rule = b.rule[i];
+    x.rule = b.rule[i] < b.n_rules ? b.rule[i] : 0xFFFFFFFFu;  // (the owner fails it alone, any rule stride)
     x.now = b.now[q];
     x.hash = hash[i];
 #if !(RL_RP_ABL & 2)
@@ -376,28 +382,60 @@ __global__ __launch_bounds__(256) void k_route_ret(const unsigned long long* __r
   ret[i] = e ? pack_fail(err_status(e)) : res[i];
 }
 
-// Per-rule stats deltas of several owners (blocks of m counters) summed into out.
+// Per-rule stats deltas of several owners (blocks of `stride` counters, the
+// first m of each) summed into out[0, m).
 __global__ __launch_bounds__(256) void k_stats_sum(const unsigned long long* __restrict__ stage, uint32_t n_blocks,
-                                                   uint32_t m, unsigned long long* __restrict__ out) {
+                                                   uint32_t m, uint32_t stride, unsigned long long* __restrict__ out) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= m) return;
   unsigned long long s = 0;
-  for (uint32_t b = 0; b < n_blocks; b++) s += stage[(size_t)b * m + i];
+  for (uint32_t b = 0; b < n_blocks; b++) s += stage[(size_t)b * stride + i];
   out[i] = s;
+}
+
+// An owner batch that cannot run: every received record answers `status`.
+__global__ __launch_bounds__(256) void k_route_fail(unsigned long long* __restrict__ ret, uint32_t n, uint32_t status) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) ret[i] = pack_fail(status);
+}
+
+// The counts message of a slice that failed on the host: no records, no
+// bytes, and the sender's meta words.
+__global__ void k_cnt_fill(unsigned long long* cnt, uint32_t n_peers, uint32_t cstride, unsigned long long meta0,
+                           unsigned long long meta1) {
+  for (uint32_t p = threadIdx.x; p < n_peers; p += blockDim.x) {
+    unsigned long long* c = cnt + (size_t)cstride * p;
+    c[0] = c[1] = 0;
+    if (cstride >= 4) {
+      c[2] = meta0;
+      c[3] = meta1;
+    }
+  }
 }
 
 }  // namespace
 
 void launch_stats_sum(const unsigned long long* stage, uint32_t n_blocks, uint32_t m, unsigned long long* out,
-                      hipStream_t st) {
-  if (m) k_stats_sum<<<cdiv(m, 256), 256, 0, st>>>(stage, n_blocks, m, out);
+                      hipStream_t st, uint32_t stride) {
+  if (m) k_stats_sum<<<cdiv(m, 256), 256, 0, st>>>(stage, n_blocks, m, stride ? stride : m, out);
+}
+
+void launch_route_fail(unsigned long long* ret, uint32_t n, uint32_t status, hipStream_t st) {
+  if (n) k_route_fail<<<cdiv(n, 256), 256, 0, st>>>(ret, n, status);
+}
+
+void launch_cnt_fill(unsigned long long* cnt, uint32_t n_peers, uint32_t cstride, unsigned long long meta0,
+                     unsigned long long meta1, hipStream_t st) {
+  k_cnt_fill<<<1, 256, 0, st>>>(cnt, n_peers, cstride, meta0, meta1);
 }
 
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
-                       uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st) {
+                       uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st, uint32_t cstride,
+                       unsigned long long meta0, unsigned long long meta1) {
   const uint32_t ntiles = b.n ? cdiv(b.n, RP_TILE) : 0u;
   if (b.n) k_rp_count<<<ntiles, 256, 0, st>>>(b, n_shards, ntiles, s.route_dest, s.route_hash, s.route_hist, s.err);
-  k_rp_scan<<<n_shards, 1024, 0, st>>>(s.route_hist, n_shards, ntiles, counts, s.route_start, s.err);
+  k_rp_scan<<<n_shards, 1024, 0, st>>>(s.route_hist, n_shards, ntiles, counts, cstride, meta0, meta1, s.route_start,
+                                       s.err);
   if (b.n)
     k_rp_pack<<<ntiles, 256, 0, st>>>(b, n_shards, ntiles, src_rank, s.route_dest, s.route_hash, s.route_hist,
                                       s.route_start, out,

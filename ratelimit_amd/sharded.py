@@ -2,11 +2,14 @@
 
 Two drivers of the same exchange:
 
-* RcclRouter (production): the whole routed step inside the library
-  (rl_comm_init + rl_do_limit_routed_async, rl_comm.hip): partition, RCCL
-  send/recv over xGMI, owner pipeline, return, scatter, with one host wait
-  per batch (its partition counts) and no Python on the per-batch path beyond
-  one ctypes call.
+* LibRouter / RcclRouter (production): the whole routed step inside the
+  library (rl_comm_init + rl_do_limit_routed_async, rl_comm.hip): partition,
+  RCCL send/recv over xGMI, owner pipeline, return, scatter, with one host
+  wait per batch (its partition counts) and no Python on the per-batch path
+  beyond one ctypes call. The same library router runs W ranks inside one
+  process over its loopback transport (loopback_id(): threads, one Backend
+  each, several on one GPU), which is how the multi-rank protocol is
+  exercised on a one-GPU machine.
 * ShardedRateLimitCache (below): the same protocol with the collectives issued
   from Python (torch.distributed all_to_all_single) around the device halves
   rl_route_pack / rl_route_do_limit / rl_route_scatter. It runs over gloo as
@@ -59,40 +62,50 @@ from ._lib import RedisError, check, lib
 WIRE_BYTES = 40  # RL_WIRE_BYTES
 
 
-class RcclRouter:
-    """DoLimit over a table hash-sharded across every rank of the default
-    process group, routed by the library over its own RCCL communicator.
+def loopback_id() -> np.ndarray:
+    """The id of a new in-process loopback world (rl_comm_loopback_id): its
+    ranks are threads of this process, one Backend each (they may share one
+    GPU), exchanging by device copies with the RCCL router's protocol."""
+    uid = np.zeros(abi.RL_COMM_ID_BYTES, np.uint8)
+    check(None, lib().rl_comm_loopback_id(abi.ptr(uid)))
+    return uid
 
-    Every rank builds one Backend (one GPU, hash_seed shared by all ranks and
-    max_rules >= world x n_rules), then calls submit() once per node batch with
-    its slice (device tensors, the rl_batch / rl_result layout; a rank may
-    pass n = 0). Results land in dev_out in arrival order; dev_out["stats"]
-    (optional) receives the deltas of this rank's requests. A submit completes
-    the previous batch (the library never waits for work it just issued);
-    dev_out is final after finish(), which every rank calls together: it
-    completes the last batch and raises RedisError if one failed on this rank.
+
+class LibRouter:
+    """DoLimit over a table hash-sharded across `world` ranks, routed by the
+    library (rl_comm_init + rl_do_limit_routed_async, rl_comm.hip).
+
+    Every rank builds one Backend (hash_seed shared by all ranks, max_rules >=
+    world x n_rules), joins the world `uid` (RCCL: rl_comm_unique_id handed to
+    every process; loopback: loopback_id(), ranks as threads), then calls
+    submit() once per node batch with its slice (device tensors, the rl_batch /
+    rl_result layout; a rank may pass n = 0). Results land in dev_out in
+    arrival order; dev_out["stats"] (optional) receives the deltas of this
+    rank's requests. A submit completes the previous batch (the library never
+    waits for work it just issued); dev_out is final after finish(), which
+    every rank calls together: it completes the last batch and raises
+    RedisError if one failed on this rank. Tensors handed to submit must stay
+    alive until the next submit (inputs) or finish (outputs).
     """
 
-    def __init__(self, backend, group=None):
+    def __init__(self, backend, world: int, rank: int, uid: np.ndarray):
         if not backend.cfg.hash_seed:
             raise ValueError("a sharded table needs an explicit hash_seed shared by every shard (owner = stem hash)")
         self.be = backend
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
-        uid = np.zeros(abi.RL_COMM_ID_BYTES, np.uint8)
-        if self.rank == 0:
-            check(None, lib().rl_comm_unique_id(abi.ptr(uid)))
-        box = [uid.tobytes()]
-        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
-        uid = np.frombuffer(box[0], np.uint8).copy()
-        check(backend.ctx, lib().rl_comm_init(backend.ctx, self.world, self.rank, abi.ptr(uid)))
+        self.world, self.rank = world, rank
+        uid = np.ascontiguousarray(uid, np.uint8)
+        check(backend.ctx, lib().rl_comm_init(backend.ctx, world, rank, abi.ptr(uid)))
         self.device = torch.device("cuda", backend.cfg.device)
+        # the batch's inputs are ordered through a stream of our own: torch's
+        # default stream has the NULL handle, which the library reads as
+        # "inputs complete at the call"
+        self.stream = torch.cuda.Stream(self.device)
 
     def submit(self, dev_in: dict, n: int, n_requests: int, n_rules: int, dev_out: dict):
         b = abi.make_batch_struct(dev_in, n, n_requests, n_rules)
         r = abi.make_result_struct(dev_out)
-        st = torch.cuda.current_stream(self.device)
-        check(self.be.ctx, lib().rl_do_limit_routed_async(self.be.ctx, b, r, st.cuda_stream))
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        check(self.be.ctx, lib().rl_do_limit_routed_async(self.be.ctx, b, r, self.stream.cuda_stream))
 
     def finish(self):
         self.be.synchronize()
@@ -100,6 +113,21 @@ class RcclRouter:
     def do_limit(self, dev_in: dict, n: int, n_requests: int, n_rules: int, dev_out: dict):
         self.submit(dev_in, n, n_requests, n_rules, dev_out)
         self.finish()
+
+
+class RcclRouter(LibRouter):
+    """LibRouter over RCCL across every rank of a torch.distributed group (one
+    process per GPU): rank 0's rl_comm_unique_id is broadcast to the others."""
+
+    def __init__(self, backend, group=None):
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        uid = np.zeros(abi.RL_COMM_ID_BYTES, np.uint8)
+        if rank == 0:
+            check(None, lib().rl_comm_unique_id(abi.ptr(uid)))
+        box = [uid.tobytes()]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        super().__init__(backend, world, rank, np.frombuffer(box[0], np.uint8).copy())
 
 
 class Exchange:
@@ -178,6 +206,12 @@ class DeviceRouteOps:
         for t in dev_out.values():
             if t is not None:
                 t.record_stream(self.ret)
+
+    def before_pack(self, slot: int):
+        # the partition rewrites slot's permutation: the scatter of the slot's
+        # previous batch (return side) must have read it
+        if self.stats_free[slot] is not None:
+            self.fwd.wait_event(self.stats_free[slot])
 
     def before_payload(self, slot: int):
         if self.recv_free[slot] is not None:
@@ -296,6 +330,7 @@ class ShardedRateLimitCache:
         self.t += 1
         nst = n_rules * abi.RL_NUM_STATS
         self._hook("begin", dev_in, dev_out)
+        self._hook("before_pack", slot)
         with self._phase("fwd", slot):
             # 1. pack by owner
             self.counts.zero_()
