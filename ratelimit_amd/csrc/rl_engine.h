@@ -45,8 +45,6 @@ struct Engine {
   hipEvent_t route_ready = nullptr;  // eng_route_do_limit: the caller's received buffers are ready
   hipEvent_t caller_ready = nullptr; // eng_do_limit_async: the caller stream's work so far (the inputs)
   bool serial_debug = false;         // RL_DEBUG_SERIAL: async batches run serially on the caller's stream
-  hipStream_t side = nullptr;     // k_runs_general beside k_table (stage B)
-  hipEvent_t side_go = nullptr, side_done = nullptr;
   uint32_t next = 0, last = NBUF - 1;  // buffer of the next / of the latest batch
   uint64_t hash_seed = 0;
   HashKey hk{};

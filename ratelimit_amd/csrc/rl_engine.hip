@@ -134,14 +134,14 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     (void)hipStreamWaitEvent(a, c->consumed[k], 0);  // ... and its routed results were read
     launch_stage_a(b, c->s[k], isolate, a, ev);
     (void)hipStreamWaitEvent(a, c->b_done[c->last], 0);  // table order
-    launch_stage_b(b, o, t, P, c->s[k], restore, a, c->side, c->side_go, c->side_done, ev);
+    launch_stage_b(b, o, t, P, c->s[k], restore, a, ev);
     (void)hipEventRecord(c->b_done[k], a);
   } else {
     if (!st) st = c->stream;
     (void)after_batches(c, st);
     hipEvent_t* ev = prof_events(c);
     launch_stage_a(b, c->s[k], isolate, st, ev);
-    launch_stage_b(b, o, t, P, c->s[k], restore, st, c->side, c->side_go, c->side_done, ev);
+    launch_stage_b(b, o, t, P, c->s[k], restore, st, ev);
     (void)hipEventRecord(c->b_done[k], st);
   }
   c->last = k;
@@ -309,11 +309,8 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   bool ok = true;
   for (uint32_t k = 0; k < NBUF; k++) ok = ok && hipStreamCreateWithFlags(&c->pipe[k], hipStreamNonBlocking) == hipSuccess;
   c->stream = c->pipe[0];
-  ok = ok && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++)
     ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess;
-  ok = ok && hipEventCreateWithFlags(&c->side_go, hipEventDisableTiming) == hipSuccess &&
-       hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming) == hipSuccess;
   ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess && dalloc(&c->hist, c->nslots) == hipSuccess;
   ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess && dalloc(&c->arena2, cfg.arena_bytes) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++) ok = ok && alloc_buffer(c->s[k], n);
@@ -391,9 +388,6 @@ void eng_destroy(Engine* c) {
   }
   for (uint32_t k = 0; k < NBUF; k++)
     if (c->pipe[k]) (void)hipStreamSynchronize(c->pipe[k]);
-  if (c->side) (void)hipStreamSynchronize(c->side);
-  if (c->side_go) (void)hipEventDestroy(c->side_go);
-  if (c->side_done) (void)hipEventDestroy(c->side_done);
   for (uint32_t k = 0; k < PROF_RING; k++)
     for (int i = 0; i <= RL_NUM_STAGES; i++)
       if (c->ev[k][i]) (void)hipEventDestroy(c->ev[k][i]);
@@ -423,7 +417,6 @@ void eng_destroy(Engine* c) {
   if (c->h_match) (void)hipHostFree(c->h_match);
   for (uint32_t k = 0; k < NBUF; k++)
     if (c->pipe[k]) (void)hipStreamDestroy(c->pipe[k]);
-  if (c->side) (void)hipStreamDestroy(c->side);
   delete c;
 }
 

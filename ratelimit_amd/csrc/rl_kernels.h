@@ -26,11 +26,7 @@ constexpr uint32_t RUN_SLOW = 1, RUN_FAST = 2, RUN_MULTI = 4;
 constexpr uint32_t KEY_HEAD = 64;         // stem bytes carried inline (zero-padded) per descriptor
 constexpr uint32_t STAT_STRIPES = 64;     // global partial stats tables
 constexpr uint32_t STAT_LDS_RULES = 512;  // rules aggregated in LDS (== LDS_RULES)
-#ifndef RL_RG_BLOCKS
-#define RL_RG_BLOCKS 64
-#endif
-constexpr uint32_t RUNS_GENERAL_BLOCKS = RL_RG_BLOCKS;  // k_runs_general grids (grid-stride over deferrals):
-constexpr uint32_t RUNS_GENERAL_LATE_BLOCKS = 8;  //   RUN_MULTI runs beside k_table / k_table's deferrals after it
+constexpr uint32_t RUNS_GENERAL_LATE_BLOCKS = 8;  // k_late's exact-path workgroups (grid-stride over deferrals)
 
 struct Wire;
 struct BatchDev {
@@ -136,10 +132,10 @@ struct Scratch {
   uint32_t* big_work;                // [n / BIG_CHUNK + PART_DIGITS] chunk work items (bucket << 16 | chunk)
   uint32_t* work_n;
   uint32_t* big_cnt;                 // [work items x (1 + 2 x BIG_HEAVY)] k_big_count per chunk
-  uint32_t* grp;                  // k_runs_general: stem group of each position of a deferred run
+  uint32_t* grp;                  // exact path: stem group of each position of a deferred run
   uint32_t* lead;                 //   first position of each group (stored from the run's start)
   uint8_t* gmask;                 //   units seen per group
-  uint32_t* defer;                // RUN_MULTI runs (k_run_check), for k_runs_general beside k_table
+  uint32_t* defer;                // RUN_MULTI runs (k_run_check); k_split marks the ones it resolves
   uint32_t* defer_n;
   uint32_t* defer2;               // runs k_table found to need the exact path (k_late)
   uint32_t* defer2_n;
@@ -182,12 +178,8 @@ struct Scratch {
 // batch's stage B; stage B (table probe, replay, decisions, stats, results)
 // must run in batch order.
 void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_t st, hipEvent_t* ev = nullptr);
-// Stage B launches the RUN_MULTI runs' exact path (k_runs_general) on `side`
-// beside k_table (after event go); the stream st waits for side_done before
-// k_finish.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                    int restore, hipStream_t st, hipStream_t side, hipEvent_t go, hipEvent_t side_done,
-                    hipEvent_t* ev = nullptr);
+                    int restore, hipStream_t st, hipEvent_t* ev = nullptr);
 // ev (optional, RL_NUM_STAGES + 1 events on stream st): recorded before
 // k_prepare, after it, after the sort, just before and just after k_table, and
 // at the end (per-stage timing, rl_profile).

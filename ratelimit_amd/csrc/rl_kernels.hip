@@ -17,9 +17,9 @@
 //                 lane per run): probe/insert the (stem, unit) slot of the HBM
 //                 table; replay short runs in registers, set up long uniform
 //                 runs for the parallel path
-//   k_runs_general the exact path (side stream): RUN_MULTI runs left
-//   k_late        k_table's exact-path deferrals + long runs decided in
-//                 parallel (k_fast_over first with the local cache on)
+//   k_late        the exact path (RUN_MULTI runs k_split left, k_table's
+//                 deferrals) + long runs decided in parallel (k_fast_over
+//                 first with the local cache on)
 //   k_finish      packed results -> code / limit_remaining / reset_s, and the
 //                 striped per-block stats -> rl_result.stats
 // plus k_sweep (epoch sweep = Redis EXPIRE), k_table_info, debug kernels.
@@ -2207,7 +2207,7 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
     const Rec x = rec[eq], y = rec[ep];
     rec[eq].lu = x.lu | (FLAG_DUP << 24);
     if (q == p + 1) rec[ep].lu = y.lu | (FLAG_DUP << 24);  // the run's head
-    // a failed descriptor (FLAG_SKIP) makes its run exact-path: k_runs_general leaves it out
+    // a failed descriptor (FLAG_SKIP) makes its run exact-path: general_body leaves it out
     const bool same = !((rec_flags(x) | rec_flags(y)) & FLAG_SKIP) && x.hlo == y.hlo &&
                       (x.lu & 0xFFFFFFu) == (y.lu & 0xFFFFFFu) &&  // hash, length, unit
                       key_equal(key_of(b, x), key_of(b, y));
@@ -2745,7 +2745,7 @@ __device__ __attribute__((always_inline)) inline void runs_body(uint32_t blk, Ba
     SlotImg im;
     load_img_lo(&t.slots[h0 >> t.shift], im);  // home slot's first sector, in flight beside the stem
     const Key k0 = key_of(b, x0);
-    // RUN_MULTI runs belong to k_runs_general; a run of one failed descriptor is done
+    // RUN_MULTI runs belong to the exact path (k_late); a run of one failed descriptor is done
     if (!(fl & RUN_MULTI) && !(rec_flags(x0) & FLAG_SKIP)) {
       const bool long_run = !restore && end - p >= LONG_RUN && !(fl & RUN_SLOW);
       bool ok = true;
@@ -2990,16 +2990,18 @@ __device__ __attribute__((always_inline)) inline void general_body(uint32_t blk,
                                                       unsigned long long* __restrict__ res,
                                                       const uint32_t* __restrict__ run_start,
                                                       const uint32_t* __restrict__ run_end,
-                                                      const uint32_t* __restrict__ defer, const uint32_t* defer_n,
+                                                      const uint32_t* __restrict__ defer_a, const uint32_t* defer_a_n,
+                                                      const uint32_t* __restrict__ defer_b, const uint32_t* defer_b_n,
                                                       uint32_t* __restrict__ grp, uint32_t* __restrict__ lead,
                                                       uint8_t* __restrict__ gmask, const uint32_t* __restrict__ keys0,
                                                       const uint32_t* __restrict__ defer1, const uint32_t* defer1_n,
                                                       unsigned long long* stats, unsigned long long* stripes,
                                                       uint32_t* err, uint32_t* errs, int restore) {
-  __shared__ uint32_t s_err, s_n, s_n1;
+  __shared__ uint32_t s_err, s_na, s_n, s_n1;
   if (threadIdx.x == 0) {
     s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_n = *defer_n;
+    s_na = *defer_a_n;
+    s_n = s_na + *defer_b_n;
     s_n1 = defer1_n ? *defer1_n : 0u;
   }
   __syncthreads();
@@ -3014,7 +3016,7 @@ __device__ __attribute__((always_inline)) inline void general_body(uint32_t blk,
   // Grid-stride over the deferred runs: the grid is small and fixed (deferrals
   // are rare), so an empty deferral list costs one short launch.
   for (uint32_t di = blk * 256 + threadIdx.x; di < s_n; di += nblk * 256) {
-    const uint32_t rr = defer[di];  // run id
+    const uint32_t rr = di < s_na ? defer_a[di] : defer_b[di - s_na];  // run id
     if (rr == DEFER_DONE) continue;  // split into ordinary runs (k_split)
     const uint32_t p = run_start[rr], end = run_end[rr];
     const uint32_t key = skeys[p];
@@ -3116,30 +3118,14 @@ __global__ __launch_bounds__(256) void k_table(uint32_t g_runs, BatchDev b, Tabl
                 restore);
 }
 
-// k_runs_general (side stream): beside k_table, the RUN_MULTI runs (defer);
-// after it, the stems k_table found under several units in the table (defer:
-// its runs, defer1: keys seen once).
-__global__ __launch_bounds__(256) void k_runs_general(BatchDev b, TableDev t, Params P, SRec rec_s,
-                                                      const uint32_t* __restrict__ skeys,
-                                                      const uint32_t* __restrict__ svals,
-                                                      unsigned long long* __restrict__ res,
-                                                      const uint32_t* __restrict__ run_start,
-                                                      const uint32_t* __restrict__ run_end,
-                                                      const uint32_t* __restrict__ defer, const uint32_t* defer_n,
-                                                      uint32_t* __restrict__ grp, uint32_t* __restrict__ lead,
-                                                      uint8_t* __restrict__ gmask, const uint32_t* __restrict__ keys0,
-                                                      const uint32_t* __restrict__ defer1, const uint32_t* defer1_n,
-                                                      unsigned long long* stats, unsigned long long* stripes,
-                                                      uint32_t* err, uint32_t* errs, int restore) {
-  general_body(blockIdx.x, gridDim.x, b, t, P, rec_s, skeys, svals, res, run_start, run_end, defer, defer_n, grp, lead,
-               gmask, keys0, defer1, defer1_n, stats, stripes, err, errs, restore);
-}
-
-// k_late (after k_table, and k_fast_over with the local cache on): the stems
-// k_table found under several units in the table (general_body, blocks
-// [0, RUNS_GENERAL_LATE_BLOCKS): defer2 = its runs, defer1 = keys seen once)
-// and the long runs' elements (fast_emit_body, the rest). The two touch
-// disjoint stems. At least 8 waves per SIMD caps the grid at 64 VGPRs: the
+// k_late (after k_table, and k_fast_over with the local cache on): the exact
+// path (general_body, blocks [0, RUNS_GENERAL_LATE_BLOCKS): the RUN_MULTI runs
+// k_split left (defer), the stems k_table found under several units in the
+// table (defer2: its runs, defer1: keys seen once)) and the long runs'
+// elements (fast_emit_body, the rest). They touch disjoint stems, and none of
+// k_table's. (Until round 3 the RUN_MULTI runs had a launch of their own on a
+// side stream beside k_table: 64 workgroups that k_finish waited for, 12% of
+// kernel time at C1 for an all-but-empty list once k_split resolves it.) At least 8 waves per SIMD caps the grid at 64 VGPRs: the
 // rare exact path spills to scratch instead of lowering the streaming part's
 // occupancy (uncapped, the exact path's 88 VGPRs slowed the long-run part
 // 55 -> 85 us at C2).
@@ -3148,6 +3134,7 @@ __global__ __launch_bounds__(256, 8) void k_late(BatchDev b, TableDev t, Params 
                                                  unsigned long long* __restrict__ res,
                                                  const uint32_t* __restrict__ run_start,
                                                  const uint32_t* __restrict__ run_end,
+                                                 const uint32_t* __restrict__ defer, const uint32_t* defer_n,
                                                  const uint32_t* __restrict__ defer2, const uint32_t* defer2_n,
                                                  uint32_t* __restrict__ grp, uint32_t* __restrict__ lead,
                                                  uint8_t* __restrict__ gmask, const uint32_t* __restrict__ keys0,
@@ -3158,8 +3145,9 @@ __global__ __launch_bounds__(256, 8) void k_late(BatchDev b, TableDev t, Params 
                                                  unsigned long long* stats, unsigned long long* stripes, uint32_t* err,
                                                  uint32_t* errs, int restore, const uint32_t* __restrict__ fast_blk) {
   if (blockIdx.x < RUNS_GENERAL_LATE_BLOCKS)
-    general_body(blockIdx.x, RUNS_GENERAL_LATE_BLOCKS, b, t, P, rec_s, skeys, svals, res, run_start, run_end, defer2,
-                 defer2_n, grp, lead, gmask, keys0, defer1, defer1_n, stats, stripes, err, errs, restore);
+    general_body(blockIdx.x, RUNS_GENERAL_LATE_BLOCKS, b, t, P, rec_s, skeys, svals, res, run_start, run_end, defer,
+                 defer_n, defer2, defer2_n, grp, lead, gmask, keys0, defer1, defer1_n, stats, stripes, err, errs,
+                 restore);
   else if (!restore)
     fast_emit_body(blockIdx.x - RUNS_GENERAL_LATE_BLOCKS, b.n, b.n_rules, t, P, rec_s, svals, res, segsum, rid,
                    run_start, run_end, run_flags, run_state, run_f, stats, stripes, err, fast_blk);
@@ -3384,8 +3372,7 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
 // result into it first. The keys seen once and the sorted path (runs
 // and its exact / parallel companions) touch disjoint stems.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                    int restore, hipStream_t st, hipStream_t side, hipEvent_t go, hipEvent_t side_done,
-                    hipEvent_t* ev) {
+                    int restore, hipStream_t st, hipEvent_t* ev) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
   k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, s.defer2_n, s.defer1_n, o.stats, m, s.fast_blk, cdiv(b.n, 256 * 32));
@@ -3393,17 +3380,9 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     const uint32_t g = cdiv(b.n, 256);
     const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
     const SRec rs{s.rec, s.vals[0]};
-    // Side stream: the RUN_MULTI runs (known since k_run_check) beside k_table.
-    // Main stream: k_table (the runs of two or more and the keys seen once),
-    // then k_late (k_table's deferrals and the long runs' elements). All these
-    // grids touch disjoint stems; k_finish waits for both streams.
-    (void)hipEventRecord(go, st);
-    (void)hipStreamWaitEvent(side, go, 0);
-    const uint32_t gs = g < RUNS_GENERAL_BLOCKS ? g : RUNS_GENERAL_BLOCKS;
-    k_runs_general<<<gs, 256, lds, side>>>(b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer,
-                                           s.defer_n, s.grp, s.lead, s.gmask, nullptr, nullptr, nullptr, o.stats,
-                                           s.stripes, s.errb, s.errs, restore);
-    (void)hipEventRecord(side_done, side);
+    // k_table (the runs of two or more and the keys seen once), then k_late
+    // (the exact path and the long runs' elements): grids whose parts touch
+    // disjoint stems.
     if (ev) (void)hipEventRecord(ev[3], st);
     const uint32_t g_runs = cdiv(b.n / 2 + BIG_HEAVY * PART_DIGITS, 256);
     k_table<<<g_runs + g, 256, lds, st>>>(g_runs, b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end,
@@ -3414,10 +3393,10 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     if (!restore && P.lc_en)
       k_fast_over<<<g, 256, 0, st>>>(b.n, rs, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
     k_late<<<RUNS_GENERAL_LATE_BLOCKS + (restore ? 0u : g), 256, lds, st>>>(
-        b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer2, s.defer2_n, s.grp, s.lead, s.gmask,
+        b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer, s.defer_n, s.defer2, s.defer2_n,
+        s.grp, s.lead, s.gmask,
         s.keys[0], s.defer1, s.defer1_n, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb,
         s.errs, restore, s.fast_blk);
-    (void)hipStreamWaitEvent(st, side_done, 0);
     if (!restore) {
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;
       const uint32_t gf = cdiv(nf * RL_NUM_STATS > b.n ? nf * RL_NUM_STATS : b.n, 256);
