@@ -205,6 +205,7 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
   const size_t items = (size_t)n / (64 * 4 * 8) + 1 + PART_DIGITS;  // BIG_CHUNK-position work items
   bool ok = dalloc(&s.big_meta, PART_DIGITS) == hipSuccess && dalloc(&s.big_n, 1) == hipSuccess &&
             dalloc(&s.big_work, items) == hipSuccess && dalloc(&s.work_n, 1) == hipSuccess &&
+            dalloc(&s.sorted_n, 1) == hipSuccess &&
             dalloc(&s.big_cnt, items * (1 + 2 * BIG_HEAVY)) == hipSuccess;
   ok = ok && dalloc(&s.rec, n) == hipSuccess && dalloc(&s.res, n) == hipSuccess;
   for (int i = 0; i < 2; i++) ok = ok && dalloc(&s.keys[i], n) == hipSuccess && dalloc(&s.vals[i], n) == hipSuccess;
@@ -227,7 +228,7 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
 }
 
 void free_buffer(Scratch& s) {
-  void* bufs[] = {s.rec, s.res, s.big_meta, s.big_n, s.big_work, s.work_n, s.big_cnt, s.keys[0], s.keys[1],
+  void* bufs[] = {s.rec, s.res, s.big_meta, s.big_n, s.big_work, s.work_n, s.sorted_n, s.big_cnt, s.keys[0], s.keys[1],
                   s.vals[0], s.vals[1], s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1,
                   s.defer1_n, s.fast_blk, s.hits_s, s.segsum, s.rid, s.run_start, s.run_flags, s.run_state, s.run_f,
                   s.runs64, s.split, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t, s.r_base};

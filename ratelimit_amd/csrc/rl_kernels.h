@@ -131,6 +131,8 @@ struct Scratch {
   uint32_t* big_n;
   uint32_t* big_work;                // [n / BIG_CHUNK + PART_DIGITS] chunk work items (bucket << 16 | chunk)
   uint32_t* work_n;
+  uint32_t* sorted_n;                // sorted positions of the batch: the descriptors whose sort key repeats
+                                     // (plus every element of a large bucket), one block per bucket
   uint32_t* big_cnt;                 // [work items x (1 + 2 x BIG_HEAVY)] k_big_count per chunk
   uint32_t* grp;                  // exact path: stem group of each position of a deferred run
   uint32_t* lead;                 //   first position of each group (stored from the run's start)

@@ -49,17 +49,18 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
                                                  const int64_t* time_floor, uint32_t* defer_n,
                                                  uint32_t* big_n, uint32_t* work_n, uint32_t* __restrict__ run_flags,
                                                  unsigned long long* num_runs, uint32_t* __restrict__ hit_a,
-                                                 unsigned long long* __restrict__ res) {
+                                                 unsigned long long* __restrict__ res, uint32_t* sorted_n) {
   __shared__ uint32_t lds[HASH_LDS_BYTES / 4 + 4];
   const uint32_t tid = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + tid;
   uint32_t bad = 0;
   if (i < b.n) run_flags[i] = 0;  // k_run_check ORs run flags in from any block
-  if (blockIdx.x == 0 && tid == 0) {  // per-batch counters: RUN_MULTI queue, run ids, large buckets
+  if (blockIdx.x == 0 && tid == 0) {  // per-batch counters: RUN_MULTI queue, run ids, large buckets, sorted positions
     *defer_n = 0;
     *num_runs = 0;
     *big_n = 0;
     *work_n = 0;
+    *sorted_n = 0;
   }
   const int64_t floor = *time_floor;
   auto time_bad = [&](int64_t t) { return t < 0 || t > (int64_t)NOW_MAX || t < floor; };
@@ -1467,14 +1468,14 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
     uint32_t* __restrict__ sh, uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
     uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end, unsigned long long* num_runs,
     uint32_t* __restrict__ drun, BigMeta* __restrict__ meta, uint32_t* big_n, uint32_t* __restrict__ work,
-    uint32_t* work_n, const uint32_t* err) {
+    uint32_t* work_n, uint32_t* sorted_n, const uint32_t* err) {
   using B = BkSmall;
   __shared__ BucketLds<B> L;
   if (*err) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, d = blockIdx.x;
   BK_STAMP(d, 0);
   bucket_setup(L, info, ntiles, d);
-  const uint32_t S = L.S, base = L.base_pos;
+  const uint32_t S = L.S;
   if (!S) return;
   if (S > B::CAP) {  // queued: hot keys sampled, their run ids and the chunk work items allocated
     sample_heavy(L, S, ntiles, pt);
@@ -1482,7 +1483,7 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
       BigMeta M;
       M.d = d;
       M.S = S;
-      M.base = base;
+      M.base = atomicAdd(sorted_n, S);  // (every element: the hot keys' bucket is mostly runs)
       M.r = L.nheavy;
       M.nchunks = M.r ? (S + BIG_CHUNK - 1) / BIG_CHUNK : 0u;
       M.item0 = M.nchunks ? atomicAdd(work_n, M.nchunks) : 0u;
@@ -1515,21 +1516,109 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
     vv[i] = e.y;
     hh[i] = e.z;
   }
-#pragma unroll
-  for (uint32_t i = 0; i < B::ITEMS; i++)
-    if (strip0 + i * 64 + lane >= S) kk[i] = 0xFFFFFFFFu;
   BK_STAMP(d, 2);
-  lds_sort3(L, kk, vv, hh, S);
+  // Keys seen once in the batch never enter the sorted order (k_table answers
+  // them in arrival order): every descriptor of a key falls in its bucket, so
+  // an LDS hash of the bucket's keys finds the duplicated ones (~5% at C1),
+  // and only those are sorted, segmented and written. Their sorted positions
+  // are one block per bucket, allocated from sorted_n (runs never cross
+  // buckets, so no order between buckets is needed).
+  uint32_t* ht = L.v;                                   // [2 CAP]: L.v and L.h (values are in registers)
+  uint8_t* df = reinterpret_cast<uint8_t*>(&L.wcnt[0][0]);  // [CAP] duplicated-key flag per position
+  static_assert(sizeof(L.wcnt) >= B::CAP, "dup flags fit the multisplit rows");
+  constexpr uint32_t HT = 2 * B::CAP, HT_SHIFT = 32 - 12;
+  static_assert(HT == 1u << 12, "hash index bits");
 #pragma unroll
   for (uint32_t i = 0; i < B::ITEMS; i++) {
     const uint32_t p = strip0 + i * 64 + lane;
-    if (p < S) {
-      sk[base + p] = kk[i];
-      sv[base + p] = vv[i];
+    if (p < S) L.k[p] = kk[i];
+  }
+  for (uint32_t j = tid; j < HT; j += B::THREADS) ht[j] = 0xFFFFFFFFu;
+  for (uint32_t j = tid; j < B::CAP / 4; j += B::THREADS) reinterpret_cast<uint32_t*>(df)[j] = 0u;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t i = 0; i < B::ITEMS; i++) {
+    const uint32_t p = strip0 + i * 64 + lane;
+    if (p >= S) continue;
+    uint32_t h = (kk[i] * 0x9E3779B1u) >> HT_SHIFT;
+    for (;;) {  // (S <= CAP = HT / 2: a free entry is always found)
+      const uint32_t o = atomicCAS(&ht[h], 0xFFFFFFFFu, p);
+      if (o == 0xFFFFFFFFu) break;  // first of its key in the bucket
+      if (L.k[o] == kk[i]) {        // seen before: both are duplicated
+        df[p] = 1;
+        df[o] = 1;
+        break;
+      }
+      h = (h + 1) & (HT - 1);
     }
   }
+  __syncthreads();
+  // compact the duplicated elements, keeping the bucket (= arrival) order
+  const uint64_t lt = (1ull << lane) - 1;
+  uint32_t cidx[B::ITEMS], wc = 0, dmask = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < B::ITEMS; i++) {
+    const uint32_t p = strip0 + i * 64 + lane;
+    const bool dup = p < S && df[p];
+    const uint64_t bl = __ballot(dup);
+    cidx[i] = wc + (uint32_t)__popcll(bl & lt);
+    wc += (uint32_t)__popcll(bl);
+    dmask |= dup ? 1u << i : 0u;
+  }
+  if (lane == 0) L.wsum[wave] = wc;
+  __syncthreads();
+  uint32_t wpre = 0, M = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < B::WAVES; w++) {
+    wpre += w < wave ? L.wsum[w] : 0u;
+    M += L.wsum[w];
+  }
+  if (!M) return;  // (uniform) every key of the bucket is seen once
+#pragma unroll
+  for (uint32_t i = 0; i < B::ITEMS; i++) {
+    if (!((dmask >> i) & 1u)) continue;
+    const uint32_t c = wpre + cidx[i];
+    L.k[c] = kk[i];
+    L.v[c] = vv[i];
+    L.h[c] = hh[i];
+  }
+  if (tid == 0) L.base_pos = atomicAdd(sorted_n, M);
+  __syncthreads();
+  const uint32_t base = L.base_pos;
+  if (M <= 64) {
+    // one wave: stable rank of (key, compact index) by comparisons
+    if (wave == 0) {
+      const bool v = lane < M;
+      const uint32_t k = v ? L.k[lane] : 0xFFFFFFFFu, x = v ? L.v[lane] : 0u, y = v ? L.h[lane] : 0u;
+      uint32_t r = 0;
+      for (uint32_t j = 0; j < M; j++) {
+        const uint32_t kj = __shfl(k, j, 64);
+        r += (kj < k || (kj == k && j < lane)) ? 1u : 0u;
+      }
+      if (v) {
+        L.k[r] = k;
+        L.v[r] = x;
+        L.h[r] = y;
+      }
+    }
+    __syncthreads();
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < B::ITEMS; i++) {
+      const uint32_t p = strip0 + i * 64 + lane;
+      kk[i] = p < M ? L.k[p] : 0xFFFFFFFFu;
+      vv[i] = p < M ? L.v[p] : 0u;
+      hh[i] = p < M ? L.h[p] : 0u;
+    }
+    __syncthreads();
+    lds_sort3(L, kk, vv, hh, M);
+  }
+  for (uint32_t p = tid; p < M; p += B::THREADS) {
+    sk[base + p] = L.k[p];
+    sv[base + p] = L.v[p];
+  }
   BK_STAMP(d, 3);
-  bucket_segment<B, true>(L, d, S, base, sk, sh, segsum, rid, run_start, run_end, num_runs, drun);
+  bucket_segment<B, true>(L, d, M, base, sk, sh, segsum, rid, run_start, run_end, num_runs, drun);
   BK_STAMP(d, 5);
 }
 
@@ -2185,14 +2274,15 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
                                                    const uint32_t* __restrict__ run_start,
                                                    uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
                                                    uint32_t* defer_n, const uint32_t* err,
-                                                   const unsigned long long* num_runs, unsigned long long* split) {
+                                                   const unsigned long long* num_runs, unsigned long long* split,
+                                                   const uint32_t* sorted_n) {
   __shared__ uint32_t s_list[CHUNK], s_cnt;
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // k_split's reservations start from the bucket kernels' count
     split[0] = 0;
     split[1] = *num_runs;
   }
   if (*err) return;
-  const uint32_t lo = max(blockIdx.x * CHUNK, 1u), hi = min(blockIdx.x * CHUNK + CHUNK, b.n);
+  const uint32_t lo = max(blockIdx.x * CHUNK, 1u), hi = min(blockIdx.x * CHUNK + CHUNK, *sorted_n);
   if (lo >= hi) return;
   // non-head positions (the second and later descriptors of a run)
   const uint32_t cnt = block_compact(lo, hi, s_list, &s_cnt, [&](uint32_t q) { return skeys[q - 1] == skeys[q]; });
@@ -2842,13 +2932,14 @@ __device__ __attribute__((always_inline)) inline void runs_body(uint32_t blk, Ba
 // local cache on, the first element f with a_f > limit_f makes every element of
 // a LATER request a local-cache hit (Set happens after request q_f's statuses),
 // i.e. a suffix of the run, which therefore never increments.
-__global__ __launch_bounds__(256) void k_fast_over(uint32_t n, SRec rec_s,
+__global__ __launch_bounds__(256) void k_fast_over(const uint32_t* sorted_n, SRec rec_s,
                                                    const uint32_t* __restrict__ segsum,
                                                    const uint32_t* __restrict__ rid,
                                                    const uint32_t* __restrict__ run_flags,
                                                    const uint4* __restrict__ run_state, uint32_t* __restrict__ run_f,
                                                    const uint32_t* err) {
   if (*err) return;
+  const uint32_t n = *sorted_n;
   const uint32_t q = blockIdx.x * 256 + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63;
   bool cand = false;
@@ -2869,7 +2960,7 @@ __global__ __launch_bounds__(256) void k_fast_over(uint32_t n, SRec rec_s,
   }
 }
 
-__device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t blk, uint32_t n, uint32_t n_rules, TableDev t, Params P,
+__device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t blk, const uint32_t* sorted_n, uint32_t n_rules, TableDev t, Params P,
                                                    SRec rec_s, const uint32_t* __restrict__ svals,
                                                    unsigned long long* __restrict__ res,
                                                    const uint32_t* __restrict__ segsum,
@@ -2881,13 +2972,15 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
                                                    const uint32_t* __restrict__ run_f, unsigned long long* stats,
                                                    unsigned long long* stripes, const uint32_t* err,
                                                    const uint32_t* __restrict__ fast_blk) {
-  __shared__ uint32_t s_err, s_fast;
+  __shared__ uint32_t s_err, s_fast, s_n;
   if (threadIdx.x == 0) {
     s_err = *err;
     s_fast = (fast_blk[blk >> 5] >> (blk & 31)) & 1u;
+    s_n = *sorted_n;
   }
   __syncthreads();
   if (s_err || !s_fast) return;  // no RUN_FAST descriptor in this block (k_table's bitmap)
+  const uint32_t n = s_n;  // sorted positions of this batch
   const bool use_lds = n_rules <= LDS_RULES;
   stats_block_begin(use_lds, n_rules);
   StatAcc acc{use_lds, stats};
@@ -3143,13 +3236,14 @@ __global__ __launch_bounds__(256, 8) void k_late(BatchDev b, TableDev t, Params 
                                                  const uint32_t* __restrict__ run_flags,
                                                  const uint4* __restrict__ run_state, const uint32_t* __restrict__ run_f,
                                                  unsigned long long* stats, unsigned long long* stripes, uint32_t* err,
-                                                 uint32_t* errs, int restore, const uint32_t* __restrict__ fast_blk) {
+                                                 uint32_t* errs, int restore, const uint32_t* __restrict__ fast_blk,
+                                                 const uint32_t* sorted_n) {
   if (blockIdx.x < RUNS_GENERAL_LATE_BLOCKS)
     general_body(blockIdx.x, RUNS_GENERAL_LATE_BLOCKS, b, t, P, rec_s, skeys, svals, res, run_start, run_end, defer,
                  defer_n, defer2, defer2_n, grp, lead, gmask, keys0, defer1, defer1_n, stats, stripes, err, errs,
                  restore);
   else if (!restore)
-    fast_emit_body(blockIdx.x - RUNS_GENERAL_LATE_BLOCKS, b.n, b.n_rules, t, P, rec_s, svals, res, segsum, rid,
+    fast_emit_body(blockIdx.x - RUNS_GENERAL_LATE_BLOCKS, sorted_n, b.n_rules, t, P, rec_s, svals, res, segsum, rid,
                    run_start, run_end, run_flags, run_state, run_f, stats, stripes, err, fast_blk);
 }
 
@@ -3337,7 +3431,7 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
   if (ev) (void)hipEventRecord(ev[0], st);
   if (g0)
     k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.keys[0], s.err, s.errs, isolate, s.time_floor, s.defer_n, s.big_n,
-                                  s.work_n, s.run_flags, s.runs64, s.hit_a, s.res);
+                                  s.work_n, s.run_flags, s.runs64, s.hit_a, s.res, s.sorted_n);
   if (ev) (void)hipEventRecord(ev[1], st);
   const uint32_t ptiles = cdiv(b.n, PART_TILE);
   if (b.n)
@@ -3348,7 +3442,7 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
     k_bucket<<<PART_DIGITS, BkSmall::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
                                                              s.keys[1], s.vals[0], s.hits_s, s.segsum, s.rid,
                                                              s.run_start, s.run_end, s.runs64, s.drun, s.big_meta, s.big_n,
-                                                             s.big_work, s.work_n, s.err);
+                                                             s.big_work, s.work_n, s.sorted_n, s.err);
     k_big_count<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
                                                                     s.big_meta, s.big_work, s.work_n, s.big_cnt,
                                                                     s.err);
@@ -3360,7 +3454,8 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
                                                               s.rid, s.run_start, s.run_end, s.runs64, s.drun, s.big_meta,
                                                               s.big_n, s.big_cnt, s.err);
     k_run_check<<<cdiv(b.n, CHUNK), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[1], s.rid, s.run_start,
-                                                s.run_flags, s.defer, s.defer_n, s.err, s.runs64, s.split);
+                                                s.run_flags, s.defer, s.defer_n, s.err, s.runs64, s.split,
+                                                s.sorted_n);
     k_split<<<SPLIT_BLOCKS, 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.vals[0], s.segsum, s.rid, s.run_start,
                                           s.run_end, s.run_flags, s.defer, s.defer_n, s.runs64, s.split, s.drun,
                                           b.n / 2 + BIG_HEAVY * PART_DIGITS, s.grp, s.lead, s.err);
@@ -3391,12 +3486,12 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
                                          s.fast_blk);
     if (ev) (void)hipEventRecord(ev[4], st);
     if (!restore && P.lc_en)
-      k_fast_over<<<g, 256, 0, st>>>(b.n, rs, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
+      k_fast_over<<<g, 256, 0, st>>>(s.sorted_n, rs, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
     k_late<<<RUNS_GENERAL_LATE_BLOCKS + (restore ? 0u : g), 256, lds, st>>>(
         b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer, s.defer_n, s.defer2, s.defer2_n,
         s.grp, s.lead, s.gmask,
         s.keys[0], s.defer1, s.defer1_n, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb,
-        s.errs, restore, s.fast_blk);
+        s.errs, restore, s.fast_blk, s.sorted_n);
     if (!restore) {
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;
       const uint32_t gf = cdiv(nf * RL_NUM_STATS > b.n ? nf * RL_NUM_STATS : b.n, 256);
