@@ -11,7 +11,10 @@ namespace rl {
 
 constexpr uint32_t PART_ITEMS = 16, PART_TILE = 256 * PART_ITEMS;  // k_part: 256 threads x PART_ITEMS
 constexpr uint32_t PART_BITS = 10, PART_DIGITS = 1u << PART_BITS;   // buckets = top key bits
-constexpr uint32_t BIG_BLOCKS = 64;                                 // k_bucket_big workgroups
+#ifndef RL_BIG_BLOCKS
+#define RL_BIG_BLOCKS 64
+#endif
+constexpr uint32_t BIG_BLOCKS = RL_BIG_BLOCKS;                      // k_bucket_big workgroups
 constexpr uint32_t BIG_ITEM_BLOCKS = 256;                           // k_big_count / k_big_place workgroups
 constexpr uint32_t BIG_HEAVY = 4;                                   // hot keys peeled off a large bucket
 

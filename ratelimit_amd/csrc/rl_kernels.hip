@@ -2234,11 +2234,19 @@ __global__ __launch_bounds__(BkBig::THREADS) void k_bucket_big(
 // table / record accesses (the runs of two or more at C1, the keys seen once at
 // C2), spreading them one per lane over the whole grid makes nearly every wave
 // pay a full chain of dependent random loads for one or two active lanes. A
-// block instead scans a CHUNK of positions with coalesced reads, compacts the
+// block instead scans a range of positions with coalesced reads, compacts the
 // active ones into LDS (any order: the items are independent) and works
 // through them with all its lanes.
 // ---------------------------------------------------------------------------
-constexpr uint32_t CHUNK = 1024;
+// k_run_check's positions per block: the sorted order holds only the runs
+// (dedup-first buckets), about half of them non-heads, so a block of 256
+// positions gives each lane about one chain of random reads (1024-position
+// blocks left ~50 busy workgroups at C1, each lane walking several chains:
+// 22 us isolated for ~53k positions).
+#ifndef RL_RC_CHUNK
+#define RL_RC_CHUNK 256
+#endif
+constexpr uint32_t RC_CHUNK = RL_RC_CHUNK;
 
 template <typename Pred>
 __device__ __attribute__((always_inline)) inline uint32_t block_compact(uint32_t lo, uint32_t hi, uint32_t* list,
@@ -2276,13 +2284,13 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
                                                    uint32_t* defer_n, const uint32_t* err,
                                                    const unsigned long long* num_runs, unsigned long long* split,
                                                    const uint32_t* sorted_n) {
-  __shared__ uint32_t s_list[CHUNK], s_cnt;
+  __shared__ uint32_t s_list[RC_CHUNK], s_cnt;
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // k_split's reservations start from the bucket kernels' count
     split[0] = 0;
     split[1] = *num_runs;
   }
   if (*err) return;
-  const uint32_t lo = max(blockIdx.x * CHUNK, 1u), hi = min(blockIdx.x * CHUNK + CHUNK, *sorted_n);
+  const uint32_t lo = max(blockIdx.x * RC_CHUNK, 1u), hi = min(blockIdx.x * RC_CHUNK + RC_CHUNK, *sorted_n);
   if (lo >= hi) return;
   // non-head positions (the second and later descriptors of a run)
   const uint32_t cnt = block_compact(lo, hi, s_list, &s_cnt, [&](uint32_t q) { return skeys[q - 1] == skeys[q]; });
@@ -3453,7 +3461,7 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
                                                               s.keys[1], s.vals[0], s.hits_s, s.hit_t, s.segsum,
                                                               s.rid, s.run_start, s.run_end, s.runs64, s.drun, s.big_meta,
                                                               s.big_n, s.big_cnt, s.err);
-    k_run_check<<<cdiv(b.n, CHUNK), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[1], s.rid, s.run_start,
+    k_run_check<<<cdiv(b.n, RC_CHUNK), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[1], s.rid, s.run_start,
                                                 s.run_flags, s.defer, s.defer_n, s.err, s.runs64, s.split,
                                                 s.sorted_n);
     k_split<<<SPLIT_BLOCKS, 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.vals[0], s.segsum, s.rid, s.run_start,
