@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--one-device", action="store_true", help="every rank uses cuda:0 (rehearsal only)")
     ap.add_argument("--serial", action="store_true",
                     help="submit every batch on one stream, unpipelined (isolated per-kernel times for profiling)")
+    ap.add_argument("--shards", type=int, default=1,
+                    help="S > 1 (N = 1): one ctx hash-sharding its table over S shards (rl_config.n_shards) on this "
+                         "GPU: host batches are cut into one slice per shard, each routed to its owners and back")
     ap.add_argument("--loopback", type=int, default=0,
                     help="W > 0: W ranks of the library router as threads of this process, all on cuda:0, "
                          "exchanging through the in-process loopback transport (the W-rank protocol on one GPU)")
@@ -138,8 +141,14 @@ def main():
     if args.serial:  # isolated kernel timings: each batch's stages serially on the bench stream
         os.environ["RL_DEBUG_SERIAL"] = "1"
     # a routed owner attributes stats per source rank: world x n_rules rule slots
-    be = Backend(0.8, False, table_slots=slots, max_batch=cap, max_rules=max(8, 2 * world), device=local,
-                 hash_seed=seed, max_stem_bytes=64 * cap)
+    if args.shards > 1 and routed:
+        raise SystemExit("--shards is a single-process option (N = 1, no --route)")
+    if args.shards > 1 and not seed:
+        import secrets
+        seed = secrets.randbits(62) + 1
+    sh = dict(n_shards=args.shards, shard_devices=[local] * args.shards) if args.shards > 1 else {}
+    be = Backend(0.8, False, table_slots=slots, max_batch=cap, max_rules=max(8, 2 * world * args.shards),
+                 device=local, hash_seed=seed, max_stem_bytes=64 * cap, **sh)
     now0 = W.NOW0
     py_route = routed and (args.route_impl == "python" or args.dist_backend == "gloo")
     if routed and not py_route:
@@ -251,7 +260,7 @@ def main():
     stage_ms, nb = be.profile_read()
     be.profile(False)
     stage_avg = {k: v / max(nb, 1) for k, v in stage_ms.items()}
-    n_unique = float(np.mean(uniq)) if world == 1 else None  # (routed: each owner's share is not tracked)
+    n_unique = float(np.mean(uniq)) if world == 1 and args.shards == 1 else None  # (routed: owners not tracked)
     n_owner = float(np.mean(recv)) if recv else float(n)
     if routed:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
@@ -328,7 +337,8 @@ def main():
                    "parallelism": ("hash-sharded table x%d, %s" % (
                                       world, "RCCL send/recv routing inside the library" if not py_route else
                                       "all_to_all routing from Python (%s)" % args.dist_backend)) if routed else
-                                  "single GPU"},
+                                  ("one ctx, table hash-sharded over %d shards on this GPU (loopback routing)"
+                                   % args.shards) if args.shards > 1 else "single GPU"},
         "p50_batch_ms": float(np.percentile(lat, 50)), "p99_batch_ms": p99, "pcie_fed": pcie,
         "roofline": roofline, "cpu_baseline": cpu, "fill_s": round(t_fill, 2),
         **({"route_host_ms_per_step": route_host} if py_route else {}),

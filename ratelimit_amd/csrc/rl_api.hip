@@ -6,27 +6,33 @@
 // With rl_config.n_shards > 1 the table is hash-sharded over the shards'
 // devices inside this one process (the reference's single service process
 // scaled out over a Redis cluster, src/redis/driver_impl.go:108-126; here the
-// cgo adapter still drives one ctx), and every batch is routed:
+// cgo adapter still drives one ctx). Each shard then also has a router
+// (rl_comm.hip) and a worker thread; the routers form an in-process loopback
+// world, so a multi-shard ctx runs exactly the protocol of one process per
+// GPU (partition by owner, counts, records and stems, owner pipelines,
+// results and stats, scatter), each shard on its own thread:
 //
-//   shard 0's device (the source): partition the batch by owner (stem hash)
-//     into wire records + stem bytes, on the forward stream;
-//   host: read the per-owner counts (the one wait per batch: the partition
-//     only, never the owners' pipelines);
-//   forward stream: copy each owner's chunk to its device (xGMI peer copies;
-//     a plain device copy when shards share a device);
-//   each owner: the normal pipelined DoLimit over its chunk (eng_route_owner);
-//   return stream: copy the packed results and stats deltas back, scatter the
-//     results to arrival order, sum the stats.
+//   host batches (rl_do_limit, rl_do_limit_host_async): the batch is cut into
+//     one request-aligned slice per shard; each shard's router copies its
+//     slice over ITS device's PCIe link, partitions it and exchanges with the
+//     others over xGMI (peer copies); the answers cross back per slice, and
+//     the per-shard stats deltas are summed on the host;
+//   device batches (rl_do_limit_async, memory of shard 0's GPU): shard 0's
+//     router takes the whole batch and the others submit empty slices.
 //
-// Batch t's partition and copies run while earlier batches' owner pipelines
-// still hold the tables; RSLOTS batches may be in flight.
+// The caller's thread only hands each batch to the workers and waits until
+// they have ENQUEUED it (never for the GPU); rl_synchronize completes the
+// in-flight batches (a collective step of the routers).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ratelimit_hip.h"
@@ -40,21 +46,28 @@ using namespace rl;
 namespace {
 
 constexpr uint32_t MAX_LOCAL_SHARDS = 16;
-constexpr uint32_t RSLOTS = 3;
 
-struct RouteSlot {
-  Wire* send_rec = nullptr;              // dev0: wire records in owner order
-  uint8_t* send_stem = nullptr;          // dev0: their stems
-  uint32_t* perm = nullptr;              // dev0: record -> batch index
-  unsigned long long* counts = nullptr;  // dev0: [2 x n] records / stem bytes per owner
-  unsigned long long* back = nullptr;    // dev0: packed results, record order
-  unsigned long long* stats_stage = nullptr;  // dev0: [n][max_rules x RL_NUM_STATS] owners' deltas
-  Wire* recv_rec[MAX_LOCAL_SHARDS] = {};      // owner devices: received records
-  uint8_t* recv_stem[MAX_LOCAL_SHARDS] = {};
-  unsigned long long* ostats[MAX_LOCAL_SHARDS] = {};
-  uint32_t k[MAX_LOCAL_SHARDS] = {};     // owner engine buffer of this slot's batch
-  hipEvent_t packed = nullptr;           // forward stream: partition + counts copy done
-  hipEvent_t done = nullptr;             // return stream: results and stats complete
+// One shard's worker: runs its router's collective steps on its own thread.
+struct ShardWorker {
+  enum Job { IDLE, BATCH, SYNC, EXIT };
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  Job job = IDLE;
+  rl_batch in{};
+  rl_result out{};
+  CommIO io{};
+  hipStream_t caller = nullptr;
+  int rc = RL_OK;
+};
+
+// Stats of a host batch in flight: each shard's deltas land in a pinned ring
+// entry (slot = the routers' slot of the batch); they are summed into the
+// caller's out->stats once the batch is complete.
+struct PendingStats {
+  bool used = false;
+  uint64_t* out = nullptr;
+  uint32_t m = 0;
 };
 
 }  // namespace
@@ -65,20 +78,16 @@ struct rl_ctx {
   Engine* e[MAX_LOCAL_SHARDS] = {};
   CommRouter* comm = nullptr;  // rl_comm_init: multi-process routing (single-shard ctx)
   std::string last_error;
-  // router (n > 1), on shard 0's device
-  int dev0 = 0;
-  hipStream_t fwd = nullptr, ret = nullptr;
-  hipEvent_t fwd_ready = nullptr, in_ready = nullptr;
-  RouteSlot slot[RSLOTS];
-  uint32_t next_slot = 0;
-  unsigned long long* h_counts = nullptr;  // pinned [RSLOTS][2 x MAX_LOCAL_SHARDS]
-  // staging for the host-buffer entry point (dev0)
-  uint8_t* d_stem = nullptr;
-  uint32_t *d_off = nullptr, *d_req = nullptr, *d_limit = nullptr, *d_hits = nullptr, *d_rule = nullptr;
-  int64_t* d_now = nullptr;
-  uint8_t *d_unit = nullptr, *d_flags = nullptr, *d_code = nullptr, *d_status = nullptr;
-  uint32_t *d_rem = nullptr, *d_reset = nullptr;
-  unsigned long long* d_stats = nullptr;
+  // shards of this ctx (n > 1)
+  CommRouter* r[MAX_LOCAL_SHARDS] = {};
+  ShardWorker w[MAX_LOCAL_SHARDS];
+  std::mutex done_mu;
+  std::condition_variable done_cv;
+  uint32_t busy = 0;
+  uint32_t batch_no = 0;                      // batches submitted (router slot = batch_no % slots)
+  std::vector<PendingStats> pend;             // [slots]
+  unsigned long long* stats_ring = nullptr;   // pinned [slots][n][stats_cap]
+  uint32_t stats_cap = 0;
 };
 
 namespace {
@@ -104,154 +113,105 @@ int from_engine(rl_ctx* c, Engine* e, int rc) {
       return fail((c), RL_E_HIP, std::string("gpu: ") + #expr + ": " + hipGetErrorString(_e));  \
   } while (0)
 
-template <typename T>
-hipError_t dalloc(T** p, size_t count) {
-  return hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T));
-}
-
 uint32_t owner_of_host(uint64_t h, uint32_t n) { return (uint32_t)(((uint64_t)(uint32_t)h * n) >> 32); }
 
-void free_router(rl_ctx* c) {
-  for (uint32_t s = 0; s < RSLOTS; s++) {
-    RouteSlot& S = c->slot[s];
-    void* dev0_bufs[] = {S.send_rec, S.send_stem, S.perm, S.counts, S.back, S.stats_stage};
-    (void)hipSetDevice(c->dev0);
-    for (void* p : dev0_bufs)
-      if (p) (void)hipFree(p);
-    for (uint32_t j = 0; j < c->n; j++) {
-      (void)hipSetDevice(c->cfg.shard_device[j]);
-      for (void* p : {(void*)S.recv_rec[j], (void*)S.recv_stem[j], (void*)S.ostats[j]})
-        if (p) (void)hipFree(p);
+void worker_main(rl_ctx* c, uint32_t j) {
+  (void)hipSetDevice(c->cfg.shard_device[j]);
+  ShardWorker& w = c->w[j];
+  for (;;) {
+    ShardWorker::Job job;
+    {
+      std::unique_lock<std::mutex> l(w.mu);
+      w.cv.wait(l, [&] { return w.job != ShardWorker::IDLE; });
+      job = w.job;
     }
-    (void)hipSetDevice(c->dev0);
-    if (S.packed) (void)hipEventDestroy(S.packed);
-    if (S.done) (void)hipEventDestroy(S.done);
+    if (job == ShardWorker::EXIT) return;
+    int rc = RL_OK;
+    if (job == ShardWorker::BATCH) {
+      rc = comm_do_limit(c->r[j], c->e[j], &w.in, &w.out, w.caller, &w.io);
+    } else {  // SYNC: the pending batch (collective), the router's streams, then the engine's error words
+      rc = comm_synchronize(c->r[j], c->e[j]);
+      const int re = eng_synchronize(c->e[j]);
+      if (!rc) rc = re;
+    }
+    {
+      std::lock_guard<std::mutex> l(w.mu);
+      w.rc = rc;
+      w.job = ShardWorker::IDLE;
+    }
+    {
+      std::lock_guard<std::mutex> l(c->done_mu);
+      c->busy--;
+    }
+    c->done_cv.notify_all();
   }
-  (void)hipSetDevice(c->dev0);
-  void* bufs[] = {c->d_stem, c->d_off, c->d_req, c->d_limit, c->d_hits, c->d_rule, c->d_now, c->d_unit,
-                  c->d_flags, c->d_code, c->d_status, c->d_rem, c->d_reset, c->d_stats};
-  for (void* p : bufs)
-    if (p) (void)hipFree(p);
-  if (c->h_counts) (void)hipHostFree(c->h_counts);
-  for (hipEvent_t ev : {c->fwd_ready, c->in_ready})
-    if (ev) (void)hipEventDestroy(ev);
-  for (hipStream_t st : {c->fwd, c->ret})
-    if (st) (void)hipStreamDestroy(st);
 }
 
-bool alloc_router(rl_ctx* c) {
-  const rl_config& g = c->cfg;
-  const uint32_t n = g.max_batch, sb = g.max_stem_bytes, m = g.max_rules * RL_NUM_STATS;
-  // every pair of distinct shard devices talks directly over xGMI
-  for (uint32_t i = 0; i < c->n; i++)
-    for (uint32_t j = 0; j < c->n; j++) {
-      const int di = g.shard_device[i], dj = g.shard_device[j];
-      if (di == dj) continue;
-      int can = 0;
-      if (hipDeviceCanAccessPeer(&can, di, dj) == hipSuccess && can) {
-        (void)hipSetDevice(di);
-        const hipError_t e = hipDeviceEnablePeerAccess(dj, 0);
-        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return false;
-        (void)hipGetLastError();
-      }
-    }
-  if (hipSetDevice(c->dev0) != hipSuccess) return false;
-  bool ok = hipStreamCreateWithFlags(&c->fwd, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->ret, hipStreamNonBlocking) == hipSuccess &&
-            hipEventCreateWithFlags(&c->fwd_ready, hipEventDisableTiming) == hipSuccess &&
-            hipEventCreateWithFlags(&c->in_ready, hipEventDisableTiming) == hipSuccess &&
-            hipHostMalloc((void**)&c->h_counts, RSLOTS * 2 * MAX_LOCAL_SHARDS * 8) == hipSuccess;
-  for (uint32_t s = 0; s < RSLOTS && ok; s++) {
-    RouteSlot& S = c->slot[s];
-    ok = dalloc(&S.send_rec, n) == hipSuccess && dalloc(&S.send_stem, (size_t)sb + 64) == hipSuccess &&
-         dalloc(&S.perm, n) == hipSuccess && dalloc(&S.counts, 2 * RL_MAX_SHARDS) == hipSuccess &&
-         dalloc(&S.back, n) == hipSuccess && dalloc(&S.stats_stage, (size_t)c->n * m) == hipSuccess &&
-         hipEventCreateWithFlags(&S.packed, hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&S.done, hipEventDisableTiming) == hipSuccess &&
-         hipEventRecord(S.done, c->ret) == hipSuccess;
-    for (uint32_t j = 0; j < c->n && ok; j++) {
-      ok = hipSetDevice(g.shard_device[j]) == hipSuccess && dalloc(&S.recv_rec[j], n) == hipSuccess &&
-           dalloc(&S.recv_stem[j], (size_t)sb + 64) == hipSuccess && dalloc(&S.ostats[j], m) == hipSuccess;
-    }
-    ok = ok && hipSetDevice(c->dev0) == hipSuccess;
+// Hand every shard its job (set up by the caller) and wait until all have
+// returned from it; the first failing shard's status and message.
+int run_shards(rl_ctx* c, ShardWorker::Job job) {
+  {
+    std::lock_guard<std::mutex> l(c->done_mu);
+    c->busy = c->n;
   }
-  ok = ok && dalloc(&c->d_stem, (size_t)sb + 64) == hipSuccess && dalloc(&c->d_off, (size_t)n + 1) == hipSuccess &&
-       dalloc(&c->d_req, n) == hipSuccess && dalloc(&c->d_limit, n) == hipSuccess &&
-       dalloc(&c->d_hits, n) == hipSuccess && dalloc(&c->d_rule, n) == hipSuccess &&
-       dalloc(&c->d_now, g.max_requests) == hipSuccess && dalloc(&c->d_unit, n) == hipSuccess &&
-       dalloc(&c->d_flags, n) == hipSuccess && dalloc(&c->d_code, n) == hipSuccess &&
-       dalloc(&c->d_status, n) == hipSuccess && dalloc(&c->d_rem, n) == hipSuccess &&
-       dalloc(&c->d_reset, n) == hipSuccess && dalloc(&c->d_stats, m) == hipSuccess;
-  ok = ok && hipStreamSynchronize(c->ret) == hipSuccess;
-  return ok;
+  for (uint32_t j = 0; j < c->n; j++) {
+    {
+      std::lock_guard<std::mutex> l(c->w[j].mu);
+      c->w[j].job = job;
+    }
+    c->w[j].cv.notify_one();
+  }
+  {
+    std::unique_lock<std::mutex> l(c->done_mu);
+    c->done_cv.wait(l, [&] { return c->busy == 0; });
+  }
+  for (uint32_t j = 0; j < c->n; j++)
+    if (c->w[j].rc) return fail(c, c->w[j].rc, eng_last_error(c->e[j]));
+  return RL_OK;
 }
 
-// One routed batch (device arrays on dev0; see the file comment).
-int routed_async(rl_ctx* c, const rl_batch* in, rl_result* out, hipStream_t caller) {
-  const uint32_t n = in->n, N = c->n;
-  if (n > c->cfg.max_batch || in->n_requests > c->cfg.max_requests || in->n_rules > c->cfg.max_rules)
-    return fail(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_rules");
-  const uint32_t s = c->next_slot;
-  c->next_slot = (s + 1) % RSLOTS;
-  RouteSlot& S = c->slot[s];
-  Engine* e0 = c->e[0];
-  API_HIP(c, hipSetDevice(c->dev0));
-  API_HIP(c, hipStreamWaitEvent(c->fwd, S.done, 0));  // the slot's previous batch is complete
-  if (caller && hipStreamQuery(caller) == hipErrorNotReady) {  // the inputs' producer (still running)
-    API_HIP(c, hipEventRecord(c->in_ready, caller));
-    API_HIP(c, hipStreamWaitEvent(c->fwd, c->in_ready, 0));
+void stop_shards(rl_ctx* c) {
+  for (uint32_t j = 0; j < c->n; j++) {
+    if (!c->w[j].th.joinable()) continue;
+    {
+      std::lock_guard<std::mutex> l(c->w[j].mu);
+      c->w[j].job = ShardWorker::EXIT;
+    }
+    c->w[j].cv.notify_one();
+    c->w[j].th.join();
   }
-  int rc = eng_route_pack(e0, in, N, 0, S.send_rec, S.send_stem, S.perm, (uint64_t*)S.counts, c->fwd);
-  if (rc) return from_engine(c, e0, rc);
-  unsigned long long* hc = c->h_counts + (size_t)s * 2 * MAX_LOCAL_SHARDS;
-  API_HIP(c, hipMemcpyAsync(hc, S.counts, 2ull * N * 8, hipMemcpyDeviceToHost, c->fwd));
-  API_HIP(c, hipEventRecord(S.packed, c->fwd));
-  API_HIP(c, hipEventSynchronize(S.packed));  // the one host wait: this batch's partition
-  uint64_t roff[MAX_LOCAL_SHARDS], soff[MAX_LOCAL_SHARDS], acc_r = 0, acc_s = 0;
-  for (uint32_t j = 0; j < N; j++) {
-    roff[j] = acc_r;
-    soff[j] = acc_s;
-    acc_r += hc[2 * j];
-    acc_s += hc[2 * j + 1];
-  }
-  if (acc_r != (n ? n : 0) && acc_r != 0) return fail(c, RL_E_INTERNAL, "gpu: routing counts do not add up");
-  for (uint32_t j = 0; j < N; j++) {
-    const int dj = c->cfg.shard_device[j];
-    if (hc[2 * j])
-      API_HIP(c, hipMemcpyPeerAsync(S.recv_rec[j], dj, S.send_rec + roff[j], c->dev0, hc[2 * j] * sizeof(Wire),
-                                    c->fwd));
-    if (hc[2 * j + 1])
-      API_HIP(c, hipMemcpyPeerAsync(S.recv_stem[j], dj, S.send_stem + soff[j], c->dev0, hc[2 * j + 1], c->fwd));
-  }
-  API_HIP(c, hipEventRecord(c->fwd_ready, c->fwd));
-  const int isolate = out->status ? 1 : 0;
-  const uint64_t zero = 0;
-  for (uint32_t j = 0; j < N; j++) {
-    rc = eng_route_owner(c->e[j], (uint32_t)hc[2 * j], S.recv_rec[j], S.recv_stem[j], hc[2 * j + 1], &zero, 1,
-                         in->n_rules, 0, S.ostats[j], isolate, c->fwd_ready, &S.k[j]);
+}
+
+// The summed stats of the host batch that used ring entry s (its shards'
+// slots are complete once their done events fired).
+int finalize_stats(rl_ctx* c, uint32_t s, bool keep) {
+  PendingStats& P = c->pend[s];
+  if (!P.used) return RL_OK;
+  P.used = false;
+  for (uint32_t j = 0; j < c->n; j++) {
+    const int rc = comm_wait_slot(c->r[j], c->e[j], s);
     if (rc) return from_engine(c, c->e[j], rc);
   }
-  API_HIP(c, hipSetDevice(c->dev0));
-  const uint32_t m = in->n_rules * RL_NUM_STATS;
-  for (uint32_t j = 0; j < N; j++) {
-    Engine* ej = c->e[j];
-    const uint32_t k = S.k[j];
-    const int dj = c->cfg.shard_device[j];
-    API_HIP(c, hipStreamWaitEvent(c->ret, ej->b_done[k], 0));
-    if (hc[2 * j])
-      API_HIP(c, hipMemcpyPeerAsync(S.back + roff[j], c->dev0, ej->s[k].res, dj, hc[2 * j] * 8, c->ret));
-    if (m) API_HIP(c, hipMemcpyPeerAsync(S.stats_stage + (size_t)j * m, c->dev0, S.ostats[j], dj, (size_t)m * 8, c->ret));
-    API_HIP(c, hipEventRecord(ej->consumed[k], c->ret));
+  if (!keep || !P.out) return RL_OK;
+  for (uint32_t i = 0; i < P.m; i++) {
+    unsigned long long v = 0;
+    for (uint32_t j = 0; j < c->n; j++) v += c->stats_ring[((size_t)s * c->n + j) * c->stats_cap + i];
+    P.out[i] = v;
   }
-  OutDev o{out->code, out->limit_remaining, out->reset_s, (unsigned long long*)out->stats, out->status};
-  launch_route_scatter(S.perm, S.back, n, o, c->ret);
-  if (m && out->stats) launch_stats_sum(S.stats_stage, N, m, (unsigned long long*)out->stats, c->ret);
-  API_HIP(c, hipGetLastError());
-  API_HIP(c, hipEventRecord(S.done, c->ret));  // (outputs: read after rl_synchronize)
   return RL_OK;
 }
 
 int synchronize_all(rl_ctx* c) {
+  if (c->n > 1) {
+    const int rc = run_shards(c, ShardWorker::SYNC);
+    const std::string msg = c->last_error;
+    for (uint32_t s = 0; s < c->pend.size(); s++) {
+      const int fr = finalize_stats(c, s, rc == RL_OK);
+      if (fr && !rc) return fr;
+    }
+    if (rc) c->last_error = msg;
+    return rc;
+  }
   int comm_rc = RL_OK;
   std::string comm_msg;
   if (c->comm) {  // (collective on a routed ctx: it completes the pending batch)
@@ -264,32 +224,89 @@ int synchronize_all(rl_ctx* c) {
     (void)eng_synchronize(c->e[0]);
     return eng_fail(c->e[0], comm_rc, comm_msg);
   }
-  if (c->n > 1) {
-    API_HIP(c, hipSetDevice(c->dev0));
-    API_HIP(c, hipStreamSynchronize(c->fwd));
-    API_HIP(c, hipStreamSynchronize(c->ret));
-  }
-  int first = RL_OK;
-  for (uint32_t j = 0; j < c->n; j++) {
-    const int rc = from_engine(c, c->e[j], eng_synchronize(c->e[j]));
-    if (rc && !first) first = rc;
-  }
-  if (first && c->n > 1) {  // keep the first failing shard's message
-    for (uint32_t j = 0; j < c->n; j++)
-      if (*eng_last_error(c->e[j])) {
-        c->last_error = eng_last_error(c->e[j]);
-        break;
-      }
-  }
-  return first;
+  return eng_synchronize(c->e[0]);
 }
 
-constexpr uint64_t MSNAP_MAGIC = 0x31304853414e534cull;  // "LSNASH01": one image per shard
+// One batch through the shards: host (slices over every shard's link) or
+// device (memory of shard 0's GPU: shard 0 takes it whole).
+int shards_submit(rl_ctx* c, const rl_batch* in, rl_result* out, bool host, hipStream_t caller) {
+  const uint32_t N = c->n, n = in->n, nq = in->n_requests;
+  const uint32_t slots = (uint32_t)c->pend.size(), s = c->batch_no % slots;
+  // the batch that used this slot of the routers is complete: its stats first
+  int rc = finalize_stats(c, s, true);
+  if (rc) return rc;
+  const uint32_t m = in->n_rules * RL_NUM_STATS;
+  if (host && m > c->stats_cap) {  // a larger stats ring: every pending batch finalized first
+    for (uint32_t k = 0; k < slots; k++)
+      if ((rc = finalize_stats(c, k, true))) return rc;
+    if (c->stats_ring) (void)hipHostFree(c->stats_ring);
+    c->stats_ring = nullptr;
+    c->stats_cap = 0;
+    API_HIP(c, hipHostMalloc((void**)&c->stats_ring, (size_t)slots * N * m * 8));
+    c->stats_cap = m;
+  }
+  // request-aligned cuts of about n / N descriptors
+  uint32_t d[MAX_LOCAL_SHARDS + 1], q[MAX_LOCAL_SHARDS + 1];
+  d[0] = 0;
+  q[0] = 0;
+  d[N] = n;
+  q[N] = nq;
+  for (uint32_t j = 1; j < N; j++) {
+    uint32_t x = host ? (uint32_t)((uint64_t)n * j / N) : n;
+    if (x < d[j - 1]) x = d[j - 1];
+    while (x > 0 && x < n && in->req_idx[x] == in->req_idx[x - 1]) x++;
+    d[j] = x;
+    q[j] = x < n ? std::min(in->req_idx[x], nq) : nq;
+    if (q[j] < q[j - 1]) q[j] = q[j - 1];
+  }
+  for (uint32_t j = 0; j < N; j++) {
+    ShardWorker& w = c->w[j];
+    w.caller = j == 0 ? caller : nullptr;
+    w.io = CommIO{};
+    w.in = *in;
+    w.out = rl_result{};
+    if (host) {
+      const uint32_t a = d[j], b = d[j + 1];
+      w.in.n = b - a;
+      w.in.n_requests = q[j + 1];  // (absolute: the slice's first request is q[j])
+      w.in.stem_off = in->stem_off + a;
+      w.in.req_idx = in->req_idx + a;
+      w.in.unit = in->unit + a;
+      w.in.flags = in->flags + a;
+      w.in.limit = in->limit + a;
+      w.in.hits = in->hits + a;
+      w.in.rule_id = in->rule_id + a;
+      w.out.code = out->code ? out->code + a : nullptr;
+      w.out.limit_remaining = out->limit_remaining ? out->limit_remaining + a : nullptr;
+      w.out.reset_s = out->reset_s ? out->reset_s + a : nullptr;
+      w.out.status = out->status ? out->status + a : nullptr;
+      w.io.host = true;
+      w.io.da = a;
+      w.io.qa = q[j];
+      w.io.stats_host = m ? c->stats_ring + ((size_t)s * N + j) * c->stats_cap : nullptr;
+    } else if (j == 0) {
+      w.out = *out;
+    } else {  // an empty slice (the exchange is collective)
+      w.in = rl_batch{};
+      w.in.n_rules = in->n_rules;
+    }
+  }
+  c->batch_no++;
+  rc = run_shards(c, ShardWorker::BATCH);
+  if (rc) return rc;
+  if (host) {
+    c->pend[s].used = true;
+    c->pend[s].out = out->stats;
+    c->pend[s].m = out->stats ? m : 0;
+  }
+  return RL_OK;
+}
 
-// Calls that read or change the table order after every submitted batch: on a
-// multi-shard or routed ctx the batches still in the router first complete
-// (on a routed ctx this makes the call collective, like rl_synchronize).
+// Settle a multi-shard or routed ctx before a call that reads or changes the
+// table (on a routed ctx this makes the call collective, like rl_synchronize).
 int settle(rl_ctx* c) { return (c->comm || c->n > 1) ? synchronize_all(c) : RL_OK; }
+
+constexpr uint64_t MSNAP_MAGIC = 0x31304853414e534cull;  // "LSNASH01": one image per shard
 
 }  // namespace
 
@@ -334,7 +351,6 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   if (!cfg.max_stem_bytes) cfg.max_stem_bytes = 128u * cfg.max_batch;
   c->n = n;
   c->cfg = cfg;
-  c->dev0 = cfg.shard_device[0];
   for (uint32_t j = 0; j < n; j++) {
     rl_config ec = cfg;
     ec.n_shards = 1;
@@ -349,10 +365,36 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   c->cfg = c->e[0]->cfg;
   c->cfg.n_shards = n;
   for (uint32_t j = 0; j < MAX_LOCAL_SHARDS; j++) c->cfg.shard_device[j] = cfg.shard_device[j];
-  if (!alloc_router(c)) {
+  // every pair of distinct shard devices talks directly over xGMI
+  for (uint32_t i = 0; i < n; i++)
+    for (uint32_t j = 0; j < n; j++) {
+      const int di = cfg.shard_device[i], dj = cfg.shard_device[j];
+      int can = 0;
+      if (di == dj || hipDeviceCanAccessPeer(&can, di, dj) != hipSuccess || !can) continue;
+      (void)hipSetDevice(di);
+      const hipError_t e = hipDeviceEnablePeerAccess(dj, 0);
+      (void)hipGetLastError();
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+        rl_destroy(c);
+        return bad("gpu: peer access between shard devices failed");
+      }
+    }
+  // the shards' routers: one in-process loopback world
+  uint8_t id[RL_COMM_ID_BYTES];
+  std::string cerr;
+  if (comm_loopback_id(id, &cerr)) {
     rl_destroy(c);
-    return bad("gpu: router allocation failed (peer access or device memory)");
+    return bad(cerr);
   }
+  for (uint32_t j = 0; j < n; j++) {
+    c->r[j] = comm_create(c->e[j], n, j, id, &cerr);
+    if (!c->r[j]) {
+      rl_destroy(c);
+      return bad(cerr);
+    }
+  }
+  c->pend.assign(comm_slots(), PendingStats{});
+  for (uint32_t j = 0; j < n; j++) c->w[j].th = std::thread(worker_main, c, j);
   return c;
 }
 
@@ -360,10 +402,13 @@ void rl_destroy(rl_ctx* c) {
   if (!c) return;
   if (c->comm) comm_destroy(c->comm);
   if (c->n > 1) {
-    (void)hipSetDevice(c->dev0);
-    if (c->fwd) (void)hipStreamSynchronize(c->fwd);
-    if (c->ret) (void)hipStreamSynchronize(c->ret);
-    free_router(c);
+    bool live = true;
+    for (uint32_t j = 0; j < c->n; j++) live = live && c->w[j].th.joinable();
+    if (live) (void)synchronize_all(c);  // (the last batches complete on every shard together)
+    stop_shards(c);
+    for (uint32_t j = 0; j < c->n; j++)
+      if (c->r[j]) comm_destroy(c->r[j]);
+    if (c->stats_ring) (void)hipHostFree(c->stats_ring);
   }
   for (uint32_t j = 0; j < c->n; j++)
     if (c->e[j]) eng_destroy(c->e[j]);
@@ -374,62 +419,37 @@ int rl_do_limit_async(rl_ctx* c, const rl_batch* in, rl_result* out, void* strea
   if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
   if (c->n == 1) return eng_do_limit_async(c->e[0], in, out, stream);
   if ((uintptr_t)in->stem_bytes & 3u) return fail(c, RL_E_INVALID, "gpu: stem_bytes must be 4-byte aligned");
-  return routed_async(c, in, out, (hipStream_t)stream);
+  return shards_submit(c, in, out, false, (hipStream_t)stream);
 }
 
-int rl_do_limit_host_async(rl_ctx* c, const rl_batch* in, rl_result* out) {
-  if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
-  if (c->n > 1) return fail(c, RL_E_INVALID, "gpu: rl_do_limit_host_async runs on a single-shard ctx");
-  return eng_do_limit_host_async(c->e[0], in, out);
-}
-
-int rl_do_limit(rl_ctx* c, const rl_batch* in, rl_result* out) {
-  if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
-  if (c->n == 1) return eng_do_limit(c->e[0], in, out);
+// A host batch for the shards: the checks of the single-table path, on the
+// whole batch (a batch is taken by every shard or by none).
+int check_host_batch(rl_ctx* c, const rl_batch* in, const rl_result* out) {
   const uint32_t n = in->n, nq = in->n_requests;
+  if (n && (!in->stem_off || !in->req_idx || !out->code || !out->limit_remaining || !out->reset_s))
+    return fail(c, RL_E_INVALID, "gpu: null argument");
   const uint64_t nb = n ? in->stem_off[n] : 0;
   if (n > c->cfg.max_batch || nq > c->cfg.max_requests || in->n_rules > c->cfg.max_rules ||
       nb > c->cfg.max_stem_bytes)
     return fail(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_rules/max_stem_bytes");
   if (n && !nq) return fail(c, RL_E_INVALID, "gpu: descriptors without requests");
-  API_HIP(c, hipSetDevice(c->dev0));
-  hipStream_t st = c->fwd;
-  API_HIP(c, hipStreamWaitEvent(st, c->slot[(c->next_slot + RSLOTS - 1) % RSLOTS].done, 0));  // staging is free
-  if (nb) API_HIP(c, hipMemcpyAsync(c->d_stem, in->stem_bytes, nb, hipMemcpyHostToDevice, st));
-  API_HIP(c, hipMemcpyAsync(c->d_off, in->stem_off, (n + 1) * 4ull, hipMemcpyHostToDevice, st));
-  if (nq) API_HIP(c, hipMemcpyAsync(c->d_now, in->now, nq * 8ull, hipMemcpyHostToDevice, st));
-  if (n) {
-    API_HIP(c, hipMemcpyAsync(c->d_req, in->req_idx, n * 4ull, hipMemcpyHostToDevice, st));
-    API_HIP(c, hipMemcpyAsync(c->d_unit, in->unit, n, hipMemcpyHostToDevice, st));
-    API_HIP(c, hipMemcpyAsync(c->d_flags, in->flags, n, hipMemcpyHostToDevice, st));
-    API_HIP(c, hipMemcpyAsync(c->d_limit, in->limit, n * 4ull, hipMemcpyHostToDevice, st));
-    API_HIP(c, hipMemcpyAsync(c->d_hits, in->hits, n * 4ull, hipMemcpyHostToDevice, st));
-    API_HIP(c, hipMemcpyAsync(c->d_rule, in->rule_id, n * 4ull, hipMemcpyHostToDevice, st));
-  }
-  rl_batch d = *in;
-  d.stem_bytes = c->d_stem;
-  d.stem_off = c->d_off;
-  d.now = c->d_now;
-  d.req_idx = c->d_req;
-  d.unit = c->d_unit;
-  d.flags = c->d_flags;
-  d.limit = c->d_limit;
-  d.hits = c->d_hits;
-  d.rule_id = c->d_rule;
-  rl_result r{c->d_code, c->d_rem, c->d_reset, (uint64_t*)c->d_stats, out->status ? c->d_status : nullptr};
-  int rc = routed_async(c, &d, &r, nullptr);
-  if (rc) return rc;
-  hipStream_t rs = c->ret;
-  if (n) {
-    API_HIP(c, hipMemcpyAsync(out->code, c->d_code, n, hipMemcpyDeviceToHost, rs));
-    API_HIP(c, hipMemcpyAsync(out->limit_remaining, c->d_rem, n * 4ull, hipMemcpyDeviceToHost, rs));
-    API_HIP(c, hipMemcpyAsync(out->reset_s, c->d_reset, n * 4ull, hipMemcpyDeviceToHost, rs));
-    if (out->status) API_HIP(c, hipMemcpyAsync(out->status, c->d_status, n, hipMemcpyDeviceToHost, rs));
-  }
-  if (in->n_rules && out->stats)
-    API_HIP(c, hipMemcpyAsync(out->stats, c->d_stats, (size_t)in->n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost,
-                              rs));
-  return synchronize_all(c);
+  return RL_OK;
+}
+
+int rl_do_limit_host_async(rl_ctx* c, const rl_batch* in, rl_result* out) {
+  if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (c->n == 1) return eng_do_limit_host_async(c->e[0], in, out);
+  if (const int rc = check_host_batch(c, in, out)) return rc;
+  return shards_submit(c, in, out, true, nullptr);
+}
+
+int rl_do_limit(rl_ctx* c, const rl_batch* in, rl_result* out) {
+  if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (c->n == 1) return eng_do_limit(c->e[0], in, out);
+  if (const int rc = check_host_batch(c, in, out)) return rc;
+  const int rc = shards_submit(c, in, out, true, nullptr);
+  const int sr = synchronize_all(c);
+  return rc ? rc : sr;
 }
 
 int rl_comm_unique_id(uint8_t* id) {

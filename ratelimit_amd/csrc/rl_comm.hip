@@ -95,6 +95,15 @@ struct CommSlot {
   uint32_t n = 0, n_rules = 0;
   int err = RL_OK;                         // the slice failed on the host: it sent nothing
   std::string errmsg;
+  CommIO io{};
+  // host-fed slices (CommIO.host): device staging at the caller's absolute
+  // offsets, allocated on first use; io slices' stats (device) for stats_host
+  uint8_t* h_stem = nullptr;
+  uint32_t *h_off = nullptr, *h_req = nullptr, *h_limit = nullptr, *h_hits = nullptr, *h_rule = nullptr;
+  int64_t* h_now = nullptr;
+  uint8_t *h_unit = nullptr, *h_flags = nullptr, *h_code = nullptr, *h_status = nullptr;
+  uint32_t *h_rem = nullptr, *h_reset = nullptr;
+  unsigned long long* io_stats = nullptr;
 };
 
 struct CommRouter {
@@ -155,7 +164,8 @@ int run_group(CommRouter* r, Engine* e, uint32_t ch, hipStream_t st) {
 
 void free_slot(CommSlot& S) {
   void* bufs[] = {S.send_rec, S.send_stem, S.perm, S.cnt, S.recv_rec, S.recv_stem, S.ret_send, S.back, S.ostats,
-                  S.stats_stage};
+                  S.stats_stage, S.h_stem, S.h_off, S.h_req, S.h_limit, S.h_hits, S.h_rule, S.h_now, S.h_unit,
+                  S.h_flags, S.h_code, S.h_status, S.h_rem, S.h_reset, S.io_stats};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (hipEvent_t ev : {S.packed, S.sent, S.done})
@@ -198,6 +208,53 @@ hipError_t grow(CommRouter* r, CommSlot& S, uint64_t n_rec, uint64_t n_stem, uin
   return hipSuccess;
 }
 
+// A host-fed slice (CommIO.host) into slot S's device staging, on the counts
+// stream (after the slot's previous batch): the same absolute offsets, so the
+// staged view *d indexes like the caller's batch. Checks the sizes the copies
+// rely on first (a failure is the slice's own: zero counts).
+int stage_host(CommRouter* r, Engine* e, CommSlot& S, const rl_batch* in, rl_batch* d) {
+  const rl_config& g = e->cfg;
+  if (!S.h_stem) {
+    const bool ok = dalloc(&S.h_stem, (size_t)g.max_stem_bytes + 64) == hipSuccess &&
+                    dalloc(&S.h_off, (size_t)g.max_batch + 1) == hipSuccess && dalloc(&S.h_req, g.max_batch) == hipSuccess &&
+                    dalloc(&S.h_limit, g.max_batch) == hipSuccess && dalloc(&S.h_hits, g.max_batch) == hipSuccess &&
+                    dalloc(&S.h_rule, g.max_batch) == hipSuccess && dalloc(&S.h_now, g.max_requests) == hipSuccess &&
+                    dalloc(&S.h_unit, g.max_batch) == hipSuccess && dalloc(&S.h_flags, g.max_batch) == hipSuccess &&
+                    dalloc(&S.h_code, g.max_batch) == hipSuccess && dalloc(&S.h_status, g.max_batch) == hipSuccess &&
+                    dalloc(&S.h_rem, g.max_batch) == hipSuccess && dalloc(&S.h_reset, g.max_batch) == hipSuccess;
+    if (!ok) return breaks(r, e, RL_E_HIP, "gpu: host-fed routing staging allocation failed");
+  }
+  const uint32_t n = in->n, da = S.io.da, qa = S.io.qa, qb = in->n_requests;
+  if (!n) {
+    *d = *in;
+    return RL_OK;
+  }
+  const uint64_t a0 = in->stem_off[0] & ~3u, a1 = in->stem_off[n];
+  if ((uint64_t)da + n > g.max_batch || qb > g.max_requests || qa > qb || a1 > g.max_stem_bytes || a1 < a0)
+    return eng_fail(e, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_stem_bytes");
+  hipStream_t st = r->cs;
+  CHK_HIP(e, hipMemcpyAsync(S.h_stem + a0, in->stem_bytes + a0, a1 - a0, hipMemcpyHostToDevice, st));
+  CHK_HIP(e, hipMemcpyAsync(S.h_off + da, in->stem_off, (n + 1) * 4ull, hipMemcpyHostToDevice, st));
+  if (qb > qa) CHK_HIP(e, hipMemcpyAsync(S.h_now + qa, in->now + qa, (qb - qa) * 8ull, hipMemcpyHostToDevice, st));
+  CHK_HIP(e, hipMemcpyAsync(S.h_req + da, in->req_idx, n * 4ull, hipMemcpyHostToDevice, st));
+  CHK_HIP(e, hipMemcpyAsync(S.h_unit + da, in->unit, n, hipMemcpyHostToDevice, st));
+  CHK_HIP(e, hipMemcpyAsync(S.h_flags + da, in->flags, n, hipMemcpyHostToDevice, st));
+  CHK_HIP(e, hipMemcpyAsync(S.h_limit + da, in->limit, n * 4ull, hipMemcpyHostToDevice, st));
+  CHK_HIP(e, hipMemcpyAsync(S.h_hits + da, in->hits, n * 4ull, hipMemcpyHostToDevice, st));
+  CHK_HIP(e, hipMemcpyAsync(S.h_rule + da, in->rule_id, n * 4ull, hipMemcpyHostToDevice, st));
+  *d = *in;
+  d->stem_bytes = S.h_stem;
+  d->stem_off = S.h_off + da;
+  d->now = S.h_now;
+  d->req_idx = S.h_req + da;
+  d->unit = S.h_unit + da;
+  d->flags = S.h_flags + da;
+  d->limit = S.h_limit + da;
+  d->hits = S.h_hits + da;
+  d->rule_id = S.h_rule + da;
+  return RL_OK;
+}
+
 // First half of a batch (slot s): partition, counts exchange, counts to the
 // host. `hostrc` != RL_OK: the slice was rejected before the partition; it
 // sends zero counts. (The next call's second half waits on the host for this
@@ -212,6 +269,12 @@ int first_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, const rl_batch
   }
   const uint64_t flags = S.out.status ? CNT_ISOLATE : 0;
   int rc = hostrc;
+  rl_batch staged;
+  if (!rc && S.io.host) {
+    rc = stage_host(r, e, S, in, &staged);
+    if (r->broken) return rc;
+    in = &staged;
+  }
   if (!rc)
     rc = eng_route_pack(e, in, W, me, S.send_rec, S.send_stem, S.perm, (uint64_t*)S.cnt, r->cs, CNT_W, S.n_rules,
                         flags);
@@ -388,6 +451,8 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
     const rl_result& out = S.out;
     const uint32_t mine = S.n_rules * RL_NUM_STATS;  // (<= m: M is the largest n_rules sent)
     OutDev o{out.code, out.limit_remaining, out.reset_s, (unsigned long long*)out.stats, out.status};
+    if (S.io.host) o = OutDev{S.h_code, S.h_rem, S.h_reset, nullptr, out.status ? S.h_status : nullptr};
+    unsigned long long* stats_out = S.io.stats_host ? S.io_stats : (unsigned long long*)out.stats;
     uint32_t* src_err = out.status ? nullptr : e->errw + NBUF + 2;
     if (direct) {
       const uint32_t k = S.k[0];
@@ -396,7 +461,15 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
     } else {
       launch_route_scatter(S.perm, S.back, n, o, r->ret, src_err);
     }
-    if (mine && out.stats) launch_stats_sum(stats_in, W, mine, (unsigned long long*)out.stats, r->ret, m);
+    if (mine && stats_out) launch_stats_sum(stats_in, W, mine, stats_out, r->ret, m);
+    if (S.io.stats_host && mine)
+      CHK_HIP(e, hipMemcpyAsync(S.io.stats_host, S.io_stats, (size_t)mine * 8, hipMemcpyDeviceToHost, r->ret));
+    if (S.io.host && n) {  // the answers cross back to the caller's host slice
+      CHK_HIP(e, hipMemcpyAsync(out.code, S.h_code, n, hipMemcpyDeviceToHost, r->ret));
+      CHK_HIP(e, hipMemcpyAsync(out.limit_remaining, S.h_rem, n * 4ull, hipMemcpyDeviceToHost, r->ret));
+      CHK_HIP(e, hipMemcpyAsync(out.reset_s, S.h_reset, n * 4ull, hipMemcpyDeviceToHost, r->ret));
+      if (out.status) CHK_HIP(e, hipMemcpyAsync(out.status, S.h_status, n, hipMemcpyDeviceToHost, r->ret));
+    }
   } else if (!r->sticky) {
     r->sticky = S.err;
     r->sticky_msg = S.errmsg;
@@ -506,7 +579,16 @@ int comm_synchronize(CommRouter* r, Engine* e) {
   return RL_OK;
 }
 
-int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, hipStream_t caller) {
+uint32_t comm_slots() { return RSLOTS; }
+
+int comm_wait_slot(CommRouter* r, Engine* e, uint32_t s) {
+  CHK_HIP(e, hipSetDevice(r->dev));
+  CHK_HIP(e, hipEventSynchronize(r->slot[s % RSLOTS].done));
+  return RL_OK;
+}
+
+int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, hipStream_t caller,
+                  const CommIO* io) {
   if (r->broken) return eng_fail(e, r->broken, r->broken_msg);
   const uint32_t n = in->n, nr = in->n_rules;
   CHK_HIP(e, hipSetDevice(r->dev));
@@ -518,6 +600,9 @@ int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, 
   S.n_rules = nr;
   S.err = RL_OK;
   S.errmsg.clear();
+  S.io = io ? *io : CommIO{};
+  if (S.io.stats_host && !S.io_stats && dalloc(&S.io_stats, r->m_max) != hipSuccess)
+    return breaks(r, e, RL_E_HIP, "gpu: routing stats staging allocation failed");
   // checks the partition does not make: a failure here still takes part in
   // the exchange (zero counts) and fails this rank's batch at rl_synchronize
   int hostrc = RL_OK;

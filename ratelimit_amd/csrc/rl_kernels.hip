@@ -3451,6 +3451,7 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
                                                              s.keys[1], s.vals[0], s.hits_s, s.segsum, s.rid,
                                                              s.run_start, s.run_end, s.runs64, s.drun, s.big_meta, s.big_n,
                                                              s.big_work, s.work_n, s.sorted_n, s.err);
+#ifndef RL_EXP_NO_BIG  // (measurement builds only: without the large-bucket kernels, C1 has none)
     k_big_count<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
                                                                     s.big_meta, s.big_work, s.work_n, s.big_cnt,
                                                                     s.err);
@@ -3461,6 +3462,7 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
                                                               s.keys[1], s.vals[0], s.hits_s, s.hit_t, s.segsum,
                                                               s.rid, s.run_start, s.run_end, s.runs64, s.drun, s.big_meta,
                                                               s.big_n, s.big_cnt, s.err);
+#endif
     k_run_check<<<cdiv(b.n, RC_CHUNK), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[1], s.rid, s.run_start,
                                                 s.run_flags, s.defer, s.defer_n, s.err, s.runs64, s.split,
                                                 s.sorted_n);

@@ -1,11 +1,15 @@
 """One rl_ctx hash-sharding its table over several GPUs (rl_config.n_shards).
 
 The multi-GPU path behind the C ABI: one process, one ctx,
-n_shards engines; every batch is partitioned by owner on shard 0's device,
-copied to the owners, answered by their pipelines and scattered back. Here all
-shards sit on cuda:0 (shard_device = [0, 0, ...]: the routing, per-owner
-pipelines, stats sums and host-side fan-out are the same code as across
-devices; only the copies are plain device copies instead of xGMI peer copies).
+n_shards engines, each with a router (rl_comm.hip) on its own worker thread,
+the routers joined in an in-process loopback world. A host batch is cut into
+request-aligned slices, one per shard, each crossing its shard's own PCIe link
+(rl_do_limit, rl_do_limit_host_async); a device batch is taken whole by shard
+0 (rl_do_limit_async). Either way every descriptor goes to its owner shard
+and back, and the shards' stats are summed. Here all shards sit on cuda:0
+(shard_device = [0, 0, ...]: the routing, per-owner pipelines, stats sums and
+slices are the same code as across devices; only the copies are plain device
+copies instead of xGMI peer copies).
 
 Answers and stats of every entry point must equal the single-table oracles
 (Python oracle for random streams, C oracle for C2 batches), and the table
@@ -217,3 +221,68 @@ def test_gpu_multishard_long_and_ragged_stems_vs_c_oracle():
                 assert np.array_equal(g[key], o[key]), (n_shards, key)
         be.close()
         co.close()
+
+
+@pytest.mark.parametrize("n_shards,lc,isolate", [(2, False, False), (3, True, True), (4, True, False)])
+def test_gpu_multishard_host_async_pipelined_vs_c_oracle(n_shards, lc, isolate):
+    """rl_do_limit_host_async on a multi-shard ctx: every slice crosses its own
+    shard's link; eight batches (more than the routers keep in flight, so the
+    stats of the oldest are summed before its slot is reused) submitted before
+    one synchronize, from page-locked buffers."""
+    from ratelimit_amd.limiter import PinnedArena
+    from ratelimit_amd.packing import PackedBatch
+    batches = _c2(n_batches=8, per_batch=5_000, seed=17)
+    co = c_oracle.COracle(0.8, lc)
+    want = [co.do_limit(*b) for b in batches]
+    co.close()
+    be = Backend(0.8, lc, table_slots=1 << 17, max_batch=1 << 15, max_rules=16, hash_seed=7, **_shards(n_shards))
+    arena = PinnedArena()
+    keep = []
+    for a, n, nq, nr in batches:
+        pb = PackedBatch({k: arena.like(v) for k, v in a.items()}, n, nq, nr)
+        out = {k: arena.like(v) for k, v in pb.alloc_result(isolate).items()}
+        keep.append((pb, out, be.do_limit_host_async(pb, out)))
+    be.synchronize()
+    for (pb, out, _), w in zip(keep, want):
+        n = pb.n
+        for k in ("code", "limit_remaining", "reset_s"):
+            assert np.array_equal(out[k][:n], w[k]), k
+        assert np.array_equal(out["stats"][:pb.n_rules * abi.RL_NUM_STATS], w["stats"])
+        if isolate:
+            assert not out["status"][:n].any()
+    be.close()
+    arena.close()
+
+
+def test_gpu_multishard_host_async_rejects_and_recovers():
+    """A host batch larger than max_batch is refused at the call (no shard
+    takes any of it); the next batches are answered exactly."""
+    from ratelimit_amd.limiter import PinnedArena
+    from ratelimit_amd.packing import PackedBatch
+    batches = _c2(n_batches=3, per_batch=3_000, seed=23)
+    big = workloads.concat_batches(_c2(n_batches=2, per_batch=3_000, seed=24))
+    be = Backend(0.8, True, table_slots=1 << 16, max_batch=8_192, max_rules=16, hash_seed=7, **_shards(2))
+    co = c_oracle.COracle(0.8, True)
+    arena = PinnedArena()
+
+    def run(a, n, nq, nr):
+        pb = PackedBatch({k: arena.like(v) for k, v in a.items()}, n, nq, nr)
+        out = {k: arena.like(v) for k, v in pb.alloc_result().items()}
+        ref = be.do_limit_host_async(pb, out)
+        return pb, out, ref
+
+    r0 = run(*batches[0])
+    be.synchronize()
+    w0 = co.do_limit(*batches[0])
+    assert np.array_equal(r0[1]["code"][:r0[0].n], w0["code"])
+    with pytest.raises(RedisError, match="RL_E_CAPACITY"):
+        run(*big)  # 12000 descriptors > max_batch: taken by no shard
+    for b in batches[1:]:
+        pb, out, _ = run(*b)
+        be.synchronize()
+        w = co.do_limit(*b)
+        for k in ("code", "limit_remaining", "reset_s", "stats"):
+            assert np.array_equal(out[k][:pb.n if k != "stats" else pb.n_rules * abi.RL_NUM_STATS], w[k]), k
+    be.close()
+    co.close()
+    arena.close()
