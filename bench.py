@@ -43,8 +43,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c1", choices=["c1", "c2", "c3"],
-                    help="c1 uniform / c2 Zipf(1.1), hits 1..8 / c3 = c1 at 62.5M tenants per GPU (1B keys on 8)")
+    ap.add_argument("--config", default="c1", choices=["c1", "c2", "c2u", "c3"],
+                    help="c1 uniform / c2 Zipf(1.1), hits 1..8 / c2u = c2 with half the hot tenants' sec descriptors overridden to MINUTE (one stem under two units) / c3 = c1 at 62.5M tenants per GPU (1B keys on 8)")
     ap.add_argument("--requests", type=int, default=500_000, help="requests per batch per GPU (2 descriptors each)")
     ap.add_argument("--tenants", type=int, default=0, help="tenants per GPU (default 10M; c3 62.5M)")
     ap.add_argument("--distinct-batches", type=int, default=4)
@@ -147,7 +147,8 @@ def main():
         import secrets
         seed = secrets.randbits(62) + 1
     sh = dict(n_shards=args.shards, shard_devices=[local] * args.shards) if args.shards > 1 else {}
-    be = Backend(0.8, False, table_slots=slots, max_batch=cap, max_rules=max(8, 2 * world * args.shards),
+    NR = args.n_rules = 3 if args.config == "c2u" else 2  # rules per batch (c2u: the override's own stats key)
+    be = Backend(0.8, False, table_slots=slots, max_batch=cap, max_rules=max(8, NR * world * args.shards),
                  device=local, hash_seed=seed, max_stem_bytes=64 * cap, **sh)
     now0 = W.NOW0
     py_route = routed and (args.route_impl == "python" or args.dist_backend == "gloo")
@@ -166,15 +167,15 @@ def main():
     out = {"code": torch.empty(n, dtype=torch.uint8, device="cuda"),
            "limit_remaining": torch.empty(n, dtype=torch.int32, device="cuda"),
            "reset_s": torch.empty(n, dtype=torch.int32, device="cuda"),
-           "stats": torch.zeros(2 * 6, dtype=torch.int64, device="cuda")}
+           "stats": torch.zeros(NR * 6, dtype=torch.int64, device="cuda")}
 
     serial_stream = main_stream.cuda_stream
 
     def do_step(inp, bn, bq):
         if routed:
-            sc.submit(inp, bn, bq, 2, out)
+            sc.submit(inp, bn, bq, NR, out)
         else:
-            be.do_limit_device(inp, out, bn, bq, 2, stream=serial_stream)  # (pipelined; --serial: RL_DEBUG_SERIAL)
+            be.do_limit_device(inp, out, bn, bq, NR, stream=serial_stream)  # (pipelined; --serial: RL_DEBUG_SERIAL)
 
     def sync():
         if routed:
@@ -196,8 +197,9 @@ def main():
     # ---- device-resident input batches + per-step clocks. Requests draw from
     # the whole node's tenant space (world * T): with routing every rank talks
     # to every owner.
-    rng = np.random.default_rng((0xC2 if args.config == "c2" else 0xC1) + 7919 * rank)
-    sampler = W.ZipfSampler(world * T, 1.1) if args.config == "c2" else None
+    zipf = args.config in ("c2", "c2u")
+    rng = np.random.default_rng((0xC2 if zipf else 0xC1) + 7919 * rank)
+    sampler = W.ZipfSampler(world * T, 1.1) if zipf else None
     dev_batches = []
     uniq = []  # descriptors k_table answers: keys seen once + runs shorter than LONG_RUN (the rest: k_late)
     host_batches = []
@@ -205,6 +207,8 @@ def main():
         ten = rng.integers(0, world * T, nq) if sampler is None else sampler.sample(rng, nq)
         if sampler is None:
             a, bn, bq, br = W.c1_batch(ten, now0)
+        elif args.config == "c2u":
+            a, bn, bq, br = W.c2u_batch(ten, now0, rng.integers(1, 9, nq).astype(np.uint32), rng)
         else:
             a, bn, bq, br = W.c1_batch(ten, now0, rng.integers(1, 9, nq).astype(np.uint32))
         _, cnt = np.unique(ten, return_counts=True)
@@ -324,7 +328,8 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, W)
 
-    dist_desc = {"c1": "uniform", "c2": "Zipf(1.1), hits 1..8", "c3": "uniform"}[args.config]
+    dist_desc = {"c1": "uniform", "c2": "Zipf(1.1), hits 1..8", "c3": "uniform",
+                 "c2u": "Zipf(1.1), hits 1..8, half the 16 hottest tenants' sec descriptors overridden to MINUTE"}[args.config]
     line = {
         "metric": METRIC, "value": value, "unit": "decisions/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -445,46 +450,60 @@ def loopback_main(args):
 
 
 def pcie_fed(args, be, host_batches, now):
-    """The same batches fed from page-locked host memory (rl_do_limit_host_async):
-    inputs cross PCIe while earlier batches compute, outputs come back
-    (code, remaining, reset). SURVEY §8(d): with requests arriving in host
-    memory, PCIe is the honest bound. Rate over args.pcie_steps queued batches,
-    then per-batch latency (submit -> outputs on the host)."""
+    """The same batches fed from page-locked host memory: inputs cross PCIe
+    while earlier batches compute, outputs come back (code, remaining, reset).
+    SURVEY §8(d): with requests arriving in host memory, PCIe is the honest
+    bound. Two input formats: the compact one (rl_do_limit_compact_async, one
+    46-B-per-descriptor buffer per batch: the reported rate) and the rl_batch
+    arrays (rl_do_limit_host_async, 60 B, under "soa"). Rate over
+    args.pcie_steps queued batches, then per-batch latency (submit -> outputs
+    on the host)."""
     from ratelimit_amd.limiter import PinnedArena
-    from ratelimit_amd.packing import PackedBatch
+    from ratelimit_amd.packing import PackedBatch, compact_batch
     arena = PinnedArena()
-    fed = []
+    soa, comp = [], []
     for a, bn, bq in host_batches:
         arr = {k: arena.like(v) for k, v in a.items()}
         arr["now"] = arena.like(np.full(bq, now, np.int64))  # (time holds: one second for the whole phase)
-        fed.append(PackedBatch(arr, bn, bq, 2))
-    outs = [{k: arena.like(v) for k, v in fed[0].alloc_result().items()} for _ in range(4)]
-    n = fed[0].n
-    bytes_in = sum(int(v.nbytes) for k, v in fed[0].arrays.items() if k != "stem_bytes") + \
-        int(fed[0].arrays["stem_off"][n])
+        soa.append(PackedBatch(arr, bn, bq, args.n_rules))
+        if args.shards == 1:  # (compact batches: single-shard ctx)
+            comp.append(compact_batch(arr, bn, bq, args.n_rules, alloc=lambda nb: arena.array(nb, np.uint8)))
+    outs = [{k: arena.like(v) for k, v in soa[0].alloc_result().items()} for _ in range(4)]
+    n = soa[0].n
     bytes_out = n * 9
-    keep = []
 
-    def submit(s):
-        keep.append(be.do_limit_host_async(fed[s % len(fed)], outs[s % len(outs)]))
+    def phase(fed, call, bytes_in):
+        keep = []
 
-    for s in range(3):
-        submit(s)
-    be.synchronize()
-    keep.clear()
-    t0 = time.perf_counter()
-    for s in range(args.pcie_steps):
-        submit(s)
-    be.synchronize()
-    el = time.perf_counter() - t0
-    keep.clear()
-    lat = []
-    for s in range(20):
-        t1 = time.perf_counter()
-        submit(s)
+        def submit(s):
+            keep.append(call(fed[s % len(fed)], outs[s % len(outs)]))
+
+        for s in range(3):
+            submit(s)
         be.synchronize()
-        lat.append((time.perf_counter() - t1) * 1e3)
         keep.clear()
+        t0 = time.perf_counter()
+        for s in range(args.pcie_steps):
+            submit(s)
+        be.synchronize()
+        el = time.perf_counter() - t0
+        keep.clear()
+        lat = []
+        for s in range(20):
+            t1 = time.perf_counter()
+            submit(s)
+            be.synchronize()
+            lat.append((time.perf_counter() - t1) * 1e3)
+            keep.clear()
+        return {"value": n * args.pcie_steps / el, "unit": "decisions/s", "ms_per_step": el / args.pcie_steps * 1e3,
+                "p50_batch_ms": float(np.percentile(lat, 50)), "p99_batch_ms": float(np.percentile(lat, 99)),
+                "h2d_bytes_per_decision": bytes_in / n, "d2h_bytes_per_decision": bytes_out / n,
+                "h2d_GBps": bytes_in * args.pcie_steps / el / 1e9, "steps": args.pcie_steps}
+
+    soa_in = sum(int(v.nbytes) for k, v in soa[0].arrays.items() if k != "stem_bytes") + \
+        int(soa[0].arrays["stem_off"][n])
+    r_soa = phase(soa, be.do_limit_host_async, soa_in)
+    r_comp = phase(comp, be.do_limit_compact_async, int(comp[0].buf.size)) if comp else None
     # the link's own rate for one large page-locked copy, the bound to read h2d_GBps against
     import torch
     big = arena.array(256 << 20, np.uint8)
@@ -499,12 +518,19 @@ def pcie_fed(args, be, host_batches, now):
     peak = 5 * (256 << 20) / (time.perf_counter() - t1) / 1e9
     del dst, src
     arena.close()
-    return {"value": n * args.pcie_steps / el, "unit": "decisions/s", "ms_per_step": el / args.pcie_steps * 1e3,
-            "h2d_peak_GBps": peak, "frac_of_h2d_peak": bytes_in * args.pcie_steps / el / 1e9 / peak,
-            "p50_batch_ms": float(np.percentile(lat, 50)), "p99_batch_ms": float(np.percentile(lat, 99)),
-            "h2d_bytes_per_decision": bytes_in / n, "d2h_bytes_per_decision": bytes_out / n,
-            "h2d_GBps": bytes_in * args.pcie_steps / el / 1e9, "steps": args.pcie_steps,
-            "buffers": "page-locked (rl_alloc_host); now constant over the phase"}
+    for r in (r_soa, r_comp):
+        if r:
+            r["h2d_peak_GBps"] = peak
+            r["frac_of_h2d_peak"] = r["h2d_GBps"] / peak
+    r_soa["format"] = "rl_batch arrays (rl_do_limit_host_async: 9 copies per batch)"
+    if not r_comp:
+        r_soa["buffers"] = "page-locked (rl_alloc_host); now constant over the phase"
+        return r_soa
+    r_comp["format"] = "rl_batch_compact (rl_do_limit_compact_async: one buffer, one copy per batch)"
+    r_comp["buffers"] = "page-locked (rl_alloc_host); now constant over the phase"
+    r_comp["soa"] = {k: r_soa[k] for k in ("value", "h2d_bytes_per_decision", "frac_of_h2d_peak", "p99_batch_ms",
+                                           "format")}
+    return r_comp
 
 
 def cpu_baseline(args, W):
@@ -521,11 +547,14 @@ def cpu_baseline(args, W):
 
     def run(co, seconds, seed):
         rng = np.random.default_rng(seed)
-        sampler = W.ZipfSampler(args.tenants, 1.1) if args.config == "c2" else None
+        sampler = W.ZipfSampler(args.tenants, 1.1) if args.config in ("c2", "c2u") else None
         done, spent, k = 0, 0.0, 0
         while spent < seconds and k < 40:
             if sampler is None:
                 a, n, nq, nr = W.c1_batch(rng.integers(0, args.tenants, args.requests), W.NOW0 + k)
+            elif args.config == "c2u":
+                a, n, nq, nr = W.c2u_batch(sampler.sample(rng, args.requests), W.NOW0 + k,
+                                           rng.integers(1, 9, args.requests).astype(np.uint32), rng)
             else:
                 a, n, nq, nr = W.c1_batch(sampler.sample(rng, args.requests), W.NOW0 + k,
                                           rng.integers(1, 9, args.requests).astype(np.uint32))

@@ -205,6 +205,49 @@ int rl_do_limit_async(rl_ctx* ctx, const rl_batch* in, rl_result* out, void* str
 int rl_do_limit_host_async(rl_ctx* ctx, const rl_batch* in, rl_result* out);
 int rl_synchronize(rl_ctx* ctx);
 
+/* ---- Compact host batch: the fed path's PCIe format ---------------------
+ * The same batch as rl_batch, laid out for the link: ONE contiguous host
+ * buffer (one copy per batch), per request its clock, HitsAddend and first
+ * descriptor (the reference's per-request fields, RateLimitRequest.HitsAddend
+ * and the UnixNow() of the DoLimit call, fixed_cache_impl.go:33-51), per
+ * descriptor its stem and a 16-bit index into a table of the batch's distinct
+ * limits (a config rule, or an interned per-request override): 46 B per
+ * descriptor at BASELINE C1 (34-B stems, two descriptors per request) against
+ * rl_batch's 60. Answers, errors and statuses are those of the equivalent
+ * rl_batch (a limit index >= n_limits is an RL_E_INVALID descriptor). */
+typedef struct rl_limit {
+  uint32_t requests_per_unit;  /* RateLimit.Limit.RequestsPerUnit */
+  uint32_t rule_id;            /* stats row of the limit (< n_rules) */
+  uint8_t unit;                /* rl_unit */
+  uint8_t flags;               /* RL_FLAG_* */
+  uint16_t reserved;
+} rl_limit;
+
+/* Sections of buf, as byte offsets (each a multiple of 4, in any order). */
+typedef struct rl_batch_compact {
+  uint32_t n;            /* descriptors */
+  uint32_t n_requests;
+  uint32_t n_rules;
+  uint32_t n_limits;     /* entries of the limit table (<= 65536) */
+  const uint8_t* buf;    /* pinned host memory (rl_alloc_host): copied once, asynchronously */
+  uint64_t buf_bytes;
+  uint64_t stem_bytes;   /* concatenated stems */
+  uint64_t stem_off;     /* uint32[n + 1], stem_off[0] == 0 */
+  uint64_t limit_idx;    /* uint16[n] */
+  uint64_t req_first;    /* uint32[n_requests + 1]: request q holds descriptors
+                            [req_first[q], req_first[q+1]); req_first[0] == 0,
+                            non-decreasing, req_first[n_requests] == n */
+  uint64_t now;          /* uint32[n_requests] UnixNow() (< 2^32 - 172800, as rl_batch.now) */
+  uint64_t hits;         /* uint32[n_requests] HitsAddend */
+  uint64_t limits;       /* rl_limit[n_limits] */
+} rl_batch_compact;
+
+/* rl_do_limit_host_async on a compact batch (single-shard ctx): buf crosses
+ * PCIe in one copy into a device staging slot while earlier batches compute,
+ * is unpacked on the GPU, and the batch is pipelined like any other; *out is
+ * read after rl_synchronize. */
+int rl_do_limit_compact_async(rl_ctx* ctx, const rl_batch_compact* in, rl_result* out);
+
 /* Epoch sweep (replaces Redis EXPIRE): tombstones every slot whose counter
  * and local-cache entries have all expired at `now`; `now` becomes a floor
  * (later requests with an earlier time fail with RL_E_TIME). */

@@ -33,6 +33,26 @@ class RlBatch(C.Structure):
                 ("rule_id", P)]
 
 
+# rl_limit (12 B): one entry of a compact batch's limit table
+LIMIT_DTYPE = np.dtype([("requests_per_unit", np.uint32), ("rule_id", np.uint32), ("unit", np.uint8),
+                        ("flags", np.uint8), ("reserved", np.uint16)])
+
+
+class RlLimit(C.Structure):
+    _fields_ = [("requests_per_unit", C.c_uint32), ("rule_id", C.c_uint32), ("unit", C.c_uint8),
+                ("flags", C.c_uint8), ("reserved", C.c_uint16)]
+
+
+assert LIMIT_DTYPE.itemsize == C.sizeof(RlLimit)
+
+
+class RlBatchCompact(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("n_requests", C.c_uint32), ("n_rules", C.c_uint32), ("n_limits", C.c_uint32),
+                ("buf", P), ("buf_bytes", C.c_uint64), ("stem_bytes", C.c_uint64), ("stem_off", C.c_uint64),
+                ("limit_idx", C.c_uint64), ("req_first", C.c_uint64), ("now", C.c_uint64), ("hits", C.c_uint64),
+                ("limits", C.c_uint64)]
+
+
 class RlResult(C.Structure):
     _fields_ = [("code", P), ("limit_remaining", P), ("reset_s", P), ("stats", P), ("status", P)]
 

@@ -443,6 +443,13 @@ int rl_do_limit_host_async(rl_ctx* c, const rl_batch* in, rl_result* out) {
   return shards_submit(c, in, out, true, nullptr);
 }
 
+int rl_do_limit_compact_async(rl_ctx* c, const rl_batch_compact* in, rl_result* out) {
+  if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (c->n > 1) return eng_fail(c->e[0], RL_E_INVALID, "gpu: compact batches need a single-shard ctx");
+  if (c->comm) return eng_fail(c->e[0], RL_E_INVALID, "gpu: compact batches are not routed (rl_do_limit_routed_async)");
+  return eng_do_limit_compact_async(c->e[0], in, out);
+}
+
 int rl_do_limit(rl_ctx* c, const rl_batch* in, rl_result* out) {
   if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
   if (c->n == 1) return eng_do_limit(c->e[0], in, out);

@@ -32,6 +32,8 @@ struct HostSlot {
   uint8_t *code = nullptr, *status = nullptr;
   uint32_t *rem = nullptr, *reset = nullptr;
   unsigned long long* stats = nullptr;
+  uint8_t* cbuf = nullptr;        // a compact batch's buffer (rl_do_limit_compact_async), allocated on first use
+  uint64_t cbuf_cap = 0;
   hipEvent_t in_done = nullptr;   // its inputs are on the device
   hipEvent_t out_done = nullptr;  // its outputs are back on the host (the slot is free)
 };
@@ -108,6 +110,7 @@ const char* eng_last_error(const Engine* c);
 int eng_do_limit(Engine* c, const rl_batch* in, rl_result* out);
 int eng_do_limit_async(Engine* c, const rl_batch* in, rl_result* out, void* stream);
 int eng_do_limit_host_async(Engine* c, const rl_batch* in, rl_result* out);
+int eng_do_limit_compact_async(Engine* c, const rl_batch_compact* in, rl_result* out);
 int eng_synchronize(Engine* c);
 int eng_sweep(Engine* c, int64_t now, uint64_t* n_evicted);
 int eng_restore(Engine* c, const rl_restore_batch* in);

@@ -132,7 +132,7 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     hipEvent_t* ev = prof_events(c);
     (void)hipStreamWaitEvent(a, c->b_done[k], 0);    // buffer k's previous batch is done
     (void)hipStreamWaitEvent(a, c->consumed[k], 0);  // ... and its routed results were read
-    launch_stage_a(b, c->s[k], isolate, a, ev);
+    launch_stage_a(b, c->s[k], isolate, P.per_second, a, ev);
     (void)hipStreamWaitEvent(a, c->b_done[c->last], 0);  // table order
     launch_stage_b(b, o, t, P, c->s[k], restore, a, ev);
     (void)hipEventRecord(c->b_done[k], a);
@@ -140,7 +140,7 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     if (!st) st = c->stream;
     (void)after_batches(c, st);
     hipEvent_t* ev = prof_events(c);
-    launch_stage_a(b, c->s[k], isolate, st, ev);
+    launch_stage_a(b, c->s[k], isolate, P.per_second, st, ev);
     launch_stage_b(b, o, t, P, c->s[k], restore, st, ev);
     (void)hipEventRecord(c->b_done[k], st);
   }
@@ -216,7 +216,7 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
        dalloc(&s.defer2_n, 1) == hipSuccess && dalloc(&s.fast_blk, (size_t)n / (256 * 32) + 1) == hipSuccess;
   ok = ok && dalloc(&s.hits_s, n) == hipSuccess && dalloc(&s.segsum, n) == hipSuccess &&
        dalloc(&s.rid, n) == hipSuccess && dalloc(&s.run_start, (size_t)n + 1) == hipSuccess &&
-       dalloc(&s.run_flags, n) == hipSuccess && dalloc(&s.run_state, n) == hipSuccess &&
+       dalloc(&s.run_flags, n) == hipSuccess && dalloc(&s.run_state, n) == hipSuccess && dalloc(&s.run_alias, n) == hipSuccess &&
        dalloc(&s.run_f, n) == hipSuccess &&
        dalloc(&s.runs64, 1) == hipSuccess && dalloc(&s.split, 2) == hipSuccess && dalloc(&s.drun, (size_t)n / 2 + BIG_HEAVY * PART_DIGITS) == hipSuccess;
   ok = ok && dalloc(&s.hit_a, n) == hipSuccess && dalloc(&s.tile, n) == hipSuccess &&
@@ -230,8 +230,8 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
 void free_buffer(Scratch& s) {
   void* bufs[] = {s.rec, s.res, s.big_meta, s.big_n, s.big_work, s.work_n, s.sorted_n, s.big_cnt, s.keys[0], s.keys[1],
                   s.vals[0], s.vals[1], s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1,
-                  s.defer1_n, s.fast_blk, s.hits_s, s.segsum, s.rid, s.run_start, s.run_flags, s.run_state, s.run_f,
-                  s.runs64, s.split, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t, s.r_base};
+                  s.defer1_n, s.fast_blk, s.hits_s, s.segsum, s.rid, s.run_start, s.run_flags, s.run_state, s.run_alias,
+                  s.run_f, s.runs64, s.split, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t, s.r_base};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
 }
@@ -367,7 +367,7 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
 void free_host_slots(Engine* c) {
   for (HostSlot& h : c->hs) {
     void* bufs[] = {h.stem, h.off, h.req, h.limit, h.hits, h.rule, h.now, h.unit, h.flags, h.code, h.status, h.rem,
-                    h.reset, h.stats};
+                    h.reset, h.stats, h.cbuf};
     for (void* p : bufs)
       if (p) (void)hipFree(p);
     if (h.in_done) (void)hipEventDestroy(h.in_done);
@@ -621,15 +621,8 @@ int eng_synchronize(Engine* c) {
 // reads *out after rl_synchronize. Pinned host buffers (rl_alloc_host) make
 // the copies truly asynchronous; the host buffers of a batch must stay
 // untouched until then.
-int eng_do_limit_host_async(Engine* c, const rl_batch* in, rl_result* out) {
-  if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
-  const uint32_t n = in->n, nq = in->n_requests;
-  if (n && (!in->stem_off || !out->code || !out->limit_remaining || !out->reset_s))
-    return set_err(c, RL_E_INVALID, "gpu: null argument");
-  const uint64_t nb = n ? in->stem_off[n] : 0;
-  int rc = check_sizes(c, in, nb);
-  if (rc) return rc;
-  HIPCHK(c, hipSetDevice(c->cfg.device));
+// The NBUF host-fed staging slots and their copy streams (first use).
+int ensure_host_slots(Engine* c) {
   if (!c->hs_ready) {
     const rl_config& g = c->cfg;
     bool ok = hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) == hipSuccess &&
@@ -653,10 +646,50 @@ int eng_do_limit_host_async(Engine* c, const rl_batch* in, rl_result* out) {
     }
     c->hs_ready = true;
   }
+  return RL_OK;
+}
+
+// Enqueue the staged batch d (device pointers; its inputs complete at
+// h.in_done) and its outputs' copies back into *out on the d2h stream.
+int host_slot_run(Engine* c, HostSlot& h, const rl_batch& d, uint64_t nb, rl_result* out) {
+  const uint32_t n = d.n;
+  hipStream_t down = c->d2h;
+  BatchDev b = dev_view(c, &d, c->cfg.max_stem_bytes);
+  b.stem_total = (uint32_t)nb;
+  OutDev o{h.code, h.rem, h.reset, d.n_rules ? h.stats : nullptr, out->status ? h.status : nullptr};
+  HIPCHK(c, hipStreamWaitEvent(c->pipe[c->next], h.in_done, 0));
+  const uint32_t k = enqueue(c, b, o, 0, nullptr, true);
+  HIPCHK(c, hipStreamWaitEvent(down, c->b_done[k], 0));
+  if (n) {
+    HIPCHK(c, hipMemcpyAsync(out->code, h.code, n, hipMemcpyDeviceToHost, down));
+    HIPCHK(c, hipMemcpyAsync(out->limit_remaining, h.rem, n * 4ull, hipMemcpyDeviceToHost, down));
+    HIPCHK(c, hipMemcpyAsync(out->reset_s, h.reset, n * 4ull, hipMemcpyDeviceToHost, down));
+    if (out->status) HIPCHK(c, hipMemcpyAsync(out->status, h.status, n, hipMemcpyDeviceToHost, down));
+  }
+  if (d.n_rules && out->stats)
+    HIPCHK(c, hipMemcpyAsync(out->stats, h.stats, (size_t)d.n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost,
+                             down));
+  HIPCHK(c, hipEventRecord(h.out_done, down));
+  HIPCHK(c, hipGetLastError());
+  c->batches++;
+  c->decisions += n;
+  return RL_OK;
+}
+
+int eng_do_limit_host_async(Engine* c, const rl_batch* in, rl_result* out) {
+  if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  const uint32_t n = in->n, nq = in->n_requests;
+  if (n && (!in->stem_off || !out->code || !out->limit_remaining || !out->reset_s))
+    return set_err(c, RL_E_INVALID, "gpu: null argument");
+  const uint64_t nb = n ? in->stem_off[n] : 0;
+  int rc = check_sizes(c, in, nb);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if ((rc = ensure_host_slots(c))) return rc;
   const uint32_t j = c->hnext;
   c->hnext = (j + 1) % NBUF;
   HostSlot& h = c->hs[j];
-  hipStream_t up = c->h2d, down = c->d2h;
+  hipStream_t up = c->h2d;
   HIPCHK(c, hipStreamWaitEvent(up, h.out_done, 0));  // the slot's previous batch is drained
   if (nb) HIPCHK(c, hipMemcpyAsync(h.stem, in->stem_bytes, nb, hipMemcpyHostToDevice, up));
   HIPCHK(c, hipMemcpyAsync(h.off, in->stem_off, (n + 1) * 4ull, hipMemcpyHostToDevice, up));
@@ -680,26 +713,69 @@ int eng_do_limit_host_async(Engine* c, const rl_batch* in, rl_result* out) {
   d.limit = h.limit;
   d.hits = h.hits;
   d.rule_id = h.rule;
-  BatchDev b = dev_view(c, &d, c->cfg.max_stem_bytes);
-  b.stem_total = (uint32_t)nb;
-  OutDev o{h.code, h.rem, h.reset, in->n_rules ? h.stats : nullptr, out->status ? h.status : nullptr};
-  HIPCHK(c, hipStreamWaitEvent(c->pipe[c->next], h.in_done, 0));
-  const uint32_t k = enqueue(c, b, o, 0, nullptr, true);
-  HIPCHK(c, hipStreamWaitEvent(down, c->b_done[k], 0));
-  if (n) {
-    HIPCHK(c, hipMemcpyAsync(out->code, h.code, n, hipMemcpyDeviceToHost, down));
-    HIPCHK(c, hipMemcpyAsync(out->limit_remaining, h.rem, n * 4ull, hipMemcpyDeviceToHost, down));
-    HIPCHK(c, hipMemcpyAsync(out->reset_s, h.reset, n * 4ull, hipMemcpyDeviceToHost, down));
-    if (out->status) HIPCHK(c, hipMemcpyAsync(out->status, h.status, n, hipMemcpyDeviceToHost, down));
+  return host_slot_run(c, h, d, nb, out);
+}
+
+// A compact batch: its one buffer crosses PCIe in one copy into the slot's
+// cbuf, k_unpack rebuilds the rl_batch arrays in the slot, then as above. Section
+// bounds are checked here; contents (offsets, request ranges, limit indices)
+// on the device, like rl_batch's.
+int eng_do_limit_compact_async(Engine* c, const rl_batch_compact* in, rl_result* out) {
+  if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  const rl_config& g = c->cfg;
+  const uint32_t n = in->n, nq = in->n_requests;
+  if (n && (!in->buf || !out->code || !out->limit_remaining || !out->reset_s))
+    return set_err(c, RL_E_INVALID, "gpu: null argument");
+  if (n > g.max_batch || nq > g.max_requests || in->n_rules > g.max_rules || in->n_limits > 65536)
+    return set_err(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_rules (or > 65536 limits)");
+  if (n && !nq) return set_err(c, RL_E_INVALID, "gpu: descriptors without requests");
+  const uint64_t B = in->buf_bytes;
+  auto sect = [&](uint64_t off, uint64_t bytes) { return off % 4 == 0 && off <= B && bytes <= B - off; };
+  if (!sect(in->stem_off, (n + 1) * 4ull) || !sect(in->limit_idx, n * 2ull) || !sect(in->req_first, (nq + 1) * 4ull) ||
+      !sect(in->now, nq * 4ull) || !sect(in->hits, nq * 4ull) || !sect(in->limits, in->n_limits * 12ull) ||
+      !sect(in->stem_bytes, 0))
+    return set_err(c, RL_E_INVALID, "gpu: compact batch section outside buf or not 4-byte aligned");
+  const uint64_t nb = n ? reinterpret_cast<const uint32_t*>(in->buf + in->stem_off)[n] : 0;
+  if (nb > g.max_stem_bytes) return set_err(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_stem_bytes");
+  if (!sect(in->stem_bytes, nb)) return set_err(c, RL_E_INVALID, "gpu: compact batch stems outside buf");
+  HIPCHK(c, hipSetDevice(g.device));
+  int rc = ensure_host_slots(c);
+  if (rc) return rc;
+  const uint32_t j = c->hnext;
+  HostSlot& h = c->hs[j];
+  if (B > h.cbuf_cap) {  // grows to the largest buffer seen (the slot's previous batch drained first)
+    HIPCHK(c, hipEventSynchronize(h.out_done));
+    if (h.cbuf) HIPCHK(c, hipFree(h.cbuf));
+    h.cbuf = nullptr;
+    h.cbuf_cap = 0;
+    HIPCHK(c, dalloc(&h.cbuf, B + 64));
+    h.cbuf_cap = B;
   }
-  if (in->n_rules && out->stats)
-    HIPCHK(c, hipMemcpyAsync(out->stats, h.stats, (size_t)in->n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost,
-                             down));
-  HIPCHK(c, hipEventRecord(h.out_done, down));
-  HIPCHK(c, hipGetLastError());
-  c->batches++;
-  c->decisions += n;
-  return RL_OK;
+  c->hnext = (j + 1) % NBUF;
+  hipStream_t up = c->h2d;
+  HIPCHK(c, hipStreamWaitEvent(up, h.out_done, 0));  // the slot's previous batch is drained
+  if (B) HIPCHK(c, hipMemcpyAsync(h.cbuf, in->buf, B, hipMemcpyHostToDevice, up));
+  HIPCHK(c, hipEventRecord(h.in_done, up));
+  // unpacked on the batch's pipeline stream, so the copy stream runs the
+  // next batch's copy back to back (on the copy stream it left a ~35 us gap
+  // per batch: the kernel and its launch)
+  HIPCHK(c, hipStreamWaitEvent(c->pipe[c->next], h.in_done, 0));
+  launch_unpack(*in, h.cbuf, h.req, h.unit, h.flags, h.limit, h.hits, h.rule, h.now, c->s[c->next].err,
+                c->pipe[c->next]);
+  rl_batch d{};
+  d.n = n;
+  d.n_requests = nq;
+  d.n_rules = in->n_rules;
+  d.stem_bytes = h.cbuf + in->stem_bytes;
+  d.stem_off = reinterpret_cast<const uint32_t*>(h.cbuf + in->stem_off);
+  d.now = h.now;
+  d.req_idx = h.req;
+  d.unit = h.unit;
+  d.flags = h.flags;
+  d.limit = h.limit;
+  d.hits = h.hits;
+  d.rule_id = h.rule;
+  return host_slot_run(c, h, d, nb, out);
 }
 
 int eng_do_limit(Engine* c, const rl_batch* in, rl_result* out) {

@@ -26,6 +26,21 @@ struct BigMeta {
 constexpr uint32_t MAX_PART_TILES = 2048;  // k_part tiles per batch (max_batch <= 2048 x 4096)
 constexpr uint32_t LONG_RUN = 32;        // runs at least this long take the parallel path
 constexpr uint32_t RUN_SLOW = 1, RUN_FAST = 2, RUN_MULTI = 4;
+// A stem under several units (per-request overrides, config_impl.go:254-265)
+// shares Redis keys across its unit slots whenever two windows coincide
+// (SECOND and MINUTE at t % 60 == 0, cache_key.go:73-74). k_split orders such
+// a stem's descriptors into one sub-run per Redis key (stem, window[, store])
+// — its "groups", consecutive, the first one the head — and the head's
+// k_table lane sets every group up for the parallel path with the key's
+// records in all unit slots as write-back targets (alias_setup).
+constexpr uint32_t RUN_NOWVAR = 8;    // the run's descriptors do not share one `now`
+constexpr uint32_t RUN_ALIAS = 16;    // a group of a multi-unit stem (or a lone run of a SLOT_EXACT stem)
+constexpr uint32_t RUN_AHEAD = 32;    // ... its first group: bits 8..15 = the stem's group count
+constexpr uint32_t RUN_MERGE = 64;    // a deferred head: the exact path replays all groups in arrival order
+constexpr uint32_t RUN_G_SHIFT = 8, RUN_UMASK_SHIFT = 16;  // group count (head), units of the group (bit u-1)
+// k_run_check's verdict on a RUN_MULTI run (k_split reads it): some element has
+// the head's stem under another unit / some element has another stem or failed
+constexpr uint32_t RUN_UNITS = 128, RUN_STEMS = 1u << 24;
 constexpr uint32_t KEY_HEAD = 64;         // stem bytes carried inline (zero-padded) per descriptor
 constexpr uint32_t STAT_STRIPES = 64;     // global partial stats tables
 constexpr uint32_t STAT_LDS_RULES = 512;  // rules aggregated in LDS (== LDS_RULES)
@@ -159,7 +174,8 @@ struct Scratch {
   uint32_t* run_end;                   // [n] one past its last
   uint32_t* part_info;                 // [256 x part tiles] k_part: offset << 16 | count per digit and tile
   uint32_t* run_flags;                 // [n] RUN_*
-  uint4* run_state;                    // [n] {slot, c0, old lc, F | which<<1}
+  uint4* run_state;                    // [n] {slot, c0, old lc, F | which<<1}; alias groups: {targets, c0, lc, F}
+  uint4* run_alias;                    // [n] alias groups: the stem's slot per unit (0xFFFFFFFF: none)
   uint32_t* run_f;                     // [n] first over-limit position
   unsigned long long* runs64;          // bucket path: runs | runs of two or more << 32
   unsigned long long* split;           // k_split: [0] reservations (ids | dup-run entries << 32), [1] runs64 before it
@@ -182,12 +198,19 @@ struct Scratch {
 // only the batch and this buffer's scratch, so it may overlap the previous
 // batch's stage B; stage B (table probe, replay, decisions, stats, results)
 // must run in batch order.
-void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_t st, hipEvent_t* ev = nullptr);
+void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_second, hipStream_t st,
+                    hipEvent_t* ev = nullptr);
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
                     int restore, hipStream_t st, hipEvent_t* ev = nullptr);
 // ev (optional, RL_NUM_STAGES + 1 events on stream st): recorded before
 // k_prepare, after it, after the sort, just before and just after k_table, and
 // at the end (per-stage timing, rl_profile).
+// A compact host batch (rl_batch_compact, device copy of its buffer at buf)
+// -> the rl_batch arrays req / unit / flags / limit / hits / rule / now. A
+// malformed request layout sets ERR_INVALID in *err (the batch fails); a limit
+// index past the table gives the descriptor unit 0 (k_prepare: RL_E_INVALID).
+void launch_unpack(const rl_batch_compact& cb, const uint8_t* buf, uint32_t* req, uint8_t* unit, uint8_t* flags,
+                   uint32_t* limit, uint32_t* hits, uint32_t* rule, int64_t* now, uint32_t* err, hipStream_t st);
 // counts: cstride u64 per owner (records, stem bytes[, meta0, meta1]).
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
                        uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st,

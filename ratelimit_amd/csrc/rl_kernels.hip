@@ -189,6 +189,57 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   emit_rec(h);
 }
 
+// ---- k_unpack: a compact host batch (rl_batch_compact: per request clock,
+// hits and first descriptor; per descriptor a 16-bit index into the batch's
+// limit table) -> the rl_batch arrays the pipeline reads. One lane per
+// descriptor (its limit) and per request (its descriptors' request index and
+// hits, its 64-bit clock). A request layout that is not a partition of
+// [0, n) into non-decreasing ranges fails the batch (ERR_INVALID): a
+// descriptor left out would keep a stale request index.
+__global__ __launch_bounds__(256) void k_unpack(uint32_t n, uint32_t nq, uint32_t n_limits,
+                                                const uint16_t* __restrict__ lidx, const rl_limit* __restrict__ lim,
+                                                const uint32_t* __restrict__ first, const uint32_t* __restrict__ now32,
+                                                const uint32_t* __restrict__ hits_q, uint32_t* __restrict__ req,
+                                                uint8_t* __restrict__ unit, uint8_t* __restrict__ flags,
+                                                uint32_t* __restrict__ limit, uint32_t* __restrict__ hits,
+                                                uint32_t* __restrict__ rule, int64_t* __restrict__ now,
+                                                uint32_t* err) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    const uint32_t k = lidx[i];
+    const rl_limit L = k < n_limits ? lim[k] : rl_limit{0, 0, 0, 0, 0};  // unit 0: the descriptor's RL_E_INVALID
+    unit[i] = L.unit;
+    flags[i] = L.flags;
+    limit[i] = L.requests_per_unit;
+    rule[i] = L.rule_id;
+  }
+  if (i < nq) {
+    const uint32_t a = first[i], z = first[i + 1];
+    if (z < a || z > n || (i == 0 && a != 0) || (i + 1 == nq && z != n)) {
+      atomicOr(err, ERR_INVALID);
+    } else {
+      const uint32_t h = hits_q[i];
+      for (uint32_t d = a; d < z; d++) {
+        req[d] = i;
+        hits[d] = h;
+      }
+    }
+    now[i] = now32[i];
+  }
+  if (i == 0 && nq == 0 && n) atomicOr(err, ERR_INVALID);  // descriptors without a request
+}
+
+void launch_unpack(const rl_batch_compact& cb, const uint8_t* buf, uint32_t* req, uint8_t* unit, uint8_t* flags,
+                   uint32_t* limit, uint32_t* hits, uint32_t* rule, int64_t* now, uint32_t* err, hipStream_t st) {
+  const uint32_t m = cb.n > cb.n_requests ? cb.n : cb.n_requests;
+  if (!m) return;
+  k_unpack<<<(m + 255) / 256, 256, 0, st>>>(
+      cb.n, cb.n_requests, cb.n_limits, reinterpret_cast<const uint16_t*>(buf + cb.limit_idx),
+      reinterpret_cast<const rl_limit*>(buf + cb.limits), reinterpret_cast<const uint32_t*>(buf + cb.req_first),
+      reinterpret_cast<const uint32_t*>(buf + cb.now), reinterpret_cast<const uint32_t*>(buf + cb.hits), req, unit,
+      flags, limit, hits, rule, now, err);
+}
+
 // The zero-padded first KEY_HEAD bytes of the stem at byte `off` of the packed
 // stems, as 4 x uint4: five aligned 16-B loads, then dword selects and funnel
 // shifts. Only chunks holding a byte of the head are loaded, so no load leaves
@@ -2283,7 +2334,8 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
                                                    uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
                                                    uint32_t* defer_n, const uint32_t* err,
                                                    const unsigned long long* num_runs, unsigned long long* split,
-                                                   const uint32_t* sorted_n) {
+                                                   const uint32_t* sorted_n, uint32_t* __restrict__ pos_unit,
+                                                   uint32_t* __restrict__ pos_hits) {
   __shared__ uint32_t s_list[RC_CHUNK], s_cnt;
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // k_split's reservations start from the bucket kernels' count
     split[0] = 0;
@@ -2306,46 +2358,145 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
     rec[eq].lu = x.lu | (FLAG_DUP << 24);
     if (q == p + 1) rec[ep].lu = y.lu | (FLAG_DUP << 24);  // the run's head
     // a failed descriptor (FLAG_SKIP) makes its run exact-path: general_body leaves it out
-    const bool same = !((rec_flags(x) | rec_flags(y)) & FLAG_SKIP) && x.hlo == y.hlo &&
-                      (x.lu & 0xFFFFFFu) == (y.lu & 0xFFFFFFu) &&  // hash, length, unit
-                      key_equal(key_of(b, x), key_of(b, y));
-    if (!same) {
-      if (!(atomicOr(&run_flags[r], RUN_MULTI) & RUN_MULTI)) defer[atomicAdd(defer_n, 1u)] = r;
-    } else {
+    const bool same_stem = !((rec_flags(x) | rec_flags(y)) & FLAG_SKIP) && x.hlo == y.hlo &&
+                           (x.lu & 0xFFFFu) == (y.lu & 0xFFFFu) &&  // hash, length
+                           key_equal(key_of(b, x), key_of(b, y));
+    const bool same = same_stem && rec_unit(x) == rec_unit(y);
+    // per position, for k_split's long runs (coalesced there instead of a
+    // random record read per element): the unit and max(1, hits)
+    pos_unit[q] = rec_unit(x) << 8;
+    pos_hits[q] = x.hits > 1 ? x.hits : 1u;
+    uint32_t f = 0;
+    if (!same)  // (+ the units seen, for k_split; a failed descriptor's unit may be out of range)
+      f = RUN_MULTI | (same_stem ? RUN_UNITS | ((1u << (rec_unit(x) - 1)) << RUN_UMASK_SHIFT) : RUN_STEMS);
+    if (x.now != y.now) {
       const uint32_t d = div_of(rec_unit(x));
-      if (x.now / d != y.now / d) atomicOr(&run_flags[r], RUN_SLOW);
+      f |= (same && x.now / d != y.now / d) ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR;
+    }
+    // a hot run's elements all find the same: read before the atomic, so a
+    // run of tens of thousands does not serialise on one word
+    if (f && (__hip_atomic_load(&run_flags[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & f) != f) {
+      const uint32_t old = atomicOr(&run_flags[r], f);
+      if ((f & RUN_MULTI) && !(old & RUN_MULTI)) defer[atomicAdd(defer_n, 1u)] = r;
     }
   }
 }
 
-// ---- k_split: hash-prefix collisions. A run is defined by the 32-bit sort
-// key; k_run_check flags it RUN_MULTI when its elements do not all share the
-// head's stem and unit. When they form at most SPLIT_MAXG distinct stems, each
-// under one unit (the usual case: unrelated keys whose hashes agree in 32
-// bits, ~100 runs per 1M batch at C1), the run is reordered stably by stem
-// into consecutive sub-runs with their own run ids, in-run sums and flags, and
-// k_table answers them like any other run (a sub-run of one element becomes a
-// key seen once) instead of the one-lane exact path, whose chain of dependent
-// table accesses outlasted k_table. Anything else (a stem under several
-// units, a 64-bit hash collision, a failed descriptor, or no room left in the
-// dup-run list) stays on the exact path. Runs over SPLIT_CAP elements take
-// split_long_body (global-memory scratch instead of LDS).
+// ---- k_split: hash-prefix collisions and multi-unit stems. A run is defined
+// by the 32-bit sort key; k_run_check flags it RUN_MULTI when its elements do
+// not all share the head's stem and unit. Its distinct stems ("families") are
+// found by the full bytes; each becomes one or more groups:
+//  * a stem under one unit is one group (the usual case: unrelated keys whose
+//    hashes agree in 32 bits, ~100 runs per 1M batch at C1);
+//  * a stem under several units (per-request overrides, config_impl.go:254-265)
+//    is one group per Redis key: the key is stem ‖ windowStart
+//    (cache_key.go:73-74), so two units whose windows coincide (SECOND and
+//    MINUTE at t % 60 == 0) share a counter and form one group in arrival
+//    order, and units whose windows differ are independent keys.
+// The run is reordered stably into consecutive sub-runs, one per group, with
+// their own run ids, in-run sums and flags, and k_table answers them like any
+// other run (a lone group of one element becomes a key seen once) instead of
+// the one-lane exact path, whose chain of dependent table accesses outlasted
+// k_table. A multi-unit stem's groups carry RUN_ALIAS (its first one
+// RUN_AHEAD and the group count): k_table's lane for the head sets all of them
+// up at once (alias_setup). Anything else stays on the exact path: a 64-bit
+// hash collision, a failed descriptor, more than SPLIT_MAXG groups, a
+// multi-unit stem whose descriptors do not share one `now`, one window of a
+// stem in both stores of the per-second split (their local-cache entry is
+// shared), or no room left in the dup-run list. Runs over SPLIT_CAP elements
+// take split_long_body (global-memory scratch instead of LDS).
 constexpr uint32_t SPLIT_CAP = 1024, SPLIT_MAXG = 8, SPLIT_BLOCKS = 128;
 constexpr uint32_t DEFER_DONE = 0xFFFFFFFFu;  // a deferral k_split resolved
+constexpr uint32_t SPLIT_BAD = 0xFFu;
+
+// Families -> groups (one thread). fmask: units seen per family (bit u-1);
+// fnow / fnv: the family leader's `now` / whether another one was seen.
+struct SplitPlan {
+  uint8_t ug[SPLIT_MAXG][4];  // group of (family, unit - 1)
+  uint8_t head[SPLIT_MAXG];   // family -> its first group
+  uint8_t ng[SPLIT_MAXG];     // family -> its group count
+  uint8_t fam[SPLIT_MAXG];    // group -> family
+  uint8_t alias[SPLIT_MAXG];  // group of a multi-unit family
+  uint8_t gmask[SPLIT_MAXG];  // group -> its units
+  uint32_t G, any_alias;
+};
+
+__device__ inline uint32_t split_plan(SplitPlan& S, uint32_t NF, const uint32_t* fmask, const uint32_t* fnow,
+                                      const uint32_t* fnv, int per_second) {
+  uint32_t G = 0;
+  S.any_alias = 0;
+  for (uint32_t f = 0; f < NF; f++) {
+    const uint32_t m = fmask[f];
+    S.head[f] = (uint8_t)G;
+    if (__popc(m) == 1) {
+      if (G >= SPLIT_MAXG) return SPLIT_BAD;
+      for (uint32_t u = 0; u < 4; u++) S.ug[f][u] = (uint8_t)G;
+      S.fam[G] = (uint8_t)f;
+      S.alias[G] = 0;
+      S.gmask[G] = (uint8_t)m;
+      S.ng[f] = 1;
+      G++;
+      continue;
+    }
+    if (fnv[f]) return SPLIT_BAD;  // one window per unit needs one `now`
+    const uint32_t now = fnow[f], first = G;
+    uint32_t w[4];
+    for (uint32_t u = 0; u < 4; u++) {
+      S.ug[f][u] = SPLIT_BAD;
+      if (!((m >> u) & 1)) continue;
+      w[u] = now - now % div_of(u + 1);
+      const bool cls = per_second && u == 0;
+      uint32_t g = SPLIT_BAD;
+      for (uint32_t v = 0; v < u; v++) {
+        if (!((m >> v) & 1) || w[v] != w[u]) continue;
+        if ((per_second && v == 0) != cls) return SPLIT_BAD;  // one window in both stores
+        g = S.ug[f][v];
+      }
+      if (g == SPLIT_BAD) {
+        if (G >= SPLIT_MAXG) return SPLIT_BAD;
+        g = G++;
+        S.fam[g] = (uint8_t)f;
+        S.alias[g] = 1;
+        S.gmask[g] = 0;
+      }
+      S.ug[f][u] = (uint8_t)g;
+      S.gmask[g] |= (uint8_t)(1u << u);
+    }
+    S.ng[f] = (uint8_t)(G - first);
+    S.any_alias = 1;
+  }
+  S.G = G;
+  return G;
+}
+
+// run_flags of group g once split (s_fl: RUN_SLOW / RUN_NOWVAR of a one-unit group)
+__device__ inline uint32_t split_group_flags(const SplitPlan& S, uint32_t g, uint32_t fl) {
+  if (!S.alias[g]) return fl;
+  const uint32_t f = S.fam[g];
+  uint32_t x = RUN_ALIAS | ((uint32_t)S.gmask[g] << RUN_UMASK_SHIFT);
+  if (S.head[f] == g) x |= RUN_AHEAD | ((uint32_t)S.ng[f] << RUN_G_SHIFT);
+  return x;
+}
 
 // ---- split_long (k_split's blocks, for RUN_MULTI runs over SPLIT_CAP
 // elements): the same reordering. Under an unlucky hash key a hot stem (tens
 // of thousands of descriptors per batch at C2) shares its sort key with
 // another stem, and the one-lane exact path replayed the whole run: 1.3 ms per
-// batch on average at C2 under seed 5 (profiles/r02/seed_sweep/). Split, the
-// hot stem is an ordinary long run for the parallel path. The per-element
-// state lives in global scratch owned by the run's range: grp (the sub-run)
-// and lead (the rank inside it) are the exact path's per-position scratch,
-// which it never reads for a run it does not see, and segsum holds the
-// permutation's source until the in-run sums overwrite it. (A kernel of its
-// own with 1024-lane blocks cost every batch 4-6 us of launch on the critical
-// path, 1-3 %, profiles/r02/ab/long_*.)
+// batch on average at C2 under seed 5 (profiles/r02/seed_sweep/); a hot stem
+// under two units (an override) is such a run in every batch. Split, each
+// group is an ordinary long run for the parallel path. The per-element state
+// lives in global scratch owned by the run's range: grp (family | unit << 8,
+// then the group) and lead (the rank inside the group) are the exact path's
+// per-position scratch, which it rewrites for any run it sees; segsum (the
+// run's in-run sums) is touched only once the split is committed: it then
+// holds the permutation's source until the new sums overwrite it. (A kernel
+// of its own with 1024-lane blocks cost every batch 4-6 us of launch on the
+// critical path, 1-3 %, profiles/r02/ab/long_*.)
 constexpr uint32_t SPLIT_UNROLL = 8;
+constexpr uint32_t SPLIT_U = 4;  // elements per lane per round of the rank and sum passes (one barrier set per NT x 4)
+// k_split's workgroup: a long run's passes are rounds of SPLIT_THREADS x SPLIT_U
+// elements (256-thread blocks left the 47k-element hot runs of C2U at ~0.5 ms)
+constexpr uint32_t SPLIT_THREADS = 1024;
 
 template <uint32_t NT>
 __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j, uint32_t r, uint32_t p, uint32_t L, BatchDev b,
@@ -2355,96 +2506,146 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
                                                           uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
                                                           unsigned long long* num_runs, unsigned long long* split,
                                                           uint32_t* __restrict__ drun, uint32_t drun_cap, uint32_t* grp,
-                                                          uint32_t* rank) {
-  constexpr uint32_t NW = NT / 64;
-  __shared__ uint32_t s_w[NW][SPLIT_MAXG], s_ws[NW];
+                                                          uint32_t* rank, uint32_t* __restrict__ pos_hits,
+                                                          uint32_t* __restrict__ hnew, int per_second, uint32_t rfl) {
+  constexpr uint32_t NW = NT / 64, R = NT * SPLIT_U;
+  __shared__ uint32_t s_w[SPLIT_U][NW][SPLIT_MAXG], s_ws[NW];
   __shared__ uint32_t s_cnt[SPLIT_MAXG], s_base[SPLIT_MAXG], s_id[SPLIT_MAXG], s_fl[SPLIT_MAXG], s_off[SPLIT_MAXG];
-  __shared__ uint32_t s_lnow[SPLIT_MAXG], s_lunit[SPLIT_MAXG];
+  __shared__ uint32_t s_lnow[SPLIT_MAXG], s_lunit[SPLIT_MAXG], s_fmask[SPLIT_MAXG], s_fnv[SPLIT_MAXG];
   __shared__ uint32_t s_bad, s_lead, s_carry;
+  __shared__ SplitPlan s_plan;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   Rec* rec = const_cast<Rec*>(rec_s.rec);
+  const uint32_t* sv = rec_s.sv;  // (= svals: unchanged until the scatter)
   {
     __syncthreads();  // the previous run's shared state has been read
     if (tid == 0) s_bad = 0;
-    __syncthreads();
-    for (uint32_t k = tid; k < L; k += NT) {
-      const uint32_t e = rec_s.sv[p + k];
-      segsum[p + k] = e;
-      grp[p + k] = 0xFFu;
-      if ((rec[e].lu >> 24) & FLAG_SKIP) s_bad = 1;
+    if (tid < SPLIT_MAXG) {
+      s_fmask[tid] = 0;
+      s_fnv[tid] = 0;
     }
-    // sub-runs, as in k_split: the first unassigned element leads, and every
-    // element with its stem joins (records read SPLIT_UNROLL at a time: the
-    // scan is a chain of random reads)
-    uint32_t G = 0;
-    for (;;) {
-      if (tid == 0) s_lead = 0xFFFFFFFFu;
-      __syncthreads();
-      for (uint32_t k = tid; k < L; k += NT)
-        if (grp[p + k] == 0xFFu) {
-          atomicMin(&s_lead, k);  // this lane's first is its smallest
-          break;
-        }
-      __syncthreads();
-      const uint32_t ld = s_lead;
-      if (ld == 0xFFFFFFFFu || s_bad || G == SPLIT_MAXG) break;  // (uniform)
-      const Rec y = rec[segsum[p + ld]];
-      const Key ky = key_of(b, y);
-      if (tid == 0) {
-        s_lnow[G] = y.now;
-        s_lunit[G] = rec_unit(y);
+    __syncthreads();
+    uint32_t NF = 0;
+    // k_run_check left each non-head position's unit << 8 in grp and its
+    // max(1, hits) in pos_hits; the head's are set here
+    if (tid == 0) {
+      const Rec y = rec[sv[p]];
+      pos_hits[p] = y.hits > 1 ? y.hits : 1u;
+      if ((rfl & (RUN_UNITS | RUN_STEMS)) == RUN_UNITS) {
+        // one stem under several units (k_run_check compared every element
+        // with the head, bytes included): one family, units known
+        grp[p] = rec_unit(y) << 8;  // family 0
+        s_lnow[0] = y.now;
+        s_lunit[0] = rec_unit(y);
+        s_fnv[0] = (rfl & RUN_NOWVAR) ? 1u : 0u;
+        s_fmask[0] = ((rfl >> RUN_UMASK_SHIFT) & 0xFu) | (1u << (rec_unit(y) - 1));
       }
-      for (uint32_t k0 = tid; k0 < L; k0 += NT * SPLIT_UNROLL) {
-        Rec x[SPLIT_UNROLL];
-        bool act[SPLIT_UNROLL];
-#pragma unroll
-        for (uint32_t u = 0; u < SPLIT_UNROLL; u++) {
-          const uint32_t k = k0 + u * NT;
-          act[u] = k < L && grp[p + k] == 0xFFu;
-          if (act[u]) x[u] = rec[segsum[p + k]];
+    }
+    if ((rfl & (RUN_UNITS | RUN_STEMS)) == RUN_UNITS) {
+      NF = 1;
+    } else {
+      for (uint32_t k = tid; k < L; k += NT) {
+        grp[p + k] = 0xFFu;
+        if ((rec[sv[p + k]].lu >> 24) & FLAG_SKIP) s_bad = 1;
+      }
+      // families, as in k_split: the first unassigned element leads, and every
+      // element with its stem joins (records read SPLIT_UNROLL at a time: the
+      // scan is a chain of random reads)
+      for (;;) {
+        if (tid == 0) s_lead = 0xFFFFFFFFu;
+        __syncthreads();
+        for (uint32_t k = tid; k < L; k += NT)
+          if ((grp[p + k] & 0xFFu) == 0xFFu) {
+            atomicMin(&s_lead, k);  // this lane's first is its smallest
+            break;
+          }
+        __syncthreads();
+        const uint32_t ld = s_lead;
+        if (ld == 0xFFFFFFFFu || s_bad || NF == SPLIT_MAXG) break;  // (uniform)
+        const Rec y = rec[sv[p + ld]];
+        const Key ky = key_of(b, y);
+        if (tid == 0) {
+          s_lnow[NF] = y.now;
+          s_lunit[NF] = rec_unit(y);
         }
+        uint32_t fm = 0, nv = 0;
+        for (uint32_t k0 = tid; k0 < L; k0 += NT * SPLIT_UNROLL) {
+          Rec x[SPLIT_UNROLL];
+          bool act[SPLIT_UNROLL];
 #pragma unroll
-        for (uint32_t u = 0; u < SPLIT_UNROLL; u++) {
-          if (!act[u] || x[u].hlo != y.hlo || (x[u].lu & 0xFFFFu) != (y.lu & 0xFFFFu)) continue;
-          if (!key_equal(key_of(b, x[u]), ky)) {
-            s_bad = 1;  // equal 64-bit hash, different stem
-          } else {
-            if (rec_unit(x[u]) != rec_unit(y)) s_bad = 1;  // one stem, several units
-            grp[p + k0 + u * NT] = G;
+          for (uint32_t u = 0; u < SPLIT_UNROLL; u++) {
+            const uint32_t k = k0 + u * NT;
+            act[u] = k < L && (grp[p + k] & 0xFFu) == 0xFFu;
+            if (act[u]) x[u] = rec[sv[p + k]];
+          }
+#pragma unroll
+          for (uint32_t u = 0; u < SPLIT_UNROLL; u++) {
+            if (!act[u] || x[u].hlo != y.hlo || (x[u].lu & 0xFFFFu) != (y.lu & 0xFFFFu)) continue;
+            if (!key_equal(key_of(b, x[u]), ky)) {
+              s_bad = 1;  // equal 64-bit hash, different stem
+            } else {
+              grp[p + k0 + u * NT] = NF | (rec_unit(x[u]) << 8);
+              fm |= 1u << (rec_unit(x[u]) - 1);
+              nv |= x[u].now != y.now;
+            }
           }
         }
+        if (fm) atomicOr(&s_fmask[NF], fm);
+        if (nv) s_fnv[NF] = 1;
+        NF++;
+        __syncthreads();
       }
-      G++;
-      __syncthreads();
+      if (tid == 0 && s_lead != 0xFFFFFFFFu) s_bad = 1;  // more than SPLIT_MAXG stems
     }
-    if (tid == 0 && s_lead != 0xFFFFFFFFu) s_bad = 1;  // more than SPLIT_MAXG stems
     __syncthreads();
-    if (s_bad || G < 2) return;  // (uniform) the exact path keeps it
-    // stable ranks inside the sub-runs: per NT-element chunk, wave ballots,
-    // then the waves before this one and the chunks before this one
+    if (s_bad) return;  // (uniform) the exact path keeps it
+    if (tid == 0 && split_plan(s_plan, NF, s_fmask, s_lnow, s_fnv, per_second) == SPLIT_BAD) s_bad = 1;
+    __syncthreads();
+    const uint32_t G = s_plan.G;
+    if (s_bad || (G < 2 && !s_plan.any_alias)) return;  // (uniform) the exact path keeps it
+    // stable ranks inside the groups: per round of R = NT x SPLIT_U elements,
+    // wave ballots per group, then the slices, waves and rounds before
     if (tid < SPLIT_MAXG) s_cnt[tid] = 0;
     __syncthreads();
-    for (uint32_t c0 = 0; c0 < L; c0 += NT) {
-      const uint32_t k = c0 + tid;
-      const uint32_t gk = k < L ? grp[p + k] : 0xFFu;
-      uint32_t mine = 0;
+    for (uint32_t c0 = 0; c0 < L; c0 += R) {
+      uint32_t gk[SPLIT_U], mine[SPLIT_U];
 #pragma unroll
-      for (uint32_t g = 0; g < SPLIT_MAXG; g++) {
-        const uint64_t m = __ballot(gk == g);
-        if (gk == g) mine = __popcll(m & lt);
-        if (lane == 0) s_w[wv][g] = __popcll(m);
+      for (uint32_t u = 0; u < SPLIT_U; u++) {
+        const uint32_t k = c0 + u * NT + tid;
+        gk[u] = 0xFFu;
+        mine[u] = 0;
+        if (k < L) {
+          const uint32_t fu = grp[p + k];
+          gk[u] = s_plan.ug[fu & 0xFFu][(fu >> 8) - 1];
+          grp[p + k] = gk[u];
+        }
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < SPLIT_U; u++) {
+#pragma unroll
+        for (uint32_t g = 0; g < SPLIT_MAXG; g++) {
+          const uint64_t m = __ballot(gk[u] == g);
+          if (gk[u] == g) mine[u] = __popcll(m & lt);
+          if (lane == 0) s_w[u][wv][g] = __popcll(m);
+        }
       }
       __syncthreads();
-      if (gk < SPLIT_MAXG) {
-        uint32_t pre = s_cnt[gk];
-        for (uint32_t w = 0; w < wv; w++) pre += s_w[w][gk];
-        rank[p + k] = pre + mine;
+#pragma unroll
+      for (uint32_t u = 0; u < SPLIT_U; u++) {
+        const uint32_t g = gk[u];
+        if (g >= SPLIT_MAXG) continue;
+        uint32_t pre = s_cnt[g];
+        for (uint32_t v = 0; v < u; v++)
+          for (uint32_t w = 0; w < NW; w++) pre += s_w[v][w][g];
+        for (uint32_t w = 0; w < wv; w++) pre += s_w[u][w][g];
+        rank[p + c0 + u * NT + tid] = pre + mine[u];
       }
       __syncthreads();
       if (tid < SPLIT_MAXG) {
         uint32_t a = 0;
-        for (uint32_t w = 0; w < NW; w++) a += s_w[w][tid];
+        for (uint32_t v = 0; v < SPLIT_U; v++)
+          for (uint32_t w = 0; w < NW; w++) a += s_w[v][w][tid];
         s_cnt[tid] += a;
       }
       __syncthreads();
@@ -2455,58 +2656,89 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
         s_base[g] = acc;
         s_fl[g] = 0;
         acc += s_cnt[g];
-        if (g >= 1 && g < G && s_cnt[g] >= 2) nd2++;
+        if (g >= 1 && g < G && (s_cnt[g] >= 2 || s_plan.alias[g])) nd2++;
       }
       const unsigned long long add = ((unsigned long long)nd2 << 32) | (unsigned long long)(G - 1);
       const unsigned long long rs = atomicAdd(&split[0], add), base = split[1];
       const bool room = (uint32_t)(base >> 32) + (uint32_t)(rs >> 32) + nd2 <= drun_cap &&
                         (uint32_t)base + (uint32_t)rs + (G - 1) <= b.n;
       if (!room) {
-        s_bad = 1;
+        s_bad = 1;  // (the reservation stays: it only makes later checks stricter)
       } else {
         const unsigned long long old = atomicAdd(num_runs, add);
         s_id[0] = r;
         uint32_t di = (uint32_t)(old >> 32);
         for (uint32_t g = 1; g < G; g++) {
           s_id[g] = (uint32_t)old + g - 1;
-          if (s_cnt[g] >= 2) drun[di++] = s_id[g];
+          if (s_cnt[g] >= 2 || s_plan.alias[g]) drun[di++] = s_id[g];
         }
       }
     }
     __syncthreads();
     if (s_bad) return;  // (uniform) no room in the dup-run list: the exact path keeps it
-    for (uint32_t k = tid; k < L; k += NT) {
-      const uint32_t g = grp[p + k], np = s_base[g] + rank[p + k], e = segsum[p + k];
-      svals[p + np] = e;
-      rid[p + np] = s_id[g];
-      const Rec x = rec[e];
-      const uint32_t d = div_of(s_lunit[g]);
-      if (x.now / d != s_lnow[g] / d) atomicOr(&s_fl[g], RUN_SLOW);
-      // a sub-run of one element is a key seen once (k_table's singleton part)
-      if (s_cnt[g] == 1) rec[e].lu = x.lu & ~(FLAG_DUP << 24);
+    // committed: segsum holds the permutation's source until the new sums
+    for (uint32_t k = tid; k < L; k += NT) segsum[p + k] = sv[p + k];
+    __syncthreads();
+    // scatter (SPLIT_U elements in flight per lane): max(1, hits) moves to
+    // hnew at the new position, so the sums below read it coalesced; only a
+    // one-unit group's records are read (its clock, its lone-element flag)
+    for (uint32_t k0 = tid; k0 < L; k0 += R) {
+      uint32_t e[SPLIT_U], np[SPLIT_U], g[SPLIT_U], h[SPLIT_U];
+      Rec x[SPLIT_U];
+#pragma unroll
+      for (uint32_t u = 0; u < SPLIT_U; u++) {
+        const uint32_t k = k0 + u * NT;
+        if (k >= L) continue;
+        g[u] = grp[p + k];
+        np[u] = s_base[g[u]] + rank[p + k];
+        e[u] = segsum[p + k];
+        h[u] = pos_hits[p + k];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < SPLIT_U; u++)
+        if (k0 + u * NT < L && !s_plan.alias[g[u]]) x[u] = rec[e[u]];
+#pragma unroll
+      for (uint32_t u = 0; u < SPLIT_U; u++) {
+        if (k0 + u * NT >= L) continue;
+        svals[p + np[u]] = e[u];
+        rid[p + np[u]] = s_id[g[u]];
+        hnew[p + np[u]] = h[u];
+        if (!s_plan.alias[g[u]]) {  // (a multi-unit stem's groups share one `now`)
+          const uint32_t f = s_plan.fam[g[u]], d = div_of(s_lunit[f]);
+          if (x[u].now != s_lnow[f])
+            atomicOr(&s_fl[g[u]], x[u].now / d != s_lnow[f] / d ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR);
+          // a lone group of one element is a key seen once (k_table's singleton part)
+          if (s_cnt[g[u]] == 1) rec[e[u]].lu = x[u].lu & ~(FLAG_DUP << 24);
+        }
+      }
     }
     if (tid == 0) s_carry = 0;
     __syncthreads();
     // in-run sums of max(1, hits) in the new order: one inclusive scan over the
-    // whole run (mod 2^32, like the bucket kernels' sums), then each sub-run
-    // subtracts the total before its start
-    for (uint32_t c0 = 0; c0 < L; c0 += NT) {
-      const uint32_t k = c0 + tid;
-      uint32_t v = 0;
-      if (k < L) {
-        const uint32_t h = rec[svals[p + k]].hits;
-        v = h > 1 ? h : 1u;
+    // whole run (mod 2^32, like the bucket kernels' sums; each lane SPLIT_U
+    // consecutive elements per round), then each group subtracts the total
+    // before its start
+    for (uint32_t c0 = 0; c0 < L; c0 += R) {
+      const uint32_t k = c0 + tid * SPLIT_U;
+      uint32_t v[SPLIT_U], t = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < SPLIT_U; u++) {
+        t += k + u < L ? hnew[p + k + u] : 0u;
+        v[u] = t;
       }
+      uint32_t inc = t;
 #pragma unroll
       for (uint32_t off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(v, off, 64);
-        if (lane >= off) v += y;
+        const uint32_t y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
       }
-      if (lane == 63) s_ws[wv] = v;
+      if (lane == 63) s_ws[wv] = inc;
       __syncthreads();
-      uint32_t pre = s_carry;
+      uint32_t pre = s_carry + inc - t;
       for (uint32_t w = 0; w < wv; w++) pre += s_ws[w];
-      if (k < L) segsum[p + k] = v + pre;
+#pragma unroll
+      for (uint32_t u = 0; u < SPLIT_U; u++)
+        if (k + u < L) segsum[p + k + u] = pre + v[u];
       __syncthreads();
       if (tid == 0) {
         uint32_t a = 0;
@@ -2526,28 +2758,30 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
       const uint32_t id = s_id[tid];
       run_start[id] = p + s_base[tid];
       run_end[id] = p + s_base[tid] + s_cnt[tid];
-      run_flags[id] = s_fl[tid];
+      run_flags[id] = split_group_flags(s_plan, tid, s_fl[tid]);
     }
     if (tid == 0) defer[j] = DEFER_DONE;
   }
 }
 
 
-__global__ __launch_bounds__(256) void k_split(BatchDev b, SRec rec_s, uint32_t* __restrict__ svals,
+__global__ __launch_bounds__(SPLIT_THREADS) void k_split(BatchDev b, SRec rec_s, uint32_t* __restrict__ svals,
                                                uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
                                                uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end,
                                                uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
                                                const uint32_t* defer_n, unsigned long long* num_runs,
                                                unsigned long long* split, uint32_t* __restrict__ drun,
                                                uint32_t drun_cap, uint32_t* grp, uint32_t* rank,
-                                               const uint32_t* err) {
+                                               uint32_t* __restrict__ pos_hits, uint32_t* __restrict__ hnew,
+                                               const uint32_t* err, int per_second) {
   __shared__ uint32_t s_e[SPLIT_CAP], s_hlo[SPLIT_CAP], s_lu[SPLIT_CAP], s_now[SPLIT_CAP], s_h[SPLIT_CAP];
   __shared__ uint32_t s_nh[SPLIT_CAP];           // max(1, hits) in the new order
-  __shared__ uint16_t s_pos[SPLIT_CAP];          // rank inside the element's sub-run
-  __shared__ uint8_t s_g[SPLIT_CAP], s_ng[SPLIT_CAP];  // sub-run of each element / of each new position
+  __shared__ uint16_t s_pos[SPLIT_CAP];          // rank inside the element's group
+  __shared__ uint8_t s_g[SPLIT_CAP], s_ng[SPLIT_CAP];  // family, then group, of each element / group of each new position
   __shared__ uint32_t s_cnt[SPLIT_MAXG], s_base[SPLIT_MAXG], s_id[SPLIT_MAXG], s_fl[SPLIT_MAXG];
-  __shared__ uint32_t s_lnow[SPLIT_MAXG], s_lunit[SPLIT_MAXG];
+  __shared__ uint32_t s_lnow[SPLIT_MAXG], s_lunit[SPLIT_MAXG], s_fmask[SPLIT_MAXG], s_fnv[SPLIT_MAXG];
   __shared__ uint32_t s_bad, s_lead;
+  __shared__ SplitPlan s_plan;
   if (*err) return;
   if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -2557,13 +2791,18 @@ __global__ __launch_bounds__(256) void k_split(BatchDev b, SRec rec_s, uint32_t*
     const uint32_t r = defer[j];
     const uint32_t p = run_start[r], L = run_end[r] - p;
     if (L > SPLIT_CAP) {  // (uniform)
-      split_long_body<256>(j, r, p, L, b, rec_s, svals, segsum, rid, run_start, run_end, run_flags, defer, num_runs,
-                           split, drun, drun_cap, grp, rank);
+      split_long_body<SPLIT_THREADS>(j, r, p, L, b, rec_s, svals, segsum, rid, run_start, run_end, run_flags, defer,
+                                     num_runs, split, drun, drun_cap, grp, rank, pos_hits, hnew, per_second,
+                                     run_flags[r]);
       continue;
     }
     __syncthreads();  // the previous run's shared state has been read
     if (tid == 0) s_bad = 0;
-    for (uint32_t k = tid; k < L; k += 256) {
+    if (tid < SPLIT_MAXG) {
+      s_fmask[tid] = 0;
+      s_fnv[tid] = 0;
+    }
+    for (uint32_t k = tid; k < L; k += SPLIT_THREADS) {
       const uint32_t e = rec_s.sv[p + k];
       const Rec x = rec[e];
       s_e[k] = e;
@@ -2574,41 +2813,48 @@ __global__ __launch_bounds__(256) void k_split(BatchDev b, SRec rec_s, uint32_t*
       s_g[k] = 0xFF;
     }
     __syncthreads();
-    for (uint32_t k = tid; k < L; k += 256)
+    for (uint32_t k = tid; k < L; k += SPLIT_THREADS)
       if ((s_lu[k] >> 24) & FLAG_SKIP) s_bad = 1;
-    // sub-runs: repeatedly the first unassigned element leads, and every
+    // families: repeatedly the first unassigned element leads, and every
     // element with its stem (hash, length, then bytes) joins
-    uint32_t G = 0;
+    uint32_t NF = 0;
     for (;;) {
       if (tid == 0) s_lead = 0xFFFFFFFFu;
       __syncthreads();
-      for (uint32_t k = tid; k < L; k += 256)
+      for (uint32_t k = tid; k < L; k += SPLIT_THREADS)
         if (s_g[k] == 0xFF) atomicMin(&s_lead, k);
       __syncthreads();
       const uint32_t ld = s_lead;
-      if (ld == 0xFFFFFFFFu || s_bad || G == SPLIT_MAXG) break;  // (uniform)
+      if (ld == 0xFFFFFFFFu || s_bad || NF == SPLIT_MAXG) break;  // (uniform)
       const Rec y = rec[s_e[ld]];
       const Key ky = key_of(b, y);
       if (tid == 0) {
-        s_lnow[G] = y.now;
-        s_lunit[G] = rec_unit(y);
+        s_lnow[NF] = y.now;
+        s_lunit[NF] = rec_unit(y);
       }
-      for (uint32_t k = tid; k < L; k += 256) {
+      for (uint32_t k = tid; k < L; k += SPLIT_THREADS) {
         if (s_g[k] != 0xFF || s_hlo[k] != y.hlo || (s_lu[k] & 0xFFFFu) != (y.lu & 0xFFFFu)) continue;
         if (!key_equal(key_of(b, rec[s_e[k]]), ky)) {
           s_bad = 1;  // equal 64-bit hash, different stem
         } else {
-          if (((s_lu[k] >> 16) & 0xFFu) != rec_unit(y)) s_bad = 1;  // one stem, several units
-          s_g[k] = (uint8_t)G;
+          atomicOr(&s_fmask[NF], 1u << (((s_lu[k] >> 16) & 0xFFu) - 1));
+          if (s_now[k] != y.now) s_fnv[NF] = 1;
+          s_g[k] = (uint8_t)NF;
         }
       }
-      G++;
+      NF++;
       __syncthreads();
     }
     if (s_lead != 0xFFFFFFFFu) s_bad = 1;  // more than SPLIT_MAXG stems (or stopped early)
     __syncthreads();
-    if (s_bad || G < 2) continue;  // (uniform) the exact path keeps it
-    // stable ranks inside the sub-runs (wave 0 walks the run in arrival order)
+    if (s_bad) continue;  // (uniform) the exact path keeps it
+    if (tid == 0 && split_plan(s_plan, NF, s_fmask, s_lnow, s_fnv, per_second) == SPLIT_BAD) s_bad = 1;
+    __syncthreads();
+    const uint32_t G = s_plan.G;
+    if (s_bad || (G < 2 && !s_plan.any_alias)) continue;  // (uniform) the exact path keeps it
+    for (uint32_t k = tid; k < L; k += SPLIT_THREADS) s_g[k] = s_plan.ug[s_g[k]][((s_lu[k] >> 16) & 0xFFu) - 1];
+    __syncthreads();
+    // stable ranks inside the groups (wave 0 walks the run in arrival order)
     if (tid < 64) {
       uint32_t cnt[SPLIT_MAXG];
 #pragma unroll
@@ -2633,10 +2879,11 @@ __global__ __launch_bounds__(256) void k_split(BatchDev b, SRec rec_s, uint32_t*
           s_fl[g] = 0;
           acc += cnt[g];
         }
-        // run ids: sub-run 0 keeps r, the others are new; the dup-run list
-        // (k_table's runs part) takes the new ones of two or more elements
+        // run ids: group 0 keeps r, the others are new; the dup-run list
+        // (k_table's runs part) takes the new ones of two or more elements and
+        // every group of a multi-unit stem
         uint32_t nd2 = 0;
-        for (uint32_t g = 1; g < G; g++) nd2 += cnt[g] >= 2 ? 1u : 0u;
+        for (uint32_t g = 1; g < G; g++) nd2 += (cnt[g] >= 2 || s_plan.alias[g]) ? 1u : 0u;
         // room: a reservation (one fetch-add; a CAS loop on the shared
         // counter serialised ~100 blocks) is checked against the bucket
         // kernels' count plus every reservation before it, so the successful
@@ -2653,34 +2900,37 @@ __global__ __launch_bounds__(256) void k_split(BatchDev b, SRec rec_s, uint32_t*
           uint32_t di = (uint32_t)(old >> 32);
           for (uint32_t g = 1; g < G; g++) {
             s_id[g] = (uint32_t)old + g - 1;
-            if (cnt[g] >= 2) drun[di++] = s_id[g];
+            if (cnt[g] >= 2 || s_plan.alias[g]) drun[di++] = s_id[g];
           }
         }
       }
     }
     __syncthreads();
     if (s_bad) continue;  // (uniform) no room in the dup-run list: the exact path keeps it
-    for (uint32_t k = tid; k < L; k += 256) {
+    for (uint32_t k = tid; k < L; k += SPLIT_THREADS) {
       const uint32_t g = s_g[k], np = s_base[g] + s_pos[k];
       svals[p + np] = s_e[k];
       rid[p + np] = s_id[g];
       s_nh[np] = s_h[k];
       s_ng[np] = (uint8_t)g;
-      const uint32_t d = div_of(s_lunit[g]);
-      if (s_now[k] / d != s_lnow[g] / d) atomicOr(&s_fl[g], RUN_SLOW);
-      // a sub-run of one element is a key seen once (k_table's singleton part)
-      if (s_cnt[g] == 1) rec[s_e[k]].lu = s_lu[k] & ~(FLAG_DUP << 24);
+      if (!s_plan.alias[g]) {  // (a multi-unit stem's groups share one `now`)
+        const uint32_t f = s_plan.fam[g], d = div_of(s_lunit[f]);
+        if (s_now[k] != s_lnow[f])
+          atomicOr(&s_fl[g], s_now[k] / d != s_lnow[f] / d ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR);
+        // a lone group of one element is a key seen once (k_table's singleton part)
+        if (s_cnt[g] == 1) rec[s_e[k]].lu = s_lu[k] & ~(FLAG_DUP << 24);
+      }
     }
     __syncthreads();
-    // inclusive sums of max(1, hits) inside each sub-run, in the new order
-    // (wave 0; the sub-runs are consecutive): segmented wave scans + carry
+    // inclusive sums of max(1, hits) inside each group, in the new order
+    // (wave 0; the groups are consecutive): segmented wave scans + carry
     if (tid < 64) {
       uint32_t carry = 0;
       for (uint32_t c0 = 0; c0 < L; c0 += 64) {
         const uint32_t k = c0 + lane;
         const bool in = k < L;
         uint32_t v = in ? s_nh[k] : 0u;
-        bool f = in && (k == 0 || s_ng[k - 1] != s_ng[k]);  // a sub-run starts here
+        bool f = in && (k == 0 || s_ng[k - 1] != s_ng[k]);  // a group starts here
 #pragma unroll
         for (uint32_t off = 1; off < 64; off <<= 1) {
           const uint32_t y = __shfl_up(v, off, 64);
@@ -2690,7 +2940,7 @@ __global__ __launch_bounds__(256) void k_split(BatchDev b, SRec rec_s, uint32_t*
             f = f || yf;
           }
         }
-        if (!f) v += carry;  // no sub-run start since the chunk began
+        if (!f) v += carry;  // no group start since the chunk began
         if (in) segsum[p + k] = v;
         carry = __shfl(v, 63, 64);
       }
@@ -2699,7 +2949,7 @@ __global__ __launch_bounds__(256) void k_split(BatchDev b, SRec rec_s, uint32_t*
       const uint32_t id = s_id[tid];
       run_start[id] = p + s_base[tid];
       run_end[id] = p + s_base[tid] + s_cnt[tid];
-      run_flags[id] = s_fl[tid];
+      run_flags[id] = split_group_flags(s_plan, tid, s_fl[tid]);
     }
     if (tid == 0) defer[j] = DEFER_DONE;
   }
@@ -2797,12 +3047,211 @@ __device__ inline void fail_range(unsigned long long* res, const uint32_t* svals
   for (uint32_t q = p; q < end; q++) res[svals[q]] = pack_fail(st);
 }
 
+// ---- alias_setup (k_table's runs part, one lane): the groups of a stem that
+// lives in the table under several units, or is seen under several in this
+// batch (k_split: one group per Redis key stem ‖ windowStart, consecutive,
+// sharing one `now`). general_step's semantics, set up for the parallel path
+// (k_fast_over / fast_emit_body) instead of replayed by one lane:
+//  * a Redis key's count and EXPIRE live in every unit slot that holds a
+//    record of its window (the same store under the per-second split); its
+//    local-cache entry in every one of them;
+//  * the count a group starts from is the first such record, in unit order,
+//    still live at `now`; its local-cache hit (F) is any record's entry live
+//    at `now` — one `now` per group, so both hold for the whole group;
+//  * each unit of a group that increments gets its record of the window
+//    (rolled into cur, or a ring record; a new one takes the live local-cache
+//    expiry of the others), and the group's last INCRBY writes its count and
+//    EXPIRE to every record of the key, its local-cache Set to all of them.
+// The rolls are done before the write-back targets are resolved. A record
+// another group finds on a ring position a roll or a new record takes is out
+// of the ring's reach after this batch in either order of the descriptors, so
+// the answers agree unless it was its key's only record (checked), or unless
+// a record is out of the ring's reach now (general_step: RL_E_TIME); then —
+// rare by construction — the stem goes to the exact path untouched (returns
+// true).
+struct AliasGroup {
+  uint32_t id, p, end, mask, w;
+};
+
+__device__ __attribute__((noinline)) bool alias_setup(const TableDev& t, const Params& P, SRec rec_s, const uint32_t* __restrict__ rid,
+                                   const uint32_t* __restrict__ run_start, const uint32_t* __restrict__ run_end,
+                                   uint32_t* __restrict__ run_flags, uint4* __restrict__ run_state,
+                                   uint4* __restrict__ run_alias, uint32_t* __restrict__ run_f,
+                                   uint32_t* __restrict__ fast_blk, unsigned long long* __restrict__ res,
+                                   const uint32_t* __restrict__ svals, uint32_t* ferr, uint32_t r, uint32_t fl,
+                                   uint32_t u0, uint64_t hs, const Key& stem, uint32_t now) {
+  AliasGroup A[4];
+  uint32_t G = 1, M;
+  A[0].id = r;
+  A[0].p = run_start[r];
+  A[0].end = run_end[r];
+  if (fl & RUN_AHEAD) {
+    G = (fl >> RUN_G_SHIFT) & 0xFFu;
+    A[0].mask = (fl >> RUN_UMASK_SHIFT) & 0xFu;
+    for (uint32_t g = 1; g < G && g < 4; g++) {
+      const uint32_t id = rid[A[g - 1].end];
+      A[g].id = id;
+      A[g].p = run_start[id];
+      A[g].end = run_end[id];
+      A[g].mask = (run_flags[id] >> RUN_UMASK_SHIFT) & 0xFu;
+    }
+    if (G > 4) return true;  // (cannot happen: one group per unit at most)
+  } else {
+    A[0].mask = 1u << (u0 - 1);
+  }
+  M = 0;
+  for (uint32_t g = 0; g < G; g++) {
+    const uint32_t d = div_of(__ffs(A[g].mask));
+    A[g].w = now - now % d;
+    M |= A[g].mask;
+  }
+  // every unit slot of the stem (created for the units seen here)
+  int64_t sidx[4];
+  Win c[4];
+  uint32_t present = 0;
+  int64_t fail = 0;
+  for (uint32_t k = 0; k < 4; k++) {
+    bool ins;
+    sidx[k] = find_slot(t, hs, slot_tag(hs, k + 1), stem, k + 1, (M >> k) & 1, &ins, ferr);
+    if (sidx[k] >= 0) {
+      present |= 1u << k;
+      c[k] = t.slots[sidx[k]].cur;
+    } else if ((M >> k) & 1) {
+      fail = sidx[k];
+    }
+  }
+  if (fail) {
+    if (P.isolate)
+      for (uint32_t g = 0; g < G; g++) fail_range(res, svals, A[g].p, A[g].end, slot_fail_status(fail));
+    return false;  // (else find_slot set the batch's error)
+  }
+  // The ring position each unit of a group may write (before F is known):
+  // the old cur's, rolled into the ring, or the group's window's (a ring
+  // record). A record another group finds there is gone once the write is
+  // done: such a record is then out of the ring's reach for good, so only the
+  // starting state of this batch could tell the two orders of the batch's
+  // descriptors apart.
+  uint32_t wpos[4];  // per unit: the window whose ring position may be written (WS_INVALID: none)
+  for (uint32_t k = 0; k < 4; k++) wpos[k] = WS_INVALID;
+  for (uint32_t g = 0; g < G; g++)
+    for (uint32_t k = 0; k < 4; k++)
+      if (((A[g].mask >> k) & 1) && c[k].ws != A[g].w)
+        wpos[k] = (c[k].ws == WS_INVALID || A[g].w > c[k].ws) ? c[k].ws : A[g].w;
+  // the groups' starting state, from the records as they are, with and
+  // without such doomed records: the alias records of one key carry one
+  // count, EXPIRE and local-cache expiry, so the two agree unless a doomed
+  // record was the only one — then the exact path decides in arrival order
+  uint32_t v0[4], lcm[4], F[4];
+  for (uint32_t g = 0; g < G; g++) {
+    const uint32_t w = A[g].w;
+    const bool cls = P.per_second && (A[g].mask & 1u);
+    bool vf = false, vfx = false;
+    uint32_t v0x = 0, lcmx = 0;
+    v0[g] = 0;
+    lcm[g] = 0;
+    for (uint32_t k = 0; k < 4; k++) {
+      if (!((present >> k) & 1)) continue;
+      const uint32_t d = div_of(k + 1);
+      Win R;
+      bool doomed = false;
+      if (c[k].ws == w) {
+        R = c[k];
+      } else if (c[k].ws == WS_INVALID || w > c[k].ws || w % d) {
+        continue;  // (unit k's keys are multiples of its div)
+      } else {
+        R = t.hist[sidx[k]].w[hist_pos(w, d)];
+        if (R.ws != w) {
+          // never written, or lost from the ring while it could be live
+          if (!hist_reach(w, c[k].ws, d) && now - w < 2u * d) return true;
+          continue;
+        }
+        doomed = wpos[k] != WS_INVALID && wpos[k] != w && hist_pos(wpos[k], d) == hist_pos(w, d);
+      }
+      const bool live = (P.per_second && k == 0) == cls && now <= R.expire;
+      lcm[g] = R.lc > lcm[g] ? R.lc : lcm[g];
+      if (!vf && live) {
+        v0[g] = R.count;
+        vf = true;
+      }
+      if (doomed) continue;
+      lcmx = R.lc > lcmx ? R.lc : lcmx;
+      if (!vfx && live) {
+        v0x = R.count;
+        vfx = true;
+      }
+    }
+    if (v0x != v0[g] || lcmx != lcm[g]) return true;
+    F[g] = (P.lc_en && now < lcm[g]) ? 1u : 0u;
+  }
+  // the new cur of each unit that rolls (groups that increment)
+  Win cn[4];
+  for (uint32_t k = 0; k < 4; k++) cn[k] = c[k];
+  for (uint32_t g = 0; g < G; g++)
+    for (uint32_t k = 0; k < 4; k++)
+      if (!F[g] && ((A[g].mask >> k) & 1) && (c[k].ws == WS_INVALID || A[g].w > c[k].ws))
+        cn[k] = Win{A[g].w, 0, 0, lcm[g]};
+  // commit: rolls and new ring records
+  for (uint32_t g = 0; g < G; g++) {
+    if (F[g]) continue;
+    for (uint32_t k = 0; k < 4; k++) {
+      if (!((A[g].mask >> k) & 1) || c[k].ws == A[g].w) continue;
+      const uint32_t d = div_of(k + 1);
+      if (c[k].ws == WS_INVALID || A[g].w > c[k].ws) {
+        if (c[k].ws != WS_INVALID) t.hist[sidx[k]].w[hist_pos(c[k].ws, d)] = c[k];
+        t.slots[sidx[k]].cur = cn[k];
+      } else {
+        Win* rr = &t.hist[sidx[k]].w[hist_pos(A[g].w, d)];
+        if (rr->ws != A[g].w) *rr = Win{A[g].w, 0, 0, lcm[g]};
+      }
+    }
+  }
+  if (__popc(present) >= 2)
+    for (uint32_t k = 0; k < 4; k++)
+      if ((present >> k) & 1) t.slots[sidx[k]].flags |= SLOT_EXACT;
+  const uint4 sl = make_uint4(present & 1 ? (uint32_t)sidx[0] : 0xFFFFFFFFu, present & 2 ? (uint32_t)sidx[1] : 0xFFFFFFFFu,
+                              present & 4 ? (uint32_t)sidx[2] : 0xFFFFFFFFu, present & 8 ? (uint32_t)sidx[3] : 0xFFFFFFFFu);
+  // write-back targets (3 bits per unit: a record of w, in the ring, same store)
+  for (uint32_t g = 0; g < G; g++) {
+    const uint32_t w = A[g].w;
+    const bool cls = P.per_second && (A[g].mask & 1u);
+    uint32_t tm = 0;
+    if (!F[g]) {
+      for (uint32_t k = 0; k < 4; k++) {
+        if (!((present >> k) & 1)) continue;
+        const uint32_t d = div_of(k + 1);
+        uint32_t bits = 0;
+        if (cn[k].ws == w) {
+          bits = 1;
+        } else if (cn[k].ws != WS_INVALID && w < cn[k].ws && w % d == 0 &&
+                   t.hist[sidx[k]].w[hist_pos(w, d)].ws == w) {
+          bits = 3;
+        }
+        if (bits && (P.per_second && k == 0) == cls) bits |= 4;
+        tm |= bits << (3 * k);
+      }
+    }
+    const uint32_t id = A[g].id;
+    run_state[id] = make_uint4(tm, v0[g], lcm[g], F[g]);
+    run_alias[id] = sl;
+    run_f[id] = 0xFFFFFFFFu;
+    run_flags[id] = (g == 0 ? fl : run_flags[id]) | RUN_FAST | RUN_ALIAS;
+    const uint32_t b0 = A[g].p >> 8, b1 = (A[g].end - 1) >> 8;
+    for (uint32_t x = b0 >> 5; x <= b1 >> 5; x++) {
+      const uint32_t lo = x == (b0 >> 5) ? (b0 & 31) : 0u, hi = x == (b1 >> 5) ? (b1 & 31) : 31u;
+      atomicOr(&fast_blk[x], (0xFFFFFFFFu >> (31 - hi)) & (0xFFFFFFFFu << lo));
+    }
+  }
+  return false;
+}
+
+
 __device__ __attribute__((always_inline)) inline void runs_body(uint32_t blk, BatchDev b, TableDev t, Params P, SRec rec_s,
                                               const uint32_t* __restrict__ skeys,
                                               const uint32_t* __restrict__ svals, unsigned long long* __restrict__ res,
                                               const uint32_t* __restrict__ run_start,
                                               const uint32_t* __restrict__ run_end,
                                               uint32_t* __restrict__ run_flags, uint4* __restrict__ run_state,
+                                              uint4* __restrict__ run_alias, const uint32_t* __restrict__ rid,
                                               uint32_t* __restrict__ run_f, const unsigned long long* num_runs,
                                               const uint32_t* __restrict__ drun,
                                               uint32_t* __restrict__ defer, uint32_t* defer_n,
@@ -2822,7 +3271,10 @@ __device__ __attribute__((always_inline)) inline void runs_body(uint32_t blk, Ba
   // the dup-run list, compacted once more (a large bucket's hot-key run left
   // to its fallback path is empty)
   const uint32_t cnt =
-      block_compact(lo, hi, s_list, &s_cnt, [&](uint32_t j) { return run_end[drun[j]] - run_start[drun[j]] >= 2; });
+      block_compact(lo, hi, s_list, &s_cnt, [&](uint32_t j) {
+        const uint32_t r = drun[j];
+        return run_end[r] - run_start[r] >= 2 || (run_flags[r] & RUN_ALIAS);  // (a multi-unit stem's groups: any size)
+      });
   // Waves without a run leave at once (no block barrier after this point):
   // stats go wave by wave to this block's stripe (or straight to the output
   // past LDS_RULES rules), not through a block-wide LDS table.
@@ -2843,8 +3295,17 @@ __device__ __attribute__((always_inline)) inline void runs_body(uint32_t blk, Ba
     SlotImg im;
     load_img_lo(&t.slots[h0 >> t.shift], im);  // home slot's first sector, in flight beside the stem
     const Key k0 = key_of(b, x0);
-    // RUN_MULTI runs belong to the exact path (k_late); a run of one failed descriptor is done
-    if (!(fl & RUN_MULTI) && !(rec_flags(x0) & FLAG_SKIP)) {
+    if (fl & RUN_AHEAD) {
+      // the groups of a stem seen under several units (k_split): set up together
+      if (restore || alias_setup(t, P, rec_s, rid, run_start, run_end, run_flags, run_state, run_alias, run_f, fast_blk,
+                                 res, svals, ferr, r, fl, u0, h0, k0, x0.now)) {
+        if (((fl >> RUN_G_SHIFT) & 0xFFu) > 1) run_flags[r] = fl | RUN_MERGE;  // exact path: every group, merged
+        defer[atomicAdd(defer_n, 1u)] = r;
+      }
+    } else if (fl & RUN_ALIAS) {
+      // a later group of such a stem: its head's lane set it up
+    } else if (!(fl & RUN_MULTI) && !(rec_flags(x0) & FLAG_SKIP)) {
+      // (RUN_MULTI runs belong to the exact path (k_late); a run of one failed descriptor is done)
       const bool long_run = !restore && end - p >= LONG_RUN && !(fl & RUN_SLOW);
       bool ok = true;
       int64_t s0 = -1;
@@ -2927,6 +3388,11 @@ __device__ __attribute__((always_inline)) inline void runs_body(uint32_t blk, Ba
         }
       } else if (s0 == SLOT_TABLE_FULL || s0 == SLOT_ARENA_FULL) {
         if (P.isolate) fail_range(res, svals, p, end, slot_fail_status(s0));  // else the batch fails
+      } else if (s0 >= 0 && !restore && !(fl & (RUN_SLOW | RUN_NOWVAR)) && !(RL_ABL & 1)) {
+        // a stem that lives under several units: the parallel path over every unit slot
+        if (alias_setup(t, P, rec_s, rid, run_start, run_end, run_flags, run_state, run_alias, run_f, fast_blk, res,
+                        svals, ferr, r, fl, u0, h0, k0, x0.now))
+          defer[atomicAdd(defer_n, 1u)] = r;
       } else {
         defer[atomicAdd(defer_n, 1u)] = r;
       }
@@ -2977,6 +3443,7 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
                                                    const uint32_t* __restrict__ run_end,
                                                    const uint32_t* __restrict__ run_flags,
                                                    const uint4* __restrict__ run_state,
+                                                   const uint4* __restrict__ run_alias,
                                                    const uint32_t* __restrict__ run_f, unsigned long long* stats,
                                                    unsigned long long* stripes, const uint32_t* err,
                                                    const uint32_t* __restrict__ fast_blk) {
@@ -2996,7 +3463,8 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
   L.reset();
   const uint32_t q = blk * 256 + threadIdx.x;
   const uint32_t r = q < n ? rid[q] : 0u;
-  if (q < n && (run_flags[r] & RUN_FAST)) {
+  const uint32_t fl = q < n ? run_flags[r] : 0u;
+  if (fl & RUN_FAST) {
     const uint4 st = run_state[r];
     if (st.w & 4u) {  // the run's window is older than the key's history (isolate): RL_E_TIME
       res[svals[q]] = pack_fail(RL_E_TIME);
@@ -3004,11 +3472,11 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
       const uint32_t f = run_f[r];
       const bool F = st.w & 1u;
       const Elem x = load_elem(rec_s[q], svals[q], false);
-      uint32_t req_f = 0xFFFFFFFFu, now_f = 0;
+      uint32_t req_f = 0xFFFFFFFFu, lc_f = 0;
       if (P.lc_en && f != 0xFFFFFFFFu) {
         const Rec xf = rec_s[f];
         req_f = xf.req;
-        now_f = xf.now;
+        lc_f = xf.now + div_of(rec_unit(xf));  // freecache Set with the over-limit descriptor's ttl
       }
       const bool masked = F || x.req > req_f;  // local-cache hit
       const uint32_t after = masked ? 0u : st.y + segsum[q];
@@ -3017,12 +3485,26 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
       if (!masked) {
         const uint32_t nq = q + 1;
         const bool last = nq == run_end[r] || rec_s[nq].req > req_f;
-        if (last) {  // the last INCRBY of the run leaves the key's state
+        if (last && (fl & RUN_ALIAS)) {  // the key's records in every unit slot (alias_setup's targets)
+          const uint4 sl = run_alias[r];
+#pragma unroll
+          for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t bits = (st.x >> (3 * k)) & 7u;
+            if (!(bits & 1u)) continue;
+            const uint32_t idx = k == 0 ? sl.x : k == 1 ? sl.y : k == 2 ? sl.z : sl.w;
+            Win* R = (bits & 2u) ? &t.hist[idx].w[hist_pos(x.w, div_of(k + 1))] : &t.slots[idx].cur;
+            if (bits & 4u) {  // same store: INCRBY + EXPIRE
+              R->count = after;
+              R->expire = x.now + x.d;
+            }
+            if (req_f != 0xFFFFFFFFu) R->lc = lc_f;
+          }
+        } else if (last) {  // the last INCRBY of the run leaves the key's state
           Win R;
           R.ws = x.w;
           R.count = after;
           R.expire = x.now + x.d;
-          R.lc = (req_f != 0xFFFFFFFFu) ? now_f + x.d : st.z;
+          R.lc = (req_f != 0xFFFFFFFFu) ? lc_f : st.z;
           if (st.w & 2u) t.hist[st.x].w[hist_pos(x.w, x.d)] = R;  // a ring record
           else t.slots[st.x].cur = R;
         }
@@ -3096,6 +3578,8 @@ __device__ __attribute__((always_inline)) inline void general_body(uint32_t blk,
                                                       uint32_t* __restrict__ grp, uint32_t* __restrict__ lead,
                                                       uint8_t* __restrict__ gmask, const uint32_t* __restrict__ keys0,
                                                       const uint32_t* __restrict__ defer1, const uint32_t* defer1_n,
+                                                      const uint32_t* __restrict__ run_flags,
+                                                      const uint32_t* __restrict__ rid,
                                                       unsigned long long* stats, unsigned long long* stripes,
                                                       uint32_t* err, uint32_t* errs, int restore) {
   __shared__ uint32_t s_err, s_na, s_n, s_n1;
@@ -3121,6 +3605,38 @@ __device__ __attribute__((always_inline)) inline void general_body(uint32_t blk,
     if (rr == DEFER_DONE) continue;  // split into ordinary runs (k_split)
     const uint32_t p = run_start[rr], end = run_end[rr];
     const uint32_t key = skeys[p];
+    const uint32_t rfl = di < s_na ? 0u : run_flags[rr];  // (defer_a: RUN_MULTI runs as the bucket kernels left them)
+    if (rfl & RUN_MERGE) {
+      // the groups of one stem seen under several units (k_split ordered them
+      // by Redis key): replayed exactly, merged back into arrival order
+      constexpr uint32_t MG = 4;
+      uint32_t cq[MG], ce[MG], um = (rfl >> RUN_UMASK_SHIFT) & 0xFu;
+      const uint32_t G = min((rfl >> RUN_G_SHIFT) & 0xFFu, MG);
+      cq[0] = p;
+      ce[0] = end;
+      for (uint32_t g = 1; g < G; g++) {
+        const uint32_t id = rid[ce[g - 1]];
+        cq[g] = run_start[id];
+        ce[g] = run_end[id];
+        um |= (run_flags[id] >> RUN_UMASK_SHIFT) & 0xFu;
+      }
+      const Rec y = rec_s[p];
+      stem_exact(t, P, res, L, acc, ferr, restore, ((uint64_t)key << 32) | y.hlo, key_at(b, rec_s, p), um,
+                 [&](auto&& f) {
+                   for (;;) {
+                     uint32_t bg = MG, be = 0xFFFFFFFFu;
+                     for (uint32_t g = 0; g < G; g++)
+                       if (cq[g] < ce[g] && svals[cq[g]] < be) {
+                         be = svals[cq[g]];
+                         bg = g;
+                       }
+                     if (bg == MG) break;
+                     f(load_elem(rec_s[cq[bg]], be, restore));
+                     cq[bg]++;
+                   }
+                 });
+      continue;
+    }
     // ---- split the run into distinct stems (hash, length, then bytes)
     uint32_t ng = 0;
     for (uint32_t q = p; q < end; q++) {
@@ -3198,13 +3714,17 @@ __device__ __attribute__((always_inline)) inline void general_body(uint32_t blk,
 //
 // k_table: the runs of two or more (runs_body, blocks [0, g_runs)) and the keys
 // seen once (unique_body, the rest).
-__global__ __launch_bounds__(256) void k_table(uint32_t g_runs, BatchDev b, TableDev t, Params P, SRec rec_s,
+#ifndef RL_KTABLE_WAVES
+#define RL_KTABLE_WAVES 1  // (A/B builds: a floor on k_table's waves per SIMD)
+#endif
+__global__ __launch_bounds__(256, RL_KTABLE_WAVES) void k_table(uint32_t g_runs, BatchDev b, TableDev t, Params P, SRec rec_s,
                                                const uint32_t* __restrict__ skeys,
                                                const uint32_t* __restrict__ svals,
                                                unsigned long long* __restrict__ res,
                                                const uint32_t* __restrict__ run_start,
                                                const uint32_t* __restrict__ run_end, uint32_t* __restrict__ run_flags,
-                                               uint4* __restrict__ run_state, uint32_t* __restrict__ run_f,
+                                               uint4* __restrict__ run_state, uint4* __restrict__ run_alias,
+                                               const uint32_t* __restrict__ rid, uint32_t* __restrict__ run_f,
                                                const unsigned long long* num_runs, const uint32_t* __restrict__ drun,
                                                uint32_t* __restrict__ defer2, uint32_t* defer2_n,
                                                const uint32_t* __restrict__ keys0, uint32_t* __restrict__ defer1,
@@ -3212,8 +3732,8 @@ __global__ __launch_bounds__(256) void k_table(uint32_t g_runs, BatchDev b, Tabl
                                                unsigned long long* stripes, uint32_t* err, uint32_t* errs, int restore,
                                                uint32_t* __restrict__ fast_blk) {
   if (blockIdx.x < g_runs)
-    runs_body(blockIdx.x, b, t, P, rec_s, skeys, svals, res, run_start, run_end, run_flags, run_state, run_f,
-              num_runs, drun, defer2, defer2_n, stats, stripes, err, errs, restore, fast_blk);
+    runs_body(blockIdx.x, b, t, P, rec_s, skeys, svals, res, run_start, run_end, run_flags, run_state, run_alias, rid,
+              run_f, num_runs, drun, defer2, defer2_n, stats, stripes, err, errs, restore, fast_blk);
   else
     unique_body(blockIdx.x - g_runs, b, t, P, rec_s.rec, keys0, res, defer1, defer1_n, stats, stripes, err, errs,
                 restore);
@@ -3242,17 +3762,18 @@ __global__ __launch_bounds__(256, 8) void k_late(BatchDev b, TableDev t, Params 
                                                  const uint32_t* __restrict__ defer1, const uint32_t* defer1_n,
                                                  const uint32_t* __restrict__ segsum, const uint32_t* __restrict__ rid,
                                                  const uint32_t* __restrict__ run_flags,
-                                                 const uint4* __restrict__ run_state, const uint32_t* __restrict__ run_f,
+                                                 const uint4* __restrict__ run_state,
+                                                 const uint4* __restrict__ run_alias, const uint32_t* __restrict__ run_f,
                                                  unsigned long long* stats, unsigned long long* stripes, uint32_t* err,
                                                  uint32_t* errs, int restore, const uint32_t* __restrict__ fast_blk,
                                                  const uint32_t* sorted_n) {
   if (blockIdx.x < RUNS_GENERAL_LATE_BLOCKS)
     general_body(blockIdx.x, RUNS_GENERAL_LATE_BLOCKS, b, t, P, rec_s, skeys, svals, res, run_start, run_end, defer,
-                 defer_n, defer2, defer2_n, grp, lead, gmask, keys0, defer1, defer1_n, stats, stripes, err, errs,
-                 restore);
+                 defer_n, defer2, defer2_n, grp, lead, gmask, keys0, defer1, defer1_n, run_flags, rid, stats, stripes,
+                 err, errs, restore);
   else if (!restore)
     fast_emit_body(blockIdx.x - RUNS_GENERAL_LATE_BLOCKS, sorted_n, b.n_rules, t, P, rec_s, svals, res, segsum, rid,
-                   run_start, run_end, run_flags, run_state, run_f, stats, stripes, err, fast_blk);
+                   run_start, run_end, run_flags, run_state, run_alias, run_f, stats, stripes, err, fast_blk);
 }
 
 // First kernel of the table stage: merge this batch's validation errors into
@@ -3434,7 +3955,8 @@ static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b -
 // whose sort key occurs more than once. Uses only this buffer's scratch and its
 // validation word s.err. Sorted keys go to keys[1] (keys[0] keeps the arrival
 // order for k_table's keys seen once), the sort permutation to vals[0].
-void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_t st, hipEvent_t* ev) {
+void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_second, hipStream_t st,
+                    hipEvent_t* ev) {
   const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
   if (ev) (void)hipEventRecord(ev[0], st);
   if (g0)
@@ -3465,10 +3987,11 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, hipStream_
 #endif
     k_run_check<<<cdiv(b.n, RC_CHUNK), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[1], s.rid, s.run_start,
                                                 s.run_flags, s.defer, s.defer_n, s.err, s.runs64, s.split,
-                                                s.sorted_n);
-    k_split<<<SPLIT_BLOCKS, 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.vals[0], s.segsum, s.rid, s.run_start,
+                                                s.sorted_n, s.grp, s.hit_t);
+    k_split<<<SPLIT_BLOCKS, SPLIT_THREADS, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.vals[0], s.segsum, s.rid, s.run_start,
                                           s.run_end, s.run_flags, s.defer, s.defer_n, s.runs64, s.split, s.drun,
-                                          b.n / 2 + BIG_HEAVY * PART_DIGITS, s.grp, s.lead, s.err);
+                                          b.n / 2 + BIG_HEAVY * PART_DIGITS, s.grp, s.lead, s.hit_t, s.vals[1], s.err,
+                                          per_second);
   }
 }
 
@@ -3491,7 +4014,8 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     if (ev) (void)hipEventRecord(ev[3], st);
     const uint32_t g_runs = cdiv(b.n / 2 + BIG_HEAVY * PART_DIGITS, 256);
     k_table<<<g_runs + g, 256, lds, st>>>(g_runs, b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end,
-                                         s.run_flags, s.run_state, s.run_f, s.runs64, s.drun, s.defer2, s.defer2_n,
+                                         s.run_flags, s.run_state, s.run_alias, s.rid, s.run_f, s.runs64, s.drun,
+                                         s.defer2, s.defer2_n,
                                          s.keys[0], s.defer1, s.defer1_n, o.stats, s.stripes, s.errb, s.errs, restore,
                                          s.fast_blk);
     if (ev) (void)hipEventRecord(ev[4], st);
@@ -3500,7 +4024,8 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     k_late<<<RUNS_GENERAL_LATE_BLOCKS + (restore ? 0u : g), 256, lds, st>>>(
         b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer, s.defer_n, s.defer2, s.defer2_n,
         s.grp, s.lead, s.gmask,
-        s.keys[0], s.defer1, s.defer1_n, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, o.stats, s.stripes, s.errb,
+        s.keys[0], s.defer1, s.defer1_n, s.segsum, s.rid, s.run_flags, s.run_state, s.run_alias, s.run_f, o.stats,
+        s.stripes, s.errb,
         s.errs, restore, s.fast_blk, s.sorted_n);
     if (!restore) {
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;

@@ -171,6 +171,15 @@ class Backend:
         check(self.ctx, lib().rl_do_limit_host_async(self.ctx, C.byref(b), C.byref(r)))
         return b, r  # (the structs the call read; kept by the caller with the arrays)
 
+    def do_limit_compact_async(self, cb, out: dict):
+        """rl_do_limit_compact_async: a CompactBatch (packing.compact_batch; its
+        buffer pinned for an asynchronous copy) in, out as do_limit_host_async;
+        final after synchronize()."""
+        r = abi.make_result_struct(out)
+        s = cb.struct()
+        check(self.ctx, lib().rl_do_limit_compact_async(self.ctx, C.byref(s), C.byref(r)))
+        return s, r
+
     # ---- config match + DoLimit on raw requests (rl_match.hip)
     def load_config(self, tree) -> None:
         """rl_config_load: ``tree`` is a ratelimit_amd.config.ConfigTree."""

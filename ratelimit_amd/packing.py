@@ -126,3 +126,65 @@ def slice_requests(arrays: Dict[str, np.ndarray], n: int, n_requests: int, r0: i
     for k in ("unit", "flags", "limit", "hits", "rule_id"):
         out[k] = np.ascontiguousarray(arrays[k][d0:d1])
     return out, d1 - d0, r1 - r0
+
+
+@dataclass
+class CompactBatch:
+    """An rl_batch_compact: one contiguous buffer (``buf``, uint8) and the byte
+    offsets of its sections (include/ratelimit_hip.h)."""
+    buf: np.ndarray
+    n: int
+    n_requests: int
+    n_rules: int
+    n_limits: int
+    offsets: Dict[str, int]
+
+    def struct(self):
+        s = abi.RlBatchCompact()
+        s.n, s.n_requests, s.n_rules, s.n_limits = self.n, self.n_requests, self.n_rules, self.n_limits
+        s.buf = abi.ptr(self.buf)
+        s.buf_bytes = int(self.buf.size)
+        for k, v in self.offsets.items():
+            setattr(s, k, int(v))
+        return s
+
+    def alloc_result(self, isolate: bool = False):
+        return PackedBatch({}, self.n, self.n_requests, self.n_rules).alloc_result(isolate)
+
+
+def compact_batch(arrays: Dict[str, np.ndarray], n: int, n_requests: int, n_rules: int, alloc=None) -> CompactBatch:
+    """The compact (PCIe) layout of a packed batch: per request its clock (u32),
+    HitsAddend and first descriptor, per descriptor its stem and an index into
+    the table of the batch's distinct (limit, rule, unit, flags). `hits` must be
+    one value per request (HitsAddend is a request field). alloc(nbytes) -> a
+    uint8 array for the buffer (default numpy; PinnedArena.array for pinned)."""
+    req = np.asarray(arrays["req_idx"][:n], np.int64)
+    hits_d = np.asarray(arrays["hits"][:n], np.uint32)
+    first = np.searchsorted(req, np.arange(n_requests + 1), side="left").astype(np.uint32)
+    if n and np.any(hits_d != np.asarray(arrays["hits"], np.uint32)[np.minimum(first[req], n - 1)]):
+        raise ValueError("hits differ inside a request (HitsAddend is per request)")
+    hits_q = np.zeros(n_requests, np.uint32)
+    has = first[1:] > first[:-1]
+    hits_q[has] = hits_d[first[:-1][has]]
+    key = np.zeros(n, abi.LIMIT_DTYPE)
+    key["requests_per_unit"] = arrays["limit"][:n]
+    key["rule_id"] = arrays["rule_id"][:n]
+    key["unit"] = arrays["unit"][:n]
+    key["flags"] = arrays["flags"][:n]
+    table, idx = np.unique(key, return_inverse=True)
+    if table.size > 65536:
+        raise ValueError("more than 65536 distinct limits in one batch")
+    stem_off = np.asarray(arrays["stem_off"][:n + 1], np.uint32)
+    nb = int(stem_off[n]) if n else 0
+    now = np.asarray(arrays["now"][:n_requests], np.int64)
+    sections = [("stem_off", stem_off), ("req_first", first), ("now", now.astype(np.uint32)), ("hits", hits_q),
+                ("limits", table), ("limit_idx", idx.astype(np.uint16)),
+                ("stem_bytes", np.asarray(arrays["stem_bytes"][:nb], np.uint8))]
+    offsets, pos = {}, 0
+    for k, a in sections:
+        offsets[k] = pos
+        pos += (a.nbytes + 3) & ~3
+    buf = np.zeros(max(pos, 4), np.uint8) if alloc is None else alloc(max(pos, 4))
+    for k, a in sections:
+        buf[offsets[k]:offsets[k] + a.nbytes] = np.frombuffer(a.tobytes(), np.uint8)
+    return CompactBatch(buf[:max(pos, 4)], n, n_requests, n_rules, int(table.size), offsets)

@@ -132,6 +132,38 @@ def c2_stream(seed=0xC2, n_tenants=10_000_000, requests_per_batch=500_000, batch
         yield c1_batch(t, now0 + k, h)
 
 
+def c2u_batch(t, now, h, rng, hot=16, p_override=0.5, override_limit=20_000):
+    """A C2 batch where requests of the `hot` hottest tenants carry, with
+    probability p_override, a per-request override on their ``tier=sec``
+    descriptor whose unit is MINUTE (config_impl.go:254-265: a fresh RateLimit,
+    its own stats key, rule id 2). The same stem is then seen under SECOND and
+    MINUTE: a Redis key shared by both units whenever t % 60 == 0
+    (cache_key.go:73-74), two independent keys otherwise."""
+    a, n, nq, _ = c1_batch(t, now, h)
+    ov = (np.asarray(t) < hot) & (rng.random(nq) < p_override)
+    idx = 2 * np.nonzero(ov)[0]  # the request's sec descriptor
+    a["unit"][idx] = 2
+    a["limit"][idx] = override_limit
+    a["rule_id"][idx] = 2
+    return a, n, nq, 3
+
+
+def c2u_stream(seed=0xC2, n_tenants=10_000_000, requests_per_batch=500_000, batches=4, now0=NOW0, s=1.1,
+               sampler=None, hot=16, p_override=0.5, now_per_request=None):
+    """C2 plus hot-tenant overrides in a second unit (c2u_batch). now_per_request:
+    optional callable (batch k, nq) -> int64[nq] clock per request."""
+    rng = np.random.default_rng(seed)
+    z = sampler or ZipfSampler(n_tenants, s)
+    for k in range(batches):
+        t = z.sample(rng, requests_per_batch)
+        h = rng.integers(1, 9, requests_per_batch).astype(np.uint32)
+        now = now0 + k if now_per_request is None else now_per_request(k, requests_per_batch)
+        yield c2u_batch(t, now, h, rng, hot, p_override)
+
+
+C2U_RULES = C1_RULES + ["bench.tenant.tier_sec(override:minute)"]
+
+
 def c0_batch(values, now_per_request):
     """C0: domain mongo_cps, descriptor [(database, v)], one per request."""
     values = np.asarray(values, np.int64)  # -2 users, -1 default, >=0 db%04d

@@ -27,6 +27,15 @@ int main(void) {
   F(rl_batch, stem_off); F(rl_batch, now); F(rl_batch, req_idx); F(rl_batch, unit); F(rl_batch, flags);
   F(rl_batch, limit); F(rl_batch, hits); F(rl_batch, rule_id);
 
+  S(rl_limit);
+  F(rl_limit, requests_per_unit); F(rl_limit, rule_id); F(rl_limit, unit); F(rl_limit, flags); F(rl_limit, reserved);
+
+  S(rl_batch_compact);
+  F(rl_batch_compact, n); F(rl_batch_compact, n_requests); F(rl_batch_compact, n_rules);
+  F(rl_batch_compact, n_limits); F(rl_batch_compact, buf); F(rl_batch_compact, buf_bytes);
+  F(rl_batch_compact, stem_bytes); F(rl_batch_compact, stem_off); F(rl_batch_compact, limit_idx);
+  F(rl_batch_compact, req_first); F(rl_batch_compact, now); F(rl_batch_compact, hits); F(rl_batch_compact, limits);
+
   S(rl_result);
   F(rl_result, code); F(rl_result, limit_remaining); F(rl_result, reset_s); F(rl_result, stats);
   F(rl_result, status);
