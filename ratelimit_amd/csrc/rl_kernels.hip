@@ -2493,10 +2493,14 @@ __device__ inline uint32_t split_group_flags(const SplitPlan& S, uint32_t g, uin
 // of its own with 1024-lane blocks cost every batch 4-6 us of launch on the
 // critical path, 1-3 %, profiles/r02/ab/long_*.)
 constexpr uint32_t SPLIT_UNROLL = 8;
-constexpr uint32_t SPLIT_U = 4;  // elements per lane per round of the rank and sum passes (one barrier set per NT x 4)
-// k_split's workgroup: a long run's passes are rounds of SPLIT_THREADS x SPLIT_U
-// elements (256-thread blocks left the 47k-element hot runs of C2U at ~0.5 ms)
-constexpr uint32_t SPLIT_THREADS = 1024;
+constexpr uint32_t SPLIT_U = 8;  // elements per lane per round of the rank, scatter and sum passes (one barrier set per NT x 8)
+constexpr uint32_t SPLIT_E = 16;  // elements in flight per lane in the elementwise passes
+// k_split's workgroup (a long run's passes are rounds of SPLIT_THREADS x SPLIT_U
+// elements; every pass is a chain of such rounds, each waiting on memory)
+#ifndef RL_SPLIT_THREADS
+#define RL_SPLIT_THREADS 256  // (1024: C2U's 58k-element runs 481 -> 377 us, but C1's k_split 18 -> 26 us)
+#endif
+constexpr uint32_t SPLIT_THREADS = RL_SPLIT_THREADS;
 
 template <uint32_t NT>
 __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j, uint32_t r, uint32_t p, uint32_t L, BatchDev b,
@@ -2519,6 +2523,13 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
   Rec* rec = const_cast<Rec*>(rec_s.rec);
   const uint32_t* sv = rec_s.sv;  // (= svals: unchanged until the scatter)
   {
+#ifdef RL_SPLIT_PROF  // (measurement builds: phase stamps of long runs, printed by one lane)
+    uint64_t ts[8];
+    ts[0] = wall_clock64();
+#define SPLIT_STAMP(i) ts[i] = wall_clock64()
+#else
+#define SPLIT_STAMP(i)
+#endif
     __syncthreads();  // the previous run's shared state has been read
     if (tid == 0) s_bad = 0;
     if (tid < SPLIT_MAXG) {
@@ -2604,6 +2615,7 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
     __syncthreads();
     const uint32_t G = s_plan.G;
     if (s_bad || (G < 2 && !s_plan.any_alias)) return;  // (uniform) the exact path keeps it
+    SPLIT_STAMP(1);
     // stable ranks inside the groups: per round of R = NT x SPLIT_U elements,
     // wave ballots per group, then the slices, waves and rounds before
     if (tid < SPLIT_MAXG) s_cnt[tid] = 0;
@@ -2650,6 +2662,7 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
       }
       __syncthreads();
     }
+    SPLIT_STAMP(2);
     if (tid == 0) {  // run ids and room, exactly as k_split
       uint32_t acc = 0, nd2 = 0;
       for (uint32_t g = 0; g < SPLIT_MAXG; g++) {
@@ -2677,14 +2690,22 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
     __syncthreads();
     if (s_bad) return;  // (uniform) no room in the dup-run list: the exact path keeps it
     // committed: segsum holds the permutation's source until the new sums
-    for (uint32_t k = tid; k < L; k += NT) segsum[p + k] = sv[p + k];
+    for (uint32_t k0 = tid; k0 < L; k0 += NT * SPLIT_E) {
+      uint32_t e[SPLIT_E];
+#pragma unroll
+      for (uint32_t u = 0; u < SPLIT_E; u++)
+        if (k0 + u * NT < L) e[u] = sv[p + k0 + u * NT];
+#pragma unroll
+      for (uint32_t u = 0; u < SPLIT_E; u++)
+        if (k0 + u * NT < L) segsum[p + k0 + u * NT] = e[u];
+    }
     __syncthreads();
+    SPLIT_STAMP(3);
     // scatter (SPLIT_U elements in flight per lane): max(1, hits) moves to
     // hnew at the new position, so the sums below read it coalesced; only a
     // one-unit group's records are read (its clock, its lone-element flag)
     for (uint32_t k0 = tid; k0 < L; k0 += R) {
-      uint32_t e[SPLIT_U], np[SPLIT_U], g[SPLIT_U], h[SPLIT_U];
-      Rec x[SPLIT_U];
+      uint32_t e[SPLIT_U], np[SPLIT_U], g[SPLIT_U], h[SPLIT_U], xnow[SPLIT_U], xlu[SPLIT_U];
 #pragma unroll
       for (uint32_t u = 0; u < SPLIT_U; u++) {
         const uint32_t k = k0 + u * NT;
@@ -2696,7 +2717,10 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
       }
 #pragma unroll
       for (uint32_t u = 0; u < SPLIT_U; u++)
-        if (k0 + u * NT < L && !s_plan.alias[g[u]]) x[u] = rec[e[u]];
+        if (k0 + u * NT < L && !s_plan.alias[g[u]]) {
+          xnow[u] = rec[e[u]].now;
+          xlu[u] = rec[e[u]].lu;
+        }
 #pragma unroll
       for (uint32_t u = 0; u < SPLIT_U; u++) {
         if (k0 + u * NT >= L) continue;
@@ -2705,15 +2729,16 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
         hnew[p + np[u]] = h[u];
         if (!s_plan.alias[g[u]]) {  // (a multi-unit stem's groups share one `now`)
           const uint32_t f = s_plan.fam[g[u]], d = div_of(s_lunit[f]);
-          if (x[u].now != s_lnow[f])
-            atomicOr(&s_fl[g[u]], x[u].now / d != s_lnow[f] / d ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR);
+          if (xnow[u] != s_lnow[f])
+            atomicOr(&s_fl[g[u]], xnow[u] / d != s_lnow[f] / d ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR);
           // a lone group of one element is a key seen once (k_table's singleton part)
-          if (s_cnt[g[u]] == 1) rec[e[u]].lu = x[u].lu & ~(FLAG_DUP << 24);
+          if (s_cnt[g[u]] == 1) rec[e[u]].lu = xlu[u] & ~(FLAG_DUP << 24);
         }
       }
     }
     if (tid == 0) s_carry = 0;
     __syncthreads();
+    SPLIT_STAMP(4);
     // in-run sums of max(1, hits) in the new order: one inclusive scan over the
     // whole run (mod 2^32, like the bucket kernels' sums; each lane SPLIT_U
     // consecutive elements per round), then each group subtracts the total
@@ -2747,12 +2772,22 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
       }
       __syncthreads();
     }
+    SPLIT_STAMP(5);
     if (tid < SPLIT_MAXG) s_off[tid] = (tid < G && s_base[tid]) ? segsum[p + s_base[tid] - 1] : 0u;
     __syncthreads();
-    for (uint32_t k = tid; k < L; k += NT) {
-      uint32_t g = 0;
-      while (g + 1 < G && k >= s_base[g + 1]) g++;
-      if (s_off[g]) segsum[p + k] -= s_off[g];
+    for (uint32_t k0 = tid; k0 < L; k0 += NT * SPLIT_E) {
+      uint32_t v[SPLIT_E];
+#pragma unroll
+      for (uint32_t u = 0; u < SPLIT_E; u++)
+        if (k0 + u * NT < L) v[u] = segsum[p + k0 + u * NT];
+#pragma unroll
+      for (uint32_t u = 0; u < SPLIT_E; u++) {
+        const uint32_t k = k0 + u * NT;
+        if (k >= L) continue;
+        uint32_t g = 0;
+        while (g + 1 < G && k >= s_base[g + 1]) g++;
+        if (s_off[g]) segsum[p + k] = v[u] - s_off[g];
+      }
     }
     if (tid < G) {
       const uint32_t id = s_id[tid];
@@ -2761,6 +2796,14 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
       run_flags[id] = split_group_flags(s_plan, tid, s_fl[tid]);
     }
     if (tid == 0) defer[j] = DEFER_DONE;
+#ifdef RL_SPLIT_PROF
+    if (tid == 0 && L > 20000) {
+      ts[6] = wall_clock64();
+      printf("split_long L=%u G=%u rfl=%x: fam %lu ranks %lu ids+copy %lu scatter %lu scan %lu sub %lu (x10ns)\n", L, G, rfl,
+             (unsigned long)(ts[1] - ts[0]), (unsigned long)(ts[2] - ts[1]), (unsigned long)(ts[3] - ts[2]),
+             (unsigned long)(ts[4] - ts[3]), (unsigned long)(ts[5] - ts[4]), (unsigned long)(ts[6] - ts[5]));
+    }
+#endif
   }
 }
 
@@ -3073,7 +3116,15 @@ struct AliasGroup {
   uint32_t id, p, end, mask, w;
 };
 
-__device__ __attribute__((noinline)) bool alias_setup(const TableDev& t, const Params& P, SRec rec_s, const uint32_t* __restrict__ rid,
+#ifndef RL_ALIAS_NOINLINE
+#define RL_ALIAS_NOINLINE 0  // (noinline: k_table gets a 448-B scratch frame; C1 -1.5 %, profiles/r03/ab_alias_variants/)
+#endif
+#if RL_ALIAS_NOINLINE
+#define RL_ALIAS_ATTR __attribute__((noinline))
+#else
+#define RL_ALIAS_ATTR inline
+#endif
+__device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SRec rec_s, const uint32_t* __restrict__ rid,
                                    const uint32_t* __restrict__ run_start, const uint32_t* __restrict__ run_end,
                                    uint32_t* __restrict__ run_flags, uint4* __restrict__ run_state,
                                    uint4* __restrict__ run_alias, uint32_t* __restrict__ run_f,
@@ -3448,6 +3499,7 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
                                                    unsigned long long* stripes, const uint32_t* err,
                                                    const uint32_t* __restrict__ fast_blk) {
   __shared__ uint32_t s_err, s_fast, s_n;
+  __syncthreads();  // (grid-stride callers: the previous block's shared state has been read)
   if (threadIdx.x == 0) {
     s_err = *err;
     s_fast = (fast_blk[blk >> 5] >> (blk & 31)) & 1u;
@@ -3771,9 +3823,11 @@ __global__ __launch_bounds__(256, 8) void k_late(BatchDev b, TableDev t, Params 
     general_body(blockIdx.x, RUNS_GENERAL_LATE_BLOCKS, b, t, P, rec_s, skeys, svals, res, run_start, run_end, defer,
                  defer_n, defer2, defer2_n, grp, lead, gmask, keys0, defer1, defer1_n, run_flags, rid, stats, stripes,
                  err, errs, restore);
-  else if (!restore)
-    fast_emit_body(blockIdx.x - RUNS_GENERAL_LATE_BLOCKS, sorted_n, b.n_rules, t, P, rec_s, svals, res, segsum, rid,
-                   run_start, run_end, run_flags, run_state, run_alias, run_f, stats, stripes, err, fast_blk);
+  else if (!restore)  // (grid-stride when the launch caps the fast part's workgroups)
+    for (uint32_t blk = blockIdx.x - RUNS_GENERAL_LATE_BLOCKS; blk * 256 < b.n;
+         blk += gridDim.x - RUNS_GENERAL_LATE_BLOCKS)
+      fast_emit_body(blk, sorted_n, b.n_rules, t, P, rec_s, svals, res, segsum, rid, run_start, run_end, run_flags,
+                     run_state, run_alias, run_f, stats, stripes, err, fast_blk);
 }
 
 // First kernel of the table stage: merge this batch's validation errors into
@@ -3999,6 +4053,9 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
 // sticky table-stage word s.errb; k_b_begin folds this batch's validation
 // result into it first. The keys seen once and the sorted path (runs
 // and its exact / parallel companions) touch disjoint stems.
+#ifndef RL_LATE_FAST_BLOCKS
+#define RL_LATE_FAST_BLOCKS 0  // cap on k_late's long-run workgroups (0: one per 256 descriptors)
+#endif
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
                     int restore, hipStream_t st, hipEvent_t* ev) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
@@ -4021,7 +4078,8 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     if (ev) (void)hipEventRecord(ev[4], st);
     if (!restore && P.lc_en)
       k_fast_over<<<g, 256, 0, st>>>(s.sorted_n, rs, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
-    k_late<<<RUNS_GENERAL_LATE_BLOCKS + (restore ? 0u : g), 256, lds, st>>>(
+    k_late<<<RUNS_GENERAL_LATE_BLOCKS + (restore ? 0u : (RL_LATE_FAST_BLOCKS && g > RL_LATE_FAST_BLOCKS
+                                                            ? RL_LATE_FAST_BLOCKS : g)), 256, lds, st>>>(
         b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer, s.defer_n, s.defer2, s.defer2_n,
         s.grp, s.lead, s.gmask,
         s.keys[0], s.defer1, s.defer1_n, s.segsum, s.rid, s.run_flags, s.run_state, s.run_alias, s.run_f, o.stats,

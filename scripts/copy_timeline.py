@@ -29,7 +29,10 @@ def main():
     cps = []
     for r in rows:
         kind = col(r, "Direction", "Operation", "Kind")
-        nb = int(col(r, "Bytes", "Size", "Copy_Bytes"))
+        try:
+            nb = int(col(r, "Bytes", "Size", "Copy_Bytes"))
+        except KeyError:  # (rocprofv3 of ROCm 7.2 records no size: durations only)
+            nb = -1
         t0, t1 = int(col(r, "Start_Timestamp")), int(col(r, "End_Timestamp"))
         cps.append((t0, t1, nb, kind))
     cps.sort()
@@ -37,7 +40,7 @@ def main():
     for c in cps:
         by.setdefault(c[3], []).append(c)
     for kind, cs in by.items():
-        big = [c for c in cs if c[2] >= min_bytes]
+        big = [c for c in cs if c[2] >= min_bytes or c[2] < 0]
         if not big:
             continue
         busy = sum(c[1] - c[0] for c in big)
@@ -57,7 +60,7 @@ def main():
                                                            c[2] / max(c[1] - c[0], 1)))
     kinds = list(by)
     if len(kinds) >= 2:
-        iv = {k: [(c[0], c[1]) for c in by[k] if c[2] >= min_bytes] for k in kinds}
+        iv = {k: [(c[0], c[1]) for c in by[k] if c[2] >= min_bytes or c[2] < 0] for k in kinds}
         a, b = kinds[0], kinds[1]
         ov = 0
         j = 0

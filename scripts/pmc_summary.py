@@ -83,11 +83,21 @@ def main():
         f = ku["fetch_size_bytes"]
         res["k_table_read_bytes_bounds"] = sorted([f * calib["random64_read_bytes_per_fetch_byte"],
                                                     f * calib["seq64_read_bytes_per_fetch_byte"]])
+    # the whole step: every per-batch kernel (not the fill / info / sweep ones)
+    per_batch = {k: v for k, v in kernels.items()
+                 if not any(x in k for x in ("k_table_info", "k_lc_count", "k_sweep", "k_arena", "k_debug"))}
+    res["step_total_bytes"] = sum(v["traffic_bytes"] for v in per_batch.values())
+    res["step_kernels"] = sorted(per_batch)
+    res["decisions_per_batch"] = 1000000
+    # the kernels that answer decisions (C2: the long runs' elements are decided in k_late, not k_table)
+    ans = [k for k in ("rl::k_table", "rl::k_late", "rl::k_fast_over") if k in kernels]
+    res["answering_kernels_bytes"] = {k: kernels[k]["traffic_bytes"] for k in ans}
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     p = os.path.join(ROOT, "profiles", "traffic_%s.json" % cfg)
     json.dump(res, open(p, "w"), indent=1)
     for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["traffic_bytes"]):
         print("%-28s read %8.1f MB  write %8.1f MB" % (k, v["read_bytes_corrected"] / 1e6, v["write_size_bytes"] / 1e6))
+    print("whole step: %.1f MB per batch of 1M" % (res["step_total_bytes"] / 1e6))
 
 
 if __name__ == "__main__":
