@@ -2513,7 +2513,8 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
                                                           uint32_t* rank, uint32_t* __restrict__ pos_hits,
                                                           uint32_t* __restrict__ hnew, int per_second, uint32_t rfl) {
   constexpr uint32_t NW = NT / 64, R = NT * SPLIT_U;
-  __shared__ uint32_t s_w[SPLIT_U][NW][SPLIT_MAXG], s_ws[NW];
+  constexpr uint32_t UR = 64 / NW < 8 ? 64 / NW : 8;  // rank rounds: UR x NW counts per group fit one wave's scan
+  __shared__ uint32_t s_x[SPLIT_MAXG][64], s_ws[NW];
   __shared__ uint32_t s_cnt[SPLIT_MAXG], s_base[SPLIT_MAXG], s_id[SPLIT_MAXG], s_fl[SPLIT_MAXG], s_off[SPLIT_MAXG];
   __shared__ uint32_t s_lnow[SPLIT_MAXG], s_lunit[SPLIT_MAXG], s_fmask[SPLIT_MAXG], s_fnv[SPLIT_MAXG];
   __shared__ uint32_t s_bad, s_lead, s_carry;
@@ -2616,14 +2617,16 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
     const uint32_t G = s_plan.G;
     if (s_bad || (G < 2 && !s_plan.any_alias)) return;  // (uniform) the exact path keeps it
     SPLIT_STAMP(1);
-    // stable ranks inside the groups: per round of R = NT x SPLIT_U elements,
-    // wave ballots per group, then the slices, waves and rounds before
+    // stable ranks inside the groups, in rounds of NT x UR elements: wave
+    // ballots count each (slice, wave)'s elements per group, one wave scan
+    // per group turns the counts into their starting ranks (the rounds
+    // before included), each element adds its rank among its wave's lanes
     if (tid < SPLIT_MAXG) s_cnt[tid] = 0;
     __syncthreads();
-    for (uint32_t c0 = 0; c0 < L; c0 += R) {
-      uint32_t gk[SPLIT_U], mine[SPLIT_U];
+    for (uint32_t c0 = 0; c0 < L; c0 += NT * UR) {
+      uint32_t gk[UR], mine[UR];
 #pragma unroll
-      for (uint32_t u = 0; u < SPLIT_U; u++) {
+      for (uint32_t u = 0; u < UR; u++) {
         const uint32_t k = c0 + u * NT + tid;
         gk[u] = 0xFFu;
         mine[u] = 0;
@@ -2634,33 +2637,33 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
         }
       }
 #pragma unroll
-      for (uint32_t u = 0; u < SPLIT_U; u++) {
+      for (uint32_t u = 0; u < UR; u++) {
 #pragma unroll
         for (uint32_t g = 0; g < SPLIT_MAXG; g++) {
+          if (g >= G) break;  // (uniform)
           const uint64_t m = __ballot(gk[u] == g);
           if (gk[u] == g) mine[u] = __popcll(m & lt);
-          if (lane == 0) s_w[u][wv][g] = __popcll(m);
+          if (lane == 0) s_x[g][u * NW + wv] = __popcll(m);
         }
       }
       __syncthreads();
+      for (uint32_t g = wv; g < G; g += NW) {
+        const uint32_t v = lane < UR * NW ? s_x[g][lane] : 0u, base = s_cnt[g];
+        uint32_t inc = v;
 #pragma unroll
-      for (uint32_t u = 0; u < SPLIT_U; u++) {
-        const uint32_t g = gk[u];
-        if (g >= SPLIT_MAXG) continue;
-        uint32_t pre = s_cnt[g];
-        for (uint32_t v = 0; v < u; v++)
-          for (uint32_t w = 0; w < NW; w++) pre += s_w[v][w][g];
-        for (uint32_t w = 0; w < wv; w++) pre += s_w[u][w][g];
-        rank[p + c0 + u * NT + tid] = pre + mine[u];
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+          const uint32_t y = __shfl_up(inc, off, 64);
+          if (lane >= off) inc += y;
+        }
+        if (lane < UR * NW) s_x[g][lane] = base + inc - v;
+        const uint32_t tot = __shfl(inc, 63, 64);
+        if (lane == 0) s_cnt[g] = base + tot;
       }
       __syncthreads();
-      if (tid < SPLIT_MAXG) {
-        uint32_t a = 0;
-        for (uint32_t v = 0; v < SPLIT_U; v++)
-          for (uint32_t w = 0; w < NW; w++) a += s_w[v][w][tid];
-        s_cnt[tid] += a;
-      }
-      __syncthreads();
+#pragma unroll
+      for (uint32_t u = 0; u < UR; u++)
+        if (gk[u] < SPLIT_MAXG) rank[p + c0 + u * NT + tid] = s_x[gk[u]][u * NW + wv] + mine[u];
+      __syncthreads();  // (the next round rewrites s_x)
     }
     SPLIT_STAMP(2);
     if (tid == 0) {  // run ids and room, exactly as k_split
