@@ -323,6 +323,15 @@ def main():
                 "descriptors_per_batch": n_owner,
                 "stage_ms": {k: round(v, 4) for k, v in stage_avg.items()},
                 "pipeline_achieved": b_alg * n_owner / (pipe_ms * 1e-3) / 1e9 if pipe_ms > 0 else None}
+    # the kernels that answer every decision: k_table (keys seen once, short
+    # runs) and the long runs' parallel path (k_fast_over, k_late), timed by the
+    # table and finish stages (finish also holds k_finish: a conservative figure)
+    ans_ms = stage_avg.get("table", 0.0) + stage_avg.get("finish", 0.0)
+    if ans_ms > 0 and not routed:
+        ach = b_alg * n_owner / (ans_ms * 1e-3) / 1e9
+        roofline["answering_kernels"] = {"kernels": "k_table + k_fast_over + k_late + k_finish", "achieved": ach,
+                                         "frac": ach / HBM_PEAK_GBS, "decisions_per_batch": n_owner,
+                                         "ms_per_batch": ans_ms}
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

@@ -2373,11 +2373,28 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
       const uint32_t d = div_of(rec_unit(x));
       f |= (same && x.now / d != y.now / d) ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR;
     }
-    // a hot run's elements all find the same: read before the atomic, so a
-    // run of tens of thousands does not serialise on one word
-    if (f && (__hip_atomic_load(&run_flags[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & f) != f) {
-      const uint32_t old = atomicOr(&run_flags[r], f);
-      if ((f & RUN_MULTI) && !(old & RUN_MULTI)) defer[atomicAdd(defer_n, 1u)] = r;
+    // a hot run fills whole waves with the same verdict: one lane per (wave,
+    // run) reads the word and ORs in what its wave found, so a run of tens of
+    // thousands does not serialise on one word (nor on one L2 line)
+    uint64_t pend = __ballot(f != 0);
+    while (pend) {  // (wave-uniform)
+      const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)pend) - 1);
+      const uint32_t rr = __shfl(r, leader, 64);
+      const bool mine = f != 0 && r == rr;
+      const uint64_t mm = __ballot(mine);
+      constexpr uint32_t kBits[] = {RUN_MULTI, RUN_UNITS, RUN_STEMS, RUN_SLOW, RUN_NOWVAR,
+                                    1u << RUN_UMASK_SHIFT, 2u << RUN_UMASK_SHIFT, 4u << RUN_UMASK_SHIFT,
+                                    8u << RUN_UMASK_SHIFT};
+      uint32_t fo = 0;
+#pragma unroll
+      for (uint32_t bi = 0; bi < sizeof(kBits) / sizeof(kBits[0]); bi++)
+        if (__ballot(mine && (f & kBits[bi]))) fo |= kBits[bi];
+      if ((threadIdx.x & 63u) == leader &&
+          (__hip_atomic_load(&run_flags[rr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & fo) != fo) {
+        const uint32_t old = atomicOr(&run_flags[rr], fo);
+        if ((fo & RUN_MULTI) && !(old & RUN_MULTI)) defer[atomicAdd(defer_n, 1u)] = rr;
+      }
+      pend &= ~mm;
     }
   }
 }
@@ -2493,10 +2510,9 @@ __device__ inline uint32_t split_group_flags(const SplitPlan& S, uint32_t g, uin
 // of its own with 1024-lane blocks cost every batch 4-6 us of launch on the
 // critical path, 1-3 %, profiles/r02/ab/long_*.)
 constexpr uint32_t SPLIT_UNROLL = 8;
-constexpr uint32_t SPLIT_U = 8;  // elements per lane per round of the rank, scatter and sum passes (one barrier set per NT x 8)
-constexpr uint32_t SPLIT_E = 16;  // elements in flight per lane in the elementwise passes
-// k_split's workgroup (a long run's passes are rounds of SPLIT_THREADS x SPLIT_U
-// elements; every pass is a chain of such rounds, each waiting on memory)
+constexpr uint32_t SPLIT_ST = 8;  // 64-element steps in flight per wave in split_long_body's walks
+// k_split's workgroup (a long run is reordered by its waves, each walking a
+// chunk of it: more waves, shorter walks, but slower short runs)
 #ifndef RL_SPLIT_THREADS
 #define RL_SPLIT_THREADS 256  // (1024: C2U's 58k-element runs 481 -> 377 us, but C1's k_split 18 -> 26 us)
 #endif
@@ -2512,12 +2528,11 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
                                                           uint32_t* __restrict__ drun, uint32_t drun_cap, uint32_t* grp,
                                                           uint32_t* rank, uint32_t* __restrict__ pos_hits,
                                                           uint32_t* __restrict__ hnew, int per_second, uint32_t rfl) {
-  constexpr uint32_t NW = NT / 64, R = NT * SPLIT_U;
-  constexpr uint32_t UR = 64 / NW < 8 ? 64 / NW : 8;  // rank rounds: UR x NW counts per group fit one wave's scan
-  __shared__ uint32_t s_x[SPLIT_MAXG][64], s_ws[NW];
+  constexpr uint32_t NW = NT / 64;
+  __shared__ uint32_t s_wc[NW][SPLIT_MAXG], s_wh[NW][SPLIT_MAXG], s_wp[NW][SPLIT_MAXG], s_ws[NW];
   __shared__ uint32_t s_cnt[SPLIT_MAXG], s_base[SPLIT_MAXG], s_id[SPLIT_MAXG], s_fl[SPLIT_MAXG], s_off[SPLIT_MAXG];
   __shared__ uint32_t s_lnow[SPLIT_MAXG], s_lunit[SPLIT_MAXG], s_fmask[SPLIT_MAXG], s_fnv[SPLIT_MAXG];
-  __shared__ uint32_t s_bad, s_lead, s_carry;
+  __shared__ uint32_t s_bad, s_lead;
   __shared__ SplitPlan s_plan;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -2617,54 +2632,54 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
     const uint32_t G = s_plan.G;
     if (s_bad || (G < 2 && !s_plan.any_alias)) return;  // (uniform) the exact path keeps it
     SPLIT_STAMP(1);
-    // stable ranks inside the groups, in rounds of NT x UR elements: wave
-    // ballots count each (slice, wave)'s elements per group, one wave scan
-    // per group turns the counts into their starting ranks (the rounds
-    // before included), each element adds its rank among its wave's lanes
-    if (tid < SPLIT_MAXG) s_cnt[tid] = 0;
-    __syncthreads();
-    for (uint32_t c0 = 0; c0 < L; c0 += NT * UR) {
-      uint32_t gk[UR], mine[UR];
+    // The reordering as wave walks (no block barrier inside a walk; ST steps
+    // of 64 elements in flight per wave): wave w owns the positions
+    // [w CH, (w+1) CH). Walk 1 counts each group's elements and sums its
+    // max(1, hits) in the wave's chunk; the chunks' starting ranks and each
+    // group's hits before it follow from the NW x G totals.
+    const uint32_t CH = ((L + NT - 1) / NT) * 64;
+    const uint32_t a0 = min(L, wv * CH), a1 = min(L, a0 + CH);
+    {
+      uint32_t cl[SPLIT_MAXG], hl[SPLIT_MAXG];
 #pragma unroll
-      for (uint32_t u = 0; u < UR; u++) {
-        const uint32_t k = c0 + u * NT + tid;
-        gk[u] = 0xFFu;
-        mine[u] = 0;
-        if (k < L) {
-          const uint32_t fu = grp[p + k];
-          gk[u] = s_plan.ug[fu & 0xFFu][(fu >> 8) - 1];
-          grp[p + k] = gk[u];
+      for (uint32_t g = 0; g < SPLIT_MAXG; g++) cl[g] = hl[g] = 0;
+      for (uint32_t c = a0; c < a1; c += 64 * SPLIT_ST) {
+        uint32_t fu[SPLIT_ST], h[SPLIT_ST];
+#pragma unroll
+        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+          const uint32_t k = c + st * 64 + lane;
+          fu[st] = k < a1 ? grp[p + k] : 0xFFFFFFFFu;
+          h[st] = k < a1 ? pos_hits[p + k] : 0u;
+        }
+#pragma unroll
+        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+          if (fu[st] == 0xFFFFFFFFu) continue;
+          const uint32_t gk = s_plan.ug[fu[st] & 0xFFu][(fu[st] >> 8) - 1];
+#pragma unroll
+          for (uint32_t g = 0; g < SPLIT_MAXG; g++)
+            if (gk == g) {
+              cl[g]++;
+              hl[g] += h[st];
+            }
         }
       }
 #pragma unroll
-      for (uint32_t u = 0; u < UR; u++) {
-#pragma unroll
-        for (uint32_t g = 0; g < SPLIT_MAXG; g++) {
-          if (g >= G) break;  // (uniform)
-          const uint64_t m = __ballot(gk[u] == g);
-          if (gk[u] == g) mine[u] = __popcll(m & lt);
-          if (lane == 0) s_x[g][u * NW + wv] = __popcll(m);
+      for (uint32_t g = 0; g < SPLIT_MAXG; g++) {
+        if (g >= G) break;  // (uniform)
+        const uint32_t cg = wave_sum32(cl[g]), hg = wave_sum32(hl[g]);
+        if (lane == 0) {
+          s_wc[wv][g] = cg;
+          s_wh[wv][g] = hg;
         }
       }
-      __syncthreads();
-      for (uint32_t g = wv; g < G; g += NW) {
-        const uint32_t v = lane < UR * NW ? s_x[g][lane] : 0u, base = s_cnt[g];
-        uint32_t inc = v;
-#pragma unroll
-        for (uint32_t off = 1; off < 64; off <<= 1) {
-          const uint32_t y = __shfl_up(inc, off, 64);
-          if (lane >= off) inc += y;
-        }
-        if (lane < UR * NW) s_x[g][lane] = base + inc - v;
-        const uint32_t tot = __shfl(inc, 63, 64);
-        if (lane == 0) s_cnt[g] = base + tot;
-      }
-      __syncthreads();
-#pragma unroll
-      for (uint32_t u = 0; u < UR; u++)
-        if (gk[u] < SPLIT_MAXG) rank[p + c0 + u * NT + tid] = s_x[gk[u]][u * NW + wv] + mine[u];
-      __syncthreads();  // (the next round rewrites s_x)
     }
+    __syncthreads();
+    if (tid < SPLIT_MAXG) {
+      uint32_t cn = 0;
+      for (uint32_t w = 0; w < NW; w++) cn += tid < G ? s_wc[w][tid] : 0u;
+      s_cnt[tid] = cn;
+    }
+    __syncthreads();
     SPLIT_STAMP(2);
     if (tid == 0) {  // run ids and room, exactly as k_split
       uint32_t acc = 0, nd2 = 0;
@@ -2692,104 +2707,138 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
     }
     __syncthreads();
     if (s_bad) return;  // (uniform) no room in the dup-run list: the exact path keeps it
-    // committed: segsum holds the permutation's source until the new sums
-    for (uint32_t k0 = tid; k0 < L; k0 += NT * SPLIT_E) {
-      uint32_t e[SPLIT_E];
-#pragma unroll
-      for (uint32_t u = 0; u < SPLIT_E; u++)
-        if (k0 + u * NT < L) e[u] = sv[p + k0 + u * NT];
-#pragma unroll
-      for (uint32_t u = 0; u < SPLIT_E; u++)
-        if (k0 + u * NT < L) segsum[p + k0 + u * NT] = e[u];
+    // each wave's starting rank per group, and each group's hits before it
+    // (groups are consecutive in the new order: the in-run sums subtract it)
+    if (tid < G) {
+      uint32_t a = s_base[tid], o = 0;
+      for (uint32_t w = 0; w < NW; w++) {
+        s_wp[w][tid] = a;
+        a += s_wc[w][tid];
+      }
+      for (uint32_t g = 0; g < (uint32_t)tid; g++)
+        for (uint32_t w = 0; w < NW; w++) o += s_wh[w][g];
+      s_off[tid] = o;
     }
     __syncthreads();
     SPLIT_STAMP(3);
-    // scatter (SPLIT_U elements in flight per lane): max(1, hits) moves to
-    // hnew at the new position, so the sums below read it coalesced; only a
-    // one-unit group's records are read (its clock, its lone-element flag)
-    for (uint32_t k0 = tid; k0 < L; k0 += R) {
-      uint32_t e[SPLIT_U], np[SPLIT_U], g[SPLIT_U], h[SPLIT_U], xnow[SPLIT_U], xlu[SPLIT_U];
+    // walk 2, the scatter: a stable rank per group from wave ballots and the
+    // wave's running counts; the element id lands in `rank` (a temporary: svals
+    // is still being read), hits in hnew, the run id in rid; only a one-unit
+    // group's records are read (its clock, its lone-element flag)
+    {
+      uint32_t run[SPLIT_MAXG];
 #pragma unroll
-      for (uint32_t u = 0; u < SPLIT_U; u++) {
-        const uint32_t k = k0 + u * NT;
-        if (k >= L) continue;
-        g[u] = grp[p + k];
-        np[u] = s_base[g[u]] + rank[p + k];
-        e[u] = segsum[p + k];
-        h[u] = pos_hits[p + k];
+      for (uint32_t g = 0; g < SPLIT_MAXG; g++) run[g] = g < G ? s_wp[wv][g] : 0u;
+      // (software-pipelined: the next ST steps' loads are issued before this
+      // step's stores, so waiting for them never waits for the stores)
+      uint32_t fu[SPLIT_ST], e[SPLIT_ST], h[SPLIT_ST];
+#pragma unroll
+      for (uint32_t st = 0; st < SPLIT_ST; st++) {
+        const uint32_t k = a0 + st * 64 + lane;
+        fu[st] = k < a1 ? grp[p + k] : 0xFFFFFFFFu;
+        e[st] = k < a1 ? sv[p + k] : 0u;
+        h[st] = k < a1 ? pos_hits[p + k] : 0u;
       }
+      for (uint32_t c = a0; c < a1; c += 64 * SPLIT_ST) {
+        uint32_t fn[SPLIT_ST], en[SPLIT_ST], hn[SPLIT_ST];
 #pragma unroll
-      for (uint32_t u = 0; u < SPLIT_U; u++)
-        if (k0 + u * NT < L && !s_plan.alias[g[u]]) {
-          xnow[u] = rec[e[u]].now;
-          xlu[u] = rec[e[u]].lu;
+        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+          const uint32_t k = c + (SPLIT_ST + st) * 64 + lane;
+          fn[st] = k < a1 ? grp[p + k] : 0xFFFFFFFFu;
+          en[st] = k < a1 ? sv[p + k] : 0u;
+          hn[st] = k < a1 ? pos_hits[p + k] : 0u;
         }
 #pragma unroll
-      for (uint32_t u = 0; u < SPLIT_U; u++) {
-        if (k0 + u * NT >= L) continue;
-        svals[p + np[u]] = e[u];
-        rid[p + np[u]] = s_id[g[u]];
-        hnew[p + np[u]] = h[u];
-        if (!s_plan.alias[g[u]]) {  // (a multi-unit stem's groups share one `now`)
-          const uint32_t f = s_plan.fam[g[u]], d = div_of(s_lunit[f]);
-          if (xnow[u] != s_lnow[f])
-            atomicOr(&s_fl[g[u]], xnow[u] / d != s_lnow[f] / d ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR);
-          // a lone group of one element is a key seen once (k_table's singleton part)
-          if (s_cnt[g[u]] == 1) rec[e[u]].lu = xlu[u] & ~(FLAG_DUP << 24);
+        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+          const uint32_t gk = fu[st] == 0xFFFFFFFFu ? 0xFFu : s_plan.ug[fu[st] & 0xFFu][(fu[st] >> 8) - 1];
+          uint32_t np = 0;
+#pragma unroll
+          for (uint32_t g = 0; g < SPLIT_MAXG; g++) {
+            if (g >= G) break;  // (uniform)
+            const uint64_t m = __ballot(gk == g);
+            if (gk == g) np = run[g] + __popcll(m & lt);
+            run[g] += __popcll(m);
+          }
+          if (gk >= SPLIT_MAXG) continue;
+          rank[p + np] = e[st];
+          rid[p + np] = s_id[gk];
+          hnew[p + np] = h[st];
+          if (!s_plan.alias[gk]) {  // (a multi-unit stem's groups share one `now`)
+            const Rec x = rec[e[st]];
+            const uint32_t f = s_plan.fam[gk], d = div_of(s_lunit[f]);
+            if (x.now != s_lnow[f])
+              atomicOr(&s_fl[gk], x.now / d != s_lnow[f] / d ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR);
+            // a lone group of one element is a key seen once (k_table's singleton part)
+            if (s_cnt[gk] == 1) rec[e[st]].lu = x.lu & ~(FLAG_DUP << 24);
+          }
+        }
+#pragma unroll
+        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+          fu[st] = fn[st];
+          e[st] = en[st];
+          h[st] = hn[st];
         }
       }
     }
-    if (tid == 0) s_carry = 0;
     __syncthreads();
     SPLIT_STAMP(4);
-    // in-run sums of max(1, hits) in the new order: one inclusive scan over the
-    // whole run (mod 2^32, like the bucket kernels' sums; each lane SPLIT_U
-    // consecutive elements per round), then each group subtracts the total
-    // before its start
-    for (uint32_t c0 = 0; c0 < L; c0 += R) {
-      const uint32_t k = c0 + tid * SPLIT_U;
-      uint32_t v[SPLIT_U], t = 0;
+    // walk 3: the hits of each wave's chunk in the new order, then inclusive
+    // sums (mod 2^32, like the bucket kernels') with the group's offset taken
+    // off, and the new permutation from `rank` into svals
+    {
+      uint32_t t = 0;
+      for (uint32_t c = a0; c < a1; c += 64 * SPLIT_ST) {
 #pragma unroll
-      for (uint32_t u = 0; u < SPLIT_U; u++) {
-        t += k + u < L ? hnew[p + k + u] : 0u;
-        v[u] = t;
+        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+          const uint32_t k = c + st * 64 + lane;
+          t += k < a1 ? hnew[p + k] : 0u;
+        }
       }
-      uint32_t inc = t;
-#pragma unroll
-      for (uint32_t off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(inc, off, 64);
-        if (lane >= off) inc += y;
-      }
-      if (lane == 63) s_ws[wv] = inc;
-      __syncthreads();
-      uint32_t pre = s_carry + inc - t;
-      for (uint32_t w = 0; w < wv; w++) pre += s_ws[w];
-#pragma unroll
-      for (uint32_t u = 0; u < SPLIT_U; u++)
-        if (k + u < L) segsum[p + k + u] = pre + v[u];
-      __syncthreads();
-      if (tid == 0) {
-        uint32_t a = 0;
-        for (uint32_t w = 0; w < NW; w++) a += s_ws[w];
-        s_carry += a;
-      }
-      __syncthreads();
+      t = wave_sum32(t);
+      if (lane == 0) s_ws[wv] = t;
     }
-    SPLIT_STAMP(5);
-    if (tid < SPLIT_MAXG) s_off[tid] = (tid < G && s_base[tid]) ? segsum[p + s_base[tid] - 1] : 0u;
     __syncthreads();
-    for (uint32_t k0 = tid; k0 < L; k0 += NT * SPLIT_E) {
-      uint32_t v[SPLIT_E];
+    SPLIT_STAMP(5);
+    {
+      uint32_t carry = 0, g = 0;
+      for (uint32_t w = 0; w < wv; w++) carry += s_ws[w];
+      uint32_t h[SPLIT_ST], e[SPLIT_ST];
 #pragma unroll
-      for (uint32_t u = 0; u < SPLIT_E; u++)
-        if (k0 + u * NT < L) v[u] = segsum[p + k0 + u * NT];
+      for (uint32_t st = 0; st < SPLIT_ST; st++) {
+        const uint32_t k = a0 + st * 64 + lane;
+        h[st] = k < a1 ? hnew[p + k] : 0u;
+        e[st] = k < a1 ? rank[p + k] : 0u;
+      }
+      for (uint32_t c = a0; c < a1; c += 64 * SPLIT_ST) {
+        uint32_t hn[SPLIT_ST], en[SPLIT_ST];  // (software-pipelined, as the scatter)
 #pragma unroll
-      for (uint32_t u = 0; u < SPLIT_E; u++) {
-        const uint32_t k = k0 + u * NT;
-        if (k >= L) continue;
-        uint32_t g = 0;
-        while (g + 1 < G && k >= s_base[g + 1]) g++;
-        if (s_off[g]) segsum[p + k] = v[u] - s_off[g];
+        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+          const uint32_t k = c + (SPLIT_ST + st) * 64 + lane;
+          hn[st] = k < a1 ? hnew[p + k] : 0u;
+          en[st] = k < a1 ? rank[p + k] : 0u;
+        }
+#pragma unroll
+        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+          const uint32_t k = c + st * 64 + lane;
+          uint32_t inc = h[st];
+#pragma unroll
+          for (uint32_t off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += y;
+          }
+          const uint32_t tot = __shfl(inc, 63, 64);
+          if (k < a1) {
+            while (g + 1 < G && k >= s_base[g + 1]) g++;  // (k grows along the walk)
+            segsum[p + k] = carry + inc - s_off[g];
+            svals[p + k] = e[st];
+          }
+          carry += tot;
+        }
+#pragma unroll
+        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+          h[st] = hn[st];
+          e[st] = en[st];
+        }
       }
     }
     if (tid < G) {
@@ -2802,7 +2851,7 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
 #ifdef RL_SPLIT_PROF
     if (tid == 0 && L > 20000) {
       ts[6] = wall_clock64();
-      printf("split_long L=%u G=%u rfl=%x: fam %lu ranks %lu ids+copy %lu scatter %lu scan %lu sub %lu (x10ns)\n", L, G, rfl,
+      printf("split_long L=%u G=%u rfl=%x: fam %lu walk1 %lu ids %lu walk2 %lu walk3a %lu walk3b %lu (x10ns)\n", L, G, rfl,
              (unsigned long)(ts[1] - ts[0]), (unsigned long)(ts[2] - ts[1]), (unsigned long)(ts[3] - ts[2]),
              (unsigned long)(ts[4] - ts[3]), (unsigned long)(ts[5] - ts[4]), (unsigned long)(ts[6] - ts[5]));
     }
@@ -3134,6 +3183,9 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
                                    uint32_t* __restrict__ fast_blk, unsigned long long* __restrict__ res,
                                    const uint32_t* __restrict__ svals, uint32_t* ferr, uint32_t r, uint32_t fl,
                                    uint32_t u0, uint64_t hs, const Key& stem, uint32_t now) {
+#ifdef RL_NO_ALIAS  // (measurement builds: what the alias path costs the common case)
+  return true;
+#endif
   AliasGroup A[4];
   uint32_t G = 1, M;
   A[0].id = r;

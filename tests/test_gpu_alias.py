@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 from oracle import c_oracle
-from ratelimit_amd import workloads
+from ratelimit_amd import abi, workloads
 from ratelimit_amd.limiter import Backend
 
 pytestmark = pytest.mark.gpu
@@ -109,3 +109,77 @@ def test_gpu_override_small_runs_vs_c_oracle():
         batches.append(workloads.c2u_batch(t, NOW0 + t0, h, rng, hot=40, p_override=0.5))
     for lc in (False, True):
         _check(batches, lc)
+
+
+@pytest.mark.parametrize("n_shards,lc", [(2, False), (3, True)])
+def test_gpu_override_multishard_ctx_vs_c_oracle(n_shards, lc):
+    """A ctx hash-sharded over n_shards tables on cuda:0: each owner's routed
+    batch (per-descriptor clocks and global request labels) goes through the
+    same groups and alias_setup."""
+    _check(_stream([38, 39, 40, 41]), lc, n_shards=n_shards, shard_devices=[0] * n_shards, hash_seed=77,
+           max_rules=16)  # (routed owners keep stats per source: shards x rules)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gpu_override_loopback_router_vs_c_oracle(world):
+    """The library router at world 2 and 4 over the loopback transport: slices
+    of hot overridden tenants routed to their owners."""
+    from test_gpu_loopback import _check as lb_check, run_world
+    cfg = (0.8, True, False)
+    batches = _stream([39, 40, 41], rpb=6000)
+    out = run_world(world, batches, cfg)
+    for r in range(world):
+        assert out[r][0] == "ok", out[r][1]
+    lb_check(out, batches, cfg, world)
+
+
+@pytest.mark.parametrize("lc", [False, True])
+def test_gpu_override_bad_descriptor_in_hot_stem_fails_alone(lc):
+    """A failed descriptor (unknown unit) inside a hot overridden stem's run:
+    with statuses it fails alone; its run goes to the exact path and every
+    other answer stays oracle-exact."""
+    from test_gpu_robustness import _drop
+    (a, n, nq, nr), = _stream([40], rpb=8000)
+    hot = np.nonzero((a["unit"] == 2) & (a["rule_id"] == 2))[0]  # overridden sec descriptors
+    bad = {k: v.copy() for k, v in a.items()}
+    i = int(hot[len(hot) // 2])
+    bad["unit"][i] = 9
+    be = Backend(0.8, lc, table_slots=1 << 17, max_batch=1 << 16, max_rules=8)
+    g = be.do_limit_arrays(bad, n, nq, nr, isolate=True)
+    keep = np.ones(n, bool)
+    keep[i] = False
+    assert g["status"][i] == abi.RL_E_INVALID and (g["status"][keep] == 0).all()
+    co = c_oracle.COracle(0.8, lc)
+    o = co.do_limit(*_drop(bad, n, nq, keep), nr)
+    co.close()
+    be.close()
+    for k in ("code", "limit_remaining", "reset_s"):
+        assert np.array_equal(g[k][keep], o[k]), k
+    assert np.array_equal(g["stats"], o["stats"])
+
+
+def test_gpu_override_restore_then_limit_vs_c_oracle():
+    """rl_restore seeding one stem under SECOND and MINUTE at a shared window
+    (restore batches run the same grouping; a multi-unit stem there takes the
+    exact path, merged in arrival order), then override batches on top."""
+    stems = [b"bench_tenant_t%010d_tier_sec_" % t for t in range(8)]
+    units = [1, 2] * 4
+    nows = [NOW0 + 40] * 8
+    counts = [5, 7, 0, 3, 90, 95, 1, 1]
+    lcs = [0, 0, 0, 0, 1, 0, 0, 0]
+    for lc in (False, True):
+        be = Backend(0.8, lc, table_slots=1 << 16, max_batch=1 << 15, max_rules=8)
+        co = c_oracle.COracle(0.8, lc)
+        be.restore([stems[k // 2 * 2] for k in range(8)], units, nows, counts, lcs)
+        co.restore([stems[k // 2 * 2] for k in range(8)], units, nows, counts, lcs)
+        rng = np.random.default_rng(3)
+        for t0 in (40, 40, 41, 60):
+            t = rng.integers(0, 8, 400)
+            h = rng.integers(1, 4, 400).astype(np.uint32)
+            a, n, nq, nr = workloads.c2u_batch(t, NOW0 + t0, h, rng, hot=8, p_override=0.5)
+            g = be.do_limit_arrays(a, n, nq, nr)
+            o = co.do_limit(a, n, nq, nr)
+            for k in ("code", "limit_remaining", "reset_s", "stats"):
+                assert np.array_equal(g[k], o[k]), (t0, k)
+        be.close()
+        co.close()
