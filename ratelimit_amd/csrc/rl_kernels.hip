@@ -2510,7 +2510,10 @@ __device__ inline uint32_t split_group_flags(const SplitPlan& S, uint32_t g, uin
 // of its own with 1024-lane blocks cost every batch 4-6 us of launch on the
 // critical path, 1-3 %, profiles/r02/ab/long_*.)
 constexpr uint32_t SPLIT_UNROLL = 8;
-constexpr uint32_t SPLIT_ST = 8;  // 64-element steps in flight per wave in split_long_body's walks
+#ifndef RL_SPLIT_ST
+#define RL_SPLIT_ST 16  // (8: C2U 3.33-3.42 G, 16: 3.52-3.53 G; 4: 2.2-3.2 G)
+#endif
+constexpr uint32_t SPLIT_ST = RL_SPLIT_ST;  // 64-element steps in flight per wave in split_long_body's walks
 // k_split's workgroup (a long run is reordered by its waves, each walking a
 // chunk of it: more waves, shorter walks, but slower short runs)
 #ifndef RL_SPLIT_THREADS
@@ -2719,6 +2722,7 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
         for (uint32_t w = 0; w < NW; w++) o += s_wh[w][g];
       s_off[tid] = o;
     }
+    if (tid < NW) s_ws[tid] = 0;
     __syncthreads();
     SPLIT_STAMP(3);
     // walk 2, the scatter: a stable rank per group from wave ballots and the
@@ -2726,9 +2730,11 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
     // is still being read), hits in hnew, the run id in rid; only a one-unit
     // group's records are read (its clock, its lone-element flag)
     {
-      uint32_t run[SPLIT_MAXG];
+      uint32_t run[SPLIT_MAXG], acc[NW];  // acc: hits landing in each wave's chunk of the new order
 #pragma unroll
       for (uint32_t g = 0; g < SPLIT_MAXG; g++) run[g] = g < G ? s_wp[wv][g] : 0u;
+#pragma unroll
+      for (uint32_t w = 0; w < NW; w++) acc[w] = 0;
       // (software-pipelined: the next ST steps' loads are issued before this
       // step's stores, so waiting for them never waits for the stores)
       uint32_t fu[SPLIT_ST], e[SPLIT_ST], h[SPLIT_ST];
@@ -2763,6 +2769,12 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
           rank[p + np] = e[st];
           rid[p + np] = s_id[gk];
           hnew[p + np] = h[st];
+          uint32_t dw = 0;  // the wave whose chunk of the new order np is in
+#pragma unroll
+          for (uint32_t w = 1; w < NW; w++) dw += np >= w * CH ? 1u : 0u;
+#pragma unroll
+          for (uint32_t w = 0; w < NW; w++)
+            if (dw == w) acc[w] += h[st];
           if (!s_plan.alias[gk]) {  // (a multi-unit stem's groups share one `now`)
             const Rec x = rec[e[st]];
             const uint32_t f = s_plan.fam[gk], d = div_of(s_lunit[f]);
@@ -2779,26 +2791,19 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
           h[st] = hn[st];
         }
       }
+#pragma unroll
+      for (uint32_t w = 0; w < NW; w++) {
+        const uint32_t t = wave_sum32(acc[w]);
+        if (lane == 0 && t) atomicAdd(&s_ws[w], t);
+      }
     }
     __syncthreads();
     SPLIT_STAMP(4);
-    // walk 3: the hits of each wave's chunk in the new order, then inclusive
-    // sums (mod 2^32, like the bucket kernels') with the group's offset taken
-    // off, and the new permutation from `rank` into svals
-    {
-      uint32_t t = 0;
-      for (uint32_t c = a0; c < a1; c += 64 * SPLIT_ST) {
-#pragma unroll
-        for (uint32_t st = 0; st < SPLIT_ST; st++) {
-          const uint32_t k = c + st * 64 + lane;
-          t += k < a1 ? hnew[p + k] : 0u;
-        }
-      }
-      t = wave_sum32(t);
-      if (lane == 0) s_ws[wv] = t;
-    }
-    __syncthreads();
     SPLIT_STAMP(5);
+    // walk 3: inclusive sums in the new order (mod 2^32, like the bucket
+    // kernels'; each wave starts from the hits of the chunks before its own,
+    // summed by the scatter) with the group's offset taken off, and the new
+    // permutation from `rank` into svals
     {
       uint32_t carry = 0, g = 0;
       for (uint32_t w = 0; w < wv; w++) carry += s_ws[w];
@@ -2817,19 +2822,27 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
           hn[st] = k < a1 ? hnew[p + k] : 0u;
           en[st] = k < a1 ? rank[p + k] : 0u;
         }
+        // the ST wave scans level by level: ST independent cross-lane chains in
+        // flight instead of one (each level is an LDS-crossbar round trip)
+        uint32_t inc[SPLIT_ST];
+#pragma unroll
+        for (uint32_t st = 0; st < SPLIT_ST; st++) inc[st] = h[st];
+#pragma unroll
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+          uint32_t y[SPLIT_ST];
+#pragma unroll
+          for (uint32_t st = 0; st < SPLIT_ST; st++) y[st] = __shfl_up(inc[st], off, 64);
+#pragma unroll
+          for (uint32_t st = 0; st < SPLIT_ST; st++)
+            if (lane >= off) inc[st] += y[st];
+        }
 #pragma unroll
         for (uint32_t st = 0; st < SPLIT_ST; st++) {
           const uint32_t k = c + st * 64 + lane;
-          uint32_t inc = h[st];
-#pragma unroll
-          for (uint32_t off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(inc, off, 64);
-            if (lane >= off) inc += y;
-          }
-          const uint32_t tot = __shfl(inc, 63, 64);
+          const uint32_t tot = __shfl(inc[st], 63, 64);
           if (k < a1) {
             while (g + 1 < G && k >= s_base[g + 1]) g++;  // (k grows along the walk)
-            segsum[p + k] = carry + inc - s_off[g];
+            segsum[p + k] = carry + inc[st] - s_off[g];
             svals[p + k] = e[st];
           }
           carry += tot;
