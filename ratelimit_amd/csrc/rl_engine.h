@@ -18,7 +18,7 @@ namespace rl {
 // Pipeline depth: scratch buffers (and streams) in flight. Stage A of up to
 // NBUF - 1 later batches may run while one batch's stage B holds the table.
 #ifndef RL_NBUF
-#define RL_NBUF 3
+#define RL_NBUF 4
 #endif
 constexpr uint32_t NBUF = RL_NBUF;
 constexpr uint32_t PROF_RING = 8;  // timed batches in flight (> NBUF)
