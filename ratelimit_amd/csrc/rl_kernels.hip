@@ -2331,6 +2331,7 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
                                                    const uint32_t* __restrict__ skeys,
                                                    const uint32_t* __restrict__ rid,
                                                    const uint32_t* __restrict__ run_start,
+                                                   uint32_t* __restrict__ run_end,
                                                    uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
                                                    uint32_t* defer_n, const uint32_t* err,
                                                    const unsigned long long* num_runs, unsigned long long* split,
@@ -2355,12 +2356,20 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
     const uint32_t p = run_start[r];
     const uint32_t eq = rec_s.sv[q], ep = rec_s.sv[p];
     const Rec x = rec[eq], y = rec[ep];
+    // a failed descriptor (FLAG_SKIP) makes its run exact-path: general_body leaves it out
+    const bool skip = (rec_flags(x) | rec_flags(y)) & FLAG_SKIP;
+    const bool same_stem = !skip && x.hlo == y.hlo && (x.lu & 0xFFFFu) == (y.lu & 0xFFFFu) &&  // hash, length
+                           key_equal(key_of(b, x), key_of(b, y));
+    if (!same_stem && !skip && q == p + 1 && run_end[r] == q + 1) {
+      // two unrelated stems sharing the 32-bit sort key (~100 runs per 1M
+      // batch at C1): each is a key seen once in the batch. Neither gets
+      // FLAG_DUP (k_table's singleton part answers both) and the run is
+      // emptied (its sorted path skips it); no k_split pass.
+      run_end[r] = p;
+      continue;
+    }
     rec[eq].lu = x.lu | (FLAG_DUP << 24);
     if (q == p + 1) rec[ep].lu = y.lu | (FLAG_DUP << 24);  // the run's head
-    // a failed descriptor (FLAG_SKIP) makes its run exact-path: general_body leaves it out
-    const bool same_stem = !((rec_flags(x) | rec_flags(y)) & FLAG_SKIP) && x.hlo == y.hlo &&
-                           (x.lu & 0xFFFFu) == (y.lu & 0xFFFFu) &&  // hash, length
-                           key_equal(key_of(b, x), key_of(b, y));
     const bool same = same_stem && rec_unit(x) == rec_unit(y);
     // per position, for k_split's long runs (coalesced there instead of a
     // random record read per element): the unit and max(1, hits)
@@ -4108,7 +4117,7 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
                                                               s.big_n, s.big_cnt, s.err);
 #endif
     k_run_check<<<cdiv(b.n, RC_CHUNK), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[1], s.rid, s.run_start,
-                                                s.run_flags, s.defer, s.defer_n, s.err, s.runs64, s.split,
+                                                s.run_end, s.run_flags, s.defer, s.defer_n, s.err, s.runs64, s.split,
                                                 s.sorted_n, s.grp, s.hit_t);
     k_split<<<SPLIT_BLOCKS, SPLIT_THREADS, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.vals[0], s.segsum, s.rid, s.run_start,
                                           s.run_end, s.run_flags, s.defer, s.defer_n, s.runs64, s.split, s.drun,
