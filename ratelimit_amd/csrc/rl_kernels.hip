@@ -742,12 +742,19 @@ struct SimpleState {
 __device__ __attribute__((always_inline)) inline int simple_pick(SimpleState& S, uint32_t w, uint32_t d) {
   if (S.cur.ws == w) return 0;
   if (S.cur.ws == WS_INVALID || w > S.cur.ws) {
-    if (S.cur.ws != WS_INVALID) {
+    if (S.cur.ws != WS_INVALID && hist_reach(S.cur.ws, w, d)) {
       // the cached record goes back first, unless the old cur takes its
       // position (then it is out of the ring's reach from the new cur)
       if (S.old_dirty && hist_pos(S.old.ws, d) != hist_pos(S.cur.ws, d)) S.ring[hist_pos(S.old.ws, d)] = S.old;
       S.old = S.cur;
       S.old_dirty = true;
+    } else if (S.cur.ws != WS_INVALID) {
+      // the old cur, and every older record, is out of the ring's reach from
+      // w: no lookup can reach them again (simple_pick answers RL_E_TIME
+      // first) and their expiry and local-cache entry are past w, so they
+      // are not written back (a key revisited after more than HIST_W windows,
+      // e.g. a SECOND key every ~20 s at C1: one random write less)
+      S.old_dirty = false;
     }
     S.cur = Win{w, 0, 0, 0};
     return 0;
@@ -3469,7 +3476,8 @@ __device__ __attribute__((always_inline)) inline void runs_body(uint32_t blk, Ba
         Win R = cur;
         if (cur.ws != el0.w) {
           if (cur.ws == WS_INVALID || el0.w > cur.ws) {
-            if (cur.ws != WS_INVALID) ring[hist_pos(cur.ws, el0.d)] = cur;
+            // (the old cur goes to the ring only while in its reach from el0.w: simple_pick)
+            if (cur.ws != WS_INVALID && hist_reach(cur.ws, el0.w, el0.d)) ring[hist_pos(cur.ws, el0.d)] = cur;
             R = Win{el0.w, 0, 0, 0};
             s->cur = R;
           } else if (hist_reach(el0.w, cur.ws, el0.d)) {

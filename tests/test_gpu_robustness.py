@@ -304,3 +304,31 @@ def test_gpu_long_runs_across_fast_blocks_vs_c_oracle():
                     assert np.array_equal(g[k], o[k]), (seed, lc, k)
             be.close()
             co.close()
+
+
+@pytest.mark.parametrize("lc", [False, True])
+def test_gpu_revisit_after_ring_reach_vs_c_oracle(lc):
+    """Keys revisited after more than the ring's 8 windows (a SECOND key every
+    ~20 s at C1): the old window is out of reach from the new one and is not
+    written back to the ring. Later batches revisit, go back inside the
+    reach (windows never written: fresh keys) and stay oracle-exact; a
+    request for the dropped window itself is RL_E_TIME, as before. Short runs
+    (one lane) and long runs (the parallel path) both roll this way."""
+    be = Backend(0.8, lc, **SMALL)
+    co = c_oracle.COracle(0.8, lc)
+    t0 = workloads.NOW0
+    ten = np.r_[np.arange(100), np.full(60, 7)]  # tenant 7 also as a long run
+    hits = np.r_[np.full(100, 30, np.uint32), np.ones(60, np.uint32)]  # over the SECOND limit: local-cache entries
+    for dt in (0, 20, 21, 15, 40, 33, 100, 612):
+        a, n, nq, nr = workloads.c1_batch(ten, t0 + dt, hits)
+        g = be.do_limit_arrays(a, n, nq, nr, isolate=True)
+        o = co.do_limit(a, n, nq, nr)
+        assert not g["status"].any(), dt
+        for k in ("code", "limit_remaining", "reset_s", "stats"):
+            assert np.array_equal(g[k], o[k]), (dt, k)
+    # a SECOND window far behind the newest (t0 + 612): out of the ring's reach
+    a, n, nq, nr = workloads.c1_batch(np.arange(10), t0 + 20)
+    g = be.do_limit_arrays(a, n, nq, nr, isolate=True)
+    assert (g["status"][0::2] == abi.RL_E_TIME).all()
+    be.close()
+    co.close()
