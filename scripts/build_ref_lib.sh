@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build the library of git revision $1 into build_abl/lib_$2.so (A/B baseline
-# for scripts/gpu_ab.sh). Uses a temporary worktree; the tree here is untouched.
+# for scripts/gpu.sh ab). Uses a temporary worktree; the tree here is untouched.
 set -e
 rev=$1; name=$2
 root=$(cd "$(dirname "$0")/.." && pwd)

@@ -3,7 +3,10 @@ union of all kernels' [start, end) against the span from the K-th last
 k_prepare to the last kernel end, and the summed time per kernel over that
 span (per batch).
 
-    python scripts/trace_busy.py <run_kernel_trace.csv> [K=40]
+    python scripts/trace_busy.py <run_kernel_trace.csv> [K=40] [first batch index]
+
+Without a first index the window ends before the last 5 % of batches (bench.py
+runs its latency and host-fed phases last).
 """
 import csv
 import re
@@ -24,8 +27,12 @@ def main():
     if len(preps) < k + 1:
         sys.exit("fewer than %d batches" % (k + 1))
     # the window: K batches ending before the latency steps (skip the last 5 % of batches)
-    tail = max(1, len(preps) // 20)
-    a, b = preps[-(k + tail)], preps[-tail]
+    if len(sys.argv) > 3:
+        f = int(sys.argv[3])
+        a, b = preps[f], preps[f + k]
+    else:
+        tail = max(1, len(preps) // 20)
+        a, b = preps[-(k + tail)], preps[-tail]
     iv = sorted((max(t0, a), min(t1, b)) for _, t0, t1 in ks if t1 > a and t0 < b)
     busy, cur0, cur1 = 0, None, None
     for s, e in iv:
