@@ -183,3 +183,15 @@ def test_gpu_override_restore_then_limit_vs_c_oracle():
                 assert np.array_equal(g[k], o[k]), (t0, k)
         be.close()
         co.close()
+
+
+@pytest.mark.parametrize("lc", [False, True])
+def test_gpu_c2u_bench_scale_vs_c_oracle(lc):
+    """BASELINE-scale C2U batches (1M descriptors; the hottest tenant's stem runs
+    tens of thousands of descriptors under two units: split_long_body's wave
+    walks over many 16-step rounds), across a minute boundary (+40: SECOND and
+    MINUTE share the key), against the C oracle."""
+    z = workloads.ZipfSampler(2_000_000, 1.1)
+    bs = list(workloads.c2u_stream(n_tenants=2_000_000, requests_per_batch=500_000, batches=4, now0=NOW0 + 38,
+                                   sampler=z))
+    _check(bs, lc, table_slots=1 << 23, max_batch=1 << 20)
