@@ -475,8 +475,7 @@ def pcie_fed(args, be, host_batches, now):
         arr = {k: arena.like(v) for k, v in a.items()}
         arr["now"] = arena.like(np.full(bq, now, np.int64))  # (time holds: one second for the whole phase)
         soa.append(PackedBatch(arr, bn, bq, args.n_rules))
-        if args.shards == 1:  # (compact batches: single-shard ctx)
-            comp.append(compact_batch(arr, bn, bq, args.n_rules, alloc=lambda nb: arena.array(nb, np.uint8)))
+        comp.append(compact_batch(arr, bn, bq, args.n_rules, alloc=lambda nb: arena.array(nb, np.uint8)))
     outs = [{k: arena.like(v) for k, v in soa[0].alloc_result().items()} for _ in range(4)]
     n = soa[0].n
     bytes_out = n * 9

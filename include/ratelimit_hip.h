@@ -242,10 +242,14 @@ typedef struct rl_batch_compact {
   uint64_t limits;       /* rl_limit[n_limits] */
 } rl_batch_compact;
 
-/* rl_do_limit_host_async on a compact batch (single-shard ctx): buf crosses
- * PCIe in one copy into a device staging slot while earlier batches compute,
- * is unpacked on the GPU, and the batch is pipelined like any other; *out is
- * read after rl_synchronize. */
+/* rl_do_limit_host_async on a compact batch: on a single-shard ctx buf
+ * crosses PCIe in one copy into a device staging slot while earlier batches
+ * compute, is unpacked on the GPU, and the batch is pipelined like any other.
+ * On a multi-shard ctx it is cut into one request-aligned slice per shard;
+ * each shard copies its slice's parts of buf over its own device's link,
+ * unpacks them and routes them like an rl_batch host slice. *out is read
+ * after rl_synchronize; buf stays untouched until then. Not on a ctx that
+ * joined a communicator (rl_do_limit_routed_async takes device batches). */
 int rl_do_limit_compact_async(rl_ctx* ctx, const rl_batch_compact* in, rl_result* out);
 
 /* Epoch sweep (replaces Redis EXPIRE): tombstones every slot whose counter

@@ -228,17 +228,20 @@ int synchronize_all(rl_ctx* c) {
 }
 
 // One batch through the shards: host (slices over every shard's link) or
-// device (memory of shard 0's GPU: shard 0 takes it whole).
-int shards_submit(rl_ctx* c, const rl_batch* in, rl_result* out, bool host, hipStream_t caller) {
+// device (memory of shard 0's GPU: shard 0 takes it whole). cb: a compact host
+// batch (in then carries only its sizes), cut at request boundaries.
+int shards_submit(rl_ctx* c, const rl_batch* in, rl_result* out, bool host, hipStream_t caller,
+                  const rl_batch_compact* cb = nullptr) {
   const uint32_t N = c->n, n = in->n, nq = in->n_requests;
   const uint32_t slots = (uint32_t)c->pend.size(), s = c->batch_no % slots;
   // the batch that used this slot of the routers is complete: its stats first
   int rc = finalize_stats(c, s, true);
   if (rc) return rc;
   const uint32_t m = in->n_rules * RL_NUM_STATS;
-  if (host && m > c->stats_cap) {  // a larger stats ring: every pending batch finalized first
-    for (uint32_t k = 0; k < slots; k++)
-      if ((rc = finalize_stats(c, k, true))) return rc;
+  if (host && m > c->stats_cap) {  // a larger stats ring: every pending batch completed and finalized first
+    // (the last batch's second half runs only at the next call or a sync:
+    // finalizing its ring entry before that read zeros)
+    if ((rc = synchronize_all(c))) return rc;
     if (c->stats_ring) (void)hipHostFree(c->stats_ring);
     c->stats_ring = nullptr;
     c->stats_cap = 0;
@@ -251,7 +254,13 @@ int shards_submit(rl_ctx* c, const rl_batch* in, rl_result* out, bool host, hipS
   q[0] = 0;
   d[N] = n;
   q[N] = nq;
+  const uint32_t* first = cb ? reinterpret_cast<const uint32_t*>(cb->buf + cb->req_first) : nullptr;
   for (uint32_t j = 1; j < N; j++) {
+    if (cb) {  // (about nq / N requests each; req_first was checked to lie in [0, n] by nobody yet: clamp)
+      q[j] = std::max(q[j - 1], (uint32_t)((uint64_t)nq * j / N));
+      d[j] = std::min(std::max(first[q[j]], d[j - 1]), n);
+      continue;
+    }
     uint32_t x = host ? (uint32_t)((uint64_t)n * j / N) : n;
     if (x < d[j - 1]) x = d[j - 1];
     while (x > 0 && x < n && in->req_idx[x] == in->req_idx[x - 1]) x++;
@@ -265,7 +274,22 @@ int shards_submit(rl_ctx* c, const rl_batch* in, rl_result* out, bool host, hipS
     w.io = CommIO{};
     w.in = *in;
     w.out = rl_result{};
-    if (host) {
+    if (host && cb) {
+      const uint32_t a = d[j], b = d[j + 1];
+      w.in = rl_batch{};
+      w.in.n = b - a;
+      w.in.n_requests = q[j + 1];  // (absolute: the slice's first request is q[j])
+      w.in.n_rules = cb->n_rules;
+      w.out.code = out->code + a;
+      w.out.limit_remaining = out->limit_remaining + a;
+      w.out.reset_s = out->reset_s + a;
+      w.out.status = out->status ? out->status + a : nullptr;
+      w.io.host = true;
+      w.io.cb = cb;
+      w.io.da = a;
+      w.io.qa = q[j];
+      w.io.stats_host = m ? c->stats_ring + ((size_t)s * N + j) * c->stats_cap : nullptr;
+    } else if (host) {
       const uint32_t a = d[j], b = d[j + 1];
       w.in.n = b - a;
       w.in.n_requests = q[j + 1];  // (absolute: the slice's first request is q[j])
@@ -445,9 +469,20 @@ int rl_do_limit_host_async(rl_ctx* c, const rl_batch* in, rl_result* out) {
 
 int rl_do_limit_compact_async(rl_ctx* c, const rl_batch_compact* in, rl_result* out) {
   if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
-  if (c->n > 1) return eng_fail(c->e[0], RL_E_INVALID, "gpu: compact batches need a single-shard ctx");
   if (c->comm) return eng_fail(c->e[0], RL_E_INVALID, "gpu: compact batches are not routed (rl_do_limit_routed_async)");
-  return eng_do_limit_compact_async(c->e[0], in, out);
+  if (c->n == 1) return eng_do_limit_compact_async(c->e[0], in, out);
+  // a multi-shard ctx: one request-aligned slice per shard, each over its own
+  // device's link (rl_comm's stage_host_compact: the slice's parts, unpacked
+  // on the device), then the shards' exchange as for rl_batch host batches
+  if (const int rc = eng_compact_check(c->e[0], in, out)) return from_engine(c, c->e[0], rc);
+  const uint32_t* first = reinterpret_cast<const uint32_t*>(in->buf + in->req_first);
+  if (in->n_requests && (first[0] != 0 || first[in->n_requests] != in->n))
+    return fail(c, RL_E_INVALID, "gpu: compact batch request layout is not a partition of the descriptors");
+  rl_batch sizes{};
+  sizes.n = in->n;
+  sizes.n_requests = in->n_requests;
+  sizes.n_rules = in->n_rules;
+  return shards_submit(c, &sizes, out, true, nullptr, in);
 }
 
 int rl_do_limit(rl_ctx* c, const rl_batch* in, rl_result* out) {

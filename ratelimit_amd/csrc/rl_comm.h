@@ -37,6 +37,9 @@ struct CommIO {
   bool host = false;
   uint32_t da = 0, qa = 0;
   unsigned long long* stats_host = nullptr;
+  // a compact host batch (rl_batch_compact): this slice is its descriptors
+  // [da, in->n + da) and requests [qa, in->n_requests), unpacked on the device
+  const rl_batch_compact* cb = nullptr;
 };
 // One routed batch: this rank's slice (device arrays, or io) -> out in arrival
 // order. Enqueues the batch's first half and runs the previous batch's second

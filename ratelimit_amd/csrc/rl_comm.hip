@@ -103,6 +103,8 @@ struct CommSlot {
   int64_t* h_now = nullptr;
   uint8_t *h_unit = nullptr, *h_flags = nullptr, *h_code = nullptr, *h_status = nullptr;
   uint32_t *h_rem = nullptr, *h_reset = nullptr;
+  uint8_t* h_cbuf = nullptr;  // compact slices: the host buffer's layout, the slice's parts
+  uint64_t h_cbuf_cap = 0;
   unsigned long long* io_stats = nullptr;
 };
 
@@ -165,7 +167,7 @@ int run_group(CommRouter* r, Engine* e, uint32_t ch, hipStream_t st) {
 void free_slot(CommSlot& S) {
   void* bufs[] = {S.send_rec, S.send_stem, S.perm, S.cnt, S.recv_rec, S.recv_stem, S.ret_send, S.back, S.ostats,
                   S.stats_stage, S.h_stem, S.h_off, S.h_req, S.h_limit, S.h_hits, S.h_rule, S.h_now, S.h_unit,
-                  S.h_flags, S.h_code, S.h_status, S.h_rem, S.h_reset, S.io_stats};
+                  S.h_flags, S.h_code, S.h_status, S.h_rem, S.h_reset, S.io_stats, S.h_cbuf};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (hipEvent_t ev : {S.packed, S.sent, S.done})
@@ -212,7 +214,8 @@ hipError_t grow(CommRouter* r, CommSlot& S, uint64_t n_rec, uint64_t n_stem, uin
 // stream (after the slot's previous batch): the same absolute offsets, so the
 // staged view *d indexes like the caller's batch. Checks the sizes the copies
 // rely on first (a failure is the slice's own: zero counts).
-int stage_host(CommRouter* r, Engine* e, CommSlot& S, const rl_batch* in, rl_batch* d) {
+// The slot's host-fed staging arrays (first use).
+int ensure_stage(CommRouter* r, Engine* e, CommSlot& S) {
   const rl_config& g = e->cfg;
   if (!S.h_stem) {
     const bool ok = dalloc(&S.h_stem, (size_t)g.max_stem_bytes + 64) == hipSuccess &&
@@ -224,6 +227,12 @@ int stage_host(CommRouter* r, Engine* e, CommSlot& S, const rl_batch* in, rl_bat
                     dalloc(&S.h_rem, g.max_batch) == hipSuccess && dalloc(&S.h_reset, g.max_batch) == hipSuccess;
     if (!ok) return breaks(r, e, RL_E_HIP, "gpu: host-fed routing staging allocation failed");
   }
+  return RL_OK;
+}
+
+int stage_host(CommRouter* r, Engine* e, CommSlot& S, const rl_batch* in, rl_batch* d) {
+  const rl_config& g = e->cfg;
+  if (const int rc = ensure_stage(r, e, S)) return rc;
   const uint32_t n = in->n, da = S.io.da, qa = S.io.qa, qb = in->n_requests;
   if (!n) {
     *d = *in;
@@ -255,6 +264,65 @@ int stage_host(CommRouter* r, Engine* e, CommSlot& S, const rl_batch* in, rl_bat
   return RL_OK;
 }
 
+// A compact slice: its stems and offsets straight into the staging above (at
+// the same absolute offsets), the rest of its parts into h_cbuf at the host
+// buffer's own offsets, then k_unpack over the slice's descriptors and
+// requests writes the staging arrays. Seven copies per slice (stems, offsets,
+// limit indices, request firsts, clocks, hits, the limit table) of 46 B per
+// descriptor at C1, against stage_host's nine of 60 B. A malformed request
+// layout fails the batch through the partition's validation word.
+int stage_host_compact(CommRouter* r, Engine* e, CommSlot& S, const rl_batch* in, rl_batch* d) {
+  const rl_batch_compact& cb = *S.io.cb;
+  const uint32_t n = in->n, da = S.io.da, db = da + n, qa = S.io.qa, qb = in->n_requests;
+  const rl_config& g = e->cfg;
+  if (const int rc = ensure_stage(r, e, S)) return rc;
+  if ((uint64_t)db > g.max_batch || qb > g.max_requests || qa > qb)
+    return eng_fail(e, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_stem_bytes");
+  if (!n) {
+    *d = *in;
+    return RL_OK;
+  }
+  if (cb.buf_bytes > S.h_cbuf_cap) {  // (the slot's previous batch is drained first)
+    CHK_HIP(e, hipEventSynchronize(S.done));
+    if (S.h_cbuf) CHK_HIP(e, hipFree(S.h_cbuf));
+    S.h_cbuf = nullptr;
+    S.h_cbuf_cap = 0;
+    if (dalloc(&S.h_cbuf, cb.buf_bytes + 64) != hipSuccess)
+      return breaks(r, e, RL_E_HIP, "gpu: compact slice staging allocation failed");
+    S.h_cbuf_cap = cb.buf_bytes;
+  }
+  const uint32_t* off = reinterpret_cast<const uint32_t*>(cb.buf + cb.stem_off);
+  const uint64_t a0 = off[da] & ~3u, a1 = off[db];
+  if (a1 > g.max_stem_bytes || a1 < a0)
+    return eng_fail(e, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_stem_bytes");
+  hipStream_t st = r->cs;
+  auto part = [&](uint64_t sect, uint64_t from, uint64_t bytes) {
+    return bytes ? hipMemcpyAsync(S.h_cbuf + sect + from, cb.buf + sect + from, bytes, hipMemcpyHostToDevice, st)
+                 : hipSuccess;
+  };
+  if (a1 > a0) CHK_HIP(e, hipMemcpyAsync(S.h_stem + a0, cb.buf + cb.stem_bytes + a0, a1 - a0, hipMemcpyHostToDevice, st));
+  CHK_HIP(e, hipMemcpyAsync(S.h_off + da, off + da, (n + 1) * 4ull, hipMemcpyHostToDevice, st));
+  CHK_HIP(e, part(cb.limit_idx, 2ull * da, 2ull * n));
+  CHK_HIP(e, part(cb.req_first, 4ull * qa, 4ull * (qb - qa + 1)));
+  CHK_HIP(e, part(cb.now, 4ull * qa, 4ull * (qb - qa)));
+  CHK_HIP(e, part(cb.hits, 4ull * qa, 4ull * (qb - qa)));
+  CHK_HIP(e, part(cb.limits, 0, 12ull * cb.n_limits));
+  launch_unpack_range(cb, S.h_cbuf, da, db, qa, qb, S.h_req, S.h_unit, S.h_flags, S.h_limit, S.h_hits, S.h_rule,
+                      S.h_now, e->errw + NBUF + 2, st);
+  CHK_HIP(e, hipGetLastError());
+  *d = *in;
+  d->stem_bytes = S.h_stem;
+  d->stem_off = S.h_off + da;
+  d->now = S.h_now;
+  d->req_idx = S.h_req + da;
+  d->unit = S.h_unit + da;
+  d->flags = S.h_flags + da;
+  d->limit = S.h_limit + da;
+  d->hits = S.h_hits + da;
+  d->rule_id = S.h_rule + da;
+  return RL_OK;
+}
+
 // First half of a batch (slot s): partition, counts exchange, counts to the
 // host. `hostrc` != RL_OK: the slice was rejected before the partition; it
 // sends zero counts. (The next call's second half waits on the host for this
@@ -271,7 +339,7 @@ int first_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, const rl_batch
   int rc = hostrc;
   rl_batch staged;
   if (!rc && S.io.host) {
-    rc = stage_host(r, e, S, in, &staged);
+    rc = S.io.cb ? stage_host_compact(r, e, S, in, &staged) : stage_host(r, e, S, in, &staged);
     if (r->broken) return rc;
     in = &staged;
   }

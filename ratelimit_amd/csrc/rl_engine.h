@@ -111,6 +111,8 @@ int eng_do_limit(Engine* c, const rl_batch* in, rl_result* out);
 int eng_do_limit_async(Engine* c, const rl_batch* in, rl_result* out, void* stream);
 int eng_do_limit_host_async(Engine* c, const rl_batch* in, rl_result* out);
 int eng_do_limit_compact_async(Engine* c, const rl_batch_compact* in, rl_result* out);
+// The compact batch's sizes and sections against the ctx's limits (no GPU work).
+int eng_compact_check(Engine* c, const rl_batch_compact* in, const rl_result* out);
 int eng_synchronize(Engine* c);
 int eng_sweep(Engine* c, int64_t now, uint64_t* n_evicted);
 int eng_restore(Engine* c, const rl_restore_batch* in);

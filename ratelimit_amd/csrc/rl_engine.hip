@@ -720,7 +720,8 @@ int eng_do_limit_host_async(Engine* c, const rl_batch* in, rl_result* out) {
 // cbuf, k_unpack rebuilds the rl_batch arrays in the slot, then as above. Section
 // bounds are checked here; contents (offsets, request ranges, limit indices)
 // on the device, like rl_batch's.
-int eng_do_limit_compact_async(Engine* c, const rl_batch_compact* in, rl_result* out) {
+// The compact batch's sizes and sections (every entry point taking one).
+int eng_compact_check(Engine* c, const rl_batch_compact* in, const rl_result* out) {
   if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
   const rl_config& g = c->cfg;
   const uint32_t n = in->n, nq = in->n_requests;
@@ -738,8 +739,18 @@ int eng_do_limit_compact_async(Engine* c, const rl_batch_compact* in, rl_result*
   const uint64_t nb = n ? reinterpret_cast<const uint32_t*>(in->buf + in->stem_off)[n] : 0;
   if (nb > g.max_stem_bytes) return set_err(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_stem_bytes");
   if (!sect(in->stem_bytes, nb)) return set_err(c, RL_E_INVALID, "gpu: compact batch stems outside buf");
+  return RL_OK;
+}
+
+int eng_do_limit_compact_async(Engine* c, const rl_batch_compact* in, rl_result* out) {
+  int rc = eng_compact_check(c, in, out);
+  if (rc) return rc;
+  const rl_config& g = c->cfg;
+  const uint32_t n = in->n, nq = in->n_requests;
+  const uint64_t B = in->buf_bytes;
+  const uint64_t nb = n ? reinterpret_cast<const uint32_t*>(in->buf + in->stem_off)[n] : 0;
   HIPCHK(c, hipSetDevice(g.device));
-  int rc = ensure_host_slots(c);
+  rc = ensure_host_slots(c);
   if (rc) return rc;
   const uint32_t j = c->hnext;
   HostSlot& h = c->hs[j];

@@ -211,6 +211,12 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
 // index past the table gives the descriptor unit 0 (k_prepare: RL_E_INVALID).
 void launch_unpack(const rl_batch_compact& cb, const uint8_t* buf, uint32_t* req, uint8_t* unit, uint8_t* flags,
                    uint32_t* limit, uint32_t* hits, uint32_t* rule, int64_t* now, uint32_t* err, hipStream_t st);
+// The same over descriptors [d0, d1) and requests [q0, q1) of the batch (a
+// multi-shard ctx's slice: buf mirrors the host buffer's layout, only the
+// slice's parts present; the outputs at the same absolute indices).
+void launch_unpack_range(const rl_batch_compact& cb, const uint8_t* buf, uint32_t d0, uint32_t d1, uint32_t q0,
+                         uint32_t q1, uint32_t* req, uint8_t* unit, uint8_t* flags, uint32_t* limit, uint32_t* hits,
+                         uint32_t* rule, int64_t* now, uint32_t* err, hipStream_t st);
 // counts: cstride u64 per owner (records, stem bytes[, meta0, meta1]).
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
                        uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st,

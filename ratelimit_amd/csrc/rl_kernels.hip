@@ -193,10 +193,11 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
 // hits and first descriptor; per descriptor a 16-bit index into the batch's
 // limit table) -> the rl_batch arrays the pipeline reads. One lane per
 // descriptor (its limit) and per request (its descriptors' request index and
-// hits, its 64-bit clock). A request layout that is not a partition of
-// [0, n) into non-decreasing ranges fails the batch (ERR_INVALID): a
-// descriptor left out would keep a stale request index.
-__global__ __launch_bounds__(256) void k_unpack(uint32_t n, uint32_t nq, uint32_t n_limits,
+// hits, its 64-bit clock), over descriptors [d0, n) and requests [q0, nq) (a
+// multi-shard ctx's slice; indices stay absolute). A request layout that is
+// not a partition of [d0, n) into non-decreasing ranges fails the batch
+// (ERR_INVALID): a descriptor left out would keep a stale request index.
+__global__ __launch_bounds__(256) void k_unpack(uint32_t d0, uint32_t n, uint32_t q0, uint32_t nq, uint32_t n_limits,
                                                 const uint16_t* __restrict__ lidx, const rl_limit* __restrict__ lim,
                                                 const uint32_t* __restrict__ first, const uint32_t* __restrict__ now32,
                                                 const uint32_t* __restrict__ hits_q, uint32_t* __restrict__ req,
@@ -204,7 +205,7 @@ __global__ __launch_bounds__(256) void k_unpack(uint32_t n, uint32_t nq, uint32_
                                                 uint32_t* __restrict__ limit, uint32_t* __restrict__ hits,
                                                 uint32_t* __restrict__ rule, int64_t* __restrict__ now,
                                                 uint32_t* err) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t i = d0 + blockIdx.x * 256 + threadIdx.x;
   if (i < n) {
     const uint32_t k = lidx[i];
     const rl_limit L = k < n_limits ? lim[k] : rl_limit{0, 0, 0, 0, 0};  // unit 0: the descriptor's RL_E_INVALID
@@ -213,9 +214,11 @@ __global__ __launch_bounds__(256) void k_unpack(uint32_t n, uint32_t nq, uint32_
     limit[i] = L.requests_per_unit;
     rule[i] = L.rule_id;
   }
-  if (i < nq) {
+  const uint32_t iq = q0 + blockIdx.x * 256 + threadIdx.x;
+  if (iq < nq) {
+    const uint32_t i = iq;
     const uint32_t a = first[i], z = first[i + 1];
-    if (z < a || z > n || (i == 0 && a != 0) || (i + 1 == nq && z != n)) {
+    if (z < a || z > n || a < d0 || (i == q0 && a != d0) || (i + 1 == nq && z != n)) {
       atomicOr(err, ERR_INVALID);
     } else {
       const uint32_t h = hits_q[i];
@@ -226,15 +229,21 @@ __global__ __launch_bounds__(256) void k_unpack(uint32_t n, uint32_t nq, uint32_
     }
     now[i] = now32[i];
   }
-  if (i == 0 && nq == 0 && n) atomicOr(err, ERR_INVALID);  // descriptors without a request
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nq == q0 && n > d0) atomicOr(err, ERR_INVALID);  // descriptors without a request
 }
 
 void launch_unpack(const rl_batch_compact& cb, const uint8_t* buf, uint32_t* req, uint8_t* unit, uint8_t* flags,
                    uint32_t* limit, uint32_t* hits, uint32_t* rule, int64_t* now, uint32_t* err, hipStream_t st) {
-  const uint32_t m = cb.n > cb.n_requests ? cb.n : cb.n_requests;
+  launch_unpack_range(cb, buf, 0, cb.n, 0, cb.n_requests, req, unit, flags, limit, hits, rule, now, err, st);
+}
+
+void launch_unpack_range(const rl_batch_compact& cb, const uint8_t* buf, uint32_t d0, uint32_t d1, uint32_t q0,
+                         uint32_t q1, uint32_t* req, uint8_t* unit, uint8_t* flags, uint32_t* limit, uint32_t* hits,
+                         uint32_t* rule, int64_t* now, uint32_t* err, hipStream_t st) {
+  const uint32_t m = d1 - d0 > q1 - q0 ? d1 - d0 : q1 - q0;
   if (!m) return;
   k_unpack<<<(m + 255) / 256, 256, 0, st>>>(
-      cb.n, cb.n_requests, cb.n_limits, reinterpret_cast<const uint16_t*>(buf + cb.limit_idx),
+      d0, d1, q0, q1, cb.n_limits, reinterpret_cast<const uint16_t*>(buf + cb.limit_idx),
       reinterpret_cast<const rl_limit*>(buf + cb.limits), reinterpret_cast<const uint32_t*>(buf + cb.req_first),
       reinterpret_cast<const uint32_t*>(buf + cb.now), reinterpret_cast<const uint32_t*>(buf + cb.hits), req, unit,
       flags, limit, hits, rule, now, err);

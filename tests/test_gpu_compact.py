@@ -28,7 +28,8 @@ def _check(got, want, batches, isolate=()):
         n, nr = batches[i][1], batches[i][3]
         for k in ("code", "limit_remaining", "reset_s"):
             assert np.array_equal(g[k][:n], w[k]), "batch %d: %s differs" % (i, k)
-        assert np.array_equal(g["stats"][:nr * abi.RL_NUM_STATS], w["stats"]), i
+        assert np.array_equal(g["stats"][:nr * abi.RL_NUM_STATS], w["stats"]), (i, g["stats"][:nr * abi.RL_NUM_STATS],
+                                                                                w["stats"])
         if i in isolate:
             assert (g["status"][:n] == 0).all()
 
@@ -134,3 +135,38 @@ def test_gpu_compact_bad_limit_index_fails_alone_and_bad_layout_fails_batch():
     with pytest.raises(RedisError):
         be.do_limit_compact_async(cb, cb.alloc_result())
     be.close()
+
+
+@pytest.mark.parametrize("n_shards,lc", [(2, False), (3, True)])
+def test_gpu_compact_multishard_matches_oracle(n_shards, lc):
+    """A ctx hash-sharded over 2-3 tables on cuda:0: each compact batch is cut
+    into request-aligned slices, each shard copies and unpacks its slice and
+    routes it (C2 and C2U batches, a status batch, ragged slices at the
+    request cuts) — answers and summed stats equal the C oracle's."""
+    z = workloads.ZipfSampler(20_000, 1.1)
+    batches = list(workloads.c2_stream(n_tenants=20_000, requests_per_batch=30_001, batches=2, sampler=z))
+    batches += list(workloads.c2u_stream(seed=5, n_tenants=20_000, requests_per_batch=29_999, batches=3,
+                                         now0=workloads.NOW0 + 38, sampler=z))
+    want = _want(batches, lc)
+    be = Backend(0.8, lc, table_slots=1 << 18, max_batch=1 << 17, max_rules=32, n_shards=n_shards,
+                 shard_devices=[0] * n_shards, hash_seed=91)
+    arena = PinnedArena()
+    keep, got = [], []
+    for i, (a, n, nq, nr) in enumerate(batches):
+        cb = compact_batch(a, n, nq, nr, alloc=lambda nb: arena.array(nb, np.uint8))
+        out = {k: arena.like(v) for k, v in cb.alloc_result(isolate=(i == 3)).items()}
+        keep.append((cb, out, be.do_limit_compact_async(cb, out)))
+        got.append(out)
+    be.synchronize()
+    _check(got, want, batches, isolate=(3,))
+    # a request layout that does not cover [0, n): refused or failed at synchronize, on every shard count
+    a, n, nq, nr = batches[0]
+    cb = compact_batch(a, n, nq, nr)
+    rf = cb.buf[cb.offsets["req_first"]:cb.offsets["req_first"] + 4 * (nq + 1)].view(np.uint32)
+    rf[nq // 2], rf[nq // 2 + 1] = rf[nq // 2 + 1], rf[nq // 2]
+    bad_out = cb.alloc_result()  # (kept until synchronize, like every output)
+    with pytest.raises(RedisError):
+        keep.append(be.do_limit_compact_async(cb, bad_out))
+        be.synchronize()
+    be.close()
+    arena.close()
