@@ -454,7 +454,10 @@ typedef struct rl_request_result {
 
 /* GetLimit + DoLimit + the unlimited mapping for a batch of raw requests.
  * Synchronous. A descriptor whose override or config unit is not 1..4 fails
- * the batch with RL_E_INVALID (the reference panics in UnitToDivider). */
+ * the batch with RL_E_INVALID (the reference panics in UnitToDivider). On a
+ * multi-shard ctx the match runs on shard 0's GPU and the matched descriptors
+ * go through the shards like a device batch (every owner answers its keys);
+ * not on a ctx that joined a communicator. */
 int rl_do_limit_requests(rl_ctx* ctx, const rl_request_batch* in, rl_request_result* out);
 
 /* ---- Host packer -------------------------------------

@@ -689,8 +689,26 @@ int rl_config_load(rl_ctx* c, const rl_config_tree* t) {
 
 int rl_do_limit_requests(rl_ctx* c, const rl_request_batch* in, rl_request_result* out) {
   if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
-  if (c->n > 1) return fail(c, RL_E_INVALID, "gpu: rl_do_limit_requests runs on a single-shard ctx");
-  return eng_do_limit_requests(c->e[0], in, out);
+  if (c->comm) return fail(c, RL_E_INVALID, "gpu: rl_do_limit_requests is not routed (rl_do_limit_routed_async)");
+  if (c->n == 1) return eng_do_limit_requests(c->e[0], in, out);
+  // a multi-shard ctx: the config match on shard 0's GPU, the matched batch
+  // through the shards as a device batch (shard 0 partitions it, every owner
+  // answers its keys), then the expansion to the request layout on shard 0
+  int rc = synchronize_all(c);  // (earlier batches first: the call is synchronous)
+  if (rc) return rc;
+  struct Run {
+    rl_ctx* c;
+    bool failed;
+  } u{c, false};
+  auto run = [](void* p, const rl_batch* din, rl_result* dout, hipStream_t st) -> int {
+    Run& r = *static_cast<Run*>(p);
+    const int sr = shards_submit(r.c, din, dout, false, st);
+    const int yr = synchronize_all(r.c);
+    r.failed = sr || yr;
+    return sr ? sr : yr;
+  };
+  rc = eng_do_limit_requests(c->e[0], in, out, run, &u);
+  return u.failed ? rc : from_engine(c, c->e[0], rc);
 }
 
 // Diagnostics, profiling and the per-rank routing halves act on shard 0.

@@ -134,7 +134,12 @@ int eng_route_scatter(Engine* c, uint32_t n, const uint32_t* perm, const uint64_
 int eng_profile(Engine* c, int enable);
 int eng_profile_read(Engine* c, double* ms, uint32_t n, uint64_t* batches);
 int eng_config_load(Engine* c, const rl_config_tree* tree);
-int eng_do_limit_requests(Engine* c, const rl_request_batch* in, rl_request_result* out);
+// The DoLimit step of eng_do_limit_requests done elsewhere (a multi-shard
+// ctx's shards): the matched batch and the result arrays in device memory of
+// c's GPU, inputs ready on `st`; returns once the results are complete.
+using RequestsDoLimit = int (*)(void* user, const rl_batch* dev_in, rl_result* dev_out, hipStream_t st);
+int eng_do_limit_requests(Engine* c, const rl_request_batch* in, rl_request_result* out, RequestsDoLimit run = nullptr,
+                          void* user = nullptr);
 int eng_local_cache_info_get(Engine* c, int64_t now, rl_local_cache_info* info);
 int eng_snapshot_size(Engine* c, uint64_t* bytes);
 int eng_snapshot_save(Engine* c, void* host, uint64_t bytes);

@@ -1071,7 +1071,8 @@ int eng_config_load(Engine* c, const rl_config_tree* t) {
   return RL_OK;
 }
 
-int eng_do_limit_requests(Engine* c, const rl_request_batch* in, rl_request_result* out) {
+int eng_do_limit_requests(Engine* c, const rl_request_batch* in, rl_request_result* out, RequestsDoLimit run,
+                          void* user) {
   if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
   // checkServiceErr(snappedConfig != nil, ...) (ratelimit.go:106)
   if (!c->cfg_loaded) return set_err(c, RL_E_INVALID, "gpu: no rate limit configuration loaded");
@@ -1187,9 +1188,20 @@ int eng_do_limit_requests(Engine* c, const rl_request_batch* in, rl_request_resu
   pb.limit = c->d_limit;
   pb.hits = c->d_hits;
   pb.rule_id = c->d_rule;
-  BatchDev b = dev_view(c, &pb, c->cfg.max_stem_bytes);
-  OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats, nullptr};
-  enqueue(c, b, o, 0, st, false);
+  if (run) {
+    rl_result dout{};
+    dout.code = c->d_code;
+    dout.limit_remaining = c->d_rem;
+    dout.reset_s = c->d_reset;
+    dout.stats = reinterpret_cast<uint64_t*>(c->d_stats);
+    const int rc = run(user, &pb, &dout, st);
+    if (rc) return rc;  // (the runner's own error report)
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+  } else {
+    BatchDev b = dev_view(c, &pb, c->cfg.max_stem_bytes);
+    OutDev o{c->d_code, c->d_rem, c->d_reset, c->d_stats, nullptr};
+    enqueue(c, b, o, 0, st, false);
+  }
   ReqOutDev ro{B + o_code, (uint32_t*)(B + o_rem), (uint32_t*)(B + o_reset), B + o_match,
                (uint32_t*)(B + o_orule), (uint32_t*)(B + o_orpu), B + o_ounit};
   launch_match_expand(r, m, c->d_code, c->d_rem, c->d_reset, ro, st);

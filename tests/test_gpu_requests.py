@@ -160,6 +160,33 @@ def test_gpu_request_stream_matches_oracle_service(seed, local_cache, prefix, ra
         svc.close()
 
 
+@pytest.mark.parametrize("n_shards,seed,local_cache", [(2, 2, True), (3, 3, False)])
+def test_gpu_request_stream_multishard_matches_oracle_service(n_shards, seed, local_cache):
+    """rl_do_limit_requests on a ctx hash-sharded over 2-3 tables on cuda:0:
+    the config match on shard 0, the matched descriptors routed to their
+    owners; statuses, codes and per-rule stats equal the oracle service's."""
+    reqs, nows = gen_requests(seed, 1200)
+    svc = GpuRateLimitService(FILES, 0.8, local_cache, "", n_shards=n_shards, shard_devices=[0] * n_shards,
+                              hash_seed=5, **SMALL)
+    store = StatsStore()
+    osvc = OracleService(RateLimitConfig(FILES, store), O.OracleFixedRateLimitCache(0.8, local_cache, ""))
+    rng = random.Random(seed * 7)
+    try:
+        i = 0
+        while i < len(reqs):
+            j = min(len(reqs), i + rng.choice([1, 7, 64, 300]))
+            got = svc.should_rate_limit_batch(reqs[i:j], nows[i:j])
+            for r, now, (gcode, gsts) in zip(reqs[i:j], nows[i:j], got):
+                ocode, osts, _ = osvc.should_rate_limit(r, now)
+                assert gcode == ocode
+                assert [st_tuple(s) for s in gsts] == [st_tuple(s) for s in osts]
+            i = j
+        want = {k: list(v.as_tuple()) for k, v in store.by_key.items() if any(v.as_tuple())}
+        assert svc.stats == want
+    finally:
+        svc.close()
+
+
 def test_gpu_request_large_batch_matches_oracle_service():
     """One 20k-request batch (~50k descriptors): compaction at scale."""
     reqs, nows = gen_requests(11, 20000, p_override=0.01)
