@@ -293,7 +293,9 @@ int stage_host_compact(CommRouter* r, Engine* e, CommSlot& S, const rl_batch* in
   }
   const uint32_t* off = reinterpret_cast<const uint32_t*>(cb.buf + cb.stem_off);
   const uint64_t a0 = off[da] & ~3u, a1 = off[db];
-  if (a1 > g.max_stem_bytes || a1 < a0)
+  if (a1 < a0 || a1 > off[cb.n])  // (offsets out of order: never read past the buffer's stems)
+    return eng_fail(e, RL_E_INVALID, "gpu: compact batch stem offsets out of order");
+  if (a1 > g.max_stem_bytes)
     return eng_fail(e, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_stem_bytes");
   hipStream_t st = r->cs;
   auto part = [&](uint64_t sect, uint64_t from, uint64_t bytes) {
