@@ -3896,7 +3896,10 @@ __global__ __launch_bounds__(256, RL_KTABLE_WAVES) void k_table(uint32_t g_runs,
 // rare exact path spills to scratch instead of lowering the streaming part's
 // occupancy (uncapped, the exact path's 88 VGPRs slowed the long-run part
 // 55 -> 85 us at C2).
-__global__ __launch_bounds__(256, 8) void k_late(BatchDev b, TableDev t, Params P, SRec rec_s,
+#ifndef RL_LATE_OCC
+#define RL_LATE_OCC 8  // k_late's waves per SIMD (8: <= 64 VGPRs, the rare exact path spills; 6: the same, 4: C2 -7 %)
+#endif
+__global__ __launch_bounds__(256, RL_LATE_OCC) void k_late(BatchDev b, TableDev t, Params P, SRec rec_s,
                                                  const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ svals,
                                                  unsigned long long* __restrict__ res,
                                                  const uint32_t* __restrict__ run_start,
