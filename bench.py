@@ -48,7 +48,11 @@ def parse():
     ap.add_argument("--requests", type=int, default=500_000, help="requests per batch per GPU (2 descriptors each)")
     ap.add_argument("--tenants", type=int, default=0, help="tenants per GPU (default 10M; c3 62.5M)")
     ap.add_argument("--distinct-batches", type=int, default=4)
-    ap.add_argument("--latency-steps", type=int, default=50)
+    ap.add_argument("--latency-steps", type=int, default=1000,
+                    help="batches timed one at a time (submit -> outputs ready): p50/p99_batch_ms")
+    ap.add_argument("--loaded-steps", type=int, default=1000,
+                    help="batches submitted at the measured headline rate with the pipeline full: "
+                         "p50/p99_loaded_batch_ms (submit -> outputs ready, rl_batch_progress)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--prof-every", type=int, default=7,
@@ -217,7 +221,7 @@ def main():
         host_batches.append((a, bn, bq))
         dev_batches.append(to_dev(a, torch))
     stem_len = 34
-    total_steps = args.warmup + args.steps + args.steps + args.latency_steps
+    total_steps = args.warmup + args.steps + args.steps + args.latency_steps + args.loaded_steps
     nows = [torch.full((nq,), now0 + s, dtype=torch.int64, device="cuda") for s in range(total_steps)]
     torch.cuda.synchronize()
 
@@ -280,6 +284,9 @@ def main():
         sync()
         lat.append((time.perf_counter() - t1) * 1e3)
     lat = np.array(lat) if lat else np.array([float("nan")])
+    loaded = None
+    if not routed and args.shards == 1 and args.loaded_steps > 0:
+        loaded = loaded_latency(be, run_step, args.loaded_steps, elapsed / args.steps)
     pcie = None if (routed or args.pcie_steps <= 0) else pcie_fed(args, be, host_batches, now0 + total_steps)
     info = be.table_info()
     if routed:
@@ -353,7 +360,10 @@ def main():
                                       "all_to_all routing from Python (%s)" % args.dist_backend)) if routed else
                                   ("one ctx, table hash-sharded over %d shards on this GPU (loopback routing)"
                                    % args.shards) if args.shards > 1 else "single GPU"},
-        "p50_batch_ms": float(np.percentile(lat, 50)), "p99_batch_ms": p99, "pcie_fed": pcie,
+        "p50_batch_ms": float(np.percentile(lat, 50)), "p99_batch_ms": p99, "latency_batches": int(lat.size),
+        **({"p50_loaded_batch_ms": loaded["p50_ms"], "p99_loaded_batch_ms": loaded["p99_ms"],
+            "loaded": loaded} if loaded else {}),
+        "pcie_fed": pcie,
         "roofline": roofline, "cpu_baseline": cpu, "fill_s": round(t_fill, 2),
         **({"route_host_ms_per_step": route_host} if py_route else {}),
     }
@@ -361,6 +371,38 @@ def main():
     be.close()
     if routed:
         dist.destroy_process_group()
+
+
+def loaded_latency(be, run_step, k_steps, interval_s):
+    """Batch latency under load: k_steps batches submitted open-loop at the
+    measured headline rate (one every interval_s, the pipeline full), each
+    timed from its submit call to the moment rl_batch_progress first reports
+    its outputs complete (polled between submissions, ~5 us resolution)."""
+    sub, done = [], []
+    s0, d0 = be.batch_progress()
+
+    def poll():
+        _, d = be.batch_progress()
+        t = time.perf_counter()
+        while len(done) < d - d0:
+            done.append(t)
+
+    t0 = time.perf_counter()
+    for i in range(k_steps):
+        target = t0 + i * interval_s
+        while time.perf_counter() < target:
+            poll()
+        sub.append(time.perf_counter())
+        run_step()
+        poll()
+    while len(done) < k_steps:
+        poll()
+    el = done[-1] - t0
+    lat = (np.array(done[:k_steps]) - np.array(sub)) * 1e3
+    return {"p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
+            "max_ms": float(lat.max()), "batches": k_steps, "offered_interval_ms": interval_s * 1e3,
+            "achieved_interval_ms": el / k_steps * 1e3,
+            "method": "open-loop submissions at the timed rate; completion = rl_batch_progress (outputs written)"}
 
 
 def loopback_main(args):
@@ -468,14 +510,15 @@ def pcie_fed(args, be, host_batches, now):
     args.pcie_steps queued batches, then per-batch latency (submit -> outputs
     on the host)."""
     from ratelimit_amd.limiter import PinnedArena
-    from ratelimit_amd.packing import PackedBatch, compact_batch
+    from ratelimit_amd.packing import PackedBatch, compact_batch, prefixed_batch
     arena = PinnedArena()
-    soa, comp = [], []
+    soa, comp, pref = [], [], []
     for a, bn, bq in host_batches:
         arr = {k: arena.like(v) for k, v in a.items()}
         arr["now"] = arena.like(np.full(bq, now, np.int64))  # (time holds: one second for the whole phase)
         soa.append(PackedBatch(arr, bn, bq, args.n_rules))
         comp.append(compact_batch(arr, bn, bq, args.n_rules, alloc=lambda nb: arena.array(nb, np.uint8)))
+        pref.append(prefixed_batch(arr, bn, bq, args.n_rules, alloc=lambda nb: arena.array(nb, np.uint8)))
     outs = [{k: arena.like(v) for k, v in soa[0].alloc_result().items()} for _ in range(4)]
     n = soa[0].n
     bytes_out = n * 9
@@ -512,6 +555,7 @@ def pcie_fed(args, be, host_batches, now):
         int(soa[0].arrays["stem_off"][n])
     r_soa = phase(soa, be.do_limit_host_async, soa_in)
     r_comp = phase(comp, be.do_limit_compact_async, int(comp[0].buf.size)) if comp else None
+    r_pref = phase(pref, be.do_limit_prefixed_async, int(pref[0].buf.size)) if pref else None
     # the link's own rate for one large page-locked copy, the bound to read h2d_GBps against
     import torch
     big = arena.array(256 << 20, np.uint8)
@@ -526,19 +570,40 @@ def pcie_fed(args, be, host_batches, now):
     peak = 5 * (256 << 20) / (time.perf_counter() - t1) / 1e9
     del dst, src
     arena.close()
-    for r in (r_soa, r_comp):
+    for r in (r_soa, r_comp, r_pref):
         if r:
             r["h2d_peak_GBps"] = peak
             r["frac_of_h2d_peak"] = r["h2d_GBps"] / peak
     r_soa["format"] = "rl_batch arrays (rl_do_limit_host_async: 9 copies per batch)"
-    if not r_comp:
-        r_soa["buffers"] = "page-locked (rl_alloc_host); now constant over the phase"
-        return r_soa
     r_comp["format"] = "rl_batch_compact (rl_do_limit_compact_async: one buffer, one copy per batch)"
-    r_comp["buffers"] = "page-locked (rl_alloc_host); now constant over the phase"
-    r_comp["soa"] = {k: r_soa[k] for k in ("value", "h2d_bytes_per_decision", "frac_of_h2d_peak", "p99_batch_ms",
-                                           "format")}
-    return r_comp
+    r_pref["format"] = ("rl_batch_prefixed (rl_do_limit_prefixed_async: one buffer, one copy per batch; each "
+                        "request's shared stem prefix once)")
+    r_pref["buffers"] = "page-locked (rl_alloc_host); now constant over the phase"
+    r_pref["host_numa"] = host_numa()
+    keys = ("value", "h2d_bytes_per_decision", "h2d_GBps", "frac_of_h2d_peak", "p99_batch_ms", "format")
+    r_pref["compact"] = {k: r_comp[k] for k in keys}
+    r_pref["soa"] = {k: r_soa[k] for k in keys}
+    return r_pref
+
+
+def host_numa():
+    """Where the fed phase ran: the GPU's NUMA node (sysfs) and the nodes of the
+    CPUs this process may run on (pinned buffers are first-touched by it)."""
+    out = {}
+    try:
+        import glob
+        nodes = sorted({open(p).read().strip() for p in glob.glob("/sys/class/drm/card*/device/numa_node")})
+        out["gpu_numa_nodes"] = nodes
+        cpus = sorted(os.sched_getaffinity(0))
+        cnodes = set()
+        for c in cpus[:256]:
+            for p in glob.glob("/sys/devices/system/cpu/cpu%d/node*" % c):
+                cnodes.add(os.path.basename(p)[4:])
+        out["cpu_numa_nodes"] = sorted(cnodes)
+        out["cpus"] = len(cpus)
+    except Exception as e:  # (informational only)
+        out["error"] = repr(e)
+    return out
 
 
 def cpu_baseline(args, W):

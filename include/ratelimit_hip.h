@@ -205,6 +205,13 @@ int rl_do_limit_async(rl_ctx* ctx, const rl_batch* in, rl_result* out, void* str
 int rl_do_limit_host_async(rl_ctx* ctx, const rl_batch* in, rl_result* out);
 int rl_synchronize(rl_ctx* ctx);
 
+/* Pipelined batchers (single-shard ctx): the number of batches submitted
+ * through rl_do_limit* so far and how many of them, in submission order, have
+ * their outputs complete (host-fed batches: copied back). Never waits, so a
+ * batcher can hand out the answers of finished batches while later ones run;
+ * device-side errors are still reported by rl_synchronize. */
+int rl_batch_progress(rl_ctx* ctx, uint64_t* submitted, uint64_t* completed);
+
 /* ---- Compact host batch: the fed path's PCIe format ---------------------
  * The same batch as rl_batch, laid out for the link: ONE contiguous host
  * buffer (one copy per batch), per request its clock, HitsAddend and first
@@ -251,6 +258,55 @@ typedef struct rl_batch_compact {
  * after rl_synchronize; buf stays untouched until then. Not on a ctx that
  * joined a communicator (rl_do_limit_routed_async takes device batches). */
 int rl_do_limit_compact_async(rl_ctx* ctx, const rl_batch_compact* in, rl_result* out);
+
+/* ---- Prefix-shared batch: the densest PCIe format ----------------------
+ * Every descriptor of one RateLimitRequest starts with the same
+ * prefix ‖ domain ‖ '_' and, in practice, with its request's leading entries
+ * (cache_key.go:62-71; nested descriptors repeat their parents'). This layout
+ * stores those shared bytes once per request and each descriptor's remaining
+ * suffix: descriptor d of request q has the stem prefix[q] ‖ suffix[d]. Per
+ * request: descriptor count and prefix length (one u32), UnixNow(), HitsAddend;
+ * per descriptor: one u32 (limit index, suffix length). 31.5 B per decision at
+ * BASELINE C1 (25-B shared prefix, two 9-B suffixes) against rl_batch_compact's
+ * 46 and rl_batch's 60. Requests form tiles of RL_PREFIXED_TILE; the index
+ * holds each tile's starting offsets, which the batcher has at hand while it
+ * appends, so the GPU unpacks every tile independently (no scan pass) and a
+ * multi-shard ctx cuts the batch at tile boundaries without reading it.
+ * Answers, errors and statuses are those of the equivalent rl_batch (a limit
+ * index >= n_limits, or a stem of 0 or more than 65535 bytes, is an
+ * RL_E_INVALID descriptor; an index that does not match the sections fails
+ * the batch with RL_E_INVALID at rl_synchronize). */
+#define RL_PREFIXED_TILE 256u
+typedef struct rl_batch_prefixed {
+  uint32_t n;            /* descriptors */
+  uint32_t n_requests;
+  uint32_t n_rules;
+  uint32_t n_limits;     /* entries of the limit table (<= 65536) */
+  const uint8_t* buf;    /* pinned host memory (rl_alloc_host): copied once, asynchronously */
+  uint64_t buf_bytes;
+  /* sections of buf, as byte offsets (each a multiple of 4, in any order) */
+  uint64_t req;          /* uint32[n_requests]: descriptors of the request (bits 0-15) | bytes of
+                            its shared prefix (bits 16-23, at most 255) << 16; bits 24-31 zero.
+                            A request's descriptors follow those of the request before it */
+  uint64_t now;          /* uint32[n_requests] UnixNow() (< 2^32 - 172800, as rl_batch.now) */
+  uint64_t hits;         /* uint32[n_requests] HitsAddend */
+  uint64_t desc;         /* uint32[n]: limit index (bits 0-15) | suffix bytes (bits 16-31) << 16 */
+  uint64_t prefix_bytes; /* the requests' shared prefixes, concatenated in request order */
+  uint64_t suffix_bytes; /* the descriptors' suffixes, concatenated in descriptor order */
+  uint64_t limits;       /* rl_limit[n_limits] */
+  uint64_t index;        /* uint32[4 x (tiles + 1)], tiles = ceil(n_requests / RL_PREFIXED_TILE):
+                            entry t = {first descriptor, first prefix byte, first suffix byte,
+                            first byte of the unpacked stems} of requests [t x TILE, (t+1) x TILE);
+                            entry 0 is zero, entry `tiles` the totals {n, prefix bytes, suffix
+                            bytes, stem bytes (<= max_stem_bytes)} */
+} rl_batch_prefixed;
+
+/* rl_do_limit_compact_async's contract for a prefix-shared batch: buf crosses
+ * PCIe in one copy (a multi-shard ctx: each shard copies the parts of its
+ * tile-aligned slice over its own device's link), is unpacked on the GPU and
+ * pipelined like any batch. *out is read after rl_synchronize; buf stays
+ * untouched until then. Not on a ctx that joined a communicator. */
+int rl_do_limit_prefixed_async(rl_ctx* ctx, const rl_batch_prefixed* in, rl_result* out);
 
 /* Epoch sweep (replaces Redis EXPIRE): tombstones every slot whose counter
  * and local-cache entries have all expired at `now`; `now` becomes a floor

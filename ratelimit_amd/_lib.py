@@ -19,7 +19,7 @@ EXPORTS = ["rl_abi_version", "rl_create", "rl_destroy", "rl_last_error", "rl_do_
            "rl_local_cache_info_get", "rl_snapshot_size", "rl_snapshot_save", "rl_snapshot_load",
            "rl_packer_create", "rl_packer_destroy", "rl_packer_pack", "rl_packer_rules", "rl_packer_rule_key",
            "rl_packer_last_error", "rl_comm_unique_id", "rl_comm_loopback_id", "rl_comm_init", "rl_do_limit_routed_async",
-           "rl_do_limit_host_async", "rl_do_limit_compact_async"]
+           "rl_do_limit_host_async", "rl_do_limit_compact_async", "rl_do_limit_prefixed_async", "rl_batch_progress"]
 
 _lib = None
 
@@ -54,7 +54,11 @@ def lib():
     L.rl_do_limit_host_async.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.POINTER(abi.RlResult)]
     if hasattr(L, "rl_do_limit_compact_async"):  # (A/B runs load libraries built before it existed)
         L.rl_do_limit_compact_async.argtypes = [C.c_void_p, C.POINTER(abi.RlBatchCompact), C.POINTER(abi.RlResult)]
+    if hasattr(L, "rl_do_limit_prefixed_async"):
+        L.rl_do_limit_prefixed_async.argtypes = [C.c_void_p, C.POINTER(abi.RlBatchPrefixed), C.POINTER(abi.RlResult)]
     L.rl_synchronize.argtypes = [C.c_void_p]
+    if hasattr(L, "rl_batch_progress"):
+        L.rl_batch_progress.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.rl_sweep.argtypes = [C.c_void_p, C.c_int64, C.POINTER(C.c_uint64)]
     L.rl_restore.argtypes = [C.c_void_p, C.POINTER(abi.RlRestoreBatch)]
     L.rl_table_info_get.argtypes = [C.c_void_p, C.POINTER(abi.RlTableInfo)]

@@ -53,6 +53,16 @@ class RlBatchCompact(C.Structure):
                 ("limits", C.c_uint64)]
 
 
+RL_PREFIXED_TILE = 256  # include/ratelimit_hip.h: requests per index tile
+
+
+class RlBatchPrefixed(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("n_requests", C.c_uint32), ("n_rules", C.c_uint32), ("n_limits", C.c_uint32),
+                ("buf", P), ("buf_bytes", C.c_uint64), ("req", C.c_uint64), ("now", C.c_uint64),
+                ("hits", C.c_uint64), ("desc", C.c_uint64), ("prefix_bytes", C.c_uint64),
+                ("suffix_bytes", C.c_uint64), ("limits", C.c_uint64), ("index", C.c_uint64)]
+
+
 class RlResult(C.Structure):
     _fields_ = [("code", P), ("limit_remaining", P), ("reset_s", P), ("stats", P), ("status", P)]
 

@@ -231,7 +231,7 @@ int synchronize_all(rl_ctx* c) {
 // device (memory of shard 0's GPU: shard 0 takes it whole). cb: a compact host
 // batch (in then carries only its sizes), cut at request boundaries.
 int shards_submit(rl_ctx* c, const rl_batch* in, rl_result* out, bool host, hipStream_t caller,
-                  const rl_batch_compact* cb = nullptr) {
+                  const rl_batch_compact* cb = nullptr, const rl_batch_prefixed* pb = nullptr) {
   const uint32_t N = c->n, n = in->n, nq = in->n_requests;
   const uint32_t slots = (uint32_t)c->pend.size(), s = c->batch_no % slots;
   // the batch that used this slot of the routers is complete: its stats first
@@ -255,7 +255,19 @@ int shards_submit(rl_ctx* c, const rl_batch* in, rl_result* out, bool host, hipS
   d[N] = n;
   q[N] = nq;
   const uint32_t* first = cb ? reinterpret_cast<const uint32_t*>(cb->buf + cb->req_first) : nullptr;
+  // a prefix-shared batch is cut at request tiles: the index holds each tile's first descriptor
+  const uint32_t tiles = pb ? (nq + RL_PREFIXED_TILE - 1) / RL_PREFIXED_TILE : 0;
+  const uint32_t* pix = pb ? reinterpret_cast<const uint32_t*>(pb->buf + pb->index) : nullptr;
+  uint32_t t[MAX_LOCAL_SHARDS + 1];
+  t[0] = 0;
+  t[N] = tiles;
   for (uint32_t j = 1; j < N; j++) {
+    if (pb) {  // (entries are checked against the sections on the device; clamp so slices stay ordered)
+      t[j] = (uint32_t)((uint64_t)tiles * j / N);
+      q[j] = std::min(t[j] * RL_PREFIXED_TILE, nq);
+      d[j] = std::min(std::max(pix[4ull * t[j]], d[j - 1]), n);
+      continue;
+    }
     if (cb) {  // (about nq / N requests each; req_first was checked to lie in [0, n] by nobody yet: clamp)
       q[j] = std::max(q[j - 1], (uint32_t)((uint64_t)nq * j / N));
       d[j] = std::min(std::max(first[q[j]], d[j - 1]), n);
@@ -274,7 +286,7 @@ int shards_submit(rl_ctx* c, const rl_batch* in, rl_result* out, bool host, hipS
     w.io = CommIO{};
     w.in = *in;
     w.out = rl_result{};
-    if (host && cb) {
+    if (host && (cb || pb)) {
       const uint32_t a = d[j], b = d[j + 1];
       w.in = rl_batch{};
       w.in.n = b - a;
@@ -286,6 +298,9 @@ int shards_submit(rl_ctx* c, const rl_batch* in, rl_result* out, bool host, hipS
       w.out.status = out->status ? out->status + a : nullptr;
       w.io.host = true;
       w.io.cb = cb;
+      w.io.pb = pb;
+      w.io.t0 = t[j];
+      w.io.t1 = t[j + 1];
       w.io.da = a;
       w.io.qa = q[j];
       w.io.stats_host = m ? c->stats_ring + ((size_t)s * N + j) * c->stats_cap : nullptr;
@@ -483,6 +498,27 @@ int rl_do_limit_compact_async(rl_ctx* c, const rl_batch_compact* in, rl_result* 
   sizes.n_requests = in->n_requests;
   sizes.n_rules = in->n_rules;
   return shards_submit(c, &sizes, out, true, nullptr, in);
+}
+
+int rl_batch_progress(rl_ctx* c, uint64_t* submitted, uint64_t* completed) {
+  if (!c) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (c->n > 1 || c->comm) return fail(c, RL_E_INVALID, "gpu: rl_batch_progress is for single-shard ctxs");
+  return eng_batch_progress(c->e[0], submitted, completed);
+}
+
+int rl_do_limit_prefixed_async(rl_ctx* c, const rl_batch_prefixed* in, rl_result* out) {
+  if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
+  if (c->comm) return eng_fail(c->e[0], RL_E_INVALID, "gpu: prefixed batches are not routed (rl_do_limit_routed_async)");
+  if (c->n == 1) return eng_do_limit_prefixed_async(c->e[0], in, out);
+  // a multi-shard ctx: one slice of request tiles per shard, each over its own
+  // device's link (rl_comm's stage_host_prefixed), then the shards' exchange
+  uint32_t tiles = 0;
+  if (const int rc = eng_prefixed_check(c->e[0], in, out, &tiles)) return from_engine(c, c->e[0], rc);
+  rl_batch sizes{};
+  sizes.n = in->n;
+  sizes.n_requests = in->n_requests;
+  sizes.n_rules = in->n_rules;
+  return shards_submit(c, &sizes, out, true, nullptr, nullptr, in);
 }
 
 int rl_do_limit(rl_ctx* c, const rl_batch* in, rl_result* out) {

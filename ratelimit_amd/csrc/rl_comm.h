@@ -40,6 +40,10 @@ struct CommIO {
   // a compact host batch (rl_batch_compact): this slice is its descriptors
   // [da, in->n + da) and requests [qa, in->n_requests), unpacked on the device
   const rl_batch_compact* cb = nullptr;
+  // a prefix-shared host batch (rl_batch_prefixed): this slice is its request
+  // tiles [t0, t1) (descriptors [da, in->n + da), requests [qa, in->n_requests))
+  const rl_batch_prefixed* pb = nullptr;
+  uint32_t t0 = 0, t1 = 0;
 };
 // One routed batch: this rank's slice (device arrays, or io) -> out in arrival
 // order. Enqueues the batch's first half and runs the previous batch's second

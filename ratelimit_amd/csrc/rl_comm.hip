@@ -325,6 +325,70 @@ int stage_host_compact(CommRouter* r, Engine* e, CommSlot& S, const rl_batch* in
   return RL_OK;
 }
 
+// A prefix-shared slice (request tiles [t0, t1)): its parts of the host
+// buffer into h_cbuf at the buffer's own offsets (index entries t0..t1, the
+// tiles' request words, clocks and hits, their descriptor words, prefix and
+// suffix bytes, the limit table), then k_unpack_prefixed over those tiles
+// writes the staging arrays and stems at their absolute offsets. Eight copies
+// of ~31.5 B per descriptor at C1; the index entries were written by the
+// batcher, so the cut reads nothing but them.
+int stage_host_prefixed(CommRouter* r, Engine* e, CommSlot& S, const rl_batch* in, rl_batch* d) {
+  const rl_batch_prefixed& pb = *S.io.pb;
+  const uint32_t n = in->n, da = S.io.da, db = da + n, qa = S.io.qa, qb = in->n_requests;
+  const rl_config& g = e->cfg;
+  if (const int rc = ensure_stage(r, e, S)) return rc;
+  if ((uint64_t)db > g.max_batch || qb > g.max_requests || qa > qb)
+    return eng_fail(e, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_stem_bytes");
+  if (S.io.t1 <= S.io.t0) {
+    *d = *in;
+    return RL_OK;
+  }
+  if (pb.buf_bytes > S.h_cbuf_cap) {  // (the slot's previous batch is drained first)
+    CHK_HIP(e, hipEventSynchronize(S.done));
+    if (S.h_cbuf) CHK_HIP(e, hipFree(S.h_cbuf));
+    S.h_cbuf = nullptr;
+    S.h_cbuf_cap = 0;
+    if (dalloc(&S.h_cbuf, pb.buf_bytes + 64) != hipSuccess)
+      return breaks(r, e, RL_E_HIP, "gpu: prefixed slice staging allocation failed");
+    S.h_cbuf_cap = pb.buf_bytes;
+  }
+  const uint32_t* ix = reinterpret_cast<const uint32_t*>(pb.buf + pb.index);
+  const uint32_t* I0 = ix + 4ull * S.io.t0;
+  const uint32_t* I1 = ix + 4ull * S.io.t1;
+  const uint32_t T = (pb.n_requests + RL_PREFIXED_TILE - 1) / RL_PREFIXED_TILE;
+  const uint32_t* tot = ix + 4ull * T;
+  // the cut's own entries bound the copies (the device checks every tile's)
+  if (I0[0] != da || I1[0] != db || I1[1] < I0[1] || I1[2] < I0[2] || I1[1] > tot[1] || I1[2] > tot[2])
+    return eng_fail(e, RL_E_INVALID, "gpu: prefixed batch index out of order");
+  hipStream_t st = r->cs;
+  auto part = [&](uint64_t sect, uint64_t from, uint64_t bytes) {
+    return bytes ? hipMemcpyAsync(S.h_cbuf + sect + from, pb.buf + sect + from, bytes, hipMemcpyHostToDevice, st)
+                 : hipSuccess;
+  };
+  CHK_HIP(e, part(pb.index, 16ull * S.io.t0, 16ull * (S.io.t1 - S.io.t0 + 1)));
+  CHK_HIP(e, part(pb.req, 4ull * qa, 4ull * (qb - qa)));
+  CHK_HIP(e, part(pb.now, 4ull * qa, 4ull * (qb - qa)));
+  CHK_HIP(e, part(pb.hits, 4ull * qa, 4ull * (qb - qa)));
+  CHK_HIP(e, part(pb.desc, 4ull * da, 4ull * n));
+  CHK_HIP(e, part(pb.prefix_bytes, I0[1], (uint64_t)I1[1] - I0[1]));
+  CHK_HIP(e, part(pb.suffix_bytes, I0[2], (uint64_t)I1[2] - I0[2]));
+  CHK_HIP(e, part(pb.limits, 0, 12ull * pb.n_limits));
+  launch_unpack_prefixed(pb, S.h_cbuf, S.io.t0, S.io.t1, S.h_stem, S.h_off, S.h_req, S.h_unit, S.h_flags, S.h_limit,
+                         S.h_hits, S.h_rule, S.h_now, e->errw + NBUF + 2, st);
+  CHK_HIP(e, hipGetLastError());
+  *d = *in;
+  d->stem_bytes = S.h_stem;
+  d->stem_off = S.h_off + da;
+  d->now = S.h_now;
+  d->req_idx = S.h_req + da;
+  d->unit = S.h_unit + da;
+  d->flags = S.h_flags + da;
+  d->limit = S.h_limit + da;
+  d->hits = S.h_hits + da;
+  d->rule_id = S.h_rule + da;
+  return RL_OK;
+}
+
 // First half of a batch (slot s): partition, counts exchange, counts to the
 // host. `hostrc` != RL_OK: the slice was rejected before the partition; it
 // sends zero counts. (The next call's second half waits on the host for this
@@ -341,7 +405,9 @@ int first_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, const rl_batch
   int rc = hostrc;
   rl_batch staged;
   if (!rc && S.io.host) {
-    rc = S.io.cb ? stage_host_compact(r, e, S, in, &staged) : stage_host(r, e, S, in, &staged);
+    rc = S.io.cb   ? stage_host_compact(r, e, S, in, &staged)
+         : S.io.pb ? stage_host_prefixed(r, e, S, in, &staged)
+                   : stage_host(r, e, S, in, &staged);
     if (r->broken) return rc;
     in = &staged;
   }

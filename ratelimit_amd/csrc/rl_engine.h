@@ -22,6 +22,7 @@ namespace rl {
 #endif
 constexpr uint32_t NBUF = RL_NBUF;
 constexpr uint32_t PROF_RING = 8;  // timed batches in flight (> NBUF)
+constexpr uint32_t PROGRESS_RING = 64;  // batches rl_batch_progress tracks in flight
 
 // Device staging of one host-fed batch in flight (eng_do_limit_host_async).
 struct HostSlot {
@@ -100,6 +101,10 @@ struct Engine {
   hipStream_t h2d = nullptr, d2h = nullptr;
   uint32_t hnext = 0;
   bool hs_ready = false;
+  // rl_batch_progress: batches submitted through the batch entry points and
+  // the ones whose outputs are complete, from a ring of completion events
+  uint64_t seq_sub = 0, seq_done = 0;
+  hipEvent_t done_ring[PROGRESS_RING] = {};
 };
 
 // Engine entry points (rl_engine.hip): the single-shard implementations of
@@ -113,7 +118,12 @@ int eng_do_limit_host_async(Engine* c, const rl_batch* in, rl_result* out);
 int eng_do_limit_compact_async(Engine* c, const rl_batch_compact* in, rl_result* out);
 // The compact batch's sizes and sections against the ctx's limits (no GPU work).
 int eng_compact_check(Engine* c, const rl_batch_compact* in, const rl_result* out);
+int eng_do_limit_prefixed_async(Engine* c, const rl_batch_prefixed* in, rl_result* out);
+// The prefix-shared batch's sizes, sections and index ends against the ctx's
+// limits (no GPU work); *tiles = its request tiles.
+int eng_prefixed_check(Engine* c, const rl_batch_prefixed* in, const rl_result* out, uint32_t* tiles);
 int eng_synchronize(Engine* c);
+int eng_batch_progress(Engine* c, uint64_t* submitted, uint64_t* completed);
 int eng_sweep(Engine* c, int64_t now, uint64_t* n_evicted);
 int eng_restore(Engine* c, const rl_restore_batch* in);
 int eng_table_info_get(Engine* c, rl_table_info* info);

@@ -148,6 +148,21 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
   return k;
 }
 
+// A batch submitted through a batch entry point is complete once the work now
+// on `st` is (its outputs written; host-fed: copied back). Keeps at most
+// PROGRESS_RING batches tracked: a caller that runs further ahead waits here
+// for the oldest one (never in a paced server).
+hipError_t track(Engine* c, hipStream_t st) {
+  if (c->seq_sub - c->seq_done >= PROGRESS_RING) {
+    const hipError_t e = hipEventSynchronize(c->done_ring[c->seq_done % PROGRESS_RING]);
+    if (e != hipSuccess) return e;
+    c->seq_done++;
+  }
+  const hipError_t e = hipEventRecord(c->done_ring[c->seq_sub % PROGRESS_RING], st);
+  c->seq_sub++;
+  return e;
+}
+
 int check_sizes(Engine* c, const rl_batch* in, uint64_t stem_bytes) {
   if (!in) return set_err(c, RL_E_INVALID, "gpu: null batch");
   if (in->n > c->cfg.max_batch || in->n_requests > c->cfg.max_requests || in->n_rules > c->cfg.max_rules ||
@@ -312,6 +327,8 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   c->stream = c->pipe[0];
   for (uint32_t k = 0; k < NBUF; k++)
     ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess;
+  for (uint32_t k = 0; k < PROGRESS_RING; k++)
+    ok = ok && hipEventCreateWithFlags(&c->done_ring[k], hipEventDisableTiming) == hipSuccess;
   ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess && dalloc(&c->hist, c->nslots) == hipSuccess;
   ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess && dalloc(&c->arena2, cfg.arena_bytes) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++) ok = ok && alloc_buffer(c->s[k], n);
@@ -397,6 +414,8 @@ void eng_destroy(Engine* c) {
     if (c->b_done[k]) (void)hipEventDestroy(c->b_done[k]);
     if (c->consumed[k]) (void)hipEventDestroy(c->consumed[k]);
   }
+  for (uint32_t k = 0; k < PROGRESS_RING; k++)
+    if (c->done_ring[k]) (void)hipEventDestroy(c->done_ring[k]);
   if (c->rs_ready) {
     c->rs.err = nullptr;  // (a word of errw)
     scratch_free(c->rs);
@@ -440,6 +459,7 @@ int eng_do_limit_async(Engine* c, const rl_batch* in, rl_result* out, void* stre
   hipStream_t st = (hipStream_t)stream;
   if (st && c->serial_debug) {
     enqueue(c, b, o, 0, st, false);
+    HIPCHK(c, track(c, st));
   } else {
     // (an idle caller stream needs no event: a cross-stream wait can stall
     // behind whatever shares the caller's hardware queue)
@@ -447,7 +467,8 @@ int eng_do_limit_async(Engine* c, const rl_batch* in, rl_result* out, void* stre
       HIPCHK(c, hipEventRecord(c->caller_ready, st));
       HIPCHK(c, hipStreamWaitEvent(c->pipe[c->next], c->caller_ready, 0));
     }
-    enqueue(c, b, o, 0, nullptr, true);
+    const uint32_t k = enqueue(c, b, o, 0, nullptr, true);
+    HIPCHK(c, track(c, c->pipe[k]));
   }
   HIPCHK(c, hipGetLastError());
   c->batches++;
@@ -612,7 +633,22 @@ int eng_synchronize(Engine* c) {
   if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   HIPCHK(c, hipDeviceSynchronize());
+  c->seq_done = c->seq_sub;
   return collect(c);
+}
+
+int eng_batch_progress(Engine* c, uint64_t* submitted, uint64_t* completed) {
+  if (!c || !submitted || !completed) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  while (c->seq_done < c->seq_sub) {
+    const hipError_t e = hipEventQuery(c->done_ring[c->seq_done % PROGRESS_RING]);
+    if (e == hipErrorNotReady) break;
+    if (e != hipSuccess) return set_err(c, RL_E_HIP, std::string("gpu: hipEventQuery: ") + hipGetErrorString(e));
+    c->seq_done++;
+  }
+  *submitted = c->seq_sub;
+  *completed = c->seq_done;
+  return RL_OK;
 }
 
 // Host buffers in and out, nothing waited for: the inputs cross PCIe on the
@@ -670,6 +706,7 @@ int host_slot_run(Engine* c, HostSlot& h, const rl_batch& d, uint64_t nb, rl_res
     HIPCHK(c, hipMemcpyAsync(out->stats, h.stats, (size_t)d.n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost,
                              down));
   HIPCHK(c, hipEventRecord(h.out_done, down));
+  HIPCHK(c, track(c, down));
   HIPCHK(c, hipGetLastError());
   c->batches++;
   c->decisions += n;
@@ -789,6 +826,83 @@ int eng_do_limit_compact_async(Engine* c, const rl_batch_compact* in, rl_result*
   return host_slot_run(c, h, d, nb, out);
 }
 
+// A prefix-shared batch (rl_batch_prefixed): the host checks only what the
+// copies and the unpack's bounds rely on — sections inside buf, the index's
+// first entry zero and its last the totals; every tile's own entry is checked
+// on the device against its sections before the tile is unpacked.
+int eng_prefixed_check(Engine* c, const rl_batch_prefixed* in, const rl_result* out, uint32_t* tiles) {
+  if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  const rl_config& g = c->cfg;
+  const uint32_t n = in->n, nq = in->n_requests;
+  if (n && (!in->buf || !out->code || !out->limit_remaining || !out->reset_s))
+    return set_err(c, RL_E_INVALID, "gpu: null argument");
+  if (n > g.max_batch || nq > g.max_requests || in->n_rules > g.max_rules || in->n_limits > 65536)
+    return set_err(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_rules (or > 65536 limits)");
+  if (n && !nq) return set_err(c, RL_E_INVALID, "gpu: descriptors without requests");
+  const uint32_t T = (nq + RL_PREFIXED_TILE - 1) / RL_PREFIXED_TILE;
+  *tiles = T;
+  const uint64_t B = in->buf_bytes;
+  auto sect = [&](uint64_t off, uint64_t bytes) { return off % 4 == 0 && off <= B && bytes <= B - off; };
+  if (!in->buf && B) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  if (!sect(in->index, 16ull * (T + 1)) || !sect(in->req, nq * 4ull) || !sect(in->now, nq * 4ull) ||
+      !sect(in->hits, nq * 4ull) || !sect(in->desc, n * 4ull) || !sect(in->limits, in->n_limits * 12ull))
+    return set_err(c, RL_E_INVALID, "gpu: prefixed batch section outside buf or not 4-byte aligned");
+  const uint32_t* ix = reinterpret_cast<const uint32_t*>(in->buf + in->index);
+  const uint32_t* tot = ix + 4ull * T;
+  if (ix[0] || ix[1] || ix[2] || ix[3] || tot[0] != n)
+    return set_err(c, RL_E_INVALID, "gpu: prefixed batch index does not start at zero or end at n");
+  if (tot[3] > g.max_stem_bytes) return set_err(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_stem_bytes");
+  if (!sect(in->prefix_bytes, tot[1]) || !sect(in->suffix_bytes, tot[2]))
+    return set_err(c, RL_E_INVALID, "gpu: prefixed batch prefix or suffix bytes outside buf");
+  return RL_OK;
+}
+
+int eng_do_limit_prefixed_async(Engine* c, const rl_batch_prefixed* in, rl_result* out) {
+  uint32_t T = 0;
+  int rc = eng_prefixed_check(c, in, out, &T);
+  if (rc) return rc;
+  const rl_config& g = c->cfg;
+  const uint32_t n = in->n, nq = in->n_requests;
+  const uint64_t B = in->buf_bytes;
+  const uint64_t nb = reinterpret_cast<const uint32_t*>(in->buf + in->index)[4ull * T + 3];
+  HIPCHK(c, hipSetDevice(g.device));
+  rc = ensure_host_slots(c);
+  if (rc) return rc;
+  const uint32_t j = c->hnext;
+  HostSlot& h = c->hs[j];
+  if (B > h.cbuf_cap) {  // grows to the largest buffer seen (the slot's previous batch drained first)
+    HIPCHK(c, hipEventSynchronize(h.out_done));
+    if (h.cbuf) HIPCHK(c, hipFree(h.cbuf));
+    h.cbuf = nullptr;
+    h.cbuf_cap = 0;
+    HIPCHK(c, dalloc(&h.cbuf, B + 64));
+    h.cbuf_cap = B;
+  }
+  c->hnext = (j + 1) % NBUF;
+  hipStream_t up = c->h2d;
+  HIPCHK(c, hipStreamWaitEvent(up, h.out_done, 0));  // the slot's previous batch is drained
+  if (B) HIPCHK(c, hipMemcpyAsync(h.cbuf, in->buf, B, hipMemcpyHostToDevice, up));
+  HIPCHK(c, hipEventRecord(h.in_done, up));
+  // unpacked on the batch's pipeline stream (as the compact batch)
+  HIPCHK(c, hipStreamWaitEvent(c->pipe[c->next], h.in_done, 0));
+  launch_unpack_prefixed(*in, h.cbuf, 0, T, h.stem, h.off, h.req, h.unit, h.flags, h.limit, h.hits, h.rule, h.now,
+                         c->s[c->next].err, c->pipe[c->next]);
+  rl_batch d{};
+  d.n = n;
+  d.n_requests = nq;
+  d.n_rules = in->n_rules;
+  d.stem_bytes = h.stem;
+  d.stem_off = h.off;
+  d.now = h.now;
+  d.req_idx = h.req;
+  d.unit = h.unit;
+  d.flags = h.flags;
+  d.limit = h.limit;
+  d.hits = h.hits;
+  d.rule_id = h.rule;
+  return host_slot_run(c, h, d, nb, out);
+}
+
 int eng_do_limit(Engine* c, const rl_batch* in, rl_result* out) {
   if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
   HIPCHK(c, hipSetDevice(c->cfg.device));
@@ -808,6 +922,7 @@ int eng_do_limit(Engine* c, const rl_batch* in, rl_result* out) {
   }
   if (in->n_rules)
     HIPCHK(c, hipMemcpyAsync(out->stats, c->d_stats, (size_t)in->n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, track(c, st));
   c->batches++;
   c->decisions += n;
   return collect(c);

@@ -220,6 +220,15 @@ void launch_unpack(const rl_batch_compact& cb, const uint8_t* buf, uint32_t* req
 void launch_unpack_range(const rl_batch_compact& cb, const uint8_t* buf, uint32_t d0, uint32_t d1, uint32_t q0,
                          uint32_t q1, uint32_t* req, uint8_t* unit, uint8_t* flags, uint32_t* limit, uint32_t* hits,
                          uint32_t* rule, int64_t* now, uint32_t* err, hipStream_t st);
+// A prefix-shared host batch (rl_batch_prefixed; buf = the device copy of its
+// buffer, or of a slice's parts at the host buffer's offsets): tiles [t0, t1)
+// -> the rl_batch arrays at their absolute indices, stems rebuilt into `stem`
+// at the index's stem offsets, off[] the stem offsets (off[n] included). The
+// totals come from the host buffer's last index entry (already checked). A
+// tile whose entry does not match its sections sets ERR_INVALID in *err.
+void launch_unpack_prefixed(const rl_batch_prefixed& pb, const uint8_t* buf, uint32_t t0, uint32_t t1, uint8_t* stem,
+                            uint32_t* off, uint32_t* req, uint8_t* unit, uint8_t* flags, uint32_t* limit,
+                            uint32_t* hits, uint32_t* rule, int64_t* now, uint32_t* err, hipStream_t st);
 // counts: cstride u64 per owner (records, stem bytes[, meta0, meta1]).
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
                        uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st,

@@ -249,6 +249,164 @@ void launch_unpack_range(const rl_batch_compact& cb, const uint8_t* buf, uint32_
       flags, limit, hits, rule, now, err);
 }
 
+// ---- k_unpack_prefixed: a prefix-shared host batch (rl_batch_prefixed) ->
+// the rl_batch arrays, stems rebuilt as prefix[q] ‖ suffix[d]. One workgroup
+// per tile of PFX_TILE requests, one lane per request; the tile's index entry
+// gives its starting descriptor, prefix, suffix and stem offsets, so tiles are
+// independent (a multi-shard slice is a tile range). The tile's own sums are
+// checked against the next entry before anything is written, and every read
+// and write stays below the index's totals (host-checked against the sections
+// and the staging capacity): a malformed index fails the batch (ERR_INVALID)
+// and never writes outside it. The tile's stems are assembled in LDS and
+// leave as whole dwords when they fit (C1: ~17 KB per tile).
+constexpr uint32_t PFX_TILE = RL_PREFIXED_TILE;
+constexpr uint32_t PFX_LDS = 24576;  // stem bytes assembled in LDS per tile
+
+__device__ inline uint32_t block_excl_scan_u32(uint32_t v, uint32_t* tmp, uint32_t* total) {
+  // 256 lanes: wave-level inclusive scans by shuffles, then across the 4 waves
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) tmp[wv] = x;
+  __syncthreads();
+  uint32_t base = 0;
+  for (uint32_t k = 0; k < wv; k++) base += tmp[k];
+  *total = tmp[0] + tmp[1] + tmp[2] + tmp[3];
+  __syncthreads();
+  return base + x - v;
+}
+
+__global__ __launch_bounds__(256) void k_unpack_prefixed(
+    uint32_t t0, uint32_t nq, uint32_t n_limits, uint4 tot, const uint32_t* __restrict__ reqw,
+    const uint32_t* __restrict__ now32, const uint32_t* __restrict__ hits_q, const uint32_t* __restrict__ descw,
+    const uint8_t* __restrict__ pfx, const uint8_t* __restrict__ sfx, const rl_limit* __restrict__ lim,
+    const uint4* __restrict__ index, uint8_t* __restrict__ stem, uint32_t* __restrict__ off,
+    uint32_t* __restrict__ req, uint8_t* __restrict__ unit, uint8_t* __restrict__ flags,
+    uint32_t* __restrict__ limit, uint32_t* __restrict__ hits, uint32_t* __restrict__ rule,
+    int64_t* __restrict__ now, uint32_t* err) {
+  __shared__ uint32_t s_tmp[4][4];
+  __shared__ uint32_t s_first[PFX_TILE + 1], s_pl[PFX_TILE], s_pin[PFX_TILE];
+  __shared__ uint32_t s_out[PFX_LDS / 4 + 2];
+  const uint32_t tid = threadIdx.x, t = t0 + blockIdx.x;
+  const uint32_t q0 = t * PFX_TILE, q = q0 + tid;
+  const uint4 I0 = index[t], I1 = index[t + 1];
+  const uint32_t rw = q < nq ? reqw[q] : 0u;
+  const uint32_t nd = rw & 0xFFFFu, pl = (rw >> 16) & 0xFFu;
+  uint32_t T_nd, T_pl;
+  const uint32_t e_nd = block_excl_scan_u32(nd, s_tmp[0], &T_nd);
+  const uint32_t e_pl = block_excl_scan_u32(pl, s_tmp[1], &T_pl);
+  // the tile's entry against its own sums and the totals (uniform per block)
+  const bool ok = I0.x <= I1.x && I0.y <= I1.y && I0.z <= I1.z && I0.w <= I1.w && I1.x <= tot.x && I1.y <= tot.y &&
+                  I1.z <= tot.z && I1.w <= tot.w && I1.x - I0.x == T_nd && I1.y - I0.y == T_pl;
+  s_first[tid] = I0.x + e_nd;
+  s_pl[tid] = pl;
+  s_pin[tid] = I0.y + e_pl;
+  if (tid == 0) s_first[PFX_TILE] = I1.x;
+  const int reserved_bits = __syncthreads_or((rw >> 24) != 0u);
+  if (!ok || reserved_bits) {
+    if (tid == 0) atomicOr(err, ERR_INVALID);
+    return;
+  }
+  if (q < nq) {
+    now[q] = now32[q];
+    const uint32_t h = hits_q[q];
+    for (uint32_t d = I0.x + e_nd, z = d + nd; d < z; d++) {
+      req[d] = q;
+      hits[d] = h;
+    }
+  }
+  // descriptors of the tile, 256 at a time: stem offsets by a block scan
+  const uint32_t D = T_nd;
+  const uint32_t span = I1.w - I0.w;
+  const bool in_lds = span <= PFX_LDS;
+  uint32_t carry_s = 0, carry_o = 0, bad = 0;
+  for (uint32_t c = 0; c < D; c += 256) {
+    const uint32_t j = c + tid, d = I0.x + j;
+    uint32_t w = 0, r = 0;
+    if (j < D) {
+      w = descw[d];
+      // request of descriptor d: the last tile request whose first descriptor <= d
+      uint32_t lo = 0, hi = PFX_TILE;  // s_first[lo] <= d < s_first[hi]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_first[mid] <= d) lo = mid;
+        else hi = mid;
+      }
+      r = lo;
+    }
+    const uint32_t sl = w >> 16, p = j < D ? s_pl[r] : 0u;
+    uint32_t T_s, T_o;
+    const uint32_t e_s = block_excl_scan_u32(sl, s_tmp[2], &T_s);
+    const uint32_t e_o = block_excl_scan_u32(p + sl, s_tmp[3], &T_o);
+    if (j < D) {
+      const uint32_t si = I0.z + carry_s + e_s;   // suffix bytes in
+      const uint32_t lo = carry_o + e_o;          // stem bytes out (tile-relative)
+      const uint32_t pi = s_pin[r];
+      if (si + sl > I1.z || pi + p > I1.y || lo + p + sl > span) {
+        bad = 1;
+      } else {
+        off[d] = I0.w + lo;
+        if (in_lds) {
+          uint8_t* o8 = reinterpret_cast<uint8_t*>(s_out) + (I0.w & 3u) + lo;
+          for (uint32_t k = 0; k < p; k++) o8[k] = pfx[pi + k];
+          for (uint32_t k = 0; k < sl; k++) o8[p + k] = sfx[si + k];
+        } else {
+          uint8_t* o8 = stem + I0.w + lo;
+          for (uint32_t k = 0; k < p; k++) o8[k] = pfx[pi + k];
+          for (uint32_t k = 0; k < sl; k++) o8[p + k] = sfx[si + k];
+        }
+      }
+      const uint32_t k = w & 0xFFFFu;
+      const rl_limit L = k < n_limits ? lim[k] : rl_limit{0, 0, 0, 0, 0};  // unit 0: RL_E_INVALID
+      unit[d] = L.unit;
+      flags[d] = L.flags;
+      limit[d] = L.requests_per_unit;
+      rule[d] = L.rule_id;
+    }
+    carry_s += T_s;
+    carry_o += T_o;
+  }
+  if (tid == 0) {
+    if (carry_s != I1.z - I0.z || carry_o != span) bad = 1;
+    off[I1.x] = I1.w;  // (the next tile writes the same value as its first offset)
+  }
+  if (bad) atomicOr(err, ERR_INVALID);
+  if (in_lds) {  // the tile's stems [I0.w, I1.w) as whole dwords, bytes at the ragged ends
+    __syncthreads();
+    const uint32_t a = I0.w, z = I1.w, sh = a & 3u;
+    const uint8_t* s8 = reinterpret_cast<const uint8_t*>(s_out);
+    const uint32_t a4 = (a + 3u) & ~3u, z4 = z & ~3u;
+    if (a4 < z4) {
+      // global byte g sits at byte g - a + sh of s_out: global dword w4 is s_out[w4 - a / 4]
+      uint32_t* o32 = reinterpret_cast<uint32_t*>(stem);
+      for (uint32_t w4 = a4 / 4 + tid; w4 < z4 / 4; w4 += 256) o32[w4] = s_out[w4 - a / 4];
+      if (tid < a4 - a) stem[a + tid] = s8[sh + tid];
+      if (tid < z - z4) stem[z4 + tid] = s8[z4 - a + sh + tid];
+    } else if (tid < z - a) {
+      stem[a + tid] = s8[sh + tid];
+    }
+  }
+}
+
+void launch_unpack_prefixed(const rl_batch_prefixed& pb, const uint8_t* buf, uint32_t t0, uint32_t t1, uint8_t* stem,
+                            uint32_t* off, uint32_t* req, uint8_t* unit, uint8_t* flags, uint32_t* limit,
+                            uint32_t* hits, uint32_t* rule, int64_t* now, uint32_t* err, hipStream_t st) {
+  if (t1 <= t0) return;
+  const uint32_t tiles = (pb.n_requests + PFX_TILE - 1) / PFX_TILE;
+  const uint32_t* host_tot = reinterpret_cast<const uint32_t*>(pb.buf + pb.index) + 4ull * tiles;
+  const uint4 tot = make_uint4(host_tot[0], host_tot[1], host_tot[2], host_tot[3]);
+  k_unpack_prefixed<<<t1 - t0, 256, 0, st>>>(
+      t0, pb.n_requests, pb.n_limits, tot, reinterpret_cast<const uint32_t*>(buf + pb.req),
+      reinterpret_cast<const uint32_t*>(buf + pb.now), reinterpret_cast<const uint32_t*>(buf + pb.hits),
+      reinterpret_cast<const uint32_t*>(buf + pb.desc), buf + pb.prefix_bytes, buf + pb.suffix_bytes,
+      reinterpret_cast<const rl_limit*>(buf + pb.limits), reinterpret_cast<const uint4*>(buf + pb.index), stem, off,
+      req, unit, flags, limit, hits, rule, now, err);
+}
+
 // The zero-padded first KEY_HEAD bytes of the stem at byte `off` of the packed
 // stems, as 4 x uint4: five aligned 16-B loads, then dword selects and funnel
 // shifts. Only chunks holding a byte of the head are loaded, so no load leaves

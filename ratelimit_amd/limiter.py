@@ -180,6 +180,21 @@ class Backend:
         check(self.ctx, lib().rl_do_limit_compact_async(self.ctx, C.byref(s), C.byref(r)))
         return s, r
 
+    def batch_progress(self):
+        """rl_batch_progress: (batches submitted, batches complete), never waits."""
+        a, b = C.c_uint64(), C.c_uint64()
+        check(self.ctx, lib().rl_batch_progress(self.ctx, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def do_limit_prefixed_async(self, pb, out: dict):
+        """rl_do_limit_prefixed_async: a PrefixedBatch (packing.prefixed_batch;
+        its buffer pinned for an asynchronous copy) in, out as
+        do_limit_host_async; final after synchronize()."""
+        r = abi.make_result_struct(out)
+        s = pb.struct()
+        check(self.ctx, lib().rl_do_limit_prefixed_async(self.ctx, C.byref(s), C.byref(r)))
+        return s, r
+
     # ---- config match + DoLimit on raw requests (rl_match.hip)
     def load_config(self, tree) -> None:
         """rl_config_load: ``tree`` is a ratelimit_amd.config.ConfigTree."""

@@ -188,3 +188,173 @@ def compact_batch(arrays: Dict[str, np.ndarray], n: int, n_requests: int, n_rule
     for k, a in sections:
         buf[offsets[k]:offsets[k] + a.nbytes] = np.frombuffer(a.tobytes(), np.uint8)
     return CompactBatch(buf[:max(pos, 4)], n, n_requests, n_rules, int(table.size), offsets)
+
+
+@dataclass
+class PrefixedBatch:
+    """An rl_batch_prefixed: one contiguous buffer (``buf``, uint8) and the byte
+    offsets of its sections (include/ratelimit_hip.h)."""
+    buf: np.ndarray
+    n: int
+    n_requests: int
+    n_rules: int
+    n_limits: int
+    offsets: Dict[str, int]
+
+    def struct(self):
+        s = abi.RlBatchPrefixed()
+        s.n, s.n_requests, s.n_rules, s.n_limits = self.n, self.n_requests, self.n_rules, self.n_limits
+        s.buf = abi.ptr(self.buf)
+        s.buf_bytes = int(self.buf.size)
+        for k, v in self.offsets.items():
+            setattr(s, k, int(v))
+        return s
+
+    def alloc_result(self, isolate: bool = False):
+        return PackedBatch({}, self.n, self.n_requests, self.n_rules).alloc_result(isolate)
+
+    def section(self, name: str, dtype, count: int) -> np.ndarray:
+        o = self.offsets[name]
+        return np.frombuffer(self.buf[o:o + count * np.dtype(dtype).itemsize].tobytes(), dtype)
+
+    def tiles(self) -> int:
+        return (self.n_requests + abi.RL_PREFIXED_TILE - 1) // abi.RL_PREFIXED_TILE
+
+
+def _request_lcp(stems2d: np.ndarray, lens: np.ndarray, first: np.ndarray, req: np.ndarray, n_requests: int,
+                 cap: int) -> np.ndarray:
+    """Per request: the longest prefix every one of its descriptors' stems
+    starts with (at most ``cap`` bytes; 0 for a request without descriptors)."""
+    n = lens.size
+    plen = np.zeros(n_requests, np.int64)
+    if n == 0:
+        return plen
+    head = first[req]                                  # first descriptor of each descriptor's request
+    L = stems2d.shape[1]
+    diff = stems2d != stems2d[head]
+    col = np.arange(L)[None, :]
+    diff |= col >= np.minimum(lens, lens[head])[:, None]
+    lcp = np.where(diff.any(axis=1), diff.argmax(axis=1), L)
+    has = first[1:] > first[:-1]
+    starts = first[:-1][has]
+    plen[has] = np.minimum.reduceat(lcp, starts)
+    return np.minimum(plen, cap)
+
+
+def prefixed_batch(arrays: Dict[str, np.ndarray], n: int, n_requests: int, n_rules: int, alloc=None,
+                   max_prefix: int = 255) -> PrefixedBatch:
+    """The prefix-shared (PCIe) layout of a packed batch: per request the bytes
+    all its descriptors' stems start with (at most ``max_prefix``), stored once,
+    with the request's clock and HitsAddend; per descriptor its remaining
+    suffix and an index into the table of the batch's distinct (limit, rule,
+    unit, flags); the tile index of starting offsets. ``hits`` must be one value
+    per request (HitsAddend is a request field). alloc(nbytes) -> a uint8 array
+    for the buffer (default numpy; PinnedArena.array for pinned)."""
+    if not 0 <= max_prefix <= 255:
+        raise ValueError("max_prefix must be 0..255")
+    req = np.asarray(arrays["req_idx"][:n], np.int64)
+    first = np.searchsorted(req, np.arange(n_requests + 1), side="left").astype(np.int64)
+    hits_d = np.asarray(arrays["hits"][:n], np.uint32)
+    if n and np.any(hits_d != hits_d[first[req]]):
+        raise ValueError("hits differ inside a request (HitsAddend is per request)")
+    nd = np.diff(first)
+    if nd.size and nd.max() > 0xFFFF:
+        raise ValueError("more than 65535 descriptors in one request")
+    hits_q = np.zeros(n_requests, np.uint32)
+    has = nd > 0
+    hits_q[has] = hits_d[first[:-1][has]]
+    key = np.zeros(n, abi.LIMIT_DTYPE)
+    key["requests_per_unit"] = arrays["limit"][:n]
+    key["rule_id"] = arrays["rule_id"][:n]
+    key["unit"] = arrays["unit"][:n]
+    key["flags"] = arrays["flags"][:n]
+    table, idx = np.unique(key, return_inverse=True)
+    if table.size > 65536:
+        raise ValueError("more than 65536 distinct limits in one batch")
+    off = np.asarray(arrays["stem_off"][:n + 1], np.int64)
+    lens = np.diff(off) if n else np.zeros(0, np.int64)
+    blob = np.asarray(arrays["stem_bytes"], np.uint8)
+    Lmax = int(lens.max()) if n else 0
+    # stems as zero-padded rows (one row per descriptor)
+    stems2d = np.zeros((n, max(Lmax, 1)), np.uint8)
+    if n:
+        cols = np.arange(max(Lmax, 1))[None, :]
+        m = cols < lens[:, None]
+        stems2d[m] = blob[(off[:-1, None] + cols)[m]]
+    plen = _request_lcp(stems2d, lens, first, req, n_requests, max_prefix)
+    pl_d = plen[req] if n else np.zeros(0, np.int64)
+    slen = lens - pl_d
+    if n and slen.max() > 0xFFFF:
+        raise ValueError("a suffix longer than 65535 bytes")
+    cols = np.arange(max(Lmax, 1))[None, :]
+    prefix_bytes = stems2d[first[:-1][has]][cols < plen[has][:, None]] if n else np.zeros(0, np.uint8)
+    suffix_bytes = stems2d[(cols >= pl_d[:, None]) & (cols < lens[:, None])] if n else np.zeros(0, np.uint8)
+    reqw = (nd.astype(np.uint32) | (plen.astype(np.uint32) << 16)).astype(np.uint32)
+    descw = (idx.astype(np.uint32) | (slen.astype(np.uint32) << 16)).astype(np.uint32)
+    # tile index: {first descriptor, prefix byte, suffix byte, stem byte} per tile of requests
+    T = (n_requests + abi.RL_PREFIXED_TILE - 1) // abi.RL_PREFIXED_TILE
+    cut = np.minimum(np.arange(T + 1, dtype=np.int64) * abi.RL_PREFIXED_TILE, n_requests)
+    cum_p = np.concatenate([[0], np.cumsum(plen)])
+    cum_s = np.concatenate([[0], np.cumsum(slen)])
+    index = np.stack([first[cut], cum_p[cut], cum_s[first[cut]], off[first[cut]] - off[0] if n else first[cut] * 0],
+                     axis=1).astype(np.uint32).reshape(-1)
+    now = np.asarray(arrays["now"][:n_requests], np.int64).astype(np.uint32)
+    sections = [("index", index), ("req", reqw), ("now", now), ("hits", hits_q), ("limits", table),
+                ("desc", descw), ("prefix_bytes", prefix_bytes.astype(np.uint8)),
+                ("suffix_bytes", suffix_bytes.astype(np.uint8))]
+    offsets, pos = {}, 0
+    for k, a in sections:
+        offsets[k] = pos
+        pos += (a.nbytes + 3) & ~3
+    buf = np.zeros(max(pos, 4), np.uint8) if alloc is None else alloc(max(pos, 4))
+    for k, a in sections:
+        buf[offsets[k]:offsets[k] + a.nbytes] = np.frombuffer(a.tobytes(), np.uint8)
+    return PrefixedBatch(buf[:max(pos, 4)], n, n_requests, n_rules, int(table.size), offsets)
+
+
+def unprefix(pb: PrefixedBatch) -> Dict[str, np.ndarray]:
+    """The rl_batch arrays a prefix-shared batch stands for (the format's
+    definition, restated on the host for the CPU tests; k_unpack_prefixed does
+    this on the GPU). Raises ValueError on an index that does not match."""
+    n, nq = pb.n, pb.n_requests
+    T = pb.tiles()
+    index = pb.section("index", np.uint32, 4 * (T + 1)).reshape(T + 1, 4).astype(np.int64)
+    reqw = pb.section("req", np.uint32, nq)
+    descw = pb.section("desc", np.uint32, n)
+    nd = (reqw & 0xFFFF).astype(np.int64)
+    plen = ((reqw >> 16) & 0xFF).astype(np.int64)
+    if np.any(reqw >> 24):
+        raise ValueError("reserved request bits set")
+    tot = index[T]
+    if nd.sum() != n or tot[0] != n or index[0].any():
+        raise ValueError("index does not match the descriptors")
+    pre = pb.section("prefix_bytes", np.uint8, int(tot[1])).tobytes()
+    suf = pb.section("suffix_bytes", np.uint8, int(tot[2])).tobytes()
+    table = pb.section("limits", abi.LIMIT_DTYPE, pb.n_limits)
+    stems, req_idx = [], []
+    p = s = d = 0
+    for q in range(nq):
+        if q % abi.RL_PREFIXED_TILE == 0:
+            t = q // abi.RL_PREFIXED_TILE
+            if tuple(index[t][:3]) != (d, p, s) or index[t][3] != sum(len(x) for x in stems):
+                raise ValueError("index entry %d does not match" % t)
+        P = pre[p:p + plen[q]]
+        p += plen[q]
+        for _ in range(nd[q]):
+            sl = int(descw[d] >> 16)
+            stems.append(P + suf[s:s + sl])
+            s += sl
+            req_idx.append(q)
+            d += 1
+    if (p, s) != (tot[1], tot[2]) or tot[3] != sum(len(x) for x in stems):
+        raise ValueError("index totals do not match")
+    k = (descw & 0xFFFF).astype(np.int64)
+    ok = k < pb.n_limits
+    kk = np.where(ok, k, 0)
+    lim = table[kk] if pb.n_limits else np.zeros(n, abi.LIMIT_DTYPE)
+    hits_q = pb.section("hits", np.uint32, nq)
+    out = arrays_from_lists(stems, pb.section("now", np.uint32, nq).astype(np.int64), req_idx,
+                            np.where(ok, lim["unit"], 0), np.where(ok, lim["flags"], 0),
+                            np.where(ok, lim["requests_per_unit"], 0), hits_q[np.asarray(req_idx, np.int64)],
+                            np.where(ok, lim["rule_id"], 0))
+    return out

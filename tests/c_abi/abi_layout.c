@@ -5,7 +5,7 @@
  * C, and prints one line per struct ("S name size") and per field
  * ("F struct field offset size") for tests/test_c_abi.py to compare with the
  * ctypes mirror in ratelimit_amd/abi.py, which the Python adapter (and the cgo
- * sketch in INTEGRATION.md) relies on. */
+ * adapter in go/src/gpu) relies on. */
 #include <stddef.h>
 #include <stdio.h>
 
@@ -35,6 +35,13 @@ int main(void) {
   F(rl_batch_compact, n_limits); F(rl_batch_compact, buf); F(rl_batch_compact, buf_bytes);
   F(rl_batch_compact, stem_bytes); F(rl_batch_compact, stem_off); F(rl_batch_compact, limit_idx);
   F(rl_batch_compact, req_first); F(rl_batch_compact, now); F(rl_batch_compact, hits); F(rl_batch_compact, limits);
+
+  S(rl_batch_prefixed);
+  F(rl_batch_prefixed, n); F(rl_batch_prefixed, n_requests); F(rl_batch_prefixed, n_rules);
+  F(rl_batch_prefixed, n_limits); F(rl_batch_prefixed, buf); F(rl_batch_prefixed, buf_bytes);
+  F(rl_batch_prefixed, req); F(rl_batch_prefixed, now); F(rl_batch_prefixed, hits); F(rl_batch_prefixed, desc);
+  F(rl_batch_prefixed, prefix_bytes); F(rl_batch_prefixed, suffix_bytes); F(rl_batch_prefixed, limits);
+  F(rl_batch_prefixed, index);
 
   S(rl_result);
   F(rl_result, code); F(rl_result, limit_remaining); F(rl_result, reset_s); F(rl_result, stats);

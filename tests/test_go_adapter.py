@@ -1,0 +1,213 @@
+"""The Go adapter (go/src/gpu, go/src/config, go/patches) against the C ABI.
+
+There is no Go toolchain here, so the Go side is checked from
+its text, against what a compiler would check at the cgo boundary:
+
+* every cgo preamble compiles as C against include/ratelimit_hip.h;
+* every C.<name> the Go files use exists in the header: functions with the
+  arity of each call, RL_* constants, rl_* types, and every C struct field
+  the Go code reads or writes (offsetof, compiled);
+* the runner patch calls the constructor with createLimiter's own arguments
+  (src/service_cmd/runner/runner.go:50) and every settings field the adapter
+  reads is one the settings patch adds or the reference already has;
+* INTEGRATION.md holds no Go code of its own (it points at these files).
+"""
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GO = os.path.join(ROOT, "go")
+HEADER = os.path.join(ROOT, "include", "ratelimit_hip.h")
+CGO_BUILTINS = {"GoString", "GoStringN", "GoBytes", "CString", "CBytes"}
+C_SCALARS = {"uint8_t", "uint16_t", "uint32_t", "uint64_t", "int8_t", "int16_t", "int32_t", "int64_t", "float",
+             "double", "char", "int", "uint", "size_t", "uchar", "schar", "short", "ushort", "long", "ulong"}
+LIBC = {"malloc", "calloc", "free", "memset", "memcpy"}
+
+
+def go_files(sub="src"):
+    out = []
+    for d, _, fs in os.walk(os.path.join(GO, sub)):
+        out += [os.path.join(d, f) for f in sorted(fs) if f.endswith(".go")]
+    return out
+
+
+def strip_go(src):
+    """Go source without comments and string literals (cgo preambles removed too)."""
+    src = re.sub(r"/\*.*?\*/", " ", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    src = re.sub(r'"(?:\\.|[^"\\])*"', '""', src)
+    src = re.sub(r"`[^`]*`", '""', src)
+    return src
+
+
+def header_api():
+    h = open(HEADER).read()
+    hs = re.sub(r"/\*.*?\*/", " ", h, flags=re.S)
+    funcs = {}
+    for m in re.finditer(r"\b(rl_\w+)\s*\(([^;{]*?)\)\s*;", hs, flags=re.S):
+        args = m.group(2).strip()
+        funcs[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    consts = set(re.findall(r"#define\s+(RL_\w+)", hs)) | set(re.findall(r"\b(RL_\w+)\s*=", hs))
+    types = set(re.findall(r"}\s*(rl_\w+)\s*;", hs)) | set(re.findall(r"typedef\s+struct\s+\w+\s+(rl_\w+)\s*;", hs))
+    return funcs, consts, types
+
+
+def call_args(src, start):
+    """Number of top-level arguments of the call whose '(' is at src[start]."""
+    depth, n, empty = 0, 1, True
+    for i in range(start, len(src)):
+        ch = src[i]
+        if ch in "([{":
+            depth += 1
+        elif ch in ")]}":
+            depth -= 1
+            if depth == 0:
+                return 0 if empty else n
+        elif ch == "," and depth == 1:
+            n += 1
+        elif depth >= 1 and not ch.isspace():
+            empty = False
+    raise AssertionError("unbalanced call")
+
+
+def gcc_syntax(code, tag):
+    with tempfile.NamedTemporaryFile("w", suffix=".c", delete=False, prefix=tag) as f:
+        f.write(code)
+        path = f.name
+    try:
+        r = subprocess.run(["gcc", "-std=c11", "-fsyntax-only", "-Wall", "-Werror", "-I", os.path.dirname(HEADER),
+                            path], capture_output=True, text=True)
+        assert r.returncode == 0, "%s:\n%s\n%s" % (tag, r.stderr, code)
+    finally:
+        os.unlink(path)
+
+
+def test_go_adapter_files_exist():
+    names = {os.path.relpath(p, GO) for p in go_files()}
+    for f in ("src/gpu/gpu.go", "src/gpu/cache_impl.go", "src/gpu/stats.go", "src/gpu/config.go",
+              "src/gpu/comm.go", "src/config/walk.go"):
+        assert f in names, f
+    for p in ("settings.go.patch", "runner.go.patch", "Dockerfile.patch"):
+        assert os.path.exists(os.path.join(GO, "patches", p)), p
+
+
+@pytest.mark.parametrize("path", [p for p in go_files() if 'import "C"' in open(p).read()],
+                         ids=lambda p: os.path.relpath(p, GO))
+def test_cgo_preamble_compiles_against_header(path):
+    src = open(path).read()
+    m = re.search(r"/\*(.*?)\*/\s*import \"C\"", src, flags=re.S)
+    assert m, "no cgo preamble before import \"C\""
+    pre = "\n".join(l for l in m.group(1).splitlines() if not l.strip().startswith("#cgo"))
+    assert '#include "ratelimit_hip.h"' in pre
+    gcc_syntax(pre + "\nint main(void) { return (int)rl_abi_version() * 0; }\n", "preamble_")
+
+
+def test_go_c_references_exist_in_header():
+    funcs, consts, types = header_api()
+    fields = set()  # (C type, field)
+    checked_calls = 0
+    for path in go_files():
+        raw = open(path).read()
+        if 'import "C"' not in raw:
+            continue
+        src = strip_go(raw)
+        # variables / fields / params of C struct types, and slices of them
+        typed = {}
+        for m in re.finditer(r"\bvar\s+(\w+)\s+C\.(rl_\w+)", src):
+            typed[m.group(1)] = m.group(2)
+        for m in re.finditer(r"^\s*(\w+)\s+\*?C\.(rl_\w+)\s*$", src, flags=re.M):
+            typed[m.group(1)] = m.group(2)
+        for m in re.finditer(r"[(,]\s*(\w+)\s+\*C\.(rl_\w+)", src):
+            typed[m.group(1)] = m.group(2)
+        elem = {}
+        for m in re.finditer(r"\b(\w+)\s+\[\]C\.(rl_\w+)", src):
+            elem[m.group(1)] = m.group(2)
+        for m in re.finditer(r"\b(\w+)\s*:=\s*\(\*\[[^\]]+\]C\.(rl_\w+)\)", src):
+            elem[m.group(1)] = m.group(2)
+        for m in re.finditer(r"\b(\w+)\s*:=\s*&(?:\w+\.)*(\w+)\[", src):
+            if m.group(2) in elem:
+                typed[m.group(1)] = elem[m.group(2)]
+        for m in re.finditer(r"C\.(rl_\w+)\{(\w+)\s*:", src):
+            fields.add((m.group(1), m.group(2)))
+        for name, t in typed.items():
+            for m in re.finditer(r"(?<![\w])%s\.([a-z_][a-z0-9_]*)\b" % re.escape(name), src):
+                fields.add((t, m.group(1)))
+        for m in re.finditer(r"\bC\.(\w+)", src):
+            name = m.group(1)
+            after = src[m.end():m.end() + 1]
+            if name in CGO_BUILTINS or name in C_SCALARS or name in LIBC:
+                continue
+            if name.startswith("RL_"):
+                assert name in consts, "%s: C.%s is not in the header" % (os.path.basename(path), name)
+            elif name in types:
+                continue
+            elif name in funcs:
+                assert after == "(", name
+                n = call_args(src, m.end())
+                assert n == funcs[name], "%s: C.%s called with %d arguments, header has %d" % (
+                    os.path.basename(path), name, n, funcs[name])
+                checked_calls += 1
+            else:
+                raise AssertionError("%s: C.%s is not declared by the header" % (os.path.basename(path), name))
+    assert checked_calls >= 15, checked_calls
+    assert len(fields) >= 40, sorted(fields)
+    code = ['#include <stddef.h>', '#include "ratelimit_hip.h"', "int main(void) {", "  size_t s = 0;"]
+    code += ["  s += offsetof(%s, %s);" % tf for tf in sorted(fields)]
+    code += ["  return (int)s * 0;", "}"]
+    gcc_syntax("\n".join(code) + "\n", "fields_")
+
+
+def _added(patch):
+    return "\n".join(l[1:] for l in open(os.path.join(GO, "patches", patch)).read().splitlines()
+                     if l.startswith("+") and not l.startswith("+++"))
+
+
+def test_runner_and_settings_patches_match_the_adapter():
+    impl = strip_go(open(os.path.join(GO, "src", "gpu", "cache_impl.go")).read())
+    m = re.search(r"func NewRateLimitCacheImplFromSettings\(([^)]*)\)\s*limiter\.RateLimitCache", impl)
+    assert m, "constructor missing"
+    params = [p.strip().split()[-1] for p in m.group(1).split(",")]
+    assert params == ["settings.Settings", "*freecache.Cache", "server.Server", "utils.TimeSource", "stats.Manager"]
+    # createLimiter(srv server.Server, s settings.Settings, localCache *freecache.Cache, statsManager stats.Manager)
+    # (runner.go:50): the case passes its own parameters, in the constructor's order
+    run = _added("runner.go.patch")
+    c = re.search(r'case "gpu":\s*return gpu\.NewRateLimitCacheImplFromSettings\((.*?)\)\s*$', run, flags=re.S | re.M)
+    assert c, run
+    args = [a.strip() for a in c.group(1).split(",") if a.strip()]
+    assert args == ["s", "localCache", "srv", "utils.NewTimeSourceImpl()", "statsManager"], args
+    assert '"github.com/envoyproxy/ratelimit/src/gpu"' in run
+    # every s.X the adapter reads: added by the settings patch, or a reference setting
+    added = set(re.findall(r"^\s*(\w+)\s+\S+\s+`envconfig", _added("settings.go.patch"), flags=re.M))
+    reference = {"NearLimitRatio", "RedisPerSecond", "ExpirationJitterMaxSeconds", "CacheKeyPrefix",
+                 "LocalCacheSizeInBytes"}
+    body = impl[m.start():impl.index("\nfunc ", m.end())]
+    used = set(re.findall(r"\bs\.(\w+)", body))
+    assert used and used <= added | reference, used - added - reference
+    assert {u for u in used if u.startswith("Gpu")} <= added
+    assert "CGO_ENABLED=1" in _added("Dockerfile.patch")
+
+
+def test_patches_apply_to_the_reference():
+    ref = "/root/reference"
+    if not os.path.isdir(os.path.join(ref, "src")):
+        pytest.skip("reference tree not present (GPU box)")
+    with tempfile.TemporaryDirectory() as d:
+        for rel in ("src/settings/settings.go", "src/service_cmd/runner/runner.go", "Dockerfile"):
+            os.makedirs(os.path.join(d, os.path.dirname(rel)), exist_ok=True)
+            with open(os.path.join(ref, rel)) as f, open(os.path.join(d, rel), "w") as g:
+                g.write(f.read())
+        for p in ("settings.go.patch", "runner.go.patch", "Dockerfile.patch"):
+            r = subprocess.run(["patch", "-p1", "--dry-run", "-d", d, "-i", os.path.join(GO, "patches", p)],
+                               capture_output=True, text=True)
+            assert r.returncode == 0, (p, r.stdout, r.stderr)
+
+
+def test_integration_md_points_at_the_go_files():
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert "```go" not in text, "Go code belongs in go/src, not in INTEGRATION.md"
+    for f in ("go/src/gpu/gpu.go", "go/src/gpu/cache_impl.go", "go/patches/runner.go.patch"):
+        assert f in text, f
