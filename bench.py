@@ -59,6 +59,8 @@ def parse():
                     help="time every k-th batch's stages with HIP events (k_table's live time for the roofline)")
     ap.add_argument("--no-fill", action="store_true")
     ap.add_argument("--pcie-steps", type=int, default=60, help="host-fed (PCIe) batches timed after the device phase")
+    ap.add_argument("--pcie-formats", default="prefixed,compact,soa",
+                    help="host-fed formats timed (the first is the reported pcie_fed rate)")
     ap.add_argument("--slots-per-key", type=float, default=4.0, help="table slots per live key (power of 2 above)")
     ap.add_argument("--hash-seed", type=int, default=0, help="stem hash key (0: drawn at random per run; reported)")
     ap.add_argument("--route", action="store_true", help="use the routed (all_to_all) path even at N=1")
@@ -519,9 +521,11 @@ def pcie_fed(args, be, host_batches, now):
         soa.append(PackedBatch(arr, bn, bq, args.n_rules))
         comp.append(compact_batch(arr, bn, bq, args.n_rules, alloc=lambda nb: arena.array(nb, np.uint8)))
         pref.append(prefixed_batch(arr, bn, bq, args.n_rules, alloc=lambda nb: arena.array(nb, np.uint8)))
-    outs = [{k: arena.like(v) for k, v in soa[0].alloc_result().items()} for _ in range(4)]
+    # outputs as the Go adapter takes them: code and LimitRemaining (5 B per
+    # decision); DurationUntilReset is computed host-side (utils.CalculateReset)
+    outs = [{k: arena.like(v) for k, v in soa[0].alloc_result(reset=False).items()} for _ in range(4)]
     n = soa[0].n
-    bytes_out = n * 9
+    bytes_out = n * 5
 
     def phase(fed, call, bytes_in):
         keep = []
@@ -553,9 +557,10 @@ def pcie_fed(args, be, host_batches, now):
 
     soa_in = sum(int(v.nbytes) for k, v in soa[0].arrays.items() if k != "stem_bytes") + \
         int(soa[0].arrays["stem_off"][n])
-    r_soa = phase(soa, be.do_limit_host_async, soa_in)
-    r_comp = phase(comp, be.do_limit_compact_async, int(comp[0].buf.size)) if comp else None
-    r_pref = phase(pref, be.do_limit_prefixed_async, int(pref[0].buf.size)) if pref else None
+    fmts = args.pcie_formats.split(",")
+    r_soa = phase(soa, be.do_limit_host_async, soa_in) if "soa" in fmts else None
+    r_comp = phase(comp, be.do_limit_compact_async, int(comp[0].buf.size)) if "compact" in fmts else None
+    r_pref = phase(pref, be.do_limit_prefixed_async, int(pref[0].buf.size)) if "prefixed" in fmts else None
     # the link's own rate for one large page-locked copy, the bound to read h2d_GBps against
     import torch
     big = arena.array(256 << 20, np.uint8)
@@ -574,16 +579,21 @@ def pcie_fed(args, be, host_batches, now):
         if r:
             r["h2d_peak_GBps"] = peak
             r["frac_of_h2d_peak"] = r["h2d_GBps"] / peak
-    r_soa["format"] = "rl_batch arrays (rl_do_limit_host_async: 9 copies per batch)"
-    r_comp["format"] = "rl_batch_compact (rl_do_limit_compact_async: one buffer, one copy per batch)"
-    r_pref["format"] = ("rl_batch_prefixed (rl_do_limit_prefixed_async: one buffer, one copy per batch; each "
-                        "request's shared stem prefix once)")
-    r_pref["buffers"] = "page-locked (rl_alloc_host); now constant over the phase"
-    r_pref["host_numa"] = host_numa()
+    named = {"soa": r_soa, "compact": r_comp, "prefixed": r_pref}
+    if r_soa:
+        r_soa["format"] = "rl_batch arrays (rl_do_limit_host_async: 9 copies per batch)"
+    if r_comp:
+        r_comp["format"] = "rl_batch_compact (rl_do_limit_compact_async: one buffer, one copy per batch)"
+    if r_pref:
+        r_pref["format"] = ("rl_batch_prefixed (rl_do_limit_prefixed_async: one buffer, one copy per batch; each "
+                            "request's shared stem prefix once)")
+    head = named[fmts[0]]
+    head["buffers"] = "page-locked (rl_alloc_host); now constant over the phase"
+    head["host_numa"] = host_numa()
     keys = ("value", "h2d_bytes_per_decision", "h2d_GBps", "frac_of_h2d_peak", "p99_batch_ms", "format")
-    r_pref["compact"] = {k: r_comp[k] for k in keys}
-    r_pref["soa"] = {k: r_soa[k] for k in keys}
-    return r_pref
+    for f in fmts[1:]:
+        head[f] = {k: named[f][k] for k in keys}
+    return head
 
 
 def host_numa():

@@ -364,11 +364,12 @@ func (this *rateLimitCacheImpl) finish(f *flight) {
 				failed = fmt.Sprintf("gpu: descriptor failed (rl_status %d)", b.Status[j])
 				continue
 			}
+			div := utils.UnitToDivider(c.limits[i].Limit.Unit)
 			st[i] = &pb.RateLimitResponse_DescriptorStatus{ // base_limiter.go:181-197
 				Code:               pb.RateLimitResponse_Code(b.Code[j]),
 				CurrentLimit:       c.limits[i].Limit,
 				LimitRemaining:     b.Remaining[j],
-				DurationUntilReset: &duration.Duration{Seconds: int64(b.Reset[j])},
+				DurationUntilReset: &duration.Duration{Seconds: div - c.now%div}, // utils.CalculateReset
 			}
 		}
 		if failed != "" {

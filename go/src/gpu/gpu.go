@@ -203,10 +203,12 @@ type PrefixedBatch struct {
 	prefix []byte
 	suffix []byte
 
-	// outputs (pinned), per descriptor in packed order, and per-rule stats deltas
+	// outputs (pinned), per descriptor in packed order, and per-rule stats
+	// deltas. DurationUntilReset is not copied back (rl_result.reset_s NULL, 4 B
+	// per decision less over PCIe): the adapter computes it from the request's
+	// clock as utils.CalculateReset does (utilities.go:32-36).
 	Code      []uint8
 	Remaining []uint32
-	Reset     []uint32
 	Status    []uint8
 	Stats     []uint64
 
@@ -220,12 +222,11 @@ func NewPrefixedBatch(maxDesc, maxRules int) *PrefixedBatch {
 	b := &PrefixedBatch{limitIdx: make(map[Limit]uint16)}
 	b.Code = bytesAt(pinned(maxDesc), maxDesc)
 	b.Remaining = u32At(pinned(4*maxDesc), maxDesc)
-	b.Reset = u32At(pinned(4*maxDesc), maxDesc)
 	b.Status = bytesAt(pinned(maxDesc), maxDesc)
 	b.Stats = u64At(pinned(8*maxRules*int(C.RL_NUM_STATS)), maxRules*int(C.RL_NUM_STATS))
 	b.Out.code = (*C.uint8_t)(unsafe.Pointer(&b.Code[0]))
 	b.Out.limit_remaining = (*C.uint32_t)(unsafe.Pointer(&b.Remaining[0]))
-	b.Out.reset_s = (*C.uint32_t)(unsafe.Pointer(&b.Reset[0]))
+	b.Out.reset_s = nil
 	b.Out.status = (*C.uint8_t)(unsafe.Pointer(&b.Status[0]))
 	b.Out.stats = (*C.uint64_t)(unsafe.Pointer(&b.Stats[0]))
 	return b

@@ -126,7 +126,11 @@ typedef struct rl_batch {
 typedef struct rl_result {
   uint8_t* code;              /* [n] rl_code */
   uint32_t* limit_remaining;  /* [n] LimitRemaining */
-  uint32_t* reset_s;          /* [n] DurationUntilReset.Seconds (1..86400) */
+  uint32_t* reset_s;          /* [n] DurationUntilReset.Seconds (1..86400). May be NULL on the
+                                 host-buffer entry points (rl_do_limit, rl_do_limit_host_async,
+                                 _compact_async, _prefixed_async): not copied back, 4 B per decision less over PCIe;
+                                 the caller computes it as utils.CalculateReset does
+                                 (utilities.go:32-36: div - now % div, now the request's clock) */
   uint64_t* stats;            /* [n_rules * RL_NUM_STATS] */
   uint8_t* status;            /* [n] or NULL. Non-NULL: per-descriptor failure isolation. A
                                  descriptor that cannot be answered (bad unit / rule id / stem length:
@@ -179,9 +183,15 @@ const char* rl_last_error(const rl_ctx* ctx);
  * Multi-GPU (rl_config.n_shards > 1): the table is hash-sharded over
  * shard_device[0..n_shards) inside this one ctx (the reference's single service
  * process scaled out over a Redis cluster, src/redis/driver_impl.go:108-126).
- * Every batch is partitioned by owner on shard 0's device, each owner's chunk
- * goes to its GPU over xGMI (peer copies), owners run their pipelines, and the
- * results come back in arrival order, stats summed. Same call, same answers. */
+ * Each shard has a worker thread and a router; the shards' routers form an
+ * in-process world (the loopback transport: device copies, over xGMI between
+ * distinct devices). A host batch is cut into one request-aligned slice per
+ * shard; each shard copies its slice over its own device's link, partitions
+ * it by owner, exchanges records with the other shards, runs the pipeline on
+ * the keys it owns, and returns the answers to the slice's source, which
+ * writes them to *out in arrival order; the stats of the slices are summed.
+ * Same call, same answers. Owners keep stats per source slice, so every shard
+ * is created with n_shards x max_rules rows (a batch may carry max_rules). */
 int rl_do_limit(rl_ctx* ctx, const rl_batch* in, rl_result* out);
 
 /* Same, with every pointer in *in / *out in device memory of ctx's GPU
@@ -190,9 +200,11 @@ int rl_do_limit(rl_ctx* ctx, const rl_batch* in, rl_result* out);
  * (the inputs' producer); with NULL the inputs must be complete at the call.
  * *out is read after rl_synchronize (the caller's stream is never made to wait
  * for a batch, which would chain the next batch's inputs behind it and
- * serialise the pipeline). Returns once the work is enqueued (a
- * multi-shard ctx first waits for this batch's owner partition, never for the
- * owners' pipelines); errors detected on the GPU surface at rl_synchronize.
+ * serialise the pipeline). Returns once the work is enqueued; errors detected
+ * on the GPU surface at rl_synchronize. On a multi-shard ctx shard 0 takes the
+ * whole device batch as its slice (the other shards' slices are empty) and
+ * routes it to the owners as above; the caller's thread waits only until every
+ * shard's worker has enqueued its part, never for the GPU.
  * stem_bytes must be 4-byte aligned (any hipMalloc / torch allocation is). */
 int rl_do_limit_async(rl_ctx* ctx, const rl_batch* in, rl_result* out, void* stream);
 
@@ -201,7 +213,12 @@ int rl_do_limit_async(rl_ctx* ctx, const rl_batch* in, rl_result* out, void* str
  * batches compute, its outputs cross back when it is done; *out is read after
  * rl_synchronize, and the host buffers of a batch stay untouched until then.
  * Pinned buffers (rl_alloc_host) make the copies asynchronous. The fed path of
- * a batcher whose requests arrive in host memory (single-shard ctx). */
+ * a batcher whose requests arrive in host memory. On a multi-shard ctx each
+ * shard's worker copies its request-aligned slice over its own link and routes
+ * it (rl_do_limit); out->stats is written at rl_synchronize (or once the
+ * ring of batches in flight comes round to this batch again).
+ * On a multi-shard ctx rl_synchronize, rl_sweep, rl_restore, the info getters
+ * and the snapshot calls first complete every shard's pending batches. */
 int rl_do_limit_host_async(rl_ctx* ctx, const rl_batch* in, rl_result* out);
 int rl_synchronize(rl_ctx* ctx);
 
@@ -416,9 +433,11 @@ int rl_route_scatter(rl_ctx* ctx, uint32_t n, const uint32_t* perm, const uint64
  * leaves the ctx's router unusable (RL_E_COMM / RL_E_HIP from every later
  * call). Replaces the Redis cluster client's key-slot routing inside one
  * service process (src/redis/driver_impl.go:108-126).
- * On a routed ctx rl_synchronize, rl_sweep, rl_restore, rl_table_info_get,
- * rl_local_cache_info_get and rl_snapshot_save / _load first complete the
- * pending batch, so they are collective like the batches. */
+ * On a routed ctx rl_synchronize, rl_sweep, rl_restore and rl_snapshot_save /
+ * _load first complete the pending batch, so they are collective like the
+ * batches. The read-only getters rl_table_info_get and rl_local_cache_info_get
+ * are not: they see every batch but the pending one, and a rank may call them
+ * alone (e.g. for its gauges). */
 #define RL_COMM_ID_BYTES 128u
 int rl_comm_unique_id(uint8_t* id);
 int rl_comm_loopback_id(uint8_t* id);

@@ -201,12 +201,14 @@ int finalize_stats(rl_ctx* c, uint32_t s, bool keep) {
   return RL_OK;
 }
 
-int synchronize_all(rl_ctx* c) {
+// keep_stats false (rl_destroy): the shards complete, but no caller memory is
+// written (the caller may have freed a pending batch's outputs).
+int synchronize_all(rl_ctx* c, bool keep_stats = true) {
   if (c->n > 1) {
     const int rc = run_shards(c, ShardWorker::SYNC);
     const std::string msg = c->last_error;
     for (uint32_t s = 0; s < c->pend.size(); s++) {
-      const int fr = finalize_stats(c, s, rc == RL_OK);
+      const int fr = finalize_stats(c, s, keep_stats && rc == RL_OK);
       if (fr && !rc) return fr;
     }
     if (rc) c->last_error = msg;
@@ -248,6 +250,8 @@ int shards_submit(rl_ctx* c, const rl_batch* in, rl_result* out, bool host, hipS
     API_HIP(c, hipHostMalloc((void**)&c->stats_ring, (size_t)slots * N * m * 8));
     c->stats_cap = m;
   }
+  if (host && c->stats_ring && c->stats_cap)  // (a slice that fails never writes its part: no stale deltas)
+    memset(c->stats_ring + (size_t)s * N * c->stats_cap, 0, (size_t)N * c->stats_cap * 8);
   // request-aligned cuts of about n / N descriptors
   uint32_t d[MAX_LOCAL_SHARDS + 1], q[MAX_LOCAL_SHARDS + 1];
   d[0] = 0;
@@ -291,10 +295,10 @@ int shards_submit(rl_ctx* c, const rl_batch* in, rl_result* out, bool host, hipS
       w.in = rl_batch{};
       w.in.n = b - a;
       w.in.n_requests = q[j + 1];  // (absolute: the slice's first request is q[j])
-      w.in.n_rules = cb->n_rules;
+      w.in.n_rules = in->n_rules;
       w.out.code = out->code + a;
       w.out.limit_remaining = out->limit_remaining + a;
-      w.out.reset_s = out->reset_s + a;
+      w.out.reset_s = out->reset_s ? out->reset_s + a : nullptr;
       w.out.status = out->status ? out->status + a : nullptr;
       w.io.host = true;
       w.io.cb = cb;
@@ -341,9 +345,16 @@ int shards_submit(rl_ctx* c, const rl_batch* in, rl_result* out, bool host, hipS
   return RL_OK;
 }
 
-// Settle a multi-shard or routed ctx before a call that reads or changes the
-// table (on a routed ctx this makes the call collective, like rl_synchronize).
+// Settle a multi-shard or routed ctx before a call that changes the table
+// (on a routed ctx this makes the call collective, like rl_synchronize).
 int settle(rl_ctx* c) { return (c->comm || c->n > 1) ? synchronize_all(c) : RL_OK; }
+// Before a read-only getter: the shards of one ctx complete their batches
+// (in-process, no peer to wait for); a routed ctx is not settled, since its
+// pending batch's second half is a collective exchange and one rank polling
+// its gauges would block on its peers. The engine getters order after every
+// batch already enqueued on the engine, so a routed ctx's getters see all
+// batches but the last one submitted.
+int settle_local(rl_ctx* c) { return c->n > 1 ? synchronize_all(c) : RL_OK; }
 
 constexpr uint64_t MSNAP_MAGIC = 0x31304853414e534cull;  // "LSNASH01": one image per shard
 
@@ -394,6 +405,9 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
     rl_config ec = cfg;
     ec.n_shards = 1;
     ec.device = cfg.shard_device[j];
+    // the shards' router keeps stats per source slice (rule' = source x n_rules + rule):
+    // an owner needs n x max_rules rows for batches of max_rules rules
+    ec.max_rules = cfg.max_rules * n;
     c->e[j] = eng_create(&ec, err, errlen);
     if (!c->e[j]) {
       const std::string m = g_api_err = (err && errlen) ? std::string(err) : std::string("gpu: shard creation failed");
@@ -403,6 +417,7 @@ rl_ctx* rl_create(const rl_config* cfg_in, char* err, size_t errlen) {
   }
   c->cfg = c->e[0]->cfg;
   c->cfg.n_shards = n;
+  c->cfg.max_rules = cfg.max_rules;  // (what a batch may carry; the shards hold n x as many rows)
   for (uint32_t j = 0; j < MAX_LOCAL_SHARDS; j++) c->cfg.shard_device[j] = cfg.shard_device[j];
   // every pair of distinct shard devices talks directly over xGMI
   for (uint32_t i = 0; i < n; i++)
@@ -443,7 +458,7 @@ void rl_destroy(rl_ctx* c) {
   if (c->n > 1) {
     bool live = true;
     for (uint32_t j = 0; j < c->n; j++) live = live && c->w[j].th.joinable();
-    if (live) (void)synchronize_all(c);  // (the last batches complete on every shard together)
+    if (live) (void)synchronize_all(c, false);  // (the last batches complete on every shard together)
     stop_shards(c);
     for (uint32_t j = 0; j < c->n; j++)
       if (c->r[j]) comm_destroy(c->r[j]);
@@ -465,7 +480,7 @@ int rl_do_limit_async(rl_ctx* c, const rl_batch* in, rl_result* out, void* strea
 // whole batch (a batch is taken by every shard or by none).
 int check_host_batch(rl_ctx* c, const rl_batch* in, const rl_result* out) {
   const uint32_t n = in->n, nq = in->n_requests;
-  if (n && (!in->stem_off || !in->req_idx || !out->code || !out->limit_remaining || !out->reset_s))
+  if (n && (!in->stem_off || !in->req_idx || !out->code || !out->limit_remaining))
     return fail(c, RL_E_INVALID, "gpu: null argument");
   const uint64_t nb = n ? in->stem_off[n] : 0;
   if (n > c->cfg.max_batch || nq > c->cfg.max_requests || in->n_rules > c->cfg.max_rules ||
@@ -625,7 +640,7 @@ int rl_restore(rl_ctx* c, const rl_restore_batch* r) {
 
 int rl_table_info_get(rl_ctx* c, rl_table_info* info) {
   if (!c || !info) return fail(c, RL_E_INVALID, "gpu: null argument");
-  if (const int src = settle(c)) return src;
+  if (const int src = settle_local(c)) return src;
   rl_table_info sum{};
   for (uint32_t j = 0; j < c->n; j++) {
     rl_table_info x{};
@@ -645,7 +660,7 @@ int rl_table_info_get(rl_ctx* c, rl_table_info* info) {
 
 int rl_local_cache_info_get(rl_ctx* c, int64_t now, rl_local_cache_info* info) {
   if (!c || !info) return fail(c, RL_E_INVALID, "gpu: null argument");
-  if (const int src = settle(c)) return src;
+  if (const int src = settle_local(c)) return src;
   rl_local_cache_info sum{};
   for (uint32_t j = 0; j < c->n; j++) {
     rl_local_cache_info x{};

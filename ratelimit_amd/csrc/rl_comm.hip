@@ -603,7 +603,7 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
     if (S.io.host && n) {  // the answers cross back to the caller's host slice
       CHK_HIP(e, hipMemcpyAsync(out.code, S.h_code, n, hipMemcpyDeviceToHost, r->ret));
       CHK_HIP(e, hipMemcpyAsync(out.limit_remaining, S.h_rem, n * 4ull, hipMemcpyDeviceToHost, r->ret));
-      CHK_HIP(e, hipMemcpyAsync(out.reset_s, S.h_reset, n * 4ull, hipMemcpyDeviceToHost, r->ret));
+      if (out.reset_s) CHK_HIP(e, hipMemcpyAsync(out.reset_s, S.h_reset, n * 4ull, hipMemcpyDeviceToHost, r->ret));
       if (out.status) CHK_HIP(e, hipMemcpyAsync(out.status, S.h_status, n, hipMemcpyDeviceToHost, r->ret));
     }
   } else if (!r->sticky) {
@@ -742,7 +742,7 @@ int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, 
   // checks the partition does not make: a failure here still takes part in
   // the exchange (zero counts) and fails this rank's batch at rl_synchronize
   int hostrc = RL_OK;
-  if (n && (!out->code || !out->limit_remaining || !out->reset_s)) {
+  if (n && (!out->code || !out->limit_remaining || (!out->reset_s && !S.io.host))) {  // (host slices: reset optional)
     hostrc = eng_fail(e, RL_E_INVALID, "gpu: null result array");
   } else if ((uint64_t)r->world * nr > e->cfg.max_rules) {
     hostrc = eng_fail(e, RL_E_CAPACITY, "gpu: routed batches need max_rules >= world x n_rules (per-source stats)");

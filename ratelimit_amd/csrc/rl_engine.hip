@@ -699,7 +699,7 @@ int host_slot_run(Engine* c, HostSlot& h, const rl_batch& d, uint64_t nb, rl_res
   if (n) {
     HIPCHK(c, hipMemcpyAsync(out->code, h.code, n, hipMemcpyDeviceToHost, down));
     HIPCHK(c, hipMemcpyAsync(out->limit_remaining, h.rem, n * 4ull, hipMemcpyDeviceToHost, down));
-    HIPCHK(c, hipMemcpyAsync(out->reset_s, h.reset, n * 4ull, hipMemcpyDeviceToHost, down));
+    if (out->reset_s) HIPCHK(c, hipMemcpyAsync(out->reset_s, h.reset, n * 4ull, hipMemcpyDeviceToHost, down));
     if (out->status) HIPCHK(c, hipMemcpyAsync(out->status, h.status, n, hipMemcpyDeviceToHost, down));
   }
   if (d.n_rules && out->stats)
@@ -716,7 +716,7 @@ int host_slot_run(Engine* c, HostSlot& h, const rl_batch& d, uint64_t nb, rl_res
 int eng_do_limit_host_async(Engine* c, const rl_batch* in, rl_result* out) {
   if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
   const uint32_t n = in->n, nq = in->n_requests;
-  if (n && (!in->stem_off || !out->code || !out->limit_remaining || !out->reset_s))
+  if (n && (!in->stem_off || !out->code || !out->limit_remaining))
     return set_err(c, RL_E_INVALID, "gpu: null argument");
   const uint64_t nb = n ? in->stem_off[n] : 0;
   int rc = check_sizes(c, in, nb);
@@ -762,7 +762,7 @@ int eng_compact_check(Engine* c, const rl_batch_compact* in, const rl_result* ou
   if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
   const rl_config& g = c->cfg;
   const uint32_t n = in->n, nq = in->n_requests;
-  if (n && (!in->buf || !out->code || !out->limit_remaining || !out->reset_s))
+  if (n && (!in->buf || !out->code || !out->limit_remaining))
     return set_err(c, RL_E_INVALID, "gpu: null argument");
   if (n > g.max_batch || nq > g.max_requests || in->n_rules > g.max_rules || in->n_limits > 65536)
     return set_err(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_rules (or > 65536 limits)");
@@ -834,7 +834,7 @@ int eng_prefixed_check(Engine* c, const rl_batch_prefixed* in, const rl_result* 
   if (!c || !in || !out) return set_err(c, RL_E_INVALID, "gpu: null argument");
   const rl_config& g = c->cfg;
   const uint32_t n = in->n, nq = in->n_requests;
-  if (n && (!in->buf || !out->code || !out->limit_remaining || !out->reset_s))
+  if (n && (!in->buf || !out->code || !out->limit_remaining))
     return set_err(c, RL_E_INVALID, "gpu: null argument");
   if (n > g.max_batch || nq > g.max_requests || in->n_rules > g.max_rules || in->n_limits > 65536)
     return set_err(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_rules (or > 65536 limits)");
@@ -918,7 +918,7 @@ int eng_do_limit(Engine* c, const rl_batch* in, rl_result* out) {
     if (out->status) HIPCHK(c, hipMemcpyAsync(out->status, c->d_status, n, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(out->code, c->d_code, n, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(out->limit_remaining, c->d_rem, n * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(out->reset_s, c->d_reset, n * 4, hipMemcpyDeviceToHost, st));
+    if (out->reset_s) HIPCHK(c, hipMemcpyAsync(out->reset_s, c->d_reset, n * 4, hipMemcpyDeviceToHost, st));
   }
   if (in->n_rules)
     HIPCHK(c, hipMemcpyAsync(out->stats, c->d_stats, (size_t)in->n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost, st));

@@ -52,11 +52,14 @@ class PackedBatch:
     def batch_struct(self):
         return abi.make_batch_struct(self.arrays, self.n, self.n_requests, self.n_rules)
 
-    def alloc_result(self, isolate: bool = False):
+    def alloc_result(self, isolate: bool = False, reset: bool = True):
+        """reset False: no reset_s array (host-buffer entry points then leave
+        DurationUntilReset to the caller, as utils.CalculateReset computes it)."""
         out = {"code": np.zeros(max(self.n, 1), np.uint8),
                "limit_remaining": np.zeros(max(self.n, 1), np.uint32),
-               "reset_s": np.zeros(max(self.n, 1), np.uint32),
                "stats": np.zeros(max(self.n_rules, 1) * abi.RL_NUM_STATS, np.uint64)}
+        if reset:
+            out["reset_s"] = np.zeros(max(self.n, 1), np.uint32)
         if isolate:
             out["status"] = np.zeros(max(self.n, 1), np.uint8)
         return out
@@ -148,8 +151,8 @@ class CompactBatch:
             setattr(s, k, int(v))
         return s
 
-    def alloc_result(self, isolate: bool = False):
-        return PackedBatch({}, self.n, self.n_requests, self.n_rules).alloc_result(isolate)
+    def alloc_result(self, isolate: bool = False, reset: bool = True):
+        return PackedBatch({}, self.n, self.n_requests, self.n_rules).alloc_result(isolate, reset)
 
 
 def compact_batch(arrays: Dict[str, np.ndarray], n: int, n_requests: int, n_rules: int, alloc=None) -> CompactBatch:
@@ -210,8 +213,8 @@ class PrefixedBatch:
             setattr(s, k, int(v))
         return s
 
-    def alloc_result(self, isolate: bool = False):
-        return PackedBatch({}, self.n, self.n_requests, self.n_rules).alloc_result(isolate)
+    def alloc_result(self, isolate: bool = False, reset: bool = True):
+        return PackedBatch({}, self.n, self.n_requests, self.n_rules).alloc_result(isolate, reset)
 
     def section(self, name: str, dtype, count: int) -> np.ndarray:
         o = self.offsets[name]

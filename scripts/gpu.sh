@@ -75,7 +75,7 @@ task_pmc() {
       ./build_tools/pmcprobe > gpurun_out/pmc_probe_$ctr.log 2>&1 || { tail -20 gpurun_out/pmc_probe_$ctr.log; return 1; }
     rm -rf gpurun_out/pmc_${cfg}_$ctr && mkdir -p gpurun_out/pmc_${cfg}_$ctr
     timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc_${cfg}_$ctr -o run -- \
-      python -u bench.py --config $cfg --steps 10 --warmup 2 --latency-steps 2 --no-cpu-baseline --pcie-steps 0 \
+      python -u bench.py --config $cfg --steps 10 --warmup 2 --latency-steps 2 --loaded-steps 0 --no-cpu-baseline --pcie-steps 0 \
       > gpurun_out/pmc_${cfg}_$ctr.log 2>&1 || { tail -20 gpurun_out/pmc_${cfg}_$ctr.log; return 1; }
   done
   python scripts/pmc_summary.py $cfg
@@ -113,13 +113,13 @@ task_ab() {
         for cfg in ${CFGS:-c1 c2}; do
           tag=$(basename "${lib:-cur}" .so)_${cfg}_$rep
           RL_LIB_PATH=${lib:+$PWD/$lib} timeout -k 10 200 python -u bench.py --config $cfg --no-cpu-baseline --steps 200 \
-            --latency-steps 5 --pcie-steps 0 > gpurun_out/ab_$tag.log 2>&1 || { tail -5 gpurun_out/ab_$tag.log; return 1; }
+            --latency-steps 5 --loaded-steps 0 --pcie-steps 0 > gpurun_out/ab_$tag.log 2>&1 || { tail -5 gpurun_out/ab_$tag.log; return 1; }
           summary gpurun_out/ab_$tag.log $tag
         done
       fi
       if [ "$mode" = "pcie" ]; then
         tag=$(basename "${lib:-cur}" .so)_pcie_$rep
-        RL_LIB_PATH=${lib:+$PWD/$lib} timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 50 --latency-steps 5 \
+        RL_LIB_PATH=${lib:+$PWD/$lib} timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 50 --latency-steps 5 --loaded-steps 0 \
           > gpurun_out/ab_$tag.log 2>&1 || { tail -5 gpurun_out/ab_$tag.log; return 1; }
         summary gpurun_out/ab_$tag.log $tag \
           '"pcie_fed %.3f G/s, soa %.3f" % (d["pcie_fed"]["value"] / 1e9, d["pcie_fed"]["soa"]["value"] / 1e9)'
@@ -127,7 +127,7 @@ task_ab() {
       if [ "$mode" = "route" ] || [ "$mode" = "pcie" ]; then
         tag=$(basename "${lib:-cur}" .so)_route_$rep
         RL_LIB_PATH=${lib:+$PWD/$lib} timeout -k 10 200 python -u bench.py --route --no-cpu-baseline --pcie-steps 0 \
-          --latency-steps 5 > gpurun_out/ab_$tag.log 2>&1 || { tail -5 gpurun_out/ab_$tag.log; return 1; }
+          --latency-steps 5 --loaded-steps 0 > gpurun_out/ab_$tag.log 2>&1 || { tail -5 gpurun_out/ab_$tag.log; return 1; }
         summary gpurun_out/ab_$tag.log $tag
       fi
     done
@@ -138,7 +138,7 @@ task_kstats() {
   local tag=${TAG:-c1_serial} f
   rm -rf gpurun_out/kstats_$tag && mkdir -p gpurun_out/kstats_$tag
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kstats_$tag -o run -- \
-    python -u bench.py --steps 50 --warmup 3 --latency-steps 3 --no-cpu-baseline --prof-every 0 \
+    python -u bench.py --steps 50 --warmup 3 --latency-steps 3 --loaded-steps 0 --no-cpu-baseline --prof-every 0 \
     ${KARGS:---config c1 --serial} > gpurun_out/kstats_$tag.log 2>&1 || { tail -20 gpurun_out/kstats_$tag.log; return 1; }
   tail -1 gpurun_out/kstats_$tag.log | cut -c1-300
   f=$(find gpurun_out/kstats_$tag -name "*kernel_trace.csv" | head -1)
@@ -149,7 +149,7 @@ task_kstats() {
 task_pcie_trace() {
   rm -rf gpurun_out/pcie_trace && mkdir -p gpurun_out/pcie_trace
   timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/pcie_trace -o run -- \
-    python -u bench.py --steps 20 --warmup 3 --latency-steps 3 --no-cpu-baseline --prof-every 0 --pcie-steps 30 ${KARGS:-} \
+    python -u bench.py --steps 20 --warmup 3 --latency-steps 3 --loaded-steps 0 --no-cpu-baseline --prof-every 0 --pcie-steps 30 ${KARGS:-} \
     > gpurun_out/pcie_trace.log 2>&1 || { tail -20 gpurun_out/pcie_trace.log; return 1; }
   tail -1 gpurun_out/pcie_trace.log | cut -c1-200
   python scripts/copy_timeline.py gpurun_out/pcie_trace > gpurun_out/pcie_timeline.txt 2>&1
@@ -163,7 +163,7 @@ task_route_trace() {
     tag=$(basename "${lib:-cur}" .so)
     rm -rf gpurun_out/rtrace_$tag && mkdir -p gpurun_out/rtrace_$tag
     RL_LIB_PATH=${lib:+$PWD/$lib} timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/rtrace_$tag \
-      -o run -- python -u bench.py --route --steps 100 --warmup 3 --latency-steps 3 --pcie-steps 0 --no-cpu-baseline ${KARGS:-} \
+      -o run -- python -u bench.py --route --steps 100 --warmup 3 --latency-steps 3 --loaded-steps 0 --pcie-steps 0 --no-cpu-baseline ${KARGS:-} \
       > gpurun_out/rtrace_$tag.log 2>&1 || { tail -5 gpurun_out/rtrace_$tag.log; return 1; }
     echo "== $tag"
     f=$(find gpurun_out/rtrace_$tag -name "*kernel_trace.csv" | head -1)
@@ -175,7 +175,7 @@ task_route_trace() {
 task_seed_sweep() {
   local cfg=${CFG:-c2} seed
   for seed in ${SEEDS:-1 2 3 4 5 6 7 8 9 10 11 12}; do
-    timeout -k 10 120 python -u bench.py --config $cfg --hash-seed $seed --steps 40 --warmup 2 --latency-steps 12 \
+    timeout -k 10 120 python -u bench.py --config $cfg --hash-seed $seed --steps 40 --warmup 2 --latency-steps 12 --loaded-steps 0 \
       --no-cpu-baseline --pcie-steps 0 > gpurun_out/seed_${cfg}_$seed.log 2>&1 || { tail -5 gpurun_out/seed_${cfg}_$seed.log; return 1; }
     summary gpurun_out/seed_${cfg}_$seed.log "seed $seed" '"p50 %.3f p99 %.3f" % (d["p50_batch_ms"], d["p99_batch_ms"])'
   done
@@ -185,7 +185,7 @@ task_split_prof() {
   local lib tag
   for lib in ${LIBS:-build_abl/lib_sprof.so}; do
     tag=$(basename $lib .so)
-    RL_LIB_PATH=$PWD/$lib timeout -k 10 200 python -u bench.py --config c2u --steps 10 --warmup 2 --latency-steps 2 \
+    RL_LIB_PATH=$PWD/$lib timeout -k 10 200 python -u bench.py --config c2u --steps 10 --warmup 2 --latency-steps 2 --loaded-steps 0 \
       --pcie-steps 0 --no-cpu-baseline > gpurun_out/split_prof_$tag.log 2>&1 || { tail -5 gpurun_out/split_prof_$tag.log; return 1; }
     echo "== $tag"; grep split_long gpurun_out/split_prof_$tag.log | tail -4
   done

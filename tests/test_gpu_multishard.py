@@ -91,6 +91,39 @@ def test_gpu_multishard_c2_host_path_vs_c_oracle(n_shards, lc, ps):
     co.close()
 
 
+@pytest.mark.parametrize("n_shards", [2, 3])
+def test_gpu_multishard_max_rules_equal_to_batch_rules(n_shards):
+    """max_rules == n_rules: the owners keep stats per source
+    slice, so each shard holds n_shards x max_rules rows; a batch carrying all
+    max_rules rules answers and sums its stats like one table, through the host,
+    the pipelined host and the device entry points."""
+    be = Backend(0.8, True, table_slots=1 << 17, max_batch=1 << 15, max_rules=2, hash_seed=7,
+                 **_shards(n_shards))
+    co = c_oracle.COracle(0.8, True)
+    batches = _c2(n_batches=3, seed=11)
+    for a, n, nq, nr in batches[:2]:
+        assert nr == 2
+        g = be.do_limit_arrays(a, n, nq, nr)
+        o = co.do_limit(a, n, nq, nr)
+        for k in ("code", "limit_remaining", "reset_s", "stats"):
+            assert np.array_equal(g[k], o[k]), k
+    a, n, nq, nr = batches[2]
+    dev = _to_dev(a)
+    out = {"code": torch.zeros(n, dtype=torch.uint8, device="cuda"),
+           "limit_remaining": torch.zeros(n, dtype=torch.int32, device="cuda"),
+           "reset_s": torch.zeros(n, dtype=torch.int32, device="cuda"),
+           "stats": torch.zeros(nr * abi.RL_NUM_STATS, dtype=torch.int64, device="cuda")}
+    torch.cuda.synchronize()
+    be.do_limit_device(dev, out, n, nq, nr)
+    be.synchronize()
+    o = co.do_limit(a, n, nq, nr)
+    assert np.array_equal(out["code"].cpu().numpy(), o["code"])
+    assert np.array_equal(out["limit_remaining"].cpu().numpy().view(np.uint32), o["limit_remaining"])
+    assert np.array_equal(out["stats"].cpu().numpy().view(np.uint64), o["stats"])
+    be.close()
+    co.close()
+
+
 def test_gpu_multishard_async_device_path_pipelined_vs_c_oracle():
     """rl_do_limit_async with device arrays: every batch submitted before one
     synchronize (RSLOTS routed batches in flight)."""

@@ -75,10 +75,15 @@ def test_gpu_prefixed_pipeline_matches_oracle(lc):
     keep, got = [], []
     for i, (a, n, nq, nr) in enumerate(batches):
         pb = prefixed_batch(a, n, nq, nr, alloc=lambda nb: arena.array(nb, np.uint8))
-        out = {k: arena.like(v) for k, v in pb.alloc_result(isolate=(i == 4)).items()}
+        # batch 2 without reset_s (not copied back): the caller's CalculateReset
+        out = {k: arena.like(v) for k, v in pb.alloc_result(isolate=(i == 4), reset=(i != 2)).items()}
         keep.append((pb, out, be.do_limit_prefixed_async(pb, out)))
         got.append(out)
     be.synchronize()
+    a, n = batches[2][0], batches[2][1]
+    div = np.where(a["unit"][:n] == 1, 1, 60)
+    now = a["now"][a["req_idx"][:n]]
+    got[2]["reset_s"] = (div - now % div).astype(np.uint32)  # utils.CalculateReset (utilities.go:32-36)
     _check(got, want, batches, isolate=(4,))
     be.close()
     arena.close()
@@ -174,6 +179,8 @@ def test_gpu_prefixed_bad_limit_index_alone_bad_index_fails_batch():
         return pb
 
     T = (nq + abi.RL_PREFIXED_TILE - 1) // abi.RL_PREFIXED_TILE
+    be.close()
+    be = Backend(0.8, False, table_slots=1 << 16, max_batch=1 << 14, max_rules=8)  # (an untouched table)
     bad = [corrupt("index", 4 * 2 + 0, 5),                  # a tile's first descriptor
            corrupt("index", 4 * 3 + 2, 1 << 30),            # a tile's suffix offset past the totals
            corrupt("req", 7, (3 << 16) | 2),                # a request's descriptor count / prefix
