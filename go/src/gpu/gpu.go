@@ -25,8 +25,9 @@ import (
 // Config mirrors rl_config: the knobs NewFixedRateLimitCacheImpl receives
 // (src/redis/fixed_cache_impl.go:118-125) plus the HBM sizing.
 type Config struct {
-	TableSlots     uint64  // 128-B slots (power of 2)
-	ArenaBytes     uint64  // overflow arena for stems longer than 80 B (0: library default)
+	TableSlots     uint64  // 64-B slots (power of 2)
+	RingLines      uint64  // 128-B history lines for keys revisited within 8 windows (0: TableSlots/4)
+	ArenaBytes     uint64  // overflow arena for stems longer than 36 B (0: library default)
 	MaxBatch       uint32  // descriptors per batch
 	MaxRequests    uint32  // requests per batch (0: MaxBatch)
 	MaxRules       uint32  // distinct rule ids (stats rows)
@@ -46,6 +47,7 @@ type Ctx struct{ c *C.rl_ctx }
 func New(cfg Config) (*Ctx, error) {
 	var rc C.rl_config
 	rc.table_slots = C.uint64_t(cfg.TableSlots)
+	rc.ring_lines = C.uint64_t(cfg.RingLines)
 	rc.arena_bytes = C.uint64_t(cfg.ArenaBytes)
 	rc.max_batch = C.uint32_t(cfg.MaxBatch)
 	rc.max_requests = C.uint32_t(cfg.MaxRequests)
@@ -138,6 +140,7 @@ func (c *Ctx) LocalCacheInfo(now int64) (LocalCacheInfo, error) {
 // TableInfo: live slots, tombstones and arena use, summed over shards.
 type TableInfo struct {
 	TableSlots, LiveSlots, Tombstones, ArenaBytesUsed, ExactStems, Batches, Decisions uint64
+	RingLines, RingLinesUsed, LostSlots                                             uint64
 }
 
 func (c *Ctx) TableInfo() (TableInfo, error) {
@@ -146,7 +149,8 @@ func (c *Ctx) TableInfo() (TableInfo, error) {
 		return TableInfo{}, err
 	}
 	return TableInfo{uint64(ti.table_slots), uint64(ti.live_slots), uint64(ti.tombstones),
-		uint64(ti.arena_bytes_used), uint64(ti.exact_stems), uint64(ti.batches), uint64(ti.decisions)}, nil
+		uint64(ti.arena_bytes_used), uint64(ti.exact_stems), uint64(ti.batches), uint64(ti.decisions),
+		uint64(ti.ring_lines), uint64(ti.ring_lines_used), uint64(ti.lost_slots)}, nil
 }
 
 // ---- pinned host memory: Go never hands Go-heap pointers to C (cgo pointer

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 2u
+#define RL_ABI_VERSION 3u
 
 /* Status codes. */
 enum rl_status {
@@ -68,8 +68,8 @@ enum rl_stat {
  * (src/redis/fixed_cache_impl.go:118-125, src/settings/settings.go:45-50)
  * plus capacity sizing for HBM. */
 typedef struct rl_config {
-  uint64_t table_slots;      /* 128-B slots in the HBM table (power of 2; 0 = default 2^24) */
-  uint64_t arena_bytes;      /* overflow arena for stems longer than 80 B (0 = default 64 MiB) */
+  uint64_t table_slots;      /* 64-B slots in the HBM table (power of 2; 0 = default 2^24) */
+  uint64_t arena_bytes;      /* overflow arena for stems longer than 36 B (0 = default 64 MiB) */
   uint32_t max_batch;        /* max descriptors per rl_do_limit call (0 = default 1<<20) */
   uint32_t max_requests;     /* max requests per call (0 = max_batch) */
   uint32_t max_rules;        /* max distinct rule ids per call (0 = default 65536) */
@@ -87,7 +87,11 @@ typedef struct rl_config {
                                 so that many stems share one sort key and one home region */
   int32_t shard_device[16];  /* HIP device of shard k < n_shards (shards may share a device);
                                 unused when n_shards <= 1 (cfg.device) */
-  int32_t reserved[8];
+  uint64_t ring_lines;       /* 128-B history lines (the 8 windows below a key's newest), taken by
+                                the keys revisited within 8 windows and returned by rl_sweep
+                                (0 = table_slots / 4). Exhausted: a key's older record is dropped
+                                and a later request for it fails with RL_E_TIME, never a wrong count */
+  int32_t reserved[6];
 } rl_config;
 
 /* One packed batch (struct of arrays). Only descriptors whose limit is
@@ -167,6 +171,10 @@ typedef struct rl_table_info {
   uint64_t exact_stems;       /* slots flagged multi-unit (exact slow path) */
   uint64_t batches;
   uint64_t decisions;
+  uint64_t ring_lines;        /* history lines in the pool (rl_config.ring_lines) */
+  uint64_t ring_lines_used;   /* lines held by slots (rl_sweep returns a swept slot's line) */
+  uint64_t lost_slots;        /* slots that could not take a line when they needed one: their
+                                 older windows fail with RL_E_TIME (size ring_lines up) */
 } rl_table_info;
 
 typedef struct rl_ctx rl_ctx;

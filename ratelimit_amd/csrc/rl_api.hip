@@ -652,6 +652,9 @@ int rl_table_info_get(rl_ctx* c, rl_table_info* info) {
     sum.arena_bytes_used += x.arena_bytes_used;
     sum.exact_stems += x.exact_stems;
     sum.decisions += x.decisions;
+    sum.ring_lines += x.ring_lines;
+    sum.ring_lines_used += x.ring_lines_used;
+    sum.lost_slots += x.lost_slots;
     sum.batches = std::max(sum.batches, x.batches);
   }
   *info = sum;

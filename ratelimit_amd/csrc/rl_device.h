@@ -13,27 +13,34 @@ namespace rl {
 // ---------------------------------------------------------------------------
 // HBM counter table.
 //
-// One slot per (stem, unit). The Redis key of the reference is
+// One 64-B slot per (stem, unit). The Redis key of the reference is
 // stem ‖ decimal(windowStart) (cache_key.go:62-74); a slot holds the state of
-// the newest window key of its (stem, unit), `cur`, and a ring beside the
-// table (`Hist`, one 128-B line per slot) holds the HIST_W windows before it:
-// window w < cur at position (w / div) % HIST_W. For a stem used with a
+// the newest window key of its (stem, unit), `cur`. For a stem used with a
 // single unit the current window is the only live key while time moves
 // forward, so the slot is recycled in place when the window advances (no
-// insert per window, no EXPIRE traffic) and the old record moves to the ring
-// with one write. The ring answers requests whose time moved back: Redis keeps
-// a key div + jitter seconds after its last hit (fixed_cache_impl.go:71-74),
-// so a request that waited in a batcher finds its window's count. A window
-// more than HIST_W windows back is RL_E_TIME for that descriptor, never a
-// silently wrong count. The ring also keeps the records a stem later seen with
-// a second unit shares with it (only possible through per-request overrides,
+// insert per window, no EXPIRE traffic). The HIST_W windows before cur live in
+// a ring line (`Hist`, 128 B: window w < cur at position (w / div) % HIST_W)
+// taken from a pool the first time the slot needs one, i.e. when a window
+// rolls while the old one is still within the ring's reach: a key revisited
+// less often than every HIST_W windows never takes one (C1's SECOND keys), so
+// the table costs 64 B per slot plus 128 B per key that keeps history. The
+// ring answers requests whose time moved back: Redis keeps a key div + jitter
+// seconds after its last hit (fixed_cache_impl.go:71-74), so a request that
+// waited in a batcher finds its window's count. A window more than HIST_W
+// windows back, or one whose record could not be kept because the pool was
+// exhausted (SLOT_LOST), is RL_E_TIME for that descriptor, never a silently
+// wrong count. The ring also keeps the records a stem later seen with a
+// second unit shares with it (only possible through per-request overrides,
 // config_impl.go:254-265; DESIGN.md §"Exact key identity").
 // ---------------------------------------------------------------------------
 constexpr uint32_t WS_INVALID = 0xFFFFFFFFu;  // record never written
-constexpr uint64_t TAG_EMPTY = 0;
-constexpr uint64_t TAG_TOMB = 1;
-constexpr uint32_t INLINE_KEY = 80;           // stem bytes stored in the slot
+constexpr uint32_t TAG_EMPTY = 0;
+constexpr uint32_t TAG_TOMB = 1;
+constexpr uint32_t KEY_IN = 36;               // a stem of at most KEY_IN bytes is stored whole in its slot
+constexpr uint32_t KEY_SPLIT = 32;            // a longer one: bytes [0, KEY_SPLIT) here, the rest in the arena
+constexpr uint32_t RING_NONE = 0xFFFFFFFFu;   // slot without a ring line
 constexpr uint8_t SLOT_EXACT = 0x1;           // stem has >1 unit slot: exact (serial) path
+constexpr uint8_t SLOT_LOST = 0x2;            // a record below cur was dropped (ring pool exhausted): RL_E_TIME
 constexpr uint32_t HIST_W = 8;                // ring records per slot: windows 1..HIST_W back from cur
 
 struct Win {
@@ -43,31 +50,28 @@ struct Win {
   uint32_t lc;      // freecache entry live while now < lc (Set ttl = div)
 };
 
-// One 128-B line. The first 64-B sector holds everything a probe of a stem of
-// at most KEY_LO bytes needs (tag, length, the current window, the stem), so
-// such a probe reads one sector; the arena offset and stem bytes KEY_LO..79
-// are in the second sector, read only for longer stems.
-constexpr uint32_t KEY_LO = 36;               // stem bytes in the first sector
-struct __attribute__((aligned(128))) Slot {
-  uint64_t tag;       // TAG_EMPTY / TAG_TOMB / mix(hash(stem), unit) >= 2
+// One 64-B sector: a probe reads exactly one sector, and only changed window
+// records are written back. A stem longer than KEY_IN keeps its first
+// KEY_SPLIT bytes here and the rest in the long-stem arena, whose offset (in
+// 16-B units) takes the slot's last stem dword.
+struct __attribute__((aligned(64))) Slot {
+  uint32_t tag;       // TAG_EMPTY / TAG_TOMB / mix(hash(stem), unit) >= 2
   uint16_t key_len;   // stem length
   uint8_t unit;       // rl_unit
-  uint8_t flags;      // SLOT_EXACT
-  Win cur;            // bytes 12..27
-  uint8_t key0[KEY_LO];               // stem bytes 0..35 (28..63)
-  uint32_t spare[4];                  // 64..79 (unused)
-  uint32_t ext_off;   // arena offset in 16-B units for bytes >= INLINE_KEY
-  uint8_t key1[INLINE_KEY - KEY_LO];  // stem bytes 36..79 (84..127)
+  uint8_t flags;      // SLOT_EXACT | SLOT_LOST
+  Win cur;            // bytes 8..23
+  uint32_t ring;      // 24..27: this slot's ring line in the pool (RING_NONE: none yet)
+  uint8_t key[KEY_IN];  // 28..63: stem bytes (key_len > KEY_IN: bytes 0..31, then the arena offset)
 };
-static_assert(offsetof(Slot, cur) == 12 && offsetof(Slot, key0) == 28 && offsetof(Slot, spare) == 64 &&
-                  offsetof(Slot, ext_off) == 80 && offsetof(Slot, key1) == 84,
-              "slot layout");
-// dword of the slot holding stem dword k (k < 20)
-__host__ __device__ constexpr uint32_t slot_key_dw(uint32_t k) { return k < KEY_LO / 4 ? 7 + k : 12 + k; }
-static_assert(sizeof(Slot) == 128, "slot must be one 128-B line");
+static_assert(offsetof(Slot, cur) == 8 && offsetof(Slot, ring) == 24 && offsetof(Slot, key) == 28, "slot layout");
+static_assert(sizeof(Slot) == 64, "slot must be one 64-B sector");
+// dword of the slot holding stem dword k (k < KEY_IN / 4)
+__host__ __device__ constexpr uint32_t slot_key_dw(uint32_t k) { return 7 + k; }
+constexpr uint32_t SLOT_EXT_DW = 15;          // arena offset of a stem longer than KEY_IN
+// stem bytes kept in the slot for a stem of len bytes
+__host__ __device__ constexpr uint32_t slot_inline(uint32_t len) { return len <= KEY_IN ? len : KEY_SPLIT; }
 
-// The window records of slot i below its cur: one 128-B line (table-parallel
-// array; line i belongs to slot i).
+// The window records below a slot's cur: one 128-B line of the ring pool.
 struct __attribute__((aligned(128))) Hist {
   Win w[HIST_W];
 };
@@ -175,8 +179,8 @@ struct DwordReader {
   }
 };
 
-__host__ __device__ inline uint64_t slot_tag(uint64_t hstem, uint32_t unit) {
-  uint64_t t = fmix64(hstem + uint64_t(unit) * 0x9E3779B97F4A7C15ull);
+__host__ __device__ inline uint32_t slot_tag(uint64_t hstem, uint32_t unit) {
+  const uint32_t t = (uint32_t)fmix64(hstem + uint64_t(unit) * 0x9E3779B97F4A7C15ull);
   return t < 2 ? t + 2 : t;
 }
 

@@ -53,8 +53,16 @@ struct Engine {
   HashKey hk{};
   // table
   Slot* slots = nullptr;
-  Hist* hist = nullptr;  // [nslots] ring lines (window records below cur)
   uint64_t nslots = 0;
+  // the ring pool (window records below the slots' cur, rl_device.h): lines,
+  // the two free lists a sweep alternates between (the current one: ring_cur),
+  // and the counters {B, taken, n} (ring_alloc, rl_kernels.hip)
+  Hist* ring = nullptr;
+  uint64_t ring_cap = 0;
+  uint32_t* ring_free[2] = {};
+  uint32_t ring_cur = 0;
+  unsigned long long* ring_ctr = nullptr;
+  uint64_t snap_free_from = 0;  // (snapshot: the first untaken free-list entry)
   uint8_t* arena = nullptr;
   uint8_t* arena2 = nullptr;  // compaction target (rl_sweep), swapped with arena
   uint64_t arena_cap16 = 0;

@@ -196,7 +196,10 @@ BatchDev dev_view(const Engine* c, const rl_batch* in, uint32_t stem_cap) {
 TableDev table_view(Engine* c) {
   TableDev t;
   t.slots = c->slots;
-  t.hist = c->hist;
+  t.ring = c->ring;
+  t.ring_free = c->ring_free[c->ring_cur];
+  t.ring_ctr = c->ring_ctr;
+  t.ring_cap = (uint32_t)c->ring_cap;
   t.mask = c->nslots - 1;
   t.arena = c->arena;
   t.arena_used16 = c->s[0].counters + 4;
@@ -302,6 +305,8 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   if (!cfg.table_slots) cfg.table_slots = 1ull << 24;
   if (cfg.table_slots & (cfg.table_slots - 1)) return fail("gpu: table_slots must be a power of two", nullptr);
   if (!cfg.arena_bytes) cfg.arena_bytes = 64ull << 20;
+  if (!cfg.ring_lines) cfg.ring_lines = std::max<uint64_t>(cfg.table_slots / 4, 1024);
+  if (cfg.ring_lines > 0xFFFFFFFEull) return fail("gpu: ring_lines must be below 2^32 - 1", nullptr);
   if (!cfg.max_batch) cfg.max_batch = 1u << 20;
   if (cfg.max_batch > MAX_PART_TILES * PART_TILE)
     return fail("gpu: max_batch must be at most 8388608 descriptors", nullptr);
@@ -320,6 +325,7 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   c->cfg.hash_seed = c->hash_seed;
   c->hk = hash_key_of(c->hash_seed, cfg.debug_hash_bits);
   c->nslots = cfg.table_slots;
+  c->ring_cap = cfg.ring_lines;
   c->arena_cap16 = cfg.arena_bytes / 16;
   const uint32_t n = cfg.max_batch;
   bool ok = true;
@@ -329,7 +335,9 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
     ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess;
   for (uint32_t k = 0; k < PROGRESS_RING; k++)
     ok = ok && hipEventCreateWithFlags(&c->done_ring[k], hipEventDisableTiming) == hipSuccess;
-  ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess && dalloc(&c->hist, c->nslots) == hipSuccess;
+  ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess && dalloc(&c->ring, c->ring_cap) == hipSuccess &&
+       dalloc(&c->ring_free[0], c->ring_cap) == hipSuccess && dalloc(&c->ring_free[1], c->ring_cap) == hipSuccess &&
+       dalloc(&c->ring_ctr, 4) == hipSuccess;
   ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess && dalloc(&c->arena2, cfg.arena_bytes) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++) ok = ok && alloc_buffer(c->s[k], n);
   Scratch& s0 = c->s[0];
@@ -366,7 +374,7 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && hipHostMalloc((void**)&c->h_counters, 8 * sizeof(unsigned long long)) == hipSuccess;
   if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
   ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
-       hipMemsetAsync(c->hist, 0xFF, c->nslots * sizeof(Hist), c->stream) == hipSuccess &&  // ws = WS_INVALID
+       hipMemsetAsync(c->ring_ctr, 0, 32, c->stream) == hipSuccess &&  // (lines are initialised when taken)
        hipMemsetAsync(c->errw, 0, (NBUF + 3) * 4, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.time_floor, 0, 8, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.counters, 0, 64, c->stream) == hipSuccess &&
@@ -424,7 +432,7 @@ void eng_destroy(Engine* c) {
   if (c->caller_ready) (void)hipEventDestroy(c->caller_ready);
   if (c->h_base) (void)hipHostFree(c->h_base);
   const Scratch& s0 = c->s[0];
-  void* bufs[] = {c->slots, c->hist, c->arena, c->arena2, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
+  void* bufs[] = {c->slots, c->ring, c->ring_free[0], c->ring_free[1], c->ring_ctr, c->arena, c->arena2, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
                   c->d_now, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_status,
                   c->d_rem,
                   c->d_reset, c->d_stats};
@@ -982,7 +990,12 @@ int eng_sweep(Engine* c, int64_t now, uint64_t* n_evicted) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (now > last) HIPCHK(c, hipMemcpyAsync(c->s[0].time_floor, &now, 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->s[0].counters, 0, 8, c->stream));
-  launch_sweep(c->slots, c->hist, c->nslots, (uint32_t)now, c->s[0].counters, c->stream);
+  {
+    const TableDev t = table_view(c);
+    launch_sweep(t, c->nslots, (uint32_t)now, c->s[0].counters, c->ring_free[c->ring_cur], c->ring_free[c->ring_cur ^ 1],
+                 c->stream);
+    c->ring_cur ^= 1;  // (later batches take lines from the list this sweep built)
+  }
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 40, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1003,11 +1016,17 @@ int eng_table_info_get(Engine* c, rl_table_info* info) {
   if (!c || !info) return set_err(c, RL_E_INVALID, "gpu: null argument");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   HIPCHK(c, after_batches(c, c->stream));
-  HIPCHK(c, hipMemsetAsync(c->s[0].counters, 0, 24, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->s[0].counters, 0, 32, c->stream));
   launch_table_info(c->slots, c->nslots, c->s[0].counters, c->stream);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 40, hipMemcpyDeviceToHost, c->stream));
+  unsigned long long rc[3];
+  HIPCHK(c, hipMemcpyAsync(rc, c->ring_ctr, 24, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  info->ring_lines = c->ring_cap;
+  info->ring_lines_used = std::min<uint64_t>(rc[0] + (rc[1] > rc[2] ? rc[1] - rc[2] : 0), c->ring_cap) -
+                          (rc[2] > rc[1] ? rc[2] - rc[1] : 0);  // (ring_alloc's counters)
+  info->lost_slots = c->h_counters[3];
   info->table_slots = c->nslots;
   info->live_slots = c->h_counters[0];
   info->tombstones = c->h_counters[1];
@@ -1347,7 +1366,7 @@ int eng_local_cache_info_get(Engine* c, int64_t now, rl_local_cache_info* info) 
   HIPCHK(c, after_batches(c, c->stream));
   unsigned long long* ctr = c->s[0].counters;
   HIPCHK(c, hipMemsetAsync(ctr + 7, 0, 8, c->stream));
-  launch_lc_count(c->slots, c->hist, c->nslots, (uint32_t)now, ctr + 7, c->stream);
+  launch_lc_count(table_view(c), c->nslots, (uint32_t)now, ctr + 7, c->stream);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(c->h_counters, ctr, 64, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1359,52 +1378,67 @@ int eng_local_cache_info_get(Engine* c, int64_t now, rl_local_cache_info* info) 
 }
 
 namespace {
-constexpr uint64_t SNAP_MAGIC = 0x33304150414e534cull;  // "LSNAPA03" (keyed hash, window ring)
+constexpr uint64_t SNAP_MAGIC = 0x34304150414e534cull;  // "LSNAPA04" (64-B slots, ring pool)
 struct SnapHeader {
   uint64_t magic, nslots, arena_used16, hash_seed;  // slots are placed by the keyed hash: restore adopts its key
   int64_t time_floor;
-  uint64_t reserved[3];
+  uint64_t ring_used;   // ring lines handed out from the pool's end (saved whole)
+  uint64_t free_left;   // the free list's untaken entries (saved, restored at its front)
+  uint64_t reserved;
 };
 static_assert(sizeof(SnapHeader) == 64, "snapshot header");
 
-int snap_state(Engine* c, uint64_t* arena_used16, int64_t* floor) {
+int snap_state(Engine* c, SnapHeader* h) {
   HIPCHK(c, hipSetDevice(c->cfg.device));
   HIPCHK(c, after_batches(c, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 64, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(floor, c->s[0].time_floor, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&h->time_floor, c->s[0].time_floor, 8, hipMemcpyDeviceToHost, c->stream));
+  unsigned long long rc[3];
+  HIPCHK(c, hipMemcpyAsync(rc, c->ring_ctr, 24, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  *arena_used16 = std::min<uint64_t>(c->h_counters[4], c->arena_cap16);
+  h->arena_used16 = std::min<uint64_t>(c->h_counters[4], c->arena_cap16);
+  h->ring_used = std::min<uint64_t>(rc[0] + (rc[1] > rc[2] ? rc[1] - rc[2] : 0), c->ring_cap);  // (ring_alloc)
+  h->free_left = rc[2] > rc[1] ? rc[2] - rc[1] : 0;
+  c->snap_free_from = rc[2] > rc[1] ? rc[1] : 0;
   return RL_OK;
+}
+
+uint64_t snap_bytes(const Engine* c, const SnapHeader& h) {
+  return sizeof(SnapHeader) + c->nslots * sizeof(Slot) + h.ring_used * sizeof(Hist) + h.free_left * 4 +
+         h.arena_used16 * 16;
 }
 }  // namespace
 
 int eng_snapshot_size(Engine* c, uint64_t* bytes) {
   if (!c || !bytes) return set_err(c, RL_E_INVALID, "gpu: null argument");
-  uint64_t au = 0;
-  int64_t fl = 0;
-  int rc = snap_state(c, &au, &fl);
+  SnapHeader h{};
+  int rc = snap_state(c, &h);
   if (rc) return rc;
-  *bytes = sizeof(SnapHeader) + c->nslots * (sizeof(Slot) + sizeof(Hist)) + au * 16;
+  *bytes = snap_bytes(c, h);
   return RL_OK;
 }
 
 int eng_snapshot_save(Engine* c, void* host, uint64_t bytes) {
   if (!c || !host) return set_err(c, RL_E_INVALID, "gpu: null argument");
   SnapHeader h{};
-  int rc = snap_state(c, &h.arena_used16, &h.time_floor);
+  int rc = snap_state(c, &h);
   if (rc) return rc;
   h.magic = SNAP_MAGIC;
   h.nslots = c->nslots;
   h.hash_seed = c->hash_seed;
-  const uint64_t tb = c->nslots * sizeof(Slot), hb = c->nslots * sizeof(Hist);
-  const uint64_t need = sizeof(SnapHeader) + tb + hb + h.arena_used16 * 16;
-  if (bytes < need) return set_err(c, RL_E_CAPACITY, "gpu: snapshot buffer smaller than rl_snapshot_size");
+  if (bytes < snap_bytes(c, h)) return set_err(c, RL_E_CAPACITY, "gpu: snapshot buffer smaller than rl_snapshot_size");
   uint8_t* p = (uint8_t*)host;
   memcpy(p, &h, sizeof h);
-  HIPCHK(c, hipMemcpy(p + sizeof h, c->slots, tb, hipMemcpyDeviceToHost));
-  HIPCHK(c, hipMemcpy(p + sizeof h + tb, c->hist, hb, hipMemcpyDeviceToHost));
-  if (h.arena_used16)
-    HIPCHK(c, hipMemcpy(p + sizeof h + tb + hb, c->arena, h.arena_used16 * 16, hipMemcpyDeviceToHost));
+  p += sizeof h;
+  const uint64_t tb = c->nslots * sizeof(Slot), rb = h.ring_used * sizeof(Hist);
+  HIPCHK(c, hipMemcpy(p, c->slots, tb, hipMemcpyDeviceToHost));
+  p += tb;
+  if (rb) HIPCHK(c, hipMemcpy(p, c->ring, rb, hipMemcpyDeviceToHost));
+  p += rb;
+  if (h.free_left)
+    HIPCHK(c, hipMemcpy(p, c->ring_free[c->ring_cur] + c->snap_free_from, h.free_left * 4, hipMemcpyDeviceToHost));
+  p += h.free_left * 4;
+  if (h.arena_used16) HIPCHK(c, hipMemcpy(p, c->arena, h.arena_used16 * 16, hipMemcpyDeviceToHost));
   return RL_OK;
 }
 
@@ -1416,16 +1450,23 @@ int eng_snapshot_load(Engine* c, const void* host, uint64_t bytes) {
   if (h.magic != SNAP_MAGIC) return set_err(c, RL_E_INVALID, "gpu: not a table snapshot");
   if (h.nslots != c->nslots) return set_err(c, RL_E_INVALID, "gpu: snapshot table_slots differ from this ctx");
   if (h.arena_used16 > c->arena_cap16) return set_err(c, RL_E_INVALID, "gpu: snapshot arena larger than this ctx's");
-  const uint64_t tb = h.nslots * sizeof(Slot), hb = h.nslots * sizeof(Hist);
-  if (bytes < sizeof h + tb + hb + h.arena_used16 * 16) return set_err(c, RL_E_INVALID, "gpu: snapshot truncated");
+  if (h.ring_used > c->ring_cap || h.free_left > c->ring_cap)
+    return set_err(c, RL_E_INVALID, "gpu: snapshot ring pool larger than this ctx's ring_lines");
+  if (bytes < snap_bytes(c, h)) return set_err(c, RL_E_INVALID, "gpu: snapshot truncated");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   HIPCHK(c, after_batches(c, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  const uint8_t* p = (const uint8_t*)host;
-  HIPCHK(c, hipMemcpy(c->slots, p + sizeof h, tb, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->hist, p + sizeof h + tb, hb, hipMemcpyHostToDevice));
-  if (h.arena_used16)
-    HIPCHK(c, hipMemcpy(c->arena, p + sizeof h + tb + hb, h.arena_used16 * 16, hipMemcpyHostToDevice));
+  const uint8_t* p = (const uint8_t*)host + sizeof h;
+  const uint64_t tb = h.nslots * sizeof(Slot), rb = h.ring_used * sizeof(Hist);
+  HIPCHK(c, hipMemcpy(c->slots, p, tb, hipMemcpyHostToDevice));
+  p += tb;
+  if (rb) HIPCHK(c, hipMemcpy(c->ring, p, rb, hipMemcpyHostToDevice));
+  p += rb;
+  if (h.free_left) HIPCHK(c, hipMemcpy(c->ring_free[c->ring_cur], p, h.free_left * 4, hipMemcpyHostToDevice));
+  p += h.free_left * 4;
+  const unsigned long long rc[3] = {h.ring_used, 0ull, h.free_left};
+  HIPCHK(c, hipMemcpy(c->ring_ctr, rc, 24, hipMemcpyHostToDevice));
+  if (h.arena_used16) HIPCHK(c, hipMemcpy(c->arena, p, h.arena_used16 * 16, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->s[0].counters + 4, &h.arena_used16, 8, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->s[0].time_floor, &h.time_floor, 8, hipMemcpyHostToDevice));
   c->hash_seed = h.hash_seed;

@@ -126,7 +126,12 @@ struct OutDev {
 
 struct TableDev {
   Slot* slots;
-  Hist* hist;  // [slots] window records below each slot's cur
+  // the ring pool: lines handed to slots on first need (Slot::ring); the last
+  // sweep's freed lines are taken first, then the pool's untouched end
+  Hist* ring;
+  const uint32_t* ring_free;     // [ring_cap] lines freed by the last sweep
+  unsigned long long* ring_ctr;  // {B, taken, n}: lines handed out from the end, numbers taken, free lines (ring_alloc)
+  uint32_t ring_cap;
   uint64_t mask;
   uint8_t* arena;
   unsigned long long* arena_used16;
@@ -251,10 +256,13 @@ void launch_route_ret(const unsigned long long* res, uint32_t n, const uint32_t*
 // out[i] = sum over blocks b of stage[b * stride + i], i < m (stride 0: m).
 void launch_stats_sum(const unsigned long long* stage, uint32_t n_blocks, uint32_t m, unsigned long long* out,
                       hipStream_t st, uint32_t stride = 0);
-void launch_sweep(Slot* slots, const Hist* hist, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st);
+// The epoch sweep: rebase the free list (free_from: the lines the previous
+// sweep freed, free_to: the list this one builds), then evict.
+void launch_sweep(const TableDev& t, uint64_t nslots, uint32_t now, unsigned long long* evicted,
+                  const uint32_t* free_from, uint32_t* free_to, hipStream_t st);
 void launch_arena_compact(Slot* slots, uint64_t nslots, const uint8_t* from, uint8_t* to, unsigned long long* used16,
                           hipStream_t st);
-void launch_lc_count(const Slot* slots, const Hist* hist, uint64_t nslots, uint32_t now, unsigned long long* out, hipStream_t st);
+void launch_lc_count(const TableDev& t, uint64_t nslots, uint32_t now, unsigned long long* out, hipStream_t st);
 void launch_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out, hipStream_t st);
 void launch_debug_keys(const BatchDev& b, uint8_t* out, uint32_t* klen, hipStream_t st);
 void launch_debug_decide(uint32_t n, const uint32_t* before, const uint32_t* after, const uint8_t* lc_hit,

@@ -530,28 +530,30 @@ __device__ inline uint32_t key_dw(const Key& key, uint32_t k) {
   return k < KEY_HEAD / 4 ? u4w(key.h[k >> 2], k & 3) : key.st.word(k);
 }
 
-// Stem bytes [INLINE_KEY, len) of `key` against the arena copy at ext_off.
+// Stem bytes [KEY_SPLIT, len) of `key` against the arena copy at ext_off.
 __device__ inline uint32_t arena_diff(const uint8_t* arena, uint32_t ext_off, const Key& key) {
   const uint32_t* ek = reinterpret_cast<const uint32_t*>(arena + (size_t)ext_off * 16);
-  const uint32_t rest = key.len - INLINE_KEY, rw = rest >> 2;
+  const uint32_t rest = key.len - KEY_SPLIT, rw = rest >> 2;
   uint32_t d = 0;
-  for (uint32_t k = 0; k < rw; k++) d |= ek[k] ^ key.st.word(INLINE_KEY / 4 + k);
-  if (rest & 3) d |= (ek[rw] ^ key.st.word(INLINE_KEY / 4 + rw)) & tail_mask(rest);
+  for (uint32_t k = 0; k < rw; k++) d |= ek[k] ^ key.st.word(KEY_SPLIT / 4 + k);
+  if (rest & 3) d |= (ek[rw] ^ key.st.word(KEY_SPLIT / 4 + rw)) & tail_mask(rest);
   return d;
 }
+
+__device__ inline uint32_t slot_ext(const Slot* s) { return reinterpret_cast<const uint32_t*>(s)[SLOT_EXT_DW]; }
 
 // Slot stem == `key`? Only the stem's own dwords are read (the last one masked).
 __device__ inline bool slot_key_equal(const Slot* s, const Key& key, const uint8_t* arena) {
   if (s->key_len != key.len) return false;
   const uint32_t* sd = reinterpret_cast<const uint32_t*>(s);
-  const uint32_t len = key.len, il = len < INLINE_KEY ? len : INLINE_KEY, nw = il >> 2;
+  const uint32_t len = key.len, il = slot_inline(len), nw = il >> 2;
   uint32_t diff = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < INLINE_KEY / 4; k++) {
+  for (uint32_t k = 0; k < KEY_IN / 4; k++) {
     if (k < nw) diff |= sd[slot_key_dw(k)] ^ key_dw(key, k);
     else if (k == nw && (il & 3)) diff |= (sd[slot_key_dw(k)] ^ key_dw(key, k)) & tail_mask(il);
   }
-  if (len > INLINE_KEY) diff |= arena_diff(arena, s->ext_off, key);
+  if (len > KEY_IN) diff |= arena_diff(arena, sd[SLOT_EXT_DW], key);
   return diff == 0;
 }
 
@@ -570,33 +572,30 @@ __device__ __attribute__((always_inline)) inline bool arena_claim(const TableDev
   }
 }
 
-// Fill a freshly claimed slot. False when the arena cannot take the stem's
-// tail: the caller returns the slot to the table as a tombstone.
+// Fill a freshly claimed slot (no ring line: taken on first need). False when
+// the arena cannot take the stem's tail: the caller returns the slot to the
+// table as a tombstone.
 __device__ __attribute__((always_inline)) inline bool slot_init(const TableDev& t, Slot* s, const Key& key, uint32_t unit) {
-  const uint32_t len = key.len, il = len < INLINE_KEY ? len : INLINE_KEY, nw = il >> 2;
-  s->ext_off = 0;
-  if (len > INLINE_KEY) {
-    const uint32_t n16 = (len - INLINE_KEY + 15) / 16;
+  const uint32_t len = key.len, il = slot_inline(len), nw = il >> 2;
+  uint32_t* sd = reinterpret_cast<uint32_t*>(s);
+  if (len > KEY_IN) {
+    const uint32_t n16 = (len - KEY_SPLIT + 15) / 16;
     unsigned long long off;
     if (!arena_claim(t, n16, &off)) return false;
-    s->ext_off = (uint32_t)off;
+    sd[SLOT_EXT_DW] = (uint32_t)off;
     uint32_t* ek = reinterpret_cast<uint32_t*>(t.arena + off * 16);
-    for (uint32_t k = 0; k < (len - INLINE_KEY + 3) / 4; k++) ek[k] = key.st.word(INLINE_KEY / 4 + k);
+    for (uint32_t k = 0; k < (len - KEY_SPLIT + 3) / 4; k++) ek[k] = key.st.word(KEY_SPLIT / 4 + k);
   }
   s->key_len = (uint16_t)len;
   s->unit = (uint8_t)unit;
   s->flags = 0;
-  uint32_t* sd = reinterpret_cast<uint32_t*>(s);
 #pragma unroll
-  for (uint32_t k = 0; k < INLINE_KEY / 4; k++) {
+  for (uint32_t k = 0; k < KEY_IN / 4; k++) {
     if (k < nw) sd[slot_key_dw(k)] = key_dw(key, k);
     else if (k == nw && (il & 3)) sd[slot_key_dw(k)] = key_dw(key, k) & tail_mask(il);
   }
   s->cur = Win{WS_INVALID, 0, 0, 0};
-  // the ring may hold a swept key's records: one full-line write clears it
-  uint4* ring = reinterpret_cast<uint4*>(&t.hist[s - t.slots]);
-#pragma unroll
-  for (uint32_t j = 0; j < HIST_W; j++) ring[j] = make_uint4(WS_INVALID, 0u, 0u, 0u);
+  s->ring = RING_NONE;
   return true;
 }
 
@@ -608,10 +607,10 @@ __device__ inline uint32_t slot_fail_status(int64_t r) {
 
 // Claim slot i (expected tag `from`) for (stem, unit) and initialise it.
 // 1: claimed, 0: lost the race, -1: the arena is full (the slot is a tombstone again).
-__device__ __attribute__((always_inline)) inline int slot_claim(const TableDev& t, uint64_t i, uint64_t from, uint64_t tag, const Key& key,
+__device__ __attribute__((always_inline)) inline int slot_claim(const TableDev& t, uint64_t i, uint32_t from, uint32_t tag, const Key& key,
                                  uint32_t unit) {
   Slot* s = &t.slots[i];
-  if (atomicCAS((unsigned long long*)&s->tag, (unsigned long long)from, (unsigned long long)tag) != from) return 0;
+  if (atomicCAS(&s->tag, from, tag) != from) return 0;
   if (slot_init(t, s, key, unit)) return 1;
   __hip_atomic_store(&s->tag, TAG_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return -1;
@@ -619,22 +618,22 @@ __device__ __attribute__((always_inline)) inline int slot_claim(const TableDev& 
 
 // Find (and optionally insert) the slot of (stem, unit). Returns SLOT_ABSENT
 // when absent and insert == false, SLOT_TABLE_FULL / SLOT_ARENA_FULL (error
-// bit set in *err) when it cannot be inserted. Linear probing over 128-B slots
+// bit set in *err) when it cannot be inserted. Linear probing over 64-B slots
 // from the home slot = top bits of the stem hash, i.e. of the sort key:
 // consecutive runs probe increasing slots (page and TLB locality). A tag
 // match is confirmed by the full stem (collision-exact). Inserts claim the
-// slot with a 64-bit CAS on its tag; only one lane ever handles a given
+// slot with a CAS on its tag; only one lane ever handles a given
 // (stem, unit) per batch (runs are grouped by stem).
-__device__ __attribute__((always_inline)) inline int64_t find_slot(const TableDev& t, uint64_t hstem, uint64_t tag, const Key& key, uint32_t unit,
+__device__ __attribute__((always_inline)) inline int64_t find_slot(const TableDev& t, uint64_t hstem, uint32_t tag, const Key& key, uint32_t unit,
                              bool insert, bool* inserted, uint32_t* err) {
   uint64_t i = hstem >> t.shift;
   int64_t tomb = -1;
   *inserted = false;
   for (uint32_t p = 0; p < t.max_probe; p++, i = (i + 1) & t.mask) {
     Slot* s = &t.slots[i];
-    const uint64_t st = __hip_atomic_load(&s->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (st == tag) {
-      if (slot_key_equal(s, key, t.arena)) return (int64_t)i;
+    const uint32_t st = __hip_atomic_load(&s->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (st == tag) {  // (a 32-bit tag is a filter: the unit and the stem bytes decide)
+      if (s->unit == unit && slot_key_equal(s, key, t.arena)) return (int64_t)i;
       continue;
     }
     if (st == TAG_TOMB) {
@@ -664,17 +663,19 @@ __device__ __attribute__((always_inline)) inline int64_t find_slot(const TableDe
   return SLOT_TABLE_FULL;
 }
 
-// A slot image for probing: the first 64-B sector (tag, length, flags, cur,
-// stem bytes 0..35). Plain loads are enough: within a launch only CAS
-// inserts change tags, and a lane only ever looks for its own stem, which no
-// other lane inserts.
+// A slot image for probing: the whole 64-B slot (tag, length, flags, cur,
+// ring line, stem bytes 0..35). Plain loads are enough: within a launch only
+// CAS inserts change tags, and a lane only ever looks for its own stem, which
+// no other lane inserts.
 struct SlotImg {
-  uint4 v[4];   // first sector
+  uint4 v[4];
   __device__ inline uint32_t dw(uint32_t k) const { return u4w(v[k >> 2], k & 3); }
-  __device__ inline uint64_t tag() const { return ((uint64_t)v[0].y << 32) | v[0].x; }
-  __device__ inline uint32_t key_len() const { return v[0].z & 0xFFFFu; }
-  __device__ inline uint32_t flags() const { return v[0].z >> 24; }
-  __device__ inline Win cur() const { return Win{v[0].w, v[1].x, v[1].y, v[1].z}; }
+  __device__ inline uint32_t tag() const { return v[0].x; }
+  __device__ inline uint32_t key_len() const { return v[0].y & 0xFFFFu; }
+  __device__ inline uint32_t unit() const { return (v[0].y >> 16) & 0xFFu; }
+  __device__ inline uint32_t flags() const { return v[0].y >> 24; }
+  __device__ inline Win cur() const { return Win{v[0].z, v[0].w, v[1].x, v[1].y}; }
+  __device__ inline uint32_t ring() const { return v[1].z; }
 };
 
 __device__ inline void load_img_lo(const Slot* s, SlotImg& im) {
@@ -683,43 +684,77 @@ __device__ inline void load_img_lo(const Slot* s, SlotImg& im) {
   for (int j = 0; j < 4; j++) im.v[j] = p[j];
 }
 
-// Stem of `key` == the slot's stem? Stem bytes beyond the first sector (stems
-// longer than KEY_LO) are read from the slot line directly.
-__device__ inline bool img_key_equal(const Slot* s, const SlotImg& im, const Key& key, const uint8_t* arena) {
+// Stem of `key` == the slot's stem? A stem longer than KEY_IN compares its
+// tail with the arena.
+__device__ inline bool img_key_equal(const SlotImg& im, const Key& key, const uint8_t* arena) {
   if (im.key_len() != key.len) return false;
-  const uint32_t len = key.len, il = len < INLINE_KEY ? len : INLINE_KEY, nw = il >> 2;
+  const uint32_t len = key.len, il = slot_inline(len), nw = il >> 2;
   uint32_t d = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < KEY_LO / 4; k++) {
+  for (uint32_t k = 0; k < KEY_IN / 4; k++) {
     if (k < nw) d |= im.dw(slot_key_dw(k)) ^ key_dw(key, k);
     else if (k == nw && (il & 3)) d |= (im.dw(slot_key_dw(k)) ^ key_dw(key, k)) & tail_mask(il);
   }
-  if (len > KEY_LO) {
-    const uint32_t* sd = reinterpret_cast<const uint32_t*>(s);
-#pragma unroll
-    for (uint32_t k = KEY_LO / 4; k < INLINE_KEY / 4; k++) {
-      if (k < nw) d |= sd[slot_key_dw(k)] ^ key_dw(key, k);
-      else if (k == nw && (il & 3)) d |= (sd[slot_key_dw(k)] ^ key_dw(key, k)) & tail_mask(il);
-    }
-    if (len > INLINE_KEY) d |= arena_diff(arena, s->ext_off, key);
-  }
+  if (len > KEY_IN) d |= arena_diff(arena, im.dw(SLOT_EXT_DW), key);
   return d == 0;
+}
+
+// ---- the ring pool. ring_ctr = {B, taken, n}: lines [0, B) have been handed
+// out from the pool's end, the current free list holds n lines, and `taken`
+// numbers the lines taken since the last sweep: number k is free[k] below n,
+// line B + (k - n) above; RING_NONE past the pool. B and n only change in
+// rl_sweep (k_ring_reset), between batches, so one counter serves both and
+// the active lanes of a wave take their numbers with one atomic.
+__device__ inline uint32_t ring_alloc(const TableDev& t) {
+  const uint64_t act = __ballot(1);
+  const uint32_t lane = __lane_id(), leader = (uint32_t)__ffsll((unsigned long long)act) - 1u;
+  unsigned long long k = 0;
+  if (lane == leader) k = atomicAdd(&t.ring_ctr[1], (unsigned long long)__popcll(act));
+  k = __shfl(k, leader, 64) + (unsigned long long)__popcll(act & ((1ull << lane) - 1ull));
+  const unsigned long long n = t.ring_ctr[2];
+  if (k < n) return t.ring_free[k];
+  const unsigned long long b = t.ring_ctr[0] + (k - n);
+  return b < t.ring_cap ? (uint32_t)b : RING_NONE;
+}
+
+// Slot s's ring line for a write: its own, or a fresh one (every record
+// WS_INVALID, recorded in the slot). Null when the pool is exhausted: the slot
+// is flagged SLOT_LOST (a record below its cur was dropped; a request for
+// such a window is RL_E_TIME from then on).
+__device__ inline Win* ring_for_write(const TableDev& t, Slot* s, uint32_t& ridx) {
+  if (ridx != RING_NONE) return t.ring[ridx].w;
+  const uint32_t k = ring_alloc(t);
+  if (k == RING_NONE) {
+    s->flags |= SLOT_LOST;
+    return nullptr;
+  }
+  uint4* line = reinterpret_cast<uint4*>(&t.ring[k]);
+#pragma unroll
+  for (uint32_t j = 0; j < HIST_W; j++) line[j] = make_uint4(WS_INVALID, 0u, 0u, 0u);
+  s->ring = k;
+  ridx = k;
+  return t.ring[k].w;
+}
+
+// The record at ring position pos of a slot whose line is ridx.
+__device__ inline Win ring_read(const TableDev& t, uint32_t ridx, uint32_t pos) {
+  return ridx == RING_NONE ? Win{WS_INVALID, 0, 0, 0} : t.ring[ridx].w[pos];
 }
 
 // find_slot with insert, returning the slot's image (a fresh slot's image for
 // an insert: no window, no flags). `im` holds the
 // home slot's first sector on entry (the caller issues that load early,
 // beside the stem's).
-__device__ __attribute__((always_inline)) inline int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint64_t tag, const Key& key, uint32_t unit,
+__device__ __attribute__((always_inline)) inline int64_t find_slot_img(const TableDev& t, uint64_t hstem, uint32_t tag, const Key& key, uint32_t unit,
                                  bool* inserted, SlotImg& im, uint32_t* err) {
   uint64_t i = hstem >> t.shift;
   int64_t tomb = -1;
   *inserted = false;
   for (uint32_t p = 0; p < t.max_probe; p++, i = (i + 1) & t.mask) {
     if (p) load_img_lo(&t.slots[i], im);
-    const uint64_t st = im.tag();
-    if (st == tag) {
-      if (img_key_equal(&t.slots[i], im, key, t.arena)) return (int64_t)i;
+    const uint32_t st = im.tag();
+    if (st == tag) {  // (a 32-bit tag is a filter: the unit and the stem bytes decide)
+      if (im.unit() == unit && img_key_equal(im, key, t.arena)) return (int64_t)i;
       continue;
     }
     if (st == TAG_TOMB) {
@@ -737,8 +772,8 @@ __device__ __attribute__((always_inline)) inline int64_t find_slot_img(const Tab
       return SLOT_ARENA_FULL;
     }
     if (at >= 0) {
-      im.v[0] = make_uint4((uint32_t)tag, (uint32_t)(tag >> 32), key.len | (unit << 16), WS_INVALID);
-      im.v[1] = make_uint4(0u, 0u, 0u, 0u);
+      im.v[0] = make_uint4(tag, key.len | (unit << 16), WS_INVALID, 0u);
+      im.v[1] = make_uint4(0u, 0u, RING_NONE, 0u);
       *inserted = true;
       return at;
     }
@@ -883,7 +918,9 @@ __device__ __attribute__((always_inline)) inline void emit(unsigned long long* r
 // the last older window touched), written back when another one is needed.
 struct SimpleState {
   Win cur, old;
-  Win* ring;  // the slot's HIST_W ring records (t.hist)
+  Slot* slot;
+  uint32_t ridx;  // the slot's ring line (RING_NONE: none yet)
+  bool lost;      // SLOT_LOST: a record below cur may have been dropped
   bool cur_dirty, old_dirty;
   uint32_t cur_req;
   bool pend;
@@ -906,13 +943,20 @@ struct SimpleState {
 // moves to the ring with one write, no read), 1 = S.old, the ring record of w
 // (loaded, or started afresh when w was never written), -1 = w is more than
 // HIST_W windows back (RL_E_TIME, never a silently wrong count).
-__device__ __attribute__((always_inline)) inline int simple_pick(SimpleState& S, uint32_t w, uint32_t d) {
+// A ring record back to the slot's line (taken on first need).
+__device__ __attribute__((always_inline)) inline void simple_put(const TableDev& t, SimpleState& S, const Win& r, uint32_t d) {
+  Win* line = ring_for_write(t, S.slot, S.ridx);
+  if (line) line[hist_pos(r.ws, d)] = r;
+  else S.lost = true;
+}
+
+__device__ __attribute__((always_inline)) inline int simple_pick(const TableDev& t, SimpleState& S, uint32_t w, uint32_t d) {
   if (S.cur.ws == w) return 0;
   if (S.cur.ws == WS_INVALID || w > S.cur.ws) {
     if (S.cur.ws != WS_INVALID && hist_reach(S.cur.ws, w, d)) {
       // the cached record goes back first, unless the old cur takes its
       // position (then it is out of the ring's reach from the new cur)
-      if (S.old_dirty && hist_pos(S.old.ws, d) != hist_pos(S.cur.ws, d)) S.ring[hist_pos(S.old.ws, d)] = S.old;
+      if (S.old_dirty && hist_pos(S.old.ws, d) != hist_pos(S.cur.ws, d)) simple_put(t, S, S.old, d);
       S.old = S.cur;
       S.old_dirty = true;
     } else if (S.cur.ws != WS_INVALID) {
@@ -928,22 +972,23 @@ __device__ __attribute__((always_inline)) inline int simple_pick(SimpleState& S,
   }
   if (!hist_reach(w, S.cur.ws, d)) return -1;
   if (S.old.ws != w) {
-    if (S.old_dirty) S.ring[hist_pos(S.old.ws, d)] = S.old;
-    const Win r = S.ring[hist_pos(w, d)];
+    if (S.old_dirty) simple_put(t, S, S.old, d);
+    if (S.lost) return -1;  // (w's record may be one the exhausted pool could not keep)
+    const Win r = ring_read(t, S.ridx, hist_pos(w, d));
     S.old = r.ws == w ? r : Win{w, 0, 0, 0};
     S.old_dirty = false;
   }
   return 1;
 }
 
-__device__ __attribute__((always_inline)) inline void simple_step(const Params& P, unsigned long long* res,
+__device__ __attribute__((always_inline)) inline void simple_step(const TableDev& t, const Params& P, unsigned long long* res,
                                                                   LaneStats& L, StatAcc& acc, SimpleState& S,
                                                                   const Elem& x, bool restore, uint32_t* err) {
   if (x.req != S.cur_req) {
     S.apply_pending();
     S.cur_req = x.req;
   }
-  const int which = simple_pick(S, x.w, x.d);
+  const int which = simple_pick(t, S, x.w, x.d);
   if (which < 0) {  // older than the ring reaches: this descriptor's RL_E_TIME
     if (P.isolate) res[x.e] = pack_fail(RL_E_TIME);
     if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
@@ -988,6 +1033,8 @@ __device__ __attribute__((always_inline)) inline void simple_step(const Params& 
 struct GeneralState {
   int64_t sidx[4];
   Win cur[4];
+  uint32_t ridx[4];  // each unit slot's ring line (RING_NONE: none yet)
+  uint32_t lost;     // bit u-1: that slot is SLOT_LOST (a record below its cur may be gone)
   uint32_t present;  // bit u-1
   uint32_t cur_req;
   uint32_t npend;
@@ -998,15 +1045,17 @@ __device__ inline bool ps_class(const Params& P, uint32_t k) { return P.per_seco
 
 // The record of window w in unit slot k (present): its cur, its ring record,
 // or null when unit k never wrote w. *lost: w may have been written but is
-// out of the ring's reach.
+// out of the ring's reach, or was dropped (SLOT_LOST).
 __device__ inline Win* gen_rec(const TableDev& t, GeneralState& G, uint32_t k, uint32_t w, bool* lost) {
   const uint32_t d = div_of(k + 1);
   Win& c = G.cur[k];
   if (c.ws == w) return &c;
   if (c.ws == WS_INVALID || w > c.ws || w % d) return nullptr;  // (unit k's keys are multiples of its div)
-  Win* r = &t.hist[G.sidx[k]].w[hist_pos(w, d)];
-  if (r->ws == w) return r;
-  if (lost && !hist_reach(w, c.ws, d)) *lost = true;
+  if (G.ridx[k] != RING_NONE) {
+    Win* r = &t.ring[G.ridx[k]].w[hist_pos(w, d)];
+    if (r->ws == w) return r;
+  }
+  if (lost && (!hist_reach(w, c.ws, d) || ((G.lost >> k) & 1))) *lost = true;
   return nullptr;
 }
 
@@ -1060,11 +1109,23 @@ __device__ inline void general_step(const TableDev& t, const Params& P, unsigned
     const uint32_t ex = x.now + x.d;
     Win& c = G.cur[ui];  // this unit's record of w: cur, a roll, or its ring record (in reach: checked above)
     if (c.ws != x.w) {
+      Slot* su = &t.slots[G.sidx[ui]];
       if (c.ws == WS_INVALID || x.w > c.ws) {
-        if (c.ws != WS_INVALID) t.hist[G.sidx[ui]].w[hist_pos(c.ws, x.d)] = c;
+        if (c.ws != WS_INVALID) {  // the old cur to the ring (dropped when the pool is exhausted: SLOT_LOST)
+          Win* line = ring_for_write(t, su, G.ridx[ui]);
+          if (line) line[hist_pos(c.ws, x.d)] = c;
+          else G.lost |= 1u << ui;
+        }
         c = Win{x.w, 0, 0, lcw};
       } else {
-        Win* r = &t.hist[G.sidx[ui]].w[hist_pos(x.w, x.d)];
+        Win* line = ring_for_write(t, su, G.ridx[ui]);
+        if (!line) {  // no room for the older window's record: this descriptor's RL_E_TIME
+          G.lost |= 1u << ui;
+          if (P.isolate) res[x.e] = pack_fail(RL_E_TIME);
+          atomicOr(err, ERR_HISTORY);
+          return;
+        }
+        Win* r = &line[hist_pos(x.w, x.d)];
         if (r->ws != x.w) *r = Win{x.w, 0, 0, lcw};
       }
     }
@@ -1105,25 +1166,28 @@ __device__ __attribute__((always_inline)) inline void replay_simple(SRec rec_s, 
                                                                     unsigned long long* res, const TableDev& t,
                                                                     const Params& P, const uint32_t* grp,
                                                                     uint32_t p, uint32_t end, uint32_t k, int64_t s0,
-                                                                    Win cur0, const Rec& x0, uint32_t e0, LaneStats& L,
+                                                                    Win cur0, uint32_t ring0, uint32_t flags0,
+                                                                    const Rec& x0, uint32_t e0, LaneStats& L,
                                                                     StatAcc& acc, uint32_t* err, bool restore) {
   Slot* s = &t.slots[s0];
   SimpleState S;
   S.cur = cur0;
   S.old = Win{WS_INVALID, 0, 0, 0};  // (never matches a pending window)
-  S.ring = t.hist[s0].w;
+  S.slot = s;
+  S.ridx = ring0;
+  S.lost = (flags0 & SLOT_LOST) != 0;
   S.cur_dirty = S.old_dirty = false;
   S.cur_req = 0xFFFFFFFFu;
   S.pend = false;
-  simple_step(P, res, L, acc, S, load_elem(x0, e0, restore), restore, err);  // element p (always stem k)
+  simple_step(t, P, res, L, acc, S, load_elem(x0, e0, restore), restore, err);  // element p (always stem k)
   for (uint32_t q = p + 1; q < end; q++) {
     if (grp && grp[q] != k) continue;
-    simple_step(P, res, L, acc, S, load_elem(rec_s[q], svals[q], restore), restore, err);
+    simple_step(t, P, res, L, acc, S, load_elem(rec_s[q], svals[q], restore), restore, err);
   }
   S.apply_pending();
   // random writes are the costly part of the probe: store only records that changed
   if (S.cur_dirty) s->cur = S.cur;
-  if (S.old_dirty) S.ring[hist_pos(S.old.ws, div_of(rec_unit(x0)))] = S.old;
+  if (S.old_dirty) simple_put(t, S, S.old, div_of(rec_unit(x0)));
 }
 
 // ===========================================================================
@@ -3314,7 +3378,8 @@ __device__ __attribute__((always_inline)) inline void unique_body(uint32_t blk, 
         if (!ok) t.slots[s0].flags |= SLOT_EXACT;
       }
       if (ok) {
-        replay_simple(SRec{rec, nullptr}, nullptr, res, t, P, nullptr, 0, 1, 0, s0, im.cur(), x, i, L, acc, ferr,
+        replay_simple(SRec{rec, nullptr}, nullptr, res, t, P, nullptr, 0, 1, 0, s0, im.cur(), im.ring(), im.flags(), x, i,
+                      L, acc, ferr,
                       restore);
       } else if (s0 == SLOT_TABLE_FULL || s0 == SLOT_ARENA_FULL) {
         if (P.isolate) res[i] = pack_fail(slot_fail_status(s0));  // else the batch fails
@@ -3410,14 +3475,19 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
   // every unit slot of the stem (created for the units seen here)
   int64_t sidx[4];
   Win c[4];
-  uint32_t present = 0;
+  uint32_t ridx[4];
+  uint32_t present = 0, lost = 0;
   int64_t fail = 0;
   for (uint32_t k = 0; k < 4; k++) {
     bool ins;
     sidx[k] = find_slot(t, hs, slot_tag(hs, k + 1), stem, k + 1, (M >> k) & 1, &ins, ferr);
+    ridx[k] = RING_NONE;
     if (sidx[k] >= 0) {
+      const Slot& su = t.slots[sidx[k]];
       present |= 1u << k;
-      c[k] = t.slots[sidx[k]].cur;
+      c[k] = su.cur;
+      ridx[k] = su.ring;
+      if (su.flags & SLOT_LOST) lost |= 1u << k;
     } else if ((M >> k) & 1) {
       fail = sidx[k];
     }
@@ -3461,10 +3531,10 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
       } else if (c[k].ws == WS_INVALID || w > c[k].ws || w % d) {
         continue;  // (unit k's keys are multiples of its div)
       } else {
-        R = t.hist[sidx[k]].w[hist_pos(w, d)];
+        R = ring_read(t, ridx[k], hist_pos(w, d));
         if (R.ws != w) {
-          // never written, or lost from the ring while it could be live
-          if (!hist_reach(w, c[k].ws, d) && now - w < 2u * d) return true;
+          // never written, or lost from the ring (or dropped, SLOT_LOST) while it could be live
+          if ((!hist_reach(w, c[k].ws, d) || ((lost >> k) & 1)) && now - w < 2u * d) return true;
           continue;
         }
         doomed = wpos[k] != WS_INVALID && wpos[k] != w && hist_pos(wpos[k], d) == hist_pos(w, d);
@@ -3492,6 +3562,16 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
     for (uint32_t k = 0; k < 4; k++)
       if (!F[g] && ((A[g].mask >> k) & 1) && (c[k].ws == WS_INVALID || A[g].w > c[k].ws))
         cn[k] = Win{A[g].w, 0, 0, lcm[g]};
+  // the ring lines the commit writes, taken first: with the pool exhausted the
+  // stem goes to the exact path untouched (which answers RL_E_TIME where a
+  // record cannot be kept)
+  for (uint32_t g = 0; g < G; g++) {
+    if (F[g]) continue;
+    for (uint32_t k = 0; k < 4; k++) {
+      if (!((A[g].mask >> k) & 1) || c[k].ws == A[g].w || c[k].ws == WS_INVALID) continue;
+      if (!ring_for_write(t, &t.slots[sidx[k]], ridx[k])) return true;
+    }
+  }
   // commit: rolls and new ring records
   for (uint32_t g = 0; g < G; g++) {
     if (F[g]) continue;
@@ -3499,10 +3579,10 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
       if (!((A[g].mask >> k) & 1) || c[k].ws == A[g].w) continue;
       const uint32_t d = div_of(k + 1);
       if (c[k].ws == WS_INVALID || A[g].w > c[k].ws) {
-        if (c[k].ws != WS_INVALID) t.hist[sidx[k]].w[hist_pos(c[k].ws, d)] = c[k];
+        if (c[k].ws != WS_INVALID) t.ring[ridx[k]].w[hist_pos(c[k].ws, d)] = c[k];
         t.slots[sidx[k]].cur = cn[k];
       } else {
-        Win* rr = &t.hist[sidx[k]].w[hist_pos(A[g].w, d)];
+        Win* rr = &t.ring[ridx[k]].w[hist_pos(A[g].w, d)];
         if (rr->ws != A[g].w) *rr = Win{A[g].w, 0, 0, lcm[g]};
       }
     }
@@ -3525,7 +3605,7 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
         if (cn[k].ws == w) {
           bits = 1;
         } else if (cn[k].ws != WS_INVALID && w < cn[k].ws && w % d == 0 &&
-                   t.hist[sidx[k]].w[hist_pos(w, d)].ws == w) {
+                   ring_read(t, ridx[k], hist_pos(w, d)).ws == w) {
           bits = 3;
         }
         if (bits && (P.per_second && k == 0) == cls) bits |= 4;
@@ -3637,22 +3717,31 @@ __device__ __attribute__((always_inline)) inline void runs_body(uint32_t blk, Ba
         Slot* s = &t.slots[s0];
         const Elem el0 = load_elem(x0, e0, false);
         const Win cur = im.cur();
-        Win* ring = t.hist[s0].w;
+        uint32_t ridx = im.ring();
         // the record of el0.w: cur, a roll (the old cur moves to the ring), or a ring record
         int which = 0;
         Win R = cur;
         if (cur.ws != el0.w) {
           if (cur.ws == WS_INVALID || el0.w > cur.ws) {
-            // (the old cur goes to the ring only while in its reach from el0.w: simple_pick)
-            if (cur.ws != WS_INVALID && hist_reach(cur.ws, el0.w, el0.d)) ring[hist_pos(cur.ws, el0.d)] = cur;
+            // (the old cur goes to the ring only while in its reach from el0.w: simple_pick;
+            // dropped, SLOT_LOST, when the pool is exhausted)
+            if (cur.ws != WS_INVALID && hist_reach(cur.ws, el0.w, el0.d)) {
+              Win* ring = ring_for_write(t, s, ridx);
+              if (ring) ring[hist_pos(cur.ws, el0.d)] = cur;
+            }
             R = Win{el0.w, 0, 0, 0};
             s->cur = R;
-          } else if (hist_reach(el0.w, cur.ws, el0.d)) {
-            which = 1;
-            R = ring[hist_pos(el0.w, el0.d)];
-            if (R.ws != el0.w) {  // never written: started afresh
-              R = Win{el0.w, 0, 0, 0};
-              ring[hist_pos(el0.w, el0.d)] = R;
+          } else if (hist_reach(el0.w, cur.ws, el0.d) && !(im.flags() & SLOT_LOST)) {
+            Win* ring = ring_for_write(t, s, ridx);
+            if (ring) {
+              which = 1;
+              R = ring[hist_pos(el0.w, el0.d)];
+              if (R.ws != el0.w) {  // never written: started afresh
+                R = Win{el0.w, 0, 0, 0};
+                ring[hist_pos(el0.w, el0.d)] = R;
+              }
+            } else {
+              which = -1;  // (no line for the record: RL_E_TIME)
             }
           } else {
             which = -1;
@@ -3687,7 +3776,8 @@ __device__ __attribute__((always_inline)) inline void runs_body(uint32_t blk, Ba
           c.count += end - p;
           sl->cur = c;
         } else {
-          replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, im.cur(), x0, e0, L, acc, ferr, restore);
+          replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, im.cur(), im.ring(), im.flags(), x0, e0, L, acc,
+                        ferr, restore);
         }
       } else if (s0 == SLOT_TABLE_FULL || s0 == SLOT_ARENA_FULL) {
         if (P.isolate) fail_range(res, svals, p, end, slot_fail_status(s0));  // else the batch fails
@@ -3796,7 +3886,7 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
             const uint32_t bits = (st.x >> (3 * k)) & 7u;
             if (!(bits & 1u)) continue;
             const uint32_t idx = k == 0 ? sl.x : k == 1 ? sl.y : k == 2 ? sl.z : sl.w;
-            Win* R = (bits & 2u) ? &t.hist[idx].w[hist_pos(x.w, div_of(k + 1))] : &t.slots[idx].cur;
+            Win* R = (bits & 2u) ? &t.ring[t.slots[idx].ring].w[hist_pos(x.w, div_of(k + 1))] : &t.slots[idx].cur;
             if (bits & 4u) {  // same store: INCRBY + EXPIRE
               R->count = after;
               R->expire = x.now + x.d;
@@ -3809,7 +3899,7 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
           R.count = after;
           R.expire = x.now + x.d;
           R.lc = (req_f != 0xFFFFFFFFu) ? lc_f : st.z;
-          if (st.w & 2u) t.hist[st.x].w[hist_pos(x.w, x.d)] = R;  // a ring record
+          if (st.w & 2u) t.ring[t.slots[st.x].ring].w[hist_pos(x.w, x.d)] = R;  // a ring record (line taken by k_table)
           else t.slots[st.x].cur = R;
         }
       }
@@ -3843,15 +3933,20 @@ __device__ inline void stem_exact(const TableDev& t, const Params& P, unsigned l
                                   Visit visit) {
   GeneralState G;
   G.present = 0;
+  G.lost = 0;
   G.cur_req = 0xFFFFFFFFu;
   G.npend = 0;
   int64_t fail = 0;
   for (uint32_t u = 1; u <= 4; u++) {
     bool ins;
     G.sidx[u - 1] = find_slot(t, hs, slot_tag(hs, u), stem, u, (um >> (u - 1)) & 1, &ins, ferr);
+    G.ridx[u - 1] = RING_NONE;
     if (G.sidx[u - 1] >= 0) {
+      const Slot& su = t.slots[G.sidx[u - 1]];
       G.present |= 1u << (u - 1);
-      G.cur[u - 1] = t.slots[G.sidx[u - 1]].cur;
+      G.cur[u - 1] = su.cur;
+      G.ridx[u - 1] = su.ring;
+      if (su.flags & SLOT_LOST) G.lost |= 1u << (u - 1);
     } else if ((um >> (u - 1)) & 1) {
       fail = G.sidx[u - 1];
     }
@@ -3990,7 +4085,8 @@ __device__ __attribute__((always_inline)) inline void general_body(uint32_t blk,
         }
       }
       if (simple) {
-        replay_simple(rec_s, svals, res, t, P, grp, q0, end, g, s0, t.slots[s0].cur, y, svals[q0], L, acc, ferr,
+        replay_simple(rec_s, svals, res, t, P, grp, q0, end, g, s0, t.slots[s0].cur, t.slots[s0].ring, t.slots[s0].flags, y,
+                      svals[q0], L, acc, ferr,
                       restore);
         continue;
       }
@@ -4141,15 +4237,16 @@ __global__ __launch_bounds__(256) void k_finish(const unsigned long long* __rest
 
 // Keys in the local over-limit cache at `now` (freecache EntryCount of live
 // entries): window records whose local-cache TTL has not passed.
-__global__ __launch_bounds__(256) void k_lc_count(const Slot* slots, const Hist* hist, uint64_t nslots,
-                                                  uint32_t now, unsigned long long* out) {
+__global__ __launch_bounds__(256) void k_lc_count(const TableDev t, uint64_t nslots, uint32_t now,
+                                                  unsigned long long* out) {
   uint32_t live = 0;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * 256) {
-    const Slot& s = slots[i];
+    const Slot& s = t.slots[i];
     if (s.tag < 2) continue;
     live += s.cur.ws != WS_INVALID && now < s.cur.lc;
+    if (s.ring == RING_NONE) continue;
     for (uint32_t j = 0; j < HIST_W; j++) {
-      const Win& w = hist[i].w[j];
+      const Win& w = t.ring[s.ring].w[j];
       live += w.ws != WS_INVALID && now < w.lc;
     }
   }
@@ -4158,23 +4255,64 @@ __global__ __launch_bounds__(256) void k_lc_count(const Slot* slots, const Hist*
 
 // ===========================================================================
 // Epoch sweep: a slot whose window records are all dead (Redis key past its
-// EXPIRE and local-cache entry past its TTL) becomes a tombstone.
+// EXPIRE and local-cache entry past its TTL) becomes a tombstone, and its
+// ring line joins the free list the next batches take lines from.
 // ===========================================================================
 __device__ inline bool win_alive(const Win& w, uint32_t now) {
   return w.ws != WS_INVALID && (now <= w.expire || now < w.lc);
 }
 
-__global__ __launch_bounds__(256) void k_sweep(Slot* slots, const Hist* hist, uint64_t nslots, uint32_t now,
-                                               unsigned long long* evicted) {
+// The free list's untaken entries move to the front of the new list (one
+// pass; k_ring_reset then restarts the counts and moves B past the lines
+// taken from the pool's end).
+__global__ __launch_bounds__(256) void k_ring_rebase(const uint32_t* __restrict__ from, uint32_t* __restrict__ to,
+                                                     const unsigned long long* ctr) {
+  const unsigned long long take = ctr[1], n = ctr[2];
+  const unsigned long long left = n > take ? n - take : 0ull;
+  for (unsigned long long k = blockIdx.x * 256ull + threadIdx.x; k < left; k += (unsigned long long)gridDim.x * 256)
+    to[k] = from[take + k];
+}
+
+__global__ void k_ring_reset(unsigned long long* ctr, uint64_t cap) {
+  const unsigned long long take = ctr[1], n = ctr[2], b = ctr[0] + (take > n ? take - n : 0ull);
+  ctr[0] = b < cap ? b : cap;
+  ctr[2] = n > take ? n - take : 0ull;
+  ctr[1] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_sweep(TableDev t, uint64_t nslots, uint32_t now, unsigned long long* evicted,
+                                               uint32_t* __restrict__ free_to) {
   uint32_t local = 0;
-  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * 256) {
-    Slot* s = &slots[i];
-    if (s->tag < 2) continue;
-    bool alive = win_alive(s->cur, now);
-    for (uint32_t j = 0; j < HIST_W && !alive; j++) alive = win_alive(hist[i].w[j], now);
-    if (!alive) {
-      s->tag = TAG_TOMB;
-      local++;
+  const uint32_t lane = threadIdx.x & 63u;
+  // (grid-stride with whole waves in the loop: the wave-aggregated append below)
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i0 = blockIdx.x * 256ull; i0 < nslots; i0 += stride) {
+    const uint64_t i = i0 + threadIdx.x;
+    bool evict = false;
+    uint32_t line = RING_NONE;
+    if (i < nslots) {
+      Slot* s = &t.slots[i];
+      if (s->tag >= 2) {
+        line = s->ring;
+        bool alive = win_alive(s->cur, now);
+        if (line != RING_NONE)
+          for (uint32_t j = 0; j < HIST_W && !alive; j++) alive = win_alive(t.ring[line].w[j], now);
+        if (!alive) {
+          s->tag = TAG_TOMB;
+          s->ring = RING_NONE;
+          evict = true;
+          local++;
+        }
+      }
+    }
+    const bool give = evict && line != RING_NONE;
+    const uint64_t m = __ballot(give);
+    if (m) {
+      const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+      unsigned long long base = 0;
+      if (lane == leader) base = atomicAdd(&t.ring_ctr[2], (unsigned long long)__popcll(m));
+      base = __shfl(base, leader, 64);
+      if (give) free_to[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = line;
     }
   }
   if (local) atomicAdd(evicted, (unsigned long long)local);
@@ -4188,26 +4326,32 @@ __global__ __launch_bounds__(256) void k_arena_compact(Slot* slots, uint64_t nsl
                                                        uint8_t* __restrict__ to, unsigned long long* used16) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * 256) {
     Slot* s = &slots[i];
-    if (s->tag < 2 || s->key_len <= INLINE_KEY) continue;
-    const uint32_t n16 = (s->key_len - INLINE_KEY + 15) / 16;
+    if (s->tag < 2 || s->key_len <= KEY_IN) continue;
+    uint32_t* sd = reinterpret_cast<uint32_t*>(s);
+    const uint32_t n16 = (s->key_len - KEY_SPLIT + 15) / 16;
     const unsigned long long off = atomicAdd(used16, (unsigned long long)n16);
-    const uint4* src = reinterpret_cast<const uint4*>(from + (size_t)s->ext_off * 16);
+    const uint4* src = reinterpret_cast<const uint4*>(from + (size_t)sd[SLOT_EXT_DW] * 16);
     uint4* dst = reinterpret_cast<uint4*>(to + off * 16);
     for (uint32_t k = 0; k < n16; k++) dst[k] = src[k];
-    s->ext_off = (uint32_t)off;
+    sd[SLOT_EXT_DW] = (uint32_t)off;
   }
 }
 
 __global__ __launch_bounds__(256) void k_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out) {
-  uint32_t live = 0, tomb = 0, exact = 0;
+  uint32_t live = 0, tomb = 0, exact = 0, lost = 0;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * 256) {
-    const uint64_t tg = slots[i].tag;
+    const uint32_t tg = slots[i].tag;
     if (tg == TAG_TOMB) tomb++;
-    else if (tg >= 2) { live++; if (slots[i].flags & SLOT_EXACT) exact++; }
+    else if (tg >= 2) {
+      live++;
+      exact += (slots[i].flags & SLOT_EXACT) != 0;
+      lost += (slots[i].flags & SLOT_LOST) != 0;
+    }
   }
   if (live) atomicAdd(&out[0], (unsigned long long)live);
   if (tomb) atomicAdd(&out[1], (unsigned long long)tomb);
   if (exact) atomicAdd(&out[2], (unsigned long long)exact);
+  if (lost) atomicAdd(&out[3], (unsigned long long)lost);
 }
 
 // ===========================================================================
@@ -4353,9 +4497,11 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
 }
 
 
-void launch_sweep(Slot* slots, const Hist* hist, uint64_t nslots, uint32_t now, unsigned long long* evicted,
-                  hipStream_t st) {
-  k_sweep<<<2048, 256, 0, st>>>(slots, hist, nslots, now, evicted);
+void launch_sweep(const TableDev& t, uint64_t nslots, uint32_t now, unsigned long long* evicted,
+                  const uint32_t* free_from, uint32_t* free_to, hipStream_t st) {
+  k_ring_rebase<<<1024, 256, 0, st>>>(free_from, free_to, t.ring_ctr);
+  k_ring_reset<<<1, 1, 0, st>>>(t.ring_ctr, t.ring_cap);
+  k_sweep<<<2048, 256, 0, st>>>(t, nslots, now, evicted, free_to);
 }
 
 void launch_arena_compact(Slot* slots, uint64_t nslots, const uint8_t* from, uint8_t* to, unsigned long long* used16,
@@ -4363,9 +4509,8 @@ void launch_arena_compact(Slot* slots, uint64_t nslots, const uint8_t* from, uin
   k_arena_compact<<<2048, 256, 0, st>>>(slots, nslots, from, to, used16);
 }
 
-void launch_lc_count(const Slot* slots, const Hist* hist, uint64_t nslots, uint32_t now, unsigned long long* out,
-                     hipStream_t st) {
-  k_lc_count<<<2048, 256, 0, st>>>(slots, hist, nslots, now, out);
+void launch_lc_count(const TableDev& t, uint64_t nslots, uint32_t now, unsigned long long* out, hipStream_t st) {
+  k_lc_count<<<2048, 256, 0, st>>>(t, nslots, now, out);
 }
 
 void launch_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out, hipStream_t st) {

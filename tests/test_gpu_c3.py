@@ -1,6 +1,6 @@
 """BASELINE configs[3] (C3) at its per-GPU shard on one MI355X: 1B keys over 8
 GPUs is 125M live keys per GPU = 62.5M tenants x {sec, min} in a 2^28-slot
-(34 GB) table. The table is filled through the normal pipeline with batches
+(17 GB of 64-B slots + 8.6 GB of ring lines) table. The table is filled through the normal pipeline with batches
 generated on the GPU, then C1-shaped 1M-descriptor batches run against it.
 
 Checked at full size (size-independent properties): every key is one live slot;
@@ -89,5 +89,7 @@ def test_gpu_c3_shard_125m_live_keys():
         co.close()
         info = be.table_info()
         assert info["live_slots"] == 2 * TENANTS
+        # SECOND keys moved 1-3 windows forward: their old cur went to a ring line
+        assert 0 < info["ring_lines_used"] <= 3 * NQ and info["lost_slots"] == 0
     finally:
         be.close()

@@ -180,3 +180,56 @@ def test_gpu_snapshot_keeps_the_ring():
             assert np.array_equal(g[k], o[k]), k
     be2.close()
     co.close()
+
+
+def test_gpu_ring_pool_exhausted_fails_never_miscounts():
+    """A pool of 64 history lines for 3000 keys moving back and forth: a slot
+    that could not take a line when its cur moved (lost_slots) fails its older
+    windows with RL_E_TIME; every descriptor that succeeds matches the oracle
+    fed only the descriptors that succeeded."""
+    be = Backend(0.8, False, table_slots=1 << 14, max_batch=1 << 14, max_rules=8, ring_lines=64)
+    co = c_oracle.COracle(0.8, False)
+    failed_total = ok_total = 0
+    try:
+        for a, n, nq, nr in _stream(6, 3_000, 4_000, 8, 3, 7):
+            g = be.do_limit_arrays(a, n, nq, nr, isolate=True)
+            failed = g["status"] != 0
+            assert (g["status"][failed] == abi.RL_E_TIME).all(), np.unique(g["status"])
+            keep = ~failed
+            o = co.do_limit(*_drop(a, n, nq, keep), nr)
+            for k in ("code", "limit_remaining", "reset_s"):
+                assert np.array_equal(g[k][keep], o[k]), k
+            failed_total += int(failed.sum())
+            ok_total += int(keep.sum())
+        info = be.table_info()
+        assert info["ring_lines"] == 64 and info["ring_lines_used"] == 64
+        assert info["lost_slots"] > 0 and failed_total > 0 and ok_total > failed_total
+    finally:
+        be.close()
+        co.close()
+
+
+def test_gpu_sweep_returns_ring_lines():
+    """rl_sweep gives a swept slot's line back: a second generation of keys
+    moving back finds the whole pool again, with no failures."""
+    be = Backend(0.8, False, table_slots=1 << 14, max_batch=1 << 14, max_rules=8, ring_lines=1024)
+    try:
+        for gen in range(3):
+            co = c_oracle.COracle(0.8, False)
+            t = W.NOW0 + gen * 100_000
+            for k in range(4):  # 400 keys, each one's cur moves forward then back
+                ten = np.arange(400) + gen * 1000
+                now = np.full(400, t + (3 if k % 2 else 0) + k)
+                b = W.c1_batch(ten, now)
+                g = be.do_limit_arrays(*b, isolate=True)
+                o = co.do_limit(*b)
+                assert (g["status"] == 0).all(), np.unique(g["status"])
+                for f in ("code", "limit_remaining", "reset_s"):
+                    assert np.array_equal(g[f], o[f]), f
+            co.close()
+            info = be.table_info()
+            assert info["lost_slots"] == 0 and 0 < info["ring_lines_used"] <= 1024
+            assert be.sweep(t + 50_000) > 0
+            assert be.table_info()["ring_lines_used"] == 0
+    finally:
+        be.close()
