@@ -39,6 +39,10 @@ constexpr uint32_t TAG_TOMB = 1;
 constexpr uint32_t KEY_IN = 36;               // a stem of at most KEY_IN bytes is stored whole in its slot
 constexpr uint32_t KEY_SPLIT = 32;            // a longer one: bytes [0, KEY_SPLIT) here, the rest in the arena
 constexpr uint32_t RING_NONE = 0xFFFFFFFFu;   // slot without a ring line
+// ring pool counters: one 128-B line per partition (RING_CTR_STRIDE u64s),
+// so concurrent allocations in different partitions never share a word
+constexpr uint32_t RING_CTR_STRIDE = 16;
+constexpr uint32_t RING_PARTS_MAX = 64;
 constexpr uint8_t SLOT_EXACT = 0x1;           // stem has >1 unit slot: exact (serial) path
 constexpr uint8_t SLOT_LOST = 0x2;            // a record below cur was dropped (ring pool exhausted): RL_E_TIME
 constexpr uint32_t HIST_W = 8;                // ring records per slot: windows 1..HIST_W back from cur

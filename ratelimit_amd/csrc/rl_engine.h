@@ -39,6 +39,10 @@ struct HostSlot {
   hipEvent_t out_done = nullptr;  // its outputs are back on the host (the slot is free)
 };
 
+struct RingPart {
+  uint64_t used, left, taken;
+};
+
 struct Engine {
   rl_config cfg;
   hipStream_t stream = nullptr;   // serial work (== pipe[0])
@@ -56,13 +60,13 @@ struct Engine {
   uint64_t nslots = 0;
   // the ring pool (window records below the slots' cur, rl_device.h): lines,
   // the two free lists a sweep alternates between (the current one: ring_cur),
-  // and the counters {B, taken, n} (ring_alloc, rl_kernels.hip)
+  // and per partition the counters {B, taken, n} (ring_alloc, rl_kernels.hip)
   Hist* ring = nullptr;
   uint64_t ring_cap = 0;
   uint32_t* ring_free[2] = {};
   uint32_t ring_cur = 0;
   unsigned long long* ring_ctr = nullptr;
-  uint64_t snap_free_from = 0;  // (snapshot: the first untaken free-list entry)
+  uint32_t ring_parts = 1, ring_part_lines = 0;  // ring_cap = ring_parts x ring_part_lines
   uint8_t* arena = nullptr;
   uint8_t* arena2 = nullptr;  // compaction target (rl_sweep), swapped with arena
   uint64_t arena_cap16 = 0;

@@ -193,13 +193,33 @@ BatchDev dev_view(const Engine* c, const rl_batch* in, uint32_t stem_cap) {
   return b;
 }
 
+// The ring pool's counters per partition, normalised as k_ring_reset would
+// leave them: `used` lines handed out from the partition's end, `left` free-list
+// entries not taken yet (they start at `taken`). Between batches.
+hipError_t ring_parts_get(Engine* c, std::vector<RingPart>& parts) {
+  std::vector<unsigned long long> ctr((size_t)c->ring_parts * RING_CTR_STRIDE);
+  hipError_t e = hipMemcpyAsync(ctr.data(), c->ring_ctr, ctr.size() * 8, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) return e;
+  parts.assign(c->ring_parts, RingPart{});
+  for (uint32_t k = 0; k < c->ring_parts; k++) {
+    const unsigned long long* r = &ctr[(size_t)k * RING_CTR_STRIDE];
+    const uint64_t b = r[0], taken = r[1], n = r[2];
+    parts[k].used = std::min<uint64_t>(b + (taken > n ? taken - n : 0), c->ring_part_lines);
+    parts[k].left = n > taken ? n - taken : 0;
+    parts[k].taken = n > taken ? taken : 0;
+  }
+  return hipSuccess;
+}
+
 TableDev table_view(Engine* c) {
   TableDev t;
   t.slots = c->slots;
   t.ring = c->ring;
   t.ring_free = c->ring_free[c->ring_cur];
   t.ring_ctr = c->ring_ctr;
-  t.ring_cap = (uint32_t)c->ring_cap;
+  t.ring_parts = c->ring_parts;
+  t.ring_part_lines = c->ring_part_lines;
   t.mask = c->nslots - 1;
   t.arena = c->arena;
   t.arena_used16 = c->s[0].counters + 4;
@@ -325,7 +345,10 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   c->cfg.hash_seed = c->hash_seed;
   c->hk = hash_key_of(c->hash_seed, cfg.debug_hash_bits);
   c->nslots = cfg.table_slots;
-  c->ring_cap = cfg.ring_lines;
+  c->ring_parts = cfg.ring_lines >= 64ull * 1024 ? RING_PARTS_MAX : 1u;  // (rl_kernels.hip, ring_alloc)
+  c->ring_part_lines = (uint32_t)(cfg.ring_lines / c->ring_parts);
+  c->ring_cap = (uint64_t)c->ring_parts * c->ring_part_lines;
+  c->cfg.ring_lines = c->ring_cap;
   c->arena_cap16 = cfg.arena_bytes / 16;
   const uint32_t n = cfg.max_batch;
   bool ok = true;
@@ -337,7 +360,7 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
     ok = ok && hipEventCreateWithFlags(&c->done_ring[k], hipEventDisableTiming) == hipSuccess;
   ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess && dalloc(&c->ring, c->ring_cap) == hipSuccess &&
        dalloc(&c->ring_free[0], c->ring_cap) == hipSuccess && dalloc(&c->ring_free[1], c->ring_cap) == hipSuccess &&
-       dalloc(&c->ring_ctr, 4) == hipSuccess;
+       dalloc(&c->ring_ctr, (size_t)RING_PARTS_MAX * RING_CTR_STRIDE) == hipSuccess;
   ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess && dalloc(&c->arena2, cfg.arena_bytes) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++) ok = ok && alloc_buffer(c->s[k], n);
   Scratch& s0 = c->s[0];
@@ -374,7 +397,8 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && hipHostMalloc((void**)&c->h_counters, 8 * sizeof(unsigned long long)) == hipSuccess;
   if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
   ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
-       hipMemsetAsync(c->ring_ctr, 0, 32, c->stream) == hipSuccess &&  // (lines are initialised when taken)
+       hipMemsetAsync(c->ring_ctr, 0, (size_t)RING_PARTS_MAX * RING_CTR_STRIDE * 8, c->stream) == hipSuccess &&
+       // (lines are initialised when taken)
        hipMemsetAsync(c->errw, 0, (NBUF + 3) * 4, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.time_floor, 0, 8, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.counters, 0, 64, c->stream) == hipSuccess &&
@@ -1020,12 +1044,11 @@ int eng_table_info_get(Engine* c, rl_table_info* info) {
   launch_table_info(c->slots, c->nslots, c->s[0].counters, c->stream);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 40, hipMemcpyDeviceToHost, c->stream));
-  unsigned long long rc[3];
-  HIPCHK(c, hipMemcpyAsync(rc, c->ring_ctr, 24, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::vector<RingPart> parts;
+  HIPCHK(c, ring_parts_get(c, parts));
   info->ring_lines = c->ring_cap;
-  info->ring_lines_used = std::min<uint64_t>(rc[0] + (rc[1] > rc[2] ? rc[1] - rc[2] : 0), c->ring_cap) -
-                          (rc[2] > rc[1] ? rc[2] - rc[1] : 0);  // (ring_alloc's counters)
+  info->ring_lines_used = 0;
+  for (const RingPart& r : parts) info->ring_lines_used += r.used - r.left;
   info->lost_slots = c->h_counters[3];
   info->table_slots = c->nslots;
   info->live_slots = c->h_counters[0];
@@ -1378,66 +1401,82 @@ int eng_local_cache_info_get(Engine* c, int64_t now, rl_local_cache_info* info) 
 }
 
 namespace {
-constexpr uint64_t SNAP_MAGIC = 0x34304150414e534cull;  // "LSNAPA04" (64-B slots, ring pool)
+constexpr uint64_t SNAP_MAGIC = 0x34304150414e534cull;  // "LSNAPA04" (64-B slots, partitioned ring pool)
 struct SnapHeader {
   uint64_t magic, nslots, arena_used16, hash_seed;  // slots are placed by the keyed hash: restore adopts its key
   int64_t time_floor;
-  uint64_t ring_used;   // ring lines handed out from the pool's end (saved whole)
-  uint64_t free_left;   // the free list's untaken entries (saved, restored at its front)
+  uint64_t ring_lines;  // ring_parts x ring_part_lines: slots hold line indices, so restore needs the same pool
+  uint32_t ring_parts, ring_part_lines;
   uint64_t reserved;
 };
 static_assert(sizeof(SnapHeader) == 64, "snapshot header");
+// then: the slots; RingPart {used, left} per partition; per partition its
+// lines [p L, p L + used); per partition its free list's `left` entries;
+// the used arena
 
-int snap_state(Engine* c, SnapHeader* h) {
+int snap_state(Engine* c, SnapHeader* h, std::vector<RingPart>& parts) {
   HIPCHK(c, hipSetDevice(c->cfg.device));
   HIPCHK(c, after_batches(c, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 64, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(&h->time_floor, c->s[0].time_floor, 8, hipMemcpyDeviceToHost, c->stream));
-  unsigned long long rc[3];
-  HIPCHK(c, hipMemcpyAsync(rc, c->ring_ctr, 24, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, ring_parts_get(c, parts));
   h->arena_used16 = std::min<uint64_t>(c->h_counters[4], c->arena_cap16);
-  h->ring_used = std::min<uint64_t>(rc[0] + (rc[1] > rc[2] ? rc[1] - rc[2] : 0), c->ring_cap);  // (ring_alloc)
-  h->free_left = rc[2] > rc[1] ? rc[2] - rc[1] : 0;
-  c->snap_free_from = rc[2] > rc[1] ? rc[1] : 0;
+  h->ring_lines = c->ring_cap;
+  h->ring_parts = c->ring_parts;
+  h->ring_part_lines = c->ring_part_lines;
   return RL_OK;
 }
 
-uint64_t snap_bytes(const Engine* c, const SnapHeader& h) {
-  return sizeof(SnapHeader) + c->nslots * sizeof(Slot) + h.ring_used * sizeof(Hist) + h.free_left * 4 +
-         h.arena_used16 * 16;
+uint64_t snap_bytes(const Engine* c, const SnapHeader& h, const std::vector<RingPart>& parts) {
+  uint64_t b = sizeof(SnapHeader) + c->nslots * sizeof(Slot) + parts.size() * 16 + h.arena_used16 * 16;
+  for (const RingPart& r : parts) b += r.used * sizeof(Hist) + r.left * 4;
+  return b;
 }
 }  // namespace
 
 int eng_snapshot_size(Engine* c, uint64_t* bytes) {
   if (!c || !bytes) return set_err(c, RL_E_INVALID, "gpu: null argument");
   SnapHeader h{};
-  int rc = snap_state(c, &h);
+  std::vector<RingPart> parts;
+  int rc = snap_state(c, &h, parts);
   if (rc) return rc;
-  *bytes = snap_bytes(c, h);
+  *bytes = snap_bytes(c, h, parts);
   return RL_OK;
 }
 
 int eng_snapshot_save(Engine* c, void* host, uint64_t bytes) {
   if (!c || !host) return set_err(c, RL_E_INVALID, "gpu: null argument");
   SnapHeader h{};
-  int rc = snap_state(c, &h);
+  std::vector<RingPart> parts;
+  int rc = snap_state(c, &h, parts);
   if (rc) return rc;
   h.magic = SNAP_MAGIC;
   h.nslots = c->nslots;
   h.hash_seed = c->hash_seed;
-  if (bytes < snap_bytes(c, h)) return set_err(c, RL_E_CAPACITY, "gpu: snapshot buffer smaller than rl_snapshot_size");
+  if (bytes < snap_bytes(c, h, parts))
+    return set_err(c, RL_E_CAPACITY, "gpu: snapshot buffer smaller than rl_snapshot_size");
   uint8_t* p = (uint8_t*)host;
   memcpy(p, &h, sizeof h);
   p += sizeof h;
-  const uint64_t tb = c->nslots * sizeof(Slot), rb = h.ring_used * sizeof(Hist);
+  const uint64_t tb = c->nslots * sizeof(Slot), L = c->ring_part_lines;
   HIPCHK(c, hipMemcpy(p, c->slots, tb, hipMemcpyDeviceToHost));
   p += tb;
-  if (rb) HIPCHK(c, hipMemcpy(p, c->ring, rb, hipMemcpyDeviceToHost));
-  p += rb;
-  if (h.free_left)
-    HIPCHK(c, hipMemcpy(p, c->ring_free[c->ring_cur] + c->snap_free_from, h.free_left * 4, hipMemcpyDeviceToHost));
-  p += h.free_left * 4;
+  for (const RingPart& r : parts) {
+    const uint64_t ul[2] = {r.used, r.left};
+    memcpy(p, ul, 16);
+    p += 16;
+  }
+  for (uint32_t k = 0; k < parts.size(); k++) {
+    if (parts[k].used) HIPCHK(c, hipMemcpy(p, c->ring + k * L, parts[k].used * sizeof(Hist), hipMemcpyDeviceToHost));
+    p += parts[k].used * sizeof(Hist);
+  }
+  for (uint32_t k = 0; k < parts.size(); k++) {
+    if (parts[k].left)
+      HIPCHK(c, hipMemcpy(p, c->ring_free[c->ring_cur] + k * L + parts[k].taken, parts[k].left * 4,
+                          hipMemcpyDeviceToHost));
+    p += parts[k].left * 4;
+  }
   if (h.arena_used16) HIPCHK(c, hipMemcpy(p, c->arena, h.arena_used16 * 16, hipMemcpyDeviceToHost));
   return RL_OK;
 }
@@ -1450,22 +1489,37 @@ int eng_snapshot_load(Engine* c, const void* host, uint64_t bytes) {
   if (h.magic != SNAP_MAGIC) return set_err(c, RL_E_INVALID, "gpu: not a table snapshot");
   if (h.nslots != c->nslots) return set_err(c, RL_E_INVALID, "gpu: snapshot table_slots differ from this ctx");
   if (h.arena_used16 > c->arena_cap16) return set_err(c, RL_E_INVALID, "gpu: snapshot arena larger than this ctx's");
-  if (h.ring_used > c->ring_cap || h.free_left > c->ring_cap)
-    return set_err(c, RL_E_INVALID, "gpu: snapshot ring pool larger than this ctx's ring_lines");
-  if (bytes < snap_bytes(c, h)) return set_err(c, RL_E_INVALID, "gpu: snapshot truncated");
+  if (h.ring_parts != c->ring_parts || h.ring_part_lines != c->ring_part_lines)
+    return set_err(c, RL_E_INVALID, "gpu: snapshot ring_lines differ from this ctx");
+  const uint8_t* p = (const uint8_t*)host + sizeof h;
+  const uint64_t tb = h.nslots * sizeof(Slot), L = c->ring_part_lines;
+  if (bytes < sizeof h + tb + h.ring_parts * 16ull) return set_err(c, RL_E_INVALID, "gpu: snapshot truncated");
+  std::vector<RingPart> parts(h.ring_parts);
+  for (uint32_t k = 0; k < h.ring_parts; k++) {
+    uint64_t ul[2];
+    memcpy(ul, p + tb + 16ull * k, 16);
+    if (ul[0] > L || ul[1] > L) return set_err(c, RL_E_INVALID, "gpu: snapshot ring partition out of range");
+    parts[k].used = ul[0];
+    parts[k].left = ul[1];
+  }
+  if (bytes < snap_bytes(c, h, parts)) return set_err(c, RL_E_INVALID, "gpu: snapshot truncated");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   HIPCHK(c, after_batches(c, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  const uint8_t* p = (const uint8_t*)host + sizeof h;
-  const uint64_t tb = h.nslots * sizeof(Slot), rb = h.ring_used * sizeof(Hist);
   HIPCHK(c, hipMemcpy(c->slots, p, tb, hipMemcpyHostToDevice));
-  p += tb;
-  if (rb) HIPCHK(c, hipMemcpy(c->ring, p, rb, hipMemcpyHostToDevice));
-  p += rb;
-  if (h.free_left) HIPCHK(c, hipMemcpy(c->ring_free[c->ring_cur], p, h.free_left * 4, hipMemcpyHostToDevice));
-  p += h.free_left * 4;
-  const unsigned long long rc[3] = {h.ring_used, 0ull, h.free_left};
-  HIPCHK(c, hipMemcpy(c->ring_ctr, rc, 24, hipMemcpyHostToDevice));
+  p += tb + h.ring_parts * 16ull;
+  for (uint32_t k = 0; k < h.ring_parts; k++) {
+    if (parts[k].used) HIPCHK(c, hipMemcpy(c->ring + k * L, p, parts[k].used * sizeof(Hist), hipMemcpyHostToDevice));
+    p += parts[k].used * sizeof(Hist);
+  }
+  std::vector<unsigned long long> ctr((size_t)RING_PARTS_MAX * RING_CTR_STRIDE, 0ull);
+  for (uint32_t k = 0; k < h.ring_parts; k++) {
+    if (parts[k].left) HIPCHK(c, hipMemcpy(c->ring_free[c->ring_cur] + k * L, p, parts[k].left * 4, hipMemcpyHostToDevice));
+    p += parts[k].left * 4;
+    ctr[(size_t)k * RING_CTR_STRIDE + 0] = parts[k].used;
+    ctr[(size_t)k * RING_CTR_STRIDE + 2] = parts[k].left;
+  }
+  HIPCHK(c, hipMemcpy(c->ring_ctr, ctr.data(), ctr.size() * 8, hipMemcpyHostToDevice));
   if (h.arena_used16) HIPCHK(c, hipMemcpy(c->arena, p, h.arena_used16 * 16, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->s[0].counters + 4, &h.arena_used16, 8, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->s[0].time_floor, &h.time_floor, 8, hipMemcpyHostToDevice));

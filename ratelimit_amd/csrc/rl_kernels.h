@@ -129,9 +129,11 @@ struct TableDev {
   // the ring pool: lines handed to slots on first need (Slot::ring); the last
   // sweep's freed lines are taken first, then the pool's untouched end
   Hist* ring;
-  const uint32_t* ring_free;     // [ring_cap] lines freed by the last sweep
-  unsigned long long* ring_ctr;  // {B, taken, n}: lines handed out from the end, numbers taken, free lines (ring_alloc)
-  uint32_t ring_cap;
+  // the pool in ring_parts partitions of ring_part_lines lines, each with its
+  // own counters (RING_CTR_STRIDE apart) and its own segment of the free list
+  const uint32_t* ring_free;     // [ring_parts * ring_part_lines] lines freed by the last sweep
+  unsigned long long* ring_ctr;  // per partition {B, taken, n} (ring_alloc)
+  uint32_t ring_parts, ring_part_lines;
   uint64_t mask;
   uint8_t* arena;
   unsigned long long* arena_used16;

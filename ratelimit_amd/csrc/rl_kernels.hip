@@ -699,22 +699,36 @@ __device__ inline bool img_key_equal(const SlotImg& im, const Key& key, const ui
   return d == 0;
 }
 
-// ---- the ring pool. ring_ctr = {B, taken, n}: lines [0, B) have been handed
-// out from the pool's end, the current free list holds n lines, and `taken`
-// numbers the lines taken since the last sweep: number k is free[k] below n,
-// line B + (k - n) above; RING_NONE past the pool. B and n only change in
-// rl_sweep (k_ring_reset), between batches, so one counter serves both and
-// the active lanes of a wave take their numbers with one atomic.
+// ---- the ring pool, in ring_parts partitions of L = ring_part_lines lines.
+// Partition p's counters {B, taken, n}: lines [0, B) of the partition have
+// been handed out from its end, its free-list segment holds n lines, and
+// `taken` numbers the lines taken since the last sweep: number k is
+// free[p L + k] below n, line p L + B + (k - n) above, none past L. B and n
+// only change in rl_sweep (k_ring_reset), between batches, so one counter
+// serves both; the active lanes of a wave take their numbers with one atomic,
+// and waves start at partitions spread by workgroup and wave, so a burst of
+// first window moves (every key revisited within 8 windows takes a line once)
+// does not serialise on one word. An exhausted partition sends the lanes on
+// to the next; RING_NONE once every partition is.
 __device__ inline uint32_t ring_alloc(const TableDev& t) {
-  const uint64_t act = __ballot(1);
-  const uint32_t lane = __lane_id(), leader = (uint32_t)__ffsll((unsigned long long)act) - 1u;
-  unsigned long long k = 0;
-  if (lane == leader) k = atomicAdd(&t.ring_ctr[1], (unsigned long long)__popcll(act));
-  k = __shfl(k, leader, 64) + (unsigned long long)__popcll(act & ((1ull << lane) - 1ull));
-  const unsigned long long n = t.ring_ctr[2];
-  if (k < n) return t.ring_free[k];
-  const unsigned long long b = t.ring_ctr[0] + (k - n);
-  return b < t.ring_cap ? (uint32_t)b : RING_NONE;
+  const uint32_t P = t.ring_parts, L = t.ring_part_lines, lane = __lane_id();
+  uint32_t p = (blockIdx.x * 4u + (threadIdx.x >> 6)) & (P - 1u);
+  for (uint32_t tries = 0; tries < P; tries++, p = (p + 1u) & (P - 1u)) {
+    unsigned long long* ctr = t.ring_ctr + (size_t)p * RING_CTR_STRIDE;
+    // (an exhausted partition: skip it without an atomic; a stale read only costs one)
+    if (tries && __hip_atomic_load(&ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ctr[2] + L - ctr[0])
+      continue;
+    const uint64_t act = __ballot(1);
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)act) - 1u;
+    unsigned long long k = 0;
+    if (lane == leader) k = atomicAdd(&ctr[1], (unsigned long long)__popcll(act));
+    k = __shfl(k, leader, 64) + (unsigned long long)__popcll(act & ((1ull << lane) - 1ull));
+    const unsigned long long n = ctr[2];
+    if (k < n) return t.ring_free[(size_t)p * L + k];
+    const unsigned long long b = ctr[0] + (k - n);
+    if (b < L) return p * L + (uint32_t)b;
+  }
+  return RING_NONE;
 }
 
 // Slot s's ring line for a write: its own, or a fresh one (every record
@@ -4262,57 +4276,47 @@ __device__ inline bool win_alive(const Win& w, uint32_t now) {
   return w.ws != WS_INVALID && (now <= w.expire || now < w.lc);
 }
 
-// The free list's untaken entries move to the front of the new list (one
-// pass; k_ring_reset then restarts the counts and moves B past the lines
-// taken from the pool's end).
+// Per partition (blockIdx.y): the free-list segment's untaken entries move to
+// the front of the new list's segment (one pass; k_ring_reset then restarts
+// the counts and moves B past the lines taken from the partition's end).
 __global__ __launch_bounds__(256) void k_ring_rebase(const uint32_t* __restrict__ from, uint32_t* __restrict__ to,
-                                                     const unsigned long long* ctr) {
-  const unsigned long long take = ctr[1], n = ctr[2];
+                                                     const unsigned long long* ctr, uint32_t L) {
+  const unsigned long long* c = ctr + (size_t)blockIdx.y * RING_CTR_STRIDE;
+  const unsigned long long take = c[1], n = c[2];
   const unsigned long long left = n > take ? n - take : 0ull;
+  const size_t base = (size_t)blockIdx.y * L;
   for (unsigned long long k = blockIdx.x * 256ull + threadIdx.x; k < left; k += (unsigned long long)gridDim.x * 256)
-    to[k] = from[take + k];
+    to[base + k] = from[base + take + k];
 }
 
-__global__ void k_ring_reset(unsigned long long* ctr, uint64_t cap) {
-  const unsigned long long take = ctr[1], n = ctr[2], b = ctr[0] + (take > n ? take - n : 0ull);
-  ctr[0] = b < cap ? b : cap;
-  ctr[2] = n > take ? n - take : 0ull;
-  ctr[1] = 0;
+__global__ void k_ring_reset(unsigned long long* ctr, uint32_t P, uint32_t L) {
+  const uint32_t p = threadIdx.x;
+  if (p >= P) return;
+  unsigned long long* c = ctr + (size_t)p * RING_CTR_STRIDE;
+  const unsigned long long take = c[1], n = c[2], b = c[0] + (take > n ? take - n : 0ull);
+  c[0] = b < L ? b : L;
+  c[2] = n > take ? n - take : 0ull;
+  c[1] = 0;
 }
 
 __global__ __launch_bounds__(256) void k_sweep(TableDev t, uint64_t nslots, uint32_t now, unsigned long long* evicted,
                                                uint32_t* __restrict__ free_to) {
   uint32_t local = 0;
-  const uint32_t lane = threadIdx.x & 63u;
-  // (grid-stride with whole waves in the loop: the wave-aggregated append below)
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t i0 = blockIdx.x * 256ull; i0 < nslots; i0 += stride) {
-    const uint64_t i = i0 + threadIdx.x;
-    bool evict = false;
-    uint32_t line = RING_NONE;
-    if (i < nslots) {
-      Slot* s = &t.slots[i];
-      if (s->tag >= 2) {
-        line = s->ring;
-        bool alive = win_alive(s->cur, now);
-        if (line != RING_NONE)
-          for (uint32_t j = 0; j < HIST_W && !alive; j++) alive = win_alive(t.ring[line].w[j], now);
-        if (!alive) {
-          s->tag = TAG_TOMB;
-          s->ring = RING_NONE;
-          evict = true;
-          local++;
-        }
-      }
-    }
-    const bool give = evict && line != RING_NONE;
-    const uint64_t m = __ballot(give);
-    if (m) {
-      const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-      unsigned long long base = 0;
-      if (lane == leader) base = atomicAdd(&t.ring_ctr[2], (unsigned long long)__popcll(m));
-      base = __shfl(base, leader, 64);
-      if (give) free_to[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = line;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * 256) {
+    Slot* s = &t.slots[i];
+    if (s->tag < 2) continue;
+    const uint32_t line = s->ring;
+    bool alive = win_alive(s->cur, now);
+    if (line != RING_NONE)
+      for (uint32_t j = 0; j < HIST_W && !alive; j++) alive = win_alive(t.ring[line].w[j], now);
+    if (alive) continue;
+    s->tag = TAG_TOMB;
+    s->ring = RING_NONE;
+    local++;
+    if (line != RING_NONE) {  // back on its partition's segment of the new list
+      const uint32_t p = line / t.ring_part_lines;
+      const unsigned long long k = atomicAdd(&t.ring_ctr[(size_t)p * RING_CTR_STRIDE + 2], 1ull);
+      free_to[(size_t)p * t.ring_part_lines + k] = line;
     }
   }
   if (local) atomicAdd(evicted, (unsigned long long)local);
@@ -4499,8 +4503,8 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
 
 void launch_sweep(const TableDev& t, uint64_t nslots, uint32_t now, unsigned long long* evicted,
                   const uint32_t* free_from, uint32_t* free_to, hipStream_t st) {
-  k_ring_rebase<<<1024, 256, 0, st>>>(free_from, free_to, t.ring_ctr);
-  k_ring_reset<<<1, 1, 0, st>>>(t.ring_ctr, t.ring_cap);
+  k_ring_rebase<<<dim3(64, t.ring_parts), 256, 0, st>>>(free_from, free_to, t.ring_ctr, t.ring_part_lines);
+  k_ring_reset<<<1, RING_PARTS_MAX, 0, st>>>(t.ring_ctr, t.ring_parts, t.ring_part_lines);
   k_sweep<<<2048, 256, 0, st>>>(t, nslots, now, evicted, free_to);
 }
 

@@ -160,18 +160,20 @@ def test_gpu_beyond_the_ring_fails_alone():
     co.close()
 
 
-def test_gpu_snapshot_keeps_the_ring():
+@pytest.mark.parametrize("ring_lines", [0, 1 << 16])
+def test_gpu_snapshot_keeps_the_ring(ring_lines):
     """rl_snapshot_save/load carry the ring: a restored ctx answers older
-    windows exactly like the one it was taken from."""
+    windows exactly like the one it was taken from (one pool partition, and
+    64 partitions)."""
     bs = _stream(5, 500, 1_000, 6, 3, 7)
-    be = Backend(0.8, True, table_slots=1 << 14, max_batch=1 << 12, max_rules=8)
+    be = Backend(0.8, True, table_slots=1 << 14, max_batch=1 << 12, max_rules=8, ring_lines=ring_lines)
     co = c_oracle.COracle(0.8, True)
     for a, n, nq, nr in bs[:4]:
         be.do_limit_arrays(a, n, nq, nr)
         co.do_limit(a, n, nq, nr)
     snap = be.snapshot()
     be.close()
-    be2 = Backend(0.8, True, table_slots=1 << 14, max_batch=1 << 12, max_rules=8)
+    be2 = Backend(0.8, True, table_slots=1 << 14, max_batch=1 << 12, max_rules=8, ring_lines=ring_lines)
     be2.load_snapshot(snap)
     for a, n, nq, nr in bs[4:]:
         g = be2.do_limit_arrays(a, n, nq, nr)
@@ -182,16 +184,18 @@ def test_gpu_snapshot_keeps_the_ring():
     co.close()
 
 
-def test_gpu_ring_pool_exhausted_fails_never_miscounts():
-    """A pool of 64 history lines for 3000 keys moving back and forth: a slot
+@pytest.mark.parametrize("ring_lines,tenants,nq", [(64, 3_000, 4_000), (1 << 16, 100_000, 150_000)])
+def test_gpu_ring_pool_exhausted_fails_never_miscounts(ring_lines, tenants, nq):
+    """A pool too small for the keys moving back and forth (one partition of
+    64 lines; 64 partitions of 1024, exhausted one after another): a slot
     that could not take a line when its cur moved (lost_slots) fails its older
     windows with RL_E_TIME; every descriptor that succeeds matches the oracle
     fed only the descriptors that succeeded."""
-    be = Backend(0.8, False, table_slots=1 << 14, max_batch=1 << 14, max_rules=8, ring_lines=64)
+    be = Backend(0.8, False, table_slots=1 << 19, max_batch=1 << 19, max_rules=8, ring_lines=ring_lines)
     co = c_oracle.COracle(0.8, False)
     failed_total = ok_total = 0
     try:
-        for a, n, nq, nr in _stream(6, 3_000, 4_000, 8, 3, 7):
+        for a, n, nq, nr in _stream(6, tenants, nq, 8, 3, 7):
             g = be.do_limit_arrays(a, n, nq, nr, isolate=True)
             failed = g["status"] != 0
             assert (g["status"][failed] == abi.RL_E_TIME).all(), np.unique(g["status"])
@@ -202,17 +206,19 @@ def test_gpu_ring_pool_exhausted_fails_never_miscounts():
             failed_total += int(failed.sum())
             ok_total += int(keep.sum())
         info = be.table_info()
-        assert info["ring_lines"] == 64 and info["ring_lines_used"] == 64
+        assert info["ring_lines"] == ring_lines and info["ring_lines_used"] == ring_lines
         assert info["lost_slots"] > 0 and failed_total > 0 and ok_total > failed_total
     finally:
         be.close()
         co.close()
 
 
-def test_gpu_sweep_returns_ring_lines():
-    """rl_sweep gives a swept slot's line back: a second generation of keys
-    moving back finds the whole pool again, with no failures."""
-    be = Backend(0.8, False, table_slots=1 << 14, max_batch=1 << 14, max_rules=8, ring_lines=1024)
+@pytest.mark.parametrize("ring_lines", [1024, 1 << 16])
+def test_gpu_sweep_returns_ring_lines(ring_lines):
+    """rl_sweep gives a swept slot's line back to its partition: a second and
+    third generation of keys moving back find the whole pool again, with no
+    failures."""
+    be = Backend(0.8, False, table_slots=1 << 14, max_batch=1 << 14, max_rules=8, ring_lines=ring_lines)
     try:
         for gen in range(3):
             co = c_oracle.COracle(0.8, False)

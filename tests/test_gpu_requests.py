@@ -237,7 +237,7 @@ def test_gpu_requests_errors():
 def test_gpu_request_long_entries_take_global_paths():
     """Entry bytes beyond a workgroup's LDS staging (16 KB) and stems beyond its
     assembly buffer (24 KB) take the global-memory paths of k_match /
-    k_match_emit; stems > 80 B also go through the table's overflow arena."""
+    k_match_emit; stems > 36 B also go through the table's overflow arena."""
     rng = random.Random(99)
     reqs, nows = [], []
     vals = ["v" + "x_" * rng.randint(40, 150) + str(i) for i in range(40)]

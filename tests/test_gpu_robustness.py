@@ -261,7 +261,7 @@ def test_gpu_cache_isolates_failed_calls():
 
 # --------------------------------------------------------------------------- arena and fast-path blocks
 def test_gpu_arena_reclaimed_by_sweep():
-    """stems longer than 80 B take arena space; the sweep's
+    """stems longer than 36 B take arena space (bytes 32 on); the sweep's
     compaction must return it, so inserting, sweeping and re-inserting far more
     long stems than the arena holds never fails."""
     from oracle import oracle as O
@@ -269,7 +269,7 @@ def test_gpu_arena_reclaimed_by_sweep():
     reg = {"r": O.RateLimitStats("r")}
     cache_prefix = "x" * 150
     t = 1_700_000_000
-    for rnd in range(8):  # 8 x 400 stems x 5 units of 16 B = 4x the 64 KiB arena
+    for rnd in range(8):  # 8 x 400 stems x 8 units of 16 B = 6x the 64 KiB arena
         calls = [(O.RateLimitRequest(cache_prefix, [O.Descriptor([("k", "r%d_%d" % (rnd, i))])], 1),
                   [O.RateLimit("r", reg["r"], O.Limit(5, O.SECOND))], t) for i in range(400)]
         from ratelimit_amd.packing import RuleInterner, pack_calls
@@ -277,7 +277,7 @@ def test_gpu_arena_reclaimed_by_sweep():
         g = be.do_limit_packed(pb)
         assert (g["limit_remaining"] == 4).all()
         lens = np.diff(pb.arrays["stem_off"].astype(np.int64))
-        assert be.table_info()["arena_bytes_used"] == int(((lens - 80 + 15) // 16 * 16).sum())
+        assert be.table_info()["arena_bytes_used"] == int(((lens - 32 + 15) // 16 * 16).sum())
         t += 5
         assert be.sweep(t) == 400
         assert be.table_info()["arena_bytes_used"] == 0
