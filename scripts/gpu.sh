@@ -23,6 +23,8 @@
 #   route-trace  routed N = 1 kernel trace per library: GPU busy fraction and
 #                kernel time per batch (trace_busy.py) [KARGS]
 #   seed-sweep   the rate per stem-hash key [CFG SEEDS]
+#   serial-trace kernel + copy trace of serial C1 batches per library (the in-tree
+#                one and build_abl/lib_*.so): k_table per batch, fill included [KARGS]
 #   split-prof   phase stamps of k_split's long body (build_abl/lib_sprof.so,
 #                built with RL_SPLIT_PROF) on C2U [LIBS]
 set -o pipefail
@@ -172,6 +174,20 @@ task_route_trace() {
   done
 }
 
+task_serial_trace() {
+  local lib tag
+  for lib in "" build_abl/lib_*.so; do
+    [ -n "$lib" ] && [ ! -e "$lib" ] && continue
+    tag=$(basename "${lib:-cur}" .so)
+    rm -rf gpurun_out/tr_$tag && mkdir -p gpurun_out/tr_$tag
+    RL_LIB_PATH=${lib:+$PWD/$lib} timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
+      -d gpurun_out/tr_$tag -o run -- python -u bench.py --steps 30 --warmup 3 --latency-steps 3 --loaded-steps 0 \
+      --no-cpu-baseline --prof-every 0 --pcie-steps 0 --serial ${KARGS:---config c1} > gpurun_out/tr_$tag.log 2>&1 \
+      || { tail -20 gpurun_out/tr_$tag.log; return 1; }
+    summary gpurun_out/tr_$tag.log $tag
+  done
+}
+
 task_seed_sweep() {
   local cfg=${CFG:-c2} seed
   for seed in ${SEEDS:-1 2 3 4 5 6 7 8 9 10 11 12}; do
@@ -201,6 +217,7 @@ for t in "$@"; do
     pmc) task_pmc ;;
     pcie-trace) task_pcie_trace ;;
     route-trace) task_route_trace ;;
+    serial-trace) task_serial_trace ;;
     seed-sweep) task_seed_sweep ;;
     split-prof) task_split_prof ;;
     *) echo "unknown task: $t"; exit 2 ;;
