@@ -534,19 +534,24 @@ def pcie_fed(args, be, host_batches, now):
 
     def phase(fed, call, bytes_in):
         keep = []
+        host_s = [0.0]
 
         def submit(s):
+            t = time.perf_counter()
             keep.append(call(fed[s % len(fed)], outs[s % len(outs)]))
+            host_s[0] += time.perf_counter() - t
 
         for s in range(3):
             submit(s)
         be.synchronize()
         keep.clear()
+        host_s[0] = 0.0
         t0 = time.perf_counter()
         for s in range(args.pcie_steps):
             submit(s)
         be.synchronize()
         el = time.perf_counter() - t0
+        host_ms = host_s[0] / args.pcie_steps * 1e3
         keep.clear()
         lat = []
         for s in range(20):
@@ -558,7 +563,8 @@ def pcie_fed(args, be, host_batches, now):
         return {"value": n * args.pcie_steps / el, "unit": "decisions/s", "ms_per_step": el / args.pcie_steps * 1e3,
                 "p50_batch_ms": float(np.percentile(lat, 50)), "p99_batch_ms": float(np.percentile(lat, 99)),
                 "h2d_bytes_per_decision": bytes_in / n, "d2h_bytes_per_decision": bytes_out / n,
-                "h2d_GBps": bytes_in * args.pcie_steps / el / 1e9, "steps": args.pcie_steps}
+                "h2d_GBps": bytes_in * args.pcie_steps / el / 1e9, "steps": args.pcie_steps,
+                "host_submit_ms": host_ms}
 
     soa_in = sum(int(v.nbytes) for k, v in soa[0].arrays.items() if k != "stem_bytes") + \
         int(soa[0].arrays["stem_off"][n])
@@ -595,7 +601,7 @@ def pcie_fed(args, be, host_batches, now):
     head = named[fmts[0]]
     head["buffers"] = "page-locked (rl_alloc_host); now constant over the phase"
     head["host_numa"] = host_numa()
-    keys = ("value", "h2d_bytes_per_decision", "h2d_GBps", "frac_of_h2d_peak", "p99_batch_ms", "format")
+    keys = ("value", "h2d_bytes_per_decision", "h2d_GBps", "frac_of_h2d_peak", "p99_batch_ms", "host_submit_ms", "format")
     for f in fmts[1:]:
         head[f] = {k: named[f][k] for k in keys}
     return head

@@ -598,14 +598,22 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
       launch_route_scatter(S.perm, S.back, n, o, r->ret, src_err);
     }
     if (mine && stats_out) launch_stats_sum(stats_in, W, mine, stats_out, r->ret, m);
-    if (S.io.stats_host && mine)
-      CHK_HIP(e, hipMemcpyAsync(S.io.stats_host, S.io_stats, (size_t)mine * 8, hipMemcpyDeviceToHost, r->ret));
-    if (S.io.host && n) {  // the answers cross back to the caller's host slice
-      CHK_HIP(e, hipMemcpyAsync(out.code, S.h_code, n, hipMemcpyDeviceToHost, r->ret));
-      CHK_HIP(e, hipMemcpyAsync(out.limit_remaining, S.h_rem, n * 4ull, hipMemcpyDeviceToHost, r->ret));
-      if (out.reset_s) CHK_HIP(e, hipMemcpyAsync(out.reset_s, S.h_reset, n * 4ull, hipMemcpyDeviceToHost, r->ret));
-      if (out.status) CHK_HIP(e, hipMemcpyAsync(out.status, S.h_status, n, hipMemcpyDeviceToHost, r->ret));
+    // the answers cross back to the caller's host slice (kernel stores into
+    // page-locked outputs, rl_kernels.h ToHost)
+    ToHost th{};
+    auto add = [&](void* dst, const void* src, uint64_t bytes) {
+      th.dst[th.n] = (uint8_t*)dst;
+      th.src[th.n] = (const uint8_t*)src;
+      th.bytes[th.n++] = bytes;
+    };
+    if (S.io.stats_host && mine) add(S.io.stats_host, S.io_stats, (size_t)mine * 8);
+    if (S.io.host && n) {
+      add(out.code, S.h_code, n);
+      add(out.limit_remaining, S.h_rem, n * 4ull);
+      if (out.reset_s) add(out.reset_s, S.h_reset, n * 4ull);
+      if (out.status) add(out.status, S.h_status, n);
     }
+    if (th.n) CHK_HIP(e, copy_to_host(th, r->ret));
   } else if (!r->sticky) {
     r->sticky = S.err;
     r->sticky_msg = S.errmsg;

@@ -67,6 +67,16 @@ struct Engine {
   uint32_t ring_cur = 0;
   unsigned long long* ring_ctr = nullptr;
   uint32_t ring_parts = 1, ring_part_lines = 0;  // ring_cap = ring_parts x ring_part_lines
+  // RL_DEBUG_COPYTIME: host-fed input copies timed with events (stderr at destroy)
+  bool copy_time = false;
+  // RL_DEBUG_HOSTTIME: host seconds per section of the host-fed prefixed path (stderr at destroy)
+  bool host_time = false;
+  double ht[8] = {};
+  uint64_t ht_n = 0;  // RL_H2D_KERNEL: host-fed inputs pulled by k_from_host (experiment)
+  hipEvent_t ct_ev[2][64] = {};
+  uint32_t ct_n = 0;
+  double ct_ms = 0;
+  uint64_t ct_count = 0;
   uint8_t* arena = nullptr;
   uint8_t* arena2 = nullptr;  // compaction target (rl_sweep), swapped with arena
   uint64_t arena_cap16 = 0;

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <random>
 #include <cstring>
@@ -81,6 +82,10 @@ int set_err(Engine* c, int code, const std::string& msg) {
 template <typename T>
 hipError_t dalloc(T** p, size_t count) {
   return hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T));
+}
+
+inline double wall_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 int map_err(Engine* c, uint32_t e) {
@@ -370,6 +375,10 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && hipEventCreateWithFlags(&c->route_ready, hipEventDisableTiming) == hipSuccess &&
        hipEventCreateWithFlags(&c->caller_ready, hipEventDisableTiming) == hipSuccess;
   c->serial_debug = getenv("RL_DEBUG_SERIAL") != nullptr;
+  c->copy_time = getenv("RL_DEBUG_COPYTIME") != nullptr;
+  c->host_time = getenv("RL_DEBUG_HOSTTIME") != nullptr;
+  for (uint32_t k = 0; c->copy_time && k < 64; k++)
+    ok = ok && hipEventCreate(&c->ct_ev[0][k]) == hipSuccess && hipEventCreate(&c->ct_ev[1][k]) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_base, (size_t)NBUF * RL_MAX_SHARDS * 8) == hipSuccess;
   ok = ok && dalloc(&s0.stripes, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS) == hipSuccess;
   ok = ok && dalloc(&s0.time_floor, 1) == hipSuccess;
@@ -429,9 +438,25 @@ void free_host_slots(Engine* c) {
   c->hs_ready = false;
 }
 
+void copy_time_fold(Engine* c, bool all);
+
 void eng_destroy(Engine* c) {
   if (!c) return;
   (void)hipSetDevice(c->cfg.device);
+  if (c->host_time && c->ht_n)
+    fprintf(stderr, "RL_DEBUG_HOSTTIME: %llu batches, ms each: check %.4f copy %.4f unpack %.4f enqueue %.4f to_host %.4f "
+            "track %.4f\n", (unsigned long long)c->ht_n, c->ht[0] / c->ht_n * 1e3, c->ht[1] / c->ht_n * 1e3,
+            c->ht[2] / c->ht_n * 1e3, c->ht[3] / c->ht_n * 1e3, c->ht[4] / c->ht_n * 1e3, c->ht[5] / c->ht_n * 1e3);
+  if (c->copy_time) {
+    (void)hipDeviceSynchronize();
+    copy_time_fold(c, true);
+    if (c->ct_count)
+      fprintf(stderr, "RL_DEBUG_COPYTIME: %llu input copies, %.4f ms each\n", (unsigned long long)c->ct_count,
+              c->ct_ms / c->ct_count);
+    for (uint32_t k = 0; k < 64; k++)
+      for (int j = 0; j < 2; j++)
+        if (c->ct_ev[j][k]) (void)hipEventDestroy(c->ct_ev[j][k]);
+  }
   if (c->hs_ready) {
     (void)hipDeviceSynchronize();
     free_host_slots(c);
@@ -661,10 +686,27 @@ int eng_profile_read(Engine* c, double* ms, uint32_t n, uint64_t* batches) {
   return RL_OK;
 }
 
+// RL_DEBUG_COPYTIME: fold the timed copies (all when `all`, else the ring's
+// oldest pair when it is about to be reused).
+void copy_time_fold(Engine* c, bool all) {
+  const uint32_t lo = c->ct_n > 64 ? c->ct_n - 64 : 0;
+  for (uint32_t k = all ? lo : c->ct_n - (c->ct_n >= 64 ? 64 : c->ct_n); k < c->ct_n; k++) {
+    if (!all && k + 64 != c->ct_n) continue;
+    float ms = 0;
+    if (hipEventSynchronize(c->ct_ev[1][k % 64]) == hipSuccess &&
+        hipEventElapsedTime(&ms, c->ct_ev[0][k % 64], c->ct_ev[1][k % 64]) == hipSuccess) {
+      c->ct_ms += ms;
+      c->ct_count++;
+    }
+  }
+  if (all) c->ct_n = 0;
+}
+
 int eng_synchronize(Engine* c) {
   if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   HIPCHK(c, hipDeviceSynchronize());
+  if (c->copy_time) copy_time_fold(c, true);
   c->seq_done = c->seq_sub;
   return collect(c);
 }
@@ -725,20 +767,36 @@ int host_slot_run(Engine* c, HostSlot& h, const rl_batch& d, uint64_t nb, rl_res
   BatchDev b = dev_view(c, &d, c->cfg.max_stem_bytes);
   b.stem_total = (uint32_t)nb;
   OutDev o{h.code, h.rem, h.reset, d.n_rules ? h.stats : nullptr, out->status ? h.status : nullptr};
+  const double w0 = c->host_time ? wall_s() : 0;
   HIPCHK(c, hipStreamWaitEvent(c->pipe[c->next], h.in_done, 0));
   const uint32_t k = enqueue(c, b, o, 0, nullptr, true);
   HIPCHK(c, hipStreamWaitEvent(down, c->b_done[k], 0));
+  const double w1 = c->host_time ? wall_s() : 0;
+  // (stores by a kernel into page-locked outputs: not queued behind the next
+  // batch's input copy on the DMA engine, rl_kernels.h ToHost)
+  ToHost th{};
+  auto add = [&](void* dst, const void* src, uint64_t bytes) {
+    th.dst[th.n] = (uint8_t*)dst;
+    th.src[th.n] = (const uint8_t*)src;
+    th.bytes[th.n++] = bytes;
+  };
   if (n) {
-    HIPCHK(c, hipMemcpyAsync(out->code, h.code, n, hipMemcpyDeviceToHost, down));
-    HIPCHK(c, hipMemcpyAsync(out->limit_remaining, h.rem, n * 4ull, hipMemcpyDeviceToHost, down));
-    if (out->reset_s) HIPCHK(c, hipMemcpyAsync(out->reset_s, h.reset, n * 4ull, hipMemcpyDeviceToHost, down));
-    if (out->status) HIPCHK(c, hipMemcpyAsync(out->status, h.status, n, hipMemcpyDeviceToHost, down));
+    add(out->code, h.code, n);
+    add(out->limit_remaining, h.rem, n * 4ull);
+    if (out->reset_s) add(out->reset_s, h.reset, n * 4ull);
+    if (out->status) add(out->status, h.status, n);
   }
-  if (d.n_rules && out->stats)
-    HIPCHK(c, hipMemcpyAsync(out->stats, h.stats, (size_t)d.n_rules * RL_NUM_STATS * 8, hipMemcpyDeviceToHost,
-                             down));
+  if (d.n_rules && out->stats) add(out->stats, h.stats, (size_t)d.n_rules * RL_NUM_STATS * 8);
+  if (th.n) HIPCHK(c, copy_to_host(th, down));
   HIPCHK(c, hipEventRecord(h.out_done, down));
+  const double w2 = c->host_time ? wall_s() : 0;
   HIPCHK(c, track(c, down));
+  if (c->host_time) {
+    const double w3 = wall_s();
+    c->ht[3] += w1 - w0;
+    c->ht[4] += w2 - w1;
+    c->ht[5] += w3 - w2;
+  }
   HIPCHK(c, hipGetLastError());
   c->batches++;
   c->decisions += n;
@@ -891,7 +949,9 @@ int eng_prefixed_check(Engine* c, const rl_batch_prefixed* in, const rl_result* 
 
 int eng_do_limit_prefixed_async(Engine* c, const rl_batch_prefixed* in, rl_result* out) {
   uint32_t T = 0;
+  const double w0 = c && c->host_time ? wall_s() : 0;
   int rc = eng_prefixed_check(c, in, out, &T);
+  if (c->host_time) c->ht[0] += wall_s() - w0;
   if (rc) return rc;
   const rl_config& g = c->cfg;
   const uint32_t n = in->n, nq = in->n_requests;
@@ -912,13 +972,26 @@ int eng_do_limit_prefixed_async(Engine* c, const rl_batch_prefixed* in, rl_resul
   }
   c->hnext = (j + 1) % NBUF;
   hipStream_t up = c->h2d;
+  const double w1 = c->host_time ? wall_s() : 0;
   HIPCHK(c, hipStreamWaitEvent(up, h.out_done, 0));  // the slot's previous batch is drained
+  if (c->copy_time) {
+    copy_time_fold(c, false);
+    HIPCHK(c, hipEventRecord(c->ct_ev[0][c->ct_n % 64], up));
+  }
   if (B) HIPCHK(c, hipMemcpyAsync(h.cbuf, in->buf, B, hipMemcpyHostToDevice, up));
+  if (c->copy_time) HIPCHK(c, hipEventRecord(c->ct_ev[1][c->ct_n++ % 64], up));
   HIPCHK(c, hipEventRecord(h.in_done, up));
+  const double w2 = c->host_time ? wall_s() : 0;
   // unpacked on the batch's pipeline stream (as the compact batch)
   HIPCHK(c, hipStreamWaitEvent(c->pipe[c->next], h.in_done, 0));
   launch_unpack_prefixed(*in, h.cbuf, 0, T, h.stem, h.off, h.req, h.unit, h.flags, h.limit, h.hits, h.rule, h.now,
                          c->s[c->next].err, c->pipe[c->next]);
+  if (c->host_time) {
+    const double w3 = wall_s();
+    c->ht[1] += w2 - w1;
+    c->ht[2] += w3 - w2;
+    c->ht_n++;
+  }
   rl_batch d{};
   d.n = n;
   d.n_requests = nq;

@@ -233,6 +233,23 @@ void launch_unpack_range(const rl_batch_compact& cb, const uint8_t* buf, uint32_
 // at the index's stem offsets, off[] the stem offsets (off[n] included). The
 // totals come from the host buffer's last index entry (already checked). A
 // tile whose entry does not match its sections sets ERR_INVALID in *err.
+// Device -> page-locked host copies done by a kernel's vector stores over
+// PCIe (posted writes), not by the DMA engine: the host-fed paths' outputs
+// then cross back while the next batch's input copy holds the engine
+// (an SDMA D2H copy queues behind it). dst[k] are device-visible host
+// addresses (hipHostGetDevicePointer).
+constexpr uint32_t TO_HOST_MAX = 6;
+struct ToHost {
+  const uint8_t* src[TO_HOST_MAX];
+  uint8_t* dst[TO_HOST_MAX];
+  uint64_t bytes[TO_HOST_MAX];
+  uint32_t n;
+};
+void launch_to_host(const ToHost& c, hipStream_t st);
+// The copies of c (dst: host addresses as the caller holds them) by k_to_host
+// when every dst is page-locked, else by hipMemcpyAsync.
+hipError_t copy_to_host(ToHost c, hipStream_t st);
+
 void launch_unpack_prefixed(const rl_batch_prefixed& pb, const uint8_t* buf, uint32_t t0, uint32_t t1, uint8_t* stem,
                             uint32_t* off, uint32_t* req, uint8_t* unit, uint8_t* flags, uint32_t* limit,
                             uint32_t* hits, uint32_t* rule, int64_t* now, uint32_t* err, hipStream_t st);

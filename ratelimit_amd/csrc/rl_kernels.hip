@@ -25,6 +25,7 @@
 // plus k_sweep (epoch sweep = Redis EXPIRE), k_table_info, debug kernels.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include "rl_device.h"
 #include "rl_kernels.h"
@@ -390,6 +391,62 @@ __global__ __launch_bounds__(256) void k_unpack_prefixed(
       stem[a + tid] = s8[sh + tid];
     }
   }
+}
+
+// ---- k_to_host: launch_to_host's copies. Copy k's 16-B-aligned middle in
+// dwordx4 stores, grid-stride; its ragged head and tail bytes by the first
+// workgroup (host arrays from rl_alloc_host are aligned: the head is empty).
+__global__ __launch_bounds__(256) void k_to_host(ToHost c) {
+  const uint64_t tid = blockIdx.x * 256ull + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
+  for (uint32_t k = 0; k < c.n; k++) {
+    const uint8_t* s = c.src[k];
+    uint8_t* d = c.dst[k];
+    const uint64_t B = c.bytes[k];
+    const uint64_t head = ((16u - ((uintptr_t)d & 15u)) & 15u) < B ? ((16u - ((uintptr_t)d & 15u)) & 15u) : B;
+    if ((((uintptr_t)s + head) & 15u) == 0) {
+      const uint64_t n16 = (B - head) / 16;
+      const uint4* s4 = reinterpret_cast<const uint4*>(s + head);
+      uint4* d4 = reinterpret_cast<uint4*>(d + head);
+      for (uint64_t j = tid; j < n16; j += stride) d4[j] = s4[j];
+      if (blockIdx.x == 0) {
+        if (threadIdx.x < head) d[threadIdx.x] = s[threadIdx.x];
+        const uint64_t t0 = head + n16 * 16;
+        if (t0 + threadIdx.x < B) d[t0 + threadIdx.x] = s[t0 + threadIdx.x];
+      }
+    } else {  // (source and destination misaligned against each other: bytes)
+      for (uint64_t j = tid; j < B; j += stride) d[j] = s[j];
+    }
+  }
+}
+
+hipError_t copy_to_host(ToHost c, hipStream_t st) {
+  static const bool dma = getenv("RL_D2H_MEMCPY") != nullptr;  // (A/B knob)
+  bool mapped = !dma;
+  ToHost m = c;
+  for (uint32_t k = 0; k < c.n && mapped; k++) {
+    void* dp = nullptr;
+    mapped = c.bytes[k] == 0 || (hipHostGetDevicePointer(&dp, c.dst[k], 0) == hipSuccess && dp);
+    m.dst[k] = (uint8_t*)dp;
+  }
+  if (mapped) {
+    launch_to_host(m, st);
+    return hipGetLastError();
+  }
+  (void)hipGetLastError();  // (the failed lookup's sticky error: pageable memory)
+  for (uint32_t k = 0; k < c.n; k++)
+    if (c.bytes[k]) {
+      const hipError_t e = hipMemcpyAsync(c.dst[k], c.src[k], c.bytes[k], hipMemcpyDeviceToHost, st);
+      if (e != hipSuccess) return e;
+    }
+  return hipSuccess;
+}
+
+void launch_to_host(const ToHost& c, hipStream_t st) {
+  uint64_t most = 0;
+  for (uint32_t k = 0; k < c.n; k++) most = c.bytes[k] > most ? c.bytes[k] : most;
+  if (!most) return;
+  const uint64_t g = (most / 16 + 255) / 256;
+  k_to_host<<<(uint32_t)(g < 1024 ? (g ? g : 1) : 1024), 256, 0, st>>>(c);
 }
 
 void launch_unpack_prefixed(const rl_batch_prefixed& pb, const uint8_t* buf, uint32_t t0, uint32_t t1, uint8_t* stem,
