@@ -72,7 +72,7 @@ struct Engine {
   // RL_DEBUG_HOSTTIME: host seconds per section of the host-fed prefixed path (stderr at destroy)
   bool host_time = false;
   double ht[8] = {};
-  uint64_t ht_n = 0;  // RL_H2D_KERNEL: host-fed inputs pulled by k_from_host (experiment)
+  uint64_t ht_n = 0;
   hipEvent_t ct_ev[2][64] = {};
   uint32_t ct_n = 0;
   double ct_ms = 0;
