@@ -21,6 +21,10 @@ namespace rl {
 #define RL_NBUF 4
 #endif
 constexpr uint32_t NBUF = RL_NBUF;
+// errw words: [0, NBUF) stage A of each buffer, [NBUF] (unused), [NBUF + 1]
+// the soft word (per-descriptor statuses), [NBUF + 2] the routing partition,
+// [ERRW_B0 + k] the table-stage word of buffer k's batch
+constexpr uint32_t ERRW_B0 = NBUF + 3, ERRW_WORDS = ERRW_B0 + NBUF;
 constexpr uint32_t PROF_RING = 8;  // timed batches in flight (> NBUF)
 constexpr uint32_t PROGRESS_RING = 64;  // batches rl_batch_progress tracks in flight
 
@@ -48,6 +52,7 @@ struct Engine {
   hipStream_t stream = nullptr;   // serial work (== pipe[0])
   hipStream_t pipe[NBUF] = {};    // one per scratch buffer
   hipEvent_t b_done[NBUF] = {};   // stage B of the last batch on each buffer is done
+  hipEvent_t b_table[NBUF] = {};  // ... its table kernels are (the next batch's stage B waits for this)
   hipEvent_t consumed[NBUF] = {}; // a routed owner batch's packed results (s[k].res) have been read
   hipEvent_t route_ready = nullptr;  // eng_route_do_limit: the caller's received buffers are ready
   hipEvent_t caller_ready = nullptr; // eng_do_limit_async: the caller stream's work so far (the inputs)

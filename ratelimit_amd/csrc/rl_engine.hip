@@ -99,21 +99,28 @@ int map_err(Engine* c, uint32_t e) {
   return set_err(c, RL_E_INTERNAL, "gpu: unknown device error");
 }
 
-// Order stream st after every batch submitted so far (their stage B, which
-// waited for all earlier ones).
-hipError_t after_batches(Engine* c, hipStream_t st) { return hipStreamWaitEvent(st, c->b_done[c->last], 0); }
+// Order stream st after every batch submitted so far: each buffer's last
+// batch to its end (a batch's k_finish may still run after the next batch's
+// stage B has started: that waits for b_table only).
+hipError_t after_batches(Engine* c, hipStream_t st) {
+  for (uint32_t k = 0; k < NBUF; k++) {
+    const hipError_t e = hipStreamWaitEvent(st, c->b_done[k], 0);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
 
 // Read (and clear) the sticky device error words; synchronises the stream,
 // which must already be ordered after all submitted work.
 // The soft word (descriptor errors answered by statuses) is cleared, not reported.
 int collect(Engine* c, hipStream_t st = nullptr) {
   if (!st) st = c->stream;
-  HIPCHK(c, hipMemcpyAsync(c->h_err, c->errw, (NBUF + 3) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(c->h_err, c->errw, ERRW_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
   uint32_t e = c->h_err[NBUF + 2];  // the routing partition's word
-  for (uint32_t j = 0; j <= NBUF; j++) e |= c->h_err[j];
+  for (uint32_t j = 0; j < NBUF; j++) e |= c->h_err[j] | c->h_err[ERRW_B0 + j];
   if (e || c->h_err[NBUF + 1]) {
-    HIPCHK(c, hipMemsetAsync(c->errw, 0, (NBUF + 3) * sizeof(uint32_t), st));
+    HIPCHK(c, hipMemsetAsync(c->errw, 0, ERRW_WORDS * sizeof(uint32_t), st));
     HIPCHK(c, hipStreamSynchronize(st));
   }
   return map_err(c, e);
@@ -138,15 +145,15 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     (void)hipStreamWaitEvent(a, c->b_done[k], 0);    // buffer k's previous batch is done
     (void)hipStreamWaitEvent(a, c->consumed[k], 0);  // ... and its routed results were read
     launch_stage_a(b, c->s[k], isolate, P.per_second, a, ev);
-    (void)hipStreamWaitEvent(a, c->b_done[c->last], 0);  // table order
-    launch_stage_b(b, o, t, P, c->s[k], restore, a, ev);
+    (void)hipStreamWaitEvent(a, c->b_table[c->last], 0);  // table order (not the previous k_finish)
+    launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, c->s[c->last].errb, c->b_table[k]);
     (void)hipEventRecord(c->b_done[k], a);
   } else {
     if (!st) st = c->stream;
     (void)after_batches(c, st);
     hipEvent_t* ev = prof_events(c);
     launch_stage_a(b, c->s[k], isolate, P.per_second, st, ev);
-    launch_stage_b(b, o, t, P, c->s[k], restore, st, ev);
+    launch_stage_b(b, o, t, P, c->s[k], restore, st, ev, c->s[c->last].errb, c->b_table[k]);
     (void)hipEventRecord(c->b_done[k], st);
   }
   c->last = k;
@@ -360,7 +367,8 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   for (uint32_t k = 0; k < NBUF; k++) ok = ok && hipStreamCreateWithFlags(&c->pipe[k], hipStreamNonBlocking) == hipSuccess;
   c->stream = c->pipe[0];
   for (uint32_t k = 0; k < NBUF; k++)
-    ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&c->b_table[k], hipEventDisableTiming) == hipSuccess;
   for (uint32_t k = 0; k < PROGRESS_RING; k++)
     ok = ok && hipEventCreateWithFlags(&c->done_ring[k], hipEventDisableTiming) == hipSuccess;
   ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess && dalloc(&c->ring, c->ring_cap) == hipSuccess &&
@@ -369,7 +377,7 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess && dalloc(&c->arena2, cfg.arena_bytes) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++) ok = ok && alloc_buffer(c->s[k], n);
   Scratch& s0 = c->s[0];
-  ok = ok && dalloc(&c->errw, NBUF + 3) == hipSuccess;
+  ok = ok && dalloc(&c->errw, ERRW_WORDS) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++)
     ok = ok && hipEventCreateWithFlags(&c->consumed[k], hipEventDisableTiming) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&c->route_ready, hipEventDisableTiming) == hipSuccess &&
@@ -380,15 +388,15 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   for (uint32_t k = 0; c->copy_time && k < 64; k++)
     ok = ok && hipEventCreate(&c->ct_ev[0][k]) == hipSuccess && hipEventCreate(&c->ct_ev[1][k]) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_base, (size_t)NBUF * RL_MAX_SHARDS * 8) == hipSuccess;
-  ok = ok && dalloc(&s0.stripes, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS) == hipSuccess;
+  for (uint32_t k = 0; k < NBUF; k++)  // per buffer: a batch's k_finish overlaps the next batch's table kernels
+    ok = ok && dalloc(&c->s[k].stripes, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS) == hipSuccess;
   ok = ok && dalloc(&s0.time_floor, 1) == hipSuccess;
   ok = ok && dalloc(&s0.counters, 8) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++) {  // shared members
     Scratch& sk = c->s[k];
     sk.err = c->errw ? c->errw + k : nullptr;
-    sk.errb = c->errw ? c->errw + NBUF : nullptr;
+    sk.errb = c->errw ? c->errw + ERRW_B0 + k : nullptr;
     sk.errs = c->errw ? c->errw + NBUF + 1 : nullptr;
-    sk.stripes = s0.stripes;
     sk.time_floor = s0.time_floor;
     sk.counters = s0.counters;
   }
@@ -402,21 +410,24 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
        dalloc(&c->d_rem, n) == hipSuccess &&
        dalloc(&c->d_reset, n) == hipSuccess;
   ok = ok && dalloc(&c->d_stats, (size_t)cfg.max_rules * RL_NUM_STATS) == hipSuccess;
-  ok = ok && hipHostMalloc((void**)&c->h_err, (NBUF + 3) * sizeof(uint32_t)) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_err, ERRW_WORDS * sizeof(uint32_t)) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_counters, 8 * sizeof(unsigned long long)) == hipSuccess;
   if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
   ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
        hipMemsetAsync(c->ring_ctr, 0, (size_t)RING_PARTS_MAX * RING_CTR_STRIDE * 8, c->stream) == hipSuccess &&
        // (lines are initialised when taken)
-       hipMemsetAsync(c->errw, 0, (NBUF + 3) * 4, c->stream) == hipSuccess &&
+       hipMemsetAsync(c->errw, 0, ERRW_WORDS * 4, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.time_floor, 0, 8, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.counters, 0, 64, c->stream) == hipSuccess &&
-       hipMemsetAsync(s0.stripes, 0, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS * 8, c->stream) ==
+       hipMemsetAsync(c->s[0].stripes, 0, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS * 8, c->stream) ==
            hipSuccess &&
        hipMemsetAsync(c->d_stem, 0, (size_t)cfg.max_stem_bytes + 64, c->stream) == hipSuccess &&
        hipStreamSynchronize(c->stream) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++)
     ok = ok && hipEventRecord(c->b_done[k], c->stream) == hipSuccess &&
+         hipEventRecord(c->b_table[k], c->stream) == hipSuccess &&
+         (k == 0 || hipMemsetAsync(c->s[k].stripes, 0, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS * 8,
+                                   c->stream) == hipSuccess) &&
          hipEventRecord(c->consumed[k], c->stream) == hipSuccess;
   if (!ok) return fail("gpu: device initialisation failed", c);
   return c;
@@ -469,6 +480,7 @@ void eng_destroy(Engine* c) {
   for (uint32_t k = 0; k < NBUF; k++) {
     free_buffer(c->s[k]);
     if (c->b_done[k]) (void)hipEventDestroy(c->b_done[k]);
+    if (c->b_table[k]) (void)hipEventDestroy(c->b_table[k]);
     if (c->consumed[k]) (void)hipEventDestroy(c->consumed[k]);
   }
   for (uint32_t k = 0; k < PROGRESS_RING; k++)
@@ -487,6 +499,8 @@ void eng_destroy(Engine* c) {
                   c->d_reset, c->d_stats};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
+  for (uint32_t k = 1; k < NBUF; k++)
+    if (c->s[k].stripes) (void)hipFree(c->s[k].stripes);
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
   for (void* p : {(void*)c->cfg_blob, (void*)c->mbuf})

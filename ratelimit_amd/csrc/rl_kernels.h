@@ -210,8 +210,11 @@ struct Scratch {
 // must run in batch order.
 void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_second, hipStream_t st,
                     hipEvent_t* ev = nullptr);
+// errb_prev: the previous batch's table-stage word (this batch's starts from
+// it); table_done (optional) is recorded once the table kernels are done, before
+// k_finish: the next batch's stage B waits for it, not for k_finish.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                    int restore, hipStream_t st, hipEvent_t* ev = nullptr);
+                    int restore, hipStream_t st, hipEvent_t* ev, const uint32_t* errb_prev, hipEvent_t table_done);
 // ev (optional, RL_NUM_STAGES + 1 events on stream st): recorded before
 // k_prepare, after it, after the sort, just before and just after k_table, and
 // at the end (per-stage timing, rl_profile).

@@ -4256,13 +4256,15 @@ __global__ __launch_bounds__(256, RL_LATE_OCC) void k_late(BatchDev b, TableDev 
 // the sticky table-stage word, clear k_table's deferral counters and this call's
 // output stats (n_rules x RL_NUM_STATS).
 __global__ __launch_bounds__(256) void k_b_begin(const uint32_t* __restrict__ erra, uint32_t* errb,
+                                                 const uint32_t* errb_prev,
                                                  uint32_t* __restrict__ defer_n, uint32_t* __restrict__ defer1_n,
                                                  unsigned long long* __restrict__ stats, uint32_t m,
                                                  uint32_t* __restrict__ fast_blk, uint32_t nw) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i == 0) {
-    const uint32_t e = *erra;
-    if (e) atomicOr(errb, e);
+    // this batch's table-stage word: the previous batch's (sticky: a failed
+    // batch fails every later one) | this batch's validation result
+    *errb = *errb_prev | *erra;
     *defer_n = 0;
     *defer1_n = 0;
   }
@@ -4517,10 +4519,11 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
 #define RL_LATE_FAST_BLOCKS 0  // cap on k_late's long-run workgroups (0: one per 256 descriptors)
 #endif
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                    int restore, hipStream_t st, hipEvent_t* ev) {
+                    int restore, hipStream_t st, hipEvent_t* ev, const uint32_t* errb_prev, hipEvent_t table_done) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
-  k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, s.defer2_n, s.defer1_n, o.stats, m, s.fast_blk, cdiv(b.n, 256 * 32));
+  k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, errb_prev, s.defer2_n, s.defer1_n, o.stats, m, s.fast_blk,
+                                cdiv(b.n, 256 * 32));
   if (b.n) {
     const uint32_t g = cdiv(b.n, 256);
     const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
@@ -4545,14 +4548,18 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
         s.keys[0], s.defer1, s.defer1_n, s.segsum, s.rid, s.run_flags, s.run_state, s.run_alias, s.run_f, o.stats,
         s.stripes, s.errb,
         s.errs, restore, s.fast_blk, s.sorted_n);
+    if (table_done) (void)hipEventRecord(table_done, st);
     if (!restore) {
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;
       const uint32_t gf = cdiv(nf * RL_NUM_STATS > b.n ? nf * RL_NUM_STATS : b.n, 256);
       k_finish<<<gf, 256, 0, st>>>(s.res, b.n, o, s.stripes, nf, s.errb, P.lc_en ? s.counters + 5 : nullptr);
     }
-  } else if (ev) {
-    (void)hipEventRecord(ev[3], st);
-    (void)hipEventRecord(ev[4], st);
+  } else {
+    if (ev) {
+      (void)hipEventRecord(ev[3], st);
+      (void)hipEventRecord(ev[4], st);
+    }
+    if (table_done) (void)hipEventRecord(table_done, st);
   }
   if (ev) (void)hipEventRecord(ev[5], st);
 }
