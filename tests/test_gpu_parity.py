@@ -497,3 +497,48 @@ def test_gpu_c4_nested_shadow_unlimited_rollover(ratio, lc, prefix):
     for i, (g, e) in enumerate(zip(got, exp)):
         assert g == e, "call %d: gpu %s oracle %s" % (i, g, e)
     assert stats == py_stats
+
+
+@pytest.mark.parametrize("shift", [1, 3, 13])
+def test_gpu_host_outputs_written_back_at_any_alignment(shift):
+    """The host-fed outputs are written by k_to_host's stores into page-locked
+    memory: arrays starting `shift` bytes into a pinned block (ragged heads and
+    tails, source and destination misaligned against each other) and a batch
+    whose stats output is pageable (every copy falls back to hipMemcpyAsync)
+    come back exactly; the bytes around each array stay untouched."""
+    from ratelimit_amd.limiter import PinnedArena
+    from ratelimit_amd.packing import PackedBatch
+    z = workloads.ZipfSampler(20_000, 1.1)
+    batches = list(workloads.c2_stream(n_tenants=20_000, requests_per_batch=9_999, batches=3, sampler=z))
+    co = c_oracle.COracle(0.8, False)
+    want = [co.do_limit(a, n, nq, nr) for a, n, nq, nr in batches]
+    co.close()
+    be = Backend(0.8, False, table_slots=1 << 18, max_batch=1 << 16, max_rules=8)
+    arena = PinnedArena()
+    keep, got, guards = [], [], []
+    for i, (a, n, nq, nr) in enumerate(batches):
+        arr = {k: arena.like(v) for k, v in a.items()}
+        pb = PackedBatch(arr, n, nq, nr)
+        out = {}
+        for k, v in pb.alloc_result(isolate=(i == 1)).items():
+            if k == "stats" and i == 2:
+                out[k] = np.zeros_like(v)  # pageable
+                continue
+            raw = arena.array(v.nbytes + shift + 64, np.uint8)
+            raw[:] = 0xA5
+            out[k] = raw[shift:shift + v.nbytes].view(v.dtype)
+            guards.append((raw, shift, v.nbytes))
+        keep.append((pb, out, be.do_limit_host_async(pb, out)))
+        got.append(out)
+    be.synchronize()
+    for i, (g, w) in enumerate(zip(got, want)):
+        n, nr = batches[i][1], batches[i][3]
+        for k in ("code", "limit_remaining", "reset_s"):
+            assert np.array_equal(g[k][:n], w[k]), "batch %d: %s differs" % (i, k)
+        assert np.array_equal(g["stats"][:nr * abi.RL_NUM_STATS], w["stats"]), i
+        if "status" in g:
+            assert (g["status"][:n] == 0).all()
+    for raw, sh, nb in guards:
+        assert (raw[:sh] == 0xA5).all() and (raw[sh + nb:] == 0xA5).all()
+    be.close()
+    arena.close()
