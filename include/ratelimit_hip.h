@@ -581,11 +581,12 @@ typedef struct rl_local_cache_info {
 int rl_local_cache_info_get(rl_ctx* ctx, int64_t now, rl_local_cache_info* info);
 
 /* Table snapshot / restore (Redis RDB-style restart): an exact image of the
- * counter table, the long-stem arena, the local-cache state and the sweep time
- * floor. rl_snapshot_size gives the bytes rl_snapshot_save writes into `host`;
- * rl_snapshot_load accepts an image from a ctx with the same table_slots and an
- * arena at least as large (RL_E_INVALID otherwise). Both order after every
- * submitted batch. */
+ * counter table, the ring-line pool's lines in use and free lists, the
+ * long-stem arena, the local-cache state and the sweep time floor.
+ * rl_snapshot_size gives the bytes rl_snapshot_save writes into `host`;
+ * rl_snapshot_load accepts an image from a ctx with the same table_slots and
+ * ring_lines and an arena at least as large (RL_E_INVALID otherwise). Both
+ * order after every submitted batch. */
 int rl_snapshot_size(rl_ctx* ctx, uint64_t* bytes);
 int rl_snapshot_save(rl_ctx* ctx, void* host, uint64_t bytes);
 int rl_snapshot_load(rl_ctx* ctx, const void* host, uint64_t bytes);
