@@ -2627,6 +2627,11 @@ __device__ __attribute__((always_inline)) inline uint32_t block_compact(uint32_t
   return *count;
 }
 
+// k_run_check's per-position word for split_long_body (grp): unit << 8 | low
+// byte (0 = the head's stem, family 0; SPLIT_POS_OTHER = another stem;
+// SPLIT_POS_SKIP = a failed descriptor) | bit 16: `now` differs from the head's
+constexpr uint32_t SPLIT_POS_OTHER = 0xFFu, SPLIT_POS_SKIP = 0xFEu, SPLIT_POS_NOWVAR = 1u << 16;
+
 // k_run_check marks every descriptor whose sort key occurs twice or more in the
 // batch (FLAG_DUP in its record, one plain store per descriptor: the thread of
 // sorted position q marks q, and the run's head when q is its second element).
@@ -2681,8 +2686,11 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
     if (q == p + 1) rec[ep].lu = y.lu | (FLAG_DUP << 24);  // the run's head
     const bool same = same_stem && rec_unit(x) == rec_unit(y);
     // per position, for k_split's long runs (coalesced there instead of a
-    // random record read per element): the unit and max(1, hits)
-    pos_unit[q] = rec_unit(x) << 8;
+    // random record read per element): the unit and max(1, hits), and how the
+    // element compares with the head (SPLIT_POS_*: family 0 = the head's stem
+    // is known without another pass over the run's records and stems)
+    pos_unit[q] = (rec_unit(x) << 8) | (skip ? SPLIT_POS_SKIP : !same_stem ? SPLIT_POS_OTHER : 0u) |
+                  (x.now != y.now ? SPLIT_POS_NOWVAR : 0u);
     pos_hits[q] = x.hits > 1 ? x.hits : 1u;
     uint32_t f = 0;
     if (!same)  // (+ the units seen, for k_split; a failed descriptor's unit may be out of range)
@@ -2893,10 +2901,31 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
     if ((rfl & (RUN_UNITS | RUN_STEMS)) == RUN_UNITS) {
       NF = 1;
     } else {
-      for (uint32_t k = tid; k < L; k += NT) {
-        grp[p + k] = 0xFFu;
-        if ((rec[sv[p + k]].lu >> 24) & FLAG_SKIP) s_bad = 1;
+      // family 0, the head's stem: from k_run_check's comparison of every
+      // element with the head (one coalesced pass; the records and stems of
+      // a hot stem's tens of thousands of descriptors are not read again)
+      uint32_t fm0 = 0, nv0 = 0;
+      for (uint32_t k = tid + 1; k < L; k += NT) {
+        const uint32_t v = grp[p + k], lo = v & 0xFFu;
+        if (lo == SPLIT_POS_SKIP) {
+          s_bad = 1;
+        } else if (lo == 0) {
+          fm0 |= 1u << (((v >> 8) & 0xFFu) - 1);
+          nv0 |= (v & SPLIT_POS_NOWVAR) ? 1u : 0u;
+        }
       }
+      if (tid == 0) {
+        const Rec y = rec[sv[p]];
+        if ((y.lu >> 24) & FLAG_SKIP) s_bad = 1;
+        grp[p] = rec_unit(y) << 8;  // family 0
+        s_lnow[0] = y.now;
+        s_lunit[0] = rec_unit(y);
+        fm0 |= 1u << (rec_unit(y) - 1);
+      }
+      if (fm0) atomicOr(&s_fmask[0], fm0);
+      if (nv0) s_fnv[0] = 1;
+      NF = 1;
+      __syncthreads();
       // families, as in k_split: the first unassigned element leads, and every
       // element with its stem joins (records read SPLIT_UNROLL at a time: the
       // scan is a chain of random reads)
@@ -2975,7 +3004,7 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
 #pragma unroll
         for (uint32_t st = 0; st < SPLIT_ST; st++) {
           if (fu[st] == 0xFFFFFFFFu) continue;
-          const uint32_t gk = s_plan.ug[fu[st] & 0xFFu][(fu[st] >> 8) - 1];
+          const uint32_t gk = s_plan.ug[fu[st] & 0xFFu][((fu[st] >> 8) & 0xFFu) - 1];
 #pragma unroll
           for (uint32_t g = 0; g < SPLIT_MAXG; g++)
             if (gk == g) {
@@ -3074,7 +3103,8 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
         }
 #pragma unroll
         for (uint32_t st = 0; st < SPLIT_ST; st++) {
-          const uint32_t gk = fu[st] == 0xFFFFFFFFu ? 0xFFu : s_plan.ug[fu[st] & 0xFFu][(fu[st] >> 8) - 1];
+          const uint32_t gk =
+              fu[st] == 0xFFFFFFFFu ? 0xFFu : s_plan.ug[fu[st] & 0xFFu][((fu[st] >> 8) & 0xFFu) - 1];
           uint32_t np = 0;
 #pragma unroll
           for (uint32_t g = 0; g < SPLIT_MAXG; g++) {
@@ -3094,12 +3124,18 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
           for (uint32_t w = 0; w < NW; w++)
             if (dw == w) acc[w] += h[st];
           if (!s_plan.alias[gk]) {  // (a multi-unit stem's groups share one `now`)
-            const Rec x = rec[e[st]];
-            const uint32_t f = s_plan.fam[gk], d = div_of(s_lunit[f]);
-            if (x.now != s_lnow[f])
-              atomicOr(&s_fl[gk], x.now / d != s_lnow[f] / d ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR);
-            // a lone group of one element is a key seen once (k_table's singleton part)
-            if (s_cnt[gk] == 1) rec[e[st]].lu = x.lu & ~(FLAG_DUP << 24);
+            const uint32_t f = s_plan.fam[gk];
+            // (the head's family: k_run_check compared `now` with the head's,
+            // s_lnow[0]; only an element whose clock differs is read again)
+            const bool known = f == 0 && s_cnt[gk] != 1 && !(fu[st] & SPLIT_POS_NOWVAR);
+            if (!known) {
+              const Rec x = rec[e[st]];
+              const uint32_t d = div_of(s_lunit[f]);
+              if (x.now != s_lnow[f])
+                atomicOr(&s_fl[gk], x.now / d != s_lnow[f] / d ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR);
+              // a lone group of one element is a key seen once (k_table's singleton part)
+              if (s_cnt[gk] == 1) rec[e[st]].lu = x.lu & ~(FLAG_DUP << 24);
+            }
           }
         }
 #pragma unroll
