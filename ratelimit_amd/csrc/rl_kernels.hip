@@ -2631,6 +2631,7 @@ __device__ __attribute__((always_inline)) inline uint32_t block_compact(uint32_t
 // byte (0 = the head's stem, family 0; SPLIT_POS_OTHER = another stem;
 // SPLIT_POS_SKIP = a failed descriptor) | bit 16: `now` differs from the head's
 constexpr uint32_t SPLIT_POS_OTHER = 0xFFu, SPLIT_POS_SKIP = 0xFEu, SPLIT_POS_NOWVAR = 1u << 16;
+constexpr uint32_t SPLIT_ULIST = 1024;  // split_long_body: other stems' positions listed in LDS
 
 // k_run_check marks every descriptor whose sort key occurs twice or more in the
 // batch (FLAG_DUP in its record, one plain store per descriptor: the thread of
@@ -2861,7 +2862,7 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
   __shared__ uint32_t s_wc[NW][SPLIT_MAXG], s_wh[NW][SPLIT_MAXG], s_wp[NW][SPLIT_MAXG], s_ws[NW];
   __shared__ uint32_t s_cnt[SPLIT_MAXG], s_base[SPLIT_MAXG], s_id[SPLIT_MAXG], s_fl[SPLIT_MAXG], s_off[SPLIT_MAXG];
   __shared__ uint32_t s_lnow[SPLIT_MAXG], s_lunit[SPLIT_MAXG], s_fmask[SPLIT_MAXG], s_fnv[SPLIT_MAXG];
-  __shared__ uint32_t s_bad, s_lead;
+  __shared__ uint32_t s_bad, s_lead, s_nu, s_ul[SPLIT_ULIST];
   __shared__ SplitPlan s_plan;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -2876,7 +2877,10 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
 #define SPLIT_STAMP(i)
 #endif
     __syncthreads();  // the previous run's shared state has been read
-    if (tid == 0) s_bad = 0;
+    if (tid == 0) {
+      s_bad = 0;
+      s_nu = 0;
+    }
     if (tid < SPLIT_MAXG) {
       s_fmask[tid] = 0;
       s_fnv[tid] = 0;
@@ -2904,6 +2908,9 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
       // family 0, the head's stem: from k_run_check's comparison of every
       // element with the head (one coalesced pass; the records and stems of
       // a hot stem's tens of thousands of descriptors are not read again)
+      // The other stems' positions (few: stems that share the hot stem's sort
+      // key by chance) are listed in LDS, so the family passes below visit
+      // only them (past SPLIT_ULIST of them: the whole run)
       uint32_t fm0 = 0, nv0 = 0;
       for (uint32_t k = tid + 1; k < L; k += NT) {
         const uint32_t v = grp[p + k], lo = v & 0xFFu;
@@ -2912,6 +2919,9 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
         } else if (lo == 0) {
           fm0 |= 1u << (((v >> 8) & 0xFFu) - 1);
           nv0 |= (v & SPLIT_POS_NOWVAR) ? 1u : 0u;
+        } else {
+          const uint32_t j = atomicAdd(&s_nu, 1u);
+          if (j < SPLIT_ULIST) s_ul[j] = k;
         }
       }
       if (tid == 0) {
@@ -2926,10 +2936,44 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
       if (nv0) s_fnv[0] = 1;
       NF = 1;
       __syncthreads();
+      const uint32_t nu = s_nu;
       // families, as in k_split: the first unassigned element leads, and every
-      // element with its stem joins (records read SPLIT_UNROLL at a time: the
-      // scan is a chain of random reads)
-      for (;;) {
+      // element with its stem joins
+      for (; nu <= SPLIT_ULIST;) {  // (the listed positions only)
+        if (tid == 0) s_lead = 0xFFFFFFFFu;
+        __syncthreads();
+        for (uint32_t j = tid; j < nu; j += NT)
+          if ((grp[p + s_ul[j]] & 0xFFu) == 0xFFu) atomicMin(&s_lead, s_ul[j]);
+        __syncthreads();
+        const uint32_t ld = s_lead;
+        if (ld == 0xFFFFFFFFu || s_bad || NF == SPLIT_MAXG) break;  // (uniform)
+        const Rec y = rec[sv[p + ld]];
+        const Key ky = key_of(b, y);
+        if (tid == 0) {
+          s_lnow[NF] = y.now;
+          s_lunit[NF] = rec_unit(y);
+        }
+        uint32_t fm = 0, nv = 0;
+        for (uint32_t j = tid; j < nu; j += NT) {
+          const uint32_t k = s_ul[j];
+          if ((grp[p + k] & 0xFFu) != 0xFFu) continue;
+          const Rec x = rec[sv[p + k]];
+          if (x.hlo != y.hlo || (x.lu & 0xFFFFu) != (y.lu & 0xFFFFu)) continue;
+          if (!key_equal(key_of(b, x), ky)) {
+            s_bad = 1;  // equal 64-bit hash, different stem
+          } else {
+            grp[p + k] = NF | (rec_unit(x) << 8);
+            fm |= 1u << (rec_unit(x) - 1);
+            nv |= x.now != y.now;
+          }
+        }
+        if (fm) atomicOr(&s_fmask[NF], fm);
+        if (nv) s_fnv[NF] = 1;
+        NF++;
+        __syncthreads();
+      }
+      // (records read SPLIT_UNROLL at a time: the scan is a chain of random reads)
+      for (; nu > SPLIT_ULIST;) {
         if (tid == 0) s_lead = 0xFFFFFFFFu;
         __syncthreads();
         for (uint32_t k = tid; k < L; k += NT)
