@@ -1321,7 +1321,7 @@ __device__ inline SegPair seg_chunk_scan(const SegChunk& c, uint32_t lane) {
 // in LDS; failing that, the three passes run chunk by chunk through HBM.
 // ===========================================================================
 constexpr uint32_t BK_HEAVY = BIG_HEAVY;  // heavy keys peeled off a large bucket
-constexpr uint32_t BK_HEAVY_MIN = 3;  // ... seen at least this often among 64 samples
+constexpr uint32_t BK_HEAVY_MIN = 3;  // ... seen at least this often among the samples (sample_heavy)
 
 template <uint32_t W, uint32_t IT>
 struct BkShape {
@@ -1797,27 +1797,56 @@ constexpr uint32_t BIG_CHUNK = BkSmall::CAP;
 constexpr uint32_t BIG_LIGHT_CAP = BkBig::CAP;
 constexpr uint32_t BIG_CNT = 1 + 2 * BK_HEAVY;  // per work item: light count, class counts, class hit sums
 
-// Hot keys of a large bucket: 64 evenly spaced positions are sampled by wave
-// 0; keys seen at least BK_HEAVY_MIN times become L.heavy[0..L.nheavy).
+// Hot keys of a large bucket: 256 evenly spaced positions are sampled by wave
+// 0 (4 per lane); keys seen at least BK_HEAVY_MIN times become
+// L.heavy[0..L.nheavy). (64 samples missed a second hot key of ~8 % of the
+// bucket now and then: its elements then overflowed the light part's LDS
+// capacity and the whole bucket took the one-workgroup radix path, ~0.8 ms.)
+constexpr uint32_t BK_SAMPLES_PER_LANE = 4;
 template <typename B>
 __device__ inline void sample_heavy(BucketLds<B>& L, uint32_t S, uint32_t ntiles, const uint4* __restrict__ pt) {
+  constexpr uint32_t R = BK_SAMPLES_PER_LANE, NS = 64 * R;
   const uint32_t lane = threadIdx.x & 63;
   if ((threadIdx.x >> 6) == 0) {
-    uint32_t p[1] = {(uint32_t)(((uint64_t)(2 * lane + 1) * S) >> 7)}, j[1];
+    uint32_t p[R], j[R], ks[R], cnt[R];
+    bool first[R];
+#pragma unroll
+    for (uint32_t i = 0; i < R; i++) p[i] = (uint32_t)(((uint64_t)(2 * (lane * R + i) + 1) * S) / (2 * NS));
     bucket_src(ntiles, p, j);
-    const uint32_t ks = pt[j[0]].x;
-    uint32_t cnt = 0;
-    bool first = true;
-    for (uint32_t q = 0; q < 64; q++) {
-      const uint32_t kq = __shfl(ks, q, 64);
-      cnt += kq == ks ? 1u : 0u;
-      if (q < lane && kq == ks) first = false;
+#pragma unroll
+    for (uint32_t i = 0; i < R; i++) {
+      ks[i] = pt[j[i]].x;
+      cnt[i] = 0;
+      first[i] = true;
     }
-    const bool cand = first && cnt >= BK_HEAVY_MIN;
-    const uint64_t b = __ballot(cand);
-    const uint32_t rank = __popcll(b & ((1ull << lane) - 1));
-    if (cand && rank < BK_HEAVY) L.heavy[rank] = ks;
-    if (lane == 0) L.nheavy = min((uint32_t)__popcll(b), BK_HEAVY);
+    for (uint32_t q = 0; q < 64; q++) {
+#pragma unroll
+      for (uint32_t r = 0; r < R; r++) {
+        const uint32_t kq = __shfl(ks[r], q, 64), g = q * R + r;
+#pragma unroll
+        for (uint32_t i = 0; i < R; i++) {
+          cnt[i] += kq == ks[i] ? 1u : 0u;
+          if (g < lane * R + i && kq == ks[i]) first[i] = false;
+        }
+      }
+    }
+    uint32_t nc = 0;  // this lane's candidates, ranked across the wave
+#pragma unroll
+    for (uint32_t i = 0; i < R; i++) nc += (first[i] && cnt[i] >= BK_HEAVY_MIN) ? 1u : 0u;
+    uint32_t incl = nc;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    uint32_t rank = incl - nc;
+#pragma unroll
+    for (uint32_t i = 0; i < R; i++)
+      if (first[i] && cnt[i] >= BK_HEAVY_MIN) {
+        if (rank < BK_HEAVY) L.heavy[rank] = ks[i];
+        rank++;
+      }
+    if (lane == 63) L.nheavy = min(incl, BK_HEAVY);
   }
   __syncthreads();
 }
