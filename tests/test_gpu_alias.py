@@ -65,6 +65,15 @@ def test_gpu_hot_override_stream_vs_c_oracle(lc, isolate):
 
 
 @pytest.mark.parametrize("lc", [False, True])
+def test_gpu_hot_override_ten_thousand_element_runs_vs_c_oracle(lc):
+    """60k requests per batch: the hottest stems' runs (~10k and ~5k
+    descriptors under two units, the size class of C2U's 58k-element runs)
+    through split_long_body's chunked wave walks, across a minute boundary
+    (+40: one shared key, a lone alias group)."""
+    _check(_stream([38, 39, 40, 41], rpb=60_000, seed=9), lc, table_slots=1 << 17, max_batch=1 << 17)
+
+
+@pytest.mark.parametrize("lc", [False, True])
 def test_gpu_override_on_and_off_vs_c_oracle(lc):
     """Batches with and without overrides, repeated and backward clocks: stems
     flagged multi-unit in the table take alias_setup alone (records of the
