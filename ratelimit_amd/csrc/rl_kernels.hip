@@ -2867,13 +2867,14 @@ __device__ inline uint32_t split_group_flags(const SplitPlan& S, uint32_t g, uin
 // critical path, 1-3 %, profiles/r02/ab/long_*.)
 constexpr uint32_t SPLIT_UNROLL = 8;
 #ifndef RL_SPLIT_ST
-#define RL_SPLIT_ST 16  // (8: C2U 3.33-3.42 G, 16: 3.52-3.53 G; 4: 2.2-3.2 G)
+#define RL_SPLIT_ST 16  // (8: C2U 3.33-3.42 G, 16: 3.52-3.53 G; 4: 2.2-3.2 G; 32 in round 4: C2 -2 %, C2U flat)
 #endif
 constexpr uint32_t SPLIT_ST = RL_SPLIT_ST;  // 64-element steps in flight per wave in split_long_body's walks
 // k_split's workgroup (a long run is reordered by its waves, each walking a
 // chunk of it: more waves, shorter walks, but slower short runs)
 #ifndef RL_SPLIT_THREADS
-#define RL_SPLIT_THREADS 256  // (1024: C2U's 58k-element runs 481 -> 377 us, but C1's k_split 18 -> 26 us)
+#define RL_SPLIT_THREADS 256  // (1024: C2U's 58k-element runs 481 -> 377 us, but C1's k_split 18 -> 26 us;
+                              //  512 in round 4: C2U +2.4 %, C2 -4 %, C1 -1.5 %)
 #endif
 constexpr uint32_t SPLIT_THREADS = RL_SPLIT_THREADS;
 
