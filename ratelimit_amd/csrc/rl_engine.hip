@@ -263,7 +263,8 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
        dalloc(&s.defer, n) == hipSuccess &&
        dalloc(&s.defer_n, 1) == hipSuccess && dalloc(&s.defer2, n) == hipSuccess &&
        dalloc(&s.defer1, n) == hipSuccess && dalloc(&s.defer1_n, 1) == hipSuccess &&
-       dalloc(&s.defer2_n, 1) == hipSuccess && dalloc(&s.fast_blk, (size_t)n / (256 * 32) + 1) == hipSuccess;
+       dalloc(&s.defer2_n, 1) == hipSuccess && dalloc(&s.fast_blk, (size_t)n / (256 * 32) + 1) == hipSuccess &&
+       dalloc(&s.uniq, n) == hipSuccess && dalloc(&s.uniq_n, 1) == hipSuccess;
   ok = ok && dalloc(&s.hits_s, n) == hipSuccess && dalloc(&s.segsum, n) == hipSuccess &&
        dalloc(&s.rid, n) == hipSuccess && dalloc(&s.run_start, (size_t)n + 1) == hipSuccess &&
        dalloc(&s.run_flags, n) == hipSuccess && dalloc(&s.run_state, n) == hipSuccess && dalloc(&s.run_alias, n) == hipSuccess &&
@@ -281,7 +282,8 @@ void free_buffer(Scratch& s) {
   void* bufs[] = {s.rec, s.res, s.big_meta, s.big_n, s.big_work, s.work_n, s.sorted_n, s.big_cnt, s.keys[0], s.keys[1],
                   s.vals[0], s.vals[1], s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1,
                   s.defer1_n, s.fast_blk, s.hits_s, s.segsum, s.rid, s.run_start, s.run_flags, s.run_state, s.run_alias,
-                  s.run_f, s.runs64, s.split, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t, s.r_base};
+                  s.run_f, s.runs64, s.split, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t, s.r_base,
+                  s.uniq, s.uniq_n};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
 }

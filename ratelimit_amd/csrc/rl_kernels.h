@@ -172,6 +172,12 @@ struct Scratch {
   uint32_t* defer1;               // keys seen once k_table found to need the exact path (arrival indices)
   uint32_t* defer1_n;
   uint32_t* fast_blk;             // bit per 256-descriptor block holding a RUN_FAST run (k_table -> k_late)
+  // the keys seen once, listed bucket by bucket ({arrival index, sort key}):
+  // k_table's singleton part walks them in this order, so a workgroup's
+  // table probes stay inside the 1/1024 of the table its bucket's home slots
+  // fall in (address-translation reach, tools/tlbprobe.hip)
+  uint2* uniq;
+  uint32_t* uniq_n;
   unsigned long long* stripes;    // STAT_STRIPES x STAT_LDS_RULES x RL_NUM_STATS
   // run segmentation (sorted order)
   uint32_t* hits_s;                    // [n] raw hits, sorted order

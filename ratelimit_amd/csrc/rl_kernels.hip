@@ -50,7 +50,8 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
                                                  const int64_t* time_floor, uint32_t* defer_n,
                                                  uint32_t* big_n, uint32_t* work_n, uint32_t* __restrict__ run_flags,
                                                  unsigned long long* num_runs, uint32_t* __restrict__ hit_a,
-                                                 unsigned long long* __restrict__ res, uint32_t* sorted_n) {
+                                                 unsigned long long* __restrict__ res, uint32_t* sorted_n,
+                                                 uint32_t* uniq_n) {
   __shared__ uint32_t lds[HASH_LDS_BYTES / 4 + 4];
   const uint32_t tid = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + tid;
@@ -62,6 +63,7 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
     *big_n = 0;
     *work_n = 0;
     *sorted_n = 0;
+    *uniq_n = 0;
   }
   const int64_t floor = *time_floor;
   auto time_bad = [&](int64_t t) { return t < 0 || t > (int64_t)NOW_MAX || t < floor; };
@@ -1490,6 +1492,7 @@ struct BucketLds {
   uint32_t acc[1 + 2 * BK_HEAVY];     // k_big_place: sums over the bucket's earlier chunks
   uint32_t lw[B::WAVES];              // per-wave light counts of a chunk
   uint32_t nheavy, nlight;
+  uint32_t ub;                        // k_bucket: this bucket's first entry in the keys-seen-once list
 };
 
 extern __shared__ uint32_t bk_seg[];  // [ntiles + 1] segment starts, then [ntiles] sources
@@ -1857,7 +1860,7 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
     uint32_t* __restrict__ sh, uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
     uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end, unsigned long long* num_runs,
     uint32_t* __restrict__ drun, BigMeta* __restrict__ meta, uint32_t* big_n, uint32_t* __restrict__ work,
-    uint32_t* work_n, uint32_t* sorted_n, const uint32_t* err) {
+    uint32_t* work_n, uint32_t* sorted_n, uint2* __restrict__ uniq, uint32_t* uniq_n, const uint32_t* err) {
   using B = BkSmall;
   __shared__ BucketLds<B> L;
   if (*err) return;
@@ -1906,12 +1909,14 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
     hh[i] = e.z;
   }
   BK_STAMP(d, 2);
-  // Keys seen once in the batch never enter the sorted order (k_table answers
-  // them in arrival order): every descriptor of a key falls in its bucket, so
-  // an LDS hash of the bucket's keys finds the duplicated ones (~5% at C1),
-  // and only those are sorted, segmented and written. Their sorted positions
-  // are one block per bucket, allocated from sorted_n (runs never cross
-  // buckets, so no order between buckets is needed).
+  // Keys seen once in the batch never enter the sorted order: every
+  // descriptor of a key falls in its bucket, so an LDS hash of the bucket's
+  // keys finds the duplicated ones (~5% at C1), and only those are sorted,
+  // segmented and written. Their sorted positions are one block per bucket,
+  // allocated from sorted_n (runs never cross buckets, so no order between
+  // buckets is needed). The keys seen once are listed, bucket by bucket, for
+  // k_table's singleton part: their home slots share the bucket's top 10
+  // bits, so a workgroup walking the list probes 1/1024 of the table.
   uint32_t* ht = L.v;                                   // [2 CAP]: L.v and L.h (values are in registers)
   uint8_t* df = reinterpret_cast<uint8_t*>(&L.wcnt[0][0]);  // [CAP] duplicated-key flag per position
   static_assert(sizeof(L.wcnt) >= B::CAP, "dup flags fit the multisplit rows");
@@ -1942,27 +1947,34 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
     }
   }
   __syncthreads();
-  // compact the duplicated elements, keeping the bucket (= arrival) order
+  // compact the duplicated elements, keeping the bucket (= arrival) order,
+  // and rank the keys seen once for the list
   const uint64_t lt = (1ull << lane) - 1;
-  uint32_t cidx[B::ITEMS], wc = 0, dmask = 0;
+  uint32_t cidx[B::ITEMS], sidx[B::ITEMS], wc = 0, ws = 0, dmask = 0, smask = 0;
 #pragma unroll
   for (uint32_t i = 0; i < B::ITEMS; i++) {
     const uint32_t p = strip0 + i * 64 + lane;
-    const bool dup = p < S && df[p];
-    const uint64_t bl = __ballot(dup);
+    const bool dup = p < S && df[p], one = p < S && !df[p];
+    const uint64_t bl = __ballot(dup), bs = __ballot(one);
     cidx[i] = wc + (uint32_t)__popcll(bl & lt);
+    sidx[i] = ws + (uint32_t)__popcll(bs & lt);
     wc += (uint32_t)__popcll(bl);
+    ws += (uint32_t)__popcll(bs);
     dmask |= dup ? 1u << i : 0u;
+    smask |= one ? 1u << i : 0u;
   }
-  if (lane == 0) L.wsum[wave] = wc;
+  if (lane == 0) {
+    L.wsum[wave] = wc;
+    L.lw[wave] = ws;
+  }
   __syncthreads();
-  uint32_t wpre = 0, M = 0;
+  uint32_t wpre = 0, M = 0, spre = 0;
 #pragma unroll
   for (uint32_t w = 0; w < B::WAVES; w++) {
     wpre += w < wave ? L.wsum[w] : 0u;
+    spre += w < wave ? L.lw[w] : 0u;
     M += L.wsum[w];
   }
-  if (!M) return;  // (uniform) every key of the bucket is seen once
 #pragma unroll
   for (uint32_t i = 0; i < B::ITEMS; i++) {
     if (!((dmask >> i) & 1u)) continue;
@@ -1971,8 +1983,16 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
     L.v[c] = vv[i];
     L.h[c] = hh[i];
   }
-  if (tid == 0) L.base_pos = atomicAdd(sorted_n, M);
+  if (tid == 0) {
+    if (M) L.base_pos = atomicAdd(sorted_n, M);
+    L.ub = M < S ? atomicAdd(uniq_n, S - M) : 0u;
+  }
   __syncthreads();
+  const uint32_t ub = L.ub + spre;
+#pragma unroll
+  for (uint32_t i = 0; i < B::ITEMS; i++)
+    if ((smask >> i) & 1u) uniq[ub + sidx[i]] = make_uint2(vv[i], kk[i]);
+  if (!M) return;  // (uniform) every key of the bucket is seen once
   const uint32_t base = L.base_pos;
   if (M <= 64) {
     // one wave: stable rank of (key, compact index) by comparisons
@@ -2680,14 +2700,30 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
                                                    uint32_t* defer_n, const uint32_t* err,
                                                    const unsigned long long* num_runs, unsigned long long* split,
                                                    const uint32_t* sorted_n, uint32_t* __restrict__ pos_unit,
-                                                   uint32_t* __restrict__ pos_hits) {
+                                                   uint32_t* __restrict__ pos_hits, uint2* __restrict__ uniq,
+                                                   uint32_t* uniq_n) {
   __shared__ uint32_t s_list[RC_CHUNK], s_cnt;
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // k_split's reservations start from the bucket kernels' count
     split[0] = 0;
     split[1] = *num_runs;
   }
   if (*err) return;
-  const uint32_t lo = max(blockIdx.x * RC_CHUNK, 1u), hi = min(blockIdx.x * RC_CHUNK + RC_CHUNK, *sorted_n);
+  const uint32_t sn = *sorted_n;
+  // a run of one (a large bucket sorts every element, light keys included) is
+  // a key seen once: onto the list of k_table's singleton part
+  for (uint32_t q0 = blockIdx.x * RC_CHUNK; q0 < min(blockIdx.x * RC_CHUNK + RC_CHUNK, sn); q0 += blockDim.x) {
+    const uint32_t q = q0 + threadIdx.x;
+    const uint32_t k = q < sn ? skeys[q] : 0u;
+    const bool one = q < sn && (q == 0 || skeys[q - 1] != k) && (q + 1 >= sn || skeys[q + 1] != k);
+    const uint64_t m = __ballot(one);
+    if (!m) continue;  // (wave-uniform)
+    const uint32_t lane = threadIdx.x & 63, leader = (uint32_t)__ffsll((unsigned long long)m) - 1;
+    uint32_t at = 0;
+    if (lane == leader) at = atomicAdd(uniq_n, (uint32_t)__popcll(m));
+    at = __shfl(at, leader, 64) + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    if (one) uniq[at] = make_uint2(rec_s.sv[q], k);
+  }
+  const uint32_t lo = max(blockIdx.x * RC_CHUNK, 1u), hi = min(blockIdx.x * RC_CHUNK + RC_CHUNK, sn);
   if (lo >= hi) return;
   // non-head positions (the second and later descriptors of a run)
   const uint32_t cnt = block_compact(lo, hi, s_list, &s_cnt, [&](uint32_t q) { return skeys[q - 1] == skeys[q]; });
@@ -2710,6 +2746,9 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
       // FLAG_DUP (k_table's singleton part answers both) and the run is
       // emptied (its sorted path skips it); no k_split pass.
       run_end[r] = p;
+      const uint32_t at = atomicAdd(uniq_n, 2u);
+      uniq[at] = make_uint2(ep, skeys[q]);
+      uniq[at + 1] = make_uint2(eq, skeys[q]);
       continue;
     }
     rec[eq].lu = x.lu | (FLAG_DUP << 24);
@@ -2878,6 +2917,15 @@ constexpr uint32_t SPLIT_ST = RL_SPLIT_ST;  // 64-element steps in flight per wa
 #endif
 constexpr uint32_t SPLIT_THREADS = RL_SPLIT_THREADS;
 
+// The keys-seen-once list (Scratch::uniq) as k_split appends to it: a lone
+// one-element group is a key seen once (rare: one atomic each).
+struct UniqList {
+  uint2* list;
+  uint32_t* n;
+  const uint32_t* skeys;  // sorted keys: a run shares its sort key
+  __device__ inline void push(uint32_t e, uint32_t p) const { list[atomicAdd(n, 1u)] = make_uint2(e, skeys[p]); }
+};
+
 template <uint32_t NT>
 __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j, uint32_t r, uint32_t p, uint32_t L, BatchDev b,
                                                           SRec rec_s, uint32_t* svals, uint32_t* segsum,
@@ -2887,7 +2935,8 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
                                                           unsigned long long* num_runs, unsigned long long* split,
                                                           uint32_t* __restrict__ drun, uint32_t drun_cap, uint32_t* grp,
                                                           uint32_t* rank, uint32_t* __restrict__ pos_hits,
-                                                          uint32_t* __restrict__ hnew, int per_second, uint32_t rfl) {
+                                                          uint32_t* __restrict__ hnew, int per_second, uint32_t rfl,
+                                                          const UniqList& uq) {
   constexpr uint32_t NW = NT / 64;
   __shared__ uint32_t s_wc[NW][SPLIT_MAXG], s_wh[NW][SPLIT_MAXG], s_wp[NW][SPLIT_MAXG], s_ws[NW];
   __shared__ uint32_t s_cnt[SPLIT_MAXG], s_base[SPLIT_MAXG], s_id[SPLIT_MAXG], s_fl[SPLIT_MAXG], s_off[SPLIT_MAXG];
@@ -3208,7 +3257,10 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
               if (x.now != s_lnow[f])
                 atomicOr(&s_fl[gk], x.now / d != s_lnow[f] / d ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR);
               // a lone group of one element is a key seen once (k_table's singleton part)
-              if (s_cnt[gk] == 1) rec[e[st]].lu = x.lu & ~(FLAG_DUP << 24);
+              if (s_cnt[gk] == 1) {
+                rec[e[st]].lu = x.lu & ~(FLAG_DUP << 24);
+                uq.push(e[st], p);
+              }
             }
           }
         }
@@ -3309,7 +3361,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_split(BatchDev b, SRec rec_s,
                                                unsigned long long* split, uint32_t* __restrict__ drun,
                                                uint32_t drun_cap, uint32_t* grp, uint32_t* rank,
                                                uint32_t* __restrict__ pos_hits, uint32_t* __restrict__ hnew,
-                                               const uint32_t* err, int per_second) {
+                                               const uint32_t* err, int per_second, UniqList uq) {
   __shared__ uint32_t s_e[SPLIT_CAP], s_hlo[SPLIT_CAP], s_lu[SPLIT_CAP], s_now[SPLIT_CAP], s_h[SPLIT_CAP];
   __shared__ uint32_t s_nh[SPLIT_CAP];           // max(1, hits) in the new order
   __shared__ uint16_t s_pos[SPLIT_CAP];          // rank inside the element's group
@@ -3329,7 +3381,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_split(BatchDev b, SRec rec_s,
     if (L > SPLIT_CAP) {  // (uniform)
       split_long_body<SPLIT_THREADS>(j, r, p, L, b, rec_s, svals, segsum, rid, run_start, run_end, run_flags, defer,
                                      num_runs, split, drun, drun_cap, grp, rank, pos_hits, hnew, per_second,
-                                     run_flags[r]);
+                                     run_flags[r], uq);
       continue;
     }
     __syncthreads();  // the previous run's shared state has been read
@@ -3454,7 +3506,10 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_split(BatchDev b, SRec rec_s,
         if (s_now[k] != s_lnow[f])
           atomicOr(&s_fl[g], s_now[k] / d != s_lnow[f] / d ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR);
         // a lone group of one element is a key seen once (k_table's singleton part)
-        if (s_cnt[g] == 1) rec[s_e[k]].lu = s_lu[k] & ~(FLAG_DUP << 24);
+        if (s_cnt[g] == 1) {
+          rec[s_e[k]].lu = s_lu[k] & ~(FLAG_DUP << 24);
+          uq.push(s_e[k], p);
+        }
       }
     }
     __syncthreads();
@@ -3492,22 +3547,42 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_split(BatchDev b, SRec rec_s,
 }
 
 // ---- k_table, keys seen once (unique_body): sort key once in the batch (no
-// FLAG_DUP), one lane each in ARRIVAL order: the record, the sort key and
-// the stem are coalesced wave reads (consecutive descriptors sit side by side
-// in the packed batch), the result a coalesced store; only the slot's first
-// sector (and the changed window record) is a random access. Such a stem has
-// no other descriptor in the batch, so the lanes are independent and this
-// part commutes with the sorted path (runs_body). A stem that lives in the
-// table under another unit too is left to k_runs_general (defer1).
+// FLAG_DUP), one lane each. Such a stem has no other descriptor in the batch,
+// so the lanes are independent and this part commutes with the sorted path
+// (runs_body). A stem that lives in the table under another unit too is left
+// to k_runs_general (defer1). Two orders, chosen per batch on the device:
+//  * a batch made mostly of keys seen once (C1, C3) is answered in ARRIVAL
+//    order: the record, the sort key and the stem are coalesced wave reads
+//    (consecutive descriptors sit side by side in the packed batch), the
+//    result a coalesced store; only the slot's first sector (and the changed
+//    window record) is a random access. A block with >= 75% of them answers in
+//    place, a sparser one compacts them onto its first lanes;
+//  * a sparser batch (hot keys, C2) walks the list the stage-A kernels leave
+//    (Scratch::uniq, bucket by bucket): every workgroup is full, and the
+//    record, stem and result are gathers. C2 4.83 -> 5.29 G (profiles/r05/).
+//    At C1 the gathers cost more than the list order saves on the table
+//    probes (a workgroup's probes inside 1/1024 of the table): 5.35 vs 5.99 G
+//    with the list for every batch; tools/orderprobe.hip prices the whole
+//    access pattern per order and layout (profiles/r05/orderprobe.txt).
+#ifndef RL_UNIQ_DENSE
+#define RL_UNIQ_DENSE 3  // (A/B builds: quarters of the batch below which the list is walked; 5 = always, 0 = never)
+#endif
 __device__ __attribute__((always_inline)) inline void unique_body(uint32_t blk, BatchDev b, TableDev t, Params P, const Rec* __restrict__ rec,
-                                                const uint32_t* __restrict__ keys0, unsigned long long* __restrict__ res,
+                                                const uint32_t* __restrict__ keys0,
+                                                const uint2* __restrict__ uniq, const uint32_t* uniq_n,
+                                                unsigned long long* __restrict__ res,
                                                 uint32_t* __restrict__ defer1, uint32_t* defer1_n,
                                                 unsigned long long* stats, unsigned long long* stripes, uint32_t* err,
                                                 uint32_t* errs, int restore) {
-  __shared__ uint32_t s_err, s_cnt, s_list[256];
-  if (threadIdx.x == 0) s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __shared__ uint32_t s_err, s_nu, s_cnt, s_list[256];
+  if (threadIdx.x == 0) {
+    s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_nu = *uniq_n;
+  }
   __syncthreads();
-  const uint32_t lo = blk * 256, hi = min(lo + 256, b.n);
+  const uint32_t nu = s_nu;
+  const bool by_list = (uint64_t)nu * 4 < (uint64_t)b.n * RL_UNIQ_DENSE;  // (uniform) fewer than 75% keys seen once
+  const uint32_t lo = blk * 256, hi = min(lo + 256, by_list ? nu : b.n);
   if (s_err || lo >= hi) return;
   if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
   uint32_t* ferr = P.isolate ? errs : err;
@@ -3518,22 +3593,28 @@ __device__ __attribute__((always_inline)) inline void unique_body(uint32_t blk, 
   L.reset();
   // not a duplicated key (the sorted path's), not failed (answered already)
   auto single = [&](uint32_t i) { return !((rec[i].lu >> 24) & (FLAG_SKIP | FLAG_DUP)); };
-  const uint32_t i0 = lo + threadIdx.x;
-  const bool own = i0 < hi && single(i0);
-  // A dense block (the bulk at C1/C3) answers in place, lane by lane; a sparse
-  // one (hot-key batches) compacts its keys seen once onto the first lanes.
   bool act;
-  uint32_t i;
-  if (__syncthreads_count(own) >= 192) {
-    act = own;
-    i = i0;
+  uint32_t i, key = 0;
+  if (by_list) {
+    const uint32_t pos = lo + threadIdx.x;
+    const uint2 ent = pos < hi ? uniq[pos] : make_uint2(0u, 0u);
+    i = ent.x;
+    key = ent.y;
+    act = pos < hi && single(i);
   } else {
-    const uint32_t cnt = block_compact(lo, hi, s_list, &s_cnt, single);
-    act = threadIdx.x < cnt;
-    i = act ? s_list[threadIdx.x] : 0u;
+    const uint32_t i0 = lo + threadIdx.x;
+    const bool own = i0 < hi && single(i0);
+    if (__syncthreads_count(own) >= 192) {
+      act = own;
+      i = i0;
+    } else {
+      const uint32_t cnt = block_compact(lo, hi, s_list, &s_cnt, single);
+      act = threadIdx.x < cnt;
+      i = act ? s_list[threadIdx.x] : 0u;
+    }
+    if (act) key = keys0[i];
   }
   if (act) {
-    const uint32_t key = keys0[i];
     const Rec x = rec[i];
     {
       const uint64_t h0 = ((uint64_t)key << 32) | x.hlo;
@@ -4311,13 +4392,14 @@ __global__ __launch_bounds__(256, RL_KTABLE_WAVES) void k_table(uint32_t g_runs,
                                                const uint32_t* __restrict__ keys0, uint32_t* __restrict__ defer1,
                                                uint32_t* defer1_n, unsigned long long* stats,
                                                unsigned long long* stripes, uint32_t* err, uint32_t* errs, int restore,
-                                               uint32_t* __restrict__ fast_blk) {
+                                               uint32_t* __restrict__ fast_blk, const uint2* __restrict__ uniq,
+                                               const uint32_t* uniq_n) {
   if (blockIdx.x < g_runs)
     runs_body(blockIdx.x, b, t, P, rec_s, skeys, svals, res, run_start, run_end, run_flags, run_state, run_alias, rid,
               run_f, num_runs, drun, defer2, defer2_n, stats, stripes, err, errs, restore, fast_blk);
   else
-    unique_body(blockIdx.x - g_runs, b, t, P, rec_s.rec, keys0, res, defer1, defer1_n, stats, stripes, err, errs,
-                restore);
+    unique_body(blockIdx.x - g_runs, b, t, P, rec_s.rec, keys0, uniq, uniq_n, res, defer1, defer1_n, stats, stripes,
+                err, errs, restore);
 }
 
 // k_late (after k_table, and k_fast_over with the local cache on): the exact
@@ -4587,7 +4669,7 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
   if (ev) (void)hipEventRecord(ev[0], st);
   if (g0)
     k_prepare<<<g0, 256, 0, st>>>(b, s.rec, s.keys[0], s.err, s.errs, isolate, s.time_floor, s.defer_n, s.big_n,
-                                  s.work_n, s.run_flags, s.runs64, s.hit_a, s.res, s.sorted_n);
+                                  s.work_n, s.run_flags, s.runs64, s.hit_a, s.res, s.sorted_n, s.uniq_n);
   if (ev) (void)hipEventRecord(ev[1], st);
   const uint32_t ptiles = cdiv(b.n, PART_TILE);
   if (b.n)
@@ -4598,7 +4680,8 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
     k_bucket<<<PART_DIGITS, BkSmall::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
                                                              s.keys[1], s.vals[0], s.hits_s, s.segsum, s.rid,
                                                              s.run_start, s.run_end, s.runs64, s.drun, s.big_meta, s.big_n,
-                                                             s.big_work, s.work_n, s.sorted_n, s.err);
+                                                             s.big_work, s.work_n, s.sorted_n, s.uniq, s.uniq_n,
+                                                             s.err);
 #ifndef RL_EXP_NO_BIG  // (measurement builds only: without the large-bucket kernels, C1 has none)
     k_big_count<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
                                                                     s.big_meta, s.big_work, s.work_n, s.big_cnt,
@@ -4613,11 +4696,11 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
 #endif
     k_run_check<<<cdiv(b.n, RC_CHUNK), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[1], s.rid, s.run_start,
                                                 s.run_end, s.run_flags, s.defer, s.defer_n, s.err, s.runs64, s.split,
-                                                s.sorted_n, s.grp, s.hit_t);
+                                                s.sorted_n, s.grp, s.hit_t, s.uniq, s.uniq_n);
     k_split<<<SPLIT_BLOCKS, SPLIT_THREADS, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.vals[0], s.segsum, s.rid, s.run_start,
                                           s.run_end, s.run_flags, s.defer, s.defer_n, s.runs64, s.split, s.drun,
                                           b.n / 2 + BIG_HEAVY * PART_DIGITS, s.grp, s.lead, s.hit_t, s.vals[1], s.err,
-                                          per_second);
+                                          per_second, UniqList{s.uniq, s.uniq_n, s.keys[1]});
   }
 }
 
@@ -4647,7 +4730,7 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
                                          s.run_flags, s.run_state, s.run_alias, s.rid, s.run_f, s.runs64, s.drun,
                                          s.defer2, s.defer2_n,
                                          s.keys[0], s.defer1, s.defer1_n, o.stats, s.stripes, s.errb, s.errs, restore,
-                                         s.fast_blk);
+                                         s.fast_blk, s.uniq, s.uniq_n);
     if (ev) (void)hipEventRecord(ev[4], st);
     if (!restore && P.lc_en)
       k_fast_over<<<g, 256, 0, st>>>(s.sorted_n, rs, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
