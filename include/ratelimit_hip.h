@@ -601,7 +601,13 @@ int rl_snapshot_load(rl_ctx* ctx, const void* host, uint64_t bytes);
  * the sums. "segment" runs up to the start of k_table (the table stage's
  * wait for the previous batch included), "table" brackets the single k_table
  * launch (the keys seen once and the short runs: the bulk of the table work),
- * "finish" the rest (deferrals, long runs, outputs). */
+ * "finish" the rest (deferrals, long runs, outputs). With n > RL_NUM_STAGES,
+ * ms[RL_NUM_STAGES] is k_table's own run time per batch, AVERAGED over every
+ * batch since profiling started or was last read (not only the timed
+ * sample): its first workgroup's start to its last workgroup's end on the
+ * device's constant clock (the kernel duration rocprofv3 reports; no event is
+ * recorded for it), where "table" also holds the launch's queueing behind the
+ * other streams' kernels and the event markers' own cost. */
 #define RL_NUM_STAGES 5
 int rl_profile(rl_ctx* ctx, int enable);
 int rl_profile_read(rl_ctx* ctx, double* ms, uint32_t n, uint64_t* batches);

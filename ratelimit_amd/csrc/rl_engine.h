@@ -113,6 +113,10 @@ struct Engine {
   hipEvent_t ev[PROF_RING][RL_NUM_STAGES + 1] = {};
   double stage_ms[RL_NUM_STAGES] = {};
   uint64_t prof_batches = 0;
+  // ... and k_table's own run time on every batch while profiling (device
+  // clock): {sum of durations in ticks, batches}, and the clock's rate (kHz)
+  unsigned long long* d_kt_acc = nullptr;
+  double wclk_khz = 0;
   // config match (rl_config_load / rl_do_limit_requests): the device trie and
   // one growable device buffer carved per call for the raw requests
   uint8_t* cfg_blob = nullptr;  // [nodes | index | prefix ‖ keys]

@@ -146,14 +146,16 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     (void)hipStreamWaitEvent(a, c->consumed[k], 0);  // ... and its routed results were read
     launch_stage_a(b, c->s[k], isolate, P.per_second, a, ev);
     (void)hipStreamWaitEvent(a, c->b_table[c->last], 0);  // table order (not the previous k_finish)
-    launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, c->s[c->last].errb, c->b_table[k]);
+    launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, c->s[c->last].errb, c->b_table[k],
+                   c->prof ? c->d_kt_acc : nullptr);
     (void)hipEventRecord(c->b_done[k], a);
   } else {
     if (!st) st = c->stream;
     (void)after_batches(c, st);
     hipEvent_t* ev = prof_events(c);
     launch_stage_a(b, c->s[k], isolate, P.per_second, st, ev);
-    launch_stage_b(b, o, t, P, c->s[k], restore, st, ev, c->s[c->last].errb, c->b_table[k]);
+    launch_stage_b(b, o, t, P, c->s[k], restore, st, ev, c->s[c->last].errb, c->b_table[k],
+                   c->prof ? c->d_kt_acc : nullptr);
     (void)hipEventRecord(c->b_done[k], st);
   }
   c->last = k;
@@ -264,7 +266,8 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
        dalloc(&s.defer_n, 1) == hipSuccess && dalloc(&s.defer2, n) == hipSuccess &&
        dalloc(&s.defer1, n) == hipSuccess && dalloc(&s.defer1_n, 1) == hipSuccess &&
        dalloc(&s.defer2_n, 1) == hipSuccess && dalloc(&s.fast_blk, (size_t)n / (256 * 32) + 1) == hipSuccess &&
-       dalloc(&s.uniq, n) == hipSuccess && dalloc(&s.uniq_n, 1) == hipSuccess;
+       dalloc(&s.uniq, n) == hipSuccess && dalloc(&s.uniq_n, 1) == hipSuccess &&
+       dalloc(&s.kt_blk, 2 * ((size_t)n / 2 + BIG_HEAVY * PART_DIGITS + 2 * (size_t)n + 512) / 256) == hipSuccess;
   ok = ok && dalloc(&s.hits_s, n) == hipSuccess && dalloc(&s.segsum, n) == hipSuccess &&
        dalloc(&s.rid, n) == hipSuccess && dalloc(&s.run_start, (size_t)n + 1) == hipSuccess &&
        dalloc(&s.run_flags, n) == hipSuccess && dalloc(&s.run_state, n) == hipSuccess && dalloc(&s.run_alias, n) == hipSuccess &&
@@ -283,7 +286,7 @@ void free_buffer(Scratch& s) {
                   s.vals[0], s.vals[1], s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1,
                   s.defer1_n, s.fast_blk, s.hits_s, s.segsum, s.rid, s.run_start, s.run_flags, s.run_state, s.run_alias,
                   s.run_f, s.runs64, s.split, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t, s.r_base,
-                  s.uniq, s.uniq_n};
+                  s.uniq, s.uniq_n, s.kt_blk};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
 }
@@ -479,6 +482,7 @@ void eng_destroy(Engine* c) {
   for (uint32_t k = 0; k < PROF_RING; k++)
     for (int i = 0; i <= RL_NUM_STAGES; i++)
       if (c->ev[k][i]) (void)hipEventDestroy(c->ev[k][i]);
+  if (c->d_kt_acc) (void)hipFree(c->d_kt_acc);
   for (uint32_t k = 0; k < NBUF; k++) {
     free_buffer(c->s[k]);
     if (c->b_done[k]) (void)hipEventDestroy(c->b_done[k]);
@@ -681,9 +685,14 @@ int eng_route_scatter(Engine* c, uint32_t n, const uint32_t* perm, const uint64_
 int eng_profile(Engine* c, int enable) {
   if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  if (enable && !c->ev[0][0])
+  if (enable && !c->ev[0][0]) {
     for (uint32_t k = 0; k < PROF_RING; k++)
       for (int i = 0; i <= RL_NUM_STAGES; i++) HIPCHK(c, hipEventCreate(&c->ev[k][i]));
+    HIPCHK(c, dalloc(&c->d_kt_acc, 2));
+    HIPCHK(c, hipMemset(c->d_kt_acc, 0, 2 * sizeof(unsigned long long)));
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->cfg.device) == hipSuccess) c->wclk_khz = khz;
+  }
   prof_fold_all(c);
   c->prof = enable > 0;
   c->prof_every = enable > 0 ? (uint32_t)enable : 1u;
@@ -696,6 +705,17 @@ int eng_profile_read(Engine* c, double* ms, uint32_t n, uint64_t* batches) {
   HIPCHK(c, hipSetDevice(c->cfg.device));
   prof_fold_all(c);
   for (uint32_t i = 0; i < n && i < RL_NUM_STAGES; i++) ms[i] = c->stage_ms[i];
+  if (n > RL_NUM_STAGES) {
+    ms[RL_NUM_STAGES] = 0;
+    if (c->d_kt_acc) {  // every batch since the last read: their k_finish kernels are done
+      unsigned long long acc[2] = {0, 0};
+      HIPCHK(c, after_batches(c, c->stream));
+      HIPCHK(c, hipMemcpyAsync(acc, c->d_kt_acc, sizeof(acc), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipMemsetAsync(c->d_kt_acc, 0, sizeof(acc), c->stream));
+      if (acc[1] && c->wclk_khz > 0) ms[RL_NUM_STAGES] = (double)acc[0] / (double)acc[1] / c->wclk_khz;
+    }
+  }
   if (batches) *batches = c->prof_batches;
   for (int i = 0; i < RL_NUM_STAGES; i++) c->stage_ms[i] = 0;
   c->prof_batches = 0;

@@ -178,6 +178,7 @@ struct Scratch {
   // fall in (address-translation reach, tools/tlbprobe.hip)
   uint2* uniq;
   uint32_t* uniq_n;
+  unsigned long long* kt_blk;  // [2 x k_table workgroups] start / end stamps (rl_profile)
   unsigned long long* stripes;    // STAT_STRIPES x STAT_LDS_RULES x RL_NUM_STATS
   // run segmentation (sorted order)
   uint32_t* hits_s;                    // [n] raw hits, sorted order
@@ -219,8 +220,12 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
 // errb_prev: the previous batch's table-stage word (this batch's starts from
 // it); table_done (optional) is recorded once the table kernels are done, before
 // k_finish: the next batch's stage B waits for it, not for k_finish.
+// kt_acc (optional, rl_profile on): k_table's duration on the device clock
+// (first workgroup start to last workgroup end) added to kt_acc[0], and 1 to
+// kt_acc[1], by k_finish.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                    int restore, hipStream_t st, hipEvent_t* ev, const uint32_t* errb_prev, hipEvent_t table_done);
+                    int restore, hipStream_t st, hipEvent_t* ev, const uint32_t* errb_prev, hipEvent_t table_done,
+                    unsigned long long* kt_acc = nullptr);
 // ev (optional, RL_NUM_STAGES + 1 events on stream st): recorded before
 // k_prepare, after it, after the sort, just before and just after k_table, and
 // at the end (per-stage timing, rl_profile).

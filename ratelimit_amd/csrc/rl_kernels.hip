@@ -4393,13 +4393,18 @@ __global__ __launch_bounds__(256, RL_KTABLE_WAVES) void k_table(uint32_t g_runs,
                                                uint32_t* defer1_n, unsigned long long* stats,
                                                unsigned long long* stripes, uint32_t* err, uint32_t* errs, int restore,
                                                uint32_t* __restrict__ fast_blk, const uint2* __restrict__ uniq,
-                                               const uint32_t* uniq_n) {
+                                               const uint32_t* uniq_n, unsigned long long* __restrict__ kt) {
+  // kt (rl_profile on): each workgroup's start and end on the device's
+  // constant clock, plain stores (one address for all of them serialised the
+  // launch: +40 %); k_finish folds them into the launch's duration
+  if (kt && threadIdx.x == 0) kt[2 * blockIdx.x] = wall_clock64();
   if (blockIdx.x < g_runs)
     runs_body(blockIdx.x, b, t, P, rec_s, skeys, svals, res, run_start, run_end, run_flags, run_state, run_alias, rid,
               run_f, num_runs, drun, defer2, defer2_n, stats, stripes, err, errs, restore, fast_blk);
   else
     unique_body(blockIdx.x - g_runs, b, t, P, rec_s.rec, keys0, uniq, uniq_n, res, defer1, defer1_n, stats, stripes,
                 err, errs, restore);
+  if (kt && threadIdx.x == 0) kt[2 * blockIdx.x + 1] = wall_clock64();
 }
 
 // k_late (after k_table, and k_fast_over with the local cache on): the exact
@@ -4470,8 +4475,32 @@ __global__ __launch_bounds__(256) void k_b_begin(const uint32_t* __restrict__ er
 // when the batch failed, so nothing leaks into the next one).
 __global__ __launch_bounds__(256) void k_finish(const unsigned long long* __restrict__ res, uint32_t n, OutDev o,
                                                 unsigned long long* __restrict__ stripes, uint32_t n_fold,
-                                                const uint32_t* err, unsigned long long* lc_ctr) {
+                                                const uint32_t* err, unsigned long long* lc_ctr,
+                                                const unsigned long long* __restrict__ kt, uint32_t kt_n,
+                                                unsigned long long* kt_acc) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (kt && blockIdx.x == 0) {  // (rl_profile) k_table's duration: first workgroup start to last end
+    __shared__ unsigned long long s_lo[256], s_hi[256];
+    unsigned long long lo = ~0ull, hi = 0;
+    for (uint32_t j = threadIdx.x; j < kt_n; j += 256) {
+      lo = min(lo, kt[2 * j]);
+      hi = max(hi, kt[2 * j + 1]);
+    }
+    s_lo[threadIdx.x] = lo;
+    s_hi[threadIdx.x] = hi;
+    __syncthreads();
+    for (uint32_t w = 128; w; w >>= 1) {
+      if (threadIdx.x < w) {
+        s_lo[threadIdx.x] = min(s_lo[threadIdx.x], s_lo[threadIdx.x + w]);
+        s_hi[threadIdx.x] = max(s_hi[threadIdx.x], s_hi[threadIdx.x + w]);
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0 && s_hi[0] > s_lo[0]) {
+      atomicAdd(&kt_acc[0], s_hi[0] - s_lo[0]);
+      atomicAdd(&kt_acc[1], 1ull);
+    }
+  }
   const bool ok = *err == 0;
   const uint32_t m = n_fold * RL_NUM_STATS;
   if (i < m) {
@@ -4712,7 +4741,8 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
 #define RL_LATE_FAST_BLOCKS 0  // cap on k_late's long-run workgroups (0: one per 256 descriptors)
 #endif
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                    int restore, hipStream_t st, hipEvent_t* ev, const uint32_t* errb_prev, hipEvent_t table_done) {
+                    int restore, hipStream_t st, hipEvent_t* ev, const uint32_t* errb_prev, hipEvent_t table_done,
+                    unsigned long long* kt_acc) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
   k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, errb_prev, s.defer2_n, s.defer1_n, o.stats, m, s.fast_blk,
@@ -4730,7 +4760,7 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
                                          s.run_flags, s.run_state, s.run_alias, s.rid, s.run_f, s.runs64, s.drun,
                                          s.defer2, s.defer2_n,
                                          s.keys[0], s.defer1, s.defer1_n, o.stats, s.stripes, s.errb, s.errs, restore,
-                                         s.fast_blk, s.uniq, s.uniq_n);
+                                         s.fast_blk, s.uniq, s.uniq_n, kt_acc ? s.kt_blk : nullptr);
     if (ev) (void)hipEventRecord(ev[4], st);
     if (!restore && P.lc_en)
       k_fast_over<<<g, 256, 0, st>>>(s.sorted_n, rs, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
@@ -4745,7 +4775,8 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     if (!restore) {
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;
       const uint32_t gf = cdiv(nf * RL_NUM_STATS > b.n ? nf * RL_NUM_STATS : b.n, 256);
-      k_finish<<<gf, 256, 0, st>>>(s.res, b.n, o, s.stripes, nf, s.errb, P.lc_en ? s.counters + 5 : nullptr);
+      k_finish<<<gf, 256, 0, st>>>(s.res, b.n, o, s.stripes, nf, s.errb, P.lc_en ? s.counters + 5 : nullptr,
+                                   kt_acc ? s.kt_blk : nullptr, g_runs + g, kt_acc);
     }
   } else {
     if (ev) {

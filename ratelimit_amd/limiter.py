@@ -28,6 +28,7 @@ from .types import OK, DescriptorStatus, Limit  # noqa: F401  (re-exported data 
 
 # rl_profile stages (include/ratelimit_hip.h RL_NUM_STAGES)
 STAGES = ("prepare", "sort", "segment", "table", "finish")
+PROFILE_FIELDS = STAGES + ("table_kernel",)  # + k_table's own run time (device clock)
 
 __all__ = ["GpuRateLimitCache", "GpuRateLimitService", "RedisError", "TimeSource"]
 
@@ -239,11 +240,13 @@ class Backend:
         check(self.ctx, lib().rl_profile(self.ctx, max(int(every), 1) if enable else 0))
 
     def profile_read(self):
-        """-> ({prepare, sort, segment, runs, finish} summed ms, batches timed); resets the sums."""
-        ms = (C.c_double * len(STAGES))()
+        """-> ({prepare, sort, segment, table, finish} summed ms over the timed batches, and
+        table_kernel: k_table's device-clock run time averaged per batch}, batches timed);
+        resets the sums."""
+        ms = (C.c_double * len(PROFILE_FIELDS))()
         nb = C.c_uint64(0)
-        check(self.ctx, lib().rl_profile_read(self.ctx, ms, len(STAGES), C.byref(nb)))
-        return dict(zip(STAGES, list(ms))), nb.value
+        check(self.ctx, lib().rl_profile_read(self.ctx, ms, len(PROFILE_FIELDS), C.byref(nb)))
+        return dict(zip(PROFILE_FIELDS, list(ms))), nb.value
 
     def synchronize(self):
         check(self.ctx, lib().rl_synchronize(self.ctx))

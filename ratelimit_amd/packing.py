@@ -361,3 +361,160 @@ def unprefix(pb: PrefixedBatch) -> Dict[str, np.ndarray]:
                             np.where(ok, lim["requests_per_unit"], 0), hits_q[np.asarray(req_idx, np.int64)],
                             np.where(ok, lim["rule_id"], 0))
     return out
+
+
+# ---------------------------------------------------------------------------
+# The Go batcher's own packing rules (go/src/gpu/cache_impl.go shared / pack,
+# go/src/gpu/gpu.go PrefixedBatch.Begin / Add / Seal), restated so that the
+# exact layout the Go adapter builds runs through the C ABI in the GPU tests:
+#  * nil limits are not packed (their status is {OK, nil, 0} host-side,
+#    base_limiter.go:78-81); UNKNOWN units panic (utilities.go:29);
+#  * a request's shared prefix is cut at ENTRY granularity: prefix ‖ domain ‖
+#    '_' plus the leading entries every packed descriptor of the request
+#    carries (cache_impl.go:231-265), then capped at 255 bytes;
+#  * the limit table is deduplicated on (RequestsPerUnit, rule id, Unit,
+#    ShadowMode) in first-seen order (gpu.go:308-323), at most max_limits;
+#  * the buffer's sections are index, req, now, hits, desc, prefix, suffix,
+#    limits, abutting at 4-byte alignment (gpu.go Begin), and buf_bytes ends
+#    at the used limit entries (Seal);
+#  * HitsAddend goes as the request carries it (the library applies
+#    utils.Max(1, h)); `now` as uint32.
+# go_statuses is cache_impl.go's finish: DurationUntilReset from the
+# request's clock (utils.CalculateReset) and one failed descriptor failing its
+# whole call.
+# ---------------------------------------------------------------------------
+GO_MAX_PREFIX = 255
+
+
+def _go_shared(prefix: str, request, limits) -> Tuple[int, int, int]:
+    """cache_impl.go shared(): (packed descriptors, shared prefix bytes, packed stems' bytes)."""
+    head = len(prefix.encode()) + len(request.domain.encode()) + 1
+    n = common = total = 0
+    ref = None
+    for d, lim in zip(request.descriptors, limits):
+        if lim is None:
+            continue
+        total += head + sum(len(k.encode()) + len(v.encode()) + 2 for k, v in d.entries)
+        if n == 0:
+            ref, common = list(d.entries), len(d.entries)
+        else:
+            k = 0
+            while k < common and k < len(d.entries) and tuple(d.entries[k]) == tuple(ref[k]):
+                k += 1
+            common = k
+        n += 1
+    if n == 0:
+        return 0, 0, 0
+    shared = head + sum(len(k.encode()) + len(v.encode()) + 2 for k, v in ref[:common])
+    return n, min(shared, GO_MAX_PREFIX), total
+
+
+def go_prefixed_batch(calls, prefix: str, interner: RuleInterner, n_rules: Optional[int] = None,
+                      max_limits: int = 65536, alloc=None):
+    """calls: (request, limits, now) in arrival order -> (PrefixedBatch, where),
+    where[c][i] = the packed index of descriptor i of call c, -1 for a nil limit."""
+    sizes = [_go_shared(prefix, req, lims) for req, lims, _ in calls]
+    nq = len(calls)
+    n = sum(s[0] for s in sizes)
+    p_bytes = sum(s[1] for s in sizes)
+    s_bytes = sum(s[2] - s[0] * s[1] for s in sizes)
+    tiles = (nq + abi.RL_PREFIXED_TILE - 1) // abi.RL_PREFIXED_TILE
+    a4 = lambda x: (x + 3) & ~3
+    offsets, pos = {}, 0
+    for name, nb in (("index", 16 * (tiles + 1)), ("req", 4 * nq), ("now", 4 * nq), ("hits", 4 * nq),
+                     ("desc", 4 * n), ("prefix_bytes", p_bytes), ("suffix_bytes", s_bytes)):
+        offsets[name] = pos
+        pos += a4(nb)
+    offsets["limits"] = pos
+    cap = pos + 12 * max_limits
+    buf = np.zeros(max(cap, 4), np.uint8) if alloc is None else alloc(max(cap, 4))
+    buf[:] = 0
+    index = np.zeros(4 * (tiles + 1), np.uint32)
+    reqw = np.zeros(nq, np.uint32)
+    nows = np.zeros(nq, np.uint32)
+    hitw = np.zeros(nq, np.uint32)
+    descw = np.zeros(n, np.uint32)
+    pre, suf = bytearray(), bytearray()
+    table = {}  # Limit -> index, first-seen order
+    where = []
+    d = n_stem = 0
+    for q, ((req, lims, now), (_nd, p_len, _tot)) in enumerate(zip(calls, sizes)):
+        if len(req.descriptors) != len(lims):
+            raise AssertionError("len(descriptors) != len(limits)")  # base_limiter.go:47
+        if q % abi.RL_PREFIXED_TILE == 0:
+            t = 4 * (q // abi.RL_PREFIXED_TILE)
+            index[t:t + 4] = (d, len(pre), len(suf), n_stem)
+        idx, suffixes = [], []
+        stem_head = None
+        for i, (desc, lim) in enumerate(zip(req.descriptors, lims)):
+            if lim is None:
+                idx.append(-1)
+                continue
+            u = int(lim.limit.unit)
+            if u not in (1, 2, 3, 4):
+                raise RuntimeError("should not get here")  # utils.UnitToDivider panic
+            stem = stem_of(prefix, req.domain, desc.entries)
+            if stem_head is None:
+                stem_head = stem[:p_len]
+            key = (int(lim.limit.requests_per_unit), interner.intern(lim.stats.key), u, bool(lim.shadow_mode))
+            k = table.get(key)
+            if k is None:
+                if len(table) == max_limits:
+                    raise ValueError("gpu: more distinct limits than the batch's table holds")
+                k = table[key] = len(table)
+            sfx = stem[p_len:]
+            if len(sfx) > 0xFFFF:
+                raise ValueError("gpu: descriptor suffix longer than 65535 bytes")
+            idx.append(d + len(suffixes))
+            suffixes.append((k, sfx, len(stem)))
+        if len(suffixes) > 0xFFFF or p_len > GO_MAX_PREFIX:
+            raise ValueError("gpu: request does not fit the prefixed layout")
+        reqw[q] = len(suffixes) | (p_len << 16)
+        nows[q] = int(now) & 0xFFFFFFFF
+        hitw[q] = int(req.hits_addend)
+        if suffixes:
+            pre += stem_head
+        for k, sfx, sl in suffixes:
+            descw[d] = k | (len(sfx) << 16)
+            suf += sfx
+            n_stem += sl
+            d += 1
+        where.append(idx)
+    t = 4 * tiles
+    index[t:t + 4] = (d, len(pre), len(suf), n_stem)
+    keys = sorted(table, key=table.get)
+    lim_arr = np.zeros(len(keys), abi.LIMIT_DTYPE)
+    lim_arr["requests_per_unit"] = [k[0] for k in keys]
+    lim_arr["rule_id"] = [k[1] for k in keys]
+    lim_arr["unit"] = [k[2] for k in keys]
+    lim_arr["flags"] = [abi.RL_FLAG_SHADOW if k[3] else 0 for k in keys]
+    for name, a in (("index", index), ("req", reqw), ("now", nows), ("hits", hitw), ("desc", descw),
+                     ("prefix_bytes", np.frombuffer(bytes(pre), np.uint8)),
+                     ("suffix_bytes", np.frombuffer(bytes(suf), np.uint8)), ("limits", lim_arr)):
+        raw = np.frombuffer(a.tobytes(), np.uint8)
+        buf[offsets[name]:offsets[name] + raw.size] = raw
+    used = offsets["limits"] + 12 * len(table)
+    nr = len(interner.keys) if n_rules is None else n_rules
+    pb = PrefixedBatch(buf[:max(used, 4)], d, nq, nr, len(table), offsets)
+    return pb, where
+
+
+def go_statuses(calls, where, out) -> list:
+    """cache_impl.go finish(): per call either its statuses as (code, limit
+    remaining, DurationUntilReset seconds or None) per descriptor, or the
+    string of the RedisError it panics with (a failed descriptor fails the
+    call)."""
+    res = []
+    for (req, lims, now), idx in zip(calls, where):
+        st, failed = [], None
+        for i, j in enumerate(idx):
+            if j < 0:
+                st.append((1, 0, None))  # {OK, nil, 0} (base_limiter.go:78-81)
+                continue
+            if out.get("status") is not None and out["status"][j] != 0:
+                failed = "gpu: descriptor failed (rl_status %d)" % out["status"][j]
+                continue
+            div = {1: 1, 2: 60, 3: 3600, 4: 86400}[int(lims[i].limit.unit)]
+            st.append((int(out["code"][j]), int(out["limit_remaining"][j]), div - int(now) % div))
+        res.append(failed if failed else st)
+    return res

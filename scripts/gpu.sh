@@ -39,7 +39,7 @@ import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric')][-1])
 out = [sys.argv[2], "%.3f G/s" % (d["value"] / 1e9), "%.4f ms" % d["ms_per_step"]]
 if d.get("roofline", {}).get("stage_ms"):
-    out.append("table %s" % d["roofline"]["stage_ms"].get("table"))
+    out.append("table %s kern %s" % (d["roofline"]["stage_ms"].get("table"), d["roofline"].get("kernel_us")))
 if sys.argv[3]:
     out.append(str(eval(sys.argv[3], {"d": d})))
 print(" ".join(out))

@@ -127,6 +127,8 @@ def test_gpu_profile_sampling_counts_and_leaves_results_unchanged():
         ms, nb = cache.backend.profile_read()
         assert nb == (n_batches + 2) // 3
         assert all(v >= 0.0 for v in ms.values()) and ms["table"] > 0.0
+        # k_table's own run time per batch (device clock, every batch)
+        assert 0.0 < ms["table_kernel"] < 10.0
         cache.backend.profile(False)
         cache.do_limit_batch(calls[-10:])
         assert cache.backend.profile_read()[1] == 0
