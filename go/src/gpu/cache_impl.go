@@ -2,6 +2,8 @@ package gpu
 
 import (
 	"fmt"
+	"math"
+	"strings"
 	"sync/atomic"
 	"time"
 
@@ -41,6 +43,15 @@ type rateLimitCacheImpl struct {
 	sweepEvery time.Duration
 	sweepLag   int64
 	batches    [2]*PrefixedBatch
+	routed     bool // the ctx joined a world of ranks: one collective batch per tick (batcherRouted)
+
+	// GPU_CONFIG_MATCH (limiter.RequestRateLimitCache): the loaded config on
+	// the device, raw requests matched there (rl_do_limit_requests)
+	configMatch  bool
+	configReady  int32 // (atomic) a config has been loaded on the device
+	rb           *RequestBatch
+	statsManager stats.Manager                              // override stats (config_impl.go:255-263)
+	limitByKey   map[string]*pb.RateLimitResponse_RateLimit // Stats.Key -> the config rule's limit (CurrentLimit)
 
 	rules     map[string]uint32      // limit.Stats.Key -> dense rule id
 	ruleStats []stats.RateLimitStats // rule id -> the counters its deltas go to
@@ -54,6 +65,19 @@ type call struct {
 	limits []*config.RateLimit
 	now    int64 // timeSource.UnixNow(), read once per request (base_limiter.go:49)
 	done   chan reply
+	raw    bool                   // DoLimitRequest: the limits are matched on the GPU
+	cfg    config.RateLimitConfig // a config to load (ConfigLoaded), not a request
+}
+
+// kind of a queued call: a DoLimit call, a raw request, a config load
+func (c *call) kind() int {
+	if c.cfg != nil {
+		return 2
+	}
+	if c.raw {
+		return 1
+	}
+	return 0
 }
 
 type reply struct {
@@ -75,11 +99,14 @@ type Options struct {
 	Window        time.Duration // GPU_BATCH_WINDOW
 	SweepInterval time.Duration // GPU_SWEEP_INTERVAL (0: never)
 	SweepLag      time.Duration // GPU_SWEEP_LAG: the sweep's time floor trails the clock by this much
+	ConfigMatch   bool          // GPU_CONFIG_MATCH: GetLimit on the GPU (not on a routed ctx)
+	StatsManager  stats.Manager // for the override stats keys the GPU match meets (ConfigMatch)
 }
 
 // NewRateLimitCacheImpl starts the batcher on an existing ctx.
 func NewRateLimitCacheImpl(ctx *Ctx, cfg Config, opt Options, timeSource utils.TimeSource,
 	cacheKeyPrefix string) *rateLimitCacheImpl {
+	cfg = cfg.Resolved() // (a zero field is the library's default: size the pinned buffers for it)
 	maxRules := int(cfg.MaxRules)
 	this := &rateLimitCacheImpl{
 		ctx:        ctx,
@@ -92,11 +119,23 @@ func NewRateLimitCacheImpl(ctx *Ctx, cfg Config, opt Options, timeSource utils.T
 		sweepEvery: opt.SweepInterval,
 		sweepLag:   int64(opt.SweepLag / time.Second),
 		rules:      map[string]uint32{},
+		routed:     ctx.Routed(),
+		// (rl_do_limit_requests is not routed: a routed ctx keeps GetLimit in Go)
+		configMatch:  opt.ConfigMatch && !ctx.Routed() && opt.StatsManager != nil,
+		statsManager: opt.StatsManager,
+		limitByKey:   map[string]*pb.RateLimitResponse_RateLimit{},
+	}
+	if this.configMatch {
+		this.rb = NewRequestBatch()
 	}
 	for i := range this.batches {
 		this.batches[i] = NewPrefixedBatch(this.maxDesc, maxRules)
 	}
-	go this.batcher()
+	if this.routed {
+		go this.batcherRouted()
+	} else {
+		go this.batcher()
+	}
 	return this
 }
 
@@ -129,8 +168,23 @@ func NewRateLimitCacheImplFromSettings(s settings.Settings, localCache *freecach
 	if err != nil {
 		logger.Fatalf("gpu: cannot create the GPU backend: %v", err)
 	}
+	if s.GpuWorld > 1 {
+		// one service process per GPU: this process is rank GPU_RANK of
+		// GPU_WORLD, every rank with the same GPU_HASH_SEED (comm.go)
+		if cfg.HashSeed == 0 {
+			logger.Fatalf("gpu: GPU_WORLD > 1 needs an explicit GPU_HASH_SEED shared by every rank")
+		}
+		id, err := CommIDFile(s.GpuCommIDFile, s.GpuRank, s.GpuCommTimeout)
+		if err == nil {
+			err = ctx.CommInit(s.GpuWorld, s.GpuRank, id)
+		}
+		if err != nil {
+			logger.Fatalf("gpu: cannot join the GPU world: %v", err)
+		}
+	}
 	impl := NewRateLimitCacheImpl(ctx, cfg, Options{Window: s.GpuBatchWindow, SweepInterval: s.GpuSweepInterval,
-		SweepLag: s.GpuSweepLag}, timeSource, s.CacheKeyPrefix)
+		SweepLag: s.GpuSweepLag, ConfigMatch: s.GpuConfigMatch, StatsManager: statsManager}, timeSource,
+		s.CacheKeyPrefix)
 	if cfg.LocalCache && srv != nil {
 		statsManager.GetStatsStore().AddStatGenerator(newLocalCacheStats(impl, srv.Scope().Scope("localcache_gpu")))
 	}
@@ -152,17 +206,170 @@ func (this *rateLimitCacheImpl) DoLimit(ctx context.Context, request *pb.RateLim
 // Flush: nothing to wait for, DoLimit returns with its answers.
 func (this *rateLimitCacheImpl) Flush() {}
 
+// ConfigLoaded (limiter.RequestRateLimitCache): the batcher loads cfg on the
+// device between two batches; requests queued after it are matched against it.
+func (this *rateLimitCacheImpl) ConfigLoaded(cfg config.RateLimitConfig) {
+	if !this.configMatch || cfg == nil {
+		return
+	}
+	c := &call{cfg: cfg, done: make(chan reply, 1)}
+	this.queue <- c
+	if r := <-c.done; r.err != "" {
+		// (requests keep the reference path: GetLimit in Go, then DoLimit)
+		logger.Errorf("gpu: config not loaded on the device: %s", r.err)
+	}
+}
+
+// DoLimitRequest (limiter.RequestRateLimitCache): GetLimit, DoLimit and the
+// unlimited mapping for the whole request on the GPU. ok == false until a
+// config is on the device (and always without GPU_CONFIG_MATCH).
+func (this *rateLimitCacheImpl) DoLimitRequest(ctx context.Context, request *pb.RateLimitRequest) (
+	[]*pb.RateLimitResponse_DescriptorStatus, bool) {
+	if !this.configMatch || atomic.LoadInt32(&this.configReady) == 0 {
+		return nil, false
+	}
+	c := &call{req: request, now: this.timeSource.UnixNow(), done: make(chan reply, 1), raw: true}
+	this.queue <- c
+	r := <-c.done
+	if r.err != "" {
+		panic(redis.RedisError(r.err)) // driver_impl.go:60-64; recovered at ratelimit.go:252-256
+	}
+	return r.statuses, true
+}
+
+// descriptorKey (src/config/config_impl.go:300-312): an override's stats key.
+func descriptorKey(domain string, d *pb_struct.RateLimitDescriptor) string {
+	parts := make([]string, 0, len(d.Entries))
+	for _, e := range d.Entries {
+		if e.Value != "" {
+			parts = append(parts, e.Key+"_"+e.Value)
+		} else {
+			parts = append(parts, e.Key)
+		}
+	}
+	return domain + "." + strings.Join(parts, ".")
+}
+
+// loadConfig (batcher goroutine): the config on the device, its rules'
+// limits kept for CurrentLimit (the reference aliases limit.Limit,
+// base_limiter.go:186).
+func (this *rateLimitCacheImpl) loadConfig(cfg config.RateLimitConfig) error {
+	limits := map[string]*pb.RateLimitResponse_RateLimit{}
+	config.Walk(cfg, func(parent int, key string, l *config.RateLimit) int {
+		if l != nil && l.Limit != nil {
+			limits[l.Stats.Key] = l.Limit
+		}
+		return 0
+	})
+	if err := this.ctx.LoadConfig(cfg, this.prefix, this.rule); err != nil {
+		return err
+	}
+	this.limitByKey = limits
+	atomic.StoreInt32(&this.configReady, 1)
+	return nil
+}
+
+// doRaw (batcher goroutine): one rl_do_limit_requests over the raw calls.
+func (this *rateLimitCacheImpl) doRaw(calls []*call) {
+	reqs := make([]*pb.RateLimitRequest, len(calls))
+	nows := make([]int64, len(calls))
+	for i, c := range calls {
+		reqs[i], nows[i] = c.req, c.now
+	}
+	full := false
+	override := func(domain string, d *pb_struct.RateLimitDescriptor) uint32 {
+		key := descriptorKey(domain, d)
+		id, ok := this.rules[key]
+		if !ok {
+			if len(this.ruleStats) == this.maxRules {
+				full = true
+				return 0
+			}
+			// GetLimit's fresh RateLimit for an override: statsManager.NewStats(key) (config_impl.go:255-263)
+			id = this.ruleStatsAdd(this.statsManager.NewStats(key))
+		}
+		return id
+	}
+	b := this.rb
+	b.Pack(reqs, nows, override, func() int { return len(this.ruleStats) })
+	var err error
+	if full {
+		err = fmt.Errorf("gpu: more than %d rule stats keys", this.maxRules)
+	} else {
+		err = this.ctx.DoLimitRequests(b)
+	}
+	j := 0
+	for _, c := range calls {
+		if err != nil {
+			c.done <- reply{err: "gpu: " + err.Error()}
+			continue
+		}
+		st := make([]*pb.RateLimitResponse_DescriptorStatus, len(c.req.Descriptors))
+		for i := range st {
+			switch b.Match[j] {
+			case MatchLimit: // ratelimit.go:186-190: DoLimit's status
+				st[i] = &pb.RateLimitResponse_DescriptorStatus{
+					Code:               pb.RateLimitResponse_Code(b.Code[j]),
+					CurrentLimit:       this.currentLimit(b.RuleID[j], b.RPU[j], b.Unit[j]),
+					LimitRemaining:     b.Remaining[j],
+					DurationUntilReset: &duration.Duration{Seconds: int64(b.Reset[j])},
+				}
+			case MatchUnlimited: // ratelimit.go:176-183
+				st[i] = &pb.RateLimitResponse_DescriptorStatus{Code: pb.RateLimitResponse_OK,
+					LimitRemaining: math.MaxUint32}
+			default: // no rule: a nil limit, {OK, nil, 0} (base_limiter.go:78-81)
+				st[i] = &pb.RateLimitResponse_DescriptorStatus{Code: pb.RateLimitResponse_OK}
+			}
+			j++
+		}
+		c.done <- reply{statuses: st}
+	}
+	if err == nil {
+		this.applyStats(b.Stats, int(b.In.n_rules))
+	}
+}
+
+// currentLimit: the matched config rule's limit proto (or an override's, fresh).
+func (this *rateLimitCacheImpl) currentLimit(rid, rpu uint32, unit uint8) *pb.RateLimitResponse_RateLimit {
+	if int(rid) < len(this.ruleStats) {
+		if l := this.limitByKey[this.ruleStats[rid].Key]; l != nil && l.RequestsPerUnit == rpu && uint8(l.Unit) == unit {
+			return l
+		}
+	}
+	return &pb.RateLimitResponse_RateLimit{RequestsPerUnit: rpu, Unit: pb.RateLimitResponse_RateLimit_Unit(unit)}
+}
+
 func (this *rateLimitCacheImpl) rule(s stats.RateLimitStats) (uint32, bool) {
 	id, ok := this.rules[s.Key]
 	if !ok {
 		if len(this.ruleStats) == this.maxRules {
 			return 0, false
 		}
-		id = uint32(len(this.ruleStats))
-		this.rules[s.Key] = id
-		this.ruleStats = append(this.ruleStats, s)
+		id = this.ruleStatsAdd(s)
 	}
 	return id, true
+}
+
+func (this *rateLimitCacheImpl) ruleStatsAdd(s stats.RateLimitStats) uint32 {
+	id := uint32(len(this.ruleStats))
+	this.rules[s.Key] = id
+	this.ruleStats = append(this.ruleStats, s)
+	return id
+}
+
+// applyStats adds a batch's per-rule deltas (stats.RateLimitStats order,
+// manager.go:47-55) to the rules' counters: the sum of what the reference Adds
+// per descriptor.
+func (this *rateLimitCacheImpl) applyStats(d []uint64, nRules int) {
+	for r := 0; r < nRules && r < len(this.ruleStats); r++ {
+		s := this.ruleStats[r]
+		for k, ctr := range []interface{ Add(uint64) }{s.TotalHits, s.OverLimit, s.NearLimit,
+			s.OverLimitWithLocalCache, s.WithinLimit, s.ShadowMode} {
+			if v := d[6*r+k]; v != 0 {
+				ctr.Add(v)
+			}
+		}
+	}
 }
 
 // batcher: the only goroutine that calls the C library.
@@ -186,23 +393,54 @@ func (this *rateLimitCacheImpl) batcher() {
 				first = <-this.queue
 			}
 		}
-		calls, total := []*call{first}, len(first.limits)
+		if first.kind() == 2 { // a config load: after every batch before it
+			if inflight != nil {
+				this.finish(inflight)
+				inflight = nil
+			}
+			msg := ""
+			if err := this.loadConfig(first.cfg); err != nil {
+				msg = err.Error()
+			}
+			first.done <- reply{err: msg}
+			continue
+		}
+		size := func(c *call) int {
+			if c.raw {
+				return len(c.req.Descriptors)
+			}
+			return len(c.limits)
+		}
+		calls, total := []*call{first}, size(first)
 		timer := time.NewTimer(this.window)
 	collect:
 		for total < this.maxDesc {
 			select {
 			case c := <-this.queue:
-				if total+len(c.limits) > this.maxDesc {
+				// one kind per batch, in arrival order
+				if c.kind() != first.kind() || total+size(c) > this.maxDesc {
 					carry = c // the next batch
 					break collect
 				}
 				calls = append(calls, c)
-				total += len(c.limits)
+				total += size(c)
 			case <-timer.C:
 				break collect
 			}
 		}
 		timer.Stop()
+		if first.raw { // (synchronous: after the DoLimit batch in flight)
+			if inflight != nil {
+				this.finish(inflight)
+				inflight = nil
+			}
+			this.doRaw(calls)
+			if this.sweepEvery > 0 && time.Since(lastSweep) >= this.sweepEvery {
+				this.housekeeping()
+				lastSweep = time.Now()
+			}
+			continue
+		}
 		// pack the next batch while the one in flight runs on the GPU
 		f := this.pack(this.batches[cur], calls)
 		if inflight != nil {
@@ -218,6 +456,65 @@ func (this *rateLimitCacheImpl) batcher() {
 			inflight = nil
 			this.housekeeping()
 			lastSweep = time.Now()
+		}
+	}
+}
+
+// batcherRouted: the batcher of a routed ctx. Submit, Synchronize and Sweep
+// are collective over the ranks, so every rank takes the same steps on the
+// same schedule: one batch per tick of the window, holding whatever calls
+// arrived (none: an empty batch, still a step of the exchange), and a sweep
+// every sweepTicks ticks. A batch that cannot be packed is replaced by an
+// empty one (its calls fail) so that no peer waits for this rank.
+func (this *rateLimitCacheImpl) batcherRouted() {
+	tick := time.NewTicker(this.window)
+	defer tick.Stop()
+	var carry *call
+	var inflight *flight
+	cur := 0
+	sweepTicks := uint64(0)
+	if this.sweepEvery > 0 && this.window > 0 {
+		sweepTicks = uint64(this.sweepEvery / this.window)
+	}
+	for n := uint64(1); ; n++ {
+		<-tick.C
+		var calls []*call
+		total := 0
+		if carry != nil {
+			calls, total, carry = append(calls, carry), len(carry.limits), nil
+		}
+	drain:
+		for total < this.maxDesc {
+			select {
+			case c := <-this.queue:
+				if total+len(c.limits) > this.maxDesc {
+					carry = c
+					break drain
+				}
+				calls = append(calls, c)
+				total += len(c.limits)
+			default:
+				break drain
+			}
+		}
+		f := this.pack(this.batches[cur], calls)
+		if inflight != nil {
+			this.finish(inflight)
+		}
+		if f.err != nil { // take part with an empty batch; the calls fail in finish
+			e := this.pack(this.batches[cur], nil)
+			if err := this.ctx.Submit(e.b); err != nil {
+				logger.Errorf("gpu: routed submit failed: %v", err)
+			}
+		} else {
+			f.err = this.ctx.Submit(f.b)
+		}
+		inflight = f
+		cur ^= 1
+		if sweepTicks > 0 && n%sweepTicks == 0 {
+			this.finish(inflight)
+			inflight = nil
+			this.housekeeping()
 		}
 	}
 }
@@ -340,8 +637,10 @@ func (this *rateLimitCacheImpl) pack(b *PrefixedBatch, calls []*call) *flight {
 // finish waits for the flight's batch and answers its calls.
 func (this *rateLimitCacheImpl) finish(f *flight) {
 	err := f.err
-	if err == nil {
-		err = this.ctx.Synchronize()
+	if err == nil || this.routed { // (routed: Synchronize is collective, every rank calls it per flight)
+		if serr := this.ctx.Synchronize(); err == nil {
+			err = serr
+		}
 	}
 	b := f.b
 	for ci, c := range f.calls {
@@ -382,18 +681,7 @@ func (this *rateLimitCacheImpl) finish(f *flight) {
 	if err != nil {
 		return
 	}
-	// per-rule deltas in stats.RateLimitStats order (manager.go:47-55): the
-	// batch's sum of what the reference Adds per descriptor
-	for r := 0; r < f.nRules; r++ {
-		s := this.ruleStats[r]
-		d := b.Stats[6*r : 6*r+6]
-		for k, ctr := range []interface{ Add(uint64) }{s.TotalHits, s.OverLimit, s.NearLimit,
-			s.OverLimitWithLocalCache, s.WithinLimit, s.ShadowMode} {
-			if d[k] != 0 {
-				ctr.Add(d[k])
-			}
-		}
-	}
+	this.applyStats(b.Stats, f.nRules)
 }
 
 // housekeeping: the EXPIRE sweep (slots whose windows all ended before now -

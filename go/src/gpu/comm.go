@@ -7,15 +7,27 @@ package gpu
 import "C"
 
 import (
+	"errors"
+	"io/ioutil"
+	"os"
 	"runtime"
+	"time"
 	"unsafe"
 )
 
 // One service process per GPU (SURVEY §8e): every rank's ctx shares
-// Config.HashSeed, rank 0 draws a communicator id and the coordinator hands
-// it to every rank; the library then routes each batch to the GPU owning its
-// keys over RCCL (xGMI) and back. Replaces the Redis cluster client's
-// key-slot routing (src/redis/driver_impl.go:108-126).
+// Config.HashSeed, rank 0 draws a communicator id and hands it to every rank
+// (CommIDFile: through a file on shared storage); the library then routes
+// each batch to the GPU owning its keys over RCCL (xGMI) and back. Replaces
+// the Redis cluster client's key-slot routing (src/redis/driver_impl.go:108-126).
+//
+// A routed ctx takes the batcher's own prefix-shared batches: Submit on it is
+// rl_do_limit_prefixed_async on a ctx that joined a communicator, and each
+// rank's batch is its slice of the node batch. Submit, Synchronize and Sweep
+// are collective there (every rank calls them the same number of times, in
+// the same order), so the batcher of a routed ctx submits one batch per tick
+// of GPU_BATCH_WINDOW, empty when its process received no call, and sweeps
+// on a tick count (cache_impl.go batcherRouted).
 
 // CommIDBytes is the size of a communicator id (an ncclUniqueId).
 const CommIDBytes = int(C.RL_COMM_ID_BYTES)
@@ -34,6 +46,34 @@ func CommUniqueID() ([]byte, error) {
 	return C.GoBytes(unsafe.Pointer(id), C.int(CommIDBytes)), nil
 }
 
+// CommIDFile hands the communicator id from rank 0 to the other ranks through
+// path: rank 0 draws it and writes it (write then rename, so no rank reads a
+// partial id); every other rank waits up to timeout for the file. A stale
+// file from an earlier run must be removed before rank 0 starts.
+func CommIDFile(path string, rank int, timeout time.Duration) ([]byte, error) {
+	if rank == 0 {
+		id, err := CommUniqueID()
+		if err != nil {
+			return nil, err
+		}
+		if err := ioutil.WriteFile(path+".tmp", id, 0600); err != nil {
+			return nil, err
+		}
+		return id, os.Rename(path+".tmp", path)
+	}
+	deadline := time.Now().Add(timeout)
+	for {
+		id, err := ioutil.ReadFile(path)
+		if err == nil && len(id) == CommIDBytes {
+			return id, nil
+		}
+		if time.Now().After(deadline) {
+			return nil, errors.New("gpu: no communicator id in " + path + " (is rank 0 up?)")
+		}
+		time.Sleep(50 * time.Millisecond)
+	}
+}
+
 // CommInit joins the ctx to the world as rank (collective: every rank, the same id).
 func (c *Ctx) CommInit(world, rank int, id []byte) error {
 	if len(id) != CommIDBytes {
@@ -41,12 +81,13 @@ func (c *Ctx) CommInit(world, rank int, id []byte) error {
 	}
 	cid := (*C.uint8_t)(C.CBytes(id))
 	defer C.free(unsafe.Pointer(cid))
-	return c.err(C.rl_comm_init(c.c, C.uint32_t(world), C.uint32_t(rank), cid))
+	if err := c.err(C.rl_comm_init(c.c, C.uint32_t(world), C.uint32_t(rank), cid)); err != nil {
+		return err
+	}
+	c.routed = world > 1
+	return nil
 }
 
-// RoutedDoLimit submits this rank's slice of the node batch (device arrays in
-// *in, *out; stream a hipStream_t or nil). Collective: every rank calls it the
-// same number of times; Synchronize (collective too) completes the last one.
-func (c *Ctx) RoutedDoLimit(in *C.rl_batch, out *C.rl_result, stream unsafe.Pointer) error {
-	return c.err(C.rl_do_limit_routed_async(c.c, in, out, stream))
-}
+// Routed reports whether the ctx joined a world of two or more ranks (its
+// Submit, Synchronize and Sweep are collective).
+func (c *Ctx) Routed() bool { return c.routed }

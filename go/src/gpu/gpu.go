@@ -41,8 +41,29 @@ type Config struct {
 	ShardDevices   []int   // > 1 entries: one table shard per device, routed inside the ctx
 }
 
+// The library's defaults for a zero Config field (include/ratelimit_hip.h rl_config).
+const (
+	DefaultMaxBatch = 1 << 20
+	DefaultMaxRules = 65536
+)
+
+// Resolved returns cfg with the zero sizing fields the batcher's own buffers
+// depend on replaced by the library's defaults (rl_create applies the same).
+func (cfg Config) Resolved() Config {
+	if cfg.MaxBatch == 0 {
+		cfg.MaxBatch = DefaultMaxBatch
+	}
+	if cfg.MaxRules == 0 {
+		cfg.MaxRules = DefaultMaxRules
+	}
+	return cfg
+}
+
 // Ctx owns one rl_ctx. One goroutine drives it at a time (the batcher).
-type Ctx struct{ c *C.rl_ctx }
+type Ctx struct {
+	c      *C.rl_ctx
+	routed bool // joined a world of two or more ranks (comm.go)
+}
 
 func New(cfg Config) (*Ctx, error) {
 	var rc C.rl_config
@@ -77,7 +98,7 @@ func New(cfg Config) (*Ctx, error) {
 	if ctx == nil {
 		return nil, errors.New(C.GoString(&msg[0]))
 	}
-	return &Ctx{ctx}, nil
+	return &Ctx{c: ctx}, nil
 }
 
 func (c *Ctx) Close() {
@@ -221,8 +242,15 @@ type PrefixedBatch struct {
 }
 
 // NewPrefixedBatch allocates the batch's pinned outputs for at most maxDesc
-// descriptors and maxRules stats rows; the input buffer grows on demand.
+// descriptors and maxRules stats rows (0: the library defaults, as rl_create
+// resolves them); the input buffer grows on demand.
 func NewPrefixedBatch(maxDesc, maxRules int) *PrefixedBatch {
+	if maxDesc <= 0 {
+		maxDesc = DefaultMaxBatch
+	}
+	if maxRules <= 0 {
+		maxRules = DefaultMaxRules
+	}
 	b := &PrefixedBatch{limitIdx: make(map[Limit]uint16)}
 	b.Code = bytesAt(pinned(maxDesc), maxDesc)
 	b.Remaining = u32At(pinned(4*maxDesc), maxDesc)
@@ -347,7 +375,9 @@ func (b *PrefixedBatch) Len() int { return b.n }
 
 // Submit queues a sealed batch: it crosses PCIe while earlier batches
 // compute; its outputs are final once Progress reports it complete, or after
-// Synchronize. The batch is untouched by Go until then.
+// Synchronize. The batch is untouched by Go until then. On a routed ctx
+// (comm.go) the batch is this rank's slice of the node batch and the call is
+// collective; an empty batch (Begin(0, 0, ...)) still takes part.
 func (c *Ctx) Submit(b *PrefixedBatch) error {
 	return c.err(C.rl_do_limit_prefixed_async(c.c, &b.In, &b.Out))
 }

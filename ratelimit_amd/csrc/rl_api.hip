@@ -523,7 +523,33 @@ int rl_batch_progress(rl_ctx* c, uint64_t* submitted, uint64_t* completed) {
 
 int rl_do_limit_prefixed_async(rl_ctx* c, const rl_batch_prefixed* in, rl_result* out) {
   if (!c || !in || !out) return fail(c, RL_E_INVALID, "gpu: null argument");
-  if (c->comm) return eng_fail(c->e[0], RL_E_INVALID, "gpu: prefixed batches are not routed (rl_do_limit_routed_async)");
+  if (c->comm) {
+    // a ctx that joined a communicator (one process per GPU): the whole
+    // prefix-shared batch is this rank's slice of the node batch, staged over
+    // this GPU's link and unpacked on it, then routed like a device slice
+    // (collective, as rl_do_limit_routed_async; out->stats = this rank's
+    // requests' deltas). The Go batcher of every rank submits one batch per
+    // tick, empty when idle.
+    uint32_t tiles = 0;
+    if (const int rc = eng_prefixed_check(c->e[0], in, out, &tiles)) {
+      // a rejected slice still takes part in the exchange (no records) and
+      // fails at rl_synchronize: no peer waits for it
+      rl_batch none{};
+      rl_result nout = *out;
+      return comm_do_limit(c->comm, c->e[0], &none, &nout, nullptr, nullptr, rc);  // (RL_OK unless the router broke)
+    }
+    rl_batch sizes{};
+    sizes.n = in->n;
+    sizes.n_requests = in->n_requests;
+    sizes.n_rules = in->n_rules;
+    CommIO io;
+    io.host = true;
+    io.pb = in;
+    io.t0 = 0;
+    io.t1 = tiles;
+    io.stats_host = in->n_rules ? (unsigned long long*)out->stats : nullptr;
+    return comm_do_limit(c->comm, c->e[0], &sizes, out, nullptr, &io);
+  }
   if (c->n == 1) return eng_do_limit_prefixed_async(c->e[0], in, out);
   // a multi-shard ctx: one slice of request tiles per shard, each over its own
   // device's link (rl_comm's stage_host_prefixed), then the shards' exchange

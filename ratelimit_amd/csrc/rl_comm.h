@@ -47,9 +47,11 @@ struct CommIO {
 };
 // One routed batch: this rank's slice (device arrays, or io) -> out in arrival
 // order. Enqueues the batch's first half and runs the previous batch's second
-// half.
+// half. host_rc != RL_OK: the caller rejected the slice (its message already
+// in the engine's last error); it still takes part in the exchange, with no
+// records, and fails at rl_synchronize.
 int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, hipStream_t caller,
-                  const CommIO* io = nullptr);
+                  const CommIO* io = nullptr, int host_rc = 0);
 // Batches a router keeps in flight (its slots, used round robin), and a wait
 // on the host for the last batch that used slot s (its outputs and, with
 // io.stats_host, its stats are then in place). Valid once the batch's second

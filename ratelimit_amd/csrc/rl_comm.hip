@@ -732,7 +732,7 @@ int comm_wait_slot(CommRouter* r, Engine* e, uint32_t s) {
 }
 
 int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, hipStream_t caller,
-                  const CommIO* io) {
+                  const CommIO* io, int host_rc) {
   if (r->broken) return eng_fail(e, r->broken, r->broken_msg);
   const uint32_t n = in->n, nr = in->n_rules;
   CHK_HIP(e, hipSetDevice(r->dev));
@@ -749,8 +749,10 @@ int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, 
     return breaks(r, e, RL_E_HIP, "gpu: routing stats staging allocation failed");
   // checks the partition does not make: a failure here still takes part in
   // the exchange (zero counts) and fails this rank's batch at rl_synchronize
-  int hostrc = RL_OK;
-  if (n && (!out->code || !out->limit_remaining || (!out->reset_s && !S.io.host))) {  // (host slices: reset optional)
+  int hostrc = host_rc;
+  if (hostrc) {
+    // (rejected by the caller: the message is the engine's last error)
+  } else if (n && (!out->code || !out->limit_remaining || (!out->reset_s && !S.io.host))) {  // (host slices: reset optional)
     hostrc = eng_fail(e, RL_E_INVALID, "gpu: null result array");
   } else if ((uint64_t)r->world * nr > e->cfg.max_rules) {
     hostrc = eng_fail(e, RL_E_CAPACITY, "gpu: routed batches need max_rules >= world x n_rules (per-source stats)");

@@ -335,3 +335,108 @@ def test_gpu_loopback_missing_peer_times_out(monkeypatch):
         rr[0].finish()  # the router stays failed
     for be in bes:
         be.close()
+
+
+@pytest.mark.parametrize("world,lc", [(2, True), (3, False)])
+def test_gpu_loopback_prefixed_host_batches_go_rules(world, lc):
+    """One process per GPU through the Go adapter's own entry point: every
+    rank packs ITS requests (an uneven, sometimes empty slice of each node
+    batch) with the Go batcher's rules into a pinned prefix-shared batch and
+    submits it with rl_do_limit_prefixed_async on its routed ctx (collective,
+    as the batcher's tick); results in pinned host memory after the collective
+    rl_synchronize. Rank-order concatenation == the C oracle over the node
+    batch, stats summed over ranks; a rank whose batch is malformed (bad tile
+    index) takes part with no records and fails alone at rl_synchronize."""
+    import os
+    from ratelimit_amd.limiter import PinnedArena
+    from ratelimit_amd.packing import go_prefixed_batch, go_statuses
+    from ratelimit_amd.sharded import LibRouter, loopback_id
+    os.environ.setdefault("RL_LOOPBACK_TIMEOUT_S", "30")
+    cfg = (0.8, lc, False)
+    calls = streams.random_stream(31 + world, n_calls=900, zipf=True, p_nil=0.15)
+    per = 150
+    node = [calls[k:k + per] for k in range(0, len(calls), per)]
+    uid = loopback_id()
+    bes = [Backend(*cfg, table_slots=1 << 18, max_batch=1 << 15, max_rules=256, device=0, hash_seed=SEED)
+           for _ in range(world)]
+    routers = [LibRouter(be, world, r, uid) for r, be in enumerate(bes)]
+    interner = RuleInterner()  # (one rule-id space for the node, as the config's)
+    for req, lims, _ in calls:
+        for l in lims:
+            if l is not None:
+                interner.intern(l.stats.key)
+    nr = len(interner.keys)
+    out = [None] * world
+    bad_rank, bad_batch = world - 1, 2
+
+    def body(r):
+        arena = PinnedArena()
+        try:
+            res = []
+            for k, part in enumerate(node):
+                cuts = _split_points(len(part), world, k)
+                mine = part[cuts[r]:cuts[r + 1]]
+                pb, where = go_prefixed_batch(mine, "", interner, n_rules=nr,
+                                              alloc=lambda nb: arena.array(nb, np.uint8))
+                if r == bad_rank and k == bad_batch and pb.n_requests:
+                    ix = np.frombuffer(pb.buf, np.uint32, count=4, offset=pb.offsets["index"])
+                    ix[0] = 7  # the index no longer starts at zero: rejected at the call
+                o = {kk: arena.like(v) for kk, v in pb.alloc_result(reset=True).items()}
+                rc = bes[r].do_limit_prefixed_async(pb, o)
+                res.append((mine, where, o, rc, pb))
+            err = None
+            try:
+                bes[r].synchronize()
+            except RedisError as e:
+                err = str(e)
+            out[r] = ("ok", res, err)
+        except Exception:
+            out[r] = ("exc", traceback.format_exc(), None)
+            try:
+                bes[r].synchronize()
+            except Exception:
+                pass
+        finally:
+            out[r] = out[r] + (arena,)
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=90)
+    assert not any(t.is_alive() for t in ts), "a loopback rank hung"
+    try:
+        for r in range(world):
+            assert out[r][0] == "ok", out[r][1]
+        # the malformed rank failed alone, at rl_synchronize
+        assert out[bad_rank][2] is not None and "index" in out[bad_rank][2]
+        for r in range(world - 1):
+            assert out[r][2] is None, out[r][2]
+        co = COracle(*cfg)
+        for k, part in enumerate(node):
+            cuts = _split_points(len(part), world, k)
+            keep = [c for r in range(world) for c in (part[cuts[r]:cuts[r + 1]]
+                                                       if not (r == bad_rank and k == bad_batch) else [])]
+            pk = pack_calls(keep, "", interner, n_rules=nr)
+            exp = co.do_limit(pk.arrays, pk.n, pk.n_requests, pk.n_rules)
+            got_code, got_rem, got_rst = [], [], []
+            tot = np.zeros(nr * abi.RL_NUM_STATS, np.uint64)
+            for r in range(world):
+                if r == bad_rank and k == bad_batch:
+                    continue
+                mine, where, o, _, pb = out[r][1][k]
+                got_code.append(o["code"][:pb.n])
+                got_rem.append(o["limit_remaining"][:pb.n])
+                got_rst.append(o["reset_s"][:pb.n])
+                tot += o["stats"][:nr * abi.RL_NUM_STATS].astype(np.uint64)
+            for f, g in (("code", got_code), ("limit_remaining", got_rem), ("reset_s", got_rst)):
+                g = np.concatenate(g) if g else np.zeros(0)
+                assert np.array_equal(g, exp[f][:pk.n]), (k, f)
+            assert np.array_equal(tot, exp["stats"]), k
+        co.close()
+    finally:
+        for r in range(world):
+            if out[r] is not None:
+                out[r][-1].close()
+        for be in bes:
+            be.close()
