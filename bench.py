@@ -63,7 +63,10 @@ def parse():
                     help="host-fed formats timed (the first is the reported pcie_fed rate)")
     ap.add_argument("--slots-per-key", type=float, default=0.0,
                     help="table slots per live key, rounded to the power of 2 above (0: 4, c3 2)")
-    ap.add_argument("--ring-lines", type=int, default=0, help="history lines (rl_config.ring_lines; 0: slots / 4)")
+    ap.add_argument("--history-entries", type=int, default=0,
+                    help="history log entries (rl_config.history_entries; 0: table slots)")
+    ap.add_argument("--jitter", type=int, default=0,
+                    help="EXPIRATION_JITTER_MAX_SECONDS (the history horizon: older windows kept div + J s)")
     ap.add_argument("--hash-seed", type=int, default=0, help="stem hash key (0: drawn at random per run; reported)")
     ap.add_argument("--route", action="store_true", help="use the routed (all_to_all) path even at N=1")
     ap.add_argument("--route-impl", default="lib", choices=["lib", "python"],
@@ -159,7 +162,8 @@ def main():
     sh = dict(n_shards=args.shards, shard_devices=[local] * args.shards) if args.shards > 1 else {}
     NR = args.n_rules = 3 if args.config == "c2u" else 2  # rules per batch (c2u: the override's own stats key)
     be = Backend(0.8, False, table_slots=slots, max_batch=cap, max_rules=max(8, NR * world * args.shards),
-                 device=local, hash_seed=seed, max_stem_bytes=64 * cap, ring_lines=args.ring_lines, **sh)
+                 device=local, hash_seed=seed, max_stem_bytes=64 * cap, history_entries=args.history_entries,
+                 jitter=args.jitter, **sh)
     now0 = W.NOW0
     py_route = routed and (args.route_impl == "python" or args.dist_backend == "gloo")
     if routed and not py_route:
@@ -376,8 +380,9 @@ def main():
                                "%d-descriptor batches per GPU, %s tenants, now +1 s per batch, all keys pre-inserted"
                                % (args.config.upper(), T / 1e6, 2 * T * world, n, dist_desc),
                    "global_batch": world * n, "batch_per_gpu": n, "live_stem_slots_per_gpu": info["live_slots"],
-                   "table_slots": slots, "ring_lines": info["ring_lines"], "ring_lines_used": info["ring_lines_used"],
-                   "table_hbm_gb": round((slots * 64 + info["ring_lines"] * 128) / 1e9, 2), "hash_seed": seed,
+                   "table_slots": slots, "history_entries": info["history_entries"],
+                   "history_appended": info["history_appended"], "history_lost": info["history_lost"], "jitter": args.jitter,
+                   "table_hbm_gb": round((slots * 64 + info["history_entries"] * 32) / 1e9, 2), "hash_seed": seed,
                    "parallelism": ("hash-sharded table x%d, %s" % (
                                       world, "RCCL send/recv routing inside the library" if not py_route else
                                       "all_to_all routing from Python (%s)" % args.dist_backend)) if routed else

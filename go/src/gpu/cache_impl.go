@@ -150,7 +150,7 @@ func NewRateLimitCacheImplFromSettings(s settings.Settings, localCache *freecach
 	timeSource utils.TimeSource, statsManager stats.Manager) limiter.RateLimitCache {
 	cfg := Config{
 		TableSlots:     s.GpuTableSlots,
-		RingLines:      s.GpuRingLines,
+		HistoryEntries: s.GpuHistoryEntries,
 		ArenaBytes:     s.GpuArenaBytes,
 		MaxBatch:       uint32(s.GpuBatchMaxDescriptors),
 		MaxRequests:    uint32(s.GpuBatchMaxRequests),

@@ -26,7 +26,7 @@ import (
 // (src/redis/fixed_cache_impl.go:118-125) plus the HBM sizing.
 type Config struct {
 	TableSlots     uint64  // 64-B slots (power of 2)
-	RingLines      uint64  // 128-B history lines for keys revisited within 8 windows (0: TableSlots/4)
+	HistoryEntries uint64  // 32-B history log entries: windows below a key's newest (0: TableSlots)
 	ArenaBytes     uint64  // overflow arena for stems longer than 36 B (0: library default)
 	MaxBatch       uint32  // descriptors per batch
 	MaxRequests    uint32  // requests per batch (0: MaxBatch)
@@ -35,7 +35,7 @@ type Config struct {
 	NearLimitRatio float32 // NEAR_LIMIT_RATIO (settings.go:48)
 	LocalCache     bool    // LOCAL_CACHE_SIZE_IN_BYTES != 0 (runner.go:95-98)
 	PerSecond      bool    // REDIS_PERSECOND: SECOND keys in their own store
-	JitterMax      int64   // EXPIRATION_JITTER_MAX_SECONDS (accepted; the draw is 0, DESIGN.md §2)
+	JitterMax      int64   // EXPIRATION_JITTER_MAX_SECONDS (the draw is 0; older windows kept div + JitterMax s)
 	Device         int     // HIP device ordinal
 	HashSeed       uint64  // stem-hash key; 0: a random secret per ctx
 	ShardDevices   []int   // > 1 entries: one table shard per device, routed inside the ctx
@@ -68,7 +68,7 @@ type Ctx struct {
 func New(cfg Config) (*Ctx, error) {
 	var rc C.rl_config
 	rc.table_slots = C.uint64_t(cfg.TableSlots)
-	rc.ring_lines = C.uint64_t(cfg.RingLines)
+	rc.history_entries = C.uint64_t(cfg.HistoryEntries)
 	rc.arena_bytes = C.uint64_t(cfg.ArenaBytes)
 	rc.max_batch = C.uint32_t(cfg.MaxBatch)
 	rc.max_requests = C.uint32_t(cfg.MaxRequests)
@@ -161,7 +161,7 @@ func (c *Ctx) LocalCacheInfo(now int64) (LocalCacheInfo, error) {
 // TableInfo: live slots, tombstones and arena use, summed over shards.
 type TableInfo struct {
 	TableSlots, LiveSlots, Tombstones, ArenaBytesUsed, ExactStems, Batches, Decisions uint64
-	RingLines, RingLinesUsed, LostSlots                                             uint64
+	HistoryEntries, HistoryAppended, HistoryLost, HistorySlots                      uint64
 }
 
 func (c *Ctx) TableInfo() (TableInfo, error) {
@@ -171,7 +171,8 @@ func (c *Ctx) TableInfo() (TableInfo, error) {
 	}
 	return TableInfo{uint64(ti.table_slots), uint64(ti.live_slots), uint64(ti.tombstones),
 		uint64(ti.arena_bytes_used), uint64(ti.exact_stems), uint64(ti.batches), uint64(ti.decisions),
-		uint64(ti.ring_lines), uint64(ti.ring_lines_used), uint64(ti.lost_slots)}, nil
+		uint64(ti.history_entries), uint64(ti.history_appended), uint64(ti.history_lost),
+		uint64(ti.history_slots)}, nil
 }
 
 // ---- pinned host memory: Go never hands Go-heap pointers to C (cgo pointer

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 3u
+#define RL_ABI_VERSION 4u
 
 /* Status codes. */
 enum rl_status {
@@ -78,8 +78,9 @@ typedef struct rl_config {
   int32_t local_cache_enabled;  /* LOCAL_CACHE_SIZE_IN_BYTES != 0 (runner.go:95-98) */
   int32_t per_second_split;     /* REDIS_PERSECOND: SECOND-unit keys in a separate store */
   int32_t device;               /* HIP device ordinal */
-  int64_t expiration_jitter_max_seconds; /* EXPIRATION_JITTER_MAX_SECONDS: accepted; the
-                                            backend fixes the draw at 0 */
+  int64_t expiration_jitter_max_seconds; /* EXPIRATION_JITTER_MAX_SECONDS (>= 0): the backend fixes
+                                            the draw at 0 and keeps a key's older
+                                            windows for div + this many seconds (the history horizon) */
   uint64_t hash_seed;        /* key of the stem hash (SipHash-1-3); 0 = drawn at random per ctx.
                                 Descriptor values are client-controlled: keep it secret. */
   uint32_t n_shards;         /* hash shards of the table held by this ctx (0 = 1); see rl_do_limit */
@@ -87,10 +88,12 @@ typedef struct rl_config {
                                 so that many stems share one sort key and one home region */
   int32_t shard_device[16];  /* HIP device of shard k < n_shards (shards may share a device);
                                 unused when n_shards <= 1 (cfg.device) */
-  uint64_t ring_lines;       /* 128-B history lines (the 8 windows below a key's newest), taken by
-                                the keys revisited within 8 windows and returned by rl_sweep
-                                (0 = table_slots / 4). Exhausted: a key's older record is dropped
-                                and a later request for it fails with RL_E_TIME, never a wrong count */
+  uint64_t history_entries;  /* 32-B entries of the history log holding the windows below a key's
+                                newest (0 = table_slots; rounded to 64 powers of two, at least
+                                max_batch / 16 each). Append-only rings: an entry overwritten while
+                                a request could still ask for its window makes that request fail
+                                with RL_E_TIME (counted in rl_table_info.history_lost), never a
+                                wrong count */
   int32_t reserved[6];
 } rl_config;
 
@@ -100,9 +103,12 @@ typedef struct rl_config {
  * Descriptors appear in arrival order: request-major, descriptor order inside
  * the request; req_idx is non-decreasing. now[] may move backwards (the
  * reference's tests do, on different keys); per (stem, unit) the table keeps
- * the 8 windows below the newest one written (Redis keeps a key div + jitter
- * seconds after its last hit, fixed_cache_impl.go:71-74): a request up to 8
- * windows back is answered exactly, an older one gets RL_E_TIME.
+ * the windows below the newest one written while a request could still ask
+ * for them (Redis keeps a key div + jitter seconds after its last hit,
+ * fixed_cache_impl.go:71-74): a request whose clock is within div +
+ * expiration_jitter_max_seconds of the key's newest window, or whose window
+ * is at most 8 windows back, is answered exactly; an older one whose window
+ * the key may have had gets RL_E_TIME.
  * The stem is the cache key without its window suffix:
  *   prefix ‖ domain ‖ '_' ‖ Σ(key ‖ '_' ‖ value ‖ '_')   (cache_key.go:62-71)
  * The full key is stem ‖ decimal((now/div)*div) (cache_key.go:73-74). */
@@ -171,10 +177,11 @@ typedef struct rl_table_info {
   uint64_t exact_stems;       /* slots flagged multi-unit (exact slow path) */
   uint64_t batches;
   uint64_t decisions;
-  uint64_t ring_lines;        /* history lines in the pool (rl_config.ring_lines) */
-  uint64_t ring_lines_used;   /* lines held by slots (rl_sweep returns a swept slot's line) */
-  uint64_t lost_slots;        /* slots that could not take a line when they needed one: their
-                                 older windows fail with RL_E_TIME (size ring_lines up) */
+  uint64_t history_entries;   /* entries of the history log (rl_config.history_entries, rounded) */
+  uint64_t history_appended;  /* records appended to the log since rl_create / rl_snapshot_load */
+  uint64_t history_lost;      /* lookups that found an entry the log had overwritten: answered
+                                 RL_E_TIME (size history_entries up) */
+  uint64_t history_slots;     /* live slots with a history chain */
 } rl_table_info;
 
 typedef struct rl_ctx rl_ctx;
@@ -581,12 +588,13 @@ typedef struct rl_local_cache_info {
 int rl_local_cache_info_get(rl_ctx* ctx, int64_t now, rl_local_cache_info* info);
 
 /* Table snapshot / restore (Redis RDB-style restart): an exact image of the
- * counter table, the ring-line pool's lines in use and free lists, the
+ * counter table, the history log's written entries and append counters, the
  * long-stem arena, the local-cache state and the sweep time floor.
  * rl_snapshot_size gives the bytes rl_snapshot_save writes into `host`;
  * rl_snapshot_load accepts an image from a ctx with the same table_slots and
- * ring_lines and an arena at least as large (RL_E_INVALID otherwise). Both
- * order after every submitted batch. */
+ * history_entries and an arena at least as large, whose live slots carry a
+ * valid unit and long-stem arena offset (RL_E_INVALID otherwise). Both order
+ * after every submitted batch. */
 int rl_snapshot_size(rl_ctx* ctx, uint64_t* bytes);
 int rl_snapshot_save(rl_ctx* ctx, void* host, uint64_t bytes);
 int rl_snapshot_load(rl_ctx* ctx, const void* host, uint64_t bytes);

@@ -23,7 +23,7 @@ class RlConfig(C.Structure):
                 ("per_second_split", C.c_int32), ("device", C.c_int32),
                 ("expiration_jitter_max_seconds", C.c_int64), ("hash_seed", C.c_uint64),
                 ("n_shards", C.c_uint32), ("debug_hash_bits", C.c_uint32), ("shard_device", C.c_int32 * 16),
-                ("ring_lines", C.c_uint64), ("reserved", C.c_int32 * 6)]
+                ("history_entries", C.c_uint64), ("reserved", C.c_int32 * 6)]
 
 
 class RlBatch(C.Structure):
@@ -75,8 +75,9 @@ class RlRestoreBatch(C.Structure):
 class RlTableInfo(C.Structure):
     _fields_ = [("table_slots", C.c_uint64), ("live_slots", C.c_uint64), ("tombstones", C.c_uint64),
                 ("arena_bytes_used", C.c_uint64), ("exact_stems", C.c_uint64),
-                ("batches", C.c_uint64), ("decisions", C.c_uint64), ("ring_lines", C.c_uint64),
-                ("ring_lines_used", C.c_uint64), ("lost_slots", C.c_uint64)]
+                ("batches", C.c_uint64), ("decisions", C.c_uint64),
+                ("history_entries", C.c_uint64), ("history_appended", C.c_uint64),
+                ("history_lost", C.c_uint64), ("history_slots", C.c_uint64)]
 
 
 class RlConfigNode(C.Structure):
@@ -141,7 +142,7 @@ BATCH_DTYPES = {"stem_bytes": np.uint8, "stem_off": np.uint32, "now": np.int64, 
                 "rule_id": np.uint32}
 RESULT_DTYPES = {"code": np.uint8, "limit_remaining": np.uint32, "reset_s": np.uint32, "stats": np.uint64,
                  "status": np.uint8}
-ABI_VERSION = 3
+ABI_VERSION = 4
 RL_COMM_ID_BYTES = 128  # include/ratelimit_hip.h
 
 

@@ -504,6 +504,8 @@ int rl_do_limit_compact_async(rl_ctx* c, const rl_batch_compact* in, rl_result* 
   // a multi-shard ctx: one request-aligned slice per shard, each over its own
   // device's link (rl_comm's stage_host_compact: the slice's parts, unpacked
   // on the device), then the shards' exchange as for rl_batch host batches
+  // (the shards hold n x max_rules rows: check the ctx's own limit first)
+  if (in->n_rules > c->cfg.max_rules) return fail(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_rules");
   if (const int rc = eng_compact_check(c->e[0], in, out)) return from_engine(c, c->e[0], rc);
   const uint32_t* first = reinterpret_cast<const uint32_t*>(in->buf + in->req_first);
   if (in->n_requests && (first[0] != 0 || first[in->n_requests] != in->n))
@@ -554,6 +556,7 @@ int rl_do_limit_prefixed_async(rl_ctx* c, const rl_batch_prefixed* in, rl_result
   // a multi-shard ctx: one slice of request tiles per shard, each over its own
   // device's link (rl_comm's stage_host_prefixed), then the shards' exchange
   uint32_t tiles = 0;
+  if (in->n_rules > c->cfg.max_rules) return fail(c, RL_E_CAPACITY, "gpu: batch exceeds configured max_rules");
   if (const int rc = eng_prefixed_check(c->e[0], in, out, &tiles)) return from_engine(c, c->e[0], rc);
   rl_batch sizes{};
   sizes.n = in->n;
@@ -678,9 +681,10 @@ int rl_table_info_get(rl_ctx* c, rl_table_info* info) {
     sum.arena_bytes_used += x.arena_bytes_used;
     sum.exact_stems += x.exact_stems;
     sum.decisions += x.decisions;
-    sum.ring_lines += x.ring_lines;
-    sum.ring_lines_used += x.ring_lines_used;
-    sum.lost_slots += x.lost_slots;
+    sum.history_entries += x.history_entries;
+    sum.history_appended += x.history_appended;
+    sum.history_lost += x.history_lost;
+    sum.history_slots += x.history_slots;
     sum.batches = std::max(sum.batches, x.batches);
   }
   *info = sum;
@@ -760,6 +764,10 @@ int rl_snapshot_load(rl_ctx* c, const void* host, uint64_t bytes) {
 
 int rl_config_load(rl_ctx* c, const rl_config_tree* t) {
   if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
+  if (c->n > 1 && t && t->nodes)  // (the shards' own check allows their n x max_rules rows)
+    for (uint32_t i = 0; i < t->n_nodes; i++)
+      if (t->nodes[i].rule_id >= c->cfg.max_rules)
+        return fail(c, RL_E_INVALID, "gpu: config node " + std::to_string(i) + ": rule id >= max_rules");
   for (uint32_t j = 0; j < c->n; j++) {
     const int rc = from_engine(c, c->e[j], eng_config_load(c->e[j], t));
     if (rc) return rc;

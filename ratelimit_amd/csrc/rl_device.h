@@ -18,34 +18,33 @@ namespace rl {
 // the newest window key of its (stem, unit), `cur`. For a stem used with a
 // single unit the current window is the only live key while time moves
 // forward, so the slot is recycled in place when the window advances (no
-// insert per window, no EXPIRE traffic). The HIST_W windows before cur live in
-// a ring line (`Hist`, 128 B: window w < cur at position (w / div) % HIST_W)
-// taken from a pool the first time the slot needs one, i.e. when a window
-// rolls while the old one is still within the ring's reach: a key revisited
-// less often than every HIST_W windows never takes one (C1's SECOND keys), so
-// the table costs 64 B per slot plus 128 B per key that keeps history. The
-// ring answers requests whose time moved back: Redis keeps a key div + jitter
-// seconds after its last hit (fixed_cache_impl.go:71-74), so a request that
-// waited in a batcher finds its window's count. A window more than HIST_W
-// windows back, or one whose record could not be kept because the pool was
-// exhausted (SLOT_LOST), is RL_E_TIME for that descriptor, never a silently
-// wrong count. The ring also keeps the records a stem later seen with a
-// second unit shares with it (only possible through per-request overrides,
-// config_impl.go:254-265; DESIGN.md §"Exact key identity").
+// insert per window, no EXPIRE traffic).
+//
+// Older windows live in the HISTORY LOG: when a key's cur moves to a newer
+// window, the old record is appended to the log (a 32-B entry in one of
+// LOG_PARTS append-only ring buffers) while a request could still ask for it,
+// and the slot's `ring` word becomes the head of the key's chain of entries,
+// newest first. Redis keeps a key div + jitter seconds after its last hit
+// (fixed_cache_impl.go:71-74), so a request that waited in a batcher, or whose
+// clock is behind, finds its window's count: a record is kept while its
+// window is within HIST_W windows of the key's newest one, or its EXPIRE (or
+// local-cache TTL) plus the horizon J (rl_config.expiration_jitter_max_seconds)
+// has not passed the newest window's start. A request older than both bounds
+// whose record is not on the chain is RL_E_TIME; any other request is answered
+// exactly (no record on the chain: the key had none, count 0). An entry the
+// log overwrote before its time (the log too small for the horizon) makes a
+// lookup that reaches it RL_E_TIME, counted in rl_table_info, never a wrong
+// count. The log replaces round 4's pool of 128-B ring lines: appends are
+// wave-aggregated and coalesced, where a line took a random write per move.
 // ---------------------------------------------------------------------------
 constexpr uint32_t WS_INVALID = 0xFFFFFFFFu;  // record never written
 constexpr uint32_t TAG_EMPTY = 0;
 constexpr uint32_t TAG_TOMB = 1;
 constexpr uint32_t KEY_IN = 36;               // a stem of at most KEY_IN bytes is stored whole in its slot
 constexpr uint32_t KEY_SPLIT = 32;            // a longer one: bytes [0, KEY_SPLIT) here, the rest in the arena
-constexpr uint32_t RING_NONE = 0xFFFFFFFFu;   // slot without a ring line
-// ring pool counters: one 128-B line per partition (RING_CTR_STRIDE u64s),
-// so concurrent allocations in different partitions never share a word
-constexpr uint32_t RING_CTR_STRIDE = 16;
-constexpr uint32_t RING_PARTS_MAX = 64;
+constexpr uint32_t RING_NONE = 0xFFFFFFFFu;   // Slot::ring of a key without logged history (= LOG_NONE)
 constexpr uint8_t SLOT_EXACT = 0x1;           // stem has >1 unit slot: exact (serial) path
-constexpr uint8_t SLOT_LOST = 0x2;            // a record below cur was dropped (ring pool exhausted): RL_E_TIME
-constexpr uint32_t HIST_W = 8;                // ring records per slot: windows 1..HIST_W back from cur
+constexpr uint32_t HIST_W = 8;                // windows 1..HIST_W back from cur are always kept
 
 struct Win {
   uint32_t ws;      // window start (Redis key suffix); WS_INVALID = no record
@@ -62,9 +61,9 @@ struct __attribute__((aligned(64))) Slot {
   uint32_t tag;       // TAG_EMPTY / TAG_TOMB / mix(hash(stem), unit) >= 2
   uint16_t key_len;   // stem length
   uint8_t unit;       // rl_unit
-  uint8_t flags;      // SLOT_EXACT | SLOT_LOST
+  uint8_t flags;      // SLOT_EXACT
   Win cur;            // bytes 8..23
-  uint32_t ring;      // 24..27: this slot's ring line in the pool (RING_NONE: none yet)
+  uint32_t ring;      // 24..27: head of the slot's history chain in the log (RING_NONE: none)
   uint8_t key[KEY_IN];  // 28..63: stem bytes (key_len > KEY_IN: bytes 0..31, then the arena offset)
 };
 static_assert(offsetof(Slot, cur) == 8 && offsetof(Slot, ring) == 24 && offsetof(Slot, key) == 28, "slot layout");
@@ -75,16 +74,23 @@ constexpr uint32_t SLOT_EXT_DW = 15;          // arena offset of a stem longer t
 // stem bytes kept in the slot for a stem of len bytes
 __host__ __device__ constexpr uint32_t slot_inline(uint32_t len) { return len <= KEY_IN ? len : KEY_SPLIT; }
 
-// The window records below a slot's cur: one 128-B line of the ring pool.
-struct __attribute__((aligned(128))) Hist {
-  Win w[HIST_W];
+// One entry of the history log: an older window record of slot `slot` (whose
+// tag was `tag` when it was written), the previous entry of the slot's chain,
+// and t_app = the slot's newest window when it was appended (never decreases
+// along a chain; an entry the log overwrote breaks that, or the owner check).
+struct __attribute__((aligned(32))) LogEnt {
+  uint32_t slot, tag, prev, t_app;
+  Win w;
 };
-static_assert(sizeof(Hist) == 128, "ring must be one 128-B line");
-__host__ __device__ inline uint32_t hist_pos(uint32_t ws, uint32_t d) { return (ws / d) % HIST_W; }
-// Window w < cur_ws is within the ring's reach (windows 1..HIST_W back). Within
-// it, the ring record at hist_pos(w) either is w's or w was never written
-// (every later write to that position is of an older window, which is out of
-// reach and therefore never written once w is in the ring).
+static_assert(sizeof(LogEnt) == 32, "log entry is two dwordx4");
+constexpr uint32_t LOG_NONE = RING_NONE;
+constexpr uint32_t LOG_PARTS = 64;                        // partitions (each its own append counter)
+constexpr uint32_t LOG_POS_BITS = 26;                     // entry pointer = part << 26 | position
+constexpr uint32_t LOG_POS_MASK = (1u << LOG_POS_BITS) - 1u;
+constexpr uint32_t LOG_PART_MAX = 1u << 25;               // entries per partition (2^31 in all)
+constexpr uint32_t LOG_CTR_STRIDE = 16;                   // counters on 128-B lines of their own
+constexpr uint32_t LOG_MAX_HOPS = 1u << 16;               // a chain walk gives up (RL_E_TIME) past this
+// Window w < cur_ws is within HIST_W windows of the key's newest one.
 __host__ __device__ inline bool hist_reach(uint32_t w, uint32_t cur_ws, uint32_t d) { return cur_ws - w <= HIST_W * d; }
 
 __host__ __device__ inline uint32_t div_of(uint32_t unit) {  // utils.UnitToDivider

@@ -43,10 +43,6 @@ struct HostSlot {
   hipEvent_t out_done = nullptr;  // its outputs are back on the host (the slot is free)
 };
 
-struct RingPart {
-  uint64_t used, left, taken;
-};
-
 struct Engine {
   rl_config cfg;
   hipStream_t stream = nullptr;   // serial work (== pipe[0])
@@ -63,15 +59,14 @@ struct Engine {
   // table
   Slot* slots = nullptr;
   uint64_t nslots = 0;
-  // the ring pool (window records below the slots' cur, rl_device.h): lines,
-  // the two free lists a sweep alternates between (the current one: ring_cur),
-  // and per partition the counters {B, taken, n} (ring_alloc, rl_kernels.hip)
-  Hist* ring = nullptr;
-  uint64_t ring_cap = 0;
-  uint32_t* ring_free[2] = {};
-  uint32_t ring_cur = 0;
-  unsigned long long* ring_ctr = nullptr;
-  uint32_t ring_parts = 1, ring_part_lines = 0;  // ring_cap = ring_parts x ring_part_lines
+  // the history log (window records below the slots' cur, rl_device.h):
+  // LOG_PARTS partitions of log_cap entries, their append counters (one
+  // 128-B line each; the line after them: the lookups that found an entry
+  // overwritten), and the horizon J in seconds
+  LogEnt* log = nullptr;
+  uint32_t log_cap = 0;
+  unsigned long long* log_ctr = nullptr;
+  uint32_t horizon = 0;
   // RL_DEBUG_COPYTIME: host-fed input copies timed with events (stderr at destroy)
   bool copy_time = false;
   // RL_DEBUG_HOSTTIME: host seconds per section of the host-fed prefixed path (stderr at destroy)

@@ -92,7 +92,10 @@ int map_err(Engine* c, uint32_t e) {
   if (!e) return RL_OK;
   if (e & ERR_TIME) return set_err(c, RL_E_TIME, "gpu: now outside [0, 2^32-172800] or before the last sweep");
   if (e & ERR_HISTORY)
-    return set_err(c, RL_E_TIME, "gpu: time moved back more than 8 windows on a key (the window ring's reach)");
+    return set_err(c, RL_E_TIME,
+                   "gpu: a request's window is older than its key's history holds (more than 8 windows and "
+                   "div + expiration_jitter_max_seconds behind the key's newest, or the history log overwrote it: "
+                   "raise history_entries)");
   if (e & ERR_INVALID) return set_err(c, RL_E_INVALID, "gpu: malformed batch (unit, rule id, request index or stem offsets)");
   if (e & ERR_TABLE_FULL) return set_err(c, RL_E_TABLE_FULL, "gpu: counter table full (raise table_slots or sweep)");
   if (e & ERR_ARENA_FULL) return set_err(c, RL_E_ARENA_FULL, "gpu: long-stem arena full (raise arena_bytes)");
@@ -207,33 +210,26 @@ BatchDev dev_view(const Engine* c, const rl_batch* in, uint32_t stem_cap) {
   return b;
 }
 
-// The ring pool's counters per partition, normalised as k_ring_reset would
-// leave them: `used` lines handed out from the partition's end, `left` free-list
-// entries not taken yet (they start at `taken`). Between batches.
-hipError_t ring_parts_get(Engine* c, std::vector<RingPart>& parts) {
-  std::vector<unsigned long long> ctr((size_t)c->ring_parts * RING_CTR_STRIDE);
-  hipError_t e = hipMemcpyAsync(ctr.data(), c->ring_ctr, ctr.size() * 8, hipMemcpyDeviceToHost, c->stream);
+// The history log's append counters (LOG_PARTS) and its lost-lookup count.
+hipError_t log_ctr_get(Engine* c, std::vector<unsigned long long>& ctr, unsigned long long* lost) {
+  std::vector<unsigned long long> h((size_t)(LOG_PARTS + 1) * LOG_CTR_STRIDE);
+  hipError_t e = hipMemcpyAsync(h.data(), c->log_ctr, h.size() * 8, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) return e;
-  parts.assign(c->ring_parts, RingPart{});
-  for (uint32_t k = 0; k < c->ring_parts; k++) {
-    const unsigned long long* r = &ctr[(size_t)k * RING_CTR_STRIDE];
-    const uint64_t b = r[0], taken = r[1], n = r[2];
-    parts[k].used = std::min<uint64_t>(b + (taken > n ? taken - n : 0), c->ring_part_lines);
-    parts[k].left = n > taken ? n - taken : 0;
-    parts[k].taken = n > taken ? taken : 0;
-  }
+  ctr.resize(LOG_PARTS);
+  for (uint32_t k = 0; k < LOG_PARTS; k++) ctr[k] = h[(size_t)k * LOG_CTR_STRIDE];
+  if (lost) *lost = h[(size_t)LOG_PARTS * LOG_CTR_STRIDE];
   return hipSuccess;
 }
 
 TableDev table_view(Engine* c) {
   TableDev t;
   t.slots = c->slots;
-  t.ring = c->ring;
-  t.ring_free = c->ring_free[c->ring_cur];
-  t.ring_ctr = c->ring_ctr;
-  t.ring_parts = c->ring_parts;
-  t.ring_part_lines = c->ring_part_lines;
+  t.log = c->log;
+  t.log_ctr = c->log_ctr;
+  t.log_cap = c->log_cap;
+  t.horizon = c->horizon;
+  t.hist_lost = c->log_ctr + (size_t)LOG_PARTS * LOG_CTR_STRIDE;
   t.mask = c->nslots - 1;
   t.arena = c->arena;
   t.arena_used16 = c->s[0].counters + 4;
@@ -342,8 +338,10 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   if (!cfg.table_slots) cfg.table_slots = 1ull << 24;
   if (cfg.table_slots & (cfg.table_slots - 1)) return fail("gpu: table_slots must be a power of two", nullptr);
   if (!cfg.arena_bytes) cfg.arena_bytes = 64ull << 20;
-  if (!cfg.ring_lines) cfg.ring_lines = std::max<uint64_t>(cfg.table_slots / 4, 1024);
-  if (cfg.ring_lines > 0xFFFFFFFEull) return fail("gpu: ring_lines must be below 2^32 - 1", nullptr);
+  if (!cfg.history_entries) cfg.history_entries = cfg.table_slots;
+  if (cfg.history_entries > (uint64_t)LOG_PARTS * LOG_PART_MAX)
+    return fail("gpu: history_entries must be at most 2^31", nullptr);
+  if (cfg.expiration_jitter_max_seconds < 0) return fail("gpu: expiration_jitter_max_seconds must be >= 0", nullptr);
   if (!cfg.max_batch) cfg.max_batch = 1u << 20;
   if (cfg.max_batch > MAX_PART_TILES * PART_TILE)
     return fail("gpu: max_batch must be at most 8388608 descriptors", nullptr);
@@ -362,10 +360,18 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   c->cfg.hash_seed = c->hash_seed;
   c->hk = hash_key_of(c->hash_seed, cfg.debug_hash_bits);
   c->nslots = cfg.table_slots;
-  c->ring_parts = cfg.ring_lines >= 64ull * 1024 ? RING_PARTS_MAX : 1u;  // (rl_kernels.hip, ring_alloc)
-  c->ring_part_lines = (uint32_t)(cfg.ring_lines / c->ring_parts);
-  c->ring_cap = (uint64_t)c->ring_parts * c->ring_part_lines;
-  c->cfg.ring_lines = c->ring_cap;
+  {
+    // per partition a power of two, and at least 1/16 of a batch: one batch's
+    // appends (at most one per descriptor, spread over the partitions by
+    // workgroup) never wrap a partition
+    const uint64_t want = std::max<uint64_t>(cfg.history_entries / LOG_PARTS, std::max<uint64_t>(cfg.max_batch / 16, 1024));
+    uint64_t cap = 1;
+    while (cap * 2 <= want && cap * 2 <= LOG_PART_MAX) cap *= 2;
+    if (cap < want && cap < LOG_PART_MAX) cap *= 2;
+    c->log_cap = (uint32_t)cap;
+    c->cfg.history_entries = (uint64_t)LOG_PARTS * cap;
+    c->horizon = (uint32_t)std::min<int64_t>(cfg.expiration_jitter_max_seconds, 1ll << 30);
+  }
   c->arena_cap16 = cfg.arena_bytes / 16;
   const uint32_t n = cfg.max_batch;
   bool ok = true;
@@ -376,9 +382,9 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
          hipEventCreateWithFlags(&c->b_table[k], hipEventDisableTiming) == hipSuccess;
   for (uint32_t k = 0; k < PROGRESS_RING; k++)
     ok = ok && hipEventCreateWithFlags(&c->done_ring[k], hipEventDisableTiming) == hipSuccess;
-  ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess && dalloc(&c->ring, c->ring_cap) == hipSuccess &&
-       dalloc(&c->ring_free[0], c->ring_cap) == hipSuccess && dalloc(&c->ring_free[1], c->ring_cap) == hipSuccess &&
-       dalloc(&c->ring_ctr, (size_t)RING_PARTS_MAX * RING_CTR_STRIDE) == hipSuccess;
+  ok = ok && dalloc(&c->slots, c->nslots) == hipSuccess &&
+       dalloc(&c->log, (size_t)LOG_PARTS * c->log_cap) == hipSuccess &&
+       dalloc(&c->log_ctr, (size_t)(LOG_PARTS + 1) * LOG_CTR_STRIDE) == hipSuccess;
   ok = ok && dalloc(&c->arena, cfg.arena_bytes) == hipSuccess && dalloc(&c->arena2, cfg.arena_bytes) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++) ok = ok && alloc_buffer(c->s[k], n);
   Scratch& s0 = c->s[0];
@@ -419,8 +425,8 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && hipHostMalloc((void**)&c->h_counters, 8 * sizeof(unsigned long long)) == hipSuccess;
   if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
   ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
-       hipMemsetAsync(c->ring_ctr, 0, (size_t)RING_PARTS_MAX * RING_CTR_STRIDE * 8, c->stream) == hipSuccess &&
-       // (lines are initialised when taken)
+       hipMemsetAsync(c->log_ctr, 0, (size_t)(LOG_PARTS + 1) * LOG_CTR_STRIDE * 8, c->stream) == hipSuccess &&
+       // (entries are written before any chain points at them)
        hipMemsetAsync(c->errw, 0, ERRW_WORDS * 4, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.time_floor, 0, 8, c->stream) == hipSuccess &&
        hipMemsetAsync(s0.counters, 0, 64, c->stream) == hipSuccess &&
@@ -499,7 +505,7 @@ void eng_destroy(Engine* c) {
   if (c->caller_ready) (void)hipEventDestroy(c->caller_ready);
   if (c->h_base) (void)hipHostFree(c->h_base);
   const Scratch& s0 = c->s[0];
-  void* bufs[] = {c->slots, c->ring, c->ring_free[0], c->ring_free[1], c->ring_ctr, c->arena, c->arena2, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
+  void* bufs[] = {c->slots, c->log, c->log_ctr, c->arena, c->arena2, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
                   c->d_now, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_status,
                   c->d_rem,
                   c->d_reset, c->d_stats};
@@ -1125,9 +1131,7 @@ int eng_sweep(Engine* c, int64_t now, uint64_t* n_evicted) {
   HIPCHK(c, hipMemsetAsync(c->s[0].counters, 0, 8, c->stream));
   {
     const TableDev t = table_view(c);
-    launch_sweep(t, c->nslots, (uint32_t)now, c->s[0].counters, c->ring_free[c->ring_cur], c->ring_free[c->ring_cur ^ 1],
-                 c->stream);
-    c->ring_cur ^= 1;  // (later batches take lines from the list this sweep built)
+    launch_sweep(t, c->nslots, (uint32_t)now, c->s[0].counters, c->stream);
   }
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 40, hipMemcpyDeviceToHost, c->stream));
@@ -1153,12 +1157,14 @@ int eng_table_info_get(Engine* c, rl_table_info* info) {
   launch_table_info(c->slots, c->nslots, c->s[0].counters, c->stream);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 40, hipMemcpyDeviceToHost, c->stream));
-  std::vector<RingPart> parts;
-  HIPCHK(c, ring_parts_get(c, parts));
-  info->ring_lines = c->ring_cap;
-  info->ring_lines_used = 0;
-  for (const RingPart& r : parts) info->ring_lines_used += r.used - r.left;
-  info->lost_slots = c->h_counters[3];
+  std::vector<unsigned long long> ctr;
+  unsigned long long lost = 0;
+  HIPCHK(c, log_ctr_get(c, ctr, &lost));  // (synchronises: h_counters is read below)
+  info->history_entries = (uint64_t)LOG_PARTS * c->log_cap;
+  info->history_appended = 0;
+  for (unsigned long long k : ctr) info->history_appended += k;
+  info->history_lost = lost;
+  info->history_slots = c->h_counters[3];
   info->table_slots = c->nslots;
   info->live_slots = c->h_counters[0];
   info->tombstones = c->h_counters[1];
@@ -1510,81 +1516,88 @@ int eng_local_cache_info_get(Engine* c, int64_t now, rl_local_cache_info* info) 
 }
 
 namespace {
-constexpr uint64_t SNAP_MAGIC = 0x34304150414e534cull;  // "LSNAPA04" (64-B slots, partitioned ring pool)
+constexpr uint64_t SNAP_MAGIC = 0x35304150414e534cull;  // "LSNAPA05" (64-B slots, history log)
 struct SnapHeader {
   uint64_t magic, nslots, arena_used16, hash_seed;  // slots are placed by the keyed hash: restore adopts its key
   int64_t time_floor;
-  uint64_t ring_lines;  // ring_parts x ring_part_lines: slots hold line indices, so restore needs the same pool
-  uint32_t ring_parts, ring_part_lines;
-  uint64_t reserved;
+  uint32_t log_parts, log_cap;  // slots hold entry pointers, so restore needs the same log geometry
+  uint64_t reserved[2];
 };
 static_assert(sizeof(SnapHeader) == 64, "snapshot header");
-// then: the slots; RingPart {used, left} per partition; per partition its
-// lines [p L, p L + used); per partition its free list's `left` entries;
-// the used arena
+// then: the slots; the LOG_PARTS append counters; per partition its written
+// entries [0, min(counter, log_cap)); the used arena
 
-int snap_state(Engine* c, SnapHeader* h, std::vector<RingPart>& parts) {
+uint64_t part_entries(unsigned long long ctr, uint32_t cap) { return std::min<uint64_t>(ctr, cap); }
+
+int snap_state(Engine* c, SnapHeader* h, std::vector<unsigned long long>& ctr) {
   HIPCHK(c, hipSetDevice(c->cfg.device));
   HIPCHK(c, after_batches(c, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 64, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(&h->time_floor, c->s[0].time_floor, 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, ring_parts_get(c, parts));
+  HIPCHK(c, log_ctr_get(c, ctr, nullptr));
   h->arena_used16 = std::min<uint64_t>(c->h_counters[4], c->arena_cap16);
-  h->ring_lines = c->ring_cap;
-  h->ring_parts = c->ring_parts;
-  h->ring_part_lines = c->ring_part_lines;
+  h->log_parts = LOG_PARTS;
+  h->log_cap = c->log_cap;
   return RL_OK;
 }
 
-uint64_t snap_bytes(const Engine* c, const SnapHeader& h, const std::vector<RingPart>& parts) {
-  uint64_t b = sizeof(SnapHeader) + c->nslots * sizeof(Slot) + parts.size() * 16 + h.arena_used16 * 16;
-  for (const RingPart& r : parts) b += r.used * sizeof(Hist) + r.left * 4;
+uint64_t snap_bytes(uint64_t nslots, const SnapHeader& h, const std::vector<unsigned long long>& ctr) {
+  uint64_t b = sizeof(SnapHeader) + nslots * sizeof(Slot) + (uint64_t)h.log_parts * 8 + h.arena_used16 * 16;
+  for (unsigned long long k : ctr) b += part_entries(k, h.log_cap) * sizeof(LogEnt);
   return b;
+}
+
+// A slot image the kernels can use without reading past the arena: a live
+// slot's unit is a rate-limit unit and a long stem's tail lies in the used
+// arena. (Chain pointers need no check: every one addresses the log, and a
+// foreign or stale entry fails its owner check: RL_E_TIME, never a count.)
+bool slots_valid(const Slot* s, uint64_t n, uint64_t arena_used16) {
+  for (uint64_t i = 0; i < n; i++) {
+    if (s[i].tag < 2) continue;
+    if (s[i].unit < RL_UNIT_SECOND || s[i].unit > RL_UNIT_DAY) return false;
+    if (s[i].key_len > KEY_IN) {
+      const uint32_t off = reinterpret_cast<const uint32_t*>(&s[i])[SLOT_EXT_DW];
+      if ((uint64_t)off + (s[i].key_len - KEY_SPLIT + 15) / 16 > arena_used16) return false;
+    }
+  }
+  return true;
 }
 }  // namespace
 
 int eng_snapshot_size(Engine* c, uint64_t* bytes) {
   if (!c || !bytes) return set_err(c, RL_E_INVALID, "gpu: null argument");
   SnapHeader h{};
-  std::vector<RingPart> parts;
-  int rc = snap_state(c, &h, parts);
+  std::vector<unsigned long long> ctr;
+  int rc = snap_state(c, &h, ctr);
   if (rc) return rc;
-  *bytes = snap_bytes(c, h, parts);
+  *bytes = snap_bytes(c->nslots, h, ctr);
   return RL_OK;
 }
 
 int eng_snapshot_save(Engine* c, void* host, uint64_t bytes) {
   if (!c || !host) return set_err(c, RL_E_INVALID, "gpu: null argument");
   SnapHeader h{};
-  std::vector<RingPart> parts;
-  int rc = snap_state(c, &h, parts);
+  std::vector<unsigned long long> ctr;
+  int rc = snap_state(c, &h, ctr);
   if (rc) return rc;
   h.magic = SNAP_MAGIC;
   h.nslots = c->nslots;
   h.hash_seed = c->hash_seed;
-  if (bytes < snap_bytes(c, h, parts))
+  if (bytes < snap_bytes(c->nslots, h, ctr))
     return set_err(c, RL_E_CAPACITY, "gpu: snapshot buffer smaller than rl_snapshot_size");
   uint8_t* p = (uint8_t*)host;
   memcpy(p, &h, sizeof h);
   p += sizeof h;
-  const uint64_t tb = c->nslots * sizeof(Slot), L = c->ring_part_lines;
+  const uint64_t tb = c->nslots * sizeof(Slot);
   HIPCHK(c, hipMemcpy(p, c->slots, tb, hipMemcpyDeviceToHost));
   p += tb;
-  for (const RingPart& r : parts) {
-    const uint64_t ul[2] = {r.used, r.left};
-    memcpy(p, ul, 16);
-    p += 16;
-  }
-  for (uint32_t k = 0; k < parts.size(); k++) {
-    if (parts[k].used) HIPCHK(c, hipMemcpy(p, c->ring + k * L, parts[k].used * sizeof(Hist), hipMemcpyDeviceToHost));
-    p += parts[k].used * sizeof(Hist);
-  }
-  for (uint32_t k = 0; k < parts.size(); k++) {
-    if (parts[k].left)
-      HIPCHK(c, hipMemcpy(p, c->ring_free[c->ring_cur] + k * L + parts[k].taken, parts[k].left * 4,
-                          hipMemcpyDeviceToHost));
-    p += parts[k].left * 4;
+  memcpy(p, ctr.data(), ctr.size() * 8);
+  p += ctr.size() * 8;
+  for (uint32_t k = 0; k < LOG_PARTS; k++) {
+    const uint64_t m = part_entries(ctr[k], c->log_cap);
+    if (m) HIPCHK(c, hipMemcpy(p, c->log + (size_t)k * c->log_cap, m * sizeof(LogEnt), hipMemcpyDeviceToHost));
+    p += m * sizeof(LogEnt);
   }
   if (h.arena_used16) HIPCHK(c, hipMemcpy(p, c->arena, h.arena_used16 * 16, hipMemcpyDeviceToHost));
   return RL_OK;
@@ -1598,37 +1611,29 @@ int eng_snapshot_load(Engine* c, const void* host, uint64_t bytes) {
   if (h.magic != SNAP_MAGIC) return set_err(c, RL_E_INVALID, "gpu: not a table snapshot");
   if (h.nslots != c->nslots) return set_err(c, RL_E_INVALID, "gpu: snapshot table_slots differ from this ctx");
   if (h.arena_used16 > c->arena_cap16) return set_err(c, RL_E_INVALID, "gpu: snapshot arena larger than this ctx's");
-  if (h.ring_parts != c->ring_parts || h.ring_part_lines != c->ring_part_lines)
-    return set_err(c, RL_E_INVALID, "gpu: snapshot ring_lines differ from this ctx");
+  if (h.log_parts != LOG_PARTS || h.log_cap != c->log_cap)
+    return set_err(c, RL_E_INVALID, "gpu: snapshot history_entries differ from this ctx");
   const uint8_t* p = (const uint8_t*)host + sizeof h;
-  const uint64_t tb = h.nslots * sizeof(Slot), L = c->ring_part_lines;
-  if (bytes < sizeof h + tb + h.ring_parts * 16ull) return set_err(c, RL_E_INVALID, "gpu: snapshot truncated");
-  std::vector<RingPart> parts(h.ring_parts);
-  for (uint32_t k = 0; k < h.ring_parts; k++) {
-    uint64_t ul[2];
-    memcpy(ul, p + tb + 16ull * k, 16);
-    if (ul[0] > L || ul[1] > L) return set_err(c, RL_E_INVALID, "gpu: snapshot ring partition out of range");
-    parts[k].used = ul[0];
-    parts[k].left = ul[1];
-  }
-  if (bytes < snap_bytes(c, h, parts)) return set_err(c, RL_E_INVALID, "gpu: snapshot truncated");
+  const uint64_t tb = h.nslots * sizeof(Slot);
+  if (bytes < sizeof h + tb + LOG_PARTS * 8ull) return set_err(c, RL_E_INVALID, "gpu: snapshot truncated");
+  std::vector<unsigned long long> ctr(LOG_PARTS);
+  memcpy(ctr.data(), p + tb, LOG_PARTS * 8);
+  if (bytes < snap_bytes(h.nslots, h, ctr)) return set_err(c, RL_E_INVALID, "gpu: snapshot truncated");
+  if (!slots_valid(reinterpret_cast<const Slot*>(p), h.nslots, h.arena_used16))
+    return set_err(c, RL_E_INVALID, "gpu: snapshot slots inconsistent (unit or long-stem arena offset)");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   HIPCHK(c, after_batches(c, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(c->slots, p, tb, hipMemcpyHostToDevice));
-  p += tb + h.ring_parts * 16ull;
-  for (uint32_t k = 0; k < h.ring_parts; k++) {
-    if (parts[k].used) HIPCHK(c, hipMemcpy(c->ring + k * L, p, parts[k].used * sizeof(Hist), hipMemcpyHostToDevice));
-    p += parts[k].used * sizeof(Hist);
+  p += tb + LOG_PARTS * 8ull;
+  for (uint32_t k = 0; k < LOG_PARTS; k++) {
+    const uint64_t m = part_entries(ctr[k], c->log_cap);
+    if (m) HIPCHK(c, hipMemcpy(c->log + (size_t)k * c->log_cap, p, m * sizeof(LogEnt), hipMemcpyHostToDevice));
+    p += m * sizeof(LogEnt);
   }
-  std::vector<unsigned long long> ctr((size_t)RING_PARTS_MAX * RING_CTR_STRIDE, 0ull);
-  for (uint32_t k = 0; k < h.ring_parts; k++) {
-    if (parts[k].left) HIPCHK(c, hipMemcpy(c->ring_free[c->ring_cur] + k * L, p, parts[k].left * 4, hipMemcpyHostToDevice));
-    p += parts[k].left * 4;
-    ctr[(size_t)k * RING_CTR_STRIDE + 0] = parts[k].used;
-    ctr[(size_t)k * RING_CTR_STRIDE + 2] = parts[k].left;
-  }
-  HIPCHK(c, hipMemcpy(c->ring_ctr, ctr.data(), ctr.size() * 8, hipMemcpyHostToDevice));
+  std::vector<unsigned long long> hc((size_t)(LOG_PARTS + 1) * LOG_CTR_STRIDE, 0ull);
+  for (uint32_t k = 0; k < LOG_PARTS; k++) hc[(size_t)k * LOG_CTR_STRIDE] = ctr[k];
+  HIPCHK(c, hipMemcpy(c->log_ctr, hc.data(), hc.size() * 8, hipMemcpyHostToDevice));
   if (h.arena_used16) HIPCHK(c, hipMemcpy(c->arena, p, h.arena_used16 * 16, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->s[0].counters + 4, &h.arena_used16, 8, hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->s[0].time_floor, &h.time_floor, 8, hipMemcpyHostToDevice));

@@ -126,14 +126,14 @@ struct OutDev {
 
 struct TableDev {
   Slot* slots;
-  // the ring pool: lines handed to slots on first need (Slot::ring); the last
-  // sweep's freed lines are taken first, then the pool's untouched end
-  Hist* ring;
-  // the pool in ring_parts partitions of ring_part_lines lines, each with its
-  // own counters (RING_CTR_STRIDE apart) and its own segment of the free list
-  const uint32_t* ring_free;     // [ring_parts * ring_part_lines] lines freed by the last sweep
-  unsigned long long* ring_ctr;  // per partition {B, taken, n} (ring_alloc)
-  uint32_t ring_parts, ring_part_lines;
+  // the history log (rl_device.h): LOG_PARTS append-only ring buffers of
+  // log_cap entries each, one append counter per partition (LOG_CTR_STRIDE
+  // apart); horizon = J seconds (rl_config.expiration_jitter_max_seconds)
+  LogEnt* log;
+  unsigned long long* log_ctr;
+  uint32_t log_cap;  // entries per partition (power of 2)
+  uint32_t horizon;
+  unsigned long long* hist_lost;  // lookups that met an entry the log had overwritten
   uint64_t mask;
   uint8_t* arena;
   unsigned long long* arena_used16;
@@ -289,10 +289,8 @@ void launch_route_ret(const unsigned long long* res, uint32_t n, const uint32_t*
 // out[i] = sum over blocks b of stage[b * stride + i], i < m (stride 0: m).
 void launch_stats_sum(const unsigned long long* stage, uint32_t n_blocks, uint32_t m, unsigned long long* out,
                       hipStream_t st, uint32_t stride = 0);
-// The epoch sweep: rebase the free list (free_from: the lines the previous
-// sweep freed, free_to: the list this one builds), then evict.
-void launch_sweep(const TableDev& t, uint64_t nslots, uint32_t now, unsigned long long* evicted,
-                  const uint32_t* free_from, uint32_t* free_to, hipStream_t st);
+// The epoch sweep: evict the slots whose records (cur and logged) are all dead.
+void launch_sweep(const TableDev& t, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st);
 void launch_arena_compact(Slot* slots, uint64_t nslots, const uint8_t* from, uint8_t* to, unsigned long long* used16,
                           hipStream_t st);
 void launch_lc_count(const TableDev& t, uint64_t nslots, uint32_t now, unsigned long long* out, hipStream_t st);

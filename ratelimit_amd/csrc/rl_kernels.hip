@@ -427,7 +427,13 @@ hipError_t copy_to_host(ToHost c, hipStream_t st) {
   ToHost m = c;
   for (uint32_t k = 0; k < c.n && mapped; k++) {
     void* dp = nullptr;
-    mapped = c.bytes[k] == 0 || (hipHostGetDevicePointer(&dp, c.dst[k], 0) == hipSuccess && dp);
+    void* de = nullptr;
+    // both ends inside one page-locked allocation (an array running past its
+    // allocation's end would have the kernel store to unmapped device VA)
+    mapped = c.bytes[k] == 0 ||
+             (hipHostGetDevicePointer(&dp, c.dst[k], 0) == hipSuccess && dp &&
+              hipHostGetDevicePointer(&de, c.dst[k] + c.bytes[k] - 1, 0) == hipSuccess &&
+              (uint8_t*)de == (uint8_t*)dp + c.bytes[k] - 1);
     m.dst[k] = (uint8_t*)dp;
   }
   if (mapped) {
@@ -631,7 +637,7 @@ __device__ __attribute__((always_inline)) inline bool arena_claim(const TableDev
   }
 }
 
-// Fill a freshly claimed slot (no ring line: taken on first need). False when
+// Fill a freshly claimed slot (no history yet). False when
 // the arena cannot take the stem's tail: the caller returns the slot to the
 // table as a tombstone.
 __device__ __attribute__((always_inline)) inline bool slot_init(const TableDev& t, Slot* s, const Key& key, uint32_t unit) {
@@ -654,7 +660,7 @@ __device__ __attribute__((always_inline)) inline bool slot_init(const TableDev& 
     else if (k == nw && (il & 3)) sd[slot_key_dw(k)] = key_dw(key, k) & tail_mask(il);
   }
   s->cur = Win{WS_INVALID, 0, 0, 0};
-  s->ring = RING_NONE;
+  s->ring = LOG_NONE;
   return true;
 }
 
@@ -723,7 +729,7 @@ __device__ __attribute__((always_inline)) inline int64_t find_slot(const TableDe
 }
 
 // A slot image for probing: the whole 64-B slot (tag, length, flags, cur,
-// ring line, stem bytes 0..35). Plain loads are enough: within a launch only
+// history chain head, stem bytes 0..35). Plain loads are enough: within a launch only
 // CAS inserts change tags, and a lane only ever looks for its own stem, which
 // no other lane inserts.
 struct SlotImg {
@@ -758,60 +764,83 @@ __device__ inline bool img_key_equal(const SlotImg& im, const Key& key, const ui
   return d == 0;
 }
 
-// ---- the ring pool, in ring_parts partitions of L = ring_part_lines lines.
-// Partition p's counters {B, taken, n}: lines [0, B) of the partition have
-// been handed out from its end, its free-list segment holds n lines, and
-// `taken` numbers the lines taken since the last sweep: number k is
-// free[p L + k] below n, line p L + B + (k - n) above, none past L. B and n
-// only change in rl_sweep (k_ring_reset), between batches, so one counter
-// serves both; the active lanes of a wave take their numbers with one atomic,
-// and waves start at partitions spread by workgroup and wave, so a burst of
-// first window moves (every key revisited within 8 windows takes a line once)
-// does not serialise on one word. An exhausted partition sends the lanes on
-// to the next; RING_NONE once every partition is.
-__device__ inline uint32_t ring_alloc(const TableDev& t) {
-  const uint32_t P = t.ring_parts, L = t.ring_part_lines, lane = __lane_id();
-  uint32_t p = (blockIdx.x * 4u + (threadIdx.x >> 6)) & (P - 1u);
-  for (uint32_t tries = 0; tries < P; tries++, p = (p + 1u) & (P - 1u)) {
-    unsigned long long* ctr = t.ring_ctr + (size_t)p * RING_CTR_STRIDE;
-    // (an exhausted partition: skip it without an atomic; a stale read only costs one)
-    if (tries && __hip_atomic_load(&ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ctr[2] + L - ctr[0])
-      continue;
-    const uint64_t act = __ballot(1);
-    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)act) - 1u;
-    unsigned long long k = 0;
-    if (lane == leader) k = atomicAdd(&ctr[1], (unsigned long long)__popcll(act));
-    k = __shfl(k, leader, 64) + (unsigned long long)__popcll(act & ((1ull << lane) - 1ull));
-    const unsigned long long n = ctr[2];
-    if (k < n) return t.ring_free[(size_t)p * L + k];
-    const unsigned long long b = ctr[0] + (k - n);
-    if (b < L) return p * L + (uint32_t)b;
-  }
-  return RING_NONE;
+// ---- the history log (rl_device.h). A record of a slot with divider d is
+// kept while a request could still ask for it: its window within HIST_W
+// windows of the key's newest (ws_new), or its EXPIRE / local-cache TTL plus
+// J + d not before ws_new (J = the horizon, rl_config's jitter bound). A
+// request whose window has no record on the chain was never written — unless
+// both bounds have passed, where a dropped record could have been: then
+// RL_E_TIME. Sound: a dropped record r has max(r.expire, r.lc) + J + d <
+// ws_new <= cur, so a request with now + J + d >= cur finds it dead (now >
+// r.expire, now >= r.lc), i.e. equal to no record. Exact therefore for every
+// request whose clock is within div + J of the key's newest window, and for
+// any within HIST_W windows of it.
+__device__ inline bool hist_keep(const TableDev& t, const Win& r, uint32_t ws_new, uint32_t d) {
+  return r.ws != WS_INVALID &&
+         (hist_reach(r.ws, ws_new, d) || (uint64_t)max(r.expire, r.lc) + t.horizon + d >= (uint64_t)ws_new);
+}
+// own: the slot's records are written by its own unit's requests only (the
+// simple path), so a record of w is dead from w + 2 div on (EXPIRE and the
+// local-cache TTL end before then); alias writes (the general path) can move
+// EXPIRE further.
+__device__ inline bool hist_absent_ok(const TableDev& t, uint32_t now, uint32_t w, uint32_t cur_ws, uint32_t d,
+                                      bool own) {
+  return hist_reach(w, cur_ws, d) || (uint64_t)now + t.horizon + d >= (uint64_t)cur_ws ||
+         (own && (uint64_t)now >= (uint64_t)w + 2ull * d);
 }
 
-// Slot s's ring line for a write: its own, or a fresh one (every record
-// WS_INVALID, recorded in the slot). Null when the pool is exhausted: the slot
-// is flagged SLOT_LOST (a record below its cur was dropped; a request for
-// such a window is RL_E_TIME from then on).
-__device__ inline Win* ring_for_write(const TableDev& t, Slot* s, uint32_t& ridx) {
-  if (ridx != RING_NONE) return t.ring[ridx].w;
-  const uint32_t k = ring_alloc(t);
-  if (k == RING_NONE) {
-    s->flags |= SLOT_LOST;
-    return nullptr;
-  }
-  uint4* line = reinterpret_cast<uint4*>(&t.ring[k]);
-#pragma unroll
-  for (uint32_t j = 0; j < HIST_W; j++) line[j] = make_uint4(WS_INVALID, 0u, 0u, 0u);
-  s->ring = k;
-  ridx = k;
-  return t.ring[k].w;
+// Append r to the chain whose head is prev (slot si, tag, newest window
+// t_app); returns the new head. The active lanes of a wave take consecutive
+// entries of one partition with one atomic (partitions spread by workgroup
+// and wave), so appends are coalesced stores.
+__device__ inline uint32_t log_append(const TableDev& t, uint32_t si, uint32_t tag, uint32_t prev, uint32_t t_app,
+                                      const Win& r) {
+  const uint32_t lane = __lane_id();
+  const uint32_t p = (blockIdx.x * 4u + (threadIdx.x >> 6)) & (LOG_PARTS - 1u);
+  const uint64_t act = __ballot(1);
+  const uint32_t leader = (uint32_t)__ffsll((unsigned long long)act) - 1u;
+  unsigned long long k = 0;
+  if (lane == leader) k = atomicAdd(&t.log_ctr[(size_t)p * LOG_CTR_STRIDE], (unsigned long long)__popcll(act));
+  k = __shfl(k, leader, 64) + (unsigned long long)__popcll(act & ((1ull << lane) - 1ull));
+  const uint32_t pos = (uint32_t)k & (t.log_cap - 1u);
+  uint4* e = reinterpret_cast<uint4*>(&t.log[(size_t)p * t.log_cap + pos]);
+  e[0] = make_uint4(si, tag, prev, t_app);
+  e[1] = make_uint4(r.ws, r.count, r.expire, r.lc);
+  return (p << LOG_POS_BITS) | pos;
 }
 
-// The record at ring position pos of a slot whose line is ridx.
-__device__ inline Win ring_read(const TableDev& t, uint32_t ridx, uint32_t pos) {
-  return ridx == RING_NONE ? Win{WS_INVALID, 0, 0, 0} : t.ring[ridx].w[pos];
+// The newest logged record of window w on slot si's chain from head (cur_ws:
+// the slot's newest window): 1 found (*out), 0 none on the chain, -1 an
+// entry on the way was overwritten (the log wrapped) before w could be ruled
+// out. An entry overwritten by a newer one of the same slot (the owner check
+// passes) lies on the chain already: the walk comes back to it, a cycle that
+// Brent's check finds within twice its length.
+__device__ inline int log_find(const TableDev& t, uint32_t head, uint32_t si, uint32_t tag, uint32_t cur_ws,
+                               uint32_t w, Win* out) {
+  uint32_t ptr = head, tprev = cur_ws, saved = LOG_NONE, power = 1, lam = 0;
+  for (uint32_t hops = 0; ptr != LOG_NONE; hops++) {
+    const uint32_t pos = ptr & LOG_POS_MASK;
+    if (hops == LOG_MAX_HOPS || pos >= t.log_cap || ptr == saved) break;
+    if (++lam == power) {
+      saved = ptr;
+      power <<= 1;
+      lam = 0;
+    }
+    const uint4* e = reinterpret_cast<const uint4*>(&t.log[(size_t)(ptr >> LOG_POS_BITS) * t.log_cap + pos]);
+    const uint4 a = e[0];
+    if (a.x != si || a.y != tag || a.w > tprev) break;  // overwritten
+    const uint4 b = e[1];
+    if (b.x == w) {
+      *out = Win{b.x, b.y, b.z, b.w};
+      return 1;
+    }
+    if (a.w <= w) return 0;  // every older entry holds a window below its t_app <= w
+    tprev = a.w;
+    ptr = a.z;
+  }
+  if (ptr == LOG_NONE) return 0;
+  atomicAdd(t.hist_lost, 1ull);
+  return -1;
 }
 
 // find_slot with insert, returning the slot's image (a fresh slot's image for
@@ -987,14 +1016,15 @@ __device__ __attribute__((always_inline)) inline void emit(unsigned long long* r
 }
 
 // ---- single (stem, unit) slot, stem never seen with another unit: registers
-// only. cur is the slot's newest window; `old` caches one ring record (that of
-// the last older window touched), written back when another one is needed.
+// only. cur is the slot's newest window; `old` caches one older record (that
+// of the last older window touched: the old cur after a roll, or one found on
+// the slot's history chain), appended to the log when another one is needed
+// or at the end, if it changed and a request could still ask for it.
 struct SimpleState {
   Win cur, old;
-  Slot* slot;
-  uint32_t ridx;  // the slot's ring line (RING_NONE: none yet)
-  bool lost;      // SLOT_LOST: a record below cur may have been dropped
-  bool cur_dirty, old_dirty;
+  uint32_t si, tag;  // the slot and its tag (owner of its log entries)
+  uint32_t chain;    // head of the slot's history chain (Slot::ring)
+  bool cur_dirty, old_dirty, chain_dirty;
   uint32_t cur_req;
   bool pend;
   uint32_t pend_w, pend_e;
@@ -1012,43 +1042,40 @@ struct SimpleState {
   }
 };
 
-// The record of window w: 0 = cur (rolled forward when w is newer: the old cur
-// moves to the ring with one write, no read), 1 = S.old, the ring record of w
-// (loaded, or started afresh when w was never written), -1 = w is more than
-// HIST_W windows back (RL_E_TIME, never a silently wrong count).
-// A ring record back to the slot's line (taken on first need).
-__device__ __attribute__((always_inline)) inline void simple_put(const TableDev& t, SimpleState& S, const Win& r, uint32_t d) {
-  Win* line = ring_for_write(t, S.slot, S.ridx);
-  if (line) line[hist_pos(r.ws, d)] = r;
-  else S.lost = true;
+// S.old to the log (a new version on the slot's chain: lookups take the newest)
+__device__ __attribute__((always_inline)) inline void simple_put(const TableDev& t, SimpleState& S) {
+  S.chain = log_append(t, S.si, S.tag, S.chain, S.cur.ws, S.old);
+  S.chain_dirty = true;
+  S.old_dirty = false;
 }
 
-__device__ __attribute__((always_inline)) inline int simple_pick(const TableDev& t, SimpleState& S, uint32_t w, uint32_t d) {
+// The record of window w: 0 = cur (rolled forward when w is newer: the old cur
+// becomes S.old while a request could still ask for it), 1 = S.old, the
+// record of an older w (found on the chain, or started afresh when w never
+// had one), -1 = w's record may have been dropped or overwritten (RL_E_TIME,
+// never a silently wrong count).
+__device__ __attribute__((always_inline)) inline int simple_pick(const TableDev& t, SimpleState& S, uint32_t w, uint32_t d,
+                                                                 uint32_t now) {
   if (S.cur.ws == w) return 0;
   if (S.cur.ws == WS_INVALID || w > S.cur.ws) {
-    if (S.cur.ws != WS_INVALID && hist_reach(S.cur.ws, w, d)) {
-      // the cached record goes back first, unless the old cur takes its
-      // position (then it is out of the ring's reach from the new cur)
-      if (S.old_dirty && hist_pos(S.old.ws, d) != hist_pos(S.cur.ws, d)) simple_put(t, S, S.old, d);
-      S.old = S.cur;
-      S.old_dirty = true;
-    } else if (S.cur.ws != WS_INVALID) {
-      // the old cur, and every older record, is out of the ring's reach from
-      // w: no lookup can reach them again (simple_pick answers RL_E_TIME
-      // first) and their expiry and local-cache entry are past w, so they
-      // are not written back (a key revisited after more than HIST_W windows,
-      // e.g. a SECOND key every ~20 s at C1: one random write less)
-      S.old_dirty = false;
+    if (S.cur.ws != WS_INVALID) {
+      if (S.old_dirty) simple_put(t, S);
+      // a key revisited after more than HIST_W windows with the horizon past
+      // (C1's SECOND keys at J = 0): nothing written
+      if (hist_keep(t, S.cur, w, d)) {
+        S.old = S.cur;
+        S.old_dirty = true;
+      }
     }
     S.cur = Win{w, 0, 0, 0};
     return 0;
   }
-  if (!hist_reach(w, S.cur.ws, d)) return -1;
   if (S.old.ws != w) {
-    if (S.old_dirty) simple_put(t, S, S.old, d);
-    if (S.lost) return -1;  // (w's record may be one the exhausted pool could not keep)
-    const Win r = ring_read(t, S.ridx, hist_pos(w, d));
-    S.old = r.ws == w ? r : Win{w, 0, 0, 0};
+    if (S.old_dirty) simple_put(t, S);
+    Win r;
+    const int f = S.chain == LOG_NONE ? 0 : log_find(t, S.chain, S.si, S.tag, S.cur.ws, w, &r);
+    if (f < 0 || (f == 0 && !hist_absent_ok(t, now, w, S.cur.ws, d, true))) return -1;
+    S.old = f ? r : Win{w, 0, 0, 0};
     S.old_dirty = false;
   }
   return 1;
@@ -1061,8 +1088,8 @@ __device__ __attribute__((always_inline)) inline void simple_step(const TableDev
     S.apply_pending();
     S.cur_req = x.req;
   }
-  const int which = simple_pick(t, S, x.w, x.d);
-  if (which < 0) {  // older than the ring reaches: this descriptor's RL_E_TIME
+  const int which = simple_pick(t, S, x.w, x.d, x.now);
+  if (which < 0) {  // its window's record may be gone: this descriptor's RL_E_TIME
     if (P.isolate) res[x.e] = pack_fail(RL_E_TIME);
     if (!(RL_ABL & 1)) atomicOr(err, ERR_HISTORY);  // (ablation builds probe garbage slots)
     return;
@@ -1101,14 +1128,18 @@ __device__ __attribute__((always_inline)) inline void simple_step(const TableDev
 }
 
 // ---- general: every unit slot of the stem, Redis keys shared across units.
-// Each unit's cur lives in registers; ring records are read and written in
-// place (the exact path is rare).
+// Each unit's cur lives in registers, with one older record per unit cached
+// beside it (as SimpleState::old: appended to the unit slot's chain when
+// another one is needed, or at the end, if it changed). The exact path is rare.
 struct GeneralState {
   int64_t sidx[4];
   Win cur[4];
-  uint32_t ridx[4];  // each unit slot's ring line (RING_NONE: none yet)
-  uint32_t lost;     // bit u-1: that slot is SLOT_LOST (a record below its cur may be gone)
-  uint32_t present;  // bit u-1
+  Win old[4];         // per unit: an older record (WS_INVALID: none cached)
+  uint32_t tag[4];    // each unit slot's tag (owner of its log entries)
+  uint32_t chain[4];  // each unit slot's history chain head
+  uint32_t odirty;    // bit u-1: old[u-1] changed
+  uint32_t cdirty;    // bit u-1: chain[u-1] changed
+  uint32_t present;   // bit u-1
   uint32_t cur_req;
   uint32_t npend;
   uint32_t pend_w[4], pend_e[4];
@@ -1116,28 +1147,54 @@ struct GeneralState {
 
 __device__ inline bool ps_class(const Params& P, uint32_t k) { return P.per_second && k == 0; }
 
-// The record of window w in unit slot k (present): its cur, its ring record,
-// or null when unit k never wrote w. *lost: w may have been written but is
-// out of the ring's reach, or was dropped (SLOT_LOST).
-__device__ inline Win* gen_rec(const TableDev& t, GeneralState& G, uint32_t k, uint32_t w, bool* lost) {
+// old[k] to the log
+__device__ inline void gen_put(const TableDev& t, GeneralState& G, uint32_t k) {
+  G.chain[k] = log_append(t, (uint32_t)G.sidx[k], G.tag[k], G.chain[k], G.cur[k].ws, G.old[k]);
+  G.cdirty |= 1u << k;
+  G.odirty &= ~(1u << k);
+}
+
+// old[k] becomes r (the one it held goes to the log first if it changed)
+__device__ inline void gen_set_old(const TableDev& t, GeneralState& G, uint32_t k, const Win& r, bool dirty) {
+  if ((G.odirty >> k) & 1) gen_put(t, G, k);
+  G.old[k] = r;
+  if (dirty) G.odirty |= 1u << k;
+}
+
+// The record of window w in unit slot k (present): its cur, its cached older
+// record (from the chain), or null when unit k has none. *lost: unit k may have
+// had one that the history no longer holds. Alias writes can move a record's
+// EXPIRE past its own unit's 2 div, so the general path does not take
+// hist_absent_ok's own-unit bound.
+__device__ inline Win* gen_rec(const TableDev& t, GeneralState& G, uint32_t k, uint32_t w, uint32_t now, bool* lost) {
   const uint32_t d = div_of(k + 1);
   Win& c = G.cur[k];
   if (c.ws == w) return &c;
   if (c.ws == WS_INVALID || w > c.ws || w % d) return nullptr;  // (unit k's keys are multiples of its div)
-  if (G.ridx[k] != RING_NONE) {
-    Win* r = &t.ring[G.ridx[k]].w[hist_pos(w, d)];
-    if (r->ws == w) return r;
+  if (G.old[k].ws == w) return &G.old[k];
+  Win r;
+  const int f = G.chain[k] == LOG_NONE ? 0 : log_find(t, G.chain[k], (uint32_t)G.sidx[k], G.tag[k], c.ws, w, &r);
+  if (f > 0) {
+    gen_set_old(t, G, k, r, false);
+    return &G.old[k];
   }
-  if (lost && (!hist_reach(w, c.ws, d) || ((G.lost >> k) & 1))) *lost = true;
+  if (lost && (f < 0 || !hist_absent_ok(t, now, w, c.ws, d, false))) *lost = true;
   return nullptr;
+}
+
+__device__ inline void gen_touch(GeneralState& G, uint32_t k, const Win* R) {
+  if (R == &G.old[k]) G.odirty |= 1u << k;
 }
 
 __device__ inline void general_apply_pending(const TableDev& t, GeneralState& G) {
   for (uint32_t j = 0; j < G.npend; j++) {
     for (uint32_t k = 0; k < 4; k++) {
       if (!(G.present >> k & 1)) continue;
-      Win* R = gen_rec(t, G, k, G.pend_w[j], nullptr);
-      if (R) R->lc = G.pend_e[j];
+      Win* R = gen_rec(t, G, k, G.pend_w[j], 0u, nullptr);
+      if (R) {
+        R->lc = G.pend_e[j];
+        gen_touch(G, k, R);
+      }
     }
   }
   G.npend = 0;
@@ -1156,12 +1213,7 @@ __device__ inline void general_step(const TableDev& t, const Params& P, unsigned
   bool vfound = false;
   for (uint32_t k = 0; k < 4; k++) {
     if (!(G.present >> k & 1)) continue;
-    bool lk = false;
-    const Win* R = gen_rec(t, G, k, x.w, &lk);
-    // A record of w that unit k wrote lives at most 2 divs past w (EXPIRE and
-    // local-cache TTL = div after a hit inside w); one lost from the ring
-    // while it could still be live cannot be answered: RL_E_TIME.
-    if (lk && x.now - x.w < 2u * div_of(k + 1)) lost = true;
+    const Win* R = gen_rec(t, G, k, x.w, x.now, &lost);
     if (!R) continue;
     if (x.now < R->lc) lc_hit = true;
     lcw = R->lc > lcw ? R->lc : lcw;
@@ -1170,7 +1222,7 @@ __device__ inline void general_step(const TableDev& t, const Params& P, unsigned
       vfound = true;
     }
   }
-  if (lost) {
+  if (lost) {  // a record of w the history may have dropped while it could be live: RL_E_TIME
     if (P.isolate) res[x.e] = pack_fail(RL_E_TIME);
     atomicOr(err, ERR_HISTORY);
     return;
@@ -1180,34 +1232,22 @@ __device__ inline void general_step(const TableDev& t, const Params& P, unsigned
   if (!lc_hit) {
     const uint32_t nv = restore ? x.h : v + x.h;
     const uint32_t ex = x.now + x.d;
-    Win& c = G.cur[ui];  // this unit's record of w: cur, a roll, or its ring record (in reach: checked above)
+    Win& c = G.cur[ui];  // this unit's record of w: cur, a roll, its cached older record or a new one
     if (c.ws != x.w) {
-      Slot* su = &t.slots[G.sidx[ui]];
       if (c.ws == WS_INVALID || x.w > c.ws) {
-        if (c.ws != WS_INVALID) {  // the old cur to the ring (dropped when the pool is exhausted: SLOT_LOST)
-          Win* line = ring_for_write(t, su, G.ridx[ui]);
-          if (line) line[hist_pos(c.ws, x.d)] = c;
-          else G.lost |= 1u << ui;
-        }
+        if (c.ws != WS_INVALID && hist_keep(t, c, x.w, x.d)) gen_set_old(t, G, ui, c, true);  // the old cur
         c = Win{x.w, 0, 0, lcw};
-      } else {
-        Win* line = ring_for_write(t, su, G.ridx[ui]);
-        if (!line) {  // no room for the older window's record: this descriptor's RL_E_TIME
-          G.lost |= 1u << ui;
-          if (P.isolate) res[x.e] = pack_fail(RL_E_TIME);
-          atomicOr(err, ERR_HISTORY);
-          return;
-        }
-        Win* r = &line[hist_pos(x.w, x.d)];
-        if (r->ws != x.w) *r = Win{x.w, 0, 0, lcw};
+      } else if (G.old[ui].ws != x.w) {  // (none found above, and none lost)
+        gen_set_old(t, G, ui, Win{x.w, 0, 0, lcw}, true);
       }
     }
     for (uint32_t k = 0; k < 4; k++) {  // Redis key stem‖w in this store: every alias record
       if (!(G.present >> k & 1) || ps_class(P, k) != ps_e) continue;
-      Win* R = gen_rec(t, G, k, x.w, nullptr);
+      Win* R = gen_rec(t, G, k, x.w, x.now, nullptr);
       if (R) {
         R->count = nv;
         R->expire = ex;
+        gen_touch(G, k, R);
       }
     }
     after = nv;
@@ -1216,8 +1256,11 @@ __device__ inline void general_step(const TableDev& t, const Params& P, unsigned
     if (x.flags) {
       for (uint32_t k = 0; k < 4; k++) {
         if (!(G.present >> k & 1)) continue;
-        Win* R = gen_rec(t, G, k, x.w, nullptr);
-        if (R) R->lc = x.now + x.d;
+        Win* R = gen_rec(t, G, k, x.w, x.now, nullptr);
+        if (R) {
+          R->lc = x.now + x.d;
+          gen_touch(G, k, R);
+        }
       }
     }
     return;
@@ -1239,17 +1282,17 @@ __device__ __attribute__((always_inline)) inline void replay_simple(SRec rec_s, 
                                                                     unsigned long long* res, const TableDev& t,
                                                                     const Params& P, const uint32_t* grp,
                                                                     uint32_t p, uint32_t end, uint32_t k, int64_t s0,
-                                                                    Win cur0, uint32_t ring0, uint32_t flags0,
+                                                                    Win cur0, uint32_t ring0, uint32_t tag0,
                                                                     const Rec& x0, uint32_t e0, LaneStats& L,
                                                                     StatAcc& acc, uint32_t* err, bool restore) {
   Slot* s = &t.slots[s0];
   SimpleState S;
   S.cur = cur0;
   S.old = Win{WS_INVALID, 0, 0, 0};  // (never matches a pending window)
-  S.slot = s;
-  S.ridx = ring0;
-  S.lost = (flags0 & SLOT_LOST) != 0;
-  S.cur_dirty = S.old_dirty = false;
+  S.si = (uint32_t)s0;
+  S.tag = tag0;
+  S.chain = ring0;
+  S.cur_dirty = S.old_dirty = S.chain_dirty = false;
   S.cur_req = 0xFFFFFFFFu;
   S.pend = false;
   simple_step(t, P, res, L, acc, S, load_elem(x0, e0, restore), restore, err);  // element p (always stem k)
@@ -1258,9 +1301,10 @@ __device__ __attribute__((always_inline)) inline void replay_simple(SRec rec_s, 
     simple_step(t, P, res, L, acc, S, load_elem(rec_s[q], svals[q], restore), restore, err);
   }
   S.apply_pending();
-  // random writes are the costly part of the probe: store only records that changed
+  // random writes are the costly part of the probe: store only what changed
+  if (S.old_dirty) simple_put(t, S);
   if (S.cur_dirty) s->cur = S.cur;
-  if (S.old_dirty) simple_put(t, S, S.old, div_of(rec_unit(x0)));
+  if (S.chain_dirty) s->ring = S.chain;
 }
 
 // ===========================================================================
@@ -3623,7 +3667,8 @@ __device__ __attribute__((always_inline)) inline void unique_body(uint32_t blk, 
       load_img_lo(&t.slots[h0 >> t.shift], im);  // home slot's first sector, in flight beside the stem
       const Key k0 = key_of(b, x);
       bool ins = false, ok = true;
-      const int64_t s0 = find_slot_img(t, h0, slot_tag(h0, u0), k0, u0, &ins, im, ferr);
+      const uint32_t tg0 = slot_tag(h0, u0);
+      const int64_t s0 = find_slot_img(t, h0, tg0, k0, u0, &ins, im, ferr);
       if (s0 < 0) {
         ok = false;
       } else if (im.flags() & SLOT_EXACT) {
@@ -3640,7 +3685,7 @@ __device__ __attribute__((always_inline)) inline void unique_body(uint32_t blk, 
         if (!ok) t.slots[s0].flags |= SLOT_EXACT;
       }
       if (ok) {
-        replay_simple(SRec{rec, nullptr}, nullptr, res, t, P, nullptr, 0, 1, 0, s0, im.cur(), im.ring(), im.flags(), x, i,
+        replay_simple(SRec{rec, nullptr}, nullptr, res, t, P, nullptr, 0, 1, 0, s0, im.cur(), im.ring(), tg0, x, i,
                       L, acc, ferr,
                       restore);
       } else if (s0 == SLOT_TABLE_FULL || s0 == SLOT_ARENA_FULL) {
@@ -3677,16 +3722,13 @@ __device__ inline void fail_range(unsigned long long* res, const uint32_t* svals
 //    still live at `now`; its local-cache hit (F) is any record's entry live
 //    at `now` — one `now` per group, so both hold for the whole group;
 //  * each unit of a group that increments gets its record of the window
-//    (rolled into cur, or a ring record; a new one takes the live local-cache
-//    expiry of the others), and the group's last INCRBY writes its count and
-//    EXPIRE to every record of the key, its local-cache Set to all of them.
-// The rolls are done before the write-back targets are resolved. A record
-// another group finds on a ring position a roll or a new record takes is out
-// of the ring's reach after this batch in either order of the descriptors, so
-// the answers agree unless it was its key's only record (checked), or unless
-// a record is out of the ring's reach now (general_step: RL_E_TIME); then —
-// rare by construction — the stem goes to the exact path untouched (returns
-// true).
+//    (rolled into cur; a new one takes the live local-cache expiry of the
+//    others), and the group's last INCRBY writes its count and EXPIRE to every
+//    record of the key, its local-cache Set to all of them.
+// The parallel path writes curs only. A group that would need a record below
+// a unit's cur (a new one, or one held in the history log, or a cur that
+// another group rolls away), or whose record the history may have dropped, is
+// left — rare by construction — to the exact path untouched (returns true).
 struct AliasGroup {
   uint32_t id, p, end, mask, w;
 };
@@ -3737,19 +3779,18 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
   // every unit slot of the stem (created for the units seen here)
   int64_t sidx[4];
   Win c[4];
-  uint32_t ridx[4];
-  uint32_t present = 0, lost = 0;
+  uint32_t chain[4];
+  uint32_t present = 0;
   int64_t fail = 0;
   for (uint32_t k = 0; k < 4; k++) {
     bool ins;
     sidx[k] = find_slot(t, hs, slot_tag(hs, k + 1), stem, k + 1, (M >> k) & 1, &ins, ferr);
-    ridx[k] = RING_NONE;
+    chain[k] = LOG_NONE;
     if (sidx[k] >= 0) {
       const Slot& su = t.slots[sidx[k]];
       present |= 1u << k;
       c[k] = su.cur;
-      ridx[k] = su.ring;
-      if (su.flags & SLOT_LOST) lost |= 1u << k;
+      chain[k] = su.ring;
     } else if ((M >> k) & 1) {
       fail = sidx[k];
     }
@@ -3759,47 +3800,39 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
       for (uint32_t g = 0; g < G; g++) fail_range(res, svals, A[g].p, A[g].end, slot_fail_status(fail));
     return false;  // (else find_slot set the batch's error)
   }
-  // The ring position each unit of a group may write (before F is known):
-  // the old cur's, rolled into the ring, or the group's window's (a ring
-  // record). A record another group finds there is gone once the write is
-  // done: such a record is then out of the ring's reach for good, so only the
-  // starting state of this batch could tell the two orders of the batch's
-  // descriptors apart.
-  uint32_t wpos[4];  // per unit: the window whose ring position may be written (WS_INVALID: none)
-  for (uint32_t k = 0; k < 4; k++) wpos[k] = WS_INVALID;
+  // the units that roll their cur forward (a group that may increment: the
+  // local-cache hit F is not known yet) and so move it to the history log
+  uint32_t rolls = 0;
   for (uint32_t g = 0; g < G; g++)
     for (uint32_t k = 0; k < 4; k++)
-      if (((A[g].mask >> k) & 1) && c[k].ws != A[g].w)
-        wpos[k] = (c[k].ws == WS_INVALID || A[g].w > c[k].ws) ? c[k].ws : A[g].w;
-  // the groups' starting state, from the records as they are, with and
-  // without such doomed records: the alias records of one key carry one
-  // count, EXPIRE and local-cache expiry, so the two agree unless a doomed
-  // record was the only one — then the exact path decides in arrival order
+      if (((A[g].mask >> k) & 1) && c[k].ws != A[g].w) {
+        if (c[k].ws != WS_INVALID && A[g].w < c[k].ws) return true;  // a new record below cur: the exact path
+        rolls |= 1u << k;
+      }
+  // The groups' starting state from the curs and the logged records. The
+  // parallel path writes curs only: a group whose key has a record in a log
+  // (or in a cur that rolls away) goes to the exact path, as does one whose
+  // record may have been dropped.
   uint32_t v0[4], lcm[4], F[4];
   for (uint32_t g = 0; g < G; g++) {
     const uint32_t w = A[g].w;
     const bool cls = P.per_second && (A[g].mask & 1u);
-    bool vf = false, vfx = false;
-    uint32_t v0x = 0, lcmx = 0;
+    bool vf = false;
     v0[g] = 0;
     lcm[g] = 0;
     for (uint32_t k = 0; k < 4; k++) {
       if (!((present >> k) & 1)) continue;
       const uint32_t d = div_of(k + 1);
       Win R;
-      bool doomed = false;
       if (c[k].ws == w) {
+        if ((rolls >> k) & 1) return true;
         R = c[k];
       } else if (c[k].ws == WS_INVALID || w > c[k].ws || w % d) {
         continue;  // (unit k's keys are multiples of its div)
       } else {
-        R = ring_read(t, ridx[k], hist_pos(w, d));
-        if (R.ws != w) {
-          // never written, or lost from the ring (or dropped, SLOT_LOST) while it could be live
-          if ((!hist_reach(w, c[k].ws, d) || ((lost >> k) & 1)) && now - w < 2u * d) return true;
-          continue;
-        }
-        doomed = wpos[k] != WS_INVALID && wpos[k] != w && hist_pos(wpos[k], d) == hist_pos(w, d);
+        const int f = chain[k] == LOG_NONE ? 0 : log_find(t, chain[k], (uint32_t)sidx[k], slot_tag(hs, k + 1), c[k].ws, w, &R);
+        if (f != 0 || !hist_absent_ok(t, now, w, c[k].ws, d, false)) return true;
+        continue;
       }
       const bool live = (P.per_second && k == 0) == cls && now <= R.expire;
       lcm[g] = R.lc > lcm[g] ? R.lc : lcm[g];
@@ -3807,14 +3840,7 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
         v0[g] = R.count;
         vf = true;
       }
-      if (doomed) continue;
-      lcmx = R.lc > lcmx ? R.lc : lcmx;
-      if (!vfx && live) {
-        v0x = R.count;
-        vfx = true;
-      }
     }
-    if (v0x != v0[g] || lcmx != lcm[g]) return true;
     F[g] = (P.lc_en && now < lcm[g]) ? 1u : 0u;
   }
   // the new cur of each unit that rolls (groups that increment)
@@ -3824,37 +3850,20 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
     for (uint32_t k = 0; k < 4; k++)
       if (!F[g] && ((A[g].mask >> k) & 1) && (c[k].ws == WS_INVALID || A[g].w > c[k].ws))
         cn[k] = Win{A[g].w, 0, 0, lcm[g]};
-  // the ring lines the commit writes, taken first: with the pool exhausted the
-  // stem goes to the exact path untouched (which answers RL_E_TIME where a
-  // record cannot be kept)
-  for (uint32_t g = 0; g < G; g++) {
-    if (F[g]) continue;
-    for (uint32_t k = 0; k < 4; k++) {
-      if (!((A[g].mask >> k) & 1) || c[k].ws == A[g].w || c[k].ws == WS_INVALID) continue;
-      if (!ring_for_write(t, &t.slots[sidx[k]], ridx[k])) return true;
-    }
-  }
-  // commit: rolls and new ring records
-  for (uint32_t g = 0; g < G; g++) {
-    if (F[g]) continue;
-    for (uint32_t k = 0; k < 4; k++) {
-      if (!((A[g].mask >> k) & 1) || c[k].ws == A[g].w) continue;
-      const uint32_t d = div_of(k + 1);
-      if (c[k].ws == WS_INVALID || A[g].w > c[k].ws) {
-        if (c[k].ws != WS_INVALID) t.ring[ridx[k]].w[hist_pos(c[k].ws, d)] = c[k];
-        t.slots[sidx[k]].cur = cn[k];
-      } else {
-        Win* rr = &t.ring[ridx[k]].w[hist_pos(A[g].w, d)];
-        if (rr->ws != A[g].w) *rr = Win{A[g].w, 0, 0, lcm[g]};
-      }
-    }
+  // commit: rolls (the old cur to the history log while a request could still ask for it)
+  for (uint32_t k = 0; k < 4; k++) {
+    if (cn[k].ws == c[k].ws) continue;
+    Slot* su = &t.slots[sidx[k]];
+    if (c[k].ws != WS_INVALID && hist_keep(t, c[k], cn[k].ws, div_of(k + 1)))
+      su->ring = log_append(t, (uint32_t)sidx[k], slot_tag(hs, k + 1), chain[k], cn[k].ws, c[k]);
+    su->cur = cn[k];
   }
   if (__popc(present) >= 2)
     for (uint32_t k = 0; k < 4; k++)
       if ((present >> k) & 1) t.slots[sidx[k]].flags |= SLOT_EXACT;
   const uint4 sl = make_uint4(present & 1 ? (uint32_t)sidx[0] : 0xFFFFFFFFu, present & 2 ? (uint32_t)sidx[1] : 0xFFFFFFFFu,
                               present & 4 ? (uint32_t)sidx[2] : 0xFFFFFFFFu, present & 8 ? (uint32_t)sidx[3] : 0xFFFFFFFFu);
-  // write-back targets (3 bits per unit: a record of w, in the ring, same store)
+  // write-back targets (per unit: bit 0 its cur holds w, bit 2 same store)
   for (uint32_t g = 0; g < G; g++) {
     const uint32_t w = A[g].w;
     const bool cls = P.per_second && (A[g].mask & 1u);
@@ -3862,14 +3871,7 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
     if (!F[g]) {
       for (uint32_t k = 0; k < 4; k++) {
         if (!((present >> k) & 1)) continue;
-        const uint32_t d = div_of(k + 1);
-        uint32_t bits = 0;
-        if (cn[k].ws == w) {
-          bits = 1;
-        } else if (cn[k].ws != WS_INVALID && w < cn[k].ws && w % d == 0 &&
-                   ring_read(t, ridx[k], hist_pos(w, d)).ws == w) {
-          bits = 3;
-        }
+        uint32_t bits = cn[k].ws == w ? 1u : 0u;
         if (bits && (P.per_second && k == 0) == cls) bits |= 4;
         tm |= bits << (3 * k);
       }
@@ -3974,62 +3976,38 @@ __device__ __attribute__((always_inline)) inline void runs_body(uint32_t blk, Ba
           if (!ok) t.slots[s0].flags |= SLOT_EXACT;
         }
       }
-      if (ok && long_run) {
+      const Elem el0 = load_elem(x0, e0, false);
+      const Win cur = im.cur();
+      // (a long run of a window older than the key's newest: replayed here, its
+      // record lives in the history log)
+      if (ok && long_run && (cur.ws == WS_INVALID || el0.w >= cur.ws)) {
         // Parallel path: pick the window record once; k_fast_* decide every element.
         Slot* s = &t.slots[s0];
-        const Elem el0 = load_elem(x0, e0, false);
-        const Win cur = im.cur();
-        uint32_t ridx = im.ring();
-        // the record of el0.w: cur, a roll (the old cur moves to the ring), or a ring record
-        int which = 0;
+        // the record of el0.w: cur, or a roll (the old cur to the history log
+        // while a request could still ask for it: simple_pick)
         Win R = cur;
         if (cur.ws != el0.w) {
-          if (cur.ws == WS_INVALID || el0.w > cur.ws) {
-            // (the old cur goes to the ring only while in its reach from el0.w: simple_pick;
-            // dropped, SLOT_LOST, when the pool is exhausted)
-            if (cur.ws != WS_INVALID && hist_reach(cur.ws, el0.w, el0.d)) {
-              Win* ring = ring_for_write(t, s, ridx);
-              if (ring) ring[hist_pos(cur.ws, el0.d)] = cur;
-            }
-            R = Win{el0.w, 0, 0, 0};
+          R = Win{el0.w, 0, 0, 0};
+          if (cur.ws != WS_INVALID && hist_keep(t, cur, el0.w, el0.d)) {
+            const uint32_t head = log_append(t, (uint32_t)s0, slot_tag(h0, u0), im.ring(), el0.w, cur);
             s->cur = R;
-          } else if (hist_reach(el0.w, cur.ws, el0.d) && !(im.flags() & SLOT_LOST)) {
-            Win* ring = ring_for_write(t, s, ridx);
-            if (ring) {
-              which = 1;
-              R = ring[hist_pos(el0.w, el0.d)];
-              if (R.ws != el0.w) {  // never written: started afresh
-                R = Win{el0.w, 0, 0, 0};
-                ring[hist_pos(el0.w, el0.d)] = R;
-              }
-            } else {
-              which = -1;  // (no line for the record: RL_E_TIME)
-            }
+            s->ring = head;
           } else {
-            which = -1;
+            s->cur = R;
           }
         }
-        bool fast = true;
-        if (which < 0) {
-          if (!(RL_ABL & 1)) atomicOr(ferr, ERR_HISTORY);  // (ablation builds probe garbage slots)
-          fast = P.isolate != 0;  // every element of the run: RL_E_TIME (k_fast_emit)
-          if (fast) run_state[r] = make_uint4((uint32_t)s0, 0u, 0u, 4u);
-        } else {
-          // A record of window w was written inside w: its EXPIRE and local-cache
-          // TTL both end at or after w + div, so they hold for the whole run.
-          const uint32_t c0 = el0.now <= R.expire ? R.count : 0u;
-          const uint32_t F = (P.lc_en && el0.now < R.lc) ? 1u : 0u;
-          run_state[r] = make_uint4((uint32_t)s0, c0, R.lc, F | ((uint32_t)which << 1));
-        }
-        if (fast) {
-          run_f[r] = 0xFFFFFFFFu;
-          run_flags[r] = fl | RUN_FAST;
-          // mark the 256-descriptor blocks of k_fast_emit this run spans
-          const uint32_t b0 = p >> 8, b1 = (end - 1) >> 8;
-          for (uint32_t w = b0 >> 5; w <= b1 >> 5; w++) {
-            const uint32_t lo = w == (b0 >> 5) ? (b0 & 31) : 0u, hi = w == (b1 >> 5) ? (b1 & 31) : 31u;
-            atomicOr(&fast_blk[w], (0xFFFFFFFFu >> (31 - hi)) & (0xFFFFFFFFu << lo));
-          }
+        // A record of window w was written inside w: its EXPIRE and local-cache
+        // TTL both end at or after w + div, so they hold for the whole run.
+        const uint32_t c0 = el0.now <= R.expire ? R.count : 0u;
+        const uint32_t F = (P.lc_en && el0.now < R.lc) ? 1u : 0u;
+        run_state[r] = make_uint4((uint32_t)s0, c0, R.lc, F);
+        run_f[r] = 0xFFFFFFFFu;
+        run_flags[r] = fl | RUN_FAST;
+        // mark the 256-descriptor blocks of k_fast_emit this run spans
+        const uint32_t b0 = p >> 8, b1 = (end - 1) >> 8;
+        for (uint32_t w = b0 >> 5; w <= b1 >> 5; w++) {
+          const uint32_t lo = w == (b0 >> 5) ? (b0 & 31) : 0u, hi = w == (b1 >> 5) ? (b1 & 31) : 31u;
+          atomicOr(&fast_blk[w], (0xFFFFFFFFu >> (31 - hi)) & (0xFFFFFFFFu << lo));
         }
       } else if (ok) {
         if (RL_ABL & 2) {
@@ -4038,8 +4016,8 @@ __device__ __attribute__((always_inline)) inline void runs_body(uint32_t blk, Ba
           c.count += end - p;
           sl->cur = c;
         } else {
-          replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, im.cur(), im.ring(), im.flags(), x0, e0, L, acc,
-                        ferr, restore);
+          replay_simple(rec_s, svals, res, t, P, nullptr, p, end, 0, s0, im.cur(), im.ring(), slot_tag(h0, u0), x0, e0, L,
+                        acc, ferr, restore);
         }
       } else if (s0 == SLOT_TABLE_FULL || s0 == SLOT_ARENA_FULL) {
         if (P.isolate) fail_range(res, svals, p, end, slot_fail_status(s0));  // else the batch fails
@@ -4122,9 +4100,7 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
   const uint32_t fl = q < n ? run_flags[r] : 0u;
   if (fl & RUN_FAST) {
     const uint4 st = run_state[r];
-    if (st.w & 4u) {  // the run's window is older than the key's history (isolate): RL_E_TIME
-      res[svals[q]] = pack_fail(RL_E_TIME);
-    } else {
+    {
       const uint32_t f = run_f[r];
       const bool F = st.w & 1u;
       const Elem x = load_elem(rec_s[q], svals[q], false);
@@ -4141,14 +4117,14 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
       if (!masked) {
         const uint32_t nq = q + 1;
         const bool last = nq == run_end[r] || rec_s[nq].req > req_f;
-        if (last && (fl & RUN_ALIAS)) {  // the key's records in every unit slot (alias_setup's targets)
+        if (last && (fl & RUN_ALIAS)) {  // the key's records in every unit slot (alias_setup's targets: curs)
           const uint4 sl = run_alias[r];
 #pragma unroll
           for (uint32_t k = 0; k < 4; k++) {
             const uint32_t bits = (st.x >> (3 * k)) & 7u;
             if (!(bits & 1u)) continue;
             const uint32_t idx = k == 0 ? sl.x : k == 1 ? sl.y : k == 2 ? sl.z : sl.w;
-            Win* R = (bits & 2u) ? &t.ring[t.slots[idx].ring].w[hist_pos(x.w, div_of(k + 1))] : &t.slots[idx].cur;
+            Win* R = &t.slots[idx].cur;
             if (bits & 4u) {  // same store: INCRBY + EXPIRE
               R->count = after;
               R->expire = x.now + x.d;
@@ -4161,8 +4137,7 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
           R.count = after;
           R.expire = x.now + x.d;
           R.lc = (req_f != 0xFFFFFFFFu) ? lc_f : st.z;
-          if (st.w & 2u) t.ring[t.slots[st.x].ring].w[hist_pos(x.w, x.d)] = R;  // a ring record (line taken by k_table)
-          else t.slots[st.x].cur = R;
+          t.slots[st.x].cur = R;
         }
       }
     }
@@ -4195,20 +4170,21 @@ __device__ inline void stem_exact(const TableDev& t, const Params& P, unsigned l
                                   Visit visit) {
   GeneralState G;
   G.present = 0;
-  G.lost = 0;
+  G.odirty = G.cdirty = 0;
   G.cur_req = 0xFFFFFFFFu;
   G.npend = 0;
   int64_t fail = 0;
   for (uint32_t u = 1; u <= 4; u++) {
     bool ins;
-    G.sidx[u - 1] = find_slot(t, hs, slot_tag(hs, u), stem, u, (um >> (u - 1)) & 1, &ins, ferr);
-    G.ridx[u - 1] = RING_NONE;
+    G.tag[u - 1] = slot_tag(hs, u);
+    G.sidx[u - 1] = find_slot(t, hs, G.tag[u - 1], stem, u, (um >> (u - 1)) & 1, &ins, ferr);
+    G.chain[u - 1] = LOG_NONE;
+    G.old[u - 1] = Win{WS_INVALID, 0, 0, 0};
     if (G.sidx[u - 1] >= 0) {
       const Slot& su = t.slots[G.sidx[u - 1]];
       G.present |= 1u << (u - 1);
       G.cur[u - 1] = su.cur;
-      G.ridx[u - 1] = su.ring;
-      if (su.flags & SLOT_LOST) G.lost |= 1u << (u - 1);
+      G.chain[u - 1] = su.ring;
     } else if ((um >> (u - 1)) & 1) {
       fail = G.sidx[u - 1];
     }
@@ -4222,8 +4198,10 @@ __device__ inline void stem_exact(const TableDev& t, const Params& P, unsigned l
   const uint8_t fl = __popc(G.present) >= 2 ? SLOT_EXACT : 0;
   for (uint32_t u = 0; u < 4; u++) {
     if (!(G.present >> u & 1)) continue;
+    if ((G.odirty >> u) & 1) gen_put(t, G, u);
     Slot* s = &t.slots[G.sidx[u]];
     s->cur = G.cur[u];
+    if ((G.cdirty >> u) & 1) s->ring = G.chain[u];
     s->flags |= fl;
   }
 }
@@ -4347,7 +4325,7 @@ __device__ __attribute__((always_inline)) inline void general_body(uint32_t blk,
         }
       }
       if (simple) {
-        replay_simple(rec_s, svals, res, t, P, grp, q0, end, g, s0, t.slots[s0].cur, t.slots[s0].ring, t.slots[s0].flags, y,
+        replay_simple(rec_s, svals, res, t, P, grp, q0, end, g, s0, t.slots[s0].cur, t.slots[s0].ring, slot_tag(hs, __ffs(um)), y,
                       svals[q0], L, acc, ferr,
                       restore);
         continue;
@@ -4529,8 +4507,30 @@ __global__ __launch_bounds__(256) void k_finish(const unsigned long long* __rest
   }
 }
 
+// Walk slot s's history chain: f(entry record, hop index) for each entry the
+// log still holds, newest first (stops where one was overwritten, or when f says so).
+template <typename F>
+__device__ inline void chain_walk(const TableDev& t, uint32_t si, const Slot& s, F f) {
+  uint32_t ptr = s.ring, tprev = s.cur.ws, saved = LOG_NONE, power = 1, lam = 0;
+  for (uint32_t hops = 0; ptr != LOG_NONE && hops < LOG_MAX_HOPS && ptr != saved; hops++) {  // (log_find's checks)
+    const uint32_t pos = ptr & LOG_POS_MASK;
+    if (pos >= t.log_cap) return;
+    if (++lam == power) {
+      saved = ptr;
+      power <<= 1;
+      lam = 0;
+    }
+    const LogEnt& e = t.log[(size_t)(ptr >> LOG_POS_BITS) * t.log_cap + pos];
+    if (e.slot != si || e.tag != s.tag || e.t_app > tprev) return;
+    if (!f(e.w, hops)) return;
+    tprev = e.t_app;
+    ptr = e.prev;
+  }
+}
+
 // Keys in the local over-limit cache at `now` (freecache EntryCount of live
-// entries): window records whose local-cache TTL has not passed.
+// entries): window records whose local-cache TTL has not passed (the newest
+// version of each window on a chain).
 __global__ __launch_bounds__(256) void k_lc_count(const TableDev t, uint64_t nslots, uint32_t now,
                                                   unsigned long long* out) {
   uint32_t live = 0;
@@ -4538,66 +4538,45 @@ __global__ __launch_bounds__(256) void k_lc_count(const TableDev t, uint64_t nsl
     const Slot& s = t.slots[i];
     if (s.tag < 2) continue;
     live += s.cur.ws != WS_INVALID && now < s.cur.lc;
-    if (s.ring == RING_NONE) continue;
-    for (uint32_t j = 0; j < HIST_W; j++) {
-      const Win& w = t.ring[s.ring].w[j];
-      live += w.ws != WS_INVALID && now < w.lc;
-    }
+    chain_walk(t, (uint32_t)i, s, [&](const Win& w, uint32_t at) {
+      if (w.ws == WS_INVALID || !(now < w.lc)) return true;
+      bool newest = true;  // no newer entry of the same window before this one
+      chain_walk(t, (uint32_t)i, s, [&](const Win& v, uint32_t at2) {
+        if (at2 >= at) return false;
+        if (v.ws == w.ws) newest = false;
+        return newest;
+      });
+      live += newest;
+      return true;
+    });
   }
   if (live) atomicAdd(out, (unsigned long long)live);
 }
 
 // ===========================================================================
 // Epoch sweep: a slot whose window records are all dead (Redis key past its
-// EXPIRE and local-cache entry past its TTL) becomes a tombstone, and its
-// ring line joins the free list the next batches take lines from.
+// EXPIRE and local-cache entry past its TTL) becomes a tombstone; its chain's
+// log entries are left to be overwritten.
 // ===========================================================================
 __device__ inline bool win_alive(const Win& w, uint32_t now) {
   return w.ws != WS_INVALID && (now <= w.expire || now < w.lc);
 }
 
-// Per partition (blockIdx.y): the free-list segment's untaken entries move to
-// the front of the new list's segment (one pass; k_ring_reset then restarts
-// the counts and moves B past the lines taken from the partition's end).
-__global__ __launch_bounds__(256) void k_ring_rebase(const uint32_t* __restrict__ from, uint32_t* __restrict__ to,
-                                                     const unsigned long long* ctr, uint32_t L) {
-  const unsigned long long* c = ctr + (size_t)blockIdx.y * RING_CTR_STRIDE;
-  const unsigned long long take = c[1], n = c[2];
-  const unsigned long long left = n > take ? n - take : 0ull;
-  const size_t base = (size_t)blockIdx.y * L;
-  for (unsigned long long k = blockIdx.x * 256ull + threadIdx.x; k < left; k += (unsigned long long)gridDim.x * 256)
-    to[base + k] = from[base + take + k];
-}
-
-__global__ void k_ring_reset(unsigned long long* ctr, uint32_t P, uint32_t L) {
-  const uint32_t p = threadIdx.x;
-  if (p >= P) return;
-  unsigned long long* c = ctr + (size_t)p * RING_CTR_STRIDE;
-  const unsigned long long take = c[1], n = c[2], b = c[0] + (take > n ? take - n : 0ull);
-  c[0] = b < L ? b : L;
-  c[2] = n > take ? n - take : 0ull;
-  c[1] = 0;
-}
-
-__global__ __launch_bounds__(256) void k_sweep(TableDev t, uint64_t nslots, uint32_t now, unsigned long long* evicted,
-                                               uint32_t* __restrict__ free_to) {
+__global__ __launch_bounds__(256) void k_sweep(TableDev t, uint64_t nslots, uint32_t now, unsigned long long* evicted) {
   uint32_t local = 0;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * 256) {
     Slot* s = &t.slots[i];
     if (s->tag < 2) continue;
-    const uint32_t line = s->ring;
     bool alive = win_alive(s->cur, now);
-    if (line != RING_NONE)
-      for (uint32_t j = 0; j < HIST_W && !alive; j++) alive = win_alive(t.ring[line].w[j], now);
+    if (!alive)
+      chain_walk(t, (uint32_t)i, *s, [&](const Win& w, uint32_t) {
+        alive = win_alive(w, now);
+        return !alive;
+      });
     if (alive) continue;
     s->tag = TAG_TOMB;
-    s->ring = RING_NONE;
+    s->ring = LOG_NONE;
     local++;
-    if (line != RING_NONE) {  // back on its partition's segment of the new list
-      const uint32_t p = line / t.ring_part_lines;
-      const unsigned long long k = atomicAdd(&t.ring_ctr[(size_t)p * RING_CTR_STRIDE + 2], 1ull);
-      free_to[(size_t)p * t.ring_part_lines + k] = line;
-    }
   }
   if (local) atomicAdd(evicted, (unsigned long long)local);
 }
@@ -4622,20 +4601,20 @@ __global__ __launch_bounds__(256) void k_arena_compact(Slot* slots, uint64_t nsl
 }
 
 __global__ __launch_bounds__(256) void k_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out) {
-  uint32_t live = 0, tomb = 0, exact = 0, lost = 0;
+  uint32_t live = 0, tomb = 0, exact = 0, hist = 0;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * 256) {
     const uint32_t tg = slots[i].tag;
     if (tg == TAG_TOMB) tomb++;
     else if (tg >= 2) {
       live++;
       exact += (slots[i].flags & SLOT_EXACT) != 0;
-      lost += (slots[i].flags & SLOT_LOST) != 0;
+      hist += slots[i].ring != LOG_NONE;
     }
   }
   if (live) atomicAdd(&out[0], (unsigned long long)live);
   if (tomb) atomicAdd(&out[1], (unsigned long long)tomb);
   if (exact) atomicAdd(&out[2], (unsigned long long)exact);
-  if (lost) atomicAdd(&out[3], (unsigned long long)lost);
+  if (hist) atomicAdd(&out[3], (unsigned long long)hist);
 }
 
 // ===========================================================================
@@ -4789,11 +4768,8 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
 }
 
 
-void launch_sweep(const TableDev& t, uint64_t nslots, uint32_t now, unsigned long long* evicted,
-                  const uint32_t* free_from, uint32_t* free_to, hipStream_t st) {
-  k_ring_rebase<<<dim3(64, t.ring_parts), 256, 0, st>>>(free_from, free_to, t.ring_ctr, t.ring_part_lines);
-  k_ring_reset<<<1, RING_PARTS_MAX, 0, st>>>(t.ring_ctr, t.ring_parts, t.ring_part_lines);
-  k_sweep<<<2048, 256, 0, st>>>(t, nslots, now, evicted, free_to);
+void launch_sweep(const TableDev& t, uint64_t nslots, uint32_t now, unsigned long long* evicted, hipStream_t st) {
+  k_sweep<<<2048, 256, 0, st>>>(t, nslots, now, evicted);
 }
 
 void launch_arena_compact(Slot* slots, uint64_t nslots, const uint8_t* from, uint8_t* to, unsigned long long* used16,

@@ -50,9 +50,9 @@ class FixedTimeSource(TimeSource):
 
 def _config(near_limit_ratio, local_cache, per_second, jitter, table_slots, max_batch, max_rules, device,
             arena_bytes, max_stem_bytes, hash_seed=0, debug_hash_bits=0, n_shards=1, shard_devices=None,
-            ring_lines=0):
+            history_entries=0):
     cfg = abi.RlConfig()
-    cfg.ring_lines = ring_lines
+    cfg.history_entries = history_entries
     cfg.table_slots = table_slots
     cfg.arena_bytes = arena_bytes
     cfg.max_batch = max_batch
@@ -108,15 +108,16 @@ class Backend:
 
     def __init__(self, near_limit_ratio=0.8, local_cache=False, per_second=False, jitter=0,
                  table_slots=1 << 20, max_batch=1 << 16, max_rules=1 << 12, device=0, arena_bytes=0,
-                 max_stem_bytes=0, hash_seed=0, debug_hash_bits=0, n_shards=1, shard_devices=None, ring_lines=0):
+                 max_stem_bytes=0, hash_seed=0, debug_hash_bits=0, n_shards=1, shard_devices=None, history_entries=0):
         """n_shards > 1: one ctx hash-shards its table over shard_devices (default:
         all on `device`) and routes every batch between them (rl_config.n_shards).
-        ring_lines: 128-B history lines (0 = table_slots / 4; rl_config.ring_lines)."""
+        history_entries: 32-B history log entries (0 = table_slots; rl_config.history_entries).
+        jitter: EXPIRATION_JITTER_MAX_SECONDS (the history horizon: older windows kept div + jitter s)."""
         L = lib()
         err = C.create_string_buffer(512)
         self.cfg = _config(near_limit_ratio, local_cache, per_second, jitter, table_slots, max_batch, max_rules,
                            device, arena_bytes, max_stem_bytes, hash_seed, debug_hash_bits, n_shards, shard_devices,
-                           ring_lines)
+                           history_entries)
         self.ctx = L.rl_create(C.byref(self.cfg), err, 512)
         if not self.ctx:
             raise RedisError(err.value.decode())

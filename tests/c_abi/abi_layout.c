@@ -20,7 +20,7 @@ int main(void) {
   F(rl_config, max_rules); F(rl_config, max_stem_bytes); F(rl_config, near_limit_ratio);
   F(rl_config, local_cache_enabled); F(rl_config, per_second_split); F(rl_config, device);
   F(rl_config, expiration_jitter_max_seconds); F(rl_config, hash_seed); F(rl_config, n_shards);
-  F(rl_config, debug_hash_bits); F(rl_config, shard_device); F(rl_config, ring_lines);
+  F(rl_config, debug_hash_bits); F(rl_config, shard_device); F(rl_config, history_entries);
   F(rl_config, reserved);
 
   S(rl_batch);
@@ -56,8 +56,8 @@ int main(void) {
   S(rl_table_info);
   F(rl_table_info, table_slots); F(rl_table_info, live_slots); F(rl_table_info, tombstones);
   F(rl_table_info, arena_bytes_used); F(rl_table_info, exact_stems); F(rl_table_info, batches);
-  F(rl_table_info, decisions); F(rl_table_info, ring_lines); F(rl_table_info, ring_lines_used);
-  F(rl_table_info, lost_slots);
+  F(rl_table_info, decisions); F(rl_table_info, history_entries); F(rl_table_info, history_appended);
+  F(rl_table_info, history_lost); F(rl_table_info, history_slots);
 
   S(rl_config_node);
   F(rl_config_node, parent); F(rl_config_node, key_off); F(rl_config_node, key_len);

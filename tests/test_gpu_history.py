@@ -1,13 +1,16 @@
-"""Time moving back: the window ring (HIST_W = 8 windows below each key's cur).
+"""Time moving back: the history log (rl_device.h).
 
 Redis keeps a window key div + jitter seconds after its last hit
 (src/redis/fixed_cache_impl.go:71-74), so a request whose clock is behind
 others (it waited in a batcher) still finds its window's count. The table
-answers every window up to 8 back from the newest one written for its
-(stem, unit) exactly, and fails a descriptor older than that with RL_E_TIME.
-These streams revisit windows 2-7 back (SECOND) and 2-8 back (MINUTE), on the
-short-run, long-run (parallel) and multi-unit (exact) paths, against the C and
-Python oracles, which model Redis keys without any window limit.
+answers exactly every request whose window is at most 8 back from the newest
+one written for its (stem, unit), and every request whose clock is within
+div + J (expiration_jitter_max_seconds) of it; an older one whose window the
+key may have had fails with RL_E_TIME. These streams revisit windows 2-8
+back, and at J = 300 / 600 windows 9-300 s back (SECOND) and 9-11 back
+(MINUTE), on the short-run, long-run (parallel) and multi-unit (exact) paths,
+against the C and Python oracles, which model Redis keys without any window
+limit.
 """
 import numpy as np
 import pytest
@@ -24,8 +27,8 @@ pytestmark = pytest.mark.gpu
 SMALL = dict(table_slots=1 << 16, max_batch=1 << 14, max_rules=1 << 10)
 
 
-def _compare(batches, lc, isolate=False):
-    be = Backend(0.8, lc, table_slots=1 << 18, max_batch=1 << 16, max_rules=8)
+def _compare(batches, lc, isolate=False, jitter=0):
+    be = Backend(0.8, lc, table_slots=1 << 18, max_batch=1 << 16, max_rules=8, jitter=jitter)
     co = c_oracle.COracle(0.8, lc)
     try:
         for i, (a, n, nq, nr) in enumerate(batches):
@@ -135,9 +138,26 @@ def test_gpu_calls_revisit_windows_vs_python_oracle(lc):
     assert stats == py_stats
 
 
-def test_gpu_beyond_the_ring_fails_alone():
-    """A window 9 back from a key's newest is beyond the ring: RL_E_TIME for
-    that descriptor only; 8 back is still exact."""
+@pytest.mark.parametrize("lc", [False, True])
+def test_gpu_second_windows_9_to_300_back_at_jitter_300_vs_c_oracle(lc):
+    """Clocks up to 299 s behind the batch's newest (J = 300): windows far
+    beyond the 8 always kept, every one answered exactly (no RL_E_TIME)."""
+    _compare(_stream(7, 3_000, 6_000, 8, 40, 299, unit=1, hot=200), lc, isolate=True, jitter=300)
+
+
+@pytest.mark.parametrize("lc", [False, True])
+def test_gpu_minute_windows_9_to_11_back_at_jitter_600_vs_c_oracle(lc):
+    _compare(_stream(8, 3_000, 6_000, 8, 200, 659, unit=2, hot=200), lc, isolate=True, jitter=600)
+
+
+@pytest.mark.parametrize("lc", [False, True])
+def test_gpu_multi_unit_stems_300_s_back_at_jitter_300_vs_c_oracle(lc):
+    _compare(_stream(9, 2_000, 4_000, 8, 30, 299, multi=True), lc, isolate=True, jitter=300)
+
+
+def test_gpu_beyond_the_history_fails_alone():
+    """At J = 0, a SECOND window 9 back from a key's newest is beyond the
+    history: RL_E_TIME for that descriptor only; 8 back is still exact."""
     be = Backend(0.8, False, **SMALL)
     co = c_oracle.COracle(0.8, False)
     t0 = W.NOW0
@@ -160,20 +180,45 @@ def test_gpu_beyond_the_ring_fails_alone():
     co.close()
 
 
-@pytest.mark.parametrize("ring_lines", [0, 1 << 16])
-def test_gpu_snapshot_keeps_the_ring(ring_lines):
-    """rl_snapshot_save/load carry the ring: a restored ctx answers older
-    windows exactly like the one it was taken from (one pool partition, and
-    64 partitions)."""
-    bs = _stream(5, 500, 1_000, 6, 3, 7)
-    be = Backend(0.8, True, table_slots=1 << 14, max_batch=1 << 12, max_rules=8, ring_lines=ring_lines)
+def test_gpu_jitter_horizon_bound():
+    """J = 300: a SECOND key hit at t0 and t0 + 400. A request 300 s behind
+    (t0 + 100, a window never written) is exact; 350 s behind, or the record
+    of t0 itself (dead and dropped), is RL_E_TIME."""
+    be = Backend(0.8, False, jitter=300, **SMALL)
+    co = c_oracle.COracle(0.8, False)
+    t0 = W.NOW0
+    for now in (t0, t0 + 400):
+        b = W.c1_batch(np.arange(4), now)
+        be.do_limit_arrays(*b, isolate=True)
+        co.do_limit(*b)
+    a, n, nq, nr = W.c1_batch(np.arange(4), np.array([t0 + 100, t0 + 50, t0, t0 + 399]))
+    g = be.do_limit_arrays(a, n, nq, nr, isolate=True)
+    failed = np.zeros(n, bool)
+    failed[[2, 4]] = True  # the SECOND descriptors of t0 + 50 and t0
+    assert (g["status"][failed] == abi.RL_E_TIME).all(), g["status"]
+    assert (g["status"][~failed] == 0).all(), g["status"]
+    o = co.do_limit(*_drop(a, n, nq, ~failed), nr)
+    for k in ("code", "limit_remaining", "reset_s"):
+        assert np.array_equal(g[k][~failed], o[k]), k
+    be.close()
+    co.close()
+
+
+@pytest.mark.parametrize("history_entries", [0, 1 << 16])
+def test_gpu_snapshot_keeps_the_history(history_entries):
+    """rl_snapshot_save/load carry the history log: a restored ctx answers
+    older windows exactly like the one it was taken from."""
+    bs = _stream(5, 500, 1_000, 6, 20, 150)
+    kw = dict(table_slots=1 << 14, max_batch=1 << 12, max_rules=8, history_entries=history_entries, jitter=300)
+    be = Backend(0.8, True, **kw)
     co = c_oracle.COracle(0.8, True)
     for a, n, nq, nr in bs[:4]:
         be.do_limit_arrays(a, n, nq, nr)
         co.do_limit(a, n, nq, nr)
+    assert be.table_info()["history_appended"] > 0
     snap = be.snapshot()
     be.close()
-    be2 = Backend(0.8, True, table_slots=1 << 14, max_batch=1 << 12, max_rules=8, ring_lines=ring_lines)
+    be2 = Backend(0.8, True, **kw)
     be2.load_snapshot(snap)
     for a, n, nq, nr in bs[4:]:
         g = be2.do_limit_arrays(a, n, nq, nr)
@@ -184,18 +229,60 @@ def test_gpu_snapshot_keeps_the_ring(ring_lines):
     co.close()
 
 
-@pytest.mark.parametrize("ring_lines,tenants,nq", [(64, 3_000, 4_000), (1 << 16, 100_000, 150_000)])
-def test_gpu_ring_pool_exhausted_fails_never_miscounts(ring_lines, tenants, nq):
-    """A pool too small for the keys moving back and forth (one partition of
-    64 lines; 64 partitions of 1024, exhausted one after another): a slot
-    that could not take a line when its cur moved (lost_slots) fails its older
-    windows with RL_E_TIME; every descriptor that succeeds matches the oracle
-    fed only the descriptors that succeeded."""
-    be = Backend(0.8, False, table_slots=1 << 19, max_batch=1 << 19, max_rules=8, ring_lines=ring_lines)
+def test_gpu_snapshot_rejects_a_bad_slot_image():
+    """A slot image whose long stem points past the used arena is refused
+    (RL_E_INVALID), not uploaded."""
+    kw = dict(table_slots=1 << 12, max_batch=1 << 10, max_rules=8)
+    be = Backend(0.8, False, **kw)
+    a, n, nq, nr = W.c1_batch(np.arange(4), W.NOW0)
+    be.do_limit_arrays(a, n, nq, nr)
+    snap = bytearray(be.snapshot())
+    slots = np.frombuffer(snap, np.uint8, count=64 * (1 << 12), offset=64).reshape(-1, 64)
+    live = np.nonzero(slots[:, :4].view(np.uint32)[:, 0] >= 2)[0]
+    assert live.size == 8
+    i = 64 + 64 * int(live[0])
+    snap[i + 4:i + 6] = np.uint16(200).tobytes()   # key_len 200: a long stem...
+    snap[i + 60:i + 64] = np.uint32(1 << 30).tobytes()  # ...whose tail lies far past the arena
+    with pytest.raises(RedisError, match="RL_E_INVALID"):
+        be.load_snapshot(np.frombuffer(bytes(snap), np.uint8))
+    be.close()
+
+
+@pytest.mark.parametrize("tenants,nq", [(3_000, 4_000), (100_000, 150_000)])
+def test_gpu_round4_pool_exhaustion_streams_are_exact(tenants, nq):
+    """The streams that exhausted round 4's ring-line pool (64 lines, and 64
+    partitions of 1024): with the history log at its default size every
+    descriptor is answered, oracle-exact, none RL_E_TIME."""
+    be = Backend(0.8, False, table_slots=1 << 19, max_batch=1 << 19, max_rules=8)
     co = c_oracle.COracle(0.8, False)
+    try:
+        for a, n, nq_, nr in _stream(6, tenants, nq, 8, 3, 7):
+            g = be.do_limit_arrays(a, n, nq_, nr, isolate=True)
+            o = co.do_limit(a, n, nq_, nr)
+            assert (g["status"] == 0).all(), np.unique(g["status"])
+            for k in ("code", "limit_remaining", "reset_s", "stats"):
+                assert np.array_equal(g[k], o[k]), k
+        info = be.table_info()
+        assert info["history_lost"] == 0 and info["history_appended"] > 0
+    finally:
+        be.close()
+        co.close()
+
+
+@pytest.mark.parametrize("lc", [False, True])
+def test_gpu_history_log_overwritten_fails_never_miscounts(lc):
+    """A log far too small for J = 300 (64 x 1024 entries against ~16k
+    appends a batch): a lookup that reaches an overwritten entry fails with
+    RL_E_TIME (counted in history_lost); every descriptor that succeeds
+    matches the oracle fed only the descriptors that succeeded. Then the same
+    keys, far ahead in time and moving back within their reach, are answered
+    exactly again (their new history is walked before the broken part)."""
+    be = Backend(0.8, lc, table_slots=1 << 16, max_batch=1 << 14, max_rules=8, history_entries=1, jitter=300)
+    co = c_oracle.COracle(0.8, lc)
     failed_total = ok_total = 0
     try:
-        for a, n, nq, nr in _stream(6, tenants, nq, 8, 3, 7):
+        assert be.table_info()["history_entries"] == 64 * 1024
+        for a, n, nq, nr in _stream(10, 3_000, 8_000, 12, 20, 299, unit=1):
             g = be.do_limit_arrays(a, n, nq, nr, isolate=True)
             failed = g["status"] != 0
             assert (g["status"][failed] == abi.RL_E_TIME).all(), np.unique(g["status"])
@@ -206,19 +293,26 @@ def test_gpu_ring_pool_exhausted_fails_never_miscounts(ring_lines, tenants, nq):
             failed_total += int(failed.sum())
             ok_total += int(keep.sum())
         info = be.table_info()
-        assert info["ring_lines"] == ring_lines and info["ring_lines_used"] == ring_lines
-        assert info["lost_slots"] > 0 and failed_total > 0 and ok_total > failed_total
+        assert info["history_lost"] > 0 and failed_total > 0 and ok_total > failed_total
+        assert info["history_appended"] > info["history_entries"]
+        for k in range(4):  # 10 000 s later: forward, then up to 5 windows back
+            t = W.NOW0 + 10_000 + 10 * k
+            ten = np.arange(1_000)
+            b = W.c1_batch(ten, t - (ten % 6) * (k % 2))
+            g = be.do_limit_arrays(*b, isolate=True)
+            o = co.do_limit(*b)
+            assert (g["status"] == 0).all(), np.unique(g["status"])
+            for f in ("code", "limit_remaining", "reset_s"):
+                assert np.array_equal(g[f], o[f]), f
     finally:
         be.close()
         co.close()
 
 
-@pytest.mark.parametrize("ring_lines", [1024, 1 << 16])
-def test_gpu_sweep_returns_ring_lines(ring_lines):
-    """rl_sweep gives a swept slot's line back to its partition: a second and
-    third generation of keys moving back find the whole pool again, with no
-    failures."""
-    be = Backend(0.8, False, table_slots=1 << 14, max_batch=1 << 14, max_rules=8, ring_lines=ring_lines)
+def test_gpu_sweep_evicts_keys_with_history():
+    """rl_sweep evicts a slot once its cur and every logged record are dead;
+    a second and third generation of keys moving back are exact again."""
+    be = Backend(0.8, False, table_slots=1 << 14, max_batch=1 << 14, max_rules=8)
     try:
         for gen in range(3):
             co = c_oracle.COracle(0.8, False)
@@ -234,8 +328,9 @@ def test_gpu_sweep_returns_ring_lines(ring_lines):
                     assert np.array_equal(g[f], o[f]), f
             co.close()
             info = be.table_info()
-            assert info["lost_slots"] == 0 and 0 < info["ring_lines_used"] <= 1024
+            assert info["history_lost"] == 0 and info["history_slots"] > 0
             assert be.sweep(t + 50_000) > 0
-            assert be.table_info()["ring_lines_used"] == 0
+            info = be.table_info()
+            assert info["history_slots"] == 0 and info["live_slots"] == 0
     finally:
         be.close()

@@ -18,6 +18,9 @@
 //   fat_res      as fat, the result stored coalesced in bucket order
 //   perm         the permutation pass fat_res would need afterwards (8-B
 //                gather by position, 8-B coalesced store)
+//   arrival_ovf_write / _rmw   arrival, and every other lane also writes a
+//                32-B record at a random place of an overflow table (half
+//                the slots' bytes) / reads it first (an open-addressing insert)
 // Usage: orderprobe [lanes=1048576] [table_log2=27]; one JSON line.
 #include <hip/hip_runtime.h>
 
@@ -45,7 +48,8 @@ __device__ __forceinline__ uint64_t mix(uint64_t k) {
 constexpr uint32_t REGIONS = 1024;
 
 template <int MODE>
-__global__ __launch_bounds__(256) void k_probe(uint4* __restrict__ slots, uint64_t nslots, const uint4* __restrict__ rec,
+__global__ __launch_bounds__(256) void k_probe(uint4* __restrict__ slots, uint64_t nslots, uint4* __restrict__ ovf,
+                                               uint64_t novf, const uint4* __restrict__ rec,
                                                const uint8_t* __restrict__ stem, const uint4* __restrict__ fat,
                                                const uint2* __restrict__ list, uint32_t n,
                                                unsigned long long* __restrict__ res, uint32_t salt) {
@@ -54,7 +58,7 @@ __global__ __launch_bounds__(256) void k_probe(uint4* __restrict__ slots, uint64
   const uint64_t h = mix(((uint64_t)salt << 32) | i);
   uint64_t s;
   uint32_t acc = 0, e = i;
-  if (MODE == 0) {
+  if (MODE == 0 || MODE >= 4) {
     s = h & (nslots - 1);
     const uint4 r0 = rec[2 * (size_t)i], r1 = rec[2 * (size_t)i + 1];
     const uint4* sp = reinterpret_cast<const uint4*>(stem + (((size_t)i * 34) & ~(size_t)15));
@@ -81,6 +85,13 @@ __global__ __launch_bounds__(256) void k_probe(uint4* __restrict__ slots, uint64
   acc ^= a0.x ^ a1.y ^ a2.z ^ a3.w;
   slots[s * 4 + 1] = make_uint4(acc, a1.y + 1, a1.z, a1.w);  // window record write-back (16 B)
   res[e] = ((unsigned long long)acc << 32) | i;
+  if (MODE >= 4 && (i & 1)) {  // the displaced window record into an overflow table (every other lane)
+    const uint64_t o = mix(h) & (novf - 1);
+    uint32_t t = 0;
+    if (MODE == 5) t = ovf[2 * o].x;  // (probe first: an open-addressing insert)
+    ovf[2 * o] = make_uint4(acc + t, i, 7u, 8u);
+    ovf[2 * o + 1] = make_uint4(i, acc, 0u, 0u);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_perm(const unsigned long long* __restrict__ src, const uint2* __restrict__ list,
@@ -124,6 +135,10 @@ int main(int argc, char** argv) {
   uint2* list;
   unsigned long long *res, *res2;
   CHK(hipMalloc(&slots, nslots * 64));
+  const uint64_t novf = nslots / 2;  // 32-B overflow entries: a table half the slots' bytes
+  uint4* ovf;
+  CHK(hipMalloc(&ovf, novf * 32));
+  CHK(hipMemset(ovf, 0, novf * 32));
   CHK(hipMalloc(&rec, (size_t)n * 32));
   CHK(hipMalloc(&stem, (size_t)n * 34 + 64));
   CHK(hipMalloc(&fat, (size_t)n * 64));
@@ -137,14 +152,16 @@ int main(int argc, char** argv) {
   const uint32_t g = (n + 255) / 256;
   k_fill_list<<<g, 256>>>(list, fat, n);
   const int reps = 20;
-  float t[5];
-  t[0] = timed([&](uint32_t s) { k_probe<0><<<g, 256>>>(slots, nslots, rec, stem, fat, list, n, res, s); }, reps);
-  t[1] = timed([&](uint32_t s) { k_probe<1><<<g, 256>>>(slots, nslots, rec, stem, fat, list, n, res, s); }, reps);
-  t[2] = timed([&](uint32_t s) { k_probe<2><<<g, 256>>>(slots, nslots, rec, stem, fat, list, n, res, s); }, reps);
-  t[3] = timed([&](uint32_t s) { k_probe<3><<<g, 256>>>(slots, nslots, rec, stem, fat, list, n, res, s); }, reps);
+  float t[7];
+  t[0] = timed([&](uint32_t s) { k_probe<0><<<g, 256>>>(slots, nslots, ovf, novf, rec, stem, fat, list, n, res, s); }, reps);
+  t[1] = timed([&](uint32_t s) { k_probe<1><<<g, 256>>>(slots, nslots, ovf, novf, rec, stem, fat, list, n, res, s); }, reps);
+  t[2] = timed([&](uint32_t s) { k_probe<2><<<g, 256>>>(slots, nslots, ovf, novf, rec, stem, fat, list, n, res, s); }, reps);
+  t[3] = timed([&](uint32_t s) { k_probe<3><<<g, 256>>>(slots, nslots, ovf, novf, rec, stem, fat, list, n, res, s); }, reps);
   t[4] = timed([&](uint32_t) { k_perm<<<g, 256>>>(res, list, n, res2); }, reps);
+  t[5] = timed([&](uint32_t s) { k_probe<4><<<g, 256>>>(slots, nslots, ovf, novf, rec, stem, fat, list, n, res, s); }, reps);
+  t[6] = timed([&](uint32_t s) { k_probe<5><<<g, 256>>>(slots, nslots, ovf, novf, rec, stem, fat, list, n, res, s); }, reps);
   printf("{\"tool\": \"orderprobe\", \"lanes\": %u, \"table_bytes\": %llu, \"us_arrival\": %.1f, \"us_gather\": %.1f, "
-         "\"us_fat\": %.1f, \"us_fat_res\": %.1f, \"us_perm\": %.1f}\n",
-         n, (unsigned long long)(nslots * 64), t[0], t[1], t[2], t[3], t[4]);
+         "\"us_fat\": %.1f, \"us_fat_res\": %.1f, \"us_perm\": %.1f, \"us_arrival_ovf_write\": %.1f, \"us_arrival_ovf_rmw\": %.1f}\n",
+         n, (unsigned long long)(nslots * 64), t[0], t[1], t[2], t[3], t[4], t[5], t[6]);
   return 0;
 }
