@@ -38,6 +38,8 @@ def lib():
         L.rlo_keys.argtypes = [C.c_void_p, C.POINTER(abi.RlBatch), C.c_void_p, C.c_void_p, C.c_uint32]
         L.rlo_near_threshold.restype = C.c_uint32
         L.rlo_near_threshold.argtypes = [C.c_uint32, C.c_float]
+        L.rlo_set_horizon.restype = None
+        L.rlo_set_horizon.argtypes = [C.c_void_p, C.c_int64]
         L.rlo_live_keys.restype = C.c_uint64
         L.rlo_live_keys.argtypes = [C.c_void_p]
         _lib = L
@@ -45,8 +47,12 @@ def lib():
 
 
 class COracle:
-    def __init__(self, near_limit_ratio=0.8, local_cache=False, per_second=False):
+    def __init__(self, near_limit_ratio=0.8, local_cache=False, per_second=False, horizon=0):
+        """horizon: keep keys for requests lagging up to horizon s + 2 windows
+        (the GPU ctx's expiration_jitter_max_seconds; GC slack only)."""
         self.h = lib().rlo_create(near_limit_ratio, int(local_cache), int(per_second))
+        if horizon:
+            lib().rlo_set_horizon(self.h, horizon)
 
     def close(self):
         if self.h:

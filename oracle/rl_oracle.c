@@ -37,11 +37,15 @@ typedef struct {
 } ent_t;
 
 /* Garbage collection (smap_rebuild) drops an entry only once it is dead for
- * any request up to GC_WINDOWS windows of its unit behind the request that
- * triggers the rebuild. Liveness is judged against each request's own clock
- * (lazy expiry), so with time moving backwards an entry dead at one request
- * is live again for an earlier one; the slack keeps every entry a request
- * within that lag can read (the GPU table's ring reaches as far, HIST_W). */
+ * any request up to GC_WINDOWS windows of its unit, or horizon + 2 windows,
+ * behind the request that triggers the rebuild. Liveness is judged against
+ * each request's own clock (lazy expiry), so with time moving backwards an
+ * entry dead at one request is live again for an earlier one; the slack keeps
+ * every entry a request within that lag can read (the GPU table's history
+ * answers as far: HIST_W windows, or div + J seconds). GC is an
+ * implementation detail of this restatement: the reference's Redis keys have
+ * no window limit, so streams whose clocks lag further are outside what the
+ * oracle models. */
 #define GC_WINDOWS 8
 
 typedef struct {
@@ -50,6 +54,7 @@ typedef struct {
   char* arena;
   uint64_t arena_used, arena_cap;
   int is_lc;  /* liveness rule differs: redis now<=expire, freecache now<expire */
+  int64_t horizon;  /* extra lag kept (rlo_set_horizon): the GPU's history horizon J */
 } smap_t;
 
 static uint64_t hash_bytes(const char* p, uint32_t n) {
@@ -109,14 +114,15 @@ static void smap_rebuild(smap_t* m, int64_t now) {
 static ent_t* smap_upsert(smap_t* m, const char* k, uint32_t n, int64_t now, int64_t div, int* created) {
   uint64_t h = hash_bytes(k, n);
   ent_t* e = smap_find(m, k, n, h);
+  const int64_t slack = GC_WINDOWS * div > m->horizon + 2 * div ? GC_WINDOWS * div : m->horizon + 2 * div;
   *created = 0;
   if (e->h) {
-    if (e->slack < GC_WINDOWS * div) e->slack = GC_WINDOWS * div;
+    if (e->slack < slack) e->slack = slack;
     return e;
   }
   if ((m->used + 1) * 2 > m->cap) { smap_rebuild(m, now); e = smap_find(m, k, n, h); }
   while (m->arena_used + n > m->arena_cap) { m->arena_cap *= 2; m->arena = (char*)realloc(m->arena, m->arena_cap); }
-  e->h = h; e->off = m->arena_used; e->len = n; e->count = 0; e->expire = -1; e->slack = GC_WINDOWS * div;
+  e->h = h; e->off = m->arena_used; e->len = n; e->count = 0; e->expire = -1; e->slack = slack;
   memcpy(m->arena + m->arena_used, k, n); m->arena_used += n; m->used++;
   *created = 1;
   return e;
@@ -177,6 +183,12 @@ rlo_ctx* rlo_create(float near_limit_ratio, int local_cache, int per_second) {
   smap_init(&c->lc, 1 << 12, 1);
   c->keycap = 1 << 16; c->keybuf = (char*)malloc(c->keycap);
   return c;
+}
+
+/* Keep entries for requests lagging up to `horizon` seconds + 2 windows (the
+ * GPU ctx's expiration_jitter_max_seconds). */
+void rlo_set_horizon(rlo_ctx* c, int64_t horizon) {
+  c->redis.horizon = c->redis_ps.horizon = c->lc.horizon = horizon;
 }
 
 void rlo_destroy(rlo_ctx* c) {

@@ -779,14 +779,15 @@ __device__ inline bool hist_keep(const TableDev& t, const Win& r, uint32_t ws_ne
   return r.ws != WS_INVALID &&
          (hist_reach(r.ws, ws_new, d) || (uint64_t)max(r.expire, r.lc) + t.horizon + d >= (uint64_t)ws_new);
 }
-// own: the slot's records are written by its own unit's requests only (the
-// simple path), so a record of w is dead from w + 2 div on (EXPIRE and the
-// local-cache TTL end before then); alias writes (the general path) can move
-// EXPIRE further.
-__device__ inline bool hist_absent_ok(const TableDev& t, uint32_t now, uint32_t w, uint32_t cur_ws, uint32_t d,
-                                      bool own) {
-  return hist_reach(w, cur_ws, d) || (uint64_t)now + t.horizon + d >= (uint64_t)cur_ws ||
-         (own && (uint64_t)now >= (uint64_t)w + 2ull * d);
+// Or w is 2 div back: a record of w holds EXPIRE and the local-cache TTL of
+// requests inside w (now + div), dead from w + 2 div on. An alias write (a
+// multi-unit stem's key written through another unit's request) can move a
+// record's EXPIRE further, but the writing unit's own record of w carries the
+// same value and is checked too (every unit slot of the stem is), under its
+// own div: a live key never goes unnoticed.
+__device__ inline bool hist_dead(uint32_t now, uint32_t w, uint32_t d) { return (uint64_t)now >= (uint64_t)w + 2ull * d; }
+__device__ inline bool hist_absent_ok(const TableDev& t, uint32_t now, uint32_t w, uint32_t cur_ws, uint32_t d) {
+  return hist_reach(w, cur_ws, d) || (uint64_t)now + t.horizon + d >= (uint64_t)cur_ws || hist_dead(now, w, d);
 }
 
 // Append r to the chain whose head is prev (slot si, tag, newest window
@@ -1074,8 +1075,9 @@ __device__ __attribute__((always_inline)) inline int simple_pick(const TableDev&
     if (S.old_dirty) simple_put(t, S);
     Win r;
     const int f = S.chain == LOG_NONE ? 0 : log_find(t, S.chain, S.si, S.tag, S.cur.ws, w, &r);
-    if (f < 0 || (f == 0 && !hist_absent_ok(t, now, w, S.cur.ws, d, true))) return -1;
-    S.old = f ? r : Win{w, 0, 0, 0};
+    // (an overwritten entry on the way: w's record may be gone, fine once dead)
+    if (f < 0 ? !hist_dead(now, w, d) : (f == 0 && !hist_absent_ok(t, now, w, S.cur.ws, d))) return -1;
+    S.old = f > 0 ? r : Win{w, 0, 0, 0};
     S.old_dirty = false;
   }
   return 1;
@@ -1163,9 +1165,7 @@ __device__ inline void gen_set_old(const TableDev& t, GeneralState& G, uint32_t 
 
 // The record of window w in unit slot k (present): its cur, its cached older
 // record (from the chain), or null when unit k has none. *lost: unit k may have
-// had one that the history no longer holds. Alias writes can move a record's
-// EXPIRE past its own unit's 2 div, so the general path does not take
-// hist_absent_ok's own-unit bound.
+// had one, still live, that the history no longer holds.
 __device__ inline Win* gen_rec(const TableDev& t, GeneralState& G, uint32_t k, uint32_t w, uint32_t now, bool* lost) {
   const uint32_t d = div_of(k + 1);
   Win& c = G.cur[k];
@@ -1178,7 +1178,7 @@ __device__ inline Win* gen_rec(const TableDev& t, GeneralState& G, uint32_t k, u
     gen_set_old(t, G, k, r, false);
     return &G.old[k];
   }
-  if (lost && (f < 0 || !hist_absent_ok(t, now, w, c.ws, d, false))) *lost = true;
+  if (lost && (f < 0 ? !hist_dead(now, w, d) : !hist_absent_ok(t, now, w, c.ws, d))) *lost = true;
   return nullptr;
 }
 
@@ -3831,7 +3831,7 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
         continue;  // (unit k's keys are multiples of its div)
       } else {
         const int f = chain[k] == LOG_NONE ? 0 : log_find(t, chain[k], (uint32_t)sidx[k], slot_tag(hs, k + 1), c[k].ws, w, &R);
-        if (f != 0 || !hist_absent_ok(t, now, w, c[k].ws, d, false)) return true;
+        if (f != 0 || !hist_absent_ok(t, now, w, c[k].ws, d)) return true;
         continue;
       }
       const bool live = (P.per_second && k == 0) == cls && now <= R.expire;

@@ -29,7 +29,7 @@ SMALL = dict(table_slots=1 << 16, max_batch=1 << 14, max_rules=1 << 10)
 
 def _compare(batches, lc, isolate=False, jitter=0):
     be = Backend(0.8, lc, table_slots=1 << 18, max_batch=1 << 16, max_rules=8, jitter=jitter)
-    co = c_oracle.COracle(0.8, lc)
+    co = c_oracle.COracle(0.8, lc, horizon=jitter)
     try:
         for i, (a, n, nq, nr) in enumerate(batches):
             g = be.do_limit_arrays(a, n, nq, nr, isolate=isolate)
@@ -185,7 +185,7 @@ def test_gpu_jitter_horizon_bound():
     (t0 + 100, a window never written) is exact; 350 s behind, or the record
     of t0 itself (dead and dropped), is RL_E_TIME."""
     be = Backend(0.8, False, jitter=300, **SMALL)
-    co = c_oracle.COracle(0.8, False)
+    co = c_oracle.COracle(0.8, False, horizon=300)
     t0 = W.NOW0
     for now in (t0, t0 + 400):
         b = W.c1_batch(np.arange(4), now)
@@ -211,7 +211,7 @@ def test_gpu_snapshot_keeps_the_history(history_entries):
     bs = _stream(5, 500, 1_000, 6, 20, 150)
     kw = dict(table_slots=1 << 14, max_batch=1 << 12, max_rules=8, history_entries=history_entries, jitter=300)
     be = Backend(0.8, True, **kw)
-    co = c_oracle.COracle(0.8, True)
+    co = c_oracle.COracle(0.8, True, horizon=300)
     for a, n, nq, nr in bs[:4]:
         be.do_limit_arrays(a, n, nq, nr)
         co.do_limit(a, n, nq, nr)
@@ -278,7 +278,7 @@ def test_gpu_history_log_overwritten_fails_never_miscounts(lc):
     keys, far ahead in time and moving back within their reach, are answered
     exactly again (their new history is walked before the broken part)."""
     be = Backend(0.8, lc, table_slots=1 << 16, max_batch=1 << 14, max_rules=8, history_entries=1, jitter=300)
-    co = c_oracle.COracle(0.8, lc)
+    co = c_oracle.COracle(0.8, lc, horizon=300)
     failed_total = ok_total = 0
     try:
         assert be.table_info()["history_entries"] == 64 * 1024

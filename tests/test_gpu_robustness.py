@@ -308,17 +308,18 @@ def test_gpu_long_runs_across_fast_blocks_vs_c_oracle():
 
 @pytest.mark.parametrize("lc", [False, True])
 def test_gpu_revisit_after_ring_reach_vs_c_oracle(lc):
-    """Keys revisited after more than the ring's 8 windows (a SECOND key every
-    ~20 s at C1): the old window is out of reach from the new one and is not
-    written back to the ring. Later batches revisit, go back inside the
-    reach (windows never written: fresh keys) and stay oracle-exact; a
-    request for the dropped window itself is RL_E_TIME, as before. Short runs
-    (one lane) and long runs (the parallel path) both roll this way."""
+    """Keys revisited after more than the 8 windows always kept (a SECOND key
+    every ~20 s at C1, J = 0): the old window is dead and not kept in the
+    history log. Later batches revisit, go back inside the reach (windows
+    never written: fresh keys) and stay oracle-exact. Far behind the newest
+    window, a request whose record the log still holds is answered exactly,
+    and one whose record was dropped is RL_E_TIME. Short runs (one lane) and
+    long runs (the parallel path) both roll this way."""
     be = Backend(0.8, lc, **SMALL)
-    co = c_oracle.COracle(0.8, lc)
+    co = c_oracle.COracle(0.8, lc, horizon=1000)  # (no GC within the stream: every key the GPU may hold)
     t0 = workloads.NOW0
     ten = np.r_[np.arange(100), np.full(60, 7)]  # tenant 7 also as a long run
-    hits = np.r_[np.full(100, 30, np.uint32), np.ones(60, np.uint32)]  # over the SECOND limit: local-cache entries
+    hits = np.r_[np.full(100, 30, np.uint32), np.ones(60, np.uint32)]
     for dt in (0, 20, 21, 15, 40, 33, 100, 612):
         a, n, nq, nr = workloads.c1_batch(ten, t0 + dt, hits)
         g = be.do_limit_arrays(a, n, nq, nr, isolate=True)
@@ -326,9 +327,19 @@ def test_gpu_revisit_after_ring_reach_vs_c_oracle(lc):
         assert not g["status"].any(), dt
         for k in ("code", "limit_remaining", "reset_s", "stats"):
             assert np.array_equal(g[k], o[k]), (dt, k)
-    # a SECOND window far behind the newest (t0 + 612): out of the ring's reach
-    a, n, nq, nr = workloads.c1_batch(np.arange(10), t0 + 20)
-    g = be.do_limit_arrays(a, n, nq, nr, isolate=True)
-    assert (g["status"][0::2] == abi.RL_E_TIME).all()
+    # SECOND windows far behind the newest (t0 + 612): t0 + 20 was logged
+    # when t0 + 21 came (in reach) and is answered; t0 + 40 was dropped when
+    # t0 + 100 came (dead, out of reach): RL_E_TIME
+    for dt, held in ((20, True), (40, False)):
+        a, n, nq, nr = workloads.c1_batch(np.r_[np.arange(10), np.full(60, 7)], t0 + dt)
+        g = be.do_limit_arrays(a, n, nq, nr, isolate=True)
+        failed = np.zeros(n, bool)
+        if not held:
+            failed[0::2] = True  # every SECOND descriptor (tenant 7's long run too)
+        assert (g["status"][failed] == abi.RL_E_TIME).all() and not g["status"][~failed].any(), (dt, g["status"])
+        from test_gpu_history import _drop
+        o = co.do_limit(*_drop(a, n, nq, ~failed), nr)
+        for k in ("code", "limit_remaining", "reset_s"):
+            assert np.array_equal(g[k][~failed], o[k]), (dt, k)
     be.close()
     co.close()
