@@ -215,7 +215,9 @@ int rl_do_limit(rl_ctx* ctx, const rl_batch* in, rl_result* out);
  * (the inputs' producer); with NULL the inputs must be complete at the call.
  * *out is read after rl_synchronize (the caller's stream is never made to wait
  * for a batch, which would chain the next batch's inputs behind it and
- * serialise the pipeline). Returns once the work is enqueued; errors detected
+ * serialise the pipeline). The inputs are read until the batch is complete
+ * (rl_synchronize, or rl_batch_progress): keep them unchanged until then.
+ * Returns once the work is enqueued; errors detected
  * on the GPU surface at rl_synchronize. On a multi-shard ctx shard 0 takes the
  * whole device batch as its slice (the other shards' slices are empty) and
  * routes it to the owners as above; the caller's thread waits only until every
@@ -431,8 +433,10 @@ int rl_route_scatter(rl_ctx* ctx, uint32_t n, const uint32_t* perm, const uint64
  * sequential INCRBY contract is kept in). Device arrays; the batch starts
  * after the work already on `stream` (NULL: inputs complete at the call). A
  * call enqueues its batch's partition and counts exchange and completes the
- * PREVIOUS batch, so the host never waits for work it just issued: a batch's
- * inputs may be reused once the next call has returned, its outputs are read
+ * PREVIOUS batch, so the host never waits for work it just issued. The
+ * descriptors a rank owns of its own slice are read in place by its owner
+ * batch (no copy): a batch's inputs may be reused once RL_ROUTED_INFLIGHT
+ * later calls have returned, or after rl_synchronize; its outputs are read
  * after rl_synchronize (collective too on such a ctx: it completes the last
  * batch). Keep `out` valid until then. out->stats = the deltas of
  * THIS rank's requests (summed over ranks: the node's). Ranks may pass
@@ -454,6 +458,7 @@ int rl_route_scatter(rl_ctx* ctx, uint32_t n, const uint32_t* perm, const uint64
  * are not: they see every batch but the pending one, and a rank may call them
  * alone (e.g. for its gauges). */
 #define RL_COMM_ID_BYTES 128u
+#define RL_ROUTED_INFLIGHT 6u  /* routed batches in flight (the input-reuse distance above) */
 int rl_comm_unique_id(uint8_t* id);
 int rl_comm_loopback_id(uint8_t* id);
 int rl_comm_init(rl_ctx* ctx, uint32_t world, uint32_t rank, const uint8_t* id);

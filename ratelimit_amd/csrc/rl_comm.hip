@@ -60,7 +60,7 @@ namespace {
 // this wait never binds (routed N=1 3.33-3.36 vs 3.22-3.30 G); the host's
 // remaining ~150 us wait per step for the counts is the partition waiting for
 // GPU capacity beside the owner pipelines (RL_DEBUG_ROUTE_TIMING).
-constexpr uint32_t RSLOTS = 6;
+constexpr uint32_t RSLOTS = RL_ROUTED_INFLIGHT;
 
 // The counts message: CNT_W u64 per peer.
 constexpr uint32_t CNT_W = 4;                 // records, stem bytes, n_rules, flags
@@ -78,6 +78,8 @@ struct CommSlot {
   Wire* send_rec = nullptr;                // partition of this rank's slice, owner order
   uint8_t* send_stem = nullptr;
   uint32_t* perm = nullptr;                // record -> slice index
+  unsigned long long* hash = nullptr;      // [slice] stem hashes (the own chunk's owner batch reads them)
+  rl_batch src{};                          // the slice as partitioned (device view): the own chunk's source
   unsigned long long* cnt = nullptr;       // [2 x CNT_W x world]: sent per peer, then received
   Wire* recv_rec = nullptr;                // chunks of every source, rank order
   uint8_t* recv_stem = nullptr;
@@ -115,12 +117,14 @@ struct CommRouter {
   uint32_t m_max = 0;
   uint32_t part_max = 0;  // owner part size: max_batch (test knob: RL_DEBUG_OWNER_PART)
   bool alias = false;     // world 1: the owner reads the partition in place, no exchange
+  bool own = true;        // this rank's own chunk read in place from its slice (no wire records, no stem copy)
   hipStream_t cs = nullptr, fwd = nullptr, ret = nullptr;
   hipEvent_t in_ready = nullptr;
   CommSlot slot[RSLOTS];
   uint32_t next = 0;
   int pending = -1;                     // slot whose second half is still to run
   unsigned long long* h_cnt = nullptr;  // pinned [RSLOTS][2 x CNT_W x world]
+  unsigned long long* d_hcnt = nullptr;  // h_cnt as the device sees it (world 1: the partition stores the counts there)
   std::vector<uint64_t> base;           // received chunk offsets in recv_stem (host)
   std::vector<uint64_t> so_r, so_b, ro_r;  // per-peer send / receive offsets (host)
   std::vector<Xfer> ops;
@@ -165,7 +169,7 @@ int run_group(CommRouter* r, Engine* e, uint32_t ch, hipStream_t st) {
 }
 
 void free_slot(CommSlot& S) {
-  void* bufs[] = {S.send_rec, S.send_stem, S.perm, S.cnt, S.recv_rec, S.recv_stem, S.ret_send, S.back, S.ostats,
+  void* bufs[] = {S.send_rec, S.send_stem, S.perm, S.hash, S.cnt, S.recv_rec, S.recv_stem, S.ret_send, S.back, S.ostats,
                   S.stats_stage, S.h_stem, S.h_off, S.h_req, S.h_limit, S.h_hits, S.h_rule, S.h_now, S.h_unit,
                   S.h_flags, S.h_code, S.h_status, S.h_rem, S.h_reset, S.io_stats, S.h_cbuf};
   for (void* p : bufs)
@@ -411,13 +415,18 @@ int first_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, const rl_batch
     if (r->broken) return rc;
     in = &staged;
   }
-  if (!rc)
+  // world 1: no exchange, the counts go straight to the host's copy (kernel
+  // stores to page-locked memory; no copy launch per batch)
+  unsigned long long* hc = r->alias && r->d_hcnt ? r->d_hcnt + (size_t)s * 2 * CNT_W * W : nullptr;
+  if (!rc) {
     rc = eng_route_pack(e, in, W, me, S.send_rec, S.send_stem, S.perm, (uint64_t*)S.cnt, r->cs, CNT_W, S.n_rules,
-                        flags);
+                        flags, r->own ? me : ROUTE_OWN_NONE, S.hash, hc);
+    S.src = *in;  // (read by this batch's owner part, in the next call)
+  }
   if (rc) {  // (a device-side malformation zeroes the counts itself and fails at rl_synchronize)
     S.err = rc;
     S.errmsg = eng_last_error(e);
-    launch_cnt_fill(S.cnt, W, CNT_W, 0, flags | CNT_FAILED, r->cs);
+    launch_cnt_fill(S.cnt, W, CNT_W, 0, flags | CNT_FAILED, r->cs, hc);
   }
   if (!r->alias) {
     r->ops.clear();
@@ -429,8 +438,9 @@ int first_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, const rl_batch
     const int g = run_group(r, e, 0, r->cs);
     if (g) return g;
   }
-  CHK_HIP(e, hipMemcpyAsync(r->h_cnt + (size_t)s * 2 * CNT_W * W, S.cnt, 2ull * CNT_W * W * 8, hipMemcpyDeviceToHost,
-                            r->cs));
+  if (!hc)
+    CHK_HIP(e, hipMemcpyAsync(r->h_cnt + (size_t)s * 2 * CNT_W * W, S.cnt, 2ull * CNT_W * W * 8, hipMemcpyDeviceToHost,
+                              r->cs));
   CHK_HIP(e, hipEventRecord(S.packed, r->cs));
   return RL_OK;
 }
@@ -499,10 +509,10 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
     }
     const int g = run_group(r, e, 1, r->fwd);
     if (g) return g;
-    if (h[CNT_W * me])
+    if (h[CNT_W * me] && !r->own)
       CHK_HIP(e, hipMemcpyAsync(S.recv_rec + r->ro_r[me], S.send_rec + r->so_r[me], h[CNT_W * me] * sizeof(Wire),
                                 hipMemcpyDeviceToDevice, r->fwd));
-    if (h[CNT_W * me + 1])
+    if (h[CNT_W * me + 1])  // (none with the own chunk read in place)
       CHK_HIP(e, hipMemcpyAsync(S.recv_stem + r->base[me], S.send_stem + r->so_b[me], h[CNT_W * me + 1],
                                 hipMemcpyDeviceToDevice, r->fwd));
   }
@@ -514,10 +524,17 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
   // the received labels.
   std::vector<uint64_t>& cut = S.cut;
   cut.assign(1, 0);
+  const uint64_t own_lo = r->ro_r[me], own_hi = r->own ? r->ro_r[me + 1] : own_lo;  // (received positions)
   if (n_recv > mb && !owner_fail) {
     std::vector<uint32_t> lab(n_recv);
     CHK_HIP(e, hipStreamSynchronize(r->fwd));
     CHK_HIP(e, hipMemcpy2D(lab.data(), 4, recv_rec, sizeof(Wire), 4, n_recv, hipMemcpyDeviceToHost));
+    if (own_hi > own_lo) {  // the own chunk has no wire labels: from its slice's request indices
+      std::vector<uint32_t> pi(own_hi - own_lo), rq(S.n);
+      CHK_HIP(e, hipMemcpy(pi.data(), S.perm + r->so_r[me], pi.size() * 4, hipMemcpyDeviceToHost));
+      CHK_HIP(e, hipMemcpy(rq.data(), S.src.req_idx, rq.size() * 4, hipMemcpyDeviceToHost));
+      for (uint64_t j = own_lo; j < own_hi; j++) lab[j] = (me << ROUTE_REQ_BITS) | rq[pi[j - own_lo]];
+    }
     uint64_t a = 0;
     while (n_recv - a > mb) {
       uint64_t b = a + mb;
@@ -542,8 +559,31 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
   } else {
     for (uint32_t q = 0; q < parts; q++) {
       const uint64_t a = cut[q], b = cut[q + 1];
+      // this part's share of the own chunk, read in place from the slice
+      OwnChunk oc{};
+      const uint64_t lo = std::max(a, own_lo), hi = std::min(b, own_hi);
+      if (lo < hi) {
+        const rl_batch& sb = S.src;
+        oc.lo = (uint32_t)(lo - a);
+        oc.n = (uint32_t)(hi - lo);
+        oc.rank = me;
+        oc.stem_total = e->cfg.max_stem_bytes;
+        oc.src_n = sb.n;
+        oc.n_rules = sb.n_rules;
+        oc.idx = S.perm + r->so_r[me] + (lo - own_lo);
+        oc.hash = S.hash;
+        oc.stem = sb.stem_bytes;
+        oc.off = sb.stem_off;
+        oc.now = sb.now;
+        oc.req = sb.req_idx;
+        oc.unit = sb.unit;
+        oc.flags = sb.flags;
+        oc.limit = sb.limit;
+        oc.hits = sb.hits;
+        oc.rule = sb.rule_id;
+      }
       const int rc = eng_route_owner(e, (uint32_t)(b - a), recv_rec + a, recv_stem, b_recv, r->base.data(), W,
-                                     (uint32_t)M, (uint32_t)M, S.ostats + q * blk, iso ? 1 : 0, S.sent, &S.k[q]);
+                                     (uint32_t)M, (uint32_t)M, S.ostats + q * blk, iso ? 1 : 0, S.sent, &S.k[q], &oc);
       if (rc) return breaks(r, e, rc, eng_last_error(e));  // (argument checks only: the sizes were checked above)
       // its packed results, before a later part can take the same engine buffer
       const uint32_t k = S.k[q];
@@ -644,6 +684,7 @@ CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t*
   const rl_config& g = e->cfg;
   r->part_max = g.max_batch;
   r->alias = world == 1 && !getenv("RL_DEBUG_ROUTE_NOALIAS");
+  r->own = !getenv("RL_DEBUG_ROUTE_NOOWN");  // (A/B knob: the own chunk as wire records and copied stems)
   r->timing = getenv("RL_DEBUG_ROUTE_TIMING") != nullptr;
   if (const char* pm = getenv("RL_DEBUG_OWNER_PART"))
     r->part_max = std::max<uint32_t>(1, std::min<uint32_t>(g.max_batch, (uint32_t)atoi(pm)));
@@ -658,10 +699,15 @@ CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t*
             hipStreamCreateWithFlags(&r->ret, hipStreamNonBlocking) == hipSuccess &&
             hipEventCreateWithFlags(&r->in_ready, hipEventDisableTiming) == hipSuccess &&
             hipHostMalloc((void**)&r->h_cnt, (size_t)RSLOTS * 2 * CNT_W * world * 8) == hipSuccess;
+  if (ok && world == 1 && hipHostGetDevicePointer((void**)&r->d_hcnt, r->h_cnt, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    r->d_hcnt = nullptr;  // (then a copy per batch)
+  }
   for (uint32_t s = 0; s < RSLOTS && ok; s++) {
     CommSlot& S = r->slot[s];
     ok = dalloc(&S.send_rec, g.max_batch) == hipSuccess && dalloc(&S.send_stem, (size_t)g.max_stem_bytes + 64) == hipSuccess &&
-         dalloc(&S.perm, g.max_batch) == hipSuccess && dalloc(&S.cnt, 2 * CNT_W * (size_t)world) == hipSuccess &&
+         dalloc(&S.perm, g.max_batch) == hipSuccess && dalloc(&S.hash, g.max_batch) == hipSuccess &&
+         dalloc(&S.cnt, 2 * CNT_W * (size_t)world) == hipSuccess &&
          dalloc(&S.back, g.max_batch) == hipSuccess &&
          dalloc(&S.stats_stage, (size_t)world * r->m_max) == hipSuccess &&
          hipEventCreateWithFlags(&S.packed, hipEventDisableTiming) == hipSuccess &&
@@ -739,6 +785,11 @@ int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, 
   const uint32_t s = r->next;
   r->next = (s + 1) % RSLOTS;
   CommSlot& S = r->slot[s];
+  // the slot's previous batch (RSLOTS calls ago) is complete: its owner part
+  // read that slice's own chunk in place, so a caller may reuse a batch's
+  // inputs once RSLOTS later calls have returned (long done by then: this
+  // wait does not bind)
+  CHK_HIP(e, hipEventSynchronize(S.done));
   S.out = *out;
   S.n = n;
   S.n_rules = nr;

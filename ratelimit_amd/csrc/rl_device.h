@@ -302,6 +302,9 @@ constexpr uint32_t FLAG_SKIP = 0x80;
 // bit 6 = the descriptor's sort key occurs more than once in the batch
 // (k_run_check): the sorted path answers it, not the keys-seen-once part.
 constexpr uint32_t FLAG_DUP = 0x40;
+// bit 5 = a routed owner batch's own-chunk record: its stem lies in the
+// source batch (BatchDev::own), not in the received stems.
+constexpr uint32_t FLAG_SRC = 0x20;
 
 constexpr uint32_t NOW_MAX = 0xFFFFFFFFu - 2u * 86400u;  // now + 2*div must fit u32
 

@@ -162,7 +162,8 @@ int eng_debug_decide(Engine* c, uint32_t n, const uint32_t* before, const uint32
 // in-library router's counts message).
 int eng_route_pack(Engine* c, const rl_batch* in, uint32_t n_shards, uint32_t src_rank, void* send_rec,
                    uint8_t* send_stem, uint32_t* perm, uint64_t* counts, void* stream, uint32_t cstride = 2,
-                   uint64_t meta0 = 0, uint64_t meta1 = 0);
+                   uint64_t meta0 = 0, uint64_t meta1 = 0, uint32_t own_rank = ROUTE_OWN_NONE,
+                   unsigned long long* hash_out = nullptr, unsigned long long* counts_host = nullptr);
 int eng_route_do_limit(Engine* c, uint32_t n, const void* recv_rec, const uint8_t* recv_stem, uint64_t recv_stem_bytes,
                        const uint64_t* src_stem_base, uint32_t n_shards, uint32_t n_rules, uint32_t rule_stride,
                        uint64_t* ret, uint64_t* stats, int isolate, void* stream);
@@ -189,10 +190,13 @@ int eng_snapshot_load(Engine* c, const void* host, uint64_t bytes);
 // rule (stats then holds n_src blocks of rule_stride x RL_NUM_STATS). The
 // packed results land in s[*slot].res (record order); b_done[*slot] marks
 // them complete and the reader must record consumed[*slot] once it has copied
-// them (the buffer is not reused before).
+// them (the buffer is not reused before). own (optional, own->n > 0): records
+// [own->lo, own->lo + own->n) are read in place from the source batch
+// (BatchDev::own; recv_rec holds nothing there).
 int eng_route_owner(Engine* c, uint32_t n, const Wire* recv_rec, const uint8_t* recv_stem, uint64_t recv_stem_bytes,
                     const uint64_t* src_stem_base, uint32_t n_src, uint32_t n_rules, uint32_t rule_stride,
-                    unsigned long long* stats, int isolate, hipEvent_t ready, uint32_t* slot);
+                    unsigned long long* stats, int isolate, hipEvent_t ready, uint32_t* slot,
+                    const OwnChunk* own = nullptr);
 
 // Record an error on the engine (its rl_last_error) and return code.
 int eng_fail(Engine* c, int code, const std::string& msg);

@@ -581,7 +581,8 @@ void scratch_free(Scratch& s) {
 // errw[NBUF + 2] (reported at rl_synchronize). counts = device memory.
 int eng_route_pack(Engine* c, const rl_batch* in, uint32_t n_shards, uint32_t src_rank, void* send_rec,
                    uint8_t* send_stem, uint32_t* perm, uint64_t* counts, void* stream, uint32_t cstride,
-                   uint64_t meta0, uint64_t meta1) {
+                   uint64_t meta0, uint64_t meta1, uint32_t own_rank, unsigned long long* hash_out,
+                   unsigned long long* counts_host) {
   if (!c || !in || !counts || (in->n && (!send_rec || !send_stem || !perm)))
     return set_err(c, RL_E_INVALID, "gpu: null argument");
   if (n_shards < 1 || n_shards > RL_MAX_SHARDS || src_rank >= n_shards)
@@ -604,17 +605,24 @@ int eng_route_pack(Engine* c, const rl_batch* in, uint32_t n_shards, uint32_t sr
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   BatchDev b = dev_view(c, in, c->cfg.max_stem_bytes);
   launch_route_pack(b, n_shards, src_rank, (Wire*)send_rec, send_stem, perm, (unsigned long long*)counts, c->rs, st,
-                    cstride, meta0, meta1);
+                    cstride, meta0, meta1, own_rank, hash_out, counts_host);
   HIPCHK(c, hipGetLastError());
   return RL_OK;
 }
 
 int eng_route_owner(Engine* c, uint32_t n, const Wire* recv_rec, const uint8_t* recv_stem, uint64_t recv_stem_bytes,
                     const uint64_t* src_stem_base, uint32_t n_src, uint32_t n_rules, uint32_t rule_stride,
-                    unsigned long long* stats, int isolate, hipEvent_t ready, uint32_t* slot) {
+                    unsigned long long* stats, int isolate, hipEvent_t ready, uint32_t* slot,
+                    const OwnChunk* own) {
   const uint32_t rules_eff = rule_stride ? n_src * rule_stride : n_rules;
-  if (!c || !src_stem_base || (n && (!recv_rec || !recv_stem)) || (rules_eff && !stats))
+  const bool has_own = own && own->n;
+  // (recv_stem may be null with no received stem bytes: an own chunk alone)
+  if (!c || !src_stem_base || (n && (!recv_rec || (!recv_stem && recv_stem_bytes))) || (rules_eff && !stats))
     return set_err(c, RL_E_INVALID, "gpu: null argument");
+  if (n && !recv_stem && !(has_own && own->n == n)) return set_err(c, RL_E_INVALID, "gpu: null argument");
+  if (has_own && ((uint64_t)own->lo + own->n > n || own->rank >= n_src || !own->idx || !own->hash || !own->stem ||
+                  ((uintptr_t)own->stem & 3u)))
+    return set_err(c, RL_E_INVALID, "gpu: bad own chunk");
   if (n_src < 1 || n_src > RL_MAX_SHARDS) return set_err(c, RL_E_INVALID, "gpu: n_shards must be 1..256");
   if (rule_stride && n_rules > rule_stride) return set_err(c, RL_E_INVALID, "gpu: n_rules exceeds the rule stride");
   // (the received stems are the caller's buffer: only 32-bit offsets bound them)
@@ -629,10 +637,12 @@ int eng_route_owner(Engine* c, uint32_t n, const Wire* recv_rec, const uint8_t* 
   HIPCHK(c, hipStreamWaitEvent(a, c->b_done[k], 0));
   HIPCHK(c, hipStreamWaitEvent(a, c->consumed[k], 0));
   if (ready) HIPCHK(c, hipStreamWaitEvent(a, ready, 0));
-  unsigned long long* hb = c->h_base + (size_t)k * RL_MAX_SHARDS;
-  HIPCHK(c, hipEventSynchronize(c->b_done[k]));  // (the pinned bases of buffer k's previous batch were read)
-  for (uint32_t j = 0; j < n_src; j++) hb[j] = src_stem_base[j];
-  HIPCHK(c, hipMemcpyAsync(sk.r_base, hb, (size_t)n_src * 8, hipMemcpyHostToDevice, a));
+  if (!(has_own && own->n == n)) {  // (an own chunk alone reads no received stems: no bases)
+    unsigned long long* hb = c->h_base + (size_t)k * RL_MAX_SHARDS;
+    HIPCHK(c, hipEventSynchronize(c->b_done[k]));  // (the pinned bases of buffer k's previous batch were read)
+    for (uint32_t j = 0; j < n_src; j++) hb[j] = src_stem_base[j];
+    HIPCHK(c, hipMemcpyAsync(sk.r_base, hb, (size_t)n_src * 8, hipMemcpyHostToDevice, a));
+  }
   // k_prepare reads the wire records in place (a malformed exchange fails
   // the batch's validation word)
   BatchDev b{};
@@ -648,6 +658,7 @@ int eng_route_owner(Engine* c, uint32_t n, const Wire* recv_rec, const uint8_t* 
   b.wbase = sk.r_base;
   b.n_src = n_src;
   b.rule_stride = rule_stride;
+  if (has_own) b.own = *own;
   OutDev o{nullptr, nullptr, nullptr, stats, isolate ? c->d_status : nullptr};
   const uint32_t kk = enqueue(c, b, o, 0, nullptr, true);
   HIPCHK(c, hipGetLastError());

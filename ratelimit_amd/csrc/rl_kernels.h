@@ -50,6 +50,27 @@ constexpr uint32_t STAT_LDS_RULES = 512;  // rules aggregated in LDS (== LDS_RUL
 constexpr uint32_t RUNS_GENERAL_LATE_BLOCKS = 8;  // k_late's exact-path workgroups (grid-stride over deferrals)
 
 struct Wire;
+// A routed owner batch's own chunk (the descriptors this rank owns of its own
+// slice), read in place from the source batch instead of as wire records and
+// copied stems: received positions [lo, lo + n) are the source's descriptors
+// idx[j - lo] (arrival order), with the stem hashes its partition computed.
+// Their records carry FLAG_SRC: their stem offsets index `stem`.
+struct OwnChunk {
+  uint32_t lo, n, rank, stem_total;  // (stem_total: the capacity; kernels refine it from off[src_n])
+  uint32_t src_n;    // the source batch's descriptors
+  uint32_t n_rules;  // the source batch's n_rules (a rule id at or above it fails alone)
+  const uint32_t* idx;
+  const unsigned long long* hash;
+  const uint8_t* stem;
+  const uint32_t* off;
+  const int64_t* now;
+  const uint32_t* req;
+  const uint8_t* unit;
+  const uint8_t* flags;
+  const uint32_t* limit;
+  const uint32_t* hits;
+  const uint32_t* rule;
+};
 struct BatchDev {
   uint32_t n, n_req, n_rules, stem_cap;
   uint32_t stem_total;  // bytes of packed stems (off[n]); reads stay below it
@@ -70,6 +91,7 @@ struct BatchDev {
   const Wire* wire;
   const unsigned long long* wbase;  // [n_src] chunk offset of each source in stem
   uint32_t n_src, rule_stride;
+  OwnChunk own;  // (n = 0: none)
 };
 
 // One descriptor, packed by k_prepare (arrival order) and gathered once into
@@ -268,12 +290,18 @@ void launch_unpack_prefixed(const rl_batch_prefixed& pb, const uint8_t* buf, uin
                             uint32_t* off, uint32_t* req, uint8_t* unit, uint8_t* flags, uint32_t* limit,
                             uint32_t* hits, uint32_t* rule, int64_t* now, uint32_t* err, hipStream_t st);
 // counts: cstride u64 per owner (records, stem bytes[, meta0, meta1]).
+// own_rank < n_shards: that owner's descriptors get a perm entry only (no
+// wire record, no stem bytes: its owner batch reads them in place,
+// BatchDev::own). hash_out: where the stem hashes go (null: the scratch's).
+constexpr uint32_t ROUTE_OWN_NONE = 0xFFFFFFFFu;
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
                        uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st,
-                       uint32_t cstride = 2, unsigned long long meta0 = 0, unsigned long long meta1 = 0);
+                       uint32_t cstride = 2, unsigned long long meta0 = 0, unsigned long long meta1 = 0,
+                       uint32_t own_rank = ROUTE_OWN_NONE, unsigned long long* hash_out = nullptr,
+                       unsigned long long* counts_host = nullptr);
 // The counts of a slice that failed on the host (zero records and bytes, meta words set).
 void launch_cnt_fill(unsigned long long* cnt, uint32_t n_peers, uint32_t cstride, unsigned long long meta0,
-                     unsigned long long meta1, hipStream_t st);
+                     unsigned long long meta1, hipStream_t st, unsigned long long* cnt_host = nullptr);
 // ret[0, n) = a failed record's packed result with rl_status `status`.
 void launch_route_fail(unsigned long long* ret, uint32_t n, uint32_t status, hipStream_t st);
 // src_err (optional): without o.status, a returned failure status sets its

@@ -77,15 +77,34 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   int64_t tnow = 0;
   unsigned long long whash = 0;
   bool layout_bad = false;
+  const bool own = b.wire && i - b.own.lo < b.own.n;  // (unsigned: lo <= i < lo + n)
+  uint32_t cap = b.stem_cap;
   if (i < b.n) {
-    if (b.wire) {
+    if (own) {
+      // this rank's own descriptor, read in place from its source batch (whose
+      // partition validated the request layout and computed the hash)
+      const uint32_t si = b.own.idx[i - b.own.lo];
+      const uint32_t sq = b.own.req[si];
+      s0 = b.own.off[si];
+      s1 = b.own.off[si + 1];
+      cap = b.own.stem_total;
+      u = b.own.unit[si];
+      fl = b.own.flags[si];
+      q = (b.own.rank << ROUTE_REQ_BITS) | sq;
+      tnow = b.own.now[sq];
+      const uint32_t r0 = b.own.rule[si] < b.own.n_rules ? b.own.rule[si] : 0xFFFFFFFFu;
+      rule = !b.rule_stride ? r0 : r0 >= b.rule_stride ? 0xFFFFFFFFu : b.own.rank * b.rule_stride + r0;
+      hits = b.own.hits[si];
+      limit = b.own.limit[si];
+      whash = b.own.hash[si];
+    } else if (b.wire) {
       const Wire w = b.wire[i];
       const uint32_t src = w.label >> ROUTE_REQ_BITS;
       const uint32_t wl = w.lu & 0xFFFFu;
       layout_bad = src >= b.n_src;
       s0 = (uint32_t)((layout_bad ? 0ull : b.wbase[src]) + w.off);
       s1 = s0 + wl;
-      if (i + 1 < b.n) {
+      if (i + 1 < b.n && !(i + 1 - b.own.lo < b.own.n)) {  // (the own chunk's records carry no wire stem)
         const Wire x = b.wire[i + 1];
         const uint32_t s2 = x.label >> ROUTE_REQ_BITS;
         layout_bad = layout_bad || s2 >= b.n_src || b.wbase[s2] + x.off != (unsigned long long)s1 || x.label < w.label;
@@ -111,7 +130,7 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
       layout_bad = (!b.now_desc && q >= b.n_req) || (i && b.req[i - 1] > q);
       tnow = b.now_desc ? b.now[i] : (q < b.n_req ? b.now[q] : 0);
     }
-    layout_bad = layout_bad || s1 < s0 || s1 > b.stem_cap;
+    layout_bad = layout_bad || s1 < s0 || s1 > cap;
   }
   // ---- per-request clock checks (whole-batch mode): now in [0, NOW_MAX], not before the last sweep
   if (!isolate) {
@@ -143,7 +162,7 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
     Rec r;
     r.hlo = (uint32_t)h;
     r.off = s0;
-    r.lu = len | (u << 16) | ((uint32_t)((fl & RL_FLAG_SHADOW) | (dstat ? FLAG_SKIP : 0u)) << 24);
+    r.lu = len | (u << 16) | ((uint32_t)((fl & RL_FLAG_SHADOW) | (dstat ? FLAG_SKIP : 0u) | (own ? FLAG_SRC : 0u)) << 24);
     r.rule = rule;
     r.req = q;
     r.now = (uint32_t)tnow;
@@ -549,11 +568,25 @@ struct Key {
   uint32_t len;
 };
 
+// The packed stems' byte counts, from the offsets (kernel-argument copies;
+// the host sets the capacity): a received batch's is set by the host, an own
+// chunk's comes from its source batch's offsets.
+__device__ inline void refine_totals(BatchDev& b) {
+  if (b.off) b.stem_total = b.off[b.n];
+  if (b.own.n) b.own.stem_total = b.own.off[b.own.src_n];
+}
+
 __device__ inline Key key_of(const BatchDev& b, const Rec& r) {
   Key k;
   k.len = rec_len(r);
-  k.st = stem_ref(b, r.off);
-  load_head(b.stem, r.off, k.len, k.h);
+  if ((rec_flags(r) & FLAG_SRC) && b.own.stem) {  // (a routed owner's own chunk: the source batch's stems)
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(b.own.stem);
+    k.st = StemRef{w + (r.off >> 2), r.off & 3u, ((b.own.stem_total + 3u) >> 2) - (r.off >> 2)};
+    load_head(b.own.stem, r.off, k.len, k.h);
+  } else {
+    k.st = stem_ref(b, r.off);
+    load_head(b.stem, r.off, k.len, k.h);
+  }
   return k;
 }
 
@@ -2771,7 +2804,7 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
   if (lo >= hi) return;
   // non-head positions (the second and later descriptors of a run)
   const uint32_t cnt = block_compact(lo, hi, s_list, &s_cnt, [&](uint32_t q) { return skeys[q - 1] == skeys[q]; });
-  if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
+  refine_totals(b);
   Rec* rec = const_cast<Rec*>(rec_s.rec);
 #pragma unroll 1
   for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
@@ -3415,7 +3448,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_split(BatchDev b, SRec rec_s,
   __shared__ uint32_t s_bad, s_lead;
   __shared__ SplitPlan s_plan;
   if (*err) return;
-  if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
+  refine_totals(b);
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t nd = *defer_n;
   Rec* rec = const_cast<Rec*>(rec_s.rec);
@@ -3628,7 +3661,7 @@ __device__ __attribute__((always_inline)) inline void unique_body(uint32_t blk, 
   const bool by_list = (uint64_t)nu * 4 < (uint64_t)b.n * RL_UNIQ_DENSE;  // (uniform) fewer than 75% keys seen once
   const uint32_t lo = blk * 256, hi = min(lo + 256, by_list ? nu : b.n);
   if (s_err || lo >= hi) return;
-  if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
+  refine_totals(b);
   uint32_t* ferr = P.isolate ? errs : err;
   const bool use_lds = !restore && b.n_rules <= LDS_RULES;
   stats_block_begin(use_lds, b.n_rules);
@@ -3912,7 +3945,7 @@ __device__ __attribute__((always_inline)) inline void runs_body(uint32_t blk, Ba
   __syncthreads();
   const uint32_t lo = blk * 256, hi = min(lo + 256, s_nr);
   if (s_err || lo >= hi) return;
-  if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
+  refine_totals(b);
   uint32_t* ferr = P.isolate ? errs : err;  // descriptor-level failures: soft word with statuses
   // the dup-run list, compacted once more (a large bucket's hot-key run left
   // to its fallback path is empty)
@@ -4230,7 +4263,7 @@ __device__ __attribute__((always_inline)) inline void general_body(uint32_t blk,
   }
   __syncthreads();
   if (s_err || (blk * 256 >= s_n && blk * 256 >= s_n1)) return;
-  if (b.off) b.stem_total = b.off[b.n];  // (routed owner batches: set by the host)
+  refine_totals(b);
   uint32_t* ferr = P.isolate ? errs : err;
   const bool use_lds = !restore && b.n_rules <= LDS_RULES;
   stats_block_begin(use_lds, b.n_rules);

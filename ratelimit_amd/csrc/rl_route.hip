@@ -98,7 +98,7 @@ __device__ inline bool rp_bad(const BatchDev& b, uint32_t i, uint32_t total) {
          s1 > total || q >= b.n_req;
 }
 
-__global__ __launch_bounds__(256) void k_rp_count(BatchDev b, uint32_t n_shards, uint32_t ntiles,
+__global__ __launch_bounds__(256) void k_rp_count(BatchDev b, uint32_t n_shards, uint32_t ntiles, uint32_t own_rank,
                                                   uint8_t* __restrict__ dest, unsigned long long* __restrict__ hash,
                                                   uint32_t* __restrict__ hist, uint32_t* err) {
   __shared__ uint32_t cr[RL_MAX_SHARDS], cb[RL_MAX_SHARDS];
@@ -122,6 +122,7 @@ __global__ __launch_bounds__(256) void k_rp_count(BatchDev b, uint32_t n_shards,
         const uint64_t h = hash_stem(b.hk, DwordReader{words + (s0 >> 2), nw - (s0 >> 2)}, s0 & 3u, len);
         d = owner_of(h, n_shards);
         hash[i] = h;
+        if (d == own_rank) len = 0;  // (the own chunk's stems stay in place: no bytes sent)
       }
       dest[i] = (uint8_t)d;
     }
@@ -152,19 +153,22 @@ __global__ __launch_bounds__(256) void k_rp_count(BatchDev b, uint32_t n_shards,
 // bytes); counts[cstride d], [cstride d + 1] = the totals (zero when the slice
 // is malformed, so the exchange stays well-formed); tot[d], tot[n_shards + d]
 // too.
-__global__ __launch_bounds__(1024) void k_rp_scan(uint32_t* __restrict__ hist, uint32_t n_shards, uint32_t ntiles,
+// (256 lanes: a workgroup of 1024 waits longer for a whole CU beside the
+// owner pipeline's kernels: 19 us in flight per batch at N = 1)
+__global__ __launch_bounds__(256) void k_rp_scan(uint32_t* __restrict__ hist, uint32_t n_shards, uint32_t ntiles,
                                                   unsigned long long* __restrict__ counts, uint32_t cstride,
                                                   unsigned long long meta0, unsigned long long meta1,
-                                                  uint32_t* __restrict__ tot, const uint32_t* err) {
+                                                  uint32_t* __restrict__ tot, const uint32_t* err,
+                                                  unsigned long long* counts_host) {
   __shared__ uint32_t tmp[32];
   const uint32_t d = blockIdx.x;
   uint32_t* rr = hist + (size_t)d * ntiles;
   uint32_t* rb = hist + ((size_t)n_shards + d) * ntiles;
   uint32_t ca = 0, cb = 0;
-  for (uint32_t base = 0; base < ntiles; base += 1024) {
+  for (uint32_t base = 0; base < ntiles; base += 256) {
     const uint32_t j = base + threadIdx.x;
     uint32_t a = j < ntiles ? rr[j] : 0u, bb = j < ntiles ? rb[j] : 0u, ta, tb;
-    block_excl2<16>(a, bb, ta, tb, tmp);
+    block_excl2<4>(a, bb, ta, tb, tmp);
     if (j < ntiles) {
       rr[j] = ca + a;
       rb[j] = cb + bb;
@@ -174,11 +178,14 @@ __global__ __launch_bounds__(1024) void k_rp_scan(uint32_t* __restrict__ hist, u
   }
   if (threadIdx.x == 0) {
     const bool ok = *err == 0;
-    counts[(size_t)cstride * d] = ok ? ca : 0u;
-    counts[(size_t)cstride * d + 1] = ok ? cb : 0u;
-    if (cstride >= 4) {  // (the in-library router's counts message: n_rules, flags)
-      counts[(size_t)cstride * d + 2] = meta0;
-      counts[(size_t)cstride * d + 3] = meta1;
+    for (unsigned long long* c : {counts, counts_host}) {  // (the host's copy: stores to page-locked memory)
+      if (!c) continue;
+      c[(size_t)cstride * d] = ok ? ca : 0u;
+      c[(size_t)cstride * d + 1] = ok ? cb : 0u;
+      if (cstride >= 4) {  // (the in-library router's counts message: n_rules, flags)
+        c[(size_t)cstride * d + 2] = meta0;
+        c[(size_t)cstride * d + 3] = meta1;
+      }
     }
     tot[d] = ca;
     tot[n_shards + d] = cb;
@@ -186,6 +193,7 @@ __global__ __launch_bounds__(1024) void k_rp_scan(uint32_t* __restrict__ hist, u
 }
 
 __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, uint32_t ntiles, uint32_t src_rank,
+                                                 uint32_t own_rank,
                                                  const uint8_t* __restrict__ dest,
                                                  const unsigned long long* __restrict__ hash,
                                                  const uint32_t* __restrict__ hist,
@@ -234,7 +242,7 @@ __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, 
     const uint32_t i = i0 + t * 64 + lane;
     const bool valid = i < b.n;
     const uint32_t d = valid ? dest[i] : 0xFFFFu;
-    const uint32_t len = valid ? b.off[i + 1] - b.off[i] : 0u;
+    const uint32_t len = valid && d != own_rank ? b.off[i + 1] - b.off[i] : 0u;
     uint64_t todo = __ballot(valid);
     uint32_t r = 0, bp = 0;
     while (todo) {
@@ -295,6 +303,10 @@ __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, 
     if (i >= b.n) continue;
     const uint32_t d = my_d[t], len = my_len[t];
     const uint32_t j = gr[d] + wr[w][d] + my_r[t];      // record index in the send buffer
+    if (d == own_rank) {  // read in place by this rank's owner batch (BatchDev::own): its position only
+      perm[j] = i;
+      continue;
+    }
     const uint32_t local = gb[d] + wb[w][d] + my_b[t];  // byte offset inside owner d's chunk
     const uint32_t q = b.req[i];
     Wire x;
@@ -402,13 +414,16 @@ __global__ __launch_bounds__(256) void k_route_fail(unsigned long long* __restri
 // The counts message of a slice that failed on the host: no records, no
 // bytes, and the sender's meta words.
 __global__ void k_cnt_fill(unsigned long long* cnt, uint32_t n_peers, uint32_t cstride, unsigned long long meta0,
-                           unsigned long long meta1) {
+                           unsigned long long meta1, unsigned long long* cnt_host) {
   for (uint32_t p = threadIdx.x; p < n_peers; p += blockDim.x) {
-    unsigned long long* c = cnt + (size_t)cstride * p;
-    c[0] = c[1] = 0;
-    if (cstride >= 4) {
-      c[2] = meta0;
-      c[3] = meta1;
+    for (unsigned long long* base : {cnt, cnt_host}) {
+      if (!base) continue;
+      unsigned long long* c = base + (size_t)cstride * p;
+      c[0] = c[1] = 0;
+      if (cstride >= 4) {
+        c[2] = meta0;
+        c[3] = meta1;
+      }
     }
   }
 }
@@ -425,19 +440,21 @@ void launch_route_fail(unsigned long long* ret, uint32_t n, uint32_t status, hip
 }
 
 void launch_cnt_fill(unsigned long long* cnt, uint32_t n_peers, uint32_t cstride, unsigned long long meta0,
-                     unsigned long long meta1, hipStream_t st) {
-  k_cnt_fill<<<1, 256, 0, st>>>(cnt, n_peers, cstride, meta0, meta1);
+                     unsigned long long meta1, hipStream_t st, unsigned long long* cnt_host) {
+  k_cnt_fill<<<1, 256, 0, st>>>(cnt, n_peers, cstride, meta0, meta1, cnt_host);
 }
 
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
                        uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st, uint32_t cstride,
-                       unsigned long long meta0, unsigned long long meta1) {
+                       unsigned long long meta0, unsigned long long meta1, uint32_t own_rank,
+                       unsigned long long* hash_out, unsigned long long* counts_host) {
   const uint32_t ntiles = b.n ? cdiv(b.n, RP_TILE) : 0u;
-  if (b.n) k_rp_count<<<ntiles, 256, 0, st>>>(b, n_shards, ntiles, s.route_dest, s.route_hash, s.route_hist, s.err);
-  k_rp_scan<<<n_shards, 1024, 0, st>>>(s.route_hist, n_shards, ntiles, counts, cstride, meta0, meta1, s.route_start,
-                                       s.err);
+  unsigned long long* hash = hash_out ? hash_out : s.route_hash;
+  if (b.n) k_rp_count<<<ntiles, 256, 0, st>>>(b, n_shards, ntiles, own_rank, s.route_dest, hash, s.route_hist, s.err);
+  k_rp_scan<<<n_shards, 256, 0, st>>>(s.route_hist, n_shards, ntiles, counts, cstride, meta0, meta1, s.route_start,
+                                       s.err, counts_host);
   if (b.n)
-    k_rp_pack<<<ntiles, 256, 0, st>>>(b, n_shards, ntiles, src_rank, s.route_dest, s.route_hash, s.route_hist,
+    k_rp_pack<<<ntiles, 256, 0, st>>>(b, n_shards, ntiles, src_rank, own_rank, s.route_dest, hash, s.route_hist,
                                       s.route_start, out,
                                       out_stem, perm, s.err);
 }

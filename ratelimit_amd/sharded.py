@@ -48,6 +48,7 @@ Rank r's slice precedes rank r+1's in the global order. An error on any rank
 raises RedisError on every rank at `finish`, like the reference's backend
 failure path (driver_impl.go:60-64); `do_limit` = submit + finish.
 """
+import collections
 import contextlib
 import time
 from typing import List, Optional
@@ -84,8 +85,10 @@ class LibRouter:
     rank's requests. A submit completes the previous batch (the library never
     waits for work it just issued); dev_out is final after finish(), which
     every rank calls together: it completes the last batch and raises
-    RedisError if one failed on this rank. Tensors handed to submit must stay
-    alive until the next submit (inputs) or finish (outputs).
+    RedisError if one failed on this rank. The library reads a batch's inputs
+    until RL_ROUTED_INFLIGHT later submits have returned (its own chunk is read
+    in place): submit holds them that long, and finish releases them. Output
+    tensors must stay alive until finish.
     """
 
     def __init__(self, backend, world: int, rank: int, uid: np.ndarray):
@@ -100,15 +103,20 @@ class LibRouter:
         # default stream has the NULL handle, which the library reads as
         # "inputs complete at the call"
         self.stream = torch.cuda.Stream(self.device)
+        self._held = collections.deque()  # the inputs of the batches the library may still read
 
     def submit(self, dev_in: dict, n: int, n_requests: int, n_rules: int, dev_out: dict):
         b = abi.make_batch_struct(dev_in, n, n_requests, n_rules)
         r = abi.make_result_struct(dev_out)
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         check(self.be.ctx, lib().rl_do_limit_routed_async(self.be.ctx, b, r, self.stream.cuda_stream))
+        self._held.append(dev_in)
+        while len(self._held) > abi.RL_ROUTED_INFLIGHT:
+            self._held.popleft()
 
     def finish(self):
         self.be.synchronize()
+        self._held.clear()
 
     def do_limit(self, dev_in: dict, n: int, n_requests: int, n_rules: int, dev_out: dict):
         self.submit(dev_in, n, n_requests, n_rules, dev_out)
