@@ -433,7 +433,8 @@ int rl_route_scatter(rl_ctx* ctx, uint32_t n, const uint32_t* perm, const uint64
  * sequential INCRBY contract is kept in). Device arrays; the batch starts
  * after the work already on `stream` (NULL: inputs complete at the call). A
  * call enqueues its batch's partition and counts exchange and completes the
- * PREVIOUS batch, so the host never waits for work it just issued. The
+ * batch RL_ROUTED_LAG calls back, so the host never waits for work it just
+ * issued and that many owner pipelines stay queued on the GPU. The
  * descriptors a rank owns of its own slice are read in place by its owner
  * batch (no copy): a batch's inputs may be reused once RL_ROUTED_INFLIGHT
  * later calls have returned, or after rl_synchronize; its outputs are read
@@ -453,12 +454,13 @@ int rl_route_scatter(rl_ctx* ctx, uint32_t n, const uint32_t* perm, const uint64
  * call). Replaces the Redis cluster client's key-slot routing inside one
  * service process (src/redis/driver_impl.go:108-126).
  * On a routed ctx rl_synchronize, rl_sweep, rl_restore and rl_snapshot_save /
- * _load first complete the pending batch, so they are collective like the
+ * _load first complete the pending batches, so they are collective like the
  * batches. The read-only getters rl_table_info_get and rl_local_cache_info_get
- * are not: they see every batch but the pending one, and a rank may call them
- * alone (e.g. for its gauges). */
+ * are not: they see every batch but the pending ones (the last RL_ROUTED_LAG
+ * submitted), and a rank may call them alone (e.g. for its gauges). */
 #define RL_COMM_ID_BYTES 128u
 #define RL_ROUTED_INFLIGHT 6u  /* routed batches in flight (the input-reuse distance above) */
+#define RL_ROUTED_LAG 2u       /* calls between a routed batch's partition and its owner pipeline */
 int rl_comm_unique_id(uint8_t* id);
 int rl_comm_loopback_id(uint8_t* id);
 int rl_comm_init(rl_ctx* ctx, uint32_t world, uint32_t rank, const uint8_t* id);

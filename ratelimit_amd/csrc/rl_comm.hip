@@ -22,10 +22,10 @@
 //                2); scatter to arrival order, sum the stats blocks.
 //
 // A call enqueues its batch's partition and counts exchange and then
-// completes the PREVIOUS batch (whose counts have had a whole call to arrive):
-// the host never waits for work it just issued, batch t's partition runs
-// beside batch t-1's owner pipeline, and rl_synchronize completes the last
-// one. RSLOTS batches may be in flight.
+// completes the batch ROUTE_LAG calls back (whose counts have had that many
+// calls to arrive): the host never waits for work it just issued, batch t's
+// partition runs beside the owner pipelines of batches t-1 .. t-LAG, and
+// rl_synchronize completes the pending ones. RSLOTS batches may be in flight.
 //
 // Failures never break the exchange. A slice the host rejects (sizes, null
 // outputs, a bad n_rules) sends zero counts with the FAILED flag and still
@@ -61,6 +61,12 @@ namespace {
 // remaining ~150 us wait per step for the counts is the partition waiting for
 // GPU capacity beside the owner pipelines (RL_DEBUG_ROUTE_TIMING).
 constexpr uint32_t RSLOTS = RL_ROUTED_INFLIGHT;
+// A call completes the batch LAG calls back (its counts have had LAG calls to
+// arrive), so LAG owner pipelines are queued ahead of the one being set up and
+// the GPU never drains while the host waits for a partition. LAG < RSLOTS (a
+// slot is reused RSLOTS calls later). RL_DEBUG_ROUTE_LAG overrides it (A/B).
+constexpr uint32_t ROUTE_LAG = RL_ROUTED_LAG;
+static_assert(ROUTE_LAG >= 1 && ROUTE_LAG < RSLOTS, "lag within the slots in flight");
 
 // The counts message: CNT_W u64 per peer.
 constexpr uint32_t CNT_W = 4;                 // records, stem bytes, n_rules, flags
@@ -122,7 +128,9 @@ struct CommRouter {
   hipEvent_t in_ready = nullptr;
   CommSlot slot[RSLOTS];
   uint32_t next = 0;
-  int pending = -1;                     // slot whose second half is still to run
+  uint32_t lag = ROUTE_LAG;             // second halves run this many calls after their first
+  uint32_t pend[RSLOTS] = {};           // slots whose second half is still to run, oldest first
+  uint32_t n_pend = 0;
   unsigned long long* h_cnt = nullptr;  // pinned [RSLOTS][2 x CNT_W x world]
   unsigned long long* d_hcnt = nullptr;  // h_cnt as the device sees it (world 1: the partition stores the counts there)
   std::vector<uint64_t> base;           // received chunk offsets in recv_stem (host)
@@ -686,6 +694,8 @@ CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t*
   r->alias = world == 1 && !getenv("RL_DEBUG_ROUTE_NOALIAS");
   r->own = !getenv("RL_DEBUG_ROUTE_NOOWN");  // (A/B knob: the own chunk as wire records and copied stems)
   r->timing = getenv("RL_DEBUG_ROUTE_TIMING") != nullptr;
+  if (const char* lg = getenv("RL_DEBUG_ROUTE_LAG"))
+    r->lag = std::max<uint32_t>(1, std::min<uint32_t>(RSLOTS - 1, (uint32_t)atoi(lg)));
   if (const char* pm = getenv("RL_DEBUG_OWNER_PART"))
     r->part_max = std::max<uint32_t>(1, std::min<uint32_t>(g.max_batch, (uint32_t)atoi(pm)));
   r->tr.reset(loopback_id(id) ? loopback_join(id, world, rank, err) : rccl_join(id, world, rank, r->dev, err));
@@ -753,9 +763,10 @@ void comm_destroy(CommRouter* r) {
 int comm_synchronize(CommRouter* r, Engine* e) {
   if (r->broken) return eng_fail(e, r->broken, r->broken_msg);
   CHK_HIP(e, hipSetDevice(r->dev));
-  if (r->pending >= 0) {
-    const uint32_t p = (uint32_t)r->pending;
-    r->pending = -1;
+  while (r->n_pend) {  // (oldest first: the order every rank runs its exchanges in)
+    const uint32_t p = r->pend[0];
+    std::copy(r->pend + 1, r->pend + r->n_pend, r->pend);
+    r->n_pend--;
     const int rc = second_half(r, e, r->slot[p], p);
     if (rc) return rc;
   }
@@ -813,14 +824,15 @@ int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, 
   int rc = first_half(r, e, S, s, in, caller, hostrc);
   r->t_first += now_s() - t0;
   if (rc) return rc;
-  // the previous batch: its counts had a whole call to arrive
-  if (r->pending >= 0) {
-    const uint32_t p = (uint32_t)r->pending;
-    r->pending = -1;
+  r->pend[r->n_pend++] = s;
+  // the batch `lag` calls back: its counts had that many calls to arrive
+  if (r->n_pend > r->lag) {
+    const uint32_t p = r->pend[0];
+    std::copy(r->pend + 1, r->pend + r->n_pend, r->pend);
+    r->n_pend--;
     rc = second_half(r, e, r->slot[p], p);
     if (rc) return rc;
   }
-  r->pending = (int)s;
   return RL_OK;
 }
 
