@@ -459,8 +459,12 @@ int rl_route_scatter(rl_ctx* ctx, uint32_t n, const uint32_t* perm, const uint64
  * are not: they see every batch but the pending ones (the last RL_ROUTED_LAG
  * submitted), and a rank may call them alone (e.g. for its gauges). */
 #define RL_COMM_ID_BYTES 128u
+#ifndef RL_ROUTED_INFLIGHT       /* (overridable only for A/B builds of the library) */
 #define RL_ROUTED_INFLIGHT 6u  /* routed batches in flight (the input-reuse distance above) */
-#define RL_ROUTED_LAG 2u       /* calls between a routed batch's partition and its owner pipeline */
+#endif
+#ifndef RL_ROUTED_LAG
+#define RL_ROUTED_LAG 3u       /* calls between a routed batch's partition and its owner pipeline */
+#endif
 int rl_comm_unique_id(uint8_t* id);
 int rl_comm_loopback_id(uint8_t* id);
 int rl_comm_init(rl_ctx* ctx, uint32_t world, uint32_t rank, const uint8_t* id);

@@ -145,7 +145,7 @@ RESULT_DTYPES = {"code": np.uint8, "limit_remaining": np.uint32, "reset_s": np.u
 ABI_VERSION = 4
 RL_COMM_ID_BYTES = 128  # include/ratelimit_hip.h
 RL_ROUTED_INFLIGHT = 6  # include/ratelimit_hip.h (routed batches in flight: the input-reuse distance)
-RL_ROUTED_LAG = 2  # include/ratelimit_hip.h (calls between a routed batch's partition and its owner pipeline)
+RL_ROUTED_LAG = 3  # include/ratelimit_hip.h (calls between a routed batch's partition and its owner pipeline)
 
 
 def make_batch_struct(arrays, n, n_requests, n_rules):

@@ -144,7 +144,7 @@ struct CommRouter {
   std::string broken_msg;
   // host seconds per phase (printed at destroy when RL_DEBUG_ROUTE_TIMING is set)
   bool timing = false;
-  double t_first = 0, t_wait_counts = 0, t_owner = 0, t_second = 0;
+  double t_first = 0, t_wait_counts = 0, t_owner = 0, t_second = 0, t_slot = 0, t_call = 0;
   uint64_t n_steps = 0;
 };
 
@@ -741,10 +741,11 @@ const char* comm_kind(const CommRouter* r) { return r && r->tr ? r->tr->kind() :
 void comm_destroy(CommRouter* r) {
   if (!r) return;
   if (r->timing && r->n_steps)
-    fprintf(stderr, "{\"route_host_us\": {\"first_half\": %.1f, \"wait_counts\": %.1f, \"owner_enqueue\": %.1f, "
-                    "\"second_half\": %.1f, \"batches\": %llu}}\n",
-            r->t_first / r->n_steps * 1e6, r->t_wait_counts / r->n_steps * 1e6, r->t_owner / r->n_steps * 1e6,
-            r->t_second / r->n_steps * 1e6, (unsigned long long)r->n_steps);
+    fprintf(stderr, "{\"route_host_us\": {\"call\": %.1f, \"slot_wait\": %.1f, \"first_half\": %.1f, "
+                    "\"wait_counts\": %.1f, \"owner_enqueue\": %.1f, \"second_half\": %.1f, \"batches\": %llu}}\n",
+            r->t_call / r->n_steps * 1e6, r->t_slot / r->n_steps * 1e6, r->t_first / r->n_steps * 1e6,
+            r->t_wait_counts / r->n_steps * 1e6, r->t_owner / r->n_steps * 1e6, r->t_second / r->n_steps * 1e6,
+            (unsigned long long)r->n_steps);
   (void)hipSetDevice(r->dev);
   for (hipStream_t st : {r->cs, r->fwd, r->ret})
     if (st) (void)hipStreamSynchronize(st);
@@ -796,11 +797,13 @@ int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, 
   const uint32_t s = r->next;
   r->next = (s + 1) % RSLOTS;
   CommSlot& S = r->slot[s];
+  const double tc = now_s();
   // the slot's previous batch (RSLOTS calls ago) is complete: its owner part
   // read that slice's own chunk in place, so a caller may reuse a batch's
   // inputs once RSLOTS later calls have returned (long done by then: this
   // wait does not bind)
   CHK_HIP(e, hipEventSynchronize(S.done));
+  r->t_slot += now_s() - tc;
   S.out = *out;
   S.n = n;
   S.n_rules = nr;
@@ -833,6 +836,7 @@ int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, 
     rc = second_half(r, e, r->slot[p], p);
     if (rc) return rc;
   }
+  r->t_call += now_s() - tc;
   return RL_OK;
 }
 

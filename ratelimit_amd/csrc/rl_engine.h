@@ -73,9 +73,9 @@ struct Engine {
   bool host_time = false;
   double ht[8] = {};
   uint64_t ht_n = 0;
-  hipEvent_t ct_ev[2][64] = {};
+  hipEvent_t ct_ev[3][64] = {};  // copy start, copy end, before the slot wait
   uint32_t ct_n = 0;
-  double ct_ms = 0;
+  double ct_ms = 0, ct_wait_ms = 0, ct_gap_ms = 0;
   uint64_t ct_count = 0;
   uint8_t* arena = nullptr;
   uint8_t* arena2 = nullptr;  // compaction target (rl_sweep), swapped with arena

@@ -397,7 +397,8 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   c->copy_time = getenv("RL_DEBUG_COPYTIME") != nullptr;
   c->host_time = getenv("RL_DEBUG_HOSTTIME") != nullptr;
   for (uint32_t k = 0; c->copy_time && k < 64; k++)
-    ok = ok && hipEventCreate(&c->ct_ev[0][k]) == hipSuccess && hipEventCreate(&c->ct_ev[1][k]) == hipSuccess;
+    ok = ok && hipEventCreate(&c->ct_ev[0][k]) == hipSuccess && hipEventCreate(&c->ct_ev[1][k]) == hipSuccess &&
+         hipEventCreate(&c->ct_ev[2][k]) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_base, (size_t)NBUF * RL_MAX_SHARDS * 8) == hipSuccess;
   for (uint32_t k = 0; k < NBUF; k++)  // per buffer: a batch's k_finish overlaps the next batch's table kernels
     ok = ok && dalloc(&c->s[k].stripes, (size_t)STAT_STRIPES * STAT_LDS_RULES * RL_NUM_STATS) == hipSuccess;
@@ -473,10 +474,11 @@ void eng_destroy(Engine* c) {
     (void)hipDeviceSynchronize();
     copy_time_fold(c, true);
     if (c->ct_count)
-      fprintf(stderr, "RL_DEBUG_COPYTIME: %llu input copies, %.4f ms each\n", (unsigned long long)c->ct_count,
-              c->ct_ms / c->ct_count);
+      fprintf(stderr, "RL_DEBUG_COPYTIME: %llu input copies, %.4f ms each, slot wait %.4f ms, gap after the previous "
+              "copy %.4f ms\n", (unsigned long long)c->ct_count, c->ct_ms / c->ct_count, c->ct_wait_ms / c->ct_count,
+              c->ct_gap_ms / c->ct_count);
     for (uint32_t k = 0; k < 64; k++)
-      for (int j = 0; j < 2; j++)
+      for (int j = 0; j < 3; j++)
         if (c->ct_ev[j][k]) (void)hipEventDestroy(c->ct_ev[j][k]);
   }
   if (c->hs_ready) {
@@ -750,6 +752,10 @@ void copy_time_fold(Engine* c, bool all) {
         hipEventElapsedTime(&ms, c->ct_ev[0][k % 64], c->ct_ev[1][k % 64]) == hipSuccess) {
       c->ct_ms += ms;
       c->ct_count++;
+      float w = 0, g = 0;
+      if (hipEventElapsedTime(&w, c->ct_ev[2][k % 64], c->ct_ev[0][k % 64]) == hipSuccess) c->ct_wait_ms += w;
+      if (k > lo && hipEventElapsedTime(&g, c->ct_ev[1][(k - 1) % 64], c->ct_ev[0][k % 64]) == hipSuccess)
+        c->ct_gap_ms += g;
     }
   }
   if (all) c->ct_n = 0;
@@ -812,6 +818,22 @@ int ensure_host_slots(Engine* c) {
   return RL_OK;
 }
 
+// The copy stream's order after the slot's previous batch (its outputs
+// drained). A cross-queue wait in front of an SDMA copy made hipMemcpyAsync
+// block the submitting thread for ~0.3 ms on some boxes, and the link idled
+// while the host caught up (0.1 ms between 0.58-ms copies): the host checks
+// the event instead (RL_COPY_STREAM_WAIT=1: the stream wait, for A/B). The
+// slot is four batches back, so the host rarely waits at all.
+hipError_t slot_drained(Engine* c, HostSlot& h, hipStream_t up) {
+  static const bool stream_wait = getenv("RL_COPY_STREAM_WAIT") != nullptr;
+  if (stream_wait) return hipStreamWaitEvent(up, h.out_done, 0);
+  const hipError_t q = hipEventQuery(h.out_done);
+  if (q == hipSuccess) return hipSuccess;
+  if (q != hipErrorNotReady) return q;
+  (void)c;
+  return hipEventSynchronize(h.out_done);
+}
+
 // Enqueue the staged batch d (device pointers; its inputs complete at
 // h.in_done) and its outputs' copies back into *out on the d2h stream.
 int host_slot_run(Engine* c, HostSlot& h, const rl_batch& d, uint64_t nb, rl_result* out) {
@@ -870,7 +892,7 @@ int eng_do_limit_host_async(Engine* c, const rl_batch* in, rl_result* out) {
   c->hnext = (j + 1) % NBUF;
   HostSlot& h = c->hs[j];
   hipStream_t up = c->h2d;
-  HIPCHK(c, hipStreamWaitEvent(up, h.out_done, 0));  // the slot's previous batch is drained
+  HIPCHK(c, slot_drained(c, h, up));  // the slot's previous batch is drained
   if (nb) HIPCHK(c, hipMemcpyAsync(h.stem, in->stem_bytes, nb, hipMemcpyHostToDevice, up));
   HIPCHK(c, hipMemcpyAsync(h.off, in->stem_off, (n + 1) * 4ull, hipMemcpyHostToDevice, up));
   if (nq) HIPCHK(c, hipMemcpyAsync(h.now, in->now, nq * 8ull, hipMemcpyHostToDevice, up));
@@ -944,7 +966,7 @@ int eng_do_limit_compact_async(Engine* c, const rl_batch_compact* in, rl_result*
   }
   c->hnext = (j + 1) % NBUF;
   hipStream_t up = c->h2d;
-  HIPCHK(c, hipStreamWaitEvent(up, h.out_done, 0));  // the slot's previous batch is drained
+  HIPCHK(c, slot_drained(c, h, up));  // the slot's previous batch is drained
   if (B) HIPCHK(c, hipMemcpyAsync(h.cbuf, in->buf, B, hipMemcpyHostToDevice, up));
   HIPCHK(c, hipEventRecord(h.in_done, up));
   // unpacked on the batch's pipeline stream, so the copy stream runs the
@@ -1026,7 +1048,8 @@ int eng_do_limit_prefixed_async(Engine* c, const rl_batch_prefixed* in, rl_resul
   c->hnext = (j + 1) % NBUF;
   hipStream_t up = c->h2d;
   const double w1 = c->host_time ? wall_s() : 0;
-  HIPCHK(c, hipStreamWaitEvent(up, h.out_done, 0));  // the slot's previous batch is drained
+  if (c->copy_time) HIPCHK(c, hipEventRecord(c->ct_ev[2][c->ct_n % 64], up));
+  HIPCHK(c, slot_drained(c, h, up));  // the slot's previous batch is drained
   if (c->copy_time) {
     copy_time_fold(c, false);
     HIPCHK(c, hipEventRecord(c->ct_ev[0][c->ct_n % 64], up));

@@ -472,8 +472,10 @@ void launch_to_host(const ToHost& c, hipStream_t st) {
   uint64_t most = 0;
   for (uint32_t k = 0; k < c.n; k++) most = c.bytes[k] > most ? c.bytes[k] : most;
   if (!most) return;
+  static const uint32_t cap = getenv("RL_D2H_BLOCKS") ? (uint32_t)atoi(getenv("RL_D2H_BLOCKS")) : 1024u;  // (A/B knob)
   const uint64_t g = (most / 16 + 255) / 256;
-  k_to_host<<<(uint32_t)(g < 1024 ? (g ? g : 1) : 1024), 256, 0, st>>>(c);
+  const uint32_t gmax = cap ? cap : 1u;
+  k_to_host<<<(uint32_t)(g < gmax ? (g ? g : 1) : gmax), 256, 0, st>>>(c);
 }
 
 void launch_unpack_prefixed(const rl_batch_prefixed& pb, const uint8_t* buf, uint32_t t0, uint32_t t1, uint8_t* stem,
