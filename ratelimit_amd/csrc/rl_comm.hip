@@ -145,7 +145,8 @@ struct CommRouter {
   // host seconds per phase (printed at destroy when RL_DEBUG_ROUTE_TIMING is set)
   bool timing = false;
   double t_first = 0, t_wait_counts = 0, t_owner = 0, t_second = 0, t_slot = 0, t_call = 0;
-  uint64_t n_steps = 0;
+  uint64_t n_steps = 0, n_slot_busy = 0, n_lat = 0;
+  double t_enq[RSLOTS] = {}, t_lat = 0;  // host time of each slot's owner enqueue; enqueue -> found done
 };
 
 inline double now_s() {
@@ -499,7 +500,10 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
     r->so_b[p + 1] = r->so_b[p] + h[CNT_W * p + 1];
     r->ro_r[p + 1] = r->ro_r[p] + hr[CNT_W * p];
   }
-  CHK_HIP(e, hipStreamWaitEvent(r->fwd, S.packed, 0));
+  // world 1: nothing crosses the fwd stream; the owner waits on the
+  // partition itself (a wait routed through fwd queued behind whatever shares
+  // its hardware queue)
+  if (!r->alias) CHK_HIP(e, hipStreamWaitEvent(r->fwd, S.packed, 0));
   if (!r->alias) CHK_HIP(e, grow(r, S, n_recv, b_recv, 1));
   // (world 1: the partition is the received batch)
   const Wire* recv_rec = r->alias ? S.send_rec : S.recv_rec;
@@ -524,7 +528,8 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
       CHK_HIP(e, hipMemcpyAsync(S.recv_stem + r->base[me], S.send_stem + r->so_b[me], h[CNT_W * me + 1],
                                 hipMemcpyDeviceToDevice, r->fwd));
   }
-  CHK_HIP(e, hipEventRecord(S.sent, r->fwd));
+  if (!r->alias) CHK_HIP(e, hipEventRecord(S.sent, r->fwd));
+  hipEvent_t const sent = r->alias ? S.packed : S.sent;  // (the received records are ready)
   // the owner pipeline, in parts of at most max_batch records. A part ends on
   // a request boundary (a request's descriptors check the local cache before
   // any of them sets it, fixed_cache_impl.go:50-66 then :100-109), so more
@@ -559,9 +564,31 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
   const bool direct = r->alias && parts == 1 && !owner_fail;
   S.k.assign(parts, 0);
   const size_t blk = (size_t)W * m;  // one part's per-source stats
+  // this rank's outputs (arrival order): the scatter writes the records that
+  // come back from owners; the own chunk's owner batch answers its own in
+  // place (k_finish, OwnChunk outputs), and at world 1 with one part its stats
+  // land in the output directly (no per-source sum)
+  const bool out_ok = !S.err && !(n && n_send != n);  // (else perm was never written: nothing is scattered)
+  const rl_result& out = S.out;
+  const uint32_t mine = S.n_rules * RL_NUM_STATS;  // (<= m: M is the largest n_rules sent)
+  OutDev o{out.code, out.limit_remaining, out.reset_s, (unsigned long long*)out.stats, out.status};
+  if (S.io.host) o = OutDev{S.h_code, S.h_rem, S.h_reset, nullptr, out.status ? S.h_status : nullptr};
+  unsigned long long* stats_out = S.io.stats_host ? S.io_stats : (unsigned long long*)out.stats;
+  uint32_t* src_err = out.status ? nullptr : e->errw + NBUF + 2;
+  const bool own_inplace = r->own && out_ok && !owner_fail;
+  const bool stats_direct = direct && out_ok && W == 1 && stats_out && mine == m && m;
+  // the own chunk's records in send order (answered in place: not scattered)
+  const uint32_t ol = own_inplace ? (uint32_t)r->so_r[me] : 0u, oh = own_inplace ? (uint32_t)r->so_r[me + 1] : 0u;
+  // world 1, one part, everything answered in place and nothing for the host
+  // to copy: the batch ends with its owner pipeline, and its completion is
+  // recorded on that pipeline's stream (the return stream shares a hardware
+  // queue with another pipeline stream: a marker there waits behind that
+  // stream's later batches)
+  const bool on_pipe = direct && !S.io.host && !S.io.stats_host &&
+                       (!out_ok || ((ol == 0 && oh >= n) && (stats_direct || !mine || !stats_out)));
   const double t2 = now_s();
   if (owner_fail) {
-    CHK_HIP(e, hipStreamWaitEvent(r->ret, S.sent, 0));
+    CHK_HIP(e, hipStreamWaitEvent(r->ret, sent, 0));
     launch_route_fail(ret_send, (uint32_t)n_recv, (uint32_t)owner_fail, r->ret);
     if (blk) CHK_HIP(e, hipMemsetAsync(S.ostats, 0, blk * 8, r->ret));
   } else {
@@ -589,13 +616,22 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
         oc.limit = sb.limit;
         oc.hits = sb.hits;
         oc.rule = sb.rule_id;
+        if (own_inplace) {
+          oc.code = o.code;
+          oc.rem = o.rem;
+          oc.reset = o.reset;
+          oc.status = o.status;
+          oc.src_err = src_err;
+        }
       }
       const int rc = eng_route_owner(e, (uint32_t)(b - a), recv_rec + a, recv_stem, b_recv, r->base.data(), W,
-                                     (uint32_t)M, (uint32_t)M, S.ostats + q * blk, iso ? 1 : 0, S.sent, &S.k[q], &oc);
+                                     (uint32_t)M, (uint32_t)M, stats_direct ? stats_out : S.ostats + q * blk,
+                                     iso ? 1 : 0, sent, &S.k[q], &oc);
       if (rc) return breaks(r, e, rc, eng_last_error(e));  // (argument checks only: the sizes were checked above)
       // its packed results, before a later part can take the same engine buffer
       const uint32_t k = S.k[q];
       CHK_HIP(e, hipSetDevice(r->dev));
+      if (on_pipe) break;
       CHK_HIP(e, hipStreamWaitEvent(r->ret, e->b_done[k], 0));
       if (direct) break;
       launch_route_ret(e->s[k].res, (uint32_t)(b - a), e->s[k].errb, ret_send + a, r->ret);
@@ -604,6 +640,7 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
   }
   const double t3 = now_s();
   r->t_owner += t3 - t2;
+  r->t_enq[s] = t3;
   // results and per-source stats back to their sources
   if (parts > 1 && m && !owner_fail) launch_stats_sum(S.ostats, parts, (uint32_t)blk, S.ostats, r->ret);
   const unsigned long long* stats_in = S.ostats;  // (world 1: this rank's block is the owner's)
@@ -619,7 +656,7 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
     }
     const int g = run_group(r, e, 2, r->ret);
     if (g) return g;
-    if (h[CNT_W * me])
+    if (h[CNT_W * me] && !own_inplace)
       CHK_HIP(e, hipMemcpyAsync(S.back + r->so_r[me], S.ret_send + r->ro_r[me], h[CNT_W * me] * 8,
                                 hipMemcpyDeviceToDevice, r->ret));
     if (m)
@@ -627,25 +664,24 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
                                 hipMemcpyDeviceToDevice, r->ret));
     stats_in = S.stats_stage;
   }
+  if (direct && (!out_ok || (ol == 0 && oh >= n))) {  // (the owner's results are not read: its buffer is free)
+    CHK_HIP(e, hipEventRecord(e->consumed[S.k[0]], on_pipe ? e->pipe[S.k[0]] : r->ret));
+  }
   if (!S.err && n && n_send != n) {
     // the partition rejected the slice on the device (zero counts; its error
     // word fails the batch at rl_synchronize): perm was never written, so
     // nothing is scattered
   } else if (!S.err) {
-    const rl_result& out = S.out;
-    const uint32_t mine = S.n_rules * RL_NUM_STATS;  // (<= m: M is the largest n_rules sent)
-    OutDev o{out.code, out.limit_remaining, out.reset_s, (unsigned long long*)out.stats, out.status};
-    if (S.io.host) o = OutDev{S.h_code, S.h_rem, S.h_reset, nullptr, out.status ? S.h_status : nullptr};
-    unsigned long long* stats_out = S.io.stats_host ? S.io_stats : (unsigned long long*)out.stats;
-    uint32_t* src_err = out.status ? nullptr : e->errw + NBUF + 2;
     if (direct) {
       const uint32_t k = S.k[0];
-      launch_route_scatter(S.perm, e->s[k].res, n, o, r->ret, src_err, e->s[k].errb);
-      CHK_HIP(e, hipEventRecord(e->consumed[k], r->ret));
+      if (!(ol == 0 && oh >= n)) {
+        launch_route_scatter(S.perm, e->s[k].res, n, o, r->ret, src_err, e->s[k].errb, ol, oh);
+        CHK_HIP(e, hipEventRecord(e->consumed[k], r->ret));
+      }
     } else {
-      launch_route_scatter(S.perm, S.back, n, o, r->ret, src_err);
+      launch_route_scatter(S.perm, S.back, n, o, r->ret, src_err, nullptr, ol, oh);
     }
-    if (mine && stats_out) launch_stats_sum(stats_in, W, mine, stats_out, r->ret, m);
+    if (mine && stats_out && !stats_direct) launch_stats_sum(stats_in, W, mine, stats_out, r->ret, m);
     // the answers cross back to the caller's host slice (kernel stores into
     // page-locked outputs, rl_kernels.h ToHost)
     ToHost th{};
@@ -667,7 +703,7 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
     r->sticky_msg = S.errmsg;
   }
   CHK_HIP(e, hipGetLastError());
-  CHK_HIP(e, hipEventRecord(S.done, r->ret));  // (outputs: read after rl_synchronize)
+  CHK_HIP(e, hipEventRecord(S.done, on_pipe ? e->pipe[S.k[0]] : r->ret));  // (outputs: read after rl_synchronize)
   r->t_second += now_s() - t1;
   r->n_steps++;
   return RL_OK;
@@ -704,9 +740,8 @@ CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t*
     return nullptr;
   }
   bool ok = hipSetDevice(r->dev) == hipSuccess &&
-            hipStreamCreateWithFlags(&r->cs, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&r->fwd, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&r->ret, hipStreamNonBlocking) == hipSuccess &&
+            rl_stream_create(&r->cs, SR_ROUTER) == hipSuccess && rl_stream_create(&r->fwd, SR_ROUTER) == hipSuccess &&
+            rl_stream_create(&r->ret, SR_ROUTER) == hipSuccess &&
             hipEventCreateWithFlags(&r->in_ready, hipEventDisableTiming) == hipSuccess &&
             hipHostMalloc((void**)&r->h_cnt, (size_t)RSLOTS * 2 * CNT_W * world * 8) == hipSuccess;
   if (ok && world == 1 && hipHostGetDevicePointer((void**)&r->d_hcnt, r->h_cnt, 0) != hipSuccess) {
@@ -742,10 +777,10 @@ void comm_destroy(CommRouter* r) {
   if (!r) return;
   if (r->timing && r->n_steps)
     fprintf(stderr, "{\"route_host_us\": {\"call\": %.1f, \"slot_wait\": %.1f, \"first_half\": %.1f, "
-                    "\"wait_counts\": %.1f, \"owner_enqueue\": %.1f, \"second_half\": %.1f, \"batches\": %llu}}\n",
+                    "\"wait_counts\": %.1f, \"owner_enqueue\": %.1f, \"second_half\": %.1f, \"batches\": %llu, \"slot_busy\": %llu, \"enqueue_to_reuse\": %.1f}}\n",
             r->t_call / r->n_steps * 1e6, r->t_slot / r->n_steps * 1e6, r->t_first / r->n_steps * 1e6,
             r->t_wait_counts / r->n_steps * 1e6, r->t_owner / r->n_steps * 1e6, r->t_second / r->n_steps * 1e6,
-            (unsigned long long)r->n_steps);
+            (unsigned long long)r->n_steps, (unsigned long long)r->n_slot_busy, r->n_lat ? r->t_lat / r->n_lat * 1e6 : 0.0);
   (void)hipSetDevice(r->dev);
   for (hipStream_t st : {r->cs, r->fwd, r->ret})
     if (st) (void)hipStreamSynchronize(st);
@@ -802,8 +837,14 @@ int comm_do_limit(CommRouter* r, Engine* e, const rl_batch* in, rl_result* out, 
   // read that slice's own chunk in place, so a caller may reuse a batch's
   // inputs once RSLOTS later calls have returned (long done by then: this
   // wait does not bind)
+  if (r->timing && hipEventQuery(S.done) == hipErrorNotReady) r->n_slot_busy++;
   CHK_HIP(e, hipEventSynchronize(S.done));
   r->t_slot += now_s() - tc;
+  if (r->t_enq[s] > 0) {
+    r->t_lat += now_s() - r->t_enq[s];
+    r->n_lat++;
+    r->t_enq[s] = 0;
+  }
   S.out = *out;
   S.n = n;
   S.n_rules = nr;

@@ -135,6 +135,14 @@ struct Engine {
 
 // Engine entry points (rl_engine.hip): the single-shard implementations of
 // the C ABI functions of the same name (rl_x -> eng_x).
+// A non-blocking stream of one of the library's roles. A stream created the
+// usual way shares one of the process's GPU_MAX_HW_QUEUES hardware queues with
+// other streams, and a marker or kernel queued on it waits behind whatever the
+// other stream queued first; RL_DEDICATED_QUEUES (bits: 1 router streams, 2
+// host copy streams, 4 pipeline streams) gives a role's streams queues of
+// their own (a CU-masked queue with every CU enabled).
+enum StreamRole : uint32_t { SR_ROUTER = 1, SR_HOSTCOPY = 2, SR_PIPE = 4 };
+hipError_t rl_stream_create(hipStream_t* st, uint32_t role);
 Engine* eng_create(const rl_config* cfg, char* err, size_t errlen);
 void eng_destroy(Engine* c);
 const char* eng_last_error(const Engine* c);

@@ -11,10 +11,12 @@
 // sees the reference's sequential INCRBY order. Every other call is serial and
 // ordered after all submitted batches.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <random>
 #include <cstring>
 #include <string>
@@ -326,6 +328,18 @@ namespace rl {
 
 const char* eng_last_error(const Engine* c) { return c ? c->last_error.c_str() : g_err.c_str(); }
 
+hipError_t rl_stream_create(hipStream_t* st, uint32_t role) {
+  static const uint32_t dedicated =
+      getenv("RL_DEDICATED_QUEUES") ? (uint32_t)strtoul(getenv("RL_DEDICATED_QUEUES"), nullptr, 0) : 0u;
+  if (!(dedicated & role)) return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+  int dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  std::vector<uint32_t> mask(((uint32_t)cus + 31) / 32, 0xFFFFFFFFu);
+  return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data());
+}
+
 Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   auto fail = [&](const std::string& m, Engine* c) -> Engine* {
     if (err && errlen) snprintf(err, errlen, "%s", m.c_str());
@@ -375,7 +389,7 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   c->arena_cap16 = cfg.arena_bytes / 16;
   const uint32_t n = cfg.max_batch;
   bool ok = true;
-  for (uint32_t k = 0; k < NBUF; k++) ok = ok && hipStreamCreateWithFlags(&c->pipe[k], hipStreamNonBlocking) == hipSuccess;
+  for (uint32_t k = 0; k < NBUF; k++) ok = ok && rl_stream_create(&c->pipe[k], SR_PIPE) == hipSuccess;
   c->stream = c->pipe[0];
   for (uint32_t k = 0; k < NBUF; k++)
     ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess &&
@@ -794,8 +808,7 @@ int eng_batch_progress(Engine* c, uint64_t* submitted, uint64_t* completed) {
 int ensure_host_slots(Engine* c) {
   if (!c->hs_ready) {
     const rl_config& g = c->cfg;
-    bool ok = hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) == hipSuccess;
+    bool ok = rl_stream_create(&c->h2d, SR_HOSTCOPY) == hipSuccess && rl_stream_create(&c->d2h, SR_HOSTCOPY) == hipSuccess;
     for (HostSlot& h : c->hs) {
       ok = ok && dalloc(&h.stem, (size_t)g.max_stem_bytes + 64) == hipSuccess &&
            dalloc(&h.off, (size_t)g.max_batch + 1) == hipSuccess && dalloc(&h.req, g.max_batch) == hipSuccess &&

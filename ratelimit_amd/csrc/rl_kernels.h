@@ -70,6 +70,14 @@ struct OwnChunk {
   const uint32_t* limit;
   const uint32_t* hits;
   const uint32_t* rule;
+  // the source batch's outputs (arrival order; null code: none): k_finish
+  // answers the own chunk in place, no packed results go back for it. Without
+  // a status array a failed descriptor ORs its error bit into src_err.
+  uint8_t* code;
+  uint32_t* rem;
+  uint32_t* reset;
+  uint8_t* status;
+  uint32_t* src_err;
 };
 struct BatchDev {
   uint32_t n, n_req, n_rules, stem_cap;
@@ -307,9 +315,12 @@ void launch_route_fail(unsigned long long* ret, uint32_t n, uint32_t status, hip
 // src_err (optional): without o.status, a returned failure status sets its
 // error bit there (the source's batch then fails at rl_synchronize). errb
 // (optional): ret is an owner batch's own results; a failed batch (*errb)
-// answers every record with its status, as k_route_ret does.
+// answers every record with its status, as k_route_ret does. Records
+// [own_lo, own_hi) are the own chunk, answered in place by the owner batch's
+// k_finish (OwnChunk outputs): skipped (all of them: no launch).
 void launch_route_scatter(const uint32_t* perm, const unsigned long long* ret, uint32_t n, const OutDev& o,
-                          hipStream_t st, uint32_t* src_err = nullptr, const uint32_t* errb = nullptr);
+                          hipStream_t st, uint32_t* src_err = nullptr, const uint32_t* errb = nullptr,
+                          uint32_t own_lo = 0, uint32_t own_hi = 0);
 // Owner side: ret[i] = res[i], or every record failed with the status of
 // *errb when the batch's table stage failed.
 void launch_route_ret(const unsigned long long* res, uint32_t n, const uint32_t* errb, unsigned long long* ret,

@@ -4490,7 +4490,7 @@ __global__ __launch_bounds__(256) void k_finish(const unsigned long long* __rest
                                                 unsigned long long* __restrict__ stripes, uint32_t n_fold,
                                                 const uint32_t* err, unsigned long long* lc_ctr,
                                                 const unsigned long long* __restrict__ kt, uint32_t kt_n,
-                                                unsigned long long* kt_acc) {
+                                                unsigned long long* kt_acc, const OwnChunk own) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (kt && blockIdx.x == 0) {  // (rl_profile) k_table's duration: first workgroup start to last end
     __shared__ unsigned long long s_lo[256], s_hi[256];
@@ -4534,6 +4534,18 @@ __global__ __launch_bounds__(256) void k_finish(const unsigned long long* __rest
       if (o.status) o.status[i] = (uint8_t)res_status(v);
     }
     hit = res_lc_hit(v);
+  }
+  // a routed owner's own chunk: answered in place in the source batch's
+  // outputs (k_route_scatter's work for these positions; a failed batch
+  // answers its status for each)
+  if (own.code && i < n && i - own.lo < own.n) {
+    const unsigned long long v = ok ? res[i] : pack_fail(err_status(*err));
+    const uint32_t e = own.idx[i - own.lo];
+    own.code[e] = (uint8_t)res_code(v);
+    own.rem[e] = res_rem(v);
+    if (own.reset) own.reset[e] = res_reset(v);
+    if (own.status) own.status[e] = (uint8_t)res_status(v);
+    else if (own.src_err && res_status(v)) atomicOr(own.src_err, status_err(res_status(v)));
   }
   if (lc_ctr && ok) {  // freecache LookupCount / HitCount (local_cache_stats.go:36-43)
     const unsigned long long w = __ballot(hit);
@@ -4790,7 +4802,7 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;
       const uint32_t gf = cdiv(nf * RL_NUM_STATS > b.n ? nf * RL_NUM_STATS : b.n, 256);
       k_finish<<<gf, 256, 0, st>>>(s.res, b.n, o, s.stripes, nf, s.errb, P.lc_en ? s.counters + 5 : nullptr,
-                                   kt_acc ? s.kt_blk : nullptr, g_runs + g, kt_acc);
+                                   kt_acc ? s.kt_blk : nullptr, g_runs + g, kt_acc, b.own);
     }
   } else {
     if (ev) {

@@ -373,9 +373,10 @@ __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, 
 
 __global__ __launch_bounds__(256) void k_route_scatter(const uint32_t* __restrict__ perm,
                                                        const unsigned long long* __restrict__ ret, uint32_t n,
-                                                       OutDev o, uint32_t* src_err, const uint32_t* errb) {
+                                                       OutDev o, uint32_t* src_err, const uint32_t* errb,
+                                                       uint32_t own_lo, uint32_t own_hi) {
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= n) return;
+  if (j >= n || (j >= own_lo && j < own_hi)) return;  // (the own chunk: answered in place by its owner batch)
   const uint32_t e = perm[j];
   const uint32_t fail = errb ? *errb : 0u;  // (results straight from an owner batch: k_route_ret's check)
   const unsigned long long v = fail ? pack_fail(err_status(fail)) : ret[j];
@@ -460,8 +461,9 @@ void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, 
 }
 
 void launch_route_scatter(const uint32_t* perm, const unsigned long long* ret, uint32_t n, const OutDev& o,
-                          hipStream_t st, uint32_t* src_err, const uint32_t* errb) {
-  if (n) k_route_scatter<<<cdiv(n, 256), 256, 0, st>>>(perm, ret, n, o, src_err, errb);
+                          hipStream_t st, uint32_t* src_err, const uint32_t* errb, uint32_t own_lo, uint32_t own_hi) {
+  if (n && !(own_lo == 0 && own_hi >= n))
+    k_route_scatter<<<cdiv(n, 256), 256, 0, st>>>(perm, ret, n, o, src_err, errb, own_lo, own_hi);
 }
 
 void launch_route_ret(const unsigned long long* res, uint32_t n, const uint32_t* errb, unsigned long long* ret,
