@@ -125,6 +125,14 @@ struct CommRouter {
   bool alias = false;     // world 1: the owner reads the partition in place, no exchange
   bool own = true;        // this rank's own chunk read in place from its slice (no wire records, no stem copy)
   hipStream_t cs = nullptr, fwd = nullptr, ret = nullptr;
+  // one_stream (default): a batch's routed work runs on the engine pipeline
+  // stream its owner part will take (partition and counts on the one its
+  // owner batch is predicted to use, records out and results back on the
+  // owner part's own), so no router marker or kernel waits behind another
+  // stream's batches on a shared hardware queue. RL_DEBUG_ROUTE_STREAMS=3:
+  // the router's own three streams (cs / fwd / ret), for A/B.
+  bool one_stream = true;
+  hipStream_t scs = nullptr;  // this call's partition stream
   hipEvent_t in_ready = nullptr;
   CommSlot slot[RSLOTS];
   uint32_t next = 0;
@@ -254,7 +262,7 @@ int stage_host(CommRouter* r, Engine* e, CommSlot& S, const rl_batch* in, rl_bat
   const uint64_t a0 = in->stem_off[0] & ~3u, a1 = in->stem_off[n];
   if ((uint64_t)da + n > g.max_batch || qb > g.max_requests || qa > qb || a1 > g.max_stem_bytes || a1 < a0)
     return eng_fail(e, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_stem_bytes");
-  hipStream_t st = r->cs;
+  hipStream_t st = r->scs;
   CHK_HIP(e, hipMemcpyAsync(S.h_stem + a0, in->stem_bytes + a0, a1 - a0, hipMemcpyHostToDevice, st));
   CHK_HIP(e, hipMemcpyAsync(S.h_off + da, in->stem_off, (n + 1) * 4ull, hipMemcpyHostToDevice, st));
   if (qb > qa) CHK_HIP(e, hipMemcpyAsync(S.h_now + qa, in->now + qa, (qb - qa) * 8ull, hipMemcpyHostToDevice, st));
@@ -310,7 +318,7 @@ int stage_host_compact(CommRouter* r, Engine* e, CommSlot& S, const rl_batch* in
     return eng_fail(e, RL_E_INVALID, "gpu: compact batch stem offsets out of order");
   if (a1 > g.max_stem_bytes)
     return eng_fail(e, RL_E_CAPACITY, "gpu: batch exceeds configured max_batch/max_requests/max_stem_bytes");
-  hipStream_t st = r->cs;
+  hipStream_t st = r->scs;
   auto part = [&](uint64_t sect, uint64_t from, uint64_t bytes) {
     return bytes ? hipMemcpyAsync(S.h_cbuf + sect + from, cb.buf + sect + from, bytes, hipMemcpyHostToDevice, st)
                  : hipSuccess;
@@ -373,7 +381,7 @@ int stage_host_prefixed(CommRouter* r, Engine* e, CommSlot& S, const rl_batch* i
   // the cut's own entries bound the copies (the device checks every tile's)
   if (I0[0] != da || I1[0] != db || I1[1] < I0[1] || I1[2] < I0[2] || I1[1] > tot[1] || I1[2] > tot[2])
     return eng_fail(e, RL_E_INVALID, "gpu: prefixed batch index out of order");
-  hipStream_t st = r->cs;
+  hipStream_t st = r->scs;
   auto part = [&](uint64_t sect, uint64_t from, uint64_t bytes) {
     return bytes ? hipMemcpyAsync(S.h_cbuf + sect + from, pb.buf + sect + from, bytes, hipMemcpyHostToDevice, st)
                  : hipSuccess;
@@ -409,10 +417,14 @@ int stage_host_prefixed(CommRouter* r, Engine* e, CommSlot& S, const rl_batch* i
 int first_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, const rl_batch* in, hipStream_t caller,
                int hostrc) {
   const uint32_t W = r->world, me = r->rank;
-  CHK_HIP(e, hipStreamWaitEvent(r->cs, S.done, 0));  // the slot's previous batch is complete
+  // (one_stream: the pipeline stream this batch's owner part is predicted to
+  // take: the engine buffer after the pending batches' owner parts)
+  r->scs = r->one_stream ? e->pipe[(e->next + r->n_pend) % NBUF] : r->cs;
+  hipStream_t cs = r->scs;
+  CHK_HIP(e, hipStreamWaitEvent(cs, S.done, 0));  // the slot's previous batch is complete
   if (caller && hipStreamQuery(caller) == hipErrorNotReady) {  // the inputs' producer (still running)
     CHK_HIP(e, hipEventRecord(r->in_ready, caller));
-    CHK_HIP(e, hipStreamWaitEvent(r->cs, r->in_ready, 0));
+    CHK_HIP(e, hipStreamWaitEvent(cs, r->in_ready, 0));
   }
   const uint64_t flags = S.out.status ? CNT_ISOLATE : 0;
   int rc = hostrc;
@@ -428,14 +440,14 @@ int first_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, const rl_batch
   // stores to page-locked memory; no copy launch per batch)
   unsigned long long* hc = r->alias && r->d_hcnt ? r->d_hcnt + (size_t)s * 2 * CNT_W * W : nullptr;
   if (!rc) {
-    rc = eng_route_pack(e, in, W, me, S.send_rec, S.send_stem, S.perm, (uint64_t*)S.cnt, r->cs, CNT_W, S.n_rules,
+    rc = eng_route_pack(e, in, W, me, S.send_rec, S.send_stem, S.perm, (uint64_t*)S.cnt, cs, CNT_W, S.n_rules,
                         flags, r->own ? me : ROUTE_OWN_NONE, S.hash, hc);
     S.src = *in;  // (read by this batch's owner part, in the next call)
   }
   if (rc) {  // (a device-side malformation zeroes the counts itself and fails at rl_synchronize)
     S.err = rc;
     S.errmsg = eng_last_error(e);
-    launch_cnt_fill(S.cnt, W, CNT_W, 0, flags | CNT_FAILED, r->cs, hc);
+    launch_cnt_fill(S.cnt, W, CNT_W, 0, flags | CNT_FAILED, cs, hc);
   }
   if (!r->alias) {
     r->ops.clear();
@@ -444,13 +456,13 @@ int first_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, const rl_batch
       r->ops.push_back({S.cnt + (size_t)CNT_W * p, CNT_W * 8ull, p, true});
       r->ops.push_back({S.cnt + (size_t)CNT_W * (W + p), CNT_W * 8ull, p, false});
     }
-    const int g = run_group(r, e, 0, r->cs);
+    const int g = run_group(r, e, 0, cs);
     if (g) return g;
   }
   if (!hc)
     CHK_HIP(e, hipMemcpyAsync(r->h_cnt + (size_t)s * 2 * CNT_W * W, S.cnt, 2ull * CNT_W * W * 8, hipMemcpyDeviceToHost,
-                              r->cs));
-  CHK_HIP(e, hipEventRecord(S.packed, r->cs));
+                              cs));
+  CHK_HIP(e, hipEventRecord(S.packed, cs));
   return RL_OK;
 }
 
@@ -503,7 +515,8 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
   // world 1: nothing crosses the fwd stream; the owner waits on the
   // partition itself (a wait routed through fwd queued behind whatever shares
   // its hardware queue)
-  if (!r->alias) CHK_HIP(e, hipStreamWaitEvent(r->fwd, S.packed, 0));
+  hipStream_t fwd = r->one_stream ? e->pipe[e->next] : r->fwd;  // (one_stream: the owner part's stream)
+  if (!r->alias) CHK_HIP(e, hipStreamWaitEvent(fwd, S.packed, 0));
   if (!r->alias) CHK_HIP(e, grow(r, S, n_recv, b_recv, 1));
   // (world 1: the partition is the received batch)
   const Wire* recv_rec = r->alias ? S.send_rec : S.recv_rec;
@@ -519,16 +532,16 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
       r->ops.push_back({S.recv_rec + r->ro_r[p], rn * sizeof(Wire), p, false});
       r->ops.push_back({S.recv_stem + r->base[p], rb, p, false});
     }
-    const int g = run_group(r, e, 1, r->fwd);
+    const int g = run_group(r, e, 1, fwd);
     if (g) return g;
     if (h[CNT_W * me] && !r->own)
       CHK_HIP(e, hipMemcpyAsync(S.recv_rec + r->ro_r[me], S.send_rec + r->so_r[me], h[CNT_W * me] * sizeof(Wire),
-                                hipMemcpyDeviceToDevice, r->fwd));
+                                hipMemcpyDeviceToDevice, fwd));
     if (h[CNT_W * me + 1])  // (none with the own chunk read in place)
       CHK_HIP(e, hipMemcpyAsync(S.recv_stem + r->base[me], S.send_stem + r->so_b[me], h[CNT_W * me + 1],
-                                hipMemcpyDeviceToDevice, r->fwd));
+                                hipMemcpyDeviceToDevice, fwd));
   }
-  if (!r->alias) CHK_HIP(e, hipEventRecord(S.sent, r->fwd));
+  if (!r->alias) CHK_HIP(e, hipEventRecord(S.sent, fwd));
   hipEvent_t const sent = r->alias ? S.packed : S.sent;  // (the received records are ready)
   // the owner pipeline, in parts of at most max_batch records. A part ends on
   // a request boundary (a request's descriptors check the local cache before
@@ -540,7 +553,7 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
   const uint64_t own_lo = r->ro_r[me], own_hi = r->own ? r->ro_r[me + 1] : own_lo;  // (received positions)
   if (n_recv > mb && !owner_fail) {
     std::vector<uint32_t> lab(n_recv);
-    CHK_HIP(e, hipStreamSynchronize(r->fwd));
+    CHK_HIP(e, hipStreamSynchronize(fwd));
     CHK_HIP(e, hipMemcpy2D(lab.data(), 4, recv_rec, sizeof(Wire), 4, n_recv, hipMemcpyDeviceToHost));
     if (own_hi > own_lo) {  // the own chunk has no wire labels: from its slice's request indices
       std::vector<uint32_t> pi(own_hi - own_lo), rq(S.n);
@@ -587,10 +600,13 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
   const bool on_pipe = direct && !S.io.host && !S.io.stats_host &&
                        (!out_ok || ((ol == 0 && oh >= n) && (stats_direct || !mine || !stats_out)));
   const double t2 = now_s();
+  // the return stream: one_stream, the last owner part's (set below), or fwd's
+  // when the owner cannot run
+  hipStream_t ret = r->one_stream ? fwd : r->ret;
   if (owner_fail) {
-    CHK_HIP(e, hipStreamWaitEvent(r->ret, sent, 0));
-    launch_route_fail(ret_send, (uint32_t)n_recv, (uint32_t)owner_fail, r->ret);
-    if (blk) CHK_HIP(e, hipMemsetAsync(S.ostats, 0, blk * 8, r->ret));
+    CHK_HIP(e, hipStreamWaitEvent(ret, sent, 0));
+    launch_route_fail(ret_send, (uint32_t)n_recv, (uint32_t)owner_fail, ret);
+    if (blk) CHK_HIP(e, hipMemsetAsync(S.ostats, 0, blk * 8, ret));
   } else {
     for (uint32_t q = 0; q < parts; q++) {
       const uint64_t a = cut[q], b = cut[q + 1];
@@ -632,17 +648,22 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
       const uint32_t k = S.k[q];
       CHK_HIP(e, hipSetDevice(r->dev));
       if (on_pipe) break;
-      CHK_HIP(e, hipStreamWaitEvent(r->ret, e->b_done[k], 0));
+      hipStream_t rs = r->one_stream ? e->pipe[k] : r->ret;
+      if (!r->one_stream) CHK_HIP(e, hipStreamWaitEvent(rs, e->b_done[k], 0));
       if (direct) break;
-      launch_route_ret(e->s[k].res, (uint32_t)(b - a), e->s[k].errb, ret_send + a, r->ret);
-      CHK_HIP(e, hipEventRecord(e->consumed[k], r->ret));
+      launch_route_ret(e->s[k].res, (uint32_t)(b - a), e->s[k].errb, ret_send + a, rs);
+      CHK_HIP(e, hipEventRecord(e->consumed[k], rs));
+    }
+    if (r->one_stream) {  // the return on the last part's stream, after every part's results
+      ret = e->pipe[S.k[parts - 1]];
+      for (uint32_t q = 0; q + 1 < parts && !direct; q++) CHK_HIP(e, hipStreamWaitEvent(ret, e->consumed[S.k[q]], 0));
     }
   }
   const double t3 = now_s();
   r->t_owner += t3 - t2;
   r->t_enq[s] = t3;
   // results and per-source stats back to their sources
-  if (parts > 1 && m && !owner_fail) launch_stats_sum(S.ostats, parts, (uint32_t)blk, S.ostats, r->ret);
+  if (parts > 1 && m && !owner_fail) launch_stats_sum(S.ostats, parts, (uint32_t)blk, S.ostats, ret);
   const unsigned long long* stats_in = S.ostats;  // (world 1: this rank's block is the owner's)
   if (!r->alias) {
     r->ops.clear();
@@ -654,18 +675,18 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
       r->ops.push_back({S.ostats + (size_t)p * m, (uint64_t)m * 8, p, true});
       r->ops.push_back({S.stats_stage + (size_t)p * m, (uint64_t)m * 8, p, false});
     }
-    const int g = run_group(r, e, 2, r->ret);
+    const int g = run_group(r, e, 2, ret);
     if (g) return g;
     if (h[CNT_W * me] && !own_inplace)
       CHK_HIP(e, hipMemcpyAsync(S.back + r->so_r[me], S.ret_send + r->ro_r[me], h[CNT_W * me] * 8,
-                                hipMemcpyDeviceToDevice, r->ret));
+                                hipMemcpyDeviceToDevice, ret));
     if (m)
       CHK_HIP(e, hipMemcpyAsync(S.stats_stage + (size_t)me * m, S.ostats + (size_t)me * m, (size_t)m * 8,
-                                hipMemcpyDeviceToDevice, r->ret));
+                                hipMemcpyDeviceToDevice, ret));
     stats_in = S.stats_stage;
   }
   if (direct && (!out_ok || (ol == 0 && oh >= n))) {  // (the owner's results are not read: its buffer is free)
-    CHK_HIP(e, hipEventRecord(e->consumed[S.k[0]], on_pipe ? e->pipe[S.k[0]] : r->ret));
+    CHK_HIP(e, hipEventRecord(e->consumed[S.k[0]], on_pipe ? e->pipe[S.k[0]] : ret));
   }
   if (!S.err && n && n_send != n) {
     // the partition rejected the slice on the device (zero counts; its error
@@ -675,13 +696,13 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
     if (direct) {
       const uint32_t k = S.k[0];
       if (!(ol == 0 && oh >= n)) {
-        launch_route_scatter(S.perm, e->s[k].res, n, o, r->ret, src_err, e->s[k].errb, ol, oh);
-        CHK_HIP(e, hipEventRecord(e->consumed[k], r->ret));
+        launch_route_scatter(S.perm, e->s[k].res, n, o, ret, src_err, e->s[k].errb, ol, oh);
+        CHK_HIP(e, hipEventRecord(e->consumed[k], ret));
       }
     } else {
-      launch_route_scatter(S.perm, S.back, n, o, r->ret, src_err, nullptr, ol, oh);
+      launch_route_scatter(S.perm, S.back, n, o, ret, src_err, nullptr, ol, oh);
     }
-    if (mine && stats_out && !stats_direct) launch_stats_sum(stats_in, W, mine, stats_out, r->ret, m);
+    if (mine && stats_out && !stats_direct) launch_stats_sum(stats_in, W, mine, stats_out, ret, m);
     // the answers cross back to the caller's host slice (kernel stores into
     // page-locked outputs, rl_kernels.h ToHost)
     ToHost th{};
@@ -697,13 +718,13 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
       if (out.reset_s) add(out.reset_s, S.h_reset, n * 4ull);
       if (out.status) add(out.status, S.h_status, n);
     }
-    if (th.n) CHK_HIP(e, copy_to_host(th, r->ret));
+    if (th.n) CHK_HIP(e, copy_to_host(th, ret));
   } else if (!r->sticky) {
     r->sticky = S.err;
     r->sticky_msg = S.errmsg;
   }
   CHK_HIP(e, hipGetLastError());
-  CHK_HIP(e, hipEventRecord(S.done, on_pipe ? e->pipe[S.k[0]] : r->ret));  // (outputs: read after rl_synchronize)
+  CHK_HIP(e, hipEventRecord(S.done, on_pipe ? e->pipe[S.k[0]] : ret));  // (outputs: read after rl_synchronize)
   r->t_second += now_s() - t1;
   r->n_steps++;
   return RL_OK;
@@ -730,6 +751,7 @@ CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t*
   r->alias = world == 1 && !getenv("RL_DEBUG_ROUTE_NOALIAS");
   r->own = !getenv("RL_DEBUG_ROUTE_NOOWN");  // (A/B knob: the own chunk as wire records and copied stems)
   r->timing = getenv("RL_DEBUG_ROUTE_TIMING") != nullptr;
+  if (const char* rs = getenv("RL_DEBUG_ROUTE_STREAMS")) r->one_stream = atoi(rs) != 3;
   if (const char* lg = getenv("RL_DEBUG_ROUTE_LAG"))
     r->lag = std::max<uint32_t>(1, std::min<uint32_t>(RSLOTS - 1, (uint32_t)atoi(lg)));
   if (const char* pm = getenv("RL_DEBUG_OWNER_PART"))
@@ -784,6 +806,7 @@ void comm_destroy(CommRouter* r) {
   (void)hipSetDevice(r->dev);
   for (hipStream_t st : {r->cs, r->fwd, r->ret})
     if (st) (void)hipStreamSynchronize(st);
+  (void)hipDeviceSynchronize();  // (one_stream: routed work on the engine's pipeline streams reads the slots)
   r->tr.reset();
   for (CommSlot& S : r->slot) free_slot(S);
   if (r->h_cnt) (void)hipHostFree(r->h_cnt);
@@ -807,6 +830,7 @@ int comm_synchronize(CommRouter* r, Engine* e) {
     if (rc) return rc;
   }
   for (hipStream_t st : {r->cs, r->fwd, r->ret}) CHK_HIP(e, hipStreamSynchronize(st));
+  for (uint32_t k = 0; k < NBUF && r->one_stream; k++) CHK_HIP(e, hipStreamSynchronize(e->pipe[k]));
   if (r->sticky) {
     const int rc = eng_fail(e, r->sticky, r->sticky_msg);
     r->sticky = RL_OK;
