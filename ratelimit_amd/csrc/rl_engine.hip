@@ -831,6 +831,19 @@ int ensure_host_slots(Engine* c) {
   return RL_OK;
 }
 
+// The streams of a host-fed batch. By default its input copy goes on the
+// pipeline stream the batch will take (c->pipe[c->next]) and its outputs'
+// copy back on the pipeline stream it took (k): a separate copy stream shares
+// a hardware queue with one of the pipeline streams, and its copies and
+// markers then wait behind that stream's later batches (the routed step's
+// measured stall, CommRouter::one_stream). RL_HOSTFED_STREAMS=2: the h2d / d2h
+// streams (A/B).
+hipStream_t hostfed_stream(Engine* c, bool input, uint32_t k = 0) {
+  static const bool own = getenv("RL_HOSTFED_STREAMS") && atoi(getenv("RL_HOSTFED_STREAMS")) == 2;
+  if (own) return input ? c->h2d : c->d2h;
+  return input ? c->pipe[c->next] : c->pipe[k];
+}
+
 // The copy stream's order after the slot's previous batch (its outputs
 // drained). A cross-queue wait in front of an SDMA copy made hipMemcpyAsync
 // block the submitting thread for ~0.3 ms on some boxes, and the link idled
@@ -851,14 +864,14 @@ hipError_t slot_drained(Engine* c, HostSlot& h, hipStream_t up) {
 // h.in_done) and its outputs' copies back into *out on the d2h stream.
 int host_slot_run(Engine* c, HostSlot& h, const rl_batch& d, uint64_t nb, rl_result* out) {
   const uint32_t n = d.n;
-  hipStream_t down = c->d2h;
   BatchDev b = dev_view(c, &d, c->cfg.max_stem_bytes);
   b.stem_total = (uint32_t)nb;
   OutDev o{h.code, h.rem, h.reset, d.n_rules ? h.stats : nullptr, out->status ? h.status : nullptr};
   const double w0 = c->host_time ? wall_s() : 0;
   HIPCHK(c, hipStreamWaitEvent(c->pipe[c->next], h.in_done, 0));
   const uint32_t k = enqueue(c, b, o, 0, nullptr, true);
-  HIPCHK(c, hipStreamWaitEvent(down, c->b_done[k], 0));
+  hipStream_t down = hostfed_stream(c, false, k);
+  if (down != c->pipe[k]) HIPCHK(c, hipStreamWaitEvent(down, c->b_done[k], 0));
   const double w1 = c->host_time ? wall_s() : 0;
   // (stores by a kernel into page-locked outputs: not queued behind the next
   // batch's input copy on the DMA engine, rl_kernels.h ToHost)
@@ -904,7 +917,7 @@ int eng_do_limit_host_async(Engine* c, const rl_batch* in, rl_result* out) {
   const uint32_t j = c->hnext;
   c->hnext = (j + 1) % NBUF;
   HostSlot& h = c->hs[j];
-  hipStream_t up = c->h2d;
+  hipStream_t up = hostfed_stream(c, true);
   HIPCHK(c, slot_drained(c, h, up));  // the slot's previous batch is drained
   if (nb) HIPCHK(c, hipMemcpyAsync(h.stem, in->stem_bytes, nb, hipMemcpyHostToDevice, up));
   HIPCHK(c, hipMemcpyAsync(h.off, in->stem_off, (n + 1) * 4ull, hipMemcpyHostToDevice, up));
@@ -978,7 +991,7 @@ int eng_do_limit_compact_async(Engine* c, const rl_batch_compact* in, rl_result*
     h.cbuf_cap = B;
   }
   c->hnext = (j + 1) % NBUF;
-  hipStream_t up = c->h2d;
+  hipStream_t up = hostfed_stream(c, true);
   HIPCHK(c, slot_drained(c, h, up));  // the slot's previous batch is drained
   if (B) HIPCHK(c, hipMemcpyAsync(h.cbuf, in->buf, B, hipMemcpyHostToDevice, up));
   HIPCHK(c, hipEventRecord(h.in_done, up));
@@ -1059,7 +1072,7 @@ int eng_do_limit_prefixed_async(Engine* c, const rl_batch_prefixed* in, rl_resul
     h.cbuf_cap = B;
   }
   c->hnext = (j + 1) % NBUF;
-  hipStream_t up = c->h2d;
+  hipStream_t up = hostfed_stream(c, true);
   const double w1 = c->host_time ? wall_s() : 0;
   if (c->copy_time) HIPCHK(c, hipEventRecord(c->ct_ev[2][c->ct_n % 64], up));
   HIPCHK(c, slot_drained(c, h, up));  // the slot's previous batch is drained
