@@ -236,12 +236,15 @@ def main():
     torch.cuda.synchronize()
 
     step = [0]
+    host_in_call = [0.0]  # host seconds inside the library's submit calls (timed steps only)
 
     def run_step():
         s = step[0]
         inp = dict(dev_batches[s % len(dev_batches)])
         inp["now"] = nows[s]
+        t = time.perf_counter()
         do_step(inp, n, nq)
+        host_in_call[0] += time.perf_counter() - t
         step[0] += 1
 
     # ---- warmup
@@ -262,11 +265,13 @@ def main():
     info0 = be.table_info()
     barrier()
     torch.cuda.synchronize()
+    host_in_call[0] = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run_step()
         if py_route:
             recv.append(sc.last_recv)
+    host_submit_ms = host_in_call[0] / args.steps * 1e3
     sync()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -389,6 +394,7 @@ def main():
                                   ("one ctx, table hash-sharded over %d shards on this GPU (loopback routing)"
                                    % args.shards) if args.shards > 1 else "single GPU"},
         "p50_batch_ms": float(np.percentile(lat, 50)), "p99_batch_ms": p99, "latency_batches": int(lat.size),
+        "host_submit_ms": round(host_submit_ms, 4),
         **({"p50_loaded_batch_ms": loaded["p50_ms"], "p99_loaded_batch_ms": loaded["p99_ms"],
             "loaded": loaded} if loaded else {}),
         "pcie_fed": pcie,
