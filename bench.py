@@ -95,6 +95,12 @@ def to_dev(a, torch):
                                 else np.ascontiguousarray(v)).cuda() for k, v in a.items()}
 
 
+def progress(msg):
+    """A phase boundary on stderr (rank 0): long runs (C3's fill) show they are alive."""
+    if os.environ.get("RANK", "0") == "0":
+        print("[bench] %s" % msg, file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     if args.loopback:
@@ -207,6 +213,7 @@ def main():
             do_step(a, bn, bq)
         sync()
     t_fill = time.perf_counter() - t_fill
+    progress("fill done (%.1f s)" % t_fill)
 
     # ---- device-resident input batches + per-step clocks. Requests draw from
     # the whole node's tenant space (world * T): with routing every rank talks
@@ -291,17 +298,22 @@ def main():
         elapsed = float(t.item())
     value = world * n * args.steps / elapsed
 
+    progress("timed steps done")
     # ---- batch latency: submit -> outputs ready, one batch at a time
     lat = []
-    for _ in range(args.latency_steps):
+    for i in range(args.latency_steps):
         t1 = time.perf_counter()
         run_step()
         sync()
         lat.append((time.perf_counter() - t1) * 1e3)
+        if i % 250 == 249 or lat[-1] > 50:
+            progress("latency batch %d: %.2f ms" % (i + 1, lat[-1]))
     lat = np.array(lat) if lat else np.array([float("nan")])
     loaded = None
     if not routed and args.shards == 1 and args.loaded_steps > 0:
+        progress("latency done")
         loaded = loaded_latency(be, run_step, args.loaded_steps, elapsed / args.steps)
+        progress("loaded latency done")
     pcie = None if (routed or args.pcie_steps <= 0) else pcie_fed(args, be, host_batches, now0 + total_steps)
     info = be.table_info()
     if routed:
@@ -597,8 +609,11 @@ def pcie_fed(args, be, host_batches, now):
         int(soa[0].arrays["stem_off"][n])
     fmts = args.pcie_formats.split(",")
     r_soa = phase(soa, be.do_limit_host_async, soa_in) if "soa" in fmts else None
+    progress("host-fed soa done")
     r_comp = phase(comp, be.do_limit_compact_async, int(comp[0].buf.size)) if "compact" in fmts else None
+    progress("host-fed compact done")
     r_pref = phase(pref, be.do_limit_prefixed_async, int(pref[0].buf.size)) if "prefixed" in fmts else None
+    progress("host-fed prefixed done")
     # the link's own rate for one large page-locked copy, the bound to read h2d_GBps against
     import torch
     big = arena.array(256 << 20, np.uint8)

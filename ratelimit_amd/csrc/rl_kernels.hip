@@ -3844,11 +3844,16 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
         if (c[k].ws != WS_INVALID && A[g].w < c[k].ws) return true;  // a new record below cur: the exact path
         rolls |= 1u << k;
       }
-  // The groups' starting state from the curs and the logged records. The
-  // parallel path writes curs only: a group whose key has a record in a log
-  // (or in a cur that rolls away) goes to the exact path, as does one whose
-  // record may have been dropped.
-  uint32_t v0[4], lcm[4], F[4];
+  // The groups' starting state from the curs and the logged records. A
+  // group's key held in a unit's history log (below that unit's cur: e.g. a
+  // SECOND slot's record of the minute's first second, which is the MINUTE
+  // key too) is read there and written back to a new version of that record
+  // appended below (lgm: bit 4g + k). A group whose record is in a cur that
+  // rolls away, or may have been dropped, goes to the exact path.
+  // A group whose record is a cur that another group rolls away (the SECOND
+  // slot's cur of the minute's first second, one second later) finds it in
+  // the roll's log entry instead (lgr: bit 4g + k), provided the roll keeps it.
+  uint32_t v0[4], lcm[4], F[4], lgm = 0, lgr = 0;
   for (uint32_t g = 0; g < G; g++) {
     const uint32_t w = A[g].w;
     const bool cls = P.per_second && (A[g].mask & 1u);
@@ -3860,14 +3865,21 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
       const uint32_t d = div_of(k + 1);
       Win R;
       if (c[k].ws == w) {
-        if ((rolls >> k) & 1) return true;
+        if ((rolls >> k) & 1) {
+          uint32_t wn = w;  // the window unit k rolls to: the newest of its groups'
+          for (uint32_t h = 0; h < G; h++)
+            if (((A[h].mask >> k) & 1) && A[h].w > wn) wn = A[h].w;
+          if (!hist_keep(t, c[k], wn, d)) return true;
+          lgr |= 1u << (4 * g + k);
+        }
         R = c[k];
       } else if (c[k].ws == WS_INVALID || w > c[k].ws || w % d) {
         continue;  // (unit k's keys are multiples of its div)
       } else {
         const int f = chain[k] == LOG_NONE ? 0 : log_find(t, chain[k], (uint32_t)sidx[k], slot_tag(hs, k + 1), c[k].ws, w, &R);
-        if (f != 0 || !hist_absent_ok(t, now, w, c[k].ws, d)) return true;
-        continue;
+        if (f < 0 || (f == 0 && !hist_absent_ok(t, now, w, c[k].ws, d))) return true;
+        if (f == 0) continue;
+        lgm |= 1u << (4 * g + k);
       }
       const bool live = (P.per_second && k == 0) == cls && now <= R.expire;
       lcm[g] = R.lc > lcm[g] ? R.lc : lcm[g];
@@ -3886,34 +3898,51 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
       if (!F[g] && ((A[g].mask >> k) & 1) && (c[k].ws == WS_INVALID || A[g].w > c[k].ws))
         cn[k] = Win{A[g].w, 0, 0, lcm[g]};
   // commit: rolls (the old cur to the history log while a request could still ask for it)
+  uint32_t rolled[4] = {LOG_NONE, LOG_NONE, LOG_NONE, LOG_NONE};  // the roll's log entry per unit
   for (uint32_t k = 0; k < 4; k++) {
     if (cn[k].ws == c[k].ws) continue;
     Slot* su = &t.slots[sidx[k]];
-    if (c[k].ws != WS_INVALID && hist_keep(t, c[k], cn[k].ws, div_of(k + 1)))
+    if (c[k].ws != WS_INVALID && hist_keep(t, c[k], cn[k].ws, div_of(k + 1))) {
       su->ring = log_append(t, (uint32_t)sidx[k], slot_tag(hs, k + 1), chain[k], cn[k].ws, c[k]);
+      rolled[k] = su->ring;
+    }
     su->cur = cn[k];
   }
   if (__popc(present) >= 2)
     for (uint32_t k = 0; k < 4; k++)
       if ((present >> k) & 1) t.slots[sidx[k]].flags |= SLOT_EXACT;
-  const uint4 sl = make_uint4(present & 1 ? (uint32_t)sidx[0] : 0xFFFFFFFFu, present & 2 ? (uint32_t)sidx[1] : 0xFFFFFFFFu,
-                              present & 4 ? (uint32_t)sidx[2] : 0xFFFFFFFFu, present & 8 ? (uint32_t)sidx[3] : 0xFFFFFFFFu);
-  // write-back targets (per unit: bit 0 its cur holds w, bit 2 same store)
+  // write-back targets (per unit: bit 0 its cur holds w, bit 1 its history
+  // log does — the record's new version appended here, whose entry pointer
+  // takes the unit's place in run_alias —, bit 2 same store)
   for (uint32_t g = 0; g < G; g++) {
     const uint32_t w = A[g].w;
     const bool cls = P.per_second && (A[g].mask & 1u);
     uint32_t tm = 0;
+    uint32_t sl[4];
+    for (uint32_t k = 0; k < 4; k++) sl[k] = (present >> k) & 1 ? (uint32_t)sidx[k] : 0xFFFFFFFFu;
     if (!F[g]) {
       for (uint32_t k = 0; k < 4; k++) {
         if (!((present >> k) & 1)) continue;
         uint32_t bits = cn[k].ws == w ? 1u : 0u;
+        if (!bits && ((lgr >> (4 * g + k)) & 1) && rolled[k] != LOG_NONE) {  // (its record rolled into the log)
+          sl[k] = rolled[k];
+          bits = 2u;
+        } else if ((lgm >> (4 * g + k)) & 1) {  // (rare: the hot key's group in another unit's log, once per batch)
+          Win R;
+          if (log_find(t, chain[k], (uint32_t)sidx[k], slot_tag(hs, k + 1), c[k].ws, w, &R) == 1) {
+            Slot* su = &t.slots[sidx[k]];
+            su->ring = log_append(t, (uint32_t)sidx[k], slot_tag(hs, k + 1), su->ring, cn[k].ws, R);
+            sl[k] = su->ring;
+            bits = 2u;
+          }
+        }
         if (bits && (P.per_second && k == 0) == cls) bits |= 4;
         tm |= bits << (3 * k);
       }
     }
     const uint32_t id = A[g].id;
     run_state[id] = make_uint4(tm, v0[g], lcm[g], F[g]);
-    run_alias[id] = sl;
+    run_alias[id] = make_uint4(sl[0], sl[1], sl[2], sl[3]);
     run_f[id] = 0xFFFFFFFFu;
     run_flags[id] = (g == 0 ? fl : run_flags[id]) | RUN_FAST | RUN_ALIAS;
     const uint32_t b0 = A[g].p >> 8, b1 = (A[g].end - 1) >> 8;
@@ -4152,14 +4181,16 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
       if (!masked) {
         const uint32_t nq = q + 1;
         const bool last = nq == run_end[r] || rec_s[nq].req > req_f;
-        if (last && (fl & RUN_ALIAS)) {  // the key's records in every unit slot (alias_setup's targets: curs)
+        if (last && (fl & RUN_ALIAS)) {  // the key's records in every unit slot (alias_setup's targets)
           const uint4 sl = run_alias[r];
 #pragma unroll
           for (uint32_t k = 0; k < 4; k++) {
             const uint32_t bits = (st.x >> (3 * k)) & 7u;
-            if (!(bits & 1u)) continue;
+            if (!(bits & 3u)) continue;
             const uint32_t idx = k == 0 ? sl.x : k == 1 ? sl.y : k == 2 ? sl.z : sl.w;
-            Win* R = &t.slots[idx].cur;
+            // a cur, or the new version alias_setup appended to the unit's history log
+            Win* R = (bits & 2u) ? &t.log[(size_t)(idx >> LOG_POS_BITS) * t.log_cap + (idx & LOG_POS_MASK)].w
+                                 : &t.slots[idx].cur;
             if (bits & 4u) {  // same store: INCRBY + EXPIRE
               R->count = after;
               R->expire = x.now + x.d;

@@ -64,6 +64,18 @@ def test_gpu_hot_override_stream_vs_c_oracle(lc, isolate):
     _check(_stream([37, 38, 39, 40, 41, 42]), lc, isolate=isolate)
 
 
+@pytest.mark.parametrize("lc,ps", [(False, False), (True, False), (True, True)])
+def test_gpu_hot_override_whole_minute_vs_c_oracle(lc, ps):
+    """Every second of a minute and into the next: the MINUTE key of a hot
+    overridden stem is also the SECOND key of the minute's first second, whose
+    record sits in the SECOND slot's cur at +41 (rolled away by that batch's
+    SECOND group: read from the roll's log entry) and in its history log from
+    +42 on (read there, written back to a new version). Both stay on the
+    parallel path (until round 5 the exact path replayed the stem by one lane
+    for the rest of the minute: C2U at 0.005 G decisions/s after 200 s)."""
+    _check(_stream(list(range(38, 104)), rpb=4_000, tenants=500, seed=13), lc, ps)
+
+
 @pytest.mark.parametrize("lc", [False, True])
 def test_gpu_hot_override_ten_thousand_element_runs_vs_c_oracle(lc):
     """60k requests per batch: the hottest stems' runs (~10k and ~5k
