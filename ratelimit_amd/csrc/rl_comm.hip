@@ -85,6 +85,7 @@ struct CommSlot {
   uint8_t* send_stem = nullptr;
   uint32_t* perm = nullptr;                // record -> slice index
   unsigned long long* hash = nullptr;      // [slice] stem hashes (the own chunk's owner batch reads them)
+  RouteBufs pb{};                          // the partition's scratch (slots' partitions may run concurrently)
   rl_batch src{};                          // the slice as partitioned (device view): the own chunk's source
   unsigned long long* cnt = nullptr;       // [2 x CNT_W x world]: sent per peer, then received
   Wire* recv_rec = nullptr;                // chunks of every source, rank order
@@ -186,7 +187,8 @@ int run_group(CommRouter* r, Engine* e, uint32_t ch, hipStream_t st) {
 }
 
 void free_slot(CommSlot& S) {
-  void* bufs[] = {S.send_rec, S.send_stem, S.perm, S.hash, S.cnt, S.recv_rec, S.recv_stem, S.ret_send, S.back, S.ostats,
+  void* bufs[] = {S.pb.dest, S.pb.hist, S.pb.start, S.send_rec, S.send_stem, S.perm, S.hash, S.cnt, S.recv_rec,
+                  S.recv_stem, S.ret_send, S.back, S.ostats,
                   S.stats_stage, S.h_stem, S.h_off, S.h_req, S.h_limit, S.h_hits, S.h_rule, S.h_now, S.h_unit,
                   S.h_flags, S.h_code, S.h_status, S.h_rem, S.h_reset, S.io_stats, S.h_cbuf};
   for (void* p : bufs)
@@ -441,7 +443,7 @@ int first_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s, const rl_batch
   unsigned long long* hc = r->alias && r->d_hcnt ? r->d_hcnt + (size_t)s * 2 * CNT_W * W : nullptr;
   if (!rc) {
     rc = eng_route_pack(e, in, W, me, S.send_rec, S.send_stem, S.perm, (uint64_t*)S.cnt, cs, CNT_W, S.n_rules,
-                        flags, r->own ? me : ROUTE_OWN_NONE, S.hash, hc);
+                        flags, r->own ? me : ROUTE_OWN_NONE, S.hash, hc, &S.pb);
     S.src = *in;  // (read by this batch's owner part, in the next call)
   }
   if (rc) {  // (a device-side malformation zeroes the counts itself and fails at rl_synchronize)
@@ -774,6 +776,8 @@ CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t*
     CommSlot& S = r->slot[s];
     ok = dalloc(&S.send_rec, g.max_batch) == hipSuccess && dalloc(&S.send_stem, (size_t)g.max_stem_bytes + 64) == hipSuccess &&
          dalloc(&S.perm, g.max_batch) == hipSuccess && dalloc(&S.hash, g.max_batch) == hipSuccess &&
+         dalloc(&S.pb.dest, g.max_batch) == hipSuccess && dalloc(&S.pb.start, 2 * (size_t)world + 1) == hipSuccess &&
+         dalloc(&S.pb.hist, 2ull * world * ((g.max_batch + ROUTE_TILE - 1) / ROUTE_TILE)) == hipSuccess &&
          dalloc(&S.cnt, 2 * CNT_W * (size_t)world) == hipSuccess &&
          dalloc(&S.back, g.max_batch) == hipSuccess &&
          dalloc(&S.stats_stage, (size_t)world * r->m_max) == hipSuccess &&

@@ -168,10 +168,20 @@ int eng_debug_decide(Engine* c, uint32_t n, const uint32_t* before, const uint32
                      uint8_t* lc_set);
 // counts: cstride u64 per owner (records, stem bytes[, meta0, meta1]: the
 // in-library router's counts message).
+// A partition's own scratch (the router's slots: partitions of consecutive
+// batches run on different pipeline streams, concurrently): owner per
+// descriptor [max_batch], per-tile counts [2 x n_shards x tiles], totals
+// [2 x n_shards + 1]. Null: the engine's single routing scratch (c->rs).
+struct RouteBufs {
+  uint8_t* dest;
+  uint32_t* hist;
+  uint32_t* start;
+};
 int eng_route_pack(Engine* c, const rl_batch* in, uint32_t n_shards, uint32_t src_rank, void* send_rec,
                    uint8_t* send_stem, uint32_t* perm, uint64_t* counts, void* stream, uint32_t cstride = 2,
                    uint64_t meta0 = 0, uint64_t meta1 = 0, uint32_t own_rank = ROUTE_OWN_NONE,
-                   unsigned long long* hash_out = nullptr, unsigned long long* counts_host = nullptr);
+                   unsigned long long* hash_out = nullptr, unsigned long long* counts_host = nullptr,
+                   const RouteBufs* bufs = nullptr);
 int eng_route_do_limit(Engine* c, uint32_t n, const void* recv_rec, const uint8_t* recv_stem, uint64_t recv_stem_bytes,
                        const uint64_t* src_stem_base, uint32_t n_shards, uint32_t n_rules, uint32_t rule_stride,
                        uint64_t* ret, uint64_t* stats, int isolate, void* stream);

@@ -598,7 +598,7 @@ void scratch_free(Scratch& s) {
 int eng_route_pack(Engine* c, const rl_batch* in, uint32_t n_shards, uint32_t src_rank, void* send_rec,
                    uint8_t* send_stem, uint32_t* perm, uint64_t* counts, void* stream, uint32_t cstride,
                    uint64_t meta0, uint64_t meta1, uint32_t own_rank, unsigned long long* hash_out,
-                   unsigned long long* counts_host) {
+                   unsigned long long* counts_host, const RouteBufs* bufs) {
   if (!c || !in || !counts || (in->n && (!send_rec || !send_stem || !perm)))
     return set_err(c, RL_E_INVALID, "gpu: null argument");
   if (n_shards < 1 || n_shards > RL_MAX_SHARDS || src_rank >= n_shards)
@@ -620,7 +620,13 @@ int eng_route_pack(Engine* c, const rl_batch* in, uint32_t n_shards, uint32_t sr
   }
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   BatchDev b = dev_view(c, in, c->cfg.max_stem_bytes);
-  launch_route_pack(b, n_shards, src_rank, (Wire*)send_rec, send_stem, perm, (unsigned long long*)counts, c->rs, st,
+  Scratch rs = c->rs;
+  if (bufs) {
+    rs.route_dest = bufs->dest;
+    rs.route_hist = bufs->hist;
+    rs.route_start = bufs->start;
+  }
+  launch_route_pack(b, n_shards, src_rank, (Wire*)send_rec, send_stem, perm, (unsigned long long*)counts, rs, st,
                     cstride, meta0, meta1, own_rank, hash_out, counts_host);
   HIPCHK(c, hipGetLastError());
   return RL_OK;
