@@ -23,8 +23,11 @@ namespace rl {
 constexpr uint32_t NBUF = RL_NBUF;
 // errw words: [0, NBUF) stage A of each buffer, [NBUF] (unused), [NBUF + 1]
 // the soft word (per-descriptor statuses), [NBUF + 2] the routing partition,
-// [ERRW_B0 + k] the table-stage word of buffer k's batch
-constexpr uint32_t ERRW_B0 = NBUF + 3, ERRW_WORDS = ERRW_B0 + NBUF;
+// [ERRW_B0 + j] the table-stage words, one per batch in a ring of ERRB_RING
+// (a batch's word is set at the end of its stage A, while up to NBUF - 1
+// earlier batches may still read theirs and their predecessors')
+constexpr uint32_t ERRB_RING = 2 * NBUF;
+constexpr uint32_t ERRW_B0 = NBUF + 3, ERRW_WORDS = ERRW_B0 + ERRB_RING;
 constexpr uint32_t PROF_RING = 8;  // timed batches in flight (> NBUF)
 constexpr uint32_t PROGRESS_RING = 64;  // batches rl_batch_progress tracks in flight
 
@@ -54,6 +57,8 @@ struct Engine {
   hipEvent_t caller_ready = nullptr; // eng_do_limit_async: the caller stream's work so far (the inputs)
   bool serial_debug = false;         // RL_DEBUG_SERIAL: async batches run serially on the caller's stream
   uint32_t next = 0, last = NBUF - 1;  // buffer of the next / of the latest batch
+  uint32_t errb_seq = NBUF;            // table-stage word of the next batch (ring position)
+  bool b_early = true;                 // k_b_begin at the end of stage A (RL_B_BEGIN_EARLY=0: in the table chain)
   uint64_t hash_seed = 0;
   HashKey hk{};
   // table

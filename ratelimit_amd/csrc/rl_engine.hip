@@ -123,7 +123,8 @@ int collect(Engine* c, hipStream_t st = nullptr) {
   HIPCHK(c, hipMemcpyAsync(c->h_err, c->errw, ERRW_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
   uint32_t e = c->h_err[NBUF + 2];  // the routing partition's word
-  for (uint32_t j = 0; j < NBUF; j++) e |= c->h_err[j] | c->h_err[ERRW_B0 + j];
+  for (uint32_t j = 0; j < NBUF; j++) e |= c->h_err[j];
+  for (uint32_t j = 0; j < ERRB_RING; j++) e |= c->h_err[ERRW_B0 + j];
   if (e || c->h_err[NBUF + 1]) {
     HIPCHK(c, hipMemsetAsync(c->errw, 0, ERRW_WORDS * sizeof(uint32_t), st));
     HIPCHK(c, hipStreamSynchronize(st));
@@ -144,23 +145,28 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
   const TableDev t = table_view(c);
   const int isolate = (!restore && o.status) ? 1 : 0;
   const Params P = params(c, isolate);
+  const uint32_t* errb_prev = c->s[c->last].errb;  // the previous batch's table-stage word
+  c->s[k].errb = c->errw + ERRW_B0 + (c->errb_seq++ % ERRB_RING);
+  const bool early = c->b_early;
   if (pipelined) {
     hipStream_t a = c->pipe[k];
     hipEvent_t* ev = prof_events(c);
     (void)hipStreamWaitEvent(a, c->b_done[k], 0);    // buffer k's previous batch is done
     (void)hipStreamWaitEvent(a, c->consumed[k], 0);  // ... and its routed results were read
     launch_stage_a(b, c->s[k], isolate, P.per_second, a, ev);
+    if (early) launch_b_begin_early(b, o, c->s[k], restore, a);  // (off the table-order chain)
     (void)hipStreamWaitEvent(a, c->b_table[c->last], 0);  // table order (not the previous k_finish)
-    launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, c->s[c->last].errb, c->b_table[k],
-                   c->prof ? c->d_kt_acc : nullptr);
+    launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
+                   early);
     (void)hipEventRecord(c->b_done[k], a);
   } else {
     if (!st) st = c->stream;
     (void)after_batches(c, st);
     hipEvent_t* ev = prof_events(c);
     launch_stage_a(b, c->s[k], isolate, P.per_second, st, ev);
-    launch_stage_b(b, o, t, P, c->s[k], restore, st, ev, c->s[c->last].errb, c->b_table[k],
-                   c->prof ? c->d_kt_acc : nullptr);
+    if (early) launch_b_begin_early(b, o, c->s[k], restore, st);
+    launch_stage_b(b, o, t, P, c->s[k], restore, st, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
+                   early);
     (void)hipEventRecord(c->b_done[k], st);
   }
   c->last = k;
@@ -390,6 +396,7 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   const uint32_t n = cfg.max_batch;
   bool ok = true;
   for (uint32_t k = 0; k < NBUF; k++) ok = ok && rl_stream_create(&c->pipe[k], SR_PIPE) == hipSuccess;
+  if (const char* be = getenv("RL_B_BEGIN_EARLY")) c->b_early = atoi(be) != 0;  // (A/B knob)
   c->stream = c->pipe[0];
   for (uint32_t k = 0; k < NBUF; k++)
     ok = ok && hipEventCreateWithFlags(&c->b_done[k], hipEventDisableTiming) == hipSuccess &&

@@ -253,9 +253,12 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
 // kt_acc (optional, rl_profile on): k_table's duration on the device clock
 // (first workgroup start to last workgroup end) added to kt_acc[0], and 1 to
 // kt_acc[1], by k_finish.
+// early: k_b_begin already ran (launch_b_begin_early, end of stage A); k_table
+// folds errb_prev into this batch's word.
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
                     int restore, hipStream_t st, hipEvent_t* ev, const uint32_t* errb_prev, hipEvent_t table_done,
-                    unsigned long long* kt_acc = nullptr);
+                    unsigned long long* kt_acc = nullptr, bool early = false);
+void launch_b_begin_early(const BatchDev& b, const OutDev& o, const Scratch& s, int restore, hipStream_t st);
 // ev (optional, RL_NUM_STAGES + 1 events on stream st): recorded before
 // k_prepare, after it, after the sort, just before and just after k_table, and
 // at the end (per-stage timing, rl_profile).

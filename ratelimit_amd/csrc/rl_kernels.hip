@@ -3652,10 +3652,10 @@ __device__ __attribute__((always_inline)) inline void unique_body(uint32_t blk, 
                                                 unsigned long long* __restrict__ res,
                                                 uint32_t* __restrict__ defer1, uint32_t* defer1_n,
                                                 unsigned long long* stats, unsigned long long* stripes, uint32_t* err,
-                                                uint32_t* errs, int restore) {
+                                                uint32_t* errs, int restore, const uint32_t* errb_prev) {
   __shared__ uint32_t s_err, s_nu, s_cnt, s_list[256];
   if (threadIdx.x == 0) {
-    s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | (errb_prev ? *errb_prev : 0u);
     s_nu = *uniq_n;
   }
   __syncthreads();
@@ -3966,11 +3966,12 @@ __device__ __attribute__((always_inline)) inline void runs_body(uint32_t blk, Ba
                                               const uint32_t* __restrict__ drun,
                                               uint32_t* __restrict__ defer, uint32_t* defer_n,
                                               unsigned long long* stats, unsigned long long* stripes, uint32_t* err,
-                                              uint32_t* errs, int restore, uint32_t* __restrict__ fast_blk) {
+                                              uint32_t* errs, int restore, uint32_t* __restrict__ fast_blk,
+                                              const uint32_t* errb_prev) {
   __shared__ uint32_t s_err, s_nr, s_cnt, s_list[256];
   // err may change while this kernel runs (other blocks): read it once per block
   if (threadIdx.x == 0) {
-    s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | (errb_prev ? *errb_prev : 0u);
     s_nr = (uint32_t)(*num_runs >> 32);  // runs of two or more (drun)
   }
   __syncthreads();
@@ -4437,17 +4438,25 @@ __global__ __launch_bounds__(256, RL_KTABLE_WAVES) void k_table(uint32_t g_runs,
                                                uint32_t* defer1_n, unsigned long long* stats,
                                                unsigned long long* stripes, uint32_t* err, uint32_t* errs, int restore,
                                                uint32_t* __restrict__ fast_blk, const uint2* __restrict__ uniq,
-                                               const uint32_t* uniq_n, unsigned long long* __restrict__ kt) {
+                                               const uint32_t* uniq_n, unsigned long long* __restrict__ kt,
+                                               const uint32_t* errb_prev) {
   // kt (rl_profile on): each workgroup's start and end on the device's
   // constant clock, plain stores (one address for all of them serialised the
   // launch: +40 %); k_finish folds them into the launch's duration
   if (kt && threadIdx.x == 0) kt[2 * blockIdx.x] = wall_clock64();
+  // early table-stage begin (errb_prev set): this batch's word holds its own
+  // validation only; the previous batch's (final: the table order) is folded
+  // in here, and every block checks both
+  if (errb_prev && blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint32_t p = *errb_prev;
+    if (p) atomicOr(err, p);
+  }
   if (blockIdx.x < g_runs)
     runs_body(blockIdx.x, b, t, P, rec_s, skeys, svals, res, run_start, run_end, run_flags, run_state, run_alias, rid,
-              run_f, num_runs, drun, defer2, defer2_n, stats, stripes, err, errs, restore, fast_blk);
+              run_f, num_runs, drun, defer2, defer2_n, stats, stripes, err, errs, restore, fast_blk, errb_prev);
   else
     unique_body(blockIdx.x - g_runs, b, t, P, rec_s.rec, keys0, uniq, uniq_n, res, defer1, defer1_n, stats, stripes,
-                err, errs, restore);
+                err, errs, restore, errb_prev);
   if (kt && threadIdx.x == 0) kt[2 * blockIdx.x + 1] = wall_clock64();
 }
 
@@ -4505,7 +4514,7 @@ __global__ __launch_bounds__(256) void k_b_begin(const uint32_t* __restrict__ er
   if (i == 0) {
     // this batch's table-stage word: the previous batch's (sticky: a failed
     // batch fails every later one) | this batch's validation result
-    *errb = *errb_prev | *erra;
+    *errb = (errb_prev ? *errb_prev : 0u) | *erra;
     *defer_n = 0;
     *defer1_n = 0;
   }
@@ -4797,13 +4806,27 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
 #ifndef RL_LATE_FAST_BLOCKS
 #define RL_LATE_FAST_BLOCKS 0  // cap on k_late's long-run workgroups (0: one per 256 descriptors)
 #endif
-void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
-                    int restore, hipStream_t st, hipEvent_t* ev, const uint32_t* errb_prev, hipEvent_t table_done,
-                    unsigned long long* kt_acc) {
+// The table stage's first kernel, early (before the table-order wait, at the
+// end of stage A): this batch's table-stage word = its own validation, its
+// deferral counters, block bitmap and output stats cleared. k_table folds the
+// previous batch's word in (launch_stage_b with early set).
+void launch_b_begin_early(const BatchDev& b, const OutDev& o, const Scratch& s, int restore, hipStream_t st) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
-  k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, errb_prev, s.defer2_n, s.defer1_n, o.stats, m, s.fast_blk,
+  k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, nullptr, s.defer2_n, s.defer1_n, o.stats, m, s.fast_blk,
                                 cdiv(b.n, 256 * 32));
+}
+
+void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
+                    int restore, hipStream_t st, hipEvent_t* ev, const uint32_t* errb_prev, hipEvent_t table_done,
+                    unsigned long long* kt_acc, bool early) {
+  const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
+  const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
+  if (!early)
+    k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, errb_prev, s.defer2_n, s.defer1_n, o.stats, m, s.fast_blk,
+                                  cdiv(b.n, 256 * 32));
+  else if (!b.n)  // (no k_table to fold the previous batch's word in)
+    k_b_begin<<<1, 256, 0, st>>>(s.errb, s.errb, errb_prev, s.defer2_n, s.defer1_n, o.stats, 0, s.fast_blk, 0);
   if (b.n) {
     const uint32_t g = cdiv(b.n, 256);
     const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
@@ -4817,7 +4840,8 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
                                          s.run_flags, s.run_state, s.run_alias, s.rid, s.run_f, s.runs64, s.drun,
                                          s.defer2, s.defer2_n,
                                          s.keys[0], s.defer1, s.defer1_n, o.stats, s.stripes, s.errb, s.errs, restore,
-                                         s.fast_blk, s.uniq, s.uniq_n, kt_acc ? s.kt_blk : nullptr);
+                                         s.fast_blk, s.uniq, s.uniq_n, kt_acc ? s.kt_blk : nullptr,
+                                         early ? errb_prev : nullptr);
     if (ev) (void)hipEventRecord(ev[4], st);
     if (!restore && P.lc_en)
       k_fast_over<<<g, 256, 0, st>>>(s.sorted_n, rs, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
