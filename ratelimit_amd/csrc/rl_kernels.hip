@@ -4422,7 +4422,7 @@ __device__ __attribute__((always_inline)) inline void general_body(uint32_t blk,
 // k_table: the runs of two or more (runs_body, blocks [0, g_runs)) and the keys
 // seen once (unique_body, the rest).
 #ifndef RL_KTABLE_WAVES
-#define RL_KTABLE_WAVES 1  // (A/B builds: a floor on k_table's waves per SIMD)
+#define RL_KTABLE_WAVES 5  // waves per SIMD: <= 96 VGPRs (110 uncapped: 4 waves); 5 vs 1: C1 +1.2 %, C2 +0.8 %, C2U -0.3 %; 6 / 8 spill in the hot path: C1 -6 / -12 % (profiles/r05/ktable_waves)
 #endif
 __global__ __launch_bounds__(256, RL_KTABLE_WAVES) void k_table(uint32_t g_runs, BatchDev b, TableDev t, Params P, SRec rec_s,
                                                const uint32_t* __restrict__ skeys,
