@@ -243,6 +243,7 @@ def main():
     torch.cuda.synchronize()
 
     step = [0]
+    host_delay = float(os.environ.get("RL_BENCH_HOST_DELAY_US", "0")) * 1e-6
     host_in_call = [0.0]  # host seconds inside the library's submit calls (timed steps only)
 
     def run_step():
@@ -252,6 +253,9 @@ def main():
         t = time.perf_counter()
         do_step(inp, n, nq)
         host_in_call[0] += time.perf_counter() - t
+        if host_delay:  # (RL_BENCH_HOST_DELAY_US: a slower submitter, to see whether the host paces the GPU)
+            while time.perf_counter() - t < host_delay:
+                pass
         step[0] += 1
 
     # ---- warmup
