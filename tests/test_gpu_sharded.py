@@ -160,3 +160,20 @@ def test_gpu_rccl_router_matches_oracle(kind, local_cache, pipelined, part, alia
             assert bad.size == 0, (k, f, bad.size, bad[:8].tolist(), out[0][k][i][bad[:8]].tolist(),
                                    exp[f][bad[:8]].tolist(), arrays["req_idx"][bad[:8]].tolist())
         assert np.array_equal(out[0][k][3], exp["stats"][:n_rules * abi.RL_NUM_STATS]), k
+
+
+def test_gpu_rccl_router_many_large_batches_pipelined():
+    """24 C2 batches of 120k descriptors submitted back to back before one
+    finish(): partitions of consecutive batches run on different pipeline
+    streams, concurrently (round 5), each on its slot's own scratch (a shared
+    one gave a bench run garbage counts), and RL_ROUTED_LAG batches are
+    pending at any time. Every answer and stat equals the C oracle's."""
+    cfg = (0.8, True, False)
+    batches = list(W.c2_stream(seed=23, n_tenants=50_000, requests_per_batch=60_000, batches=24))
+    out = _run(1, "nccl", batches, cfg, True, impl="rccl", max_batch=1 << 18)
+    co = COracle(*cfg)
+    for k, (arrays, n, nq, n_rules) in enumerate(batches):
+        exp = co.do_limit(arrays, n, nq, n_rules)
+        for f, i in (("code", 0), ("limit_remaining", 1), ("reset_s", 2)):
+            assert np.array_equal(out[0][k][i], exp[f]), (k, f)
+        assert np.array_equal(out[0][k][3], exp["stats"][:n_rules * abi.RL_NUM_STATS]), k
