@@ -44,7 +44,12 @@ constexpr uint32_t RUN_G_SHIFT = 8, RUN_UMASK_SHIFT = 16;  // group count (head)
 // k_run_check's verdict on a RUN_MULTI run (k_split reads it): some element has
 // the head's stem under another unit / some element has another stem or failed
 constexpr uint32_t RUN_UNITS = 128, RUN_STEMS = 1u << 24;
-constexpr uint32_t KEY_HEAD = 64;         // stem bytes carried inline (zero-padded) per descriptor
+#ifndef RL_KEY_HEAD
+#define RL_KEY_HEAD 64
+#endif
+constexpr uint32_t KEY_HEAD = RL_KEY_HEAD;  // stem bytes carried inline (zero-padded) per descriptor (a multiple of 16)
+constexpr uint32_t KEY_HV = KEY_HEAD / 16;  // ... as uint4s
+static_assert(KEY_HEAD % 16 == 0 && KEY_HEAD >= 48 && KEY_HEAD <= 64, "key head: 48 or 64 bytes (>= KEY_IN)");
 constexpr uint32_t STAT_STRIPES = 64;     // global partial stats tables
 constexpr uint32_t STAT_LDS_RULES = 512;  // rules aggregated in LDS (== LDS_RULES)
 constexpr uint32_t RUNS_GENERAL_LATE_BLOCKS = 8;  // k_late's exact-path workgroups (grid-stride over deferrals)

@@ -497,15 +497,15 @@ void launch_unpack_prefixed(const rl_batch_prefixed& pb, const uint8_t* buf, uin
 // stems, as 4 x uint4: five aligned 16-B loads, then dword selects and funnel
 // shifts. Only chunks holding a byte of the head are loaded, so no load leaves
 // the 16-B blocks (hence the pages) the stem occupies.
-__device__ inline void load_head(const uint8_t* stem, uint32_t off, uint32_t len, uint4 out[4]) {
+__device__ inline void load_head(const uint8_t* stem, uint32_t off, uint32_t len, uint4 out[KEY_HV]) {
   const uint32_t hl = len < KEY_HEAD ? len : KEY_HEAD;
   const uint32_t mis = (uint32_t)((uintptr_t)stem & 15u);
   const uint4* c16 = reinterpret_cast<const uint4*>(stem - mis);
   const uint32_t a = off + mis;
   const uint32_t c0 = a >> 4, last = (a + (hl ? hl : 1u) - 1u) >> 4;
-  uint32_t w[20];
+  uint32_t w[4 * (KEY_HV + 1)];
 #pragma unroll
-  for (uint32_t j = 0; j < 5; j++) {
+  for (uint32_t j = 0; j < KEY_HV + 1; j++) {
     const uint4 v = c0 + j <= last ? c16[c0 + j] : make_uint4(0u, 0u, 0u, 0u);
     w[4 * j] = v.x;
     w[4 * j + 1] = v.y;
@@ -513,19 +513,19 @@ __device__ inline void load_head(const uint8_t* stem, uint32_t off, uint32_t len
     w[4 * j + 3] = v.w;
   }
   const uint32_t q = (a >> 2) & 3u, sb = a & 3u;
-  uint32_t x[17];
+  uint32_t x[4 * KEY_HV + 1];
 #pragma unroll
-  for (uint32_t k = 0; k < 17; k++) x[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
-  uint32_t o[16];
+  for (uint32_t k = 0; k < 4 * KEY_HV + 1; k++) x[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
+  uint32_t o[4 * KEY_HV];
 #pragma unroll
-  for (uint32_t k = 0; k < 16; k++) {
+  for (uint32_t k = 0; k < 4 * KEY_HV; k++) {
     uint32_t v = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sb);
     if (4 * k >= hl) v = 0;
     else if (4 * k + 4 > hl) v &= (1u << ((hl - 4 * k) * 8)) - 1u;
     o[k] = v;
   }
 #pragma unroll
-  for (uint32_t v = 0; v < 4; v++) out[v] = make_uint4(o[4 * v], o[4 * v + 1], o[4 * v + 2], o[4 * v + 3]);
+  for (uint32_t v = 0; v < KEY_HV; v++) out[v] = make_uint4(o[4 * v], o[4 * v + 1], o[4 * v + 2], o[4 * v + 3]);
 }
 
 // ===========================================================================
@@ -565,7 +565,7 @@ __device__ inline bool stem_words_equal(const StemRef& x, const StemRef& y, uint
 // (read from the packed stems with aligned 16-B loads) and, for stems longer
 // than 64 B only, the rest through a StemRef.
 struct Key {
-  uint4 h[4];
+  uint4 h[KEY_HV];
   StemRef st;  // full stem (bytes >= KEY_HEAD read from here)
   uint32_t len;
 };
@@ -597,14 +597,14 @@ __device__ inline Key key_at(const BatchDev& b, SRec rec_s, uint32_t q) { return
 __device__ inline uint32_t head_diff(const uint4* x, const uint4* y) {
   uint32_t d = 0;
 #pragma unroll
-  for (uint32_t v = 0; v < 4; v++) {
+  for (uint32_t v = 0; v < KEY_HV; v++) {
     const uint4 a = x[v], c = y[v];
     d |= (a.x ^ c.x) | (a.y ^ c.y) | (a.z ^ c.z) | (a.w ^ c.w);
   }
   return d;
 }
 
-// bytes [64, len) of two stems (words 16.. of their StemRefs)
+// bytes [KEY_HEAD, len) of two stems (words KEY_HEAD / 4.. of their StemRefs)
 __device__ inline uint32_t tail_diff(const StemRef& x, const StemRef& y, uint32_t len) {
   uint32_t d = 0;
   const uint32_t nw = len >> 2;
