@@ -100,6 +100,13 @@ struct Engine {
   uint32_t *d_rem = nullptr, *d_reset = nullptr;
   unsigned long long* d_stats = nullptr;
   uint32_t* h_err = nullptr;  // pinned [4]
+  // k_split_long (the runs over 1024 elements on 1024-lane workgroups) is
+  // launched only while recent batches had such runs: k_split writes a
+  // buffer's word when it meets one; an empty launch of 1024-lane workgroups
+  // costs C1 / C2 about 1-2.5 % (profiles/r05/split_long/)
+  uint32_t* h_long = nullptr;  // pinned [NBUF]
+  uint32_t long_recent = 0;    // batches left in long-run mode
+  int long_mode = 1;           // RL_SPLIT_LONG: 0 never, 1 while recent batches had long runs, 2 always
   unsigned long long* h_counters = nullptr;
   std::string last_error;
   uint64_t batches = 0, decisions = 0;

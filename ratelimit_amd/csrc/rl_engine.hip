@@ -148,12 +148,23 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
   const uint32_t* errb_prev = c->s[c->last].errb;  // the previous batch's table-stage word
   c->s[k].errb = c->errw + ERRW_B0 + (c->errb_seq++ % ERRB_RING);
   const bool early = c->b_early;
+  bool lng = c->long_mode == 2;  // k_split_long for this batch: a recent batch had a run over 1024 elements
+  if (c->long_mode == 1) {
+    for (uint32_t j = 0; j < NBUF; j++)
+      if (__atomic_load_n(&c->h_long[j], __ATOMIC_RELAXED)) {
+        __atomic_store_n(&c->h_long[j], 0u, __ATOMIC_RELAXED);
+        c->long_recent = 4 * NBUF;
+      }
+    lng = c->long_recent > 0;
+    if (c->long_recent) c->long_recent--;
+  }
+  uint32_t* hint = c->long_mode ? c->h_long + k : nullptr;
   if (pipelined) {
     hipStream_t a = c->pipe[k];
     hipEvent_t* ev = prof_events(c);
     (void)hipStreamWaitEvent(a, c->b_done[k], 0);    // buffer k's previous batch is done
     (void)hipStreamWaitEvent(a, c->consumed[k], 0);  // ... and its routed results were read
-    launch_stage_a(b, c->s[k], isolate, P.per_second, a, ev);
+    launch_stage_a(b, c->s[k], isolate, P.per_second, a, ev, hint, lng);
     if (early) launch_b_begin_early(b, o, c->s[k], restore, a);  // (off the table-order chain)
     (void)hipStreamWaitEvent(a, c->b_table[c->last], 0);  // table order (not the previous k_finish)
     launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
@@ -163,7 +174,7 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     if (!st) st = c->stream;
     (void)after_batches(c, st);
     hipEvent_t* ev = prof_events(c);
-    launch_stage_a(b, c->s[k], isolate, P.per_second, st, ev);
+    launch_stage_a(b, c->s[k], isolate, P.per_second, st, ev, hint, lng);
     if (early) launch_b_begin_early(b, o, c->s[k], restore, st);
     launch_stage_b(b, o, t, P, c->s[k], restore, st, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
                    early);
@@ -271,6 +282,7 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
        dalloc(&s.defer1, n) == hipSuccess && dalloc(&s.defer1_n, 1) == hipSuccess &&
        dalloc(&s.defer2_n, 1) == hipSuccess && dalloc(&s.fast_blk, (size_t)n / (256 * 32) + 1) == hipSuccess &&
        dalloc(&s.uniq, n) == hipSuccess && dalloc(&s.uniq_n, 1) == hipSuccess &&
+       dalloc(&s.long_runs, (size_t)n / 1024 + 2) == hipSuccess &&
        dalloc(&s.kt_blk, 2 * ((size_t)n / 2 + BIG_HEAVY * PART_DIGITS + 2 * (size_t)n + 512) / 256) == hipSuccess;
   ok = ok && dalloc(&s.hits_s, n) == hipSuccess && dalloc(&s.segsum, n) == hipSuccess &&
        dalloc(&s.rid, n) == hipSuccess && dalloc(&s.run_start, (size_t)n + 1) == hipSuccess &&
@@ -290,7 +302,7 @@ void free_buffer(Scratch& s) {
                   s.vals[0], s.vals[1], s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1,
                   s.defer1_n, s.fast_blk, s.hits_s, s.segsum, s.rid, s.run_start, s.run_flags, s.run_state, s.run_alias,
                   s.run_f, s.runs64, s.split, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t, s.r_base,
-                  s.uniq, s.uniq_n, s.kt_blk};
+                  s.uniq, s.uniq_n, s.long_runs, s.kt_blk};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
 }
@@ -445,6 +457,9 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && dalloc(&c->d_stats, (size_t)cfg.max_rules * RL_NUM_STATS) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_err, ERRW_WORDS * sizeof(uint32_t)) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_counters, 8 * sizeof(unsigned long long)) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_long, NBUF * sizeof(uint32_t)) == hipSuccess;
+  if (ok) memset(c->h_long, 0, NBUF * sizeof(uint32_t));
+  if (const char* sl = getenv("RL_SPLIT_LONG")) c->long_mode = atoi(sl);  // (A/B knob)
   if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
   ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
        hipMemsetAsync(c->log_ctr, 0, (size_t)(LOG_PARTS + 1) * LOG_CTR_STRIDE * 8, c->stream) == hipSuccess &&
@@ -538,6 +553,7 @@ void eng_destroy(Engine* c) {
     if (c->s[k].stripes) (void)hipFree(c->s[k].stripes);
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
+  if (c->h_long) (void)hipHostFree(c->h_long);
   for (void* p : {(void*)c->cfg_blob, (void*)c->mbuf})
     if (p) (void)hipFree(p);
   if (c->h_match) (void)hipHostFree(c->h_match);

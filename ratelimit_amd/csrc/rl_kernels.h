@@ -213,6 +213,7 @@ struct Scratch {
   // fall in (address-translation reach, tools/tlbprobe.hip)
   uint2* uniq;
   uint32_t* uniq_n;
+  uint32_t* long_runs;  // [1 + n / 1024 + 1] runs over SPLIT_CAP elements: count, then defer indices (k_split_long)
   unsigned long long* kt_blk;  // [2 x k_table workgroups] start / end stamps (rl_profile)
   unsigned long long* stripes;    // STAT_STRIPES x STAT_LDS_RULES x RL_NUM_STATS
   // run segmentation (sorted order)
@@ -250,8 +251,11 @@ struct Scratch {
 // only the batch and this buffer's scratch, so it may overlap the previous
 // batch's stage B; stage B (table probe, replay, decisions, stats, results)
 // must run in batch order.
+// long_hint: a host word k_split sets when it meets a run over 1024 elements;
+// long_kernel: such runs go to k_split_long's 1024-lane workgroups (else
+// k_split's own 256-lane ones walk them)
 void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_second, hipStream_t st,
-                    hipEvent_t* ev = nullptr);
+                    hipEvent_t* ev = nullptr, uint32_t* long_hint = nullptr, bool long_kernel = false);
 // errb_prev: the previous batch's table-stage word (this batch's starts from
 // it); table_done (optional) is recorded once the table kernels are done, before
 // k_finish: the next batch's stage B waits for it, not for k_finish.

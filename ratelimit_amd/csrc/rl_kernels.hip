@@ -2442,6 +2442,32 @@ __device__ inline uint32_t wave_sum32(uint32_t x) {
   return x;
 }
 
+// Inclusive sum over the wave's lanes (all 64 active) by DPP: row_shr 1, 2, 4,
+// 8 inside each row of 16, then row_bcast 15 / 31 carry each row's total into
+// the rows above. Twelve VALU operations; __shfl_up's six levels are six
+// ds_bpermute round trips through the LDS crossbar plus their address math.
+#ifndef RL_DPP_SCAN
+#define RL_DPP_SCAN 1
+#endif
+__device__ __attribute__((always_inline)) inline uint32_t wave_incl_add(uint32_t x) {
+#if RL_DPP_SCAN
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 (rows 1, 3)
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 (rows 2, 3)
+#else
+  const uint32_t lane = __lane_id();
+#pragma unroll
+  for (uint32_t off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+#endif
+  return x;
+}
+
 // Load one chunk of a queued bucket (BkSmall shape) and classify it: cls =
 // hot key index c < r, r for a light element, 0xFF past the bucket.
 __device__ inline void big_chunk_load(const BigMeta& M, uint32_t j, uint32_t ntiles, const uint4* __restrict__ pt,
@@ -2589,18 +2615,13 @@ __global__ __launch_bounds__(BkSmall::THREADS) void k_big_place(
         if (c >= M.r) continue;  // uniform
         const bool mine = cls[i] == c;
         const uint64_t b = __ballot(mine);
-        uint32_t x = mine ? hv : 0u;  // inclusive scan of the class's hits over the lanes
-#pragma unroll
-        for (uint32_t off = 1; off < 64; off <<= 1) {
-          const uint32_t y = __shfl_up(x, off, 64);
-          if (lane >= off) x += y;
-        }
+        const uint32_t x = wave_incl_add(mine ? hv : 0u);  // inclusive scan of the class's hits over the lanes
         if (mine) {
           rk[i] = wc[c] + __popcll(b & lt_mask);
           hp[i] = wh[c] + x;
         }
         wc[c] += __popcll(b);
-        wh[c] += __shfl(x, 63, 64);
+        wh[c] += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
       }
     }
     if (lane == 0) {
@@ -2780,11 +2801,12 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
                                                    const unsigned long long* num_runs, unsigned long long* split,
                                                    const uint32_t* sorted_n, uint32_t* __restrict__ pos_unit,
                                                    uint32_t* __restrict__ pos_hits, uint2* __restrict__ uniq,
-                                                   uint32_t* uniq_n) {
+                                                   uint32_t* uniq_n, uint32_t* long_runs) {
   __shared__ uint32_t s_list[RC_CHUNK], s_cnt;
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // k_split's reservations start from the bucket kernels' count
     split[0] = 0;
     split[1] = *num_runs;
+    long_runs[0] = 0;
   }
   if (*err) return;
   const uint32_t sn = *sorted_n;
@@ -2990,6 +3012,20 @@ constexpr uint32_t SPLIT_UNROLL = 8;
 constexpr uint32_t SPLIT_ST = RL_SPLIT_ST;  // 64-element steps in flight per wave in split_long_body's walks
 // k_split's workgroup (a long run is reordered by its waves, each walking a
 // chunk of it: more waves, shorter walks, but slower short runs)
+// k_split_long's workgroup (0: k_split's own workgroups walk the long runs)
+// and its steps in flight per wave (<= 128 VGPRs at 1024 lanes)
+#ifndef RL_SPLIT_LONG_THREADS
+#define RL_SPLIT_LONG_THREADS 1024
+#endif
+#ifndef RL_SPLIT_LONG_ST
+#define RL_SPLIT_LONG_ST 8
+#endif
+#ifndef RL_SPLIT_LONG_OCC
+#define RL_SPLIT_LONG_OCC 4  // k_split_long's minimum waves per SIMD (8: <= 64 VGPRs)
+#endif
+#ifndef RL_SPLIT_LONG_BLOCKS
+#define RL_SPLIT_LONG_BLOCKS 8
+#endif
 #ifndef RL_SPLIT_THREADS
 #define RL_SPLIT_THREADS 256  // (1024: C2U's 58k-element runs 481 -> 377 us, but C1's k_split 18 -> 26 us;
                               //  512 in round 4: C2U +2.4 %, C2 -4 %, C1 -1.5 %)
@@ -3005,7 +3041,7 @@ struct UniqList {
   __device__ inline void push(uint32_t e, uint32_t p) const { list[atomicAdd(n, 1u)] = make_uint2(e, skeys[p]); }
 };
 
-template <uint32_t NT>
+template <uint32_t NT, uint32_t ST>
 __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j, uint32_t r, uint32_t p, uint32_t L, BatchDev b,
                                                           SRec rec_s, uint32_t* svals, uint32_t* segsum,
                                                           uint32_t* __restrict__ rid, uint32_t* __restrict__ run_start,
@@ -3195,16 +3231,16 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
       uint32_t cl[SPLIT_MAXG], hl[SPLIT_MAXG];
 #pragma unroll
       for (uint32_t g = 0; g < SPLIT_MAXG; g++) cl[g] = hl[g] = 0;
-      for (uint32_t c = a0; c < a1; c += 64 * SPLIT_ST) {
-        uint32_t fu[SPLIT_ST], h[SPLIT_ST];
+      for (uint32_t c = a0; c < a1; c += 64 * ST) {
+        uint32_t fu[ST], h[ST];
 #pragma unroll
-        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+        for (uint32_t st = 0; st < ST; st++) {
           const uint32_t k = c + st * 64 + lane;
           fu[st] = k < a1 ? grp[p + k] : 0xFFFFFFFFu;
           h[st] = k < a1 ? pos_hits[p + k] : 0u;
         }
 #pragma unroll
-        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+        for (uint32_t st = 0; st < ST; st++) {
           if (fu[st] == 0xFFFFFFFFu) continue;
           const uint32_t gk = s_plan.ug[fu[st] & 0xFFu][((fu[st] >> 8) & 0xFFu) - 1];
 #pragma unroll
@@ -3286,25 +3322,25 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
       for (uint32_t w = 0; w < NW; w++) acc[w] = 0;
       // (software-pipelined: the next ST steps' loads are issued before this
       // step's stores, so waiting for them never waits for the stores)
-      uint32_t fu[SPLIT_ST], e[SPLIT_ST], h[SPLIT_ST];
+      uint32_t fu[ST], e[ST], h[ST];
 #pragma unroll
-      for (uint32_t st = 0; st < SPLIT_ST; st++) {
+      for (uint32_t st = 0; st < ST; st++) {
         const uint32_t k = a0 + st * 64 + lane;
         fu[st] = k < a1 ? grp[p + k] : 0xFFFFFFFFu;
         e[st] = k < a1 ? sv[p + k] : 0u;
         h[st] = k < a1 ? pos_hits[p + k] : 0u;
       }
-      for (uint32_t c = a0; c < a1; c += 64 * SPLIT_ST) {
-        uint32_t fn[SPLIT_ST], en[SPLIT_ST], hn[SPLIT_ST];
+      for (uint32_t c = a0; c < a1; c += 64 * ST) {
+        uint32_t fn[ST], en[ST], hn[ST];
 #pragma unroll
-        for (uint32_t st = 0; st < SPLIT_ST; st++) {
-          const uint32_t k = c + (SPLIT_ST + st) * 64 + lane;
+        for (uint32_t st = 0; st < ST; st++) {
+          const uint32_t k = c + (ST + st) * 64 + lane;
           fn[st] = k < a1 ? grp[p + k] : 0xFFFFFFFFu;
           en[st] = k < a1 ? sv[p + k] : 0u;
           hn[st] = k < a1 ? pos_hits[p + k] : 0u;
         }
 #pragma unroll
-        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+        for (uint32_t st = 0; st < ST; st++) {
           const uint32_t gk =
               fu[st] == 0xFFFFFFFFu ? 0xFFu : s_plan.ug[fu[st] & 0xFFu][((fu[st] >> 8) & 0xFFu) - 1];
           uint32_t np = 0;
@@ -3319,12 +3355,14 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
           rank[p + np] = e[st];
           rid[p + np] = s_id[gk];
           hnew[p + np] = h[st];
-          uint32_t dw = 0;  // the wave whose chunk of the new order np is in
+          if constexpr (NW <= 4) {  // (more waves: walk 3 sums its chunks in a pass of its own)
+            uint32_t dw = 0;  // the wave whose chunk of the new order np is in
 #pragma unroll
-          for (uint32_t w = 1; w < NW; w++) dw += np >= w * CH ? 1u : 0u;
+            for (uint32_t w = 1; w < NW; w++) dw += np >= w * CH ? 1u : 0u;
 #pragma unroll
-          for (uint32_t w = 0; w < NW; w++)
-            if (dw == w) acc[w] += h[st];
+            for (uint32_t w = 0; w < NW; w++)
+              if (dw == w) acc[w] += h[st];
+          }
           if (!s_plan.alias[gk]) {  // (a multi-unit stem's groups share one `now`)
             const uint32_t f = s_plan.fam[gk];
             // (the head's family: k_run_check compared `now` with the head's,
@@ -3344,19 +3382,28 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
           }
         }
 #pragma unroll
-        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+        for (uint32_t st = 0; st < ST; st++) {
           fu[st] = fn[st];
           e[st] = en[st];
           h[st] = hn[st];
         }
       }
+      if constexpr (NW <= 4) {
 #pragma unroll
-      for (uint32_t w = 0; w < NW; w++) {
-        const uint32_t t = wave_sum32(acc[w]);
-        if (lane == 0 && t) atomicAdd(&s_ws[w], t);
+        for (uint32_t w = 0; w < NW; w++) {
+          const uint32_t t = wave_sum32(acc[w]);
+          if (lane == 0 && t) atomicAdd(&s_ws[w], t);
+        }
       }
     }
     __syncthreads();
+    if constexpr (NW > 4) {  // each wave's chunk of the new order: its hits, summed
+      uint32_t t = 0;
+      for (uint32_t k = a0 + lane; k < a1; k += 64) t += hnew[p + k];
+      t = wave_sum32(t);
+      if (lane == 0) s_ws[wv] = t;
+      __syncthreads();
+    }
     SPLIT_STAMP(4);
     SPLIT_STAMP(5);
     // walk 3: inclusive sums in the new order (mod 2^32, like the bucket
@@ -3366,39 +3413,29 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
     {
       uint32_t carry = 0, g = 0;
       for (uint32_t w = 0; w < wv; w++) carry += s_ws[w];
-      uint32_t h[SPLIT_ST], e[SPLIT_ST];
+      uint32_t h[ST], e[ST];
 #pragma unroll
-      for (uint32_t st = 0; st < SPLIT_ST; st++) {
+      for (uint32_t st = 0; st < ST; st++) {
         const uint32_t k = a0 + st * 64 + lane;
         h[st] = k < a1 ? hnew[p + k] : 0u;
         e[st] = k < a1 ? rank[p + k] : 0u;
       }
-      for (uint32_t c = a0; c < a1; c += 64 * SPLIT_ST) {
-        uint32_t hn[SPLIT_ST], en[SPLIT_ST];  // (software-pipelined, as the scatter)
+      for (uint32_t c = a0; c < a1; c += 64 * ST) {
+        uint32_t hn[ST], en[ST];  // (software-pipelined, as the scatter)
 #pragma unroll
-        for (uint32_t st = 0; st < SPLIT_ST; st++) {
-          const uint32_t k = c + (SPLIT_ST + st) * 64 + lane;
+        for (uint32_t st = 0; st < ST; st++) {
+          const uint32_t k = c + (ST + st) * 64 + lane;
           hn[st] = k < a1 ? hnew[p + k] : 0u;
           en[st] = k < a1 ? rank[p + k] : 0u;
         }
-        // the ST wave scans level by level: ST independent cross-lane chains in
-        // flight instead of one (each level is an LDS-crossbar round trip)
-        uint32_t inc[SPLIT_ST];
+        // the ST wave scans (DPP: ST independent chains of VALU operations)
+        uint32_t inc[ST];
 #pragma unroll
-        for (uint32_t st = 0; st < SPLIT_ST; st++) inc[st] = h[st];
+        for (uint32_t st = 0; st < ST; st++) inc[st] = wave_incl_add(h[st]);
 #pragma unroll
-        for (uint32_t off = 1; off < 64; off <<= 1) {
-          uint32_t y[SPLIT_ST];
-#pragma unroll
-          for (uint32_t st = 0; st < SPLIT_ST; st++) y[st] = __shfl_up(inc[st], off, 64);
-#pragma unroll
-          for (uint32_t st = 0; st < SPLIT_ST; st++)
-            if (lane >= off) inc[st] += y[st];
-        }
-#pragma unroll
-        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+        for (uint32_t st = 0; st < ST; st++) {
           const uint32_t k = c + st * 64 + lane;
-          const uint32_t tot = __shfl(inc[st], 63, 64);
+          const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc[st], 63);
           if (k < a1) {
             while (g + 1 < G && k >= s_base[g + 1]) g++;  // (k grows along the walk)
             segsum[p + k] = carry + inc[st] - s_off[g];
@@ -3407,7 +3444,7 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
           carry += tot;
         }
 #pragma unroll
-        for (uint32_t st = 0; st < SPLIT_ST; st++) {
+        for (uint32_t st = 0; st < ST; st++) {
           h[st] = hn[st];
           e[st] = en[st];
         }
@@ -3432,6 +3469,34 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
 }
 
 
+// k_split_long: the runs over SPLIT_CAP elements k_split listed (long_runs[0]
+// of them, defer indices from long_runs[1]), one per workgroup of
+// RL_SPLIT_LONG_THREADS lanes. split_long_body's walks are a wave's chain of
+// steps (one wave per SIMD at 256 lanes: each step's LDS lookup, ballots and
+// stores wait on one another), so four times the waves walk a four times
+// shorter chunk each; k_split itself keeps 256-lane workgroups for the many
+// short runs (C1's k_split at 1024 lanes: 18 -> 26 us).
+#if RL_SPLIT_LONG_THREADS
+__global__ __launch_bounds__(RL_SPLIT_LONG_THREADS, RL_SPLIT_LONG_OCC) void k_split_long(
+    BatchDev b, SRec rec_s, uint32_t* __restrict__ svals, uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
+    uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end, uint32_t* __restrict__ run_flags,
+    uint32_t* __restrict__ defer, unsigned long long* num_runs, unsigned long long* split, uint32_t* __restrict__ drun,
+    uint32_t drun_cap, uint32_t* grp, uint32_t* rank, uint32_t* __restrict__ pos_hits, uint32_t* __restrict__ hnew,
+    const uint32_t* err, int per_second, UniqList uq, const uint32_t* __restrict__ long_runs) {
+  if (*err) return;
+  refine_totals(b);
+  const uint32_t nl = long_runs[0];
+  for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+    const uint32_t j = long_runs[1 + i], r = defer[j];
+    const uint32_t p = run_start[r], L = run_end[r] - p;
+    split_long_body<RL_SPLIT_LONG_THREADS, RL_SPLIT_LONG_ST>(j, r, p, L, b, rec_s, svals, segsum, rid, run_start,
+                                                             run_end, run_flags, defer, num_runs, split, drun,
+                                                             drun_cap, grp, rank, pos_hits, hnew, per_second,
+                                                             run_flags[r], uq);
+  }
+}
+#endif
+
 __global__ __launch_bounds__(SPLIT_THREADS) void k_split(BatchDev b, SRec rec_s, uint32_t* __restrict__ svals,
                                                uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
                                                uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end,
@@ -3440,7 +3505,8 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_split(BatchDev b, SRec rec_s,
                                                unsigned long long* split, uint32_t* __restrict__ drun,
                                                uint32_t drun_cap, uint32_t* grp, uint32_t* rank,
                                                uint32_t* __restrict__ pos_hits, uint32_t* __restrict__ hnew,
-                                               const uint32_t* err, int per_second, UniqList uq) {
+                                               const uint32_t* err, int per_second, UniqList uq,
+                                               uint32_t* __restrict__ long_runs, uint32_t* long_hint, int delegate) {
   __shared__ uint32_t s_e[SPLIT_CAP], s_hlo[SPLIT_CAP], s_lu[SPLIT_CAP], s_now[SPLIT_CAP], s_h[SPLIT_CAP];
   __shared__ uint32_t s_nh[SPLIT_CAP];           // max(1, hits) in the new order
   __shared__ uint16_t s_pos[SPLIT_CAP];          // rank inside the element's group
@@ -3458,9 +3524,16 @@ __global__ __launch_bounds__(SPLIT_THREADS) void k_split(BatchDev b, SRec rec_s,
     const uint32_t r = defer[j];
     const uint32_t p = run_start[r], L = run_end[r] - p;
     if (L > SPLIT_CAP) {  // (uniform)
-      split_long_body<SPLIT_THREADS>(j, r, p, L, b, rec_s, svals, segsum, rid, run_start, run_end, run_flags, defer,
-                                     num_runs, split, drun, drun_cap, grp, rank, pos_hits, hnew, per_second,
-                                     run_flags[r], uq);
+      if (tid == 0 && long_hint) *long_hint = 1u;  // (the host's cue to launch k_split_long for the next batches)
+#if RL_SPLIT_LONG_THREADS
+      if (delegate) {
+        if (tid == 0) long_runs[1 + atomicAdd(&long_runs[0], 1u)] = j;  // k_split_long's
+        continue;
+      }
+#endif
+      split_long_body<SPLIT_THREADS, SPLIT_ST>(j, r, p, L, b, rec_s, svals, segsum, rid, run_start, run_end, run_flags,
+                                               defer, num_runs, split, drun, drun_cap, grp, rank, pos_hits, hnew,
+                                               per_second, run_flags[r], uq);
       continue;
     }
     __syncthreads();  // the previous run's shared state has been read
@@ -4759,7 +4832,7 @@ static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b -
 // validation word s.err. Sorted keys go to keys[1] (keys[0] keeps the arrival
 // order for k_table's keys seen once), the sort permutation to vals[0].
 void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_second, hipStream_t st,
-                    hipEvent_t* ev) {
+                    hipEvent_t* ev, uint32_t* long_hint, bool long_kernel) {
   const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
   if (ev) (void)hipEventRecord(ev[0], st);
   if (g0)
@@ -4791,11 +4864,19 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
 #endif
     k_run_check<<<cdiv(b.n, RC_CHUNK), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[1], s.rid, s.run_start,
                                                 s.run_end, s.run_flags, s.defer, s.defer_n, s.err, s.runs64, s.split,
-                                                s.sorted_n, s.grp, s.hit_t, s.uniq, s.uniq_n);
+                                                s.sorted_n, s.grp, s.hit_t, s.uniq, s.uniq_n, s.long_runs);
     k_split<<<SPLIT_BLOCKS, SPLIT_THREADS, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.vals[0], s.segsum, s.rid, s.run_start,
                                           s.run_end, s.run_flags, s.defer, s.defer_n, s.runs64, s.split, s.drun,
                                           b.n / 2 + BIG_HEAVY * PART_DIGITS, s.grp, s.lead, s.hit_t, s.vals[1], s.err,
-                                          per_second, UniqList{s.uniq, s.uniq_n, s.keys[1]});
+                                          per_second, UniqList{s.uniq, s.uniq_n, s.keys[1]}, s.long_runs, long_hint,
+                                          long_kernel ? 1 : 0);
+#if RL_SPLIT_LONG_THREADS
+    if (long_kernel)
+      k_split_long<<<RL_SPLIT_LONG_BLOCKS, RL_SPLIT_LONG_THREADS, 0, st>>>(
+          b, SRec{s.rec, s.vals[0]}, s.vals[0], s.segsum, s.rid, s.run_start, s.run_end, s.run_flags, s.defer,
+          s.runs64, s.split, s.drun, b.n / 2 + BIG_HEAVY * PART_DIGITS, s.grp, s.lead, s.hit_t, s.vals[1], s.err,
+          per_second, UniqList{s.uniq, s.uniq_n, s.keys[1]}, s.long_runs);
+#endif
   }
 }
 
