@@ -3841,6 +3841,38 @@ struct AliasGroup {
   uint32_t id, p, end, mask, w;
 };
 
+// A stem's unit slots in one walk of its probe sequence (they share the home
+// slot: the unit is in the tag, not in the hash): per unit, the first slot of
+// its tag, unit and stem before the first empty slot, with its cur and
+// history head from the same 64-B image. Returns the units found, and
+// UNIT_WALK_ENDED when the walk reached an empty slot (a unit not found is
+// then absent). find_slot takes the rest (inserts; a probe window without an
+// empty slot). Four walks, one per unit, of a few dependent loads each took
+// ~20 us per hot stem under k_table's load (RL_ALIAS_PROF builds).
+#ifndef RL_ALIAS_ONE_WALK
+#define RL_ALIAS_ONE_WALK 1
+#endif
+constexpr uint32_t UNIT_WALK_ENDED = 0x10u;
+__device__ inline uint32_t find_unit_slots(const TableDev& t, uint64_t hs, const Key& stem, int64_t sidx[4], Win c[4],
+                                           uint32_t chain[4]) {
+  uint64_t i = hs >> t.shift;
+  uint32_t found = 0;
+  SlotImg im;
+  for (uint32_t p = 0; p < t.max_probe && found != 0xFu; p++, i = (i + 1) & t.mask) {
+    load_img_lo(&t.slots[i], im);
+    const uint32_t st = im.tag();
+    if (st == TAG_EMPTY) return found | UNIT_WALK_ENDED;
+    const uint32_t u = im.unit();
+    if (u < 1 || u > 4 || ((found >> (u - 1)) & 1) || st != slot_tag(hs, u) || !img_key_equal(im, stem, t.arena))
+      continue;
+    sidx[u - 1] = (int64_t)i;
+    c[u - 1] = im.cur();
+    chain[u - 1] = im.ring();
+    found |= 1u << (u - 1);
+  }
+  return found;
+}
+
 #ifndef RL_ALIAS_NOINLINE
 #define RL_ALIAS_NOINLINE 0  // (noinline: k_table gets a 448-B scratch frame; C1 -1.5 %, profiles/r03/ab_alias_variants/)
 #endif
@@ -3858,6 +3890,13 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
                                    uint32_t u0, uint64_t hs, const Key& stem, uint32_t now) {
 #ifdef RL_NO_ALIAS  // (measurement builds: what the alias path costs the common case)
   return true;
+#endif
+#ifdef RL_ALIAS_PROF  // (measurement builds: phase stamps of the setup of long alias groups)
+  uint64_t ta[4];
+  ta[0] = wall_clock64();
+#define ALIAS_STAMP(i) ta[i] = wall_clock64()
+#else
+#define ALIAS_STAMP(i)
 #endif
   AliasGroup A[4];
   uint32_t G = 1, M;
@@ -3890,10 +3929,23 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
   uint32_t chain[4];
   uint32_t present = 0;
   int64_t fail = 0;
+#if RL_ALIAS_ONE_WALK
+  const uint32_t fr = find_unit_slots(t, hs, stem, sidx, c, chain);
+#else
+  const uint32_t fr = 0;
+#endif
   for (uint32_t k = 0; k < 4; k++) {
+    if ((fr >> k) & 1) {  // (found by the one walk: image read there)
+      present |= 1u << k;
+      continue;
+    }
+    chain[k] = LOG_NONE;
+    if ((fr & UNIT_WALK_ENDED) && !((M >> k) & 1)) {  // absent: the walk reached an empty slot first
+      sidx[k] = SLOT_ABSENT;
+      continue;
+    }
     bool ins;
     sidx[k] = find_slot(t, hs, slot_tag(hs, k + 1), stem, k + 1, (M >> k) & 1, &ins, ferr);
-    chain[k] = LOG_NONE;
     if (sidx[k] >= 0) {
       const Slot& su = t.slots[sidx[k]];
       present |= 1u << k;
@@ -3908,6 +3960,7 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
       for (uint32_t g = 0; g < G; g++) fail_range(res, svals, A[g].p, A[g].end, slot_fail_status(fail));
     return false;  // (else find_slot set the batch's error)
   }
+  ALIAS_STAMP(1);
   // the units that roll their cur forward (a group that may increment: the
   // local-cache hit F is not known yet) and so move it to the history log
   uint32_t rolls = 0;
@@ -3963,6 +4016,7 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
     }
     F[g] = (P.lc_en && now < lcm[g]) ? 1u : 0u;
   }
+  ALIAS_STAMP(2);
   // the new cur of each unit that rolls (groups that increment)
   Win cn[4];
   for (uint32_t k = 0; k < 4; k++) cn[k] = c[k];
@@ -4024,6 +4078,12 @@ __device__ RL_ALIAS_ATTR bool alias_setup(const TableDev& t, const Params& P, SR
       atomicOr(&fast_blk[x], (0xFFFFFFFFu >> (31 - hi)) & (0xFFFFFFFFu << lo));
     }
   }
+#ifdef RL_ALIAS_PROF
+  ta[3] = wall_clock64();
+  if (A[0].end - A[0].p > 4000)
+    printf("alias_setup G=%u L=%u: slots %lu reads %lu commit %lu (x10ns)\n", G, A[0].end - A[0].p,
+           (unsigned long)(ta[1] - ta[0]), (unsigned long)(ta[2] - ta[1]), (unsigned long)(ta[3] - ta[2]));
+#endif
   return false;
 }
 
