@@ -85,6 +85,18 @@ def test_gpu_hot_override_ten_thousand_element_runs_vs_c_oracle(lc):
     _check(_stream([38, 39, 40, 41], rpb=60_000, seed=9), lc, table_slots=1 << 17, max_batch=1 << 17)
 
 
+@pytest.mark.parametrize("mode", ["0", "2"])
+def test_gpu_long_splits_inline_and_on_the_long_kernel_vs_c_oracle(monkeypatch, mode):
+    """The runs over 1024 elements walked by k_split's own 256-lane workgroups
+    (RL_SPLIT_LONG=0) and by k_split_long's 1024-lane ones for every batch (2);
+    the default (1) switches between the two after the first such batch. Also
+    forced sort-key collisions, whose long runs of many stems end on the exact
+    path from either kernel."""
+    monkeypatch.setenv("RL_SPLIT_LONG", mode)
+    _check(_stream([38, 39, 40, 41], rpb=60_000, seed=9), True, table_slots=1 << 17, max_batch=1 << 17)
+    _check(_stream([39, 40, 41], tenants=3000, rpb=8000), False, debug_hash_bits=6)
+
+
 @pytest.mark.parametrize("lc", [False, True])
 def test_gpu_override_on_and_off_vs_c_oracle(lc):
     """Batches with and without overrides, repeated and backward clocks: stems
