@@ -3497,7 +3497,13 @@ __global__ __launch_bounds__(RL_SPLIT_LONG_THREADS, RL_SPLIT_LONG_OCC) void k_sp
 }
 #endif
 
-__global__ __launch_bounds__(SPLIT_THREADS) void k_split(BatchDev b, SRec rec_s, uint32_t* __restrict__ svals,
+// k_split's minimum waves per SIMD (1: what the inline long walk asks for,
+// 221 VGPRs; 4: 128, the long walk spills — it runs here only until the host
+// switches to k_split_long —: C1, C2, C2U flat, profiles/r05/split_long/)
+#ifndef RL_SPLIT_OCC
+#define RL_SPLIT_OCC 1
+#endif
+__global__ __launch_bounds__(SPLIT_THREADS, RL_SPLIT_OCC) void k_split(BatchDev b, SRec rec_s, uint32_t* __restrict__ svals,
                                                uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
                                                uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end,
                                                uint32_t* __restrict__ run_flags, uint32_t* __restrict__ defer,
