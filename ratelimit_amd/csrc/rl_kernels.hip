@@ -867,6 +867,14 @@ __device__ inline int log_find(const TableDev& t, uint32_t head, uint32_t si, ui
     if (a.x != si || a.y != tag || a.w > tprev) break;  // overwritten
     const uint4 b = e[1];
     if (b.x == w) {
+      // Another lane's append may have overwritten the entry between the two
+      // 16-B loads as the log wraps (header of the old owner, record of the
+      // new): the header, re-read past this CU's L1, must be the one checked.
+      const uint32_t* hd = reinterpret_cast<const uint32_t*>(e);
+      if (__hip_atomic_load(hd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.x ||
+          __hip_atomic_load(hd + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.y ||
+          __hip_atomic_load(hd + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.w)
+        break;  // (treated as overwritten)
       *out = Win{b.x, b.y, b.z, b.w};
       return 1;
     }
