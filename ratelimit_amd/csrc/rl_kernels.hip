@@ -2926,7 +2926,10 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
 // stem in both stores of the per-second split (their local-cache entry is
 // shared), or no room left in the dup-run list. Runs over SPLIT_CAP elements
 // take split_long_body (global-memory scratch instead of LDS).
-constexpr uint32_t SPLIT_CAP = 1024, SPLIT_MAXG = 8, SPLIT_BLOCKS = 128;
+#ifndef RL_SPLIT_BLOCKS
+#define RL_SPLIT_BLOCKS 128  // k_split's workgroups (a grid-stride loop over the deferred runs)
+#endif
+constexpr uint32_t SPLIT_CAP = 1024, SPLIT_MAXG = 8, SPLIT_BLOCKS = RL_SPLIT_BLOCKS;
 constexpr uint32_t DEFER_DONE = 0xFFFFFFFFu;  // a deferral k_split resolved
 constexpr uint32_t SPLIT_BAD = 0xFFu;
 
