@@ -1360,6 +1360,7 @@ __device__ __attribute__((always_inline)) inline void replay_simple(SRec rec_s, 
 // it in SEG_ITEMS chunks of 64 (one position per lane), so every load and
 // store is a coalesced 256-B wave access; scans are wave shuffles.
 // ===========================================================================
+__device__ __attribute__((always_inline)) inline uint32_t wave_incl_add(uint32_t x);
 struct SegPair {
   uint32_t f, s;
 };
@@ -1371,12 +1372,7 @@ struct SegChunk {
 };
 
 __device__ inline SegPair seg_chunk_scan(const SegChunk& c, uint32_t lane) {
-  uint32_t P = c.h;
-#pragma unroll
-  for (uint32_t off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(P, off, 64);
-    if (lane >= off) P += y;
-  }
+  const uint32_t P = wave_incl_add(c.h);  // (all 64 lanes active: the callers' chunk loops are wave-uniform)
   const uint64_t le = c.heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
   const uint32_t lh = le ? 63u - (uint32_t)__clzll((long long)le) : 0u;
   const uint32_t Plh = __shfl(P, lh, 64), hlh = __shfl(c.h, lh, 64);
