@@ -55,6 +55,8 @@ def parse():
                          "p50/p99_loaded_batch_ms (submit -> outputs ready, rl_batch_progress)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the CPU baseline (0: the process's CPU share, cpu_share())")
     ap.add_argument("--prof-every", type=int, default=7,
                     help="time every k-th batch's stages with HIP events (k_table's live time for the roofline)")
     ap.add_argument("--no-fill", action="store_true")
@@ -218,23 +220,13 @@ def main():
     # ---- device-resident input batches + per-step clocks. Requests draw from
     # the whole node's tenant space (world * T): with routing every rank talks
     # to every owner.
-    zipf = args.config in ("c2", "c2u")
-    rng = np.random.default_rng((0xC2 if zipf else 0xC1) + 7919 * rank)
-    sampler = W.ZipfSampler(world * T, 1.1) if zipf else None
+    sampler = W.ZipfSampler(world * T, 1.1) if args.config in ("c2", "c2u") else None
     dev_batches = []
     uniq = []  # descriptors k_table answers: keys seen once + runs shorter than LONG_RUN (the rest: k_late)
     host_batches = []
-    for _ in range(args.distinct_batches):
-        ten = rng.integers(0, world * T, nq) if sampler is None else sampler.sample(rng, nq)
-        if sampler is None:
-            a, bn, bq, br = W.c1_batch(ten, now0)
-        elif args.config == "c2u":
-            a, bn, bq, br = W.c2u_batch(ten, now0, rng.integers(1, 9, nq).astype(np.uint32), rng)
-        else:
-            a, bn, bq, br = W.c1_batch(ten, now0, rng.integers(1, 9, nq).astype(np.uint32))
+    for a, bn, bq, ten in make_batches(args, W, rank, world * T, sampler):
         _, cnt = np.unique(ten, return_counts=True)
         uniq.append(2 * int(cnt[cnt < LONG_RUN].sum()))  # (a tenant's two stems: one per unit)
-        a.pop("now")
         host_batches.append((a, bn, bq))
         dev_batches.append(to_dev(a, torch))
     stem_len = 34
@@ -287,6 +279,10 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
+    # (after the timed region) the last timed batch's answers, checked below against the oracle
+    last_out = {k: v.cpu().numpy().view(np.uint32) if v.dtype == torch.int32 else v.cpu().numpy()
+                for k, v in out.items()}
+    last_step = step[0] - 1
     route_host = {k: round(v / args.steps * 1e3, 4) for k, v in sc.host_s.items()} if py_route else None
     info1 = be.table_info()
     if routed and not recv:  # decisions this rank's table answered per owner batch
@@ -327,6 +323,23 @@ def main():
         p99 = float(lt.item())
     else:
         p99 = float(np.percentile(lat, 99))
+
+    # ---- self-check (outside every timed region): the last timed batch's
+    # answers for a tenant subset against the C oracle replaying that subset's
+    # whole history (fill, warmup, timed steps, every rank's slices in global
+    # order); keys are independent, so the subset's answers must be equal.
+    # A wrong-answer fast path cannot post a line.
+    check = verify(args, W, last_out, last_step, host_batches[0][1], world, rank, T, now0, sampler)
+    if routed:
+        ok = torch.tensor([1 if check["verified"] else 0], dtype=torch.int32,
+                          device="cuda" if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        check["verified"] = check["verified"] and bool(ok.item())
+    if not check["verified"]:
+        print("[bench] SELF-CHECK FAILED (rank %d): %s" % (rank, json.dumps(check)), file=sys.stderr, flush=True)
+        be.close()
+        raise SystemExit(1)
+    progress("self-check: %d descriptors equal to the oracle" % check["checked"])
 
     if rank != 0:
         be.close()
@@ -415,12 +428,94 @@ def main():
             "loaded": loaded} if loaded else {}),
         "pcie_fed": pcie,
         "roofline": roofline, "cpu_baseline": cpu, "fill_s": round(t_fill, 2),
+        "verified": check["verified"], "self_check": check,
         **({"route_host_ms_per_step": route_host} if py_route else {}),
     }
     print(json.dumps(line), flush=True)
     be.close()
     if routed:
         dist.destroy_process_group()
+
+
+def make_batches(args, W, rank, tenants, sampler):
+    """Rank `rank`'s distinct input batches (deterministic per rank, so any
+    rank can regenerate any other's for the self-check): (arrays without
+    now, n, n_requests, tenant of each request)."""
+    rng = np.random.default_rng((0xC2 if sampler is not None else 0xC1) + 7919 * rank)
+    nq = args.requests
+    out = []
+    for _ in range(args.distinct_batches):
+        ten = rng.integers(0, tenants, nq) if sampler is None else sampler.sample(rng, nq)
+        if sampler is None:
+            a, bn, bq, br = W.c1_batch(ten, W.NOW0)
+        elif args.config == "c2u":
+            a, bn, bq, br = W.c2u_batch(ten, W.NOW0, rng.integers(1, 9, nq).astype(np.uint32), rng)
+        else:
+            a, bn, bq, br = W.c1_batch(ten, W.NOW0, rng.integers(1, 9, nq).astype(np.uint32))
+        a.pop("now")
+        out.append((a, bn, bq, ten))
+    return out
+
+
+def select(a, n, nq, keep, now):
+    """Batch a (without now) restricted to the descriptors where keep is True,
+    every request at clock `now`."""
+    idx = np.nonzero(keep[:n])[0]
+    off = a["stem_off"].astype(np.int64)
+    L = off[idx + 1] - off[idx]
+    o = np.zeros(idx.size + 1, np.uint32)
+    o[1:] = np.cumsum(L)
+    # (gather the kept stems' bytes with one index array)
+    pos = np.repeat(off[idx] - o[:-1], L) + np.arange(int(o[-1]))
+    out = {"stem_bytes": a["stem_bytes"][pos], "stem_off": o, "now": np.full(nq, now, np.int64)}
+    for k in ("req_idx", "unit", "flags", "limit", "hits", "rule_id"):
+        out[k] = a[k][idx]
+    return out, idx.size, nq
+
+
+def verify(args, W, got, last_step, n, world, rank, T, now0, sampler, modulus=128):
+    """The bench's answers for the last timed step, checked against the C
+    oracle (oracle/rl_oracle.c) on the tenants t % (modulus * world) == 77:
+    the oracle replays exactly their history (the fill at now0 - 1, then every
+    step s <= last_step: batch s % distinct of every rank, rank-major, at
+    now0 + s). Also: the per-rule TotalHits deltas sum to the batch's hits."""
+    from oracle.c_oracle import COracle
+    t0 = time.perf_counter()
+    M = modulus * world
+    r0 = 77 % M
+    co = COracle(0.8, False, False)
+    own = make_batches(args, W, rank, world * T, sampler)
+    ranks = [own if q == rank else make_batches(args, W, q, world * T, sampler) for q in range(world)]
+    checked, bad = 0, {}
+    try:
+        if not args.no_fill:
+            co.do_limit(*W.c1_batch(np.arange(r0, world * T, M), now0 - 1))
+        for s in range(last_step + 1):
+            for q in range(world):
+                a, bn, bq, ten = ranks[q][s % len(ranks[q])]
+                keep = (ten % M == r0)[a["req_idx"]]
+                if not keep.any():
+                    continue
+                o = co.do_limit(*select(a, bn, bq, keep, now0 + s), args.n_rules)
+                if q == rank and s == last_step:
+                    for f in ("code", "limit_remaining", "reset_s"):
+                        g = got[f][:n][keep]
+                        if not np.array_equal(g, o[f]):
+                            i = np.nonzero(g != o[f])[0]
+                            bad[f] = {"mismatches": int(i.size), "first": int(i[0]), "gpu": int(g[i[0]]),
+                                      "oracle": int(o[f][i[0]])}
+                    checked = int(keep.sum())
+    finally:
+        co.close()
+    a = own[last_step % len(own)][0]
+    hits = int(np.maximum(a["hits"], 1).astype(np.int64).sum())
+    total_hits = int(got["stats"].reshape(-1, 6)[:, 0].astype(np.int64).sum())
+    if total_hits != hits:
+        bad["total_hits"] = {"gpu": total_hits, "batch": hits}
+    return {"verified": not bad and checked > 0, "checked": checked, "step": last_step,
+            "subset": "tenants t %% %d == %d" % (M, r0), "mismatches": bad or None,
+            "oracle": "oracle/rl_oracle.c (C restatement), the subset's whole history replayed",
+            "seconds": round(time.perf_counter() - t0, 2)}
 
 
 def loaded_latency(be, run_step, k_steps, interval_s):
@@ -679,11 +774,8 @@ def cpu_baseline(args, W):
     in-process stores, one thread each; bit-equal to the sequential replay,
     tests/test_c_oracle.py), plus the single-thread rate on a shorter sample."""
     from oracle.c_oracle import COracle, COracleMT
-    try:
-        ncpu = len(os.sched_getaffinity(0))
-    except AttributeError:
-        ncpu = os.cpu_count() or 1
-    threads = max(1, min(16, ncpu, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+    share = cpu_share()
+    threads = args.cpu_threads or share["cores"]
 
     def run(co, seconds, seed):
         rng = np.random.default_rng(seed)
@@ -709,10 +801,43 @@ def cpu_baseline(args, W):
     v1, k1, s1 = run(COracle(0.8, False, False), args.cpu_seconds / 3, 0xC1 + 1)
     vt, kt, st = run(COracleMT(0.8, False, False, threads), args.cpu_seconds, 0xC1 + 2)
     return {"value": vt, "unit": "decisions/s", "cores": threads, "kind": "port",
-            "value_1_core": v1,
+            "value_1_core": v1, "speedup_vs_1_core": vt / v1 if v1 else None,
+            "cores_basis": share["basis"], "host_cpus": share,
             "sample": "%d consecutive %s batches x %d descriptors (%.1f s wall), C restatement oracle sharded by "
-                      "stem hash over %d threads (one store each); 1 thread: %d batches (%.1f s)"
+                      "stem hash over %d threads (one store each, a persistent pool: hash, scatter and replay "
+                      "phases O(n / threads) each); 1 thread: %d batches (%.1f s)"
                       % (kt, args.config.upper(), 2 * args.requests, st, threads, k1, s1)}
+
+
+def cpu_share():
+    """The host CPUs this process may use: the affinity mask, capped by the
+    cgroup's CPU quota and by OMP_NUM_THREADS (the GPU box sets it to the
+    box's CPU share: one GPU's lease is 16 of a node's cores, though its
+    affinity mask lists them all)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            quota = max(1, q // per) if q > 0 else None
+        except (OSError, ValueError):
+            quota = None
+    omp = os.environ.get("OMP_NUM_THREADS")
+    omp = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
+    cores = min([aff] + [x for x in (quota, omp) if x])
+    basis = ("all %d CPUs of the affinity mask" % aff if cores == aff else
+             "the cgroup CPU quota (%d of %d CPUs in the affinity mask)" % (quota, aff) if cores == quota else
+             "OMP_NUM_THREADS=%d, this host's CPU share for the process (%d CPUs in the affinity mask)" % (omp, aff))
+    return {"cores": cores, "affinity_cpus": aff, "cgroup_quota_cpus": quota, "omp_num_threads": omp,
+            "basis": basis}
 
 
 if __name__ == "__main__":

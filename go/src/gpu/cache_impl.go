@@ -58,6 +58,45 @@ type rateLimitCacheImpl struct {
 
 	// local-cache gauges, refreshed by the batcher (gpuLocalCacheStats reads them)
 	lcEntries, lcLookups, lcHits, lcMisses uint64
+
+	// health (GPU_HEALTH_CHECK_DEVICE): a device-level library failure marks
+	// the server's health check failed, the next success marks it OK again,
+	// as the Redis pool does on its connections (src/redis/driver_impl.go:31-52)
+	health healthMonitor
+}
+
+// healthMonitor flips the server's health check on device-level failures
+// (rl_status RL_E_HIP, RL_E_COMM, RL_E_INTERNAL: the GPU or its runtime, not
+// a request): the pod stops reporting SERVING while its device cannot answer.
+// Request-level failures (RL_E_TIME, RL_E_INVALID, RL_E_CAPACITY, a full
+// table) leave it as it is. Batcher goroutine only.
+type healthMonitor struct {
+	srv       server.Server // nil: no health check (tests, GPU_HEALTH_CHECK_DEVICE=false)
+	unhealthy bool
+}
+
+func deviceFailure(err error) bool {
+	e, ok := err.(*Error)
+	return ok && (e.Status == StatusHIP || e.Status == StatusComm || e.Status == StatusInternal)
+}
+
+// observe: the outcome of one library call that reached the device (a batch,
+// a request batch, a sweep).
+func (h *healthMonitor) observe(err error) {
+	if h.srv == nil {
+		return
+	}
+	if deviceFailure(err) {
+		if !h.unhealthy {
+			logger.Errorf("gpu: device failure, health check failed: %v", err)
+			h.srv.HealthCheckFail()
+			h.unhealthy = true
+		}
+	} else if err == nil && h.unhealthy {
+		logger.Warnf("gpu: device answering again, health check OK")
+		h.srv.HealthCheckOK()
+		h.unhealthy = false
+	}
 }
 
 type call struct {
@@ -101,6 +140,7 @@ type Options struct {
 	SweepLag      time.Duration // GPU_SWEEP_LAG: the sweep's time floor trails the clock by this much
 	ConfigMatch   bool          // GPU_CONFIG_MATCH: GetLimit on the GPU (not on a routed ctx)
 	StatsManager  stats.Manager // for the override stats keys the GPU match meets (ConfigMatch)
+	HealthServer  server.Server // GPU_HEALTH_CHECK_DEVICE: the server whose health check device failures flip (nil: none)
 }
 
 // NewRateLimitCacheImpl starts the batcher on an existing ctx.
@@ -125,6 +165,7 @@ func NewRateLimitCacheImpl(ctx *Ctx, cfg Config, opt Options, timeSource utils.T
 		statsManager: opt.StatsManager,
 		limitByKey:   map[string]*pb.RateLimitResponse_RateLimit{},
 	}
+	this.health.srv = opt.HealthServer
 	if this.configMatch {
 		this.rb = NewRequestBatch()
 	}
@@ -182,9 +223,12 @@ func NewRateLimitCacheImplFromSettings(s settings.Settings, localCache *freecach
 			logger.Fatalf("gpu: cannot join the GPU world: %v", err)
 		}
 	}
-	impl := NewRateLimitCacheImpl(ctx, cfg, Options{Window: s.GpuBatchWindow, SweepInterval: s.GpuSweepInterval,
-		SweepLag: s.GpuSweepLag, ConfigMatch: s.GpuConfigMatch, StatsManager: statsManager}, timeSource,
-		s.CacheKeyPrefix)
+	opt := Options{Window: s.GpuBatchWindow, SweepInterval: s.GpuSweepInterval, SweepLag: s.GpuSweepLag,
+		ConfigMatch: s.GpuConfigMatch, StatsManager: statsManager}
+	if s.GpuHealthCheckDevice && srv != nil {
+		opt.HealthServer = srv
+	}
+	impl := NewRateLimitCacheImpl(ctx, cfg, opt, timeSource, s.CacheKeyPrefix)
 	if cfg.LocalCache && srv != nil {
 		statsManager.GetStatsStore().AddStatGenerator(newLocalCacheStats(impl, srv.Scope().Scope("localcache_gpu")))
 	}
@@ -194,7 +238,7 @@ func NewRateLimitCacheImplFromSettings(s settings.Settings, localCache *freecach
 func (this *rateLimitCacheImpl) DoLimit(ctx context.Context, request *pb.RateLimitRequest,
 	limits []*config.RateLimit) []*pb.RateLimitResponse_DescriptorStatus {
 	assert.Assert(len(request.Descriptors) == len(limits)) // base_limiter.go:47
-	c := &call{request, limits, this.timeSource.UnixNow(), make(chan reply, 1)}
+	c := &call{req: request, limits: limits, now: this.timeSource.UnixNow(), done: make(chan reply, 1)}
 	this.queue <- c
 	r := <-c.done
 	if r.err != "" {
@@ -297,6 +341,7 @@ func (this *rateLimitCacheImpl) doRaw(calls []*call) {
 		err = fmt.Errorf("gpu: more than %d rule stats keys", this.maxRules)
 	} else {
 		err = this.ctx.DoLimitRequests(b)
+		this.health.observe(err)
 	}
 	j := 0
 	for _, c := range calls {
@@ -642,6 +687,7 @@ func (this *rateLimitCacheImpl) finish(f *flight) {
 			err = serr
 		}
 	}
+	this.health.observe(err)
 	b := f.b
 	for ci, c := range f.calls {
 		idx := f.where[ci]
@@ -689,9 +735,11 @@ func (this *rateLimitCacheImpl) finish(f *flight) {
 // local-cache gauges.
 func (this *rateLimitCacheImpl) housekeeping() {
 	now := this.timeSource.UnixNow()
-	if _, err := this.ctx.Sweep(now - this.sweepLag); err != nil {
+	_, err := this.ctx.Sweep(now - this.sweepLag)
+	if err != nil {
 		logger.Errorf("gpu: sweep failed: %v", err)
 	}
+	this.health.observe(err)
 	if info, err := this.ctx.LocalCacheInfo(now); err == nil {
 		atomic.StoreUint64(&this.lcEntries, info.EntryCount)
 		atomic.StoreUint64(&this.lcLookups, info.LookupCount)

@@ -115,6 +115,14 @@ func (c *Ctx) err(rc C.int) error {
 	return &Error{Status: int(rc), Msg: C.GoString(C.rl_last_error(c.c))}
 }
 
+// rl_status codes of a device-level failure (the GPU or its runtime, not a
+// request): the batcher's health monitor fails the server's health check on them.
+const (
+	StatusHIP      = int(C.RL_E_HIP)
+	StatusComm     = int(C.RL_E_COMM)
+	StatusInternal = int(C.RL_E_INTERNAL)
+)
+
 // Error is a library failure: the adapter turns it into
 // panic(redis.RedisError(...)) (src/redis/driver_impl.go:60-64).
 type Error struct {
@@ -154,14 +162,14 @@ func (c *Ctx) LocalCacheInfo(now int64) (LocalCacheInfo, error) {
 	if err := c.err(C.rl_local_cache_info_get(c.c, C.int64_t(now), &lc)); err != nil {
 		return LocalCacheInfo{}, err
 	}
-	return LocalCacheInfo{uint64(lc.entry_count), uint64(lc.lookup_count), uint64(lc.hit_count),
-		uint64(lc.miss_count)}, nil
+	return LocalCacheInfo{EntryCount: uint64(lc.entry_count), LookupCount: uint64(lc.lookup_count),
+		HitCount: uint64(lc.hit_count), MissCount: uint64(lc.miss_count)}, nil
 }
 
 // TableInfo: live slots, tombstones and arena use, summed over shards.
 type TableInfo struct {
 	TableSlots, LiveSlots, Tombstones, ArenaBytesUsed, ExactStems, Batches, Decisions uint64
-	HistoryEntries, HistoryAppended, HistoryLost, HistorySlots                      uint64
+	HistoryEntries, HistoryAppended, HistoryLost, HistorySlots, HistoryRefused      uint64
 }
 
 func (c *Ctx) TableInfo() (TableInfo, error) {
@@ -169,10 +177,12 @@ func (c *Ctx) TableInfo() (TableInfo, error) {
 	if err := c.err(C.rl_table_info_get(c.c, &ti)); err != nil {
 		return TableInfo{}, err
 	}
-	return TableInfo{uint64(ti.table_slots), uint64(ti.live_slots), uint64(ti.tombstones),
-		uint64(ti.arena_bytes_used), uint64(ti.exact_stems), uint64(ti.batches), uint64(ti.decisions),
-		uint64(ti.history_entries), uint64(ti.history_appended), uint64(ti.history_lost),
-		uint64(ti.history_slots)}, nil
+	return TableInfo{TableSlots: uint64(ti.table_slots), LiveSlots: uint64(ti.live_slots),
+		Tombstones: uint64(ti.tombstones), ArenaBytesUsed: uint64(ti.arena_bytes_used),
+		ExactStems: uint64(ti.exact_stems), Batches: uint64(ti.batches), Decisions: uint64(ti.decisions),
+		HistoryEntries: uint64(ti.history_entries), HistoryAppended: uint64(ti.history_appended),
+		HistoryLost: uint64(ti.history_lost), HistorySlots: uint64(ti.history_slots),
+		HistoryRefused: uint64(ti.history_refused)}, nil
 }
 
 // ---- pinned host memory: Go never hands Go-heap pointers to C (cgo pointer

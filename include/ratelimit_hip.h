@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 4u
+#define RL_ABI_VERSION 5u
 
 /* Status codes. */
 enum rl_status {
@@ -182,6 +182,10 @@ typedef struct rl_table_info {
   uint64_t history_lost;      /* lookups that found an entry the log had overwritten: answered
                                  RL_E_TIME (size history_entries up) */
   uint64_t history_slots;     /* live slots with a history chain */
+  uint64_t history_refused;   /* records the log refused: their partition had taken
+                                 history_entries / 64 appends in one batch already (a batch's
+                                 appends never wrap a partition onto its own entries); a later
+                                 lookup of such a window is RL_E_TIME (size history_entries up) */
 } rl_table_info;
 
 typedef struct rl_ctx rl_ctx;
@@ -369,6 +373,29 @@ int rl_debug_decide(rl_ctx* ctx, uint32_t n, const uint32_t* before, const uint3
                     const uint8_t* unit, const uint8_t* flags, const int64_t* now,
                     uint8_t* code, uint32_t* remaining, uint32_t* reset_s,
                     uint64_t* stat_deltas /* n * RL_NUM_STATS */, uint8_t* lc_set);
+/* rl_debug_log_tear (tests; libraries built with RL_LOG_TEAR, else RL_E_INVALID):
+ * replays a concurrent writer of a history-log entry between a lookup's loads.
+ * With arm != NULL it arms a one-shot tear: the first entry the next lookup
+ * (log_find) reads is overwritten by `entry`, the writer's steps applied by the
+ * reading lane itself: sched[i] of them before the reader's i-th load (header,
+ * record, header re-read; non-decreasing), the rest after its verdict. With
+ * out != NULL (after the batches that should have fired it) it reads the
+ * outcome back and disarms. The lookup uses a record only if the writer and
+ * reader protocols keep header and record of one write together; the tests
+ * check that over every schedule. */
+typedef struct rl_log_tear {
+  uint32_t armed;      /* in: 1; out: 2 once a lookup fired it */
+  uint32_t protocol;   /* 0: the library's writer (header BUSY, record, header: 3 steps);
+                          1: round 5's order (header, record: 2 steps) */
+  uint32_t sched[3];   /* writer steps done before the reader's header load, record load, re-read */
+  uint32_t entry[8];   /* the overwriting entry: slot, tag, prev, t_app, then the record ws, count,
+                          expire, lc; 0xFFFFFFFF in slot / tag / prev / t_app = the entry's own */
+  uint32_t before[8];  /* out: the entry before the tear */
+  uint32_t seen[12];   /* out: the reader's header, record and header re-read */
+  int32_t verdict;     /* out: 1 the record was used (its window), 0 the walk moved on, -1 rejected */
+  uint32_t reserved;
+} rl_log_tear;
+int rl_debug_log_tear(rl_ctx* ctx, const rl_log_tear* arm, rl_log_tear* out);
 
 /* ---- Multi-GPU routing across processes (one single-shard rl_ctx per GPU) ---
  * SURVEY.md §8e. For one process per GPU (torch.distributed / RCCL), each rank

@@ -18,6 +18,7 @@
  * packed stem, followed by strconv.FormatInt((now/div)*div, 10).
  * Pinned against tests/golden (see tests/test_c_oracle.py).
  */
+#define _POSIX_C_SOURCE 200809L /* pthread_barrier_t under -std=c11 */
 #include <math.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -316,75 +317,147 @@ int rlo_do_limit(rlo_ctx* c, const rl_batch* b, rl_result* o) {
  * of a stem, always land in one shard), each shard replaying its descriptors in
  * arrival order on its own thread. Keys never interact, so the results equal
  * the sequential replay's bit for bit (tests/test_c_oracle.py checks that). */
-typedef struct rlo_mt {
+typedef struct rlo_mt rlo_mt;
+typedef struct {
+  rlo_mt* m;
+  int t;
+  uint64_t* stats;  /* this shard's per-rule deltas of the current batch */
+  int rc;
+} mt_worker_t;
+
+/* A pool of T threads, created once: per batch, three phases between
+ * barriers — (0) each thread hashes its slice of the descriptors to shards and
+ * counts them per shard, (1) each scatters its slice into the shards' index
+ * lists at offsets the main thread took from the counts (slices in order, so
+ * every list is in arrival order), (2) each replays its shard's list. Every
+ * phase is O(n / T) per thread: the rate scales with the cores. */
+struct rlo_mt {
   int T;
   rlo_ctx** sh;
-} rlo_mt;
+  pthread_t* th;
+  mt_worker_t* w;
+  pthread_barrier_t go, done;
+  int phase, quit;
+  const rl_batch* b;
+  rl_result* o;
+  uint16_t* shard;   /* [n] shard of each descriptor */
+  uint32_t* cnt;     /* [T x T] cnt[t * T + s]: descriptors of slice t in shard s; then their offsets */
+  uint32_t* idx;     /* [n] the shards' index lists, concatenated */
+  uint32_t* base;    /* [T + 1] shard s's list starts at idx + base[s] */
+  uint32_t cap;      /* n the arrays are sized for */
+};
+
+static void mt_phase(rlo_mt* m, int t) {
+  const rl_batch* b = m->b;
+  const int T = m->T;
+  const uint32_t a = (uint32_t)((uint64_t)b->n * t / T), e = (uint32_t)((uint64_t)b->n * (t + 1) / T);
+  if (m->phase == 0) {
+    uint32_t* c = m->cnt + (size_t)t * T;
+    memset(c, 0, sizeof(uint32_t) * T);
+    for (uint32_t i = a; i < e; i++) {
+      const uint32_t s0 = b->stem_off[i];
+      const uint16_t s = (uint16_t)(hash_bytes((const char*)b->stem_bytes + s0, b->stem_off[i + 1] - s0) % (uint64_t)T);
+      m->shard[i] = s;
+      c[s]++;
+    }
+  } else if (m->phase == 1) {
+    uint32_t* c = m->cnt + (size_t)t * T;  /* (now this slice's next position per shard) */
+    for (uint32_t i = a; i < e; i++) m->idx[c[m->shard[i]]++] = i;
+  } else {
+    mt_worker_t* w = &m->w[t];
+    memset(w->stats, 0, sizeof(uint64_t) * RL_NUM_STATS * (b->n_rules ? b->n_rules : 1));
+    w->rc = do_limit_idx(m->sh[t], b, m->idx + m->base[t], m->base[t + 1] - m->base[t], m->o, w->stats);
+  }
+}
+
+static void* mt_main(void* arg) {
+  mt_worker_t* w = (mt_worker_t*)arg;
+  rlo_mt* m = w->m;
+  for (;;) {
+    pthread_barrier_wait(&m->go);
+    if (m->quit) return NULL;
+    mt_phase(m, w->t);
+    pthread_barrier_wait(&m->done);
+  }
+}
 
 rlo_mt* rlo_mt_create(float near_limit_ratio, int local_cache, int per_second, int threads) {
   if (threads < 1) threads = 1;
+  if (threads > 65535) threads = 65535;
   rlo_mt* m = (rlo_mt*)calloc(1, sizeof(rlo_mt));
   m->T = threads;
   m->sh = (rlo_ctx**)calloc(threads, sizeof(rlo_ctx*));
   for (int t = 0; t < threads; t++) m->sh[t] = rlo_create(near_limit_ratio, local_cache, per_second);
+  m->cnt = (uint32_t*)calloc((size_t)threads * threads, sizeof(uint32_t));
+  m->base = (uint32_t*)calloc((size_t)threads + 1, sizeof(uint32_t));
+  m->w = (mt_worker_t*)calloc(threads, sizeof(mt_worker_t));
+  m->th = (pthread_t*)calloc(threads, sizeof(pthread_t));
+  pthread_barrier_init(&m->go, NULL, (unsigned)threads + 1);
+  pthread_barrier_init(&m->done, NULL, (unsigned)threads + 1);
+  for (int t = 0; t < threads; t++) {
+    m->w[t].m = m;
+    m->w[t].t = t;
+    pthread_create(&m->th[t], NULL, mt_main, &m->w[t]);
+  }
   return m;
 }
 
 void rlo_mt_destroy(rlo_mt* m) {
   if (!m) return;
-  for (int t = 0; t < m->T; t++) rlo_destroy(m->sh[t]);
-  free(m->sh); free(m);
+  m->quit = 1;
+  pthread_barrier_wait(&m->go);
+  for (int t = 0; t < m->T; t++) pthread_join(m->th[t], NULL);
+  pthread_barrier_destroy(&m->go);
+  pthread_barrier_destroy(&m->done);
+  for (int t = 0; t < m->T; t++) {
+    rlo_destroy(m->sh[t]);
+    free(m->w[t].stats);
+  }
+  free(m->sh); free(m->th); free(m->w); free(m->cnt); free(m->base);
+  free(m->shard); free(m->idx);
+  free(m);
 }
 
-typedef struct {
-  rlo_mt* m; const rl_batch* b; rl_result* o;
-  uint16_t* shard; int t, phase, rc;
-  uint64_t* stats;
-} mt_job;
-
-static void* mt_worker(void* arg) {
-  mt_job* j = (mt_job*)arg;
-  const rl_batch* b = j->b;
-  const int T = j->m->T;
-  if (j->phase == 0) { /* shard of every descriptor in this thread's slice */
-    uint32_t a = (uint32_t)((uint64_t)b->n * j->t / T), e = (uint32_t)((uint64_t)b->n * (j->t + 1) / T);
-    for (uint32_t i = a; i < e; i++) {
-      uint32_t s0 = b->stem_off[i];
-      j->shard[i] = (uint16_t)(hash_bytes((const char*)b->stem_bytes + s0, b->stem_off[i + 1] - s0) % (uint64_t)T);
-    }
-    return NULL;
-  }
-  uint32_t cnt = 0;
-  for (uint32_t i = 0; i < b->n; i++) cnt += j->shard[i] == j->t;
-  uint32_t* idx = (uint32_t*)malloc(sizeof(uint32_t) * (cnt ? cnt : 1));
-  uint32_t k = 0;
-  for (uint32_t i = 0; i < b->n; i++) if (j->shard[i] == j->t) idx[k++] = i;
-  j->stats = (uint64_t*)calloc((size_t)(b->n_rules ? b->n_rules : 1) * RL_NUM_STATS, sizeof(uint64_t));
-  j->rc = do_limit_idx(j->m->sh[j->t], b, idx, cnt, j->o, j->stats);
-  free(idx);
-  return NULL;
+static void mt_run(rlo_mt* m, int phase) {
+  m->phase = phase;
+  pthread_barrier_wait(&m->go);
+  pthread_barrier_wait(&m->done);
 }
 
 int rlo_mt_do_limit(rlo_mt* m, const rl_batch* b, rl_result* o) {
   const int T = m->T;
-  uint16_t* shard = (uint16_t*)malloc(sizeof(uint16_t) * (b->n ? b->n : 1));
-  mt_job* jobs = (mt_job*)calloc(T, sizeof(mt_job));
-  pthread_t* th = (pthread_t*)calloc(T, sizeof(pthread_t));
-  int rc = RL_OK;
-  for (int phase = 0; phase < 2; phase++) {
-    for (int t = 0; t < T; t++) {
-      jobs[t] = (mt_job){m, b, o, shard, t, phase, RL_OK, jobs[t].stats};
-      pthread_create(&th[t], NULL, mt_worker, &jobs[t]);
-    }
-    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+  if (b->n > m->cap || !m->shard) {
+    free(m->shard); free(m->idx);
+    m->cap = b->n > m->cap ? b->n : (m->cap ? m->cap : 1);
+    m->shard = (uint16_t*)malloc(sizeof(uint16_t) * m->cap);
+    m->idx = (uint32_t*)malloc(sizeof(uint32_t) * m->cap);
   }
+  for (int t = 0; t < T; t++) {
+    free(m->w[t].stats);
+    m->w[t].stats = (uint64_t*)calloc((size_t)(b->n_rules ? b->n_rules : 1) * RL_NUM_STATS, sizeof(uint64_t));
+  }
+  m->b = b;
+  m->o = o;
+  mt_run(m, 0);
+  /* shard s's list: slices 0..T-1 in order */
+  uint32_t pos = 0;
+  for (int s = 0; s < T; s++) {
+    m->base[s] = pos;
+    for (int t = 0; t < T; t++) {
+      const uint32_t c = m->cnt[(size_t)t * T + s];
+      m->cnt[(size_t)t * T + s] = pos;
+      pos += c;
+    }
+  }
+  m->base[T] = pos;
+  mt_run(m, 1);
+  mt_run(m, 2);
+  int rc = RL_OK;
   if (b->n_rules) memset(o->stats, 0, sizeof(uint64_t) * RL_NUM_STATS * b->n_rules);
   for (int t = 0; t < T; t++) {
-    if (jobs[t].rc) rc = jobs[t].rc;
-    for (uint64_t i = 0; i < (uint64_t)b->n_rules * RL_NUM_STATS; i++) o->stats[i] += jobs[t].stats[i];
-    free(jobs[t].stats);
+    if (m->w[t].rc) rc = m->w[t].rc;
+    for (uint64_t i = 0; i < (uint64_t)b->n_rules * RL_NUM_STATS; i++) o->stats[i] += m->w[t].stats[i];
   }
-  free(th); free(jobs); free(shard);
   return rc;
 }
 

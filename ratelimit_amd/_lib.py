@@ -10,6 +10,7 @@ from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RL_LIB_PATH") or os.path.join(HERE, "libratelimit_hip.so")  # override: profiling builds
+TEAR_LIB_PATH = os.path.join(HERE, "libratelimit_hip_tear.so")  # RL_LOG_TEAR build (tests/test_gpu_log_tear.py)
 
 EXPORTS = ["rl_abi_version", "rl_create", "rl_destroy", "rl_last_error", "rl_do_limit", "rl_do_limit_async",
            "rl_synchronize", "rl_sweep", "rl_restore", "rl_table_info_get", "rl_table_info_shard", "rl_alloc_host",
@@ -19,21 +20,32 @@ EXPORTS = ["rl_abi_version", "rl_create", "rl_destroy", "rl_last_error", "rl_do_
            "rl_local_cache_info_get", "rl_snapshot_size", "rl_snapshot_save", "rl_snapshot_load",
            "rl_packer_create", "rl_packer_destroy", "rl_packer_pack", "rl_packer_rules", "rl_packer_rule_key",
            "rl_packer_last_error", "rl_comm_unique_id", "rl_comm_loopback_id", "rl_comm_init", "rl_do_limit_routed_async",
-           "rl_do_limit_host_async", "rl_do_limit_compact_async", "rl_do_limit_prefixed_async", "rl_batch_progress"]
+           "rl_do_limit_host_async", "rl_do_limit_compact_async", "rl_do_limit_prefixed_async", "rl_batch_progress",
+           "rl_debug_log_tear"]
 
-_lib = None
+_libs = {}
 
 
 class RedisError(RuntimeError):
-    """Mirror of redis.RedisError (src/redis/driver.go:6-10): backend failure."""
+    """Mirror of redis.RedisError (src/redis/driver.go:6-10): backend failure.
+    status: the library's rl_status (None: raised by the host code)."""
+
+    def __init__(self, msg, status=None):
+        super().__init__(msg)
+        self.status = status
 
 
 def lib():
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError("libratelimit_hip.so not built (%s): run `python -m ratelimit_amd.build`" % LIB_PATH)
+    """The product library (or RL_LIB_PATH's build)."""
+    return load(LIB_PATH)
+
+
+def load(path):
+    """A build of the library at `path`, loaded once per process."""
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
+        raise RuntimeError("libratelimit_hip.so not built (%s): run `python -m ratelimit_amd.build`" % path)
     # One HIP runtime per process: torch ships its own libamdhip64.so.7. Loaded
     # first, it also serves this library (same soname); loaded after ours, torch
     # would bring a second runtime that finds no GPU. Device tensors handed to
@@ -42,7 +54,7 @@ def lib():
         import torch  # noqa: F401
     except ImportError:
         pass
-    L = C.CDLL(LIB_PATH)
+    L = C.CDLL(path)
     L.rl_abi_version.restype = C.c_uint32
     L.rl_create.restype = C.c_void_p
     L.rl_create.argtypes = [C.POINTER(abi.RlConfig), C.c_char_p, C.c_size_t]
@@ -97,13 +109,15 @@ def lib():
     L.rl_packer_rule_key.argtypes = [C.c_void_p, C.c_uint32]
     L.rl_packer_last_error.restype = C.c_char_p
     L.rl_packer_last_error.argtypes = [C.c_void_p]
+    if hasattr(L, "rl_debug_log_tear"):
+        L.rl_debug_log_tear.argtypes = [C.c_void_p, C.POINTER(abi.RlLogTear), C.POINTER(abi.RlLogTear)]
     if L.rl_abi_version() != abi.ABI_VERSION:
         raise RuntimeError("libratelimit_hip.so ABI mismatch")
-    _lib = L
+    _libs[path] = L
     return L
 
 
-def check(ctx, rc):
+def check(ctx, rc, L=None):
     if rc != 0:
-        msg = lib().rl_last_error(ctx).decode(errors="replace")
-        raise RedisError("%s [%s]" % (msg, abi.STATUS_NAMES.get(rc, rc)))
+        msg = (L or lib()).rl_last_error(ctx).decode(errors="replace")
+        raise RedisError("%s [%s]" % (msg, abi.STATUS_NAMES.get(rc, rc)), rc)

@@ -77,7 +77,14 @@ class RlTableInfo(C.Structure):
                 ("arena_bytes_used", C.c_uint64), ("exact_stems", C.c_uint64),
                 ("batches", C.c_uint64), ("decisions", C.c_uint64),
                 ("history_entries", C.c_uint64), ("history_appended", C.c_uint64),
-                ("history_lost", C.c_uint64), ("history_slots", C.c_uint64)]
+                ("history_lost", C.c_uint64), ("history_slots", C.c_uint64), ("history_refused", C.c_uint64)]
+
+
+class RlLogTear(C.Structure):
+    """rl_log_tear (include/ratelimit_hip.h): rl_debug_log_tear's armed tear and its outcome."""
+    _fields_ = [("armed", C.c_uint32), ("protocol", C.c_uint32), ("sched", C.c_uint32 * 3),
+                ("entry", C.c_uint32 * 8), ("before", C.c_uint32 * 8), ("seen", C.c_uint32 * 12),
+                ("verdict", C.c_int32), ("reserved", C.c_uint32)]
 
 
 class RlConfigNode(C.Structure):
@@ -142,7 +149,7 @@ BATCH_DTYPES = {"stem_bytes": np.uint8, "stem_off": np.uint32, "now": np.int64, 
                 "rule_id": np.uint32}
 RESULT_DTYPES = {"code": np.uint8, "limit_remaining": np.uint32, "reset_s": np.uint32, "stats": np.uint64,
                  "status": np.uint8}
-ABI_VERSION = 4
+ABI_VERSION = 5
 RL_COMM_ID_BYTES = 128  # include/ratelimit_hip.h
 RL_ROUTED_INFLIGHT = 6  # include/ratelimit_hip.h (routed batches in flight: the input-reuse distance)
 RL_ROUTED_LAG = 3  # include/ratelimit_hip.h (calls between a routed batch's partition and its owner pipeline)

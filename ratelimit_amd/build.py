@@ -10,6 +10,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libratelimit_hip.so")
+# The same library with the history log's tear hook compiled into its lookups
+# (RL_LOG_TEAR: rl_debug_log_tear, tests/test_gpu_log_tear.py); only
+# rl_kernels.hip differs. The product library has no hook.
+TEAR_LIB = os.path.join(HERE, "libratelimit_hip_tear.so")
 SOURCES = ["rl_kernels.hip", "rl_route.hip", "rl_match.hip", "rl_engine.hip", "rl_transport.hip", "rl_comm.hip",
            "rl_api.hip",
            "rl_pack.cpp"]
@@ -22,9 +26,9 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-ffp-contract=
 
 
 def _stale():
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(TEAR_LIB):
         return True
-    t = os.path.getmtime(LIB)
+    t = min(os.path.getmtime(LIB), os.path.getmtime(TEAR_LIB))
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.abspath(__file__)]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
@@ -36,21 +40,36 @@ def build(force=False, verbose=False, out=None, defines=()):
         return LIB
     objs, procs = [], []
     tag = "" if out is None else "_%x" % (hash(lib) & 0xFFFFFF)
-    for s in SOURCES:  # (compiled side by side: one hipcc per source)
-        o = os.path.join(CSRC, os.path.splitext(s)[0] + tag + ".o")
-        cmd = [HIPCC] + FLAGS + ["-D" + d for d in defines] + ["-c", os.path.join(CSRC, s), "-o", o]
+
+    def compile_(s, o, extra=()):
+        cmd = [HIPCC] + FLAGS + ["-D" + d for d in tuple(defines) + tuple(extra)] + ["-c", os.path.join(CSRC, s),
+                                                                                     "-o", o]
         if verbose:
             print(" ".join(cmd))
         procs.append((subprocess.Popen(cmd), cmd))
+
+    for s in SOURCES:  # (compiled side by side: one hipcc per source)
+        o = os.path.join(CSRC, os.path.splitext(s)[0] + tag + ".o")
+        compile_(s, o)
         objs.append(o)
+    tear_obj = None
+    if out is None:
+        tear_obj = os.path.join(CSRC, "rl_kernels_tear.o")
+        compile_("rl_kernels.hip", tear_obj, ["RL_LOG_TEAR=1"])
     for p, cmd in procs:
         if p.wait() != 0:
             raise subprocess.CalledProcessError(p.returncode, cmd)
-    # RCCL is dlopen'ed by rl_comm.hip (libdl), never linked
-    cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", lib] + objs + ["-ldl"]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd)
+
+    def link(path, objects):  # (RCCL is dlopen'ed by rl_comm.hip (libdl), never linked)
+        cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", path] + objects + ["-ldl"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+
+    link(lib, objs)
+    if tear_obj:
+        link(TEAR_LIB, [tear_obj] + objs[1:])
+        os.remove(tear_obj)
     for o in objs:
         os.remove(o)
     return lib

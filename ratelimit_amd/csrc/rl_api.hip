@@ -685,6 +685,7 @@ int rl_table_info_get(rl_ctx* c, rl_table_info* info) {
     sum.history_appended += x.history_appended;
     sum.history_lost += x.history_lost;
     sum.history_slots += x.history_slots;
+    sum.history_refused += x.history_refused;
     sum.batches = std::max(sum.batches, x.batches);
   }
   *info = sum;
@@ -808,6 +809,11 @@ int rl_table_info_shard(rl_ctx* c, uint32_t shard, rl_table_info* info) {
 int rl_debug_keys(rl_ctx* c, const rl_batch* in, uint8_t* out_bytes, uint32_t* out_off, uint32_t out_cap) {
   if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
   return from_engine(c, c->e[0], eng_debug_keys(c->e[0], in, out_bytes, out_off, out_cap));
+}
+
+int rl_debug_log_tear(rl_ctx* c, const rl_log_tear* arm, rl_log_tear* out) {
+  if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
+  return from_engine(c, c->e[0], eng_debug_log_tear(c->e[0], arm, out));
 }
 
 int rl_debug_decide(rl_ctx* c, uint32_t n, const uint32_t* before, const uint32_t* after, const uint8_t* lc_hit,

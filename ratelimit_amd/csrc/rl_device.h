@@ -89,6 +89,18 @@ constexpr uint32_t LOG_POS_BITS = 26;                     // entry pointer = par
 constexpr uint32_t LOG_POS_MASK = (1u << LOG_POS_BITS) - 1u;
 constexpr uint32_t LOG_PART_MAX = 1u << 25;               // entries per partition (2^31 in all)
 constexpr uint32_t LOG_CTR_STRIDE = 16;                   // counters on 128-B lines of their own
+// Word k of partition p's line: [0] the append counter, [1] its value when the
+// batch's table stage began (k_log_epoch). Line LOG_PARTS: [0] lookups that met
+// an overwritten entry, [1] appends refused (below).
+constexpr uint32_t LOG_CTR_EPOCH = 1;
+// Chain pointer standing for a record the log could not keep (its partition
+// had taken log_cap appends in this batch already): its position is past any
+// partition, so a walk that reaches it fails like one that meets an
+// overwritten entry (RL_E_TIME unless the window is dead).
+constexpr uint32_t LOG_LOST = LOG_POS_MASK;
+static_assert(LOG_LOST != LOG_NONE && (LOG_LOST & LOG_POS_MASK) >= LOG_PART_MAX, "LOG_LOST is no position");
+// An entry's header tag while the entry is being written (tags are >= 2).
+constexpr uint32_t LOG_TAG_BUSY = 0;
 constexpr uint32_t LOG_MAX_HOPS = 1u << 16;               // a chain walk gives up (RL_E_TIME) past this
 // Window w < cur_ws is within HIST_W windows of the key's newest one.
 __host__ __device__ inline bool hist_reach(uint32_t w, uint32_t cur_ws, uint32_t d) { return cur_ws - w <= HIST_W * d; }

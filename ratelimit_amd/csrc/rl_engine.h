@@ -72,6 +72,7 @@ struct Engine {
   uint32_t log_cap = 0;
   unsigned long long* log_ctr = nullptr;
   uint32_t horizon = 0;
+  uint32_t* tear = nullptr;  // rl_debug_log_tear's armed state (device; RL_LOG_TEAR builds)
   // RL_DEBUG_COPYTIME: host-fed input copies timed with events (stderr at destroy)
   bool copy_time = false;
   // RL_DEBUG_HOSTTIME: host seconds per section of the host-fed prefixed path (stderr at destroy)
@@ -174,6 +175,7 @@ int eng_sweep(Engine* c, int64_t now, uint64_t* n_evicted);
 int eng_restore(Engine* c, const rl_restore_batch* in);
 int eng_table_info_get(Engine* c, rl_table_info* info);
 int eng_debug_keys(Engine* c, const rl_batch* in, uint8_t* out_bytes, uint32_t* out_off, uint32_t out_cap);
+int eng_debug_log_tear(Engine* c, const rl_log_tear* arm, rl_log_tear* out);
 int eng_debug_decide(Engine* c, uint32_t n, const uint32_t* before, const uint32_t* after, const uint8_t* lc_hit,
                      const uint32_t* hits, const uint32_t* limit, const uint8_t* unit, const uint8_t* flags,
                      const int64_t* now, uint8_t* code, uint32_t* remaining, uint32_t* reset_s, uint64_t* stat_deltas,

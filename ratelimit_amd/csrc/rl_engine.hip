@@ -230,7 +230,8 @@ BatchDev dev_view(const Engine* c, const rl_batch* in, uint32_t stem_cap) {
 }
 
 // The history log's append counters (LOG_PARTS) and its lost-lookup count.
-hipError_t log_ctr_get(Engine* c, std::vector<unsigned long long>& ctr, unsigned long long* lost) {
+hipError_t log_ctr_get(Engine* c, std::vector<unsigned long long>& ctr, unsigned long long* lost,
+                       unsigned long long* refused = nullptr) {
   std::vector<unsigned long long> h((size_t)(LOG_PARTS + 1) * LOG_CTR_STRIDE);
   hipError_t e = hipMemcpyAsync(h.data(), c->log_ctr, h.size() * 8, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -238,6 +239,7 @@ hipError_t log_ctr_get(Engine* c, std::vector<unsigned long long>& ctr, unsigned
   ctr.resize(LOG_PARTS);
   for (uint32_t k = 0; k < LOG_PARTS; k++) ctr[k] = h[(size_t)k * LOG_CTR_STRIDE];
   if (lost) *lost = h[(size_t)LOG_PARTS * LOG_CTR_STRIDE];
+  if (refused) *refused = h[(size_t)LOG_PARTS * LOG_CTR_STRIDE + 1];
   return hipSuccess;
 }
 
@@ -249,6 +251,7 @@ TableDev table_view(Engine* c) {
   t.log_cap = c->log_cap;
   t.horizon = c->horizon;
   t.hist_lost = c->log_ctr + (size_t)LOG_PARTS * LOG_CTR_STRIDE;
+  t.tear = c->tear;
   t.mask = c->nslots - 1;
   t.arena = c->arena;
   t.arena_used16 = c->s[0].counters + 4;
@@ -543,7 +546,7 @@ void eng_destroy(Engine* c) {
   if (c->caller_ready) (void)hipEventDestroy(c->caller_ready);
   if (c->h_base) (void)hipHostFree(c->h_base);
   const Scratch& s0 = c->s[0];
-  void* bufs[] = {c->slots, c->log, c->log_ctr, c->arena, c->arena2, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
+  void* bufs[] = {c->slots, c->log, c->log_ctr, c->tear, c->arena, c->arena2, c->errw, s0.stripes, s0.time_floor, s0.counters, c->d_stem, c->d_off,
                   c->d_now, c->d_req, c->d_unit, c->d_flags, c->d_limit, c->d_hits, c->d_rule, c->d_code, c->d_status,
                   c->d_rem,
                   c->d_reset, c->d_stats};
@@ -1247,12 +1250,13 @@ int eng_table_info_get(Engine* c, rl_table_info* info) {
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(c->h_counters, c->s[0].counters, 40, hipMemcpyDeviceToHost, c->stream));
   std::vector<unsigned long long> ctr;
-  unsigned long long lost = 0;
-  HIPCHK(c, log_ctr_get(c, ctr, &lost));  // (synchronises: h_counters is read below)
+  unsigned long long lost = 0, refused = 0;
+  HIPCHK(c, log_ctr_get(c, ctr, &lost, &refused));  // (synchronises: h_counters is read below)
   info->history_entries = (uint64_t)LOG_PARTS * c->log_cap;
   info->history_appended = 0;
   for (unsigned long long k : ctr) info->history_appended += k;
   info->history_lost = lost;
+  info->history_refused = refused;
   info->history_slots = c->h_counters[3];
   info->table_slots = c->nslots;
   info->live_slots = c->h_counters[0];
@@ -1299,6 +1303,31 @@ int eng_debug_keys(Engine* c, const rl_batch* in, uint8_t* out_bytes, uint32_t* 
   delete[] h_out;
   delete[] h_len;
   return rc;
+}
+
+int eng_debug_log_tear(Engine* c, const rl_log_tear* arm, rl_log_tear* out) {
+  if (!c) return set_err(c, RL_E_INVALID, "gpu: null ctx");
+  if (!log_tear_hook()) return set_err(c, RL_E_INVALID, "gpu: rl_debug_log_tear needs a library built with RL_LOG_TEAR");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, after_batches(c, c->stream));
+  if (!c->tear) {
+    HIPCHK(c, dalloc(&c->tear, sizeof(rl_log_tear) / 4));
+    HIPCHK(c, hipMemsetAsync(c->tear, 0, sizeof(rl_log_tear), c->stream));
+  }
+  if (out) {
+    HIPCHK(c, hipMemcpyAsync(out, c->tear, sizeof *out, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->tear, 0, 4, c->stream));  // disarmed
+  }
+  if (arm) {
+    if (arm->protocol > 1 || arm->sched[0] > arm->sched[1] || arm->sched[1] > arm->sched[2])
+      return set_err(c, RL_E_INVALID, "gpu: bad rl_log_tear");
+    rl_log_tear a = *arm;
+    a.armed = 1;
+    a.verdict = 0;
+    HIPCHK(c, hipMemcpyAsync(c->tear, &a, sizeof a, hipMemcpyHostToDevice, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return RL_OK;
 }
 
 int eng_debug_decide(Engine* c, uint32_t n, const uint32_t* before, const uint32_t* after, const uint8_t* lc_hit,

@@ -168,7 +168,8 @@ struct TableDev {
   unsigned long long* log_ctr;
   uint32_t log_cap;  // entries per partition (power of 2)
   uint32_t horizon;
-  unsigned long long* hist_lost;  // lookups that met an entry the log had overwritten
+  unsigned long long* hist_lost;  // lookups that met an entry the log had overwritten ([1]: appends refused)
+  uint32_t* tear;  // RL_LOG_TEAR builds only (tests): an armed rl_log_tear, or null
   uint64_t mask;
   uint8_t* arena;
   unsigned long long* arena_used16;
@@ -346,6 +347,8 @@ void launch_arena_compact(Slot* slots, uint64_t nslots, const uint8_t* from, uin
                           hipStream_t st);
 void launch_lc_count(const TableDev& t, uint64_t nslots, uint32_t now, unsigned long long* out, hipStream_t st);
 void launch_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out, hipStream_t st);
+// Built with RL_LOG_TEAR (rl_debug_log_tear's hook in the history log's lookups)?
+bool log_tear_hook();
 void launch_debug_keys(const BatchDev& b, uint8_t* out, uint32_t* klen, hipStream_t st);
 void launch_debug_decide(uint32_t n, const uint32_t* before, const uint32_t* after, const uint8_t* lc_hit,
                          const uint32_t* hits, const uint32_t* limit, const uint8_t* unit, const uint8_t* flags,

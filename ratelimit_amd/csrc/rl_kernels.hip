@@ -825,25 +825,144 @@ __device__ inline bool hist_absent_ok(const TableDev& t, uint32_t now, uint32_t 
   return hist_reach(w, cur_ws, d) || (uint64_t)now + t.horizon + d >= (uint64_t)cur_ws || hist_dead(now, w, d);
 }
 
+// ---- Publishing an entry while others may read it. A lookup can reach an
+// entry that is being overwritten: its chain was appended in an earlier batch
+// and the partition has wrapped onto it since. Each entry is two 16-B halves
+// (a dwordx4 is written and read whole); the writer and the reader follow a
+// seqlock so a lookup never pairs one write's header with another's record:
+//  - writer: the header with its tag BUSY, then the record, then the header
+//    (LOG_WRITE_STEPS stores, in program order: the compiler barriers keep
+//    them in order, and the hardware applies one wave's stores to one 128-B
+//    line in order, in this CU's path and in the L2 channel that owns the line;
+//    another XCD sees the line only as whole write-backs of that L2's state,
+//    i.e. after some prefix of the three stores);
+//  - reader: the header, the record, the header again past this CU's L1; the
+//    record is used (even only to rule the entry out) when both headers are
+//    equal and carry the owner's tag. A record changed between the two header
+//    loads was written after an invalidation the second load sees (BUSY, or a
+//    newer header).
+// This holds when at most one writer writes an entry in a batch's table stage:
+// log_append refuses an append that would overwrite an entry the same batch
+// appended (the partition's counter at the batch's start, k_log_epoch), and
+// the only other write, k_late's alias write-back, goes to an entry appended
+// earlier in the same batch, which is therefore never overwritten under it.
+// RL_LOG_TEAR builds (tests/test_gpu_log_tear.py) replay a concurrent writer's
+// steps between the reader's loads in every interleaving.
+__device__ __forceinline__ void log_order() { __asm__ __volatile__("" ::: "memory"); }
+constexpr uint32_t LOG_WRITE_STEPS = 3;
+
+// Step s of writing entry e (header h, record r). legacy: round 5's order
+// (header, record; 2 steps), kept for the tear tests only.
+__device__ __forceinline__ void log_write_step(uint4* e, uint32_t s, const uint4& h, const uint4& r, bool legacy) {
+  if (legacy) {
+    if (s == 0) e[0] = h;
+    else e[1] = r;
+  } else if (s == 0) {
+    e[0] = make_uint4(h.x, LOG_TAG_BUSY, h.z, h.w);
+  } else if (s == 1) {
+    e[1] = r;
+  } else {
+    e[0] = h;
+  }
+  log_order();
+}
+
 // Append r to the chain whose head is prev (slot si, tag, newest window
-// t_app); returns the new head. The active lanes of a wave take consecutive
-// entries of one partition with one atomic (partitions spread by workgroup
-// and wave), so appends are coalesced stores.
+// t_app); returns the new head, or LOG_LOST when the partition has taken
+// log_cap appends in this batch already (one batch's appends never wrap a
+// partition onto its own entries; counted in rl_table_info.history_refused).
+// The active lanes of a wave take consecutive entries of one partition with
+// one atomic (partitions spread by workgroup and wave), so appends are
+// coalesced stores.
 __device__ inline uint32_t log_append(const TableDev& t, uint32_t si, uint32_t tag, uint32_t prev, uint32_t t_app,
                                       const Win& r) {
   const uint32_t lane = __lane_id();
   const uint32_t p = (blockIdx.x * 4u + (threadIdx.x >> 6)) & (LOG_PARTS - 1u);
   const uint64_t act = __ballot(1);
   const uint32_t leader = (uint32_t)__ffsll((unsigned long long)act) - 1u;
+  unsigned long long* line = &t.log_ctr[(size_t)p * LOG_CTR_STRIDE];
   unsigned long long k = 0;
-  if (lane == leader) k = atomicAdd(&t.log_ctr[(size_t)p * LOG_CTR_STRIDE], (unsigned long long)__popcll(act));
+  if (lane == leader) k = atomicAdd(line, (unsigned long long)__popcll(act));
   k = __shfl(k, leader, 64) + (unsigned long long)__popcll(act & ((1ull << lane) - 1ull));
+  if (k - line[LOG_CTR_EPOCH] >= t.log_cap) {
+    atomicAdd(t.hist_lost + 1, 1ull);
+    return LOG_LOST;
+  }
   const uint32_t pos = (uint32_t)k & (t.log_cap - 1u);
   uint4* e = reinterpret_cast<uint4*>(&t.log[(size_t)p * t.log_cap + pos]);
-  e[0] = make_uint4(si, tag, prev, t_app);
-  e[1] = make_uint4(r.ws, r.count, r.expire, r.lc);
+  const uint4 h = make_uint4(si, tag, prev, t_app), rv = make_uint4(r.ws, r.count, r.expire, r.lc);
+#pragma unroll
+  for (uint32_t s = 0; s < LOG_WRITE_STEPS; s++) log_write_step(e, s, h, rv, false);
   return (p << LOG_POS_BITS) | pos;
 }
+
+// The header of e re-read past this CU's L1 (agent scope).
+__device__ __forceinline__ uint4 log_hdr_reread(const uint4* e) {
+  const uint32_t* hd = reinterpret_cast<const uint32_t*>(e);
+  return make_uint4(__hip_atomic_load(hd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                    __hip_atomic_load(hd + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                    __hip_atomic_load(hd + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                    __hip_atomic_load(hd + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+#ifndef RL_LOG_TEAR
+#define RL_LOG_TEAR 0
+#endif
+#if RL_LOG_TEAR
+// Test builds: the armed rl_log_tear (include/ratelimit_hip.h, u32 words)
+// fires at the first entry the next lookup reads. Its writer's steps are
+// applied by the reading lane itself between its loads, per the schedule.
+enum : uint32_t { TR_ARMED = 0, TR_PROTO = 1, TR_SCHED = 2, TR_ENTRY = 5, TR_BEFORE = 13, TR_SEEN = 21,
+                  TR_VERDICT = 33 };
+struct LogTear {
+  uint32_t* p = nullptr;
+  uint4 h, r;
+  uint32_t done = 0, n = 0;
+  bool legacy = false;
+  __device__ inline void fire(const TableDev& t, uint4* e, uint32_t si, uint32_t tag) {
+    if (!t.tear || atomicCAS(&t.tear[TR_ARMED], 1u, 2u) != 1u) return;
+    p = t.tear;
+    const uint4 a = e[0], b = e[1];
+    const uint32_t o[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}, own[4] = {si, tag, a.z, a.w};
+    uint32_t v[8];
+    for (uint32_t k = 0; k < 8; k++) {
+      p[TR_BEFORE + k] = o[k];
+      v[k] = p[TR_ENTRY + k];
+      if (k < 4 && v[k] == 0xFFFFFFFFu) v[k] = own[k];  // (the entry's own slot / tag / prev / t_app)
+    }
+    h = make_uint4(v[0], v[1], v[2], v[3]);
+    r = make_uint4(v[4], v[5], v[6], v[7]);
+    legacy = p[TR_PROTO] != 0;
+    n = legacy ? 2u : LOG_WRITE_STEPS;
+  }
+  __device__ inline void to(uint4* e, uint32_t upto) {  // the writer's steps before the reader's next load
+    for (; p && done < upto && done < n; done++) log_write_step(e, done, h, r, legacy);
+  }
+  __device__ inline void before_load(uint4* e, uint32_t i) {
+    if (p) to(e, p[TR_SCHED + i]);
+  }
+  __device__ inline void seen(uint32_t i, const uint4& v) {
+    if (!p) return;
+    p[TR_SEEN + 4 * i] = v.x;
+    p[TR_SEEN + 4 * i + 1] = v.y;
+    p[TR_SEEN + 4 * i + 2] = v.z;
+    p[TR_SEEN + 4 * i + 3] = v.w;
+  }
+  __device__ inline void verdict(uint4* e, int v) {
+    if (!p) return;
+    to(e, n);  // (the writer finishes)
+    p[TR_VERDICT] = (uint32_t)v;
+    p = nullptr;
+  }
+};
+#else
+struct LogTear {  // (product builds: no hook)
+  __device__ __forceinline__ void fire(const TableDev&, uint4*, uint32_t, uint32_t) {}
+  __device__ __forceinline__ void before_load(uint4*, uint32_t) {}
+  __device__ __forceinline__ void seen(uint32_t, const uint4&) {}
+  __device__ __forceinline__ void verdict(uint4*, int) {}
+};
+#endif
 
 // The newest logged record of window w on slot si's chain from head (cur_ws:
 // the slot's newest window): 1 found (*out), 0 none on the chain, -1 an
@@ -862,22 +981,31 @@ __device__ inline int log_find(const TableDev& t, uint32_t head, uint32_t si, ui
       power <<= 1;
       lam = 0;
     }
-    const uint4* e = reinterpret_cast<const uint4*>(&t.log[(size_t)(ptr >> LOG_POS_BITS) * t.log_cap + pos]);
+    uint4* e = reinterpret_cast<uint4*>(&t.log[(size_t)(ptr >> LOG_POS_BITS) * t.log_cap + pos]);
+    LogTear tr;
+    tr.fire(t, e, si, tag);
+    tr.before_load(e, 0);
     const uint4 a = e[0];
-    if (a.x != si || a.y != tag || a.w > tprev) break;  // overwritten
+    tr.seen(0, a);
+    log_order();
+    tr.before_load(e, 1);
     const uint4 b = e[1];
+    tr.seen(1, b);
+    log_order();
+    tr.before_load(e, 2);
+    const uint4 a2 = log_hdr_reread(e);
+    tr.seen(2, a2);
+    // overwritten (owner, order), being written (BUSY), or rewritten between the loads
+    if (a.x != si || a.y != tag || a.w > tprev || a2.x != a.x || a2.y != a.y || a2.z != a.z || a2.w != a.w) {
+      tr.verdict(e, -1);
+      break;
+    }
     if (b.x == w) {
-      // Another lane's append may have overwritten the entry between the two
-      // 16-B loads as the log wraps (header of the old owner, record of the
-      // new): the header, re-read past this CU's L1, must be the one checked.
-      const uint32_t* hd = reinterpret_cast<const uint32_t*>(e);
-      if (__hip_atomic_load(hd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.x ||
-          __hip_atomic_load(hd + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.y ||
-          __hip_atomic_load(hd + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.w)
-        break;  // (treated as overwritten)
+      tr.verdict(e, 1);
       *out = Win{b.x, b.y, b.z, b.w};
       return 1;
     }
+    tr.verdict(e, 0);
     if (a.w <= w) return 0;  // every older entry holds a window below its t_app <= w
     tprev = a.w;
     ptr = a.z;
@@ -4335,7 +4463,10 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
             const uint32_t bits = (st.x >> (3 * k)) & 7u;
             if (!(bits & 3u)) continue;
             const uint32_t idx = k == 0 ? sl.x : k == 1 ? sl.y : k == 2 ? sl.z : sl.w;
-            // a cur, or the new version alias_setup appended to the unit's history log
+            // a cur, or the new version alias_setup appended to the unit's history
+            // log in this batch (no append of the batch overwrites it: log_append;
+            // LOG_LOST when the log refused it: the window's later lookups fail)
+            if ((bits & 2u) && (idx & LOG_POS_MASK) >= t.log_cap) continue;
             Win* R = (bits & 2u) ? &t.log[(size_t)(idx >> LOG_POS_BITS) * t.log_cap + (idx & LOG_POS_MASK)].w
                                  : &t.slots[idx].cur;
             if (bits & 4u) {  // same store: INCRBY + EXPIRE
@@ -4646,6 +4777,15 @@ __global__ __launch_bounds__(256, RL_LATE_OCC) void k_late(BatchDev b, TableDev 
          blk += gridDim.x - RUNS_GENERAL_LATE_BLOCKS)
       fast_emit_body(blk, sorted_n, b.n_rules, t, P, rec_s, svals, res, segsum, rid, run_start, run_end, run_flags,
                      run_state, run_alias, run_f, stats, stripes, err, fast_blk);
+}
+
+// The history log's append counters as the batch's table stage begins (the
+// previous batch's k_late is done): log_append refuses to wrap a partition onto
+// entries of the batch itself, so each entry has one writer per batch (the
+// seqlock above).
+__global__ __launch_bounds__(64) void k_log_epoch(unsigned long long* __restrict__ log_ctr) {
+  unsigned long long* line = log_ctr + (size_t)threadIdx.x * LOG_CTR_STRIDE;
+  line[LOG_CTR_EPOCH] = line[0];
 }
 
 // First kernel of the table stage: merge this batch's validation errors into
@@ -4976,6 +5116,8 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
                     unsigned long long* kt_acc, bool early) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
+  static_assert(LOG_PARTS == 64, "k_log_epoch: one lane per partition");
+  if (b.n) k_log_epoch<<<1, LOG_PARTS, 0, st>>>(t.log_ctr);
   if (!early)
     k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, errb_prev, s.defer2_n, s.defer1_n, o.stats, m, s.fast_blk,
                                   cdiv(b.n, 256 * 32));
@@ -5040,6 +5182,8 @@ void launch_lc_count(const TableDev& t, uint64_t nslots, uint32_t now, unsigned 
 void launch_table_info(const Slot* slots, uint64_t nslots, unsigned long long* out, hipStream_t st) {
   k_table_info<<<2048, 256, 0, st>>>(slots, nslots, out);
 }
+
+bool log_tear_hook() { return RL_LOG_TEAR != 0; }
 
 void launch_debug_keys(const BatchDev& b, uint8_t* out, uint32_t* klen, hipStream_t st) {
   if (b.n) k_debug_keys<<<cdiv(b.n, 256), 256, 0, st>>>(b, out, klen);

@@ -22,7 +22,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from . import abi
-from ._lib import RedisError, check, lib
+from ._lib import RedisError, check, lib, load
 from .packing import PackedBatch, RuleInterner, pack_calls
 from .types import OK, DescriptorStatus, Limit  # noqa: F401  (re-exported data model)
 
@@ -108,12 +108,14 @@ class Backend:
 
     def __init__(self, near_limit_ratio=0.8, local_cache=False, per_second=False, jitter=0,
                  table_slots=1 << 20, max_batch=1 << 16, max_rules=1 << 12, device=0, arena_bytes=0,
-                 max_stem_bytes=0, hash_seed=0, debug_hash_bits=0, n_shards=1, shard_devices=None, history_entries=0):
+                 max_stem_bytes=0, hash_seed=0, debug_hash_bits=0, n_shards=1, shard_devices=None, history_entries=0,
+                 library=None):
         """n_shards > 1: one ctx hash-shards its table over shard_devices (default:
         all on `device`) and routes every batch between them (rl_config.n_shards).
         history_entries: 32-B history log entries (0 = table_slots; rl_config.history_entries).
-        jitter: EXPIRATION_JITTER_MAX_SECONDS (the history horizon: older windows kept div + jitter s)."""
-        L = lib()
+        jitter: EXPIRATION_JITTER_MAX_SECONDS (the history horizon: older windows kept div + jitter s).
+        library: a path to another build of the library (tests: the RL_LOG_TEAR build); default the product's."""
+        L = self.L = lib() if library is None else load(library)
         err = C.create_string_buffer(512)
         self.cfg = _config(near_limit_ratio, local_cache, per_second, jitter, table_slots, max_batch, max_rules,
                            device, arena_bytes, max_stem_bytes, hash_seed, debug_hash_bits, n_shards, shard_devices,
@@ -122,9 +124,12 @@ class Backend:
         if not self.ctx:
             raise RedisError(err.value.decode())
 
+    def _check(self, rc):
+        check(self.ctx, rc, self.L)
+
     def close(self):
         if getattr(self, "ctx", None):
-            lib().rl_destroy(self.ctx)
+            self.L.rl_destroy(self.ctx)
             self.ctx = None
 
     def __del__(self):
@@ -140,7 +145,7 @@ class Backend:
         out = pb.alloc_result(isolate)
         b = pb.batch_struct()
         r = abi.make_result_struct(out)
-        check(self.ctx, lib().rl_do_limit(self.ctx, C.byref(b), C.byref(r)))
+        self._check(self.L.rl_do_limit(self.ctx, C.byref(b), C.byref(r)))
         n, nr = pb.n, pb.n_rules
         res = {"code": out["code"][:n], "limit_remaining": out["limit_remaining"][:n],
                "reset_s": out["reset_s"][:n], "stats": out["stats"][:nr * abi.RL_NUM_STATS]}
@@ -163,7 +168,7 @@ class Backend:
             stream = torch.cuda.current_stream().cuda_stream
         b = abi.make_batch_struct(dev_in, n, n_requests, n_rules)
         r = abi.make_result_struct(dev_out)
-        check(self.ctx, lib().rl_do_limit_async(self.ctx, C.byref(b), C.byref(r),
+        self._check(self.L.rl_do_limit_async(self.ctx, C.byref(b), C.byref(r),
                                                 C.c_void_p(stream) if stream else None))
 
     def do_limit_host_async(self, pb: PackedBatch, out: dict):
@@ -174,7 +179,7 @@ class Backend:
         asynchronous."""
         b = pb.batch_struct()
         r = abi.make_result_struct(out)
-        check(self.ctx, lib().rl_do_limit_host_async(self.ctx, C.byref(b), C.byref(r)))
+        self._check(self.L.rl_do_limit_host_async(self.ctx, C.byref(b), C.byref(r)))
         return b, r  # (the structs the call read; kept by the caller with the arrays)
 
     def do_limit_compact_async(self, cb, out: dict):
@@ -183,13 +188,13 @@ class Backend:
         final after synchronize()."""
         r = abi.make_result_struct(out)
         s = cb.struct()
-        check(self.ctx, lib().rl_do_limit_compact_async(self.ctx, C.byref(s), C.byref(r)))
+        self._check(self.L.rl_do_limit_compact_async(self.ctx, C.byref(s), C.byref(r)))
         return s, r
 
     def batch_progress(self):
         """rl_batch_progress: (batches submitted, batches complete), never waits."""
         a, b = C.c_uint64(), C.c_uint64()
-        check(self.ctx, lib().rl_batch_progress(self.ctx, C.byref(a), C.byref(b)))
+        self._check(self.L.rl_batch_progress(self.ctx, C.byref(a), C.byref(b)))
         return a.value, b.value
 
     def do_limit_prefixed_async(self, pb, out: dict):
@@ -198,7 +203,7 @@ class Backend:
         do_limit_host_async; final after synchronize()."""
         r = abi.make_result_struct(out)
         s = pb.struct()
-        check(self.ctx, lib().rl_do_limit_prefixed_async(self.ctx, C.byref(s), C.byref(r)))
+        self._check(self.L.rl_do_limit_prefixed_async(self.ctx, C.byref(s), C.byref(r)))
         return s, r
 
     # ---- config match + DoLimit on raw requests (rl_match.hip)
@@ -212,7 +217,7 @@ class Backend:
         t.key_bytes = abi.ptr(kb)
         t.key_bytes_len = sum(len(k) for k in tree.keys)
         t.cache_key_prefix = abi.ptr(pre)
-        check(self.ctx, lib().rl_config_load(self.ctx, C.byref(t)))
+        self._check(self.L.rl_config_load(self.ctx, C.byref(t)))
 
     def do_limit_requests(self, arrays: dict, n_rules: int) -> dict:
         """rl_do_limit_requests on pack_requests() arrays -> per-descriptor results + stats."""
@@ -231,14 +236,14 @@ class Backend:
         r = abi.RlRequestResult()
         for k in out:
             setattr(r, k, abi.ptr(out[k]))
-        check(self.ctx, lib().rl_do_limit_requests(self.ctx, C.byref(b), C.byref(r)))
+        self._check(self.L.rl_do_limit_requests(self.ctx, C.byref(b), C.byref(r)))
         res = {k: v[:n] for k, v in out.items() if k != "stats"}
         res["stats"] = out["stats"][:n_rules * abi.RL_NUM_STATS]
         return res
 
     def profile(self, enable: bool, every: int = 1):
         """Time every ``every``-th batch's stages with HIP events (rl_profile)."""
-        check(self.ctx, lib().rl_profile(self.ctx, max(int(every), 1) if enable else 0))
+        self._check(self.L.rl_profile(self.ctx, max(int(every), 1) if enable else 0))
 
     def profile_read(self):
         """-> ({prepare, sort, segment, table, finish} summed ms over the timed batches, and
@@ -246,11 +251,11 @@ class Backend:
         resets the sums."""
         ms = (C.c_double * len(PROFILE_FIELDS))()
         nb = C.c_uint64(0)
-        check(self.ctx, lib().rl_profile_read(self.ctx, ms, len(PROFILE_FIELDS), C.byref(nb)))
+        self._check(self.L.rl_profile_read(self.ctx, ms, len(PROFILE_FIELDS), C.byref(nb)))
         return dict(zip(PROFILE_FIELDS, list(ms))), nb.value
 
     def synchronize(self):
-        check(self.ctx, lib().rl_synchronize(self.ctx))
+        self._check(self.L.rl_synchronize(self.ctx))
 
     def restore(self, stems: Sequence[bytes], units, nows, counts, lc=None):
         from .packing import arrays_from_lists
@@ -263,46 +268,46 @@ class Backend:
         rb.n = n
         rb.stem_bytes, rb.stem_off, rb.unit = abi.ptr(a["stem_bytes"]), abi.ptr(a["stem_off"]), abi.ptr(a["unit"])
         rb.now, rb.count, rb.lc = abi.ptr(nowa), abi.ptr(cnt), abi.ptr(lca)
-        check(self.ctx, lib().rl_restore(self.ctx, C.byref(rb)))
+        self._check(self.L.rl_restore(self.ctx, C.byref(rb)))
 
     def sweep(self, now: int) -> int:
         ev = C.c_uint64(0)
-        check(self.ctx, lib().rl_sweep(self.ctx, now, C.byref(ev)))
+        self._check(self.L.rl_sweep(self.ctx, now, C.byref(ev)))
         return ev.value
 
     def table_info(self, shard=None) -> dict:
         """Table counters summed over shards (or of one shard)."""
         info = abi.RlTableInfo()
         if shard is None:
-            check(self.ctx, lib().rl_table_info_get(self.ctx, C.byref(info)))
+            self._check(self.L.rl_table_info_get(self.ctx, C.byref(info)))
         else:
-            check(self.ctx, lib().rl_table_info_shard(self.ctx, shard, C.byref(info)))
+            self._check(self.L.rl_table_info_shard(self.ctx, shard, C.byref(info)))
         return {f: getattr(info, f) for f, _ in abi.RlTableInfo._fields_}
 
     def local_cache_info(self, now: int) -> dict:
         """localCacheStats gauges (src/limiter/local_cache_stats.go:20-43)."""
         info = abi.RlLocalCacheInfo()
-        check(self.ctx, lib().rl_local_cache_info_get(self.ctx, now, C.byref(info)))
+        self._check(self.L.rl_local_cache_info_get(self.ctx, now, C.byref(info)))
         return {f: getattr(info, f) for f, _ in abi.RlLocalCacheInfo._fields_}
 
     def snapshot(self) -> np.ndarray:
         """Exact table image (counters, local cache, arena, time floor) as host bytes."""
         nb = C.c_uint64(0)
-        check(self.ctx, lib().rl_snapshot_size(self.ctx, C.byref(nb)))
+        self._check(self.L.rl_snapshot_size(self.ctx, C.byref(nb)))
         buf = np.empty(nb.value, np.uint8)
-        check(self.ctx, lib().rl_snapshot_save(self.ctx, abi.ptr(buf), nb.value))
+        self._check(self.L.rl_snapshot_save(self.ctx, abi.ptr(buf), nb.value))
         return buf
 
     def load_snapshot(self, buf: np.ndarray) -> None:
         buf = np.ascontiguousarray(buf, np.uint8)
-        check(self.ctx, lib().rl_snapshot_load(self.ctx, abi.ptr(buf), buf.size))
+        self._check(self.L.rl_snapshot_load(self.ctx, abi.ptr(buf), buf.size))
 
     def debug_keys(self, pb: PackedBatch) -> List[str]:
         cap = int(pb.arrays["stem_off"][-1]) + 24 * pb.n + 1
         buf = np.zeros(cap, np.uint8)
         off = np.zeros(pb.n + 1, np.uint32)
         b = pb.batch_struct()
-        check(self.ctx, lib().rl_debug_keys(self.ctx, C.byref(b), abi.ptr(buf), abi.ptr(off), cap))
+        self._check(self.L.rl_debug_keys(self.ctx, C.byref(b), abi.ptr(buf), abi.ptr(off), cap))
         return [bytes(buf[off[i]:off[i + 1]]).decode() for i in range(pb.n)]
 
     def debug_decide(self, before, after, lc_hit, hits, limit, unit, flags, now):
@@ -315,20 +320,52 @@ class Backend:
         reset = np.zeros(n, np.uint32)
         deltas = np.zeros(n * abi.RL_NUM_STATS, np.uint64)
         lc_set = np.zeros(n, np.uint8)
-        check(self.ctx, lib().rl_debug_decide(self.ctx, n, *[abi.ptr(x) for x in a], abi.ptr(code), abi.ptr(rem),
+        self._check(self.L.rl_debug_decide(self.ctx, n, *[abi.ptr(x) for x in a], abi.ptr(code), abi.ptr(rem),
                                               abi.ptr(reset), abi.ptr(deltas), abi.ptr(lc_set)))
         return code, rem, reset, deltas.reshape(n, abi.RL_NUM_STATS), lc_set
 
 
+# rl_status of a device-level failure: the GPU or its runtime, not a request
+DEVICE_FAILURES = (abi.RL_E_HIP, abi.RL_E_COMM, abi.RL_E_INTERNAL)
+
+
+class HealthMonitor:
+    """The batcher's health monitor (go/src/gpu/cache_impl.go healthMonitor):
+    a device-level failure fails the server's health check once, the next
+    success marks it OK again — what the Redis pool does on its connections
+    (src/redis/driver_impl.go:31-52, server.HealthCheckFail / HealthCheckOK,
+    src/server/server.go:47-48). Request-level failures (RL_E_TIME,
+    RL_E_INVALID, RL_E_CAPACITY, a full table) leave it as it is. `server`:
+    an object with health_check_fail() and health_check_ok() (None: off)."""
+
+    def __init__(self, server=None):
+        self.server = server
+        self.unhealthy = False
+
+    def observe(self, err):
+        if self.server is None:
+            return
+        if isinstance(err, RedisError) and err.status in DEVICE_FAILURES:
+            if not self.unhealthy:
+                self.server.health_check_fail()
+                self.unhealthy = True
+        elif err is None and self.unhealthy:
+            self.server.health_check_ok()
+            self.unhealthy = False
+
+
 class GpuRateLimitCache:
-    """limiter.RateLimitCache backed by libratelimit_hip.so (BACKEND_TYPE=gpu)."""
+    """limiter.RateLimitCache backed by libratelimit_hip.so (BACKEND_TYPE=gpu).
+    health_server (GPU_HEALTH_CHECK_DEVICE): the server whose health check a
+    device failure fails (HealthMonitor)."""
 
     def __init__(self, time_source: Optional[TimeSource] = None, near_limit_ratio: float = 0.8,
                  local_cache: bool = False, cache_key_prefix: str = "", per_second: bool = False,
-                 expiration_jitter_max_seconds: int = 0, **backend_kw):
+                 expiration_jitter_max_seconds: int = 0, health_server=None, **backend_kw):
         self.time_source = time_source or TimeSource()
         self.prefix = cache_key_prefix
         self.interner = RuleInterner()
+        self.health = HealthMonitor(health_server)
         self.backend = Backend(near_limit_ratio, local_cache, per_second, expiration_jitter_max_seconds,
                                **backend_kw)
 
@@ -348,7 +385,12 @@ class GpuRateLimitCache:
         that RPC only, as checkError does per DoLimit, fixed_cache_impl.go:90-95);
         every other call is answered."""
         pb = pack_calls(calls, self.prefix, self.interner)
-        res = self.backend.do_limit_packed(pb, isolate)
+        try:
+            res = self.backend.do_limit_packed(pb, isolate)
+        except RedisError as e:
+            self.health.observe(e)
+            raise
+        self.health.observe(None)
         outs = [[DescriptorStatus(OK, None, 0, None) for _ in req.descriptors] for req, _, _ in calls]
         code, rem, rst = res["code"], res["limit_remaining"], res["reset_s"]
         failed = {}

@@ -57,7 +57,11 @@ int main(void) {
   F(rl_table_info, table_slots); F(rl_table_info, live_slots); F(rl_table_info, tombstones);
   F(rl_table_info, arena_bytes_used); F(rl_table_info, exact_stems); F(rl_table_info, batches);
   F(rl_table_info, decisions); F(rl_table_info, history_entries); F(rl_table_info, history_appended);
-  F(rl_table_info, history_lost); F(rl_table_info, history_slots);
+  F(rl_table_info, history_lost); F(rl_table_info, history_slots); F(rl_table_info, history_refused);
+
+  S(rl_log_tear);
+  F(rl_log_tear, armed); F(rl_log_tear, protocol); F(rl_log_tear, sched); F(rl_log_tear, entry);
+  F(rl_log_tear, before); F(rl_log_tear, seen); F(rl_log_tear, verdict); F(rl_log_tear, reserved);
 
   S(rl_config_node);
   F(rl_config_node, parent); F(rl_config_node, key_off); F(rl_config_node, key_len);

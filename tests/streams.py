@@ -8,6 +8,7 @@ HOUR keys of one stem can share a Redis key at aligned window starts), window
 rollover across second/minute/hour boundaries, and hot keys.
 """
 import random
+import numpy as np
 
 from oracle import oracle as O
 
@@ -156,3 +157,18 @@ def python_oracle_run(calls, ratio=0.8, local_cache=False, prefix="", per_second
             if l is not None:
                 stats[l.stats.key] = l.stats.as_tuple()
     return outs, stats
+
+
+def drop_descriptors(a, n, nq, keep):
+    """The packed batch without the descriptors where keep is False (the
+    oracle's input when the GPU failed those alone: RL_E_TIME descriptors do
+    not INCRBY)."""
+    idx = np.nonzero(keep[:n])[0]
+    off = a["stem_off"]
+    o = np.zeros(idx.size + 1, np.uint32)
+    o[1:] = np.cumsum(off[idx + 1] - off[idx])
+    out = {"stem_bytes": np.concatenate([a["stem_bytes"][off[i]:off[i + 1]] for i in idx])
+           if idx.size else np.zeros(0, np.uint8), "stem_off": o, "now": a["now"]}
+    for k in ("req_idx", "unit", "flags", "limit", "hits", "rule_id"):
+        out[k] = a[k][idx]
+    return out, idx.size, nq

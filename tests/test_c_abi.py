@@ -36,7 +36,8 @@ MIRROR = {"rl_config": abi.RlConfig, "rl_batch": abi.RlBatch, "rl_result": abi.R
           "rl_config_node": abi.RlConfigNode, "rl_config_tree": abi.RlConfigTree,
           "rl_request_batch": abi.RlRequestBatch, "rl_request_result": abi.RlRequestResult,
           "rl_local_cache_info": abi.RlLocalCacheInfo, "rl_limit": abi.RlLimit,
-          "rl_batch_compact": abi.RlBatchCompact, "rl_batch_prefixed": abi.RlBatchPrefixed}
+          "rl_batch_compact": abi.RlBatchCompact, "rl_batch_prefixed": abi.RlBatchPrefixed,
+          "rl_log_tear": abi.RlLogTear}
 
 
 def _build(src, out, extra=()):

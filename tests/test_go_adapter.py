@@ -274,3 +274,56 @@ def test_routed_ctx_has_a_go_entry_point():
     assert "RoutedDoLimit" not in comm and "func CommIDFile(" in comm and "func (c *Ctx) CommInit(" in comm
     impl = strip_go(open(os.path.join(GO, "src", "gpu", "cache_impl.go")).read())
     assert "go this.batcherRouted()" in impl and "ctx.CommInit(s.GpuWorld, s.GpuRank, id)" in impl
+
+
+def test_go_struct_literals_are_keyed():
+    """No positional literal of a multi-field struct declared in go/src, and
+    every key a declared field (tests/go_lint.py: the composite-literal part
+    of `go vet`, which this image cannot run)."""
+    import go_lint
+    findings, types = go_lint.lint_tree(os.path.join(GO, "src"))
+    assert not findings, "\n".join(findings)
+    assert {"call", "flight", "reply", "TableInfo", "Options"} <= set(types["gpu"])
+
+
+def test_go_lint_names_the_round5_call_literal():
+    """Round 5's `&call{request, limits, now, done}` (4 values; `call` has 6
+    fields) is flagged; its keyed form is not; an unknown key is."""
+    import go_lint
+    src = open(os.path.join(GO, "src", "gpu", "cache_impl.go")).read()
+    types = go_lint.struct_fields(src)
+    assert len(types["call"]) == 6, types["call"]
+    bad = "func f() { c := &call{request, limits, this.timeSource.UnixNow(), make(chan reply, 1)} }"
+    f = go_lint.lint_source(bad, types, path="cache_impl.go")
+    assert any("positional literal of a 6-field struct (4 values)" in x for x in f), f
+    good = "func f() { c := &call{req: request, limits: limits, now: 1, done: make(chan reply, 1)} }"
+    assert go_lint.lint_source(good, types) == []
+    assert go_lint.lint_source("func f() { _ = reply{error: \"x\"} }", types)  # (the field is err)
+    # slice literals of the type and the type's own declaration are not struct literals
+    assert go_lint.lint_source("func f() { calls := []*call{first}; _ = calls }", types) == []
+
+
+def test_device_failures_flip_the_health_check():
+    """GPU loss fails the server's health check (the Redis pool does
+    it on its connections, src/redis/driver_impl.go:31-52): the batcher feeds
+    every batch's, request batch's and sweep's outcome to healthMonitor, which
+    calls srv.HealthCheckFail() on a device-level rl_status and HealthCheckOK()
+    at the next success; GPU_HEALTH_CHECK_DEVICE (default true) enables it."""
+    impl = strip_go(open(os.path.join(GO, "src", "gpu", "cache_impl.go")).read())
+    for fn in ("finish", "doRaw", "housekeeping"):
+        m = re.search(r"func \(this \*rateLimitCacheImpl\) %s\(" % fn, impl)
+        nxt = impl.find("\nfunc ", m.end())
+        body = impl[m.end():nxt if nxt >= 0 else len(impl)]
+        assert "this.health.observe(" in body, fn
+    m = re.search(r"func \(h \*healthMonitor\) observe\(err error\) \{", impl)
+    body = impl[m.end():impl.index("\nfunc ", m.end()) if "\nfunc " in impl[m.end():] else len(impl)]
+    assert "h.srv.HealthCheckFail()" in body and "h.srv.HealthCheckOK()" in body
+    dev = re.search(r"func deviceFailure\(err error\) bool \{(.*?)\n\}", impl, flags=re.S).group(1)
+    assert "StatusHIP" in dev and "StatusComm" in dev and "StatusInternal" in dev
+    gpu = strip_go(open(os.path.join(GO, "src", "gpu", "gpu.go")).read())
+    for name, c in (("StatusHIP", "RL_E_HIP"), ("StatusComm", "RL_E_COMM"), ("StatusInternal", "RL_E_INTERNAL")):
+        assert re.search(r"%s\s*=\s*int\(C\.%s\)" % (name, c), gpu), name
+    ctor = impl[impl.index("func NewRateLimitCacheImplFromSettings("):]
+    assert "s.GpuHealthCheckDevice && srv != nil" in ctor and "opt.HealthServer = srv" in ctor
+    assert re.search(r"GpuHealthCheckDevice\s+bool\s+`envconfig:\"GPU_HEALTH_CHECK_DEVICE\" default:\"true\"`",
+                     _added("settings.go.patch"))

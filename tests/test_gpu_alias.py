@@ -17,6 +17,7 @@ import pytest
 from oracle import c_oracle
 from ratelimit_amd import abi, workloads
 from ratelimit_amd.limiter import Backend
+import streams
 
 pytestmark = pytest.mark.gpu
 
@@ -228,3 +229,34 @@ def test_gpu_c2u_bench_scale_vs_c_oracle(lc):
     bs = list(workloads.c2u_stream(n_tenants=2_000_000, requests_per_batch=500_000, batches=4, now0=NOW0 + 38,
                                    sampler=z))
     _check(bs, lc, table_slots=1 << 23, max_batch=1 << 20)
+
+
+@pytest.mark.parametrize("lc", [False, True])
+def test_gpu_hot_override_far_too_small_log_fails_never_miscounts(lc):
+    """the alias groups' records in a history log far too small
+    (64 x 1024 entries, wrapping every few batches, J = 300): k_late writes a
+    group's count back into the log entry alias_setup appended in the same
+    batch, which no append of that batch may overwrite (log_append refuses
+    instead). Every descriptor is RL_E_TIME or equal to the oracle fed only
+    the descriptors that succeeded."""
+    be = Backend(0.8, lc, table_slots=1 << 17, max_batch=1 << 14, max_rules=8, history_entries=1, jitter=300)
+    co = c_oracle.COracle(0.8, lc, horizon=300)
+    failed_total = ok_total = 0
+    try:
+        assert be.table_info()["history_entries"] == 64 * 1024
+        for a, n, nq, nr in _stream(list(range(38, 98)) + list(range(40, 70)), rpb=8_000, tenants=30_000, seed=21):
+            g = be.do_limit_arrays(a, n, nq, nr, isolate=True)
+            failed = g["status"] != 0
+            assert (g["status"][failed] == abi.RL_E_TIME).all(), np.unique(g["status"])
+            keep = ~failed
+            o = co.do_limit(*streams.drop_descriptors(a, n, nq, keep), nr)
+            for k in ("code", "limit_remaining", "reset_s"):
+                assert np.array_equal(g[k][keep], o[k]), k
+            failed_total += int(failed.sum())
+            ok_total += int(keep.sum())
+        info = be.table_info()
+        assert info["history_appended"] > info["history_entries"]  # the log wrapped
+        assert ok_total > failed_total
+    finally:
+        be.close()
+        co.close()

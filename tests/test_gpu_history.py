@@ -47,16 +47,7 @@ def _compare(batches, lc, isolate=False, jitter=0):
 
 
 def _drop(a, n, nq, keep):
-    """The packed batch without the descriptors where keep is False."""
-    idx = np.nonzero(keep[:n])[0]
-    off = a["stem_off"]
-    o = np.zeros(idx.size + 1, np.uint32)
-    o[1:] = np.cumsum(off[idx + 1] - off[idx])
-    out = {"stem_bytes": np.concatenate([a["stem_bytes"][off[i]:off[i + 1]] for i in idx]), "stem_off": o,
-           "now": a["now"]}
-    for k in ("req_idx", "unit", "flags", "limit", "hits", "rule_id"):
-        out[k] = a[k][idx]
-    return out, idx.size, nq
+    return streams.drop_descriptors(a, n, nq, keep)
 
 
 def _stream(seed, n_tenants, nq, batches, step, max_back, unit=None, multi=False, hot=0):

@@ -134,3 +134,42 @@ def test_gpu_profile_sampling_counts_and_leaves_results_unchanged():
         assert cache.backend.profile_read()[1] == 0
     finally:
         cache.close()
+
+
+def test_gpu_cache_health_check_follows_device_failures():
+    """GpuRateLimitCache's health monitor on the real library: batches keep
+    the check quiet, a request-level failure (a malformed unit: RL_E_INVALID)
+    too; a device-level failure of a batch (RL_E_HIP, injected at the backend
+    call: a dead device cannot be made on demand) fails it and the next
+    answered batch marks it OK."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_health_cpu import FakeServer
+    from oracle import oracle as O
+    from ratelimit_amd.limiter import FixedTimeSource, GpuRateLimitCache
+    from ratelimit_amd import abi
+    srv = FakeServer()
+    cache = GpuRateLimitCache(FixedTimeSource(1_700_000_000), health_server=srv, table_slots=1 << 12,
+                              max_batch=1 << 10, max_rules=8)
+    req = O.RateLimitRequest("d", [O.Descriptor([("k", "v")])], 1)
+    lim = [O.RateLimit("d.k_v", O.RateLimitStats("d.k_v"), O.Limit(5, O.SECOND))]
+    try:
+        cache.do_limit(None, req, lim)
+        bad = [O.RateLimit("d.k_v", O.RateLimitStats("d.k_v"), O.Limit(5, 9))]
+        with pytest.raises(RedisError):
+            cache.do_limit(None, req, bad)
+        assert srv.calls == []
+        real = cache.backend.do_limit_packed
+
+        def dead(*a, **k):
+            raise RedisError("gpu: hipErrorLaunchFailure [RL_E_HIP]", abi.RL_E_HIP)
+        cache.backend.do_limit_packed = dead
+        with pytest.raises(RedisError):
+            cache.do_limit(None, req, lim)
+        assert srv.calls == ["fail"]
+        cache.backend.do_limit_packed = real
+        assert cache.do_limit(None, req, lim)[0].limit_remaining == 3
+        assert srv.calls == ["fail", "ok"]
+    finally:
+        cache.close()
