@@ -108,6 +108,9 @@ struct Engine {
   uint32_t* h_long = nullptr;  // pinned [NBUF]
   uint32_t long_recent = 0;    // batches left in long-run mode
   int long_mode = 1;           // RL_SPLIT_LONG: 0 never, 1 while recent batches had long runs, 2 always
+  uint32_t* h_big = nullptr;   // pinned [NBUF]: k_bucket queued a large bucket (hot keys)
+  uint32_t big_recent = 0;     // batches left with full large-bucket grids
+  int big_mode = 1;            // RL_BIG_CUE: 0 full grids always, 1 while recent batches had large buckets
   unsigned long long* h_counters = nullptr;
   std::string last_error;
   uint64_t batches = 0, decisions = 0;

@@ -159,12 +159,26 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     if (c->long_recent) c->long_recent--;
   }
   uint32_t* hint = c->long_mode ? c->h_long + k : nullptr;
+  // the large-bucket kernels' grids: full while recent batches had a bucket
+  // too large for k_bucket (hot keys: C2, C2U), one workgroup each otherwise
+  // (C1, C3): they are grid-stride, so an unexpected one is still sorted
+  bool big_full = c->big_mode == 0;
+  if (c->big_mode == 1) {
+    for (uint32_t j = 0; j < NBUF; j++)
+      if (__atomic_load_n(&c->h_big[j], __ATOMIC_RELAXED)) {
+        __atomic_store_n(&c->h_big[j], 0u, __ATOMIC_RELAXED);
+        c->big_recent = 4 * NBUF;
+      }
+    big_full = c->big_recent > 0;
+    if (c->big_recent) c->big_recent--;
+  }
+  uint32_t* bhint = c->big_mode == 1 ? c->h_big + k : nullptr;
   if (pipelined) {
     hipStream_t a = c->pipe[k];
     hipEvent_t* ev = prof_events(c);
     (void)hipStreamWaitEvent(a, c->b_done[k], 0);    // buffer k's previous batch is done
     (void)hipStreamWaitEvent(a, c->consumed[k], 0);  // ... and its routed results were read
-    launch_stage_a(b, c->s[k], isolate, P.per_second, a, ev, hint, lng);
+    launch_stage_a(b, c->s[k], isolate, P.per_second, a, ev, hint, lng, bhint, big_full);
     if (early) launch_b_begin_early(b, o, c->s[k], restore, a);  // (off the table-order chain)
     (void)hipStreamWaitEvent(a, c->b_table[c->last], 0);  // table order (not the previous k_finish)
     launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
@@ -174,7 +188,7 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     if (!st) st = c->stream;
     (void)after_batches(c, st);
     hipEvent_t* ev = prof_events(c);
-    launch_stage_a(b, c->s[k], isolate, P.per_second, st, ev, hint, lng);
+    launch_stage_a(b, c->s[k], isolate, P.per_second, st, ev, hint, lng, bhint, big_full);
     if (early) launch_b_begin_early(b, o, c->s[k], restore, st);
     launch_stage_b(b, o, t, P, c->s[k], restore, st, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
                    early);
@@ -396,9 +410,12 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   c->hk = hash_key_of(c->hash_seed, cfg.debug_hash_bits);
   c->nslots = cfg.table_slots;
   {
-    // per partition a power of two, and at least 1/16 of a batch: one batch's
-    // appends (at most one per descriptor, spread over the partitions by
-    // workgroup) never wrap a partition
+    // per partition a power of two, and at least 1/16 of a batch. A batch's
+    // appends are spread over the partitions by workgroup and wave, but a
+    // skewed one (a hot key replayed serially, the exact path's 8 workgroups)
+    // can send more than that to one partition: log_append then refuses the
+    // excess (rl_table_info.history_refused; those windows' later lookups are
+    // RL_E_TIME) rather than wrap onto entries of the same batch
     const uint64_t want = std::max<uint64_t>(cfg.history_entries / LOG_PARTS, std::max<uint64_t>(cfg.max_batch / 16, 1024));
     uint64_t cap = 1;
     while (cap * 2 <= want && cap * 2 <= LOG_PART_MAX) cap *= 2;
@@ -463,6 +480,9 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && hipHostMalloc((void**)&c->h_long, NBUF * sizeof(uint32_t)) == hipSuccess;
   if (ok) memset(c->h_long, 0, NBUF * sizeof(uint32_t));
   if (const char* sl = getenv("RL_SPLIT_LONG")) c->long_mode = atoi(sl);  // (A/B knob)
+  ok = ok && hipHostMalloc((void**)&c->h_big, NBUF * sizeof(uint32_t)) == hipSuccess;
+  if (ok) memset(c->h_big, 0, NBUF * sizeof(uint32_t));
+  if (const char* bc = getenv("RL_BIG_CUE")) c->big_mode = atoi(bc);  // (A/B knob)
   if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
   ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
        hipMemsetAsync(c->log_ctr, 0, (size_t)(LOG_PARTS + 1) * LOG_CTR_STRIDE * 8, c->stream) == hipSuccess &&
@@ -557,6 +577,7 @@ void eng_destroy(Engine* c) {
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->h_counters) (void)hipHostFree(c->h_counters);
   if (c->h_long) (void)hipHostFree(c->h_long);
+  if (c->h_big) (void)hipHostFree(c->h_big);
   for (void* p : {(void*)c->cfg_blob, (void*)c->mbuf})
     if (p) (void)hipFree(p);
   if (c->h_match) (void)hipHostFree(c->h_match);

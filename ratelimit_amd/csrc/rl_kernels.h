@@ -254,9 +254,14 @@ struct Scratch {
 // must run in batch order.
 // long_hint: a host word k_split sets when it meets a run over 1024 elements;
 // long_kernel: such runs go to k_split_long's 1024-lane workgroups (else
-// k_split's own 256-lane ones walk them)
+// k_split's own 256-lane ones walk them). big_hint: a host word k_bucket sets
+// when it queues a bucket too large for its LDS (hot keys); big_full: the
+// large-bucket kernels get their full grids (else one workgroup each: they are
+// grid-stride, so a batch with a large bucket the host did not expect is
+// still answered, more slowly; C1 never has one)
 void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_second, hipStream_t st,
-                    hipEvent_t* ev = nullptr, uint32_t* long_hint = nullptr, bool long_kernel = false);
+                    hipEvent_t* ev = nullptr, uint32_t* long_hint = nullptr, bool long_kernel = false,
+                    uint32_t* big_hint = nullptr, bool big_full = true);
 // errb_prev: the previous batch's table-stage word (this batch's starts from
 // it); table_done (optional) is recorded once the table kernels are done, before
 // k_finish: the next batch's stage B waits for it, not for k_finish.

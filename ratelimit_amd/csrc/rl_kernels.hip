@@ -896,13 +896,21 @@ __device__ inline uint32_t log_append(const TableDev& t, uint32_t si, uint32_t t
   return (p << LOG_POS_BITS) | pos;
 }
 
+#ifndef RL_LOG_REREAD
+#define RL_LOG_REREAD 1  // (diagnostic builds: 0 = re-read only a found record's header (round 5), 2 = a plain re-read)
+#endif
 // The header of e re-read past this CU's L1 (agent scope).
 __device__ __forceinline__ uint4 log_hdr_reread(const uint4* e) {
+#if RL_LOG_REREAD == 2
+  log_order();
+  return *e;
+#else
   const uint32_t* hd = reinterpret_cast<const uint32_t*>(e);
   return make_uint4(__hip_atomic_load(hd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                     __hip_atomic_load(hd + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                     __hip_atomic_load(hd + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                     __hip_atomic_load(hd + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#endif
 }
 
 #ifndef RL_LOG_TEAR
@@ -993,7 +1001,11 @@ __device__ inline int log_find(const TableDev& t, uint32_t head, uint32_t si, ui
     tr.seen(1, b);
     log_order();
     tr.before_load(e, 2);
+#if RL_LOG_REREAD == 0
+    const uint4 a2 = b.x == w ? log_hdr_reread(e) : a;
+#else
     const uint4 a2 = log_hdr_reread(e);
+#endif
     tr.seen(2, a2);
     // overwritten (owner, order), being written (BUSY), or rewritten between the loads
     if (a.x != si || a.y != tag || a.w > tprev || a2.x != a.x || a2.y != a.y || a2.z != a.z || a2.w != a.w) {
@@ -2071,7 +2083,8 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
     uint32_t* __restrict__ sh, uint32_t* __restrict__ segsum, uint32_t* __restrict__ rid,
     uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_end, unsigned long long* num_runs,
     uint32_t* __restrict__ drun, BigMeta* __restrict__ meta, uint32_t* big_n, uint32_t* __restrict__ work,
-    uint32_t* work_n, uint32_t* sorted_n, uint2* __restrict__ uniq, uint32_t* uniq_n, const uint32_t* err) {
+    uint32_t* work_n, uint32_t* sorted_n, uint2* __restrict__ uniq, uint32_t* uniq_n, const uint32_t* err,
+    uint32_t* big_hint) {
   using B = BkSmall;
   __shared__ BucketLds<B> L;
   if (*err) return;
@@ -2097,6 +2110,7 @@ __global__ __launch_bounds__(BkSmall::THREADS, 4) void k_bucket(
       for (uint32_t c = 0; c < BK_HEAVY; c++) M.heavy[c] = c < M.r ? L.heavy[c] : 0u;
       const uint32_t b = atomicAdd(big_n, 1u);
       meta[b] = M;
+      if (big_hint) *big_hint = 1u;  // (the host's cue: full large-bucket grids for the next batches)
       L.rb = b;
       L.nruns = M.item0;
       L.hcarry = M.nchunks;
@@ -4698,6 +4712,9 @@ __device__ __attribute__((always_inline)) inline void general_body(uint32_t blk,
 //
 // k_table: the runs of two or more (runs_body, blocks [0, g_runs)) and the keys
 // seen once (unique_body, the rest).
+#ifndef RL_KT_UNIQ_FIRST
+#define RL_KT_UNIQ_FIRST 0
+#endif
 #ifndef RL_KTABLE_WAVES
 #define RL_KTABLE_WAVES 5  // waves per SIMD: <= 96 VGPRs (110 uncapped: 4 waves); 5 vs 1: C1 +1.2 %, C2 +0.8 %, C2U -0.3 %; 6 / 8 spill in the hot path: C1 -6 / -12 % (profiles/r05/ktable_waves)
 #endif
@@ -4728,12 +4745,23 @@ __global__ __launch_bounds__(256, RL_KTABLE_WAVES) void k_table(uint32_t g_runs,
     const uint32_t p = *errb_prev;
     if (p) atomicOr(err, p);
   }
+#if RL_KT_UNIQ_FIRST  // (A/B builds: the keys seen once take the grid's first workgroups, the runs part the last)
+  const uint32_t g_uniq = gridDim.x - g_runs;
+  if (blockIdx.x >= g_uniq)
+    runs_body(blockIdx.x - g_uniq, b, t, P, rec_s, skeys, svals, res, run_start, run_end, run_flags, run_state,
+              run_alias, rid, run_f, num_runs, drun, defer2, defer2_n, stats, stripes, err, errs, restore, fast_blk,
+              errb_prev);
+  else
+    unique_body(blockIdx.x, b, t, P, rec_s.rec, keys0, uniq, uniq_n, res, defer1, defer1_n, stats, stripes, err, errs,
+                restore, errb_prev);
+#else
   if (blockIdx.x < g_runs)
     runs_body(blockIdx.x, b, t, P, rec_s, skeys, svals, res, run_start, run_end, run_flags, run_state, run_alias, rid,
               run_f, num_runs, drun, defer2, defer2_n, stats, stripes, err, errs, restore, fast_blk, errb_prev);
   else
     unique_body(blockIdx.x - g_runs, b, t, P, rec_s.rec, keys0, uniq, uniq_n, res, defer1, defer1_n, stats, stripes,
                 err, errs, restore, errb_prev);
+#endif
   if (kt && threadIdx.x == 0) kt[2 * blockIdx.x + 1] = wall_clock64();
 }
 
@@ -5045,7 +5073,7 @@ static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b -
 // validation word s.err. Sorted keys go to keys[1] (keys[0] keeps the arrival
 // order for k_table's keys seen once), the sort permutation to vals[0].
 void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_second, hipStream_t st,
-                    hipEvent_t* ev, uint32_t* long_hint, bool long_kernel) {
+                    hipEvent_t* ev, uint32_t* long_hint, bool long_kernel, uint32_t* big_hint, bool big_full) {
   const uint32_t g0 = cdiv(b.n > b.n_req ? b.n : b.n_req, 256);
   if (ev) (void)hipEventRecord(ev[0], st);
   if (g0)
@@ -5062,15 +5090,16 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
                                                              s.keys[1], s.vals[0], s.hits_s, s.segsum, s.rid,
                                                              s.run_start, s.run_end, s.runs64, s.drun, s.big_meta, s.big_n,
                                                              s.big_work, s.work_n, s.sorted_n, s.uniq, s.uniq_n,
-                                                             s.err);
+                                                             s.err, big_hint);
 #ifndef RL_EXP_NO_BIG  // (measurement builds only: without the large-bucket kernels, C1 has none)
-    k_big_count<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
+    const uint32_t gi = big_full ? BIG_ITEM_BLOCKS : 1u, gb = big_full ? BIG_BLOCKS : 1u;
+    k_big_count<<<gi, BkSmall::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
                                                                     s.big_meta, s.big_work, s.work_n, s.big_cnt,
                                                                     s.err);
-    k_big_place<<<BIG_ITEM_BLOCKS, BkSmall::THREADS, seg_lds, st>>>(
+    k_big_place<<<gi, BkSmall::THREADS, seg_lds, st>>>(
         s.tile, s.part_info, ptiles, s.big_meta, s.big_work, s.work_n, s.big_cnt, s.keys[1],
         s.vals[0], s.hits_s, s.segsum, s.rid, s.run_start, s.run_end, s.drun, s.err);
-    k_bucket_big<<<BIG_BLOCKS, BkBig::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
+    k_bucket_big<<<gb, BkBig::THREADS, seg_lds, st>>>(s.tile, s.part_info, ptiles,
                                                               s.keys[1], s.vals[0], s.hits_s, s.hit_t, s.segsum,
                                                               s.rid, s.run_start, s.run_end, s.runs64, s.drun, s.big_meta,
                                                               s.big_n, s.big_cnt, s.err);

@@ -20,6 +20,7 @@ for rep in $(seq $REPS); do
        python -u bench.py $A --prof-every 0 > $OUT/tr_${v}_${CFG}_$rep.log 2>&1) || { tail -5 $OUT/tr_${v}_${CFG}_$rep.log; exit 1; }
     tr=$(find $OUT/tr_${v}_$rep -name "*kernel_trace.csv" | head -1)
     python scripts/trace_timed.py "$tr" $OUT/tr_${v}_${CFG}_$rep.log $OUT/timed_${v}_${CFG}_$rep.json 5 > /dev/null || exit 1
+    python scripts/kstats_tail.py "$tr" 200 $OUT/kstats_${v}_${CFG}_$rep.json > $OUT/kstats_${v}_${CFG}_$rep.txt || exit 1
     python - $log $OUT/timed_${v}_${CFG}_$rep.json "$v $CFG $rep" <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric')][-1])

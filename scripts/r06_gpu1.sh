@@ -6,9 +6,11 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 T="--timeout 120 --timeout-method thread"
+if [ "${NEW:-1}" = "1" ]; then
 timeout -k 10 300 python -u -m pytest tests/test_gpu_log_tear.py tests/test_gpu_alias.py tests/test_gpu_history.py -x -v $T \
   > gpurun_out/pytest_new.log 2>&1 || { tail -40 gpurun_out/pytest_new.log; exit 1; }
 tail -3 gpurun_out/pytest_new.log
+fi
 timeout -k 10 480 python -u -m pytest tests -m gpu -x -q $T > gpurun_out/pytest_gpu.log 2>&1 \
   || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
 tail -3 gpurun_out/pytest_gpu.log

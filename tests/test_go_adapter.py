@@ -327,3 +327,17 @@ def test_device_failures_flip_the_health_check():
     assert "s.GpuHealthCheckDevice && srv != nil" in ctor and "opt.HealthServer = srv" in ctor
     assert re.search(r"GpuHealthCheckDevice\s+bool\s+`envconfig:\"GPU_HEALTH_CHECK_DEVICE\" default:\"true\"`",
                      _added("settings.go.patch"))
+
+
+def test_local_cache_gauges_are_the_reference_eight():
+    """limiter.localCacheStats publishes eight freecache gauges
+    (src/limiter/local_cache_stats.go:20-43) and the reference's gauge test
+    checks that every one exists (fixed_cache_impl_test.go:150-167): the GPU
+    adapter registers the same names."""
+    names = {"evacuateCount", "expiredCount", "entryCount", "averageAccessTime", "hitCount", "missCount",
+             "lookupCount", "overwriteCount"}
+    src = open(os.path.join(GO, "src", "gpu", "stats.go")).read()
+    got = set(re.findall(r'scope\.NewGauge\("(\w+)"\)', src))
+    assert got == names, got ^ names
+    gen = src[src.index("func (s localCacheStats) GenerateStats()"):]
+    assert all(("s.%s.Set(" % n) in gen for n in names)

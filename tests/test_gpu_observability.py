@@ -138,7 +138,7 @@ def test_gpu_profile_sampling_counts_and_leaves_results_unchanged():
 
 def test_gpu_cache_health_check_follows_device_failures():
     """GpuRateLimitCache's health monitor on the real library: batches keep
-    the check quiet, a request-level failure (a malformed unit: RL_E_INVALID)
+    the check quiet, a request-level failure (a clock past 32 bits: RL_E_TIME)
     too; a device-level failure of a batch (RL_E_HIP, injected at the backend
     call: a dead device cannot be made on demand) fails it and the next
     answered batch marks it OK."""
@@ -156,9 +156,10 @@ def test_gpu_cache_health_check_follows_device_failures():
     lim = [O.RateLimit("d.k_v", O.RateLimitStats("d.k_v"), O.Limit(5, O.SECOND))]
     try:
         cache.do_limit(None, req, lim)
-        bad = [O.RateLimit("d.k_v", O.RateLimitStats("d.k_v"), O.Limit(5, 9))]
-        with pytest.raises(RedisError):
-            cache.do_limit(None, req, bad)
+        cache.time_source = FixedTimeSource(1 << 33)  # a clock past the table's 32 bits: RL_E_TIME
+        with pytest.raises(RedisError, match="RL_E_TIME"):
+            cache.do_limit(None, req, lim)
+        cache.time_source = FixedTimeSource(1_700_000_000)
         assert srv.calls == []
         real = cache.backend.do_limit_packed
 
