@@ -193,11 +193,17 @@ def main():
 
     serial_stream = main_stream.cuda_stream
 
-    def do_step(inp, bn, bq):
+    # the last timed batch writes its own outputs (the self-check reads them;
+    # batches in flight share `out`, whose stats several batches add into)
+    out_chk = {k: torch.zeros_like(v) for k, v in out.items()}
+    check_step = args.warmup + args.steps - 1
+
+    def do_step(inp, bn, bq, o=None):
+        o = out if o is None else o
         if routed:
-            sc.submit(inp, bn, bq, NR, out)
+            sc.submit(inp, bn, bq, NR, o)
         else:
-            be.do_limit_device(inp, out, bn, bq, NR, stream=serial_stream)  # (pipelined; --serial: RL_DEBUG_SERIAL)
+            be.do_limit_device(inp, o, bn, bq, NR, stream=serial_stream)  # (pipelined; --serial: RL_DEBUG_SERIAL)
 
     def sync():
         if routed:
@@ -243,7 +249,7 @@ def main():
         inp = dict(dev_batches[s % len(dev_batches)])
         inp["now"] = nows[s]
         t = time.perf_counter()
-        do_step(inp, n, nq)
+        do_step(inp, n, nq, out_chk if s == check_step else None)
         host_in_call[0] += time.perf_counter() - t
         if host_delay:  # (RL_BENCH_HOST_DELAY_US: a slower submitter, to see whether the host paces the GPU)
             while time.perf_counter() - t < host_delay:
@@ -281,8 +287,9 @@ def main():
     barrier()
     # (after the timed region) the last timed batch's answers, checked below against the oracle
     last_out = {k: v.cpu().numpy().view(np.uint32) if v.dtype == torch.int32 else v.cpu().numpy()
-                for k, v in out.items()}
-    last_step = step[0] - 1
+                for k, v in out_chk.items()}
+    last_step = check_step
+    assert step[0] - 1 == check_step
     route_host = {k: round(v / args.steps * 1e3, 4) for k, v in sc.host_s.items()} if py_route else None
     info1 = be.table_info()
     if routed and not recv:  # decisions this rank's table answered per owner batch

@@ -84,15 +84,20 @@ struct __attribute__((aligned(32))) LogEnt {
 };
 static_assert(sizeof(LogEnt) == 32, "log entry is two dwordx4");
 constexpr uint32_t LOG_NONE = RING_NONE;
-constexpr uint32_t LOG_PARTS = 64;                        // partitions (each its own append counter)
-constexpr uint32_t LOG_POS_BITS = 26;                     // entry pointer = part << 26 | position
+#ifndef RL_LOG_PARTS_LOG2
+#define RL_LOG_PARTS_LOG2 6  // (A/B builds: 8 = 256 partitions)
+#endif
+constexpr uint32_t LOG_PARTS = 1u << RL_LOG_PARTS_LOG2;   // partitions (each its own append counter)
+constexpr uint32_t LOG_POS_BITS = 32 - RL_LOG_PARTS_LOG2; // entry pointer = part << LOG_POS_BITS | position
 constexpr uint32_t LOG_POS_MASK = (1u << LOG_POS_BITS) - 1u;
-constexpr uint32_t LOG_PART_MAX = 1u << 25;               // entries per partition (2^31 in all)
+constexpr uint32_t LOG_PART_MAX = 1u << (LOG_POS_BITS - 1);  // entries per partition (2^31 in all)
+static_assert(LOG_PARTS <= 256, "k_b_begin copies the counters with one workgroup");
 constexpr uint32_t LOG_CTR_STRIDE = 16;                   // counters on 128-B lines of their own
-// Word k of partition p's line: [0] the append counter, [1] its value when the
-// batch's table stage began (k_log_epoch). Line LOG_PARTS: [0] lookups that met
-// an overwritten entry, [1] appends refused (below).
-constexpr uint32_t LOG_CTR_EPOCH = 1;
+// Word 0 of partition p's line: the append counter. Line LOG_PARTS: [0]
+// lookups that met an overwritten entry, [1] appends refused (below). Each
+// batch's k_b_begin copies the counters to the batch's own array
+// (Scratch::log_epoch, lines of their own: the counters' lines take every
+// append's atomic).
 // Chain pointer standing for a record the log could not keep (its partition
 // had taken log_cap appends in this batch already): its position is past any
 // partition, so a walk that reaches it fails like one that meets an

@@ -142,7 +142,8 @@ Params params(Engine* c, int isolate = 0);
 uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hipStream_t st, bool pipelined) {
   const uint32_t k = c->next;
   c->next = (k + 1) % NBUF;
-  const TableDev t = table_view(c);
+  TableDev t = table_view(c);
+  t.log_epoch = c->s[k].log_epoch;  // (k_b_begin sets it for this batch)
   const int isolate = (!restore && o.status) ? 1 : 0;
   const Params P = params(c, isolate);
   const uint32_t* errb_prev = c->s[c->last].errb;  // the previous batch's table-stage word
@@ -179,7 +180,7 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     (void)hipStreamWaitEvent(a, c->b_done[k], 0);    // buffer k's previous batch is done
     (void)hipStreamWaitEvent(a, c->consumed[k], 0);  // ... and its routed results were read
     launch_stage_a(b, c->s[k], isolate, P.per_second, a, ev, hint, lng, bhint, big_full);
-    if (early) launch_b_begin_early(b, o, c->s[k], restore, a);  // (off the table-order chain)
+    if (early) launch_b_begin_early(b, o, c->s[k], restore, a, c->log_ctr);  // (off the table-order chain)
     (void)hipStreamWaitEvent(a, c->b_table[c->last], 0);  // table order (not the previous k_finish)
     launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
                    early);
@@ -189,7 +190,7 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     (void)after_batches(c, st);
     hipEvent_t* ev = prof_events(c);
     launch_stage_a(b, c->s[k], isolate, P.per_second, st, ev, hint, lng, bhint, big_full);
-    if (early) launch_b_begin_early(b, o, c->s[k], restore, st);
+    if (early) launch_b_begin_early(b, o, c->s[k], restore, st, c->log_ctr);
     launch_stage_b(b, o, t, P, c->s[k], restore, st, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
                    early);
     (void)hipEventRecord(c->b_done[k], st);
@@ -266,6 +267,7 @@ TableDev table_view(Engine* c) {
   t.horizon = c->horizon;
   t.hist_lost = c->log_ctr + (size_t)LOG_PARTS * LOG_CTR_STRIDE;
   t.tear = c->tear;
+  t.log_epoch = nullptr;  // (a batch's: enqueue)
   t.mask = c->nslots - 1;
   t.arena = c->arena;
   t.arena_used16 = c->s[0].counters + 4;
@@ -298,6 +300,7 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
        dalloc(&s.defer_n, 1) == hipSuccess && dalloc(&s.defer2, n) == hipSuccess &&
        dalloc(&s.defer1, n) == hipSuccess && dalloc(&s.defer1_n, 1) == hipSuccess &&
        dalloc(&s.defer2_n, 1) == hipSuccess && dalloc(&s.fast_blk, (size_t)n / (256 * 32) + 1) == hipSuccess &&
+       dalloc(&s.log_epoch, LOG_PARTS) == hipSuccess &&
        dalloc(&s.uniq, n) == hipSuccess && dalloc(&s.uniq_n, 1) == hipSuccess &&
        dalloc(&s.long_runs, (size_t)n / 1024 + 2) == hipSuccess &&
        dalloc(&s.kt_blk, 2 * ((size_t)n / 2 + BIG_HEAVY * PART_DIGITS + 2 * (size_t)n + 512) / 256) == hipSuccess;
@@ -319,7 +322,7 @@ void free_buffer(Scratch& s) {
                   s.vals[0], s.vals[1], s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1,
                   s.defer1_n, s.fast_blk, s.hits_s, s.segsum, s.rid, s.run_start, s.run_flags, s.run_state, s.run_alias,
                   s.run_f, s.runs64, s.split, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t, s.r_base,
-                  s.uniq, s.uniq_n, s.long_runs, s.kt_blk};
+                  s.uniq, s.uniq_n, s.long_runs, s.kt_blk, s.log_epoch};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
 }

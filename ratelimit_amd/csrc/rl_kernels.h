@@ -169,6 +169,7 @@ struct TableDev {
   uint32_t log_cap;  // entries per partition (power of 2)
   uint32_t horizon;
   unsigned long long* hist_lost;  // lookups that met an entry the log had overwritten ([1]: appends refused)
+  const unsigned long long* log_epoch;  // this batch's [LOG_PARTS] append-counter floor (Scratch::log_epoch)
   uint32_t* tear;  // RL_LOG_TEAR builds only (tests): an armed rl_log_tear, or null
   uint64_t mask;
   uint8_t* arena;
@@ -208,6 +209,7 @@ struct Scratch {
   uint32_t* defer1;               // keys seen once k_table found to need the exact path (arrival indices)
   uint32_t* defer1_n;
   uint32_t* fast_blk;             // bit per 256-descriptor block holding a RUN_FAST run (k_table -> k_late)
+  unsigned long long* log_epoch;  // [LOG_PARTS] the history log's append counters as k_b_begin saw them (log_append)
   // the keys seen once, listed bucket by bucket ({arrival index, sort key}):
   // k_table's singleton part walks them in this order, so a workgroup's
   // table probes stay inside the 1/1024 of the table its bucket's home slots
@@ -273,7 +275,8 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
                     int restore, hipStream_t st, hipEvent_t* ev, const uint32_t* errb_prev, hipEvent_t table_done,
                     unsigned long long* kt_acc = nullptr, bool early = false);
-void launch_b_begin_early(const BatchDev& b, const OutDev& o, const Scratch& s, int restore, hipStream_t st);
+void launch_b_begin_early(const BatchDev& b, const OutDev& o, const Scratch& s, int restore, hipStream_t st,
+                          const unsigned long long* log_ctr);
 // ev (optional, RL_NUM_STAGES + 1 events on stream st): recorded before
 // k_prepare, after it, after the sort, just before and just after k_table, and
 // at the end (per-stage timing, rl_profile).

@@ -843,13 +843,26 @@ __device__ inline bool hist_absent_ok(const TableDev& t, uint32_t now, uint32_t 
 //    newer header).
 // This holds when at most one writer writes an entry in a batch's table stage:
 // log_append refuses an append that would overwrite an entry the same batch
-// appended (the partition's counter at the batch's start, k_log_epoch), and
+// appended (the partition's counter at the batch's start, or earlier: k_b_begin), and
 // the only other write, k_late's alias write-back, goes to an entry appended
 // earlier in the same batch, which is therefore never overwritten under it.
 // RL_LOG_TEAR builds (tests/test_gpu_log_tear.py) replay a concurrent writer's
 // steps between the reader's loads in every interleaving.
-__device__ __forceinline__ void log_order() { __asm__ __volatile__("" ::: "memory"); }
-constexpr uint32_t LOG_WRITE_STEPS = 3;
+#ifndef RL_LOG_ORDER
+#define RL_LOG_ORDER 1  // (A/B builds: 0 = no compiler barriers between the entry's stores and loads)
+#endif
+#ifndef RL_LOG_BUSY
+#define RL_LOG_BUSY 1  // (A/B builds: 0 = round 5's 2-step writer)
+#endif
+#ifndef RL_LOG_GUARD
+#define RL_LOG_GUARD 1  // (A/B builds: 0 = no per-batch wrap guard)
+#endif
+__device__ __forceinline__ void log_order() {
+#if RL_LOG_ORDER
+  __asm__ __volatile__("" ::: "memory");
+#endif
+}
+constexpr uint32_t LOG_WRITE_STEPS = RL_LOG_BUSY ? 3 : 2;
 
 // Step s of writing entry e (header h, record r). legacy: round 5's order
 // (header, record; 2 steps), kept for the tear tests only.
@@ -884,7 +897,12 @@ __device__ inline uint32_t log_append(const TableDev& t, uint32_t si, uint32_t t
   unsigned long long k = 0;
   if (lane == leader) k = atomicAdd(line, (unsigned long long)__popcll(act));
   k = __shfl(k, leader, 64) + (unsigned long long)__popcll(act & ((1ull << lane) - 1ull));
-  if (k - line[LOG_CTR_EPOCH] >= t.log_cap) {
+  if (RL_LOG_GUARD && k - t.log_epoch[p] >= t.log_cap) {
+#ifdef RL_LOG_DEBUG  // (diagnostic builds: who was refused)
+    if (atomicAdd(t.hist_lost + 2, 1ull) < 40)
+      printf("refused: grid %u block %u thread %u part %u k %llu epoch %llu cap %u active %d si %u t_app %u ws %u\n",
+             gridDim.x, blockIdx.x, threadIdx.x, p, k, t.log_epoch[p], t.log_cap, __popcll(act), si, t_app, r.ws);
+#endif
     atomicAdd(t.hist_lost + 1, 1ull);
     return LOG_LOST;
   }
@@ -892,7 +910,7 @@ __device__ inline uint32_t log_append(const TableDev& t, uint32_t si, uint32_t t
   uint4* e = reinterpret_cast<uint4*>(&t.log[(size_t)p * t.log_cap + pos]);
   const uint4 h = make_uint4(si, tag, prev, t_app), rv = make_uint4(r.ws, r.count, r.expire, r.lc);
 #pragma unroll
-  for (uint32_t s = 0; s < LOG_WRITE_STEPS; s++) log_write_step(e, s, h, rv, false);
+  for (uint32_t s = 0; s < LOG_WRITE_STEPS; s++) log_write_step(e, s, h, rv, !RL_LOG_BUSY);
   return (p << LOG_POS_BITS) | pos;
 }
 
@@ -1313,16 +1331,24 @@ __device__ __attribute__((always_inline)) inline void simple_step(const TableDev
 }
 
 // ---- general: every unit slot of the stem, Redis keys shared across units.
-// Each unit's cur lives in registers, with one older record per unit cached
-// beside it (as SimpleState::old: appended to the unit slot's chain when
-// another one is needed, or at the end, if it changed). The exact path is rare.
+// Each unit's cur lives in registers, with two older records per unit cached
+// beside it (old, and vic: the one old held before), each appended to the
+// unit slot's chain when a third one is needed, or at the end, if it changed.
+// Two, because a multi-unit stem's replay alternates between two older windows
+// of one slot: a SECOND request's own window and the minute's first second,
+// which is also the key of every MINUTE request of that minute
+// (cache_key.go:73-74); with one, every switch appended a version (one per
+// descriptor of a hot stem: thousands into one partition per batch). The exact
+// path is rare.
 struct GeneralState {
   int64_t sidx[4];
   Win cur[4];
   Win old[4];         // per unit: an older record (WS_INVALID: none cached)
+  Win vic[4];         // per unit: the older record old held before (WS_INVALID: none)
   uint32_t tag[4];    // each unit slot's tag (owner of its log entries)
   uint32_t chain[4];  // each unit slot's history chain head
   uint32_t odirty;    // bit u-1: old[u-1] changed
+  uint32_t vdirty;    // bit u-1: vic[u-1] changed
   uint32_t cdirty;    // bit u-1: chain[u-1] changed
   uint32_t present;   // bit u-1
   uint32_t cur_req;
@@ -1332,18 +1358,22 @@ struct GeneralState {
 
 __device__ inline bool ps_class(const Params& P, uint32_t k) { return P.per_second && k == 0; }
 
-// old[k] to the log
-__device__ inline void gen_put(const TableDev& t, GeneralState& G, uint32_t k) {
-  G.chain[k] = log_append(t, (uint32_t)G.sidx[k], G.tag[k], G.chain[k], G.cur[k].ws, G.old[k]);
+// old[k] (vic: vic[k]) to the log
+__device__ inline void gen_put(const TableDev& t, GeneralState& G, uint32_t k, bool vic = false) {
+  G.chain[k] = log_append(t, (uint32_t)G.sidx[k], G.tag[k], G.chain[k], G.cur[k].ws, vic ? G.vic[k] : G.old[k]);
   G.cdirty |= 1u << k;
-  G.odirty &= ~(1u << k);
+  if (vic) G.vdirty &= ~(1u << k);
+  else G.odirty &= ~(1u << k);
 }
 
-// old[k] becomes r (the one it held goes to the log first if it changed)
+// old[k] becomes r; the one it held becomes vic[k] (whose record goes to the
+// log first if it changed)
 __device__ inline void gen_set_old(const TableDev& t, GeneralState& G, uint32_t k, const Win& r, bool dirty) {
-  if ((G.odirty >> k) & 1) gen_put(t, G, k);
+  if ((G.vdirty >> k) & 1) gen_put(t, G, k, true);
+  G.vic[k] = G.old[k];
+  G.vdirty = (G.vdirty & ~(1u << k)) | (G.odirty & (1u << k));
   G.old[k] = r;
-  if (dirty) G.odirty |= 1u << k;
+  G.odirty = (G.odirty & ~(1u << k)) | (dirty ? 1u << k : 0u);
 }
 
 // The record of window w in unit slot k (present): its cur, its cached older
@@ -1355,6 +1385,15 @@ __device__ inline Win* gen_rec(const TableDev& t, GeneralState& G, uint32_t k, u
   if (c.ws == w) return &c;
   if (c.ws == WS_INVALID || w > c.ws || w % d) return nullptr;  // (unit k's keys are multiples of its div)
   if (G.old[k].ws == w) return &G.old[k];
+  if (G.vic[k].ws == w) {  // the two cached older records trade places
+    const Win v = G.vic[k];
+    G.vic[k] = G.old[k];
+    G.old[k] = v;
+    const uint32_t b = 1u << k, od = G.odirty & b;
+    G.odirty = (G.odirty & ~b) | (G.vdirty & b);
+    G.vdirty = (G.vdirty & ~b) | od;
+    return &G.old[k];
+  }
   Win r;
   const int f = G.chain[k] == LOG_NONE ? 0 : log_find(t, G.chain[k], (uint32_t)G.sidx[k], G.tag[k], c.ws, w, &r);
   if (f > 0) {
@@ -4528,7 +4567,7 @@ __device__ inline void stem_exact(const TableDev& t, const Params& P, unsigned l
                                   Visit visit) {
   GeneralState G;
   G.present = 0;
-  G.odirty = G.cdirty = 0;
+  G.odirty = G.vdirty = G.cdirty = 0;
   G.cur_req = 0xFFFFFFFFu;
   G.npend = 0;
   int64_t fail = 0;
@@ -4537,7 +4576,7 @@ __device__ inline void stem_exact(const TableDev& t, const Params& P, unsigned l
     G.tag[u - 1] = slot_tag(hs, u);
     G.sidx[u - 1] = find_slot(t, hs, G.tag[u - 1], stem, u, (um >> (u - 1)) & 1, &ins, ferr);
     G.chain[u - 1] = LOG_NONE;
-    G.old[u - 1] = Win{WS_INVALID, 0, 0, 0};
+    G.old[u - 1] = G.vic[u - 1] = Win{WS_INVALID, 0, 0, 0};
     if (G.sidx[u - 1] >= 0) {
       const Slot& su = t.slots[G.sidx[u - 1]];
       G.present |= 1u << (u - 1);
@@ -4556,6 +4595,7 @@ __device__ inline void stem_exact(const TableDev& t, const Params& P, unsigned l
   const uint8_t fl = __popc(G.present) >= 2 ? SLOT_EXACT : 0;
   for (uint32_t u = 0; u < 4; u++) {
     if (!(G.present >> u & 1)) continue;
+    if ((G.vdirty >> u) & 1) gen_put(t, G, u, true);
     if ((G.odirty >> u) & 1) gen_put(t, G, u);
     Slot* s = &t.slots[G.sidx[u]];
     s->cur = G.cur[u];
@@ -4807,15 +4847,6 @@ __global__ __launch_bounds__(256, RL_LATE_OCC) void k_late(BatchDev b, TableDev 
                      run_state, run_alias, run_f, stats, stripes, err, fast_blk);
 }
 
-// The history log's append counters as the batch's table stage begins (the
-// previous batch's k_late is done): log_append refuses to wrap a partition onto
-// entries of the batch itself, so each entry has one writer per batch (the
-// seqlock above).
-__global__ __launch_bounds__(64) void k_log_epoch(unsigned long long* __restrict__ log_ctr) {
-  unsigned long long* line = log_ctr + (size_t)threadIdx.x * LOG_CTR_STRIDE;
-  line[LOG_CTR_EPOCH] = line[0];
-}
-
 // First kernel of the table stage: merge this batch's validation errors into
 // the sticky table-stage word, clear k_table's deferral counters and this call's
 // output stats (n_rules x RL_NUM_STATS).
@@ -4823,8 +4854,16 @@ __global__ __launch_bounds__(256) void k_b_begin(const uint32_t* __restrict__ er
                                                  const uint32_t* errb_prev,
                                                  uint32_t* __restrict__ defer_n, uint32_t* __restrict__ defer1_n,
                                                  unsigned long long* __restrict__ stats, uint32_t m,
-                                                 uint32_t* __restrict__ fast_blk, uint32_t nw) {
+                                                 uint32_t* __restrict__ fast_blk, uint32_t nw,
+                                                 const unsigned long long* log_ctr,
+                                                 unsigned long long* __restrict__ log_epoch) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  // the history log's append counters now: at most their values when this
+  // batch's table stage starts (early: at the end of its stage A, while
+  // earlier batches may still append), so log_append's bound is the same or
+  // stricter (one batch's appends never wrap a partition onto its own entries)
+  if (log_ctr && i < LOG_PARTS)
+    log_epoch[i] = __hip_atomic_load(log_ctr + (size_t)i * LOG_CTR_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (i == 0) {
     // this batch's table-stage word: the previous batch's (sticky: a failed
     // batch fails every later one) | this batch's validation result
@@ -5133,11 +5172,12 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
 // end of stage A): this batch's table-stage word = its own validation, its
 // deferral counters, block bitmap and output stats cleared. k_table folds the
 // previous batch's word in (launch_stage_b with early set).
-void launch_b_begin_early(const BatchDev& b, const OutDev& o, const Scratch& s, int restore, hipStream_t st) {
+void launch_b_begin_early(const BatchDev& b, const OutDev& o, const Scratch& s, int restore, hipStream_t st,
+                          const unsigned long long* log_ctr) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
   k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, nullptr, s.defer2_n, s.defer1_n, o.stats, m, s.fast_blk,
-                                cdiv(b.n, 256 * 32));
+                                cdiv(b.n, 256 * 32), log_ctr, s.log_epoch);
 }
 
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
@@ -5145,13 +5185,12 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
                     unsigned long long* kt_acc, bool early) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
-  static_assert(LOG_PARTS == 64, "k_log_epoch: one lane per partition");
-  if (b.n) k_log_epoch<<<1, LOG_PARTS, 0, st>>>(t.log_ctr);
   if (!early)
     k_b_begin<<<gb, 256, 0, st>>>(s.err, s.errb, errb_prev, s.defer2_n, s.defer1_n, o.stats, m, s.fast_blk,
-                                  cdiv(b.n, 256 * 32));
+                                  cdiv(b.n, 256 * 32), t.log_ctr, s.log_epoch);
   else if (!b.n)  // (no k_table to fold the previous batch's word in)
-    k_b_begin<<<1, 256, 0, st>>>(s.errb, s.errb, errb_prev, s.defer2_n, s.defer1_n, o.stats, 0, s.fast_blk, 0);
+    k_b_begin<<<1, 256, 0, st>>>(s.errb, s.errb, errb_prev, s.defer2_n, s.defer1_n, o.stats, 0, s.fast_blk, 0,
+                                 nullptr, nullptr);
   if (b.n) {
     const uint32_t g = cdiv(b.n, 256);
     const size_t lds = (!restore && b.n_rules <= LDS_RULES) ? (size_t)b.n_rules * RL_NUM_STATS * 8 : 0;
