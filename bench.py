@@ -573,7 +573,7 @@ def loopback_main(args):
 
     from ratelimit_amd import workloads as W
     from ratelimit_amd.limiter import Backend
-    from ratelimit_amd.sharded import LibRouter, loopback_id
+    from ratelimit_amd.sharded import WIRE_BYTES, LibRouter, loopback_id
     R = args.loopback
     nq, n, T = args.requests, 2 * args.requests, args.tenants
     slots = 1 << max(16, int(np.ceil(np.log2(args.slots_per_key * 2 * T))))
@@ -585,7 +585,7 @@ def loopback_main(args):
                    max_stem_bytes=64 * cap) for _ in range(R)]
     routers = [LibRouter(be, R, r, uid) for r, be in enumerate(bes)]
     gate = threading.Barrier(R)
-    times, fills, errs = [0.0] * R, [0.0] * R, [None] * R
+    times, fills, errs, stem_mean = [0.0] * R, [0.0] * R, [None] * R, [0.0] * R
 
     def body(r):
         try:
@@ -609,6 +609,7 @@ def loopback_main(args):
             for _ in range(args.distinct_batches):
                 a, _, _, _ = W.c1_batch(rng.integers(0, R * T, nq), W.NOW0)
                 a.pop("now")
+                stem_mean[r] = float(a["stem_off"][n]) / n
                 batches.append(to_dev(a, torch))
             total = args.warmup + args.steps
             nows = [torch.full((nq,), W.NOW0 + s, dtype=torch.int64, device="cuda") for s in range(total)]
@@ -648,6 +649,13 @@ def loopback_main(args):
                    "live_stem_slots": sum(i["live_slots"] for i in info),
                    "parallelism": "hash-sharded table x%d, library router over the loopback transport" % R},
         "fill_s": round(max(fills), 2),
+        # what one remote descriptor moves over the links: its wire record and
+        # stem bytes out, its 8-B packed result back ((R-1)/R of a uniform
+        # slice is remote; the own chunk moves nothing)
+        "wire": {"record_bytes": WIRE_BYTES, "mean_stem_bytes": round(float(np.mean(stem_mean)), 2),
+                 "result_bytes": 8,
+                 "bytes_per_remote_descriptor": round(WIRE_BYTES + float(np.mean(stem_mean)) + 8, 2),
+                 "remote_fraction": (R - 1) / R},
     }
     print(json.dumps(line), flush=True)
 

@@ -510,7 +510,11 @@ func (this *rateLimitCacheImpl) batcher() {
 // same schedule: one batch per tick of the window, holding whatever calls
 // arrived (none: an empty batch, still a step of the exchange), and a sweep
 // every sweepTicks ticks. A batch that cannot be packed is replaced by an
-// empty one (its calls fail) so that no peer waits for this rank.
+// empty one (its calls fail) so that no peer waits for this rank. The
+// previous tick's calls are answered through the collective Synchronize,
+// which completes every pending routed batch: one routed batch in flight per
+// tick (DESIGN.md §6). Every rank sweeps on the same tick; the library applies
+// the least of the ranks' floors on all of them.
 func (this *rateLimitCacheImpl) batcherRouted() {
 	tick := time.NewTicker(this.window)
 	defer tick.Stop()

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 5u
+#define RL_ABI_VERSION 6u
 
 /* Status codes. */
 enum rl_status {
@@ -407,8 +407,10 @@ int rl_debug_log_tear(rl_ctx* ctx, const rl_log_tear* arm, rl_log_tear* out);
  *
  * rl_route_pack (source side): stable-partitions the batch `in` by owner shard
  * and writes, in owner order, one RL_WIRE_BYTES record per descriptor (its
- * fields and keyed 64-bit stem hash, so owners never rehash) to
- * send_rec and its stem bytes to send_stem (capacity: the batch's stem bytes).
+ * fields, its request's clock as 32 bits, and the keyed 64-bit stem hash, so
+ * owners never rehash; no stem offset) to send_rec and its stem bytes to
+ * send_stem (capacity: the batch's stem bytes), each owner's stems in its
+ * records' order.
  * perm[j] = batch index of record j. counts[2*d], [2*d+1] (device memory) =
  * records / stem bytes for owner d (all zero when the batch is malformed). Request
  * indices must be < 2^24; the global request label is src_rank << 24 | req_idx,
@@ -417,7 +419,8 @@ int rl_debug_log_tear(rl_ctx* ctx, const rl_log_tear* arm, rl_log_tear* out);
  * rl_route_do_limit (owner side): DoLimit over the n records received from all
  * sources (concatenated in source-rank order) with their stems (recv_stem,
  * 4-byte aligned, recv_stem_bytes long; src_stem_base = host array of each
- * source's chunk offset in recv_stem), pipelined on the ctx's streams once the
+ * source's chunk offset in recv_stem: the chunks abut in source order, and
+ * each record's stem starts where the previous record's ends), pipelined on the ctx's streams once the
  * work already on `stream` is done; then, on `stream`, ret[j] = the packed
  * result of record j (bits 0-31 remaining, 32-51 reset_s, 52-55 status, 56-61
  * code, 62 local-cache hit). stats: rule_stride == 0: n_rules x RL_NUM_STATS
@@ -427,7 +430,7 @@ int rl_debug_log_tear(rl_ctx* ctx, const rl_log_tear* arm, rl_log_tear* out);
  *
  * rl_route_scatter (source side): results returned in record order (ret, n =
  * the batch size) -> out (device SoA, status optional) in arrival order. */
-#define RL_WIRE_BYTES 40u
+#define RL_WIRE_BYTES 32u
 #define RL_MAX_SHARDS 256u
 int rl_route_pack(rl_ctx* ctx, const rl_batch* in, uint32_t n_shards, uint32_t src_rank, void* send_rec,
                   uint8_t* send_stem, uint32_t* perm, uint64_t* counts, void* stream);
@@ -482,7 +485,10 @@ int rl_route_scatter(rl_ctx* ctx, uint32_t n, const uint32_t* perm, const uint64
  * service process (src/redis/driver_impl.go:108-126).
  * On a routed ctx rl_synchronize, rl_sweep, rl_restore and rl_snapshot_save /
  * _load first complete the pending batches, so they are collective like the
- * batches. The read-only getters rl_table_info_get and rl_local_cache_info_get
+ * batches. rl_sweep there applies one floor on every rank: the least `now`
+ * the ranks passed (a rank passing an out-of-range time fails alone and does
+ * not vote), so a rank's requests are never refused by an owner whose clock
+ * runs ahead of its own. The read-only getters rl_table_info_get and rl_local_cache_info_get
  * are not: they see every batch but the pending ones (the last RL_ROUTED_LAG
  * submitted), and a rank may call them alone (e.g. for its gauges). */
 #define RL_COMM_ID_BYTES 128u

@@ -149,7 +149,7 @@ BATCH_DTYPES = {"stem_bytes": np.uint8, "stem_off": np.uint32, "now": np.int64, 
                 "rule_id": np.uint32}
 RESULT_DTYPES = {"code": np.uint8, "limit_remaining": np.uint32, "reset_s": np.uint32, "stats": np.uint64,
                  "status": np.uint8}
-ABI_VERSION = 5
+ABI_VERSION = 6
 RL_COMM_ID_BYTES = 128  # include/ratelimit_hip.h
 RL_ROUTED_INFLIGHT = 6  # include/ratelimit_hip.h (routed batches in flight: the input-reuse distance)
 RL_ROUTED_LAG = 3  # include/ratelimit_hip.h (calls between a routed batch's partition and its owner pipeline)

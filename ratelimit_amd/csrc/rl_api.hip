@@ -617,6 +617,10 @@ int rl_sweep(rl_ctx* c, int64_t now, uint64_t* n_evicted) {
   if (!c) return fail(c, RL_E_INVALID, "gpu: null ctx");
   int rc = settle(c);
   if (rc) return rc;
+  if (c->comm) {  // (routed: one floor for the world, the least of the ranks' now)
+    rc = from_engine(c, c->e[0], comm_sweep_floor(c->comm, c->e[0], now, &now));
+    if (rc) return rc;
+  }
   uint64_t total = 0;
   for (uint32_t j = 0; j < c->n; j++) {
     uint64_t ev = 0;

@@ -23,6 +23,8 @@ int comm_loopback_id(uint8_t* id, std::string* err);
 CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t* id, std::string* err);
 void comm_destroy(CommRouter* r);
 const char* comm_kind(const CommRouter* r);  // "rccl" or "loopback"
+// rl_sweep on a routed ctx (collective): the least `now` over the ranks
+int comm_sweep_floor(CommRouter* r, Engine* e, int64_t now, int64_t* floor);
 // A slice that is not plain device memory of this rank's GPU (the shards of
 // one ctx, rl_api.hip). host: `in` and `out` are host memory; `in` is an
 // absolute-index view of the caller's whole batch (stem_off / req_idx / unit /

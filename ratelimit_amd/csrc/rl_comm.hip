@@ -92,6 +92,11 @@ struct CommSlot {
   uint8_t* recv_stem = nullptr;
   unsigned long long* ret_send = nullptr;  // packed results of the received records
   uint64_t cap_rec = 0, cap_stem = 0;
+  uint32_t* woff = nullptr;                // an exchange run in several owner parts: the records' stem offsets
+  unsigned long long* wtsum = nullptr;     // (and the scan's tile sums and verdict)
+  unsigned long long* wbase = nullptr;     // [RL_MAX_SHARDS] the chunk bases the scan checks (device)
+  unsigned long long* h_wbase = nullptr;   // (pinned staging)
+  uint64_t cap_woff = 0;
   unsigned long long* back = nullptr;      // this rank's results, record order
   unsigned long long* ostats = nullptr;    // [cap_parts][world x m_max]: owner deltas per source
   uint32_t cap_parts = 0;
@@ -142,6 +147,7 @@ struct CommRouter {
   uint32_t n_pend = 0;
   unsigned long long* h_cnt = nullptr;  // pinned [RSLOTS][2 x CNT_W x world]
   unsigned long long* d_hcnt = nullptr;  // h_cnt as the device sees it (world 1: the partition stores the counts there)
+  long long* d_floor = nullptr;          // [1 + world]: this rank's sweep time, then each peer's (comm_sweep_floor)
   std::vector<uint64_t> base;           // received chunk offsets in recv_stem (host)
   std::vector<uint64_t> so_r, so_b, ro_r;  // per-peer send / receive offsets (host)
   std::vector<Xfer> ops;
@@ -188,11 +194,12 @@ int run_group(CommRouter* r, Engine* e, uint32_t ch, hipStream_t st) {
 
 void free_slot(CommSlot& S) {
   void* bufs[] = {S.pb.dest, S.pb.hist, S.pb.start, S.send_rec, S.send_stem, S.perm, S.hash, S.cnt, S.recv_rec,
-                  S.recv_stem, S.ret_send, S.back, S.ostats,
+                  S.recv_stem, S.ret_send, S.back, S.ostats, S.woff, S.wtsum, S.wbase,
                   S.stats_stage, S.h_stem, S.h_off, S.h_req, S.h_limit, S.h_hits, S.h_rule, S.h_now, S.h_unit,
                   S.h_flags, S.h_code, S.h_status, S.h_rem, S.h_reset, S.io_stats, S.h_cbuf};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
+  if (S.h_wbase) (void)hipHostFree(S.h_wbase);
   for (hipEvent_t ev : {S.packed, S.sent, S.done})
     if (ev) (void)hipEventDestroy(ev);
   S = CommSlot{};
@@ -230,6 +237,23 @@ hipError_t grow(CommRouter* r, CommSlot& S, uint64_t n_rec, uint64_t n_stem, uin
     if ((e = dalloc(&S.ostats, (size_t)parts * r->world * r->m_max)) != hipSuccess) return e;
     S.cap_parts = parts;
   }
+  return hipSuccess;
+}
+
+// Slot S's stem-offset scan buffers hold n records' offsets (+ the total).
+hipError_t grow_woff(CommSlot& S, uint64_t n) {
+  if (n <= S.cap_woff) return hipSuccess;
+  hipError_t e = hipEventSynchronize(S.done);
+  if (e != hipSuccess) return e;
+  (void)hipFree(S.woff);
+  (void)hipFree(S.wtsum);
+  S.woff = nullptr;
+  S.wtsum = nullptr;
+  S.cap_woff = 0;
+  if ((e = dalloc(&S.woff, n + 1)) != hipSuccess || (e = dalloc(&S.wtsum, WIRE_SCAN_WORDS(n))) != hipSuccess) return e;
+  if (!S.wbase && (e = dalloc(&S.wbase, RL_MAX_SHARDS)) != hipSuccess) return e;
+  if (!S.h_wbase && (e = hipHostMalloc((void**)&S.h_wbase, RL_MAX_SHARDS * 8)) != hipSuccess) return e;
+  S.cap_woff = n;
   return hipSuccess;
 }
 
@@ -543,8 +567,21 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
       CHK_HIP(e, hipMemcpyAsync(S.recv_stem + r->base[me], S.send_stem + r->so_b[me], h[CNT_W * me + 1],
                                 hipMemcpyDeviceToDevice, fwd));
   }
-  if (!r->alias) CHK_HIP(e, hipEventRecord(S.sent, fwd));
-  hipEvent_t const sent = r->alias ? S.packed : S.sent;  // (the received records are ready)
+  const uint64_t own_lo = r->ro_r[me], own_hi = r->own ? r->ro_r[me + 1] : own_lo;  // (received positions)
+  // an exchange answered in several owner parts (below): the records' stem
+  // offsets, scanned once over all of them (one part scans its own)
+  const bool scan_all = n_recv > mb && !owner_fail && n_recv > own_hi - own_lo;
+  if (scan_all) {
+    CHK_HIP(e, grow_woff(S, n_recv));
+    if (r->alias) CHK_HIP(e, hipStreamWaitEvent(fwd, S.packed, 0));
+    CHK_HIP(e, hipEventSynchronize(S.done));  // (the slot's previous batch read the staged bases)
+    std::copy(r->base.begin(), r->base.end(), S.h_wbase);
+    CHK_HIP(e, hipMemcpyAsync(S.wbase, S.h_wbase, (size_t)W * 8, hipMemcpyHostToDevice, fwd));
+    launch_wire_offsets(recv_rec, (uint32_t)n_recv, (uint32_t)own_lo, (uint32_t)own_hi, S.wbase, W, b_recv, S.woff,
+                        S.wtsum, fwd);
+  }
+  if (!r->alias || scan_all) CHK_HIP(e, hipEventRecord(S.sent, fwd));
+  hipEvent_t const sent = r->alias && !scan_all ? S.packed : S.sent;  // (the received records are ready)
   // the owner pipeline, in parts of at most max_batch records. A part ends on
   // a request boundary (a request's descriptors check the local cache before
   // any of them sets it, fixed_cache_impl.go:50-66 then :100-109), so more
@@ -552,7 +589,6 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
   // the received labels.
   std::vector<uint64_t>& cut = S.cut;
   cut.assign(1, 0);
-  const uint64_t own_lo = r->ro_r[me], own_hi = r->own ? r->ro_r[me + 1] : own_lo;  // (received positions)
   if (n_recv > mb && !owner_fail) {
     std::vector<uint32_t> lab(n_recv);
     CHK_HIP(e, hipStreamSynchronize(fwd));
@@ -644,7 +680,8 @@ int second_half(CommRouter* r, Engine* e, CommSlot& S, uint32_t s) {
       }
       const int rc = eng_route_owner(e, (uint32_t)(b - a), recv_rec + a, recv_stem, b_recv, r->base.data(), W,
                                      (uint32_t)M, (uint32_t)M, stats_direct ? stats_out : S.ostats + q * blk,
-                                     iso ? 1 : 0, sent, &S.k[q], &oc);
+                                     iso ? 1 : 0, sent, &S.k[q], &oc, scan_all ? S.woff + a : nullptr,
+                                     scan_all ? S.wtsum + WIRE_SCAN_TILES(n_recv) : nullptr);
       if (rc) return breaks(r, e, rc, eng_last_error(e));  // (argument checks only: the sizes were checked above)
       // its packed results, before a later part can take the same engine buffer
       const uint32_t k = S.k[q];
@@ -767,7 +804,8 @@ CommRouter* comm_create(Engine* e, uint32_t world, uint32_t rank, const uint8_t*
             rl_stream_create(&r->cs, SR_ROUTER) == hipSuccess && rl_stream_create(&r->fwd, SR_ROUTER) == hipSuccess &&
             rl_stream_create(&r->ret, SR_ROUTER) == hipSuccess &&
             hipEventCreateWithFlags(&r->in_ready, hipEventDisableTiming) == hipSuccess &&
-            hipHostMalloc((void**)&r->h_cnt, (size_t)RSLOTS * 2 * CNT_W * world * 8) == hipSuccess;
+            hipHostMalloc((void**)&r->h_cnt, (size_t)RSLOTS * 2 * CNT_W * world * 8) == hipSuccess &&
+            dalloc(&r->d_floor, (size_t)world + 1) == hipSuccess;
   if (ok && world == 1 && hipHostGetDevicePointer((void**)&r->d_hcnt, r->h_cnt, 0) != hipSuccess) {
     (void)hipGetLastError();
     r->d_hcnt = nullptr;  // (then a copy per batch)
@@ -814,6 +852,7 @@ void comm_destroy(CommRouter* r) {
   r->tr.reset();
   for (CommSlot& S : r->slot) free_slot(S);
   if (r->h_cnt) (void)hipHostFree(r->h_cnt);
+  if (r->d_floor) (void)hipFree(r->d_floor);
   if (r->in_ready) (void)hipEventDestroy(r->in_ready);
   for (hipStream_t st : {r->cs, r->fwd, r->ret})
     if (st) (void)hipStreamDestroy(st);
@@ -841,6 +880,38 @@ int comm_synchronize(CommRouter* r, Engine* e) {
     r->sticky_msg.clear();
     return rc;
   }
+  return RL_OK;
+}
+
+// The sweep floor of the whole world: the least `now` any rank passed to its
+// rl_sweep. Every rank sweeps its own shard, and an owner checks a peer's
+// requests against its floor, so one floor for all ranks means a rank whose
+// clock trails a peer's (or whose caller sweeps with a larger lag) never sees
+// its requests refused for a time its own clock has not reached. Collective
+// like the routed batches (channel 0, quiet here: comm_synchronize ran
+// first). A rank whose `now` is out of range takes part with no vote (its own
+// eng_sweep then refuses the time).
+int comm_sweep_floor(CommRouter* r, Engine* e, int64_t now, int64_t* floor) {
+  *floor = now;
+  if (r->broken) return eng_fail(e, r->broken, r->broken_msg);
+  if (r->world == 1) return RL_OK;
+  CHK_HIP(e, hipSetDevice(r->dev));
+  const bool vote = now >= 0 && now <= (int64_t)NOW_MAX;
+  std::vector<long long> v(r->world + 1, INT64_MAX);
+  v[0] = vote ? now : INT64_MAX;
+  CHK_HIP(e, hipMemcpyAsync(r->d_floor, v.data(), 8, hipMemcpyHostToDevice, r->cs));
+  r->ops.clear();
+  for (uint32_t p = 0; p < r->world; p++) {
+    if (p == r->rank) continue;
+    r->ops.push_back({r->d_floor, 8, p, true});
+    r->ops.push_back({r->d_floor + 1 + p, 8, p, false});
+  }
+  if (const int rc = run_group(r, e, 0, r->cs)) return rc;
+  CHK_HIP(e, hipMemcpyAsync(v.data(), r->d_floor, v.size() * 8, hipMemcpyDeviceToHost, r->cs));
+  CHK_HIP(e, hipStreamSynchronize(r->cs));
+  if (!vote) return RL_OK;
+  for (uint32_t p = 0; p < r->world; p++)
+    if (p != r->rank) *floor = std::min<int64_t>(*floor, v[1 + p]);
   return RL_OK;
 }
 

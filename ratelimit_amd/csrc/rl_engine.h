@@ -227,11 +227,14 @@ int eng_snapshot_load(Engine* c, const void* host, uint64_t bytes);
 // them complete and the reader must record consumed[*slot] once it has copied
 // them (the buffer is not reused before). own (optional, own->n > 0): records
 // [own->lo, own->lo + own->n) are read in place from the source batch
-// (BatchDev::own; recv_rec holds nothing there).
+// (BatchDev::own; recv_rec holds nothing there). woff, wbad (optional): the
+// records' stem offsets and the scan's verdict word (launch_wire_offsets over
+// the whole exchange, when it runs in parts); null: scanned here.
 int eng_route_owner(Engine* c, uint32_t n, const Wire* recv_rec, const uint8_t* recv_stem, uint64_t recv_stem_bytes,
                     const uint64_t* src_stem_base, uint32_t n_src, uint32_t n_rules, uint32_t rule_stride,
                     unsigned long long* stats, int isolate, hipEvent_t ready, uint32_t* slot,
-                    const OwnChunk* own = nullptr);
+                    const OwnChunk* own = nullptr, const uint32_t* woff = nullptr,
+                    const unsigned long long* wbad = nullptr);
 
 // Record an error on the engine (its rl_last_error) and return code.
 int eng_fail(Engine* c, int code, const std::string& msg);

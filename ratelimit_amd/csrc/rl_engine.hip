@@ -313,7 +313,8 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
        dalloc(&s.hit_t, n) == hipSuccess;
   ok = ok && dalloc(&s.run_end, n) == hipSuccess &&
        dalloc(&s.part_info, (size_t)PART_DIGITS * std::max((n + PART_TILE - 1) / PART_TILE, 1u)) == hipSuccess;
-  ok = ok && dalloc(&s.r_base, RL_MAX_SHARDS) == hipSuccess;
+  ok = ok && dalloc(&s.r_base, RL_MAX_SHARDS) == hipSuccess && dalloc(&s.woff, (size_t)n + 1) == hipSuccess &&
+       dalloc(&s.wtsum, WIRE_SCAN_WORDS(n)) == hipSuccess;
   return ok;
 }
 
@@ -322,7 +323,7 @@ void free_buffer(Scratch& s) {
                   s.vals[0], s.vals[1], s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1,
                   s.defer1_n, s.fast_blk, s.hits_s, s.segsum, s.rid, s.run_start, s.run_flags, s.run_state, s.run_alias,
                   s.run_f, s.runs64, s.split, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t, s.r_base,
-                  s.uniq, s.uniq_n, s.long_runs, s.kt_blk, s.log_epoch};
+                  s.uniq, s.uniq_n, s.long_runs, s.kt_blk, s.log_epoch, s.woff, s.wtsum};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
 }
@@ -685,7 +686,7 @@ int eng_route_pack(Engine* c, const rl_batch* in, uint32_t n_shards, uint32_t sr
 int eng_route_owner(Engine* c, uint32_t n, const Wire* recv_rec, const uint8_t* recv_stem, uint64_t recv_stem_bytes,
                     const uint64_t* src_stem_base, uint32_t n_src, uint32_t n_rules, uint32_t rule_stride,
                     unsigned long long* stats, int isolate, hipEvent_t ready, uint32_t* slot,
-                    const OwnChunk* own) {
+                    const OwnChunk* own, const uint32_t* woff, const unsigned long long* wbad) {
   const uint32_t rules_eff = rule_stride ? n_src * rule_stride : n_rules;
   const bool has_own = own && own->n;
   // (recv_stem may be null with no received stem bytes: an own chunk alone)
@@ -714,6 +715,12 @@ int eng_route_owner(Engine* c, uint32_t n, const Wire* recv_rec, const uint8_t* 
     HIPCHK(c, hipEventSynchronize(c->b_done[k]));  // (the pinned bases of buffer k's previous batch were read)
     for (uint32_t j = 0; j < n_src; j++) hb[j] = src_stem_base[j];
     HIPCHK(c, hipMemcpyAsync(sk.r_base, hb, (size_t)n_src * 8, hipMemcpyHostToDevice, a));
+    if (!woff) {  // (the records' stem offsets: the lengths scanned here, unless the caller did it for every part)
+      launch_wire_offsets(recv_rec, n, has_own ? own->lo : 0u, has_own ? own->lo + own->n : 0u, sk.r_base, n_src,
+                          recv_stem_bytes, sk.woff, sk.wtsum, a);
+      woff = sk.woff;
+      wbad = sk.wtsum + WIRE_SCAN_TILES(n);
+    }
   }
   // k_prepare reads the wire records in place (a malformed exchange fails
   // the batch's validation word)
@@ -727,6 +734,8 @@ int eng_route_owner(Engine* c, uint32_t n, const Wire* recv_rec, const uint8_t* 
   b.now_desc = 1;
   b.stem = recv_stem;
   b.wire = recv_rec;
+  b.woff = woff;
+  b.wbad = wbad;
   b.wbase = sk.r_base;
   b.n_src = n_src;
   b.rule_stride = rule_stride;

@@ -100,8 +100,11 @@ struct BatchDev {
   const uint32_t* rule;
   // routed owner batch (eng_route_owner): the received wire records replace
   // the arrays above (off, now, req, unit, flags, limit, hits, rule = null);
-  // the stem of record j starts at wbase[source] + wire[j].off
+  // the stem of record j starts at woff[j] and must lie inside its source's
+  // chunk [wbase[src], wbase[src + 1]) (the last source's ends at stem_total)
   const Wire* wire;
+  const uint32_t* woff;             // [n] stem offset of each record (launch_wire_offsets)
+  const unsigned long long* wbad;   // the offset scan's verdict (non-zero: a chunk's lengths do not add up)
   const unsigned long long* wbase;  // [n_src] chunk offset of each source in stem
   uint32_t n_src, rule_stride;
   OwnChunk own;  // (n = 0: none)
@@ -139,16 +142,19 @@ __host__ __device__ inline uint32_t rec_flags(const Rec& r) { return r.lu >> 24;
 constexpr uint32_t ROUTE_REQ_BITS = 24;  // label = source rank << 24 | request index
 constexpr uint32_t ROUTE_MAX_REQ = 1u << ROUTE_REQ_BITS;
 constexpr uint32_t ROUTE_TILE = 512;  // descriptors per partition tile (rl_route.hip RP_TILE)
+// No stem offset: the stems of the records follow each other in record order
+// (each source's chunk, sources in rank order), so the owner derives every
+// offset from the lengths (launch_wire_offsets, one scan per exchange).
 struct __attribute__((aligned(8))) Wire {
-  uint32_t label;  // global request label (non-decreasing in global arrival order)
-  uint32_t off;    // stem byte offset inside the owner's chunk of this source
+  uint32_t label;  // global request label (non-decreasing in global arrival order); first field (rl_comm reads it strided)
   uint32_t lu;     // stem length (16) | unit << 16 | flags << 24
   uint32_t limit;
   uint32_t hits;
   uint32_t rule;
-  int64_t now;
+  uint32_t now;    // the request's clock as the table keeps it (WIRE_NOW_BAD: outside [0, NOW_MAX] at the source)
   unsigned long long hash;  // keyed stem hash (source side): the owner's sort key and slot tag
 };
+constexpr uint32_t WIRE_NOW_BAD = 0xFFFFFFFFu;  // (> NOW_MAX: the owner's clock check fails it)
 static_assert(sizeof(Wire) == RL_WIRE_BYTES, "wire record size is part of the ABI");
 
 struct OutDev {
@@ -248,6 +254,8 @@ struct Scratch {
   uint32_t* route_hist;              // [2 x RL_MAX_SHARDS x tiles] per-tile counts (routing scratch only)
   // routed owner batches (eng_route_owner)
   unsigned long long* r_base;        // [RL_MAX_SHARDS] received stem chunk starts per source
+  uint32_t* woff;                    // [max_batch + 1] received records' stem offsets (rl_route_do_limit)
+  unsigned long long* wtsum;         // [WIRE_SCAN_WORDS(max_batch)] its scan's tile sums and verdict
 };
 
 // The two stages of one batch. Stage A (validate, hash, sort, segment) touches
@@ -323,6 +331,20 @@ void launch_unpack_prefixed(const rl_batch_prefixed& pb, const uint8_t* buf, uin
 // wire record, no stem bytes: its owner batch reads them in place,
 // BatchDev::own). hash_out: where the stem hashes go (null: the scratch's).
 constexpr uint32_t ROUTE_OWN_NONE = 0xFFFFFFFFu;
+// Stem offsets of n received wire records: woff[j] = the lengths of records
+// [0, j) summed, the records [olo, ohi) (the own chunk, stems read in place)
+// counted as 0; woff[n] = the total. A sum past 32 bits saturates (the owner's
+// bounds check then fails the record). Every source's chunk must start at its
+// base (wbase[src], device) and end at the next one's (the last at
+// stem_total): else tsum[WIRE_SCAN_TILES(n)] (the scan's verdict word,
+// BatchDev::wbad) is set and the owner batches reading these offsets fail
+// (RL_E_INVALID) instead of reading shifted keys. tsum: WIRE_SCAN_WORDS(n).
+constexpr uint32_t WIRE_SCAN_TILE = 2048;
+inline uint32_t WIRE_SCAN_TILES(uint64_t n) { return (uint32_t)((n + WIRE_SCAN_TILE) / WIRE_SCAN_TILE); }
+inline uint32_t WIRE_SCAN_WORDS(uint64_t n) { return WIRE_SCAN_TILES(n) + 1; }
+void launch_wire_offsets(const Wire* w, uint32_t n, uint32_t olo, uint32_t ohi, const unsigned long long* wbase,
+                         uint32_t n_src, unsigned long long stem_total, uint32_t* woff, unsigned long long* tsum,
+                         hipStream_t st);
 void launch_route_pack(const BatchDev& b, uint32_t n_shards, uint32_t src_rank, Wire* out, uint8_t* out_stem,
                        uint32_t* perm, unsigned long long* counts, const Scratch& s, hipStream_t st,
                        uint32_t cstride = 2, unsigned long long meta0 = 0, unsigned long long meta1 = 0,

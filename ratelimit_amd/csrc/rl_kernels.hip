@@ -69,10 +69,11 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   auto time_bad = [&](int64_t t) { return t < 0 || t > (int64_t)NOW_MAX || t < floor; };
 
   // ---- the descriptor: packed arrays, or (routed owner batch) its wire
-  // record, whose stem sits at its source's chunk base + off; chunks arrive in
-  // source order, so consecutive records' stems must abut (a malformed
-  // exchange fails the batch, never a wrong key). rule_stride > 0 attributes
-  // stats per source (rule' = source x rule_stride + rule).
+  // record, whose stem starts at woff[i] (the lengths of the records before
+  // it, summed); chunks arrive in source order, so the stem must lie inside
+  // its source's chunk (a malformed exchange fails the batch, never a wrong
+  // key). rule_stride > 0 attributes stats per source (rule' = source x
+  // rule_stride + rule).
   uint32_t s0 = 0, s1 = 0, u = 0, q = 0, fl = 0, rule = 0, hits = 0, limit = 0, dstat = 0, len = 0;
   int64_t tnow = 0;
   unsigned long long whash = 0;
@@ -102,14 +103,17 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
       const uint32_t src = w.label >> ROUTE_REQ_BITS;
       const uint32_t wl = w.lu & 0xFFFFu;
       layout_bad = src >= b.n_src;
-      s0 = (uint32_t)((layout_bad ? 0ull : b.wbase[src]) + w.off);
-      s1 = s0 + wl;
-      if (i + 1 < b.n && !(i + 1 - b.own.lo < b.own.n)) {  // (the own chunk's records carry no wire stem)
-        const Wire x = b.wire[i + 1];
-        const uint32_t s2 = x.label >> ROUTE_REQ_BITS;
-        layout_bad = layout_bad || s2 >= b.n_src || b.wbase[s2] + x.off != (unsigned long long)s1 || x.label < w.label;
+      s0 = b.woff[i];
+      const unsigned long long e0 = (unsigned long long)s0 + wl;
+      s1 = (uint32_t)e0;
+      if (!layout_bad) {
+        const unsigned long long c0 = b.wbase[src], c1 = src + 1 < b.n_src ? b.wbase[src + 1] : b.stem_total;
+        layout_bad = s0 < c0 || e0 > c1;
       }
-      layout_bad = layout_bad || s1 > b.stem_total;
+      if (i + 1 < b.n && !(i + 1 - b.own.lo < b.own.n))  // (the own chunk's records carry no wire label)
+        layout_bad = layout_bad || b.wire[i + 1].label < w.label;
+      layout_bad = layout_bad || *b.wbad != 0;  // (a chunk whose lengths do not add up: every offset after it is shifted)
+      layout_bad = layout_bad || e0 > b.stem_total;
       u = (w.lu >> 16) & 0xFFu;
       fl = w.lu >> 24;
       q = w.label;
@@ -5146,11 +5150,13 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
     k_run_check<<<cdiv(b.n, RC_CHUNK), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[1], s.rid, s.run_start,
                                                 s.run_end, s.run_flags, s.defer, s.defer_n, s.err, s.runs64, s.split,
                                                 s.sorted_n, s.grp, s.hit_t, s.uniq, s.uniq_n, s.long_runs);
+#ifndef RL_EXP_NO_SPLIT  // (measurement builds only: C1 defers no run to k_split)
     k_split<<<SPLIT_BLOCKS, SPLIT_THREADS, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.vals[0], s.segsum, s.rid, s.run_start,
                                           s.run_end, s.run_flags, s.defer, s.defer_n, s.runs64, s.split, s.drun,
                                           b.n / 2 + BIG_HEAVY * PART_DIGITS, s.grp, s.lead, s.hit_t, s.vals[1], s.err,
                                           per_second, UniqList{s.uniq, s.uniq_n, s.keys[1]}, s.long_runs, long_hint,
                                           long_kernel ? 1 : 0);
+#endif
 #if RL_SPLIT_LONG_THREADS
     if (long_kernel)
       k_split_long<<<RL_SPLIT_LONG_BLOCKS, RL_SPLIT_LONG_THREADS, 0, st>>>(
@@ -5209,6 +5215,7 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     if (ev) (void)hipEventRecord(ev[4], st);
     if (!restore && P.lc_en)
       k_fast_over<<<g, 256, 0, st>>>(s.sorted_n, rs, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
+#ifndef RL_EXP_NO_LATE  // (measurement builds only: C1 leaves k_late nothing to do)
     k_late<<<RUNS_GENERAL_LATE_BLOCKS + (restore ? 0u : (RL_LATE_FAST_BLOCKS && g > RL_LATE_FAST_BLOCKS
                                                             ? RL_LATE_FAST_BLOCKS : g)), 256, lds, st>>>(
         b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer, s.defer_n, s.defer2, s.defer2_n,
@@ -5216,6 +5223,7 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
         s.keys[0], s.defer1, s.defer1_n, s.segsum, s.rid, s.run_flags, s.run_state, s.run_alias, s.run_f, o.stats,
         s.stripes, s.errb,
         s.errs, restore, s.fast_blk, s.sorted_n);
+#endif
     if (table_done) (void)hipEventRecord(table_done, st);
     if (!restore) {
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;

@@ -34,7 +34,7 @@ __device__ inline uint32_t owner_of(uint64_t h, uint32_t n_shards) {
 // Partition of a slice by owner, in three launches over tiles of RP_TILE
 // descriptors (all HBM-streaming; the byte moves go through LDS):
 //   k_rp_count  keyed stem hash (kept for the wire record: owners never
-//               rehash) -> owner per descriptor (dest, u8), per-tile record
+//               rehash; no stem offset: owners scan the lengths) -> owner per descriptor (dest, u8), per-tile record
 //               and stem-byte counts per owner;
 //   k_rp_scan   per owner: exclusive scan of the tile counts, the totals
 //               (= the exchange counts);
@@ -307,16 +307,16 @@ __global__ __launch_bounds__(256) void k_rp_pack(BatchDev b, uint32_t n_shards, 
       perm[j] = i;
       continue;
     }
-    const uint32_t local = gb[d] + wb[w][d] + my_b[t];  // byte offset inside owner d's chunk
+    const uint32_t local = gb[d] + wb[w][d] + my_b[t];  // byte offset inside owner d's chunk (not sent: the owner scans lengths)
     const uint32_t q = b.req[i];
+    const int64_t tq = b.now[q];
     Wire x;
     x.label = (src_rank << ROUTE_REQ_BITS) | q;
-    x.off = local;
     x.lu = len | ((uint32_t)b.unit[i] << 16) | ((uint32_t)b.flags[i] << 24);
     x.limit = b.limit[i];
     x.hits = b.hits[i];
     x.rule = b.rule[i] < b.n_rules ? b.rule[i] : 0xFFFFFFFFu;  // (the owner fails it alone, any rule stride)
-    x.now = b.now[q];
+    x.now = tq < 0 || tq > (int64_t)NOW_MAX ? WIRE_NOW_BAD : (uint32_t)tq;  // (the owner fails it: RL_E_TIME)
     x.hash = hash[i];
 #if !(RL_RP_ABL & 2)
     out[j] = x;
@@ -429,7 +429,100 @@ __global__ void k_cnt_fill(unsigned long long* cnt, uint32_t n_peers, uint32_t c
   }
 }
 
+// ---- owner side: the received records' stem offsets ----------------------
+// Two passes over tiles of WIRE_SCAN_TILE records (8 per thread): k_ws_tiles
+// stores each record's stem length (0 in the own chunk [olo, ohi), whose stems
+// are read in place) into woff and the tile's sum into tsum; k_ws_offsets adds
+// the sums of the tiles before its own and turns woff's lengths into
+// exclusive offsets in place (each thread reads its 8 lengths before writing).
+constexpr uint32_t WS_ITEMS = WIRE_SCAN_TILE / 256;
+
+__device__ inline unsigned long long block_sum64(unsigned long long v, unsigned long long* tmp) {
+#pragma unroll
+  for (uint32_t o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (lane_id() == 0) tmp[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = tmp[0] + tmp[1] + tmp[2] + tmp[3];
+  __syncthreads();
+  return v;
+}
+
+__global__ __launch_bounds__(256) void k_ws_tiles(const Wire* __restrict__ w, uint32_t n, uint32_t olo, uint32_t ohi,
+                                                  uint32_t* __restrict__ woff, unsigned long long* __restrict__ tsum) {
+  __shared__ unsigned long long tmp[4];
+  if (blockIdx.x == 0 && threadIdx.x == 0) tsum[gridDim.x] = 0;  // (the verdict: k_ws_offsets sets it)
+  const uint32_t j0 = blockIdx.x * WIRE_SCAN_TILE + threadIdx.x * WS_ITEMS;
+  unsigned long long acc = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < WS_ITEMS; t++) {
+    const uint32_t j = j0 + t;
+    const uint32_t len = j < n && !(j - olo < ohi - olo) ? (w[j].lu & 0xFFFFu) : 0u;
+    if (j < n) woff[j] = len;
+    acc += len;
+  }
+  acc = block_sum64(acc, tmp);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_ws_offsets(const Wire* __restrict__ w, uint32_t n, uint32_t olo,
+                                                    uint32_t ohi, const unsigned long long* __restrict__ wbase,
+                                                    uint32_t n_src, unsigned long long total,
+                                                    unsigned long long* __restrict__ tsum,
+                                                    uint32_t* __restrict__ woff) {
+  __shared__ unsigned long long tmp[4], wtot[4];
+  unsigned long long base = 0;  // the tiles before this one
+  for (uint32_t k = threadIdx.x; k < blockIdx.x; k += 256) base += tsum[k];
+  base = block_sum64(base, tmp);
+  const uint32_t j0 = blockIdx.x * WIRE_SCAN_TILE + threadIdx.x * WS_ITEMS;
+  uint32_t len[WS_ITEMS];
+  unsigned long long mine = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < WS_ITEMS; t++) {
+    len[t] = j0 + t < n ? woff[j0 + t] : 0u;
+    mine += len[t];
+  }
+  // exclusive prefix of `mine` over the block's threads (wave scan, then waves)
+  unsigned long long inc = mine;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(inc, o, 64);
+    if (lane_id() >= o) inc += y;
+  }
+  const uint32_t wv = threadIdx.x >> 6;
+  if (lane_id() == 63) wtot[wv] = inc;
+  __syncthreads();
+  unsigned long long at = base + inc - mine;
+  for (uint32_t k = 0; k < wv; k++) at += wtot[k];
+  bool bad = false;
+  auto own = [&](uint32_t j) { return j - olo < ohi - olo; };
+#pragma unroll
+  for (uint32_t t = 0; t < WS_ITEMS; t++) {
+    const uint32_t j = j0 + t;
+    if (j <= n) woff[j] = at < (1ull << 32) ? (uint32_t)at : 0xFFFFFFFFu;  // (woff[n]: the total)
+    if (j < n && !own(j)) {  // a source's chunk starts at its base and ends at the next one's
+      const uint32_t src = w[j].label >> ROUTE_REQ_BITS;
+      if (src >= n_src) {
+        bad = true;
+      } else {
+        if (j == 0 || own(j - 1) || (w[j - 1].label >> ROUTE_REQ_BITS) != src) bad = bad || at != wbase[src];
+        if (j + 1 == n || own(j + 1) || (w[j + 1].label >> ROUTE_REQ_BITS) != src)
+          bad = bad || at + len[t] != (src + 1 < n_src ? wbase[src + 1] : total);
+      }
+    }
+    at += len[t];
+  }
+  if (__any(bad) && (threadIdx.x & 63u) == 0) atomicOr(tsum + gridDim.x, 1ull);
+}
+
 }  // namespace
+
+void launch_wire_offsets(const Wire* w, uint32_t n, uint32_t olo, uint32_t ohi, const unsigned long long* wbase,
+                         uint32_t n_src, unsigned long long stem_total, uint32_t* woff, unsigned long long* tsum,
+                         hipStream_t st) {
+  const uint32_t tiles = WIRE_SCAN_TILES(n);  // (n + 1 entries: a tile more when n is a multiple of the tile)
+  k_ws_tiles<<<tiles, 256, 0, st>>>(w, n, olo, ohi, woff, tsum);
+  k_ws_offsets<<<tiles, 256, 0, st>>>(w, n, olo, ohi, wbase, n_src, stem_total, tsum, woff);
+}
 
 void launch_stats_sum(const unsigned long long* stage, uint32_t n_blocks, uint32_t m, unsigned long long* out,
                       hipStream_t st, uint32_t stride) {

@@ -60,7 +60,7 @@ import torch.distributed as dist
 from . import abi
 from ._lib import RedisError, check, lib
 
-WIRE_BYTES = 40  # RL_WIRE_BYTES
+WIRE_BYTES = 32  # RL_WIRE_BYTES
 
 
 def loopback_id() -> np.ndarray:

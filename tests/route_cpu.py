@@ -5,8 +5,9 @@ box that is DeviceRouteOps (rl_route_* kernels). Here the same protocol runs
 over gloo with numpy packing and the C oracle as each owner's table, so the
 host-side exchange (split sizes, ordering across ranks, inverse routing,
 stats all_reduce, error agreement) is tested without a GPU. The wire layout is
-the C ABI's (RL_WIRE_BYTES records: label, off, lu, limit, hits, rule, now,
-stem hash; the CPU owners here do not read the hash and it is left 0).
+the C ABI's (RL_WIRE_BYTES records: label, lu, limit, hits, rule, 32-bit
+now, stem hash; no stem offset: each owner chunk's stems follow its records'
+order; the CPU owners here do not read the hash and it is left 0).
 """
 import zlib
 
@@ -17,9 +18,10 @@ from oracle.c_oracle import COracle
 from ratelimit_amd import abi
 from ratelimit_amd._lib import RedisError
 
-WIRE = np.dtype([("label", "<u4"), ("off", "<u4"), ("lu", "<u4"), ("limit", "<u4"), ("hits", "<u4"),
-                 ("rule", "<u4"), ("now", "<i8"), ("hash", "<u8")])
-assert WIRE.itemsize == 40
+WIRE = np.dtype([("label", "<u4"), ("lu", "<u4"), ("limit", "<u4"), ("hits", "<u4"), ("rule", "<u4"),
+                 ("now", "<u4"), ("hash", "<u8")])
+assert WIRE.itemsize == 32
+NOW_MAX = 0xFFFFFFFF - 2 * 86400
 
 
 def owner_of(stem: bytes, world: int) -> int:
@@ -40,15 +42,14 @@ class CpuRouteOps:
         order = np.argsort(dest, kind="stable")
         rec = np.zeros(n, WIRE)
         counts = np.zeros((world, 2), np.uint64)
-        chunk_off = np.zeros(world, np.int64)
         blob = bytearray()
         for j, e in enumerate(order):
             d = dest[e]
             s = stems[e]
             q = int(a["req_idx"][e])
-            rec[j] = ((rank << 24) | q, chunk_off[d], len(s) | (int(a["unit"][e]) << 16) | (int(a["flags"][e]) << 24),
-                      a["limit"][e], a["hits"][e], a["rule_id"][e], a["now"][q], 0)
-            chunk_off[d] += len(s)
+            t = int(a["now"][q])
+            rec[j] = ((rank << 24) | q, len(s) | (int(a["unit"][e]) << 16) | (int(a["flags"][e]) << 24),
+                      a["limit"][e], a["hits"][e], a["rule_id"][e], t if 0 <= t <= NOW_MAX else 0xFFFFFFFF, 0)
             counts[d, 0] += 1
             counts[d, 1] += len(s)
             blob += s
@@ -63,14 +64,16 @@ class CpuRouteOps:
         rec = recv_rec[:n * WIRE.itemsize].numpy().view(WIRE)
         blob = recv_stem[:stem_bytes].numpy()
         src = rec["label"] >> 24
-        starts = np.asarray(src_base, np.int64)[src] + rec["off"]
-        lens = rec["lu"] & 0xFFFF
-        assert n == 0 or np.all(starts[1:] == starts[:-1] + lens[:-1]), "stems must abut"
+        lens = (rec["lu"] & 0xFFFF).astype(np.int64)
+        starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)  # (the owner's length scan)
+        base = np.asarray(src_base, np.int64)
+        ends = np.append(base[1:], stem_bytes)
+        assert n == 0 or (np.all(starts >= base[src]) and np.all(starts + lens <= ends[src])), "stem outside its chunk"
         labels, first, req = np.unique(rec["label"], return_index=True, return_inverse=True)
         arrays = {"stem_bytes": blob.copy() if stem_bytes else np.zeros(4, np.uint8),
                   "stem_off": np.concatenate([starts, [starts[-1] + lens[-1]]]).astype(np.uint32) if n else
                   np.zeros(1, np.uint32),
-                  "now": rec["now"][first].copy() if n else np.zeros(1, np.int64),
+                  "now": rec["now"][first].astype(np.int64) if n else np.zeros(1, np.int64),
                   "req_idx": req.astype(np.uint32), "unit": ((rec["lu"] >> 16) & 0xFF).astype(np.uint8),
                   "flags": (rec["lu"] >> 24).astype(np.uint8), "limit": rec["limit"].copy(),
                   "hits": rec["hits"].copy(),

@@ -54,7 +54,7 @@ def _dev(a, dev):
 
 
 def run_world(world, batches, cfg, *, max_batch=1 << 15, max_rules=64, slices=None, isolate=(), n_rules_of=None,
-              serial=False, table_slots=1 << 18, after=None):
+              serial=False, table_slots=1 << 18, after=None, before=None):
     """Drive `world` loopback ranks over `batches`. slices(k) -> request cut
     points (default: uneven random); isolate: ranks passing out.status;
     n_rules_of(rank, k) overrides a rank's n_rules. Returns per rank either
@@ -73,6 +73,8 @@ def run_world(world, batches, cfg, *, max_batch=1 << 15, max_rules=64, slices=No
         dev = torch.device("cuda", 0)
         keep = []
         try:
+            if before:
+                before(r, bes[r])
             for k, (arrays, n, nq, n_rules) in enumerate(batches):
                 cuts = slices(k) if slices else _split_points(nq, world, k)
                 sub, sn, snq = slice_requests(arrays, n, nq, cuts[r], cuts[r + 1])
@@ -311,6 +313,30 @@ def test_gpu_loopback_sweep_and_table_info_are_collective():
     live = sum(info[r][0] for r in range(2))
     assert live == len(keys), (live, len(keys))
     assert sum(info[r][1] for r in range(2)) == live and all(info[r][2] == 0 for r in range(2))
+
+
+def test_gpu_loopback_sweep_floor_is_the_least_over_ranks():
+    """A routed rl_sweep applies one floor on every rank, the least `now` the
+    ranks passed: rank 0 sweeps at NOW0 + 3 and rank 1 at NOW0 - 100, so the
+    batches at NOW0 .. NOW0 + 2 that rank 1 sends to owner 0 are answered (a
+    floor of rank 0's own would refuse them with RL_E_TIME); a third rank
+    passing an out-of-range time fails its own sweep and does not vote."""
+    cfg = (0.8, False, False)
+    batches = _c2_batches(71, requests=2_000, batches=3)
+    swept = {}
+
+    def before(r, be):
+        t = {0: W.NOW0 + 3, 1: W.NOW0 - 100, 2: -1}[r]
+        try:
+            swept[r] = be.sweep(t)
+        except RedisError as e:
+            swept[r] = e.status
+
+    out = run_world(3, batches, cfg, before=before)
+    assert swept[0] == 0 and swept[1] == 0 and swept[2] == abi.RL_E_TIME, swept
+    for r in range(3):
+        assert out[r][0] == "ok", out[r][1]
+    _check(out, batches, cfg, 3)
 
 
 def test_gpu_loopback_missing_peer_times_out(monkeypatch):
