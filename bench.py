@@ -343,7 +343,8 @@ def main():
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         check["verified"] = check["verified"] and bool(ok.item())
     if not check["verified"]:
-        print("[bench] SELF-CHECK FAILED (rank %d): %s" % (rank, json.dumps(check)), file=sys.stderr, flush=True)
+        print("[bench] SELF-CHECK FAILED (rank %d): %s; no result line (unverified rate %.4g decisions/s, %.4f ms "
+              "per step)" % (rank, json.dumps(check), value, elapsed / args.steps * 1e3), file=sys.stderr, flush=True)
         be.close()
         raise SystemExit(1)
     progress("self-check: %d descriptors equal to the oracle" % check["checked"])

@@ -10,8 +10,13 @@ for rep in $(seq $REPS); do
     for cfg in $CFGS; do
       tag=$(basename "${lib:-cur}" .so)_${cfg}_$rep
       RL_LIB_PATH=${lib:+$PWD/$lib} timeout -k 10 240 python -u bench.py --config $cfg --no-cpu-baseline --steps 200 \
-        --latency-steps 5 --loaded-steps 0 --pcie-steps 0 $BARGS > gpurun_out/ab/$tag.log 2>&1 \
-        || { tail -5 gpurun_out/ab/$tag.log; exit 1; }
+        --latency-steps 5 --loaded-steps 0 --pcie-steps 0 $BARGS > gpurun_out/ab/$tag.log 2>&1
+      rc=$?
+      if [ $rc -ne 0 ]; then  # (a probe build that skips work fails the self-check: report its unverified rate)
+        grep -q "SELF-CHECK FAILED" gpurun_out/ab/$tag.log || { tail -5 gpurun_out/ab/$tag.log; exit 1; }
+        echo "$tag $(grep -o 'unverified rate [^)]*' gpurun_out/ab/$tag.log) (self-check failed: a probe, not a result)"
+        continue
+      fi
       python - gpurun_out/ab/$tag.log $tag <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric')][-1])
