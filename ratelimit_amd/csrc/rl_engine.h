@@ -111,6 +111,9 @@ struct Engine {
   uint32_t* h_big = nullptr;   // pinned [NBUF]: k_bucket queued a large bucket (hot keys)
   uint32_t big_recent = 0;     // batches left with full large-bucket grids
   int big_mode = 1;            // RL_BIG_CUE: 0 full grids always, 1 while recent batches had large buckets
+  uint32_t* h_late = nullptr;  // pinned [NBUF]: k_late met a long run (RUN_FAST) in this buffer's batch
+  uint32_t late_recent = 0;    // batches left with k_late's full long-run grid
+  int late_mode = 1;           // RL_LATE_CUE: 0 full grid always, 1 while recent batches had long runs
   unsigned long long* h_counters = nullptr;
   std::string last_error;
   uint64_t batches = 0, decisions = 0;

@@ -174,6 +174,19 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     if (c->big_recent) c->big_recent--;
   }
   uint32_t* bhint = c->big_mode == 1 ? c->h_big + k : nullptr;
+  // k_late's long-run part likewise: one workgroup per 256 sorted positions
+  // while recent batches had long runs, else a few that walk the bitmap
+  bool late_full = c->late_mode == 0;
+  if (c->late_mode == 1) {
+    for (uint32_t j = 0; j < NBUF; j++)
+      if (__atomic_load_n(&c->h_late[j], __ATOMIC_RELAXED)) {
+        __atomic_store_n(&c->h_late[j], 0u, __ATOMIC_RELAXED);
+        c->late_recent = 4 * NBUF;
+      }
+    late_full = c->late_recent > 0;
+    if (c->late_recent) c->late_recent--;
+  }
+  uint32_t* lhint = c->late_mode == 1 ? c->h_late + k : nullptr;
   if (pipelined) {
     hipStream_t a = c->pipe[k];
     hipEvent_t* ev = prof_events(c);
@@ -183,7 +196,7 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     if (early) launch_b_begin_early(b, o, c->s[k], restore, a, c->log_ctr);  // (off the table-order chain)
     (void)hipStreamWaitEvent(a, c->b_table[c->last], 0);  // table order (not the previous k_finish)
     launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
-                   early);
+                   early, lhint, late_full);
     (void)hipEventRecord(c->b_done[k], a);
   } else {
     if (!st) st = c->stream;
@@ -192,7 +205,7 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     launch_stage_a(b, c->s[k], isolate, P.per_second, st, ev, hint, lng, bhint, big_full);
     if (early) launch_b_begin_early(b, o, c->s[k], restore, st, c->log_ctr);
     launch_stage_b(b, o, t, P, c->s[k], restore, st, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
-                   early);
+                   early, lhint, late_full);
     (void)hipEventRecord(c->b_done[k], st);
   }
   c->last = k;
@@ -487,6 +500,9 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   ok = ok && hipHostMalloc((void**)&c->h_big, NBUF * sizeof(uint32_t)) == hipSuccess;
   if (ok) memset(c->h_big, 0, NBUF * sizeof(uint32_t));
   if (const char* bc = getenv("RL_BIG_CUE")) c->big_mode = atoi(bc);  // (A/B knob)
+  ok = ok && hipHostMalloc((void**)&c->h_late, NBUF * sizeof(uint32_t)) == hipSuccess;
+  if (ok) memset(c->h_late, 0, NBUF * sizeof(uint32_t));
+  if (const char* lc = getenv("RL_LATE_CUE")) c->late_mode = atoi(lc);  // (A/B knob)
   if (!ok) return fail("gpu: device allocation failed (table_slots/arena/max_batch too large?)", c);
   ok = hipMemsetAsync(c->slots, 0, c->nslots * sizeof(Slot), c->stream) == hipSuccess &&
        hipMemsetAsync(c->log_ctr, 0, (size_t)(LOG_PARTS + 1) * LOG_CTR_STRIDE * 8, c->stream) == hipSuccess &&
@@ -582,6 +598,7 @@ void eng_destroy(Engine* c) {
   if (c->h_counters) (void)hipHostFree(c->h_counters);
   if (c->h_long) (void)hipHostFree(c->h_long);
   if (c->h_big) (void)hipHostFree(c->h_big);
+  if (c->h_late) (void)hipHostFree(c->h_late);
   for (void* p : {(void*)c->cfg_blob, (void*)c->mbuf})
     if (p) (void)hipFree(p);
   if (c->h_match) (void)hipHostFree(c->h_match);

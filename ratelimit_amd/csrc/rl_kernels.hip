@@ -4475,13 +4475,16 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
                                                    const uint4* __restrict__ run_alias,
                                                    const uint32_t* __restrict__ run_f, unsigned long long* stats,
                                                    unsigned long long* stripes, const uint32_t* err,
-                                                   const uint32_t* __restrict__ fast_blk) {
+                                                   const uint32_t* __restrict__ fast_blk, uint32_t* hint) {
   __shared__ uint32_t s_err, s_fast, s_n;
   __syncthreads();  // (grid-stride callers: the previous block's shared state has been read)
   if (threadIdx.x == 0) {
     s_err = *err;
-    s_fast = (fast_blk[blk >> 5] >> (blk & 31)) & 1u;
+    const uint32_t word = fast_blk[blk >> 5];
+    s_fast = (word >> (blk & 31)) & 1u;
     s_n = *sorted_n;
+    // the host's cue (one store per bitmap word): this batch had long runs
+    if (hint && s_fast && (uint32_t)(__ffs(word) - 1) == (blk & 31)) *hint = 1u;
   }
   __syncthreads();
   if (s_err || !s_fast) return;  // no RUN_FAST descriptor in this block (k_table's bitmap)
@@ -4512,7 +4515,10 @@ __device__ __attribute__((always_inline)) inline void fast_emit_body(uint32_t bl
       emit(res, L, acc, x, d, masked);
       if (!masked) {
         const uint32_t nq = q + 1;
-        const bool last = nq == run_end[r] || rec_s[nq].req > req_f;
+        // (the next element's request only matters below an over-limit one:
+        // no gather of its record otherwise, e.g. every element with the local
+        // cache off)
+        const bool last = nq == run_end[r] || (req_f != 0xFFFFFFFFu && rec_s[nq].req > req_f);
         if (last && (fl & RUN_ALIAS)) {  // the key's records in every unit slot (alias_setup's targets)
           const uint4 sl = run_alias[r];
 #pragma unroll
@@ -4756,6 +4762,50 @@ __device__ __attribute__((always_inline)) inline void general_body(uint32_t blk,
 //
 // k_table: the runs of two or more (runs_body, blocks [0, g_runs)) and the keys
 // seen once (unique_body, the rest).
+// k_late's long-run part on a few workgroups (recent batches had no long
+// runs): workgroup k of F reads 256 words of k_table's bitmap at once and walks
+// only the marked blocks, so an empty bitmap costs one load per lane; a long
+// run that does appear is still answered (and cues full grids for the next
+// batches).
+__device__ __attribute__((always_inline)) inline void late_scan(uint32_t k, uint32_t F, BatchDev b, TableDev t, Params P,
+                                                   SRec rec_s, const uint32_t* __restrict__ svals,
+                                                   unsigned long long* __restrict__ res,
+                                                   const uint32_t* __restrict__ segsum, const uint32_t* __restrict__ rid,
+                                                   const uint32_t* __restrict__ run_start,
+                                                   const uint32_t* __restrict__ run_end,
+                                                   const uint32_t* __restrict__ run_flags,
+                                                   const uint4* __restrict__ run_state,
+                                                   const uint4* __restrict__ run_alias, const uint32_t* __restrict__ run_f,
+                                                   unsigned long long* stats, unsigned long long* stripes,
+                                                   const uint32_t* err, const uint32_t* __restrict__ fast_blk,
+                                                   const uint32_t* sorted_n, uint32_t* hint) {
+  __shared__ uint32_t s_w[256], s_word[256], s_cnt;
+  const uint32_t nw = (b.n + 256u * 32u - 1) / (256u * 32u);
+  for (uint32_t w0 = k * 256; w0 < nw; w0 += F * 256) {
+    __syncthreads();
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    const uint32_t w = w0 + threadIdx.x;
+    const uint32_t word = w < nw ? fast_blk[w] : 0u;
+    if (word) {
+      const uint32_t at = atomicAdd(&s_cnt, 1u);
+      s_w[at] = w;
+      s_word[at] = word;
+    }
+    __syncthreads();
+    const uint32_t cnt = s_cnt;
+    for (uint32_t j = 0; j < cnt; j++) {
+      uint32_t bits = s_word[j];
+      while (bits) {
+        const uint32_t blk = s_w[j] * 32 + (uint32_t)(__ffs(bits) - 1);
+        bits &= bits - 1;
+        fast_emit_body(blk, sorted_n, b.n_rules, t, P, rec_s, svals, res, segsum, rid, run_start, run_end, run_flags,
+                       run_state, run_alias, run_f, stats, stripes, err, fast_blk, hint);
+      }
+    }
+  }
+}
+
 #ifndef RL_KT_UNIQ_FIRST
 #define RL_KT_UNIQ_FIRST 0
 #endif
@@ -4779,6 +4829,7 @@ __global__ __launch_bounds__(256, RL_KTABLE_WAVES) void k_table(uint32_t g_runs,
                                                const uint32_t* uniq_n, unsigned long long* __restrict__ kt,
                                                const uint32_t* errb_prev) {
   // kt (rl_profile on): each workgroup's start and end on the device's
+
   // constant clock, plain stores (one address for all of them serialised the
   // launch: +40 %); k_finish folds them into the launch's duration
   if (kt && threadIdx.x == 0) kt[2 * blockIdx.x] = wall_clock64();
@@ -4839,16 +4890,22 @@ __global__ __launch_bounds__(256, RL_LATE_OCC) void k_late(BatchDev b, TableDev 
                                                  const uint4* __restrict__ run_alias, const uint32_t* __restrict__ run_f,
                                                  unsigned long long* stats, unsigned long long* stripes, uint32_t* err,
                                                  uint32_t* errs, int restore, const uint32_t* __restrict__ fast_blk,
-                                                 const uint32_t* sorted_n) {
-  if (blockIdx.x < RUNS_GENERAL_LATE_BLOCKS)
+                                                 const uint32_t* sorted_n, uint32_t* hint, int scan) {
+  if (blockIdx.x < RUNS_GENERAL_LATE_BLOCKS) {
     general_body(blockIdx.x, RUNS_GENERAL_LATE_BLOCKS, b, t, P, rec_s, skeys, svals, res, run_start, run_end, defer,
                  defer_n, defer2, defer2_n, grp, lead, gmask, keys0, defer1, defer1_n, run_flags, rid, stats, stripes,
                  err, errs, restore);
-  else if (!restore)  // (grid-stride when the launch caps the fast part's workgroups)
+  } else if (restore) {
+  } else if (!scan) {  // one workgroup per 256 sorted positions (grid-stride when the launch caps them)
     for (uint32_t blk = blockIdx.x - RUNS_GENERAL_LATE_BLOCKS; blk * 256 < b.n;
          blk += gridDim.x - RUNS_GENERAL_LATE_BLOCKS)
       fast_emit_body(blk, sorted_n, b.n_rules, t, P, rec_s, svals, res, segsum, rid, run_start, run_end, run_flags,
-                     run_state, run_alias, run_f, stats, stripes, err, fast_blk);
+                     run_state, run_alias, run_f, stats, stripes, err, fast_blk, hint);
+  } else {
+    late_scan(blockIdx.x - RUNS_GENERAL_LATE_BLOCKS, gridDim.x - RUNS_GENERAL_LATE_BLOCKS, b, t, P, rec_s, svals, res,
+              segsum, rid, run_start, run_end, run_flags, run_state, run_alias, run_f, stats, stripes, err, fast_blk,
+              sorted_n, hint);
+  }
 }
 
 // First kernel of the table stage: merge this batch's validation errors into
@@ -5174,6 +5231,7 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
 #ifndef RL_LATE_FAST_BLOCKS
 #define RL_LATE_FAST_BLOCKS 0  // cap on k_late's long-run workgroups (0: one per 256 descriptors)
 #endif
+constexpr uint32_t LATE_SCAN_BLOCKS = 4;  // k_late's long-run workgroups while recent batches had none
 // The table stage's first kernel, early (before the table-order wait, at the
 // end of stage A): this batch's table-stage word = its own validation, its
 // deferral counters, block bitmap and output stats cleared. k_table folds the
@@ -5188,7 +5246,7 @@ void launch_b_begin_early(const BatchDev& b, const OutDev& o, const Scratch& s, 
 
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
                     int restore, hipStream_t st, hipEvent_t* ev, const uint32_t* errb_prev, hipEvent_t table_done,
-                    unsigned long long* kt_acc, bool early) {
+                    unsigned long long* kt_acc, bool early, uint32_t* late_hint, bool late_full) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
   if (!early)
@@ -5216,13 +5274,16 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
     if (!restore && P.lc_en)
       k_fast_over<<<g, 256, 0, st>>>(s.sorted_n, rs, s.segsum, s.rid, s.run_flags, s.run_state, s.run_f, s.errb);
 #ifndef RL_EXP_NO_LATE  // (measurement builds only: C1 leaves k_late nothing to do)
-    k_late<<<RUNS_GENERAL_LATE_BLOCKS + (restore ? 0u : (RL_LATE_FAST_BLOCKS && g > RL_LATE_FAST_BLOCKS
-                                                            ? RL_LATE_FAST_BLOCKS : g)), 256, lds, st>>>(
+    // its long-run part: one workgroup per 256 sorted positions while recent
+    // batches had long runs (C2, C2U), else LATE_SCAN_BLOCKS walking the bitmap
+    const uint32_t gl = restore ? 0u : !late_full ? LATE_SCAN_BLOCKS
+                                     : (RL_LATE_FAST_BLOCKS && g > RL_LATE_FAST_BLOCKS ? RL_LATE_FAST_BLOCKS : g);
+    k_late<<<RUNS_GENERAL_LATE_BLOCKS + gl, 256, lds, st>>>(
         b, t, P, rs, s.keys[1], s.vals[0], s.res, s.run_start, s.run_end, s.defer, s.defer_n, s.defer2, s.defer2_n,
         s.grp, s.lead, s.gmask,
         s.keys[0], s.defer1, s.defer1_n, s.segsum, s.rid, s.run_flags, s.run_state, s.run_alias, s.run_f, o.stats,
         s.stripes, s.errb,
-        s.errs, restore, s.fast_blk, s.sorted_n);
+        s.errs, restore, s.fast_blk, s.sorted_n, late_hint, late_full ? 0 : 1);
 #endif
     if (table_done) (void)hipEventRecord(table_done, st);
     if (!restore) {

@@ -1,11 +1,11 @@
-# Round 6: k_late's long-run grid cue. Parity (alias / hot-key / parity
-# suites), then C1 and C2 A/B of the cue (default) against full grids always
-# (RL_LATE_CUE=0, the round-5 launch), alternating on one box.
+# Round 6: k_late folded into k_table (tail workgroups) while recent batches had no long runs.
+# Parity (alias, parity, history, full-size suites), then C1 and C2 A/B: default (cue + fold)
+# against RL_LATE_CUE=0 (k_late a launch of its own, full grid: the round-5 launch).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 timeout -k 10 700 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_alias.py \
-  tests/test_gpu_parity.py > gpurun_out/r06_late_tests.txt 2>&1 || { tail -40 gpurun_out/r06_late_tests.txt; exit 1; }
+  tests/test_gpu_parity.py tests/test_gpu_history.py tests/test_gpu_edges.py tests/test_gpu_robustness.py > gpurun_out/r06_late_tests.txt 2>&1 || { tail -40 gpurun_out/r06_late_tests.txt; exit 1; }
 tail -2 gpurun_out/r06_late_tests.txt
 mkdir -p gpurun_out/ab_late
 for rep in 1 2 3; do

@@ -98,6 +98,17 @@ def test_gpu_long_splits_inline_and_on_the_long_kernel_vs_c_oracle(monkeypatch, 
     _check(_stream([39, 40, 41], tenants=3000, rpb=8000), False, debug_hash_bits=6)
 
 
+@pytest.mark.parametrize("mode", ["0", "2"])
+def test_gpu_long_runs_on_full_and_scanning_late_grids_vs_c_oracle(monkeypatch, mode):
+    """k_late's long-run part on one workgroup per 256 sorted positions for
+    every batch (RL_LATE_CUE=0) and on the few workgroups that walk k_table's
+    bitmap for every batch (2); the default (1) uses the second until a batch
+    has long runs. Hot keys under two units (alias groups), local cache on."""
+    monkeypatch.setenv("RL_LATE_CUE", mode)
+    _check(_stream([38, 39, 40, 41], rpb=20_000, seed=5), True, table_slots=1 << 17, max_batch=1 << 17)
+    _check(_stream(list(range(38, 50)), rpb=4_000, tenants=500, seed=13), False)
+
+
 @pytest.mark.parametrize("lc", [False, True])
 def test_gpu_override_on_and_off_vs_c_oracle(lc):
     """Batches with and without overrides, repeated and backward clocks: stems
