@@ -194,9 +194,16 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     (void)hipStreamWaitEvent(a, c->consumed[k], 0);  // ... and its routed results were read
     launch_stage_a(b, c->s[k], isolate, P.per_second, a, ev, hint, lng, bhint, big_full);
     if (early) launch_b_begin_early(b, o, c->s[k], restore, a, c->log_ctr);  // (off the table-order chain)
-    (void)hipStreamWaitEvent(a, c->b_table[c->last], 0);  // table order (not the previous k_finish)
-    launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
-                   early, lhint, late_full);
+    if (c->sb) {  // (RL_SB: every batch's table stage on one stream, in order; k_finish back on the batch's)
+      (void)hipEventRecord(c->a_done[k], a);
+      (void)hipStreamWaitEvent(c->sb, c->a_done[k], 0);
+      launch_stage_b(b, o, t, P, c->s[k], restore, c->sb, ev, errb_prev, c->b_table[k],
+                     c->prof ? c->d_kt_acc : nullptr, early, lhint, late_full, a);
+    } else {
+      (void)hipStreamWaitEvent(a, c->b_table[c->last], 0);  // table order (not the previous k_finish)
+      launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
+                     early, lhint, late_full);
+    }
     (void)hipEventRecord(c->b_done[k], a);
   } else {
     if (!st) st = c->stream;
@@ -445,6 +452,18 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   const uint32_t n = cfg.max_batch;
   bool ok = true;
   for (uint32_t k = 0; k < NBUF; k++) ok = ok && rl_stream_create(&c->pipe[k], SR_PIPE) == hipSuccess;
+  if (const char* sbm = getenv("RL_SB")) {  // (A/B knob: 1 = one table-stage stream, 2 = the same at high priority)
+    const int m = atoi(sbm);
+    if (m == 2) {
+      int lo = 0, hi = 0;
+      ok = ok && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+           hipStreamCreateWithPriority(&c->sb, hipStreamNonBlocking, hi) == hipSuccess;
+    } else if (m == 1) {
+      ok = ok && hipStreamCreateWithFlags(&c->sb, hipStreamNonBlocking) == hipSuccess;
+    }
+    for (uint32_t k = 0; k < NBUF && c->sb; k++)
+      ok = ok && hipEventCreateWithFlags(&c->a_done[k], hipEventDisableTiming) == hipSuccess;
+  }
   if (const char* be = getenv("RL_B_BEGIN_EARLY")) c->b_early = atoi(be) != 0;  // (A/B knob)
   c->stream = c->pipe[0];
   for (uint32_t k = 0; k < NBUF; k++)
@@ -574,6 +593,7 @@ void eng_destroy(Engine* c) {
     free_buffer(c->s[k]);
     if (c->b_done[k]) (void)hipEventDestroy(c->b_done[k]);
     if (c->b_table[k]) (void)hipEventDestroy(c->b_table[k]);
+    if (c->a_done[k]) (void)hipEventDestroy(c->a_done[k]);
     if (c->consumed[k]) (void)hipEventDestroy(c->consumed[k]);
   }
   for (uint32_t k = 0; k < PROGRESS_RING; k++)
@@ -604,6 +624,7 @@ void eng_destroy(Engine* c) {
   if (c->h_match) (void)hipHostFree(c->h_match);
   for (uint32_t k = 0; k < NBUF; k++)
     if (c->pipe[k]) (void)hipStreamDestroy(c->pipe[k]);
+  if (c->sb) (void)hipStreamDestroy(c->sb);
   delete c;
 }
 

@@ -283,7 +283,7 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
                     int restore, hipStream_t st, hipEvent_t* ev, const uint32_t* errb_prev, hipEvent_t table_done,
                     unsigned long long* kt_acc = nullptr, bool early = false, uint32_t* late_hint = nullptr,
-                    bool late_full = true);
+                    bool late_full = true, hipStream_t fin_st = nullptr);
 void launch_b_begin_early(const BatchDev& b, const OutDev& o, const Scratch& s, int restore, hipStream_t st,
                           const unsigned long long* log_ctr);
 // ev (optional, RL_NUM_STAGES + 1 events on stream st): recorded before

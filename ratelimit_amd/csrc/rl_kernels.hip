@@ -5246,7 +5246,8 @@ void launch_b_begin_early(const BatchDev& b, const OutDev& o, const Scratch& s, 
 
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
                     int restore, hipStream_t st, hipEvent_t* ev, const uint32_t* errb_prev, hipEvent_t table_done,
-                    unsigned long long* kt_acc, bool early, uint32_t* late_hint, bool late_full) {
+                    unsigned long long* kt_acc, bool early, uint32_t* late_hint, bool late_full,
+                    hipStream_t fin_st) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
   if (!early)
@@ -5286,6 +5287,10 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
         s.errs, restore, s.fast_blk, s.sorted_n, late_hint, late_full ? 0 : 1);
 #endif
     if (table_done) (void)hipEventRecord(table_done, st);
+    if (fin_st && fin_st != st) {  // (k_finish on the batch's own stream, off the table-order stream)
+      (void)hipStreamWaitEvent(fin_st, table_done, 0);
+      st = fin_st;
+    }
     if (!restore) {
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;
       const uint32_t gf = cdiv(nf * RL_NUM_STATS > b.n ? nf * RL_NUM_STATS : b.n, 256);
