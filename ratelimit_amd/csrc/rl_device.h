@@ -316,9 +316,8 @@ __host__ __device__ inline bool res_lc_hit(unsigned long long v) { return (v >> 
 // failed (its status is already in its packed result): every table kernel
 // leaves it alone.
 constexpr uint32_t FLAG_SKIP = 0x80;
-// bit 6 = the descriptor's sort key occurs more than once in the batch
-// (k_run_check): the sorted path answers it, not the keys-seen-once part.
-constexpr uint32_t FLAG_DUP = 0x40;
+// (bit 6, free: until round 6 the mark of a sort key that occurs more than
+// once in the batch, now the byte array BatchDev::dup)
 // bit 5 = a routed owner batch's own-chunk record: its stem lies in the
 // source batch (BatchDev::own), not in the received stems.
 constexpr uint32_t FLAG_SRC = 0x20;

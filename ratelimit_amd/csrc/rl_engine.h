@@ -52,8 +52,6 @@ struct Engine {
   hipStream_t pipe[NBUF] = {};    // one per scratch buffer
   hipEvent_t b_done[NBUF] = {};   // stage B of the last batch on each buffer is done
   hipEvent_t b_table[NBUF] = {};  // ... its table kernels are (the next batch's stage B waits for this)
-  hipStream_t sb = nullptr;       // RL_SB: the table stage of every batch, in order (null: on each batch's stream)
-  hipEvent_t a_done[NBUF] = {};   // (RL_SB) a batch's stage A is done
   hipEvent_t consumed[NBUF] = {}; // a routed owner batch's packed results (s[k].res) have been read
   hipEvent_t route_ready = nullptr;  // eng_route_do_limit: the caller's received buffers are ready
   hipEvent_t caller_ready = nullptr; // eng_do_limit_async: the caller stream's work so far (the inputs)

@@ -139,8 +139,10 @@ Params params(Engine* c, int isolate = 0);
 // stream as soon as the buffer is free, stage B after the previous batch's
 // stage B. Serial: both stages on `st` after all earlier work. With rl_profile
 // on, the stage boundaries are recorded on the batch's stream either way.
-uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hipStream_t st, bool pipelined) {
+uint32_t enqueue(Engine* c, const BatchDev& b_in, const OutDev& o, int restore, hipStream_t st, bool pipelined) {
   const uint32_t k = c->next;
+  BatchDev b = b_in;
+  b.dup = c->s[k].dup;  // (this buffer's duplicate marks)
   c->next = (k + 1) % NBUF;
   TableDev t = table_view(c);
   t.log_epoch = c->s[k].log_epoch;  // (k_b_begin sets it for this batch)
@@ -194,16 +196,9 @@ uint32_t enqueue(Engine* c, const BatchDev& b, const OutDev& o, int restore, hip
     (void)hipStreamWaitEvent(a, c->consumed[k], 0);  // ... and its routed results were read
     launch_stage_a(b, c->s[k], isolate, P.per_second, a, ev, hint, lng, bhint, big_full);
     if (early) launch_b_begin_early(b, o, c->s[k], restore, a, c->log_ctr);  // (off the table-order chain)
-    if (c->sb) {  // (RL_SB: every batch's table stage on one stream, in order; k_finish back on the batch's)
-      (void)hipEventRecord(c->a_done[k], a);
-      (void)hipStreamWaitEvent(c->sb, c->a_done[k], 0);
-      launch_stage_b(b, o, t, P, c->s[k], restore, c->sb, ev, errb_prev, c->b_table[k],
-                     c->prof ? c->d_kt_acc : nullptr, early, lhint, late_full, a);
-    } else {
-      (void)hipStreamWaitEvent(a, c->b_table[c->last], 0);  // table order (not the previous k_finish)
-      launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
-                     early, lhint, late_full);
-    }
+    (void)hipStreamWaitEvent(a, c->b_table[c->last], 0);  // table order (not the previous k_finish)
+    launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
+                   early, lhint, late_full);
     (void)hipEventRecord(c->b_done[k], a);
   } else {
     if (!st) st = c->stream;
@@ -334,7 +329,7 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
   ok = ok && dalloc(&s.run_end, n) == hipSuccess &&
        dalloc(&s.part_info, (size_t)PART_DIGITS * std::max((n + PART_TILE - 1) / PART_TILE, 1u)) == hipSuccess;
   ok = ok && dalloc(&s.r_base, RL_MAX_SHARDS) == hipSuccess && dalloc(&s.woff, (size_t)n + 1) == hipSuccess &&
-       dalloc(&s.wtsum, WIRE_SCAN_WORDS(n)) == hipSuccess;
+       dalloc(&s.wtsum, WIRE_SCAN_WORDS(n)) == hipSuccess && dalloc(&s.dup, n) == hipSuccess;
   return ok;
 }
 
@@ -343,7 +338,7 @@ void free_buffer(Scratch& s) {
                   s.vals[0], s.vals[1], s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1,
                   s.defer1_n, s.fast_blk, s.hits_s, s.segsum, s.rid, s.run_start, s.run_flags, s.run_state, s.run_alias,
                   s.run_f, s.runs64, s.split, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t, s.r_base,
-                  s.uniq, s.uniq_n, s.long_runs, s.kt_blk, s.log_epoch, s.woff, s.wtsum};
+                  s.uniq, s.uniq_n, s.long_runs, s.kt_blk, s.log_epoch, s.woff, s.wtsum, s.dup};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
 }
@@ -452,18 +447,6 @@ Engine* eng_create(const rl_config* cfg_in, char* err, size_t errlen) {
   const uint32_t n = cfg.max_batch;
   bool ok = true;
   for (uint32_t k = 0; k < NBUF; k++) ok = ok && rl_stream_create(&c->pipe[k], SR_PIPE) == hipSuccess;
-  if (const char* sbm = getenv("RL_SB")) {  // (A/B knob: 1 = one table-stage stream, 2 = the same at high priority)
-    const int m = atoi(sbm);
-    if (m == 2) {
-      int lo = 0, hi = 0;
-      ok = ok && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
-           hipStreamCreateWithPriority(&c->sb, hipStreamNonBlocking, hi) == hipSuccess;
-    } else if (m == 1) {
-      ok = ok && hipStreamCreateWithFlags(&c->sb, hipStreamNonBlocking) == hipSuccess;
-    }
-    for (uint32_t k = 0; k < NBUF && c->sb; k++)
-      ok = ok && hipEventCreateWithFlags(&c->a_done[k], hipEventDisableTiming) == hipSuccess;
-  }
   if (const char* be = getenv("RL_B_BEGIN_EARLY")) c->b_early = atoi(be) != 0;  // (A/B knob)
   c->stream = c->pipe[0];
   for (uint32_t k = 0; k < NBUF; k++)
@@ -593,7 +576,6 @@ void eng_destroy(Engine* c) {
     free_buffer(c->s[k]);
     if (c->b_done[k]) (void)hipEventDestroy(c->b_done[k]);
     if (c->b_table[k]) (void)hipEventDestroy(c->b_table[k]);
-    if (c->a_done[k]) (void)hipEventDestroy(c->a_done[k]);
     if (c->consumed[k]) (void)hipEventDestroy(c->consumed[k]);
   }
   for (uint32_t k = 0; k < PROGRESS_RING; k++)
@@ -624,7 +606,6 @@ void eng_destroy(Engine* c) {
   if (c->h_match) (void)hipHostFree(c->h_match);
   for (uint32_t k = 0; k < NBUF; k++)
     if (c->pipe[k]) (void)hipStreamDestroy(c->pipe[k]);
-  if (c->sb) (void)hipStreamDestroy(c->sb);
   delete c;
 }
 

@@ -10,7 +10,7 @@
 //                 k_bucket_big), run ids, run bounds and in-run prefix sums of
 //                 hits: each stem's descriptors together, in arrival order
 //   k_run_check   one stem and one unit per run (else RUN_MULTI); marks the
-//                 descriptors of runs (FLAG_DUP)
+//                 descriptors of runs (BatchDev::dup)
 //   k_split       RUN_MULTI runs of a few single-unit stems -> per-stem runs
 //   ---- stage B (the table; batch order) ----
 //   k_table       keys seen once (arrival order) and runs of two or more (one
@@ -56,7 +56,10 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   const uint32_t tid = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + tid;
   uint32_t bad = 0;
-  if (i < b.n) run_flags[i] = 0;  // k_run_check ORs run flags in from any block
+  if (i < b.n) {
+    run_flags[i] = 0;  // k_run_check ORs run flags in from any block
+    b.dup[i] = 0;      // ... and marks the duplicated keys
+  }
   if (blockIdx.x == 0 && tid == 0) {  // per-batch counters: RUN_MULTI queue, run ids, large buckets, sorted positions
     *defer_n = 0;
     *num_runs = 0;
@@ -2972,7 +2975,7 @@ constexpr uint32_t SPLIT_POS_OTHER = 0xFFu, SPLIT_POS_SKIP = 0xFEu, SPLIT_POS_NO
 constexpr uint32_t SPLIT_ULIST = 1024;  // split_long_body: other stems' positions listed in LDS
 
 // k_run_check marks every descriptor whose sort key occurs twice or more in the
-// batch (FLAG_DUP in its record, one plain store per descriptor: the thread of
+// batch (BatchDev::dup, one byte store per descriptor: the thread of
 // sorted position q marks q, and the run's head when q is its second element).
 // k_table answers the unmarked ones in arrival order and the runs in sorted
 // order. A run must hold one stem under one unit and one window: every
@@ -3033,7 +3036,7 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
     if (!same_stem && !skip && q == p + 1 && run_end[r] == q + 1) {
       // two unrelated stems sharing the 32-bit sort key (~100 runs per 1M
       // batch at C1): each is a key seen once in the batch. Neither gets
-      // FLAG_DUP (k_table's singleton part answers both) and the run is
+      // a dup mark (k_table's singleton part answers both) and the run is
       // emptied (its sorted path skips it); no k_split pass.
       run_end[r] = p;
       const uint32_t at = atomicAdd(uniq_n, 2u);
@@ -3041,8 +3044,8 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
       uniq[at + 1] = make_uint2(eq, skeys[q]);
       continue;
     }
-    rec[eq].lu = x.lu | (FLAG_DUP << 24);
-    if (q == p + 1) rec[ep].lu = y.lu | (FLAG_DUP << 24);  // the run's head
+    b.dup[eq] = 1;  // (a byte array, not the record: no partial store into a 32-B record per duplicate)
+    if (q == p + 1) b.dup[ep] = 1;  // the run's head
     const bool same = same_stem && rec_unit(x) == rec_unit(y);
     // per position, for k_split's long runs (coalesced there instead of a
     // random record read per element): the unit and max(1, hits), and how the
@@ -3567,7 +3570,7 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
                 atomicOr(&s_fl[gk], x.now / d != s_lnow[f] / d ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR);
               // a lone group of one element is a key seen once (k_table's singleton part)
               if (s_cnt[gk] == 1) {
-                rec[e[st]].lu = x.lu & ~(FLAG_DUP << 24);
+                b.dup[e[st]] = 0;
                 uq.push(e[st], p);
               }
             }
@@ -3857,7 +3860,7 @@ __global__ __launch_bounds__(SPLIT_THREADS, RL_SPLIT_OCC) void k_split(BatchDev 
           atomicOr(&s_fl[g], s_now[k] / d != s_lnow[f] / d ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR);
         // a lone group of one element is a key seen once (k_table's singleton part)
         if (s_cnt[g] == 1) {
-          rec[s_e[k]].lu = s_lu[k] & ~(FLAG_DUP << 24);
+          b.dup[s_e[k]] = 0;
           uq.push(s_e[k], p);
         }
       }
@@ -3897,7 +3900,7 @@ __global__ __launch_bounds__(SPLIT_THREADS, RL_SPLIT_OCC) void k_split(BatchDev 
 }
 
 // ---- k_table, keys seen once (unique_body): sort key once in the batch (no
-// FLAG_DUP), one lane each. Such a stem has no other descriptor in the batch,
+// dup mark), one lane each. Such a stem has no other descriptor in the batch,
 // so the lanes are independent and this part commutes with the sorted path
 // (runs_body). A stem that lives in the table under another unit too is left
 // to k_runs_general (defer1). Two orders, chosen per batch on the device:
@@ -3942,7 +3945,7 @@ __device__ __attribute__((always_inline)) inline void unique_body(uint32_t blk, 
   LaneStats L;
   L.reset();
   // not a duplicated key (the sorted path's), not failed (answered already)
-  auto single = [&](uint32_t i) { return !((rec[i].lu >> 24) & (FLAG_SKIP | FLAG_DUP)); };
+  auto single = [&](uint32_t i) { return !((rec[i].lu >> 24) & FLAG_SKIP) && !b.dup[i]; };
   bool act;
   uint32_t i, key = 0;
   if (by_list) {
@@ -5246,8 +5249,7 @@ void launch_b_begin_early(const BatchDev& b, const OutDev& o, const Scratch& s, 
 
 void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const Params& P, const Scratch& s,
                     int restore, hipStream_t st, hipEvent_t* ev, const uint32_t* errb_prev, hipEvent_t table_done,
-                    unsigned long long* kt_acc, bool early, uint32_t* late_hint, bool late_full,
-                    hipStream_t fin_st) {
+                    unsigned long long* kt_acc, bool early, uint32_t* late_hint, bool late_full) {
   const uint32_t m = restore ? 0u : b.n_rules * RL_NUM_STATS;
   const uint32_t gb = m ? (cdiv(m, 256) < 64 ? cdiv(m, 256) : 64) : 1;
   if (!early)
@@ -5287,10 +5289,6 @@ void launch_stage_b(const BatchDev& b, const OutDev& o, const TableDev& t, const
         s.errs, restore, s.fast_blk, s.sorted_n, late_hint, late_full ? 0 : 1);
 #endif
     if (table_done) (void)hipEventRecord(table_done, st);
-    if (fin_st && fin_st != st) {  // (k_finish on the batch's own stream, off the table-order stream)
-      (void)hipStreamWaitEvent(fin_st, table_done, 0);
-      st = fin_st;
-    }
     if (!restore) {
       const uint32_t nf = b.n_rules <= LDS_RULES ? b.n_rules : 0u;
       const uint32_t gf = cdiv(nf * RL_NUM_STATS > b.n ? nf * RL_NUM_STATS : b.n, 256);

@@ -1,0 +1,11 @@
+# Round 6: duplicate marks in a byte array (BatchDev::dup) instead of a
+# partial store into each duplicate's 32-B record: parity suites, then C1 /
+# C2 / C2U A/B against the previous HEAD's library, alternating on one box.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_alias.py \
+  tests/test_gpu_parity.py tests/test_gpu_history.py tests/test_gpu_edges.py tests/test_gpu_robustness.py \
+  tests/test_gpu_loopback.py > gpurun_out/r06_dup_tests.txt 2>&1 || { tail -40 gpurun_out/r06_dup_tests.txt; exit 1; }
+tail -2 gpurun_out/r06_dup_tests.txt
+bash scripts/ab_libs.sh "c1 c2 c2u" 2 build_abl/lib_head_predup.so
