@@ -85,7 +85,9 @@ typedef struct rl_config {
                                 Descriptor values are client-controlled: keep it secret. */
   uint32_t n_shards;         /* hash shards of the table held by this ctx (0 = 1); see rl_do_limit */
   uint32_t debug_hash_bits;  /* tests only: keep the top N bits of the hash's high word (0 = all 32),
-                                so that many stems share one sort key and one home region */
+                                so that many stems share one sort key and one home region;
+                                33..63: keep the top N - 32 bits and set the others (sort keys
+                                at the top of the range) */
   int32_t shard_device[16];  /* HIP device of shard k < n_shards (shards may share a device);
                                 unused when n_shards <= 1 (cfg.device) */
   uint64_t history_entries;  /* 32-B entries of the history log holding the windows below a key's

@@ -137,7 +137,7 @@ struct HashKey {
 
 __host__ __device__ inline HashKey hash_key_of(uint64_t seed, uint32_t hi_bits) {
   return HashKey{fmix64(seed ^ 0x243F6A8885A308D3ull), fmix64(seed + 0x13198A2E03707344ull),
-                 hi_bits == 0 || hi_bits > 32 ? 32u : hi_bits};
+                 hi_bits == 0 || hi_bits > 63 ? 32u : hi_bits};
 }
 
 struct StemHasher {
@@ -163,6 +163,7 @@ struct StemHasher {
     round(); round(); round();
     uint64_t x = v0 ^ v1 ^ v2 ^ v3;
     if (hi_bits < 32) x &= ~(((1ull << (32 - hi_bits)) - 1) << 32);
+    else if (hi_bits > 32) x |= ((1ull << (64 - hi_bits)) - 1) << 32;  // (33..63: the dropped bits set)
     return x ? x : 1;
   }
 };
@@ -316,8 +317,16 @@ __host__ __device__ inline bool res_lc_hit(unsigned long long v) { return (v >> 
 // failed (its status is already in its packed result): every table kernel
 // leaves it alone.
 constexpr uint32_t FLAG_SKIP = 0x80;
+// k_run_check marks a descriptor whose sort key occurs more than once in the
+// batch by overwriting its arrival-order key (Scratch::keys[0], read after the
+// partition only by the keys-seen-once part) with KEY_DUP: a random 4-B store
+// into a 4-B-per-descriptor array instead of into its 32-B record, and no
+// extra read where the keys are read anyway. k_prepare keeps KEY_DUP out of
+// the real keys (a stem whose hash starts with it sorts as KEY_DUP - 1, its
+// slot tags and home slot likewise: collisions are resolved by the stems).
+constexpr uint32_t KEY_DUP = 0xFFFFFFFFu;
 // (bit 6, free: until round 6 the mark of a sort key that occurs more than
-// once in the batch, now the byte array BatchDev::dup)
+// once in the batch; now KEY_DUP in the arrival-order keys)
 // bit 5 = a routed owner batch's own-chunk record: its stem lies in the
 // source batch (BatchDev::own), not in the received stems.
 constexpr uint32_t FLAG_SRC = 0x20;

@@ -141,8 +141,7 @@ Params params(Engine* c, int isolate = 0);
 // on, the stage boundaries are recorded on the batch's stream either way.
 uint32_t enqueue(Engine* c, const BatchDev& b_in, const OutDev& o, int restore, hipStream_t st, bool pipelined) {
   const uint32_t k = c->next;
-  BatchDev b = b_in;
-  b.dup = c->s[k].dup;  // (this buffer's duplicate marks)
+  const BatchDev& b = b_in;
   c->next = (k + 1) % NBUF;
   TableDev t = table_view(c);
   t.log_epoch = c->s[k].log_epoch;  // (k_b_begin sets it for this batch)
@@ -329,7 +328,7 @@ bool alloc_buffer(Scratch& s, uint32_t n) {
   ok = ok && dalloc(&s.run_end, n) == hipSuccess &&
        dalloc(&s.part_info, (size_t)PART_DIGITS * std::max((n + PART_TILE - 1) / PART_TILE, 1u)) == hipSuccess;
   ok = ok && dalloc(&s.r_base, RL_MAX_SHARDS) == hipSuccess && dalloc(&s.woff, (size_t)n + 1) == hipSuccess &&
-       dalloc(&s.wtsum, WIRE_SCAN_WORDS(n)) == hipSuccess && dalloc(&s.dup, n) == hipSuccess;
+       dalloc(&s.wtsum, WIRE_SCAN_WORDS(n)) == hipSuccess;
   return ok;
 }
 
@@ -338,7 +337,7 @@ void free_buffer(Scratch& s) {
                   s.vals[0], s.vals[1], s.grp, s.lead, s.gmask, s.defer, s.defer_n, s.defer2, s.defer2_n, s.defer1,
                   s.defer1_n, s.fast_blk, s.hits_s, s.segsum, s.rid, s.run_start, s.run_flags, s.run_state, s.run_alias,
                   s.run_f, s.runs64, s.split, s.drun, s.run_end, s.part_info, s.hit_a, s.tile, s.hit_t, s.r_base,
-                  s.uniq, s.uniq_n, s.long_runs, s.kt_blk, s.log_epoch, s.woff, s.wtsum, s.dup};
+                  s.uniq, s.uniq_n, s.long_runs, s.kt_blk, s.log_epoch, s.woff, s.wtsum};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
 }

@@ -102,7 +102,6 @@ struct BatchDev {
   // the arrays above (off, now, req, unit, flags, limit, hits, rule = null);
   // the stem of record j starts at woff[j] and must lie inside its source's
   // chunk [wbase[src], wbase[src + 1]) (the last source's ends at stem_total)
-  uint8_t* dup;  // [n] (per-batch scratch): 1 = the descriptor's sort key occurs twice or more (k_run_check)
   const Wire* wire;
   const uint32_t* woff;             // [n] stem offset of each record (launch_wire_offsets)
   const unsigned long long* wbad;   // the offset scan's verdict (non-zero: a chunk's lengths do not add up)
@@ -255,7 +254,6 @@ struct Scratch {
   uint32_t* route_hist;              // [2 x RL_MAX_SHARDS x tiles] per-tile counts (routing scratch only)
   // routed owner batches (eng_route_owner)
   unsigned long long* r_base;        // [RL_MAX_SHARDS] received stem chunk starts per source
-  uint8_t* dup;                      // [n] BatchDev::dup
   uint32_t* woff;                    // [max_batch + 1] received records' stem offsets (rl_route_do_limit)
   unsigned long long* wtsum;         // [WIRE_SCAN_WORDS(max_batch)] its scan's tile sums and verdict
 };

@@ -56,10 +56,7 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   const uint32_t tid = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + tid;
   uint32_t bad = 0;
-  if (i < b.n) {
-    run_flags[i] = 0;  // k_run_check ORs run flags in from any block
-    b.dup[i] = 0;      // ... and marks the duplicated keys
-  }
+  if (i < b.n) run_flags[i] = 0;  // k_run_check ORs run flags in from any block
   if (blockIdx.x == 0 && tid == 0) {  // per-batch counters: RUN_MULTI queue, run ids, large buckets, sorted positions
     *defer_n = 0;
     *num_runs = 0;
@@ -165,7 +162,7 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
   if (bad) atomicOr(err, bad);
 
   auto emit_rec = [&](uint64_t h) {
-    keys[i] = (uint32_t)(h >> 32);
+    keys[i] = (uint32_t)(h >> 32) == KEY_DUP ? KEY_DUP - 1u : (uint32_t)(h >> 32);  // (KEY_DUP: k_run_check's mark)
     Rec r;
     r.hlo = (uint32_t)h;
     r.off = s0;
@@ -2993,7 +2990,7 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
                                                    const unsigned long long* num_runs, unsigned long long* split,
                                                    const uint32_t* sorted_n, uint32_t* __restrict__ pos_unit,
                                                    uint32_t* __restrict__ pos_hits, uint2* __restrict__ uniq,
-                                                   uint32_t* uniq_n, uint32_t* long_runs) {
+                                                   uint32_t* uniq_n, uint32_t* long_runs, uint32_t* __restrict__ keys0) {
   __shared__ uint32_t s_list[RC_CHUNK], s_cnt;
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // k_split's reservations start from the bucket kernels' count
     split[0] = 0;
@@ -3044,8 +3041,8 @@ __global__ __launch_bounds__(256) void k_run_check(BatchDev b, SRec rec_s,
       uniq[at + 1] = make_uint2(eq, skeys[q]);
       continue;
     }
-    b.dup[eq] = 1;  // (a byte array, not the record: no partial store into a 32-B record per duplicate)
-    if (q == p + 1) b.dup[ep] = 1;  // the run's head
+    keys0[eq] = KEY_DUP;  // (the arrival-order key, not the record: KEY_DUP)
+    if (q == p + 1) keys0[ep] = KEY_DUP;  // the run's head
     const bool same = same_stem && rec_unit(x) == rec_unit(y);
     // per position, for k_split's long runs (coalesced there instead of a
     // random record read per element): the unit and max(1, hits), and how the
@@ -3233,7 +3230,14 @@ struct UniqList {
   uint2* list;
   uint32_t* n;
   const uint32_t* skeys;  // sorted keys: a run shares its sort key
-  __device__ inline void push(uint32_t e, uint32_t p) const { list[atomicAdd(n, 1u)] = make_uint2(e, skeys[p]); }
+  uint32_t* keys0;        // arrival-order keys (KEY_DUP marks)
+  // descriptor e (its run starts at sorted position p) is a key seen once
+  // after all: its arrival-order key back, and onto k_table's list
+  __device__ inline void single(uint32_t e, uint32_t p) const {
+    const uint32_t k = skeys[p];
+    keys0[e] = k;
+    list[atomicAdd(n, 1u)] = make_uint2(e, k);
+  }
 };
 
 template <uint32_t NT, uint32_t ST>
@@ -3570,8 +3574,7 @@ __device__ __attribute__((always_inline)) inline void split_long_body(uint32_t j
                 atomicOr(&s_fl[gk], x.now / d != s_lnow[f] / d ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR);
               // a lone group of one element is a key seen once (k_table's singleton part)
               if (s_cnt[gk] == 1) {
-                b.dup[e[st]] = 0;
-                uq.push(e[st], p);
+                uq.single(e[st], p);
               }
             }
           }
@@ -3860,8 +3863,7 @@ __global__ __launch_bounds__(SPLIT_THREADS, RL_SPLIT_OCC) void k_split(BatchDev 
           atomicOr(&s_fl[g], s_now[k] / d != s_lnow[f] / d ? RUN_SLOW | RUN_NOWVAR : RUN_NOWVAR);
         // a lone group of one element is a key seen once (k_table's singleton part)
         if (s_cnt[g] == 1) {
-          b.dup[s_e[k]] = 0;
-          uq.push(s_e[k], p);
+          uq.single(s_e[k], p);
         }
       }
     }
@@ -3945,7 +3947,7 @@ __device__ __attribute__((always_inline)) inline void unique_body(uint32_t blk, 
   LaneStats L;
   L.reset();
   // not a duplicated key (the sorted path's), not failed (answered already)
-  auto single = [&](uint32_t i) { return !((rec[i].lu >> 24) & FLAG_SKIP) && !b.dup[i]; };
+  auto single = [&](uint32_t i) { return keys0[i] != KEY_DUP && !((rec[i].lu >> 24) & FLAG_SKIP); };
   bool act;
   uint32_t i, key = 0;
   if (by_list) {
@@ -5209,12 +5211,12 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
 #endif
     k_run_check<<<cdiv(b.n, RC_CHUNK), 256, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.keys[1], s.rid, s.run_start,
                                                 s.run_end, s.run_flags, s.defer, s.defer_n, s.err, s.runs64, s.split,
-                                                s.sorted_n, s.grp, s.hit_t, s.uniq, s.uniq_n, s.long_runs);
+                                                s.sorted_n, s.grp, s.hit_t, s.uniq, s.uniq_n, s.long_runs, s.keys[0]);
 #ifndef RL_EXP_NO_SPLIT  // (measurement builds only: C1 defers no run to k_split)
     k_split<<<SPLIT_BLOCKS, SPLIT_THREADS, 0, st>>>(b, SRec{s.rec, s.vals[0]}, s.vals[0], s.segsum, s.rid, s.run_start,
                                           s.run_end, s.run_flags, s.defer, s.defer_n, s.runs64, s.split, s.drun,
                                           b.n / 2 + BIG_HEAVY * PART_DIGITS, s.grp, s.lead, s.hit_t, s.vals[1], s.err,
-                                          per_second, UniqList{s.uniq, s.uniq_n, s.keys[1]}, s.long_runs, long_hint,
+                                          per_second, UniqList{s.uniq, s.uniq_n, s.keys[1], s.keys[0]}, s.long_runs, long_hint,
                                           long_kernel ? 1 : 0);
 #endif
 #if RL_SPLIT_LONG_THREADS
@@ -5222,7 +5224,7 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
       k_split_long<<<RL_SPLIT_LONG_BLOCKS, RL_SPLIT_LONG_THREADS, 0, st>>>(
           b, SRec{s.rec, s.vals[0]}, s.vals[0], s.segsum, s.rid, s.run_start, s.run_end, s.run_flags, s.defer,
           s.runs64, s.split, s.drun, b.n / 2 + BIG_HEAVY * PART_DIGITS, s.grp, s.lead, s.hit_t, s.vals[1], s.err,
-          per_second, UniqList{s.uniq, s.uniq_n, s.keys[1]}, s.long_runs);
+          per_second, UniqList{s.uniq, s.uniq_n, s.keys[1], s.keys[0]}, s.long_runs);
 #endif
   }
 }

@@ -110,6 +110,18 @@ def test_gpu_long_runs_on_full_and_scanning_late_grids_vs_c_oracle(monkeypatch, 
 
 
 @pytest.mark.parametrize("lc", [False, True])
+def test_gpu_sort_keys_at_the_top_of_the_range_vs_c_oracle(lc):
+    """debug_hash_bits=33: every stem's sort key is 0x7FFFFFFF or 0xFFFFFFFF,
+    and the second is KEY_DUP, k_run_check's duplicate mark in the
+    arrival-order keys, so k_prepare files those stems under 0xFFFFFFFE. Batches
+    of one request (its two stems seen once, or a collision pair) and batches
+    of 300 (two sort keys for every stem: mixed-stem runs through k_split and
+    the exact path)."""
+    _check(_stream(list(range(38, 68)), tenants=30, rpb=1, p_override=0.3), lc, debug_hash_bits=33)
+    _check(_stream([39, 40, 41], tenants=40, rpb=300, p_override=0.3), lc, debug_hash_bits=33)
+
+
+@pytest.mark.parametrize("lc", [False, True])
 def test_gpu_override_on_and_off_vs_c_oracle(lc):
     """Batches with and without overrides, repeated and backward clocks: stems
     flagged multi-unit in the table take alias_setup alone (records of the
