@@ -202,7 +202,7 @@ class LoopTransport : public Transport {
       }
       hipEvent_t d = nullptr;
       if ((he = hipStreamWaitEvent(st, m->ready, 0)) != hipSuccess ||
-          (he = hipMemcpyAsync(x.buf, m->src, x.bytes, hipMemcpyDefault, st)) != hipSuccess ||
+          (he = hipMemcpyAsync(x.buf, m->src, x.bytes, hipMemcpyDeviceToDevice, st)) != hipSuccess ||
           (he = hipEventCreateWithFlags(&d, hipEventDisableTiming)) != hipSuccess ||
           (he = hipEventRecord(d, st)) != hipSuccess)
         return hip_fail("receive", he);
