@@ -1685,7 +1685,10 @@ int eng_local_cache_info_get(Engine* c, int64_t now, rl_local_cache_info* info) 
 }
 
 namespace {
-constexpr uint64_t SNAP_MAGIC = 0x35304150414e534cull;  // "LSNAPA05" (64-B slots, history log)
+// "LSNAPA06": 64-B slots, history log; since round 6 a stem whose hash's high
+// word is KEY_DUP homes as KEY_DUP - 1 (rl_device.h), so a round-5 image ("05")
+// is refused rather than loaded with such a stem where lookups no longer go
+constexpr uint64_t SNAP_MAGIC = 0x36304150414e534cull;
 struct SnapHeader {
   uint64_t magic, nslots, arena_used16, hash_seed;  // slots are placed by the keyed hash: restore adopts its key
   int64_t time_floor;
