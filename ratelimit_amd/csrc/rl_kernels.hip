@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void k_prepare(BatchDev b, Rec* __restrict__ r
     r.hits = hits;
     r.limit = limit;
     rec[i] = r;
-    hit_a[i] = r.hits;
+    if (b.wire) hit_a[i] = r.hits;  // (a routed owner batch; else k_part reads the batch's own hits array)
     if (dstat && isolate) {  // answered here: the table kernels skip it
       res[i] = pack_fail(dstat);
       atomicOr(errs, dstat == RL_E_TIME ? ERR_TIME : ERR_INVALID);
@@ -5187,7 +5187,7 @@ void launch_stage_a(const BatchDev& b, const Scratch& s, int isolate, int per_se
   if (ev) (void)hipEventRecord(ev[1], st);
   const uint32_t ptiles = cdiv(b.n, PART_TILE);
   if (b.n)
-    k_part<<<ptiles, 256, 0, st>>>(s.keys[0], s.hit_a, s.tile, b.n, ptiles, s.part_info, s.err);
+    k_part<<<ptiles, 256, 0, st>>>(s.keys[0], b.wire ? s.hit_a : b.hits, s.tile, b.n, ptiles, s.part_info, s.err);
   if (ev) (void)hipEventRecord(ev[2], st);
   if (b.n) {
     const size_t seg_lds = (2ull * ptiles + 1) * 4;
