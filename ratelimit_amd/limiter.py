@@ -171,6 +171,13 @@ class Backend:
         self._check(self.L.rl_do_limit_async(self.ctx, C.byref(b), C.byref(r),
                                                 C.c_void_p(stream) if stream else None))
 
+    def do_limit_structs(self, b, r, stream=None):
+        """rl_do_limit_async with prebuilt rl_batch / rl_result structs (device
+        arrays; the structs are read during the call only): what a C or Go
+        caller does per batch. stream: a hipStream_t handle, or None (the
+        inputs are complete at the call)."""
+        self._check(self.L.rl_do_limit_async(self.ctx, C.byref(b), C.byref(r), C.c_void_p(stream) if stream else None))
+
     def do_limit_host_async(self, pb: PackedBatch, out: dict):
         """rl_do_limit_host_async: host arrays in (pb) and out (dict of numpy
         arrays: code, limit_remaining, reset_s, stats[, status]), nothing waited
