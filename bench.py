@@ -57,8 +57,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the CPU baseline (0: the process's CPU share, cpu_share())")
-    ap.add_argument("--prof-every", type=int, default=7,
-                    help="time every k-th batch's stages with HIP events (k_table's live time for the roofline)")
+    ap.add_argument("--prof-every", type=int, default=13,
+                    help="time every k-th batch's stages with HIP events and k_table's run time on the device "
+                         "clock (the roofline's live time; the k-th timed batch first: 1 sample in 20 steps, 15 in "
+                         "200; each sample costs its batch a few us, profiles/r06/prof_cost/)")
     ap.add_argument("--no-fill", action="store_true")
     ap.add_argument("--pcie-steps", type=int, default=60, help="host-fed (PCIe) batches timed after the device phase")
     ap.add_argument("--pcie-formats", default="prefixed,compact,soa",
@@ -379,7 +381,7 @@ def main():
     # workgroup start to last workgroup end, as rocprofv3's kernel trace
     # measures it), and the HIP events around the launch on its stream (which
     # also hold the launch's wait behind the other streams' kernels)
-    kern_ms = stage_ms.get("table_kernel", 0.0)  # (already a per-batch average, over every timed batch)
+    kern_ms = stage_ms.get("table_kernel", 0.0)  # (already a per-batch average, over the sampled timed batches)
     ev_ms = stage_avg["table"]
     achieved = b_alg * n_unique / (kern_ms * 1e-3) / 1e9 if (kern_ms > 0 and n_unique) else None
     achieved_ev = b_alg * n_unique / (ev_ms * 1e-3) / 1e9 if (ev_ms > 0 and n_unique) else None
@@ -399,7 +401,7 @@ def main():
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                 "kernel_us": round(kern_ms * 1e3, 2) if kern_ms > 0 else None,
                 "time_basis": "k_table's own run time per launch on the device clock (first workgroup start to "
-                              "last workgroup end = rocprofv3 kernel duration), averaged over every timed batch",
+                              "last workgroup end = rocprofv3 kernel duration), averaged over the sampled timed batches (every --prof-every-th)",
                 "event_bracket": {"us": round(ev_ms * 1e3, 2) if ev_ms > 0 else None, "achieved": achieved_ev,
                                   "frac": (achieved_ev / HBM_PEAK_GBS) if achieved_ev else None,
                                   "basis": "HIP events around the k_table launch on its stream (includes its "

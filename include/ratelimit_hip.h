@@ -646,9 +646,11 @@ int rl_snapshot_save(rl_ctx* ctx, void* host, uint64_t bytes);
 int rl_snapshot_load(rl_ctx* ctx, const void* host, uint64_t bytes);
 
 /* Per-stage device timing (HIP events on the batch stream), for benchmarks.
- * rl_profile(ctx, k) with k >= 1 starts accumulating over every k-th batch
- * (1 = every batch; the event markers cost stage B a few microseconds per
- * batch, so a sparse sample keeps the timed pipeline unchanged), 0 stops;
+ * rl_profile(ctx, k) with k >= 1 starts accumulating over every k-th batch,
+ * the first sampled one being the k-th submitted after the call (1 = every
+ * batch; the event markers and k_table's per-workgroup clock reads cost a
+ * sampled batch a few microseconds, so a sparse sample keeps the timed
+ * pipeline unchanged), 0 stops;
  * rl_profile_read fills ms[0..n) with
  * the summed milliseconds of the stages {prepare, sort, segment, table, finish}
  * and *batches with the number of batches timed (it synchronises), then resets

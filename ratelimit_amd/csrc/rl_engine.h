@@ -127,7 +127,7 @@ struct Engine {
   hipEvent_t ev[PROF_RING][RL_NUM_STAGES + 1] = {};
   double stage_ms[RL_NUM_STAGES] = {};
   uint64_t prof_batches = 0;
-  // ... and k_table's own run time on every batch while profiling (device
+  // ... and k_table's own run time on those batches (device
   // clock): {sum of durations in ticks, batches}, and the clock's rate (kHz)
   unsigned long long* d_kt_acc = nullptr;
   double wclk_khz = 0;

@@ -196,7 +196,7 @@ uint32_t enqueue(Engine* c, const BatchDev& b_in, const OutDev& o, int restore, 
     launch_stage_a(b, c->s[k], isolate, P.per_second, a, ev, hint, lng, bhint, big_full);
     if (early) launch_b_begin_early(b, o, c->s[k], restore, a, c->log_ctr);  // (off the table-order chain)
     (void)hipStreamWaitEvent(a, c->b_table[c->last], 0);  // table order (not the previous k_finish)
-    launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
+    launch_stage_b(b, o, t, P, c->s[k], restore, a, ev, errb_prev, c->b_table[k], ev ? c->d_kt_acc : nullptr,
                    early, lhint, late_full);
     (void)hipEventRecord(c->b_done[k], a);
   } else {
@@ -205,7 +205,7 @@ uint32_t enqueue(Engine* c, const BatchDev& b_in, const OutDev& o, int restore, 
     hipEvent_t* ev = prof_events(c);
     launch_stage_a(b, c->s[k], isolate, P.per_second, st, ev, hint, lng, bhint, big_full);
     if (early) launch_b_begin_early(b, o, c->s[k], restore, st, c->log_ctr);
-    launch_stage_b(b, o, t, P, c->s[k], restore, st, ev, errb_prev, c->b_table[k], c->prof ? c->d_kt_acc : nullptr,
+    launch_stage_b(b, o, t, P, c->s[k], restore, st, ev, errb_prev, c->b_table[k], ev ? c->d_kt_acc : nullptr,
                    early, lhint, late_full);
     (void)hipEventRecord(c->b_done[k], st);
   }
@@ -812,7 +812,9 @@ int eng_profile(Engine* c, int enable) {
   prof_fold_all(c);
   c->prof = enable > 0;
   c->prof_every = enable > 0 ? (uint32_t)enable : 1u;
-  c->prof_skip = 0;
+  // (the first sampled batch is the k-th: a timed region's first batch, whose
+  // stage A runs with nothing beside it, is not one of them)
+  c->prof_skip = c->prof_every - 1;
   return RL_OK;
 }
 

@@ -109,8 +109,8 @@ def test_gpu_snapshot_restore_continues_exactly():
 
 
 def test_gpu_profile_sampling_counts_and_leaves_results_unchanged():
-    """rl_profile(ctx, k) times every k-th batch (bench --prof-every) and does
-    not change any decision."""
+    """rl_profile(ctx, k) times every k-th batch, the k-th submitted after the
+    call first (bench --prof-every), and does not change any decision."""
     calls = stream(11, n_calls=1400)
     oc = O.OracleFixedRateLimitCache(0.8, True)
     cache = GpuRateLimitCache(FixedTimeSource(0), 0.8, True, **SMALL)
@@ -125,9 +125,9 @@ def test_gpu_profile_sampling_counts_and_leaves_results_unchanged():
             assert [[st(s) for s in g] for g in got] == [[st(s) for s in w] for w in want]
             n_batches += 1
         ms, nb = cache.backend.profile_read()
-        assert nb == (n_batches + 2) // 3
+        assert nb == n_batches // 3
         assert all(v >= 0.0 for v in ms.values()) and ms["table"] > 0.0
-        # k_table's own run time per batch (device clock, every batch)
+        # k_table's own run time per sampled batch (device clock)
         assert 0.0 < ms["table_kernel"] < 10.0
         cache.backend.profile(False)
         cache.do_limit_batch(calls[-10:])
