@@ -272,6 +272,11 @@ def main():
                 pass
         step[0] += 1
 
+    # (the table counters before the warmup: k_table_info scans the whole
+    # table, and run between the warmup and the timed region it would leave
+    # the timed batches a cold Infinity Cache; routed runs use the delta per
+    # owner batch, warmup batches included)
+    info0 = be.table_info()
     # ---- warmup
     for _ in range(args.warmup):
         run_step()
@@ -287,7 +292,6 @@ def main():
     if py_route:
         for k in sc.host_s:
             sc.host_s[k] = 0.0
-    info0 = be.table_info()
     barrier()
     torch.cuda.synchronize()
     host_in_call[0] = 0.0
